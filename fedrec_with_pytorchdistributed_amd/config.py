@@ -1,0 +1,228 @@
+"""Typed configuration for the federated news-recommendation engine.
+
+Every hard-coded constant of the reference is a field here:
+
+* npratio / max_his_len          -> reference ``dataset.py:8-9``
+* news_dim 400                   -> ``encoder.py:14,38``; ``client.py:33,35``
+* user heads / d_k / query dim   -> ``encoder.py:39-47``
+* text additive hidden 768 // 2  -> ``encoder.py:20-21``
+* user dropout 0.2               -> ``encoder.py:43,50``
+* lr 5e-5 (both Adams)           -> ``model.py:22-23``
+* DP C=2, delta=1e-5, epochs=50  -> ``client.py:220-223``
+* snapshot path / data dir       -> ``client.py:213,229``
+
+Values are overridable with ``--key=value`` flags (dotted keys reach the nested
+sections, e.g. ``--dp.epsilon=10``).  The reference's positional argv contract is
+handled by the entrypoint shims (``client.py`` etc.), which build a config and then
+apply any trailing ``--key=value`` overrides.
+
+Behavioural quirks of the reference are individual switches in
+:class:`Compat`; ``--compat.reference_quirks=1`` turns all of them on at once.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+
+@dataclass
+class BackboneConfig:
+    """Transformer text backbone.  Defaults = ``distilbert-base-uncased`` config (E2)."""
+
+    name: str = "distilbert"  # distilbert | bert-base
+    vocab_size: int = 30522
+    dim: int = 768
+    n_layers: int = 6
+    n_heads: int = 12
+    hidden_dim: int = 3072
+    max_position: int = 512
+    ln_eps: float = 1e-12
+    dropout: float = 0.1
+    frozen: bool = True  # reference freezes DistilBERT (model.py:25-26)
+    init_std: float = 0.02
+
+    @staticmethod
+    def preset(name: str) -> "BackboneConfig":
+        if name in ("distilbert", "distilbert-base-uncased"):
+            return BackboneConfig(name="distilbert")
+        if name in ("bert-base", "bert-base-uncased"):
+            # BASELINE config 5: unfrozen BERT-base text encoder (12 layers, same widths).
+            return BackboneConfig(name="bert-base", n_layers=12, frozen=False)
+        if name == "tiny":  # test-only preset
+            return BackboneConfig(name="tiny", vocab_size=30522, dim=64, n_layers=2,
+                                  n_heads=4, hidden_dim=128)
+        raise ValueError(f"unknown backbone preset {name!r}")
+
+
+@dataclass
+class DPConfig:
+    """Local differential privacy on per-occurrence news-vector gradients (client.py:87-89)."""
+
+    enabled: bool = False
+    epsilon: float = 0.0
+    delta: float = 1e-5
+    clip: float = 2.0  # MAX_GRAD_NORM (client.py:220)
+    epochs: int = 50  # EPOCHS used for calibration (client.py:223)
+    noise_multiplier: Optional[float] = None  # explicit sigma overrides calibration
+
+
+@dataclass
+class SecAggConfig:
+    """Pairwise-mask secure aggregation (README.md:56,65 describes it; never implemented there)."""
+
+    enabled: bool = False
+    frac_bits: int = 16  # fixed-point fraction bits for uint32 quantisation
+    clip_value: float = 1024.0  # |x| bound before quantisation
+
+
+@dataclass
+class Compat:
+    """Switches that reproduce reference quirks.  All default to the fixed behaviour."""
+
+    reference_quirks: bool = False  # master switch: turns every switch below on
+    grad_double_last_batch: bool = False  # Q2: user grads x2, last batch only
+    replay_train_mode: bool = False  # Q4: epoch-end replay re-runs the backbone with dropout
+    no_history_truncation: bool = False  # Q6: pad to 50 but never truncate
+    ldp_no_clip: bool = False  # Q10: no clip, noise std = sigma (not sigma*C)
+    resplit_shard: bool = False  # Q11: DistributedSampler re-splits the private shard
+    validate_last_only: bool = False  # Q9: report the last impression's metrics
+
+    def resolved(self) -> "Compat":
+        if not self.reference_quirks:
+            return self
+        return Compat(True, True, True, True, True, True, True)
+
+
+@dataclass
+class FedRecConfig:
+    # --- model (encoder.py / attention.py) -------------------------------------------
+    news_dim: int = 400
+    user_heads: int = 20
+    user_head_dim: int = 20
+    user_query_dim: int = 200
+    user_dropout: float = 0.2
+    text_query_dim: int = 384  # DistilBERT hidden // 2 (encoder.py:20-21)
+    title_len: int = 50
+    backbone: BackboneConfig = field(default_factory=BackboneConfig)
+    score_act: str = "sigmoid"  # Q1: CE over sigmoid scores (model.py:123); "identity" optional
+    mask_padding: bool = False  # Q7: reference never masks padding in pools/user MHA
+
+    # --- data (dataset.py) -----------------------------------------------------------
+    npratio: int = 4
+    max_his_len: int = 50
+    data_dir: str = "UserData"
+
+    # --- optimisation (model.py:22-23) -----------------------------------------------
+    lr: float = 5e-5
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_eps: float = 1e-8
+    batch_size: int = 16
+    total_epochs: int = 1
+    save_every: int = 1
+    global_rounds: int = 1
+
+    # --- federation ------------------------------------------------------------------
+    mode: str = "fedavg_star"  # fedavg_star | grad_avg | param_avg
+    local_update: str = "auto"  # per_epoch | per_step | auto (per_step for grad_avg)
+    param_avg_every: int = 0  # PA: all-reduce every K local steps (0 = once per epoch)
+    server_trains: bool = False  # main.py variant: every participant trains
+    weighted_fedavg: bool = False  # Q12: reference mean is unweighted (server.py:49)
+    sync: str = "trainable"  # Q15: trainable | full (the reference syncs all 116 tensors)
+    quorum: float = 1.0  # fraction of clients needed to aggregate a round
+    collective_timeout_s: float = 600.0  # reference: 2 days (client.py:227)
+    round_timeout_s: float = 3600.0
+
+    # --- privacy / secure aggregation --------------------------------------------------
+    dp: DPConfig = field(default_factory=DPConfig)
+    secagg: SecAggConfig = field(default_factory=SecAggConfig)
+
+    # --- engine ------------------------------------------------------------------------
+    precision: str = "bf16"  # backbone compute dtype: bf16 | fp32
+    news_cache: str = "none"  # none | vectors  (HBM-resident per-epoch news table, §7.1)
+    device: str = "auto"  # auto | cpu | cuda
+    allreduce: str = "rccl"  # rccl | xgmi (custom one-shot all-reduce)
+    seed: int = 0
+
+    # --- io / observability ------------------------------------------------------------
+    snapshot_path: str = "snapshot.pt"
+    metrics_path: str = ""  # JSONL; empty = metrics.jsonl beside the snapshot on rank 0
+    run_name: str = "fedrec"
+    wandb_project: str = "Node4"  # only used when FEDREC_WANDB=1 and wandb is importable
+    verbose: bool = True
+
+    compat: Compat = field(default_factory=Compat)
+
+    # ------------------------------------------------------------------------------------
+    def resolved_local_update(self) -> str:
+        if self.local_update != "auto":
+            return self.local_update
+        return "per_step" if self.mode == "grad_avg" else "per_epoch"
+
+    def quirks(self) -> Compat:
+        return self.compat.resolved()
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    def to_json(self) -> str:
+        return json.dumps(self.to_dict(), sort_keys=True)
+
+    @staticmethod
+    def from_dict(d: Dict[str, Any]) -> "FedRecConfig":
+        cfg = FedRecConfig()
+        for k, v in d.items():
+            _set_dotted(cfg, k, v, flat=False)
+        return cfg
+
+    def apply_overrides(self, args: List[str]) -> List[str]:
+        """Consume ``--key=value`` items; return the arguments that were not overrides."""
+        rest = []
+        for a in args:
+            if a.startswith("--") and "=" in a:
+                k, v = a[2:].split("=", 1)
+                _set_dotted(self, k.replace("-", "_"), v, flat=True)
+            else:
+                rest.append(a)
+        if self.backbone.name != BackboneConfig().name and self.backbone == BackboneConfig(
+            name=self.backbone.name
+        ):
+            # a bare --backbone.name=bert-base selects the full preset
+            self.backbone = BackboneConfig.preset(self.backbone.name)
+        return rest
+
+
+def _coerce(old: Any, v: Any) -> Any:
+    if not isinstance(v, str):
+        return v
+    if isinstance(old, bool):
+        return v.lower() in ("1", "true", "yes", "on")
+    if isinstance(old, int) and not isinstance(old, bool):
+        return int(float(v))
+    if isinstance(old, float):
+        return float(v)
+    if old is None:
+        try:
+            return float(v)
+        except ValueError:
+            return v
+    return v
+
+
+def _set_dotted(obj: Any, key: str, value: Any, flat: bool) -> None:
+    parts = key.split(".")
+    for p in parts[:-1]:
+        if not hasattr(obj, p):
+            raise KeyError(f"unknown config section {p!r} in {key!r}")
+        obj = getattr(obj, p)
+    last = parts[-1]
+    if not hasattr(obj, last):
+        raise KeyError(f"unknown config key {key!r}")
+    old = getattr(obj, last)
+    if dataclasses.is_dataclass(old) and isinstance(value, dict):
+        for k, v in value.items():
+            _set_dotted(old, k, v, flat=False)
+        return
+    setattr(obj, last, _coerce(old, value))

@@ -1,0 +1,175 @@
+"""Transformer text backbone with DistilBERT's module tree (so the state_dict keys are the
+reference's ``text_encoder.DistillBert.*`` keys) and a compute path built
+on the engine's own ops instead of HF modules.
+
+Reference: ``encoder.py:19,27`` -- ``DistilBertModel.from_pretrained(...)(tokens,
+attention_mask=mask)[0]``; frozen at ``model.py:25-26``; 6 post-LN blocks (C26).
+
+Compute layout (MI355X path):
+
+* the fp32 ``nn.Parameter`` tensors stay the source of truth (state_dict round-trips a
+  reference checkpoint bit-exactly);
+* :meth:`compute_weights` packs them once into device-resident compute tensors: Q|K|V
+  fused into one ``[3D, D]`` bf16 weight (one GEMM with N = 2304 instead of three),
+  biases fp32.  The pack is cached and rebuilt only when the fp32 weights change
+  (``invalidate()``: load_state_dict, optimizer step in unfrozen mode);
+* :meth:`forward` runs ``embed_ln -> [qkv GEMM -> title attention -> out GEMM(+res) -> LN
+  -> FFN1 GEMM(+GELU) -> FFN2 GEMM(+res) -> LN] x L`` through :mod:`..ops`.
+
+Initialisation follows HF DistilBERT ``_init_weights`` (normal(0, 0.02) for linears and
+embeddings, zero biases, LN = (1, 0), padding row 0 of the word table zeroed).  There are
+no pretrained weights offline.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+from torch import nn
+
+from ..config import BackboneConfig
+from .. import ops
+
+
+class _Embeddings(nn.Module):
+    def __init__(self, c: BackboneConfig):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(c.vocab_size, c.dim, padding_idx=0)
+        self.position_embeddings = nn.Embedding(c.max_position, c.dim)
+        self.LayerNorm = nn.LayerNorm(c.dim, eps=c.ln_eps)
+
+
+class _Attention(nn.Module):
+    def __init__(self, c: BackboneConfig):
+        super().__init__()
+        self.q_lin = nn.Linear(c.dim, c.dim)
+        self.k_lin = nn.Linear(c.dim, c.dim)
+        self.v_lin = nn.Linear(c.dim, c.dim)
+        self.out_lin = nn.Linear(c.dim, c.dim)
+
+
+class _FFN(nn.Module):
+    def __init__(self, c: BackboneConfig):
+        super().__init__()
+        self.lin1 = nn.Linear(c.dim, c.hidden_dim)
+        self.lin2 = nn.Linear(c.hidden_dim, c.dim)
+
+
+class _Block(nn.Module):
+    def __init__(self, c: BackboneConfig):
+        super().__init__()
+        self.attention = _Attention(c)
+        self.sa_layer_norm = nn.LayerNorm(c.dim, eps=c.ln_eps)
+        self.ffn = _FFN(c)
+        self.output_layer_norm = nn.LayerNorm(c.dim, eps=c.ln_eps)
+
+
+class _Transformer(nn.Module):
+    def __init__(self, c: BackboneConfig):
+        super().__init__()
+        self.layer = nn.ModuleList([_Block(c) for _ in range(c.n_layers)])
+
+
+class Backbone(nn.Module):
+    """``DistillBert`` sub-module of the text encoder."""
+
+    def __init__(self, c: BackboneConfig):
+        super().__init__()
+        self.cfg = c
+        self.embeddings = _Embeddings(c)
+        self.transformer = _Transformer(c)
+        self._pack: Optional[Dict] = None
+        self._pack_key = None
+        self.reset_parameters()
+
+    # -------------------------------------------------------------------------------
+    @torch.no_grad()
+    def reset_parameters(self) -> None:
+        std = self.cfg.init_std
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                m.weight.normal_(0.0, std)
+                m.bias.zero_()
+            elif isinstance(m, nn.Embedding):
+                m.weight.normal_(0.0, std)
+                if m.padding_idx is not None:
+                    m.weight[m.padding_idx].zero_()
+            elif isinstance(m, nn.LayerNorm):
+                m.weight.fill_(1.0)
+                m.bias.zero_()
+        self.invalidate()
+
+    def invalidate(self) -> None:
+        self._pack = None
+
+    def _load_from_state_dict(self, *args, **kwargs):  # keep the compute pack coherent
+        self.invalidate()
+        return super()._load_from_state_dict(*args, **kwargs)
+
+    @torch.no_grad()
+    def compute_weights(self, dtype: torch.dtype) -> Dict:
+        dev = self.embeddings.word_embeddings.weight.device
+        key = (dtype, dev)
+        if self._pack is not None and self._pack_key == key:
+            return self._pack
+        e = self.embeddings
+        pack: Dict = {
+            "word": e.word_embeddings.weight.detach().to(dtype).contiguous(),
+            "pos": e.position_embeddings.weight.detach().to(dtype).contiguous(),
+            "emb_ln_w": e.LayerNorm.weight.detach().float().contiguous(),
+            "emb_ln_b": e.LayerNorm.bias.detach().float().contiguous(),
+            "layers": [],
+        }
+        for blk in self.transformer.layer:
+            a = blk.attention
+            pack["layers"].append({
+                "wqkv": torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0).to(dtype).contiguous(),
+                "bqkv": torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0).float().contiguous(),
+                "wo": a.out_lin.weight.detach().to(dtype).contiguous(),
+                "bo": a.out_lin.bias.detach().float().contiguous(),
+                "ln1_w": blk.sa_layer_norm.weight.detach().float().contiguous(),
+                "ln1_b": blk.sa_layer_norm.bias.detach().float().contiguous(),
+                "w1": blk.ffn.lin1.weight.detach().to(dtype).contiguous(),
+                "b1": blk.ffn.lin1.bias.detach().float().contiguous(),
+                "w2": blk.ffn.lin2.weight.detach().to(dtype).contiguous(),
+                "b2": blk.ffn.lin2.bias.detach().float().contiguous(),
+                "ln2_w": blk.output_layer_norm.weight.detach().float().contiguous(),
+                "ln2_b": blk.output_layer_norm.bias.detach().float().contiguous(),
+            })
+        self._pack, self._pack_key = pack, key
+        return pack
+
+    # -------------------------------------------------------------------------------
+    @torch.no_grad()
+    def forward(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+        """``tokens, mask [n, T]`` -> last hidden state ``[n*T, D]`` in ``dtype`` (eval mode)."""
+        c = self.cfg
+        P = self.compute_weights(dtype)
+        x = ops.embed_ln(tokens, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps, dtype)
+        for L in P["layers"]:
+            qkv = ops.linear(x, L["wqkv"], L["bqkv"], out_dtype=dtype)
+            ctx = ops.title_attention(qkv, mask, c.n_heads)
+            h = ops.linear(ctx, L["wo"], L["bo"], residual=x, out_dtype=dtype)
+            x = ops.layer_norm(h, L["ln1_w"], L["ln1_b"], c.ln_eps, dtype)
+            f = ops.linear(x, L["w1"], L["b1"], act="gelu", out_dtype=dtype)
+            h = ops.linear(f, L["w2"], L["b2"], residual=x, out_dtype=dtype)
+            x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, dtype)
+        return x
+
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        """Keys as HF ``DistilBertModel`` names them (for parity tests)."""
+        return {k: v for k, v in self.state_dict().items()}
+
+
+def param_names(c: BackboneConfig) -> List[str]:
+    names = ["embeddings.word_embeddings.weight", "embeddings.position_embeddings.weight",
+             "embeddings.LayerNorm.weight", "embeddings.LayerNorm.bias"]
+    for i in range(c.n_layers):
+        p = f"transformer.layer.{i}."
+        for m in ("attention.q_lin", "attention.k_lin", "attention.v_lin", "attention.out_lin"):
+            names += [p + m + ".weight", p + m + ".bias"]
+        names += [p + "sa_layer_norm.weight", p + "sa_layer_norm.bias"]
+        for m in ("ffn.lin1", "ffn.lin2"):
+            names += [p + m + ".weight", p + m + ".bias"]
+        names += [p + "output_layer_norm.weight", p + "output_layer_norm.bias"]
+    return names

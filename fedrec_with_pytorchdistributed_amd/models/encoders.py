@@ -1,0 +1,101 @@
+"""Text encoder (backbone + additive-attention head + FC 400) and user encoder.
+
+Module trees mirror the reference so state_dict keys match:
+
+* ``TextEncoder``  (``encoder.py:12-30``): ``DistillBert`` / ``additive_attention``
+  (``att_fc1 [384,768]``, ``att_fc2 [1,384]``) / ``fc [400,768]``.
+* ``UserEncoder``  (``encoder.py:36-56``): ``multihead_attention`` (``W_Q, W_K, W_V``
+  ``[400,400]``, Xavier-uniform weights, ``attention.py:64-67``; no output projection) /
+  ``additive_attention`` (``att_fc1 [200,400]``, ``att_fc2 [1,200]``).
+
+The text encoder is split into :meth:`TextEncoder.hidden` (frozen backbone, no grad,
+bf16 on the device) and :meth:`TextEncoder.head` (trainable), which is what lets the
+engine dedup titles, cache hidden states, and run the head VJP without re-running the
+backbone.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..config import FedRecConfig
+from ..ops import functional as OF
+from .backbone import Backbone
+
+
+class AdditiveAttention(nn.Module):
+    """``attention.py:8-26``; the pooling has no padding mask (Q7)."""
+
+    def __init__(self, d_h: int, hidden_size: int = 200):
+        super().__init__()
+        self.att_fc1 = nn.Linear(d_h, hidden_size)
+        self.att_fc2 = nn.Linear(hidden_size, 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return OF.additive_pool(x, self.att_fc1, self.att_fc2)
+
+
+class MultiHeadAttention(nn.Module):
+    """``attention.py:50-82`` (no output projection, no mask)."""
+
+    def __init__(self, d_model: int, n_heads: int, d_k: int, d_v: int):
+        super().__init__()
+        assert d_k == d_v
+        self.n_heads, self.d_k = n_heads, d_k
+        self.W_Q = nn.Linear(d_model, d_k * n_heads)
+        self.W_K = nn.Linear(d_model, d_k * n_heads)
+        self.W_V = nn.Linear(d_model, d_v * n_heads)
+        for m in (self.W_Q, self.W_K, self.W_V):
+            nn.init.xavier_uniform_(m.weight, gain=1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        w = torch.cat([self.W_Q.weight, self.W_K.weight, self.W_V.weight], 0)
+        b = torch.cat([self.W_Q.bias, self.W_K.bias, self.W_V.bias], 0)
+        qkv = F.linear(x, w, b)  # one [B*H, 400] x [400, 1200] GEMM
+        return OF.user_attention(qkv, self.n_heads, self.d_k)
+
+
+class UserEncoder(nn.Module):
+    def __init__(self, cfg: FedRecConfig):
+        super().__init__()
+        self.dropout_rate = cfg.user_dropout
+        self.multihead_attention = MultiHeadAttention(cfg.news_dim, cfg.user_heads, cfg.user_head_dim,
+                                                      cfg.user_head_dim)
+        self.additive_attention = AdditiveAttention(cfg.news_dim, cfg.user_query_dim)
+
+    def forward(self, clicked: torch.Tensor) -> torch.Tensor:
+        x = F.dropout(clicked, p=self.dropout_rate, training=self.training)
+        y = self.multihead_attention(x)
+        return self.additive_attention(y)
+
+
+class TextEncoder(nn.Module):
+    def __init__(self, cfg: FedRecConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.DistillBert = Backbone(cfg.backbone)
+        d = cfg.backbone.dim
+        self.additive_attention = AdditiveAttention(d, cfg.text_query_dim)
+        self.fc = nn.Linear(d, cfg.news_dim)
+
+    @property
+    def compute_dtype(self) -> torch.dtype:
+        dev = self.fc.weight.device
+        if dev.type == "cuda" and self.cfg.precision == "bf16":
+            return torch.bfloat16
+        return torch.float32
+
+    def hidden(self, text: torch.Tensor) -> torch.Tensor:
+        """Frozen backbone: ``text [n,2,T]`` -> last hidden state ``[n,T,D]`` (no grad)."""
+        n, _, T = text.shape
+        h = self.DistillBert(text[:, 0, :], text[:, 1, :], self.compute_dtype)
+        return h.view(n, T, -1)
+
+    def head(self, hidden: torch.Tensor) -> torch.Tensor:
+        """Trainable head: ``[n,T,D] -> [n,400]`` (fp32)."""
+        pooled = self.additive_attention(hidden)
+        return F.linear(pooled, self.fc.weight, self.fc.bias)
+
+    def forward(self, text: torch.Tensor) -> torch.Tensor:
+        return self.head(self.hidden(text))

@@ -1,0 +1,113 @@
+"""The federated model container (reference ``UserModel``, ``model.py:10-129``).
+
+Holds ``text_encoder`` + ``user_encoder`` in registration order, so ``state_dict()`` has
+exactly the reference's 116 keys (E2), and lays every *trainable* parameter out in one
+contiguous fp32 buffer (:class:`FlatParams`): parameters, gradients and both Adam moments
+are flat, so the gradient all-reduce is one RCCL call over one bucket and Adam is one
+kernel (replacing the reference's two ``torch.optim.Adam`` instances, ``model.py:22-23``,
+which always step together in ``update()``, ``model.py:66-70``).
+
+Trainable set (frozen backbone, ``model.py:25-26``): text head 603,281 + user encoder
+561,601 = 1,164,882 params in 16 tensors (4.66 MB fp32).  With
+``backbone.frozen=False`` (BASELINE config 5) the backbone joins the flat store.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterator, List, Tuple
+
+import torch
+from torch import nn
+
+from ..config import FedRecConfig
+from .encoders import TextEncoder, UserEncoder
+
+
+class FlatParams:
+    """Parameters re-pointed into one flat fp32 buffer (+ flat grad, Adam m/v)."""
+
+    ALIGN = 64  # elements; keeps every view 256-B aligned for vector loads
+
+    def __init__(self, named: List[Tuple[str, nn.Parameter]]):
+        self.names = [n for n, _ in named]
+        self.params = [p for _, p in named]
+        offs, o = [], 0
+        for p in self.params:
+            offs.append(o)
+            o += -(-p.numel() // self.ALIGN) * self.ALIGN
+        self.offsets = offs
+        self.numel_padded = o
+        self.numel = sum(p.numel() for p in self.params)
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.flat = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.step = 0
+        with torch.no_grad():
+            for p, off in zip(self.params, offs):
+                n = p.numel()
+                self.flat[off:off + n].copy_(p.detach().reshape(-1).float())
+                p.data = self.flat[off:off + n].view_as(p)
+                p.grad = self.grad[off:off + n].view_as(p)
+
+    def views(self) -> Iterator[Tuple[str, torch.Tensor, int]]:
+        for n, p, off in zip(self.names, self.params, self.offsets):
+            yield n, p, off
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+        # autograd may have replaced .grad (e.g. set_to_none elsewhere): re-point
+        for p, off in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
+                p.grad = self.grad[off:off + p.numel()].view_as(p)
+
+    def state(self) -> Dict[str, torch.Tensor]:
+        return {"m": self.m.detach().cpu(), "v": self.v.detach().cpu(), "step": torch.tensor(self.step)}
+
+    def load_state(self, s: Dict[str, torch.Tensor]) -> None:
+        self.m.copy_(s["m"].to(self.m.device))
+        self.v.copy_(s["v"].to(self.v.device))
+        self.step = int(s["step"])
+
+
+class FedRecModel(nn.Module):
+    def __init__(self, cfg: FedRecConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.text_encoder = TextEncoder(cfg)
+        self.user_encoder = UserEncoder(cfg)
+        if cfg.backbone.frozen:
+            for p in self.text_encoder.DistillBert.parameters():
+                p.requires_grad_(False)
+        self.flat: FlatParams | None = None
+
+    # -------------------------------------------------------------------------------
+    def trainable_named(self) -> List[Tuple[str, nn.Parameter]]:
+        return [(n, p) for n, p in self.named_parameters() if p.requires_grad]
+
+    def build_flat(self) -> FlatParams:
+        """Call after moving the model to its device."""
+        self.flat = FlatParams(self.trainable_named())
+        return self.flat
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        # copy in place so the flat views stay attached
+        res = super().load_state_dict(state_dict, strict=strict, assign=False)
+        self.text_encoder.DistillBert.invalidate()
+        return res
+
+    def num_params(self) -> Tuple[int, int]:
+        tot = sum(p.numel() for p in self.parameters())
+        tr = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        return tot, tr
+
+    def sync_tensors(self, full: bool) -> List[torch.Tensor]:
+        """What a round broadcast/average moves: the flat trainable buffer, or (``sync=full``,
+        Q15) every parameter like the reference (``server.py:76-77``)."""
+        if not full:
+            return [self.flat.flat] if self.flat is not None else [p.data for p in self.parameters() if p.requires_grad]
+        out = []
+        if self.flat is not None:
+            out.append(self.flat.flat)
+        out += [p.data for p in self.parameters() if not p.requires_grad]
+        return out

@@ -1,0 +1,166 @@
+"""Fused ops of the engine.
+
+Device tensors run the hand-written HIP/CDNA4 kernels of ``csrc/`` (``torch.ops.fedrec``);
+host tensors run the torch-eager oracle in :mod:`.reference` (the CPU/gloo plumbing
+configuration and the numerics reference of the tests).  On a device tensor a missing
+extension is an error -- there is no silent eager fallback.
+
+Kernel map:
+
+====================  ===========================  ===========================================
+op                    reference site               kernel (csrc/)
+====================  ===========================  ===========================================
+embed_ln              HF embeddings (K01)          embed_ln.hip: gather + pos add + LayerNorm
+linear                q/k/v/out/lin1/lin2, heads   gemm_bf16.hip: MFMA 16x16x32 bf16, fused
+                      (K02, K05, K06, K07)         bias / GELU / tanh / residual epilogues
+layer_norm            sa/output LN (K04)           layernorm.hip: one wave per row
+title_attention       HF attention (K03)           title_attn.hip: MFMA QK^T / PV, T pad 64
+additive_pool_*       attention.py:14-26 (K06/12)  additive_pool.hip: score, eps-softmax, pool
+user_attention_*      attention.py:32-82 (K11)     user_attn.hip: 20 heads x d_k 20
+score_ce              model.py:121-126 (K13)       score_ce.hip: sigmoid-CE fwd+bwd fused
+segment_sum_rows      client.py:26-48,87-89        news_grad.hip: deterministic segment sum
+                      (K16, K17)                   + LDP clip + Philox Gaussian noise
+adam_flat             model.py:89,93 (K20)         adam.hip: one pass over the flat buffer
+dedup / sample_batch  dataset.py:69-86 (K18)       batch.hip: on-device sampling + unique
+====================  ===========================  ===========================================
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import native
+from . import reference as ref
+
+_ACT = {"none": 0, "gelu": 1, "tanh": 2}
+
+
+def _dev(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ---------------------------------------------------------------------------------------
+def embed_ln(tokens, word, pos, ln_w, ln_b, eps: float, dtype=torch.float32):
+    if _dev(word):
+        return native.require_for(word).embed_ln(tokens.contiguous(), word, pos, ln_w, ln_b, float(eps))
+    return ref.embed_ln(tokens, word, pos, ln_w, ln_b, eps).to(dtype)
+
+
+def linear(x, w, b=None, act: str = "none", residual=None, out_dtype=None):
+    """``act(x @ w^T + b) + residual``; bf16 device inputs run the MFMA GEMM."""
+    if _dev(x) and x.dtype == torch.bfloat16:
+        return native.require_for(x).linear(x.contiguous(), w, b, _ACT[act], residual)
+    y = ref.linear(x, w, b, act, residual)
+    return y.to(out_dtype or x.dtype)
+
+
+def layer_norm(x, w, b, eps: float, dtype=None):
+    if _dev(x) and x.dtype == torch.bfloat16:
+        return native.require_for(x).layer_norm(x, w, b, float(eps))
+    return ref.layer_norm(x, w, b, eps).to(dtype or x.dtype)
+
+
+def title_attention(qkv, mask, n_heads: int):
+    if _dev(qkv) and qkv.dtype == torch.bfloat16:
+        return native.require_for(qkv).title_attention(qkv, mask.contiguous(), int(n_heads))
+    return ref.title_attention(qkv, mask, n_heads).to(qkv.dtype)
+
+
+def additive_pool_fwd(x, e, w2, b2) -> Tuple[torch.Tensor, torch.Tensor]:
+    """-> ``(pooled fp32 [n,D], alpha fp32 [n,T])``."""
+    if _dev(x):
+        return tuple(native.require_for(x).additive_pool_fwd(x.contiguous(), e.contiguous(),
+                                                             w2.reshape(-1).float().contiguous(),
+                                                             b2.reshape(-1).float().contiguous()))
+    return ref.additive_pool_fwd(x, e, w2, b2)
+
+
+def additive_pool_bwd(x, e, alpha, w2, g, want_dx: bool):
+    """-> ``(dx_direct|None, dpre, dw2, db2)`` with ``dpre = da w2 (1 - e^2)`` (tanh folded)."""
+    if _dev(x):
+        dx, dpre, dw2, db2 = native.require_for(x).additive_pool_bwd(
+            x.contiguous(), e.contiguous(), alpha.contiguous(), w2.reshape(-1).float().contiguous(),
+            g.float().contiguous(), bool(want_dx))
+        return (dx if want_dx else None), dpre, dw2, db2
+    dx, de, dw2, db2 = ref.additive_pool_bwd(x, e, alpha, w2, g)
+    dpre = de * (1.0 - e.float() ** 2)
+    return (dx if want_dx else None), dpre, dw2, db2
+
+
+def user_attention_fwd(qkv, heads: int, head_dim: int):
+    """-> ``(ctx [B,H,h*d], saved)``; ``saved`` is whatever the backward needs."""
+    if _dev(qkv):
+        return tuple(native.require_for(qkv).user_attention_fwd(qkv.contiguous(), heads, head_dim))
+    return ref.user_attention_fwd(qkv, heads, head_dim)
+
+
+def user_attention_bwd(qkv, saved, dctx, heads: int, head_dim: int):
+    if _dev(qkv):
+        return native.require_for(qkv).user_attention_bwd(qkv.contiguous(), saved, dctx.contiguous(),
+                                                          heads, head_dim)
+    return ref.user_attention_bwd(qkv, saved, dctx, heads, head_dim)
+
+
+def score_ce(cand, user, act: str = "sigmoid"):
+    """-> ``(loss [], scores [B,C], dcand [B,C,D], duser [B,D])`` (grads of the mean loss)."""
+    if _dev(cand):
+        return tuple(native.require_for(cand).score_ce(cand.float().contiguous(), user.float().contiguous(),
+                                                       1 if act == "sigmoid" else 0))
+    return ref.score_ce_fwd_bwd(cand, user, act)
+
+
+def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: float = 0.0,
+                     seed: int = 0, offset: int = 0, generator=None, seg=None):
+    """Per-news gradient reduction ``out[inv[r]] += clip(rows[r]) + N(0, noise_std)``.
+
+    ``seg = (perm, seg_ptr)`` (rows grouped by output id) enables the deterministic,
+    atomic-free device kernel; it is produced by :func:`dedup`.
+    """
+    if _dev(rows):
+        if seg is None:
+            perm, ptr = segments_from_inv(inv, num_out)
+        else:
+            perm, ptr = seg
+        return native.require_for(rows).segment_sum_rows(rows.float().contiguous(), perm, ptr, int(num_out),
+                                                         float(clip), float(noise_std), int(seed), int(offset))
+    if noise_std > 0 and generator is None:
+        generator = torch.Generator().manual_seed((int(seed) * 1_000_003 + int(offset)) & 0x7FFFFFFFFFFF)
+    return ref.segment_sum_rows(rows, inv, num_out, clip, noise_std, generator)
+
+
+def segments_from_inv(inv: torch.Tensor, num_out: int):
+    inv = inv.reshape(-1).long()
+    perm = torch.sort(inv, stable=True).indices.to(torch.int32)
+    cnt = torch.bincount(inv, minlength=num_out)
+    ptr = torch.zeros(num_out + 1, dtype=torch.int32, device=inv.device)
+    ptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    return perm, ptr
+
+
+def adam_flat(p, g, m, v, step: int, lr: float, b1: float, b2: float, eps: float,
+              grad_scale: float = 1.0, p_lowp: Optional[torch.Tensor] = None) -> None:
+    """One fused Adam step over flat fp32 buffers (torch.optim.Adam semantics)."""
+    if _dev(p):
+        bc1 = 1.0 - b1 ** step
+        bc2 = 1.0 - b2 ** step
+        native.require_for(p).adam_flat(p, g, m, v, p_lowp, float(lr), float(b1), float(b2), float(eps),
+                                        float(bc1), float(bc2), float(grad_scale))
+        return
+    ref.adam_step(p, g, m, v, step, lr, b1, b2, eps, grad_scale)
+    if p_lowp is not None:
+        p_lowp.copy_(p)
+
+
+def dedup(ids: torch.Tensor, num_news: int):
+    """Unique news ids of a batch -> ``(uniq [U], inv [R], perm [R], seg_ptr [U+1])``.
+
+    ``uniq`` is sorted (deterministic), ``inv[r]`` maps each occurrence to its row of
+    ``uniq``, ``perm``/``seg_ptr`` group occurrences by row for :func:`segment_sum_rows`.
+    """
+    flat = ids.reshape(-1)
+    if _dev(flat):
+        return tuple(native.require_for(flat).dedup(flat.to(torch.int32).contiguous(), int(num_news)))
+    uniq, inv = torch.unique(flat.long(), sorted=True, return_inverse=True)
+    perm, ptr = segments_from_inv(inv, uniq.numel())
+    return uniq.to(torch.int32), inv.to(torch.int32), perm, ptr

@@ -1,0 +1,123 @@
+"""Autograd wiring of the fused ops.
+
+Each ``Function`` has a hand-written forward *and* backward kernel pair (device) or the
+oracle pair (host); torch autograd only strings them together.  The small user-side
+projections (``[B*H, 400] x [400, 1200]``) and the head FC stay plain library GEMMs.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .. import ops
+
+
+class AdditivePoolFn(torch.autograd.Function):
+    """``AdditiveAttention`` (``attention.py:8-26``): ``x [n,T,D] -> [n,D]``.
+
+    Forward: ``e = tanh(x W1^T + b1)`` (GEMM with a tanh epilogue), then the fused
+    score / eps-softmax / weighted-sum kernel.  Backward: the fused kernel yields
+    ``alpha g`` and ``dpre = da w2 (1 - e^2)``; ``dW1 = dpre^T x``, ``dx += dpre W1``.
+    """
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        n, T, D = x.shape
+        x2 = x.reshape(n * T, D)
+        w1c = w1.to(x.dtype) if x.dtype != w1.dtype else w1
+        e = ops.linear(x2, w1c, b1.float() if x.dtype == torch.bfloat16 else b1, act="tanh")
+        e = e.reshape(n, T, -1)
+        pooled, alpha = ops.additive_pool_fwd(x, e, w2, b2)
+        ctx.save_for_backward(x, e, alpha, w1, w2)
+        return pooled
+
+    @staticmethod
+    def backward(ctx, g):
+        x, e, alpha, w1, w2 = ctx.saved_tensors
+        want_dx = ctx.needs_input_grad[0]
+        dx_dir, dpre, dw2, db2 = ops.additive_pool_bwd(x, e, alpha, w2, g, want_dx)
+        n, T, D = x.shape
+        dpre2 = dpre.reshape(n * T, -1)
+        x2 = x.reshape(n * T, D)
+        dw1 = db1 = None
+        if ctx.needs_input_grad[1]:
+            dw1 = dpre2.float().t() @ x2.float()
+        if ctx.needs_input_grad[2]:
+            db1 = dpre2.float().sum(0)
+        dx = None
+        if want_dx:
+            dx = (dx_dir.float() + (dpre2.float() @ w1.float()).reshape(n, T, D)).to(x.dtype)
+        return dx, dw1, db1, dw2.reshape(1, -1).to(w2.dtype), db2.reshape(1).to(w2.dtype)
+
+
+class UserAttentionFn(torch.autograd.Function):
+    """``ScaledDotProductAttention`` over 20 heads x d_k 20 (``attention.py:32-82``)."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads: int, head_dim: int):
+        out, saved = ops.user_attention_fwd(qkv, heads, head_dim)
+        ctx.save_for_backward(qkv, saved)
+        ctx.heads, ctx.head_dim = heads, head_dim
+        return out
+
+    @staticmethod
+    def backward(ctx, dctx):
+        qkv, saved = ctx.saved_tensors
+        return ops.user_attention_bwd(qkv, saved, dctx, ctx.heads, ctx.head_dim), None, None
+
+
+class ScoreCEFn(torch.autograd.Function):
+    """``CE(sigmoid(<cand, u>), 0)`` with the gradients computed in the same kernel."""
+
+    @staticmethod
+    def forward(ctx, cand, user, act: str = "sigmoid"):
+        loss, scores, dcand, duser = ops.score_ce(cand, user, act)
+        ctx.save_for_backward(dcand, duser)
+        ctx.mark_non_differentiable(scores)
+        return loss, scores
+
+    @staticmethod
+    def backward(ctx, gloss, gscores):
+        dcand, duser = ctx.saved_tensors
+        return dcand * gloss, duser * gloss, None
+
+
+class NewsGatherFn(torch.autograd.Function):
+    """Rows of the per-batch news table for every candidate/history occurrence.
+
+    Backward is the per-news gradient reduction of the reference (``client.py:26-48``,
+    ``model.py:105-109``) with the optional LDP step (``client.py:87-89``) fused in:
+    per-occurrence clip + Gaussian noise, then a deterministic segment sum.
+    """
+
+    @staticmethod
+    def forward(ctx, table, inv, perm, seg_ptr, clip: float, noise_std: float, seed: int, offset: int):
+        ctx.save_for_backward(inv, perm, seg_ptr)
+        ctx.n = table.shape[0]
+        ctx.ldp = (clip, noise_std, seed, offset)
+        return table.index_select(0, inv.long())
+
+    @staticmethod
+    def backward(ctx, g):
+        inv, perm, seg_ptr = ctx.saved_tensors
+        clip, noise, seed, offset = ctx.ldp
+        d = ops.segment_sum_rows(g, inv, ctx.n, clip, noise, seed, offset, seg=(perm, seg_ptr))
+        return d, None, None, None, None, None, None, None
+
+
+def additive_pool(x, lin1: torch.nn.Linear, lin2: torch.nn.Linear):
+    return AdditivePoolFn.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+
+
+def user_attention(qkv, heads: int, head_dim: int):
+    return UserAttentionFn.apply(qkv, heads, head_dim)
+
+
+def score_ce(cand, user, act: str = "sigmoid") -> Tuple[torch.Tensor, torch.Tensor]:
+    return ScoreCEFn.apply(cand, user, act)
+
+
+def news_gather(table, inv, perm, seg_ptr, clip: float = 0.0, noise_std: float = 0.0,
+                seed: int = 0, offset: int = 0):
+    return NewsGatherFn.apply(table, inv, perm, seg_ptr, clip, noise_std, seed, offset)

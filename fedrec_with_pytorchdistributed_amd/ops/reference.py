@@ -1,0 +1,220 @@
+"""Torch-eager oracle for every fused op (fp32).  This is both the CPU execution path
+(BASELINE config 1: CPU/gloo plumbing) and the numerics reference that each HIP kernel is
+tested against.
+
+Math is traced to the reference:
+
+* DistilBERT block: HF post-LN block; attention scores ``q k^T / sqrt(d)`` with key padding
+  filled with ``finfo.min`` (so an all-zero mask -- news row 0 -- gives a *uniform*
+  softmax, E1/K03), GELU(erf) FFN, LayerNorm eps 1e-12.
+* Additive attention (``attention.py:14-26``): ``alpha = exp(a) / (sum exp(a) + 1e-8)``
+  with ``a = w2 . tanh(W1 x + b1) + b2``; no mask (Q7).
+* Scaled dot-product attention (``attention.py:37-45``): ``A = exp(S) / (rowsum + 1e-8)``,
+  no max subtraction (Q8), no mask.
+* Score (``model.py:121-126``): ``CE(sigmoid(<cand, u>), label=0)``, mean over the batch.
+
+The eps-normalised softmaxes are evaluated in the algebraically identical stable form
+``exp(s - m) / (sum exp(s - m) + eps * exp(-m))`` (identical in exact arithmetic; the
+literal form overflows for scores > 88).  ``literal=True`` selects the reference's form.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+EPS_SOFTMAX = 1e-8
+
+
+# ---------------------------------------------------------------------------------------
+# eps-softmax helpers
+# ---------------------------------------------------------------------------------------
+def eps_softmax(s: torch.Tensor, dim: int, eps: float = EPS_SOFTMAX, literal: bool = False) -> torch.Tensor:
+    if literal:
+        e = torch.exp(s)
+        return e / (e.sum(dim, keepdim=True) + eps)
+    m = s.amax(dim, keepdim=True).clamp_min(-1e30)
+    e = torch.exp(s - m)
+    return e / (e.sum(dim, keepdim=True) + eps * torch.exp(-m))
+
+
+def eps_softmax_backward(p: torch.Tensor, dp: torch.Tensor, dim: int) -> torch.Tensor:
+    """``d s`` for ``p = eps_softmax(s)``: the eps term only rescales, so the Jacobian keeps
+    the softmax form ``p (dp - sum p dp)``."""
+    return p * (dp - (p * dp).sum(dim, keepdim=True))
+
+
+# ---------------------------------------------------------------------------------------
+# text backbone (DistilBERT-shaped) pieces
+# ---------------------------------------------------------------------------------------
+def embed_ln(tokens: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, ln_w: torch.Tensor,
+             ln_b: torch.Tensor, eps: float) -> torch.Tensor:
+    """``LN(word[tok] + pos[0..T-1])`` -> ``[n*T, D]`` (HF Embeddings, eval mode)."""
+    n, T = tokens.shape
+    x = word[tokens.long()] + pos[:T].unsqueeze(0)
+    x = F.layer_norm(x.float(), (word.shape[1],), ln_w.float(), ln_b.float(), eps)
+    return x.reshape(n * T, -1)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "none",
+           residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    y = x.float() @ w.float().t()
+    if b is not None:
+        y = y + b.float()
+    if act == "gelu":
+        y = F.gelu(y)  # erf form (HF "gelu")
+    elif act == "tanh":
+        y = torch.tanh(y)
+    elif act != "none":
+        raise ValueError(act)
+    if residual is not None:
+        y = y + residual.float()
+    return y
+
+
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+
+
+def title_attention(qkv: torch.Tensor, mask: torch.Tensor, n_heads: int) -> torch.Tensor:
+    """HF DistilBERT eager attention.  ``qkv`` ``[n*T, 3D]`` (q | k | v), ``mask`` ``[n, T]``."""
+    n, T = mask.shape
+    D = qkv.shape[1] // 3
+    dh = D // n_heads
+    q, k, v = qkv.float().view(n, T, 3, n_heads, dh).permute(2, 0, 3, 1, 4)
+    q = q / math.sqrt(dh)
+    s = q @ k.transpose(-1, -2)  # [n, h, T, T]
+    keep = (mask != 0).view(n, 1, 1, T)
+    s = s.masked_fill(~keep, torch.finfo(torch.float32).min)
+    p = torch.softmax(s, dim=-1)
+    ctx = p @ v  # [n, h, T, dh]
+    return ctx.permute(0, 2, 1, 3).reshape(n * T, D)
+
+
+def backbone_forward(tokens: torch.Tensor, mask: torch.Tensor, params: dict, n_layers: int,
+                     n_heads: int, eps: float) -> torch.Tensor:
+    """Whole frozen backbone in eval mode -> last hidden state ``[n*T, D]`` (fp32)."""
+    x = embed_ln(tokens, params["word"], params["pos"], params["emb_ln_w"], params["emb_ln_b"], eps)
+    for i in range(n_layers):
+        L = params["layers"][i]
+        qkv = linear(x, L["wqkv"], L["bqkv"])
+        ctx = title_attention(qkv, mask, n_heads)
+        h = linear(ctx, L["wo"], L["bo"], residual=x)
+        x = layer_norm(h, L["ln1_w"], L["ln1_b"], eps)
+        f = linear(x, L["w1"], L["b1"], act="gelu")
+        h = linear(f, L["w2"], L["b2"], residual=x)
+        x = layer_norm(h, L["ln2_w"], L["ln2_b"], eps)
+    return x
+
+
+# ---------------------------------------------------------------------------------------
+# additive attention pooling (text head and user encoder)
+# ---------------------------------------------------------------------------------------
+def additive_pool_fwd(x: torch.Tensor, e: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+                      literal: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``x [n,T,D]``, ``e = tanh(W1 x + b1) [n,T,Q]`` -> ``(pooled [n,D], alpha [n,T])``."""
+    a = e.float() @ w2.float().reshape(-1) + b2.float().reshape(())
+    alpha = eps_softmax(a, dim=1, literal=literal)
+    pooled = torch.einsum("nt,ntd->nd", alpha, x.float())
+    return pooled, alpha
+
+
+def additive_pool_bwd(x: torch.Tensor, e: torch.Tensor, alpha: torch.Tensor, w2: torch.Tensor,
+                      g: torch.Tensor):
+    """Backward of :func:`additive_pool_fwd` -> ``(dx_direct [n,T,D], de [n,T,Q], dw2 [Q], db2 [])``.
+
+    ``dx_direct`` is the ``alpha_t g`` term only; the ``W1^T dpre`` term is added by the
+    caller (``dpre = de * (1 - e^2)``: ``e`` is a tanh output).
+    """
+    xf, ef, g = x.float(), e.float(), g.float()
+    dalpha = torch.einsum("ntd,nd->nt", xf, g)
+    da = eps_softmax_backward(alpha, dalpha, dim=1)
+    dx = alpha.unsqueeze(-1) * g.unsqueeze(1)
+    de = da.unsqueeze(-1) * w2.float().reshape(1, 1, -1)
+    dw2 = torch.einsum("nt,ntq->q", da, ef)
+    db2 = da.sum()
+    return dx, de, dw2, db2
+
+
+# ---------------------------------------------------------------------------------------
+# user-side multi-head attention (attention.py:32-82)
+# ---------------------------------------------------------------------------------------
+def user_attention_fwd(qkv: torch.Tensor, n_heads: int, head_dim: int,
+                       literal: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``qkv [B,H,3*h*d]`` -> ``(ctx [B,H,h*d], A [B,h,H,H])``."""
+    B, H, _ = qkv.shape
+    q, k, v = qkv.float().view(B, H, 3, n_heads, head_dim).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / math.sqrt(head_dim)
+    A = eps_softmax(s, dim=-1, literal=literal)
+    ctx = (A @ v).permute(0, 2, 1, 3).reshape(B, H, n_heads * head_dim)
+    return ctx, A
+
+
+def user_attention_bwd(qkv: torch.Tensor, A: torch.Tensor, dctx: torch.Tensor, n_heads: int,
+                       head_dim: int) -> torch.Tensor:
+    B, H, _ = qkv.shape
+    q, k, v = qkv.float().view(B, H, 3, n_heads, head_dim).permute(2, 0, 3, 1, 4)
+    dc = dctx.float().view(B, H, n_heads, head_dim).permute(0, 2, 1, 3)
+    dA = dc @ v.transpose(-1, -2)
+    dv = A.transpose(-1, -2) @ dc
+    dS = eps_softmax_backward(A, dA, dim=-1) / math.sqrt(head_dim)
+    dq = dS @ k
+    dk = dS.transpose(-1, -2) @ q
+    d = torch.stack([dq, dk, dv], 0)  # [3,B,h,H,d]
+    return d.permute(1, 3, 0, 2, 4).reshape(B, H, 3 * n_heads * head_dim)
+
+
+# ---------------------------------------------------------------------------------------
+# scoring + loss (model.py:121-126)
+# ---------------------------------------------------------------------------------------
+def score_ce_fwd_bwd(cand: torch.Tensor, user: torch.Tensor, act: str = "sigmoid",
+                     label: int = 0):
+    """Returns ``(loss, scores [B,C], dcand [B,C,D], duser [B,D])`` for a mean CE over the
+    batch with target column ``label`` (always 0 in the reference, ``dataset.py:85``)."""
+    c, u = cand.float(), user.float()
+    z = torch.einsum("bcd,bd->bc", c, u)
+    s = torch.sigmoid(z) if act == "sigmoid" else z
+    B = s.shape[0]
+    lse = torch.logsumexp(s, dim=1)
+    loss = (lse - s[:, label]).mean()
+    ds = torch.softmax(s, dim=1)
+    ds[:, label] -= 1.0
+    ds = ds / B
+    dz = ds * s * (1.0 - s) if act == "sigmoid" else ds
+    dcand = dz.unsqueeze(-1) * u.unsqueeze(1)
+    duser = torch.einsum("bc,bcd->bd", dz, c)
+    return loss, s, dcand, duser
+
+
+# ---------------------------------------------------------------------------------------
+# per-news gradient reduction (+ LDP) : client.py:26-48, 87-89; model.py:105-109
+# ---------------------------------------------------------------------------------------
+def segment_sum_rows(rows: torch.Tensor, inv: torch.Tensor, num_out: int,
+                     clip: float = 0.0, noise_std: float = 0.0,
+                     generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """``out[inv[r]] += clip_r(rows[r]) + N(0, noise_std)`` -> ``[num_out, D]`` (fp32)."""
+    g = rows.float()
+    if clip > 0:
+        nrm = g.norm(dim=1, keepdim=True)
+        g = g * torch.clamp(clip / (nrm + 1e-12), max=1.0)
+    if noise_std > 0:
+        g = g + torch.randn(g.shape, generator=generator, device=g.device) * noise_std
+    out = torch.zeros(num_out, g.shape[1], dtype=torch.float32, device=g.device)
+    out.index_add_(0, inv.long(), g)
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# Adam (torch defaults: no weight decay, no amsgrad; bias correction)
+# ---------------------------------------------------------------------------------------
+def adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int,
+              lr: float, b1: float, b2: float, eps: float, grad_scale: float = 1.0) -> None:
+    gs = g * grad_scale
+    m.mul_(b1).add_(gs, alpha=1 - b1)
+    v.mul_(b2).addcmul_(gs, gs, value=1 - b2)
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
