@@ -1,0 +1,107 @@
+// On-device batch builder: news-id de-duplication for one training step.
+//
+// The reference encodes every candidate/history occurrence separately (model.py:41-61;
+// E8: 39 unique titles out of 324 encoded).  This kernel turns the R = B*(C+H) occurrence
+// ids of a batch into
+//   uniq[U]      sorted unique news ids        -> the only titles the backbone encodes
+//   inv[R]       occurrence -> row of uniq     -> gather of news vectors
+//   perm[R]      occurrences grouped by row    -> deterministic per-news gradient sums
+//   seg_ptr[U+1] segment offsets into perm     (replaces the host dict of client.py:26-48)
+// in ONE workgroup: a bitonic sort of (id << 32 | occurrence) keys in LDS (stable by
+// construction), then a block-wide scan of the "new id" flags.  R <= 8192 (64 KB of keys);
+// larger batches take the sort-based torch path on the host side of the binding.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXR = 8192;
+constexpr int NT = 1024;
+
+__global__ __launch_bounds__(NT) void dedup_kernel(const int* __restrict__ ids, int R, int P, int* __restrict__ uniq,
+                                                   int* __restrict__ inv, int* __restrict__ perm,
+                                                   int* __restrict__ seg_ptr, int* __restrict__ u_count) {
+  __shared__ unsigned long long key[MAXR];
+  __shared__ int part[NT];
+  __shared__ int wsum[NT / 64];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < P; i += NT)
+    key[i] = i < R ? (((unsigned long long)(unsigned)ids[i]) << 32) | (unsigned)i : ~0ull;
+  __syncthreads();
+  // bitonic sort, ascending
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += NT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = key[i], b = key[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            key[i] = b;
+            key[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // flags + block scan: thread handles a contiguous run of E elements
+  const int E = (R + NT - 1) / NT;
+  const int b0 = tid * E;
+  int cnt = 0;
+  for (int e = 0; e < E; ++e) {
+    const int i = b0 + e;
+    if (i < R) cnt += (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32)) ? 1 : 0;
+  }
+  // inclusive scan of cnt over the block
+  const int lane = tid & 63, w = tid >> 6;
+  int x = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (w == 0) {
+    int s = lane < NT / 64 ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(s, o, 64);
+      if (lane >= o) s += y;
+    }
+    if (lane < NT / 64) wsum[lane] = s;
+  }
+  __syncthreads();
+  int run = x - cnt + (w > 0 ? wsum[w - 1] : 0);  // exclusive prefix of this thread's run
+  for (int e = 0; e < E; ++e) {
+    const int i = b0 + e;
+    if (i >= R) break;
+    const int id = (int)(key[i] >> 32);
+    const int r = (int)(key[i] & 0xffffffffu);
+    const bool f = (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32));
+    if (f) {
+      uniq[run] = id;
+      seg_ptr[run] = i;
+      ++run;
+    }
+    perm[i] = r;
+    inv[r] = run - 1;
+  }
+  if (tid == NT - 1) {
+    const int U = wsum[NT / 64 - 1];
+    *u_count = U;
+    seg_ptr[U] = R;
+  }
+  (void)part;
+}
+
+}  // namespace
+
+extern "C" int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count,
+                        hipStream_t s) {
+  if (R > MAXR || R < 1) return 1;
+  int P = 1;
+  while (P < R) P <<= 1;
+  hipLaunchKernelGGL(dedup_kernel, dim3(1), dim3(NT), 0, s, ids, R, P, uniq, inv, perm, seg_ptr, u_count);
+  return 0;
+}

@@ -1,0 +1,353 @@
+// torch.ops.fedrec.* registrations for the gfx950 kernels (TORCH_LIBRARY; no pybind).
+//
+// Each op validates shapes/dtypes on the host (a kernel never sees a shape it was not
+// written for), allocates outputs with the caching allocator, and launches on the current
+// HIP stream.  The kernels live in *.hip files compiled without torch headers; they export
+// plain C launchers (fr_*) that return a non-zero code for an unsupported shape.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <tuple>
+
+extern "C" {
+int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K,
+                    int act, hipStream_t s);
+int fr_layer_norm_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
+                       hipStream_t s);
+int fr_embed_ln_bf16(const int* tokens, const void* word, const void* pos, const float* w, const float* b, void* y,
+                     int rows, int D, int T, float eps, hipStream_t s);
+int fr_title_attention_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
+                            hipStream_t s);
+int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const float* b2, float* out, float* alpha,
+                         int n, int T, int D, int Q, int is_bf16, hipStream_t s);
+int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g, float* dx,
+                         void* dpre, float* dw2, float* db2, int n, int T, int D, int Q, int is_bf16, hipStream_t s);
+int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, hipStream_t s);
+int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
+                     int dk, hipStream_t s);
+int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
+                int C, int D, int sigm, hipStream_t s);
+int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, float* out, int U, int D, float clip,
+                        float noise_std, unsigned long long seed, unsigned long long offset, hipStream_t s);
+int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
+                 float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
+int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count, hipStream_t s);
+int fr_secagg_mask(const float* x, int* out, long n, float scale, float clipv, const unsigned long long* seeds,
+                   const int* signs, int npeers, unsigned long long round, hipStream_t s);
+int fr_secagg_unmask(const int* x, float* out, long n, float inv_scale, hipStream_t s);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "fedrec: ", name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), "fedrec: ", name, " must be contiguous");
+}
+
+void check_rc(int rc, const char* op) { TORCH_CHECK(rc == 0, "fedrec::", op, ": unsupported shape (code ", rc, ")"); }
+
+at::Tensor linear(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b, int64_t act,
+                  const c10::optional<at::Tensor>& residual) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "fedrec::linear: bf16 x/w");
+  const c10::DeviceGuard g(x.device());
+  const int64_t K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "fedrec::linear: K mismatch");
+  const int64_t M = x.numel() / K;
+  auto out_shape = x.sizes().vec();
+  out_shape.back() = N;
+  auto out = at::empty(out_shape, x.options());
+  const float* bp = nullptr;
+  at::Tensor bf;
+  if (b.has_value() && b->defined()) {
+    bf = b->to(at::kFloat).contiguous();
+    TORCH_CHECK(bf.numel() == N, "fedrec::linear: bias size");
+    bp = bf.data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    check_dev(*residual, "residual");
+    TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->numel() == M * N, "fedrec::linear: residual");
+    rp = residual->data_ptr();
+  }
+  if (M == 0) return out;
+  check_rc(fr_gemm_nt_bf16(x.data_ptr(), w.data_ptr(), bp, rp, out.data_ptr(), (int)M, (int)N, (int)K, (int)act,
+                           cur_stream()),
+           "linear");
+  return out;
+}
+
+at::Tensor layer_norm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::layer_norm: bf16");
+  const c10::DeviceGuard g(x.device());
+  const int64_t D = x.size(-1);
+  auto wf = w.to(at::kFloat).contiguous(), bf = b.to(at::kFloat).contiguous();
+  auto y = at::empty_like(x);
+  check_rc(fr_layer_norm_bf16(x.data_ptr(), wf.data_ptr<float>(), bf.data_ptr<float>(), y.data_ptr(),
+                              (int)(x.numel() / D), (int)D, (float)eps, cur_stream()),
+           "layer_norm");
+  return y;
+}
+
+at::Tensor embed_ln(const at::Tensor& tokens, const at::Tensor& word, const at::Tensor& pos, const at::Tensor& w,
+                    const at::Tensor& b, double eps) {
+  check_dev(word, "word");
+  check_dev(pos, "pos");
+  TORCH_CHECK(word.scalar_type() == at::kBFloat16 && pos.scalar_type() == at::kBFloat16, "fedrec::embed_ln: bf16");
+  const c10::DeviceGuard g(word.device());
+  auto tok = tokens.to(at::kInt).contiguous();
+  TORCH_CHECK(tok.dim() == 2, "fedrec::embed_ln: tokens [n, T]");
+  const int64_t n = tok.size(0), T = tok.size(1), D = word.size(1);
+  TORCH_CHECK(T <= pos.size(0), "fedrec::embed_ln: T > max positions");
+  auto wf = w.to(at::kFloat).contiguous(), bf = b.to(at::kFloat).contiguous();
+  auto y = at::empty({n * T, D}, word.options());
+  check_rc(fr_embed_ln_bf16(tok.data_ptr<int>(), word.data_ptr(), pos.data_ptr(), wf.data_ptr<float>(),
+                            bf.data_ptr<float>(), y.data_ptr(), (int)(n * T), (int)D, (int)T, (float)eps, cur_stream()),
+           "embed_ln");
+  return y;
+}
+
+at::Tensor title_attention(const at::Tensor& qkv, const at::Tensor& mask, int64_t n_heads) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16, "fedrec::title_attention: bf16");
+  const c10::DeviceGuard g(qkv.device());
+  auto mk = mask.to(at::kInt).contiguous();
+  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
+  TORCH_CHECK(qkv.numel() == n * T * 3 * D, "fedrec::title_attention: qkv shape");
+  auto out = at::empty({n * T, D}, qkv.options());
+  check_rc(fr_title_attention_bf16(qkv.data_ptr(), mk.data_ptr<int>(), out.data_ptr(), (int)n, (int)T, (int)n_heads,
+                                   (int)D, cur_stream()),
+           "title_attention");
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> additive_pool_fwd(const at::Tensor& x, const at::Tensor& e, const at::Tensor& w2,
+                                                     const at::Tensor& b2) {
+  check_dev(x, "x");
+  check_dev(e, "e");
+  TORCH_CHECK(x.dim() == 3 && e.dim() == 3 && x.scalar_type() == e.scalar_type(), "fedrec::additive_pool_fwd");
+  const c10::DeviceGuard g(x.device());
+  const int64_t n = x.size(0), T = x.size(1), D = x.size(2), Q = e.size(2);
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || x.scalar_type() == at::kFloat, "fedrec::additive_pool_fwd: dtype");
+  auto out = at::empty({n, D}, x.options().dtype(at::kFloat));
+  auto alpha = at::empty({n, T}, x.options().dtype(at::kFloat));
+  check_rc(fr_additive_pool_fwd(x.data_ptr(), e.data_ptr(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+                                out.data_ptr<float>(), alpha.data_ptr<float>(), (int)n, (int)T, (int)D, (int)Q, bf,
+                                cur_stream()),
+           "additive_pool_fwd");
+  return {out, alpha};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(const at::Tensor& x, const at::Tensor& e,
+                                                                             const at::Tensor& alpha,
+                                                                             const at::Tensor& w2, const at::Tensor& g,
+                                                                             bool want_dx) {
+  check_dev(x, "x");
+  check_dev(e, "e");
+  check_dev(alpha, "alpha");
+  check_dev(g, "g");
+  const c10::DeviceGuard dg(x.device());
+  const int64_t n = x.size(0), T = x.size(1), D = x.size(2), Q = e.size(2);
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor dx = want_dx ? at::empty({n, T, D}, fopt) : at::empty({0}, fopt);
+  auto dpre = at::empty({n, T, Q}, e.options());
+  auto dw2 = at::zeros({Q}, fopt);
+  auto db2 = at::zeros({1}, fopt);
+  check_rc(fr_additive_pool_bwd(x.data_ptr(), e.data_ptr(), alpha.data_ptr<float>(), w2.data_ptr<float>(),
+                                g.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr, dpre.data_ptr(),
+                                dw2.data_ptr<float>(), db2.data_ptr<float>(), (int)n, (int)T, (int)D, (int)Q, bf,
+                                cur_stream()),
+           "additive_pool_bwd");
+  return {dx, dpre, dw2, db2};
+}
+
+std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int64_t heads, int64_t head_dim) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.dim() == 3, "fedrec::user_attention_fwd: fp32 [B,H,3D]");
+  const c10::DeviceGuard g(qkv.device());
+  const int64_t B = qkv.size(0), H = qkv.size(1);
+  TORCH_CHECK(qkv.size(2) == 3 * heads * head_dim, "fedrec::user_attention_fwd: width");
+  auto ctx = at::empty({B, H, heads * head_dim}, qkv.options());
+  auto stats = at::empty({B, heads, H, 2}, qkv.options());
+  check_rc(fr_user_attn_fwd(qkv.data_ptr<float>(), ctx.data_ptr<float>(), stats.data_ptr<float>(), (int)B, (int)H,
+                            (int)heads, (int)head_dim, cur_stream()),
+           "user_attention_fwd");
+  return {ctx, stats};
+}
+
+at::Tensor user_attention_bwd(const at::Tensor& qkv, const at::Tensor& stats, const at::Tensor& dctx, int64_t heads,
+                              int64_t head_dim) {
+  check_dev(qkv, "qkv");
+  check_dev(stats, "stats");
+  check_dev(dctx, "dctx");
+  const c10::DeviceGuard g(qkv.device());
+  const int64_t B = qkv.size(0), H = qkv.size(1);
+  auto d = dctx.to(at::kFloat).contiguous();
+  auto dqkv = at::empty_like(qkv);
+  check_rc(fr_user_attn_bwd(qkv.data_ptr<float>(), stats.data_ptr<float>(), d.data_ptr<float>(), dqkv.data_ptr<float>(),
+                            (int)B, (int)H, (int)heads, (int)head_dim, cur_stream()),
+           "user_attention_bwd");
+  return dqkv;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Tensor& cand, const at::Tensor& user,
+                                                                    int64_t act) {
+  check_dev(cand, "cand");
+  check_dev(user, "user");
+  TORCH_CHECK(cand.scalar_type() == at::kFloat && user.scalar_type() == at::kFloat, "fedrec::score_ce: fp32");
+  const c10::DeviceGuard g(cand.device());
+  const int64_t B = cand.size(0), C = cand.size(1), D = cand.size(2);
+  TORCH_CHECK(user.size(0) == B && user.size(1) == D, "fedrec::score_ce: user shape");
+  auto loss = at::empty({}, cand.options());
+  auto scores = at::empty({B, C}, cand.options());
+  auto dcand = at::empty_like(cand);
+  auto duser = at::empty_like(user);
+  check_rc(fr_score_ce(cand.data_ptr<float>(), user.data_ptr<float>(), loss.data_ptr<float>(), scores.data_ptr<float>(),
+                       dcand.data_ptr<float>(), duser.data_ptr<float>(), (int)B, (int)C, (int)D, (int)act,
+                       cur_stream()),
+           "score_ce");
+  return {loss, scores, dcand, duser};
+}
+
+at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, const at::Tensor& seg_ptr, int64_t num_out,
+                            double clip, double noise_std, int64_t seed, int64_t offset) {
+  check_dev(rows, "rows");
+  check_dev(perm, "perm");
+  check_dev(seg_ptr, "seg_ptr");
+  TORCH_CHECK(rows.scalar_type() == at::kFloat && perm.scalar_type() == at::kInt && seg_ptr.scalar_type() == at::kInt,
+              "fedrec::segment_sum_rows: dtypes");
+  TORCH_CHECK(seg_ptr.numel() == num_out + 1, "fedrec::segment_sum_rows: seg_ptr size");
+  const c10::DeviceGuard g(rows.device());
+  const int64_t D = rows.size(-1);
+  auto out = at::empty({num_out, D}, rows.options());
+  check_rc(fr_segment_sum_rows(rows.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(),
+                               out.data_ptr<float>(), (int)num_out, (int)D, (float)clip, (float)noise_std,
+                               (unsigned long long)seed, (unsigned long long)offset, cur_stream()),
+           "segment_sum_rows");
+  return out;
+}
+
+void adam_flat(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, const c10::optional<at::Tensor>& plow,
+               double lr, double b1, double b2, double eps, double bc1, double bc2, double grad_scale) {
+  check_dev(p, "p");
+  check_dev(g, "g");
+  check_dev(m, "m");
+  check_dev(v, "v");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(),
+              "fedrec::adam_flat: fp32 flat buffers of one size");
+  void* lp = nullptr;
+  if (plow.has_value() && plow->defined()) {
+    check_dev(*plow, "p_lowp");
+    TORCH_CHECK(plow->scalar_type() == at::kBFloat16 && plow->numel() == p.numel(), "fedrec::adam_flat: p_lowp");
+    lp = plow->data_ptr();
+  }
+  const c10::DeviceGuard dg(p.device());
+  check_rc(fr_adam_flat(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), lp,
+                        (long)p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)bc1, (float)bc2,
+                        (float)grad_scale, cur_stream()),
+           "adam_flat");
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dedup(const at::Tensor& ids, int64_t num_news) {
+  check_dev(ids, "ids");
+  TORCH_CHECK(ids.scalar_type() == at::kInt && ids.dim() == 1, "fedrec::dedup: int32 [R]");
+  const c10::DeviceGuard g(ids.device());
+  const int64_t R = ids.numel();
+  auto opt = ids.options();
+  if (R == 0 || R > 8192) {  // large batches: sort-based path (still on the device)
+    auto sorted = at::sort(ids.to(at::kLong), /*stable=*/true, 0, false);
+    auto sid = std::get<0>(sorted);
+    auto perm = std::get<1>(sorted).to(at::kInt);
+    auto uq = std::get<0>(at::_unique2(sid, true, true, true));
+    (void)num_news;
+    auto flags = at::ones({R}, opt);
+    if (R > 1) flags.slice(0, 1).copy_(sid.slice(0, 1).ne(sid.slice(0, 0, R - 1)).to(at::kInt));
+    auto rank = at::cumsum(flags, 0).to(at::kInt) - 1;
+    auto inv = at::empty({R}, opt);
+    inv.index_put_({perm.to(at::kLong)}, rank);
+    const int64_t U = uq.numel();
+    auto counts = at::bincount(rank.to(at::kLong), {}, U);
+    auto seg = at::zeros({U + 1}, opt);
+    seg.slice(0, 1).copy_(at::cumsum(counts, 0).to(at::kInt));
+    return {uq.to(at::kInt), inv, perm, seg};
+  }
+  auto uniq = at::empty({R}, opt);
+  auto inv = at::empty({R}, opt);
+  auto perm = at::empty({R}, opt);
+  auto seg = at::empty({R + 1}, opt);
+  auto ucount = at::empty({1}, opt);
+  check_rc(fr_dedup(ids.data_ptr<int>(), (int)R, uniq.data_ptr<int>(), inv.data_ptr<int>(), perm.data_ptr<int>(),
+                    seg.data_ptr<int>(), ucount.data_ptr<int>(), cur_stream()),
+           "dedup");
+  const int64_t U = ucount.item<int>();  // the backbone grid depends on U: one small D2H per step
+  return {uniq.slice(0, 0, U), inv, perm, seg.slice(0, 0, U + 1)};
+}
+
+std::tuple<at::Tensor> secagg_mask(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs, double scale,
+                                   double clipv, int64_t round) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "fedrec::secagg_mask: fp32");
+  const c10::DeviceGuard g(x.device());
+  auto sd = seeds.to(x.device(), at::kLong).contiguous();
+  auto sg = signs.to(x.device(), at::kInt).contiguous();
+  auto out = at::empty(x.sizes(), x.options().dtype(at::kInt));
+  check_rc(fr_secagg_mask(x.data_ptr<float>(), out.data_ptr<int>(), (long)x.numel(), (float)scale, (float)clipv,
+                          (const unsigned long long*)sd.data_ptr<int64_t>(), sg.data_ptr<int>(), (int)sd.numel(),
+                          (unsigned long long)round, cur_stream()),
+           "secagg_mask");
+  return {out};
+}
+
+at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kInt, "fedrec::secagg_unmask: int32");
+  const c10::DeviceGuard g(x.device());
+  auto out = at::empty(x.sizes(), x.options().dtype(at::kFloat));
+  check_rc(fr_secagg_unmask(x.data_ptr<int>(), out.data_ptr<float>(), (long)x.numel(), (float)inv_scale, cur_stream()),
+           "secagg_unmask");
+  return out;
+}
+
+}  // namespace
+
+TORCH_LIBRARY(fedrec, m) {
+  m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
+  m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps) -> Tensor");
+  m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
+  m.def("title_attention(Tensor qkv, Tensor mask, int n_heads) -> Tensor");
+  m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2) -> (Tensor, Tensor)");
+  m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim) -> (Tensor, Tensor)");
+  m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim) -> Tensor");
+  m.def("score_ce(Tensor cand, Tensor user, int act) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset) -> Tensor");
+  m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
+  m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("secagg_mask(Tensor x, Tensor seeds, Tensor signs, float scale, float clipv, int round) -> (Tensor)");
+  m.def("secagg_unmask(Tensor x, float inv_scale) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
+  m.impl("linear", &linear);
+  m.impl("layer_norm", &layer_norm);
+  m.impl("embed_ln", &embed_ln);
+  m.impl("title_attention", &title_attention);
+  m.impl("additive_pool_fwd", &additive_pool_fwd);
+  m.impl("additive_pool_bwd", &additive_pool_bwd);
+  m.impl("user_attention_fwd", &user_attention_fwd);
+  m.impl("user_attention_bwd", &user_attention_bwd);
+  m.impl("score_ce", &score_ce);
+  m.impl("segment_sum_rows", &segment_sum_rows);
+  m.impl("adam_flat", &adam_flat);
+  m.impl("dedup", &dedup);
+  m.impl("secagg_mask", &secagg_mask);
+  m.impl("secagg_unmask", &secagg_unmask);
+}

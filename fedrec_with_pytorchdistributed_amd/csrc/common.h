@@ -1,0 +1,89 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernels of the engine.
+//
+// * wave64 everywhere: lane = threadIdx.x & 63, reductions use __shfl_xor over 64 lanes;
+// * bf16 is clang's native __bf16 (f32->bf16 lowers to v_cvt_pk_bf16_f32 on gfx950,
+//   which keeps NaNs -- MI355X_MICROARCH.md "Correctness boundaries");
+// * MFMA fragment types for v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16;
+// * a Philox-4x32-10 counter RNG (LDP noise, dropout, secure-aggregation masks).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+#define GLOBAL_PTR(T, p) ((__attribute__((address_space(1))) T*)(p))
+
+#define FR_CHECK_LAUNCH() (void)0
+
+static __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+static __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static __device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// reduce across the lanes that share (lane & 15): xor 16 and 32
+static __device__ __forceinline__ float group4_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+static __device__ __forceinline__ float group4_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, __shfl_xor(v, 32, 64));
+  return v;
+}
+
+static __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+static __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+// ---------------------------------------------------------------------------------------
+// Philox-4x32-10 (Salmon et al. 2011); counter = (offset, idx), key = seed.
+struct Philox {
+  static __device__ __forceinline__ void round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
+                                               uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  static __device__ __forceinline__ uint4 gen(uint64_t seed, uint64_t offset, uint64_t idx) {
+    uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32), c2 = (uint32_t)offset, c3 = (uint32_t)(offset >> 32);
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      round(c0, c1, c2, c3, k0, k1);
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+  }
+};
+
+static __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // (0, 1]
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// Box-Muller: two standard normals from two uniforms
+static __device__ __forceinline__ float2 box_muller(uint32_t a, uint32_t b) {
+  float u1 = u32_to_unit(a), u2 = u32_to_unit(b);
+  float r = sqrtf(-2.0f * logf(u1));
+  float s, c;
+  __sincosf(6.283185307179586f * u2, &s, &c);
+  return make_float2(r * c, r * s);
+}

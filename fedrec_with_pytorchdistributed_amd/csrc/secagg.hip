@@ -1,0 +1,64 @@
+// Pairwise-mask secure aggregation (described in the reference README.md:56,65 but never
+// implemented there; BASELINE config 5).
+//
+// Client i uploads   y_i = Q(x_i) + sum_{j != i} sign_ij * PRG(seed_ij, round)   (mod 2^32)
+// with Q(x) = round(clamp(x, -c, c) * 2^f) as a two's-complement int32 and sign_ij = +1 for
+// i < j, -1 for i > j.  The pairwise masks cancel exactly in the wrap-around int32 sum, so
+// the all-reduce (RCCL int32 SUM over xGMI) yields sum_i Q(x_i) bit-exactly while no
+// single upload reveals x_i.  Fixed point (not float) masking is what makes cancellation
+// exact.  PRG = Philox-4x32-10 keyed by the pair seed, counter =
+// (round, element).
+#include "common.h"
+
+namespace {
+
+constexpr int MAXP = 64;
+
+__global__ __launch_bounds__(256) void mask_kernel(const float* __restrict__ x, int* __restrict__ out, long n,
+                                                   float scale, float clipv, const unsigned long long* __restrict__ seeds,
+                                                   const int* __restrict__ signs, int npeers, unsigned long long round) {
+  __shared__ unsigned long long sd[MAXP];
+  __shared__ int sg[MAXP];
+  for (int i = threadIdx.x; i < npeers; i += blockDim.x) {
+    sd[i] = seeds[i];
+    sg[i] = signs[i];
+  }
+  __syncthreads();
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = fminf(fmaxf(x[i], -clipv), clipv);
+    uint32_t acc = (uint32_t)(int32_t)rintf(v * scale);
+    for (int p = 0; p < npeers; ++p) {
+      const uint32_t r = Philox::gen(sd[p], round, (unsigned long long)i).x;
+      acc += sg[p] > 0 ? r : (uint32_t)(0u - r);
+    }
+    out[i] = (int32_t)acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void unmask_kernel(const int* __restrict__ x, float* __restrict__ out, long n,
+                                                     float inv_scale) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = (float)x[i] * inv_scale;
+}
+
+unsigned grid_for(long n) {
+  long b = (n + 255) / 256;
+  return (unsigned)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+extern "C" int fr_secagg_mask(const float* x, int* out, long n, float scale, float clipv, const unsigned long long* seeds,
+                              const int* signs, int npeers, unsigned long long round, hipStream_t s) {
+  if (npeers > MAXP) return 1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(mask_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, out, n, scale, clipv, seeds, signs, npeers,
+                     round);
+  return 0;
+}
+
+extern "C" int fr_secagg_unmask(const int* x, float* out, long n, float inv_scale, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(unmask_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, out, n, inv_scale);
+  return 0;
+}

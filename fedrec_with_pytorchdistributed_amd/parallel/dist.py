@@ -1,0 +1,111 @@
+"""Process groups: one process per GPU, roles decided by the entrypoint (not by rank).
+
+* **data plane** -- RCCL (PyTorch's ``nccl`` backend on ROCm) over the client GPUs: the
+  flat trainable bucket (4.66 MB fp32) is all-reduced / broadcast in ONE call, replacing
+  the reference's 116 per-tensor gloo messages (``server.py:76-77``) and DDP buckets;
+* **control plane** -- gloo on the host over *every* participant (coordinator + clients):
+  round flags, role discovery, sample counts, metrics, heartbeats.
+
+Roles are exchanged with ``all_gather_object`` so the coordinator can be any rank (the
+reference hard-codes ``src=1``, Q13).  On a CPU-only run both planes are gloo.
+
+Collective timeouts default to minutes, not the reference's 2 days (``client.py:227``).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = field(default_factory=lambda: torch.device("cpu"))
+    role: str = "client"
+    roles: List[str] = field(default_factory=lambda: ["client"])
+    ctrl_group: Optional[object] = None  # gloo, everybody
+    data_group: Optional[object] = None  # RCCL (or gloo on CPU), clients only
+    client_ranks: List[int] = field(default_factory=lambda: [0])
+    initialized: bool = False
+
+    @property
+    def client_index(self) -> int:
+        return self.client_ranks.index(self.rank) if self.rank in self.client_ranks else -1
+
+    @property
+    def num_clients(self) -> int:
+        return len(self.client_ranks)
+
+    @property
+    def coordinator(self) -> Optional[int]:
+        return self.roles.index("server") if "server" in self.roles else None
+
+    def barrier(self, group=None) -> None:
+        if self.initialized:
+            dist.barrier(group=group or self.ctrl_group)
+
+
+def _env_int(k: str, d: int) -> int:
+    v = os.environ.get(k)
+    return int(v) if v is not None else d
+
+
+def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0) -> DistContext:
+    world = _env_int("WORLD_SIZE", 1)
+    rank = _env_int("RANK", 0)
+    local_rank = _env_int("LOCAL_RANK", 0)
+    use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available() and role == "client")
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+    ctx = DistContext(rank, world, local_rank, dev, role, [role], None, None, [0], False)
+    if world == 1:
+        return ctx
+    timeout = datetime.timedelta(seconds=timeout_s)
+    gpu_job = torch.cuda.is_available() and device != "cpu"
+    backend = "cpu:gloo,cuda:nccl" if gpu_job else "gloo"
+    kw = {"device_id": dev} if use_cuda else {}
+    try:
+        dist.init_process_group(backend=backend, init_method="env://", timeout=timeout, **kw)
+    except TypeError:
+        dist.init_process_group(backend=backend, init_method="env://", timeout=timeout)
+    ctx.initialized = True
+    ctx.ctrl_group = dist.new_group(backend="gloo", timeout=timeout)
+    roles: List[Optional[str]] = [None] * world
+    dist.all_gather_object(roles, role, group=ctx.ctrl_group)
+    ctx.roles = [str(r) for r in roles]
+    ctx.client_ranks = [i for i, r in enumerate(ctx.roles) if r == "client"]
+    data_backend = "nccl" if gpu_job else "gloo"
+    # every rank must call new_group, members or not
+    ctx.data_group = dist.new_group(ranks=ctx.client_ranks, backend=data_backend, timeout=timeout)
+    return ctx
+
+
+def shutdown(ctx: DistContext) -> None:
+    if ctx.initialized and dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+
+
+def make_grad_allreduce(ctx: DistContext):
+    """Sum the flat gradient over the client data group; returns the 1/W scale Adam applies."""
+    if ctx.num_clients <= 1 or not ctx.initialized:
+        return None
+    W = ctx.num_clients
+
+    def _ar(flat_grad: torch.Tensor) -> float:
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=ctx.data_group)
+        return 1.0 / W
+
+    return _ar

@@ -1,0 +1,185 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 oracle (ops/reference.py).
+
+bf16 kernels are compared with tolerances scaled to bf16 rounding; fp32 kernels tightly.
+"""
+import math
+
+import pytest
+import torch
+
+from fedrec_with_pytorchdistributed_amd import ops
+from fedrec_with_pytorchdistributed_amd.ops import native
+from fedrec_with_pytorchdistributed_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.mark.parametrize("M,N,K,act,res", [(1000, 2304, 768, "none", False), (777, 768, 3072, "none", True),
+                                           (256, 3072, 768, "gelu", False), (130, 384, 768, "tanh", False),
+                                           (5, 128, 64, "none", True)])
+def test_gemm_bf16(dev, M, N, K, act, res):
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    x = (torch.randn(M, K, generator=g) * 0.5).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(dev)
+    r = torch.randn(M, N, generator=g).to(dev, torch.bfloat16) if res else None
+    y = native.lib().linear(x, w, b, {"none": 0, "gelu": 1, "tanh": 2}[act], r)
+    y_ref = ref.linear(x.float(), w.float(), b, act, r.float() if res else None)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert rel_err(y, y_ref) < 1e-2
+
+
+def test_gemm_asymmetric_exact(dev):
+    # A = I-like, asymmetric B: catches row/col swaps in the C write (guide §3)
+    M = N = 128
+    K = 128
+    x = torch.eye(M, K, device=dev, dtype=torch.bfloat16)
+    w = torch.arange(N * K, device=dev, dtype=torch.float32).remainder(97).reshape(N, K).to(torch.bfloat16)
+    y = native.lib().linear(x, w, None, 0, None)
+    assert torch.equal(y.float(), w.float().t())
+
+
+def test_layer_norm(dev):
+    x = torch.randn(333, 768, device=dev).to(torch.bfloat16) * 3 + 1
+    w = torch.randn(768, device=dev)
+    b = torch.randn(768, device=dev)
+    y = native.lib().layer_norm(x, w, b, 1e-12)
+    assert rel_err(y, ref.layer_norm(x.float(), w, b, 1e-12)) < 1e-2
+
+
+def test_embed_ln(dev):
+    n, T, D = 37, 50, 768
+    word = (torch.randn(30522, D, device=dev) * 0.02).to(torch.bfloat16)
+    pos = (torch.randn(512, D, device=dev) * 0.02).to(torch.bfloat16)
+    tok = torch.randint(0, 30522, (n, T), device=dev, dtype=torch.int32)
+    w, b = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    y = native.lib().embed_ln(tok, word, pos, w, b, 1e-12)
+    y_ref = ref.embed_ln(tok.long(), word.float(), pos.float(), w, b, 1e-12)
+    assert rel_err(y, y_ref) < 1e-2
+
+
+@pytest.mark.parametrize("T", [50, 64, 17, 1])
+def test_title_attention(dev, T):
+    n, H, D = 9, 12, 768
+    qkv = torch.randn(n * T, 3 * D, device=dev).to(torch.bfloat16)
+    mask = (torch.rand(n, T, device=dev) < 0.7).to(torch.int32)
+    mask[:, 0] = 1
+    mask[0] = 0  # the <unk> row: all keys masked -> uniform (HF finfo.min semantics)
+    out = native.lib().title_attention(qkv, mask, H)
+    out_ref = ref.title_attention(qkv.float(), mask, H)
+    assert torch.isfinite(out.float()).all()
+    assert rel_err(out, out_ref) < 2e-2
+
+
+@pytest.mark.parametrize("dtype,D,Q", [(torch.bfloat16, 768, 384), (torch.float32, 400, 200)])
+def test_additive_pool(dev, dtype, D, Q):
+    n, T = 23, 50
+    x = torch.randn(n, T, D, device=dev).to(dtype)
+    e = torch.tanh(torch.randn(n, T, Q, device=dev)).to(dtype)
+    w2 = torch.randn(Q, device=dev) * 0.1
+    b2 = torch.randn(1, device=dev)
+    out, alpha = ops.additive_pool_fwd(x, e, w2, b2)
+    o_ref, a_ref = ref.additive_pool_fwd(x.float(), e.float(), w2, b2)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert rel_err(out, o_ref) < tol and rel_err(alpha, a_ref) < tol
+    g = torch.randn(n, D, device=dev)
+    dx, dpre, dw2, db2 = ops.additive_pool_bwd(x, e, alpha, w2, g, True)
+    rdx, rde, rdw2, rdb2 = ref.additive_pool_bwd(x.float(), e.float(), a_ref, w2, g)
+    rdpre = rde * (1 - e.float() ** 2)
+    assert rel_err(dx, rdx) < tol
+    assert rel_err(dpre, rdpre) < 2 * tol
+    assert rel_err(dw2, rdw2) < 2 * tol
+    assert abs(float(db2) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
+
+
+def test_user_attention(dev):
+    B, H, NH, DK = 7, 50, 20, 20
+    qkv = torch.randn(B, H, 3 * NH * DK, device=dev)
+    ctx, stats = ops.user_attention_fwd(qkv, NH, DK)
+    c_ref, A = ref.user_attention_fwd(qkv, NH, DK)
+    assert rel_err(ctx, c_ref) < 1e-5
+    d = torch.randn_like(ctx)
+    dq = ops.user_attention_bwd(qkv, stats, d, NH, DK)
+    dq_ref = ref.user_attention_bwd(qkv, A, d, NH, DK)
+    assert rel_err(dq, dq_ref) < 1e-4
+
+
+def test_score_ce(dev):
+    B, C, D = 33, 5, 400
+    cand = torch.randn(B, C, D, device=dev) * 0.1
+    u = torch.randn(B, D, device=dev) * 0.1
+    loss, s, dc, du = ops.score_ce(cand, u, "sigmoid")
+    l2, s2, dc2, du2 = ref.score_ce_fwd_bwd(cand, u, "sigmoid")
+    assert abs(float(loss) - float(l2)) < 1e-5
+    assert rel_err(s, s2) < 1e-6 and rel_err(dc, dc2) < 1e-5 and rel_err(du, du2) < 1e-5
+
+
+def test_dedup_and_segment_sum(dev):
+    ids = torch.randint(0, 500, (64 * 55,), device=dev, dtype=torch.int32)
+    uniq, inv, perm, ptr = ops.dedup(ids, 500)
+    u_ref = torch.unique(ids.cpu())
+    assert torch.equal(uniq.cpu().long(), u_ref.long())
+    assert torch.equal(uniq[inv.long()], ids)
+    rows = torch.randn(ids.numel(), 400, device=dev)
+    out = ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr))
+    o_ref = ref.segment_sum_rows(rows, inv, uniq.numel())
+    assert rel_err(out, o_ref) < 1e-6
+    # clipping
+    out_c = ops.segment_sum_rows(rows, inv, uniq.numel(), clip=2.0, seg=(perm, ptr))
+    oc_ref = ref.segment_sum_rows(rows, inv, uniq.numel(), clip=2.0)
+    assert rel_err(out_c, oc_ref) < 1e-5
+
+
+def test_ldp_noise_statistics(dev):
+    R, D = 4096, 400
+    rows = torch.zeros(R, D, device=dev)
+    inv = torch.arange(R, device=dev, dtype=torch.int32)
+    perm, ptr = ops.segments_from_inv(inv, R)
+    out = ops.segment_sum_rows(rows, inv, R, clip=2.0, noise_std=3.0, seed=5, offset=1, seg=(perm, ptr))
+    assert abs(float(out.mean())) < 0.02
+    assert abs(float(out.std()) - 3.0) < 0.03
+    out2 = ops.segment_sum_rows(rows, inv, R, clip=2.0, noise_std=3.0, seed=5, offset=1, seg=(perm, ptr))
+    assert torch.equal(out, out2)  # counter-based: reproducible
+
+
+def test_adam_flat(dev):
+    n = 4096
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    p2, m2, v2 = p.clone().cpu(), m.clone().cpu(), v.clone().cpu()
+    for step in (1, 2, 3):
+        ops.adam_flat(p, g, m, v, step, 1e-3, 0.9, 0.999, 1e-8, grad_scale=0.5)
+        ref.adam_step(p2, g.cpu(), m2, v2, step, 1e-3, 0.9, 0.999, 1e-8, grad_scale=0.5)
+    assert rel_err(p, p2) < 1e-6
+    # compare with torch.optim.Adam
+    tp = torch.nn.Parameter(torch.ones(8))
+    opt = torch.optim.Adam([tp], lr=5e-5)
+    fp, fm, fv = torch.ones(8, device=dev), torch.zeros(8, device=dev), torch.zeros(8, device=dev)
+    for step in (1, 2):
+        tp.grad = torch.full((8,), 0.3)
+        opt.step()
+        ops.adam_flat(fp, torch.full((8,), 0.3, device=dev), fm, fv, step, 5e-5, 0.9, 0.999, 1e-8)
+    assert torch.allclose(fp.cpu(), tp.detach(), atol=1e-7)
+
+
+def test_secagg_cancels_exactly(dev):
+    from fedrec_with_pytorchdistributed_amd.parallel import secagg
+
+    W, n = 4, 10_000
+    xs = [torch.randn(n, device=dev) for _ in range(W)]
+    seeds = secagg.pair_seeds(W, base_seed=123)
+    masked = [secagg.mask_local(xs[i], i, W, seeds, round_idx=3) for i in range(W)]
+    total = masked[0].clone()
+    for t in masked[1:]:
+        total += t  # int32 wrap-around == RCCL int32 SUM
+    got = secagg.unmask_sum(total)
+    q = [secagg.quantize_ref(x) for x in xs]
+    exp = sum(q[1:], q[0].clone())
+    assert torch.equal(got, secagg.dequantize_ref(exp))
