@@ -1,0 +1,94 @@
+"""GEMM microbenchmark at the DistilBERT shapes of one training step (M = unique titles x 50).
+
+Interleaves every variant in ONE process (cdna_hip_programming.md §5.4 rule 24) on random
+data (rule 25) and reports the median TFLOP/s per variant:
+  ours-128  : 128x128x64 tile, 4 waves, glds double buffer
+  ours-256  : 256x256x64 tile, 8 waves, glds double buffer
+  ours-256p : the same, persistent (next tile's first K-tile overlaps the epilogue)
+  hipblaslt : torch.nn.functional.linear (bias fused), the library baseline
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import json
+import statistics
+
+import torch
+import torch.nn.functional as F
+
+from fedrec_with_pytorchdistributed_amd.ops import native
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=78850)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    lib = native.lib()
+    dev = torch.device("cuda")
+    shapes = [("qkv", 2304, 768, 0, False), ("out_proj+res", 768, 768, 0, True), ("ffn1+gelu", 3072, 768, 1, False),
+              ("ffn2+res", 768, 3072, 0, True), ("head_fc1+tanh", 384, 768, 2, False)]
+    res = {}
+    for name, N, K, act, has_res in shapes:
+        x = (torch.rand(a.M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        b = torch.rand(N, device=dev)
+        r = (torch.rand(a.M, N, device=dev) * 2 - 1).to(torch.bfloat16) if has_res else None
+        flops = 2.0 * a.M * N * K
+        variants = {}
+
+        def ours(v):
+            def f():
+                lib.gemm_set_variant(v)
+                return lib.linear(x, w, b, act, r)
+            return f
+
+        variants["ours-128"] = ours(0)
+        if N % 256 == 0:
+            variants["ours-256"] = ours(1)
+            variants["ours-256p"] = ours(2)
+        bb = b.to(torch.bfloat16)
+
+        def lt():
+            y = F.linear(x, w, bb)
+            if act == 1:
+                y = F.gelu(y)
+            elif act == 2:
+                y = torch.tanh(y)
+            if r is not None:
+                y = y + r
+            return y
+
+        variants["hipblaslt(+eager epilogue)"] = lt
+        times = {k: [] for k in variants}
+        for f in variants.values():
+            f()
+        torch.cuda.synchronize()
+        for _ in range(a.rounds):
+            for k, f in variants.items():
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(5):
+                    f()
+                e.record()
+                torch.cuda.synchronize()
+                times[k].append(s.elapsed_time(e) / 5)
+        lib.gemm_set_variant(-1)
+        ref = variants["hipblaslt(+eager epilogue)"]().float()
+        row = {}
+        for k, ts in times.items():
+            med = statistics.median(ts)
+            err = float((variants[k]().float() - ref).norm() / ref.norm()) if k.startswith("ours") else 0.0
+            row[k] = {"ms": round(med, 4), "tflops": round(flops / med / 1e9, 1), "rel_err_vs_lib": round(err, 5)}
+        res[f"{name} M={a.M} N={N} K={K}"] = row
+        print(name, json.dumps(row), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

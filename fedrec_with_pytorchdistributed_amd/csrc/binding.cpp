@@ -12,6 +12,7 @@
 #include <tuple>
 
 extern "C" {
+void fr_gemm_set_variant(int v);
 int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K,
                     int act, hipStream_t s);
 int fr_layer_norm_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
@@ -316,9 +317,12 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
   return out;
 }
 
+void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
+
 }  // namespace
 
 TORCH_LIBRARY(fedrec, m) {
+  m.def("gemm_set_variant(int v) -> ()", &gemm_set_variant);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");

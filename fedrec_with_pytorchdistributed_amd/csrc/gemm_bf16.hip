@@ -28,7 +28,16 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int STAGE_BYTES = (BM + BN) * BK * 2;  // 32 KB
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// GELU(erf) with erf from Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16 output
+// rounding): one rcp + one exp + 6 FMA, no range branches (ocml erff costs ~3x in the epilogue).
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __frcp_rn(1.0f + 0.3275911f * ax);
+  const float y = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float r = 1.0f - y * __expf(-ax * ax);
+  return copysignf(r, x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
 template <int ACT>
 __device__ __forceinline__ float act_fn(float x) {
@@ -136,9 +145,248 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const bf16* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256x256x64 block tile, 512 threads = 8 waves (2 along M x 4 along N), 128x64 per wave
+// (8x4 MFMA tiles -> 128 accumulator VGPRs), 64 KB per LDS stage, two stages, one block
+// per CU.  Twice the FLOP per staged byte of the 128x128 tile (128 vs 64 FLOP/B), which is
+// what the L2 can feed at MFMA rate (~34 TB/s aggregate L2 vs ~39 TB/s the small tile needs).
+constexpr int BM2 = 256, BN2 = 256;
+constexpr int STAGE2 = (BM2 + BN2) * BK * 2;  // 64 KB
+
+__device__ __forceinline__ void stage_tile2(char* smem, int st, const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                            int M, int K, int m0, int n0, int k0, int wave, int lane) {
+  char* base = smem + st * STAGE2;
+  const int rsub = lane >> 3;
+  const int chunk = (lane & 7) ^ rsub;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 32 + i * 8 + rsub;  // 0..255
+    int gm = m0 + row;
+    gm = gm < M ? gm : M - 1;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, A + (size_t)gm * K + k0 + chunk * 8),
+                                     LDS_PTR(void, base + (wave * 32 + i * 8) * 128), 16, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 32 + i * 8 + rsub;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W + (size_t)(n0 + row) * K + k0 + chunk * 8),
+                                     LDS_PTR(void, base + BM2 * 128 + (wave * 32 + i * 8) * 128), 16, 0, 0);
+  }
+}
+
+template <int ACT, bool HAS_BIAS, bool HAS_RES>
+__global__ __launch_bounds__(512, 1) void gemm_nt_256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                             const float* __restrict__ bias,
+                                                             const bf16* __restrict__ R, bf16* __restrict__ C, int M,
+                                                             int N, int K, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE2];
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, q = nwg >> 3, rmd = nwg & 7;
+  const int tile = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + (bid >> 3);
+  const int mt = tile / tiles_n, nt = tile - mt * tiles_n;
+  const int m0 = mt * BM2, n0 = nt * BN2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage_tile2(smem, 0, A, W, M, K, m0, n0, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage_tile2(smem, cur ^ 1, A, W, M, K, m0, n0, (kt + 1) * BK, wave, lane);
+    const char* As = smem + cur * STAGE2;
+    const char* Bs = As + BM2 * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int phys = ((kk * 4 + fq) ^ (fr & 7)) * 16;
+      bf16x8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *(const bf16x8*)(Bs + (wn * 64 + j * 16 + fr) * 128 + phys);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(As + (wm * 128 + (h * 4 + i) * 16 + fr) * 128 + phys);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[h * 4 + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nb = n0 + wn * 64 + j * 16 + fq * 4;
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if constexpr (HAS_BIAS) {
+        const float4 bb = *(const float4*)(bias + nb);
+        v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
+      }
+      v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+      if constexpr (HAS_RES) {
+        const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
+        v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+      }
+      bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+      *(bf16x4*)(C + (size_t)m * N + nb) = o;
+    }
+  }
+}
+
+// Persistent form of the 256x256 kernel: one block per CU walks the tiles; the first K-tile
+// of the NEXT tile is issued before the current tile's epilogue, so tile prologue latency
+// and the epilogue (bias/act/residual/stores) overlap instead of idling the matrix cores.
+// Tile order: iteration `it` covers tiles [it*G, it*G+G); XCD x (blocks b % 8 == x) takes a
+// contiguous run of G/8 of them, so concurrently running tiles of one XCD share A panels.
+template <int ACT, bool HAS_BIAS, bool HAS_RES>
+__global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                              const float* __restrict__ bias,
+                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
+                                                              int N, int K, int tiles_n, int ntiles) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE2];
+  const int G = gridDim.x, b = blockIdx.x;
+  const bool xcd_map = (G % 8) == 0;
+  auto map = [&](int it) -> int { return it * G + (xcd_map ? (b & 7) * (G >> 3) + (b >> 3) : b); };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / BK;
+  int it = 0;
+  int t = map(0);
+  if (t >= ntiles) return;
+  {
+    const int mt = t / tiles_n;
+    stage_tile2(smem, 0, A, W, M, K, mt * BM2, (t - mt * tiles_n) * BN2, 0, wave, lane);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int buf = 0;
+  while (true) {
+    const int mt = t / tiles_n, nt = t - mt * tiles_n;
+    const int m0 = mt * BM2, n0 = nt * BN2;
+    const int tn = map(it + 1);
+    const bool has_next = tn < ntiles;
+    const int mtn = tn / tiles_n;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) stage_tile2(smem, buf ^ 1, A, W, M, K, m0, n0, (kt + 1) * BK, wave, lane);
+      else if (has_next) stage_tile2(smem, buf ^ 1, A, W, M, K, mtn * BM2, (tn - mtn * tiles_n) * BN2, 0, wave, lane);
+      const char* As = smem + buf * STAGE2;
+      const char* Bs = As + BM2 * 128;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int phys = ((kk * 4 + fq) ^ (fr & 7)) * 16;
+        bf16x8 bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * 64 + j * 16 + fr) * 128 + phys);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 a[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(As + (wm * 128 + (h * 4 + i) * 16 + fr) * 128 + phys);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], a[i], acc[h * 4 + i][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      }
+      if (kt + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();  // last k-tile: everyone is done reading `buf` before it is restaged
+      buf ^= 1;
+    }
+    // epilogue of tile t while tile tn's first K-tile is in flight
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nb = n0 + wn * 64 + j * 16 + fq * 4;
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if constexpr (HAS_BIAS) {
+          const float4 bb = *(const float4*)(bias + nb);
+          v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
+        }
+        v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+        if constexpr (HAS_RES) {
+          const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
+          v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+        }
+        bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+        *(bf16x4*)(C + (size_t)m * N + nb) = o;
+      }
+    }
+    if (!has_next) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    t = tn;
+    ++it;
+  }
+}
+
+int g_num_cus = 0;
+
+int g_gemm_variant = -1;  // -1 auto, 0 = 128x128, 1 = 256x256
+
 template <int ACT>
 void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, bf16* C, int M, int N, int K,
                 hipStream_t s) {
+  const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && N % BN2 == 0 && M >= 4096);
+  if (big && N % BN2 == 0 && g_gemm_variant != 1) {
+    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
+    if (g_num_cus == 0) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
+    dim3 grid(G), block(512);
+#define LP(HB, HR) hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
+    if (bias && R) LP(true, true);
+    else if (bias) LP(true, false);
+    else if (R) LP(false, true);
+    else LP(false, false);
+#undef LP
+    return;
+  }
+  if (big && N % BN2 == 0) {
+    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2;
+    dim3 grid(tiles_m * tiles_n), block(512);
+#define L2(HB, HR) hipLaunchKernelGGL((gemm_nt_256_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n)
+    if (bias && R) L2(true, true);
+    else if (bias) L2(true, false);
+    else if (R) L2(false, true);
+    else L2(false, false);
+#undef L2
+    return;
+  }
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   dim3 grid(tiles_m * tiles_n), block(256);
   if (bias && R) hipLaunchKernelGGL((gemm_nt_kernel<ACT, true, true>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n);
@@ -148,6 +396,8 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
 }
 
 }  // namespace
+
+extern "C" void fr_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 extern "C" int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N,
                                int K, int act, hipStream_t s) {

@@ -42,7 +42,11 @@ class AdditivePoolFn(torch.autograd.Function):
         x2 = x.reshape(n * T, D)
         dw1 = db1 = None
         if ctx.needs_input_grad[1]:
-            dw1 = dpre2.float().t() @ x2.float()
+            if x2.is_cuda and x2.dtype == torch.bfloat16:
+                # weight gradient reduced over all n*T tokens: bf16 MFMA GEMM, fp32 output
+                dw1 = torch.mm(dpre2.t(), x2, out_dtype=torch.float32)
+            else:
+                dw1 = dpre2.float().t() @ x2.float()
         if ctx.needs_input_grad[2]:
             db1 = dpre2.float().sum(0)
         dx = None

@@ -1,0 +1,80 @@
+"""Checkpoints in the reference layout.
+
+* ``snapshot.pt``: ``{"MODEL_STATE": state_dict, "EPOCHS_RUN": int}`` -- exactly the two keys
+  the reference reads (``client.py:133-147``), with the same 116-key fp32 state_dict, so a
+  reference snapshot loads here and ours loads there.  Optional extra keys the reference
+  ignores: ``NEXT_EPOCH``, ``OPTIM_STATE`` (flat Adam m/v/step), ``ROUND``, ``RNG``,
+  ``CONFIG``.
+* resume (Q14): the reference restarts *at* ``EPOCHS_RUN`` (re-running the saved epoch);
+  here resumption starts at ``NEXT_EPOCH`` (written explicitly), or ``EPOCHS_RUN + 1`` for
+  a reference-written file.
+* writes are atomic (tmp file + ``os.replace``) and done by one rank only (the reference
+  has every DDP rank write the same file concurrently, ``Gradient_Averaging_main.py:140``).
+* ``model.pt`` / ``received_model_{k}.pt`` / ``global_model_round{r}.pt``: raw state_dicts.
+
+Loading always uses ``torch.load(weights_only=True)``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, Optional
+
+import torch
+
+from ..models.fedrec_model import FedRecModel
+
+
+def cpu_state_dict(model: FedRecModel) -> Dict[str, torch.Tensor]:
+    return {k: v.detach().to("cpu", torch.float32).clone() for k, v in model.state_dict().items()}
+
+
+def atomic_save(obj: Any, path: str) -> None:
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    tmp = f"{path}.tmp.{os.getpid()}"
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
+
+
+def save_snapshot(path: str, model: FedRecModel, epoch: int, *, round_idx: Optional[int] = None,
+                  optim: bool = True, config: Optional[dict] = None) -> None:
+    snap: Dict[str, Any] = {"MODEL_STATE": cpu_state_dict(model), "EPOCHS_RUN": int(epoch),
+                            "NEXT_EPOCH": int(epoch) + 1}
+    if optim and model.flat is not None:
+        snap["OPTIM_STATE"] = model.flat.state()
+    if round_idx is not None:
+        snap["ROUND"] = int(round_idx)
+    snap["RNG"] = torch.get_rng_state()
+    if config is not None:
+        snap["CONFIG"] = config
+    atomic_save(snap, path)
+
+
+def load_snapshot(path: str, model: FedRecModel, map_location="cpu") -> Dict[str, Any]:
+    """Load a snapshot (ours or the reference's) into ``model``; returns resume info."""
+    snap = torch.load(path, map_location=map_location, weights_only=True)
+    if "MODEL_STATE" not in snap:
+        raise ValueError(f"{path}: not a snapshot (no MODEL_STATE)")
+    model.load_state_dict(snap["MODEL_STATE"])
+    if "OPTIM_STATE" in snap and model.flat is not None:
+        model.flat.load_state(snap["OPTIM_STATE"])
+    nxt = int(snap.get("NEXT_EPOCH", int(snap["EPOCHS_RUN"]) + 1))
+    return {"epochs_run": int(snap["EPOCHS_RUN"]), "next_epoch": nxt, "round": snap.get("ROUND")}
+
+
+def save_state_dict(path: str, model: FedRecModel) -> None:
+    atomic_save(cpu_state_dict(model), path)
+
+
+def load_state_dict(path: str) -> Dict[str, torch.Tensor]:
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def flat_to_state_dict(model: FedRecModel, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """Full state_dict with the trainable tensors taken from ``flat`` (a flat fp32 buffer
+    in ``model.flat`` layout) -- e.g. a received global model in reference format."""
+    sd = cpu_state_dict(model)
+    f = flat.detach().to("cpu", torch.float32)
+    for name, p, off in model.flat.views():
+        sd[name] = f[off:off + p.numel()].view(p.shape).clone()
+    return sd

@@ -183,3 +183,28 @@ def test_secagg_cancels_exactly(dev):
     q = [secagg.quantize_ref(x) for x in xs]
     exp = sum(q[1:], q[0].clone())
     assert torch.equal(got, secagg.dequantize_ref(exp))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K,act,res", [(5000, 768, 768, "none", True), (4133, 2304, 768, "gelu", False),
+                                           (70000, 768, 3072, "none", True)])
+def test_gemm_variants(dev, variant, M, N, K, act, res):
+    lib = native.lib()
+    g = torch.Generator(device="cpu").manual_seed(M)
+    x = (torch.rand(M, K, generator=g) * 2 - 1).to(dev, torch.bfloat16)
+    w = ((torch.rand(N, K, generator=g) * 2 - 1) / K ** 0.5).to(dev, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(dev)
+    r = torch.randn(M, N, generator=g).to(dev, torch.bfloat16) if res else None
+    lib.gemm_set_variant(variant)
+    try:
+        y = lib.linear(x, w, b, {"none": 0, "gelu": 1, "tanh": 2}[act], r)
+    finally:
+        lib.gemm_set_variant(-1)
+    # fp32 reference on device (exact erf GELU)
+    y_ref = torch.nn.functional.linear(x.float(), w.float(), b)
+    if act == "gelu":
+        y_ref = torch.nn.functional.gelu(y_ref)
+    if res:
+        y_ref = y_ref + r.float()
+    assert rel_err(y, y_ref) < 1e-2
+    assert torch.isfinite(y.float()).all()
