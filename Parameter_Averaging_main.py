@@ -1,0 +1,12 @@
+"""torchrun entrypoint, argv-compatible with the reference's Parameter_Averaging_main.py (Parameter_Averaging_main.py:190-196).
+
+See fedrec_with_pytorchdistributed_amd/cli.py for the argument contract and overrides."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from fedrec_with_pytorchdistributed_amd.cli import main_param_avg  # noqa: E402
+
+if __name__ == "__main__":
+    sys.exit(main_param_avg())

@@ -103,7 +103,7 @@ class FedRecConfig:
     user_head_dim: int = 20
     user_query_dim: int = 200
     user_dropout: float = 0.2
-    text_query_dim: int = 384  # DistilBERT hidden // 2 (encoder.py:20-21)
+    text_query_dim: int = 0  # 0 = backbone dim // 2 = 384 for DistilBERT (encoder.py:20-21)
     title_len: int = 50
     backbone: BackboneConfig = field(default_factory=BackboneConfig)
     score_act: str = "sigmoid"  # Q1: CE over sigmoid scores (model.py:123); "identity" optional

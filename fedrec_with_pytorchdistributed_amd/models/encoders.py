@@ -76,7 +76,7 @@ class TextEncoder(nn.Module):
         self.cfg = cfg
         self.DistillBert = Backbone(cfg.backbone)
         d = cfg.backbone.dim
-        self.additive_attention = AdditiveAttention(d, cfg.text_query_dim)
+        self.additive_attention = AdditiveAttention(d, cfg.text_query_dim or d // 2)
         self.fc = nn.Linear(d, cfg.news_dim)
 
     @property

@@ -57,21 +57,27 @@ def _env_int(k: str, d: int) -> int:
     return int(v) if v is not None else d
 
 
-def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0) -> DistContext:
+def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0, gpu_offset: int = 0) -> DistContext:
+    """``gpu_offset``: GPU index = LOCAL_RANK - offset (a one-torchrun star run puts the
+    coordinator on local rank 0 and the clients on GPUs 0..W-1)."""
     world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local_rank = _env_int("LOCAL_RANK", 0)
-    use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available() and role == "client")
+    cpu_only = os.environ.get("FEDREC_CPU_ONLY", "0") == "1"
+    use_cuda = not cpu_only and ((device == "cuda") or (device == "auto" and torch.cuda.is_available()
+                                                        and role == "client"))
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        gi = max(0, local_rank - gpu_offset)
+        torch.cuda.set_device(gi)
+        dev = torch.device("cuda", gi)
     else:
         dev = torch.device("cpu")
     ctx = DistContext(rank, world, local_rank, dev, role, [role], None, None, [0], False)
     if world == 1:
         return ctx
     timeout = datetime.timedelta(seconds=timeout_s)
-    gpu_job = torch.cuda.is_available() and device != "cpu"
+    # every rank must pick the same backends: decided by the machine, not by this rank's role
+    gpu_job = torch.cuda.is_available() and os.environ.get("FEDREC_CPU_ONLY", "0") != "1"
     backend = "cpu:gloo,cuda:nccl" if gpu_job else "gloo"
     kw = {"device_id": dev} if use_cuda else {}
     try:

@@ -197,7 +197,11 @@ class LocalEngine:
         self.news_table = None
 
     # -------------------------------------------------------------------------------
-    def train_epoch(self, max_steps: Optional[int] = None, log_every: int = 0) -> Dict[str, float]:
+    def train_epoch(self, max_steps: Optional[int] = None, log_every: int = 0,
+                    step_hook: Optional[Callable[[int], None]] = None) -> Dict[str, float]:
+        """One local epoch.  ``max_steps`` caps the batches (synchronous modes pass the
+        minimum over clients so every rank issues the same collectives); ``step_hook(n)``
+        runs after every step (parameter averaging every K steps)."""
         sched = self.cfg.resolved_local_update()
         t0 = time.perf_counter()
         losses = []
@@ -212,6 +216,8 @@ class LocalEngine:
                 loss = self.accumulate_step(cand, his)
             losses.append(loss)
             n += 1
+            if step_hook is not None:
+                step_hook(n)
             if log_every and n % log_every == 0:
                 obs.log(f"[rank {self.rank}] epoch {self.epoch} step {n} loss {float(loss):.4f}")
             if max_steps is not None and n >= max_steps:

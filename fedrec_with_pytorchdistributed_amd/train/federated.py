@@ -1,0 +1,374 @@
+"""Federation drivers: the three aggregation strategies of the reference.
+
+``run_grad_avg``   Gradient_Averaging_main.py / main.py (C13a/b, C35): synchronous DP --
+                   every step the flat gradient bucket (1.16M fp32) is all-reduced over the
+                   client GPUs (RCCL/xGMI) and one fused Adam step follows.  Fixes E4/E5:
+                   any number of batches per epoch, BOTH encoders synchronised.
+``run_param_avg``  Parameter_Averaging_main.py (C13c, C36): local training, then the
+                   parameters are averaged by all-reduce once per epoch (or every
+                   ``param_avg_every`` local steps) -- local SGD / serverless FedAvg.
+``run_star_*``     client.py / server.py (C06-C11): a coordinator broadcasts the global
+                   model, clients train ``total_epochs`` local epochs, upload, and the
+                   coordinator averages (unweighted like ``server.py:49``, or weighted by
+                   sample count) -- through the fault-tolerant store control plane, with
+                   quorum, timeouts, NaN-rejection and optional secure aggregation; or with
+                   ``allreduce`` aggregation, the clients average among themselves over RCCL
+                   and only the result goes to the coordinator.
+
+All modes write ``snapshot.pt`` in the reference layout (rank 0 / coordinator, atomic) and
+JSONL metrics with the reference's metric names.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..config import FedRecConfig
+from ..data.shard import Shard
+from ..data.synthetic import SynthSpec, SyntheticCorpus
+from ..models.fedrec_model import FedRecModel
+from ..parallel import comm
+from ..parallel import secagg
+from ..parallel.control import ControlPlane
+from ..parallel.dist import DistContext, make_grad_allreduce
+from ..privacy.rdp import calibrate_client_sigma
+from ..utils import obs
+from ..utils.fault import FaultInjector
+from . import checkpoint as ckpt
+from .engine import LocalEngine
+
+METRIC_KEYS = ("training_loss", "validation_loss", "valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10")
+
+
+# ---------------------------------------------------------------------------------------
+def load_client_shard(cfg: FedRecConfig, ctx: DistContext) -> Shard:
+    """``data_dir`` forms: a reference ``UserData`` dir (``{client}`` is replaced by the
+    client index for single-node multi-client runs), or ``synthetic:<preset>[:<seed>]``."""
+    k, W = max(ctx.client_index, 0), max(ctx.num_clients, 1)
+    if cfg.data_dir.startswith("synthetic:"):
+        parts = cfg.data_dir.split(":")
+        spec = SynthSpec.preset(parts[1])
+        spec.seed = int(parts[2]) if len(parts) > 2 else cfg.seed
+        shard = SyntheticCorpus(spec).client_shard(k, W)
+    else:
+        shard = Shard.load(cfg.data_dir.replace("{client}", str(k)))
+    if cfg.quirks().resplit_shard and W > 1:
+        shard = shard.split_train(k, W)  # Q11: DistributedSampler re-split (client.py:249)
+    return shard
+
+
+def build_model(cfg: FedRecConfig, device: torch.device) -> FedRecModel:
+    torch.manual_seed(cfg.seed)  # identical init on every participant
+    model = FedRecModel(cfg).to(device)
+    model.build_flat()
+    return model
+
+
+def _metrics_writer(cfg: FedRecConfig, is_writer: bool) -> obs.MetricsWriter:
+    path = cfg.metrics_path or os.path.join(os.path.dirname(os.path.abspath(cfg.snapshot_path)), "metrics.jsonl")
+    return obs.MetricsWriter(path if is_writer else None, cfg.run_name, cfg.wandb_project, cfg.to_dict())
+
+
+def _reduce_metrics(ctx: DistContext, train: Dict, val: Dict) -> Dict:
+    """Corpus-level metrics over all clients: one packed gloo all-reduce (X8 replacement)."""
+    n = float(val.get("n_valid", 0))
+    v = torch.tensor([train.get("training_loss", 0.0) * train.get("steps", 0), train.get("steps", 0),
+                      train.get("impressions", 0), val.get("validation_loss", 0.0) * n,
+                      val.get("valid_auc", 0.0) * n, val.get("valid_mrr", 0.0) * n,
+                      val.get("val_ndcg@5", 0.0) * n, val.get("val_ndcg@10", 0.0) * n, n], dtype=torch.float64)
+    v = torch.nan_to_num(v)
+    t = torch.tensor([train.get("epoch_s", 0.0)], dtype=torch.float64)
+    if ctx.initialized and ctx.num_clients > 1:
+        dist.all_reduce(v, group=ctx.ctrl_group)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
+    steps, nv = max(v[1].item(), 1), max(v[8].item(), 1)
+    return {"training_loss": v[0].item() / steps, "validation_loss": v[3].item() / nv, "valid_auc": v[4].item() / nv,
+            "valid_mrr": v[5].item() / nv, "val_ndcg@5": v[6].item() / nv, "val_ndcg@10": v[7].item() / nv,
+            "impressions": v[2].item(), "epoch_s": t.item(), "impressions_per_s": v[2].item() / max(t.item(), 1e-9)}
+
+
+def _min_over_clients(ctx: DistContext, x: int) -> int:
+    if not ctx.initialized or ctx.num_clients <= 1:
+        return x
+    t = torch.tensor([x], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.ctrl_group)
+    return int(t.item())
+
+
+def _sync_initial(model: FedRecModel, ctx: DistContext, full: bool) -> None:
+    """DDP-style start: every client takes client 0's parameters (X6, one bucketed call)."""
+    if ctx.initialized and ctx.num_clients > 1:
+        comm.broadcast_(model.sync_tensors(full), src=ctx.client_ranks[0], group=ctx.data_group)
+        model.text_encoder.DistillBert.invalidate()
+
+
+def _maybe_dp(cfg: FedRecConfig, eng: LocalEngine) -> Optional[float]:
+    if not cfg.dp.enabled:
+        return None
+    if cfg.dp.noise_multiplier is not None:
+        return float(cfg.dp.noise_multiplier)
+    return calibrate_client_sigma(cfg.dp.epsilon, cfg.dp.delta, cfg.batch_size, len(eng.shard.train),
+                                  cfg.dp.epochs)
+
+
+def _dump_flat(model: FedRecModel, ctx: DistContext) -> None:
+    """Test hook: ``FEDREC_DUMP_FLAT=<dir>`` saves each rank's final trainable parameters."""
+    d = os.environ.get("FEDREC_DUMP_FLAT")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        torch.save(model.flat.flat.detach().cpu(), os.path.join(d, f"rank{ctx.rank}.pt"))
+
+
+def _resume(cfg: FedRecConfig, model: FedRecModel) -> int:
+    if cfg.snapshot_path and os.path.exists(cfg.snapshot_path):
+        info = ckpt.load_snapshot(cfg.snapshot_path, model)
+        obs.log(f"resuming from {cfg.snapshot_path}: epochs_run={info['epochs_run']} -> epoch {info['next_epoch']}")
+        return info["next_epoch"]
+    return 0
+
+
+# ---------------------------------------------------------------------------------------
+def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
+    shard = load_client_shard(cfg, ctx)
+    model = build_model(cfg, ctx.device)
+    start = _resume(cfg, model)
+    _sync_initial(model, ctx, cfg.sync == "full")
+    eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=make_grad_allreduce(ctx))
+    eng.sigma = _maybe_dp(cfg, eng)
+    eng.epoch = start
+    writer = _metrics_writer(cfg, ctx.client_index == 0)
+    steps = _min_over_clients(ctx, eng.sampler.num_batches())  # every rank issues the same all-reduces
+    last = {}
+    for epoch in range(start, cfg.total_epochs):
+        tr = eng.train_epoch(max_steps=steps)
+        va = eng.validate()
+        last = _reduce_metrics(ctx, tr, va)
+        last.update({"epoch": epoch, "mode": "grad_avg", "clients": ctx.num_clients})
+        if ctx.client_index == 0:
+            writer.write(last)
+            obs.log(f"[grad_avg] epoch {epoch}: " + ", ".join(f"{k}={last[k]:.4f}" for k in METRIC_KEYS))
+            if cfg.save_every and (epoch % cfg.save_every == 0 or epoch == cfg.total_epochs - 1):
+                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict())
+    _dump_flat(model, ctx)
+    return last
+
+
+def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
+    shard = load_client_shard(cfg, ctx)
+    model = build_model(cfg, ctx.device)
+    start = _resume(cfg, model)
+    full = cfg.sync == "full"
+    _sync_initial(model, ctx, full)
+    eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=None)
+    eng.sigma = _maybe_dp(cfg, eng)
+    eng.epoch = start
+    writer = _metrics_writer(cfg, ctx.client_index == 0)
+    W = ctx.num_clients
+    sched = cfg.resolved_local_update()
+    K = cfg.param_avg_every if sched == "per_step" else 0
+    steps = _min_over_clients(ctx, eng.sampler.num_batches()) if K else None
+
+    def average():
+        if ctx.initialized and W > 1:
+            with obs.range("param_allreduce"):
+                comm.allreduce_(model.sync_tensors(full), ctx.data_group, scale=1.0 / W)
+            model.text_encoder.DistillBert.invalidate()
+
+    hook = (lambda n: average() if n % K == 0 else None) if K else None
+    last = {}
+    for epoch in range(start, cfg.total_epochs):
+        tr = eng.train_epoch(max_steps=steps, step_hook=hook)
+        if not K or (steps or 0) % K:
+            average()  # once per epoch (Parameter_Averaging_main.py:144-148)
+        va = eng.validate()
+        last = _reduce_metrics(ctx, tr, va)
+        last.update({"epoch": epoch, "mode": "param_avg", "clients": W})
+        if ctx.client_index == 0:
+            writer.write(last)
+            obs.log(f"[param_avg] epoch {epoch}: " + ", ".join(f"{k}={last[k]:.4f}" for k in METRIC_KEYS))
+            if cfg.save_every and (epoch % cfg.save_every == 0 or epoch == cfg.total_epochs - 1):
+                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict())
+    _dump_flat(model, ctx)
+    return last
+
+
+# ---------------------------------------------------------------------------------------
+# star topology: coordinator + clients over the store control plane
+# ---------------------------------------------------------------------------------------
+def _aggregation(cfg: FedRecConfig, ctx: DistContext) -> str:
+    if cfg.quorum < 1.0 or cfg.secagg.enabled or not ctx.initialized:
+        return "upload"
+    return os.environ.get("FEDREC_STAR_AGG", "allreduce")
+
+
+def _client_upload_tensor(model: FedRecModel, cfg: FedRecConfig) -> torch.Tensor:
+    return model.flat.flat.detach().float()
+
+
+def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -> Dict:
+    cp = ControlPlane.from_default(run_id, cfg.round_timeout_s)
+    k = ctx.client_index
+    shard = load_client_shard(cfg, ctx)
+    model = build_model(cfg, ctx.device)  # created ONCE: Adam moments persist across rounds
+    eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=None)
+    fault = FaultInjector("client", k)
+    agg = _aggregation(cfg, ctx)
+    full = cfg.sync == "full"
+    writer = _metrics_writer(cfg, False)
+    # secure aggregation: pairwise seeds by Diffie-Hellman over the control plane
+    seeds_row = None
+    if cfg.secagg.enabled:
+        kp = secagg.KeyPair()
+        cp.set(f"pk/{k}", secagg.public_bytes(kp))
+        pubs = [cp.get(f"pk/{j}") for j in range(ctx.num_clients)]
+        seeds_row = secagg.seeds_from_publics(kp, k, pubs)
+    r = int(cp.get("start").decode())  # the coordinator may be resuming at a later round
+    last: Dict = {}
+    while True:
+        flag = cp.get(f"r{r}/go").decode()
+        if flag != "1":
+            break
+        g = cp.get_tensor(f"r{r}/global")
+        with torch.no_grad():
+            model.flat.flat.copy_(g.to(model.flat.flat.device))
+        if full:
+            bb = cp.get_tensor(f"r{r}/backbone")
+            _load_flat_backbone(model, bb)
+        model.text_encoder.DistillBert.invalidate()
+        eng.sigma = _maybe_dp(cfg, eng)
+        eng.epoch = 0
+        tr, va = {}, {}
+        for _ in range(cfg.total_epochs):  # Trainer(...).train(total_epochs) per round (client.py:283-284)
+            tr = eng.train_epoch()
+            va = eng.validate()
+        meta = {"client": k, "n_train": len(shard.train), **{m: float(v) for m, v in {**tr, **va}.items()
+                                                             if isinstance(v, (int, float))}}
+        up = _client_upload_tensor(model, cfg).clone()
+        fault.before_upload(r, up)
+        if agg == "allreduce":
+            w = float(len(shard.train)) if cfg.weighted_fedavg else 1.0
+            wt = torch.tensor([w], device=up.device, dtype=torch.float32)
+            up.mul_(wt)
+            comm.allreduce_([up, wt], ctx.data_group)
+            up.div_(wt)
+            if k == 0:
+                cp.put_tensor(f"r{r}/avg", up.cpu())
+            cp.put_json(f"r{r}/meta/{k}", meta)
+        else:
+            if cfg.secagg.enabled:
+                w = float(len(shard.train)) if cfg.weighted_fedavg else 1.0
+                masked = secagg.mask_local(up * w, k, ctx.num_clients, seeds_row, r, cfg.secagg.frac_bits,
+                                           cfg.secagg.clip_value)
+                cp.put_tensor(f"r{r}/up/{k}", masked.cpu())
+            else:
+                cp.put_tensor(f"r{r}/up/{k}", up.cpu())
+            cp.put_json(f"r{r}/meta/{k}", meta)
+        last = meta
+        r += 1
+    _dump_flat(model, ctx)
+    return last
+
+
+def _flat_backbone(model: FedRecModel) -> torch.Tensor:
+    ps = [p.detach().reshape(-1).float().cpu() for p in model.parameters() if not p.requires_grad]
+    return torch.cat(ps) if ps else torch.zeros(0)
+
+
+def _load_flat_backbone(model: FedRecModel, flat: torch.Tensor) -> None:
+    o = 0
+    with torch.no_grad():
+        for p in model.parameters():
+            if not p.requires_grad:
+                n = p.numel()
+                p.copy_(flat[o:o + n].view_as(p))
+                o += n
+
+
+def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -> Dict:
+    """Coordinator: holds the global model on the host (it never trains -- C20's
+    ServerUserModel is only a parameter container; here it is the flat buffer)."""
+    cp = ControlPlane.from_default(run_id, cfg.round_timeout_s)
+    W = ctx.num_clients
+    model = build_model(cfg, torch.device("cpu"))
+    start_round = 0
+    if cfg.snapshot_path and os.path.exists(cfg.snapshot_path):
+        info = ckpt.load_snapshot(cfg.snapshot_path, model)
+        start_round = int(info.get("round") or 0) + 1 if info.get("round") is not None else 0
+        obs.log(f"[server] resuming at round {start_round}")
+    writer = _metrics_writer(cfg, True)
+    agg = _aggregation(cfg, ctx)
+    need = max(1, int(math.ceil(cfg.quorum * W)))
+    full = cfg.sync == "full"
+    hist = []
+    cp.set("start", str(start_round))
+    for r in range(start_round, cfg.global_rounds):
+        t0 = time.perf_counter()
+        cp.put_tensor(f"r{r}/global", model.flat.flat)
+        if full:
+            cp.put_tensor(f"r{r}/backbone", _flat_backbone(model))
+        cp.set(f"r{r}/go", "1")
+        if agg == "allreduce":
+            avg = cp.get_tensor(f"r{r}/avg", cfg.round_timeout_s)
+            metas = [cp.get_json(f"r{r}/meta/{k}") for k in range(W)]
+            accepted = list(range(W))
+            new = avg
+        else:
+            keys = [f"r{r}/up/{k}" for k in range(W)]
+            present = cp.wait_any(keys, need, cfg.round_timeout_s)
+            ups, metas, accepted = [], [], []
+            for key in present:
+                k = int(key.rsplit("/", 1)[1])
+                try:
+                    t = cp.get_tensor(key)
+                    meta = cp.get_json(f"r{r}/meta/{k}", 30.0)
+                except Exception as e:  # corrupt blob / missing meta -> drop this client
+                    obs.log(f"[server] round {r}: dropping client {k}: {e}")
+                    continue
+                if not cfg.secagg.enabled and not torch.isfinite(t).all():
+                    obs.log(f"[server] round {r}: client {k} sent non-finite parameters; rejected")
+                    continue
+                ups.append(t)
+                metas.append(meta)
+                accepted.append(k)
+            if cfg.secagg.enabled and len(accepted) != W:
+                raise RuntimeError(f"secure aggregation needs every client (got {len(accepted)}/{W})")
+            if len(accepted) < need:
+                raise RuntimeError(f"round {r}: quorum not reached ({len(accepted)}/{W} < {need}); aborting")
+            weights = [float(m["n_train"]) if cfg.weighted_fedavg else 1.0 for m in metas]
+            if cfg.secagg.enabled:
+                tot = ups[0].clone()
+                for t in ups[1:]:
+                    tot = (tot.view(torch.int32).numpy().astype(np.uint32) +
+                           t.view(torch.int32).numpy().astype(np.uint32)).view(np.int32)
+                    tot = torch.from_numpy(tot.copy())
+                new = secagg.unmask_sum(tot, cfg.secagg.frac_bits) / sum(weights)
+            else:
+                acc = torch.zeros_like(ups[0], dtype=torch.float64)
+                for t, w in zip(ups, weights):
+                    acc += t.double() * w  # server.py:46-50 (unweighted unless weighted_fedavg)
+                new = (acc / sum(weights)).float()
+        with torch.no_grad():
+            model.flat.flat.copy_(new)
+        dt = time.perf_counter() - t0
+        rec = {"round": r, "clients_accepted": len(accepted), "clients": W, "round_s": dt}
+        for key in ("training_loss", "validation_loss", "valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):
+            vals = [m[key] for m in metas if key in m]
+            if vals:
+                rec[key] = float(np.mean(vals))
+        imps = sum(m.get("impressions", 0.0) for m in metas)
+        rec["impressions_per_s"] = imps / max(dt, 1e-9)
+        writer.write(rec)
+        hist.append(rec)
+        obs.log(f"[server] round {r}: {len(accepted)}/{W} clients, {dt:.2f}s, auc={rec.get('valid_auc', float('nan')):.4f}")
+        if cfg.snapshot_path:
+            ckpt.save_snapshot(cfg.snapshot_path, model, r, round_idx=r, optim=False, config=cfg.to_dict())
+            gpath = os.path.join(os.path.dirname(os.path.abspath(cfg.snapshot_path)), f"global_model_round{r}.pt")
+            ckpt.save_state_dict(gpath, model)
+    cp.set(f"r{max(cfg.global_rounds, start_round)}/go", "0")  # server.py:105 stop flag
+    return hist[-1] if hist else {}
