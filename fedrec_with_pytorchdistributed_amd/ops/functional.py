@@ -11,6 +11,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import ops
+from .reference import _f
 
 
 class AdditivePoolFn(torch.autograd.Function):
@@ -46,12 +47,12 @@ class AdditivePoolFn(torch.autograd.Function):
                 # weight gradient reduced over all n*T tokens: bf16 MFMA GEMM, fp32 output
                 dw1 = torch.mm(dpre2.t(), x2, out_dtype=torch.float32)
             else:
-                dw1 = dpre2.float().t() @ x2.float()
+                dw1 = _f(dpre2).t() @ _f(x2)
         if ctx.needs_input_grad[2]:
-            db1 = dpre2.float().sum(0)
+            db1 = _f(dpre2).sum(0)
         dx = None
         if want_dx:
-            dx = (dx_dir.float() + (dpre2.float() @ w1.float()).reshape(n, T, D)).to(x.dtype)
+            dx = (_f(dx_dir) + (_f(dpre2) @ _f(w1)).reshape(n, T, D)).to(x.dtype)
         return dx, dw1, db1, dw2.reshape(1, -1).to(w2.dtype), db2.reshape(1).to(w2.dtype)
 
 

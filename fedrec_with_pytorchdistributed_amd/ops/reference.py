@@ -28,6 +28,11 @@ import torch.nn.functional as F
 EPS_SOFTMAX = 1e-8
 
 
+def _f(t: torch.Tensor) -> torch.Tensor:
+    """Compute dtype of the oracle: fp32, or fp64 when the caller is in fp64 (tests)."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
 # ---------------------------------------------------------------------------------------
 # eps-softmax helpers
 # ---------------------------------------------------------------------------------------
@@ -54,15 +59,15 @@ def embed_ln(tokens: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, ln_w: 
     """``LN(word[tok] + pos[0..T-1])`` -> ``[n*T, D]`` (HF Embeddings, eval mode)."""
     n, T = tokens.shape
     x = word[tokens.long()] + pos[:T].unsqueeze(0)
-    x = F.layer_norm(x.float(), (word.shape[1],), ln_w.float(), ln_b.float(), eps)
+    x = F.layer_norm(_f(x), (word.shape[1],), _f(ln_w), _f(ln_b), eps)
     return x.reshape(n * T, -1)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "none",
            residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-    y = x.float() @ w.float().t()
+    y = _f(x) @ _f(w).t()
     if b is not None:
-        y = y + b.float()
+        y = y + _f(b)
     if act == "gelu":
         y = F.gelu(y)  # erf form (HF "gelu")
     elif act == "tanh":
@@ -70,12 +75,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str
     elif act != "none":
         raise ValueError(act)
     if residual is not None:
-        y = y + residual.float()
+        y = y + _f(residual)
     return y
 
 
 def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
-    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+    return F.layer_norm(_f(x), (x.shape[-1],), _f(w), _f(b), eps)
 
 
 def title_attention(qkv: torch.Tensor, mask: torch.Tensor, n_heads: int) -> torch.Tensor:
@@ -83,7 +88,7 @@ def title_attention(qkv: torch.Tensor, mask: torch.Tensor, n_heads: int) -> torc
     n, T = mask.shape
     D = qkv.shape[1] // 3
     dh = D // n_heads
-    q, k, v = qkv.float().view(n, T, 3, n_heads, dh).permute(2, 0, 3, 1, 4)
+    q, k, v = _f(qkv).view(n, T, 3, n_heads, dh).permute(2, 0, 3, 1, 4)
     q = q / math.sqrt(dh)
     s = q @ k.transpose(-1, -2)  # [n, h, T, T]
     keep = (mask != 0).view(n, 1, 1, T)
@@ -115,9 +120,9 @@ def backbone_forward(tokens: torch.Tensor, mask: torch.Tensor, params: dict, n_l
 def additive_pool_fwd(x: torch.Tensor, e: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
                       literal: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """``x [n,T,D]``, ``e = tanh(W1 x + b1) [n,T,Q]`` -> ``(pooled [n,D], alpha [n,T])``."""
-    a = e.float() @ w2.float().reshape(-1) + b2.float().reshape(())
+    a = _f(e) @ _f(w2).reshape(-1) + _f(b2).reshape(())
     alpha = eps_softmax(a, dim=1, literal=literal)
-    pooled = torch.einsum("nt,ntd->nd", alpha, x.float())
+    pooled = torch.einsum("nt,ntd->nd", alpha, _f(x))
     return pooled, alpha
 
 
@@ -128,11 +133,11 @@ def additive_pool_bwd(x: torch.Tensor, e: torch.Tensor, alpha: torch.Tensor, w2:
     ``dx_direct`` is the ``alpha_t g`` term only; the ``W1^T dpre`` term is added by the
     caller (``dpre = de * (1 - e^2)``: ``e`` is a tanh output).
     """
-    xf, ef, g = x.float(), e.float(), g.float()
+    xf, ef, g = _f(x), _f(e), _f(g)
     dalpha = torch.einsum("ntd,nd->nt", xf, g)
     da = eps_softmax_backward(alpha, dalpha, dim=1)
     dx = alpha.unsqueeze(-1) * g.unsqueeze(1)
-    de = da.unsqueeze(-1) * w2.float().reshape(1, 1, -1)
+    de = da.unsqueeze(-1) * _f(w2).reshape(1, 1, -1)
     dw2 = torch.einsum("nt,ntq->q", da, ef)
     db2 = da.sum()
     return dx, de, dw2, db2
@@ -145,7 +150,7 @@ def user_attention_fwd(qkv: torch.Tensor, n_heads: int, head_dim: int,
                        literal: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """``qkv [B,H,3*h*d]`` -> ``(ctx [B,H,h*d], A [B,h,H,H])``."""
     B, H, _ = qkv.shape
-    q, k, v = qkv.float().view(B, H, 3, n_heads, head_dim).permute(2, 0, 3, 1, 4)
+    q, k, v = _f(qkv).view(B, H, 3, n_heads, head_dim).permute(2, 0, 3, 1, 4)
     s = q @ k.transpose(-1, -2) / math.sqrt(head_dim)
     A = eps_softmax(s, dim=-1, literal=literal)
     ctx = (A @ v).permute(0, 2, 1, 3).reshape(B, H, n_heads * head_dim)
@@ -155,8 +160,8 @@ def user_attention_fwd(qkv: torch.Tensor, n_heads: int, head_dim: int,
 def user_attention_bwd(qkv: torch.Tensor, A: torch.Tensor, dctx: torch.Tensor, n_heads: int,
                        head_dim: int) -> torch.Tensor:
     B, H, _ = qkv.shape
-    q, k, v = qkv.float().view(B, H, 3, n_heads, head_dim).permute(2, 0, 3, 1, 4)
-    dc = dctx.float().view(B, H, n_heads, head_dim).permute(0, 2, 1, 3)
+    q, k, v = _f(qkv).view(B, H, 3, n_heads, head_dim).permute(2, 0, 3, 1, 4)
+    dc = _f(dctx).view(B, H, n_heads, head_dim).permute(0, 2, 1, 3)
     dA = dc @ v.transpose(-1, -2)
     dv = A.transpose(-1, -2) @ dc
     dS = eps_softmax_backward(A, dA, dim=-1) / math.sqrt(head_dim)
@@ -173,7 +178,7 @@ def score_ce_fwd_bwd(cand: torch.Tensor, user: torch.Tensor, act: str = "sigmoid
                      label: int = 0):
     """Returns ``(loss, scores [B,C], dcand [B,C,D], duser [B,D])`` for a mean CE over the
     batch with target column ``label`` (always 0 in the reference, ``dataset.py:85``)."""
-    c, u = cand.float(), user.float()
+    c, u = _f(cand), _f(user)
     z = torch.einsum("bcd,bd->bc", c, u)
     s = torch.sigmoid(z) if act == "sigmoid" else z
     B = s.shape[0]
@@ -195,7 +200,7 @@ def segment_sum_rows(rows: torch.Tensor, inv: torch.Tensor, num_out: int,
                      clip: float = 0.0, noise_std: float = 0.0,
                      generator: Optional[torch.Generator] = None) -> torch.Tensor:
     """``out[inv[r]] += clip_r(rows[r]) + N(0, noise_std)`` -> ``[num_out, D]`` (fp32)."""
-    g = rows.float()
+    g = _f(rows)
     if clip > 0:
         nrm = g.norm(dim=1, keepdim=True)
         g = g * torch.clamp(clip / (nrm + 1e-12), max=1.0)

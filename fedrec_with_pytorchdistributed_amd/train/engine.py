@@ -113,8 +113,8 @@ class LocalEngine:
         his_v = rows[B * C:].view(B, H, -1)
         return uniq, v, cand_v, his_v
 
-    def train_step(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
-        """``per_step`` schedule: grads -> all-reduce -> Adam.  Returns the (device) loss."""
+    def forward_backward(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
+        """Loss of one batch with every trainable gradient left in ``flat.grad``."""
         self.model.train()
         self.flat.zero_grad()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True)
@@ -123,8 +123,13 @@ class LocalEngine:
             loss, _ = OF.score_ce(cand_v, u, self.score_act)
         with obs.range("backward"):
             loss.backward()
-        self.optimizer_step()
         return loss.detach()
+
+    def train_step(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
+        """``per_step`` schedule: grads -> all-reduce -> Adam.  Returns the (device) loss."""
+        loss = self.forward_backward(cand, his)
+        self.optimizer_step()
+        return loss
 
     def optimizer_step(self, extra_scale: float = 1.0) -> None:
         scale = extra_scale
