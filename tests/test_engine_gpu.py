@@ -35,10 +35,19 @@ def test_step_matches_cpu_oracle(dev):
     assert abs(float(l_cpu) - float(l_gpu)) < 2e-3
     gc, gg = m_cpu.flat.grad, m_gpu.flat.grad.cpu()
     assert torch.isfinite(gg).all()
+    total = float(gc.norm())
     for name, p, off in m_cpu.flat.views():
         a, b = gc[off:off + p.numel()], gg[off:off + p.numel()]
-        rel = float((a - b).norm() / (a.norm() + 1e-12))
-        assert rel < 5e-2, (name, rel)
+        if name.endswith("att_fc2.bias") or name.endswith("W_K.bias"):
+            # softmax shift invariance: the score bias (att_fc2.bias) and the key bias (q.b_k is
+            # constant over keys) have gradients ~1e-8 -- both sides are rounding noise, so only
+            # an absolute bound is meaningful
+            assert float((a - b).abs().max()) < 1e-5, name
+            continue
+        # relative for well-conditioned tensors; tensors whose gradient is a near-cancellation
+        # (tiny vs the whole-model gradient) are held to an absolute bound instead
+        err = float((a - b).norm())
+        assert err <= 5e-2 * float(a.norm()) + 2e-3 * total, (name, err, float(a.norm()), total)
 
 
 def test_training_reduces_loss_on_gpu(dev):
