@@ -50,6 +50,9 @@ def main():
         if N % 256 == 0:
             variants["ours-256"] = ours(1)
             variants["ours-256p"] = ours(2)
+            variants["ours-256s"] = ours(3)
+            variants["ours-256p-split"] = ours(4)
+            variants["ours-256p-split-pipe"] = ours(5)
         bb = b.to(torch.bfloat16)
 
         def lt():

@@ -174,6 +174,29 @@ __device__ __forceinline__ void stage_tile2(char* smem, int st, const bf16* __re
   }
 }
 
+// one quarter of stage_tile2 (2 of its 8 glds): q = 0,1 -> A rows, q = 2,3 -> W rows
+__device__ __forceinline__ void stage_quarter2(char* smem, int st, int q, const bf16* __restrict__ A,
+                                               const bf16* __restrict__ W, int M, int K, int m0, int n0, int k0,
+                                               int wave, int lane) {
+  char* base = smem + st * STAGE2;
+  const int rsub = lane >> 3;
+  const int chunk = (lane & 7) ^ rsub;
+#pragma unroll
+  for (int i2 = 0; i2 < 2; ++i2) {
+    const int i = (q & 1) * 2 + i2;
+    const int row = wave * 32 + i * 8 + rsub;
+    if (q < 2) {
+      int gm = m0 + row;
+      gm = gm < M ? gm : M - 1;
+      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, A + (size_t)gm * K + k0 + chunk * 8),
+                                       LDS_PTR(void, base + (wave * 32 + i * 8) * 128), 16, 0, 0);
+    } else {
+      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W + (size_t)(n0 + row) * K + k0 + chunk * 8),
+                                       LDS_PTR(void, base + BM2 * 128 + (wave * 32 + i * 8) * 128), 16, 0, 0);
+    }
+  }
+}
+
 template <int ACT, bool HAS_BIAS, bool HAS_RES>
 __global__ __launch_bounds__(512, 1) void gemm_nt_256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                              const float* __restrict__ bias,
@@ -255,7 +278,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256_kernel(const bf16* __restr
 // and the epilogue (bias/act/residual/stores) overlap instead of idling the matrix cores.
 // Tile order: iteration `it` covers tiles [it*G, it*G+G); XCD x (blocks b % 8 == x) takes a
 // contiguous run of G/8 of them, so concurrently running tiles of one XCD share A panels.
-template <int ACT, bool HAS_BIAS, bool HAS_RES>
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool SPLIT, bool PIPE = false>
 __global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                               const float* __restrict__ bias,
                                                               const bf16* __restrict__ R, bf16* __restrict__ C, int M,
@@ -290,10 +313,45 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __rest
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) stage_tile2(smem, buf ^ 1, A, W, M, K, m0, n0, (kt + 1) * BK, wave, lane);
-      else if (has_next) stage_tile2(smem, buf ^ 1, A, W, M, K, mtn * BM2, (tn - mtn * tiles_n) * BN2, 0, wave, lane);
+      const bool st_next = (kt + 1 < nk) || has_next;
+      const int sm0 = (kt + 1 < nk) ? m0 : mtn * BM2;
+      const int sn0 = (kt + 1 < nk) ? n0 : (tn - mtn * tiles_n) * BN2;
+      const int sk0 = (kt + 1 < nk) ? (kt + 1) * BK : 0;
+      if (!SPLIT && st_next) stage_tile2(smem, buf ^ 1, A, W, M, K, sm0, sn0, sk0, wave, lane);
       const char* As = smem + buf * STAGE2;
       const char* Bs = As + BM2 * 128;
+      if constexpr (PIPE) {
+        // fragments for group g+1 are read while group g's 16 MFMAs issue (register double buffer)
+        const char* arow = As + (wm * 128 + fr) * 128;
+        const char* brow = Bs + (wn * 64 + fr) * 128;
+        auto physk = [&](int kk) { return ((kk * 4 + fq) ^ (fr & 7)) * 16; };
+        bf16x8 a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b0[j] = *(const bf16x8*)(brow + j * 16 * 128 + physk(0));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a0[i] = *(const bf16x8*)(arow + i * 16 * 128 + physk(0));
+#define FR_GROUP(G, ACUR, ANXT, BCUR)                                                                  \
+  {                                                                                                    \
+    if (G < 3) {                                                                                       \
+      const int kn = (G + 1) >> 1, hn = (G + 1) & 1;                                                   \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) ANXT[i] =                                          \
+          *(const bf16x8*)(arow + (hn * 4 + i) * 16 * 128 + physk(kn));                                \
+      if (G == 1) {                                                                                    \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) b1[j] = *(const bf16x8*)(brow + j * 16 * 128 + physk(1)); \
+      }                                                                                                \
+    }                                                                                                  \
+    if (SPLIT && st_next) stage_quarter2(smem, buf ^ 1, G, A, W, M, K, sm0, sn0, sk0, wave, lane);     \
+    __builtin_amdgcn_s_setprio(1);                                                                     \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j)        \
+        acc[(G & 1) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BCUR[j], ACUR[i], acc[(G & 1) * 4 + i][j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                                     \
+  }
+        FR_GROUP(0, a0, a1, b0)
+        FR_GROUP(1, a1, a0, b0)
+        FR_GROUP(2, a0, a1, b1)
+        FR_GROUP(3, a1, a0, b1)
+#undef FR_GROUP
+      } else
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int phys = ((kk * 4 + fq) ^ (fr & 7)) * 16;
@@ -302,6 +360,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __rest
         for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * 64 + j * 16 + fr) * 128 + phys);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+          if (SPLIT && st_next) stage_quarter2(smem, buf ^ 1, kk * 2 + h, A, W, M, K, sm0, sn0, sk0, wave, lane);
           bf16x8 a[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(As + (wm * 128 + (h * 4 + i) * 16 + fr) * 128 + phys);
@@ -350,6 +409,130 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Variant 3: 256x256 tile, BK = 32, FOUR LDS stages (32 KB each) and a load stream that runs
+// three K-steps ahead of the MFMAs -- continuously, across tile boundaries (persistent).
+// The per-step sync is `s_waitcnt vmcnt(8) lgkmcnt(0); s_barrier` in one asm statement:
+// it retires only the OLDEST outstanding step (each step is 4 glds per thread), so two
+// steps stay in flight across every barrier (cdna_hip_programming.md §5 "Pipelining across
+// barriers": __syncthreads() would drain vmcnt to 0 here).  LDS rows are 64 B; the 16-B
+// chunk c of row r is stored at c ^ ((r >> 2) & 3), which spreads the 16 rows a ds_read_b128
+// lane group touches over all 16 slots of a 256-B bank row.
+constexpr int BK3 = 32;
+constexpr int STAGE3 = (BM2 + BN2) * BK3 * 2;  // 32 KB
+constexpr int NST3 = 4;
+
+__device__ __forceinline__ void stage_tile3(char* smem, int st, const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                            int M, int K, int m0, int n0, int k0, int wave, int lane) {
+  char* base = smem + st * STAGE3;
+  const int rsub = lane >> 2;                     // row within the 16-row piece
+  const int chunk = (lane & 3) ^ ((lane >> 4) & 3);  // logical chunk fetched into physical slot lane & 3
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + rsub;  // 0..255
+    int gm = m0 + row;
+    gm = gm < M ? gm : M - 1;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, A + (size_t)gm * K + k0 + chunk * 8),
+                                     LDS_PTR(void, base + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + rsub;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W + (size_t)(n0 + row) * K + k0 + chunk * 8),
+                                     LDS_PTR(void, base + BM2 * 64 + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+  }
+}
+
+template <int ACT, bool HAS_BIAS, bool HAS_RES>
+__global__ __launch_bounds__(512, 1) void gemm_nt_256s_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                              const float* __restrict__ bias,
+                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
+                                                              int N, int K, int tiles_n, int ntiles) {
+  __shared__ __attribute__((aligned(16))) char smem[NST3 * STAGE3];
+  const int G = gridDim.x, b = blockIdx.x;
+  const bool xcd_map = (G % 8) == 0;
+  const int slot = xcd_map ? (b & 7) * (G >> 3) + (b >> 3) : b;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / BK3;
+  const int my_tiles = slot < ntiles ? (ntiles - 1 - slot) / G + 1 : 0;
+  const int total = my_tiles * nk;  // this block's (tile, k-step) sequence
+  if (total == 0) return;
+  // loader cursor: global step index -> (tile, k)
+  auto issue = [&](int gs) {
+    const int ti = gs / nk, kk = gs - ti * nk;
+    const int t = ti * G + slot;
+    const int mt = t / tiles_n;
+    stage_tile3(smem, gs & (NST3 - 1), A, W, M, K, mt * BM2, (t - mt * tiles_n) * BN2, kk * BK3, wave, lane);
+  };
+  // prologue: three steps in flight (pad with real issues only)
+  issue(0);
+  if (total > 1) issue(1);
+  if (total > 2) issue(2);
+  if (total > 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+
+  int gs = 0;
+  for (int ti = 0; ti < my_tiles; ++ti) {
+    const int t = ti * G + slot;
+    const int mt = t / tiles_n, nt = t - mt * tiles_n;
+    const int m0 = mt * BM2, n0 = nt * BN2;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nk; ++k, ++gs) {
+      const bool more = gs + 3 < total;
+      if (more) issue(gs + 3);
+      const char* As = smem + (gs & (NST3 - 1)) * STAGE3;
+      const char* Bs = As + BM2 * 64;
+      const int rsw = (fr >> 2) & 3;
+      const int phys = ((fq ^ rsw)) * 16;
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * 64 + j * 16 + fr) * 64 + phys);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(As + (wm * 128 + (h * 4 + i) * 16 + fr) * 64 + phys);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], a[i], acc[h * 4 + i][j], 0, 0, 0);
+      }
+      // retire step gs+1 (the oldest in flight); keep the younger ones flying
+      if (more) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (gs + 2 < total) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nb = n0 + wn * 64 + j * 16 + fq * 4;
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if constexpr (HAS_BIAS) {
+          const float4 bb = *(const float4*)(bias + nb);
+          v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
+        }
+        v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+        if constexpr (HAS_RES) {
+          const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
+          v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+        }
+        bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+        *(bf16x4*)(C + (size_t)m * N + nb) = o;
+      }
+    }
+  }
+}
+
 int g_num_cus = 0;
 
 int g_gemm_variant = -1;  // -1 auto, 0 = 128x128, 1 = 256x256
@@ -358,6 +541,24 @@ template <int ACT>
 void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, bf16* C, int M, int N, int K,
                 hipStream_t s) {
   const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && N % BN2 == 0 && M >= 4096);
+  if (big && N % BN2 == 0 && g_gemm_variant == 3 && K % BK3 == 0) {
+    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
+    if (g_num_cus == 0) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
+    dim3 grid(G), block(512);
+#define LS(HB, HR) hipLaunchKernelGGL((gemm_nt_256s_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
+    if (bias && R) LS(true, true);
+    else if (bias) LS(true, false);
+    else if (R) LS(false, true);
+    else LS(false, false);
+#undef LS
+    return;
+  }
   if (big && N % BN2 == 0 && g_gemm_variant != 1) {
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     if (g_num_cus == 0) {
@@ -368,7 +569,18 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
     }
     int G = ntiles < g_num_cus ? ntiles : g_num_cus;
     dim3 grid(G), block(512);
-#define LP(HB, HR) hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
+#define LP(HB, HR)                                                                                          \
+  do {                                                                                                      \
+    if (g_gemm_variant == 4)                                                                                \
+      hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR, true>), grid, block, 0, s, A, W, bias, R, C, M, N, K, \
+                         tiles_n, ntiles);                                                                   \
+    else if (g_gemm_variant == 5 || g_gemm_variant < 0)                                                      \
+      hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR, true, true>), grid, block, 0, s, A, W, bias, R, C, M, N, \
+                         K, tiles_n, ntiles);                                                                \
+    else                                                                                                    \
+      hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR, false>), grid, block, 0, s, A, W, bias, R, C, M, N,   \
+                         K, tiles_n, ntiles);                                                                \
+  } while (0)
     if (bias && R) LP(true, true);
     else if (bias) LP(true, false);
     else if (R) LP(false, true);

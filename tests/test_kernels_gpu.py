@@ -185,7 +185,7 @@ def test_secagg_cancels_exactly(dev):
     assert torch.equal(got, secagg.dequantize_ref(exp))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("M,N,K,act,res", [(5000, 768, 768, "none", True), (4133, 2304, 768, "gelu", False),
                                            (70000, 768, 3072, "none", True)])
 def test_gemm_variants(dev, variant, M, N, K, act, res):
