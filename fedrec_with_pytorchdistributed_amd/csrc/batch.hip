@@ -97,6 +97,64 @@ __global__ __launch_bounds__(NT) void dedup_kernel(const int* __restrict__ ids, 
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// Batch sampler (reference TrainDataset.__getitem__, dataset.py:69-86, with newsample
+// dataset.py:10-14): one wave per impression of the batch.
+//   cand[b] = [pos, 4 negatives]   n >= 4: uniformly random ordered 4-subset (random.sample)
+//                                  n <  4: the negatives in order, then <unk> (id 0)
+//   his[b]  = the last min(len, H) history ids, zero padded (truncate) / first H (compat)
+// Randomness: Philox(seed, offset = step) with counter (impression, draw): reproducible and
+// independent of the launch geometry.
+__global__ __launch_bounds__(256) void sample_kernel(const int* __restrict__ rows, const int* __restrict__ pos,
+                                                     const long long* __restrict__ neg_ptr, const int* __restrict__ negs,
+                                                     const long long* __restrict__ his_ptr, const int* __restrict__ his,
+                                                     int* __restrict__ cand, int* __restrict__ hout, int B, int npr,
+                                                     int H, int truncate, unsigned long long seed,
+                                                     unsigned long long offset) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int r = rows[b];
+  const long long n0 = neg_ptr[r], n = neg_ptr[r + 1] - n0;
+  int* cb = cand + (size_t)b * (npr + 1);
+  if (lane == 0) {
+    cb[0] = pos[r];
+    if (n < npr) {
+      for (int j = 0; j < npr; ++j) cb[1 + j] = j < n ? negs[n0 + j] : 0;
+    } else {
+      int pick[16];
+      int got = 0;
+      unsigned long long ctr = (unsigned long long)r << 20;
+      while (got < npr) {
+        const uint4 x = Philox::gen(seed, offset, ctr++);
+        const uint32_t u[4] = {x.x, x.y, x.z, x.w};
+        for (int t = 0; t < 4 && got < npr; ++t) {
+          const int idx = (int)(((unsigned long long)u[t] * (unsigned long long)n) >> 32);
+          bool dup = false;
+          for (int q = 0; q < got; ++q) dup |= pick[q] == idx;
+          if (!dup) pick[got++] = idx;
+        }
+      }
+      for (int j = 0; j < npr; ++j) cb[1 + j] = negs[n0 + pick[j]];
+    }
+  }
+  const long long h0 = his_ptr[r], hl = his_ptr[r + 1] - h0;
+  const long long take = hl < H ? hl : H;
+  const long long start = truncate ? h0 + hl - take : h0;
+  int* hb = hout + (size_t)b * H;
+  for (int j = lane; j < H; j += 64) hb[j] = j < take ? his[start + j] : 0;
+}
+
+extern "C" int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs,
+                               const long long* his_ptr, const int* his, int* cand, int* hout, int B, int npr, int H,
+                               int truncate, unsigned long long seed, unsigned long long offset, hipStream_t s) {
+  if (npr > 16 || B < 0) return 1;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(sample_kernel, dim3((B + 3) / 4), dim3(256), 0, s, rows, pos, neg_ptr, negs, his_ptr, his, cand,
+                     hout, B, npr, H, truncate, seed, offset);
+  return 0;
+}
+
 extern "C" int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count,
                         hipStream_t s) {
   if (R > MAXR || R < 1) return 1;

@@ -34,6 +34,9 @@ int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, 
                         float noise_std, unsigned long long seed, unsigned long long offset, hipStream_t s);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
+int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
+                    const int* his, int* cand, int* hout, int B, int npr, int H, int truncate, unsigned long long seed,
+                    unsigned long long offset, hipStream_t s);
 int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count, hipStream_t s);
 int fr_secagg_mask(const float* x, int* out, long n, float scale, float clipv, const unsigned long long* seeds,
                    const int* signs, int npeers, unsigned long long round, hipStream_t s);
@@ -292,6 +295,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dedup(const at::Tenso
   return {uniq.slice(0, 0, U), inv, perm, seg.slice(0, 0, U + 1)};
 }
 
+std::tuple<at::Tensor, at::Tensor> sample_batch(const at::Tensor& rows, const at::Tensor& pos, const at::Tensor& neg_ptr,
+                                                const at::Tensor& negs, const at::Tensor& his_ptr, const at::Tensor& his,
+                                                int64_t npratio, int64_t H, bool truncate, int64_t seed,
+                                                int64_t offset) {
+  for (auto* t : {&rows, &pos, &negs, &his}) {
+    check_dev(*t, "sample_batch input");
+    TORCH_CHECK(t->scalar_type() == at::kInt, "fedrec::sample_batch: int32 ids");
+  }
+  check_dev(neg_ptr, "neg_ptr");
+  check_dev(his_ptr, "his_ptr");
+  TORCH_CHECK(neg_ptr.scalar_type() == at::kLong && his_ptr.scalar_type() == at::kLong, "fedrec::sample_batch: int64 ptr");
+  TORCH_CHECK(neg_ptr.numel() == pos.numel() + 1 && his_ptr.numel() == pos.numel() + 1, "fedrec::sample_batch: CSR");
+  const c10::DeviceGuard g(rows.device());
+  const int64_t B = rows.numel();
+  auto cand = at::empty({B, npratio + 1}, rows.options());
+  auto hout = at::empty({B, H}, rows.options());
+  check_rc(fr_sample_batch(rows.data_ptr<int>(), pos.data_ptr<int>(), (const long long*)neg_ptr.data_ptr<int64_t>(),
+                           negs.data_ptr<int>(), (const long long*)his_ptr.data_ptr<int64_t>(), his.data_ptr<int>(),
+                           cand.data_ptr<int>(), hout.data_ptr<int>(), (int)B, (int)npratio, (int)H, truncate ? 1 : 0,
+                           (unsigned long long)seed, (unsigned long long)offset, cur_stream()),
+           "sample_batch");
+  return {cand, hout};
+}
+
 std::tuple<at::Tensor> secagg_mask(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs, double scale,
                                    double clipv, int64_t round) {
   check_dev(x, "x");
@@ -335,6 +362,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset) -> Tensor");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset) -> (Tensor, Tensor)");
   m.def("secagg_mask(Tensor x, Tensor seeds, Tensor signs, float scale, float clipv, int round) -> (Tensor)");
   m.def("secagg_unmask(Tensor x, float inv_scale) -> Tensor");
 }
@@ -352,6 +380,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("segment_sum_rows", &segment_sum_rows);
   m.impl("adam_flat", &adam_flat);
   m.impl("dedup", &dedup);
+  m.impl("sample_batch", &sample_batch);
   m.impl("secagg_mask", &secagg_mask);
   m.impl("secagg_unmask", &secagg_unmask);
 }

@@ -111,3 +111,46 @@ def validation_batches(arr: ImpressionArrays, batch_size: int, npratio: int = 4,
     for s in range(0, n, batch_size):
         rows = np.arange(s, min(s + batch_size, n))
         yield valid_candidates(arr, rows, npratio), _pad_history(arr, rows, max_his, truncate)
+
+
+class DeviceSampler:
+    """The shard's impression CSR resident in HBM; each batch is assembled by the
+    ``sample_batch`` HIP kernel (no host work, no H2D copy per step).  Same distribution as
+    :class:`HostSampler` (a different PRNG: Philox keyed by (seed, rank, step))."""
+
+    def __init__(self, arr: ImpressionArrays, batch_size: int, device, npratio: int = 4, max_his: int = 50,
+                 truncate: bool = True, seed: int = 0, rank: int = 0, shuffle: bool = True, drop_last: bool = False):
+        import torch
+
+        self.B, self.npratio, self.truncate = batch_size, npratio, truncate
+        self.seed, self.rank, self.shuffle, self.drop_last = seed, rank, shuffle, drop_last
+        self.n = len(arr)
+        lens = np.diff(arr.his_ptr)
+        self.H = max_his if truncate else max(max_his, int(lens.max()) if len(lens) else max_his)
+        t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(device)
+        self.pos = t(arr.pos, torch.int32)
+        self.neg_ptr = t(arr.neg_ptr, torch.int64)
+        self.negs = t(arr.neg_ids if len(arr.neg_ids) else np.zeros(1, np.int32), torch.int32)
+        self.his_ptr = t(arr.his_ptr, torch.int64)
+        self.his = t(arr.his_ids if len(arr.his_ids) else np.zeros(1, np.int32), torch.int32)
+        self.device = device
+        self.step = 0
+
+    def num_batches(self) -> int:
+        return self.n // self.B if self.drop_last else -(-self.n // self.B)
+
+    def epoch(self, epoch: int):
+        import torch
+
+        from ..ops import native
+
+        lib = native.lib()
+        rng = np.random.Generator(np.random.PCG64([self.seed, self.rank, epoch, 17]))
+        order = rng.permutation(self.n) if self.shuffle else np.arange(self.n)
+        order = torch.as_tensor(order.astype(np.int32)).to(self.device)
+        seed = (self.seed * 1_000_003 + self.rank) & 0x7FFFFFFF
+        for b in range(self.num_batches()):
+            rows = order[b * self.B:(b + 1) * self.B]
+            self.step += 1
+            yield lib.sample_batch(rows, self.pos, self.neg_ptr, self.negs, self.his_ptr, self.his, self.npratio,
+                                   self.H, self.truncate, seed, self.step)

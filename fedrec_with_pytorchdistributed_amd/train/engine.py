@@ -33,7 +33,7 @@ import torch
 
 from .. import ops
 from ..config import FedRecConfig
-from ..data.sampler import HostSampler, validation_batches
+from ..data.sampler import DeviceSampler, HostSampler, validation_batches
 from ..data.shard import Shard
 from ..eval.metrics import batch_metrics
 from ..models.fedrec_model import FedRecModel
@@ -53,8 +53,12 @@ class LocalEngine:
         self.flat = model.flat if model.flat is not None else model.build_flat()
         self.tokens = torch.as_tensor(shard.news_index, dtype=torch.int32).to(device)  # HBM resident
         self.N = shard.num_news
-        self.sampler = HostSampler(shard.train, cfg.batch_size, cfg.npratio, cfg.max_his_len,
-                                   truncate=not self.q.no_history_truncation, seed=cfg.seed, rank=rank)
+        if device.type == "cuda" and cfg.device_sampler:
+            self.sampler = DeviceSampler(shard.train, cfg.batch_size, device, cfg.npratio, cfg.max_his_len,
+                                         truncate=not self.q.no_history_truncation, seed=cfg.seed, rank=rank)
+        else:
+            self.sampler = HostSampler(shard.train, cfg.batch_size, cfg.npratio, cfg.max_his_len,
+                                       truncate=not self.q.no_history_truncation, seed=cfg.seed, rank=rank)
         # grad_allreduce(flat_grad) -> scale to apply (1/W); None = local only
         self.grad_allreduce = grad_allreduce
         self.sigma: Optional[float] = None  # LDP noise multiplier (set by the client driver)
@@ -79,7 +83,9 @@ class LocalEngine:
             return 0.0, float(self.sigma)
         return float(self.cfg.dp.clip), float(self.sigma * self.cfg.dp.clip)
 
-    def to_device(self, a: np.ndarray) -> torch.Tensor:
+    def to_device(self, a) -> torch.Tensor:
+        if isinstance(a, torch.Tensor):
+            return a.to(self.device, non_blocking=True)
         t = torch.from_numpy(np.ascontiguousarray(a))
         if self.device.type == "cuda":
             t = t.pin_memory().to(self.device, non_blocking=True)

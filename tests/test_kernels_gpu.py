@@ -208,3 +208,38 @@ def test_gemm_variants(dev, variant, M, N, K, act, res):
         y_ref = y_ref + r.float()
     assert rel_err(y, y_ref) < 1e-2
     assert torch.isfinite(y.float()).all()
+
+
+def test_device_sampler_semantics(dev):
+    import numpy as np
+    from fedrec_with_pytorchdistributed_amd.data.sampler import DeviceSampler
+    from fedrec_with_pytorchdistributed_amd.data.synthetic import make_client_shards
+    s = make_client_shards("tiny", 1)[0]
+    arr = s.train
+    ds = DeviceSampler(arr, 32, dev)
+    cand, his = next(iter(ds.epoch(0)))
+    assert cand.shape == (32, 5) and his.shape == (32, 50)
+    rng = np.random.Generator(np.random.PCG64([0, 0, 0, 17]))
+    order = rng.permutation(len(arr))[:32]
+    c, h = cand.cpu().numpy(), his.cpu().numpy()
+    for i, r in enumerate(order):
+        negs = arr.negs(r)
+        assert c[i, 0] == arr.pos[r]
+        if len(negs) >= 4:
+            picks = c[i, 1:].tolist()
+            assert set(picks) <= set(negs.tolist())
+        hh = arr.his(r)
+        k = min(len(hh), 50)
+        assert np.array_equal(h[i, :k], hh[-k:]) and np.all(h[i, k:] == 0)
+    # distinct positions: sample from a list of distinct ids and check no repeats
+    from fedrec_with_pytorchdistributed_amd.data.shard import ImpressionArrays
+    a2 = ImpressionArrays(np.zeros(256, np.int32), np.arange(257, dtype=np.int64) * 6,
+                          np.tile(np.arange(6, dtype=np.int32), 256), np.zeros(257, np.int64),
+                          np.zeros(0, np.int32), np.zeros(256, np.int32))
+    ds2 = DeviceSampler(a2, 256, dev, shuffle=False)
+    c2, _ = next(iter(ds2.epoch(0)))
+    c2 = c2.cpu().numpy()[:, 1:]
+    assert all(len(set(r.tolist())) == 4 for r in c2)
+    # every element is reachable and roughly uniform
+    counts = np.bincount(c2.ravel(), minlength=6)
+    assert counts.min() > 0.5 * counts.mean()
