@@ -15,6 +15,11 @@ extern "C" {
 void fr_gemm_set_variant(int v);
 int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K,
                     int act, hipStream_t s);
+int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db, int rows, int D,
+                           float eps, hipStream_t s);
+int fr_gelu_bf16(const void* z, const void* dh, void* out, long n, int bwd, hipStream_t s);
+int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles, int T, int H,
+                                int D, hipStream_t s);
 int fr_layer_norm_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
                        hipStream_t s);
 int fr_embed_ln_bf16(const int* tokens, const void* word, const void* pos, const float* w, const float* b, void* y,
@@ -97,6 +102,52 @@ at::Tensor layer_norm(const at::Tensor& x, const at::Tensor& w, const at::Tensor
                               (int)(x.numel() / D), (int)D, (float)eps, cur_stream()),
            "layer_norm");
   return y;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd(const at::Tensor& x, const at::Tensor& w,
+                                                               const at::Tensor& dy, double eps) {
+  check_dev(x, "x");
+  check_dev(dy, "dy");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "fedrec::layer_norm_bwd: bf16");
+  const c10::DeviceGuard g(x.device());
+  const int64_t D = x.size(-1);
+  auto wf = w.to(at::kFloat).contiguous();
+  auto dx = at::empty_like(x);
+  auto dw = at::zeros({D}, x.options().dtype(at::kFloat));
+  auto db = at::zeros({D}, x.options().dtype(at::kFloat));
+  check_rc(fr_layer_norm_bwd_bf16(x.data_ptr(), wf.data_ptr<float>(), dy.data_ptr(), dx.data_ptr(), dw.data_ptr<float>(),
+                                  db.data_ptr<float>(), (int)(x.numel() / D), (int)D, (float)eps, cur_stream()),
+           "layer_norm_bwd");
+  return {dx, dw, db};
+}
+
+at::Tensor gelu(const at::Tensor& z, const c10::optional<at::Tensor>& dh) {
+  check_dev(z, "z");
+  TORCH_CHECK(z.scalar_type() == at::kBFloat16, "fedrec::gelu: bf16");
+  const c10::DeviceGuard g(z.device());
+  auto out = at::empty_like(z);
+  const void* dp = nullptr;
+  if (dh.has_value() && dh->defined()) {
+    check_dev(*dh, "dh");
+    TORCH_CHECK(dh->scalar_type() == at::kBFloat16 && dh->numel() == z.numel(), "fedrec::gelu: dh");
+    dp = dh->data_ptr();
+  }
+  check_rc(fr_gelu_bf16(z.data_ptr(), dp, out.data_ptr(), (long)z.numel(), dp ? 1 : 0, cur_stream()), "gelu");
+  return out;
+}
+
+at::Tensor title_attention_bwd(const at::Tensor& qkv, const at::Tensor& dout, const at::Tensor& mask, int64_t n_heads) {
+  check_dev(qkv, "qkv");
+  check_dev(dout, "dout");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && dout.scalar_type() == at::kBFloat16, "fedrec::title_attention_bwd");
+  const c10::DeviceGuard g(qkv.device());
+  auto mk = mask.to(at::kInt).contiguous();
+  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
+  auto dqkv = at::empty_like(qkv);
+  check_rc(fr_title_attention_bwd_bf16(qkv.data_ptr(), dout.data_ptr(), mk.data_ptr<int>(), dqkv.data_ptr(), (int)n,
+                                       (int)T, (int)n_heads, (int)D, cur_stream()),
+           "title_attention_bwd");
+  return dqkv;
 }
 
 at::Tensor embed_ln(const at::Tensor& tokens, const at::Tensor& word, const at::Tensor& pos, const at::Tensor& w,
@@ -352,6 +403,9 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("gemm_set_variant(int v) -> ()", &gemm_set_variant);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps) -> Tensor");
+  m.def("layer_norm_bwd(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("gelu(Tensor z, Tensor? dh) -> Tensor");
+  m.def("title_attention_bwd(Tensor qkv, Tensor dout, Tensor mask, int n_heads) -> Tensor");
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("title_attention(Tensor qkv, Tensor mask, int n_heads) -> Tensor");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2) -> (Tensor, Tensor)");
@@ -370,6 +424,9 @@ TORCH_LIBRARY(fedrec, m) {
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("linear", &linear);
   m.impl("layer_norm", &layer_norm);
+  m.impl("layer_norm_bwd", &layer_norm_bwd);
+  m.impl("gelu", &gelu);
+  m.impl("title_attention_bwd", &title_attention_bwd);
   m.impl("embed_ln", &embed_ln);
   m.impl("title_attention", &title_attention);
   m.impl("additive_pool_fwd", &additive_pool_fwd);

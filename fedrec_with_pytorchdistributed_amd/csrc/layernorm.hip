@@ -81,7 +81,158 @@ __global__ __launch_bounds__(256) void ln_kernel(const bf16* __restrict__ x, con
   }
 }
 
+// LayerNorm backward (unfrozen backbone): y = (x - mu) * rstd * w + b
+//   dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
+//   dw = sum_rows dy * xhat, db = sum_rows dy   (per-lane partials over a grid-stride of
+//   rows, reduced across the block's waves in LDS, one atomic per column per block)
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                     const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                     float* __restrict__ dw, float* __restrict__ db, int rows, int D,
+                                                     float eps) {
+  __shared__ float red[2][4][256 * MAXC];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nc = (D + 255) >> 8;
+  float pw[MAXC][4], pb[MAXC][4];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pw[c][k] = pb[c][k] = 0.f;
+  for (int row = blockIdx.x * 4 + wv; row < rows; row += gridDim.x * 4) {
+    float v[MAXC][4], g[MAXC][4], dyv[MAXC][4];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int i = c * 256 + lane * 4;
+      const bool ok = c < nc && i < D;
+      bf16x4 a = ok ? *(const bf16x4*)(x + (size_t)row * D + i) : bf16x4{0, 0, 0, 0};
+      bf16x4 d = ok ? *(const bf16x4*)(dy + (size_t)row * D + i) : bf16x4{0, 0, 0, 0};
+      float4 ww = ok ? *(const float4*)(w + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float wa[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[c][k] = (float)a[k];
+        dyv[c][k] = (float)d[k];
+        g[c][k] = dyv[c][k] * wa[k];
+        s += v[c][k];
+      }
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int i = c * 256 + lane * 4;
+      if (c < nc && i < D) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d = v[c][k] - mean;
+          q += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int i = c * 256 + lane * 4;
+      if (c < nc && i < D) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float xh = (v[c][k] - mean) * rstd;
+          v[c][k] = xh;
+          sg += g[c][k];
+          sgx += g[c][k] * xh;
+          pw[c][k] += dyv[c][k] * xh;
+          pb[c][k] += dyv[c][k];
+        }
+      }
+    }
+    const float mg = wave_sum(sg) / (float)D, mgx = wave_sum(sgx) / (float)D;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int i = c * 256 + lane * 4;
+      if (c < nc && i < D) {
+        bf16x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = f2bf(rstd * (g[c][k] - mg - v[c][k] * mgx));
+        *(bf16x4*)(dx + (size_t)row * D + i) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[0][wv][(c * 64 + lane) * 4 + k] = pw[c][k];
+      red[1][wv][(c * 64 + lane) * 4 + k] = pb[c][k];
+    }
+  __syncthreads();
+  for (int j = threadIdx.x; j < nc * 256; j += 256) {
+    const int c = j >> 8, rem = j & 255, ln = rem >> 2, k = rem & 3;
+    const int i = c * 256 + ln * 4 + k;
+    if (i < D) {
+      const int idx = (c * 64 + ln) * 4 + k;
+      atomicAdd(dw + i, red[0][0][idx] + red[0][1][idx] + red[0][2][idx] + red[0][3][idx]);
+      atomicAdd(db + i, red[1][0][idx] + red[1][1][idx] + red[1][2][idx] + red[1][3][idx]);
+    }
+  }
+}
+
+__device__ __forceinline__ float erf_fast2(float x) {
+  const float ax = fabsf(x);
+  const float t = __frcp_rn(1.0f + 0.3275911f * ax);
+  const float y = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.0f - y * __expf(-ax * ax), x);
+}
+
+// GELU(erf) forward / backward as streaming kernels (training mode keeps the pre-activation)
+__global__ __launch_bounds__(256) void gelu_kernel(const bf16* __restrict__ z, const bf16* __restrict__ dh,
+                                                   bf16* __restrict__ out, long n4, int bwd) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const bf16x4 zz = *(const bf16x4*)(z + 4 * i);
+    bf16x4 o;
+    if (bwd) {
+      const bf16x4 gg = *(const bf16x4*)(dh + 4 * i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x = (float)zz[k];
+        const float cdf = 0.5f * (1.0f + erf_fast2(x * 0.70710678118654752f));
+        const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+        o[k] = f2bf((float)gg[k] * (cdf + x * pdf));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x = (float)zz[k];
+        o[k] = f2bf(0.5f * x * (1.0f + erf_fast2(x * 0.70710678118654752f)));
+      }
+    }
+    *(bf16x4*)(out + 4 * i) = o;
+  }
+}
+
 }  // namespace
+
+extern "C" int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db,
+                                      int rows, int D, float eps, hipStream_t s) {
+  if (D % 4 != 0 || D > 256 * MAXC) return 1;
+  if (rows == 0) return 0;
+  int blocks = (rows + 3) / 4;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy, (bf16*)dx, dw, db,
+                     rows, D, eps);
+  return 0;
+}
+
+extern "C" int fr_gelu_bf16(const void* z, const void* dh, void* out, long n, int bwd, hipStream_t s) {
+  if (n % 4 != 0) return 1;
+  const long n4 = n / 4;
+  if (n4 == 0) return 0;
+  long b = (n4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  hipLaunchKernelGGL(gelu_kernel, dim3((unsigned)b), dim3(256), 0, s, (const bf16*)z, (const bf16*)dh, (bf16*)out, n4,
+                     bwd);
+  return 0;
+}
 
 extern "C" int fr_layer_norm_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
                                   hipStream_t s) {

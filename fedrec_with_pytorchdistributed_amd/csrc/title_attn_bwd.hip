@@ -1,0 +1,244 @@
+// Backward of the DistilBERT title self-attention (unfrozen backbone, BASELINE config 5).
+//
+// One wave per (title, head), T <= 64, head dim 64, everything recomputed from qkv (no
+// stored probabilities -- the forward never writes P):
+//
+//   S^T = K Q^T / 8  -> masked softmax -> P^T        (as the forward; lane = query column)
+//   dP^T = V dO^T                                    (same MFMA layout as S^T)
+//   D_t  = sum_s P_ts dP_ts ;  dS_ts = keep_s * P_ts (dP_ts - D_t) / 8
+//   dQ = dS K          A operand straight from the dS^T registers (k permuted as in the
+//                      forward's P.V), B = K by transposed LDS reads
+//   dV = P^T dO, dK = dS^T Q
+//                      A operand = P^T / dS^T rows: written once to LDS as bf16 [s][t] and
+//                      read back with ds_read_b128; B = dO / Q by transposed LDS reads
+//
+// HF masked_fill semantics: a masked key's score is a constant, so its dS is exactly 0 (the
+// all-masked <unk> row still passes gradient to V through its uniform P).
+// qkv/dqkv: [n*T, 3*D] bf16; dout: [n*T, D] bf16; mask: [n, T] int32.
+#include "common.h"
+
+namespace {
+
+constexpr int DH = 64;
+constexpr int WPB = 2;  // waves per block (32 KB LDS per wave)
+
+__device__ __forceinline__ bf16x8 tr_pair(const bf16* base_lo, const bf16* base_hi) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base_lo));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base_hi));
+  bf16x4 a = __builtin_bit_cast(bf16x4, lo), b = __builtin_bit_cast(bf16x4, hi);
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+__global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __restrict__ qkv,
+                                                                  const bf16* __restrict__ dout,
+                                                                  const int* __restrict__ mask,
+                                                                  bf16* __restrict__ dqkv, int n_titles, int T, int H,
+                                                                  int D) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[WPB][4][64 * DH];  // Q, K, dO, P^T/dS^T scratch
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pair = blockIdx.x * WPB + wave;
+  const bool active = pair < n_titles * H;
+  const int title = active ? pair / H : 0;
+  const int h = active ? pair - title * H : 0;
+  const size_t row0 = (size_t)title * T;
+  const int ld = 3 * D;
+  const bf16* qb = qkv + row0 * ld + h * DH;
+  const bf16* kb = qb + D;
+  const bf16* vb = qb + 2 * D;
+  const bf16* gb = dout + row0 * D + h * DH;
+  bf16* Qs = lds[wave][0];
+  bf16* Ks = lds[wave][1];
+  bf16* Gs = lds[wave][2];
+  bf16* Ps = lds[wave][3];
+  // stage Q, K, dO row-major [64][64] (rows >= T zero)
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int idx = c * 64 + lane;
+    const int r = idx >> 3, ch = idx & 7;
+    const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool ok = r < T;
+    *(bf16x8*)(Qs + r * DH + ch * 8) = ok ? *(const bf16x8*)(qb + (size_t)r * ld + ch * 8) : z;
+    *(bf16x8*)(Ks + r * DH + ch * 8) = ok ? *(const bf16x8*)(kb + (size_t)r * ld + ch * 8) : z;
+    *(bf16x8*)(Gs + r * DH + ch * 8) = ok ? *(const bf16x8*)(gb + (size_t)r * D + ch * 8) : z;
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  // ---- S^T = K Q^T and dP^T = V dO^T ----
+  f32x4 st[4][4], dp[4][4];
+#pragma unroll
+  for (int is = 0; is < 4; ++is)
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) st[is][jq] = dp[is][jq] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kd = 0; kd < 2; ++kd) {
+    bf16x8 kf[4], qf[4], vf[4], gf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int r = i * 16 + fr;
+      r = r < T ? r : T - 1;
+      kf[i] = *(const bf16x8*)(kb + (size_t)r * ld + kd * 32 + fq * 8);
+      qf[i] = *(const bf16x8*)(qb + (size_t)r * ld + kd * 32 + fq * 8);
+      vf[i] = *(const bf16x8*)(vb + (size_t)r * ld + kd * 32 + fq * 8);
+      gf[i] = *(const bf16x8*)(gb + (size_t)r * D + kd * 32 + fq * 8);
+    }
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq) {
+        st[is][jq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[is], qf[jq], st[is][jq], 0, 0, 0);
+        dp[is][jq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[is], gf[jq], dp[is][jq], 0, 0, 0);
+      }
+  }
+  // ---- softmax (forward recompute) and dS ----
+  float keep[4][4], kadd[4][4];
+#pragma unroll
+  for (int is = 0; is < 4; ++is)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int s = is * 16 + fq * 4 + r;
+      const bool valid = s < T;
+      const bool on = valid && mask[row0 + s] != 0;
+      keep[is][r] = on ? 1.f : 0.f;
+      kadd[is][r] = valid ? (on ? 0.f : -3.4028234663852886e38f) : -INFINITY;
+    }
+  bf16x8 dsf[4][2];
+#pragma unroll
+  for (int jq = 0; jq < 4; ++jq) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sc = kadd[is][r] == 0.f ? st[is][jq][r] * 0.125f : kadd[is][r];
+        st[is][jq][r] = sc;
+        m = fmaxf(m, sc);
+      }
+    m = group4_max(m);
+    float l = 0.f;
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __expf(st[is][jq][r] - m);
+        st[is][jq][r] = p;
+        l += p;
+      }
+    l = group4_sum(l);
+    const float inv = 1.0f / l;
+    float dsum = 0.f;
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[is][jq][r] *= inv;
+        dsum += st[is][jq][r] * dp[is][jq][r];
+      }
+    dsum = group4_sum(dsum);
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dp[is][jq][r] = keep[is][r] * st[is][jq][r] * (dp[is][jq][r] - dsum) * 0.125f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        f[r] = f2bf(dp[2 * ks][jq][r]);
+        f[4 + r] = f2bf(dp[2 * ks + 1][jq][r]);
+      }
+      dsf[jq][ks] = f;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  const int qq = fr >> 2, pp = fr & 3;
+  // ---- dQ = dS K (A from registers, B = K via transposed reads) ----
+  f32x4 o[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) o[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int jd = 0; jd < 4; ++jd) {
+      const bf16* a0 = Ks + (ks * 32 + fq * 4 + qq) * DH + jd * 16 + pp * 4;
+      const bf16x8 kfr = tr_pair(a0, a0 + 16 * DH);
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq) o[jq][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf[jq][ks], kfr, o[jq][jd], 0, 0, 0);
+    }
+  bf16* dq = dqkv + row0 * ld + h * DH;
+  if (active) {
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = jq * 16 + fq * 4 + r;
+        if (t < T) {
+#pragma unroll
+          for (int jd = 0; jd < 4; ++jd) dq[(size_t)t * ld + jd * 16 + fr] = f2bf(o[jq][jd][r]);
+        }
+      }
+  }
+  // ---- dV = P^T dO and dK = dS^T Q: A rows [s][t] via an LDS transpose of P^T / dS^T ----
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    // write X^T[s][t] (X = P for dV, dS for dK) as bf16 row-major [s][t]
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int s = is * 16 + fq * 4 + r, t = jq * 16 + fr;
+          Ps[s * 64 + t] = f2bf(pass == 0 ? st[is][jq][r] : dp[is][jq][r]);
+        }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    const bf16* Bsrc = pass == 0 ? Gs : Qs;  // dO for dV, Q for dK
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) o[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(Ps + (i * 16 + fr) * 64 + kt * 32 + fq * 8);
+#pragma unroll
+      for (int jd = 0; jd < 4; ++jd) {
+        // B[k = t][d]: rows t = 32kt + 8fq + j  -> two transposed 4-row reads
+        const bf16* b0 = Bsrc + (kt * 32 + fq * 8 + qq) * DH + jd * 16 + pp * 4;
+        const bf16x8 bfr = tr_pair(b0, b0 + 4 * DH);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, o[i][jd], 0, 0, 0);
+      }
+    }
+    bf16* dst = dqkv + row0 * ld + (pass == 0 ? 2 * D : D) + h * DH;
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int s = i * 16 + fq * 4 + r;
+          if (s < T) {
+#pragma unroll
+            for (int jd = 0; jd < 4; ++jd) dst[(size_t)s * ld + jd * 16 + fr] = f2bf(o[i][jd][r]);
+          }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+}  // namespace
+
+extern "C" int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv,
+                                           int n_titles, int T, int H, int D, hipStream_t s) {
+  if (T < 1 || T > 64 || D != H * DH) return 1;
+  const int pairs = n_titles * H;
+  if (pairs == 0) return 0;
+  hipLaunchKernelGGL(title_attn_bwd_kernel, dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, (const bf16*)qkv,
+                     (const bf16*)dout, mask, (bf16*)dqkv, n_titles, T, H, D);
+  return 0;
+}

@@ -156,6 +156,48 @@ class Backbone(nn.Module):
             x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, dtype)
         return x
 
+    def forward_train(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+        """Differentiable forward for an unfrozen backbone (BASELINE config 5), eval-mode math
+        (no dropout).  Device: our kernels + their backward kernels through autograd
+        Functions whose gradients land in the fp32 master parameters; host: the oracle ops
+        under plain autograd."""
+        from ..ops import functional as OF
+        from ..ops import reference as R
+
+        c = self.cfg
+        e = self.embeddings
+        if not tokens.is_cuda or dtype != torch.bfloat16:
+            x = R.embed_ln(tokens, e.word_embeddings.weight, e.position_embeddings.weight, e.LayerNorm.weight,
+                           e.LayerNorm.bias, c.ln_eps)
+            for blk in self.transformer.layer:
+                a = blk.attention
+                wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
+                bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
+                qkv = R.linear(x, wqkv, bqkv)
+                ctx = R.title_attention(qkv, mask, c.n_heads)
+                x = R.layer_norm(R.linear(ctx, a.out_lin.weight, a.out_lin.bias, residual=x),
+                                 blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps)
+                f = R.linear(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, act="gelu")
+                x = R.layer_norm(R.linear(f, blk.ffn.lin2.weight, blk.ffn.lin2.bias, residual=x),
+                                 blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
+            return x
+        P = self.compute_weights(dtype)
+        x = OF.EmbedLNFn.apply(tokens.contiguous(), e.word_embeddings.weight, e.position_embeddings.weight,
+                               e.LayerNorm.weight, e.LayerNorm.bias, c.ln_eps, P["word"], P["pos"])
+        for blk, L in zip(self.transformer.layer, P["layers"]):
+            a = blk.attention
+            wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
+            bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
+            qkv = OF.LinearTFn.apply(x, wqkv, bqkv, None, L["wqkv"])
+            ctx = OF.TitleAttentionFn.apply(qkv, mask.contiguous(), c.n_heads)
+            h = OF.LinearTFn.apply(ctx, a.out_lin.weight, a.out_lin.bias, x, L["wo"])
+            x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps)
+            z = OF.LinearTFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, None, L["w1"])
+            f = OF.GeluFn.apply(z)
+            h = OF.LinearTFn.apply(f, blk.ffn.lin2.weight, blk.ffn.lin2.bias, x, L["w2"])
+            x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
+        return x
+
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
         """Keys as HF ``DistilBertModel`` names them (for parity tests)."""
         return {k: v for k, v in self.state_dict().items()}

@@ -87,9 +87,14 @@ class TextEncoder(nn.Module):
         return torch.float32
 
     def hidden(self, text: torch.Tensor) -> torch.Tensor:
-        """Frozen backbone: ``text [n,2,T]`` -> last hidden state ``[n,T,D]`` (no grad)."""
+        """``text [n,2,T]`` -> last hidden state ``[n,T,D]``: no-grad inference for the frozen
+        backbone (the reference, model.py:25-26); a differentiable forward when unfrozen."""
         n, _, T = text.shape
-        h = self.DistillBert(text[:, 0, :], text[:, 1, :], self.compute_dtype)
+        bb = self.DistillBert
+        if not bb.cfg.frozen and torch.is_grad_enabled():
+            h = bb.forward_train(text[:, 0, :].contiguous(), text[:, 1, :].contiguous(), self.compute_dtype)
+        else:
+            h = bb(text[:, 0, :], text[:, 1, :], self.compute_dtype)
         return h.view(n, T, -1)
 
     def head(self, hidden: torch.Tensor) -> torch.Tensor:

@@ -52,7 +52,11 @@ class AdditivePoolFn(torch.autograd.Function):
             db1 = _f(dpre2).sum(0)
         dx = None
         if want_dx:
-            dx = (_f(dx_dir) + (_f(dpre2) @ _f(w1)).reshape(n, T, D)).to(x.dtype)
+            if x2.is_cuda and x2.dtype == torch.bfloat16:
+                dxp = torch.mm(dpre2, w1.to(torch.bfloat16), out_dtype=torch.float32)
+            else:
+                dxp = _f(dpre2) @ _f(w1)
+            dx = (_f(dx_dir) + dxp.reshape(n, T, D)).to(x.dtype)
         return dx, dw1, db1, dw2.reshape(1, -1).to(w2.dtype), db2.reshape(1).to(w2.dtype)
 
 
@@ -126,3 +130,92 @@ def score_ce(cand, user, act: str = "sigmoid") -> Tuple[torch.Tensor, torch.Tens
 def news_gather(table, inv, perm, seg_ptr, clip: float = 0.0, noise_std: float = 0.0,
                 seed: int = 0, offset: int = 0):
     return NewsGatherFn.apply(table, inv, perm, seg_ptr, clip, noise_std, seed, offset)
+
+
+# ---------------------------------------------------------------------------------------
+# training-mode backbone (unfrozen encoder, BASELINE config 5): forward on the fp32 master
+# parameters through their bf16 compute copies; backward kernels for attention / LayerNorm /
+# GELU, and library GEMMs (bf16 in, fp32 out) for dX / dW.
+# ---------------------------------------------------------------------------------------
+class LinearTFn(torch.autograd.Function):
+    """``y = x @ wlow^T + b (+ residual)`` with ``wlow`` = bf16 copy of the fp32 ``w``."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, residual, wlow):
+        ctx.save_for_backward(x, wlow)
+        ctx.has_res = residual is not None
+        return ops.linear(x, wlow, b, residual=residual)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wlow = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.mm(dy, wlow) if ctx.needs_input_grad[0] else None
+        dw = torch.mm(dy.t(), x, out_dtype=torch.float32) if dy.is_cuda else _f(dy).t() @ _f(x)
+        db = _f(dy).sum(0)
+        return dx, dw, db, (dy if ctx.has_res else None), None
+
+
+class GeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z):
+        ctx.save_for_backward(z)
+        return ops.native.require_for(z).gelu(z, None)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (z,) = ctx.saved_tensors
+        return ops.native.require_for(z).gelu(z, dh.contiguous())
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps: float):
+        ctx.save_for_backward(x, w)
+        ctx.eps = eps
+        return ops.layer_norm(x, w, b, eps)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx, dw, db = ops.native.require_for(x).layer_norm_bwd(x, w, dy.contiguous(), float(ctx.eps))
+        return dx, dw, db, None
+
+
+class TitleAttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, mask, heads: int):
+        ctx.save_for_backward(qkv, mask)
+        ctx.heads = heads
+        return ops.title_attention(qkv, mask, heads)
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, mask = ctx.saved_tensors
+        return ops.native.require_for(qkv).title_attention_bwd(qkv, dout.contiguous(), mask, ctx.heads), None, None
+
+
+class EmbedLNFn(torch.autograd.Function):
+    """``LN(word[tok] + pos[t])``; backward = LN backward, then a scatter-add into the word
+    table rows and a per-position sum into the position table."""
+
+    @staticmethod
+    def forward(ctx, tokens, word, pos, w, b, eps: float, word_low, pos_low):
+        ctx.save_for_backward(tokens, word_low, pos_low, w)
+        ctx.eps = eps
+        ctx.shapes = (word.shape, pos.shape)
+        return ops.embed_ln(tokens, word_low, pos_low, w, b, eps)
+
+    @staticmethod
+    def backward(ctx, dy):
+        tokens, word_low, pos_low, w = ctx.saved_tensors
+        n, T = tokens.shape
+        x0 = (word_low.index_select(0, tokens.reshape(-1).long()).view(n, T, -1) + pos_low[:T].unsqueeze(0))
+        x0 = x0.reshape(n * T, -1).contiguous()
+        dx0, dw, db = ops.native.require_for(x0).layer_norm_bwd(x0, w, dy.contiguous(), float(ctx.eps))
+        dword = torch.zeros(ctx.shapes[0], dtype=torch.float32, device=dy.device)
+        dword.index_add_(0, tokens.reshape(-1).long(), dx0.float())
+        dword[0] = 0.0  # nn.Embedding(padding_idx=0): the pad row never receives gradient
+        dpos = torch.zeros(ctx.shapes[1], dtype=torch.float32, device=dy.device)
+        dpos[:T] = dx0.float().view(n, T, -1).sum(0)
+        return None, dword, dpos, dw, db, None, None, None

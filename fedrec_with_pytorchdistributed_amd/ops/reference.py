@@ -58,7 +58,8 @@ def embed_ln(tokens: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, ln_w: 
              ln_b: torch.Tensor, eps: float) -> torch.Tensor:
     """``LN(word[tok] + pos[0..T-1])`` -> ``[n*T, D]`` (HF Embeddings, eval mode)."""
     n, T = tokens.shape
-    x = word[tokens.long()] + pos[:T].unsqueeze(0)
+    # F.embedding(padding_idx=0) like HF's nn.Embedding: the pad row gets no gradient
+    x = F.embedding(tokens.long(), word, padding_idx=0) + pos[:T].unsqueeze(0)
     x = F.layer_norm(_f(x), (word.shape[1],), _f(ln_w), _f(ln_b), eps)
     return x.reshape(n * T, -1)
 

@@ -82,3 +82,38 @@ def test_per_epoch_schedule_and_news_cache(dev):
     assert not torch.equal(before, m.flat.flat)
     v = eng.validate(limit=64)
     assert 0.0 <= v["valid_auc"] <= 1.0
+
+
+def test_unfrozen_backbone_grads_match_cpu(dev):
+    """BASELINE config 5 path: gradients through the whole (unfrozen) text encoder."""
+    cfg = _cfg()
+    cfg.backbone.frozen = False
+    torch.manual_seed(0)
+    m_cpu = FedRecModel(cfg)
+    m_gpu = copy.deepcopy(m_cpu).to(dev)
+    m_cpu.build_flat()
+    m_gpu.build_flat()
+    assert m_cpu.flat.numel > 20_000_000  # the backbone is in the trainable set
+    shard = make_client_shards("tiny", 1)[0]
+    cfg.batch_size = 8
+    e_cpu = LocalEngine(cfg, m_cpu, shard, torch.device("cpu"))
+    e_gpu = LocalEngine(cfg, m_gpu, shard, dev)
+    cand, his = next(iter(e_cpu.sampler.epoch(0)))
+    l_cpu = e_cpu.forward_backward(e_cpu.to_device(cand), e_cpu.to_device(his))
+    l_gpu = e_gpu.forward_backward(e_gpu.to_device(cand), e_gpu.to_device(his))
+    assert abs(float(l_cpu) - float(l_gpu)) < 3e-3
+    gc, gg = m_cpu.flat.grad, m_gpu.flat.grad.cpu()
+    total = float(gc.norm())
+    checked = 0
+    for name, p, off in m_cpu.flat.views():
+        if "DistillBert" not in name or name.endswith("position_embeddings.weight"):
+            continue
+        a, b = gc[off:off + p.numel()], gg[off:off + p.numel()]
+        err = float((a - b).norm())
+        assert err <= 8e-2 * float(a.norm()) + 2e-3 * total, (name, err, float(a.norm()), total)
+        checked += 1
+    assert checked > 20
+    # one optimizer step refreshes the bf16 compute copies of the backbone
+    before = m_gpu.text_encoder.DistillBert.compute_weights(torch.bfloat16)["w1"] if False else None
+    e_gpu.optimizer_step()
+    assert m_gpu.text_encoder.DistillBert._pack is None

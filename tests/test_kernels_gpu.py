@@ -243,3 +243,46 @@ def test_device_sampler_semantics(dev):
     # every element is reachable and roughly uniform
     counts = np.bincount(c2.ravel(), minlength=6)
     assert counts.min() > 0.5 * counts.mean()
+
+
+@pytest.mark.parametrize("T", [50, 64, 9])
+def test_title_attention_bwd(dev, T):
+    n, H, D = 5, 12, 768
+    qkv = torch.randn(n * T, 3 * D, device=dev).to(torch.bfloat16)
+    mask = (torch.rand(n, T, device=dev) < 0.7).to(torch.int32)
+    mask[:, 0] = 1
+    mask[1] = 0  # all-masked row
+    dout = torch.randn(n * T, D, device=dev).to(torch.bfloat16)
+    dq = native.lib().title_attention_bwd(qkv, dout, mask, H)
+    x = qkv.float().detach().requires_grad_(True)
+    y = ref.title_attention(x, mask, H)
+    y.backward(dout.float())
+    ref_g = x.grad
+    assert torch.isfinite(dq.float()).all()
+    for part in range(3):
+        a = dq.float()[:, part * D:(part + 1) * D]
+        b = ref_g[:, part * D:(part + 1) * D]
+        assert rel_err(a, b) < 3e-2, (part, rel_err(a, b))
+
+
+def test_layer_norm_bwd(dev):
+    x = (torch.randn(1000, 768, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    w = torch.randn(768, device=dev)
+    dy = torch.randn(1000, 768, device=dev).to(torch.bfloat16)
+    dx, dw, db = native.lib().layer_norm_bwd(x, w, dy, 1e-12)
+    xf = x.float().requires_grad_(True)
+    wf = w.clone().requires_grad_(True)
+    bf = torch.zeros(768, device=dev, requires_grad=True)
+    torch.nn.functional.layer_norm(xf, (768,), wf, bf, 1e-12).backward(dy.float())
+    assert rel_err(dx, xf.grad) < 1e-2 and rel_err(dw, wf.grad) < 1e-3 and rel_err(db, bf.grad) < 1e-4
+
+
+def test_gelu_fwd_bwd(dev):
+    z = (torch.randn(4096, device=dev) * 3).to(torch.bfloat16)
+    dh = torch.randn(4096, device=dev).to(torch.bfloat16)
+    h = native.lib().gelu(z, None)
+    dz = native.lib().gelu(z, dh)
+    zf = z.float().requires_grad_(True)
+    hf = torch.nn.functional.gelu(zf)
+    hf.backward(dh.float())
+    assert rel_err(h, hf) < 5e-3 and rel_err(dz, zf.grad) < 5e-3
