@@ -32,6 +32,13 @@ sys.path.insert(0, ROOT)
 
 REF_IMPRESSIONS_PER_S = 1.87  # BASELINE.md §2 (reference code, bs 16)
 METRIC = "impressions/sec/node per FedAvg round + MIND AUC, 8 client-GPUs"
+_DB = "DistilBERT-base text encoder (6L/768/12H, frozen, random init) + additive head + 20-head user encoder"
+MODELS = {2: _DB, 3: _DB, 4: _DB,
+          5: "BERT-base-shaped text encoder (12L/768/12H, UNFROZEN, random init) + additive head + 20-head user encoder"}
+MODES = {2: "Gradient_Averaging (RCCL all-reduce of flat 4.66 MB grad bucket per step)",
+         3: "Parameter_Averaging (local Adam steps, RCCL all-reduce of the parameters every {k} steps)",
+         4: "Gradient_Averaging + LDP (fused per-occurrence clip C=2 + Gaussian noise, eps=10 calibrated)",
+         5: "Gradient_Averaging with secure aggregation (pairwise-masked int32 RCCL all-reduce of all 110M grads)"}
 
 
 def main() -> int:
@@ -41,7 +48,11 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="impressions per GPU per step")
     ap.add_argument("--preset", default="mind-small")
-    ap.add_argument("--mode", default="grad_avg", choices=["grad_avg"])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="BASELINE.json config: 2 GA (headline), 3 parameter averaging every --pa-every "
+                         "steps, 4 GA + fused LDP, 5 unfrozen BERT-base + secure-aggregation GA")
+    ap.add_argument("--pa-every", type=int, default=8)
+    ap.add_argument("--dp-epsilon", type=float, default=10.0)
     ap.add_argument("--valid-limit", type=int, default=2048)
     ap.add_argument("--no-valid", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
@@ -66,14 +77,40 @@ def main() -> int:
     if dev.type == "cuda":
         native.lib()  # hard requirement on the GPU path
 
-    cfg = FedRecConfig(mode="grad_avg", batch_size=args.batch, seed=0)
+    from fedrec_with_pytorchdistributed_amd.config import BackboneConfig
+    from fedrec_with_pytorchdistributed_amd.parallel import comm
+    from fedrec_with_pytorchdistributed_amd.privacy.rdp import calibrate_client_sigma
+
+    cfg = FedRecConfig(mode="grad_avg" if args.config != 3 else "param_avg", batch_size=args.batch, seed=0)
+    if args.config == 3:
+        cfg.local_update = "per_step"
+    if args.config == 5:
+        cfg.backbone = BackboneConfig.preset("bert-base")  # 12 layers, unfrozen
     torch.manual_seed(0)  # same init on every client (GA keeps them identical)
     model = FedRecModel(cfg).to(dev)
     model.build_flat()
     spec = SynthSpec.preset(args.preset)
     corpus = SyntheticCorpus(spec)
     shard = corpus.client_shard(ctx.rank, world)
-    eng = LocalEngine(cfg, model, shard, dev, rank=ctx.rank, grad_allreduce=fdist.make_grad_allreduce(ctx))
+    if args.config == 5:
+        ar = fdist.make_secure_grad_allreduce(ctx)
+    elif args.config == 3:
+        ar = None
+    else:
+        ar = fdist.make_grad_allreduce(ctx)
+    eng = LocalEngine(cfg, model, shard, dev, rank=ctx.rank, grad_allreduce=ar)
+    if args.config == 4:
+        cfg.dp.enabled, cfg.dp.epsilon = True, args.dp_epsilon
+        eng.sigma = calibrate_client_sigma(cfg.dp.epsilon, cfg.dp.delta, cfg.batch_size, len(shard.train), cfg.dp.epochs)
+    pa_state = {"n": 0}
+
+    def step(c, h):
+        loss = eng.train_step(c, h)
+        if args.config == 3:
+            pa_state["n"] += 1
+            if world > 1 and pa_state["n"] % args.pa_every == 0:
+                comm.allreduce_(model.sync_tensors(False), ctx.data_group, scale=1.0 / world)
+        return loss
 
     # batches: sampled on the fly inside the timed loop (host sampler + H2D copy)
     it = iter(())
@@ -94,7 +131,7 @@ def main() -> int:
             torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
-        eng.train_step(*next_batch())
+        step(*next_batch())
     sync()
     if ctx.initialized:
         dist.barrier(group=ctx.ctrl_group)
@@ -102,7 +139,7 @@ def main() -> int:
     t0 = time.perf_counter()
     losses = []
     for _ in range(args.steps):
-        losses.append(eng.train_step(*next_batch()))
+        losses.append(step(*next_batch()))
     sync()
     if ctx.initialized:
         dist.barrier(group=ctx.ctrl_group)
@@ -138,16 +175,16 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / REF_IMPRESSIONS_PER_S, 2),
-            "dtype": "bf16",
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": f"synthetic ({args.preset} MIND-format shard per client, random-init weights)",
             "config": {
-                "model": "DistilBERT-base text encoder (6L/768/12H, frozen, random init) + additive head + "
-                         "20-head user encoder",
+                "model": MODELS[args.config],
                 "global_batch": args.batch * world,
                 "seq_len": cfg.title_len,
                 "history_len": cfg.max_his_len,
                 "parallelism": f"dp{world}",
-                "mode": "Gradient_Averaging (RCCL all-reduce of flat 4.66 MB grad bucket per step)",
+                "mode": MODES[args.config].format(k=args.pa_every),
+                "baseline_config": args.config,
             },
             "train_loss": round(loss, 5),
             "valid_auc": None if auc is None else round(auc, 4),

@@ -37,6 +37,8 @@ int fr_score_ce(const float* cand, const float* user, float* loss, float* scores
                 int C, int D, int sigm, hipStream_t s);
 int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, float* out, int U, int D, float clip,
                         float noise_std, unsigned long long seed, unsigned long long offset, hipStream_t s);
+int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
+                unsigned long long offset, hipStream_t s);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
@@ -283,9 +285,15 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
   const c10::DeviceGuard g(rows.device());
   const int64_t D = rows.size(-1);
   auto out = at::empty({num_out, D}, rows.options());
-  check_rc(fr_segment_sum_rows(rows.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(),
-                               out.data_ptr<float>(), (int)num_out, (int)D, (float)clip, (float)noise_std,
-                               (unsigned long long)seed, (unsigned long long)offset, cur_stream()),
+  at::Tensor src = rows;
+  if (clip > 0.0 || noise_std > 0.0) {  // LDP: clip + noise every occurrence first (parallel pass)
+    src = at::empty_like(rows);
+    check_rc(fr_ldp_rows(rows.data_ptr<float>(), src.data_ptr<float>(), (int)(rows.numel() / D), (int)D, (float)clip,
+                         (float)noise_std, (unsigned long long)seed, (unsigned long long)offset, cur_stream()),
+             "ldp_rows");
+  }
+  check_rc(fr_segment_sum_rows(src.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(),
+                               out.data_ptr<float>(), (int)num_out, (int)D, 0.f, 0.f, 0ull, 0ull, cur_stream()),
            "segment_sum_rows");
   return out;
 }

@@ -10,49 +10,63 @@
 //
 // LDP: per-occurrence L2 clip to C (clip > 0), then Gaussian noise N(0, std) with
 // std = sigma * C (default) or sigma (reference quirk Q10: no clip, std = sigma).  Noise
-// comes from Philox-4x32-10 keyed by (seed, offset=step) with counter = occurrence*D + d,
-// so a row's noise does not depend on which wave processes it.
+// comes from Philox-4x32-10 keyed by (seed, offset=step) with a counter derived from the
+// occurrence row, so it does not depend on which wave processes it.  Two passes: the
+// per-occurrence clip+noise pass is embarrassingly parallel; the segment sum is skewed.
 #include "common.h"
 
 namespace {
 
 constexpr int MAXV = 8;   // D <= 512
-constexpr int NW = 4;     // waves per segment
+constexpr int NW = 16;    // waves per segment block
 constexpr int UNR = 4;    // rows in flight per wave
 
-// one row's (clipped, noised) contribution added into acc
-__device__ __forceinline__ void add_row(float (&acc)[MAXV], const float (&v)[MAXV], int r, int D, int lane, float clip,
-                                        float noise_std, unsigned long long seed, unsigned long long offset) {
-  float f = 1.0f;
-  if (clip > 0.f) {
-    float sq = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) sq += v[k] * v[k];
-    const float nrm = sqrtf(wave_sum(sq));
-    f = fminf(1.0f, clip / (nrm + 1e-12f));
-  }
+// Pass 1 (LDP only): one wave per occurrence row -- clip to C, add N(0, std).  Fully
+// parallel over all R = B*(C+H) occurrences, so the per-element Philox work never sits
+// behind one popular news id.  Each Philox call yields 4 uniforms -> 4 normals (2 x
+// Box-Muller), counter = (row, element group of 4): independent of the launch geometry.
+__global__ __launch_bounds__(256) void ldp_rows_kernel(const float* __restrict__ rows, float* __restrict__ out, int R,
+                                                       int D, float clip, float noise_std, unsigned long long seed,
+                                                       unsigned long long offset) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* g = rows + (size_t)r * D;
+  float v[MAXV];
+  float sq = 0.f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int d = lane + 64 * k;
-    if (d < D) {
-      float x = v[k] * f;
-      if (noise_std > 0.f) {
-        const uint4 rnd = Philox::gen(seed, offset, (unsigned long long)r * D + d);
-        x += noise_std * box_muller(rnd.x, rnd.y).x;
-      }
-      acc[k] += x;
+    v[k] = d < D ? g[d] : 0.f;
+    sq += v[k] * v[k];
+  }
+  float f = 1.0f;
+  if (clip > 0.f) f = fminf(1.0f, clip / (sqrtf(wave_sum(sq)) + 1e-12f));
+  // element d = lane + 64k; noise for elements (4j .. 4j+3) of the row from counter (r, j)
+#pragma unroll
+  for (int k = 0; k < MAXV; k += 4) {
+    // lanes of this pass cover elements lane + 64k .. lane + 64(k+3): counter per (r, lane, k/4)
+    float nz[4] = {0.f, 0.f, 0.f, 0.f};
+    if (noise_std > 0.f) {
+      const uint4 rnd = Philox::gen(seed, offset, ((unsigned long long)r << 16) | (unsigned)(lane * 2 + (k >> 2)));
+      const float2 a = box_muller(rnd.x, rnd.y), b = box_muller(rnd.z, rnd.w);
+      nz[0] = a.x; nz[1] = a.y; nz[2] = b.x; nz[3] = b.y;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = lane + 64 * (k + t);
+      if (d < D) out[(size_t)r * D + d] = v[k + t] * f + noise_std * nz[t];
     }
   }
 }
 
-// One 256-thread block per output row (segment).  Wave w takes occurrences beg+w, beg+w+4,
-// ... with UNR independent row loads in flight (popular news -- and the <unk>/pad row 0 that
-// every short history points at -- have hundreds of occurrences per batch); the 4 wave
-// partials are combined in LDS in a fixed order, so the result is deterministic.
-__global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ rows, const int* __restrict__ perm,
-                                                     const int* __restrict__ seg_ptr, float* __restrict__ out, int U,
-                                                     int D, float clip, float noise_std, unsigned long long seed,
-                                                     unsigned long long offset) {
+// Pass 2: deterministic segment sum.  One 1024-thread block (16 waves) per output row:
+// wave w takes occurrences beg+w, beg+w+16, ... with UNR row loads in flight; the 16
+// partials are combined in LDS in a fixed order.  The <unk>/pad row 0 -- every short
+// history points at it, ~1000 occurrences per batch -- is spread over 16 waves.
+__global__ __launch_bounds__(1024) void segsum_kernel(const float* __restrict__ rows, const int* __restrict__ perm,
+                                                      const int* __restrict__ seg_ptr, float* __restrict__ out, int U,
+                                                      int D) {
   __shared__ float part[NW][64 * MAXV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int u = blockIdx.x;
@@ -62,40 +76,50 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ r
   const int beg = seg_ptr[u], end = seg_ptr[u + 1];
   for (int i0 = beg + w; i0 < end; i0 += NW * UNR) {
     float v[UNR][MAXV];
-    int rr[UNR];
 #pragma unroll
     for (int j = 0; j < UNR; ++j) {
       const int i = i0 + j * NW;
-      rr[j] = i < end ? perm[i] : -1;
-    }
-#pragma unroll
-    for (int j = 0; j < UNR; ++j) {
-      const float* g = rows + (size_t)(rr[j] < 0 ? 0 : rr[j]) * D;
+      const int r = i < end ? perm[i] : -1;
+      const float* g = rows + (size_t)(r < 0 ? 0 : r) * D;
 #pragma unroll
       for (int k = 0; k < MAXV; ++k) {
         const int d = lane + 64 * k;
-        v[j][k] = (rr[j] >= 0 && d < D) ? g[d] : 0.f;
+        v[j][k] = (r >= 0 && d < D) ? g[d] : 0.f;
       }
     }
 #pragma unroll
     for (int j = 0; j < UNR; ++j)
-      if (rr[j] >= 0) add_row(acc, v[j], rr[j], D, lane, clip, noise_std, seed, offset);
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) acc[k] += v[j][k];
   }
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) part[w][lane + 64 * k] = acc[k];
   __syncthreads();
   float* o = out + (size_t)u * D;
-  for (int d = threadIdx.x; d < D; d += 256) o[d] = ((part[0][d] + part[1][d]) + part[2][d]) + part[3][d];
+  for (int d = threadIdx.x; d < D; d += 1024) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) t += part[q][d];
+    o[d] = t;
+  }
 }
 
 }  // namespace
+
+extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std,
+                           unsigned long long seed, unsigned long long offset, hipStream_t s) {
+  if (D > 64 * MAXV) return 1;
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(ldp_rows_kernel, dim3((R + 3) / 4), dim3(256), 0, s, rows, out, R, D, clip, noise_std, seed,
+                     offset);
+  return 0;
+}
 
 extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, float* out, int U, int D,
                                    float clip, float noise_std, unsigned long long seed, unsigned long long offset,
                                    hipStream_t s) {
   if (D > 64 * MAXV) return 1;
   if (U == 0) return 0;
-  hipLaunchKernelGGL(segsum_kernel, dim3(U), dim3(256), 0, s, rows, perm, seg_ptr, out, U, D, clip,
-                     noise_std, seed, offset);
+  hipLaunchKernelGGL(segsum_kernel, dim3(U), dim3(1024), 0, s, rows, perm, seg_ptr, out, U, D);
   return 0;
 }

@@ -14,6 +14,7 @@ Collective timeouts default to minutes, not the reference's 2 days (``client.py:
 from __future__ import annotations
 
 import datetime
+import math
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -112,6 +113,58 @@ def make_grad_allreduce(ctx: DistContext):
 
     def _ar(flat_grad: torch.Tensor) -> float:
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=ctx.data_group)
+        return 1.0 / W
+
+    return _ar
+
+
+def make_secure_grad_allreduce(ctx: DistContext, frac_bits: Optional[int] = None, clip: float = 32.0,
+                               timeout_s: float = 600.0, run_id: str = "secagg-ga"):
+    """Gradient averaging under pairwise-mask secure aggregation (BASELINE config 5).
+
+    Each client uploads ``Q(g) + sum_j +-PRG(s_ij, step)`` as wrap-around int32; one RCCL
+    int32 SUM all-reduce cancels the masks exactly; the result is dequantised in place.
+    Pair seeds come from a Diffie-Hellman exchange of public keys over the store.  The
+    fixed-point range must hold the W-client sum: ``W * clip * 2^frac_bits < 2^31``.
+
+    ``frac_bits=None`` (default) picks the fixed-point scale per step: the clients agree on
+    ``m = max_k max|g_k|`` with one scalar MAX all-reduce (the only value revealed beyond
+    the sum) and use the largest power of two with ``W * m * 2^f < 2^30`` -- a fixed
+    2^-22 grid is coarser than the small gradients of the head layers, which Adam's
+    normalisation then amplifies."""
+    from . import secagg
+    from .control import ControlPlane
+
+    if ctx.num_clients <= 1 or not ctx.initialized:
+        return None
+    W, k = ctx.num_clients, ctx.client_index
+    if frac_bits is not None and W * clip * (1 << frac_bits) >= 2 ** 31:
+        raise ValueError(f"secure aggregation range overflow: {W} x {clip} x 2^{frac_bits} >= 2^31")
+    cp = ControlPlane.from_default(run_id, timeout_s)
+    kp = secagg.KeyPair()
+    cp.set(f"pk/{k}", secagg.public_bytes(kp))
+    pubs = [cp.get(f"pk/{j}") for j in range(W)]
+    seeds_row = secagg.seeds_from_publics(kp, k, pubs)
+    state = {"step": 0}
+
+    def _scale(flat_grad: torch.Tensor):
+        if frac_bits is not None:
+            return frac_bits, clip
+        m = torch.nan_to_num(flat_grad.abs().max().float().reshape(1), nan=0.0, posinf=3.0e38)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=ctx.data_group)
+        mv = max(float(m.item()), 1e-30)
+        f = int(math.floor(math.log2((2.0 ** 30) / (W * mv))))
+        f = max(0, min(f, 56))
+        return f, mv
+
+    def _ar(flat_grad: torch.Tensor) -> float:
+        fb, cl = _scale(flat_grad)
+        q = secagg.mask_local(flat_grad, k, W, seeds_row, state["step"], fb, cl)
+        if q.device != flat_grad.device:
+            q = q.to(flat_grad.device)
+        dist.all_reduce(q, op=dist.ReduceOp.SUM, group=ctx.data_group)
+        flat_grad.copy_(secagg.unmask_sum(q, fb).view_as(flat_grad))
+        state["step"] += 1
         return 1.0 / W
 
     return _ar

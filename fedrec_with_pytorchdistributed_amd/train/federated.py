@@ -36,7 +36,7 @@ from ..models.fedrec_model import FedRecModel
 from ..parallel import comm
 from ..parallel import secagg
 from ..parallel.control import ControlPlane
-from ..parallel.dist import DistContext, make_grad_allreduce
+from ..parallel.dist import DistContext, make_grad_allreduce, make_secure_grad_allreduce
 from ..privacy.rdp import calibrate_client_sigma
 from ..utils import obs
 from ..utils.fault import FaultInjector
@@ -139,7 +139,9 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     model = build_model(cfg, ctx.device)
     start = _resume(cfg, model)
     _sync_initial(model, ctx, cfg.sync == "full")
-    eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=make_grad_allreduce(ctx))
+    ar = (make_secure_grad_allreduce(ctx, timeout_s=cfg.collective_timeout_s) if cfg.secagg.enabled
+          else make_grad_allreduce(ctx))
+    eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=ar)
     eng.sigma = _maybe_dp(cfg, eng)
     eng.epoch = start
     writer = _metrics_writer(cfg, ctx.client_index == 0)

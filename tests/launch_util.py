@@ -5,6 +5,7 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,13 +22,18 @@ def run_ranks(argvs, env_extra=None, timeout=240, cwd=None):
     still running at the timeout are killed (returncode None)."""
     port = free_port()
     procs = []
+    # run in a scratch directory so default output paths (metrics.jsonl, snapshots) never
+    # land in the source tree; entry scripts are resolved against the repo root
+    cwd = cwd or tempfile.mkdtemp(prefix="fedrec_ranks_")
+    argvs = [[os.path.join(ROOT, a[0]) if a and a[0].endswith(".py") and not os.path.isabs(a[0]) else a[0], *a[1:]]
+             for a in argvs]
     for r, argv in enumerate(argvs):
         env = dict(os.environ)
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(len(argvs)), "MASTER_ADDR": "127.0.0.1",
                     "MASTER_PORT": str(port), "FEDREC_CPU_ONLY": "1", "OMP_NUM_THREADS": "1",
                     "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", ""), "FEDREC_QUIET": "0"})
         env.update(env_extra or {})
-        procs.append(subprocess.Popen([sys.executable, *argv], cwd=cwd or ROOT, env=env, stdout=subprocess.PIPE,
+        procs.append(subprocess.Popen([sys.executable, *argv], cwd=cwd, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
     deadline = time.monotonic() + timeout
     outs = []

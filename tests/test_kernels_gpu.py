@@ -145,6 +145,27 @@ def test_ldp_noise_statistics(dev):
     assert abs(float(out.std()) - 3.0) < 0.03
     out2 = ops.segment_sum_rows(rows, inv, R, clip=2.0, noise_std=3.0, seed=5, offset=1, seg=(perm, ptr))
     assert torch.equal(out, out2)  # counter-based: reproducible
+    # element-wise independence: neighbouring elements / rows uncorrelated
+    z = out / 3.0
+    assert abs(float((z[:, :-1] * z[:, 1:]).mean())) < 0.01
+    assert abs(float((z[:-1] * z[1:]).mean())) < 0.01
+    out3 = ops.segment_sum_rows(rows, inv, R, clip=2.0, noise_std=3.0, seed=5, offset=2, seg=(perm, ptr))
+    assert abs(float((out3 * out).mean()) / 9.0) < 0.01  # new step offset -> fresh noise
+
+
+def test_segment_sum_skewed_pad_row(dev):
+    """The pad/<unk> news id collects most history occurrences in a real batch (one segment
+    of ~2000 rows next to hundreds of 1-row segments): exact vs the fp32 oracle."""
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(1, 700, (64 * 55,), generator=g, dtype=torch.int32)
+    ids[torch.rand(ids.numel(), generator=g) < 0.6] = 0
+    ids = ids.to(dev)
+    uniq, inv, perm, ptr = ops.dedup(ids, 700)
+    rows = torch.randn(ids.numel(), 400, device=dev)
+    out = ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr))
+    assert rel_err(out, ref.segment_sum_rows(rows, inv, uniq.numel())) < 1e-6
+    out_c = ops.segment_sum_rows(rows, inv, uniq.numel(), clip=1.5, seg=(perm, ptr))
+    assert rel_err(out_c, ref.segment_sum_rows(rows, inv, uniq.numel(), clip=1.5)) < 1e-5
 
 
 def test_adam_flat(dev):
