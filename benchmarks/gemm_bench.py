@@ -26,18 +26,22 @@ def main():
     ap.add_argument("--M", type=int, default=78850)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--out", default="")
+    ap.add_argument("--shapes", default="model", help="model | square (8192^3 / 4096^3, no epilogue)")
     a = ap.parse_args()
     lib = native.lib()
     dev = torch.device("cuda")
     shapes = [("qkv", 2304, 768, 0, False), ("out_proj+res", 768, 768, 0, True), ("ffn1+gelu", 3072, 768, 1, False),
               ("ffn2+res", 768, 3072, 0, True), ("head_fc1+tanh", 384, 768, 2, False)]
+    if a.shapes == "square":
+        shapes = [("sq8192", 8192, 8192, 0, False), ("sq4096", 4096, 4096, 0, False)]
     res = {}
     for name, N, K, act, has_res in shapes:
-        x = (torch.rand(a.M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        M = N if name.startswith("sq") else a.M
+        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         b = torch.rand(N, device=dev)
-        r = (torch.rand(a.M, N, device=dev) * 2 - 1).to(torch.bfloat16) if has_res else None
-        flops = 2.0 * a.M * N * K
+        r = (torch.rand(M, N, device=dev) * 2 - 1).to(torch.bfloat16) if has_res else None
+        flops = 2.0 * M * N * K
         variants = {}
 
         def ours(v):
@@ -53,6 +57,7 @@ def main():
             variants["ours-256s"] = ours(3)
             variants["ours-256p-split"] = ours(4)
             variants["ours-256p-split-pipe"] = ours(5)
+            variants["ours-pingpong"] = ours(6)
         bb = b.to(torch.bfloat16)
 
         def lt():
@@ -86,7 +91,7 @@ def main():
             med = statistics.median(ts)
             err = float((variants[k]().float() - ref).norm() / ref.norm()) if k.startswith("ours") else 0.0
             row[k] = {"ms": round(med, 4), "tflops": round(flops / med / 1e9, 1), "rel_err_vs_lib": round(err, 5)}
-        res[f"{name} M={a.M} N={N} K={K}"] = row
+        res[f"{name} M={M} N={N} K={K}"] = row
         print(name, json.dumps(row), flush=True)
     if a.out:
         with open(a.out, "w") as f:

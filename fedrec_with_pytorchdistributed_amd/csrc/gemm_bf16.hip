@@ -21,6 +21,11 @@
 //     XCD's L2 (bijective remap, §5.5 T1).
 // Requirements (checked on the host): N % 128 == 0, K % 64 == 0; any M (rows clamped on
 // load, masked on store).
+//
+// Variants (fr_gemm_set_variant; -1 = auto): 0 the 128x128 kernel above; 1 256x256; 2 its
+// persistent form; 3 BK=32 four-stage; 4/5 persistent with split staging (+ register-
+// pipelined fragments); 6 persistent 256x256 ping-pong (two wave rows half a phase apart).
+// Auto: 6 for N % 256 == 0 without GELU, 5 with GELU, 0 otherwise (benchmarks/gemm_bench.py).
 #include "common.h"
 
 namespace {
@@ -533,6 +538,222 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256s_kernel(const bf16* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Variant 6: 256x256x64 persistent "ping-pong" GEMM (cdna_hip_programming.md §5, 256² 8-phase
+// template), 512 threads = 8 waves (2 along M x 4 along N), 128x64 outputs per wave.
+//
+// * LDS = 2 K-buffers x 4 half-tiles x 16 KB = 128 KB (one block per CU).  A half-tile is
+//   128 rows x 64 K of ONE operand: A_h0 = the rows of output quadrant qm = 0 of both wave
+//   rows, A_h1 = qm = 1; B_h0 = columns of quadrant qn = 0 of all four wave columns, B_h1 =
+//   qn = 1.  Each half is staged by all 512 threads with 2 global_load_lds x 16 B.
+// * A K-step is 4 phases; phase = [ds_read fragments + stage one half-tile] s_barrier
+//   [16 MFMAs of one 64x32 quadrant] s_barrier.  Quadrant order (0,0) (0,1) (1,1) (1,0)
+//   keeps one operand in registers between phases (24 ds_read_b128 per K-step per wave).
+// * Waves of M-row 1 execute one extra s_barrier up front, so the two wave rows run half a
+//   phase apart: on every SIMD one wave issues MFMAs while its partner reads LDS/stages.
+// * Stage schedule (step s, phase j): j0 -> A_h1 of s+1; j1 -> A_h0 of s+2; j2 -> B_h0 of
+//   s+2; j3 -> B_h1 of s+2, then s_waitcnt vmcnt(6) retires everything of step s+1 (the
+//   three younger half-tiles stay in flight across the barrier).  Every half is restaged
+//   >= 1 phase after its last ds_read (whose lgkmcnt(0) precedes that phase's barrier)
+//   and read >= 1 phase after the wait that retires it.
+// * The K-step stream runs across output tiles (persistent, one block per CU, XCD-aware
+//   tile walk): the next tile's first half-tiles are in flight during the current tile's
+//   last phases; each wave row stores its tile while the other row is still on MFMAs.
+constexpr int PP_HALF = 16384;
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int ACT, bool HAS_BIAS, bool HAS_RES>
+__global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                            const float* __restrict__ bias,
+                                                            const bf16* __restrict__ R, bf16* __restrict__ C, int M,
+                                                            int N, int K, int tiles_n, int ntiles) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * PP_HALF];
+  const int G = gridDim.x, b = blockIdx.x;
+  const int c = (G % 8 == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
+  if (c >= ntiles) return;
+  const int nk = K >> 6;
+  const int S = ((ntiles - c + G - 1) / G) * nk;  // K-steps of this block's stream
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rsub = lane >> 3, schunk = (lane & 7) ^ rsub;
+
+  // Per-thread source offsets (elements, < 2^31: checked on the host) of the 8 rows this
+  // thread stages per K-step -- 2 per half-tile -- for the current tile and the next one.
+  // Computed once per tile, so a phase's staging is 2 adds + 2 glds (no index math).
+  int ocur[4][2], onxt[4][2];
+  auto tile_offs = [&](int itile, int (&o)[4][2]) {
+    int t = itile * G + c;
+    t = t < ntiles ? t : c;
+    const int mt = t / tiles_n;
+    const int m0 = mt * 256, n0 = (t - mt * tiles_n) * 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rho = wave * 16 + i * 8 + rsub;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int gm = m0 + (rho >> 6) * 128 + h * 64 + (rho & 63);
+        gm = gm < M ? gm : M - 1;
+        o[h][i] = gm * K + schunk * 8;
+        o[2 + h][i] = (n0 + (rho >> 5) * 64 + h * 32 + (rho & 31)) * K + schunk * 8;
+      }
+    }
+  };
+  // stage half h of K-step g (tile-relative K index kts; `nx` = g lies in the next tile)
+  auto stage = [&](int g, int h, int kts, bool nx) {
+    if (g >= S) return;
+    char* dst = smem + ((g & 1) * 4 + h) * PP_HALF;
+    const bf16* base = (h < 2 ? A : W) + kts * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int off = nx ? onxt[h][i] : ocur[h][i];
+      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, base + off),
+                                       LDS_PTR(void, dst + (wave * 16 + i * 8) * 128), 16, 0, 0);
+    }
+  };
+
+  // prologue: step 0 (all four halves) + step 1's A_h0, B_h0, B_h1; retire step 0
+  tile_offs(0, ocur);
+  tile_offs(1, onxt);
+  stage(0, 0, 0, false); stage(0, 2, 0, false); stage(0, 3, 0, false); stage(0, 1, 0, false);
+  stage(1, 0, 1, false); stage(1, 2, 1, false); stage(1, 3, 1, false);
+  if (S > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (wr == 1) pp_barrier();
+
+  f32x4 acc[2][4][2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[q][i][p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = (wr * 64 + fr) * 128, brow = (wc * 32 + fr) * 128;
+  const int ph0 = ((0 * 4 + fq) ^ (fr & 7)) * 16, ph1 = ((1 * 4 + fq) ^ (fr & 7)) * 16;
+  auto read_a = [&](const char* hb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *(const bf16x8*)(hb + arow + i * 16 * 128 + ph0);
+      af[i][1] = *(const bf16x8*)(hb + arow + i * 16 * 128 + ph1);
+    }
+  };
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf[j][0] = *(const bf16x8*)(hb + brow + j * 16 * 128 + ph0);
+      bf[j][1] = *(const bf16x8*)(hb + brow + j * 16 * 128 + ph1);
+    }
+  };
+#define PP_MFMA(QM, QN, BF)                                                                             \
+  {                                                                                                     \
+    pp_barrier();                                                                                       \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                \
+    __builtin_amdgcn_s_setprio(1);                                                                      \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) _Pragma("unroll") for (int i = 0; i < 4; ++i)      \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[QM][i][QN][j] =                               \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j][kk], af[i][kk], acc[QM][i][QN][j], 0, 0, 0);  \
+    __builtin_amdgcn_s_setprio(0);                                                                      \
+    pp_barrier();                                                                                       \
+  }
+
+  int kt = 0, it = 0;
+  for (int g = 0; g < S; ++g) {
+    const char* buf = smem + (g & 1) * 4 * PP_HALF;
+    const bool nx1 = kt + 1 >= nk, nx2 = kt + 2 >= nk;  // nk >= 2 (host): g+2 is at most one tile ahead
+    const int k1 = nx1 ? kt + 1 - nk : kt + 1, k2 = nx2 ? kt + 2 - nk : kt + 2;
+    // phase 0: quadrant (0,0)
+    read_a(buf);
+    read_b(buf + 2 * PP_HALF, b0);
+    stage(g + 1, 1, k1, nx1);
+    PP_MFMA(0, 0, b0)
+    // phase 1: quadrant (0,1)
+    read_b(buf + 3 * PP_HALF, b1);
+    stage(g + 2, 0, k2, nx2);
+    PP_MFMA(0, 1, b1)
+    // phase 2: quadrant (1,1)
+    read_a(buf + PP_HALF);
+    stage(g + 2, 2, k2, nx2);
+    PP_MFMA(1, 1, b1)
+    // phase 3: quadrant (1,0); retire step g+1
+    stage(g + 2, 3, k2, nx2);
+    if (g + 2 < S) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PP_MFMA(1, 0, b0)
+    if (++kt == nk) {
+      // epilogue: this wave row's 128 x 64 of the finished tile.  Bias once per tile; the
+      // residual rows of one 64-row quadrant are all loaded before any is consumed (one
+      // memory round trip per quadrant instead of one per row).
+      const int t = it * G + c;
+      const int mt = t / tiles_n;
+      const int m0 = mt * 256, n0 = (t - mt * tiles_n) * 256;
+      const int nb0 = n0 + wc * 64 + fq * 4;
+      float4 bb[2][2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bb[p][j] = HAS_BIAS ? *(const float4*)(bias + nb0 + p * 32 + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        bf16x4 rr[4][2][2];
+        if constexpr (HAS_RES) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            int m = m0 + wr * 128 + q * 64 + i * 16 + fr;
+            m = m < M ? m : M - 1;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) rr[i][p][j] = *(const bf16x4*)(R + (size_t)m * N + nb0 + p * 32 + j * 16);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wr * 128 + q * 64 + i * 16 + fr;
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              f32x4& a4 = acc[q][i][p][j];
+              float v0 = act_fn<ACT>(a4[0] + bb[p][j].x), v1 = act_fn<ACT>(a4[1] + bb[p][j].y);
+              float v2 = act_fn<ACT>(a4[2] + bb[p][j].z), v3 = act_fn<ACT>(a4[3] + bb[p][j].w);
+              if constexpr (HAS_RES) {
+                v0 += (float)rr[i][p][j][0]; v1 += (float)rr[i][p][j][1];
+                v2 += (float)rr[i][p][j][2]; v3 += (float)rr[i][p][j][3];
+              }
+              if (m < M) {
+                bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+                *(bf16x4*)(C + (size_t)m * N + nb0 + p * 32 + j * 16) = o;
+              }
+              a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+      }
+      kt = 0;
+      ++it;
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ocur[h][i] = onxt[h][i];
+      tile_offs(it + 1, onxt);
+    }
+  }
+#undef PP_MFMA
+  if (wr == 0) pp_barrier();  // balance the staggered row's extra barrier
+}
+
 int g_num_cus = 0;
 
 int g_gemm_variant = -1;  // -1 auto, 0 = 128x128, 1 = 256x256
@@ -541,6 +762,28 @@ template <int ACT>
 void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, bf16* C, int M, int N, int K,
                 hipStream_t s) {
   const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && N % BN2 == 0 && M >= 4096);
+  // auto policy (measured, profiles/gemm_bench_r1_pp.json): the ping-pong kernel (6) wins on the
+  // bias / bias+residual shapes; with the GELU epilogue the non-staggered split-pipe kernel (5)
+  // hides the longer epilogue better.
+  const bool pp = g_gemm_variant == 6 || (g_gemm_variant < 0 && ACT != 1);
+  if (big && N % BN2 == 0 && pp && K >= 128 && (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
+    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
+    if (g_num_cus == 0) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
+    dim3 grid(G), block(512);
+#define LPP(HB, HR) hipLaunchKernelGGL((gemm_nt_pp_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
+    if (bias && R) LPP(true, true);
+    else if (bias) LPP(true, false);
+    else if (R) LPP(false, true);
+    else LPP(false, false);
+#undef LPP
+    return;
+  }
   if (big && N % BN2 == 0 && g_gemm_variant == 3 && K % BK3 == 0) {
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     if (g_num_cus == 0) {
