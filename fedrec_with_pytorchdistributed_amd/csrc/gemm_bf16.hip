@@ -25,7 +25,7 @@
 // Variants (fr_gemm_set_variant; -1 = auto): 0 the 128x128 kernel above; 1 256x256; 2 its
 // persistent form; 3 BK=32 four-stage; 4/5 persistent with split staging (+ register-
 // pipelined fragments); 6 persistent 256x256 ping-pong (two wave rows half a phase apart).
-// Auto: 6 for N % 256 == 0 without GELU, 5 with GELU, 0 otherwise (benchmarks/gemm_bench.py).
+// Auto: 6 for N % 256 == 0 (K >= 128), 0 otherwise (benchmarks/gemm_bench.py).
 #include "common.h"
 
 namespace {
@@ -49,6 +49,40 @@ __device__ __forceinline__ float act_fn(float x) {
   if constexpr (ACT == 1) return gelu_erf(x);
   else if constexpr (ACT == 2) return tanhf(x);
   else return x;
+}
+
+// GELU(erf) on a pair, written so the polynomial and scalings lower to packed f32 VALU
+// (v_pk_fma_f32 / v_pk_mul_f32: two elements per instruction); only v_rcp / v_exp stay
+// per element.  Same A&S 7.1.26 erf as gelu_erf, algebra folded:
+//   Phi(x) = 1 - h (x >= 0), h (x < 0),  h = 0.5 * P(t) * exp(-z^2),  z = |x| / sqrt(2),
+//   t = 1 / (1 + p z)  ->  GELU = x >= 0 ? x - x h : x h.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_pair(f32x2 x) {
+  const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f32x2 d = z * 0.3275911f + 1.0f;
+  f32x2 t;
+  t.x = __builtin_amdgcn_rcpf(d.x);
+  t.y = __builtin_amdgcn_rcpf(d.y);
+  const f32x2 P = t * (0.127414796f + t * (-0.142248368f + t * (0.7107068705f + t * (-0.7265760135f + t * 0.5307027145f))));
+  const f32x2 q = z * z * -1.44269504088896341f;
+  f32x2 e;
+  e.x = __builtin_amdgcn_exp2f(q.x);
+  e.y = __builtin_amdgcn_exp2f(q.y);
+  const f32x2 r = x * (P * e);
+  f32x2 o;
+  o.x = x.x >= 0.f ? x.x - r.x : r.x;
+  o.y = x.y >= 0.f ? x.y - r.y : r.y;
+  return o;
+}
+
+template <int ACT>
+__device__ __forceinline__ void act4(float& v0, float& v1, float& v2, float& v3) {
+  if constexpr (ACT == 1) {
+    const f32x2 a = gelu_pair(f32x2{v0, v1}), b = gelu_pair(f32x2{v2, v3});
+    v0 = a.x; v1 = a.y; v2 = b.x; v3 = b.y;
+  } else {
+    v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+  }
 }
 
 // issue the glds for one K-tile into stage `st`
@@ -139,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const bf16* __restrict_
         const float4 bb = *(const float4*)(bias + nb);
         v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
       }
-      v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+      act4<ACT>(v0, v1, v2, v3);
       if constexpr (HAS_RES) {
         const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
         v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
@@ -267,7 +301,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256_kernel(const bf16* __restr
         const float4 bb = *(const float4*)(bias + nb);
         v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
       }
-      v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+      act4<ACT>(v0, v1, v2, v3);
       if constexpr (HAS_RES) {
         const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
         v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
@@ -397,7 +431,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __rest
           const float4 bb = *(const float4*)(bias + nb);
           v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
         }
-        v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+        act4<ACT>(v0, v1, v2, v3);
         if constexpr (HAS_RES) {
           const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
           v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
@@ -526,7 +560,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256s_kernel(const bf16* __rest
           const float4 bb = *(const float4*)(bias + nb);
           v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
         }
-        v0 = act_fn<ACT>(v0); v1 = act_fn<ACT>(v1); v2 = act_fn<ACT>(v2); v3 = act_fn<ACT>(v3);
+        act4<ACT>(v0, v1, v2, v3);
         if constexpr (HAS_RES) {
           const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
           v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
@@ -727,8 +761,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restri
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
               f32x4& a4 = acc[q][i][p][j];
-              float v0 = act_fn<ACT>(a4[0] + bb[p][j].x), v1 = act_fn<ACT>(a4[1] + bb[p][j].y);
-              float v2 = act_fn<ACT>(a4[2] + bb[p][j].z), v3 = act_fn<ACT>(a4[3] + bb[p][j].w);
+              float v0 = a4[0] + bb[p][j].x, v1 = a4[1] + bb[p][j].y;
+              float v2 = a4[2] + bb[p][j].z, v3 = a4[3] + bb[p][j].w;
+              act4<ACT>(v0, v1, v2, v3);
               if constexpr (HAS_RES) {
                 v0 += (float)rr[i][p][j][0]; v1 += (float)rr[i][p][j][1];
                 v2 += (float)rr[i][p][j][2]; v3 += (float)rr[i][p][j][3];
@@ -762,10 +797,9 @@ template <int ACT>
 void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, bf16* C, int M, int N, int K,
                 hipStream_t s) {
   const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && N % BN2 == 0 && M >= 4096);
-  // auto policy (measured, profiles/gemm_bench_r1_pp.json): the ping-pong kernel (6) wins on the
-  // bias / bias+residual shapes; with the GELU epilogue the non-staggered split-pipe kernel (5)
-  // hides the longer epilogue better.
-  const bool pp = g_gemm_variant == 6 || (g_gemm_variant < 0 && ACT != 1);
+  // auto policy (measured, profiles/gemm_bench_r1_pp.json): the ping-pong kernel (6) on every
+  // N % 256 == 0 shape (with the packed-f32 GELU epilogue it also edges out variant 5 on FFN1).
+  const bool pp = g_gemm_variant == 6 || g_gemm_variant < 0;
   if (big && N % BN2 == 0 && pp && K >= 128 && (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     if (g_num_cus == 0) {

@@ -1,5 +1,4 @@
 #!/bin/bash
 source "$(dirname "$0")/gpu_round.sh"
-run kgemm 300 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm_variants and 6"
+run kgemm 300 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm"
 run gemm 600 python benchmarks/gemm_bench.py --out gpurun_out/gemm_bench_pp.json
-run gemmsq 600 python benchmarks/gemm_bench.py --shapes square --rounds 5 --out gpurun_out/gemm_bench_sq.json
