@@ -1,0 +1,87 @@
+"""Per-kernel microbenchmarks at the shapes of one training step (mind-small, B = 64 ->
+~1577 unique titles x 50 tokens).  Reports median time, achieved HBM bandwidth (bytes the
+kernel must move at minimum) and, for the MFMA kernels, TFLOP/s.
+
+    python benchmarks/kernel_bench.py [--titles 1577] [--out gpurun_out/kernel_bench.json]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from fedrec_with_pytorchdistributed_amd.ops import native
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--titles", type=int, default=1577)
+    ap.add_argument("--T", type=int, default=50)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    lib = native.lib()
+    dev = torch.device("cuda")
+    n, T, D, H = a.titles, a.T, 768, 12
+    M = n * T
+    g = torch.Generator(device="cpu").manual_seed(0)
+    res = {}
+
+    def rec(name, ms, nbytes, flops=0.0):
+        row = {"ms": round(ms, 4), "GB/s": round(nbytes / ms / 1e6, 1)}
+        if flops:
+            row["TFLOP/s"] = round(flops / ms / 1e9, 1)
+        res[name] = row
+        print(name, row, flush=True)
+
+    want = lambda k: not a.only or k in a.only.split(",")
+    qkv = (torch.randn(M, 3 * D, generator=g) * 0.5).to(dev, torch.bfloat16)
+    lens = torch.randint(8, T + 1, (n,), generator=g)
+    mask = (torch.arange(T)[None, :] < lens[:, None]).to(torch.int32).to(dev)
+    if want("title_attention"):
+        for w in (-2, -1, 0, 1, 2, 4):
+            lib.title_attn_set_waves(w)
+            ms = timeit(lambda: lib.title_attention(qkv, mask, H))
+            rec(f"title_attention[{w}w]", ms, qkv.numel() * 2 + M * D * 2, 4.0 * n * H * T * T * 64)
+        lib.title_attn_set_waves(-2)
+    if want("title_attention_bwd"):
+        dout = (torch.randn(M, D, generator=g) * 0.1).to(dev, torch.bfloat16)
+        ms = timeit(lambda: lib.title_attention_bwd(qkv, dout, mask, H))
+        rec("title_attention_bwd", ms, qkv.numel() * 4 + M * D * 2, 8.0 * n * H * T * T * 64)
+    x = (torch.randn(M, D, generator=g)).to(dev, torch.bfloat16)
+    w, b = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    if want("layer_norm"):
+        ms = timeit(lambda: lib.layer_norm(x, w, b, 1e-12))
+        rec("layer_norm", ms, 2 * M * D * 2)
+    if want("embed_ln"):
+        word = (torch.randn(30522, D, generator=g) * 0.02).to(dev, torch.bfloat16)
+        pos = (torch.randn(512, D, generator=g) * 0.02).to(dev, torch.bfloat16)
+        tok = torch.randint(0, 30522, (n, T), generator=g, dtype=torch.int32).to(dev)
+        ms = timeit(lambda: lib.embed_ln(tok, word, pos, w, b, 1e-12))
+        rec("embed_ln", ms, 2 * M * D * 2)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

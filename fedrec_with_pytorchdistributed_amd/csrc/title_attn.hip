@@ -11,7 +11,7 @@
 //                          HF semantics: padded keys (mask 0) score finfo.min, so an all-zero
 //                          mask (news row 0) yields a uniform distribution over the T keys;
 //                          keys >= T (tile padding) are excluded (-inf)
-//   O = P . V              P re-used from the S^T accumulator layout as the A operand: the
+//   O^T = V^T . P^T        P re-used from the S^T accumulator layout as the B operand: the
 //                          k order inside a 32-key step is permuted (keys 4g..4g+3 and
 //                          16+4g..16+4g+3 for lane group g) and the V fragment is read with
 //                          the SAME permutation through two transposed LDS reads
@@ -25,11 +25,12 @@ namespace {
 
 constexpr int DH = 64;
 
-__global__ __launch_bounds__(256) void title_attn_kernel(const bf16* __restrict__ qkv, const int* __restrict__ mask,
-                                                         bf16* __restrict__ out, int n_titles, int T, int H, int D) {
-  __shared__ __attribute__((aligned(16))) bf16 vs[4][64 * DH];  // 32 KB
+template <int NWAVE>
+__global__ __launch_bounds__(64 * NWAVE) void title_attn_kernel(const bf16* __restrict__ qkv, const int* __restrict__ mask,
+                                                                bf16* __restrict__ out, int n_titles, int T, int H, int D) {
+  __shared__ __attribute__((aligned(16))) bf16 vs[NWAVE][64 * DH];  // 8 KB per wave
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pair = blockIdx.x * 4 + wave;
+  const int pair = blockIdx.x * NWAVE + wave;
   const bool active = pair < n_titles * H;
   const int title = active ? pair / H : 0;
   const int h = active ? pair - title * H : 0;
@@ -76,13 +77,15 @@ __global__ __launch_bounds__(256) void title_attn_kernel(const bf16* __restrict_
 
   // ---- masked softmax over keys s = 16 is + 4 fq + r, for query t = 16 jq + fr ----
   const float scale = 0.125f;  // 1/sqrt(64)
+  // the title's key mask as one 64-bit ballot (one coalesced load instead of 16 per lane)
+  const unsigned long long mbits = __ballot(lane < T && mask[row0 + (lane < T ? lane : 0)] != 0);
   float kadd[4][4];            // 0 (valid), -FLT_MAX (masked, HF finfo.min), -inf (tile padding)
 #pragma unroll
   for (int is = 0; is < 4; ++is)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int s = is * 16 + fq * 4 + r;
-      kadd[is][r] = (s < T) ? (mask[row0 + s] != 0 ? 0.f : -3.4028234663852886e38f) : -INFINITY;
+      kadd[is][r] = (s < T) ? (((mbits >> s) & 1ull) ? 0.f : -3.4028234663852886e38f) : -INFINITY;
     }
   bf16x8 pf[4][2];
 #pragma unroll
@@ -143,32 +146,242 @@ __global__ __launch_bounds__(256) void title_attn_kernel(const bf16* __restrict_
       bf16x4 lob = __builtin_bit_cast(bf16x4, lo), hib = __builtin_bit_cast(bf16x4, hi);
       bf16x8 vf = {lob[0], lob[1], lob[2], lob[3], hib[0], hib[1], hib[2], hib[3]};
 #pragma unroll
-      for (int jq = 0; jq < 4; ++jq) o[jq][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[jq][ks], vf, o[jq][jd], 0, 0, 0);
+      for (int jq = 0; jq < 4; ++jq) o[jq][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[jq][ks], o[jq][jd], 0, 0, 0);
     }
   }
   if (!active) return;
-  // ---- store: lane holds O[t = 16 jq + 4 fq + r][d = 16 jd + fr] ----
+  // ---- store: O^T accumulators (V as the A operand) -> lane holds O[t = 16 jq + fr][d = 16 jd
+  // + 4 fq + r], 4 consecutive d -> one 8-byte store per (jq, jd) ----
   bf16* ob = out + row0 * D + h * DH;
 #pragma unroll
-  for (int jq = 0; jq < 4; ++jq)
+  for (int jq = 0; jq < 4; ++jq) {
+    const int t = jq * 16 + fr;
+    if (t < T) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = jq * 16 + fq * 4 + r;
-      if (t < T) {
-#pragma unroll
-        for (int jd = 0; jd < 4; ++jd) ob[(size_t)t * D + jd * 16 + fr] = f2bf(o[jq][jd][r]);
+      for (int jd = 0; jd < 4; ++jd) {
+        const bf16x4 v = {f2bf(o[jq][jd][0]), f2bf(o[jq][jd][1]), f2bf(o[jq][jd][2]), f2bf(o[jq][jd][3])};
+        *(bf16x4*)(ob + (size_t)t * D + jd * 16 + fq * 4) = v;
       }
     }
+  }
 }
 
+// Persistent form: a fixed grid of waves walks the (title, head) pairs with stride; the next
+// pair's K/Q fragments, V rows and mask are loaded into registers while the current pair's
+// softmax and P.V run, so every wave keeps one pair's ~19 KB in flight at all times (the
+// one-shot kernel above spends ~2/3 of each wave's life waiting for its loads).
+struct TAIn {
+  bf16x8 kf[2][4], qf[2][4], vv[8];
+  int mbit;
+};
+
+// K/Q fragments + mask of `pair` (issued right after the S MFMAs have read the previous ones)
+__device__ __forceinline__ void ta_load_kq(TAIn& in, const bf16* __restrict__ qkv, const int* __restrict__ mask,
+                                           int pair, int T, int H, int D, int lane) {
+  const int title = pair / H, h = pair - title * H;
+  const int ld = 3 * D;
+  const bf16* qb = qkv + (size_t)title * T * ld + h * DH;
+  const bf16* kb = qb + D;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int kd = 0; kd < 2; ++kd)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int r = i * 16 + fr;
+      r = r < T ? r : T - 1;
+      in.kf[kd][i] = *(const bf16x8*)(kb + r * ld + kd * 32 + fq * 8);
+      in.qf[kd][i] = *(const bf16x8*)(qb + r * ld + kd * 32 + fq * 8);
+    }
+  in.mbit = mask[(size_t)title * T + (lane < T ? lane : 0)];
+}
+
+// V rows of `pair` (issued once the softmax no longer holds the score registers)
+__device__ __forceinline__ void ta_load_v(TAIn& in, const bf16* __restrict__ qkv, int pair, int T, int H, int D,
+                                          int lane) {
+  const int title = pair / H, h = pair - title * H;
+  const int ld = 3 * D;
+  const bf16* vb = qkv + (size_t)title * T * ld + 2 * D + h * DH;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int idx = c * 64 + lane;
+    int r = idx >> 3;
+    r = r < T ? r : T - 1;  // rows >= T are zeroed when written to LDS
+    in.vv[c] = *(const bf16x8*)(vb + r * ld + (idx & 7) * 8);
+  }
+}
+
+template <int OCC, int DEPTH>
+__global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __restrict__ qkv, const int* __restrict__ mask,
+                                                          bf16* __restrict__ out, int n_pairs, int T, int H, int D) {
+  __shared__ __attribute__((aligned(16))) bf16 vs[4][64 * DH];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int stride = gridDim.x * 4;
+  int pair = blockIdx.x * 4 + wave;
+  if (pair >= n_pairs) return;
+  bf16* myv = vs[wave];
+  const int fr = lane & 15, fq = lane >> 4;
+  const int qq = fr >> 2, pp = fr & 3;
+  // one pair: consumes `in`, then refills it with the pair DEPTH strides ahead
+  auto step = [&](TAIn& in, int pair) {
+    const int title = pair / H, h = pair - title * H;
+    const size_t row0 = (size_t)title * T;
+    // V -> LDS (the previous pair's transposed reads were consumed by its MFMAs)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int idx = c * 64 + lane;
+      const int r = idx >> 3;
+      *(bf16x8*)(myv + r * DH + (idx & 7) * 8) = r < T ? in.vv[c] : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    const unsigned long long mbits = __ballot(lane < T && in.mbit != 0);
+    f32x4 st[4][4];
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq) st[is][jq] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kd = 0; kd < 2; ++kd)
+#pragma unroll
+      for (int is = 0; is < 4; ++is)
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq)
+          st[is][jq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(in.kf[kd][is], in.qf[kd][jq], st[is][jq], 0, 0, 0);
+    // prefetch the next pair (its registers are free once the S MFMAs have read them)
+    const int next = pair + DEPTH * stride;
+    if (next < n_pairs) ta_load_kq(in, qkv, mask, next, T, H, D, lane);
+
+    const float scale = 0.125f;
+    bf16x8 pf[4][2];
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int is = 0; is < 4; ++is)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int sidx = is * 16 + fq * 4 + r;
+          const float a = (sidx < T) ? (((mbits >> sidx) & 1ull) ? 0.f : -3.4028234663852886e38f) : -INFINITY;
+          const float sc = (a == 0.f) ? st[is][jq][r] * scale : a;
+          st[is][jq][r] = sc;
+          m = fmaxf(m, sc);
+        }
+      m = group4_max(m);
+      float l = 0.f;
+#pragma unroll
+      for (int is = 0; is < 4; ++is)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(st[is][jq][r] - m);
+          st[is][jq][r] = e;
+          l += e;
+        }
+      const float inv = 1.0f / group4_sum(l);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f[r] = f2bf(st[2 * ks][jq][r] * inv);
+          f[4 + r] = f2bf(st[2 * ks + 1][jq][r] * inv);
+        }
+        pf[jq][ks] = f;
+      }
+    }
+    if (next < n_pairs) ta_load_v(in, qkv, next, T, H, D, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V image is in LDS
+    __builtin_amdgcn_wave_barrier();
+    f32x4 o[4][4];
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq)
+#pragma unroll
+      for (int jd = 0; jd < 4; ++jd) o[jq][jd] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int jd = 0; jd < 4; ++jd) {
+        const bf16* a0 = myv + (ks * 32 + fq * 4 + qq) * DH + jd * 16 + pp * 4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0 + 16 * DH));
+        bf16x4 lob = __builtin_bit_cast(bf16x4, lo), hib = __builtin_bit_cast(bf16x4, hi);
+        bf16x8 vf = {lob[0], lob[1], lob[2], lob[3], hib[0], hib[1], hib[2], hib[3]};
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) o[jq][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[jq][ks], o[jq][jd], 0, 0, 0);
+      }
+    bf16* ob = out + row0 * D + h * DH;
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) {
+      const int t = jq * 16 + fr;
+      if (t < T) {
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) {
+          const bf16x4 v = {f2bf(o[jq][jd][0]), f2bf(o[jq][jd][1]), f2bf(o[jq][jd][2]), f2bf(o[jq][jd][3])};
+          *(bf16x4*)(ob + (size_t)t * D + jd * 16 + fq * 4) = v;
+        }
+      }
+    }
+  };
+  TAIn in0, in1;
+  ta_load_kq(in0, qkv, mask, pair, T, H, D, lane);
+  ta_load_v(in0, qkv, pair, T, H, D, lane);
+  if (DEPTH == 2 && pair + stride < n_pairs) {
+    ta_load_kq(in1, qkv, mask, pair + stride, T, H, D, lane);
+    ta_load_v(in1, qkv, pair + stride, T, H, D, lane);
+  }
+  while (true) {
+    step(in0, pair);
+    pair += stride;
+    if (pair >= n_pairs) break;
+    // the next pair overwrites this wave's V image: its transposed reads must be done
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    if (DEPTH == 2) {
+      step(in1, pair);
+      pair += stride;
+      if (pair >= n_pairs) break;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+int g_ta_waves = -2;  // default: persistent, 2-deep prefetch, 1 wave per SIMD (kernel_bench.py)
+int g_ta_cus = 0;
+
 }  // namespace
+
+extern "C" void fr_title_attn_set_waves(int w) { g_ta_waves = w; }
 
 extern "C" int fr_title_attention_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
                                        hipStream_t s) {
   if (T < 1 || T > 64 || D != H * DH) return 1;
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
-  hipLaunchKernelGGL(title_attn_kernel, dim3((pairs + 3) / 4), dim3(256), 0, s, (const bf16*)qkv, mask, (bf16*)out,
-                     n_titles, T, H, D);
+  const int w = g_ta_waves;
+  if (w <= 0) {  // persistent, prefetching: w = 0 -> 2 waves/SIMD (spills a little), w = -1 -> 1 wave/SIMD
+    if (g_ta_cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_ta_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_ta_cus <= 0) g_ta_cus = 256;
+    }
+    int blocks = g_ta_cus * (w == 0 ? 2 : 1);
+    const int need = (pairs + 3) / 4;
+    blocks = blocks < need ? blocks : need;
+    if (w == -2)
+      hipLaunchKernelGGL((title_attn_pkernel<1, 2>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, mask, (bf16*)out, pairs,
+                         T, H, D);
+    else if (w == 0)
+      hipLaunchKernelGGL((title_attn_pkernel<2, 1>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, mask, (bf16*)out, pairs, T,
+                         H, D);
+    else
+      hipLaunchKernelGGL((title_attn_pkernel<1, 1>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, mask, (bf16*)out, pairs, T,
+                         H, D);
+  } else if (w == 1)
+    hipLaunchKernelGGL(title_attn_kernel<1>, dim3(pairs), dim3(64), 0, s, (const bf16*)qkv, mask, (bf16*)out, n_titles, T, H, D);
+  else if (w == 4)
+    hipLaunchKernelGGL(title_attn_kernel<4>, dim3((pairs + 3) / 4), dim3(256), 0, s, (const bf16*)qkv, mask, (bf16*)out,
+                       n_titles, T, H, D);
+  else
+    hipLaunchKernelGGL(title_attn_kernel<2>, dim3((pairs + 1) / 2), dim3(128), 0, s, (const bf16*)qkv, mask, (bf16*)out,
+                       n_titles, T, H, D);
   return 0;
 }

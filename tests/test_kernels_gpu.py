@@ -76,6 +76,28 @@ def test_title_attention(dev, T):
     assert rel_err(out, out_ref) < 2e-2
 
 
+@pytest.mark.parametrize("waves", [-2, -1, 0, 1, 2, 4])
+@pytest.mark.parametrize("n,T", [(700, 50), (3, 33)])
+def test_title_attention_launch_variants(dev, waves, n, T):
+    """Every launch form (persistent prefetching with 1 or 2 waves/SIMD; 1/2/4 waves per
+    block) on enough titles that each persistent wave walks several (title, head) pairs."""
+    H, D = 12, 768
+    g = torch.Generator().manual_seed(n + T)
+    qkv = torch.randn(n * T, 3 * D, generator=g).to(dev, torch.bfloat16)
+    lens = torch.randint(1, T + 1, (n,), generator=g)
+    mask = (torch.arange(T)[None, :] < lens[:, None]).to(torch.int32).to(dev)
+    mask[0] = 0
+    lib = native.lib()
+    lib.title_attn_set_waves(waves)
+    try:
+        out = lib.title_attention(qkv, mask, H)
+        assert torch.equal(lib.title_attention(qkv, mask, H), out)
+    finally:
+        lib.title_attn_set_waves(-2)
+    assert torch.isfinite(out.float()).all()
+    assert rel_err(out, ref.title_attention(qkv.float(), mask, H)) < 2e-2
+
+
 @pytest.mark.parametrize("dtype,D,Q", [(torch.bfloat16, 768, 384), (torch.float32, 400, 200)])
 def test_additive_pool(dev, dtype, D, Q):
     n, T = 23, 50
