@@ -70,14 +70,20 @@ def main():
     x = (torch.randn(M, D, generator=g)).to(dev, torch.bfloat16)
     w, b = torch.randn(D, device=dev), torch.randn(D, device=dev)
     if want("layer_norm"):
-        ms = timeit(lambda: lib.layer_norm(x, w, b, 1e-12))
-        rec("layer_norm", ms, 2 * M * D * 2)
+        for wide in (0, 1):
+            lib.ln_set_wide(wide)
+            ms = timeit(lambda: lib.layer_norm(x, w, b, 1e-12))
+            rec(f"layer_norm[wide={wide}]", ms, 2 * M * D * 2)
+        lib.ln_set_wide(1)
     if want("embed_ln"):
         word = (torch.randn(30522, D, generator=g) * 0.02).to(dev, torch.bfloat16)
         pos = (torch.randn(512, D, generator=g) * 0.02).to(dev, torch.bfloat16)
         tok = torch.randint(0, 30522, (n, T), generator=g, dtype=torch.int32).to(dev)
-        ms = timeit(lambda: lib.embed_ln(tok, word, pos, w, b, 1e-12))
-        rec("embed_ln", ms, 2 * M * D * 2)
+        for wide in (0, 1):
+            lib.ln_set_wide(wide)
+            ms = timeit(lambda: lib.embed_ln(tok, word, pos, w, b, 1e-12))
+            rec(f"embed_ln[wide={wide}]", ms, 2 * M * D * 2)
+        lib.ln_set_wide(1)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)

@@ -14,6 +14,7 @@
 extern "C" {
 void fr_gemm_set_variant(int v);
 void fr_title_attn_set_waves(int w);
+void fr_ln_set_wide(int v);
 int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K,
                     int act, hipStream_t s);
 int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db, int rows, int D,
@@ -406,12 +407,14 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
 
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
+void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 
 }  // namespace
 
 TORCH_LIBRARY(fedrec, m) {
   m.def("gemm_set_variant(int v) -> ()", &gemm_set_variant);
   m.def("title_attn_set_waves(int w) -> ()", &title_attn_set_waves);
+  m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("layer_norm_bwd(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor)");

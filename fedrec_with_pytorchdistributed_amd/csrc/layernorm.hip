@@ -81,6 +81,103 @@ __global__ __launch_bounds__(256) void ln_kernel(const bf16* __restrict__ x, con
   }
 }
 
+// Wide form for D % 256 == 0 (D = 768: 3 chunks): a half-wave (32 lanes) per row, each lane
+// owning NC 16-byte chunks (8 bf16) at [256c + 8l', +8) -- every load/store is dwordx4 and a
+// wave keeps RPW rows (RPW/2 per half) in flight before the first reduction.  Stats as
+// above (two-pass from registers), reductions over the 32 lanes of the half.
+template <bool EMBED, int NC, int RPH>
+__global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, const int* __restrict__ tokens,
+                                                   const bf16* __restrict__ word, const bf16* __restrict__ pos,
+                                                   const float* __restrict__ w, const float* __restrict__ b,
+                                                   bf16* __restrict__ y, int rows, int T, float eps) {
+  constexpr int D = 256 * NC;
+  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row0 = (wave * 2 + half) * RPH;
+  float v[RPH][NC][8];
+#pragma unroll
+  for (int q = 0; q < RPH; ++q) {
+    int row = row0 + q;
+    row = row < rows ? row : rows - 1;
+    const bf16* s0;
+    const bf16* s1 = nullptr;
+    if constexpr (EMBED) {
+      s0 = word + (size_t)tokens[row] * D;
+      s1 = pos + (size_t)(row % T) * D;
+    } else {
+      s0 = x + (size_t)row * D;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = c * 256 + hl * 8;
+      const bf16x8 a = *(const bf16x8*)(s0 + i);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[q][c][k] = (float)a[k];
+      if constexpr (EMBED) {
+        const bf16x8 p = *(const bf16x8*)(s1 + i);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[q][c][k] += (float)p[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < RPH; ++q) {
+    const int row = row0 + q;
+    float sm = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sm += v[q][c][k];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+    const float mean = sm * (1.0f / D);
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[q][c][k] - mean;
+        sq += d * d;
+      }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    const float rstd = rsqrtf(sq * (1.0f / D) + eps);
+    if (row < rows) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int i = c * 256 + hl * 8;
+        const float4 w0 = *(const float4*)(w + i), w1 = *(const float4*)(w + i + 4);
+        const float4 b0 = *(const float4*)(b + i), b1 = *(const float4*)(b + i + 4);
+        const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = f2bf((v[q][c][k] - mean) * rstd * ww[k] + bb[k]);
+        *(bf16x8*)(y + (size_t)row * D + i) = o;
+      }
+    }
+  }
+}
+
+template <bool EMBED>
+bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* pos, const float* w, const float* b,
+                 bf16* y, int rows, int D, int T, float eps, hipStream_t s) {
+  constexpr int RPH = 2;                // rows per half-wave -> 4 per wave, 16 per 256-thread block
+  constexpr int RPB = 8 * RPH;
+  const int blocks = (rows + RPB - 1) / RPB;
+  if (D == 768)
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 3, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+  else if (D == 512)
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 2, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+  else if (D == 1024)
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 4, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+  else if (D == 256)
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 1, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+  else
+    return false;
+  return true;
+}
+
 // LayerNorm backward (unfrozen backbone): y = (x - mu) * rstd * w + b
 //   dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 //   dw = sum_rows dy * xhat, db = sum_rows dy   (per-lane partials over a grid-stride of
@@ -210,7 +307,11 @@ __global__ __launch_bounds__(256) void gelu_kernel(const bf16* __restrict__ z, c
   }
 }
 
+int g_ln_wide = 1;
+
 }  // namespace
+
+extern "C" void fr_ln_set_wide(int v) { g_ln_wide = v; }
 
 extern "C" int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db,
                                       int rows, int D, float eps, hipStream_t s) {
@@ -238,6 +339,8 @@ extern "C" int fr_layer_norm_bf16(const void* x, const float* w, const float* b,
                                   hipStream_t s) {
   if (D % 4 != 0 || D > 256 * MAXC) return 1;
   if (rows == 0) return 0;
+  if (g_ln_wide && launch_ln16<false>((const bf16*)x, nullptr, nullptr, nullptr, w, b, (bf16*)y, rows, D, 1, eps, s))
+    return 0;
   hipLaunchKernelGGL((ln_kernel<false>), dim3((rows + 3) / 4), dim3(256), 0, s, (const bf16*)x, nullptr, nullptr,
                      nullptr, w, b, (bf16*)y, rows, D, 1, eps);
   return 0;
@@ -247,6 +350,8 @@ extern "C" int fr_embed_ln_bf16(const int* tokens, const void* word, const void*
                                 void* y, int rows, int D, int T, float eps, hipStream_t s) {
   if (D % 4 != 0 || D > 256 * MAXC) return 1;
   if (rows == 0) return 0;
+  if (g_ln_wide && launch_ln16<true>(nullptr, tokens, (const bf16*)word, (const bf16*)pos, w, b, (bf16*)y, rows, D, T, eps, s))
+    return 0;
   hipLaunchKernelGGL((ln_kernel<true>), dim3((rows + 3) / 4), dim3(256), 0, s, nullptr, tokens, (const bf16*)word,
                      (const bf16*)pos, w, b, (bf16*)y, rows, D, T, eps);
   return 0;

@@ -52,6 +52,26 @@ def test_layer_norm(dev):
     assert rel_err(y, ref.layer_norm(x.float(), w, b, 1e-12)) < 1e-2
 
 
+@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("rows,D", [(1, 768), (333, 768), (77, 512), (5000, 768)])
+def test_layer_norm_forms(dev, wide, rows, D):
+    x = torch.randn(rows, D, device=dev).to(torch.bfloat16) * 3 + 1
+    w, b = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    lib = native.lib()
+    lib.ln_set_wide(wide)
+    try:
+        y = lib.layer_norm(x, w, b, 1e-12)
+        word = (torch.randn(1000, D, device=dev) * 0.5).to(torch.bfloat16)
+        pos = (torch.randn(64, D, device=dev) * 0.5).to(torch.bfloat16)
+        tok = torch.randint(0, 1000, (rows,), device=dev, dtype=torch.int32)
+        e = lib.embed_ln(tok.view(rows, 1), word, pos, w, b, 1e-12)
+    finally:
+        lib.ln_set_wide(1)
+    assert rel_err(y, ref.layer_norm(x.float(), w, b, 1e-12)) < 1e-2
+    e_ref = ref.embed_ln(tok.view(rows, 1).long(), word.float(), pos.float(), w, b, 1e-12)
+    assert rel_err(e, e_ref) < 1e-2
+
+
 def test_embed_ln(dev):
     n, T, D = 37, 50, 768
     word = (torch.randn(30522, D, device=dev) * 0.02).to(torch.bfloat16)
