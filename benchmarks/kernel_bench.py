@@ -84,6 +84,25 @@ def main():
             ms = timeit(lambda: lib.embed_ln(tok, word, pos, w, b, 1e-12))
             rec(f"embed_ln[wide={wide}]", ms, 2 * M * D * 2)
         lib.ln_set_wide(1)
+    if want("additive_pool"):
+        from fedrec_with_pytorchdistributed_amd import ops
+        xh = x.view(n, T, D)
+        e = torch.tanh(torch.randn(n, T, 384, generator=g)).to(dev, torch.bfloat16)
+        w2 = torch.randn(384, device=dev) * 0.1
+        b2 = torch.randn(1, device=dev)
+        ms = timeit(lambda: ops.additive_pool_fwd(xh, e, w2, b2))
+        rec("additive_pool_fwd", ms, x.numel() * 2 + e.numel() * 2)
+        _, alpha = ops.additive_pool_fwd(xh, e, w2, b2)
+        gg = torch.randn(n, D, device=dev)
+        ms = timeit(lambda: ops.additive_pool_bwd(xh, e, alpha, w2, gg, False))
+        rec("additive_pool_bwd", ms, x.numel() * 2 + e.numel() * 4)
+    if want("wgrad"):
+        from fedrec_with_pytorchdistributed_amd.ops.functional import wgrad
+        dy = torch.randn(M, 384, generator=g).to(dev, torch.bfloat16)
+        ms = timeit(lambda: wgrad(dy, x))
+        rec("wgrad_splitk", ms, dy.numel() * 2 + x.numel() * 2, 2.0 * M * 384 * D)
+        ms = timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32))
+        rec("wgrad_mm", ms, dy.numel() * 2 + x.numel() * 2, 2.0 * M * 384 * D)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)

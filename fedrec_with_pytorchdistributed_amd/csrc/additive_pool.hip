@@ -69,11 +69,13 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
                                                        const float* __restrict__ alpha, const float* __restrict__ w2,
                                                        const float* __restrict__ g, float* __restrict__ dx,
                                                        TX* __restrict__ dpre, float* __restrict__ dw2,
-                                                       float* __restrict__ db2, int T, int D, int Q) {
+                                                       float* __restrict__ db2, int T, int D, int Q, int R) {
   __shared__ float da_s[MAXT];
   __shared__ float al_s[MAXT];
   __shared__ float red[4];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  dw2 += (size_t)(n % R) * Q;  // R accumulator replicas: 1/R of the atomic contention
+  db2 += n % R;
   const TX* xe = x + (size_t)n * T * D;
   const TX* ee = e + (size_t)n * T * Q;
   const float* gn = g + (size_t)n * D;
@@ -121,13 +123,181 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Text-head (bf16) forms with 16-byte accesses: every x / e / dpre access is one bf16x8 per
+// lane.  Requires D % 8 == 0, Q % 8 == 0, D/8 <= 128, Q/8 <= 256.
+__device__ __forceinline__ void unpack8(const bf16x8 v, float (&f)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = (float)v[k];
+}
+
+__global__ __launch_bounds__(256) void pool_fwd16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ e,
+                                                         const float* __restrict__ w2, const float* __restrict__ b2,
+                                                         float* __restrict__ out, float* __restrict__ alpha_out, int T,
+                                                         int D, int Q) {
+  __shared__ float a_s[MAXT];
+  __shared__ float part[2][1024];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16* xe = x + (size_t)n * T * D;
+  const bf16* ee = e + (size_t)n * T * Q;
+  const int QC = Q >> 3, DC = D >> 3;
+  // a_t = w2 . e_t + b2: one wave per t, lanes over 8-wide q chunks (w2 chunk kept in registers)
+  float wq[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int qc = lane + 64 * c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wq[c][k] = qc < QC ? w2[qc * 8 + k] : 0.f;
+  }
+  for (int t = wave; t < T; t += 4) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int qc = lane + 64 * c;
+      if (qc < QC) {
+        float f[8];
+        unpack8(*(const bf16x8*)(ee + (size_t)t * Q + qc * 8), f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sacc += f[k] * wq[c][k];
+      }
+    }
+    sacc = wave_sum(sacc);
+    if (lane == 0) a_s[t] = sacc + b2[0];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float m = -INFINITY;
+    for (int t = lane; t < T; t += 64) m = fmaxf(m, a_s[t]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int t = lane; t < T; t += 64) {
+      const float p = __expf(a_s[t] - m);
+      a_s[t] = p;
+      l += p;
+    }
+    const float inv = 1.0f / (wave_sum(l) + 1e-8f * __expf(-m));
+    for (int t = lane; t < T; t += 64) {
+      const float al = a_s[t] * inv;
+      a_s[t] = al;
+      alpha_out[(size_t)n * T + t] = al;
+    }
+  }
+  __syncthreads();
+  // out = sum_t alpha_t x_t: thread (t-group tg of 2, chunk dc) accumulates 8 columns
+  const int dc = tid % DC, tg = tid / DC;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (tg < 2) {
+    for (int t = tg; t < T; t += 2) {
+      float f[8];
+      unpack8(*(const bf16x8*)(xe + (size_t)t * D + dc * 8), f);
+      const float al = a_s[t];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += al * f[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[tg][dc * 8 + k] = acc[k];
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += 256) out[(size_t)n * D + d] = part[0][d] + part[1][d];
+}
+
+__global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ e,
+                                                         const float* __restrict__ alpha, const float* __restrict__ w2,
+                                                         const float* __restrict__ g, bf16* __restrict__ dpre,
+                                                         float* __restrict__ dw2, float* __restrict__ db2, int T, int D,
+                                                         int Q, int R) {
+  __shared__ float da_s[MAXT];
+  __shared__ float al_s[MAXT];
+  __shared__ float part[8][256 * 8 / 4];  // per t-group dw2 partials (Q <= 512 for TG >= 4)
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  dw2 += (size_t)(n % R) * Q;  // R accumulator replicas: 1/R of the atomic contention
+  db2 += n % R;
+  const bf16* xe = x + (size_t)n * T * D;
+  const bf16* ee = e + (size_t)n * T * Q;
+  const float* gn = g + (size_t)n * D;
+  const int QC = Q >> 3, DC = D >> 3;
+  for (int t = tid; t < T; t += 256) al_s[t] = alpha[(size_t)n * T + t];
+  // dalpha_t = x_t . g (g chunks in registers)
+  float gv[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int dcc = lane + 64 * c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[c][k] = dcc < DC ? gn[dcc * 8 + k] : 0.f;
+  }
+  for (int t = wave; t < T; t += 4) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int dcc = lane + 64 * c;
+      if (dcc < DC) {
+        float f[8];
+        unpack8(*(const bf16x8*)(xe + (size_t)t * D + dcc * 8), f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sacc += f[k] * gv[c][k];
+      }
+    }
+    sacc = wave_sum(sacc);
+    if (lane == 0) da_s[t] = sacc;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float sacc = 0.f;
+    for (int t = lane; t < T; t += 64) sacc += al_s[t] * da_s[t];
+    sacc = wave_sum(sacc);
+    float sd = 0.f;
+    for (int t = lane; t < T; t += 64) {
+      const float v = al_s[t] * (da_s[t] - sacc);
+      da_s[t] = v;
+      sd += v;
+    }
+    sd = wave_sum(sd);
+    if (lane == 0) atomicAdd(db2, sd);
+  }
+  __syncthreads();
+  // dpre_t = da_t w2 (1 - e_t^2) (bf16x8 stores); dw2 += sum_t da_t e_t
+  const int TG = 256 / QC;
+  const int qc = tid % QC, tg = tid / QC;
+  if (tg < TG) {
+    float wv[8], acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      wv[k] = w2[qc * 8 + k];
+      acc[k] = 0.f;
+    }
+    for (int t = tg; t < T; t += TG) {
+      float f[8];
+      unpack8(*(const bf16x8*)(ee + (size_t)t * Q + qc * 8), f);
+      const float da = da_s[t];
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc[k] += da * f[k];
+        o[k] = f2bf(da * wv[k] * (1.0f - f[k] * f[k]));
+      }
+      *(bf16x8*)(dpre + ((size_t)n * T + t) * Q + qc * 8) = o;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[tg][qc * 8 + k] = acc[k];
+  }
+  __syncthreads();
+  for (int q = tid; q < Q; q += 256) {
+    float sacc = 0.f;
+    for (int j = 0; j < TG; ++j) sacc += part[j][q];
+    atomicAdd(dw2 + q, sacc);
+  }
+}
+
 }  // namespace
 
 extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const float* b2, float* out,
                                     float* alpha, int n, int T, int D, int Q, int is_bf16, hipStream_t s) {
   if (T > MAXT) return 1;
   if (n == 0) return 0;
-  if (is_bf16)
+  if (is_bf16 && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256)
+    hipLaunchKernelGGL(pool_fwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, w2, b2, out, alpha,
+                       T, D, Q);
+  else if (is_bf16)
     hipLaunchKernelGGL(pool_fwd_kernel<bf16>, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, w2, b2, out,
                        alpha, T, D, Q);
   else
@@ -136,16 +306,20 @@ extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w
   return 0;
 }
 
+// dw2 / db2 point at R zeroed replicas ([R, Q] / [R]); the caller sums them.
 extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g,
-                                    float* dx, void* dpre, float* dw2, float* db2, int n, int T, int D, int Q,
+                                    float* dx, void* dpre, float* dw2, float* db2, int n, int T, int D, int Q, int R,
                                     int is_bf16, hipStream_t s) {
   if (T > MAXT) return 1;
   if (n == 0) return 0;
-  if (is_bf16)
+  if (is_bf16 && dx == nullptr && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256)
+    hipLaunchKernelGGL(pool_bwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, alpha, w2, g,
+                       (bf16*)dpre, dw2, db2, T, D, Q, R);
+  else if (is_bf16)
     hipLaunchKernelGGL(pool_bwd_kernel<bf16>, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, alpha, w2, g,
-                       dx, (bf16*)dpre, dw2, db2, T, D, Q);
+                       dx, (bf16*)dpre, dw2, db2, T, D, Q, R);
   else
     hipLaunchKernelGGL(pool_bwd_kernel<float>, dim3(n), dim3(256), 0, s, (const float*)x, (const float*)e, alpha, w2,
-                       g, dx, (float*)dpre, dw2, db2, T, D, Q);
+                       g, dx, (float*)dpre, dw2, db2, T, D, Q, R);
   return 0;
 }

@@ -9,6 +9,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <tuple>
 
 extern "C" {
@@ -31,7 +32,8 @@ int fr_title_attention_bf16(const void* qkv, const int* mask, void* out, int n_t
 int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const float* b2, float* out, float* alpha,
                          int n, int T, int D, int Q, int is_bf16, hipStream_t s);
 int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g, float* dx,
-                         void* dpre, float* dw2, float* db2, int n, int T, int D, int Q, int is_bf16, hipStream_t s);
+                         void* dpre, float* dw2, float* db2, int n, int T, int D, int Q, int R, int is_bf16,
+                         hipStream_t s);
 int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, hipStream_t s);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
                      int dk, hipStream_t s);
@@ -218,13 +220,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(con
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor dx = want_dx ? at::empty({n, T, D}, fopt) : at::empty({0}, fopt);
   auto dpre = at::empty({n, T, Q}, e.options());
-  auto dw2 = at::zeros({Q}, fopt);
-  auto db2 = at::zeros({1}, fopt);
+  const int64_t R = std::max<int64_t>(1, std::min<int64_t>(n, 64));  // atomic replicas
+  auto dw2r = at::zeros({R, Q}, fopt);
+  auto db2r = at::zeros({R}, fopt);
+  float* db2p = db2r.data_ptr<float>();
   check_rc(fr_additive_pool_bwd(x.data_ptr(), e.data_ptr(), alpha.data_ptr<float>(), w2.data_ptr<float>(),
                                 g.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr, dpre.data_ptr(),
-                                dw2.data_ptr<float>(), db2.data_ptr<float>(), (int)n, (int)T, (int)D, (int)Q, bf,
-                                cur_stream()),
+                                dw2r.data_ptr<float>(), db2p, (int)n, (int)T, (int)D, (int)Q, (int)R,
+                                bf, cur_stream()),
            "additive_pool_bwd");
+  auto dw2 = dw2r.sum(0);
+  auto db2 = db2r.sum().view({1});
   return {dx, dpre, dw2, db2};
 }
 

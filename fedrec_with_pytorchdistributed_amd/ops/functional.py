@@ -14,6 +14,32 @@ from .. import ops
 from .reference import _f
 
 
+def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
+    """``dy^T x`` in fp32 for ``dy [M, N]``, ``x [M, K]`` with a long reduction dim M.
+
+    On the device with bf16 operands this is a split-K batched MFMA GEMM: M is cut into
+    ``splits`` row chunks (free views, no copies), one fp32-output GEMM per chunk in a
+    single bmm launch, then an fp32 sum of the partials.  The library picks a handful of
+    output tiles for the un-split product ([384, 768] from 78850 rows: 18 tiles, 155 TF)."""
+    if not (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
+        return _f(dy).t() @ _f(x)
+    M = dy.shape[0]
+    S = max(1, min(splits, M // 2048))
+    if S == 1:
+        return torch.mm(dy.t(), x, out_dtype=torch.float32)
+    c = M // S
+    M0 = S * c
+    out = torch.bmm(dy[:M0].view(S, c, -1).transpose(1, 2), x[:M0].view(S, c, -1), out_dtype=torch.float32).sum(0)
+    if M0 < M:
+        out += torch.mm(dy[M0:].t(), x[M0:], out_dtype=torch.float32)
+    return out
+
+
+def bgrad(dy: torch.Tensor) -> torch.Tensor:
+    """Column sum in fp32 without materialising an fp32 copy of ``dy``."""
+    return dy.sum(0, dtype=torch.float64 if dy.dtype == torch.float64 else torch.float32)
+
+
 class AdditivePoolFn(torch.autograd.Function):
     """``AdditiveAttention`` (``attention.py:8-26``): ``x [n,T,D] -> [n,D]``.
 
@@ -43,13 +69,9 @@ class AdditivePoolFn(torch.autograd.Function):
         x2 = x.reshape(n * T, D)
         dw1 = db1 = None
         if ctx.needs_input_grad[1]:
-            if x2.is_cuda and x2.dtype == torch.bfloat16:
-                # weight gradient reduced over all n*T tokens: bf16 MFMA GEMM, fp32 output
-                dw1 = torch.mm(dpre2.t(), x2, out_dtype=torch.float32)
-            else:
-                dw1 = _f(dpre2).t() @ _f(x2)
+            dw1 = wgrad(dpre2, x2)  # reduced over all n*T tokens (split-K on the device)
         if ctx.needs_input_grad[2]:
-            db1 = _f(dpre2).sum(0)
+            db1 = bgrad(dpre2)
         dx = None
         if want_dx:
             if x2.is_cuda and x2.dtype == torch.bfloat16:
@@ -151,8 +173,8 @@ class LinearTFn(torch.autograd.Function):
         x, wlow = ctx.saved_tensors
         dy = dy.contiguous()
         dx = torch.mm(dy, wlow) if ctx.needs_input_grad[0] else None
-        dw = torch.mm(dy.t(), x, out_dtype=torch.float32) if dy.is_cuda else _f(dy).t() @ _f(x)
-        db = _f(dy).sum(0)
+        dw = wgrad(dy, x)
+        db = bgrad(dy)
         return dx, dw, db, (dy if ctx.has_res else None), None
 
 

@@ -118,7 +118,8 @@ def test_title_attention_launch_variants(dev, waves, n, T):
     assert rel_err(out, ref.title_attention(qkv.float(), mask, H)) < 2e-2
 
 
-@pytest.mark.parametrize("dtype,D,Q", [(torch.bfloat16, 768, 384), (torch.float32, 400, 200)])
+@pytest.mark.parametrize("dtype,D,Q", [(torch.bfloat16, 768, 384), (torch.float32, 400, 200), (torch.bfloat16, 64, 32),
+                                       (torch.bfloat16, 512, 256)])
 def test_additive_pool(dev, dtype, D, Q):
     n, T = 23, 50
     x = torch.randn(n, T, D, device=dev).to(dtype)
@@ -137,6 +138,11 @@ def test_additive_pool(dev, dtype, D, Q):
     assert rel_err(dpre, rdpre) < 2 * tol
     assert rel_err(dw2, rdw2) < 2 * tol
     assert abs(float(db2) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
+    # frozen-backbone form (no dx): the vectorised text-head kernel for bf16
+    _, dpre_n, dw2_n, db2_n = ops.additive_pool_bwd(x, e, alpha, w2, g, False)
+    assert rel_err(dpre_n, rdpre) < 2 * tol
+    assert rel_err(dw2_n, rdw2) < 2 * tol
+    assert abs(float(db2_n) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
 
 
 def test_user_attention(dev):
@@ -208,6 +214,15 @@ def test_segment_sum_skewed_pad_row(dev):
     assert rel_err(out, ref.segment_sum_rows(rows, inv, uniq.numel())) < 1e-6
     out_c = ops.segment_sum_rows(rows, inv, uniq.numel(), clip=1.5, seg=(perm, ptr))
     assert rel_err(out_c, ref.segment_sum_rows(rows, inv, uniq.numel(), clip=1.5)) < 1e-5
+
+
+def test_wgrad_split_k(dev):
+    from fedrec_with_pytorchdistributed_amd.ops.functional import bgrad, wgrad
+    for M in (78850, 5000, 999):
+        dy = torch.randn(M, 384, device=dev).to(torch.bfloat16)
+        x = torch.randn(M, 768, device=dev).to(torch.bfloat16)
+        assert rel_err(wgrad(dy, x), dy.float().t() @ x.float()) < 1e-5
+        assert rel_err(bgrad(dy), dy.float().sum(0)) < 1e-5
 
 
 def test_adam_flat(dev):
