@@ -204,14 +204,15 @@ __global__ __launch_bounds__(256) void pool_fwd16_kernel(const bf16* __restrict_
 __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ e,
                                                          const float* __restrict__ alpha, const float* __restrict__ w2,
                                                          const float* __restrict__ g, bf16* __restrict__ dpre,
-                                                         float* __restrict__ dw2, float* __restrict__ db2, int T, int D,
-                                                         int Q, int R) {
+                                                         float* __restrict__ dw2, float* __restrict__ db2,
+                                                         float* __restrict__ dsum, int T, int D, int Q, int R) {
   __shared__ float da_s[MAXT];
   __shared__ float al_s[MAXT];
   __shared__ float part[8][256 * 8 / 4];  // per t-group dw2 partials (Q <= 512 for TG >= 4)
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   dw2 += (size_t)(n % R) * Q;  // R accumulator replicas: 1/R of the atomic contention
   db2 += n % R;
+  dsum += (size_t)(n % R) * Q;  // column sums of dpre (= the att_fc1 bias gradient)
   const bf16* xe = x + (size_t)n * T * D;
   const bf16* ee = e + (size_t)n * T * Q;
   const float* gn = g + (size_t)n * D;
@@ -258,12 +259,14 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
   // dpre_t = da_t w2 (1 - e_t^2) (bf16x8 stores); dw2 += sum_t da_t e_t
   const int TG = 256 / QC;
   const int qc = tid % QC, tg = tid / QC;
+  float bs[8];
   if (tg < TG) {
     float wv[8], acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       wv[k] = w2[qc * 8 + k];
       acc[k] = 0.f;
+      bs[k] = 0.f;
     }
     for (int t = tg; t < T; t += TG) {
       float f[8];
@@ -274,6 +277,7 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
       for (int k = 0; k < 8; ++k) {
         acc[k] += da * f[k];
         o[k] = f2bf(da * wv[k] * (1.0f - f[k] * f[k]));
+        bs[k] += (float)o[k];  // the rounded value the dW1 GEMM consumes
       }
       *(bf16x8*)(dpre + ((size_t)n * T + t) * Q + qc * 8) = o;
     }
@@ -285,6 +289,17 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
     float sacc = 0.f;
     for (int j = 0; j < TG; ++j) sacc += part[j][q];
     atomicAdd(dw2 + q, sacc);
+  }
+  __syncthreads();
+  if (tg < TG) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[tg][qc * 8 + k] = bs[k];
+  }
+  __syncthreads();
+  for (int q = tid; q < Q; q += 256) {
+    float sacc = 0.f;
+    for (int j = 0; j < TG; ++j) sacc += part[j][q];
+    atomicAdd(dsum + q, sacc);
   }
 }
 
@@ -307,19 +322,24 @@ extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w
 }
 
 // dw2 / db2 point at R zeroed replicas ([R, Q] / [R]); the caller sums them.
+// dsum ([R, Q] zeroed): column sums of dpre, produced only by the vectorised text-head kernel.
+// Returns 0 when dsum was produced, -1 when the generic kernel ran (caller reduces dpre),
+// > 0 on argument errors.
 extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g,
-                                    float* dx, void* dpre, float* dw2, float* db2, int n, int T, int D, int Q, int R,
-                                    int is_bf16, hipStream_t s) {
+                                    float* dx, void* dpre, float* dw2, float* db2, float* dsum, int n, int T, int D,
+                                    int Q, int R, int is_bf16, hipStream_t s) {
   if (T > MAXT) return 1;
-  if (n == 0) return 0;
-  if (is_bf16 && dx == nullptr && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256)
+  if (n == 0) return -1;
+  if (is_bf16 && dx == nullptr && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256) {
     hipLaunchKernelGGL(pool_bwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, alpha, w2, g,
-                       (bf16*)dpre, dw2, db2, T, D, Q, R);
-  else if (is_bf16)
+                       (bf16*)dpre, dw2, db2, dsum, T, D, Q, R);
+    return 0;
+  }
+  if (is_bf16)
     hipLaunchKernelGGL(pool_bwd_kernel<bf16>, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, alpha, w2, g,
                        dx, (bf16*)dpre, dw2, db2, T, D, Q, R);
   else
     hipLaunchKernelGGL(pool_bwd_kernel<float>, dim3(n), dim3(256), 0, s, (const float*)x, (const float*)e, alpha, w2,
                        g, dx, (float*)dpre, dw2, db2, T, D, Q, R);
-  return 0;
+  return -1;
 }

@@ -32,8 +32,8 @@ int fr_title_attention_bf16(const void* qkv, const int* mask, void* out, int n_t
 int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const float* b2, float* out, float* alpha,
                          int n, int T, int D, int Q, int is_bf16, hipStream_t s);
 int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g, float* dx,
-                         void* dpre, float* dw2, float* db2, int n, int T, int D, int Q, int R, int is_bf16,
-                         hipStream_t s);
+                         void* dpre, float* dw2, float* db2, float* dsum, int n, int T, int D, int Q, int R,
+                         int is_bf16, hipStream_t s);
 int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, hipStream_t s);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
                      int dk, hipStream_t s);
@@ -206,10 +206,9 @@ std::tuple<at::Tensor, at::Tensor> additive_pool_fwd(const at::Tensor& x, const 
   return {out, alpha};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(const at::Tensor& x, const at::Tensor& e,
-                                                                             const at::Tensor& alpha,
-                                                                             const at::Tensor& w2, const at::Tensor& g,
-                                                                             bool want_dx) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(
+    const at::Tensor& x, const at::Tensor& e, const at::Tensor& alpha, const at::Tensor& w2, const at::Tensor& g,
+    bool want_dx) {
   check_dev(x, "x");
   check_dev(e, "e");
   check_dev(alpha, "alpha");
@@ -221,17 +220,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(con
   at::Tensor dx = want_dx ? at::empty({n, T, D}, fopt) : at::empty({0}, fopt);
   auto dpre = at::empty({n, T, Q}, e.options());
   const int64_t R = std::max<int64_t>(1, std::min<int64_t>(n, 64));  // atomic replicas
-  auto dw2r = at::zeros({R, Q}, fopt);
-  auto db2r = at::zeros({R}, fopt);
-  float* db2p = db2r.data_ptr<float>();
-  check_rc(fr_additive_pool_bwd(x.data_ptr(), e.data_ptr(), alpha.data_ptr<float>(), w2.data_ptr<float>(),
-                                g.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr, dpre.data_ptr(),
-                                dw2r.data_ptr<float>(), db2p, (int)n, (int)T, (int)D, (int)Q, (int)R,
-                                bf, cur_stream()),
-           "additive_pool_bwd");
-  auto dw2 = dw2r.sum(0);
-  auto db2 = db2r.sum().view({1});
-  return {dx, dpre, dw2, db2};
+  auto red = at::zeros({2 * R * Q + R}, fopt);  // [dw2 replicas | dpre col-sum replicas | db2 replicas]
+  float* dw2p = red.data_ptr<float>();
+  float* dsump = dw2p + R * Q;
+  float* db2p = dsump + R * Q;
+  const int rc = fr_additive_pool_bwd(x.data_ptr(), e.data_ptr(), alpha.data_ptr<float>(), w2.data_ptr<float>(),
+                                      g.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr, dpre.data_ptr(),
+                                      dw2p, db2p, dsump, (int)n, (int)T, (int)D, (int)Q, (int)R, bf, cur_stream());
+  TORCH_CHECK(rc <= 0, "fedrec::additive_pool_bwd: kernel launch rejected the arguments (code ", rc, ")");
+  auto parts = red.narrow(0, 0, 2 * R * Q).view({2, R, Q}).sum(1);
+  auto dw2 = parts.select(0, 0);
+  auto dsum = rc == 0 ? parts.select(0, 1) : at::empty({0}, fopt);
+  auto db2 = red.narrow(0, 2 * R * Q, R).sum().view({1});
+  return {dx, dpre, dw2, db2, dsum};
 }
 
 std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int64_t heads, int64_t head_dim) {
@@ -429,7 +430,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("title_attention(Tensor qkv, Tensor mask, int n_heads) -> Tensor");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2) -> (Tensor, Tensor)");
-  m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim) -> (Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act) -> (Tensor, Tensor, Tensor, Tensor)");

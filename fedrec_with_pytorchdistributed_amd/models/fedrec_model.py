@@ -61,6 +61,29 @@ class FlatParams:
             if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
                 p.grad = self.grad[off:off + p.numel()].view_as(p)
 
+    def begin_backward(self) -> None:
+        """Detach ``.grad`` so autograd hands over fresh gradient tensors instead of
+        accumulating into the flat views one add kernel per parameter."""
+        for p in self.params:
+            p.grad = None
+
+    def end_backward(self) -> None:
+        """Gather the fresh gradients into the flat buffer (one multi-tensor copy launch;
+        parameters that got no gradient are zeroed) and re-point ``.grad`` at it."""
+        dst, src, missing = [], [], []
+        for p, off in zip(self.params, self.offsets):
+            view = self.grad[off:off + p.numel()].view_as(p)
+            if p.grad is None:
+                missing.append(view)
+            elif p.grad.data_ptr() != view.data_ptr():
+                dst.append(view)
+                src.append(p.grad)
+            p.grad = view
+        if dst:
+            torch._foreach_copy_(dst, src)
+        if missing:
+            torch._foreach_zero_(missing)
+
     def state(self) -> Dict[str, torch.Tensor]:
         return {"m": self.m.detach().cpu(), "v": self.v.detach().cpu(), "step": torch.tensor(self.step)}
 

@@ -76,16 +76,20 @@ def additive_pool_fwd(x, e, w2, b2) -> Tuple[torch.Tensor, torch.Tensor]:
     return ref.additive_pool_fwd(x, e, w2, b2)
 
 
-def additive_pool_bwd(x, e, alpha, w2, g, want_dx: bool):
-    """-> ``(dx_direct|None, dpre, dw2, db2)`` with ``dpre = da w2 (1 - e^2)`` (tanh folded)."""
+def additive_pool_bwd(x, e, alpha, w2, g, want_dx: bool, want_colsum: bool = False):
+    """-> ``(dx_direct|None, dpre, dw2, db2)`` with ``dpre = da w2 (1 - e^2)`` (tanh folded);
+    ``want_colsum`` appends ``dpre`` summed over all tokens (the first linear's bias
+    gradient) when the kernel produced it for free, else None."""
     if _dev(x):
-        dx, dpre, dw2, db2 = native.require_for(x).additive_pool_bwd(
+        dx, dpre, dw2, db2, dsum = native.require_for(x).additive_pool_bwd(
             x.contiguous(), e.contiguous(), alpha.contiguous(), w2.reshape(-1).float().contiguous(),
             g.float().contiguous(), bool(want_dx))
-        return (dx if want_dx else None), dpre, dw2, db2
+        out = (dx if want_dx else None), dpre, dw2, db2
+        return out + ((dsum if dsum.numel() else None),) if want_colsum else out
     dx, de, dw2, db2 = ref.additive_pool_bwd(x, e, alpha, w2, g)
     dpre = de * (1.0 - e.float() ** 2)
-    return (dx if want_dx else None), dpre, dw2, db2
+    out = (dx if want_dx else None), dpre, dw2, db2
+    return out + (None,) if want_colsum else out
 
 
 def user_attention_fwd(qkv, heads: int, head_dim: int):

@@ -63,7 +63,7 @@ class AdditivePoolFn(torch.autograd.Function):
     def backward(ctx, g):
         x, e, alpha, w1, w2 = ctx.saved_tensors
         want_dx = ctx.needs_input_grad[0]
-        dx_dir, dpre, dw2, db2 = ops.additive_pool_bwd(x, e, alpha, w2, g, want_dx)
+        dx_dir, dpre, dw2, db2, dsum = ops.additive_pool_bwd(x, e, alpha, w2, g, want_dx, want_colsum=True)
         n, T, D = x.shape
         dpre2 = dpre.reshape(n * T, -1)
         x2 = x.reshape(n * T, D)
@@ -71,7 +71,7 @@ class AdditivePoolFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw1 = wgrad(dpre2, x2)  # reduced over all n*T tokens (split-K on the device)
         if ctx.needs_input_grad[2]:
-            db1 = bgrad(dpre2)
+            db1 = dsum if dsum is not None else bgrad(dpre2)
         dx = None
         if want_dx:
             if x2.is_cuda and x2.dtype == torch.bfloat16:

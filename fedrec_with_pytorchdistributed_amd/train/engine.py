@@ -122,13 +122,14 @@ class LocalEngine:
     def forward_backward(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
         """Loss of one batch with every trainable gradient left in ``flat.grad``."""
         self.model.train()
-        self.flat.zero_grad()
+        self.flat.begin_backward()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True)
         with obs.range("user_fwd"):
             u = self.model.user_encoder(his_v)
             loss, _ = OF.score_ce(cand_v, u, self.score_act)
         with obs.range("backward"):
             loss.backward()
+        self.flat.end_backward()
         return loss.detach()
 
     def train_step(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:

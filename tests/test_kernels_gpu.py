@@ -139,8 +139,10 @@ def test_additive_pool(dev, dtype, D, Q):
     assert rel_err(dw2, rdw2) < 2 * tol
     assert abs(float(db2) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
     # frozen-backbone form (no dx): the vectorised text-head kernel for bf16
-    _, dpre_n, dw2_n, db2_n = ops.additive_pool_bwd(x, e, alpha, w2, g, False)
+    _, dpre_n, dw2_n, db2_n, dsum = ops.additive_pool_bwd(x, e, alpha, w2, g, False, want_colsum=True)
     assert rel_err(dpre_n, rdpre) < 2 * tol
+    if dsum is not None:  # fused column sum == sum of the (rounded) dpre it wrote
+        assert rel_err(dsum, dpre_n.float().sum((0, 1))) < 1e-4
     assert rel_err(dw2_n, rdw2) < 2 * tol
     assert abs(float(db2_n) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
 
