@@ -32,6 +32,9 @@ def main():
     dev = torch.device("cuda")
     shapes = [("qkv", 2304, 768, 0, False), ("out_proj+res", 768, 768, 0, True), ("ffn1+gelu", 3072, 768, 1, False),
               ("ffn2+res", 768, 3072, 0, True), ("head_fc1+tanh", 384, 768, 2, False)]
+    if a.shapes == "nores":  # the residual shapes without their residual (LN-side residual study)
+        shapes = [("out_proj", 768, 768, 0, False), ("out_proj+res", 768, 768, 0, True),
+                  ("ffn2", 768, 3072, 0, False), ("ffn2+res", 768, 3072, 0, True)]
     if a.shapes == "square":
         shapes = [("sq8192", 8192, 8192, 0, False), ("sq4096", 4096, 4096, 0, False)]
     res = {}

@@ -75,6 +75,9 @@ def main():
             ms = timeit(lambda: lib.layer_norm(x, w, b, 1e-12))
             rec(f"layer_norm[wide={wide}]", ms, 2 * M * D * 2)
         lib.ln_set_wide(1)
+        r = torch.randn(M, D, generator=g).to(dev, torch.bfloat16)
+        ms = timeit(lambda: lib.layer_norm(x, w, b, 1e-12, r))
+        rec("layer_norm+residual", ms, 3 * M * D * 2)
     if want("embed_ln"):
         word = (torch.randn(30522, D, generator=g) * 0.02).to(dev, torch.bfloat16)
         pos = (torch.randn(512, D, generator=g) * 0.02).to(dev, torch.bfloat16)

@@ -24,7 +24,7 @@ int fr_gelu_bf16(const void* z, const void* dh, void* out, long n, int bwd, hipS
 int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles, int T, int H,
                                 int D, hipStream_t s);
 int fr_layer_norm_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
-                       hipStream_t s);
+                       const void* res, hipStream_t s);
 int fr_embed_ln_bf16(const int* tokens, const void* word, const void* pos, const float* w, const float* b, void* y,
                      int rows, int D, int T, float eps, hipStream_t s);
 int fr_title_attention_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
@@ -97,15 +97,23 @@ at::Tensor linear(const at::Tensor& x, const at::Tensor& w, const c10::optional<
   return out;
 }
 
-at::Tensor layer_norm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps) {
+at::Tensor layer_norm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps,
+                      const c10::optional<at::Tensor>& residual) {
   check_dev(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::layer_norm: bf16");
   const c10::DeviceGuard g(x.device());
   const int64_t D = x.size(-1);
   auto wf = w.to(at::kFloat).contiguous(), bf = b.to(at::kFloat).contiguous();
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    check_dev(*residual, "residual");
+    TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->numel() == x.numel(),
+                "fedrec::layer_norm: residual must match x (bf16)");
+    rp = residual->data_ptr();
+  }
   auto y = at::empty_like(x);
   check_rc(fr_layer_norm_bf16(x.data_ptr(), wf.data_ptr<float>(), bf.data_ptr<float>(), y.data_ptr(),
-                              (int)(x.numel() / D), (int)D, (float)eps, cur_stream()),
+                              (int)(x.numel() / D), (int)D, (float)eps, rp, cur_stream()),
            "layer_norm");
   return y;
 }
@@ -423,7 +431,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attn_set_waves(int w) -> ()", &title_attn_set_waves);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
-  m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps) -> Tensor");
+  m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual=None) -> Tensor");
   m.def("layer_norm_bwd(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("gelu(Tensor z, Tensor? dh) -> Tensor");
   m.def("title_attention_bwd(Tensor qkv, Tensor dout, Tensor mask, int n_heads) -> Tensor");

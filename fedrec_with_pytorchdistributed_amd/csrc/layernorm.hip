@@ -18,7 +18,8 @@ template <bool EMBED>
 __global__ __launch_bounds__(256) void ln_kernel(const bf16* __restrict__ x, const int* __restrict__ tokens,
                                                  const bf16* __restrict__ word, const bf16* __restrict__ pos,
                                                  const float* __restrict__ w, const float* __restrict__ b,
-                                                 bf16* __restrict__ y, int rows, int D, int T, float eps) {
+                                                 bf16* __restrict__ y, int rows, int D, int T, float eps,
+                                                 const bf16* __restrict__ res) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -32,6 +33,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const bf16* __restrict__ x, con
     src1 = pos + (size_t)(row % T) * D;
   } else {
     src0 = x + (size_t)row * D;
+    if (res != nullptr) src1 = res + (size_t)row * D;  // LN(x + residual)
   }
   float s = 0.f;
 #pragma unroll
@@ -41,7 +43,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const bf16* __restrict__ x, con
       bf16x4 a = *(const bf16x4*)(src0 + i);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[c][k] = (float)a[k];
-      if constexpr (EMBED) {
+      if (EMBED || src1 != nullptr) {
         bf16x4 p = *(const bf16x4*)(src1 + i);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[c][k] += (float)p[k];
@@ -89,7 +91,8 @@ template <bool EMBED, int NC, int RPH>
 __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, const int* __restrict__ tokens,
                                                    const bf16* __restrict__ word, const bf16* __restrict__ pos,
                                                    const float* __restrict__ w, const float* __restrict__ b,
-                                                   bf16* __restrict__ y, int rows, int T, float eps) {
+                                                   bf16* __restrict__ y, int rows, int T, float eps,
+                                                   const bf16* __restrict__ res) {
   constexpr int D = 256 * NC;
   const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -106,6 +109,7 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
       s1 = pos + (size_t)(row % T) * D;
     } else {
       s0 = x + (size_t)row * D;
+      if (res != nullptr) s1 = res + (size_t)row * D;  // LN(x + residual)
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
       const bf16x8 a = *(const bf16x8*)(s0 + i);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[q][c][k] = (float)a[k];
-      if constexpr (EMBED) {
+      if (EMBED || s1 != nullptr) {
         const bf16x8 p = *(const bf16x8*)(s1 + i);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[q][c][k] += (float)p[k];
@@ -161,18 +165,18 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
 
 template <bool EMBED>
 bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* pos, const float* w, const float* b,
-                 bf16* y, int rows, int D, int T, float eps, hipStream_t s) {
+                 bf16* y, int rows, int D, int T, float eps, hipStream_t s, const bf16* res = nullptr) {
   constexpr int RPH = 2;                // rows per half-wave -> 4 per wave, 16 per 256-thread block
   constexpr int RPB = 8 * RPH;
   const int blocks = (rows + RPB - 1) / RPB;
   if (D == 768)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 3, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 3, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
   else if (D == 512)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 2, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 2, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
   else if (D == 1024)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 4, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 4, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
   else if (D == 256)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 1, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 1, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
   else
     return false;
   return true;
@@ -335,14 +339,16 @@ extern "C" int fr_gelu_bf16(const void* z, const void* dh, void* out, long n, in
   return 0;
 }
 
+// y = LN(x [+ res]) * w + b; res may be null
 extern "C" int fr_layer_norm_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
-                                  hipStream_t s) {
+                                  const void* res, hipStream_t s) {
   if (D % 4 != 0 || D > 256 * MAXC) return 1;
   if (rows == 0) return 0;
-  if (g_ln_wide && launch_ln16<false>((const bf16*)x, nullptr, nullptr, nullptr, w, b, (bf16*)y, rows, D, 1, eps, s))
+  if (g_ln_wide && launch_ln16<false>((const bf16*)x, nullptr, nullptr, nullptr, w, b, (bf16*)y, rows, D, 1, eps, s,
+                                      (const bf16*)res))
     return 0;
   hipLaunchKernelGGL((ln_kernel<false>), dim3((rows + 3) / 4), dim3(256), 0, s, (const bf16*)x, nullptr, nullptr,
-                     nullptr, w, b, (bf16*)y, rows, D, 1, eps);
+                     nullptr, w, b, (bf16*)y, rows, D, 1, eps, (const bf16*)res);
   return 0;
 }
 
@@ -353,6 +359,6 @@ extern "C" int fr_embed_ln_bf16(const int* tokens, const void* word, const void*
   if (g_ln_wide && launch_ln16<true>(nullptr, tokens, (const bf16*)word, (const bf16*)pos, w, b, (bf16*)y, rows, D, T, eps, s))
     return 0;
   hipLaunchKernelGGL((ln_kernel<true>), dim3((rows + 3) / 4), dim3(256), 0, s, nullptr, tokens, (const bf16*)word,
-                     (const bf16*)pos, w, b, (bf16*)y, rows, D, T, eps);
+                     (const bf16*)pos, w, b, (bf16*)y, rows, D, T, eps, nullptr);
   return 0;
 }

@@ -55,10 +55,12 @@ def linear(x, w, b=None, act: str = "none", residual=None, out_dtype=None):
     return y.to(out_dtype or x.dtype)
 
 
-def layer_norm(x, w, b, eps: float, dtype=None):
+def layer_norm(x, w, b, eps: float, dtype=None, residual=None):
+    """``LN(x [+ residual]) * w + b`` (the residual add is fused into the LN kernel)."""
     if _dev(x) and x.dtype == torch.bfloat16:
-        return native.require_for(x).layer_norm(x, w, b, float(eps))
-    return ref.layer_norm(x, w, b, eps).to(dtype or x.dtype)
+        return native.require_for(x).layer_norm(x, w, b, float(eps), residual)
+    h = x if residual is None else x.float() + residual.float()
+    return ref.layer_norm(h, w, b, eps).to(dtype or x.dtype)
 
 
 def title_attention(qkv, mask, n_heads: int):

@@ -80,11 +80,10 @@ def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0, g
     # every rank must pick the same backends: decided by the machine, not by this rank's role
     gpu_job = torch.cuda.is_available() and os.environ.get("FEDREC_CPU_ONLY", "0") != "1"
     backend = "cpu:gloo,cuda:nccl" if gpu_job else "gloo"
-    kw = {"device_id": dev} if use_cuda else {}
-    try:
-        dist.init_process_group(backend=backend, init_method="env://", timeout=timeout, **kw)
-    except TypeError:
-        dist.init_process_group(backend=backend, init_method="env://", timeout=timeout)
+    # no device_id: that would make the default group initialise its RCCL communicator eagerly,
+    # a collective the CPU coordinator of a star run never joins (hang); the RCCL data group
+    # below is created among the GPU clients only and initialises on first use.
+    dist.init_process_group(backend=backend, init_method="env://", timeout=timeout)
     ctx.initialized = True
     ctx.ctrl_group = dist.new_group(backend="gloo", timeout=timeout)
     roles: List[Optional[str]] = [None] * world

@@ -68,6 +68,13 @@ def test_layer_norm_forms(dev, wide, rows, D):
     finally:
         lib.ln_set_wide(1)
     assert rel_err(y, ref.layer_norm(x.float(), w, b, 1e-12)) < 1e-2
+    r = torch.randn(rows, D, device=dev).to(torch.bfloat16)
+    lib.ln_set_wide(wide)
+    try:
+        yr = lib.layer_norm(x, w, b, 1e-12, r)
+    finally:
+        lib.ln_set_wide(1)
+    assert rel_err(yr, ref.layer_norm(x.float() + r.float(), w, b, 1e-12)) < 1e-2
     e_ref = ref.embed_ln(tok.view(rows, 1).long(), word.float(), pos.float(), w, b, 1e-12)
     assert rel_err(e, e_ref) < 1e-2
 
