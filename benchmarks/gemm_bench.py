@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--M", type=int, default=78850)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--out", default="")
+    ap.add_argument("--diag", action="store_true", help="add the no-store diagnostic variant (timing only)")
+    ap.add_argument("--only-shape", default="", help="run just this shape name (profiling)")
+    ap.add_argument("--only-variants", default="", help="comma list of variant names to keep (profiling)")
     ap.add_argument("--shapes", default="model", help="model | square (8192^3 / 4096^3, no epilogue)")
     a = ap.parse_args()
     lib = native.lib()
@@ -37,6 +40,8 @@ def main():
                   ("ffn2", 768, 3072, 0, False), ("ffn2+res", 768, 3072, 0, True)]
     if a.shapes == "square":
         shapes = [("sq8192", 8192, 8192, 0, False), ("sq4096", 4096, 4096, 0, False)]
+    if a.only_shape:
+        shapes = [s_ for s_ in shapes if s_[0] == a.only_shape]
     res = {}
     for name, N, K, act, has_res in shapes:
         M = N if name.startswith("sq") else a.M
@@ -61,6 +66,10 @@ def main():
             variants["ours-256p-split"] = ours(4)
             variants["ours-256p-split-pipe"] = ours(5)
             variants["ours-pingpong"] = ours(6)
+            if N <= 3072:
+                variants["ours-pingpong-v9"] = ours(9)
+            if a.diag:
+                variants["diag-pingpong-nostore"] = ours(7)
         bb = b.to(torch.bfloat16)
 
         def lt():
@@ -74,6 +83,9 @@ def main():
             return y
 
         variants["hipblaslt(+eager epilogue)"] = lt
+        if a.only_variants:
+            keep = [("hipblaslt(+eager epilogue)" if k == "lib" else k) for k in a.only_variants.split(",")]
+            variants = {k: v for k, v in variants.items() if k in keep}
         times = {k: [] for k in variants}
         for f in variants.values():
             f()
@@ -88,11 +100,11 @@ def main():
                 torch.cuda.synchronize()
                 times[k].append(s.elapsed_time(e) / 5)
         lib.gemm_set_variant(-1)
-        ref = variants["hipblaslt(+eager epilogue)"]().float()
+        ref = lt().float()
         row = {}
         for k, ts in times.items():
             med = statistics.median(ts)
-            err = float((variants[k]().float() - ref).norm() / ref.norm()) if k.startswith("ours") else 0.0
+            err = float((variants[k]().float() - ref).norm() / ref.norm()) if k.startswith("ours") else float("nan")
             row[k] = {"ms": round(med, 4), "tflops": round(flops / med / 1e9, 1), "rel_err_vs_lib": round(err, 5)}
         res[f"{name} M={M} N={N} K={K}"] = row
         print(name, json.dumps(row), flush=True)

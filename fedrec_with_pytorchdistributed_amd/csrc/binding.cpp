@@ -16,8 +16,8 @@ extern "C" {
 void fr_gemm_set_variant(int v);
 void fr_title_attn_set_waves(int w);
 void fr_ln_set_wide(int v);
-int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K,
-                    int act, hipStream_t s);
+int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K, int act,
+                    int c_rows, hipStream_t s);
 int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db, int rows, int D,
                            float eps, hipStream_t s);
 int fr_gelu_bf16(const void* z, const void* dh, void* out, long n, int bwd, hipStream_t s);
@@ -76,7 +76,9 @@ at::Tensor linear(const at::Tensor& x, const at::Tensor& w, const c10::optional<
   const int64_t M = x.numel() / K;
   auto out_shape = x.sizes().vec();
   out_shape.back() = N;
-  auto out = at::empty(out_shape, x.options());
+  // rows padded to the 256-row tile: the GEMM epilogue then stores without a row predicate
+  const int64_t c_rows = (M + 255) / 256 * 256;
+  auto out = at::empty({c_rows * N}, x.options()).narrow(0, 0, M * N).view(out_shape);
   const float* bp = nullptr;
   at::Tensor bf;
   if (b.has_value() && b->defined()) {
@@ -92,7 +94,7 @@ at::Tensor linear(const at::Tensor& x, const at::Tensor& w, const c10::optional<
   }
   if (M == 0) return out;
   check_rc(fr_gemm_nt_bf16(x.data_ptr(), w.data_ptr(), bp, rp, out.data_ptr(), (int)M, (int)N, (int)K, (int)act,
-                           cur_stream()),
+                           (int)c_rows, cur_stream()),
            "linear");
   return out;
 }

@@ -25,7 +25,8 @@
 // Variants (fr_gemm_set_variant; -1 = auto): 0 the 128x128 kernel above; 1 256x256; 2 its
 // persistent form; 3 BK=32 four-stage; 4/5 persistent with split staging (+ register-
 // pipelined fragments); 6 persistent 256x256 ping-pong (two wave rows half a phase apart).
-// Auto: 6 for N % 256 == 0 (K >= 128), 0 otherwise (benchmarks/gemm_bench.py).
+// 9 = ping-pong with a store-tolerant stage schedule.  Auto: 9 for N % 256 == 0, N <= 3072,
+// K >= 128 (row-padded C); 6 for other N % 256 == 0; 0 otherwise (benchmarks/gemm_bench.py).
 #include "common.h"
 
 namespace {
@@ -594,6 +595,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256s_kernel(const bf16* __rest
 //   tile walk): the next tile's first half-tiles are in flight during the current tile's
 //   last phases; each wave row stores its tile while the other row is still on MFMAs.
 constexpr int PP_HALF = 16384;
+constexpr int PP2_MAXN = 3072;  // bias staged in LDS by variant 9
 
 __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -603,7 +605,7 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int ACT, bool HAS_BIAS, bool HAS_RES>
+template <int ACT, bool HAS_BIAS, bool HAS_RES, int EPI = 0>  // EPI 1: diagnostic build, stores suppressed
 __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                             const float* __restrict__ bias,
                                                             const bf16* __restrict__ R, bf16* __restrict__ C, int M,
@@ -768,7 +770,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restri
                 v0 += (float)rr[i][p][j][0]; v1 += (float)rr[i][p][j][1];
                 v2 += (float)rr[i][p][j][2]; v3 += (float)rr[i][p][j][3];
               }
-              if (m < M) {
+              if (m < M && (EPI == 0 || v0 == 1234.5f)) {
                 bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
                 *(bf16x4*)(C + (size_t)m * N + nb0 + p * 32 + j * 16) = o;
               }
@@ -789,28 +791,286 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restri
   if (wr == 0) pp_barrier();  // balance the staggered row's extra barrier
 }
 
+// Store one 32-column group of a 16x16 MFMA row block: lane (fr, fq) holds columns
+// [4fq, 4fq+4) of frag j = 0 (v0) and of frag j = 1 (v1, +16).  One v_permlane16_swap per
+// dword pair gives every lane 8 contiguous columns -- fq 0: 0-7, 1: 16-23, 2: 8-15,
+// 3: 24-31 -- so the group goes out as ONE 16-byte store per lane instead of two 8-byte
+// ones (cdna_hip_programming.md T21).
+__device__ __forceinline__ void store_pair16(bf16* __restrict__ crow, const float (&v0)[4], const float (&v1)[4],
+                                             int fq) {
+  const bf16x4 o0 = {f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3])};
+  const bf16x4 o1 = {f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+  uint2 a = __builtin_bit_cast(uint2, o0), b = __builtin_bit_cast(uint2, o1);
+  auto r = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  a.x = r[0];
+  b.x = r[1];
+  r = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  a.y = r[0];
+  b.y = r[1];
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  *GLOBAL_PTR(u32x4, crow + (fq & 1) * 16 + (fq >> 1) * 8) = u32x4{a.x, a.y, b.x, b.y};
+}
+
+// ---------------------------------------------------------------------------------------
+// Variant 9: the ping-pong kernel with a store-tolerant stage schedule.  Profiling variant 6
+// (scripts/gpu_gemm_pmc.sh) showed the epilogue stores cost +81 % SQ_WAIT_ANY: vmcnt retires
+// in issue order, so the next K-step's counted wait -- which needs a half-tile staged AFTER
+// the stores -- also waits for every store to be acknowledged.  Here all four half-tiles of
+// step g+2 are staged during step g (A_h0 @ phase 1, B_h0 @ 2, B_h1 + A_h1 @ 3), so the
+// half-tiles that the wait after an epilogue needs were issued BEFORE its stores and the wait
+// can leave them outstanding: vmcnt(8) normally, vmcnt(8 + 16) in the step after a tile's
+// epilogue (exactly 16 unconditional dwordx4 stores per wave: C has round_up(M, 256) rows,
+// so no row predicate; bias comes from LDS, so the epilogue issues no loads; with a residual
+// its loads would break the count, so HAS_RES keeps vmcnt(8)).  One more half-tile is in
+// flight per wait than in variant 6.  WAR: every half is restaged >= 1 phase after its last
+// read (A_h1 is read in phase 2 and restaged in phase 3).
+template <int ACT, bool HAS_BIAS, bool HAS_RES>
+__global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                             const float* __restrict__ bias,
+                                                             const bf16* __restrict__ R, bf16* __restrict__ C, int M,
+                                                             int N, int K, int tiles_n, int ntiles) {
+  // ONE __shared__ object (staging halves + the bias vector): a second one makes hipcc drain
+  // vmcnt(0) before every fragment read (cdna_hip_programming.md §5 "Three .s-level traps")
+  __shared__ __attribute__((aligned(16))) char smem[8 * PP_HALF + (HAS_BIAS ? PP2_MAXN * 4 : 0)];
+  float* bias_s = (float*)(smem + 8 * PP_HALF);
+  const int G = gridDim.x, b = blockIdx.x;
+  const int c = (G % 8 == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
+  if (c >= ntiles) return;
+  const int nk = K >> 6;
+  const int S = ((ntiles - c + G - 1) / G) * nk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rsub = lane >> 3, schunk = (lane & 7) ^ rsub;
+  if constexpr (HAS_BIAS) {
+    for (int i = tid; i < N; i += 512) bias_s[i] = bias[i];
+  }
+  int ocur[4][2], onxt[4][2];
+  auto tile_offs = [&](int itile, int (&o)[4][2]) {
+    int t = itile * G + c;
+    t = t < ntiles ? t : c;
+    const int mt = t / tiles_n;
+    const int m0 = mt * 256, n0 = (t - mt * tiles_n) * 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rho = wave * 16 + i * 8 + rsub;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int gm = m0 + (rho >> 6) * 128 + h * 64 + (rho & 63);
+        gm = gm < M ? gm : M - 1;
+        o[h][i] = gm * K + schunk * 8;
+        o[2 + h][i] = (n0 + (rho >> 5) * 64 + h * 32 + (rho & 31)) * K + schunk * 8;
+      }
+    }
+  };
+  auto stage = [&](int g, int h, int kts, bool nx) {
+    if (g >= S) return;
+    char* dst = smem + ((g & 1) * 4 + h) * PP_HALF;
+    const bf16* base = (h < 2 ? A : W) + kts * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int off = nx ? onxt[h][i] : ocur[h][i];
+      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, base + off),
+                                       LDS_PTR(void, dst + (wave * 16 + i * 8) * 128), 16, 0, 0);
+    }
+  };
+  // prologue: steps 0 and 1 (all halves); retire step 0 (bias loads are older: retired too)
+  tile_offs(0, ocur);
+  tile_offs(1, onxt);
+  const bool nx_1 = nk < 2;  // nk >= 2 on the host path: step 1 is in tile 0
+  stage(0, 0, 0, false); stage(0, 2, 0, false); stage(0, 3, 0, false); stage(0, 1, 0, false);
+  stage(1, 0, 1, nx_1); stage(1, 2, 1, nx_1); stage(1, 3, 1, nx_1); stage(1, 1, 1, nx_1);
+  if (S > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (wr == 1) pp_barrier();
+
+  f32x4 acc[2][4][2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[q][i][p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = (wr * 64 + fr) * 128, brow = (wc * 32 + fr) * 128;
+  const int ph0 = ((0 * 4 + fq) ^ (fr & 7)) * 16, ph1 = ((1 * 4 + fq) ^ (fr & 7)) * 16;
+  auto read_a = [&](const char* hb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *(const bf16x8*)(hb + arow + i * 16 * 128 + ph0);
+      af[i][1] = *(const bf16x8*)(hb + arow + i * 16 * 128 + ph1);
+    }
+  };
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf[j][0] = *(const bf16x8*)(hb + brow + j * 16 * 128 + ph0);
+      bf[j][1] = *(const bf16x8*)(hb + brow + j * 16 * 128 + ph1);
+    }
+  };
+#define PP_MFMA(QM, QN, BF)                                                                             \
+  {                                                                                                     \
+    pp_barrier();                                                                                       \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                \
+    __builtin_amdgcn_s_setprio(1);                                                                      \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) _Pragma("unroll") for (int i = 0; i < 4; ++i)      \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[QM][i][QN][j] =                               \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j][kk], af[i][kk], acc[QM][i][QN][j], 0, 0, 0);  \
+    __builtin_amdgcn_s_setprio(0);                                                                      \
+    pp_barrier();                                                                                       \
+  }
+
+  int kt = 0, it = 0;
+  bool after_epi = false;  // the previous step ended with a tile epilogue (its 32 stores in flight)
+  for (int g = 0; g < S; ++g) {
+    const char* buf = smem + (g & 1) * 4 * PP_HALF;
+    const bool nx2 = kt + 2 >= nk;
+    const int k2 = nx2 ? kt + 2 - nk : kt + 2;
+    // phase 0: quadrant (0,0)
+    read_a(buf);
+    read_b(buf + 2 * PP_HALF, b0);
+    PP_MFMA(0, 0, b0)
+    // phase 1: quadrant (0,1)
+    read_b(buf + 3 * PP_HALF, b1);
+    stage(g + 2, 0, k2, nx2);
+    PP_MFMA(0, 1, b1)
+    // phase 2: quadrant (1,1)
+    read_a(buf + PP_HALF);
+    stage(g + 2, 2, k2, nx2);
+    PP_MFMA(1, 1, b1)
+    // phase 3: quadrant (1,0); stage the rest of g+2, retire step g+1
+    stage(g + 2, 3, k2, nx2);
+    stage(g + 2, 1, k2, nx2);
+    if (g + 2 >= S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (!HAS_RES && after_epi) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 loads + 16 stores
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    after_epi = false;
+    PP_MFMA(1, 0, b0)
+    if (++kt == nk) {
+      const int t = it * G + c;
+      const int mt = t / tiles_n;
+      const int m0 = mt * 256, n0 = (t - mt * tiles_n) * 256;
+      const int nb0 = n0 + wc * 64 + fq * 4;
+      f32x4 bb[2][2];
+      if constexpr (HAS_BIAS) {
+        // bias via opaque ds_reads (a plain read of the staging object would also drain vmcnt)
+        const uint32_t ba = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + 8 * PP_HALF + nb0 * 4;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(bb[0][0]) : "v"(ba));
+        asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(bb[0][1]) : "v"(ba));
+        asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(bb[1][0]) : "v"(ba));
+        asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(bb[1][1]) : "v"(ba));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bb[0][0]), "+v"(bb[0][1]), "+v"(bb[1][0]), "+v"(bb[1][1]));
+      } else {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) bb[p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        bf16x4 rr[4][2][2];
+        if constexpr (HAS_RES) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            int m = m0 + wr * 128 + q * 64 + i * 16 + fr;
+            m = m < M ? m : M - 1;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) rr[i][p][j] = *(const bf16x4*)(R + (size_t)m * N + nb0 + p * 32 + j * 16);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wr * 128 + q * 64 + i * 16 + fr;  // < round_up(M, 256): C is padded
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            float v[2][4];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              f32x4& a4 = acc[q][i][p][j];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[j][e] = a4[e] + bb[p][j][e];
+              act4<ACT>(v[j][0], v[j][1], v[j][2], v[j][3]);
+              if constexpr (HAS_RES) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[j][e] += (float)rr[i][p][j][e];
+              }
+              a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            store_pair16(C + (size_t)m * N + n0 + wc * 64 + p * 32, v[0], v[1], fq);
+          }
+        }
+      }
+      after_epi = true;
+      kt = 0;
+      ++it;
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ocur[h][i] = onxt[h][i];
+      tile_offs(it + 1, onxt);
+    }
+  }
+#undef PP_MFMA
+  if (wr == 0) pp_barrier();
+}
+
 int g_num_cus = 0;
 
 int g_gemm_variant = -1;  // -1 auto, 0 = 128x128, 1 = 256x256
 
 template <int ACT>
 void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, bf16* C, int M, int N, int K,
-                hipStream_t s) {
+                int c_rows, hipStream_t s) {
   const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && N % BN2 == 0 && M >= 4096);
   // auto policy (measured, profiles/gemm_bench_r1_pp.json): the ping-pong kernel (6) on every
   // N % 256 == 0 shape (with the packed-f32 GELU epilogue it also edges out variant 5 on FFN1).
-  const bool pp = g_gemm_variant == 6 || g_gemm_variant < 0;
-  if (big && N % BN2 == 0 && pp && K >= 128 && (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
+  // auto: variant 9 wherever it applies (measured: profiles/gemm_bench_r1_v9.json), else 6
+  const bool v9 = g_gemm_variant == 9 || g_gemm_variant < 0;
+  if (big && N % BN2 == 0 && v9 && K >= 128 && N <= PP2_MAXN && c_rows >= ((M + 255) / 256) * 256 &&
+      (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     if (g_num_cus == 0) {
       int dev = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (g_num_cus <= 0) g_num_cus = 256;
     }
     int G = ntiles < g_num_cus ? ntiles : g_num_cus;
     dim3 grid(G), block(512);
-#define LPP(HB, HR) hipLaunchKernelGGL((gemm_nt_pp_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
+#define LPP2(HB, HR) hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
+    if (bias && R) LPP2(true, true);
+    else if (bias) LPP2(true, false);
+    else if (R) LPP2(false, true);
+    else LPP2(false, false);
+#undef LPP2
+    return;
+  }
+  const bool pp = g_gemm_variant == 6 || g_gemm_variant == 7 || g_gemm_variant < 0;
+  if (big && N % BN2 == 0 && pp && K >= 128 && (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
+    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
+    if (g_num_cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
+    dim3 grid(G), block(512);
+#define LPP(HB, HR)                                                                                       \
+  do {                                                                                                    \
+    if (g_gemm_variant == 7) /* diagnostic: no stores (timing only, output undefined) */                  \
+      hipLaunchKernelGGL((gemm_nt_pp_kernel<ACT, HB, HR, 1>), grid, block, 0, s, A, W, bias, R, C, M, N, K, \
+                         tiles_n, ntiles);                                                                \
+    else                                                                                                  \
+      hipLaunchKernelGGL((gemm_nt_pp_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K,    \
+                         tiles_n, ntiles);                                                                \
+  } while (0)
     if (bias && R) LPP(true, true);
     else if (bias) LPP(true, false);
     else if (R) LPP(false, true);
@@ -822,8 +1082,8 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     if (g_num_cus == 0) {
       int dev = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (g_num_cus <= 0) g_num_cus = 256;
     }
     int G = ntiles < g_num_cus ? ntiles : g_num_cus;
@@ -840,8 +1100,8 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     if (g_num_cus == 0) {
       int dev = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (g_num_cus <= 0) g_num_cus = 256;
     }
     int G = ntiles < g_num_cus ? ntiles : g_num_cus;
@@ -888,17 +1148,18 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
 
 extern "C" void fr_gemm_set_variant(int v) { g_gemm_variant = v; }
 
+// c_rows: rows allocated in C (>= M); round_up(M, 256) lets variant 9 store without a row predicate
 extern "C" int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N,
-                               int K, int act, hipStream_t s) {
+                               int K, int act, int c_rows, hipStream_t s) {
   if (N % BN != 0 || K % BK != 0 || M <= 0) return 1;
   const bf16* a = (const bf16*)A;
   const bf16* w = (const bf16*)W;
   const bf16* r = (const bf16*)R;
   bf16* c = (bf16*)C;
   switch (act) {
-    case 0: launch_act<0>(a, w, bias, r, c, M, N, K, s); break;
-    case 1: launch_act<1>(a, w, bias, r, c, M, N, K, s); break;
-    case 2: launch_act<2>(a, w, bias, r, c, M, N, K, s); break;
+    case 0: launch_act<0>(a, w, bias, r, c, M, N, K, c_rows, s); break;
+    case 1: launch_act<1>(a, w, bias, r, c, M, N, K, c_rows, s); break;
+    case 2: launch_act<2>(a, w, bias, r, c, M, N, K, c_rows, s); break;
     default: return 2;
   }
   return 0;

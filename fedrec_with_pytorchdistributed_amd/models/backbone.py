@@ -13,8 +13,8 @@ Compute layout (MI355X path):
   fused into one ``[3D, D]`` bf16 weight (one GEMM with N = 2304 instead of three),
   biases fp32.  The pack is cached and rebuilt only when the fp32 weights change
   (``invalidate()``: load_state_dict, optimizer step in unfrozen mode);
-* :meth:`forward` runs ``embed_ln -> [qkv GEMM -> title attention -> out GEMM(+res) -> LN
-  -> FFN1 GEMM(+GELU) -> FFN2 GEMM(+res) -> LN] x L`` through :mod:`..ops`.
+* :meth:`forward` runs ``embed_ln -> [qkv GEMM -> title attention -> out GEMM -> LN(+res)
+  -> FFN1 GEMM(+GELU) -> FFN2 GEMM -> LN(+res)] x L`` through :mod:`..ops`.
 
 Initialisation follows HF DistilBERT ``_init_weights`` (normal(0, 0.02) for linears and
 embeddings, zero biases, LN = (1, 0), padding row 0 of the word table zeroed).  There are
@@ -149,11 +149,13 @@ class Backbone(nn.Module):
         for L in P["layers"]:
             qkv = ops.linear(x, L["wqkv"], L["bqkv"], out_dtype=dtype)
             ctx = ops.title_attention(qkv, mask, c.n_heads)
-            h = ops.linear(ctx, L["wo"], L["bo"], residual=x, out_dtype=dtype)
-            x = ops.layer_norm(h, L["ln1_w"], L["ln1_b"], c.ln_eps, dtype)
+            # residual adds ride in the LayerNorm kernel (LN(h + x)): a residual read in the GEMM
+            # epilogue stalls the ping-pong schedule (out-proj 638 -> 850 TF without it)
+            h = ops.linear(ctx, L["wo"], L["bo"], out_dtype=dtype)
+            x = ops.layer_norm(h, L["ln1_w"], L["ln1_b"], c.ln_eps, dtype, residual=x)
             f = ops.linear(x, L["w1"], L["b1"], act="gelu", out_dtype=dtype)
-            h = ops.linear(f, L["w2"], L["b2"], residual=x, out_dtype=dtype)
-            x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, dtype)
+            h = ops.linear(f, L["w2"], L["b2"], out_dtype=dtype)
+            x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, dtype, residual=x)
         return x
 
     def forward_train(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
