@@ -68,6 +68,7 @@ def main():
             variants["ours-pingpong"] = ours(6)
             if N <= 3072:
                 variants["ours-pingpong-v9"] = ours(9)
+                variants["ours-pingpong-v10-deferred"] = ours(10)
             if a.diag:
                 variants["diag-pingpong-nostore"] = ours(7)
         bb = b.to(torch.bfloat16)

@@ -824,7 +824,11 @@ __device__ __forceinline__ void store_pair16(bf16* __restrict__ crow, const floa
 // its loads would break the count, so HAS_RES keeps vmcnt(8)).  One more half-tile is in
 // flight per wait than in variant 6.  WAR: every half is restaged >= 1 phase after its last
 // read (A_h1 is read in phase 2 and restaged in phase 3).
-template <int ACT, bool HAS_BIAS, bool HAS_RES>
+// DEFER (variant 10, no residual): a finished tile's epilogue is spread over the next tile's
+// first K-step -- quadrant q is stored in the load section of the phase whose MFMAs next write
+// it (4 x 16-B stores per phase), so each wave row's epilogue overlaps the other row's MFMAs
+// instead of stalling it at a barrier.
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DEFER = false>
 __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                              const float* __restrict__ bias,
                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
@@ -924,8 +928,36 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     pp_barrier();                                                                                       \
   }
 
+  // deferred epilogue: store quadrant (QM, QN) of the pending tile (pm0, pn0), then zero it
+  int pm0 = 0, pn0 = 0;
+  bool pend = false, after_pend = false;
+  const uint32_t bias_lds = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + 8 * PP_HALF;
+#define PP2_STORE_Q(QM, QN)                                                                         \
+  {                                                                                                 \
+    const int nq = pn0 + wc * 64 + QN * 32;                                                         \
+    f32x4 bq0 = f32x4{0.f, 0.f, 0.f, 0.f}, bq1 = f32x4{0.f, 0.f, 0.f, 0.f};                         \
+    if constexpr (HAS_BIAS) {                                                                       \
+      const uint32_t ba = bias_lds + (nq + fq * 4) * 4;                                             \
+      asm volatile("ds_read_b128 %0, %1" : "=v"(bq0) : "v"(ba));                                   \
+      asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(bq1) : "v"(ba));                         \
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bq0), "+v"(bq1));                                 \
+    }                                                                                               \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+      float v0[4], v1[4];                                                                           \
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                              \
+        v0[e] = acc[QM][i][QN][0][e] + bq0[e];                                                      \
+        v1[e] = acc[QM][i][QN][1][e] + bq1[e];                                                      \
+      }                                                                                             \
+      act4<ACT>(v0[0], v0[1], v0[2], v0[3]);                                                        \
+      act4<ACT>(v1[0], v1[1], v1[2], v1[3]);                                                        \
+      store_pair16(C + (size_t)(pm0 + wr * 128 + QM * 64 + i * 16 + fr) * N + nq, v0, v1, fq);     \
+      acc[QM][i][QN][0] = f32x4{0.f, 0.f, 0.f, 0.f};                                                \
+      acc[QM][i][QN][1] = f32x4{0.f, 0.f, 0.f, 0.f};                                                \
+    }                                                                                               \
+  }
+
   int kt = 0, it = 0;
-  bool after_epi = false;  // the previous step ended with a tile epilogue (its 32 stores in flight)
+  bool after_epi = false;  // the previous step ended with a tile epilogue (its 16 stores in flight)
   for (int g = 0; g < S; ++g) {
     const char* buf = smem + (g & 1) * 4 * PP_HALF;
     const bool nx2 = kt + 2 >= nk;
@@ -933,24 +965,50 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     // phase 0: quadrant (0,0)
     read_a(buf);
     read_b(buf + 2 * PP_HALF, b0);
+    if (DEFER && pend) PP2_STORE_Q(0, 0)
     PP_MFMA(0, 0, b0)
     // phase 1: quadrant (0,1)
     read_b(buf + 3 * PP_HALF, b1);
     stage(g + 2, 0, k2, nx2);
+    if (DEFER && pend) PP2_STORE_Q(0, 1)
     PP_MFMA(0, 1, b1)
     // phase 2: quadrant (1,1)
     read_a(buf + PP_HALF);
     stage(g + 2, 2, k2, nx2);
+    if (DEFER && pend) PP2_STORE_Q(1, 1)
     PP_MFMA(1, 1, b1)
-    // phase 3: quadrant (1,0); stage the rest of g+2, retire step g+1
+    // phase 3: quadrant (1,0); stage the rest of g+2, retire step g+1 (issued during step g-1,
+    // so everything of this step may stay in flight: its 8 loads and, deferred, 16 stores)
     stage(g + 2, 3, k2, nx2);
     stage(g + 2, 1, k2, nx2);
+    if (DEFER && pend) PP2_STORE_Q(1, 0)
     if (g + 2 >= S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (!HAS_RES && after_epi) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 loads + 16 stores
+    else if (DEFER && pend) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");        // 8 loads + 16 stores
+    else if (DEFER && after_pend) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // + last phase's 4 stores
+    else if (!DEFER && !HAS_RES && after_epi) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 + 16 stores
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    after_pend = DEFER && pend;
+    pend = false;
     after_epi = false;
     PP_MFMA(1, 0, b0)
-    if (++kt == nk) {
+    if (DEFER && ++kt == nk) {
+      const int t = it * G + c;
+      const int mt = t / tiles_n;
+      pm0 = mt * 256;
+      pn0 = (t - mt * tiles_n) * 256;
+      if (g + 1 < S) {
+        pend = true;
+      } else {
+        PP2_STORE_Q(0, 0) PP2_STORE_Q(0, 1) PP2_STORE_Q(1, 1) PP2_STORE_Q(1, 0)
+      }
+      kt = 0;
+      ++it;
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ocur[h][i] = onxt[h][i];
+      tile_offs(it + 1, onxt);
+    } else if (!DEFER && ++kt == nk) {
       const int t = it * G + c;
       const int mt = t / tiles_n;
       const int m0 = mt * 256, n0 = (t - mt * tiles_n) * 256;
@@ -1017,6 +1075,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     }
   }
 #undef PP_MFMA
+#undef PP2_STORE_Q
   if (wr == 0) pp_barrier();
 }
 
@@ -1031,7 +1090,7 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
   // auto policy (measured, profiles/gemm_bench_r1_pp.json): the ping-pong kernel (6) on every
   // N % 256 == 0 shape (with the packed-f32 GELU epilogue it also edges out variant 5 on FFN1).
   // auto: variant 9 wherever it applies (measured: profiles/gemm_bench_r1_v9.json), else 6
-  const bool v9 = g_gemm_variant == 9 || g_gemm_variant < 0;
+  const bool v9 = g_gemm_variant == 9 || g_gemm_variant == 10 || g_gemm_variant < 0;
   if (big && N % BN2 == 0 && v9 && K >= 128 && N <= PP2_MAXN && c_rows >= ((M + 255) / 256) * 256 &&
       (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
@@ -1043,7 +1102,15 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
     }
     int G = ntiles < g_num_cus ? ntiles : g_num_cus;
     dim3 grid(G), block(512);
-#define LPP2(HB, HR) hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
+#define LPP2(HB, HR)                                                                                          \
+  do {                                                                                                        \
+    if (!HR && g_gemm_variant == 10)                                                                          \
+      hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, HB, false, true>), grid, block, 0, s, A, W, bias, R, C, M, N, \
+                         K, tiles_n, ntiles);                                                                 \
+    else                                                                                                      \
+      hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K,       \
+                         tiles_n, ntiles);                                                                    \
+  } while (0)
     if (bias && R) LPP2(true, true);
     else if (bias) LPP2(true, false);
     else if (R) LPP2(false, true);

@@ -1,5 +1,4 @@
 #!/bin/bash
 source "$(dirname "$0")/gpu_round.sh"
 run kgemm 300 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm"
-run gemm 600 python benchmarks/gemm_bench.py --diag --out gpurun_out/gemm_bench_v9.json
-run gemmnr 600 python benchmarks/gemm_bench.py --shapes nores --out gpurun_out/gemm_bench_nores.json
+run gemm 600 python benchmarks/gemm_bench.py --diag --out gpurun_out/gemm_bench_v10.json
