@@ -56,6 +56,8 @@ def main() -> int:
     ap.add_argument("--valid-limit", type=int, default=2048)
     ap.add_argument("--no-valid", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--backbone", default="", help="test-only override of the backbone preset (e.g. 'tiny' for the "
+                                                    "multi-process CPU test); the reported model says so")
     args = ap.parse_args()
 
     import numpy as np
@@ -86,6 +88,12 @@ def main() -> int:
         cfg.local_update = "per_step"
     if args.config == 5:
         cfg.backbone = BackboneConfig.preset("bert-base")  # 12 layers, unfrozen
+    model_name = MODELS[args.config]
+    if args.backbone:
+        frozen = cfg.backbone.frozen
+        cfg.backbone = BackboneConfig.preset(args.backbone)
+        cfg.backbone.frozen = frozen
+        model_name = f"TEST ONLY: {args.backbone} backbone (not the BASELINE model)"
     torch.manual_seed(0)  # same init on every client (GA keeps them identical)
     model = FedRecModel(cfg).to(dev)
     model.build_flat()
@@ -178,7 +186,7 @@ def main() -> int:
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": f"synthetic ({args.preset} MIND-format shard per client, random-init weights)",
             "config": {
-                "model": MODELS[args.config],
+                "model": model_name,
                 "global_batch": args.batch * world,
                 "seq_len": cfg.title_len,
                 "history_len": cfg.max_his_len,

@@ -149,6 +149,9 @@ class FedRecConfig:
 
     # --- io / observability ------------------------------------------------------------
     snapshot_path: str = "snapshot.pt"
+    # reference round interchange files (client.py:288 model.pt, server.py:27
+    # received_model_{k}.pt), written beside snapshot_path; off by default (270 MB each)
+    round_artifacts: bool = False
     metrics_path: str = ""  # JSONL; empty = metrics.jsonl beside the snapshot on rank 0
     run_name: str = "fedrec"
     wandb_project: str = "Node4"  # only used when FEDREC_WANDB=1 and wandb is importable

@@ -209,6 +209,10 @@ def _aggregation(cfg: FedRecConfig, ctx: DistContext) -> str:
     return os.environ.get("FEDREC_STAR_AGG", "allreduce")
 
 
+def _artifact_dir(cfg: FedRecConfig) -> str:
+    return os.path.dirname(os.path.abspath(cfg.snapshot_path or "snapshot.pt"))
+
+
 def _client_upload_tensor(model: FedRecModel, cfg: FedRecConfig) -> torch.Tensor:
     return model.flat.flat.detach().float()
 
@@ -252,6 +256,9 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         meta = {"client": k, "n_train": len(shard.train), **{m: float(v) for m, v in {**tr, **va}.items()
                                                              if isinstance(v, (int, float))}}
         up = _client_upload_tensor(model, cfg).clone()
+        if cfg.round_artifacts:  # client.py:288 torch.save(model.state_dict(), "model.pt")
+            sub = "" if ctx.num_clients == 1 else f"client{k}"
+            ckpt.save_state_dict(os.path.join(_artifact_dir(cfg), sub, "model.pt"), model)
         fault.before_upload(r, up)
         if agg == "allreduce":
             w = float(len(shard.train)) if cfg.weighted_fedavg else 1.0
@@ -338,6 +345,9 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                 ups.append(t)
                 metas.append(meta)
                 accepted.append(k)
+                if cfg.round_artifacts and not cfg.secagg.enabled:  # server.py:27 received_model_{k}.pt
+                    ckpt.atomic_save(ckpt.flat_to_state_dict(model, t),
+                                     os.path.join(_artifact_dir(cfg), f"received_model_{k}.pt"))
             if cfg.secagg.enabled and len(accepted) != W:
                 raise RuntimeError(f"secure aggregation needs every client (got {len(accepted)}/{W})")
             if len(accepted) < need:

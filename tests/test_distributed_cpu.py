@@ -57,8 +57,8 @@ def test_param_avg_every_k_steps(tmp_path):
 @pytest.mark.slow
 def test_star_fedavg_server_plus_two_clients(tmp_path):
     snap = str(tmp_path / "server_snapshot.pt")
-    server = ["server.py", "2", *TINY, f"--snapshot_path={snap}"]
-    client = ["client.py", "1", "16", "1", "0", "c", *TINY, f"--snapshot_path={tmp_path}/c.pt"]
+    server = ["server.py", "2", *TINY, f"--snapshot_path={snap}", "--round_artifacts=1"]
+    client = ["client.py", "1", "16", "1", "0", "c", *TINY, f"--snapshot_path={tmp_path}/c.pt", "--round_artifacts=1"]
     # the coordinator is rank 1 here on purpose: roles come from the entrypoint (Q13)
     outs = run_ranks([client, server, client], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump"),
                                                 "FEDREC_STAR_AGG": "upload"})
@@ -67,13 +67,18 @@ def test_star_fedavg_server_plus_two_clients(tmp_path):
     assert [h["round"] for h in hist] == [0, 1] and all(h["clients_accepted"] == 2 for h in hist)
     assert os.path.exists(tmp_path / "global_model_round1.pt")
     g = torch.load(tmp_path / "global_model_round1.pt", weights_only=True)
-    # the server's global model is the mean of the two client uploads of the last round
-    c0 = torch.load(tmp_path / "dump" / "rank0.pt")
-    c2 = torch.load(tmp_path / "dump" / "rank2.pt")
     snapd = torch.load(snap, weights_only=True)
     assert snapd["ROUND"] == 1
-    fc = g["text_encoder.fc.weight"].reshape(-1)
-    assert fc.numel() > 0
+    # reference interchange files: each client's model.pt (client.py:288) and the server's
+    # received_model_{k}.pt (server.py:27); the global model is their unweighted mean
+    # (server.py:46-50) -- all in the 116-key reference state_dict layout
+    r0 = torch.load(tmp_path / "received_model_0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "received_model_1.pt", weights_only=True)
+    m0 = torch.load(tmp_path / "client0" / "model.pt", weights_only=True)
+    assert set(r0) == set(g) == set(m0)
+    for key in ("text_encoder.fc.weight", "user_encoder.additive_attention.att_fc1.weight"):
+        assert torch.allclose(g[key], (r0[key] + r1[key]) / 2, atol=1e-6), key
+    assert not torch.equal(r0["text_encoder.fc.weight"], r1["text_encoder.fc.weight"])
 
 
 @pytest.mark.slow
@@ -153,4 +158,27 @@ def test_grad_avg_secure_aggregation_matches_plain(tmp_path):
     b = torch.load(tmp_path / "sec" / "rank0.pt")
     c = torch.load(tmp_path / "sec" / "rank1.pt")
     assert torch.equal(b, c)
-    assert float((a - b).abs().max()) < 2e-5  # fixed 2^-22 grid gave 8.6e-4 (Adam amplifies)
+    # Adam normalises each coordinate, so a gradient near the fixed-point step can move its
+    # parameter by up to lr per step either way: bound the bulk tightly, the tail by lr * steps
+    d = (a - b).abs()
+    assert float(torch.quantile(d.float(), 0.999)) < 1e-6
+    assert float((d > 1e-6).float().mean()) < 1e-4
+    assert float(d.max()) < 5e-5 * 40  # lr x (an upper bound on the epoch's steps)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("config", [2, 3, 4])
+def test_bench_contract_two_ranks(config):
+    """bench.py under the driver's multi-rank launch contract (gloo here, RCCL on the node):
+    exactly one JSON line, from rank 0, with the whole-job value and the BASELINE metric."""
+    argv = ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "4", "--preset", "tiny",
+            "--backbone", "tiny", "--config", str(config), "--pa-every", "1", "--valid-limit", "16"]
+    outs = run_ranks([argv, argv], timeout=300)
+    _ok(outs)
+    lines = [[l for l in out.splitlines() if l.startswith("{")] for _, out in outs]
+    assert len(lines[0]) == 1 and lines[1] == []
+    r = json.loads(lines[0][0])
+    assert r["metric"].startswith("impressions/sec/node") and r["n_gpus"] == 2 and r["steps"] == 2
+    assert r["config"]["global_batch"] == 8 and r["config"]["parallelism"] == "dp2"
+    assert abs(r["value"] - 8 * 2 / (r["ms_per_step"] * 2 / 1000)) / r["value"] < 0.01
+    assert r["scaling"] == "weak" and r["higher_is_better"] is True

@@ -117,3 +117,20 @@ def test_unfrozen_backbone_grads_match_cpu(dev):
     before = m_gpu.text_encoder.DistillBert.compute_weights(torch.bfloat16)["w1"] if False else None
     e_gpu.optimizer_step()
     assert m_gpu.text_encoder.DistillBert._pack is None
+
+
+def test_learns_planted_signal_on_gpu(dev):
+    """Quality: through the full 6-layer frozen random-init DistilBERT, three local epochs on the
+    planted-topic synthetic shard lifts validation AUC well above chance (plain-CE scorer,
+    lr 1e-4: profiles/quality_r1_*_lr1e-4.jsonl reach 0.78 on mind-small in 3 epochs)."""
+    cfg = FedRecConfig(mode="grad_avg", batch_size=64, lr=1e-4, score_act="identity")
+    torch.manual_seed(0)
+    m = FedRecModel(cfg).to(dev)
+    m.build_flat()
+    shard = make_client_shards("small", 1)[0]
+    eng = LocalEngine(cfg, m, shard, dev)
+    auc0 = eng.validate(limit=1024)["valid_auc"]
+    for _ in range(3):
+        eng.train_epoch()
+    auc1 = eng.validate(limit=1024)["valid_auc"]
+    assert auc1 > 0.6 and auc1 > auc0 + 0.05, (auc0, auc1)
