@@ -159,6 +159,24 @@ def main() -> int:
         elapsed = float(t.item())
     loss = float(torch.stack(losses).float().mean())
 
+    # untimed: the data-plane share of a step -- the same flat-bucket RCCL all-reduce the GA
+    # step issues, alone, averaged over 20 calls (bus bandwidth = 2 (W-1)/W x bytes / time)
+    comm_ms = busbw = None
+    if ctx.initialized and world > 1 and dev.type == "cuda" and args.config in (2, 4):
+        g = torch.zeros_like(model.flat.grad)
+        for _ in range(3):
+            dist.all_reduce(g, group=ctx.data_group)
+        sync()
+        dist.barrier(group=ctx.ctrl_group)
+        t1 = time.perf_counter()
+        for _ in range(20):
+            dist.all_reduce(g, group=ctx.data_group)
+        sync()
+        ct = torch.tensor([(time.perf_counter() - t1) / 20], dtype=torch.float64)
+        dist.all_reduce(ct, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
+        comm_ms = 1000.0 * float(ct.item())
+        busbw = 2.0 * (world - 1) / world * g.numel() * g.element_size() / (comm_ms / 1000.0) / 1e9
+
     auc = None
     if not args.no_valid:
         m = eng.validate(batch_size=256, limit=args.valid_limit)
@@ -195,6 +213,8 @@ def main() -> int:
                 "baseline_config": args.config,
             },
             "train_loss": round(loss, 5),
+            "grad_allreduce_ms": None if comm_ms is None else round(comm_ms, 4),
+            "grad_allreduce_busbw_GBps": None if busbw is None else round(busbw, 2),
             "valid_auc": None if auc is None else round(auc, 4),
         }
         print(json.dumps(out), flush=True)

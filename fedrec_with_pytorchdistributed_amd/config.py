@@ -144,7 +144,6 @@ class FedRecConfig:
     news_cache: str = "none"  # none | vectors  (HBM-resident per-epoch news table, §7.1)
     device_sampler: bool = True  # GPU: negative sampling + batch assembly by the HIP sampler
     device: str = "auto"  # auto | cpu | cuda
-    allreduce: str = "rccl"  # rccl | xgmi (custom one-shot all-reduce)
     seed: int = 0
 
     # --- io / observability ------------------------------------------------------------
