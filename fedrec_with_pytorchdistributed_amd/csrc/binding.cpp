@@ -52,6 +52,16 @@ int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr
 int fr_secagg_mask(const float* x, int* out, long n, float scale, float clipv, const unsigned long long* seeds,
                    const int* signs, int npeers, unsigned long long round, hipStream_t s);
 int fr_secagg_unmask(const int* x, float* out, long n, float inv_scale, hipStream_t s);
+int fr_title_plan(const int* mask, int n, int T, int* rowmap, int* src, int* kv_start, int* kv_len, int* n_kv,
+                  hipStream_t s);
+int fr_title_attention_packed_bf16(const void* qkv, const int* rowmap, const int* kv_start, const int* kv_len, void* out,
+                                   int n_titles, int T, int H, int D, hipStream_t s);
+int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* bias, void* C, int M, int N, int K, int c_rows,
+                          const int* full_rows, int n_partial, hipStream_t s);
+int fr_embed_ln_rows_bf16(const int* tokens, const int* src, const void* word, const void* pos, const float* w,
+                          const float* b, void* y, int rows, int D, int T, float eps, hipStream_t s);
+int fr_layer_norm_scatter_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
+                               const void* res, const int* dst, hipStream_t s);
 }
 
 namespace {
@@ -422,6 +432,115 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
   return out;
 }
 
+// ---- packed title rows (frozen backbone forward; title_attn.hip) ----------------------------
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> title_plan(const at::Tensor& mask) {
+  check_dev(mask, "mask");
+  const c10::DeviceGuard g(mask.device());
+  auto mk = mask.to(at::kInt).contiguous();
+  TORCH_CHECK(mk.dim() == 2, "fedrec::title_plan: mask [n, T]");
+  const int64_t n = mk.size(0), T = mk.size(1);
+  TORCH_CHECK(T >= 1 && T <= 64, "fedrec::title_plan: T in [1, 64]");
+  auto io = mk.options();
+  auto rowmap = at::empty({n, T}, io), src = at::empty({n * T}, io);
+  auto kv_start = at::empty({n}, io), kv_len = at::empty({n}, io), n_kv = at::zeros({1}, io);
+  check_rc(fr_title_plan(mk.data_ptr<int>(), (int)n, (int)T, rowmap.data_ptr<int>(), src.data_ptr<int>(),
+                         kv_start.data_ptr<int>(), kv_len.data_ptr<int>(), n_kv.data_ptr<int>(), cur_stream()),
+           "title_plan");
+  return {rowmap, src, kv_start, kv_len, n_kv};
+}
+
+at::Tensor embed_ln_rows(const at::Tensor& tokens, const at::Tensor& src, const at::Tensor& word, const at::Tensor& pos,
+                         const at::Tensor& w, const at::Tensor& b, double eps) {
+  check_dev(word, "word");
+  check_dev(pos, "pos");
+  check_dev(src, "src");
+  TORCH_CHECK(word.scalar_type() == at::kBFloat16 && pos.scalar_type() == at::kBFloat16, "fedrec::embed_ln_rows: bf16");
+  const c10::DeviceGuard g(word.device());
+  auto tok = tokens.to(at::kInt).contiguous();
+  TORCH_CHECK(tok.dim() == 2 && src.scalar_type() == at::kInt && src.numel() == tok.numel(),
+              "fedrec::embed_ln_rows: tokens [n, T], src [n*T] int32");
+  const int64_t n = tok.size(0), T = tok.size(1), D = word.size(1);
+  TORCH_CHECK(T <= pos.size(0) && D % 256 == 0, "fedrec::embed_ln_rows: T <= max positions, D % 256 == 0");
+  auto wf = w.to(at::kFloat).contiguous(), bf = b.to(at::kFloat).contiguous();
+  auto y = at::empty({n * T, D}, word.options());
+  check_rc(fr_embed_ln_rows_bf16(tok.data_ptr<int>(), src.data_ptr<int>(), word.data_ptr(), pos.data_ptr(),
+                                 wf.data_ptr<float>(), bf.data_ptr<float>(), y.data_ptr(), (int)(n * T), (int)D, (int)T,
+                                 (float)eps, cur_stream()),
+           "embed_ln_rows");
+  return y;
+}
+
+at::Tensor linear_split(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                        const at::Tensor& full_rows, int64_t n_partial) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  check_dev(full_rows, "full_rows");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "fedrec::linear_split: bf16 x/w");
+  TORCH_CHECK(full_rows.scalar_type() == at::kInt && full_rows.numel() == 1, "fedrec::linear_split: full_rows int32[1]");
+  const c10::DeviceGuard g(x.device());
+  const int64_t K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && n_partial > 0 && n_partial <= N, "fedrec::linear_split: shapes");
+  const int64_t M = x.numel() / K;
+  const int64_t c_rows = (M + 255) / 256 * 256;
+  auto out = at::empty({c_rows * N}, x.options()).narrow(0, 0, M * N).view({M, N});
+  const float* bp = nullptr;
+  at::Tensor bf;
+  if (b.has_value() && b->defined()) {
+    bf = b->to(at::kFloat).contiguous();
+    TORCH_CHECK(bf.numel() == N, "fedrec::linear_split: bias size");
+    bp = bf.data_ptr<float>();
+  }
+  if (M == 0) return out;
+  check_rc(fr_gemm_nt_bf16_split(x.data_ptr(), w.data_ptr(), bp, out.data_ptr(), (int)M, (int)N, (int)K, (int)c_rows,
+                                 full_rows.data_ptr<int>(), (int)n_partial, cur_stream()),
+           "linear_split");
+  return out;
+}
+
+at::Tensor title_attention_packed(const at::Tensor& qkv, const at::Tensor& rowmap, const at::Tensor& kv_start,
+                                  const at::Tensor& kv_len, int64_t n_heads) {
+  check_dev(qkv, "qkv");
+  check_dev(rowmap, "rowmap");
+  check_dev(kv_start, "kv_start");
+  check_dev(kv_len, "kv_len");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16, "fedrec::title_attention_packed: bf16");
+  TORCH_CHECK(rowmap.dim() == 2 && rowmap.scalar_type() == at::kInt, "fedrec::title_attention_packed: rowmap [n, T]");
+  const c10::DeviceGuard g(qkv.device());
+  const int64_t n = rowmap.size(0), T = rowmap.size(1), D = qkv.size(-1) / 3;
+  TORCH_CHECK(qkv.numel() == n * T * 3 * D && kv_start.numel() == n && kv_len.numel() == n,
+              "fedrec::title_attention_packed: shapes");
+  auto out = at::empty({n * T, D}, qkv.options());
+  check_rc(fr_title_attention_packed_bf16(qkv.data_ptr(), rowmap.data_ptr<int>(), kv_start.data_ptr<int>(),
+                                          kv_len.data_ptr<int>(), out.data_ptr(), (int)n, (int)T, (int)n_heads, (int)D,
+                                          cur_stream()),
+           "title_attention_packed");
+  return out;
+}
+
+at::Tensor layer_norm_scatter(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps,
+                              const c10::optional<at::Tensor>& residual, const at::Tensor& dst) {
+  check_dev(x, "x");
+  check_dev(dst, "dst");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::layer_norm_scatter: bf16");
+  const c10::DeviceGuard g(x.device());
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(dst.scalar_type() == at::kInt && dst.numel() == rows && D % 256 == 0,
+              "fedrec::layer_norm_scatter: dst int32[rows], D % 256 == 0");
+  auto wf = w.to(at::kFloat).contiguous(), bf = b.to(at::kFloat).contiguous();
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    check_dev(*residual, "residual");
+    TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->numel() == x.numel(),
+                "fedrec::layer_norm_scatter: residual must match x (bf16)");
+    rp = residual->data_ptr();
+  }
+  auto y = at::empty_like(x);
+  check_rc(fr_layer_norm_scatter_bf16(x.data_ptr(), wf.data_ptr<float>(), bf.data_ptr<float>(), y.data_ptr(), (int)rows,
+                                      (int)D, (float)eps, rp, dst.data_ptr<int>(), cur_stream()),
+           "layer_norm_scatter");
+  return y;
+}
+
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
@@ -450,6 +569,11 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset) -> (Tensor, Tensor)");
   m.def("secagg_mask(Tensor x, Tensor seeds, Tensor signs, float scale, float clipv, int round) -> (Tensor)");
   m.def("secagg_unmask(Tensor x, float inv_scale) -> Tensor");
+  m.def("title_plan(Tensor mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("embed_ln_rows(Tensor tokens, Tensor src, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
+  m.def("linear_split(Tensor x, Tensor w, Tensor? b, Tensor full_rows, int n_partial) -> Tensor");
+  m.def("title_attention_packed(Tensor qkv, Tensor rowmap, Tensor kv_start, Tensor kv_len, int n_heads) -> Tensor");
+  m.def("layer_norm_scatter(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual, Tensor dst) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
@@ -471,4 +595,9 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("sample_batch", &sample_batch);
   m.impl("secagg_mask", &secagg_mask);
   m.impl("secagg_unmask", &secagg_unmask);
+  m.impl("title_plan", &title_plan);
+  m.impl("embed_ln_rows", &embed_ln_rows);
+  m.impl("linear_split", &linear_split);
+  m.impl("title_attention_packed", &title_attention_packed);
+  m.impl("layer_norm_scatter", &layer_norm_scatter);
 }

@@ -832,13 +832,39 @@ template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DEFER = false>
 __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                              const float* __restrict__ bias,
                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
-                                                             int N, int K, int tiles_n, int ntiles) {
+                                                             int N, int K, int tiles_n, int ntiles,
+                                                             const int* __restrict__ full_rows = nullptr,
+                                                             int tiles_np = 0) {
   // ONE __shared__ object (staging halves + the bias vector): a second one makes hipcc drain
   // vmcnt(0) before every fragment read (cdna_hip_programming.md §5 "Three .s-level traps")
   __shared__ __attribute__((aligned(16))) char smem[8 * PP_HALF + (HAS_BIAS ? PP2_MAXN * 4 : 0)];
   float* bias_s = (float*)(smem + 8 * PP_HALF);
   const int G = gridDim.x, b = blockIdx.x;
   const int c = (G % 8 == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
+  // row-split tile list (packed title rows, fr_gemm_nt_bf16_split): row tiles below
+  // *full_rows (a device count: no host sync) take all tiles_n column tiles, the rest only
+  // the first tiles_np (the Q columns); without full_rows the map is the plain one
+  int full_t = ntiles;
+  if (full_rows != nullptr) {
+    const int tiles_m = (M + 255) >> 8;
+    int fm = (*full_rows + 255) >> 8;
+    fm = fm < tiles_m ? fm : tiles_m;
+    full_t = fm * tiles_n;
+    ntiles = full_t + (tiles_m - fm) * tiles_np;
+  }
+  auto tile_mn = [&](int t, int& m0_, int& n0_) {
+    int mt_, nt_;
+    if (t < full_t) {
+      mt_ = t / tiles_n;
+      nt_ = t - mt_ * tiles_n;
+    } else {
+      const int u = t - full_t, q = u / tiles_np;
+      mt_ = full_t / tiles_n + q;
+      nt_ = u - q * tiles_np;
+    }
+    m0_ = mt_ * 256;
+    n0_ = nt_ * 256;
+  };
   if (c >= ntiles) return;
   const int nk = K >> 6;
   const int S = ((ntiles - c + G - 1) / G) * nk;
@@ -853,8 +879,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
   auto tile_offs = [&](int itile, int (&o)[4][2]) {
     int t = itile * G + c;
     t = t < ntiles ? t : c;
-    const int mt = t / tiles_n;
-    const int m0 = mt * 256, n0 = (t - mt * tiles_n) * 256;
+    int m0, n0;
+    tile_mn(t, m0, n0);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int rho = wave * 16 + i * 8 + rsub;
@@ -992,10 +1018,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     after_epi = false;
     PP_MFMA(1, 0, b0)
     if (DEFER && ++kt == nk) {
-      const int t = it * G + c;
-      const int mt = t / tiles_n;
-      pm0 = mt * 256;
-      pn0 = (t - mt * tiles_n) * 256;
+      tile_mn(it * G + c, pm0, pn0);
       if (g + 1 < S) {
         pend = true;
       } else {
@@ -1009,9 +1032,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
         for (int i = 0; i < 2; ++i) ocur[h][i] = onxt[h][i];
       tile_offs(it + 1, onxt);
     } else if (!DEFER && ++kt == nk) {
-      const int t = it * G + c;
-      const int mt = t / tiles_n;
-      const int m0 = mt * 256, n0 = (t - mt * tiles_n) * 256;
+      int m0, n0;
+      tile_mn(it * G + c, m0, n0);
       const int nb0 = n0 + wc * 64 + fq * 4;
       f32x4 bb[2][2];
       if constexpr (HAS_BIAS) {
@@ -1229,5 +1251,39 @@ extern "C" int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, 
     case 2: launch_act<2>(a, w, bias, r, c, M, N, K, c_rows, s); break;
     default: return 2;
   }
+  return 0;
+}
+
+// Row-split GEMM for the packed title layout: rows [0, *full_rows) get all N columns, the
+// remaining rows only the first n_partial (the Q third of the fused QKV weight: padding
+// tokens are never read as keys or values).  full_rows stays on the device (the count comes
+// from the row-plan kernel of the same step), so no host synchronisation.  Shapes outside
+// the ping-pong kernel's domain fall back to the full product (same values in the columns
+// that are read).
+extern "C" int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,
+                                     int c_rows, const int* full_rows, int n_partial, hipStream_t s) {
+  if (N % BN != 0 || K % BK != 0 || M <= 0) return 1;
+  const bool ok = (g_gemm_variant == 9 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 && N <= PP2_MAXN &&
+                  K >= 128 && n_partial % BN2 == 0 && n_partial > 0 && n_partial <= N &&
+                  c_rows >= ((M + 255) / 256) * 256 && (long long)M * K < (1ll << 31) &&
+                  (long long)N * K < (1ll << 31);
+  if (!ok) return fr_gemm_nt_bf16(A, W, bias, nullptr, C, M, N, K, 0, c_rows, s);
+  const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles_max = tiles_m * tiles_n;
+  if (g_num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  const int G = ntiles_max < g_num_cus ? ntiles_max : g_num_cus;
+  const bf16* a = (const bf16*)A;
+  const bf16* w = (const bf16*)W;
+  bf16* c = (bf16*)C;
+  if (bias)
+    hipLaunchKernelGGL((gemm_nt_pp2_kernel<0, true, false>), dim3(G), dim3(512), 0, s, a, w, bias, nullptr, c, M, N, K,
+                       tiles_n, ntiles_max, full_rows, n_partial / BN2);
+  else
+    hipLaunchKernelGGL((gemm_nt_pp2_kernel<0, false, false>), dim3(G), dim3(512), 0, s, a, w, bias, nullptr, c, M, N, K,
+                       tiles_n, ntiles_max, full_rows, n_partial / BN2);
   return 0;
 }

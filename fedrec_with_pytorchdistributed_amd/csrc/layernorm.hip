@@ -92,7 +92,9 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
                                                    const bf16* __restrict__ word, const bf16* __restrict__ pos,
                                                    const float* __restrict__ w, const float* __restrict__ b,
                                                    bf16* __restrict__ y, int rows, int T, float eps,
-                                                   const bf16* __restrict__ res) {
+                                                   const bf16* __restrict__ res, const int* __restrict__ ridx) {
+  // ridx (packed title rows): EMBED -> row r embeds flat token ridx[r] (token id and position
+  // from it); otherwise -> row r is stored to output row ridx[r] (back to title order)
   constexpr int D = 256 * NC;
   const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -105,8 +107,9 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
     const bf16* s0;
     const bf16* s1 = nullptr;
     if constexpr (EMBED) {
-      s0 = word + (size_t)tokens[row] * D;
-      s1 = pos + (size_t)(row % T) * D;
+      const int sr = ridx != nullptr ? ridx[row] : row;
+      s0 = word + (size_t)tokens[sr] * D;
+      s1 = pos + (size_t)(sr % T) * D;
     } else {
       s0 = x + (size_t)row * D;
       if (res != nullptr) s1 = res + (size_t)row * D;  // LN(x + residual)
@@ -147,6 +150,7 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
     for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
     const float rstd = rsqrtf(sq * (1.0f / D) + eps);
     if (row < rows) {
+      const int orow = (!EMBED && ridx != nullptr) ? ridx[row] : row;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int i = c * 256 + hl * 8;
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
         bf16x8 o;
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = f2bf((v[q][c][k] - mean) * rstd * ww[k] + bb[k]);
-        *(bf16x8*)(y + (size_t)row * D + i) = o;
+        *(bf16x8*)(y + (size_t)orow * D + i) = o;
       }
     }
   }
@@ -165,18 +169,19 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
 
 template <bool EMBED>
 bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* pos, const float* w, const float* b,
-                 bf16* y, int rows, int D, int T, float eps, hipStream_t s, const bf16* res = nullptr) {
+                 bf16* y, int rows, int D, int T, float eps, hipStream_t s, const bf16* res = nullptr,
+                 const int* ridx = nullptr) {
   constexpr int RPH = 2;                // rows per half-wave -> 4 per wave, 16 per 256-thread block
   constexpr int RPB = 8 * RPH;
   const int blocks = (rows + RPB - 1) / RPB;
   if (D == 768)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 3, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 3, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res, ridx);
   else if (D == 512)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 2, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 2, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res, ridx);
   else if (D == 1024)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 4, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 4, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res, ridx);
   else if (D == 256)
-    hipLaunchKernelGGL((ln16_kernel<EMBED, 1, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res);
+    hipLaunchKernelGGL((ln16_kernel<EMBED, 1, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res, ridx);
   else
     return false;
   return true;
@@ -361,4 +366,21 @@ extern "C" int fr_embed_ln_bf16(const int* tokens, const void* word, const void*
   hipLaunchKernelGGL((ln_kernel<true>), dim3((rows + 3) / 4), dim3(256), 0, s, nullptr, tokens, (const bf16*)word,
                      (const bf16*)pos, w, b, (bf16*)y, rows, D, T, eps, nullptr);
   return 0;
+}
+
+// Packed-row variants (title_attn.hip, title_plan_kernel): embedding of row r = flat token
+// src[r] of tokens [n*T]; LayerNorm storing row r to output row dst[r].  D % 256 == 0 only.
+extern "C" int fr_embed_ln_rows_bf16(const int* tokens, const int* src, const void* word, const void* pos,
+                                     const float* w, const float* b, void* y, int rows, int D, int T, float eps,
+                                     hipStream_t s) {
+  if (rows == 0) return 0;
+  return launch_ln16<true>(nullptr, tokens, (const bf16*)word, (const bf16*)pos, w, b, (bf16*)y, rows, D, T, eps, s,
+                           nullptr, src) ? 0 : 1;
+}
+
+extern "C" int fr_layer_norm_scatter_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D,
+                                          float eps, const void* res, const int* dst, hipStream_t s) {
+  if (rows == 0) return 0;
+  return launch_ln16<false>((const bf16*)x, nullptr, nullptr, nullptr, w, b, (bf16*)y, rows, D, 1, eps, s,
+                            (const bf16*)res, dst) ? 0 : 1;
 }

@@ -343,6 +343,264 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Packed-row layout (frozen backbone forward).  The n*T token rows of a batch are reordered
+// so that every row the attention reads as a key/value ("kv rows": mask 1, or every row of an
+// all-masked title) comes first, title-major and in position order, followed by the
+// query-only rows (mask 0).  Only the kv rows need K and V, so the fused QKV GEMM computes
+// all 3*D columns for them and only the Q columns for the rest (~2/3 of MIND title tokens
+// are padding).  Attention has no positional term, so permuting its keys changes nothing;
+// positions enter through the embedding, which reads each row's source index.
+//
+// title_plan_kernel (one 1024-thread block): kv count per title, exclusive scan ->
+// kv_start, then rowmap[i*T + t] (packed row of token t of title i) and its inverse src.
+// kv_len[i] < 0 marks an all-masked title (HF: uniform attention over all T keys).
+__global__ __launch_bounds__(1024) void title_plan_kernel(const int* __restrict__ mask, int n, int T,
+                                                          int* __restrict__ rowmap, int* __restrict__ src,
+                                                          int* __restrict__ kv_start, int* __restrict__ kv_len,
+                                                          int* __restrict__ n_kv) {
+  __shared__ int wsum[16];
+  __shared__ int carry_s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry_s = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + tid;
+    int cnt = 0;
+    if (i < n) {
+      for (int t = 0; t < T; ++t) cnt += mask[(size_t)i * T + t] != 0;
+      kv_len[i] = cnt == 0 ? -T : cnt;
+      if (cnt == 0) cnt = T;
+    }
+    int x = cnt;  // inclusive scan within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+      int w = lane < 16 ? wsum[lane] : 0;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const int y = __shfl_up(w, o, 64);
+        if (lane >= o) w += y;
+      }
+      if (lane < 16) wsum[lane] = w;
+    }
+    __syncthreads();
+    const int carry = carry_s;
+    if (i < n) kv_start[i] = carry + (wave ? wsum[wave - 1] : 0) + x - cnt;
+    __syncthreads();
+    if (tid == 0) carry_s = carry + wsum[15];
+    __syncthreads();
+  }
+  const int R = carry_s;
+  if (tid == 0) *n_kv = R;
+  // rows: title i's kv rows at kv_start[i].., its query-only rows at R + i*T - kv_start[i]..
+  // (the same thread wrote kv_len[i] / kv_start[i] above)
+  for (int i = tid; i < n; i += 1024) {
+    const bool allm = kv_len[i] < 0;
+    int a = kv_start[i], b = R + i * T - kv_start[i];
+    for (int t = 0; t < T; ++t) {
+      const bool kv = allm || mask[(size_t)i * T + t] != 0;
+      const int row = kv ? a++ : b++;
+      rowmap[(size_t)i * T + t] = row;
+      src[row] = i * T + t;
+    }
+  }
+}
+
+struct TPIn {
+  bf16x8 kf[2][4], qf[2][4], vv[8];
+  int qrow[4];
+  int kstart, klen;  // klen < 0: all-masked title, uniform over -klen keys
+};
+
+__device__ __forceinline__ void tp_load_kq(TPIn& in, const bf16* __restrict__ qkv, const int* __restrict__ rowmap,
+                                           const int* __restrict__ kv_start, const int* __restrict__ kv_len,
+                                           int pair, int T, int H, int D, int lane) {
+  const int title = pair / H, h = pair - title * H;
+  const int ld = 3 * D;
+  const int fr = lane & 15, fq = lane >> 4;
+  in.kstart = kv_start[title];
+  in.klen = kv_len[title];
+  const int nk = in.klen < 0 ? -in.klen : in.klen;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = i * 16 + fr;
+    in.qrow[i] = rowmap[(size_t)title * T + (t < T ? t : T - 1)];
+  }
+  const bf16* qb = qkv + h * DH;
+  const bf16* kb = qkv + D + h * DH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int sk = i * 16 + fr;
+    const size_t krow = (size_t)in.kstart + (sk < nk ? sk : nk - 1);
+#pragma unroll
+    for (int kd = 0; kd < 2; ++kd) {
+      if (i * 16 < nk) in.kf[kd][i] = *(const bf16x8*)(kb + krow * ld + kd * 32 + fq * 8);
+      in.qf[kd][i] = *(const bf16x8*)(qb + (size_t)in.qrow[i] * ld + kd * 32 + fq * 8);
+    }
+  }
+}
+
+__device__ __forceinline__ void tp_load_v(TPIn& in, const bf16* __restrict__ qkv, int pair, int H, int D, int lane) {
+  const int h = pair % H;
+  const int ld = 3 * D;
+  const int nk = in.klen < 0 ? -in.klen : in.klen;
+  const bf16* vb = qkv + 2 * D + h * DH;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int idx = c * 64 + lane;
+    const int r = idx >> 3;
+    in.vv[c] = r < nk ? *(const bf16x8*)(vb + ((size_t)in.kstart + r) * ld + (idx & 7) * 8)
+                      : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+// Persistent 2-deep prefetching form (as title_attn_pkernel) over the packed rows; key tiles
+// of 16 beyond the title's kv count are skipped (a MIND title has ~16 real tokens: 1 of the
+// 4 key tiles, 1 of the 2 P.V k-steps).
+__global__ __launch_bounds__(256, 1) void title_attn_packed_kernel(const bf16* __restrict__ qkv,
+                                                                   const int* __restrict__ rowmap,
+                                                                   const int* __restrict__ kv_start,
+                                                                   const int* __restrict__ kv_len,
+                                                                   bf16* __restrict__ out, int n_pairs, int T, int H,
+                                                                   int D) {
+  __shared__ __attribute__((aligned(16))) bf16 vs[4][64 * DH];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int stride = gridDim.x * 4;
+  int pair = blockIdx.x * 4 + wave;
+  if (pair >= n_pairs) return;
+  bf16* myv = vs[wave];
+  const int fr = lane & 15, fq = lane >> 4;
+  const int qq = fr >> 2, pp = fr & 3;
+  auto step = [&](TPIn& in, int pair) {
+    const int h = pair % H;
+    const int klen = in.klen, nk = klen < 0 ? -klen : klen;
+    const bool allm = klen < 0;
+    const int nks = (nk + 15) >> 4;  // 16-key tiles in use (wave-uniform)
+    int qrow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qrow[i] = in.qrow[i];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int idx = c * 64 + lane;
+      *(bf16x8*)(myv + (idx >> 3) * DH + (idx & 7) * 8) = in.vv[c];
+    }
+    f32x4 st[4][4];
+#pragma unroll
+    for (int is = 0; is < 4; ++is)
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq) st[is][jq] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kd = 0; kd < 2; ++kd)
+#pragma unroll
+      for (int is = 0; is < 4; ++is)
+        if (is < nks) {
+#pragma unroll
+          for (int jq = 0; jq < 4; ++jq)
+            st[is][jq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(in.kf[kd][is], in.qf[kd][jq], st[is][jq], 0, 0, 0);
+        }
+    const int next = pair + 2 * stride;
+    if (next < n_pairs) tp_load_kq(in, qkv, rowmap, kv_start, kv_len, next, T, H, D, lane);
+
+    const float scale = 0.125f;
+    bf16x8 pf[4][2];
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int is = 0; is < 4; ++is)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int sidx = is * 16 + fq * 4 + r;
+          const float a = sidx < nk ? (allm ? -3.4028234663852886e38f : 0.f) : -INFINITY;
+          const float sc = (a == 0.f) ? st[is][jq][r] * scale : a;
+          st[is][jq][r] = sc;
+          m = fmaxf(m, sc);
+        }
+      m = group4_max(m);
+      float l = 0.f;
+#pragma unroll
+      for (int is = 0; is < 4; ++is)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(st[is][jq][r] - m);
+          st[is][jq][r] = e;
+          l += e;
+        }
+      const float inv = 1.0f / group4_sum(l);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f[r] = f2bf(st[2 * ks][jq][r] * inv);
+          f[4 + r] = f2bf(st[2 * ks + 1][jq][r] * inv);
+        }
+        pf[jq][ks] = f;
+      }
+    }
+    if (next < n_pairs) tp_load_v(in, qkv, next, H, D, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V image is in LDS
+    __builtin_amdgcn_wave_barrier();
+    f32x4 o[4][4];
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq)
+#pragma unroll
+      for (int jd = 0; jd < 4; ++jd) o[jq][jd] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      if (ks * 32 < nk) {
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) {
+          const bf16* a0 = myv + (ks * 32 + fq * 4 + qq) * DH + jd * 16 + pp * 4;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0 + 16 * DH));
+          bf16x4 lob = __builtin_bit_cast(bf16x4, lo), hib = __builtin_bit_cast(bf16x4, hi);
+          bf16x8 vf = {lob[0], lob[1], lob[2], lob[3], hib[0], hib[1], hib[2], hib[3]};
+#pragma unroll
+          for (int jq = 0; jq < 4; ++jq)
+            o[jq][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[jq][ks], o[jq][jd], 0, 0, 0);
+        }
+      }
+    bf16* ob = out + h * DH;
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) {
+      const int t = jq * 16 + fr;
+      if (t < T) {
+#pragma unroll
+        for (int jd = 0; jd < 4; ++jd) {
+          const bf16x4 v = {f2bf(o[jq][jd][0]), f2bf(o[jq][jd][1]), f2bf(o[jq][jd][2]), f2bf(o[jq][jd][3])};
+          *(bf16x4*)(ob + (size_t)qrow[jq] * D + jd * 16 + fq * 4) = v;
+        }
+      }
+    }
+  };
+  TPIn in0, in1;
+  tp_load_kq(in0, qkv, rowmap, kv_start, kv_len, pair, T, H, D, lane);
+  tp_load_v(in0, qkv, pair, H, D, lane);
+  if (pair + stride < n_pairs) {
+    tp_load_kq(in1, qkv, rowmap, kv_start, kv_len, pair + stride, T, H, D, lane);
+    tp_load_v(in1, qkv, pair + stride, H, D, lane);
+  }
+  while (true) {
+    step(in0, pair);
+    pair += stride;
+    if (pair >= n_pairs) break;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    step(in1, pair);
+    pair += stride;
+    if (pair >= n_pairs) break;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 int g_ta_waves = -2;  // default: persistent, 2-deep prefetch, 1 wave per SIMD (kernel_bench.py)
 int g_ta_cus = 0;
 
@@ -383,5 +641,34 @@ extern "C" int fr_title_attention_bf16(const void* qkv, const int* mask, void* o
   else
     hipLaunchKernelGGL(title_attn_kernel<2>, dim3((pairs + 1) / 2), dim3(128), 0, s, (const bf16*)qkv, mask, (bf16*)out,
                        n_titles, T, H, D);
+  return 0;
+}
+
+extern "C" int fr_title_plan(const int* mask, int n, int T, int* rowmap, int* src, int* kv_start, int* kv_len, int* n_kv,
+                             hipStream_t s) {
+  if (T < 1 || T > 64 || n < 0) return 1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(title_plan_kernel, dim3(1), dim3(1024), 0, s, mask, n, T, rowmap, src, kv_start, kv_len, n_kv);
+  return 0;
+}
+
+// qkv: [n*T, 3*D] in packed row order (K/V columns valid on kv rows only); out: [n*T, D]
+// in packed row order.
+extern "C" int fr_title_attention_packed_bf16(const void* qkv, const int* rowmap, const int* kv_start, const int* kv_len,
+                                              void* out, int n_titles, int T, int H, int D, hipStream_t s) {
+  if (T < 1 || T > 64 || D != H * DH) return 1;
+  const int pairs = n_titles * H;
+  if (pairs == 0) return 0;
+  if (g_ta_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_ta_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_ta_cus <= 0) g_ta_cus = 256;
+  }
+  int blocks = g_ta_cus;
+  const int need = (pairs + 3) / 4;
+  blocks = blocks < need ? blocks : need;
+  hipLaunchKernelGGL(title_attn_packed_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, rowmap, kv_start, kv_len,
+                     (bf16*)out, pairs, T, H, D);
   return 0;
 }

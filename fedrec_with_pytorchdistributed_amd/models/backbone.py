@@ -22,6 +22,7 @@ no pretrained weights offline.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -145,6 +146,9 @@ class Backbone(nn.Module):
         """``tokens, mask [n, T]`` -> last hidden state ``[n*T, D]`` in ``dtype`` (eval mode)."""
         c = self.cfg
         P = self.compute_weights(dtype)
+        if (tokens.is_cuda and dtype == torch.bfloat16 and c.dim % 256 == 0 and c.n_layers > 0
+                and tokens.shape[1] <= 64 and os.environ.get("FEDREC_TITLE_PACK", "1") != "0"):
+            return self._forward_packed(tokens, mask, P)
         x = ops.embed_ln(tokens, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps, dtype)
         for L in P["layers"]:
             qkv = ops.linear(x, L["wqkv"], L["bqkv"], out_dtype=dtype)
@@ -156,6 +160,30 @@ class Backbone(nn.Module):
             f = ops.linear(x, L["w1"], L["b1"], act="gelu", out_dtype=dtype)
             h = ops.linear(f, L["w2"], L["b2"], out_dtype=dtype)
             x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, dtype, residual=x)
+        return x
+
+    def _forward_packed(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict) -> torch.Tensor:
+        """The same forward over the packed row order of ``ops.title_plan``: the rows read as
+        keys/values (real tokens) come first, so the fused QKV GEMM skips the K and V columns
+        of every padding row (~2/3 of MIND title rows) and the attention skips key tiles past
+        each title's length.  All other ops are row-wise; the last LayerNorm stores rows back
+        in title order, so the output is identical in layout (and, up to fp32 summation
+        order, in value) to the unpacked path."""
+        c = self.cfg
+        rowmap, src, kv_start, kv_len, n_kv = ops.title_plan(mask)
+        x = ops.embed_ln_rows(tokens, src, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps)
+        last = len(P["layers"]) - 1
+        for li, L in enumerate(P["layers"]):
+            qkv = ops.linear_split(x, L["wqkv"], L["bqkv"], n_kv, c.dim)
+            ctx = ops.title_attention_packed(qkv, rowmap, kv_start, kv_len, c.n_heads)
+            h = ops.linear(ctx, L["wo"], L["bo"])
+            x = ops.layer_norm(h, L["ln1_w"], L["ln1_b"], c.ln_eps, residual=x)
+            f = ops.linear(x, L["w1"], L["b1"], act="gelu")
+            h = ops.linear(f, L["w2"], L["b2"])
+            if li == last:
+                x = ops.layer_norm_scatter(h, L["ln2_w"], L["ln2_b"], c.ln_eps, x, src)
+            else:
+                x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, residual=x)
         return x
 
     def forward_train(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

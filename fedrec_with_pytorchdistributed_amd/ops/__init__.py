@@ -15,6 +15,7 @@ linear                q/k/v/out/lin1/lin2, heads   gemm_bf16.hip: MFMA 16x16x32 
                       (K02, K05, K06, K07)         bias / GELU / tanh / residual epilogues
 layer_norm            sa/output LN (K04)           layernorm.hip: one wave per row
 title_attention       HF attention (K03)           title_attn.hip: MFMA QK^T / PV, T pad 64
+title_plan + *_packed frozen-backbone forward      title_attn.hip: pad tokens get Q only (no K/V)
 additive_pool_*       attention.py:14-26 (K06/12)  additive_pool.hip: score, eps-softmax, pool
 user_attention_*      attention.py:32-82 (K11)     user_attn.hip: 20 heads x d_k 20
 score_ce              model.py:121-126 (K13)       score_ce.hip: sigmoid-CE fwd+bwd fused
@@ -67,6 +68,35 @@ def title_attention(qkv, mask, n_heads: int):
     if _dev(qkv) and qkv.dtype == torch.bfloat16:
         return native.require_for(qkv).title_attention(qkv, mask.contiguous(), int(n_heads))
     return ref.title_attention(qkv, mask, n_heads).to(qkv.dtype)
+
+
+# ---- packed title rows (frozen backbone forward, csrc/title_attn.hip) -----------------------
+def title_plan(mask):
+    """``mask [n, T]`` -> ``(rowmap [n,T], src [n*T], kv_start [n], kv_len [n], n_kv [1])`` int32:
+    the packed row order (key/value rows first, then query-only rows) and its inverse."""
+    if _dev(mask):
+        return tuple(native.require_for(mask).title_plan(mask.contiguous()))
+    return ref.title_plan(mask)
+
+
+def embed_ln_rows(tokens, src, word, pos, ln_w, ln_b, eps: float):
+    """Embedding + LN of packed row r = flat token ``src[r]`` of ``tokens [n, T]``."""
+    return native.require_for(word).embed_ln_rows(tokens.contiguous(), src, word, pos, ln_w, ln_b, float(eps))
+
+
+def linear_split(x, w, b, full_rows, n_partial: int):
+    """``x @ w^T + b`` with rows ``>= full_rows[0]`` computed on the first ``n_partial``
+    output columns only (the rest of those rows is left unwritten)."""
+    return native.require_for(x).linear_split(x.contiguous(), w, b, full_rows, int(n_partial))
+
+
+def title_attention_packed(qkv, rowmap, kv_start, kv_len, n_heads: int):
+    return native.require_for(qkv).title_attention_packed(qkv, rowmap, kv_start, kv_len, int(n_heads))
+
+
+def layer_norm_scatter(x, w, b, eps: float, residual, dst):
+    """``LN(x + residual)`` with row r stored at output row ``dst[r]``."""
+    return native.require_for(x).layer_norm_scatter(x, w, b, float(eps), residual, dst)
 
 
 def additive_pool_fwd(x, e, w2, b2) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -224,3 +224,25 @@ def adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor
     bc2 = 1 - b2 ** step
     denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
     p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+def title_plan(mask: torch.Tensor):
+    """Oracle of ``title_plan_kernel``: kv rows (mask 1, or every row of an all-masked title)
+    first, title-major in position order, then the query-only rows; ``kv_len < 0`` marks an
+    all-masked title."""
+    m = mask.to(torch.int64) != 0
+    n, T = m.shape
+    allm = ~m.any(1)
+    kv = m | allm[:, None]
+    cnt = kv.sum(1)
+    kv_start = torch.cumsum(cnt, 0) - cnt
+    R = int(cnt.sum())
+    rank_kv = torch.cumsum(kv.long(), 1) - kv.long()
+    rank_q = torch.cumsum((~kv).long(), 1) - (~kv).long()
+    q_start = R + torch.arange(n) * T - kv_start
+    rowmap = torch.where(kv, kv_start[:, None] + rank_kv, q_start[:, None] + rank_q)
+    src = torch.empty(n * T, dtype=torch.int64)
+    src[rowmap.reshape(-1)] = torch.arange(n * T)
+    kv_len = torch.where(allm, -T * torch.ones_like(cnt), cnt)
+    i32 = torch.int32
+    return (rowmap.to(i32), src.to(i32), kv_start.to(i32), kv_len.to(i32), torch.tensor([R], dtype=i32))

@@ -379,3 +379,40 @@ def test_checkpoint_roundtrip_reference_layout(tmp_path):
     # a reference-written snapshot (two keys only) resumes at EPOCHS_RUN + 1 (Q14 fix)
     torch.save({"MODEL_STATE": m.state_dict(), "EPOCHS_RUN": 2}, tmp_path / "ref.pt")
     assert ck.load_snapshot(str(tmp_path / "ref.pt"), m2)["next_epoch"] == 3
+
+
+def test_title_plan_oracle_semantics():
+    """Packed title rows (frozen-backbone forward): the plan is a permutation whose first
+    n_kv rows are exactly the key/value rows, and attention computed from the packed layout
+    -- keys = each title's kv rows only -- equals HF-semantics attention on the plain layout."""
+    from fedrec_with_pytorchdistributed_amd.ops import reference as R
+
+    g = torch.Generator().manual_seed(0)
+    n, T, H, D = 23, 11, 2, 128
+    m = (torch.rand(n, T, generator=g) < 0.5).to(torch.int32)
+    m[3] = 0  # all masked
+    rowmap, src, kv_start, kv_len, n_kv = R.title_plan(m)
+    assert sorted(src.tolist()) == list(range(n * T))
+    assert torch.equal(src[rowmap.reshape(-1).long()], torch.arange(n * T, dtype=torch.int32))
+    kv = (m != 0) | ~(m != 0).any(1, keepdim=True)
+    assert int(n_kv) == int(kv.sum())
+    assert bool((rowmap.reshape(-1)[kv.reshape(-1)] < int(n_kv)).all())
+    assert int(kv_len[3]) == -T and bool((kv_len[torch.arange(n) != 3] == kv.sum(1)[torch.arange(n) != 3]).all())
+    qkv = torch.randn(n * T, 3 * D, generator=g, dtype=torch.float64)
+    want = R.title_attention(qkv, m, H)
+    packed = qkv[src.long()]
+    out = torch.empty(n * T, D, dtype=torch.float64)
+    dh = D // H
+    for i in range(n):
+        nk, ks = abs(int(kv_len[i])), int(kv_start[i])
+        qrows = rowmap[i].long()
+        for h in range(H):
+            q = packed[qrows, h * dh:(h + 1) * dh]
+            k = packed[ks:ks + nk, D + h * dh:D + (h + 1) * dh]
+            v = packed[ks:ks + nk, 2 * D + h * dh:2 * D + (h + 1) * dh]
+            s = q @ k.t() / dh ** 0.5
+            if int(kv_len[i]) < 0:
+                s = torch.zeros_like(s)  # HF: finfo.min on every key -> uniform
+            out[qrows, h * dh:(h + 1) * dh] = torch.softmax(s, -1) @ v
+    got = out[rowmap.reshape(-1).long()]  # back to title-major rows
+    assert torch.allclose(got, want, atol=1e-10)
