@@ -63,6 +63,28 @@ def main():
             ms = timeit(lambda: lib.title_attention(qkv, mask, H))
             rec(f"title_attention[{w}w]", ms, qkv.numel() * 2 + M * D * 2, 4.0 * n * H * T * T * 64)
         lib.title_attn_set_waves(-2)
+    if want("packed"):
+        # MIND-like title lengths ([CLS] + ~14 words + [SEP], synthetic generator's distribution)
+        plens = (torch.randn(n, generator=g) * 5 + 16).round().clamp(5, 38).long()
+        pmask = (torch.arange(T)[None, :] < plens[:, None]).to(torch.int32).to(dev)
+        ms = timeit(lambda: lib.title_plan(pmask))
+        rec("title_plan", ms, pmask.numel() * 4 * 3)
+        rowmap, src, kv_start, kv_len, qstart, n_kv = lib.title_plan(pmask)
+        R = int(n_kv.item())
+        ms = timeit(lambda: lib.title_attention_packed(qkv, rowmap, kv_start, kv_len, qstart, H))
+        rec("title_attention_packed", ms, M * D * 2 + R * 2 * D * 2 + M * D * 2,
+            4.0 * H * 64 * float((plens * T).sum()))
+        for w in (-2,):
+            lib.title_attn_set_waves(w)
+            ms = timeit(lambda: lib.title_attention(qkv, pmask, H))
+            rec("title_attention_unpacked_same_lengths", ms, qkv.numel() * 2 + M * D * 2, 4.0 * n * H * T * T * 64)
+        xin = (torch.randn(M, D, generator=g) * 0.5).to(dev, torch.bfloat16)
+        wq = (torch.randn(3 * D, D, generator=g) * 0.03).to(dev, torch.bfloat16)
+        bq = torch.randn(3 * D, device=dev)
+        ms = timeit(lambda: lib.linear_split(xin, wq, bq, n_kv, D))
+        rec("qkv_linear_split", ms, 0, 2.0 * D * (R * 3 * D + (M - R) * D))
+        ms = timeit(lambda: lib.linear(xin, wq, bq, 0, None))
+        rec("qkv_linear_full", ms, 0, 2.0 * M * D * 3 * D)
     if want("title_attention_bwd"):
         dout = (torch.randn(M, D, generator=g) * 0.1).to(dev, torch.bfloat16)
         ms = timeit(lambda: lib.title_attention_bwd(qkv, dout, mask, H))

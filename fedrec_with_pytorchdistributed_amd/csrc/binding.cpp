@@ -52,10 +52,10 @@ int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr
 int fr_secagg_mask(const float* x, int* out, long n, float scale, float clipv, const unsigned long long* seeds,
                    const int* signs, int npeers, unsigned long long round, hipStream_t s);
 int fr_secagg_unmask(const int* x, float* out, long n, float inv_scale, hipStream_t s);
-int fr_title_plan(const int* mask, int n, int T, int* rowmap, int* src, int* kv_start, int* kv_len, int* n_kv,
-                  hipStream_t s);
-int fr_title_attention_packed_bf16(const void* qkv, const int* rowmap, const int* kv_start, const int* kv_len, void* out,
-                                   int n_titles, int T, int H, int D, hipStream_t s);
+int fr_title_plan(const int* mask, int n, int T, int* rowmap, int* src, int* kv_start, int* kv_len, int* qstart,
+                  int* n_kv, hipStream_t s);
+int fr_title_attention_packed_bf16(const void* qkv, const int* rowmap, const int* kv_start, const int* kv_len,
+                                   const int* qstart, void* out, int n_titles, int T, int H, int D, hipStream_t s);
 int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* bias, void* C, int M, int N, int K, int c_rows,
                           const int* full_rows, int n_partial, hipStream_t s);
 int fr_embed_ln_rows_bf16(const int* tokens, const int* src, const void* word, const void* pos, const float* w,
@@ -433,7 +433,7 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
 }
 
 // ---- packed title rows (frozen backbone forward; title_attn.hip) ----------------------------
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> title_plan(const at::Tensor& mask) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> title_plan(const at::Tensor& mask) {
   check_dev(mask, "mask");
   const c10::DeviceGuard g(mask.device());
   auto mk = mask.to(at::kInt).contiguous();
@@ -442,11 +442,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> title_pla
   TORCH_CHECK(T >= 1 && T <= 64, "fedrec::title_plan: T in [1, 64]");
   auto io = mk.options();
   auto rowmap = at::empty({n, T}, io), src = at::empty({n * T}, io);
-  auto kv_start = at::empty({n}, io), kv_len = at::empty({n}, io), n_kv = at::zeros({1}, io);
+  auto kv_start = at::empty({n}, io), kv_len = at::empty({n}, io), qstart = at::empty({n}, io);
+  auto n_kv = at::zeros({1}, io);
   check_rc(fr_title_plan(mk.data_ptr<int>(), (int)n, (int)T, rowmap.data_ptr<int>(), src.data_ptr<int>(),
-                         kv_start.data_ptr<int>(), kv_len.data_ptr<int>(), n_kv.data_ptr<int>(), cur_stream()),
+                         kv_start.data_ptr<int>(), kv_len.data_ptr<int>(), qstart.data_ptr<int>(), n_kv.data_ptr<int>(),
+                         cur_stream()),
            "title_plan");
-  return {rowmap, src, kv_start, kv_len, n_kv};
+  return {rowmap, src, kv_start, kv_len, qstart, n_kv};
 }
 
 at::Tensor embed_ln_rows(const at::Tensor& tokens, const at::Tensor& src, const at::Tensor& word, const at::Tensor& pos,
@@ -498,7 +500,7 @@ at::Tensor linear_split(const at::Tensor& x, const at::Tensor& w, const c10::opt
 }
 
 at::Tensor title_attention_packed(const at::Tensor& qkv, const at::Tensor& rowmap, const at::Tensor& kv_start,
-                                  const at::Tensor& kv_len, int64_t n_heads) {
+                                  const at::Tensor& kv_len, const at::Tensor& qstart, int64_t n_heads) {
   check_dev(qkv, "qkv");
   check_dev(rowmap, "rowmap");
   check_dev(kv_start, "kv_start");
@@ -507,11 +509,13 @@ at::Tensor title_attention_packed(const at::Tensor& qkv, const at::Tensor& rowma
   TORCH_CHECK(rowmap.dim() == 2 && rowmap.scalar_type() == at::kInt, "fedrec::title_attention_packed: rowmap [n, T]");
   const c10::DeviceGuard g(qkv.device());
   const int64_t n = rowmap.size(0), T = rowmap.size(1), D = qkv.size(-1) / 3;
-  TORCH_CHECK(qkv.numel() == n * T * 3 * D && kv_start.numel() == n && kv_len.numel() == n,
+  check_dev(qstart, "qstart");
+  TORCH_CHECK(qkv.numel() == n * T * 3 * D && kv_start.numel() == n && kv_len.numel() == n && qstart.numel() == n,
               "fedrec::title_attention_packed: shapes");
   auto out = at::empty({n * T, D}, qkv.options());
   check_rc(fr_title_attention_packed_bf16(qkv.data_ptr(), rowmap.data_ptr<int>(), kv_start.data_ptr<int>(),
-                                          kv_len.data_ptr<int>(), out.data_ptr(), (int)n, (int)T, (int)n_heads, (int)D,
+                                          kv_len.data_ptr<int>(), qstart.data_ptr<int>(), out.data_ptr(), (int)n, (int)T,
+                                          (int)n_heads, (int)D,
                                           cur_stream()),
            "title_attention_packed");
   return out;
@@ -569,10 +573,10 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset) -> (Tensor, Tensor)");
   m.def("secagg_mask(Tensor x, Tensor seeds, Tensor signs, float scale, float clipv, int round) -> (Tensor)");
   m.def("secagg_unmask(Tensor x, float inv_scale) -> Tensor");
-  m.def("title_plan(Tensor mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("title_plan(Tensor mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("embed_ln_rows(Tensor tokens, Tensor src, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("linear_split(Tensor x, Tensor w, Tensor? b, Tensor full_rows, int n_partial) -> Tensor");
-  m.def("title_attention_packed(Tensor qkv, Tensor rowmap, Tensor kv_start, Tensor kv_len, int n_heads) -> Tensor");
+  m.def("title_attention_packed(Tensor qkv, Tensor rowmap, Tensor kv_start, Tensor kv_len, Tensor qstart, int n_heads) -> Tensor");
   m.def("layer_norm_scatter(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual, Tensor dst) -> Tensor");
 }
 

@@ -87,3 +87,24 @@ static __device__ __forceinline__ float2 box_muller(uint32_t a, uint32_t b) {
   __sincosf(6.283185307179586f * u2, &s, &c);
   return make_float2(r * c, r * s);
 }
+
+// 16-byte stores of a 16x16x32 accumulator pair: lane (fr, fq) holds 4 consecutive columns
+// [4fq, +4) of two 16-column groups v0 (cols 0..15) and v1 (cols 16..31) of one row; one
+// permlane16 swap between lanes l and l^16 (same row) regroups them so every lane stores 8
+// consecutive bf16 (half the store instructions of 8-byte stores; MI355X_MICROARCH.md
+// "attention epilogue store tail").  Every lane must execute the swaps; `store` masks only
+// the write.
+static __device__ __forceinline__ void store_pair16_if(bf16* __restrict__ crow, const float (&v0)[4],
+                                                       const float (&v1)[4], int fq, bool store) {
+  const bf16x4 o0 = {f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3])};
+  const bf16x4 o1 = {f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+  uint2 a = __builtin_bit_cast(uint2, o0), b = __builtin_bit_cast(uint2, o1);
+  auto r = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  a.x = r[0];
+  b.x = r[1];
+  r = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  a.y = r[0];
+  b.y = r[1];
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  if (store) *GLOBAL_PTR(u32x4_t, crow + (fq & 1) * 16 + (fq >> 1) * 8) = u32x4_t{a.x, a.y, b.x, b.y};
+}

@@ -214,7 +214,10 @@ template <int OCC, int DEPTH>
 __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __restrict__ qkv, const int* __restrict__ mask,
                                                           bf16* __restrict__ out, int n_pairs, int T, int H, int D) {
   __shared__ __attribute__((aligned(16))) bf16 vs[4][64 * DH];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index via readfirstlane: the compiler then knows pair / next are wave-uniform, so the
+  // prefetch guards are scalar branches (a "divergent" guard around loads makes it drain
+  // vmcnt(0) at the loop head and the 2-deep prefetch stops overlapping anything)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int stride = gridDim.x * 4;
   int pair = blockIdx.x * 4 + wave;
   if (pair >= n_pairs) return;
@@ -310,12 +313,11 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
 #pragma unroll
     for (int jq = 0; jq < 4; ++jq) {
       const int t = jq * 16 + fr;
-      if (t < T) {
 #pragma unroll
-        for (int jd = 0; jd < 4; ++jd) {
-          const bf16x4 v = {f2bf(o[jq][jd][0]), f2bf(o[jq][jd][1]), f2bf(o[jq][jd][2]), f2bf(o[jq][jd][3])};
-          *(bf16x4*)(ob + (size_t)t * D + jd * 16 + fq * 4) = v;
-        }
+      for (int p2 = 0; p2 < 2; ++p2) {
+        const float v0[4] = {o[jq][2 * p2][0], o[jq][2 * p2][1], o[jq][2 * p2][2], o[jq][2 * p2][3]};
+        const float v1[4] = {o[jq][2 * p2 + 1][0], o[jq][2 * p2 + 1][1], o[jq][2 * p2 + 1][2], o[jq][2 * p2 + 1][3]};
+        store_pair16_if(ob + (size_t)(t < T ? t : 0) * D + p2 * 32, v0, v1, fq, t < T);
       }
     }
   };
@@ -352,63 +354,70 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
 // are padding).  Attention has no positional term, so permuting its keys changes nothing;
 // positions enter through the embedding, which reads each row's source index.
 //
-// title_plan_kernel (one 1024-thread block): kv count per title, exclusive scan ->
-// kv_start, then rowmap[i*T + t] (packed row of token t of title i) and its inverse src.
-// kv_len[i] < 0 marks an all-masked title (HF: uniform attention over all T keys).
-__global__ __launch_bounds__(1024) void title_plan_kernel(const int* __restrict__ mask, int n, int T,
-                                                          int* __restrict__ rowmap, int* __restrict__ src,
-                                                          int* __restrict__ kv_start, int* __restrict__ kv_len,
-                                                          int* __restrict__ n_kv) {
-  __shared__ int wsum[16];
-  __shared__ int carry_s;
+// title_count_kernel: one wave per title, kv_len[i] = popcount of its mask (-T if all
+// masked).  title_rows_kernel: 16 titles per block; the block first reduces kv counts over
+// all titles (its prefix and the total R; n ints from L2, no separate scan pass), then each
+// wave assigns its title's rows from ballot ranks: rowmap[i*T + t] (packed row of token t
+// of title i), its inverse src, and kv_start[i].  kv_len[i] < 0 marks an all-masked title
+// (HF: uniform attention over all T keys); qstart[i] = the title's first query-only row.
+__global__ __launch_bounds__(256) void title_count_kernel(const int* __restrict__ mask, int n, int T,
+                                                          int* __restrict__ kv_len) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const unsigned long long b = __ballot(lane < T && mask[(size_t)i * T + (lane < T ? lane : 0)] != 0);
+  const int c = __popcll(b);
+  if (lane == 0) kv_len[i] = c == 0 ? -T : c;
+}
+
+__global__ __launch_bounds__(1024) void title_rows_kernel(const int* __restrict__ mask, int n, int T,
+                                                          const int* __restrict__ kv_len, int* __restrict__ rowmap,
+                                                          int* __restrict__ src, int* __restrict__ kv_start,
+                                                          int* __restrict__ qstart, int* __restrict__ n_kv) {
+  __shared__ int red[3][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) carry_s = 0;
-  __syncthreads();
-  for (int base = 0; base < n; base += 1024) {
-    const int i = base + tid;
-    int cnt = 0;
-    if (i < n) {
-      for (int t = 0; t < T; ++t) cnt += mask[(size_t)i * T + t] != 0;
-      kv_len[i] = cnt == 0 ? -T : cnt;
-      if (cnt == 0) cnt = T;
-    }
-    int x = cnt;  // inclusive scan within the wave
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    if (wave == 0) {
-      int w = lane < 16 ? wsum[lane] : 0;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const int y = __shfl_up(w, o, 64);
-        if (lane >= o) w += y;
-      }
-      if (lane < 16) wsum[lane] = w;
-    }
-    __syncthreads();
-    const int carry = carry_s;
-    if (i < n) kv_start[i] = carry + (wave ? wsum[wave - 1] : 0) + x - cnt;
-    __syncthreads();
-    if (tid == 0) carry_s = carry + wsum[15];
-    __syncthreads();
+  const int i0 = blockIdx.x * 16;
+  int pre = 0, tot = 0;
+  for (int j = tid; j < n; j += 1024) {
+    const int c = abs(kv_len[j]);
+    tot += c;
+    pre += j < i0 ? c : 0;
   }
-  const int R = carry_s;
-  if (tid == 0) *n_kv = R;
-  // rows: title i's kv rows at kv_start[i].., its query-only rows at R + i*T - kv_start[i]..
-  // (the same thread wrote kv_len[i] / kv_start[i] above)
-  for (int i = tid; i < n; i += 1024) {
-    const bool allm = kv_len[i] < 0;
-    int a = kv_start[i], b = R + i * T - kv_start[i];
-    for (int t = 0; t < T; ++t) {
-      const bool kv = allm || mask[(size_t)i * T + t] != 0;
-      const int row = kv ? a++ : b++;
-      rowmap[(size_t)i * T + t] = row;
-      src[row] = i * T + t;
-    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pre += __shfl_xor(pre, o, 64);
+    tot += __shfl_xor(tot, o, 64);
+  }
+  const int i = i0 + wave;
+  const int kl = i < n ? kv_len[i] : 0;
+  if (lane == 0) {
+    red[0][wave] = pre;
+    red[1][wave] = tot;
+    red[2][wave] = abs(kl);  // this block's titles, for the in-block prefix
+  }
+  __syncthreads();
+  pre = 0;
+  tot = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    pre += red[0][w] + (w < wave ? red[2][w] : 0);
+    tot += red[1][w];
+  }
+  if (blockIdx.x == 0 && tid == 0) *n_kv = tot;
+  if (i >= n) return;
+  const bool in = lane < T;
+  const bool kv = in && (kl < 0 || mask[(size_t)i * T + (in ? lane : 0)] != 0);
+  const unsigned long long b = __ballot(kv);
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int rk = __popcll(b & below);
+  const int row = kv ? pre + rk : tot + i * T - pre + (lane - rk);
+  if (in) {
+    rowmap[(size_t)i * T + lane] = row;
+    src[row] = i * T + lane;
+  }
+  if (lane == 0) {
+    kv_start[i] = pre;
+    qstart[i] = tot + i * T - pre;
   }
 }
 
@@ -420,17 +429,24 @@ struct TPIn {
 
 __device__ __forceinline__ void tp_load_kq(TPIn& in, const bf16* __restrict__ qkv, const int* __restrict__ rowmap,
                                            const int* __restrict__ kv_start, const int* __restrict__ kv_len,
-                                           int pair, int T, int H, int D, int lane) {
+                                           const int* __restrict__ qstart, int pair, int T, int H, int D, int lane) {
   const int title = pair / H, h = pair - title * H;
   const int ld = 3 * D;
   const int fr = lane & 15, fq = lane >> 4;
   in.kstart = kv_start[title];
   in.klen = kv_len[title];
+  const int qs = qstart[title];
   const int nk = in.klen < 0 ? -in.klen : in.klen;
+  // the title's T rows are its kv rows [kstart, +nk) and its query-only rows [qs, +T-nk); the
+  // j-th query is the j-th of those rows (attention is order-free over queries too: each
+  // output goes to its own packed row), so no rowmap load precedes the Q loads.  Every load
+  // is unconditional (rows clamped): a load under a lane predicate makes the compiler drain
+  // vmcnt(0) at the loop head and the prefetch pipeline stalls.
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int t = i * 16 + fr;
-    in.qrow[i] = rowmap[(size_t)title * T + (t < T ? t : T - 1)];
+    int t = i * 16 + fr;
+    t = t < T ? t : T - 1;
+    in.qrow[i] = t < nk ? in.kstart + t : qs + (t - nk);
   }
   const bf16* qb = qkv + h * DH;
   const bf16* kb = qkv + D + h * DH;
@@ -440,7 +456,7 @@ __device__ __forceinline__ void tp_load_kq(TPIn& in, const bf16* __restrict__ qk
     const size_t krow = (size_t)in.kstart + (sk < nk ? sk : nk - 1);
 #pragma unroll
     for (int kd = 0; kd < 2; ++kd) {
-      if (i * 16 < nk) in.kf[kd][i] = *(const bf16x8*)(kb + krow * ld + kd * 32 + fq * 8);
+      in.kf[kd][i] = *(const bf16x8*)(kb + krow * ld + kd * 32 + fq * 8);
       in.qf[kd][i] = *(const bf16x8*)(qb + (size_t)in.qrow[i] * ld + kd * 32 + fq * 8);
     }
   }
@@ -455,8 +471,7 @@ __device__ __forceinline__ void tp_load_v(TPIn& in, const bf16* __restrict__ qkv
   for (int c = 0; c < 8; ++c) {
     const int idx = c * 64 + lane;
     const int r = idx >> 3;
-    in.vv[c] = r < nk ? *(const bf16x8*)(vb + ((size_t)in.kstart + r) * ld + (idx & 7) * 8)
-                      : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    in.vv[c] = *(const bf16x8*)(vb + ((size_t)in.kstart + (r < nk ? r : nk - 1)) * ld + (idx & 7) * 8);
   }
 }
 
@@ -467,10 +482,14 @@ __global__ __launch_bounds__(256, 1) void title_attn_packed_kernel(const bf16* _
                                                                    const int* __restrict__ rowmap,
                                                                    const int* __restrict__ kv_start,
                                                                    const int* __restrict__ kv_len,
+                                                                   const int* __restrict__ qstart,
                                                                    bf16* __restrict__ out, int n_pairs, int T, int H,
                                                                    int D) {
   __shared__ __attribute__((aligned(16))) bf16 vs[4][64 * DH];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index via readfirstlane: the compiler then knows pair / next are wave-uniform, so the
+  // prefetch guards are scalar branches (a "divergent" guard around loads makes it drain
+  // vmcnt(0) at the loop head and the 2-deep prefetch stops overlapping anything)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int stride = gridDim.x * 4;
   int pair = blockIdx.x * 4 + wave;
   if (pair >= n_pairs) return;
@@ -486,9 +505,9 @@ __global__ __launch_bounds__(256, 1) void title_attn_packed_kernel(const bf16* _
 #pragma unroll
     for (int i = 0; i < 4; ++i) qrow[i] = in.qrow[i];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < 8; ++c) {  // V rows past the title's keys are zero (P is 0 there, 0 * x may be NaN)
       const int idx = c * 64 + lane;
-      *(bf16x8*)(myv + (idx >> 3) * DH + (idx & 7) * 8) = in.vv[c];
+      *(bf16x8*)(myv + (idx >> 3) * DH + (idx & 7) * 8) = (idx >> 3) < nk ? in.vv[c] : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
     f32x4 st[4][4];
 #pragma unroll
@@ -504,8 +523,10 @@ __global__ __launch_bounds__(256, 1) void title_attn_packed_kernel(const bf16* _
           for (int jq = 0; jq < 4; ++jq)
             st[is][jq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(in.kf[kd][is], in.qf[kd][jq], st[is][jq], 0, 0, 0);
         }
-    const int next = pair + 2 * stride;
-    if (next < n_pairs) tp_load_kq(in, qkv, rowmap, kv_start, kv_len, next, T, H, D, lane);
+    // prefetch 2 strides ahead, unconditionally (clamped to the last pair: a conditional load
+    // leaves the waitcnt pass a path with fewer loads in flight and it drains to vmcnt(0))
+    const int next = min(pair + 2 * stride, n_pairs - 1);
+    tp_load_kq(in, qkv, rowmap, kv_start, kv_len, qstart, next, T, H, D, lane);
 
     const float scale = 0.125f;
     bf16x8 pf[4][2];
@@ -544,7 +565,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_packed_kernel(const bf16* _
         pf[jq][ks] = f;
       }
     }
-    if (next < n_pairs) tp_load_v(in, qkv, next, H, D, lane);
+    tp_load_v(in, qkv, next, H, D, lane);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V image is in LDS
     __builtin_amdgcn_wave_barrier();
     f32x4 o[4][4];
@@ -570,23 +591,22 @@ __global__ __launch_bounds__(256, 1) void title_attn_packed_kernel(const bf16* _
     bf16* ob = out + h * DH;
 #pragma unroll
     for (int jq = 0; jq < 4; ++jq) {
-      const int t = jq * 16 + fr;
-      if (t < T) {
 #pragma unroll
-        for (int jd = 0; jd < 4; ++jd) {
-          const bf16x4 v = {f2bf(o[jq][jd][0]), f2bf(o[jq][jd][1]), f2bf(o[jq][jd][2]), f2bf(o[jq][jd][3])};
-          *(bf16x4*)(ob + (size_t)qrow[jq] * D + jd * 16 + fq * 4) = v;
-        }
+      for (int p2 = 0; p2 < 2; ++p2) {
+        const float v0[4] = {o[jq][2 * p2][0], o[jq][2 * p2][1], o[jq][2 * p2][2], o[jq][2 * p2][3]};
+        const float v1[4] = {o[jq][2 * p2 + 1][0], o[jq][2 * p2 + 1][1], o[jq][2 * p2 + 1][2], o[jq][2 * p2 + 1][3]};
+        // t >= T lanes hold the clamped query T-1: they store the same values to the same row,
+        // so the stores need no lane predicate (a predicated store is a divergent branch)
+        store_pair16_if(ob + (size_t)qrow[jq] * D + p2 * 32, v0, v1, fq, true);
       }
     }
   };
   TPIn in0, in1;
-  tp_load_kq(in0, qkv, rowmap, kv_start, kv_len, pair, T, H, D, lane);
+  tp_load_kq(in0, qkv, rowmap, kv_start, kv_len, qstart, pair, T, H, D, lane);
   tp_load_v(in0, qkv, pair, H, D, lane);
-  if (pair + stride < n_pairs) {
-    tp_load_kq(in1, qkv, rowmap, kv_start, kv_len, pair + stride, T, H, D, lane);
-    tp_load_v(in1, qkv, pair + stride, H, D, lane);
-  }
+  const int p1 = min(pair + stride, n_pairs - 1);
+  tp_load_kq(in1, qkv, rowmap, kv_start, kv_len, qstart, p1, T, H, D, lane);
+  tp_load_v(in1, qkv, p1, H, D, lane);
   while (true) {
     step(in0, pair);
     pair += stride;
@@ -644,18 +664,21 @@ extern "C" int fr_title_attention_bf16(const void* qkv, const int* mask, void* o
   return 0;
 }
 
-extern "C" int fr_title_plan(const int* mask, int n, int T, int* rowmap, int* src, int* kv_start, int* kv_len, int* n_kv,
-                             hipStream_t s) {
+extern "C" int fr_title_plan(const int* mask, int n, int T, int* rowmap, int* src, int* kv_start, int* kv_len,
+                             int* qstart, int* n_kv, hipStream_t s) {
   if (T < 1 || T > 64 || n < 0) return 1;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(title_plan_kernel, dim3(1), dim3(1024), 0, s, mask, n, T, rowmap, src, kv_start, kv_len, n_kv);
+  hipLaunchKernelGGL(title_count_kernel, dim3((n + 3) / 4), dim3(256), 0, s, mask, n, T, kv_len);
+  hipLaunchKernelGGL(title_rows_kernel, dim3((n + 15) / 16), dim3(1024), 0, s, mask, n, T, kv_len, rowmap, src, kv_start,
+                     qstart, n_kv);
   return 0;
 }
 
 // qkv: [n*T, 3*D] in packed row order (K/V columns valid on kv rows only); out: [n*T, D]
 // in packed row order.
 extern "C" int fr_title_attention_packed_bf16(const void* qkv, const int* rowmap, const int* kv_start, const int* kv_len,
-                                              void* out, int n_titles, int T, int H, int D, hipStream_t s) {
+                                              const int* qstart, void* out, int n_titles, int T, int H, int D,
+                                              hipStream_t s) {
   if (T < 1 || T > 64 || D != H * DH) return 1;
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
@@ -669,6 +692,6 @@ extern "C" int fr_title_attention_packed_bf16(const void* qkv, const int* rowmap
   const int need = (pairs + 3) / 4;
   blocks = blocks < need ? blocks : need;
   hipLaunchKernelGGL(title_attn_packed_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, rowmap, kv_start, kv_len,
-                     (bf16*)out, pairs, T, H, D);
+                     qstart, (bf16*)out, pairs, T, H, D);
   return 0;
 }

@@ -170,12 +170,12 @@ class Backbone(nn.Module):
         in title order, so the output is identical in layout (and, up to fp32 summation
         order, in value) to the unpacked path."""
         c = self.cfg
-        rowmap, src, kv_start, kv_len, n_kv = ops.title_plan(mask)
+        rowmap, src, kv_start, kv_len, qstart, n_kv = ops.title_plan(mask)
         x = ops.embed_ln_rows(tokens, src, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps)
         last = len(P["layers"]) - 1
         for li, L in enumerate(P["layers"]):
             qkv = ops.linear_split(x, L["wqkv"], L["bqkv"], n_kv, c.dim)
-            ctx = ops.title_attention_packed(qkv, rowmap, kv_start, kv_len, c.n_heads)
+            ctx = ops.title_attention_packed(qkv, rowmap, kv_start, kv_len, qstart, c.n_heads)
             h = ops.linear(ctx, L["wo"], L["bo"])
             x = ops.layer_norm(h, L["ln1_w"], L["ln1_b"], c.ln_eps, residual=x)
             f = ops.linear(x, L["w1"], L["b1"], act="gelu")

@@ -72,7 +72,7 @@ def title_attention(qkv, mask, n_heads: int):
 
 # ---- packed title rows (frozen backbone forward, csrc/title_attn.hip) -----------------------
 def title_plan(mask):
-    """``mask [n, T]`` -> ``(rowmap [n,T], src [n*T], kv_start [n], kv_len [n], n_kv [1])`` int32:
+    """``mask [n, T]`` -> ``(rowmap [n,T], src [n*T], kv_start [n], kv_len [n], qstart [n], n_kv [1])``:
     the packed row order (key/value rows first, then query-only rows) and its inverse."""
     if _dev(mask):
         return tuple(native.require_for(mask).title_plan(mask.contiguous()))
@@ -90,8 +90,8 @@ def linear_split(x, w, b, full_rows, n_partial: int):
     return native.require_for(x).linear_split(x.contiguous(), w, b, full_rows, int(n_partial))
 
 
-def title_attention_packed(qkv, rowmap, kv_start, kv_len, n_heads: int):
-    return native.require_for(qkv).title_attention_packed(qkv, rowmap, kv_start, kv_len, int(n_heads))
+def title_attention_packed(qkv, rowmap, kv_start, kv_len, qstart, n_heads: int):
+    return native.require_for(qkv).title_attention_packed(qkv, rowmap, kv_start, kv_len, qstart, int(n_heads))
 
 
 def layer_norm_scatter(x, w, b, eps: float, residual, dst):

@@ -227,9 +227,9 @@ def adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor
 
 
 def title_plan(mask: torch.Tensor):
-    """Oracle of ``title_plan_kernel``: kv rows (mask 1, or every row of an all-masked title)
+    """Oracle of the title_count/title_rows kernels: kv rows (mask 1, or every row of an all-masked title)
     first, title-major in position order, then the query-only rows; ``kv_len < 0`` marks an
-    all-masked title."""
+    all-masked title; ``qstart`` = each title's first query-only row."""
     m = mask.to(torch.int64) != 0
     n, T = m.shape
     allm = ~m.any(1)
@@ -244,5 +244,7 @@ def title_plan(mask: torch.Tensor):
     src = torch.empty(n * T, dtype=torch.int64)
     src[rowmap.reshape(-1)] = torch.arange(n * T)
     kv_len = torch.where(allm, -T * torch.ones_like(cnt), cnt)
+    qstart = q_start
     i32 = torch.int32
-    return (rowmap.to(i32), src.to(i32), kv_start.to(i32), kv_len.to(i32), torch.tensor([R], dtype=i32))
+    return (rowmap.to(i32), src.to(i32), kv_start.to(i32), kv_len.to(i32), qstart.to(i32),
+            torch.tensor([R], dtype=i32))

@@ -33,7 +33,7 @@ def test_title_plan_matches_oracle(dev, n, T, prefix):
     m = _mask(n, T, g, prefix)
     got = native.lib().title_plan(m.to(dev))
     want = ref.title_plan(m)
-    for a, b, name in zip(got, want, ("rowmap", "src", "kv_start", "kv_len", "n_kv")):
+    for a, b, name in zip(got, want, ("rowmap", "src", "kv_start", "kv_len", "qstart", "n_kv")):
         assert torch.equal(a.cpu(), b), name
 
 
@@ -45,12 +45,12 @@ def test_title_attention_packed(dev, n, T, prefix):
     qkv = torch.randn(n * T, 3 * D, generator=g).to(torch.bfloat16)
     want = ref.title_attention(qkv.float(), m, H)  # title-major rows
     lib = native.lib()
-    rowmap, src, kv_start, kv_len, n_kv = lib.title_plan(m.to(dev))
+    rowmap, src, kv_start, kv_len, qstart, n_kv = lib.title_plan(m.to(dev))
     srcl = src.long().cpu()
     packed = qkv[srcl].clone()
     R = int(n_kv.item())
     packed[R:, D:] = float("nan")  # K/V of query-only rows must never be read
-    out = lib.title_attention_packed(packed.to(dev), rowmap, kv_start, kv_len, H)
+    out = lib.title_attention_packed(packed.to(dev), rowmap, kv_start, kv_len, qstart, H)
     got = torch.empty_like(out.cpu())
     got[srcl] = out.cpu()
     assert torch.isfinite(got.float()).all()
@@ -82,7 +82,7 @@ def test_embed_rows_and_scatter_ln(dev):
     pos = (torch.randn(512, D, generator=g) * 0.02).to(dev, torch.bfloat16)
     w, b = torch.randn(D, generator=g).to(dev), torch.randn(D, generator=g).to(dev)
     lib = native.lib()
-    _, src, _, _, _ = lib.title_plan(m.to(dev))
+    _, src, _, _, _, _ = lib.title_plan(m.to(dev))
     e = lib.embed_ln_rows(tok.to(dev), src, word, pos, w, b, 1e-12)
     e_ref = lib.embed_ln(tok.to(dev), word, pos, w, b, 1e-12)
     assert torch.equal(e, e_ref[src.long()])

@@ -391,7 +391,7 @@ def test_title_plan_oracle_semantics():
     n, T, H, D = 23, 11, 2, 128
     m = (torch.rand(n, T, generator=g) < 0.5).to(torch.int32)
     m[3] = 0  # all masked
-    rowmap, src, kv_start, kv_len, n_kv = R.title_plan(m)
+    rowmap, src, kv_start, kv_len, qstart, n_kv = R.title_plan(m)
     assert sorted(src.tolist()) == list(range(n * T))
     assert torch.equal(src[rowmap.reshape(-1).long()], torch.arange(n * T, dtype=torch.int32))
     kv = (m != 0) | ~(m != 0).any(1, keepdim=True)
