@@ -98,8 +98,11 @@ def main():
             rec(f"layer_norm[wide={wide}]", ms, 2 * M * D * 2)
         lib.ln_set_wide(1)
         r = torch.randn(M, D, generator=g).to(dev, torch.bfloat16)
-        ms = timeit(lambda: lib.layer_norm(x, w, b, 1e-12, r))
-        rec("layer_norm+residual", ms, 3 * M * D * 2)
+        for wide in (0, 1, 2, 3):  # 1/2/3: half-wave rows, 2/1/4 rows per half-wave
+            lib.ln_set_wide(wide)
+            ms = timeit(lambda: lib.layer_norm(x, w, b, 1e-12, r))
+            rec(f"layer_norm+residual[wide={wide}]", ms, 3 * M * D * 2)
+        lib.ln_set_wide(1)
     if want("embed_ln"):
         word = (torch.randn(30522, D, generator=g) * 0.02).to(dev, torch.bfloat16)
         pos = (torch.randn(512, D, generator=g) * 0.02).to(dev, torch.bfloat16)

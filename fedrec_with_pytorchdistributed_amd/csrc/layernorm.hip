@@ -167,12 +167,10 @@ __global__ __launch_bounds__(256) void ln16_kernel(const bf16* __restrict__ x, c
   }
 }
 
-template <bool EMBED>
-bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* pos, const float* w, const float* b,
-                 bf16* y, int rows, int D, int T, float eps, hipStream_t s, const bf16* res = nullptr,
-                 const int* ridx = nullptr) {
-  constexpr int RPH = 2;                // rows per half-wave -> 4 per wave, 16 per 256-thread block
-  constexpr int RPB = 8 * RPH;
+template <bool EMBED, int RPH>
+bool launch_ln16_r(const bf16* x, const int* tok, const bf16* word, const bf16* pos, const float* w, const float* b,
+                   bf16* y, int rows, int D, int T, float eps, hipStream_t s, const bf16* res, const int* ridx) {
+  constexpr int RPB = 8 * RPH;  // 8 half-waves per 256-thread block
   const int blocks = (rows + RPB - 1) / RPB;
   if (D == 768)
     hipLaunchKernelGGL((ln16_kernel<EMBED, 3, RPH>), dim3(blocks), dim3(256), 0, s, x, tok, word, pos, w, b, y, rows, T, eps, res, ridx);
@@ -185,6 +183,20 @@ bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* po
   else
     return false;
   return true;
+}
+
+// 0: wave-per-row kernel; 1 (default) / 2 / 3: half-wave rows with 1 / 2 / 4 rows per half-wave.
+// Measured interleaved at 78850 x 768 (benchmarks/ln_ab.py): LN + residual 75 / 83 / 100 us,
+// plain LN 43 / 46.5 / 52 us -- one row per half-wave keeps the most rows in flight per CU.
+int g_ln_wide = 1;
+
+template <bool EMBED>
+bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* pos, const float* w, const float* b,
+                 bf16* y, int rows, int D, int T, float eps, hipStream_t s, const bf16* res = nullptr,
+                 const int* ridx = nullptr) {
+  if (g_ln_wide == 2) return launch_ln16_r<EMBED, 2>(x, tok, word, pos, w, b, y, rows, D, T, eps, s, res, ridx);
+  if (g_ln_wide == 3) return launch_ln16_r<EMBED, 4>(x, tok, word, pos, w, b, y, rows, D, T, eps, s, res, ridx);
+  return launch_ln16_r<EMBED, 1>(x, tok, word, pos, w, b, y, rows, D, T, eps, s, res, ridx);
 }
 
 // LayerNorm backward (unfrozen backbone): y = (x - mu) * rstd * w + b
@@ -315,8 +327,6 @@ __global__ __launch_bounds__(256) void gelu_kernel(const bf16* __restrict__ z, c
     *(bf16x4*)(out + 4 * i) = o;
   }
 }
-
-int g_ln_wide = 1;
 
 }  // namespace
 

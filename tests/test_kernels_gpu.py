@@ -52,7 +52,7 @@ def test_layer_norm(dev):
     assert rel_err(y, ref.layer_norm(x.float(), w, b, 1e-12)) < 1e-2
 
 
-@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("wide", [0, 1, 2, 3])
 @pytest.mark.parametrize("rows,D", [(1, 768), (333, 768), (77, 512), (5000, 768)])
 def test_layer_norm_forms(dev, wide, rows, D):
     x = torch.randn(rows, D, device=dev).to(torch.bfloat16) * 3 + 1
