@@ -143,6 +143,9 @@ class FedRecConfig:
     precision: str = "bf16"  # backbone compute dtype: bf16 | fp32
     news_cache: str = "none"  # none | vectors  (HBM-resident per-epoch news table, §7.1)
     device_sampler: bool = True  # GPU: negative sampling + batch assembly by the HIP sampler
+    # per-step GA: run the gradient all-reduce + Adam on a side stream, overlapped with the next
+    # step's (parameter-free) frozen-backbone forward.  auto = GPU + all-reduce + frozen backbone
+    overlap_optimizer: str = "auto"  # auto | on | off
     device: str = "auto"  # auto | cpu | cuda
     seed: int = 0
 

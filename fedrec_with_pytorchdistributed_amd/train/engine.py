@@ -69,6 +69,14 @@ class LocalEngine:
         self.news_table: Optional[torch.Tensor] = None
         self.replay_chunk = 1024
         self.last_stats: Dict[str, float] = {}
+        # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
+        # the next step samples, dedups and runs the frozen backbone, none of which reads the
+        # trainable parameters; everything that does calls sync_params() first
+        ov = cfg.overlap_optimizer
+        self.overlap = device.type == "cuda" and cfg.backbone.frozen and (
+            ov == "on" or (ov == "auto" and grad_allreduce is not None))
+        self._side = torch.cuda.Stream(device) if self.overlap else None
+        self._params_ready: Optional[torch.cuda.Event] = None
 
     # -------------------------------------------------------------------------------
     @property
@@ -91,12 +99,19 @@ class LocalEngine:
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t
 
+    def sync_params(self) -> None:
+        """Make the current stream wait for a pending overlapped optimizer step."""
+        if self._params_ready is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._params_ready)
+            self._params_ready = None
+
     def news_vectors(self, uniq: torch.Tensor, grad: bool) -> torch.Tensor:
         te = self.model.text_encoder
         if not grad and self.news_table is not None:
             return self.news_table.index_select(0, uniq.long())
         text = self.tokens.index_select(0, uniq.long())
-        hid = te.hidden(text)
+        hid = te.hidden(text)  # frozen backbone: overlaps the previous step's all-reduce + Adam
+        self.sync_params()
         if grad:
             return te.head(hid)
         with torch.no_grad():
@@ -122,6 +137,8 @@ class LocalEngine:
     def forward_backward(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
         """Loss of one batch with every trainable gradient left in ``flat.grad``."""
         self.model.train()
+        if self.cfg.news_cache == "vectors" or not self.cfg.backbone.frozen:
+            self.sync_params()
         self.flat.begin_backward()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True)
         with obs.range("user_fwd"):
@@ -135,10 +152,26 @@ class LocalEngine:
     def train_step(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
         """``per_step`` schedule: grads -> all-reduce -> Adam.  Returns the (device) loss."""
         loss = self.forward_backward(cand, his)
-        self.optimizer_step()
+        self.optimizer_step(overlap=True)
         return loss
 
-    def optimizer_step(self, extra_scale: float = 1.0) -> None:
+    def optimizer_step(self, extra_scale: float = 1.0, overlap: bool = False) -> None:
+        """All-reduce the flat gradient (if any) and take one fused Adam step.  ``overlap``
+        (per-step schedule only): enqueue both on the side stream and return at once; the
+        next reader of the parameters waits in :meth:`sync_params`."""
+        if overlap and self.overlap:
+            main = torch.cuda.current_stream(self.device)
+            self._side.wait_stream(main)  # the gradients of this step are complete
+            with torch.cuda.stream(self._side):
+                self._optimizer_step(extra_scale)
+                ev = torch.cuda.Event()
+                ev.record(self._side)
+            self._params_ready = ev
+            return
+        self.sync_params()
+        self._optimizer_step(extra_scale)
+
+    def _optimizer_step(self, extra_scale: float) -> None:
         scale = extra_scale
         if self.grad_allreduce is not None:
             with obs.range("allreduce"):
@@ -153,6 +186,7 @@ class LocalEngine:
 
     # -------------------------------------------------------------------------------
     def _begin_epoch_accumulate(self) -> None:
+        self.sync_params()
         D = self.cfg.news_dim
         self.G = torch.zeros(self.N, D, dtype=torch.float32, device=self.device)
         self.touched = torch.zeros(self.N, dtype=torch.bool, device=self.device)
@@ -162,6 +196,7 @@ class LocalEngine:
 
     @torch.no_grad()
     def encode_all(self, grad: bool = False, chunk: int = 2048) -> torch.Tensor:
+        self.sync_params()
         self.model.eval()
         out = torch.empty(self.N, self.cfg.news_dim, dtype=torch.float32, device=self.device)
         for s in range(0, self.N, chunk):
@@ -188,6 +223,7 @@ class LocalEngine:
         """Replay the per-news gradients through the head, then one Adam step."""
         if n_steps == 0:
             return
+        self.sync_params()
         if self.q.grad_double_last_batch:
             user_scale, head_scale = 2.0, 1.0  # Q2: collect() doubles the last batch's grads
         else:
@@ -229,6 +265,7 @@ class LocalEngine:
             losses.append(loss)
             n += 1
             if step_hook is not None:
+                self.sync_params()  # hooks (parameter averaging every K steps) read the parameters
                 step_hook(n)
             if log_every and n % log_every == 0:
                 obs.log(f"[rank {self.rank}] epoch {self.epoch} step {n} loss {float(loss):.4f}")
@@ -250,6 +287,7 @@ class LocalEngine:
     @torch.no_grad()
     def validate(self, batch_size: int = 256, limit: Optional[int] = None) -> Dict[str, float]:
         """Corpus-mean AUC/MRR/nDCG over the validation impressions (fix of Q9)."""
+        self.sync_params()
         self.model.eval()
         scores_all, losses = [], []
         for cand_np, his_np in validation_batches(self.shard.valid, batch_size, self.cfg.npratio,

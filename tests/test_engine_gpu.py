@@ -134,3 +134,29 @@ def test_learns_planted_signal_on_gpu(dev):
         eng.train_epoch()
     auc1 = eng.validate(limit=1024)["valid_auc"]
     assert auc1 > 0.6 and auc1 > auc0 + 0.05, (auc0, auc1)
+
+
+def test_overlapped_optimizer_matches_serial(dev):
+    """Adam (and, with N > 1, the all-reduce) on a side stream overlapping the next step's
+    frozen-backbone forward gives the parameters of the serial schedule.  Run-to-run
+    variation of the serial schedule itself (fp32 atomics in a few backward kernels) is the
+    yardstick: a race would show up as a far larger difference."""
+    shard = make_client_shards("tiny", 1)[0]
+    out = {}
+    for mode in ("off", "on", "off2"):
+        cfg = _cfg()
+        cfg.lr = 1e-3
+        cfg.overlap_optimizer = mode[:3] if mode != "on" else "on"
+        torch.manual_seed(0)
+        m = FedRecModel(cfg).to(dev)
+        m.build_flat()
+        eng = LocalEngine(cfg, m, shard, dev)
+        assert eng.overlap == (mode == "on")
+        for c, h in list(eng.sampler.epoch(0))[:6]:
+            eng.train_step(eng.to_device(c), eng.to_device(h))
+        eng.sync_params()
+        torch.cuda.synchronize(dev)
+        out[mode] = m.flat.flat.clone()
+    base = float((out["off2"] - out["off"]).abs().max())
+    diff = float((out["on"] - out["off"]).abs().max())
+    assert diff <= max(2 * base, 1e-6) + 1e-5, (diff, base)
