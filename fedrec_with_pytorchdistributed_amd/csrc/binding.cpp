@@ -62,6 +62,9 @@ int fr_embed_ln_rows_bf16(const int* tokens, const int* src, const void* word, c
                           const float* b, void* y, int rows, int D, int T, float eps, hipStream_t s);
 int fr_layer_norm_scatter_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
                                const void* res, const int* dst, hipStream_t s);
+int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s);
+int fr_colsum_chunks();
+int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword, hipStream_t s);
 }
 
 namespace {
@@ -545,6 +548,36 @@ at::Tensor layer_norm_scatter(const at::Tensor& x, const at::Tensor& w, const at
   return y;
 }
 
+// ---- training-path reductions (train_grad.hip) ----------------------------------------------
+at::Tensor colsum(const at::Tensor& x) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::colsum: bf16");
+  const c10::DeviceGuard g(x.device());
+  const int64_t N = x.size(-1), M = x.numel() / N;
+  auto out = at::empty({N}, x.options().dtype(at::kFloat));
+  if (M == 0) return out.zero_();
+  auto partial = at::empty({(int64_t)fr_colsum_chunks() * N}, x.options().dtype(at::kFloat));
+  check_rc(fr_colsum_bf16(x.data_ptr(), (int)M, (int)N, partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream()),
+           "colsum");
+  return out;
+}
+
+at::Tensor embed_grad(const at::Tensor& dx, const at::Tensor& sorted, const at::Tensor& perm, int64_t num_rows) {
+  check_dev(dx, "dx");
+  check_dev(sorted, "sorted");
+  check_dev(perm, "perm");
+  TORCH_CHECK(dx.scalar_type() == at::kBFloat16 && dx.dim() == 2, "fedrec::embed_grad: dx bf16 [R, D]");
+  TORCH_CHECK(sorted.scalar_type() == at::kInt && perm.scalar_type() == at::kInt && sorted.numel() == dx.size(0) &&
+                  perm.numel() == dx.size(0),
+              "fedrec::embed_grad: sorted/perm int32 [R]");
+  const c10::DeviceGuard g(dx.device());
+  auto dword = at::zeros({num_rows, dx.size(1)}, dx.options().dtype(at::kFloat));
+  check_rc(fr_embed_grad_bf16(dx.data_ptr(), sorted.data_ptr<int>(), perm.data_ptr<int>(), (int)dx.size(0),
+                              (int)dx.size(1), dword.data_ptr<float>(), cur_stream()),
+           "embed_grad");
+  return dword;
+}
+
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
@@ -578,6 +611,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("linear_split(Tensor x, Tensor w, Tensor? b, Tensor full_rows, int n_partial) -> Tensor");
   m.def("title_attention_packed(Tensor qkv, Tensor rowmap, Tensor kv_start, Tensor kv_len, Tensor qstart, int n_heads) -> Tensor");
   m.def("layer_norm_scatter(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual, Tensor dst) -> Tensor");
+  m.def("colsum(Tensor x) -> Tensor");
+  m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
@@ -604,4 +639,6 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("linear_split", &linear_split);
   m.impl("title_attention_packed", &title_attention_packed);
   m.impl("layer_norm_scatter", &layer_norm_scatter);
+  m.impl("colsum", &colsum);
+  m.impl("embed_grad", &embed_grad);
 }

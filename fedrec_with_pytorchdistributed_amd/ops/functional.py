@@ -24,6 +24,10 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
     if not (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
         return _f(dy).t() @ _f(x)
     M = dy.shape[0]
+    # enough split-K chunks for ~2 output tiles per CU (the library tiles 256x256), no more:
+    # every chunk adds an [N, K] fp32 partial that the final sum reads back
+    tiles = -(-dy.shape[1] // 256) * -(-x.shape[1] // 256)
+    splits = min(splits, max(1, -(-512 // tiles)))
     S = max(1, min(splits, M // 2048))
     if S == 1:
         return torch.mm(dy.t(), x, out_dtype=torch.float32)
@@ -36,7 +40,10 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
 
 
 def bgrad(dy: torch.Tensor) -> torch.Tensor:
-    """Column sum in fp32 without materialising an fp32 copy of ``dy``."""
+    """Column sum in fp32 without materialising an fp32 copy of ``dy`` (bf16 device tensors:
+    the two-pass ``colsum`` kernel of ``train_grad.hip``)."""
+    if dy.is_cuda and dy.dtype == torch.bfloat16 and dy.shape[-1] % 8 == 0:
+        return ops.native.require_for(dy).colsum(dy.reshape(-1, dy.shape[-1]).contiguous())
     return dy.sum(0, dtype=torch.float64 if dy.dtype == torch.float64 else torch.float32)
 
 
@@ -235,9 +242,16 @@ class EmbedLNFn(torch.autograd.Function):
         x0 = (word_low.index_select(0, tokens.reshape(-1).long()).view(n, T, -1) + pos_low[:T].unsqueeze(0))
         x0 = x0.reshape(n * T, -1).contiguous()
         dx0, dw, db = ops.native.require_for(x0).layer_norm_bwd(x0, w, dy.contiguous(), float(ctx.eps))
-        dword = torch.zeros(ctx.shapes[0], dtype=torch.float32, device=dy.device)
-        dword.index_add_(0, tokens.reshape(-1).long(), dx0.float())
+        flat_tok = tokens.reshape(-1)
+        if dx0.is_cuda and dx0.dtype == torch.bfloat16 and dx0.shape[1] % 256 == 0:
+            # sort-based, deterministic, skips the pad token (most rows): no atomic hot spot
+            srt, perm = torch.sort(flat_tok.to(torch.int32), stable=True)
+            dword = ops.native.require_for(dx0).embed_grad(dx0, srt.to(torch.int32), perm.to(torch.int32),
+                                                            ctx.shapes[0][0])
+        else:
+            dword = torch.zeros(ctx.shapes[0], dtype=torch.float32, device=dy.device)
+            dword.index_add_(0, flat_tok.long(), dx0.float())
         dword[0] = 0.0  # nn.Embedding(padding_idx=0): the pad row never receives gradient
         dpos = torch.zeros(ctx.shapes[1], dtype=torch.float32, device=dy.device)
-        dpos[:T] = dx0.float().view(n, T, -1).sum(0)
+        dpos[:T] = bgrad(dx0.view(n, -1)).view(T, -1)  # per-position sum over titles
         return None, dword, dpos, dw, db, None, None, None

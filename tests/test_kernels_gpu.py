@@ -379,3 +379,26 @@ def test_gelu_fwd_bwd(dev):
     hf = torch.nn.functional.gelu(zf)
     hf.backward(dh.float())
     assert rel_err(h, hf) < 5e-3 and rel_err(dz, zf.grad) < 5e-3
+
+
+@pytest.mark.parametrize("M,N", [(78850, 768), (5000, 3072), (3, 2304), (1001, 38400)])
+def test_colsum(dev, M, N):
+    x = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    got = native.lib().colsum(x)
+    want = x.float().sum(0)
+    assert rel_err(got, want) < 1e-5
+
+
+def test_embed_grad(dev):
+    """Sort-based word-embedding gradient == index_add with the pad row zeroed."""
+    R, D, V = 20000, 768, 3000
+    tok = torch.randint(0, V, (R,), device=dev, dtype=torch.int32)
+    tok[::3] = 0  # lots of pad tokens
+    tok[:500] = 101  # a heavy [CLS]-like token
+    dx = torch.randn(R, D, device=dev).to(torch.bfloat16)
+    srt, perm = torch.sort(tok, stable=True)
+    got = native.lib().embed_grad(dx, srt.to(torch.int32), perm.to(torch.int32), V)
+    want = torch.zeros(V, D, device=dev).index_add_(0, tok.long(), dx.float())
+    want[0] = 0
+    got[0] = 0
+    assert rel_err(got, want) < 1e-5
