@@ -64,6 +64,8 @@ int fr_layer_norm_scatter_bf16(const void* x, const float* w, const float* b, vo
                                const void* res, const int* dst, hipStream_t s);
 int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s);
 int fr_colsum_chunks();
+int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* C, void* Z, int M, int N, int K,
+                         int c_rows, hipStream_t s);
 int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword, hipStream_t s);
 }
 
@@ -548,6 +550,34 @@ at::Tensor layer_norm_scatter(const at::Tensor& x, const at::Tensor& w, const at
   return y;
 }
 
+// ---- training FFN1: h = GELU(z), z = x w^T + b from one GEMM pass ------------------------------
+std::tuple<at::Tensor, at::Tensor> linear_gelu_dual(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "fedrec::linear_gelu_dual: bf16");
+  const c10::DeviceGuard g(x.device());
+  const int64_t K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "fedrec::linear_gelu_dual: K mismatch");
+  const int64_t M = x.numel() / K;
+  const int64_t c_rows = (M + 255) / 256 * 256;
+  auto h = at::empty({c_rows * N}, x.options()).narrow(0, 0, M * N).view({M, N});
+  auto z = at::empty({c_rows * N}, x.options()).narrow(0, 0, M * N).view({M, N});
+  auto bf = b.to(at::kFloat).contiguous();
+  TORCH_CHECK(bf.numel() == N, "fedrec::linear_gelu_dual: bias size");
+  if (M == 0) return {h, z};
+  const int rc = fr_gemm_nt_bf16_dual(x.data_ptr(), w.data_ptr(), bf.data_ptr<float>(), h.data_ptr(), z.data_ptr(),
+                                      (int)M, (int)N, (int)K, (int)c_rows, cur_stream());
+  if (rc == 3) {  // outside the fused kernel's domain: GEMM, then the GELU pass
+    check_rc(fr_gemm_nt_bf16(x.data_ptr(), w.data_ptr(), bf.data_ptr<float>(), nullptr, z.data_ptr(), (int)M, (int)N,
+                             (int)K, 0, (int)c_rows, cur_stream()),
+             "linear_gelu_dual");
+    check_rc(fr_gelu_bf16(z.data_ptr(), nullptr, h.data_ptr(), (long)(M * N), 0, cur_stream()), "linear_gelu_dual");
+  } else {
+    check_rc(rc, "linear_gelu_dual");
+  }
+  return {h, z};
+}
+
 // ---- training-path reductions (train_grad.hip) ----------------------------------------------
 at::Tensor colsum(const at::Tensor& x) {
   check_dev(x, "x");
@@ -612,6 +642,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attention_packed(Tensor qkv, Tensor rowmap, Tensor kv_start, Tensor kv_len, Tensor qstart, int n_heads) -> Tensor");
   m.def("layer_norm_scatter(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual, Tensor dst) -> Tensor");
   m.def("colsum(Tensor x) -> Tensor");
+  m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
 }
 
@@ -640,5 +671,6 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("title_attention_packed", &title_attention_packed);
   m.impl("layer_norm_scatter", &layer_norm_scatter);
   m.impl("colsum", &colsum);
+  m.impl("linear_gelu_dual", &linear_gelu_dual);
   m.impl("embed_grad", &embed_grad);
 }

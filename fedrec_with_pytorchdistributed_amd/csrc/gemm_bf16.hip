@@ -828,13 +828,15 @@ __device__ __forceinline__ void store_pair16(bf16* __restrict__ crow, const floa
 // first K-step -- quadrant q is stored in the load section of the phase whose MFMAs next write
 // it (4 x 16-B stores per phase), so each wave row's epilogue overlaps the other row's MFMAs
 // instead of stalling it at a barrier.
-template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DEFER = false>
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DEFER = false, bool DUAL = false>
 __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                              const float* __restrict__ bias,
                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
                                                              int N, int K, int tiles_n, int ntiles,
                                                              const int* __restrict__ full_rows = nullptr,
-                                                             int tiles_np = 0) {
+                                                             int tiles_np = 0, bf16* __restrict__ Z = nullptr) {
+  // DUAL (training FFN1): the epilogue also stores the pre-activation z = acc + bias to Z
+  // (the GELU backward needs it), so no separate activation pass reads z back
   // ONE __shared__ object (staging halves + the bias vector): a second one makes hipcc drain
   // vmcnt(0) before every fragment read (cdna_hip_programming.md §5 "Three .s-level traps")
   __shared__ __attribute__((aligned(16))) char smem[8 * PP_HALF + (HAS_BIAS ? PP2_MAXN * 4 : 0)];
@@ -1011,6 +1013,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     if (g + 2 >= S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if (DEFER && pend) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");        // 8 loads + 16 stores
     else if (DEFER && after_pend) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // + last phase's 4 stores
+    else if (!DEFER && !HAS_RES && after_epi && DUAL) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 8 + 32 stores
     else if (!DEFER && !HAS_RES && after_epi) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 + 16 stores
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     after_pend = DEFER && pend;
@@ -1069,12 +1072,16 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
           const int m = m0 + wr * 128 + q * 64 + i * 16 + fr;  // < round_up(M, 256): C is padded
 #pragma unroll
           for (int p = 0; p < 2; ++p) {
-            float v[2][4];
+            float v[2][4], zv[2][4];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
               f32x4& a4 = acc[q][i][p][j];
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[j][e] = a4[e] + bb[p][j][e];
+              if constexpr (DUAL) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) zv[j][e] = v[j][e];
+              }
               act4<ACT>(v[j][0], v[j][1], v[j][2], v[j][3]);
               if constexpr (HAS_RES) {
 #pragma unroll
@@ -1083,6 +1090,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
               a4 = f32x4{0.f, 0.f, 0.f, 0.f};
             }
             store_pair16(C + (size_t)m * N + n0 + wc * 64 + p * 32, v[0], v[1], fq);
+            if constexpr (DUAL) store_pair16(Z + (size_t)m * N + n0 + wc * 64 + p * 32, zv[0], zv[1], fq);
           }
         }
       }
@@ -1285,5 +1293,26 @@ extern "C" int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* 
   else
     hipLaunchKernelGGL((gemm_nt_pp2_kernel<0, false, false>), dim3(G), dim3(512), 0, s, a, w, bias, nullptr, c, M, N, K,
                        tiles_n, ntiles_max, full_rows, n_partial / BN2);
+  return 0;
+}
+
+// Training FFN1: C = GELU(A W^T + bias) and Z = A W^T + bias from one pass (variant-9 kernel,
+// its domain only: returns 3 otherwise and the caller runs GEMM + separate GELU).
+extern "C" int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* C, void* Z, int M, int N, int K,
+                                    int c_rows, hipStream_t s) {
+  const bool ok = (g_gemm_variant == 9 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 && N <= PP2_MAXN &&
+                  K >= 128 && K % BK == 0 && bias != nullptr && c_rows >= ((M + 255) / 256) * 256 &&
+                  (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31);
+  if (!ok) return 3;
+  const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
+  if (g_num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  const int G = ntiles < g_num_cus ? ntiles : g_num_cus;
+  hipLaunchKernelGGL((gemm_nt_pp2_kernel<1, true, false, false, true>), dim3(G), dim3(512), 0, s, (const bf16*)A,
+                     (const bf16*)W, bias, nullptr, (bf16*)C, M, N, K, tiles_n, ntiles, nullptr, 0, (bf16*)Z);
   return 0;
 }

@@ -222,8 +222,7 @@ class Backbone(nn.Module):
             ctx = OF.TitleAttentionFn.apply(qkv, mask.contiguous(), c.n_heads)
             h = OF.LinearTFn.apply(ctx, a.out_lin.weight, a.out_lin.bias, x, L["wo"])
             x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps)
-            z = OF.LinearTFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, None, L["w1"])
-            f = OF.GeluFn.apply(z)
+            f = OF.LinearGeluTFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, L["w1"])
             h = OF.LinearTFn.apply(f, blk.ffn.lin2.weight, blk.ffn.lin2.bias, x, L["w2"])
             x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
         return x

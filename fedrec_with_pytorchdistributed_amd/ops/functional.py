@@ -185,6 +185,25 @@ class LinearTFn(torch.autograd.Function):
         return dx, dw, db, (dy if ctx.has_res else None), None
 
 
+class LinearGeluTFn(torch.autograd.Function):
+    """``h = GELU(x @ wlow^T + b)`` (training FFN1).  One GEMM pass stores both ``h`` and the
+    pre-activation ``z`` the backward needs (dual-store epilogue), instead of GEMM -> z ->
+    a separate GELU pass reading z back."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wlow):
+        h, z = ops.native.require_for(x).linear_gelu_dual(x.contiguous(), wlow, b)
+        ctx.save_for_backward(x, wlow, z)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, wlow, z = ctx.saved_tensors
+        dz = ops.native.require_for(z).gelu(z, dh.contiguous())
+        dx = torch.mm(dz, wlow) if ctx.needs_input_grad[0] else None
+        return dx, wgrad(dz, x), bgrad(dz), None
+
+
 class GeluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z):

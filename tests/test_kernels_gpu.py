@@ -402,3 +402,21 @@ def test_embed_grad(dev):
     want[0] = 0
     got[0] = 0
     assert rel_err(got, want) < 1e-5
+
+
+@pytest.mark.parametrize("M", [78850, 5000, 300])
+def test_linear_gelu_dual(dev, M):
+    """Training FFN1: the dual-store GEMM gives z = x w^T + b and GELU(z) in one pass (the
+    300-row case takes the GEMM + GELU fallback)."""
+    K, N = 768, 3072
+    x = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=dev)
+    lib = native.lib()
+    h, z = lib.linear_gelu_dual(x, w, b)
+    z_ref = lib.linear(x, w, b, 0, None)
+    h_ref = lib.linear(x, w, b, 1, None)
+    assert torch.equal(z, z_ref)
+    assert rel_err(h, h_ref) < 5e-3
+    sl = slice(0, min(M, 1024))
+    assert rel_err(h[sl], torch.nn.functional.gelu(x[sl].float() @ w.float().t() + b)) < 1e-2
