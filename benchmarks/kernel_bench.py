@@ -131,6 +131,13 @@ def main():
         rec("wgrad_splitk", ms, dy.numel() * 2 + x.numel() * 2, 2.0 * M * 384 * D)
         ms = timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32))
         rec("wgrad_mm", ms, dy.numel() * 2 + x.numel() * 2, 2.0 * M * 384 * D)
+    if want("train"):  # unfrozen-backbone reductions (config 5)
+        for N in (768, 2304, 3072):
+            dyb = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+            ms = timeit(lambda: lib.colsum(dyb))
+            rec(f"colsum[N={N}]", ms, dyb.numel() * 2)
+            ms = timeit(lambda: dyb.sum(0, dtype=torch.float32))
+            rec(f"torch_sum[N={N}]", ms, dyb.numel() * 2)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)

@@ -66,7 +66,8 @@ int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipS
 int fr_colsum_chunks();
 int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* C, void* Z, int M, int N, int K,
                          int c_rows, hipStream_t s);
-int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword, hipStream_t s);
+int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword, int* scratch,
+                       hipStream_t s);
 }
 
 namespace {
@@ -602,8 +603,9 @@ at::Tensor embed_grad(const at::Tensor& dx, const at::Tensor& sorted, const at::
               "fedrec::embed_grad: sorted/perm int32 [R]");
   const c10::DeviceGuard g(dx.device());
   auto dword = at::zeros({num_rows, dx.size(1)}, dx.options().dtype(at::kFloat));
+  auto scratch = at::zeros({dx.size(0) + 1}, sorted.options());
   check_rc(fr_embed_grad_bf16(dx.data_ptr(), sorted.data_ptr<int>(), perm.data_ptr<int>(), (int)dx.size(0),
-                              (int)dx.size(1), dword.data_ptr<float>(), cur_stream()),
+                              (int)dx.size(1), dword.data_ptr<float>(), scratch.data_ptr<int>(), cur_stream()),
            "embed_grad");
   return dword;
 }

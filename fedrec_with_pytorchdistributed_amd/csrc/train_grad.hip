@@ -11,25 +11,28 @@
 
 namespace {
 
-constexpr int CS_CHUNKS = 128;
+constexpr int CS_MAX_CHUNKS = 256;
 
-// grid (ceil(N / 512), CS_CHUNKS); lane owns 8 consecutive columns, the 4 waves of a block
-// stride over the chunk's rows; partial[chunk][n]
+// grid (ceil(N / 512), chunks); lane owns 8 consecutive columns, the 4 waves of a block
+// stride over the chunk's rows (4 rows in flight per wave); partial[chunk][n].  chunks is
+// chosen so the grid has ~1024 blocks whatever N is.
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restrict__ x, int M, int N,
                                                              float* __restrict__ partial) {
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c0 = blockIdx.x * 512 + lane * 8;
-  const int rows_per = (M + CS_CHUNKS - 1) / CS_CHUNKS;
+  const int rows_per = (M + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c0 < N) {
     int r = r0 + wave;
-    for (; r + 4 < r1; r += 8) {  // two rows in flight per wave
+    for (; r + 12 < r1; r += 16) {
       const bf16x8 a = *(const bf16x8*)(x + (size_t)r * N + c0);
       const bf16x8 b = *(const bf16x8*)(x + (size_t)(r + 4) * N + c0);
+      const bf16x8 c = *(const bf16x8*)(x + (size_t)(r + 8) * N + c0);
+      const bf16x8 d = *(const bf16x8*)(x + (size_t)(r + 12) * N + c0);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += (float)a[k] + (float)b[k];
+      for (int k = 0; k < 8; ++k) acc[k] += ((float)a[k] + (float)b[k]) + ((float)c[k] + (float)d[k]);
     }
     for (; r < r1; r += 4) {
       const bf16x8 a = *(const bf16x8*)(x + (size_t)r * N + c0);
@@ -46,27 +49,46 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restr
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial, int N,
-                                                           float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
+// 64 columns per block, the 16 waves split the chunks (<= 16 loads per lane), fixed-order
+// LDS combine
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ partial, int N, int chunks,
+                                                            float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int k = 0; k < CS_CHUNKS; ++k) s += partial[(size_t)k * N + c];
-  out[c] = s;
+  if (c < N)
+    for (int k = wave; k < chunks; k += 16) s += partial[(size_t)k * N + c];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    out[c] = t;
+  }
 }
 
+constexpr int EG_HEAVY = 64;  // segments longer than this go to the block-per-segment kernel
+
 // one wave per sorted position b; only the first occurrence of each token (b == 0 or a new
-// id) works: it sums rows perm[b .. end) of dx in sorted (= occurrence) order.  D % 256 == 0.
+// id) works: it sums rows perm[b .. end) of dx in sorted (= occurrence) order.  Segments
+// longer than EG_HEAVY ([CLS], [SEP], frequent words) are appended to `heavy` instead.
 __global__ __launch_bounds__(256) void embed_grad_kernel(const bf16* __restrict__ dx, const int* __restrict__ sorted,
                                                          const int* __restrict__ perm, int R, int D,
-                                                         float* __restrict__ dword) {
+                                                         float* __restrict__ dword, int* __restrict__ heavy,
+                                                         int* __restrict__ n_heavy) {
   const int b = blockIdx.x * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= R) return;
   const int tok = sorted[b];
   if (tok == 0 || (b > 0 && sorted[b - 1] == tok)) return;
   int e = b + 1;
-  while (e < R && sorted[e] == tok) ++e;
+  while (e < R && e - b <= EG_HEAVY && sorted[e] == tok) ++e;
+  if (e - b > EG_HEAVY) {
+    if (lane == 0) heavy[atomicAdd(n_heavy, 1)] = b;
+    return;
+  }
   for (int c0 = lane * 4; c0 < D; c0 += 256) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     for (int r = b; r < e; ++r) {
@@ -80,23 +102,77 @@ __global__ __launch_bounds__(256) void embed_grad_kernel(const bf16* __restrict_
   }
 }
 
+// heavy segments: a persistent grid of 1024-thread blocks walks the heavy list; wave w of a
+// block sums rows b+w, b+w+16, ... (lanes over columns, 12 per lane for D = 768), then a
+// fixed-order combine of the 16 wave partials through LDS.  D <= 768.
+__global__ __launch_bounds__(1024) void embed_grad_heavy_kernel(const bf16* __restrict__ dx,
+                                                                const int* __restrict__ sorted,
+                                                                const int* __restrict__ perm, int R, int D,
+                                                                float* __restrict__ dword,
+                                                                const int* __restrict__ heavy,
+                                                                const int* __restrict__ n_heavy) {
+  __shared__ float part[16][768];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nh = *n_heavy;
+  const int nc = D / 256;  // column groups of 4 per lane
+  for (int h = blockIdx.x; h < nh; h += gridDim.x) {
+    const int b = heavy[h];
+    const int tok = sorted[b];
+    int e = b + 1;
+    while (e < R && sorted[e] == tok) ++e;
+    float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int r = b + wave; r < e; r += 16) {
+      const bf16* row = dx + (size_t)perm[r] * D;
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        if (j < nc) {
+          const bf16x4 v = *(const bf16x4*)(row + j * 256 + lane * 4);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[j][k] += (float)v[k];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j < nc) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) part[wave][j * 256 + lane * 4 + k] = acc[j][k];
+      }
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 1024) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) sum += part[w][c];
+      dword[(size_t)tok * D + c] = sum;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
-// partial: CS_CHUNKS * N floats of scratch
+// partial: fr_colsum_chunks() * N floats of scratch
 extern "C" int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s) {
   if (N % 8 != 0 || M <= 0) return 1;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 511) / 512, CS_CHUNKS), dim3(256), 0, s, (const bf16*)x, M, N,
-                     partial);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, partial, N, out);
+  const int cb = (N + 511) / 512;
+  int chunks = 1024 / cb;
+  chunks = chunks < 16 ? 16 : (chunks > CS_MAX_CHUNKS ? CS_MAX_CHUNKS : chunks);
+  chunks = chunks < M ? chunks : M;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cb, chunks), dim3(256), 0, s, (const bf16*)x, M, N, partial);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, partial, N, chunks, out);
   return 0;
 }
 
-extern "C" int fr_colsum_chunks() { return CS_CHUNKS; }
+extern "C" int fr_colsum_chunks() { return CS_MAX_CHUNKS; }
 
-// dword must be zeroed by the caller (rows of tokens absent from the batch stay zero)
+// dword must be zeroed by the caller (rows of tokens absent from the batch stay zero);
+// scratch: R + 1 ints (heavy list + its count, zeroed by the caller)
 extern "C" int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword,
-                                  hipStream_t s) {
-  if (D % 256 != 0 || R <= 0) return R < 0 ? 1 : 0;
-  hipLaunchKernelGGL(embed_grad_kernel, dim3((R + 3) / 4), dim3(256), 0, s, (const bf16*)dx, sorted, perm, R, D, dword);
+                                  int* scratch, hipStream_t s) {
+  if (D % 256 != 0 || D > 768 || R < 0) return 1;
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(embed_grad_kernel, dim3((R + 3) / 4), dim3(256), 0, s, (const bf16*)dx, sorted, perm, R, D, dword,
+                     scratch + 1, scratch);
+  hipLaunchKernelGGL(embed_grad_heavy_kernel, dim3(256), dim3(1024), 0, s, (const bf16*)dx, sorted, perm, R, D, dword,
+                     scratch + 1, scratch);
   return 0;
 }
