@@ -164,20 +164,22 @@ __global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __
       const bf16* a0 = Ks + (ks * 32 + fq * 4 + qq) * DH + jd * 16 + pp * 4;
       const bf16x8 kfr = tr_pair(a0, a0 + 16 * DH);
 #pragma unroll
-      for (int jq = 0; jq < 4; ++jq) o[jq][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf[jq][ks], kfr, o[jq][jd], 0, 0, 0);
+      // K^T as the A operand: the accumulator is dQ^T, so a lane holds 4 consecutive head
+      // dims d = 16 jd + 4 fq + r of one query t = 16 jq + fr -> 16-byte stores below
+      for (int jq = 0; jq < 4; ++jq) o[jq][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kfr, dsf[jq][ks], o[jq][jd], 0, 0, 0);
     }
   bf16* dq = dqkv + row0 * ld + h * DH;
   if (active) {
 #pragma unroll
-    for (int jq = 0; jq < 4; ++jq)
+    for (int jq = 0; jq < 4; ++jq) {
+      const int t = jq * 16 + fr;  // lanes l and l^16 share t (the permlane16 pairs agree)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = jq * 16 + fq * 4 + r;
-        if (t < T) {
-#pragma unroll
-          for (int jd = 0; jd < 4; ++jd) dq[(size_t)t * ld + jd * 16 + fr] = f2bf(o[jq][jd][r]);
-        }
+      for (int p2 = 0; p2 < 2; ++p2) {
+        const float v0[4] = {o[jq][2 * p2][0], o[jq][2 * p2][1], o[jq][2 * p2][2], o[jq][2 * p2][3]};
+        const float v1[4] = {o[jq][2 * p2 + 1][0], o[jq][2 * p2 + 1][1], o[jq][2 * p2 + 1][2], o[jq][2 * p2 + 1][3]};
+        store_pair16_if(dq + (size_t)(t < T ? t : 0) * ld + p2 * 32, v0, v1, fq, t < T);
       }
+    }
   }
   // ---- dV = P^T dO and dK = dS^T Q: A rows [s][t] via an LDS transpose of P^T / dS^T ----
 #pragma unroll
@@ -210,21 +212,21 @@ __global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __
         const bf16* b0 = Bsrc + (kt * 32 + fq * 8 + qq) * DH + jd * 16 + pp * 4;
         const bf16x8 bfr = tr_pair(b0, b0 + 4 * DH);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, o[i][jd], 0, 0, 0);
+        for (int i = 0; i < 4; ++i) o[i][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr, af[i], o[i][jd], 0, 0, 0);
       }
     }
     bf16* dst = dqkv + row0 * ld + (pass == 0 ? 2 * D : D) + h * DH;
-    if (active) {
+    if (active) {  // transposed accumulator: lane = key s = 16 i + fr, 4 consecutive d per (i, jd)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const int sk = i * 16 + fr;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int s = i * 16 + fq * 4 + r;
-          if (s < T) {
-#pragma unroll
-            for (int jd = 0; jd < 4; ++jd) dst[(size_t)s * ld + jd * 16 + fr] = f2bf(o[i][jd][r]);
-          }
+        for (int p2 = 0; p2 < 2; ++p2) {
+          const float v0[4] = {o[i][2 * p2][0], o[i][2 * p2][1], o[i][2 * p2][2], o[i][2 * p2][3]};
+          const float v1[4] = {o[i][2 * p2 + 1][0], o[i][2 * p2 + 1][1], o[i][2 * p2 + 1][2], o[i][2 * p2 + 1][3]};
+          store_pair16_if(dst + (size_t)(sk < T ? sk : 0) * ld + p2 * 32, v0, v1, fq, sk < T);
         }
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
