@@ -182,3 +182,12 @@ def test_bench_contract_two_ranks(config):
     assert r["config"]["global_batch"] == 8 and r["config"]["parallelism"] == "dp2"
     assert abs(r["value"] - 8 * 2 / (r["ms_per_step"] * 2 / 1000)) / r["value"] < 0.01
     assert r["scaling"] == "weak" and r["higher_is_better"] is True
+
+
+@pytest.mark.slow
+def test_allreduce_sweep_two_ranks():
+    argv = ["benchmarks/allreduce_bench.py", "--max-mb", "0.1", "--iters", "2", "--warmup", "1"]
+    outs = run_ranks([argv, argv], timeout=120)
+    _ok(outs)
+    rows = [json.loads(l) for l in outs[0][1].splitlines() if l.startswith("{")]
+    assert rows and all(r["world"] == 2 and r["us"] > 0 for r in rows)
