@@ -168,7 +168,45 @@ class Backbone(nn.Module):
         of every padding row (~2/3 of MIND title rows) and the attention skips key tiles past
         each title's length.  All other ops are row-wise; the last LayerNorm stores rows back
         in title order, so the output is identical in layout (and, up to fp32 summation
-        order, in value) to the unpacked path."""
+        order, in value) to the unpacked path.
+
+        ``FEDREC_BACKBONE_STREAMS=2``: the titles are split in two halves that run on two
+        HIP streams, interleaved layer by layer, so one half's LayerNorm / attention and the
+        tail of its persistent GEMMs can overlap the other half's kernels."""
+        ns = int(os.environ.get("FEDREC_BACKBONE_STREAMS", "1"))
+        n = tokens.shape[0]
+        if ns < 2 or n < 64:
+            out = [None]
+            for _ in self._packed_stages(tokens, mask, P, out, 0):
+                pass
+            return out[0]
+        main = torch.cuda.current_stream(tokens.device)
+        if getattr(self, "_streams", None) is None or len(self._streams) != ns:
+            self._streams = [torch.cuda.Stream(tokens.device) for _ in range(ns)]
+        bounds = [round(i * n / ns) for i in range(ns + 1)]
+        gens, outs = [], []
+        for i, st in enumerate(self._streams):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                gens.append(self._packed_stages(tokens[bounds[i]:bounds[i + 1]], mask[bounds[i]:bounds[i + 1]], P,
+                                                holder=outs, slot=i))
+        outs.extend([None] * ns)
+        live = list(range(ns))
+        while live:
+            for i in list(live):
+                with torch.cuda.stream(self._streams[i]):
+                    try:
+                        next(gens[i])
+                    except StopIteration:
+                        live.remove(i)
+        for st in self._streams:
+            main.wait_stream(st)
+        for t, st in zip(outs, self._streams):
+            t.record_stream(main)
+        return torch.cat(outs, 0)
+
+    def _packed_stages(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict, holder: list, slot: int):
+        """Generator: one ``yield`` per transformer layer (lets two halves interleave)."""
         c = self.cfg
         rowmap, src, kv_start, kv_len, qstart, n_kv = ops.title_plan(mask)
         x = ops.embed_ln_rows(tokens, src, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps)
@@ -184,7 +222,8 @@ class Backbone(nn.Module):
                 x = ops.layer_norm_scatter(h, L["ln2_w"], L["ln2_b"], c.ln_eps, x, src)
             else:
                 x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, residual=x)
-        return x
+            yield li
+        holder[slot] = x
 
     def forward_train(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
         """Differentiable forward for an unfrozen backbone (BASELINE config 5), eval-mode math
