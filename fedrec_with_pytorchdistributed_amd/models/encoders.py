@@ -32,7 +32,9 @@ class AdditiveAttention(nn.Module):
         self.att_fc1 = nn.Linear(d_h, hidden_size)
         self.att_fc2 = nn.Linear(hidden_size, 1)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, keep: torch.Tensor | None = None) -> torch.Tensor:
+        if keep is not None:  # mask_padding (Q7 option)
+            return OF.masked_additive_pool(x, self.att_fc1, self.att_fc2, keep)
         return OF.additive_pool(x, self.att_fc1, self.att_fc2)
 
 
@@ -49,10 +51,12 @@ class MultiHeadAttention(nn.Module):
         for m in (self.W_Q, self.W_K, self.W_V):
             nn.init.xavier_uniform_(m.weight, gain=1)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, keep: torch.Tensor | None = None) -> torch.Tensor:
         w = torch.cat([self.W_Q.weight, self.W_K.weight, self.W_V.weight], 0)
         b = torch.cat([self.W_Q.bias, self.W_K.bias, self.W_V.bias], 0)
         qkv = F.linear(x, w, b)  # one [B*H, 400] x [400, 1200] GEMM
+        if keep is not None:  # mask_padding (Q7 option): attention.py:76-78 key mask
+            return OF.masked_user_attention(qkv, self.n_heads, self.d_k, keep)
         return OF.user_attention(qkv, self.n_heads, self.d_k)
 
 
@@ -63,11 +67,15 @@ class UserEncoder(nn.Module):
         self.multihead_attention = MultiHeadAttention(cfg.news_dim, cfg.user_heads, cfg.user_head_dim,
                                                       cfg.user_head_dim)
         self.additive_attention = AdditiveAttention(cfg.news_dim, cfg.user_query_dim)
+        self.mask_padding = cfg.mask_padding
 
-    def forward(self, clicked: torch.Tensor) -> torch.Tensor:
+    def forward(self, clicked: torch.Tensor, his_ids: torch.Tensor | None = None) -> torch.Tensor:
+        """``clicked [B,H,400]``; ``his_ids [B,H]`` (0 = padding) masks the padded history
+        slots when ``mask_padding`` is on (the reference attends over them: Q7)."""
+        keep = (his_ids != 0) if (self.mask_padding and his_ids is not None) else None
         x = F.dropout(clicked, p=self.dropout_rate, training=self.training)
-        y = self.multihead_attention(x)
-        return self.additive_attention(y)
+        y = self.multihead_attention(x, keep)
+        return self.additive_attention(y, keep)
 
 
 class TextEncoder(nn.Module):
@@ -97,10 +105,12 @@ class TextEncoder(nn.Module):
             h = bb(text[:, 0, :], text[:, 1, :], self.compute_dtype)
         return h.view(n, T, -1)
 
-    def head(self, hidden: torch.Tensor) -> torch.Tensor:
-        """Trainable head: ``[n,T,D] -> [n,400]`` (fp32)."""
-        pooled = self.additive_attention(hidden)
+    def head(self, hidden: torch.Tensor, token_mask: torch.Tensor | None = None) -> torch.Tensor:
+        """Trainable head: ``[n,T,D] -> [n,400]`` (fp32).  ``token_mask [n,T]`` excludes padding
+        tokens from the pooling when ``mask_padding`` is on (the reference pools over them: Q7)."""
+        keep = (token_mask != 0) if (self.cfg.mask_padding and token_mask is not None) else None
+        pooled = self.additive_attention(hidden, keep)
         return F.linear(pooled, self.fc.weight, self.fc.bias)
 
     def forward(self, text: torch.Tensor) -> torch.Tensor:
-        return self.head(self.hidden(text))
+        return self.head(self.hidden(text), text[:, 1, :])

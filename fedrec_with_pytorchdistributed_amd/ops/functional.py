@@ -8,6 +8,8 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import math
+
 import torch
 
 from .. import ops
@@ -150,6 +152,38 @@ def additive_pool(x, lin1: torch.nn.Linear, lin2: torch.nn.Linear):
 
 def user_attention(qkv, heads: int, head_dim: int):
     return UserAttentionFn.apply(qkv, heads, head_dim)
+
+
+# ---------------------------------------------------------------------------------------
+# padding masks (config mask_padding): the reference passes mask=None everywhere,
+# but its AdditiveAttention / ScaledDotProductAttention take an optional mask that multiplies
+# exp(score) before the +1e-8 normalisation (attention.py:20-22, 40-42).  Opt-in, plain
+# autograd (not a hot path of any BASELINE config); stable form exp(a - m) with the 1e-8
+# term scaled by e^{-m}, exactly as the fused kernels treat the unmasked case.
+# ---------------------------------------------------------------------------------------
+def _masked_eps_softmax(a: torch.Tensor, keep: torch.Tensor, dim: int) -> torch.Tensor:
+    m = a.masked_fill(~keep, float("-inf")).amax(dim=dim, keepdim=True)
+    m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))  # all masked: every weight is 0
+    e = torch.exp(a - m) * keep
+    return e / (e.sum(dim=dim, keepdim=True) + 1e-8 * torch.exp(-m))
+
+
+def masked_additive_pool(x, lin1: torch.nn.Linear, lin2: torch.nn.Linear, keep: torch.Tensor):
+    """``x [n,T,D]``, ``keep [n,T]`` (bool) -> ``[n,D]`` fp32."""
+    xf = x.float()
+    e = torch.tanh(torch.nn.functional.linear(xf, lin1.weight, lin1.bias))
+    a = torch.nn.functional.linear(e, lin2.weight, lin2.bias).squeeze(-1)
+    alpha = _masked_eps_softmax(a, keep, dim=1)
+    return torch.einsum("nt,ntd->nd", alpha, xf)
+
+
+def masked_user_attention(qkv, heads: int, head_dim: int, keep: torch.Tensor):
+    """``qkv [B,H,3*h*d]``, key mask ``keep [B,H]`` -> ``ctx [B,H,h*d]``."""
+    B, H, _ = qkv.shape
+    q, k, v = qkv.float().view(B, H, 3, heads, head_dim).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / math.sqrt(head_dim)
+    A = _masked_eps_softmax(s, keep.view(B, 1, 1, H), dim=-1)
+    return (A @ v).permute(0, 2, 1, 3).reshape(B, H, heads * head_dim)
 
 
 def score_ce(cand, user, act: str = "sigmoid") -> Tuple[torch.Tensor, torch.Tensor]:

@@ -113,9 +113,9 @@ class LocalEngine:
         hid = te.hidden(text)  # frozen backbone: overlaps the previous step's all-reduce + Adam
         self.sync_params()
         if grad:
-            return te.head(hid)
+            return te.head(hid, text[:, 1, :])
         with torch.no_grad():
-            return te.head(hid)
+            return te.head(hid, text[:, 1, :])
 
     # -------------------------------------------------------------------------------
     def _forward_rows(self, cand: torch.Tensor, his: torch.Tensor, grad_news: bool):
@@ -142,7 +142,7 @@ class LocalEngine:
         self.flat.begin_backward()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True)
         with obs.range("user_fwd"):
-            u = self.model.user_encoder(his_v)
+            u = self.model.user_encoder(his_v, his)
             loss, _ = OF.score_ce(cand_v, u, self.score_act)
         with obs.range("backward"):
             loss.backward()
@@ -212,7 +212,7 @@ class LocalEngine:
             self.flat.grad.zero_()  # Q2: optimizer.zero_grad() each batch (client.py:75)
         self.model.text_encoder.eval()  # gen_news_vecs runs the text encoder in eval (model.py:42)
         uniq, v, cand_v, his_v = self._forward_rows(cand, his, grad_news=False)
-        u = self.model.user_encoder(his_v)
+        u = self.model.user_encoder(his_v, his)
         loss, _ = OF.score_ce(cand_v, u, self.score_act)
         loss.backward()
         self.G.index_add_(0, uniq.long(), v.grad)
@@ -237,7 +237,7 @@ class LocalEngine:
             text = self.tokens.index_select(0, cid.long())
             with obs.range("replay"):
                 hid = te.hidden(text)  # compat Q4 would re-run with dropout (train mode)
-                v = te.head(hid)
+                v = te.head(hid, text[:, 1, :])
                 v.backward(self.G.index_select(0, cid.long()) * head_scale)
         self.optimizer_step()
         self.G = None
@@ -301,7 +301,7 @@ class LocalEngine:
             rows = v.index_select(0, inv.long())
             cand_v = rows[: B * C].view(B, C, -1)
             his_v = rows[B * C:].view(B, his.shape[1], -1)
-            u = self.model.user_encoder(his_v)
+            u = self.model.user_encoder(his_v, his)
             loss, s, _, _ = ops.score_ce(cand_v, u, self.score_act)
             losses.append(float(loss) * B)
             scores_all.append(s.float().cpu().numpy())

@@ -416,3 +416,33 @@ def test_title_plan_oracle_semantics():
             out[qrows, h * dh:(h + 1) * dh] = torch.softmax(s, -1) @ v
     got = out[rowmap.reshape(-1).long()]  # back to title-major rows
     assert torch.allclose(got, want, atol=1e-10)
+
+
+def test_mask_padding_option_ignores_padding():
+    """``mask_padding`` (Q7 option): padded history slots and padding tokens no longer move the
+    user / news vectors; with the option off the reference behaviour (they do) is kept."""
+    from fedrec_with_pytorchdistributed_amd.config import BackboneConfig, FedRecConfig
+    from fedrec_with_pytorchdistributed_amd.models.fedrec_model import FedRecModel
+
+    for on in (False, True):
+        cfg = FedRecConfig(mask_padding=on, user_dropout=0.0)
+        cfg.backbone = BackboneConfig.preset("tiny")
+        torch.manual_seed(0)
+        m = FedRecModel(cfg).eval()
+        B, H, D = 3, 7, cfg.news_dim
+        his = torch.tensor([[5, 6, 0, 0, 0, 0, 0], [1, 2, 3, 4, 5, 6, 7], [0] * 7])
+        v = torch.randn(B, H, D)
+        v2 = v.clone()
+        v2[his == 0] = torch.randn(int((his == 0).sum()), D)  # change only the padded slots
+        with torch.no_grad():
+            u1, u2 = m.user_encoder(v, his), m.user_encoder(v2, his)
+        assert torch.isfinite(u1).all() and torch.isfinite(u2).all()
+        same_user = torch.allclose(u1[:2], u2[:2], atol=1e-6)
+        assert same_user == on
+        hid = torch.randn(2, 9, cfg.backbone.dim)
+        tmask = torch.tensor([[1, 1, 1, 0, 0, 0, 0, 0, 0], [1, 1, 1, 1, 1, 1, 1, 1, 1]])
+        hid2 = hid.clone()
+        hid2[0, 3:] = torch.randn(6, cfg.backbone.dim)
+        with torch.no_grad():
+            n1, n2 = m.text_encoder.head(hid, tmask), m.text_encoder.head(hid2, tmask)
+        assert torch.allclose(n1[0], n2[0], atol=1e-6) == on
