@@ -125,10 +125,10 @@ class FedRecConfig:
     global_rounds: int = 1
 
     # --- federation ------------------------------------------------------------------
-    mode: str = "fedavg_star"  # fedavg_star | grad_avg | param_avg
+    # fedavg_star | grad_avg | param_avg (main.py, "every participant trains", is grad_avg)
+    mode: str = "fedavg_star"
     local_update: str = "auto"  # per_epoch | per_step | auto (per_step for grad_avg)
     param_avg_every: int = 0  # PA: all-reduce every K local steps (0 = once per epoch)
-    server_trains: bool = False  # main.py variant: every participant trains
     weighted_fedavg: bool = False  # Q12: reference mean is unweighted (server.py:49)
     sync: str = "trainable"  # Q15: trainable | full (the reference syncs all 116 tensors)
     quorum: float = 1.0  # fraction of clients needed to aggregate a round
