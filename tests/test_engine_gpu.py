@@ -113,10 +113,13 @@ def test_unfrozen_backbone_grads_match_cpu(dev):
         assert err <= 8e-2 * float(a.norm()) + 2e-3 * total, (name, err, float(a.norm()), total)
         checked += 1
     assert checked > 20
-    # one optimizer step refreshes the bf16 compute copies of the backbone
-    before = m_gpu.text_encoder.DistillBert.compute_weights(torch.bfloat16)["w1"] if False else None
+    # one optimizer step invalidates the bf16 compute copies of the backbone, and the next
+    # pack carries the updated weights
+    w1_before = m_gpu.text_encoder.DistillBert.compute_weights(torch.bfloat16)["layers"][0]["w1"].clone()
     e_gpu.optimizer_step()
     assert m_gpu.text_encoder.DistillBert._pack is None
+    w1_after = m_gpu.text_encoder.DistillBert.compute_weights(torch.bfloat16)["layers"][0]["w1"]
+    assert not torch.equal(w1_before, w1_after)
 
 
 def test_learns_planted_signal_on_gpu(dev):
