@@ -10,7 +10,9 @@ sample a batch of ``--batch`` impressions from the client's private synthetic MI
 6-layer DistilBERT forward over the unique titles (hand-written MFMA kernels) ->
 text head -> user encoder -> sigmoid-CE loss -> backward (user encoder, per-news
 gradient segment sum, text-head VJP) -> RCCL all-reduce of the 1.16M trainable grads ->
-fused Adam.  Nothing is cached across steps (no news-vector or hidden-state cache).
+fused Adam.  Nothing is cached across steps (no news-vector or hidden-state cache).  The
+next batch's sampling + dedup run on a lookahead stream during the current step, and (N > 1)
+the all-reduce + Adam on a side stream during the next step's frozen-backbone forward.
 
 ``value`` = total impressions/s over all GPUs (weak scaling: ``--batch`` per GPU).
 ``vs_baseline`` divides by the reference's best measured throughput, 1.87 impressions/s
@@ -112,34 +114,36 @@ def main() -> int:
         eng.sigma = calibrate_client_sigma(cfg.dp.epsilon, cfg.dp.delta, cfg.batch_size, len(shard.train), cfg.dp.epochs)
     pa_state = {"n": 0}
 
-    def step(c, h):
-        loss = eng.train_step(c, h)
+    def step(pre):
+        loss = eng.train_prepared(pre)
         if args.config == 3:
             pa_state["n"] += 1
             if world > 1 and pa_state["n"] % args.pa_every == 0:
                 comm.allreduce_(model.sync_tensors(False), ctx.data_group, scale=1.0 / world)
         return loss
 
-    # batches: sampled on the fly inside the timed loop (host sampler + H2D copy)
+    # batches: sampled on the device inside the timed loop, one step ahead -- the next batch's
+    # sampling + dedup run on the engine's lookahead stream while the current step computes
     it = iter(())
     epoch = [0]
 
     def next_batch():
         nonlocal it
         while True:
-            try:
-                c, h = next(it)
-                return eng.to_device(c), eng.to_device(h)
-            except StopIteration:
-                it = iter(eng.sampler.epoch(epoch[0]))
-                epoch[0] += 1
+            pre = eng._next_prepared(it)
+            if pre is not None:
+                return pre
+            it = iter(eng.sampler.epoch(epoch[0]))
+            epoch[0] += 1
 
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    pre = next_batch()
     for _ in range(args.warmup):
-        step(*next_batch())
+        step(pre)
+        pre = next_batch()
     sync()
     if ctx.initialized:
         dist.barrier(group=ctx.ctrl_group)
@@ -147,7 +151,8 @@ def main() -> int:
     t0 = time.perf_counter()
     losses = []
     for _ in range(args.steps):
-        losses.append(step(*next_batch()))
+        losses.append(step(pre))
+        pre = next_batch()  # the batch of the step after this one (K prepares per K steps)
     sync()
     if ctx.initialized:
         dist.barrier(group=ctx.ctrl_group)

@@ -25,8 +25,9 @@ Two update schedules (Q3):
 from __future__ import annotations
 
 import math
+import os
 import time
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, NamedTuple, Optional, Tuple
 
 import numpy as np
 import torch
@@ -39,6 +40,15 @@ from ..eval.metrics import batch_metrics
 from ..models.fedrec_model import FedRecModel
 from ..ops import functional as OF
 from ..utils import obs
+
+
+class Prepared(NamedTuple):
+    """A sampled batch with its dedup done ahead of time (``LocalEngine.prepare``)."""
+
+    cand: torch.Tensor
+    his: torch.Tensor
+    dedup: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]]
+    ready: Optional[torch.cuda.Event]
 
 
 class LocalEngine:
@@ -77,6 +87,11 @@ class LocalEngine:
             ov == "on" or (ov == "auto" and grad_allreduce is not None))
         self._side = torch.cuda.Stream(device) if self.overlap else None
         self._params_ready: Optional[torch.cuda.Event] = None
+        # batch lookahead (GPU): the next batch is sampled and de-duplicated on its own stream
+        # while the current step runs, so the dedup's host read of the unique count (the
+        # backbone's M) no longer drains the GPU at every step start
+        lookahead = device.type == "cuda" and os.environ.get("FEDREC_LOOKAHEAD", "1") != "0"
+        self._prep = torch.cuda.Stream(device) if lookahead else None
 
     # -------------------------------------------------------------------------------
     @property
@@ -118,11 +133,34 @@ class LocalEngine:
             return te.head(hid, text[:, 1, :])
 
     # -------------------------------------------------------------------------------
-    def _forward_rows(self, cand: torch.Tensor, his: torch.Tensor, grad_news: bool):
+    def prepare(self, batch_fn: Callable[[], Tuple]) -> Prepared:
+        """Sample a batch (``batch_fn() -> (cand, his)``) and de-duplicate its news ids.  On the
+        GPU both run on the lookahead stream: the only host wait (the unique count) waits for
+        that stream alone, so a step's dedup overlaps the previous step's kernels."""
+        if self._prep is None:
+            c, h = batch_fn()
+            return Prepared(self.to_device(c), self.to_device(h), None, None)
+        main = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self._prep):
+            c, h = batch_fn()
+            c, h = self.to_device(c), self.to_device(h)
+            ids = torch.cat([c.reshape(-1), h.reshape(-1)])
+            dd = ops.dedup(ids, self.N)
+            ev = torch.cuda.Event()
+            ev.record(self._prep)
+        for t in (c, h, *dd):
+            t.record_stream(main)
+        return Prepared(c, h, tuple(dd), ev)
+
+    def _forward_rows(self, cand: torch.Tensor, his: torch.Tensor, grad_news: bool, pre: Optional[Prepared] = None):
         B, C = cand.shape
         H = his.shape[1]
-        ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
-        uniq, inv, perm, ptr = ops.dedup(ids, self.N)
+        if pre is not None and pre.dedup is not None:
+            torch.cuda.current_stream(self.device).wait_event(pre.ready)
+            uniq, inv, perm, ptr = pre.dedup
+        else:
+            ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
+            uniq, inv, perm, ptr = ops.dedup(ids, self.N)
         with obs.range("news_encode"):
             v = self.news_vectors(uniq, grad=grad_news)
         if not grad_news:
@@ -134,13 +172,13 @@ class LocalEngine:
         his_v = rows[B * C:].view(B, H, -1)
         return uniq, v, cand_v, his_v
 
-    def forward_backward(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
+    def forward_backward(self, cand: torch.Tensor, his: torch.Tensor, pre: Optional[Prepared] = None) -> torch.Tensor:
         """Loss of one batch with every trainable gradient left in ``flat.grad``."""
         self.model.train()
         if self.cfg.news_cache == "vectors" or not self.cfg.backbone.frozen:
             self.sync_params()
         self.flat.begin_backward()
-        _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True)
+        _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True, pre=pre)
         with obs.range("user_fwd"):
             u = self.model.user_encoder(his_v, his)
             loss, _ = OF.score_ce(cand_v, u, self.score_act)
@@ -149,11 +187,14 @@ class LocalEngine:
         self.flat.end_backward()
         return loss.detach()
 
-    def train_step(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
+    def train_step(self, cand: torch.Tensor, his: torch.Tensor, pre: Optional[Prepared] = None) -> torch.Tensor:
         """``per_step`` schedule: grads -> all-reduce -> Adam.  Returns the (device) loss."""
-        loss = self.forward_backward(cand, his)
+        loss = self.forward_backward(cand, his, pre)
         self.optimizer_step(overlap=True)
         return loss
+
+    def train_prepared(self, pre: Prepared) -> torch.Tensor:
+        return self.train_step(pre.cand, pre.his, pre)
 
     def optimizer_step(self, extra_scale: float = 1.0, overlap: bool = False) -> None:
         """All-reduce the flat gradient (if any) and take one fused Adam step.  ``overlap``
@@ -244,6 +285,16 @@ class LocalEngine:
         self.touched = None
         self.news_table = None
 
+    def _next_prepared(self, it) -> Optional[Prepared]:
+        """The next batch of a sampler iterator, sampled and de-duplicated ahead (None at the
+        end of the epoch)."""
+        if self._prep is None:
+            b = next(it, None)
+            return None if b is None else Prepared(self.to_device(b[0]), self.to_device(b[1]), None, None)
+        with torch.cuda.stream(self._prep):  # the device sampler's kernel runs on the lookahead stream
+            b = next(it, None)
+        return None if b is None else self.prepare(lambda: b)
+
     # -------------------------------------------------------------------------------
     def train_epoch(self, max_steps: Optional[int] = None, log_every: int = 0,
                     step_hook: Optional[Callable[[int], None]] = None) -> Dict[str, float]:
@@ -256,12 +307,22 @@ class LocalEngine:
         n = 0
         if sched == "per_epoch":
             self._begin_epoch_accumulate()
-        for cand_np, his_np in self.sampler.epoch(self.epoch):
-            cand, his = self.to_device(cand_np), self.to_device(his_np)
+        it = iter(self.sampler.epoch(self.epoch))
+        nxt = self._next_prepared(it) if sched == "per_step" else None
+        while True:
             if sched == "per_step":
-                loss = self.train_step(cand, his)
+                pre = nxt
+                if pre is None:
+                    break
+                loss = self.train_prepared(pre)
+                # sample + dedup the next batch while this step's kernels run
+                last = max_steps is not None and n + 1 >= max_steps
+                nxt = None if last else self._next_prepared(it)
             else:
-                loss = self.accumulate_step(cand, his)
+                b = next(it, None)
+                if b is None:
+                    break
+                loss = self.accumulate_step(self.to_device(b[0]), self.to_device(b[1]))
             losses.append(loss)
             n += 1
             if step_hook is not None:
