@@ -19,64 +19,91 @@ namespace {
 constexpr int DK = 20;
 constexpr int MAXH = 64;
 
+// K/V rows staged as [H][DK] fp32 (80-B rows, 16-B aligned): every key row is 5 broadcast
+// ds_read_b128 instead of 20 ds_read_b32
+__device__ __forceinline__ float dot20(const float (&q)[DK], const float* __restrict__ row) {
+  float d = 0.f;
+#pragma unroll
+  for (int c4 = 0; c4 < DK / 4; ++c4) {
+    const float4 k = *(const float4*)(row + 4 * c4);
+    d += q[4 * c4] * k.x + q[4 * c4 + 1] * k.y + q[4 * c4 + 2] * k.z + q[4 * c4 + 3] * k.w;
+  }
+  return d;
+}
+
+__device__ __forceinline__ void axpy20(float (&acc)[DK], float a, const float* __restrict__ row) {
+#pragma unroll
+  for (int c4 = 0; c4 < DK / 4; ++c4) {
+    const float4 v = *(const float4*)(row + 4 * c4);
+    acc[4 * c4] += a * v.x;
+    acc[4 * c4 + 1] += a * v.y;
+    acc[4 * c4 + 2] += a * v.z;
+    acc[4 * c4 + 3] += a * v.w;
+  }
+}
+
 __global__ __launch_bounds__(128) void user_attn_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
                                                             float* __restrict__ stats, int B, int H, int NH) {
-  __shared__ float ks[2][MAXH][DK + 1];
-  __shared__ float vs[2][MAXH][DK + 1];
+  __shared__ __attribute__((aligned(16))) float ks[2][MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float vs[2][MAXH][DK];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pair = blockIdx.x * 2 + wave;
   const bool active = pair < B * NH;
   const int b = active ? pair / NH : 0, h = active ? pair - b * NH : 0;
   const int ld = 3 * NH * DK, D = NH * DK;
   const float* base = qkv + (size_t)b * H * ld + h * DK;
-  for (int i = lane; i < H * DK; i += 64) {
-    const int r = i / DK, c = i - r * DK;
-    ks[wave][r][c] = base[(size_t)r * ld + D + c];
-    vs[wave][r][c] = base[(size_t)r * ld + 2 * D + c];
+  for (int i = lane; i < H * DK / 4; i += 64) {  // 16-B chunks (DK % 4 == 0, rows 16-B aligned)
+    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+    *(float4*)&ks[wave][r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
+    *(float4*)&vs[wave][r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
   }
   __syncthreads();
   if (!active || lane >= H) return;
   float q[DK];
 #pragma unroll
-  for (int c = 0; c < DK; ++c) q[c] = base[(size_t)lane * ld + c];
-  const float scale = rsqrtf((float)DK);
-  float m = -INFINITY;
-  for (int s = 0; s < H; ++s) {
-    float d = 0.f;
-#pragma unroll
-    for (int c = 0; c < DK; ++c) d += q[c] * ks[wave][s][c];
-    m = fmaxf(m, d * scale);
+  for (int c4 = 0; c4 < DK / 4; ++c4) {
+    const float4 v = *(const float4*)(base + (size_t)lane * ld + 4 * c4);
+    q[4 * c4] = v.x;
+    q[4 * c4 + 1] = v.y;
+    q[4 * c4 + 2] = v.z;
+    q[4 * c4 + 3] = v.w;
   }
+  const float scale = rsqrtf((float)DK);
+#pragma unroll
+  for (int c = 0; c < DK; ++c) q[c] *= scale;
+  float m = -INFINITY;
+  for (int s = 0; s < H; ++s) m = fmaxf(m, dot20(q, &ks[wave][s][0]));
   float acc[DK];
 #pragma unroll
   for (int c = 0; c < DK; ++c) acc[c] = 0.f;
   float l = 0.f;
   for (int s = 0; s < H; ++s) {
-    float d = 0.f;
-#pragma unroll
-    for (int c = 0; c < DK; ++c) d += q[c] * ks[wave][s][c];
-    const float p = __expf(d * scale - m);
+    const float p = __expf(dot20(q, &ks[wave][s][0]) - m);
     l += p;
-#pragma unroll
-    for (int c = 0; c < DK; ++c) acc[c] += p * vs[wave][s][c];
+    axpy20(acc, p, &vs[wave][s][0]);
   }
   l += 1e-8f * __expf(-m);
   const float inv = 1.0f / l;
   float* o = ctx + ((size_t)b * H + lane) * D + h * DK;
 #pragma unroll
-  for (int c = 0; c < DK; ++c) o[c] = acc[c] * inv;
+  for (int c4 = 0; c4 < DK / 4; ++c4)
+    *(float4*)(o + 4 * c4) = make_float4(acc[4 * c4] * inv, acc[4 * c4 + 1] * inv, acc[4 * c4 + 2] * inv,
+                                         acc[4 * c4 + 3] * inv);
   float* st = stats + (((size_t)b * NH + h) * H + lane) * 2;
   st[0] = m;
   st[1] = inv;
 }
 
+// Backward, 2 passes over the keys (was 3): lane = query t accumulates
+//   u = sum_s A_ts dA_ts k_s, w = sum_s A_ts k_s, D_t = sum_s A_ts dA_ts
+// in ONE pass and forms dq_t = scale (u - D_t w); lane = key s then accumulates dk_s, dv_s.
 __global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ stats,
                                                            const float* __restrict__ dctx, float* __restrict__ dqkv,
                                                            int B, int H, int NH) {
-  __shared__ float qs[MAXH][DK + 1];
-  __shared__ float ks[MAXH][DK + 1];
-  __shared__ float vs[MAXH][DK + 1];
-  __shared__ float gs[MAXH][DK + 1];
+  __shared__ __attribute__((aligned(16))) float qs[MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float ks[MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float vs[MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float gs[MAXH][DK];
   __shared__ float ms[MAXH], is_[MAXH], Ds[MAXH];
   const int lane = threadIdx.x;
   const int pair = blockIdx.x;
@@ -84,12 +111,12 @@ __global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restri
   const int ld = 3 * NH * DK, D = NH * DK;
   const float* base = qkv + (size_t)b * H * ld + h * DK;
   const float* gb = dctx + (size_t)b * H * D + h * DK;
-  for (int i = lane; i < H * DK; i += 64) {
-    const int r = i / DK, c = i - r * DK;
-    qs[r][c] = base[(size_t)r * ld + c];
-    ks[r][c] = base[(size_t)r * ld + D + c];
-    vs[r][c] = base[(size_t)r * ld + 2 * D + c];
-    gs[r][c] = gb[(size_t)r * D + c];
+  for (int i = lane; i < H * DK / 4; i += 64) {
+    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+    *(float4*)&qs[r][c] = *(const float4*)(base + (size_t)r * ld + c);
+    *(float4*)&ks[r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
+    *(float4*)&vs[r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
+    *(float4*)&gs[r][c] = *(const float4*)(gb + (size_t)r * D + c);
   }
   const float* st = stats + ((size_t)b * NH + h) * H * 2;
   for (int t = lane; t < H; t += 64) {
@@ -99,67 +126,56 @@ __global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restri
   __syncthreads();
   const float scale = rsqrtf((float)DK);
   float* dbase = dqkv + (size_t)b * H * ld + h * DK;
-  // pass 1: lane = query t -> D_t, dq_t
   if (lane < H) {
     const int t = lane;
     const float m = ms[t], inv = is_[t];
+    float q[DK], g[DK], u[DK], w[DK];
+#pragma unroll
+    for (int c = 0; c < DK; ++c) {
+      q[c] = qs[t][c] * scale;
+      g[c] = gs[t][c];
+      u[c] = w[c] = 0.f;
+    }
     float Dt = 0.f;
     for (int s = 0; s < H; ++s) {
-      float d = 0.f, dA = 0.f;
-#pragma unroll
-      for (int c = 0; c < DK; ++c) {
-        d += qs[t][c] * ks[s][c];
-        dA += gs[t][c] * vs[s][c];
-      }
-      Dt += __expf(d * scale - m) * inv * dA;
+      const float A = __expf(dot20(q, &ks[s][0]) - m) * inv;
+      const float dA = dot20(g, &vs[s][0]);
+      Dt += A * dA;
+      axpy20(u, A * dA, &ks[s][0]);
+      axpy20(w, A, &ks[s][0]);
     }
     Ds[t] = Dt;
-    float dq[DK];
-#pragma unroll
-    for (int c = 0; c < DK; ++c) dq[c] = 0.f;
-    for (int s = 0; s < H; ++s) {
-      float d = 0.f, dA = 0.f;
-#pragma unroll
-      for (int c = 0; c < DK; ++c) {
-        d += qs[t][c] * ks[s][c];
-        dA += gs[t][c] * vs[s][c];
-      }
-      const float A = __expf(d * scale - m) * inv;
-      const float dS = A * (dA - Dt) * scale;
-#pragma unroll
-      for (int c = 0; c < DK; ++c) dq[c] += dS * ks[s][c];
-    }
     float* o = dbase + (size_t)t * ld;
 #pragma unroll
-    for (int c = 0; c < DK; ++c) o[c] = dq[c];
+    for (int c4 = 0; c4 < DK / 4; ++c4) {
+      const int c = 4 * c4;
+      *(float4*)(o + c) = make_float4(scale * (u[c] - Dt * w[c]), scale * (u[c + 1] - Dt * w[c + 1]),
+                                      scale * (u[c + 2] - Dt * w[c + 2]), scale * (u[c + 3] - Dt * w[c + 3]));
+    }
   }
   __syncthreads();
-  // pass 2: lane = key s -> dk_s, dv_s
   if (lane < H) {
     const int s = lane;
-    float dk[DK], dv[DK];
+    float k[DK], v[DK], dk[DK], dv[DK];
 #pragma unroll
-    for (int c = 0; c < DK; ++c) dk[c] = dv[c] = 0.f;
+    for (int c = 0; c < DK; ++c) {
+      k[c] = ks[s][c] * scale;
+      v[c] = vs[s][c];
+      dk[c] = dv[c] = 0.f;
+    }
     for (int t = 0; t < H; ++t) {
-      float d = 0.f, dA = 0.f;
-#pragma unroll
-      for (int c = 0; c < DK; ++c) {
-        d += qs[t][c] * ks[s][c];
-        dA += gs[t][c] * vs[s][c];
-      }
-      const float A = __expf(d * scale - ms[t]) * is_[t];
+      const float A = __expf(dot20(k, &qs[t][0]) - ms[t]) * is_[t];
+      const float dA = dot20(v, &gs[t][0]);
       const float dS = A * (dA - Ds[t]) * scale;
-#pragma unroll
-      for (int c = 0; c < DK; ++c) {
-        dk[c] += dS * qs[t][c];
-        dv[c] += A * gs[t][c];
-      }
+      axpy20(dk, dS, &qs[t][0]);
+      axpy20(dv, A, &gs[t][0]);
     }
     float* o = dbase + (size_t)s * ld;
 #pragma unroll
-    for (int c = 0; c < DK; ++c) {
-      o[D + c] = dk[c];
-      o[2 * D + c] = dv[c];
+    for (int c4 = 0; c4 < DK / 4; ++c4) {
+      const int c = 4 * c4;
+      *(float4*)(o + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
+      *(float4*)(o + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
     }
   }
 }
