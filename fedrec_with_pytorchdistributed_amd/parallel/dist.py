@@ -69,6 +69,10 @@ def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0, g
                                                         and role == "client"))
     if use_cuda:
         gi = max(0, local_rank - gpu_offset)
+        if os.environ.get("FEDREC_SHARE_GPU", "0") == "1":
+            # rehearsal of the multi-client path on a box with fewer GPUs than ranks (tests
+            # only: RCCL refuses two ranks on one device, so pair it with FEDREC_DATA_BACKEND=gloo)
+            gi %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(gi)
         dev = torch.device("cuda", gi)
     else:
@@ -90,7 +94,7 @@ def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0, g
     dist.all_gather_object(roles, role, group=ctx.ctrl_group)
     ctx.roles = [str(r) for r in roles]
     ctx.client_ranks = [i for i, r in enumerate(ctx.roles) if r == "client"]
-    data_backend = "nccl" if gpu_job else "gloo"
+    data_backend = os.environ.get("FEDREC_DATA_BACKEND") or ("nccl" if gpu_job else "gloo")
     # every rank must call new_group, members or not
     ctx.data_group = dist.new_group(ranks=ctx.client_ranks, backend=data_backend, timeout=timeout)
     return ctx
