@@ -17,7 +17,8 @@
 
 namespace {
 
-constexpr int MAXT = 128;
+constexpr int MAXT = 128;    // vectorised text-head kernels (titles: T = 50)
+constexpr int MAXT_G = 2048;  // generic kernels: long user histories (Q6: never truncated)
 
 template <typename T>
 __device__ __forceinline__ float ld(const T* p) { return (float)*p; }
@@ -27,7 +28,7 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const TX* __restrict__ x,
                                                        const float* __restrict__ w2, const float* __restrict__ b2,
                                                        float* __restrict__ out, float* __restrict__ alpha_out, int T,
                                                        int D, int Q) {
-  __shared__ float a_s[MAXT];
+  __shared__ float a_s[MAXT_G];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const TX* xe = x + (size_t)n * T * D;
   const TX* ee = e + (size_t)n * T * Q;
@@ -70,8 +71,8 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
                                                        const float* __restrict__ g, float* __restrict__ dx,
                                                        TX* __restrict__ dpre, float* __restrict__ dw2,
                                                        float* __restrict__ db2, int T, int D, int Q, int R) {
-  __shared__ float da_s[MAXT];
-  __shared__ float al_s[MAXT];
+  __shared__ float da_s[MAXT_G];
+  __shared__ float al_s[MAXT_G];
   __shared__ float red[4];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   dw2 += (size_t)(n % R) * Q;  // R accumulator replicas: 1/R of the atomic contention
@@ -307,9 +308,9 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
 
 extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const float* b2, float* out,
                                     float* alpha, int n, int T, int D, int Q, int is_bf16, hipStream_t s) {
-  if (T > MAXT) return 1;
+  if (T > MAXT_G) return 1;
   if (n == 0) return 0;
-  if (is_bf16 && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256)
+  if (is_bf16 && T <= MAXT && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256)
     hipLaunchKernelGGL(pool_fwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, w2, b2, out, alpha,
                        T, D, Q);
   else if (is_bf16)
@@ -328,9 +329,9 @@ extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w
 extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g,
                                     float* dx, void* dpre, float* dw2, float* db2, float* dsum, int n, int T, int D,
                                     int Q, int R, int is_bf16, hipStream_t s) {
-  if (T > MAXT) return 1;
+  if (T > MAXT_G) return 1;
   if (n == 0) return -1;
-  if (is_bf16 && dx == nullptr && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256) {
+  if (is_bf16 && T <= MAXT && dx == nullptr && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256) {
     hipLaunchKernelGGL(pool_bwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, alpha, w2, g,
                        (bf16*)dpre, dw2, db2, dsum, T, D, Q, R);
     return 0;

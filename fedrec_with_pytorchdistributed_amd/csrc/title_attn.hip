@@ -628,9 +628,13 @@ int g_ta_cus = 0;
 
 extern "C" void fr_title_attn_set_waves(int w) { g_ta_waves = w; }
 
+extern "C" int fr_title_attention_long_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H,
+                                            int D, hipStream_t s);  // title_attn_long.hip, 64 < T <= 512
+
 extern "C" int fr_title_attention_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
                                        hipStream_t s) {
-  if (T < 1 || T > 64 || D != H * DH) return 1;
+  if (T > 64) return fr_title_attention_long_bf16(qkv, mask, out, n_titles, T, H, D, s);
+  if (T < 1 || D != H * DH) return 1;
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
   const int w = g_ta_waves;

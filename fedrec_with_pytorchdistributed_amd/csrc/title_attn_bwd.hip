@@ -235,9 +235,13 @@ __global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __
 
 }  // namespace
 
+extern "C" int fr_title_attention_bwd_long_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv,
+                                                int n_titles, int T, int H, int D, hipStream_t s);  // title_attn_long.hip
+
 extern "C" int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv,
                                            int n_titles, int T, int H, int D, hipStream_t s) {
-  if (T < 1 || T > 64 || D != H * DH) return 1;
+  if (T > 64) return fr_title_attention_bwd_long_bf16(qkv, dout, mask, dqkv, n_titles, T, H, D, s);
+  if (T < 1 || D != H * DH) return 1;
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
   hipLaunchKernelGGL(title_attn_bwd_kernel, dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, (const bf16*)qkv,

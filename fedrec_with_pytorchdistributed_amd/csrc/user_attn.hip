@@ -180,22 +180,200 @@ __global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Long histories (H > 64): the reference pads but never truncates (dataset.py:84, quirk Q6;
+// its shipped shard has H = 76), and SURVEY §5.7 asks for H limited only by memory.  Same
+// math, one wave per (impression, head), query rows in chunks of 64 (lane = row), keys /
+// values streamed through LDS in chunks of 64 rows.  Forward: online softmax (running max
+// with rescale), so (m, 1/l) come out exactly as in the short kernel.  Backward: pass A
+// (lane = query) keeps D_t in LDS for pass B (lane = key); per-row m, 1/l, D live in LDS,
+// so H <= MAXL.
+constexpr int CH = 64;
+constexpr int MAXL = 2048;
+
+__device__ __forceinline__ void stage_rows(float (*dst)[DK], const float* __restrict__ src, size_t ld, int r0,
+                                           int n, int lane) {
+  for (int i = lane; i < n * DK / 4; i += 64) {
+    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+    *(float4*)&dst[r][c] = *(const float4*)(src + (size_t)(r0 + r) * ld + c);
+  }
+}
+
+__device__ __forceinline__ void load_row(float (&x)[DK], const float* __restrict__ p, float s) {
+#pragma unroll
+  for (int c4 = 0; c4 < DK / 4; ++c4) {
+    const float4 v = *(const float4*)(p + 4 * c4);
+    x[4 * c4] = v.x * s;
+    x[4 * c4 + 1] = v.y * s;
+    x[4 * c4 + 2] = v.z * s;
+    x[4 * c4 + 3] = v.w * s;
+  }
+}
+
+__global__ __launch_bounds__(64) void user_attn_fwd_long_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
+                                                                float* __restrict__ stats, int B, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float ks[CH][DK];
+  __shared__ __attribute__((aligned(16))) float vs[CH][DK];
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  const float scale = rsqrtf((float)DK);
+  for (int t0 = 0; t0 < H; t0 += CH) {
+    const int t = t0 + lane;
+    const bool valid = t < H;
+    float q[DK], acc[DK];
+    load_row(q, base + (size_t)(valid ? t : 0) * ld, scale);
+#pragma unroll
+    for (int c = 0; c < DK; ++c) acc[c] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    for (int s0 = 0; s0 < H; s0 += CH) {
+      const int n = min(CH, H - s0);
+      __syncthreads();
+      stage_rows(ks, base + D, ld, s0, n, lane);
+      stage_rows(vs, base + 2 * D, ld, s0, n, lane);
+      __syncthreads();
+      float mc = m;
+      for (int s = 0; s < n; ++s) mc = fmaxf(mc, dot20(q, &ks[s][0]));
+      const float alpha = __expf(m - mc);  // 0 on the first chunk (m = -inf)
+      l *= alpha;
+#pragma unroll
+      for (int c = 0; c < DK; ++c) acc[c] *= alpha;
+      for (int s = 0; s < n; ++s) {
+        const float p = __expf(dot20(q, &ks[s][0]) - mc);
+        l += p;
+        axpy20(acc, p, &vs[s][0]);
+      }
+      m = mc;
+    }
+    if (!valid) continue;
+    l += 1e-8f * __expf(-m);
+    const float inv = 1.0f / l;
+    float* o = ctx + ((size_t)b * H + t) * D + h * DK;
+#pragma unroll
+    for (int c4 = 0; c4 < DK / 4; ++c4)
+      *(float4*)(o + 4 * c4) = make_float4(acc[4 * c4] * inv, acc[4 * c4 + 1] * inv, acc[4 * c4 + 2] * inv,
+                                           acc[4 * c4 + 3] * inv);
+    float* st = stats + (((size_t)b * NH + h) * H + t) * 2;
+    st[0] = m;
+    st[1] = inv;
+  }
+}
+
+__global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __restrict__ qkv,
+                                                                const float* __restrict__ stats,
+                                                                const float* __restrict__ dctx,
+                                                                float* __restrict__ dqkv, int B, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float xs[CH][DK];  // keys (pass A) / queries (pass B)
+  __shared__ __attribute__((aligned(16))) float ys[CH][DK];  // values (pass A) / dctx rows (pass B)
+  __shared__ float ms[MAXL], is_[MAXL], Ds[MAXL];
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  const float* gb = dctx + (size_t)b * H * D + h * DK;
+  float* dbase = dqkv + (size_t)b * H * ld + h * DK;
+  const float* st = stats + ((size_t)b * NH + h) * H * 2;
+  for (int t = lane; t < H; t += 64) {
+    ms[t] = st[2 * t];
+    is_[t] = st[2 * t + 1];
+  }
+  const float scale = rsqrtf((float)DK);
+  // pass A: lane = query t -> dq_t = scale (u - D_t w), D_t kept in LDS
+  for (int t0 = 0; t0 < H; t0 += CH) {
+    const int t = t0 + lane;
+    const bool valid = t < H;
+    const int tc = valid ? t : 0;
+    float q[DK], g[DK], u[DK], w[DK];
+    load_row(q, base + (size_t)tc * ld, scale);
+    load_row(g, gb + (size_t)tc * D, 1.f);
+#pragma unroll
+    for (int c = 0; c < DK; ++c) u[c] = w[c] = 0.f;
+    __syncthreads();  // ms / is_ written above (first chunk)
+    const float m = ms[tc], inv = is_[tc];
+    float Dt = 0.f;
+    for (int s0 = 0; s0 < H; s0 += CH) {
+      const int n = min(CH, H - s0);
+      __syncthreads();
+      stage_rows(xs, base + D, ld, s0, n, lane);
+      stage_rows(ys, base + 2 * D, ld, s0, n, lane);
+      __syncthreads();
+      for (int s = 0; s < n; ++s) {
+        const float A = __expf(dot20(q, &xs[s][0]) - m) * inv;
+        const float dA = dot20(g, &ys[s][0]);
+        Dt += A * dA;
+        axpy20(u, A * dA, &xs[s][0]);
+        axpy20(w, A, &xs[s][0]);
+      }
+    }
+    if (!valid) continue;
+    Ds[t] = Dt;
+    float* o = dbase + (size_t)t * ld;
+#pragma unroll
+    for (int c4 = 0; c4 < DK / 4; ++c4) {
+      const int c = 4 * c4;
+      *(float4*)(o + c) = make_float4(scale * (u[c] - Dt * w[c]), scale * (u[c + 1] - Dt * w[c + 1]),
+                                      scale * (u[c + 2] - Dt * w[c + 2]), scale * (u[c + 3] - Dt * w[c + 3]));
+    }
+  }
+  // pass B: lane = key s -> dk_s = sum_t dS_ts q_t, dv_s = sum_t A_ts dctx_t
+  for (int s0 = 0; s0 < H; s0 += CH) {
+    const int s = s0 + lane;
+    const bool valid = s < H;
+    const int sc = valid ? s : 0;
+    float k[DK], v[DK], dk[DK], dv[DK];
+    load_row(k, base + (size_t)sc * ld + D, scale);
+    load_row(v, base + (size_t)sc * ld + 2 * D, 1.f);
+#pragma unroll
+    for (int c = 0; c < DK; ++c) dk[c] = dv[c] = 0.f;
+    for (int t0 = 0; t0 < H; t0 += CH) {
+      const int n = min(CH, H - t0);
+      __syncthreads();  // also orders pass A's Ds writes before these reads
+      stage_rows(xs, base, ld, t0, n, lane);
+      stage_rows(ys, gb, D, t0, n, lane);
+      __syncthreads();
+      for (int j = 0; j < n; ++j) {
+        const int t = t0 + j;
+        const float A = __expf(dot20(k, &xs[j][0]) - ms[t]) * is_[t];
+        const float dA = dot20(v, &ys[j][0]);
+        const float dS = A * (dA - Ds[t]) * scale;
+        axpy20(dk, dS, &xs[j][0]);
+        axpy20(dv, A, &ys[j][0]);
+      }
+    }
+    if (!valid) continue;
+    float* o = dbase + (size_t)s * ld;
+#pragma unroll
+    for (int c4 = 0; c4 < DK / 4; ++c4) {
+      const int c = 4 * c4;
+      *(float4*)(o + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
+      *(float4*)(o + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk,
                                 hipStream_t s) {
-  if (dk != DK || H > MAXH || H < 1) return 1;
+  if (dk != DK || H > MAXL || H < 1) return 1;
   const int pairs = B * NH;
   if (pairs == 0) return 0;
-  hipLaunchKernelGGL(user_attn_fwd_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
+  if (H > MAXH)
+    hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH);
+  else
+    hipLaunchKernelGGL(user_attn_fwd_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
   return 0;
 }
 
 extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H,
                                 int NH, int dk, hipStream_t s) {
-  if (dk != DK || H > MAXH || H < 1) return 1;
+  if (dk != DK || H > MAXL || H < 1) return 1;
   const int pairs = B * NH;
   if (pairs == 0) return 0;
-  hipLaunchKernelGGL(user_attn_bwd_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
+  if (H > MAXH)
+    hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
+  else
+    hipLaunchKernelGGL(user_attn_bwd_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   return 0;
 }

@@ -19,8 +19,12 @@ def _cfg():
     return cfg
 
 
-def test_step_matches_cpu_oracle(dev):
+@pytest.mark.parametrize("untruncated", [False, True])
+def test_step_matches_cpu_oracle(dev, untruncated):
+    """``untruncated``: the reference's Q6 (histories padded, never truncated) -- batches of the
+    tiny shard then carry histories > 64, the long-history user attention / pool kernels."""
     cfg = _cfg()
+    cfg.compat.no_history_truncation = untruncated
     torch.manual_seed(0)
     m_cpu = FedRecModel(cfg)
     m_gpu = copy.deepcopy(m_cpu).to(dev)
@@ -30,6 +34,7 @@ def test_step_matches_cpu_oracle(dev):
     e_cpu = LocalEngine(cfg, m_cpu, shard, torch.device("cpu"))
     e_gpu = LocalEngine(cfg, m_gpu, shard, dev)
     cand, his = next(iter(e_cpu.sampler.epoch(0)))
+    assert (his.shape[1] > 64) == untruncated
     l_cpu = e_cpu.forward_backward(e_cpu.to_device(cand), e_cpu.to_device(his))
     l_gpu = e_gpu.forward_backward(e_gpu.to_device(cand), e_gpu.to_device(his))
     assert abs(float(l_cpu) - float(l_gpu)) < 2e-3

@@ -90,8 +90,9 @@ def test_embed_ln(dev):
     assert rel_err(y, y_ref) < 1e-2
 
 
-@pytest.mark.parametrize("T", [50, 64, 17, 1])
+@pytest.mark.parametrize("T", [50, 64, 17, 1, 65, 130, 512])
 def test_title_attention(dev, T):
+    """T > 64 runs title_attn_long.hip (online softmax over 64-key LDS chunks, up to 512)."""
     n, H, D = 9, 12, 768
     qkv = torch.randn(n * T, 3 * D, device=dev).to(torch.bfloat16)
     mask = (torch.rand(n, T, device=dev) < 0.7).to(torch.int32)
@@ -154,8 +155,11 @@ def test_additive_pool(dev, dtype, D, Q):
     assert abs(float(db2_n) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
 
 
-def test_user_attention(dev):
-    B, H, NH, DK = 7, 50, 20, 20
+@pytest.mark.parametrize("H", [1, 50, 64, 65, 76, 200])
+def test_user_attention(dev, H):
+    """H > 64 runs the long-history kernels (online softmax over 64-row LDS chunks): the
+    reference never truncates histories (Q6; its shipped shard has H = 76)."""
+    B, NH, DK = 7, 20, 20
     qkv = torch.randn(B, H, 3 * NH * DK, device=dev)
     ctx, stats = ops.user_attention_fwd(qkv, NH, DK)
     c_ref, A = ref.user_attention_fwd(qkv, NH, DK)
@@ -164,6 +168,23 @@ def test_user_attention(dev):
     dq = ops.user_attention_bwd(qkv, stats, d, NH, DK)
     dq_ref = ref.user_attention_bwd(qkv, A, d, NH, DK)
     assert rel_err(dq, dq_ref) < 1e-4
+
+
+@pytest.mark.parametrize("T", [76, 300])
+def test_additive_pool_long_fp32(dev, T):
+    """User-side pooling over long (untruncated, Q6) histories: the generic kernels."""
+    n, D, Q = 5, 400, 200
+    x = torch.randn(n, T, D, device=dev)
+    e = torch.tanh(torch.randn(n, T, Q, device=dev))
+    w2 = torch.randn(Q, device=dev) * 0.1
+    b2 = torch.randn(1, device=dev)
+    out, alpha = ops.additive_pool_fwd(x, e, w2, b2)
+    o_ref, a_ref = ref.additive_pool_fwd(x, e, w2, b2)
+    assert rel_err(out, o_ref) < 1e-5 and rel_err(alpha, a_ref) < 1e-5
+    g = torch.randn(n, D, device=dev)
+    dx, dpre, dw2, db2 = ops.additive_pool_bwd(x, e, alpha, w2, g, True)
+    rdx, rde, rdw2, rdb2 = ref.additive_pool_bwd(x, e, a_ref, w2, g)
+    assert rel_err(dx, rdx) < 1e-5 and rel_err(dpre, rde * (1 - e ** 2)) < 1e-4 and rel_err(dw2, rdw2) < 1e-4
 
 
 def test_score_ce(dev):
@@ -338,7 +359,7 @@ def test_device_sampler_semantics(dev):
     assert counts.min() > 0.5 * counts.mean()
 
 
-@pytest.mark.parametrize("T", [50, 64, 9])
+@pytest.mark.parametrize("T", [50, 64, 9, 65, 200])
 def test_title_attention_bwd(dev, T):
     n, H, D = 5, 12, 768
     qkv = torch.randn(n * T, 3 * D, device=dev).to(torch.bfloat16)
@@ -420,3 +441,23 @@ def test_linear_gelu_dual(dev, M):
     assert rel_err(h, h_ref) < 5e-3
     sl = slice(0, min(M, 1024))
     assert rel_err(h[sl], torch.nn.functional.gelu(x[sl].float() @ w.float().t() + b)) < 1e-2
+
+
+def test_backbone_long_titles_match_reference(dev):
+    """A 2-layer DistilBERT-width backbone on 96-token titles (T > 64: unpacked path, long
+    attention kernels) against the fp32 eager oracle with the same weights."""
+    from fedrec_with_pytorchdistributed_amd.config import BackboneConfig
+    from fedrec_with_pytorchdistributed_amd.models.backbone import Backbone
+
+    torch.manual_seed(0)
+    bb = Backbone(BackboneConfig(name="distilbert-2l", n_layers=2)).to(dev)
+    n, T = 6, 96
+    tok = torch.randint(1000, 29000, (n, T), device=dev, dtype=torch.int32)
+    lens = torch.tensor([96, 70, 65, 20, 3, 0])
+    mask = (torch.arange(T)[None, :] < lens[:, None]).to(torch.int32).to(dev)
+    tok = tok * mask
+    y = bb.forward(tok, mask, torch.bfloat16)
+    P = bb.compute_weights(torch.float32)
+    y_ref = ref.backbone_forward(tok.long(), mask, P, 2, 12, bb.cfg.ln_eps)
+    assert torch.isfinite(y.float()).all()
+    assert rel_err(y, y_ref) < 2e-2
