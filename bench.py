@@ -163,6 +163,9 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
         elapsed = float(t.item())
     loss = float(torch.stack(losses).float().mean())
+    if ctx.initialized:  # FEDREC_COLL_CHECK=1: every client issued the same collective sequence
+        from fedrec_with_pytorchdistributed_amd.parallel.collcheck import CHECK
+        CHECK.verify(ctx.ctrl_group, "bench")
 
     # untimed: the data-plane share of a step -- the same flat-bucket RCCL all-reduce the GA
     # step issues, alone, averaged over 20 calls (bus bandwidth = 2 (W-1)/W x bytes / time)

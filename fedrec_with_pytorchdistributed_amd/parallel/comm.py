@@ -14,6 +14,8 @@ import torch
 import torch.distributed as dist
 from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
 
+from .collcheck import CHECK
+
 BUCKET_BYTES = 28 << 20
 
 
@@ -36,9 +38,11 @@ def allreduce_(tensors: List[torch.Tensor], group, op=dist.ReduceOp.SUM, scale: 
     for b in _buckets(tensors, bucket_bytes):
         if len(b) == 1:
             flat = b[0] if b[0].is_contiguous() else b[0].contiguous()
+            CHECK.record("all_reduce", flat, str(op).split(".")[-1])
             works.append((b, flat, dist.all_reduce(flat, op=op, group=group, async_op=True)))
         else:
             flat = _flatten_dense_tensors(b)
+            CHECK.record("all_reduce", flat, str(op).split(".")[-1])
             works.append((b, flat, dist.all_reduce(flat, op=op, group=group, async_op=True)))
     for b, flat, w in works:
         w.wait()
@@ -55,9 +59,11 @@ def allreduce_(tensors: List[torch.Tensor], group, op=dist.ReduceOp.SUM, scale: 
 def broadcast_(tensors: List[torch.Tensor], src: int, group, bucket_bytes: int = BUCKET_BYTES) -> None:
     for b in _buckets(tensors, bucket_bytes):
         if len(b) == 1 and b[0].is_contiguous():
+            CHECK.record("broadcast", b[0], f"src={src}")
             dist.broadcast(b[0], src=src, group=group)
         else:
             flat = _flatten_dense_tensors(b)
+            CHECK.record("broadcast", flat, f"src={src}")
             dist.broadcast(flat, src=src, group=group)
             for t, s in zip(b, _unflatten_dense_tensors(flat, b)):
                 t.copy_(s)

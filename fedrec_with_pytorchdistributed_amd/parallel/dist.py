@@ -22,6 +22,8 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from .collcheck import CHECK
+
 
 @dataclass
 class DistContext:
@@ -115,6 +117,7 @@ def make_grad_allreduce(ctx: DistContext):
     W = ctx.num_clients
 
     def _ar(flat_grad: torch.Tensor) -> float:
+        CHECK.record("all_reduce", flat_grad, "grad")
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=ctx.data_group)
         return 1.0 / W
 
@@ -154,6 +157,7 @@ def make_secure_grad_allreduce(ctx: DistContext, frac_bits: Optional[int] = None
         if frac_bits is not None:
             return frac_bits, clip
         m = torch.nan_to_num(flat_grad.abs().max().float().reshape(1), nan=0.0, posinf=3.0e38)
+        CHECK.record("all_reduce", m, "secagg-max")
         dist.all_reduce(m, op=dist.ReduceOp.MAX, group=ctx.data_group)
         mv = max(float(m.item()), 1e-30)
         f = int(math.floor(math.log2((2.0 ** 30) / (W * mv))))
@@ -165,6 +169,7 @@ def make_secure_grad_allreduce(ctx: DistContext, frac_bits: Optional[int] = None
         q = secagg.mask_local(flat_grad, k, W, seeds_row, state["step"], fb, cl)
         if q.device != flat_grad.device:
             q = q.to(flat_grad.device)
+        CHECK.record("all_reduce", q, "secagg-sum")
         dist.all_reduce(q, op=dist.ReduceOp.SUM, group=ctx.data_group)
         flat_grad.copy_(secagg.unmask_sum(q, fb).view_as(flat_grad))
         state["step"] += 1
