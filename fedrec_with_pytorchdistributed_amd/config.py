@@ -134,6 +134,12 @@ class FedRecConfig:
     quorum: float = 1.0  # fraction of clients needed to aggregate a round
     collective_timeout_s: float = 600.0  # reference: 2 days (client.py:227)
     round_timeout_s: float = 3600.0
+    # star-mode liveness: clients bump a progress counter in the store at most
+    # every heartbeat_s (per training step, around validation and upload); the coordinator
+    # declares a client dead when its counter has not moved for heartbeat_timeout_s (0 = off)
+    # and aggregates the quorum without waiting out round_timeout_s
+    heartbeat_s: float = 2.0
+    heartbeat_timeout_s: float = 300.0
 
     # --- privacy / secure aggregation --------------------------------------------------
     dp: DPConfig = field(default_factory=DPConfig)

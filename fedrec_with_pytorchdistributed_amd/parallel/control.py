@@ -119,9 +119,58 @@ class ControlPlane:
         return json.loads(self.get(key, timeout_s).decode())
 
     # --- heartbeats ----------------------------------------------------------------------
-    def heartbeat(self, who: str) -> None:
-        self.set(f"hb/{who}", str(time.time()))
+    # A heartbeat is a progress COUNTER, not a timestamp: the coordinator times how long a
+    # counter has stood still on its own monotonic clock, so client clock skew across nodes
+    # cannot fake liveness or death.
+    def heartbeat(self, who: str) -> int:
+        return self.add(f"hb/{who}", 1)
 
-    def last_heartbeat(self, who: str) -> Optional[float]:
+    def heartbeat_count(self, who: str) -> int:
         k = f"hb/{who}"
-        return float(self.store.get(k).decode()) if self.store.check([k]) else None
+        return int(self.store.get(k).decode()) if self.store.check([k]) else 0
+
+    def wait_uploads(self, keys: Dict[int, str], need: int, timeout_s: float, hb_timeout_s: float = 0.0,
+                     who=lambda k: f"client{k}", poll_s: float = 0.05, log=None):
+        """Wait for every client's upload key, or until each missing client is declared dead
+        (heartbeat counter unchanged for ``hb_timeout_s``) with ``need`` uploads present, or
+        until ``timeout_s``.  Returns ``(present_keys, dead_clients)``."""
+        now = time.monotonic()
+        deadline = now + timeout_s
+        seen = {k: (self.heartbeat_count(who(k)), now) for k in keys}
+        dead: set = set()
+        while True:
+            present = [k for k in keys if self.store.check([keys[k]])]
+            now = time.monotonic()
+            if len(present) == len(keys) or now > deadline:
+                break
+            if hb_timeout_s > 0:
+                for k in keys:
+                    if k in present or k in dead:
+                        continue
+                    c = self.heartbeat_count(who(k))
+                    if c != seen[k][0]:
+                        seen[k] = (c, now)
+                    elif now - seen[k][1] > hb_timeout_s:
+                        dead.add(k)
+                        if log is not None:
+                            log(f"client {k}: no heartbeat for {hb_timeout_s:.0f}s (counter {c}); declared dead")
+                if dead and all(k in present or k in dead for k in keys):
+                    break
+            time.sleep(poll_s)
+        return [keys[k] for k in keys if k in present], sorted(dead)
+
+
+class Heartbeat:
+    """Client side: ``beat()`` bumps the counter, at most once per ``interval_s``."""
+
+    def __init__(self, cp: ControlPlane, who: str, interval_s: float):
+        self.cp, self.who, self.interval = cp, who, interval_s
+        self._last = -1e30
+
+    def __call__(self, *_args, force: bool = False) -> None:
+        if self.interval <= 0 and not force:
+            return
+        now = time.monotonic()
+        if force or now - self._last >= self.interval:
+            self._last = now
+            self.cp.heartbeat(self.who)

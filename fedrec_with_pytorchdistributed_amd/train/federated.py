@@ -35,7 +35,8 @@ from ..data.synthetic import SynthSpec, SyntheticCorpus
 from ..models.fedrec_model import FedRecModel
 from ..parallel import comm
 from ..parallel import secagg
-from ..parallel.control import ControlPlane
+from ..parallel.collcheck import CHECK
+from ..parallel.control import ControlPlane, Heartbeat
 from ..parallel.dist import DistContext, make_grad_allreduce, make_secure_grad_allreduce
 from ..privacy.rdp import calibrate_client_sigma
 from ..utils import obs
@@ -150,6 +151,7 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     for epoch in range(start, cfg.total_epochs):
         tr = eng.train_epoch(max_steps=steps)
         va = eng.validate()
+        CHECK.verify(ctx.ctrl_group, f"grad_avg epoch {epoch}")
         last = _reduce_metrics(ctx, tr, va)
         last.update({"epoch": epoch, "mode": "grad_avg", "clients": ctx.num_clients})
         if ctx.client_index == 0:
@@ -189,6 +191,7 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
         if not K or (steps or 0) % K:
             average()  # once per epoch (Parameter_Averaging_main.py:144-148)
         va = eng.validate()
+        CHECK.verify(ctx.ctrl_group, f"param_avg epoch {epoch}")
         last = _reduce_metrics(ctx, tr, va)
         last.update({"epoch": epoch, "mode": "param_avg", "clients": W})
         if ctx.client_index == 0:
@@ -235,11 +238,13 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         pubs = [cp.get(f"pk/{j}") for j in range(ctx.num_clients)]
         seeds_row = secagg.seeds_from_publics(kp, k, pubs)
     r = int(cp.get("start").decode())  # the coordinator may be resuming at a later round
+    beat = Heartbeat(cp, f"client{k}", cfg.heartbeat_s)
     last: Dict = {}
     while True:
         flag = cp.get(f"r{r}/go").decode()
         if flag != "1":
             break
+        beat(force=True)
         g = cp.get_tensor(f"r{r}/global")
         with torch.no_grad():
             model.flat.flat.copy_(g.to(model.flat.flat.device))
@@ -251,14 +256,17 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         eng.epoch = 0
         tr, va = {}, {}
         for _ in range(cfg.total_epochs):  # Trainer(...).train(total_epochs) per round (client.py:283-284)
-            tr = eng.train_epoch()
+            tr = eng.train_epoch(step_hook=beat)
+            beat()
             va = eng.validate()
+            beat()
         meta = {"client": k, "n_train": len(shard.train), **{m: float(v) for m, v in {**tr, **va}.items()
                                                              if isinstance(v, (int, float))}}
         up = _client_upload_tensor(model, cfg).clone()
         if cfg.round_artifacts:  # client.py:288 torch.save(model.state_dict(), "model.pt")
             sub = "" if ctx.num_clients == 1 else f"client{k}"
             ckpt.save_state_dict(os.path.join(_artifact_dir(cfg), sub, "model.pt"), model)
+        beat(force=True)
         fault.before_upload(r, up)
         if agg == "allreduce":
             w = float(len(shard.train)) if cfg.weighted_fedavg else 1.0
@@ -322,14 +330,16 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         if full:
             cp.put_tensor(f"r{r}/backbone", _flat_backbone(model))
         cp.set(f"r{r}/go", "1")
+        dead: List[int] = []
         if agg == "allreduce":
             avg = cp.get_tensor(f"r{r}/avg", cfg.round_timeout_s)
             metas = [cp.get_json(f"r{r}/meta/{k}") for k in range(W)]
             accepted = list(range(W))
             new = avg
         else:
-            keys = [f"r{r}/up/{k}" for k in range(W)]
-            present = cp.wait_any(keys, need, cfg.round_timeout_s)
+            keys = {k: f"r{r}/up/{k}" for k in range(W)}
+            present, dead = cp.wait_uploads(keys, need, cfg.round_timeout_s, cfg.heartbeat_timeout_s,
+                                            log=lambda m: obs.log(f"[server] round {r}: {m}"))
             ups, metas, accepted = [], [], []
             for key in present:
                 k = int(key.rsplit("/", 1)[1])
@@ -368,7 +378,7 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         with torch.no_grad():
             model.flat.flat.copy_(new)
         dt = time.perf_counter() - t0
-        rec = {"round": r, "clients_accepted": len(accepted), "clients": W, "round_s": dt}
+        rec = {"round": r, "clients_accepted": len(accepted), "clients": W, "clients_dead": dead, "round_s": dt}
         for key in ("training_loss", "validation_loss", "valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):
             vals = [m[key] for m in metas if key in m]
             if vals:

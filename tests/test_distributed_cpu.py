@@ -100,6 +100,23 @@ def test_star_quorum_survives_killed_client(tmp_path):
 
 
 @pytest.mark.slow
+def test_star_heartbeat_detects_killed_client_early(tmp_path):
+    """A killed client stops heartbeating: with a 10-minute round timeout the coordinator
+    still closes the round after heartbeat_timeout_s (quorum 0.5) and logs it dead."""
+    import time as _t
+    hb = ["--quorum=0.5", "--round_timeout_s=600", "--heartbeat_timeout_s=8", "--heartbeat_s=0.5"]
+    server = ["server.py", "2", *TINY, *hb, f"--snapshot_path={tmp_path}/s.pt"]
+    client = ["client.py", "1", "16", "1", "0", "c", *TINY, *hb]
+    t0 = _t.monotonic()
+    outs = run_ranks([server, client, client], {"FEDREC_FAULT": "client:1:round:1:kill"}, timeout=300)
+    assert outs[0][0] == 0, outs[0][1][-3000:]
+    assert _t.monotonic() - t0 < 240
+    hist = _metrics(str(tmp_path / "metrics.jsonl"))
+    assert [h["clients_accepted"] for h in hist] == [2, 1]
+    assert hist[1]["clients_dead"] == [1]
+
+
+@pytest.mark.slow
 def test_star_rejects_nan_upload(tmp_path):
     server = ["server.py", "1", *TINY, "--quorum=0.5", "--round_timeout_s=60", f"--snapshot_path={tmp_path}/s.pt"]
     client = ["client.py", "1", "16", "1", "0", "c", *TINY, "--quorum=0.5"]
@@ -191,3 +208,30 @@ def test_allreduce_sweep_two_ranks():
     _ok(outs)
     rows = [json.loads(l) for l in outs[0][1].splitlines() if l.startswith("{")]
     assert rows and all(r["world"] == 2 and r["us"] > 0 for r in rows)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("diverge", [False, True])
+def test_collective_checker_two_ranks(diverge):
+    """SURVEY §5.2 collective-sequence checker: identical sequences pass; a rank that issues a
+    bucket with another reduction is reported on every rank with the first differing collective."""
+    argv = ["tests/_collcheck_worker.py"] + (["--diverge"] if diverge else [])
+    outs = run_ranks([argv, argv], {"FEDREC_COLL_CHECK": "1"}, timeout=120)
+    _ok(outs)
+    for _, out in outs:
+        line = [l for l in out.splitlines() if l.startswith("COLLCHECK")][0]
+        if not diverge:
+            assert line == "COLLCHECK OK 5"
+        else:
+            assert "MISMATCH" in line and "first difference at collective #4" in line
+            assert "all_reduce|float32|8|SUM" in line and "all_reduce|float32|8|MAX" in line
+
+
+@pytest.mark.slow
+def test_grad_avg_with_collective_checker(tmp_path):
+    """The real GA / PA call sites under FEDREC_COLL_CHECK=1: the per-epoch verification passes."""
+    snap = str(tmp_path / "snapshot.pt")
+    for script in ("Gradient_Averaging_main.py", "Parameter_Averaging_main.py"):
+        argv = [script, "2", "16", "1", *TINY, f"--snapshot_path={snap}"]
+        outs = run_ranks([argv, argv], {"FEDREC_COLL_CHECK": "1"})
+        _ok(outs)

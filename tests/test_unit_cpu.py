@@ -446,3 +446,36 @@ def test_mask_padding_option_ignores_padding():
         with torch.no_grad():
             n1, n2 = m.text_encoder.head(hid, tmask), m.text_encoder.head(hid2, tmask)
         assert torch.allclose(n1[0], n2[0], atol=1e-6) == on
+
+
+def test_heartbeat_liveness_declares_silent_client_dead():
+    """a client whose progress counter stands still for heartbeat_timeout is
+    declared dead and the coordinator stops waiting (quorum), long before round_timeout."""
+    import threading
+    import time as _t
+
+    from fedrec_with_pytorchdistributed_amd.parallel.control import ControlPlane, Heartbeat
+
+    cp = ControlPlane(run_id="hbtest", timeout_s=5)
+    stop = threading.Event()
+    beat = Heartbeat(cp, "client0", 0.05)
+
+    def live():  # client 0 trains (beats), uploads after 0.6 s; client 1 never beats
+        t0 = _t.monotonic()
+        while not stop.is_set():
+            beat()
+            if _t.monotonic() - t0 > 0.6 and not cp.has("r0/up/0"):
+                cp.set("r0/up/0", b"x")
+            _t.sleep(0.01)
+
+    th = threading.Thread(target=live)
+    th.start()
+    try:
+        t0 = _t.monotonic()
+        present, dead = cp.wait_uploads({0: "r0/up/0", 1: "r0/up/1"}, 1, timeout_s=60, hb_timeout_s=1.0)
+        dt = _t.monotonic() - t0
+    finally:
+        stop.set()
+        th.join()
+    assert present == ["r0/up/0"] and dead == [1] and dt < 10
+    assert cp.heartbeat_count("client0") > 5 and cp.heartbeat_count("client1") == 0
