@@ -42,6 +42,9 @@ class BackboneConfig:
     dropout: float = 0.1
     frozen: bool = True  # reference freezes DistilBERT (model.py:25-26)
     init_std: float = 0.02
+    # local Hugging Face checkpoint (directory from save_pretrained, or one weights file) of
+    # DistilBERT / BERT; "" = random init (no pretrained weights ship offline)
+    pretrained: str = ""
 
     @staticmethod
     def preset(name: str) -> "BackboneConfig":

@@ -83,6 +83,10 @@ class TextEncoder(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.DistillBert = Backbone(cfg.backbone)
+        if cfg.backbone.pretrained:  # encoder.py:19 from_pretrained, from a LOCAL checkpoint
+            from .pretrained import load_pretrained_backbone
+
+            load_pretrained_backbone(self.DistillBert, cfg.backbone.pretrained)
         d = cfg.backbone.dim
         self.additive_attention = AdditiveAttention(d, cfg.text_query_dim or d // 2)
         self.fc = nn.Linear(d, cfg.news_dim)

@@ -296,7 +296,7 @@ def test_secagg_cancels_exactly(dev):
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10])
 @pytest.mark.parametrize("M,N,K,act,res", [(5000, 768, 768, "none", True), (4133, 2304, 768, "gelu", False),
                                            (70000, 768, 3072, "none", True), (78850, 2304, 768, "none", False),
-                                           (300, 256, 64, "tanh", True)])
+                                           (300, 256, 64, "tanh", True), (78850, 384, 768, "tanh", False)])
 def test_gemm_variants(dev, variant, M, N, K, act, res):
     lib = native.lib()
     g = torch.Generator(device="cpu").manual_seed(M)

@@ -479,3 +479,40 @@ def test_heartbeat_liveness_declares_silent_client_dead():
         th.join()
     assert present == ["r0/up/0"] and dead == [1] and dt < 10
     assert cp.heartbeat_count("client0") > 5 and cp.heartbeat_count("client1") == 0
+
+
+@pytest.mark.parametrize("kind", ["distilbert", "bert"])
+def test_pretrained_backbone_from_local_hf_checkpoint(tmp_path, kind):
+    """``--backbone.pretrained=DIR`` (encoder.py:19 from_pretrained, offline): a checkpoint
+    written by HF save_pretrained loads into the backbone and reproduces HF's forward; BERT
+    keys are remapped and its token-type row folded into the position table."""
+    pytest.importorskip("transformers")
+    from transformers import BertConfig, BertModel, DistilBertConfig, DistilBertModel
+
+    torch.manual_seed(1)
+    if kind == "distilbert":
+        hf = DistilBertModel(DistilBertConfig(dim=64, n_layers=2, n_heads=4, hidden_dim=128, max_position_embeddings=64,
+                                              attn_implementation="eager")).eval()
+    else:
+        hf = BertModel(BertConfig(hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128,
+                                  max_position_embeddings=64, attn_implementation="eager"),
+                       add_pooling_layer=False).eval()
+        with torch.no_grad():  # non-trivial token-type row 0
+            hf.embeddings.token_type_embeddings.weight.normal_(0, 0.5)
+    hf.save_pretrained(str(tmp_path / "ckpt"))
+    cfg = FedRecConfig()
+    cfg.backbone = BackboneConfig(name="t", dim=64, n_layers=2, n_heads=4, hidden_dim=128, max_position=64,
+                                  pretrained=str(tmp_path / "ckpt"))
+    m = FedRecModel(cfg)
+    tok = torch.randint(1, 30000, (5, 40))
+    mask = torch.ones(5, 40, dtype=torch.long)
+    mask[1, 15:] = 0
+    with torch.no_grad():
+        ours = m.text_encoder.DistillBert(tok, mask, torch.float32).view(5, 40, -1)
+        theirs = hf(tok, attention_mask=mask)[0]
+    assert torch.allclose(ours, theirs, atol=3e-5), (ours - theirs).abs().max()
+    # a mismatched configured backbone is refused with a clear message
+    cfg.backbone = BackboneConfig(name="t", dim=64, n_layers=3, n_heads=4, hidden_dim=128, max_position=64,
+                                  pretrained=str(tmp_path / "ckpt"))
+    with pytest.raises(ValueError, match="n_layers"):
+        FedRecModel(cfg)
