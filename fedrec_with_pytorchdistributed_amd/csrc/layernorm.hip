@@ -185,15 +185,126 @@ bool launch_ln16_r(const bf16* x, const int* tok, const bf16* word, const bf16* 
   return true;
 }
 
-// 0: wave-per-row kernel; 1 (default) / 2 / 3: half-wave rows with 1 / 2 / 4 rows per half-wave.
+// Persistent form of ln16 (plain LN / LN + residual / scattered store): a grid of 8 blocks
+// per CU, each half-wave walks rows with a grid stride, loads w / b ONCE into registers
+// (the one-shot kernel re-reads 192 B of w / b per lane per row: 12 extra vector loads per
+// 9 data accesses) and keeps the next row's loads in flight while it normalises the current.
+template <int NC>
+__global__ __launch_bounds__(256) void ln16p_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                    const float* __restrict__ b, bf16* __restrict__ y, int rows,
+                                                    float eps, const bf16* __restrict__ res,
+                                                    const int* __restrict__ ridx) {
+  constexpr int D = 256 * NC;
+  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const int hw = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half;
+  const int nhw = gridDim.x * 8;
+  int row = hw;
+  if (row >= rows) return;
+  float ww[NC][8], bb[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = c * 256 + hl * 8;
+    const float4 w0 = *(const float4*)(w + i), w1 = *(const float4*)(w + i + 4);
+    const float4 b0 = *(const float4*)(b + i), b1 = *(const float4*)(b + i + 4);
+    ww[c][0] = w0.x; ww[c][1] = w0.y; ww[c][2] = w0.z; ww[c][3] = w0.w;
+    ww[c][4] = w1.x; ww[c][5] = w1.y; ww[c][6] = w1.z; ww[c][7] = w1.w;
+    bb[c][0] = b0.x; bb[c][1] = b0.y; bb[c][2] = b0.z; bb[c][3] = b0.w;
+    bb[c][4] = b1.x; bb[c][5] = b1.y; bb[c][6] = b1.z; bb[c][7] = b1.w;
+  }
+  const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  bf16x8 ax[NC], ar[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    ax[c] = *(const bf16x8*)(x + (size_t)row * D + c * 256 + hl * 8);
+    ar[c] = res != nullptr ? *(const bf16x8*)(res + (size_t)row * D + c * 256 + hl * 8) : zero;
+  }
+  while (true) {
+    const int nrow = row + nhw;
+    const int lrow = nrow < rows ? nrow : rows - 1;  // clamped: the prefetch is unconditional
+    bf16x8 nx[NC], nr[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      nx[c] = *(const bf16x8*)(x + (size_t)lrow * D + c * 256 + hl * 8);
+      nr[c] = res != nullptr ? *(const bf16x8*)(res + (size_t)lrow * D + c * 256 + hl * 8) : zero;
+    }
+    float v[NC][8];
+    float sm = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[c][k] = (float)ax[c][k] + (float)ar[c][k];
+        sm += v[c][k];
+      }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+    const float mean = sm * (1.0f / D);
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[c][k] - mean;
+        sq += d * d;
+      }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    const float rstd = rsqrtf(sq * (1.0f / D) + eps);
+    const int orow = ridx != nullptr ? ridx[row] : row;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = f2bf((v[c][k] - mean) * rstd * ww[c][k] + bb[c][k]);
+      *(bf16x8*)(y + (size_t)orow * D + c * 256 + hl * 8) = o;
+    }
+    if (nrow >= rows) break;
+    row = nrow;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      ax[c] = nx[c];
+      ar[c] = nr[c];
+    }
+  }
+}
+
+int g_ln_cus = 0;
+
+bool launch_ln16p(const bf16* x, const float* w, const float* b, bf16* y, int rows, int D, float eps, hipStream_t s,
+                  const bf16* res, const int* ridx) {
+  if (g_ln_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_ln_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_ln_cus <= 0) g_ln_cus = 256;
+  }
+  int blocks = g_ln_cus * 8;
+  const int need = (rows + 7) / 8;
+  blocks = blocks < need ? blocks : need;
+  if (D == 768)
+    hipLaunchKernelGGL((ln16p_kernel<3>), dim3(blocks), dim3(256), 0, s, x, w, b, y, rows, eps, res, ridx);
+  else if (D == 512)
+    hipLaunchKernelGGL((ln16p_kernel<2>), dim3(blocks), dim3(256), 0, s, x, w, b, y, rows, eps, res, ridx);
+  else if (D == 1024)
+    hipLaunchKernelGGL((ln16p_kernel<4>), dim3(blocks), dim3(256), 0, s, x, w, b, y, rows, eps, res, ridx);
+  else if (D == 256)
+    hipLaunchKernelGGL((ln16p_kernel<1>), dim3(blocks), dim3(256), 0, s, x, w, b, y, rows, eps, res, ridx);
+  else
+    return false;
+  return true;
+}
+
+// 0: wave-per-row kernel; 1 (default) / 2 / 3: half-wave rows with 1 / 2 / 4 rows per half-wave;
+// 4: the persistent half-wave kernel above (non-embedding forms only).
 // Measured interleaved at 78850 x 768 (benchmarks/ln_ab.py): LN + residual 75 / 83 / 100 us,
 // plain LN 43 / 46.5 / 52 us -- one row per half-wave keeps the most rows in flight per CU.
-int g_ln_wide = 1;
+int g_ln_wide = 4;
 
 template <bool EMBED>
 bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* pos, const float* w, const float* b,
                  bf16* y, int rows, int D, int T, float eps, hipStream_t s, const bf16* res = nullptr,
                  const int* ridx = nullptr) {
+  if (!EMBED && g_ln_wide == 4) return launch_ln16p(x, w, b, y, rows, D, eps, s, res, ridx);
   if (g_ln_wide == 2) return launch_ln16_r<EMBED, 2>(x, tok, word, pos, w, b, y, rows, D, T, eps, s, res, ridx);
   if (g_ln_wide == 3) return launch_ln16_r<EMBED, 4>(x, tok, word, pos, w, b, y, rows, D, T, eps, s, res, ridx);
   return launch_ln16_r<EMBED, 1>(x, tok, word, pos, w, b, y, rows, D, T, eps, s, res, ridx);

@@ -48,7 +48,16 @@ def lib():
                 _error = RuntimeError(f"failed to load {SO_PATH}: {e}")
                 raise _error
             _loaded = True
+            _apply_env_knobs(torch.ops.fedrec)
     return torch.ops.fedrec
+
+
+def _apply_env_knobs(ops) -> None:
+    """Kernel-variant switches for A/B runs (unset = the measured defaults)."""
+    if os.environ.get("FEDREC_LN_WIDE"):
+        ops.ln_set_wide(int(os.environ["FEDREC_LN_WIDE"]))
+    if os.environ.get("FEDREC_GEMM_VARIANT"):
+        ops.gemm_set_variant(int(os.environ["FEDREC_GEMM_VARIANT"]))
 
 
 def require_for(t: torch.Tensor):

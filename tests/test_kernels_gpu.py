@@ -52,7 +52,7 @@ def test_layer_norm(dev):
     assert rel_err(y, ref.layer_norm(x.float(), w, b, 1e-12)) < 1e-2
 
 
-@pytest.mark.parametrize("wide", [0, 1, 2, 3])
+@pytest.mark.parametrize("wide", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("rows,D", [(1, 768), (333, 768), (77, 512), (5000, 768)])
 def test_layer_norm_forms(dev, wide, rows, D):
     x = torch.randn(rows, D, device=dev).to(torch.bfloat16) * 3 + 1
@@ -66,14 +66,14 @@ def test_layer_norm_forms(dev, wide, rows, D):
         tok = torch.randint(0, 1000, (rows,), device=dev, dtype=torch.int32)
         e = lib.embed_ln(tok.view(rows, 1), word, pos, w, b, 1e-12)
     finally:
-        lib.ln_set_wide(1)
+        lib.ln_set_wide(4)
     assert rel_err(y, ref.layer_norm(x.float(), w, b, 1e-12)) < 1e-2
     r = torch.randn(rows, D, device=dev).to(torch.bfloat16)
     lib.ln_set_wide(wide)
     try:
         yr = lib.layer_norm(x, w, b, 1e-12, r)
     finally:
-        lib.ln_set_wide(1)
+        lib.ln_set_wide(4)
     assert rel_err(yr, ref.layer_norm(x.float() + r.float(), w, b, 1e-12)) < 1e-2
     e_ref = ref.embed_ln(tok.view(rows, 1).long(), word.float(), pos.float(), w, b, 1e-12)
     assert rel_err(e, e_ref) < 1e-2
