@@ -15,6 +15,7 @@
 extern "C" {
 void fr_gemm_set_variant(int v);
 void fr_title_attn_set_waves(int w);
+void fr_title_attn_bwd_set_variant(int v);
 void fr_ln_set_wide(int v);
 int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K, int act,
                     int c_rows, hipStream_t s);
@@ -612,6 +613,7 @@ at::Tensor embed_grad(const at::Tensor& dx, const at::Tensor& sorted, const at::
 
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
+void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 
 }  // namespace
@@ -619,6 +621,7 @@ void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 TORCH_LIBRARY(fedrec, m) {
   m.def("gemm_set_variant(int v) -> ()", &gemm_set_variant);
   m.def("title_attn_set_waves(int w) -> ()", &title_attn_set_waves);
+  m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual=None) -> Tensor");

@@ -359,15 +359,23 @@ def test_device_sampler_semantics(dev):
     assert counts.min() > 0.5 * counts.mean()
 
 
+@pytest.mark.parametrize("variant", [1, 0])
 @pytest.mark.parametrize("T", [50, 64, 9, 65, 200])
-def test_title_attention_bwd(dev, T):
-    n, H, D = 5, 12, 768
+def test_title_attention_bwd(dev, T, variant):
+    """variant 1 = persistent prefetching kernel (default), 0 = one-shot; n = 120 titles (1440 pairs > 1024
+    persistent waves) so waves walk more than one (title, head) pair."""
+    n, H, D = 120, 12, 768
     qkv = torch.randn(n * T, 3 * D, device=dev).to(torch.bfloat16)
     mask = (torch.rand(n, T, device=dev) < 0.7).to(torch.int32)
     mask[:, 0] = 1
     mask[1] = 0  # all-masked row
     dout = torch.randn(n * T, D, device=dev).to(torch.bfloat16)
-    dq = native.lib().title_attention_bwd(qkv, dout, mask, H)
+    native.lib().title_attn_bwd_set_variant(variant)
+    try:
+        dq = native.lib().title_attention_bwd(qkv, dout, mask, H)
+        assert torch.equal(native.lib().title_attention_bwd(qkv, dout, mask, H), dq)
+    finally:
+        native.lib().title_attn_bwd_set_variant(1)
     x = qkv.float().detach().requires_grad_(True)
     y = ref.title_attention(x, mask, H)
     y.backward(dout.float())
