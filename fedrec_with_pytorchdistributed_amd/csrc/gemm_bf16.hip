@@ -86,6 +86,23 @@ __device__ __forceinline__ void act4(float& v0, float& v1, float& v2, float& v3)
   }
 }
 
+// residual combine: ACT 0-2 add R; ACT 3 (training FFN2 dgrad, dz = dF * GELU'(z)) multiplies
+// by GELU'(R) with R = the saved pre-activation z -- the GELU backward rides in the epilogue
+// of the GEMM that produces dF instead of a separate pass over dF and z
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
+  return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+template <int ACT>
+__device__ __forceinline__ void res4(float& v0, float& v1, float& v2, float& v3, float r0, float r1, float r2,
+                                     float r3) {
+  if constexpr (ACT == 3) {
+    v0 *= gelu_grad(r0); v1 *= gelu_grad(r1); v2 *= gelu_grad(r2); v3 *= gelu_grad(r3);
+  } else {
+    v0 += r0; v1 += r1; v2 += r2; v3 += r3;
+  }
+}
+
 // issue the glds for one K-tile into stage `st`
 __device__ __forceinline__ void stage_tile(char* smem, int st, const bf16* __restrict__ A, const bf16* __restrict__ W,
                                            int M, int K, int m0, int n0, int k0, int wave, int lane) {
@@ -177,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const bf16* __restrict_
       act4<ACT>(v0, v1, v2, v3);
       if constexpr (HAS_RES) {
         const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
-        v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+        res4<ACT>(v0, v1, v2, v3, (float)rr[0], (float)rr[1], (float)rr[2], (float)rr[3]);
       }
       bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
       *(bf16x4*)(C + (size_t)m * N + nb) = o;
@@ -305,7 +322,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256_kernel(const bf16* __restr
       act4<ACT>(v0, v1, v2, v3);
       if constexpr (HAS_RES) {
         const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
-        v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+        res4<ACT>(v0, v1, v2, v3, (float)rr[0], (float)rr[1], (float)rr[2], (float)rr[3]);
       }
       bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
       *(bf16x4*)(C + (size_t)m * N + nb) = o;
@@ -435,7 +452,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __rest
         act4<ACT>(v0, v1, v2, v3);
         if constexpr (HAS_RES) {
           const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
-          v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+          res4<ACT>(v0, v1, v2, v3, (float)rr[0], (float)rr[1], (float)rr[2], (float)rr[3]);
         }
         bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
         *(bf16x4*)(C + (size_t)m * N + nb) = o;
@@ -564,7 +581,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_256s_kernel(const bf16* __rest
         act4<ACT>(v0, v1, v2, v3);
         if constexpr (HAS_RES) {
           const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
-          v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+          res4<ACT>(v0, v1, v2, v3, (float)rr[0], (float)rr[1], (float)rr[2], (float)rr[3]);
         }
         bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
         *(bf16x4*)(C + (size_t)m * N + nb) = o;
@@ -767,8 +784,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restri
               float v2 = a4[2] + bb[p][j].z, v3 = a4[3] + bb[p][j].w;
               act4<ACT>(v0, v1, v2, v3);
               if constexpr (HAS_RES) {
-                v0 += (float)rr[i][p][j][0]; v1 += (float)rr[i][p][j][1];
-                v2 += (float)rr[i][p][j][2]; v3 += (float)rr[i][p][j][3];
+                res4<ACT>(v0, v1, v2, v3, (float)rr[i][p][j][0], (float)rr[i][p][j][1], (float)rr[i][p][j][2],
+                          (float)rr[i][p][j][3]);
               }
               if (m < M && (EPI == 0 || v0 == 1234.5f)) {
                 bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
@@ -1084,8 +1101,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
               }
               act4<ACT>(v[j][0], v[j][1], v[j][2], v[j][3]);
               if constexpr (HAS_RES) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[j][e] += (float)rr[i][p][j][e];
+                res4<ACT>(v[j][0], v[j][1], v[j][2], v[j][3], (float)rr[i][p][j][0], (float)rr[i][p][j][1],
+                          (float)rr[i][p][j][2], (float)rr[i][p][j][3]);
               }
               a4 = f32x4{0.f, 0.f, 0.f, 0.f};
             }
@@ -1257,6 +1274,10 @@ extern "C" int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, 
     case 0: launch_act<0>(a, w, bias, r, c, M, N, K, c_rows, s); break;
     case 1: launch_act<1>(a, w, bias, r, c, M, N, K, c_rows, s); break;
     case 2: launch_act<2>(a, w, bias, r, c, M, N, K, c_rows, s); break;
+    case 3:  // C = (A W^T) * GELU'(R): needs R, no bias
+      if (r == nullptr || bias != nullptr) return 2;
+      launch_act<3>(a, w, bias, r, c, M, N, K, c_rows, s);
+      break;
     default: return 2;
   }
   return 0;

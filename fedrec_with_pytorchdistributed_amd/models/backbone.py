@@ -257,6 +257,14 @@ class Backbone(nn.Module):
             a = blk.attention
             wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
             bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
+            if os.environ.get("FEDREC_TRAIN_BLOCKS", "1") != "0":  # fused block Functions (default)
+                h = OF.AttnBlockFn.apply(x, wqkv, bqkv, a.out_lin.weight, a.out_lin.bias, mask.contiguous(),
+                                         c.n_heads, L["wqkv"], L["wo"])
+                x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps)
+                h = OF.MLPBlockFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, blk.ffn.lin2.weight,
+                                        blk.ffn.lin2.bias, L["w1"], L["w2"])
+                x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
+                continue
             qkv = OF.LinearTFn.apply(x, wqkv, bqkv, None, L["wqkv"])
             ctx = OF.TitleAttentionFn.apply(qkv, mask.contiguous(), c.n_heads)
             h = OF.LinearTFn.apply(ctx, a.out_lin.weight, a.out_lin.bias, x, L["wo"])

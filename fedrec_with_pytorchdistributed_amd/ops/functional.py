@@ -238,6 +238,59 @@ class LinearGeluTFn(torch.autograd.Function):
         return dx, wgrad(dz, x), bgrad(dz), None
 
 
+class AttnBlockFn(torch.autograd.Function):
+    """``h = out_proj(attention(x Wqkv^T + bqkv)) + x`` (one post-LN block's attention half,
+    unfrozen backbone).  One Function so the residual gradient joins the QKV input gradient
+    inside the dgrad GEMM (``dh.addmm_(dqkv, Wqkv)``: beta = 1 accumulate) instead of an
+    extra bf16 add pass over [M, 768] that autograd would insert for the two uses of ``x``."""
+
+    @staticmethod
+    def forward(ctx, x, wqkv, bqkv, wo, bo, mask, heads: int, wqkv_low, wo_low):
+        qkv = ops.linear(x, wqkv_low, bqkv)
+        c = ops.title_attention(qkv, mask, heads)
+        h = ops.linear(c, wo_low, bo, residual=x)
+        ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low)
+        ctx.heads = heads
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, qkv, c, mask, wqkv_low, wo_low = ctx.saved_tensors
+        dh = dh.contiguous()
+        dwo, dbo = wgrad(dh, c), bgrad(dh)
+        dc = torch.mm(dh, wo_low)
+        dqkv = ops.native.require_for(qkv).title_attention_bwd(qkv, dc, mask, ctx.heads)
+        dwqkv, dbqkv = wgrad(dqkv, x), bgrad(dqkv)
+        dx = dh.addmm_(dqkv, wqkv_low)  # dh is ours (consumed above): residual + QKV dgrad
+        return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None
+
+
+class MLPBlockFn(torch.autograd.Function):
+    """``h = GELU(x W1^T + b1) W2^T + b2 + x`` (FFN half of a block, unfrozen backbone).
+    Backward: the GELU derivative rides in the epilogue of the GEMM that forms dF
+    (``act = 3``: ``dz = (dh W2) * GELU'(z)``, z saved by the dual-store forward GEMM), and
+    the residual gradient joins the FFN1 dgrad via ``addmm_``."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low):
+        lib = ops.native.require_for(x)
+        f, z = lib.linear_gelu_dual(x.contiguous(), w1_low, b1)
+        h = ops.linear(f, w2_low, b2, residual=x)
+        ctx.save_for_backward(x, f, z, w1_low, w2_low)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, f, z, w1_low, w2_low = ctx.saved_tensors
+        lib = ops.native.require_for(x)
+        dh = dh.contiguous()
+        dw2, db2 = wgrad(dh, f), bgrad(dh)
+        dz = lib.linear(dh, w2_low.t().contiguous(), None, 3, z)  # (dh W2) * GELU'(z), one pass
+        dw1, db1 = wgrad(dz, x), bgrad(dz)
+        dx = dh.addmm_(dz, w1_low)
+        return dx, dw1, db1, dw2, db2, None, None
+
+
 class GeluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z):

@@ -469,3 +469,26 @@ def test_backbone_long_titles_match_reference(dev):
     y_ref = ref.backbone_forward(tok.long(), mask, P, 2, 12, bb.cfg.ln_eps)
     assert torch.isfinite(y.float()).all()
     assert rel_err(y, y_ref) < 2e-2
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6, 9])
+@pytest.mark.parametrize("M", [300, 9000])
+def test_gemm_gelu_bwd_epilogue(dev, variant, M):
+    """act = 3 (training FFN2 dgrad): C = (A W^T) * GELU'(R) with R = the saved pre-activation,
+    every GEMM variant, against the fp32 product times autograd's exact-erf GELU derivative."""
+    N, K = 3072, 768
+    g = torch.Generator(device="cpu").manual_seed(M + variant)
+    a = (torch.randn(M, K, generator=g) * 0.5).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(dev, torch.bfloat16)
+    z = (torch.randn(M, N, generator=g) * 2).to(dev, torch.bfloat16)
+    lib = native.lib()
+    lib.gemm_set_variant(variant)
+    try:
+        y = lib.linear(a, w, None, 3, z)
+    finally:
+        lib.gemm_set_variant(-1)
+    zf = z.float().requires_grad_(True)
+    torch.nn.functional.gelu(zf).backward(torch.ones_like(zf))
+    ref_y = (a.float() @ w.float().t()) * zf.grad
+    assert torch.isfinite(y.float()).all()
+    assert rel_err(y, ref_y) < 1e-2
