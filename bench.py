@@ -150,7 +150,10 @@ def main() -> int:
     sync()
     t0 = time.perf_counter()
     losses = []
+    uniq = []  # unique titles per step (the backbone's work; it varies by batch and client)
     for _ in range(args.steps):
+        if pre.dedup is not None:
+            uniq.append(int(pre.dedup[0].numel()))
         losses.append(step(pre))
         pre = next_batch()  # the batch of the step after this one (K prepares per K steps)
     sync()
@@ -158,10 +161,18 @@ def main() -> int:
         dist.barrier(group=ctx.ctrl_group)
     sync()
     elapsed = time.perf_counter() - t0
+    fastest = elapsed
+    u_mean = float(np.mean(uniq)) if uniq else None
     if ctx.initialized:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
-        elapsed = float(t.item())
+        tmin = torch.tensor([fastest], dtype=torch.float64)
+        dist.all_reduce(tmin, op=dist.ReduceOp.MIN, group=ctx.ctrl_group)
+        elapsed, fastest = float(t.item()), float(tmin.item())
+        if u_mean is not None:
+            tu = torch.tensor([u_mean], dtype=torch.float64)
+            dist.all_reduce(tu, group=ctx.ctrl_group)
+            u_mean = float(tu.item()) / world
     loss = float(torch.stack(losses).float().mean())
     if ctx.initialized:  # FEDREC_COLL_CHECK=1: every client issued the same collective sequence
         from fedrec_with_pytorchdistributed_amd.parallel.collcheck import CHECK
@@ -221,6 +232,8 @@ def main() -> int:
                 "baseline_config": args.config,
             },
             "train_loss": round(loss, 5),
+            "fastest_rank_ms_per_step": round(1000.0 * fastest / args.steps, 3),
+            "unique_titles_per_step": None if u_mean is None else round(u_mean, 1),
             "grad_allreduce_ms": None if comm_ms is None else round(comm_ms, 4),
             "grad_allreduce_busbw_GBps": None if busbw is None else round(busbw, 2),
             "valid_auc": None if auc is None else round(auc, 4),
