@@ -20,7 +20,7 @@ void fr_ln_set_wide(int v);
 int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K, int act,
                     int c_rows, hipStream_t s);
 int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db, int rows, int D,
-                           float eps, hipStream_t s);
+                           float eps, hipStream_t s, float* dxs);
 int fr_gelu_bf16(const void* z, const void* dh, void* out, long n, int bwd, hipStream_t s);
 int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles, int T, int H,
                                 int D, hipStream_t s);
@@ -137,8 +137,9 @@ at::Tensor layer_norm(const at::Tensor& x, const at::Tensor& w, const at::Tensor
   return y;
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd(const at::Tensor& x, const at::Tensor& w,
-                                                               const at::Tensor& dy, double eps) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_impl(const at::Tensor& x, const at::Tensor& w,
+                                                                             const at::Tensor& dy, double eps,
+                                                                             bool want_dxsum) {
   check_dev(x, "x");
   check_dev(dy, "dy");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "fedrec::layer_norm_bwd: bf16");
@@ -148,10 +149,25 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd(const at::Tensor& 
   auto dx = at::empty_like(x);
   auto dw = at::zeros({D}, x.options().dtype(at::kFloat));
   auto db = at::zeros({D}, x.options().dtype(at::kFloat));
+  at::Tensor dxs = want_dxsum ? at::zeros({D}, x.options().dtype(at::kFloat)) : at::Tensor();
   check_rc(fr_layer_norm_bwd_bf16(x.data_ptr(), wf.data_ptr<float>(), dy.data_ptr(), dx.data_ptr(), dw.data_ptr<float>(),
-                                  db.data_ptr<float>(), (int)(x.numel() / D), (int)D, (float)eps, cur_stream()),
+                                  db.data_ptr<float>(), (int)(x.numel() / D), (int)D, (float)eps, cur_stream(),
+                                  want_dxsum ? dxs.data_ptr<float>() : nullptr),
            "layer_norm_bwd");
-  return {dx, dw, db};
+  return {dx, dw, db, dxs};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd(const at::Tensor& x, const at::Tensor& w,
+                                                               const at::Tensor& dy, double eps) {
+  auto r = layer_norm_bwd_impl(x, w, dy, eps, false);
+  return {std::get<0>(r), std::get<1>(r), std::get<2>(r)};
+}
+
+// + the column sums of dx (bias gradient of the layer feeding the LayerNorm)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_colsum(const at::Tensor& x,
+                                                                                 const at::Tensor& w,
+                                                                                 const at::Tensor& dy, double eps) {
+  return layer_norm_bwd_impl(x, w, dy, eps, true);
 }
 
 at::Tensor gelu(const at::Tensor& z, const c10::optional<at::Tensor>& dh) {
@@ -626,6 +642,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual=None) -> Tensor");
   m.def("layer_norm_bwd(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("layer_norm_bwd_colsum(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("gelu(Tensor z, Tensor? dh) -> Tensor");
   m.def("title_attention_bwd(Tensor qkv, Tensor dout, Tensor mask, int n_heads) -> Tensor");
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
@@ -655,6 +672,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("linear", &linear);
   m.impl("layer_norm", &layer_norm);
   m.impl("layer_norm_bwd", &layer_norm_bwd);
+  m.impl("layer_norm_bwd_colsum", &layer_norm_bwd_colsum);
   m.impl("gelu", &gelu);
   m.impl("title_attention_bwd", &title_attention_bwd);
   m.impl("embed_ln", &embed_ln);

@@ -317,15 +317,17 @@ bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* po
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                      const bf16* __restrict__ dy, bf16* __restrict__ dx,
                                                      float* __restrict__ dw, float* __restrict__ db, int rows, int D,
-                                                     float eps) {
-  __shared__ float red[2][4][256 * MAXC];
+                                                     float eps, float* __restrict__ dxs) {
+  // dxs (optional): column sums of the bf16 dx it writes -- the bias gradient of the linear
+  // layer that produced the LN input (config 5 training blocks), without a separate pass
+  __shared__ float red[3][4][256 * MAXC];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nc = (D + 255) >> 8;
-  float pw[MAXC][4], pb[MAXC][4];
+  float pw[MAXC][4], pb[MAXC][4], px[MAXC][4];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) pw[c][k] = pb[c][k] = 0.f;
+    for (int k = 0; k < 4; ++k) pw[c][k] = pb[c][k] = px[c][k] = 0.f;
   for (int row = blockIdx.x * 4 + wv; row < rows; row += gridDim.x * 4) {
     float v[MAXC][4], g[MAXC][4], dyv[MAXC][4];
     float s = 0.f;
@@ -382,7 +384,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x,
       if (c < nc && i < D) {
         bf16x4 o;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = f2bf(rstd * (g[c][k] - mg - v[c][k] * mgx));
+        for (int k = 0; k < 4; ++k) {
+          o[k] = f2bf(rstd * (g[c][k] - mg - v[c][k] * mgx));
+          px[c][k] += (float)o[k];
+        }
         *(bf16x4*)(dx + (size_t)row * D + i) = o;
       }
     }
@@ -393,6 +398,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x,
     for (int k = 0; k < 4; ++k) {
       red[0][wv][(c * 64 + lane) * 4 + k] = pw[c][k];
       red[1][wv][(c * 64 + lane) * 4 + k] = pb[c][k];
+      red[2][wv][(c * 64 + lane) * 4 + k] = px[c][k];
     }
   __syncthreads();
   for (int j = threadIdx.x; j < nc * 256; j += 256) {
@@ -402,6 +408,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x,
       const int idx = (c * 64 + ln) * 4 + k;
       atomicAdd(dw + i, red[0][0][idx] + red[0][1][idx] + red[0][2][idx] + red[0][3][idx]);
       atomicAdd(db + i, red[1][0][idx] + red[1][1][idx] + red[1][2][idx] + red[1][3][idx]);
+      if (dxs != nullptr) atomicAdd(dxs + i, red[2][0][idx] + red[2][1][idx] + red[2][2][idx] + red[2][3][idx]);
     }
   }
 }
@@ -444,13 +451,13 @@ __global__ __launch_bounds__(256) void gelu_kernel(const bf16* __restrict__ z, c
 extern "C" void fr_ln_set_wide(int v) { g_ln_wide = v; }
 
 extern "C" int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db,
-                                      int rows, int D, float eps, hipStream_t s) {
+                                      int rows, int D, float eps, hipStream_t s, float* dxs) {
   if (D % 4 != 0 || D > 256 * MAXC) return 1;
   if (rows == 0) return 0;
   int blocks = (rows + 3) / 4;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy, (bf16*)dx, dw, db,
-                     rows, D, eps);
+                     rows, D, eps, dxs);
   return 0;
 }
 

@@ -258,12 +258,16 @@ class Backbone(nn.Module):
             wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
             bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
             if os.environ.get("FEDREC_TRAIN_BLOCKS", "1") != "0":  # fused block Functions (default)
+                # box: each LN backward hands its dx column sums (the bias grad of the block
+                # half feeding it) to that block's backward, which runs next
+                fuse = os.environ.get("FEDREC_LN_COLSUM", "1") != "0"
+                box1, box2 = ({}, {}) if fuse else (None, None)
                 h = OF.AttnBlockFn.apply(x, wqkv, bqkv, a.out_lin.weight, a.out_lin.bias, mask.contiguous(),
-                                         c.n_heads, L["wqkv"], L["wo"])
-                x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps)
+                                         c.n_heads, L["wqkv"], L["wo"], box1)
+                x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps, box1)
                 h = OF.MLPBlockFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, blk.ffn.lin2.weight,
-                                        blk.ffn.lin2.bias, L["w1"], L["w2"])
-                x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
+                                        blk.ffn.lin2.bias, L["w1"], L["w2"], box2)
+                x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps, box2)
                 continue
             qkv = OF.LinearTFn.apply(x, wqkv, bqkv, None, L["wqkv"])
             ctx = OF.TitleAttentionFn.apply(qkv, mask.contiguous(), c.n_heads)

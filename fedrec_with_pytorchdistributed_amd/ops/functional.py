@@ -245,24 +245,26 @@ class AttnBlockFn(torch.autograd.Function):
     extra bf16 add pass over [M, 768] that autograd would insert for the two uses of ``x``."""
 
     @staticmethod
-    def forward(ctx, x, wqkv, bqkv, wo, bo, mask, heads: int, wqkv_low, wo_low):
+    def forward(ctx, x, wqkv, bqkv, wo, bo, mask, heads: int, wqkv_low, wo_low, box=None):
         qkv = ops.linear(x, wqkv_low, bqkv)
         c = ops.title_attention(qkv, mask, heads)
         h = ops.linear(c, wo_low, bo, residual=x)
         ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low)
         ctx.heads = heads
+        ctx.box = box
         return h
 
     @staticmethod
     def backward(ctx, dh):
         x, qkv, c, mask, wqkv_low, wo_low = ctx.saved_tensors
         dh = dh.contiguous()
-        dwo, dbo = wgrad(dh, c), bgrad(dh)
+        dbo = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN1's backward
+        dwo, dbo = wgrad(dh, c), (dbo if dbo is not None else bgrad(dh))
         dc = torch.mm(dh, wo_low)
         dqkv = ops.native.require_for(qkv).title_attention_bwd(qkv, dc, mask, ctx.heads)
         dwqkv, dbqkv = wgrad(dqkv, x), bgrad(dqkv)
         dx = dh.addmm_(dqkv, wqkv_low)  # dh is ours (consumed above): residual + QKV dgrad
-        return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None
+        return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None, None
 
 
 class MLPBlockFn(torch.autograd.Function):
@@ -272,11 +274,12 @@ class MLPBlockFn(torch.autograd.Function):
     the residual gradient joins the FFN1 dgrad via ``addmm_``."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low):
+    def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low, box=None):
         lib = ops.native.require_for(x)
         f, z = lib.linear_gelu_dual(x.contiguous(), w1_low, b1)
         h = ops.linear(f, w2_low, b2, residual=x)
         ctx.save_for_backward(x, f, z, w1_low, w2_low)
+        ctx.box = box
         return h
 
     @staticmethod
@@ -284,11 +287,12 @@ class MLPBlockFn(torch.autograd.Function):
         x, f, z, w1_low, w2_low = ctx.saved_tensors
         lib = ops.native.require_for(x)
         dh = dh.contiguous()
-        dw2, db2 = wgrad(dh, f), bgrad(dh)
+        db2 = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN2's backward
+        dw2, db2 = wgrad(dh, f), (db2 if db2 is not None else bgrad(dh))
         dz = lib.linear(dh, w2_low.t().contiguous(), None, 3, z)  # (dh W2) * GELU'(z), one pass
         dw1, db1 = wgrad(dz, x), bgrad(dz)
         dx = dh.addmm_(dz, w1_low)
-        return dx, dw1, db1, dw2, db2, None, None
+        return dx, dw1, db1, dw2, db2, None, None, None
 
 
 class GeluFn(torch.autograd.Function):
@@ -304,17 +308,26 @@ class GeluFn(torch.autograd.Function):
 
 
 class LayerNormFn(torch.autograd.Function):
+    """``box`` (optional dict): the backward also leaves the column sums of its dx in
+    ``box["colsum"]`` -- the bias gradient of the block Function that produced the LN input
+    and runs its backward right after (one pass instead of a separate colsum over dx)."""
+
     @staticmethod
-    def forward(ctx, x, w, b, eps: float):
+    def forward(ctx, x, w, b, eps: float, box=None):
         ctx.save_for_backward(x, w)
         ctx.eps = eps
+        ctx.box = box
         return ops.layer_norm(x, w, b, eps)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx, dw, db = ops.native.require_for(x).layer_norm_bwd(x, w, dy.contiguous(), float(ctx.eps))
-        return dx, dw, db, None
+        lib = ops.native.require_for(x)
+        if ctx.box is not None:
+            dx, dw, db, ctx.box["colsum"] = lib.layer_norm_bwd_colsum(x, w, dy.contiguous(), float(ctx.eps))
+        else:
+            dx, dw, db = lib.layer_norm_bwd(x, w, dy.contiguous(), float(ctx.eps))
+        return dx, dw, db, None, None
 
 
 class TitleAttentionFn(torch.autograd.Function):

@@ -392,6 +392,9 @@ def test_layer_norm_bwd(dev):
     w = torch.randn(768, device=dev)
     dy = torch.randn(1000, 768, device=dev).to(torch.bfloat16)
     dx, dw, db = native.lib().layer_norm_bwd(x, w, dy, 1e-12)
+    dx2, dw2, db2, dxs = native.lib().layer_norm_bwd_colsum(x, w, dy, 1e-12)
+    assert torch.equal(dx2, dx) and rel_err(dw2, dw) < 1e-5 and rel_err(db2, db) < 1e-5
+    assert rel_err(dxs, dx.float().sum(0)) < 1e-4  # fused bias gradient of the layer feeding the LN
     xf = x.float().requires_grad_(True)
     wf = w.clone().requires_grad_(True)
     bf = torch.zeros(768, device=dev, requires_grad=True)
