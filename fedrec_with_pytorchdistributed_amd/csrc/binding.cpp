@@ -40,8 +40,10 @@ int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, fl
                      int dk, hipStream_t s);
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
                 int C, int D, int sigm, hipStream_t s);
-int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, float* out, int U, int D, float clip,
-                        float noise_std, unsigned long long seed, unsigned long long offset, hipStream_t s);
+int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U, int D,
+                        int R, float* scratch, hipStream_t s);
+int fr_segsum_chunks(int R);
+void fr_segsum_set_variant(int v);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
                 unsigned long long offset, hipStream_t s);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
@@ -327,7 +329,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Te
 }
 
 at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, const at::Tensor& seg_ptr, int64_t num_out,
-                            double clip, double noise_std, int64_t seed, int64_t offset) {
+                            double clip, double noise_std, int64_t seed, int64_t offset,
+                            const c10::optional<at::Tensor>& inv) {
   check_dev(rows, "rows");
   check_dev(perm, "perm");
   check_dev(seg_ptr, "seg_ptr");
@@ -344,8 +347,17 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
                          (float)noise_std, (unsigned long long)seed, (unsigned long long)offset, cur_stream()),
              "ldp_rows");
   }
-  check_rc(fr_segment_sum_rows(src.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(),
-                               out.data_ptr<float>(), (int)num_out, (int)D, 0.f, 0.f, 0ull, 0ull, cur_stream()),
+  const int64_t R = perm.numel();
+  auto scratch = at::empty({(int64_t)fr_segsum_chunks((int)R) * 2 * D}, rows.options());
+  const int* invp = nullptr;
+  if (inv.has_value() && inv->defined()) {
+    check_dev(*inv, "inv");
+    TORCH_CHECK(inv->scalar_type() == at::kInt && inv->numel() == R, "fedrec::segment_sum_rows: inv int32[R]");
+    invp = inv->data_ptr<int>();
+  }
+  check_rc(fr_segment_sum_rows(src.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(), invp,
+                               out.data_ptr<float>(), (int)num_out, (int)D, (int)R, scratch.data_ptr<float>(),
+                               cur_stream()),
            "segment_sum_rows");
   return out;
 }
@@ -630,6 +642,7 @@ at::Tensor embed_grad(const at::Tensor& dx, const at::Tensor& sorted, const at::
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
+void segsum_set_variant(int64_t v) { fr_segsum_set_variant((int)v); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 
 }  // namespace
@@ -638,6 +651,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("gemm_set_variant(int v) -> ()", &gemm_set_variant);
   m.def("title_attn_set_waves(int w) -> ()", &title_attn_set_waves);
   m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
+  m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual=None) -> Tensor");
@@ -652,7 +666,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim) -> (Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset) -> Tensor");
+  m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None) -> Tensor");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset) -> (Tensor, Tensor)");

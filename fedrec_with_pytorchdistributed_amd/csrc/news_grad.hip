@@ -104,7 +104,113 @@ __global__ __launch_bounds__(1024) void segsum_kernel(const float* __restrict__ 
   }
 }
 
+// Chunked form (default): the one-block-per-output form above launches a 1024-thread block
+// for every unique news (~1,600 per step, most with 1-3 occurrences) and serialises the
+// ~1,000-occurrence pad row on one CU.  Here the grouped occurrence list (perm order) is cut
+// into fixed chunks of SCH positions, one wave per chunk: the wave loads all its rows at once
+// (SCH loads in flight), sums each segment run in order, and writes a segment that lies
+// wholly inside the chunk straight to out[u]; a segment crossing a chunk edge leaves a
+// partial in scratch[chunk][slot] (slot 0: started before the chunk, slot 1: ends after it).
+// A second pass sums the partials of every crossing segment in chunk order.  The chunk grid
+// is fixed by R alone, so the result is deterministic, and no float atomics are used.
+constexpr int SCH = 16;
+
+__global__ __launch_bounds__(256) void segsum_chunk_kernel(const float* __restrict__ rows, const int* __restrict__ perm,
+                                                           const int* __restrict__ seg_ptr, const int* __restrict__ inv,
+                                                           float* __restrict__ out, float* __restrict__ scratch, int U,
+                                                           int R, int D) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int p0 = c * SCH;
+  if (p0 >= R) return;
+  const int p1 = min(p0 + SCH, R);
+  int u = inv[perm[p0]];  // segment of position p0
+  float v[SCH][MAXV];
+#pragma unroll
+  for (int j = 0; j < SCH; ++j) {
+    const int pp = p0 + j;
+    const int r = perm[pp < p1 ? pp : p1 - 1];
+    const float* g = rows + (size_t)r * D;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int d = lane + 64 * k;
+      v[j][k] = d < D ? g[d] : 0.f;
+    }
+  }
+  float acc[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) acc[k] = 0.f;
+  int s_beg = seg_ptr[u], s_end = seg_ptr[u + 1];
+#pragma unroll
+  for (int j = 0; j < SCH; ++j) {
+    const int pp = p0 + j;
+    if (pp < p1) {
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) acc[k] += v[j][k];
+      if (pp + 1 == s_end || pp + 1 == p1) {  // flush the run of segment u
+        float* dst;
+        if (s_beg >= p0 && s_end <= p1) dst = out + (size_t)u * D;
+        else dst = scratch + ((size_t)c * 2 + (s_beg < p0 ? 0 : 1)) * D;
+#pragma unroll
+        for (int k = 0; k < MAXV; ++k) {
+          const int d = lane + 64 * k;
+          if (d < D) dst[d] = acc[k];
+          acc[k] = 0.f;
+        }
+        if (pp + 1 == s_end && pp + 1 < p1) {
+          ++u;
+          s_beg = s_end;
+          s_end = seg_ptr[u + 1];
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__ seg_ptr, float* __restrict__ out,
+                                                         const float* __restrict__ scratch, int U, int D) {
+  // partials of a crossing segment: [scratch[c0][1], scratch[c0+1][0], ..., scratch[c1][0]];
+  // wave w sums entries w, w+4, w+8, ... (4 loads in flight), then the 4 sums add in order --
+  // a fixed partition, so the result does not depend on timing
+  __shared__ float part[4][64 * MAXV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int u = blockIdx.x;
+  const int beg = seg_ptr[u], end = seg_ptr[u + 1];
+  const int c0 = beg / SCH, c1 = (end - 1) / SCH;
+  if (c0 == c1) return;  // written whole by the chunk pass (block-uniform exit)
+  const int n = c1 - c0 + 1;
+  float acc[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) acc[k] = 0.f;
+  for (int i0 = w; i0 < n; i0 += 16) {
+    float v[4][MAXV];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + 4 * j;
+      const size_t slot = i == 0 ? (size_t)c0 * 2 + 1 : (size_t)(c0 + i) * 2;
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) {
+        const int d = lane + 64 * k;
+        v[j][k] = (i < n && d < D) ? scratch[slot * D + d] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) acc[k] += v[j][k];
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) part[w][lane + 64 * k] = acc[k];
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += 256) out[(size_t)u * D + d] = ((part[0][d] + part[1][d]) + part[2][d]) + part[3][d];
+}
+
+int g_segsum_variant = 1;  // 1: chunked (default), 0: one block per output row
+
 }  // namespace
+
+extern "C" void fr_segsum_set_variant(int v) { g_segsum_variant = v; }
+extern "C" int fr_segsum_chunks(int R) { return (R + SCH - 1) / SCH; }
 
 extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std,
                            unsigned long long seed, unsigned long long offset, hipStream_t s) {
@@ -115,11 +221,18 @@ extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float cl
   return 0;
 }
 
-extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, float* out, int U, int D,
-                                   float clip, float noise_std, unsigned long long seed, unsigned long long offset,
-                                   hipStream_t s) {
+// scratch: fr_segsum_chunks(R) * 2 * D floats (chunked form); R = total occurrences = seg_ptr[U]
+extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out,
+                                   int U, int D, int R, float* scratch, hipStream_t s) {
   if (D > 64 * MAXV) return 1;
   if (U == 0) return 0;
+  if (g_segsum_variant == 1 && scratch != nullptr && inv != nullptr && R > 0) {
+    const int nch = (R + SCH - 1) / SCH;
+    hipLaunchKernelGGL(segsum_chunk_kernel, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out, scratch,
+                       U, R, D);
+    hipLaunchKernelGGL(segsum_fix_kernel, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
+    return 0;
+  }
   hipLaunchKernelGGL(segsum_kernel, dim3(U), dim3(1024), 0, s, rows, perm, seg_ptr, out, U, D);
   return 0;
 }

@@ -158,8 +158,11 @@ def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: floa
             perm, ptr = segments_from_inv(inv, num_out)
         else:
             perm, ptr = seg
+        inv32 = inv.reshape(-1)
+        inv32 = inv32 if inv32.dtype == torch.int32 else inv32.to(torch.int32)
         return native.require_for(rows).segment_sum_rows(rows.float().contiguous(), perm, ptr, int(num_out),
-                                                         float(clip), float(noise_std), int(seed), int(offset))
+                                                         float(clip), float(noise_std), int(seed), int(offset),
+                                                         inv32.contiguous())
     if noise_std > 0 and generator is None:
         generator = torch.Generator().manual_seed((int(seed) * 1_000_003 + int(offset)) & 0x7FFFFFFFFFFF)
     return ref.segment_sum_rows(rows, inv, num_out, clip, noise_std, generator)

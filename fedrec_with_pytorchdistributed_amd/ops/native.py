@@ -58,6 +58,8 @@ def _apply_env_knobs(ops) -> None:
         ops.ln_set_wide(int(os.environ["FEDREC_LN_WIDE"]))
     if os.environ.get("FEDREC_TAB_VARIANT"):
         ops.title_attn_bwd_set_variant(int(os.environ["FEDREC_TAB_VARIANT"]))
+    if os.environ.get("FEDREC_SEGSUM_VARIANT"):
+        ops.segsum_set_variant(int(os.environ["FEDREC_SEGSUM_VARIANT"]))
     if os.environ.get("FEDREC_GEMM_VARIANT"):
         ops.gemm_set_variant(int(os.environ["FEDREC_GEMM_VARIANT"]))
 
