@@ -42,3 +42,22 @@ def test_bench_two_clients_on_gpu(dev):
     r = json.loads(lines[0][0])
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["value"] > 0
     assert r["dtype"] == "bf16" and r["train_loss"] == r["train_loss"]  # not NaN
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,ranks", [(2, 4), (3, 2), (4, 2), (5, 2)])
+def test_bench_configs_multi_client_on_gpu(dev, config, ranks):
+    """Every BASELINE config through bench.py with several clients on one GPU (gloo data
+    plane): GA at 4 ranks, parameter averaging, LDP, and the unfrozen BERT-base with secure
+    aggregation (pairwise masks over the store, int32 all-reduce)."""
+    argv = ["bench.py", "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--preset", "small", "--valid-limit", "32",
+            "--config", str(config), "--pa-every", "1"]
+    if config == 5:
+        argv += ["--batch", "16"]
+    outs = run_ranks([argv] * ranks, SHARE, timeout=600)
+    _ok(outs)
+    lines = [l for l in outs[0][1].splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == ranks and r["config"]["baseline_config"] == config
+    assert r["value"] > 0 and r["train_loss"] == r["train_loss"]
