@@ -82,7 +82,7 @@ class LocalEngine:
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
         # trainable parameters; everything that does calls sync_params() first
-        ov = cfg.overlap_optimizer
+        ov = os.environ.get("FEDREC_OVERLAP_OPTIMIZER", cfg.overlap_optimizer)  # env: A/B runs
         self.overlap = device.type == "cuda" and cfg.backbone.frozen and (
             ov == "on" or (ov == "auto" and grad_allreduce is not None))
         self._side = torch.cuda.Stream(device) if self.overlap else None
