@@ -351,15 +351,31 @@ class LocalEngine:
         self.sync_params()
         self.model.eval()
         scores_all, losses = [], []
+        # the parameters do not change during validation, so every news vector is a constant:
+        # when the batches would encode more titles than the corpus holds (a full validation
+        # split: >= 5 titles per impression, popular titles in every batch), encode each title
+        # ONCE into a table and gather -- per-title results are the same either way (every
+        # kernel computes a title's rows independently of the rest of the batch)
+        n_imp = len(self.shard.valid) if limit is None else min(limit, len(self.shard.valid))
+        table = None
+        if self.news_table is not None:
+            table = self.news_table
+        elif (os.environ.get("FEDREC_VALID_TABLE", "1") == "2"  # 0: never, 1: auto (default), 2: always
+              or (os.environ.get("FEDREC_VALID_TABLE", "1") == "1" and n_imp * (self.cfg.npratio + 1) > self.N)):
+            table = self.encode_all(grad=False)
+            self.model.eval()
         for cand_np, his_np in validation_batches(self.shard.valid, batch_size, self.cfg.npratio,
                                                   self.cfg.max_his_len, not self.q.no_history_truncation,
                                                   limit):
             cand, his = self.to_device(cand_np), self.to_device(his_np)
             B, C = cand.shape
             ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
-            uniq, inv, _, _ = ops.dedup(ids, self.N)
-            v = self.news_vectors(uniq, grad=False)
-            rows = v.index_select(0, inv.long())
+            if table is not None:
+                rows = table.index_select(0, ids.long())
+            else:
+                uniq, inv, _, _ = ops.dedup(ids, self.N)
+                v = self.news_vectors(uniq, grad=False)
+                rows = v.index_select(0, inv.long())
             cand_v = rows[: B * C].view(B, C, -1)
             his_v = rows[B * C:].view(B, his.shape[1], -1)
             u = self.model.user_encoder(his_v, his)

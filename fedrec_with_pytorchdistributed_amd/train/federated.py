@@ -255,13 +255,18 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         eng.sigma = _maybe_dp(cfg, eng)
         eng.epoch = 0
         tr, va = {}, {}
+        t_train = t_valid = 0.0
         for _ in range(cfg.total_epochs):  # Trainer(...).train(total_epochs) per round (client.py:283-284)
+            t0 = time.perf_counter()
             tr = eng.train_epoch(step_hook=beat)
             beat()
+            t1 = time.perf_counter()
             va = eng.validate()
             beat()
-        meta = {"client": k, "n_train": len(shard.train), **{m: float(v) for m, v in {**tr, **va}.items()
-                                                             if isinstance(v, (int, float))}}
+            t_train += t1 - t0
+            t_valid += time.perf_counter() - t1
+        meta = {"client": k, "n_train": len(shard.train), "train_s": t_train, "valid_s": t_valid,
+                **{m: float(v) for m, v in {**tr, **va}.items() if isinstance(v, (int, float))}}
         up = _client_upload_tensor(model, cfg).clone()
         if cfg.round_artifacts:  # client.py:288 torch.save(model.state_dict(), "model.pt")
             sub = "" if ctx.num_clients == 1 else f"client{k}"
@@ -379,7 +384,8 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
             model.flat.flat.copy_(new)
         dt = time.perf_counter() - t0
         rec = {"round": r, "clients_accepted": len(accepted), "clients": W, "clients_dead": dead, "round_s": dt}
-        for key in ("training_loss", "validation_loss", "valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):
+        for key in ("training_loss", "validation_loss", "valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10",
+                    "train_s", "valid_s"):
             vals = [m[key] for m in metas if key in m]
             if vals:
                 rec[key] = float(np.mean(vals))

@@ -189,3 +189,22 @@ def test_mask_padding_step_on_gpu(dev):
         assert not torch.equal(before, m.flat.flat)
     assert all(torch.isfinite(torch.tensor(v)) for v in losses.values())
     assert losses[True] != losses[False]
+
+
+def test_validation_news_table_matches_per_batch(dev, monkeypatch):
+    """Validation with one news table per pass (every title encoded once, then gathered) gives
+    the per-batch path's scores: the parameters are fixed during validation and every kernel
+    computes a title independently of the rest of its batch."""
+    cfg = _cfg()
+    torch.manual_seed(0)
+    m = FedRecModel(cfg).to(dev)
+    m.build_flat()
+    eng = LocalEngine(cfg, m, make_client_shards("tiny", 1)[0], dev)
+    monkeypatch.setenv("FEDREC_VALID_TABLE", "0")
+    a = eng.validate(batch_size=64)
+    monkeypatch.setenv("FEDREC_VALID_TABLE", "2")
+    b = eng.validate(batch_size=64)
+    assert a["n_valid"] == b["n_valid"] > 0
+    for k in ("valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):
+        assert abs(a[k] - b[k]) < 1e-4, (k, a[k], b[k])
+    assert abs(a["validation_loss"] - b["validation_loss"]) < 1e-4
