@@ -65,7 +65,7 @@ int fr_embed_ln_rows_bf16(const int* tokens, const int* src, const void* word, c
                           const float* b, void* y, int rows, int D, int T, float eps, hipStream_t s);
 int fr_layer_norm_scatter_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
                                const void* res, const int* dst, hipStream_t s);
-int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s);
+int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s, int ld);
 int fr_colsum_chunks();
 int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* C, void* Z, int M, int N, int K,
                          int c_rows, hipStream_t s);
@@ -610,14 +610,20 @@ std::tuple<at::Tensor, at::Tensor> linear_gelu_dual(const at::Tensor& x, const a
 
 // ---- training-path reductions (train_grad.hip) ----------------------------------------------
 at::Tensor colsum(const at::Tensor& x) {
-  check_dev(x, "x");
+  TORCH_CHECK(x.is_cuda(), "fedrec::colsum: x must be a device tensor");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::colsum: bf16");
   const c10::DeviceGuard g(x.device());
+  // contiguous [.., N], or a 2-D column slice with unit column stride (row stride = ld)
+  const bool strided = x.dim() == 2 && x.stride(1) == 1 && x.stride(0) != x.size(1);
+  TORCH_CHECK(strided || x.is_contiguous(), "fedrec::colsum: contiguous rows or a 2-D column slice");
   const int64_t N = x.size(-1), M = x.numel() / N;
+  const int64_t ld = strided ? x.stride(0) : N;
+  TORCH_CHECK(((uintptr_t)x.data_ptr()) % 16 == 0, "fedrec::colsum: 16-byte aligned rows");
   auto out = at::empty({N}, x.options().dtype(at::kFloat));
   if (M == 0) return out.zero_();
   auto partial = at::empty({(int64_t)fr_colsum_chunks() * N}, x.options().dtype(at::kFloat));
-  check_rc(fr_colsum_bf16(x.data_ptr(), (int)M, (int)N, partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream()),
+  check_rc(fr_colsum_bf16(x.data_ptr(), (int)M, (int)N, partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream(),
+                          (int)ld),
            "colsum");
   return out;
 }

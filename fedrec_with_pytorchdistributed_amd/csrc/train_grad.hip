@@ -17,7 +17,7 @@ constexpr int CS_MAX_CHUNKS = 256;
 // stride over the chunk's rows (4 rows in flight per wave); partial[chunk][n].  chunks is
 // chosen so the grid has ~1024 blocks whatever N is.
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restrict__ x, int M, int N,
-                                                             float* __restrict__ partial) {
+                                                             float* __restrict__ partial, int ld) {
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c0 = blockIdx.x * 512 + lane * 8;
@@ -27,15 +27,15 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restr
   if (c0 < N) {
     int r = r0 + wave;
     for (; r + 12 < r1; r += 16) {
-      const bf16x8 a = *(const bf16x8*)(x + (size_t)r * N + c0);
-      const bf16x8 b = *(const bf16x8*)(x + (size_t)(r + 4) * N + c0);
-      const bf16x8 c = *(const bf16x8*)(x + (size_t)(r + 8) * N + c0);
-      const bf16x8 d = *(const bf16x8*)(x + (size_t)(r + 12) * N + c0);
+      const bf16x8 a = *(const bf16x8*)(x + (size_t)r * ld + c0);
+      const bf16x8 b = *(const bf16x8*)(x + (size_t)(r + 4) * ld + c0);
+      const bf16x8 c = *(const bf16x8*)(x + (size_t)(r + 8) * ld + c0);
+      const bf16x8 d = *(const bf16x8*)(x + (size_t)(r + 12) * ld + c0);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += ((float)a[k] + (float)b[k]) + ((float)c[k] + (float)d[k]);
     }
     for (; r < r1; r += 4) {
-      const bf16x8 a = *(const bf16x8*)(x + (size_t)r * N + c0);
+      const bf16x8 a = *(const bf16x8*)(x + (size_t)r * ld + c0);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += (float)a[k];
     }
@@ -151,13 +151,15 @@ __global__ __launch_bounds__(1024) void embed_grad_heavy_kernel(const bf16* __re
 }  // namespace
 
 // partial: fr_colsum_chunks() * N floats of scratch
-extern "C" int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s) {
-  if (N % 8 != 0 || M <= 0) return 1;
+// ld: row stride in elements (>= N, a multiple of 8: e.g. the Q third of a [M, 3D] tensor)
+extern "C" int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s, int ld) {
+  if (ld <= 0) ld = N;
+  if (N % 8 != 0 || ld % 8 != 0 || ld < N || M <= 0) return 1;
   const int cb = (N + 511) / 512;
   int chunks = 1024 / cb;
   chunks = chunks < 16 ? 16 : (chunks > CS_MAX_CHUNKS ? CS_MAX_CHUNKS : chunks);
   chunks = chunks < M ? chunks : M;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cb, chunks), dim3(256), 0, s, (const bf16*)x, M, N, partial);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cb, chunks), dim3(256), 0, s, (const bf16*)x, M, N, partial, ld);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, partial, N, chunks, out);
   return 0;
 }

@@ -238,6 +238,9 @@ class LinearGeluTFn(torch.autograd.Function):
         return dx, wgrad(dz, x), bgrad(dz), None
 
 
+_QKV_BIAS_SHORTCUT = __import__("os").environ.get("FEDREC_QKV_BIAS_SHORTCUT", "1") != "0"
+
+
 class AttnBlockFn(torch.autograd.Function):
     """``h = out_proj(attention(x Wqkv^T + bqkv)) + x`` (one post-LN block's attention half,
     unfrozen backbone).  One Function so the residual gradient joins the QKV input gradient
@@ -249,20 +252,30 @@ class AttnBlockFn(torch.autograd.Function):
         qkv = ops.linear(x, wqkv_low, bqkv)
         c = ops.title_attention(qkv, mask, heads)
         h = ops.linear(c, wo_low, bo, residual=x)
-        ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low)
+        ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low, wo)
         ctx.heads = heads
         ctx.box = box
         return h
 
     @staticmethod
     def backward(ctx, dh):
-        x, qkv, c, mask, wqkv_low, wo_low = ctx.saved_tensors
+        x, qkv, c, mask, wqkv_low, wo_low, wo = ctx.saved_tensors
         dh = dh.contiguous()
         dbo = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN1's backward
         dwo, dbo = wgrad(dh, c), (dbo if dbo is not None else bgrad(dh))
         dc = torch.mm(dh, wo_low)
         dqkv = ops.native.require_for(qkv).title_attention_bwd(qkv, dc, mask, ctx.heads)
-        dwqkv, dbqkv = wgrad(dqkv, x), bgrad(dqkv)
+        dwqkv = wgrad(dqkv, x)
+        if _QKV_BIAS_SHORTCUT and dqkv.is_cuda:
+            # column sums of dQ | dK | dV without reading dK and dV: every softmax row sums to
+            # one, so sum_s dV_s = sum_t dctx_t = dbo Wo; and sum_s dS_ts = 0 for every query
+            # (shift invariance), so the key-bias gradient is identically zero
+            Dm = wo.shape[0]
+            dbqkv = torch.cat([ops.native.require_for(dqkv).colsum(dqkv[:, :Dm]),
+                               torch.zeros(Dm, device=dqkv.device, dtype=torch.float32),
+                               (dbo.float().unsqueeze(0) @ wo.float()).squeeze(0)])
+        else:
+            dbqkv = bgrad(dqkv)
         dx = dh.addmm_(dqkv, wqkv_low)  # dh is ours (consumed above): residual + QKV dgrad
         return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None, None
 
