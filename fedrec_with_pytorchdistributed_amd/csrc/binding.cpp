@@ -66,6 +66,8 @@ int fr_embed_ln_rows_bf16(const int* tokens, const int* src, const void* word, c
 int fr_layer_norm_scatter_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
                                const void* res, const int* dst, hipStream_t s);
 int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s, int ld);
+int fr_gemm_gelu_bwd_colpart(const void* A, const void* W, const void* Z, void* C, float* colpart, int M, int N, int K,
+                             int c_rows, hipStream_t s);
 int fr_colsum_chunks();
 int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* C, void* Z, int M, int N, int K,
                          int c_rows, hipStream_t s);
@@ -609,6 +611,30 @@ std::tuple<at::Tensor, at::Tensor> linear_gelu_dual(const at::Tensor& x, const a
 }
 
 // ---- training-path reductions (train_grad.hip) ----------------------------------------------
+// dz = (dh W^T) * GELU'(z) and its column sums (FFN1 bias gradient) from one GEMM pass;
+// returns (dz, colsum) -- colsum is undefined when the shape is outside the fused kernel's
+// domain (the caller then sums dz itself)
+std::tuple<at::Tensor, at::Tensor> linear_gelu_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& z) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  check_dev(z, "z");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && z.scalar_type() == at::kBFloat16,
+              "fedrec::linear_gelu_bwd: bf16");
+  const c10::DeviceGuard g(x.device());
+  const int64_t K = x.size(-1), N = w.size(0), M = x.numel() / K;
+  TORCH_CHECK(w.size(1) == K && z.numel() == M * N, "fedrec::linear_gelu_bwd: shapes");
+  const int64_t c_rows = (M + 255) / 256 * 256;
+  auto out = at::empty({c_rows * N}, x.options()).narrow(0, 0, M * N).view({M, N});
+  auto part = at::empty({c_rows / 256 * 2, N}, x.options().dtype(at::kFloat));
+  const int rc = fr_gemm_gelu_bwd_colpart(x.data_ptr(), w.data_ptr(), z.data_ptr(), out.data_ptr(),
+                                          part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)c_rows, cur_stream());
+  if (rc == 0) return {out, part.sum(0)};
+  check_rc(fr_gemm_nt_bf16(x.data_ptr(), w.data_ptr(), nullptr, z.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K, 3,
+                           (int)c_rows, cur_stream()),
+           "linear_gelu_bwd");
+  return {out, at::Tensor()};
+}
+
 at::Tensor colsum(const at::Tensor& x) {
   TORCH_CHECK(x.is_cuda(), "fedrec::colsum: x must be a device tensor");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::colsum: bf16");
@@ -660,6 +686,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
+  m.def("linear_gelu_bwd(Tensor x, Tensor w, Tensor z) -> (Tensor, Tensor)");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual=None) -> Tensor");
   m.def("layer_norm_bwd(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layer_norm_bwd_colsum(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -690,6 +717,7 @@ TORCH_LIBRARY(fedrec, m) {
 
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("linear", &linear);
+  m.impl("linear_gelu_bwd", &linear_gelu_bwd);
   m.impl("layer_norm", &layer_norm);
   m.impl("layer_norm_bwd", &layer_norm_bwd);
   m.impl("layer_norm_bwd_colsum", &layer_norm_bwd_colsum);

@@ -851,7 +851,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
                                                              int N, int K, int tiles_n, int ntiles,
                                                              const int* __restrict__ full_rows = nullptr,
-                                                             int tiles_np = 0, bf16* __restrict__ Z = nullptr) {
+                                                             int tiles_np = 0, bf16* __restrict__ Z = nullptr,
+                                                             float* __restrict__ colpart = nullptr) {
+  // colpart (ACT 3, training FFN2 dgrad): per-(row tile, wave row) column sums of the dz the
+  // epilogue writes, [tiles_m * 2, N] -- the FFN1 bias gradient without a pass over dz
   // DUAL (training FFN1): the epilogue also stores the pre-activation z = acc + bias to Z
   // (the GELU backward needs it), so no separate activation pass reads z back
   // ONE __shared__ object (staging halves + the bias vector): a second one makes hipcc drain
@@ -1070,6 +1073,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
 #pragma unroll
           for (int j = 0; j < 2; ++j) bb[p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+      float csum[2][2][4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) csum[p][j][e] = 0.f;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         bf16x4 rr[4][2][2];
@@ -1104,10 +1114,43 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
                 res4<ACT>(v[j][0], v[j][1], v[j][2], v[j][3], (float)rr[i][p][j][0], (float)rr[i][p][j][1],
                           (float)rr[i][p][j][2], (float)rr[i][p][j][3]);
               }
+              if constexpr (ACT == 3) {
+                if (colpart != nullptr && m < M) {  // padded rows (m >= M) hold duplicates: excluded
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) csum[p][j][e] += v[j][e];
+                }
+              }
               a4 = f32x4{0.f, 0.f, 0.f, 0.f};
             }
             store_pair16(C + (size_t)m * N + n0 + wc * 64 + p * 32, v[0], v[1], fq);
             if constexpr (DUAL) store_pair16(Z + (size_t)m * N + n0 + wc * 64 + p * 32, zv[0], zv[1], fq);
+          }
+        }
+      }
+      if constexpr (ACT == 3) {
+        if (colpart != nullptr) {
+          // rows of this wave are (fr, i, q): sum the 16 fr lanes; lane fr == 0 of each fq
+          // group then holds 16 column sums -> 4 x 16-byte stores
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float x = csum[p][j][e];
+                x += __shfl_xor(x, 1, 64);
+                x += __shfl_xor(x, 2, 64);
+                x += __shfl_xor(x, 4, 64);
+                x += __shfl_xor(x, 8, 64);
+                csum[p][j][e] = x;
+              }
+          if (fr == 0) {
+            float* cp = colpart + (size_t)((m0 >> 8) * 2 + wr) * N + n0 + wc * 64 + fq * 4;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+                *(float4*)(cp + p * 32 + j * 16) = make_float4(csum[p][j][0], csum[p][j][1], csum[p][j][2], csum[p][j][3]);
           }
         }
       }
@@ -1319,6 +1362,28 @@ extern "C" int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* 
 
 // Training FFN1: C = GELU(A W^T + bias) and Z = A W^T + bias from one pass (variant-9 kernel,
 // its domain only: returns 3 otherwise and the caller runs GEMM + separate GELU).
+// Training FFN2 dgrad with the GELU derivative and the FFN1 bias gradient: C = (A W^T) *
+// GELU'(Z) and colpart[tiles_m * 2, N] = per-(row tile, wave row) column sums of C (summed on
+// the host side in a fixed order).  Variant-9 kernel only: returns 3 outside its domain.
+extern "C" int fr_gemm_gelu_bwd_colpart(const void* A, const void* W, const void* Z, void* C, float* colpart, int M,
+                                        int N, int K, int c_rows, hipStream_t s) {
+  const bool ok = (g_gemm_variant == 9 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 && N <= PP2_MAXN &&
+                  K >= 128 && K % BK == 0 && c_rows >= ((M + 255) / 256) * 256 &&
+                  (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31);
+  if (!ok) return 3;
+  const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
+  if (g_num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  const int G = ntiles < g_num_cus ? ntiles : g_num_cus;
+  hipLaunchKernelGGL((gemm_nt_pp2_kernel<3, false, true>), dim3(G), dim3(512), 0, s, (const bf16*)A, (const bf16*)W,
+                     nullptr, (const bf16*)Z, (bf16*)C, M, N, K, tiles_n, ntiles, nullptr, 0, nullptr, colpart);
+  return 0;
+}
+
 extern "C" int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* C, void* Z, int M, int N, int K,
                                     int c_rows, hipStream_t s) {
   const bool ok = (g_gemm_variant == 9 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 && N <= PP2_MAXN &&

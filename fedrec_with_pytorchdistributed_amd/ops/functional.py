@@ -238,6 +238,7 @@ class LinearGeluTFn(torch.autograd.Function):
         return dx, wgrad(dz, x), bgrad(dz), None
 
 
+_DZ_COLSUM_OFF = __import__("os").environ.get("FEDREC_DZ_COLSUM", "1") == "0"  # A/B runs
 _QKV_BIAS_SHORTCUT = __import__("os").environ.get("FEDREC_QKV_BIAS_SHORTCUT", "1") != "0"
 
 
@@ -302,8 +303,11 @@ class MLPBlockFn(torch.autograd.Function):
         dh = dh.contiguous()
         db2 = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN2's backward
         dw2, db2 = wgrad(dh, f), (db2 if db2 is not None else bgrad(dh))
-        dz = lib.linear(dh, w2_low.t().contiguous(), None, 3, z)  # (dh W2) * GELU'(z), one pass
-        dw1, db1 = wgrad(dz, x), bgrad(dz)
+        # (dh W2) * GELU'(z) and its column sums (the FFN1 bias gradient) from one GEMM pass
+        dz, db1 = lib.linear_gelu_bwd(dh, w2_low.t().contiguous(), z)
+        dw1 = wgrad(dz, x)
+        if db1 is None or _DZ_COLSUM_OFF:
+            db1 = bgrad(dz)
         dx = dh.addmm_(dz, w1_low)
         return dx, dw1, db1, dw2, db2, None, None, None
 

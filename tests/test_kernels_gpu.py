@@ -521,3 +521,24 @@ def test_gemm_gelu_bwd_epilogue(dev, variant, M):
     ref_y = (a.float() @ w.float().t()) * zf.grad
     assert torch.isfinite(y.float()).all()
     assert rel_err(y, ref_y) < 1e-2
+
+
+@pytest.mark.parametrize("M", [300, 9000, 78850])
+def test_linear_gelu_bwd_with_colsum(dev, M):
+    """Training FFN2 dgrad op: dz = (dh W^T) * GELU'(z) plus the FFN1 bias gradient (column sums
+    of dz) from the same GEMM pass; small M falls back to the plain kernels (colsum None)."""
+    N, K = 3072, 768
+    g = torch.Generator(device="cpu").manual_seed(M)
+    a = (torch.randn(M, K, generator=g) * 0.5).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(dev, torch.bfloat16)
+    z = (torch.randn(M, N, generator=g) * 2).to(dev, torch.bfloat16)
+    lib = native.lib()
+    dz, cs = lib.linear_gelu_bwd(a, w, z)
+    assert torch.equal(dz, lib.linear(a, w, None, 3, z))
+    if M >= 4096:
+        assert cs is not None
+        assert rel_err(cs, dz.float().sum(0)) < 2e-3
+        dz2, cs2 = lib.linear_gelu_bwd(a, w, z)
+        assert torch.equal(cs2, cs)  # deterministic partials + fixed-order sum
+    else:
+        assert cs is None
