@@ -165,9 +165,13 @@ def test_overlapped_optimizer_matches_serial(dev):
         eng.sync_params()
         torch.cuda.synchronize(dev)
         out[mode] = m.flat.flat.clone()
-    base = float((out["off2"] - out["off"]).abs().max())
-    diff = float((out["on"] - out["off"]).abs().max())
-    assert diff <= max(2 * base, 1e-6) + 1e-5, (diff, base)
+    # L2 norms over every trainable parameter: Adam turns the run-to-run noise of parameters
+    # whose gradient is ~0 (e.g. the key biases: softmax shift invariance) into full +-lr
+    # steps, so a max-abs statistic is one noisy sample; a race (parameters read mid-update)
+    # would move the whole vector, far beyond the serial schedule's own spread
+    base = float((out["off2"] - out["off"]).norm())
+    diff = float((out["on"] - out["off"]).norm())
+    assert diff <= 3 * base + 1e-4, (diff, base)
 
 
 def test_mask_padding_step_on_gpu(dev):
