@@ -66,6 +66,8 @@ int fr_embed_ln_rows_bf16(const int* tokens, const int* src, const void* word, c
 int fr_layer_norm_scatter_bf16(const void* x, const float* w, const float* b, void* y, int rows, int D, float eps,
                                const void* res, const int* dst, hipStream_t s);
 int fr_colsum_bf16(const void* x, int M, int N, float* partial, float* out, hipStream_t s, int ld);
+int fr_gelu_bwd_colsum_bf16(const void* df, const void* z, void* dz, int M, int N, float* partial, float* out,
+                            hipStream_t s);
 int fr_gemm_gelu_bwd_colpart(const void* A, const void* W, const void* Z, void* C, float* colpart, int M, int N, int K,
                              int c_rows, hipStream_t s);
 int fr_colsum_chunks();
@@ -635,6 +637,24 @@ std::tuple<at::Tensor, at::Tensor> linear_gelu_bwd(const at::Tensor& x, const at
   return {out, at::Tensor()};
 }
 
+// streaming GELU backward + its column sums: (dz, colsum)
+std::tuple<at::Tensor, at::Tensor> gelu_bwd_colsum(const at::Tensor& df, const at::Tensor& z) {
+  check_dev(df, "df");
+  check_dev(z, "z");
+  TORCH_CHECK(df.scalar_type() == at::kBFloat16 && z.scalar_type() == at::kBFloat16 && df.numel() == z.numel(),
+              "fedrec::gelu_bwd_colsum: bf16, same shape");
+  const c10::DeviceGuard g(df.device());
+  const int64_t N = df.size(-1), M = df.numel() / N;
+  auto dz = at::empty_like(df);
+  auto out = at::zeros({N}, df.options().dtype(at::kFloat));
+  if (M == 0) return {dz, out};
+  auto partial = at::empty({(int64_t)fr_colsum_chunks() * N}, df.options().dtype(at::kFloat));
+  check_rc(fr_gelu_bwd_colsum_bf16(df.data_ptr(), z.data_ptr(), dz.data_ptr(), (int)M, (int)N,
+                                   partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream()),
+           "gelu_bwd_colsum");
+  return {dz, out};
+}
+
 at::Tensor colsum(const at::Tensor& x) {
   TORCH_CHECK(x.is_cuda(), "fedrec::colsum: x must be a device tensor");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::colsum: bf16");
@@ -687,6 +707,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("linear_gelu_bwd(Tensor x, Tensor w, Tensor z) -> (Tensor, Tensor)");
+  m.def("gelu_bwd_colsum(Tensor df, Tensor z) -> (Tensor, Tensor)");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual=None) -> Tensor");
   m.def("layer_norm_bwd(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layer_norm_bwd_colsum(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -718,6 +739,7 @@ TORCH_LIBRARY(fedrec, m) {
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("linear", &linear);
   m.impl("linear_gelu_bwd", &linear_gelu_bwd);
+  m.impl("gelu_bwd_colsum", &gelu_bwd_colsum);
   m.impl("layer_norm", &layer_norm);
   m.impl("layer_norm_bwd", &layer_norm_bwd);
   m.impl("layer_norm_bwd_colsum", &layer_norm_bwd_colsum);

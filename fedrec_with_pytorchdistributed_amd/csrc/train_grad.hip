@@ -51,6 +51,64 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restr
 
 // 64 columns per block, the 16 waves split the chunks (<= 16 loads per lane), fixed-order
 // LDS combine
+// GELU backward with the column sums of its output (training FFN1: dz = dF * GELU'(z) and
+// the FFN1 bias gradient) in one streaming pass -- same grid / partials as colsum, so the
+// sums are deterministic.  GELU' with erf from Abramowitz-Stegun 7.1.26 (|err| <= 1.5e-7).
+__device__ __forceinline__ float gelu_grad_s(float x) {
+  const float z = x * 0.70710678118654752f, az = fabsf(z);
+  const float t = __frcp_rn(1.0f + 0.3275911f * az);
+  const float y = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float erfv = copysignf(1.0f - y * __expf(-az * az), z);
+  return 0.5f * (1.0f + erfv) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_colsum_partial_kernel(const bf16* __restrict__ df,
+                                                                      const bf16* __restrict__ zz,
+                                                                      bf16* __restrict__ dz, int M, int N,
+                                                                      float* __restrict__ partial) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + lane * 8;
+  const int rows_per = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < N) {
+    int r = r0 + wave;
+    for (; r + 4 < r1; r += 8) {  // two rows in flight per wave
+      const size_t o0 = (size_t)r * N + c0, o1 = (size_t)(r + 4) * N + c0;
+      const bf16x8 g0 = *(const bf16x8*)(df + o0), z0 = *(const bf16x8*)(zz + o0);
+      const bf16x8 g1 = *(const bf16x8*)(df + o1), z1 = *(const bf16x8*)(zz + o1);
+      bf16x8 d0, d1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        d0[k] = f2bf((float)g0[k] * gelu_grad_s((float)z0[k]));
+        d1[k] = f2bf((float)g1[k] * gelu_grad_s((float)z1[k]));
+        acc[k] += (float)d0[k] + (float)d1[k];
+      }
+      *(bf16x8*)(dz + o0) = d0;
+      *(bf16x8*)(dz + o1) = d1;
+    }
+    for (; r < r1; r += 4) {
+      const size_t o0 = (size_t)r * N + c0;
+      const bf16x8 g0 = *(const bf16x8*)(df + o0), z0 = *(const bf16x8*)(zz + o0);
+      bf16x8 d0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        d0[k] = f2bf((float)g0[k] * gelu_grad_s((float)z0[k]));
+        acc[k] += (float)d0[k];
+      }
+      *(bf16x8*)(dz + o0) = d0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[wave][lane * 8 + k] = acc[k];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int c = blockIdx.x * 512 + i;
+    if (c < N) partial[(size_t)blockIdx.y * N + c] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
 __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ partial, int N, int chunks,
                                                             float* __restrict__ out) {
   __shared__ float red[16][64];
@@ -165,6 +223,20 @@ extern "C" int fr_colsum_bf16(const void* x, int M, int N, float* partial, float
 }
 
 extern "C" int fr_colsum_chunks() { return CS_MAX_CHUNKS; }
+
+// dz = df * GELU'(z) (bf16 [M, N], contiguous) and out[N] = column sums of dz
+extern "C" int fr_gelu_bwd_colsum_bf16(const void* df, const void* z, void* dz, int M, int N, float* partial,
+                                       float* out, hipStream_t s) {
+  if (N % 8 != 0 || M <= 0) return 1;
+  const int cb = (N + 511) / 512;
+  int chunks = 2048 / cb;
+  chunks = chunks < 16 ? 16 : (chunks > CS_MAX_CHUNKS ? CS_MAX_CHUNKS : chunks);
+  chunks = chunks < M ? chunks : M;
+  hipLaunchKernelGGL(gelu_bwd_colsum_partial_kernel, dim3(cb, chunks), dim3(256), 0, s, (const bf16*)df,
+                     (const bf16*)z, (bf16*)dz, M, N, partial);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, partial, N, chunks, out);
+  return 0;
+}
 
 // dword must be zeroed by the caller (rows of tokens absent from the batch stay zero);
 // scratch: R + 1 ints (heavy list + its count, zeroed by the caller)

@@ -238,7 +238,7 @@ class LinearGeluTFn(torch.autograd.Function):
         return dx, wgrad(dz, x), bgrad(dz), None
 
 
-_DZ_COLSUM_OFF = __import__("os").environ.get("FEDREC_DZ_COLSUM", "1") == "0"  # A/B runs
+_DZ_MODE = __import__("os").environ.get("FEDREC_DZ_MODE", "gemm")  # gemm | stream (A/B runs)
 _QKV_BIAS_SHORTCUT = __import__("os").environ.get("FEDREC_QKV_BIAS_SHORTCUT", "1") != "0"
 
 
@@ -303,11 +303,18 @@ class MLPBlockFn(torch.autograd.Function):
         dh = dh.contiguous()
         db2 = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN2's backward
         dw2, db2 = wgrad(dh, f), (db2 if db2 is not None else bgrad(dh))
-        # (dh W2) * GELU'(z) and its column sums (the FFN1 bias gradient) from one GEMM pass
-        dz, db1 = lib.linear_gelu_bwd(dh, w2_low.t().contiguous(), z)
+        if _DZ_MODE == "gemm":
+            # (dh W2) * GELU'(z) and its column sums from our GEMM's epilogue in one pass (the
+            # aux-input epilogue makes that GEMM 650 us vs 480 for the forward FFN1 shape; the
+            # "stream" form measured the same step time: bench_r1_cfg5_dzmode_ab.jsonl)
+            dz, db1 = lib.linear_gelu_bwd(dh, w2_low.t().contiguous(), z)
+            if db1 is None:
+                db1 = bgrad(dz)
+        else:
+            # library dF GEMM, then one streaming pass: dz = dF * GELU'(z) and its column sums
+            # (the FFN1 bias gradient), deterministic partials
+            dz, db1 = lib.gelu_bwd_colsum(torch.mm(dh, w2_low), z)
         dw1 = wgrad(dz, x)
-        if db1 is None or _DZ_COLSUM_OFF:
-            db1 = bgrad(dz)
         dx = dh.addmm_(dz, w1_low)
         return dx, dw1, db1, dw2, db2, None, None, None
 

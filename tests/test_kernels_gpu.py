@@ -542,3 +542,19 @@ def test_linear_gelu_bwd_with_colsum(dev, M):
         assert torch.equal(cs2, cs)  # deterministic partials + fixed-order sum
     else:
         assert cs is None
+
+
+@pytest.mark.parametrize("M,N", [(78850, 3072), (300, 3072), (5, 64)])
+def test_gelu_bwd_colsum(dev, M, N):
+    """Streaming training-FFN1 backward: dz = dF * GELU'(z) (exact-erf autograd reference) and
+    its column sums (the FFN1 bias gradient), deterministic."""
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    df = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    z = (torch.randn(M, N, generator=g) * 2).to(dev, torch.bfloat16)
+    dz, cs = native.lib().gelu_bwd_colsum(df, z)
+    zf = z.float().requires_grad_(True)
+    torch.nn.functional.gelu(zf).backward(df.float())
+    assert rel_err(dz, zf.grad) < 5e-3
+    assert rel_err(cs, dz.float().sum(0)) < 1e-5
+    dz2, cs2 = native.lib().gelu_bwd_colsum(df, z)
+    assert torch.equal(dz2, dz) and torch.equal(cs2, cs)
