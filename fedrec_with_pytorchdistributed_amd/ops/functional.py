@@ -16,6 +16,9 @@ from .. import ops
 from .reference import _f
 
 
+_WGRAD_TILES = int(__import__("os").environ.get("FEDREC_WGRAD_TILES", "512"))  # split-K target (A/B runs)
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
     """``dy^T x`` in fp32 for ``dy [M, N]``, ``x [M, K]`` with a long reduction dim M.
 
@@ -29,7 +32,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
     # enough split-K chunks for ~2 output tiles per CU (the library tiles 256x256), no more:
     # every chunk adds an [N, K] fp32 partial that the final sum reads back
     tiles = -(-dy.shape[1] // 256) * -(-x.shape[1] // 256)
-    splits = min(splits, max(1, -(-512 // tiles)))
+    splits = min(splits, max(1, -(-_WGRAD_TILES // tiles)))
     S = max(1, min(splits, M // 2048))
     if S == 1:
         return torch.mm(dy.t(), x, out_dtype=torch.float32)
