@@ -246,13 +246,13 @@ class LocalEngine:
             out[s:s + len(ids)] = self.model.text_encoder(text).float()
         return out
 
-    def accumulate_step(self, cand: torch.Tensor, his: torch.Tensor) -> torch.Tensor:
+    def accumulate_step(self, cand: torch.Tensor, his: torch.Tensor, pre: Optional[Prepared] = None) -> torch.Tensor:
         """``per_epoch`` schedule: user grads + per-news gradient table, no optimizer step."""
         self.model.train()
         if self.q.grad_double_last_batch:
             self.flat.grad.zero_()  # Q2: optimizer.zero_grad() each batch (client.py:75)
         self.model.text_encoder.eval()  # gen_news_vecs runs the text encoder in eval (model.py:42)
-        uniq, v, cand_v, his_v = self._forward_rows(cand, his, grad_news=False)
+        uniq, v, cand_v, his_v = self._forward_rows(cand, his, grad_news=False, pre=pre)
         u = self.model.user_encoder(his_v, his)
         loss, _ = OF.score_ce(cand_v, u, self.score_act)
         loss.backward()
@@ -308,21 +308,18 @@ class LocalEngine:
         if sched == "per_epoch":
             self._begin_epoch_accumulate()
         it = iter(self.sampler.epoch(self.epoch))
-        nxt = self._next_prepared(it) if sched == "per_step" else None
+        nxt = self._next_prepared(it)
         while True:
+            pre = nxt
+            if pre is None:
+                break
             if sched == "per_step":
-                pre = nxt
-                if pre is None:
-                    break
                 loss = self.train_prepared(pre)
-                # sample + dedup the next batch while this step's kernels run
-                last = max_steps is not None and n + 1 >= max_steps
-                nxt = None if last else self._next_prepared(it)
             else:
-                b = next(it, None)
-                if b is None:
-                    break
-                loss = self.accumulate_step(self.to_device(b[0]), self.to_device(b[1]))
+                loss = self.accumulate_step(pre.cand, pre.his, pre)
+            # sample + dedup the next batch while this step's kernels run (both schedules)
+            last = max_steps is not None and n + 1 >= max_steps
+            nxt = None if last else self._next_prepared(it)
             losses.append(loss)
             n += 1
             if step_hook is not None:
