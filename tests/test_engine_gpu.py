@@ -159,19 +159,27 @@ def test_overlapped_optimizer_matches_serial(dev):
         m = FedRecModel(cfg).to(dev)
         m.build_flat()
         eng = LocalEngine(cfg, m, shard, dev)
+        init = m.flat.flat.detach().clone()
         assert eng.overlap == (mode == "on")
         for c, h in list(eng.sampler.epoch(0))[:6]:
             eng.train_step(eng.to_device(c), eng.to_device(h))
         eng.sync_params()
         torch.cuda.synchronize(dev)
         out[mode] = m.flat.flat.clone()
-    # L2 norms over every trainable parameter: Adam turns the run-to-run noise of parameters
-    # whose gradient is ~0 (e.g. the key biases: softmax shift invariance) into full +-lr
-    # steps, so a max-abs statistic is one noisy sample; a race (parameters read mid-update)
-    # would move the whole vector, far beyond the serial schedule's own spread
-    base = float((out["off2"] - out["off"]).norm())
-    diff = float((out["on"] - out["off"]).norm())
-    assert diff <= 3 * base + 1e-4, (diff, base)
+        m0 = init.to(dev)
+    # Parameters whose gradient is identically ~0 (softmax shift invariance: the score biases
+    # att_fc2.bias and the user-attention key bias W_K.bias) are left out: Adam turns the
+    # rounding noise of a ~1e-9 gradient into full +-lr steps of random sign, so they carry
+    # no signal about the schedule.  Over the rest (L2), a race -- parameters read
+    # mid-update -- would move the whole vector far beyond the serial schedule's own spread.
+    keep = torch.zeros_like(out["off"], dtype=torch.bool)
+    for name, p, off in m.flat.views():
+        if not (name.endswith("att_fc2.bias") or name.endswith("W_K.bias")):
+            keep[off:off + p.numel()] = True
+    base = float((out["off2"] - out["off"])[keep].norm())
+    diff = float((out["on"] - out["off"])[keep].norm())
+    ref = float((out["off"] - m0)[keep].norm())  # how far 6 steps move the parameters
+    assert diff <= 3 * base + 1e-4 * ref, (diff, base, ref)
 
 
 def test_mask_padding_step_on_gpu(dev):
