@@ -1,0 +1,78 @@
+"""Summarise rocprofv3 ``--pmc`` passes (scripts/gpu_pmc_cfg2.sh) per kernel family.
+
+Each pass is its own run of the same short bench, so counters are joined per kernel family
+(summed over that family's dispatches), not per dispatch.  Derived metrics:
+
+* ``clock_GHz``     GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time (DVFS-lowered clock)
+* ``mfma_util``     SQ_VALU_MFMA_BUSY_CYCLES / (clock cycles x 256 CUs x 4 SIMDs)
+* ``lds_conflict``  SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles per LDS-array cycle)
+* ``hbm_TBps``      (FETCH_SIZE + WRITE_SIZE) [KB] / kernel wall time
+
+Usage: python benchmarks/pmc_summary.py gpurun_out/pmc2 > profiles/pmc_r1_cfg2.json
+"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def family(name: str) -> str:
+    m = re.search(r"gemm_nt_pp2_kernel<(\d)", name)
+    if m:
+        return {"0": "gemm_pp2 (QKV / out-proj / FFN2, bias)", "1": "gemm_pp2 + GELU (FFN1)"}.get(m.group(1), "gemm_pp2")
+    for key, fam in (("ln16p_kernel", "layernorm (persistent, + residual)"),
+                     ("title_attn_packed_kernel", "title attention (packed)"),
+                     ("gemm_nt_kernel", "gemm_nt 128x128 (text head)"),
+                     ("dedup_kernel", "dedup (lookahead)"), ("sample_kernel", "sample (lookahead)"),
+                     ("Cijk_", "hipBLASLt / rocBLAS"), ("user_attn", "user attention"),
+                     ("pool_", "additive pool"), ("adam_kernel", "adam")):
+        if key in name:
+            return fam
+    return "other"
+
+
+def load(path: str):
+    per = defaultdict(lambda: defaultdict(float))
+    dur = defaultdict(dict)  # family -> dispatch -> ns
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            fam = family(r["Kernel_Name"])
+            per[fam][r["Counter_Name"]] += float(r["Counter_Value"])
+            dur[fam][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return per, {k: sum(v.values()) for k, v in dur.items()}, {k: len(v) for k, v in dur.items()}
+
+
+def main(d: str) -> None:
+    out = defaultdict(dict)
+    for p in ("p1", "p2", "p3"):
+        fn = os.path.join(d, f"{p}_counter_collection.csv")
+        if not os.path.exists(fn):
+            continue
+        per, dur, n = load(fn)
+        for fam, cs in per.items():
+            out[fam].update(cs)
+            out[fam][f"wall_ns_{p}"] = dur[fam]
+            out[fam]["dispatches"] = n[fam]
+    res = {}
+    for fam, c in out.items():
+        r = dict(c)
+        w1 = c.get("wall_ns_p1", 0)
+        if w1 and "GRBM_GUI_ACTIVE" in c:
+            clk = c["GRBM_GUI_ACTIVE"] / 8 / w1  # cycles per ns = GHz
+            r["clock_GHz"] = round(clk, 3)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+                r["mfma_util"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (clk * w1 * 256 * 4), 4)
+        if c.get("SQ_LDS_IDX_ACTIVE"):
+            r["lds_conflict"] = round(c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"], 4)
+        if "FETCH_SIZE" in c and c.get("wall_ns_p2"):
+            r["read_TBps"] = round(c["FETCH_SIZE"] * 1024 / c["wall_ns_p2"] / 1e3, 3)
+        if "WRITE_SIZE" in c and c.get("wall_ns_p3"):
+            r["write_TBps"] = round(c["WRITE_SIZE"] * 1024 / c["wall_ns_p3"] / 1e3, 3)
+        res[fam] = r
+    print(json.dumps(dict(sorted(res.items(), key=lambda kv: -kv[1].get("wall_ns_p1", 0))), indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc2")
