@@ -27,7 +27,11 @@ def family(name: str) -> str:
                      ("gemm_nt_kernel", "gemm_nt 128x128 (text head)"),
                      ("dedup_kernel", "dedup (lookahead)"), ("sample_kernel", "sample (lookahead)"),
                      ("Cijk_", "hipBLASLt / rocBLAS"), ("user_attn", "user attention"),
-                     ("pool_", "additive pool"), ("adam_kernel", "adam")):
+                     ("pool_", "additive pool"), ("adam_kernel", "adam"),
+                     ("ldp_rows_kernel", "LDP clip + Philox noise (config 4)"),
+                     ("segsum_chunk_kernel", "news-grad segment sum (chunked)"),
+                     ("segsum_fix_kernel", "news-grad segment sum edge fix-up"),
+                     ("segsum_kernel", "news-grad segment sum")):
         if key in name:
             return fam
     return "other"
