@@ -150,7 +150,13 @@ class FedRecConfig:
 
     # --- engine ------------------------------------------------------------------------
     precision: str = "bf16"  # backbone compute dtype: bf16 | fp32
-    news_cache: str = "none"  # none | vectors  (HBM-resident per-epoch news table, §7.1)
+    # HBM-resident cache of the frozen backbone's hidden states [N, T, D]:
+    # auto = on for a frozen backbone on the device when the table fits in a quarter of the
+    # free HBM; hidden = always (also on the host); none = re-encode the batch's titles
+    news_cache: str = "auto"  # auto | hidden | none   ("vectors" = hidden + epoch_news_table on)
+    # per_epoch schedule: the news vectors are constant within a local epoch (the head only
+    # steps at epoch end), so encode the whole news table once per epoch and gather rows
+    epoch_news_table: str = "auto"  # auto (= on when the hidden cache is) | on | off
     device_sampler: bool = True  # GPU: negative sampling + batch assembly by the HIP sampler
     # per-step GA: run the gradient all-reduce + Adam on a side stream, overlapped with the next
     # step's (parameter-free) frozen-backbone forward.  auto = GPU + all-reduce + frozen backbone

@@ -81,6 +81,7 @@ class Backbone(nn.Module):
         self.transformer = _Transformer(c)
         self._pack: Optional[Dict] = None
         self._pack_key = None
+        self.version = 0  # bumped whenever the weights may have changed (hidden-state caches key on it)
         self.reset_parameters()
 
     # -------------------------------------------------------------------------------
@@ -102,6 +103,7 @@ class Backbone(nn.Module):
 
     def invalidate(self) -> None:
         self._pack = None
+        self.version += 1
 
     def _load_from_state_dict(self, *args, **kwargs):  # keep the compute pack coherent
         self.invalidate()

@@ -3,11 +3,15 @@
 Replaces the reference's ``train_on_step`` / ``UserModel.forward/collect/update`` hot path
 (``client.py:61-101``, ``model.py:41-129``) with a device-resident design:
 
-* the client's token table ``bert_news_index`` ``[N, 2, T]`` lives in HBM;
+* the client's token table ``bert_news_index`` ``[N, 2, T]`` lives in HBM, and so (frozen
+  backbone, ``news_cache``) do the backbone's last hidden states of every title
+  (:mod:`.news_cache`): DistilBERT runs once per title per training run instead of once per
+  occurrence per step (``model.py:41-61``) and again in the replay (``model.py:83-87``);
 * each step de-duplicates the batch's news ids on the device (the reference re-encodes
-  every occurrence: only 39 of 324 titles were unique in E8), encodes the unique titles
-  once, gathers rows for candidates/history, and scatters the per-occurrence gradients
-  back with a deterministic segment sum (``client.py:26-48``) -- LDP clip + noise fused;
+  every occurrence: only 39 of 324 titles were unique in E8), runs the trainable head on
+  the unique titles' cached hidden states, gathers rows for candidates/history, and
+  scatters the per-occurrence gradients back with a deterministic segment sum
+  (``client.py:26-48``) -- LDP clip + noise fused;
 * no host round trip for vectors or gradients (K08, K15 removed).
 
 Two update schedules (Q3):
@@ -19,7 +23,7 @@ Two update schedules (Q3):
     news vectors are fixed within a local epoch (computed in eval mode, ``model.py:42``);
     per-news gradients accumulate in an HBM table ``G [N, 400]``; at epoch end the head
     VJP replays ``G`` over the touched news (``model.py:72-90``) and both encoders take one
-    Adam step (``model.py:66-70``).  ``news_cache=vectors`` precomputes the whole news
+    Adam step (``model.py:66-70``).  ``epoch_news_table`` precomputes the whole news
     table once per epoch (exact: the head is constant within the epoch).
 """
 from __future__ import annotations
@@ -40,6 +44,7 @@ from ..eval.metrics import batch_metrics
 from ..models.fedrec_model import FedRecModel
 from ..ops import functional as OF
 from ..utils import obs
+from .news_cache import HiddenCache
 
 
 class Prepared(NamedTuple):
@@ -77,7 +82,10 @@ class LocalEngine:
         self.G: Optional[torch.Tensor] = None
         self.touched: Optional[torch.Tensor] = None
         self.news_table: Optional[torch.Tensor] = None
-        self.replay_chunk = 1024
+        self.hcache = self._make_hidden_cache()
+        self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
+                            or (cfg.epoch_news_table == "auto" and self.hcache is not None))
+        self.replay_chunk = 4096 if self.hcache is not None else 1024
         self.last_stats: Dict[str, float] = {}
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
@@ -92,6 +100,32 @@ class LocalEngine:
         # backbone's M) no longer drains the GPU at every step start
         lookahead = device.type == "cuda" and os.environ.get("FEDREC_LOOKAHEAD", "1") != "0"
         self._prep = torch.cuda.Stream(device) if lookahead else None
+
+    def _make_hidden_cache(self) -> Optional[HiddenCache]:
+        """The HBM hidden-state cache when the config asks for it and it fits."""
+        mode = self.cfg.news_cache
+        if mode == "none" or not self.cfg.backbone.frozen:
+            return None
+        te = self.model.text_encoder
+        if mode in ("auto", "vectors"):
+            if self.device.type != "cuda":
+                return None
+            need = HiddenCache.nbytes_for(self.N, self.tokens.shape[2], self.cfg.backbone.dim, te.compute_dtype)
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if need > free // 4:
+                obs.log(f"[rank {self.rank}] hidden-state cache off: {need / 2**30:.1f} GiB > 1/4 of "
+                        f"{free / 2**30:.1f} GiB free")
+                return None
+        elif mode != "hidden":
+            raise ValueError(f"news_cache={mode!r}: expected auto | hidden | none | vectors")
+        return HiddenCache(te, self.tokens)
+
+    def build_cache(self) -> Optional[float]:
+        """(Re)build the hidden-state cache now; returns its build time in seconds (None: no cache)."""
+        if self.hcache is None:
+            return None
+        self.sync_params()
+        return self.hcache.build()
 
     # -------------------------------------------------------------------------------
     @property
@@ -120,17 +154,27 @@ class LocalEngine:
             torch.cuda.current_stream(self.device).wait_event(self._params_ready)
             self._params_ready = None
 
+    def _hidden(self, ids: torch.Tensor):
+        """Backbone hidden states ``[n, T, D]`` of titles ``ids`` and their token masks (the
+        mask only when the head uses it).  From the HBM cache when it is on; otherwise the
+        frozen / unfrozen backbone runs on the titles."""
+        if self.hcache is not None:
+            hid = self.hcache.rows(ids)
+            mask = self.tokens.index_select(0, ids.long())[:, 1, :] if self.cfg.mask_padding else None
+            return hid, mask
+        text = self.tokens.index_select(0, ids.long())
+        return self.model.text_encoder.hidden(text), text[:, 1, :]
+
     def news_vectors(self, uniq: torch.Tensor, grad: bool) -> torch.Tensor:
         te = self.model.text_encoder
         if not grad and self.news_table is not None:
             return self.news_table.index_select(0, uniq.long())
-        text = self.tokens.index_select(0, uniq.long())
-        hid = te.hidden(text)  # frozen backbone: overlaps the previous step's all-reduce + Adam
+        hid, mask = self._hidden(uniq)  # parameter-free: overlaps the previous step's all-reduce + Adam
         self.sync_params()
         if grad:
-            return te.head(hid, text[:, 1, :])
+            return te.head(hid, mask)
         with torch.no_grad():
-            return te.head(hid, text[:, 1, :])
+            return te.head(hid, mask)
 
     # -------------------------------------------------------------------------------
     def prepare(self, batch_fn: Callable[[], Tuple]) -> Prepared:
@@ -175,7 +219,7 @@ class LocalEngine:
     def forward_backward(self, cand: torch.Tensor, his: torch.Tensor, pre: Optional[Prepared] = None) -> torch.Tensor:
         """Loss of one batch with every trainable gradient left in ``flat.grad``."""
         self.model.train()
-        if self.cfg.news_cache == "vectors" or not self.cfg.backbone.frozen:
+        if self.epoch_table or not self.cfg.backbone.frozen:
             self.sync_params()
         self.flat.begin_backward()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True, pre=pre)
@@ -232,7 +276,7 @@ class LocalEngine:
         self.G = torch.zeros(self.N, D, dtype=torch.float32, device=self.device)
         self.touched = torch.zeros(self.N, dtype=torch.bool, device=self.device)
         self.flat.zero_grad()
-        if self.cfg.news_cache == "vectors":
+        if self.epoch_table:
             self.news_table = self.encode_all(grad=False)
 
     @torch.no_grad()
@@ -242,8 +286,8 @@ class LocalEngine:
         out = torch.empty(self.N, self.cfg.news_dim, dtype=torch.float32, device=self.device)
         for s in range(0, self.N, chunk):
             ids = torch.arange(s, min(s + chunk, self.N), device=self.device, dtype=torch.int32)
-            text = self.tokens.index_select(0, ids.long())
-            out[s:s + len(ids)] = self.model.text_encoder(text).float()
+            hid, mask = self._hidden(ids)
+            out[s:s + len(ids)] = self.model.text_encoder.head(hid, mask).float()
         return out
 
     def accumulate_step(self, cand: torch.Tensor, his: torch.Tensor, pre: Optional[Prepared] = None) -> torch.Tensor:
@@ -272,13 +316,20 @@ class LocalEngine:
         self.flat.grad.mul_(user_scale)  # only user grads are non-zero at this point
         ids = torch.nonzero(self.touched).reshape(-1).to(torch.int32)
         te = self.model.text_encoder
-        te.train(self.q.replay_train_mode)
+        # Q4 (compat): the reference replays the text encoder in train mode (model.py:73), i.e.
+        # re-runs DistilBERT with dropout on the touched titles; the default is the exact
+        # eval-mode VJP over the hidden states the vectors were computed from (E10)
+        train_mode = self.q.replay_train_mode
+        te.train(train_mode)
         for s in range(0, ids.numel(), self.replay_chunk):
             cid = ids[s:s + self.replay_chunk]
-            text = self.tokens.index_select(0, cid.long())
             with obs.range("replay"):
-                hid = te.hidden(text)  # compat Q4 would re-run with dropout (train mode)
-                v = te.head(hid, text[:, 1, :])
+                if train_mode:
+                    text = self.tokens.index_select(0, cid.long())
+                    hid, mask = te.hidden(text), text[:, 1, :]
+                else:
+                    hid, mask = self._hidden(cid)
+                v = te.head(hid, mask)
                 v.backward(self.G.index_select(0, cid.long()) * head_scale)
         self.optimizer_step()
         self.G = None

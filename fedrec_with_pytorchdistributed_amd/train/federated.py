@@ -102,11 +102,19 @@ def _min_over_clients(ctx: DistContext, x: int) -> int:
     return int(t.item())
 
 
+def _backbone_synced(model: FedRecModel, full: bool) -> None:
+    """Parameters were overwritten by a collective: the backbone changed iff it was part of
+    the synced set (``sync=full``, or an unfrozen backbone is trainable), and only then do
+    its compute pack and the HBM hidden-state cache have to be rebuilt."""
+    if full or not model.cfg.backbone.frozen:
+        model.text_encoder.DistillBert.invalidate()
+
+
 def _sync_initial(model: FedRecModel, ctx: DistContext, full: bool) -> None:
     """DDP-style start: every client takes client 0's parameters (X6, one bucketed call)."""
     if ctx.initialized and ctx.num_clients > 1:
         comm.broadcast_(model.sync_tensors(full), src=ctx.client_ranks[0], group=ctx.data_group)
-        model.text_encoder.DistillBert.invalidate()
+        _backbone_synced(model, full)
 
 
 def _maybe_dp(cfg: FedRecConfig, eng: LocalEngine) -> Optional[float]:
@@ -182,7 +190,7 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
         if ctx.initialized and W > 1:
             with obs.range("param_allreduce"):
                 comm.allreduce_(model.sync_tensors(full), ctx.data_group, scale=1.0 / W)
-            model.text_encoder.DistillBert.invalidate()
+            _backbone_synced(model, full)
 
     hook = (lambda n: average() if n % K == 0 else None) if K else None
     last = {}
@@ -251,7 +259,7 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         if full:
             bb = cp.get_tensor(f"r{r}/backbone")
             _load_flat_backbone(model, bb)
-        model.text_encoder.DistillBert.invalidate()
+        _backbone_synced(model, full)
         eng.sigma = _maybe_dp(cfg, eng)
         eng.epoch = 0
         tr, va = {}, {}
