@@ -39,7 +39,13 @@ class BackboneConfig:
     hidden_dim: int = 3072
     max_position: int = 512
     ln_eps: float = 1e-12
+    # HF DistilBERT train-mode dropout (Philox counter masks, ops.dropout_add / title attention):
+    # `dropout` after the embedding LayerNorm and after FFN lin2, `attention_dropout` on the
+    # attention probabilities.  Active in the unfrozen training forward (config 5) and in the
+    # reference-compat train-mode replay (Q4); the frozen backbone's vectors are eval-mode
+    # (model.py:42), so its hidden-state cache never sees dropout.
     dropout: float = 0.1
+    attention_dropout: float = 0.1
     frozen: bool = True  # reference freezes DistilBERT (model.py:25-26)
     init_std: float = 0.02
     # local Hugging Face checkpoint (directory from save_pretrained, or one weights file) of

@@ -75,6 +75,13 @@ int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* 
                          int c_rows, hipStream_t s);
 int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword, int* scratch,
                        hipStream_t s);
+int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
+                        unsigned long long offset, hipStream_t s);
+int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
+                                 float pdrop, unsigned long long seed, unsigned long long offset, hipStream_t s);
+int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles,
+                                     int T, int H, int D, float pdrop, unsigned long long seed,
+                                     unsigned long long offset, hipStream_t s);
 }
 
 namespace {
@@ -202,6 +209,59 @@ at::Tensor title_attention_bwd(const at::Tensor& qkv, const at::Tensor& dout, co
   check_rc(fr_title_attention_bwd_bf16(qkv.data_ptr(), dout.data_ptr(), mk.data_ptr<int>(), dqkv.data_ptr(), (int)n,
                                        (int)T, (int)n_heads, (int)D, cur_stream()),
            "title_attention_bwd");
+  return dqkv;
+}
+
+// ---- dropout (backbone train mode; dropout.hip, title_attn*.hip) ------------------------------
+at::Tensor dropout_add(const at::Tensor& h, const c10::optional<at::Tensor>& res, double p, int64_t seed,
+                       int64_t offset) {
+  check_dev(h, "h");
+  TORCH_CHECK(h.scalar_type() == at::kBFloat16, "fedrec::dropout_add: bf16");
+  const c10::DeviceGuard g(h.device());
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_dev(*res, "res");
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->numel() == h.numel(), "fedrec::dropout_add: res");
+    rp = res->data_ptr();
+  }
+  auto out = at::empty_like(h);
+  check_rc(fr_dropout_add_bf16(h.data_ptr(), rp, out.data_ptr(), (long)h.numel(), (float)p, (unsigned long long)seed,
+                               (unsigned long long)offset, cur_stream()),
+           "dropout_add");
+  return out;
+}
+
+at::Tensor title_attention_drop(const at::Tensor& qkv, const at::Tensor& mask, int64_t n_heads, double p, int64_t seed,
+                                int64_t offset) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16, "fedrec::title_attention_drop: bf16");
+  const c10::DeviceGuard g(qkv.device());
+  auto mk = mask.to(at::kInt).contiguous();
+  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
+  TORCH_CHECK(qkv.numel() == n * T * 3 * D, "fedrec::title_attention_drop: qkv shape");
+  auto out = at::empty({n * T, D}, qkv.options());
+  check_rc(fr_title_attention_drop_bf16(qkv.data_ptr(), mk.data_ptr<int>(), out.data_ptr(), (int)n, (int)T,
+                                        (int)n_heads, (int)D, (float)p, (unsigned long long)seed,
+                                        (unsigned long long)offset, cur_stream()),
+           "title_attention_drop");
+  return out;
+}
+
+at::Tensor title_attention_bwd_drop(const at::Tensor& qkv, const at::Tensor& dout, const at::Tensor& mask,
+                                    int64_t n_heads, double p, int64_t seed, int64_t offset) {
+  check_dev(qkv, "qkv");
+  check_dev(dout, "dout");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && dout.scalar_type() == at::kBFloat16,
+              "fedrec::title_attention_bwd_drop");
+  const c10::DeviceGuard g(qkv.device());
+  auto mk = mask.to(at::kInt).contiguous();
+  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
+  TORCH_CHECK(qkv.numel() == n * T * 3 * D && dout.numel() == n * T * D, "fedrec::title_attention_bwd_drop: shapes");
+  auto dqkv = at::empty_like(qkv);
+  check_rc(fr_title_attention_bwd_drop_bf16(qkv.data_ptr(), dout.data_ptr(), mk.data_ptr<int>(), dqkv.data_ptr(),
+                                            (int)n, (int)T, (int)n_heads, (int)D, (float)p, (unsigned long long)seed,
+                                            (unsigned long long)offset, cur_stream()),
+           "title_attention_bwd_drop");
   return dqkv;
 }
 
@@ -734,6 +794,9 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
+  m.def("dropout_add(Tensor h, Tensor? res, float p, int seed, int offset) -> Tensor");
+  m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
+  m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
@@ -766,4 +829,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("colsum", &colsum);
   m.impl("linear_gelu_dual", &linear_gelu_dual);
   m.impl("embed_grad", &embed_grad);
+  m.impl("dropout_add", &dropout_add);
+  m.impl("title_attention_drop", &title_attention_drop);
+  m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);
 }

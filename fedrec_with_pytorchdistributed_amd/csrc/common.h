@@ -79,6 +79,17 @@ static __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // (0, 1]
   return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
 }
 
+// Dropout (HF train mode): element e of a dropout site keeps with probability 1-p
+// and is scaled by 1/(1-p).  The mask is a pure function of (seed, offset, e): Philox counter
+// e >> 2, component e & 3, keep iff unit(x) > p -- so a backward kernel regenerates exactly
+// the forward's mask and the torch oracle (ops/reference.py philox4x32) reproduces it bit for bit.
+static __device__ __forceinline__ float drop_scale(uint32_t x, float p, float inv_keep) {
+  return u32_to_unit(x) > p ? inv_keep : 0.f;
+}
+static __device__ __forceinline__ uint32_t u4_get(const uint4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
 // Box-Muller: two standard normals from two uniforms
 static __device__ __forceinline__ float2 box_muller(uint32_t a, uint32_t b) {
   float u1 = u32_to_unit(a), u2 = u32_to_unit(b);

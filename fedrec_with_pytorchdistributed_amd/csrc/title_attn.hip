@@ -25,9 +25,13 @@ namespace {
 
 constexpr int DH = 64;
 
-template <int NWAVE>
+// DROP: HF attention-probability dropout (train mode): P_ts *= keep(pair, t, s) / (1 - p) with the
+// Philox mask of element ((pair * 64 + t) * 64 + s) -- title_attn_bwd.hip regenerates it
+template <int NWAVE, bool DROP>
 __global__ __launch_bounds__(64 * NWAVE) void title_attn_kernel(const bf16* __restrict__ qkv, const int* __restrict__ mask,
-                                                                bf16* __restrict__ out, int n_titles, int T, int H, int D) {
+                                                                bf16* __restrict__ out, int n_titles, int T, int H, int D,
+                                                                float pdrop, unsigned long long seed,
+                                                                unsigned long long offset) {
   __shared__ __attribute__((aligned(16))) bf16 vs[NWAVE][64 * DH];  // 8 KB per wave
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pair = blockIdx.x * NWAVE + wave;
@@ -112,6 +116,16 @@ __global__ __launch_bounds__(64 * NWAVE) void title_attn_kernel(const bf16* __re
       }
     l = group4_sum(l);
     const float inv = 1.0f / l;
+    if constexpr (DROP) {
+      const float inv_keep = 1.0f / (1.0f - pdrop);
+      const int t = jq * 16 + fr;
+#pragma unroll
+      for (int is = 0; is < 4; ++is) {
+        const uint4 rnd = Philox::gen(seed, offset, ((unsigned long long)pair * 64 + t) * 16 + is * 4 + fq);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[is][jq][r] *= drop_scale(u4_get(rnd, r), pdrop, inv_keep);
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 f;
@@ -658,13 +672,26 @@ extern "C" int fr_title_attention_bf16(const void* qkv, const int* mask, void* o
       hipLaunchKernelGGL((title_attn_pkernel<1, 1>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, mask, (bf16*)out, pairs, T,
                          H, D);
   } else if (w == 1)
-    hipLaunchKernelGGL(title_attn_kernel<1>, dim3(pairs), dim3(64), 0, s, (const bf16*)qkv, mask, (bf16*)out, n_titles, T, H, D);
+    hipLaunchKernelGGL((title_attn_kernel<1, false>), dim3(pairs), dim3(64), 0, s, (const bf16*)qkv, mask, (bf16*)out,
+                       n_titles, T, H, D, 0.f, 0ull, 0ull);
   else if (w == 4)
-    hipLaunchKernelGGL(title_attn_kernel<4>, dim3((pairs + 3) / 4), dim3(256), 0, s, (const bf16*)qkv, mask, (bf16*)out,
-                       n_titles, T, H, D);
+    hipLaunchKernelGGL((title_attn_kernel<4, false>), dim3((pairs + 3) / 4), dim3(256), 0, s, (const bf16*)qkv, mask,
+                       (bf16*)out, n_titles, T, H, D, 0.f, 0ull, 0ull);
   else
-    hipLaunchKernelGGL(title_attn_kernel<2>, dim3((pairs + 1) / 2), dim3(128), 0, s, (const bf16*)qkv, mask, (bf16*)out,
-                       n_titles, T, H, D);
+    hipLaunchKernelGGL((title_attn_kernel<2, false>), dim3((pairs + 1) / 2), dim3(128), 0, s, (const bf16*)qkv, mask,
+                       (bf16*)out, n_titles, T, H, D, 0.f, 0ull, 0ull);
+  return 0;
+}
+
+// train-mode forward with attention-probability dropout (T <= 64; 2 = unsupported shape)
+extern "C" int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H,
+                                            int D, float pdrop, unsigned long long seed, unsigned long long offset,
+                                            hipStream_t s) {
+  if (T < 1 || T > 64 || D != H * DH || !(pdrop > 0.f && pdrop < 1.f)) return 2;
+  const int pairs = n_titles * H;
+  if (pairs == 0) return 0;
+  hipLaunchKernelGGL((title_attn_kernel<2, true>), dim3((pairs + 1) / 2), dim3(128), 0, s, (const bf16*)qkv, mask,
+                     (bf16*)out, n_titles, T, H, D, pdrop, seed, offset);
   return 0;
 }
 

@@ -29,11 +29,15 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16* base_lo, const bf16* base_
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+// DROP: the forward applied P~ = P o Z (Z = keep / (1 - p), title_attn.hip's Philox mask), so
+// dP = (dO V^T) o Z, D_t = sum_s P_ts dP_ts, dS as below, and dV = P~^T dO
+template <bool DROP>
 __global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __restrict__ qkv,
                                                                   const bf16* __restrict__ dout,
                                                                   const int* __restrict__ mask,
                                                                   bf16* __restrict__ dqkv, int n_titles, int T, int H,
-                                                                  int D) {
+                                                                  int D, float pdrop, unsigned long long seed,
+                                                                  unsigned long long offset) {
   __shared__ __attribute__((aligned(16))) bf16 lds[WPB][4][64 * DH];  // Q, K, dO, P^T/dS^T scratch
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pair = blockIdx.x * WPB + wave;
@@ -124,19 +128,36 @@ __global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __
       }
     l = group4_sum(l);
     const float inv = 1.0f / l;
+    float z[4][4];
+#pragma unroll
+    for (int is = 0; is < 4; ++is) {
+      if constexpr (DROP) {
+        const uint4 rnd = Philox::gen(seed, offset, ((unsigned long long)pair * 64 + jq * 16 + fr) * 16 + is * 4 + fq);
+        const float inv_keep = 1.0f / (1.0f - pdrop);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[is][r] = drop_scale(u4_get(rnd, r), pdrop, inv_keep);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[is][r] = 1.f;
+      }
+    }
     float dsum = 0.f;
 #pragma unroll
     for (int is = 0; is < 4; ++is)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         st[is][jq][r] *= inv;
+        if constexpr (DROP) dp[is][jq][r] *= z[is][r];
         dsum += st[is][jq][r] * dp[is][jq][r];
       }
     dsum = group4_sum(dsum);
 #pragma unroll
     for (int is = 0; is < 4; ++is)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dp[is][jq][r] = keep[is][r] * st[is][jq][r] * (dp[is][jq][r] - dsum) * 0.125f;
+      for (int r = 0; r < 4; ++r) {
+        dp[is][jq][r] = keep[is][r] * st[is][jq][r] * (dp[is][jq][r] - dsum) * 0.125f;
+        if constexpr (DROP) st[is][jq][r] *= z[is][r];  // P~ for dV
+      }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 f;
@@ -507,7 +528,18 @@ extern "C" int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, co
                        mask, (bf16*)dqkv, pairs, T, H, D);
     return 0;
   }
-  hipLaunchKernelGGL(title_attn_bwd_kernel, dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, (const bf16*)qkv,
-                     (const bf16*)dout, mask, (bf16*)dqkv, n_titles, T, H, D);
+  hipLaunchKernelGGL((title_attn_bwd_kernel<false>), dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s,
+                     (const bf16*)qkv, (const bf16*)dout, mask, (bf16*)dqkv, n_titles, T, H, D, 0.f, 0ull, 0ull);
+  return 0;
+}
+
+extern "C" int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv,
+                                                int n_titles, int T, int H, int D, float pdrop, unsigned long long seed,
+                                                unsigned long long offset, hipStream_t s) {
+  if (T < 1 || T > 64 || D != H * DH || !(pdrop > 0.f && pdrop < 1.f)) return 2;
+  const int pairs = n_titles * H;
+  if (pairs == 0) return 0;
+  hipLaunchKernelGGL((title_attn_bwd_kernel<true>), dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s,
+                     (const bf16*)qkv, (const bf16*)dout, mask, (bf16*)dqkv, n_titles, T, H, D, pdrop, seed, offset);
   return 0;
 }

@@ -82,6 +82,11 @@ class Backbone(nn.Module):
         self._pack: Optional[Dict] = None
         self._pack_key = None
         self.version = 0  # bumped whenever the weights may have changed (hidden-state caches key on it)
+        # train-mode dropout: Philox key (the engine sets seed + rank) and a per-forward counter;
+        # a forward's sites use offsets 1024 * call + {0: embeddings, 1 + 2l: attention of
+        # layer l, 2 + 2l: FFN of layer l}, so the backward regenerates every mask
+        self.drop_seed = 0
+        self._drop_calls = 0
         self.reset_parameters()
 
     # -------------------------------------------------------------------------------
@@ -143,11 +148,27 @@ class Backbone(nn.Module):
         return pack
 
     # -------------------------------------------------------------------------------
+    def dropout_sites(self):
+        """Per-forward dropout sites ``(embed, [(attn_l, ffn_l)])``, each ``(p, seed, offset)`` or
+        None (p = 0)."""
+        c = self.cfg
+        base = self._drop_calls * 1024
+        self._drop_calls += 1
+
+        def site(p, k):
+            return (float(p), int(self.drop_seed), base + k) if p > 0 else None
+
+        return site(c.dropout, 0), [(site(c.attention_dropout, 1 + 2 * i), site(c.dropout, 2 + 2 * i))
+                                    for i in range(c.n_layers)]
+
     @torch.no_grad()
-    def forward(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
-        """``tokens, mask [n, T]`` -> last hidden state ``[n*T, D]`` in ``dtype`` (eval mode)."""
+    def forward(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype, dropout: bool = False) -> torch.Tensor:
+        """``tokens, mask [n, T]`` -> last hidden state ``[n*T, D]`` in ``dtype`` (eval mode;
+        ``dropout`` = HF train-mode dropout, used by the reference-compat replay Q4)."""
         c = self.cfg
         P = self.compute_weights(dtype)
+        if dropout:
+            return self._forward_dropout(tokens, mask, P)
         if (tokens.is_cuda and dtype == torch.bfloat16 and c.dim % 256 == 0 and c.n_layers > 0
                 and tokens.shape[1] <= 64 and os.environ.get("FEDREC_TITLE_PACK", "1") != "0"):
             return self._forward_packed(tokens, mask, P)
@@ -162,6 +183,27 @@ class Backbone(nn.Module):
             f = ops.linear(x, L["w1"], L["b1"], act="gelu", out_dtype=dtype)
             h = ops.linear(f, L["w2"], L["b2"], out_dtype=dtype)
             x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, dtype, residual=x)
+        return x
+
+    def _forward_dropout(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict) -> torch.Tensor:
+        """Train-mode forward without gradients (frozen backbone, Q4 replay): the unpacked
+        path with HF DistilBERT's three dropout sites (csrc/dropout.hip, title_attn.hip)."""
+        c = self.cfg
+        emb, layers = self.dropout_sites()
+        x = ops.embed_ln(tokens, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps, P["word"].dtype)
+        if emb is not None:
+            x = ops.dropout_add(x, None, *emb)
+        for L, (sa, sf) in zip(P["layers"], layers):
+            qkv = ops.linear(x, L["wqkv"], L["bqkv"])
+            ctx = ops.title_attention(qkv, mask, c.n_heads, sa)
+            h = ops.linear(ctx, L["wo"], L["bo"])
+            x = ops.layer_norm(h, L["ln1_w"], L["ln1_b"], c.ln_eps, residual=x)
+            f = ops.linear(x, L["w1"], L["b1"], act="gelu")
+            h = ops.linear(f, L["w2"], L["b2"])
+            if sf is not None:
+                x = ops.layer_norm(ops.dropout_add(h, x, *sf), L["ln2_w"], L["ln2_b"], c.ln_eps)
+            else:
+                x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, residual=x)
         return x
 
     def _forward_packed(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict) -> torch.Tensor:
@@ -227,48 +269,61 @@ class Backbone(nn.Module):
             yield li
         holder[slot] = x
 
-    def forward_train(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
-        """Differentiable forward for an unfrozen backbone (BASELINE config 5), eval-mode math
-        (no dropout).  Device: our kernels + their backward kernels through autograd
-        Functions whose gradients land in the fp32 master parameters; host: the oracle ops
-        under plain autograd."""
+    def forward_train(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype,
+                      dropout: bool = False) -> torch.Tensor:
+        """Differentiable forward for an unfrozen backbone (BASELINE config 5); ``dropout`` =
+        HF train mode (embedding / attention-probability / FFN dropout with Philox counter
+        masks that the backward regenerates).  Device: our kernels + their backward kernels
+        through autograd Functions whose gradients land in the fp32 master parameters; host:
+        the oracle ops (same masks, bit for bit) under plain autograd."""
         from ..ops import functional as OF
         from ..ops import reference as R
 
         c = self.cfg
         e = self.embeddings
+        emb, sites = self.dropout_sites() if dropout else (None, [(None, None)] * c.n_layers)
         if not tokens.is_cuda or dtype != torch.bfloat16:
             x = R.embed_ln(tokens, e.word_embeddings.weight, e.position_embeddings.weight, e.LayerNorm.weight,
                            e.LayerNorm.bias, c.ln_eps)
-            for blk in self.transformer.layer:
+            if emb is not None:
+                x = R.dropout_add(x, None, *emb)
+            for blk, (sa, sf) in zip(self.transformer.layer, sites):
                 a = blk.attention
                 wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
                 bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
                 qkv = R.linear(x, wqkv, bqkv)
-                ctx = R.title_attention(qkv, mask, c.n_heads)
+                ctx = R.title_attention(qkv, mask, c.n_heads, sa)
                 x = R.layer_norm(R.linear(ctx, a.out_lin.weight, a.out_lin.bias, residual=x),
                                  blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps)
                 f = R.linear(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, act="gelu")
-                x = R.layer_norm(R.linear(f, blk.ffn.lin2.weight, blk.ffn.lin2.bias, residual=x),
-                                 blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
+                if sf is not None:
+                    h = R.dropout_add(R.linear(f, blk.ffn.lin2.weight, blk.ffn.lin2.bias), x, *sf)
+                else:
+                    h = R.linear(f, blk.ffn.lin2.weight, blk.ffn.lin2.bias, residual=x)
+                x = R.layer_norm(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
             return x
         P = self.compute_weights(dtype)
         x = OF.EmbedLNFn.apply(tokens.contiguous(), e.word_embeddings.weight, e.position_embeddings.weight,
                                e.LayerNorm.weight, e.LayerNorm.bias, c.ln_eps, P["word"], P["pos"])
-        for blk, L in zip(self.transformer.layer, P["layers"]):
+        if emb is not None:
+            x = OF.DropoutFn.apply(x, *emb)
+        blocks = os.environ.get("FEDREC_TRAIN_BLOCKS", "1") != "0"
+        if not blocks and dropout:
+            raise ValueError("FEDREC_TRAIN_BLOCKS=0 (per-op A/B path) has no dropout; use the block path")
+        for blk, L, (sa, sf) in zip(self.transformer.layer, P["layers"], sites):
             a = blk.attention
             wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
             bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
-            if os.environ.get("FEDREC_TRAIN_BLOCKS", "1") != "0":  # fused block Functions (default)
+            if blocks:  # fused block Functions (default)
                 # box: each LN backward hands its dx column sums (the bias grad of the block
                 # half feeding it) to that block's backward, which runs next
                 fuse = os.environ.get("FEDREC_LN_COLSUM", "1") != "0"
                 box1, box2 = ({}, {}) if fuse else (None, None)
                 h = OF.AttnBlockFn.apply(x, wqkv, bqkv, a.out_lin.weight, a.out_lin.bias, mask.contiguous(),
-                                         c.n_heads, L["wqkv"], L["wo"], box1)
+                                         c.n_heads, L["wqkv"], L["wo"], box1, sa)
                 x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps, box1)
                 h = OF.MLPBlockFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, blk.ffn.lin2.weight,
-                                        blk.ffn.lin2.bias, L["w1"], L["w2"], box2)
+                                        blk.ffn.lin2.bias, L["w1"], L["w2"], box2, sf)
                 x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps, box2)
                 continue
             qkv = OF.LinearTFn.apply(x, wqkv, bqkv, None, L["wqkv"])

@@ -64,10 +64,33 @@ def layer_norm(x, w, b, eps: float, dtype=None, residual=None):
     return ref.layer_norm(h, w, b, eps).to(dtype or x.dtype)
 
 
-def title_attention(qkv, mask, n_heads: int):
+def title_attention(qkv, mask, n_heads: int, drop=None):
+    """``drop = (p, seed, offset)``: train-mode dropout on the attention probabilities."""
     if _dev(qkv) and qkv.dtype == torch.bfloat16:
+        if drop is not None:
+            p, seed, off = drop
+            return native.require_for(qkv).title_attention_drop(qkv, mask.contiguous(), int(n_heads), float(p),
+                                                                int(seed), int(off))
         return native.require_for(qkv).title_attention(qkv, mask.contiguous(), int(n_heads))
-    return ref.title_attention(qkv, mask, n_heads).to(qkv.dtype)
+    return ref.title_attention(qkv, mask, n_heads, drop).to(qkv.dtype)
+
+
+def title_attention_bwd(qkv, dout, mask, n_heads: int, drop=None):
+    lib = native.require_for(qkv)
+    if drop is not None:
+        p, seed, off = drop
+        return lib.title_attention_bwd_drop(qkv, dout.contiguous(), mask.contiguous(), int(n_heads), float(p),
+                                            int(seed), int(off))
+    return lib.title_attention_bwd(qkv, dout.contiguous(), mask.contiguous(), int(n_heads))
+
+
+def dropout_add(h, res, p: float, seed: int, offset: int):
+    """``res + h o Z`` (``res`` may be None): Z = keep / (1 - p) from the element-indexed
+    Philox mask (csrc/dropout.hip).  Its own backward: ``dh = dout o Z``."""
+    if _dev(h) and h.dtype == torch.bfloat16:
+        r = None if res is None else res.contiguous()
+        return native.require_for(h).dropout_add(h.contiguous(), r, float(p), int(seed), int(offset))
+    return ref.dropout_add(h, res, p, seed, offset).to(h.dtype)
 
 
 # ---- packed title rows (frozen backbone forward, csrc/title_attn.hip) -----------------------

@@ -245,20 +245,37 @@ _DZ_MODE = __import__("os").environ.get("FEDREC_DZ_MODE", "gemm")  # gemm | stre
 _QKV_BIAS_SHORTCUT = __import__("os").environ.get("FEDREC_QKV_BIAS_SHORTCUT", "1") != "0"
 
 
+class DropoutFn(torch.autograd.Function):
+    """Train-mode dropout with the counter-based mask (``ops.dropout_add``): the backward
+    regenerates Z from (seed, offset) instead of storing it."""
+
+    @staticmethod
+    def forward(ctx, x, p: float, seed: int, offset: int):
+        ctx.drop = (p, seed, offset)
+        return ops.dropout_add(x, None, p, seed, offset)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.dropout_add(g.contiguous(), None, *ctx.drop), None, None, None
+
+
 class AttnBlockFn(torch.autograd.Function):
     """``h = out_proj(attention(x Wqkv^T + bqkv)) + x`` (one post-LN block's attention half,
     unfrozen backbone).  One Function so the residual gradient joins the QKV input gradient
     inside the dgrad GEMM (``dh.addmm_(dqkv, Wqkv)``: beta = 1 accumulate) instead of an
-    extra bf16 add pass over [M, 768] that autograd would insert for the two uses of ``x``."""
+    extra bf16 add pass over [M, 768] that autograd would insert for the two uses of ``x``.
+    ``drop = (p, seed, offset)``: train-mode dropout of the attention probabilities (HF
+    DistilBERT has no dropout after ``out_lin``)."""
 
     @staticmethod
-    def forward(ctx, x, wqkv, bqkv, wo, bo, mask, heads: int, wqkv_low, wo_low, box=None):
+    def forward(ctx, x, wqkv, bqkv, wo, bo, mask, heads: int, wqkv_low, wo_low, box=None, drop=None):
         qkv = ops.linear(x, wqkv_low, bqkv)
-        c = ops.title_attention(qkv, mask, heads)
+        c = ops.title_attention(qkv, mask, heads, drop)
         h = ops.linear(c, wo_low, bo, residual=x)
         ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low, wo)
         ctx.heads = heads
         ctx.box = box
+        ctx.drop = drop
         return h
 
     @staticmethod
@@ -268,12 +285,13 @@ class AttnBlockFn(torch.autograd.Function):
         dbo = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN1's backward
         dwo, dbo = wgrad(dh, c), (dbo if dbo is not None else bgrad(dh))
         dc = torch.mm(dh, wo_low)
-        dqkv = ops.native.require_for(qkv).title_attention_bwd(qkv, dc, mask, ctx.heads)
+        dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
         dwqkv = wgrad(dqkv, x)
-        if _QKV_BIAS_SHORTCUT and dqkv.is_cuda:
+        if _QKV_BIAS_SHORTCUT and dqkv.is_cuda and ctx.drop is None:
             # column sums of dQ | dK | dV without reading dK and dV: every softmax row sums to
             # one, so sum_s dV_s = sum_t dctx_t = dbo Wo; and sum_s dS_ts = 0 for every query
-            # (shift invariance), so the key-bias gradient is identically zero
+            # (shift invariance), so the key-bias gradient is identically zero.  (Not with
+            # attention dropout: the dropped rows of P~ no longer sum to one.)
             Dm = wo.shape[0]
             dbqkv = torch.cat([ops.native.require_for(dqkv).colsum(dqkv[:, :Dm]),
                                torch.zeros(Dm, device=dqkv.device, dtype=torch.float32),
@@ -281,30 +299,39 @@ class AttnBlockFn(torch.autograd.Function):
         else:
             dbqkv = bgrad(dqkv)
         dx = dh.addmm_(dqkv, wqkv_low)  # dh is ours (consumed above): residual + QKV dgrad
-        return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None, None
+        return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None, None, None
 
 
 class MLPBlockFn(torch.autograd.Function):
-    """``h = GELU(x W1^T + b1) W2^T + b2 + x`` (FFN half of a block, unfrozen backbone).
+    """``h = drop(GELU(x W1^T + b1) W2^T + b2) + x`` (FFN half of a block, unfrozen backbone;
+    ``drop = (p, seed, offset)`` = HF ``FFN.dropout`` in train mode, else identity).
     Backward: the GELU derivative rides in the epilogue of the GEMM that forms dF
     (``act = 3``: ``dz = (dh W2) * GELU'(z)``, z saved by the dual-store forward GEMM), and
     the residual gradient joins the FFN1 dgrad via ``addmm_``."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low, box=None):
+    def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low, box=None, drop=None):
         lib = ops.native.require_for(x)
         f, z = lib.linear_gelu_dual(x.contiguous(), w1_low, b1)
-        h = ops.linear(f, w2_low, b2, residual=x)
+        if drop is None:
+            h = ops.linear(f, w2_low, b2, residual=x)
+        else:  # dropout + residual in one elementwise pass over the lin2 output
+            h = ops.dropout_add(ops.linear(f, w2_low, b2), x, *drop)
         ctx.save_for_backward(x, f, z, w1_low, w2_low)
         ctx.box = box
+        ctx.drop = drop
         return h
 
     @staticmethod
     def backward(ctx, dh):
         x, f, z, w1_low, w2_low = ctx.saved_tensors
         lib = ops.native.require_for(x)
-        dh = dh.contiguous()
+        dres = dh.contiguous()  # the residual branch's gradient
         db2 = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN2's backward
+        if ctx.drop is not None:  # the lin2 branch sees dh o Z; LN2's column sums are of dh itself
+            dh, db2 = ops.dropout_add(dres, None, *ctx.drop), None
+        else:
+            dh = dres
         dw2, db2 = wgrad(dh, f), (db2 if db2 is not None else bgrad(dh))
         if _DZ_MODE == "gemm":
             # (dh W2) * GELU'(z) and its column sums from our GEMM's epilogue in one pass (the
@@ -318,8 +345,8 @@ class MLPBlockFn(torch.autograd.Function):
             # (the FFN1 bias gradient), deterministic partials
             dz, db1 = lib.gelu_bwd_colsum(torch.mm(dh, w2_low), z)
         dw1 = wgrad(dz, x)
-        dx = dh.addmm_(dz, w1_low)
-        return dx, dw1, db1, dw2, db2, None, None, None
+        dx = dres.addmm_(dz, w1_low)
+        return dx, dw1, db1, dw2, db2, None, None, None, None
 
 
 class GeluFn(torch.autograd.Function):

@@ -52,6 +52,57 @@ def eps_softmax_backward(p: torch.Tensor, dp: torch.Tensor, dim: int) -> torch.T
 
 
 # ---------------------------------------------------------------------------------------
+# counter-based RNG (bit-exact twin of csrc/common.h Philox / drop_scale)
+# ---------------------------------------------------------------------------------------
+_U32 = 0xFFFFFFFF
+
+
+def philox4x32(seed: int, offset: int, ctr: torch.Tensor) -> torch.Tensor:
+    """Philox-4x32-10 (Salmon et al. 2011) with the kernels' layout: counter words
+    (ctr lo, ctr hi, offset lo, offset hi), key (seed lo, seed hi).  ``ctr`` int64 -> ``[..., 4]``
+    int64 holding uint32 values.  int64 products wrap mod 2^64, which keeps the low 64 bits of
+    the 32x32 product exact -- all mul-hi / mul-lo need."""
+    ctr = ctr.to(torch.int64)
+    c0, c1 = ctr & _U32, (ctr >> 32) & _U32
+    c2 = torch.full_like(ctr, int(offset) & _U32)
+    c3 = torch.full_like(ctr, (int(offset) >> 32) & _U32)
+    k0, k1 = int(seed) & _U32, (int(seed) >> 32) & _U32
+    for _ in range(10):
+        p0 = c0 * 0xD2511F53
+        p1 = c2 * 0xCD9E8D57
+        c0, c1, c2, c3 = ((p1 >> 32) & _U32) ^ c1 ^ k0, p1 & _U32, ((p0 >> 32) & _U32) ^ c3 ^ k1, p0 & _U32
+        k0 = (k0 + 0x9E3779B9) & _U32
+        k1 = (k1 + 0xBB67AE85) & _U32
+    return torch.stack([c0, c1, c2, c3], -1)
+
+
+def dropout_scale(index: torch.Tensor, p: float, seed: int, offset: int) -> torch.Tensor:
+    """Dropout multiplier of element ``index`` (int64): ``keep / (1 - p)`` with keep iff
+    ``unit(x) > p`` where x = component ``index & 3`` of Philox counter ``index >> 2``."""
+    x = philox4x32(seed, offset, index >> 2).gather(-1, (index & 3).unsqueeze(-1)).squeeze(-1)
+    u = ((x >> 8) + 1).to(torch.float32) * (1.0 / 16777216.0)
+    pf = torch.tensor(p, dtype=torch.float32)
+    inv_keep = torch.tensor(1.0, dtype=torch.float32) / (1.0 - pf)
+    return torch.where(u > pf, inv_keep, torch.zeros((), dtype=torch.float32))
+
+
+def dropout_add(h: torch.Tensor, res: Optional[torch.Tensor], p: float, seed: int, offset: int) -> torch.Tensor:
+    """``res + h o Z`` with Z the element-indexed mask of ``csrc/dropout.hip``."""
+    z = dropout_scale(torch.arange(h.numel(), device=h.device), p, seed, offset).view(h.shape).to(_f(h).dtype)
+    out = _f(h) * z
+    return out if res is None else out + _f(res)
+
+
+def attention_dropout_scale(n: int, n_heads: int, T: int, p: float, seed: int, offset: int) -> torch.Tensor:
+    """``[n, h, T, T]`` multipliers of the attention probabilities: element (title, head, t, s)
+    is mask index ``((title * h + head) * 64 + t) * 64 + s`` (title_attn.hip, T <= 64)."""
+    pair = torch.arange(n * n_heads, dtype=torch.int64).view(n, n_heads, 1, 1)
+    t = torch.arange(T, dtype=torch.int64).view(1, 1, T, 1)
+    s = torch.arange(T, dtype=torch.int64).view(1, 1, 1, T)
+    return dropout_scale((pair * 64 + t) * 64 + s, p, seed, offset)
+
+
+# ---------------------------------------------------------------------------------------
 # text backbone (DistilBERT-shaped) pieces
 # ---------------------------------------------------------------------------------------
 def embed_ln(tokens: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, ln_w: torch.Tensor,
@@ -84,8 +135,10 @@ def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) ->
     return F.layer_norm(_f(x), (x.shape[-1],), _f(w), _f(b), eps)
 
 
-def title_attention(qkv: torch.Tensor, mask: torch.Tensor, n_heads: int) -> torch.Tensor:
-    """HF DistilBERT eager attention.  ``qkv`` ``[n*T, 3D]`` (q | k | v), ``mask`` ``[n, T]``."""
+def title_attention(qkv: torch.Tensor, mask: torch.Tensor, n_heads: int, drop=None) -> torch.Tensor:
+    """HF DistilBERT eager attention.  ``qkv`` ``[n*T, 3D]`` (q | k | v), ``mask`` ``[n, T]``;
+    ``drop = (p, seed, offset)``: train-mode dropout on the probabilities (HF
+    ``nn.functional.dropout(attn_weights)``) with the kernels' Philox mask."""
     n, T = mask.shape
     D = qkv.shape[1] // 3
     dh = D // n_heads
@@ -95,6 +148,8 @@ def title_attention(qkv: torch.Tensor, mask: torch.Tensor, n_heads: int) -> torc
     keep = (mask != 0).view(n, 1, 1, T)
     s = s.masked_fill(~keep, torch.finfo(torch.float32).min)
     p = torch.softmax(s, dim=-1)
+    if drop is not None:
+        p = p * attention_dropout_scale(n, n_heads, T, *drop).to(p.device, p.dtype)
     ctx = p @ v  # [n, h, T, dh]
     return ctx.permute(0, 2, 1, 3).reshape(n * T, D)
 

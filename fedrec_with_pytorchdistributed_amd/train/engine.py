@@ -82,6 +82,8 @@ class LocalEngine:
         self.G: Optional[torch.Tensor] = None
         self.touched: Optional[torch.Tensor] = None
         self.news_table: Optional[torch.Tensor] = None
+        # train-mode dropout masks of the backbone (unfrozen training, Q4 replay): Philox key per client
+        model.text_encoder.DistillBert.drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 1
         self.hcache = self._make_hidden_cache()
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
@@ -324,9 +326,9 @@ class LocalEngine:
         for s in range(0, ids.numel(), self.replay_chunk):
             cid = ids[s:s + self.replay_chunk]
             with obs.range("replay"):
-                if train_mode:
+                if train_mode:  # DistilBERT with its dropout (p = backbone.dropout / attention_dropout)
                     text = self.tokens.index_select(0, cid.long())
-                    hid, mask = te.hidden(text), text[:, 1, :]
+                    hid, mask = te.hidden(text, dropout=True), text[:, 1, :]
                 else:
                     hid, mask = self._hidden(cid)
                 v = te.head(hid, mask)
