@@ -167,6 +167,11 @@ class FedRecConfig:
     # per-step GA: run the gradient all-reduce + Adam on a side stream, overlapped with the next
     # step's (parameter-free) frozen-backbone forward.  auto = GPU + all-reduce + frozen backbone
     overlap_optimizer: str = "auto"  # auto | on | off
+    # per-step schedule on the device with the hidden-state cache: capture forward + backward of
+    # a step in a HIP graph per (batch shape, unique-title bucket) and replay it (one launch
+    # instead of ~60 host-issued kernels); the all-reduce + Adam stay eager.  auto = on there
+    # unless LDP noise is on (its Philox offset advances per step on the host)
+    step_graph: str = "auto"  # auto | on | off
     device: str = "auto"  # auto | cpu | cuda
     seed: int = 0
 

@@ -394,7 +394,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Te
 
 at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, const at::Tensor& seg_ptr, int64_t num_out,
                             double clip, double noise_std, int64_t seed, int64_t offset,
-                            const c10::optional<at::Tensor>& inv) {
+                            const c10::optional<at::Tensor>& inv, bool zero_empty) {
   check_dev(rows, "rows");
   check_dev(perm, "perm");
   check_dev(seg_ptr, "seg_ptr");
@@ -403,7 +403,9 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
   TORCH_CHECK(seg_ptr.numel() == num_out + 1, "fedrec::segment_sum_rows: seg_ptr size");
   const c10::DeviceGuard g(rows.device());
   const int64_t D = rows.size(-1);
-  auto out = at::empty({num_out, D}, rows.options());
+  // the kernels write only rows whose segment has occurrences; zero_empty (padded unique
+  // lists of the step graphs) clears the rest first
+  auto out = zero_empty ? at::zeros({num_out, D}, rows.options()) : at::empty({num_out, D}, rows.options());
   at::Tensor src = rows;
   if (clip > 0.0 || noise_std > 0.0) {  // LDP: clip + noise every occurrence first (parallel pass)
     src = at::empty_like(rows);
@@ -780,7 +782,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim) -> (Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None) -> Tensor");
+  m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False) -> Tensor");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset) -> (Tensor, Tensor)");

@@ -170,7 +170,7 @@ def score_ce(cand, user, act: str = "sigmoid"):
 
 
 def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: float = 0.0,
-                     seed: int = 0, offset: int = 0, generator=None, seg=None):
+                     seed: int = 0, offset: int = 0, generator=None, seg=None, zero_empty: bool = False):
     """Per-news gradient reduction ``out[inv[r]] += clip(rows[r]) + N(0, noise_std)``.
 
     ``seg = (perm, seg_ptr)`` (rows grouped by output id) enables the deterministic,
@@ -185,7 +185,7 @@ def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: floa
         inv32 = inv32 if inv32.dtype == torch.int32 else inv32.to(torch.int32)
         return native.require_for(rows).segment_sum_rows(rows.float().contiguous(), perm, ptr, int(num_out),
                                                          float(clip), float(noise_std), int(seed), int(offset),
-                                                         inv32.contiguous())
+                                                         inv32.contiguous(), bool(zero_empty))
     if noise_std > 0 and generator is None:
         generator = torch.Generator().manual_seed((int(seed) * 1_000_003 + int(offset)) & 0x7FFFFFFFFFFF)
     return ref.segment_sum_rows(rows, inv, num_out, clip, noise_std, generator)

@@ -135,18 +135,20 @@ class NewsGatherFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, table, inv, perm, seg_ptr, clip: float, noise_std: float, seed: int, offset: int):
+    def forward(ctx, table, inv, perm, seg_ptr, clip: float, noise_std: float, seed: int, offset: int,
+                padded: bool = False):
         ctx.save_for_backward(inv, perm, seg_ptr)
         ctx.n = table.shape[0]
         ctx.ldp = (clip, noise_std, seed, offset)
+        ctx.padded = padded  # table rows no occurrence maps to (step graphs): their gradient is 0
         return table.index_select(0, inv.long())
 
     @staticmethod
     def backward(ctx, g):
         inv, perm, seg_ptr = ctx.saved_tensors
         clip, noise, seed, offset = ctx.ldp
-        d = ops.segment_sum_rows(g, inv, ctx.n, clip, noise, seed, offset, seg=(perm, seg_ptr))
-        return d, None, None, None, None, None, None, None
+        d = ops.segment_sum_rows(g, inv, ctx.n, clip, noise, seed, offset, seg=(perm, seg_ptr), zero_empty=ctx.padded)
+        return d, None, None, None, None, None, None, None, None
 
 
 def additive_pool(x, lin1: torch.nn.Linear, lin2: torch.nn.Linear):
@@ -194,8 +196,8 @@ def score_ce(cand, user, act: str = "sigmoid") -> Tuple[torch.Tensor, torch.Tens
 
 
 def news_gather(table, inv, perm, seg_ptr, clip: float = 0.0, noise_std: float = 0.0,
-                seed: int = 0, offset: int = 0):
-    return NewsGatherFn.apply(table, inv, perm, seg_ptr, clip, noise_std, seed, offset)
+                seed: int = 0, offset: int = 0, padded: bool = False):
+    return NewsGatherFn.apply(table, inv, perm, seg_ptr, clip, noise_std, seed, offset, padded)
 
 
 # ---------------------------------------------------------------------------------------

@@ -54,6 +54,49 @@ class Prepared(NamedTuple):
     his: torch.Tensor
     dedup: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]]
     ready: Optional[torch.cuda.Event]
+    padded: bool = False  # dedup's unique list padded with rows no occurrence maps to (step graphs)
+
+
+class _StepGraph:
+    """Static inputs + the captured graph of one (batch shape, unique-title bucket)."""
+
+    def __init__(self, eng: "LocalEngine", pre: Prepared, ucap: int):
+        uniq, inv, perm, ptr = pre.dedup
+        dev = eng.device
+        self.cand = torch.zeros_like(pre.cand)
+        self.his = torch.zeros_like(pre.his)
+        self.uniq = torch.zeros(ucap, dtype=uniq.dtype, device=dev)
+        self.inv = torch.zeros_like(inv)
+        self.perm = torch.zeros_like(perm)
+        self.ptr = torch.zeros(ucap + 1, dtype=ptr.dtype, device=dev)
+        self.load(pre, int(uniq.numel()))
+        static = Prepared(self.cand, self.his, (self.uniq, self.inv, self.perm, self.ptr), None, True)
+        main = torch.cuda.current_stream(dev)
+        eng.sync_params()
+        # warm up on a side stream (autograd / allocator state), then capture on it
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                eng.forward_backward(self.cand, self.his, static)
+        main.wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        # a private memory pool per graph (~250 MB of step activations at B = 64): sharing the
+        # first graph's pool (graph.pool()) trips an allocator assert in this torch build when
+        # eager steps of other engines run between the captures
+        with torch.cuda.graph(self.graph):
+            self.loss = eng.forward_backward(self.cand, self.his, static)
+
+    def load(self, pre: Prepared, U: int) -> None:
+        uniq, inv, perm, ptr = pre.dedup
+        self.cand.copy_(pre.cand)
+        self.his.copy_(pre.his)
+        self.uniq[:U].copy_(uniq)
+        self.uniq[U:].zero_()
+        self.inv.copy_(inv)
+        self.perm.copy_(perm)
+        self.ptr[:U + 1].copy_(ptr)
+        self.ptr[U + 1:].fill_(inv.numel())  # padded segments are empty
 
 
 class LocalEngine:
@@ -88,6 +131,11 @@ class LocalEngine:
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
         self.replay_chunk = 4096 if self.hcache is not None else 1024
+        # HIP graphs of the per-step forward + backward (see _graph_step)
+        sg = os.environ.get("FEDREC_STEP_GRAPH", cfg.step_graph)
+        self.step_graphs = device.type == "cuda" and self.hcache is not None and (
+            sg == "on" or (sg == "auto" and not cfg.dp.enabled))
+        self._graphs: Dict[tuple, "_StepGraph"] = {}
         self.last_stats: Dict[str, float] = {}
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
@@ -182,7 +230,10 @@ class LocalEngine:
     def prepare(self, batch_fn: Callable[[], Tuple]) -> Prepared:
         """Sample a batch (``batch_fn() -> (cand, his)``) and de-duplicate its news ids.  On the
         GPU both run on the lookahead stream: the only host wait (the unique count) waits for
-        that stream alone, so a step's dedup overlaps the previous step's kernels."""
+        that stream alone, so a step's dedup overlaps the previous step's kernels.
+        ``batch_fn`` must produce its tensors on the lookahead stream (the device sampler does,
+        via :meth:`_next_prepared`) or return host arrays / tensors already complete: the
+        lookahead stream does not wait for other streams."""
         if self._prep is None:
             c, h = batch_fn()
             return Prepared(self.to_device(c), self.to_device(h), None, None)
@@ -202,7 +253,8 @@ class LocalEngine:
         B, C = cand.shape
         H = his.shape[1]
         if pre is not None and pre.dedup is not None:
-            torch.cuda.current_stream(self.device).wait_event(pre.ready)
+            if pre.ready is not None:
+                torch.cuda.current_stream(self.device).wait_event(pre.ready)
             uniq, inv, perm, ptr = pre.dedup
         else:
             ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
@@ -212,7 +264,8 @@ class LocalEngine:
         if not grad_news:
             v = v.detach().requires_grad_(True)
         clip, std = self._ldp()
-        rows = OF.news_gather(v, inv, perm, ptr, clip, std, self.cfg.seed * 7919 + self.rank, self.noise_offset)
+        padded = pre is not None and pre.padded
+        rows = OF.news_gather(v, inv, perm, ptr, clip, std, self.cfg.seed * 7919 + self.rank, self.noise_offset, padded)
         self.noise_offset += 1
         cand_v = rows[: B * C].view(B, C, -1)
         his_v = rows[B * C:].view(B, H, -1)
@@ -240,7 +293,47 @@ class LocalEngine:
         return loss
 
     def train_prepared(self, pre: Prepared) -> torch.Tensor:
+        if self.step_graphs and pre.dedup is not None and not (self.cfg.dp.enabled and self.sigma):
+            loss = self._graph_step(pre)
+            if loss is not None:
+                self.optimizer_step(overlap=True)
+                return loss
         return self.train_step(pre.cand, pre.his, pre)
+
+    # ---- HIP graph of the per-step forward + backward ------------------------------------
+    GRAPH_BUCKET = 128  # unique titles are padded up to a multiple of this (padded rows: id 0)
+    MAX_GRAPHS = 16
+
+    def _graph_step(self, pre: Prepared) -> Optional[torch.Tensor]:
+        """Forward + backward of one step by replaying a captured HIP graph.
+
+        The step's only data-dependent shape is the number U of unique titles: it is padded to
+        a multiple of GRAPH_BUCKET with news id 0, whose rows no occurrence maps to -- their
+        head outputs are never gathered and their per-news gradient (a segment sum over no
+        occurrences) is 0, so the trainable gradient is the eager step's (up to fp32
+        summation order in the split-K weight gradients).  One graph per (batch shape, bucket,
+        cache build); the batch is copied into the graph's static inputs, then one replay
+        runs ~60 kernels with no host in between.  Returns None when a new graph is not
+        allowed (the caller runs the step eagerly)."""
+        uniq, inv, perm, ptr = pre.dedup
+        U = int(uniq.numel())
+        ucap = -(-U // self.GRAPH_BUCKET) * self.GRAPH_BUCKET
+        key = (tuple(pre.cand.shape), tuple(pre.his.shape), int(inv.numel()), ucap, self.hcache.builds)
+        g = self._graphs.get(key)
+        main = torch.cuda.current_stream(self.device)
+        if pre.ready is not None:
+            main.wait_event(pre.ready)
+        if g is None:
+            if len(self._graphs) >= self.MAX_GRAPHS:
+                return None
+            if any(k[-1] != self.hcache.builds for k in self._graphs):  # a rebuilt cache: old graphs are stale
+                self._graphs = {k: v for k, v in self._graphs.items() if k[-1] == self.hcache.builds}
+            g = _StepGraph(self, pre, ucap)
+            self._graphs[key] = g
+        g.load(pre, U)
+        self.sync_params()
+        g.graph.replay()
+        return g.loss.clone()
 
     def optimizer_step(self, extra_scale: float = 1.0, overlap: bool = False) -> None:
         """All-reduce the flat gradient (if any) and take one fused Adam step.  ``overlap``

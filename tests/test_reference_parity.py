@@ -39,7 +39,7 @@ def setup(ref):
     shard = Shard.load(f"{refharness.REFERENCE_PATH}/UserData")
     cfg = FedRecConfig(mode="fedavg_star", batch_size=2, user_dropout=0.0)
     cfg.compat.reference_quirks = True  # Q2 (x2, last batch), Q6 (no truncation), Q9, Q10, Q11 ...
-    cfg.backbone = BackboneConfig()  # distilbert-base-uncased shape, random init
+    cfg.backbone = BackboneConfig(dropout=0.0, attention_dropout=0.0)  # distilbert-base shape, random init
     torch.manual_seed(0)
     ours = FedRecModel(cfg)
     ours.build_flat()
