@@ -44,21 +44,35 @@ def _dev(t: torch.Tensor) -> bool:
 # ---------------------------------------------------------------------------------------
 def embed_ln(tokens, word, pos, ln_w, ln_b, eps: float, dtype=torch.float32):
     if _dev(word):
+        if word.dtype != torch.bfloat16:
+            native.no_kernel("embed_ln", word)
         return native.require_for(word).embed_ln(tokens.contiguous(), word, pos, ln_w, ln_b, float(eps))
     return ref.embed_ln(tokens, word, pos, ln_w, ln_b, eps).to(dtype)
 
 
 def linear(x, w, b=None, act: str = "none", residual=None, out_dtype=None):
     """``act(x @ w^T + b) + residual``; bf16 device inputs run the MFMA GEMM."""
-    if _dev(x) and x.dtype == torch.bfloat16:
+    if _dev(x):
+        if x.dtype != torch.bfloat16:
+            native.no_kernel("linear", x)
         return native.require_for(x).linear(x.contiguous(), w, b, _ACT[act], residual)
     y = ref.linear(x, w, b, act, residual)
     return y.to(out_dtype or x.dtype)
 
 
+def linear_lib(x, w, b=None, act: str = "none"):
+    """fp32 ``act(x @ w^T + b)`` through the vendor GEMM (hipBLASLt on the device).  Used by
+    the user encoder's additive-attention projection, which runs in fp32 like the reference
+    (its [B*H, 400] x [400, 200] shape is below the bf16 MFMA kernel's N % 128 tiling)."""
+    y = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
+    return torch.tanh(y) if act == "tanh" else (torch.nn.functional.gelu(y) if act == "gelu" else y)
+
+
 def layer_norm(x, w, b, eps: float, dtype=None, residual=None):
     """``LN(x [+ residual]) * w + b`` (the residual add is fused into the LN kernel)."""
-    if _dev(x) and x.dtype == torch.bfloat16:
+    if _dev(x):
+        if x.dtype != torch.bfloat16:
+            native.no_kernel("layer_norm", x)
         return native.require_for(x).layer_norm(x, w, b, float(eps), residual)
     h = x if residual is None else x.float() + residual.float()
     return ref.layer_norm(h, w, b, eps).to(dtype or x.dtype)
@@ -66,7 +80,9 @@ def layer_norm(x, w, b, eps: float, dtype=None, residual=None):
 
 def title_attention(qkv, mask, n_heads: int, drop=None):
     """``drop = (p, seed, offset)``: train-mode dropout on the attention probabilities."""
-    if _dev(qkv) and qkv.dtype == torch.bfloat16:
+    if _dev(qkv):
+        if qkv.dtype != torch.bfloat16:
+            native.no_kernel("title_attention", qkv)
         if drop is not None:
             p, seed, off = drop
             return native.require_for(qkv).title_attention_drop(qkv, mask.contiguous(), int(n_heads), float(p),
@@ -87,7 +103,9 @@ def title_attention_bwd(qkv, dout, mask, n_heads: int, drop=None):
 def dropout_add(h, res, p: float, seed: int, offset: int):
     """``res + h o Z`` (``res`` may be None): Z = keep / (1 - p) from the element-indexed
     Philox mask (csrc/dropout.hip).  Its own backward: ``dh = dout o Z``."""
-    if _dev(h) and h.dtype == torch.bfloat16:
+    if _dev(h):
+        if h.dtype != torch.bfloat16:
+            native.no_kernel("dropout_add", h)
         r = None if res is None else res.contiguous()
         return native.require_for(h).dropout_add(h.contiguous(), r, float(p), int(seed), int(offset))
     return ref.dropout_add(h, res, p, seed, offset).to(h.dtype)

@@ -64,8 +64,12 @@ class AdditivePoolFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2):
         n, T, D = x.shape
         x2 = x.reshape(n * T, D)
-        w1c = w1.to(x.dtype) if x.dtype != w1.dtype else w1
-        e = ops.linear(x2, w1c, b1.float() if x.dtype == torch.bfloat16 else b1, act="tanh")
+        if x.dtype == torch.bfloat16:  # text head on the device: MFMA GEMM + tanh epilogue
+            e = ops.linear(x2, w1.to(x.dtype), b1.float(), act="tanh")
+        elif x.is_cuda:  # user encoder (fp32): explicit vendor GEMM, see ops.linear_lib
+            e = ops.linear_lib(x2, w1, b1, act="tanh")
+        else:
+            e = ops.linear(x2, w1, b1, act="tanh")
         e = e.reshape(n, T, -1)
         pooled, alpha = ops.additive_pool_fwd(x, e, w2, b2)
         ctx.save_for_backward(x, e, alpha, w1, w2)

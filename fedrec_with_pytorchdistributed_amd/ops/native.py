@@ -71,5 +71,8 @@ def require_for(t: torch.Tensor):
     return lib()
 
 
-def strict() -> bool:
-    return os.environ.get("FEDREC_ALLOW_EAGER", "0") != "1"
+def no_kernel(op: str, t: torch.Tensor):
+    """A device tensor reached an op that has no HIP kernel for its dtype: fail loudly (the
+    engine never silently runs a torch-eager replacement on the device)."""
+    raise RuntimeError(f"fedrec::{op}: no HIP kernel for {t.dtype} device tensors (the device path is bf16; "
+                       f"--precision=fp32 runs on the host only)")

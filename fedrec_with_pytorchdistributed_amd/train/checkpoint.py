@@ -36,30 +36,66 @@ def atomic_save(obj: Any, path: str) -> None:
     os.replace(tmp, path)
 
 
+def rng_state() -> Dict[str, Any]:
+    """Host and device torch generator states (user dropout, host sampling fallbacks)."""
+    st: Dict[str, Any] = {"RNG": torch.get_rng_state()}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        st["RNG_CUDA"] = torch.cuda.get_rng_state_all()
+    return st
+
+
+def restore_rng(snap: Dict[str, Any]) -> bool:
+    """Restore what :func:`rng_state` saved; device states only onto the same device count."""
+    done = False
+    if isinstance(snap.get("RNG"), torch.Tensor):
+        torch.set_rng_state(snap["RNG"])
+        done = True
+    cu = snap.get("RNG_CUDA")
+    if cu is not None and torch.cuda.is_available() and len(cu) == torch.cuda.device_count():
+        torch.cuda.set_rng_state_all(cu)
+    return done
+
+
 def save_snapshot(path: str, model: FedRecModel, epoch: int, *, round_idx: Optional[int] = None,
-                  optim: bool = True, config: Optional[dict] = None) -> None:
+                  optim: bool = True, config: Optional[dict] = None,
+                  engine: Optional[Dict[str, int]] = None) -> None:
+    """``engine``: the engine's own counters (Philox offsets of LDP noise / dropout, sampler
+    epoch) so a resumed run draws fresh randomness instead of replaying the saved one."""
     snap: Dict[str, Any] = {"MODEL_STATE": cpu_state_dict(model), "EPOCHS_RUN": int(epoch),
                             "NEXT_EPOCH": int(epoch) + 1}
     if optim and model.flat is not None:
         snap["OPTIM_STATE"] = model.flat.state()
     if round_idx is not None:
         snap["ROUND"] = int(round_idx)
-    snap["RNG"] = torch.get_rng_state()
+    snap.update(rng_state())
+    if engine is not None:
+        snap["ENGINE"] = {k: int(v) for k, v in engine.items()}
     if config is not None:
         snap["CONFIG"] = config
     atomic_save(snap, path)
 
 
-def load_snapshot(path: str, model: FedRecModel, map_location="cpu") -> Dict[str, Any]:
-    """Load a snapshot (ours or the reference's) into ``model``; returns resume info."""
+def load_snapshot(path: str, model: FedRecModel, map_location="cpu", rng: bool = True) -> Dict[str, Any]:
+    """Load a snapshot (ours or the reference's) into ``model`` -- parameters, Adam moments
+    and step, the torch RNG states -- and return the resume info."""
     snap = torch.load(path, map_location=map_location, weights_only=True)
     if "MODEL_STATE" not in snap:
         raise ValueError(f"{path}: not a snapshot (no MODEL_STATE)")
     model.load_state_dict(snap["MODEL_STATE"])
     if "OPTIM_STATE" in snap and model.flat is not None:
         model.flat.load_state(snap["OPTIM_STATE"])
+    restored = restore_rng(snap) if rng else False
     nxt = int(snap.get("NEXT_EPOCH", int(snap["EPOCHS_RUN"]) + 1))
-    return {"epochs_run": int(snap["EPOCHS_RUN"]), "next_epoch": nxt, "round": snap.get("ROUND")}
+    return {"epochs_run": int(snap["EPOCHS_RUN"]), "next_epoch": nxt, "round": snap.get("ROUND"),
+            "rng_restored": restored, "engine": snap.get("ENGINE", {})}
+
+
+def client_snapshot_path(snapshot_path: str, client: int) -> str:
+    """Per-client snapshot of a star-mode client (``client{k}_snapshot.pt`` beside the
+    coordinator's ``snapshot.pt``): the reference client auto-loads its own ``snapshot.pt``
+    at start (``client.py:125-127``); here every client resumes its Adam state from its file."""
+    d, f = os.path.split(snapshot_path)
+    return os.path.join(d, f"client{client}_{f}")
 
 
 def save_state_dict(path: str, model: FedRecModel) -> None:

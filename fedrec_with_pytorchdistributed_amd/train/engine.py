@@ -102,6 +102,9 @@ class _StepGraph:
 class LocalEngine:
     def __init__(self, cfg: FedRecConfig, model: FedRecModel, shard: Shard, device: torch.device,
                  rank: int = 0, grad_allreduce: Optional[Callable[[torch.Tensor], float]] = None):
+        if device.type == "cuda" and cfg.precision != "bf16":
+            raise ValueError(f"precision={cfg.precision!r} on the device: the HIP kernels compute in bf16 "
+                             "(fp32 is the host/oracle path; there is no eager fallback on the device)")
         self.cfg = cfg
         self.q = cfg.quirks()
         self.model = model
@@ -150,6 +153,16 @@ class LocalEngine:
         # backbone's M) no longer drains the GPU at every step start
         lookahead = device.type == "cuda" and os.environ.get("FEDREC_LOOKAHEAD", "1") != "0"
         self._prep = torch.cuda.Stream(device) if lookahead else None
+
+    def state(self) -> Dict[str, int]:
+        """Counters that key the engine's randomness (checkpointed with the snapshot)."""
+        return {"noise_offset": self.noise_offset, "epoch": self.epoch,
+                "drop_calls": self.model.text_encoder.DistillBert._drop_calls}
+
+    def load_state(self, st: Dict[str, int]) -> None:
+        self.noise_offset = int(st.get("noise_offset", self.noise_offset))
+        self.epoch = int(st.get("epoch", self.epoch))
+        self.model.text_encoder.DistillBert._drop_calls = int(st.get("drop_calls", 0))
 
     def _make_hidden_cache(self) -> Optional[HiddenCache]:
         """The HBM hidden-state cache when the config asks for it and it fits."""

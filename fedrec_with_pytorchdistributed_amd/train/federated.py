@@ -23,7 +23,7 @@ from __future__ import annotations
 import math
 import os
 import time
-from typing import Dict, List, Optional
+from typing import Tuple, Dict, List, Optional
 
 import numpy as np
 import torch
@@ -134,24 +134,27 @@ def _dump_flat(model: FedRecModel, ctx: DistContext) -> None:
         torch.save(model.flat.flat.detach().cpu(), os.path.join(d, f"rank{ctx.rank}.pt"))
 
 
-def _resume(cfg: FedRecConfig, model: FedRecModel) -> int:
+def _resume(cfg: FedRecConfig, model: FedRecModel) -> Tuple[int, Dict]:
+    """(next epoch, engine counters) of ``cfg.snapshot_path`` when it exists (params, Adam
+    moments and RNG states are restored into ``model`` / torch)."""
     if cfg.snapshot_path and os.path.exists(cfg.snapshot_path):
         info = ckpt.load_snapshot(cfg.snapshot_path, model)
         obs.log(f"resuming from {cfg.snapshot_path}: epochs_run={info['epochs_run']} -> epoch {info['next_epoch']}")
-        return info["next_epoch"]
-    return 0
+        return info["next_epoch"], info["engine"]
+    return 0, {}
 
 
 # ---------------------------------------------------------------------------------------
 def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     shard = load_client_shard(cfg, ctx)
     model = build_model(cfg, ctx.device)
-    start = _resume(cfg, model)
+    start, est = _resume(cfg, model)
     _sync_initial(model, ctx, cfg.sync == "full")
     ar = (make_secure_grad_allreduce(ctx, timeout_s=cfg.collective_timeout_s) if cfg.secagg.enabled
           else make_grad_allreduce(ctx))
     eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=ar)
     eng.sigma = _maybe_dp(cfg, eng)
+    eng.load_state(est)
     eng.epoch = start
     writer = _metrics_writer(cfg, ctx.client_index == 0)
     steps = _min_over_clients(ctx, eng.sampler.num_batches())  # every rank issues the same all-reduces
@@ -166,7 +169,7 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
             writer.write(last)
             obs.log(f"[grad_avg] epoch {epoch}: " + ", ".join(f"{k}={last[k]:.4f}" for k in METRIC_KEYS))
             if cfg.save_every and (epoch % cfg.save_every == 0 or epoch == cfg.total_epochs - 1):
-                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict())
+                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict(), engine=eng.state())
     _dump_flat(model, ctx)
     return last
 
@@ -174,11 +177,12 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
 def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     shard = load_client_shard(cfg, ctx)
     model = build_model(cfg, ctx.device)
-    start = _resume(cfg, model)
+    start, est = _resume(cfg, model)
     full = cfg.sync == "full"
     _sync_initial(model, ctx, full)
     eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=None)
     eng.sigma = _maybe_dp(cfg, eng)
+    eng.load_state(est)
     eng.epoch = start
     writer = _metrics_writer(cfg, ctx.client_index == 0)
     W = ctx.num_clients
@@ -206,7 +210,7 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
             writer.write(last)
             obs.log(f"[param_avg] epoch {epoch}: " + ", ".join(f"{k}={last[k]:.4f}" for k in METRIC_KEYS))
             if cfg.save_every and (epoch % cfg.save_every == 0 or epoch == cfg.total_epochs - 1):
-                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict())
+                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict(), engine=eng.state())
     _dump_flat(model, ctx)
     return last
 
@@ -246,6 +250,14 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         pubs = [cp.get(f"pk/{j}") for j in range(ctx.num_clients)]
         seeds_row = secagg.seeds_from_publics(kp, k, pubs)
     r = int(cp.get("start").decode())  # the coordinator may be resuming at a later round
+    # the client's own snapshot (client.py:125-127 auto-loads snapshot.pt): Adam moments + step,
+    # RNG states and engine counters; the trainable parameters are overwritten by the round's
+    # global model below, exactly as the reference's broadcast overwrites them
+    csnap = ckpt.client_snapshot_path(cfg.snapshot_path, k) if cfg.snapshot_path else ""
+    if csnap and os.path.exists(csnap):
+        info = ckpt.load_snapshot(csnap, model)
+        eng.load_state(info["engine"])
+        obs.log(f"[client {k}] resumed {csnap} (round {info['round']}, Adam step {model.flat.step})")
     beat = Heartbeat(cp, f"client{k}", cfg.heartbeat_s)
     last: Dict = {}
     while True:
@@ -276,6 +288,8 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         meta = {"client": k, "n_train": len(shard.train), "train_s": t_train, "valid_s": t_valid,
                 **{m: float(v) for m, v in {**tr, **va}.items() if isinstance(v, (int, float))}}
         up = _client_upload_tensor(model, cfg).clone()
+        if csnap:
+            ckpt.save_snapshot(csnap, model, r, round_idx=r, engine=eng.state())
         if cfg.round_artifacts:  # client.py:288 torch.save(model.state_dict(), "model.pt")
             sub = "" if ctx.num_clients == 1 else f"client{k}"
             ckpt.save_state_dict(os.path.join(_artifact_dir(cfg), sub, "model.pt"), model)

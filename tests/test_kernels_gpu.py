@@ -558,3 +558,14 @@ def test_gelu_bwd_colsum(dev, M, N):
     assert rel_err(cs, dz.float().sum(0)) < 1e-5
     dz2, cs2 = native.lib().gelu_bwd_colsum(df, z)
     assert torch.equal(dz2, dz) and torch.equal(cs2, cs)
+
+
+def test_device_ops_refuse_non_bf16(dev):
+    """A device tensor of a dtype without a kernel raises instead of running torch eager."""
+    from fedrec_with_pytorchdistributed_amd import ops as O
+    x = torch.randn(256, 768, device=dev)
+    w = torch.randn(384, 768, device=dev)
+    with pytest.raises(RuntimeError, match="no HIP kernel"):
+        O.linear(x, w)
+    with pytest.raises(RuntimeError, match="no HIP kernel"):
+        O.layer_norm(x, torch.ones(768, device=dev), torch.zeros(768, device=dev), 1e-12)
