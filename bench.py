@@ -51,7 +51,8 @@ MODELS = {2: _DB, 3: _DB, 4: _DB,
 MODES = {2: "Gradient_Averaging (RCCL all-reduce of flat 4.66 MB grad bucket per step)",
          3: "Parameter_Averaging (local Adam steps, RCCL all-reduce of the parameters every {k} steps)",
          4: "Gradient_Averaging + LDP (fused per-occurrence clip C=2 + Gaussian noise, eps=10 calibrated)",
-         5: "Gradient_Averaging with secure aggregation (pairwise-masked int32 RCCL all-reduce of all 110M grads)"}
+         5: "Gradient_Averaging with secure aggregation (pairwise-masked int32 RCCL all-reduce of all 110M grads "
+            "in 28 MB buckets during the backward)"}
 
 
 def main() -> int:
@@ -119,12 +120,14 @@ def main() -> int:
     corpus = SyntheticCorpus(spec)
     shard = corpus.client_shard(ctx.rank, world)
     if args.config == 5:
-        ar = fdist.make_secure_grad_allreduce(ctx)
+        ar = None  # bucketed masked all-reduce during the backward (engine.set_reducer below)
     elif args.config == 3:
         ar = None
     else:
         ar = fdist.make_grad_allreduce(ctx)
     eng = LocalEngine(cfg, model, shard, dev, rank=ctx.rank, grad_allreduce=ar)
+    if args.config == 5:
+        eng.set_reducer(fdist.make_bucket_reducer(ctx, model.flat, secure=True))
     if args.config == 4:
         cfg.dp.enabled, cfg.dp.epsilon = True, args.dp_epsilon
         eng.sigma = calibrate_client_sigma(cfg.dp.epsilon, cfg.dp.delta, cfg.batch_size, len(shard.train), cfg.dp.epochs)

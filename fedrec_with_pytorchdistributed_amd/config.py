@@ -211,18 +211,21 @@ class FedRecConfig:
 
     def apply_overrides(self, args: List[str]) -> List[str]:
         """Consume ``--key=value`` items; return the arguments that were not overrides."""
-        rest = []
+        rest, kv = [], []
         for a in args:
             if a.startswith("--") and "=" in a:
                 k, v = a[2:].split("=", 1)
-                _set_dotted(self, k.replace("-", "_"), v, flat=True)
+                kv.append((k.replace("-", "_"), v))
             else:
                 rest.append(a)
-        if self.backbone.name != BackboneConfig().name and self.backbone == BackboneConfig(
-            name=self.backbone.name
-        ):
-            # a bare --backbone.name=bert-base selects the full preset
-            self.backbone = BackboneConfig.preset(self.backbone.name)
+        # --backbone.name=X selects the whole preset first; the other backbone.* overrides
+        # (frozen, dropout, ...) then apply on top of it, in any argument order
+        for k, v in kv:
+            if k == "backbone.name":
+                self.backbone = BackboneConfig.preset(v)
+        for k, v in kv:
+            if k != "backbone.name":
+                _set_dotted(self, k, v, flat=True)
         return rest
 
 

@@ -75,6 +75,9 @@ int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* 
                          int c_rows, hipStream_t s);
 int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword, int* scratch,
                        hipStream_t s);
+int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int W, const unsigned long long* seeds,
+                       const int* signs, int npeers, unsigned long long round, hipStream_t s);
+int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
 int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
@@ -533,6 +536,38 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
   return out;
 }
 
+// device-scale secure aggregation (bucketed GA): the fixed-point exponent is derived on the device
+// from m = the clients' MAX-all-reduced max|x| -- no host read, no host sync
+at::Tensor secagg_mask_dev(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs, const at::Tensor& m,
+                           int64_t W, int64_t round) {
+  check_dev(x, "x");
+  check_dev(seeds, "seeds");
+  check_dev(signs, "signs");
+  check_dev(m, "m");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && seeds.scalar_type() == at::kLong &&
+                  signs.scalar_type() == at::kInt && seeds.numel() == signs.numel(),
+              "fedrec::secagg_mask_dev: dtypes");
+  const c10::DeviceGuard g(x.device());
+  auto out = at::empty(x.sizes(), x.options().dtype(at::kInt));
+  check_rc(fr_secagg_mask_dev(x.data_ptr<float>(), out.data_ptr<int>(), (long)x.numel(), m.data_ptr<float>(), (int)W,
+                              (const unsigned long long*)seeds.data_ptr<int64_t>(), signs.data_ptr<int>(),
+                              (int)seeds.numel(), (unsigned long long)round, cur_stream()),
+           "secagg_mask_dev");
+  return out;
+}
+
+void secagg_unmask_dev_(const at::Tensor& q, const at::Tensor& m, int64_t W, at::Tensor out) {
+  check_dev(q, "q");
+  check_dev(m, "m");
+  check_dev(out, "out");
+  TORCH_CHECK(q.scalar_type() == at::kInt && out.scalar_type() == at::kFloat && q.numel() == out.numel(),
+              "fedrec::secagg_unmask_dev_");
+  const c10::DeviceGuard g(q.device());
+  check_rc(fr_secagg_unmask_dev(q.data_ptr<int>(), out.data_ptr<float>(), (long)q.numel(), m.data_ptr<float>(), (int)W,
+                                cur_stream()),
+           "secagg_unmask_dev_");
+}
+
 // ---- packed title rows (frozen backbone forward; title_attn.hip) ----------------------------
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> title_plan(const at::Tensor& mask) {
   check_dev(mask, "mask");
@@ -796,6 +831,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
+  m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");
+  m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");
   m.def("dropout_add(Tensor h, Tensor? res, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
@@ -832,6 +869,8 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("linear_gelu_dual", &linear_gelu_dual);
   m.impl("embed_grad", &embed_grad);
   m.impl("dropout_add", &dropout_add);
+  m.impl("secagg_mask_dev", &secagg_mask_dev);
+  m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);
 }

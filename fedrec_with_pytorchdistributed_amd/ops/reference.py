@@ -76,30 +76,41 @@ def philox4x32(seed: int, offset: int, ctr: torch.Tensor) -> torch.Tensor:
     return torch.stack([c0, c1, c2, c3], -1)
 
 
-def dropout_scale(index: torch.Tensor, p: float, seed: int, offset: int) -> torch.Tensor:
-    """Dropout multiplier of element ``index`` (int64): ``keep / (1 - p)`` with keep iff
-    ``unit(x) > p`` where x = component ``index & 3`` of Philox counter ``index >> 2``."""
-    x = philox4x32(seed, offset, index >> 2).gather(-1, (index & 3).unsqueeze(-1)).squeeze(-1)
-    u = ((x >> 8) + 1).to(torch.float32) * (1.0 / 16777216.0)
+def _keep_scale(words: torch.Tensor, p: float) -> torch.Tensor:
+    """uint32 words (int64) -> dropout multipliers: keep / (1 - p), keep iff unit(x) > p."""
+    u = ((words >> 8) + 1).to(torch.float32) * (1.0 / 16777216.0)
     pf = torch.tensor(p, dtype=torch.float32)
     inv_keep = torch.tensor(1.0, dtype=torch.float32) / (1.0 - pf)
     return torch.where(u > pf, inv_keep, torch.zeros((), dtype=torch.float32))
 
 
+def dropout_scale(index: torch.Tensor, p: float, seed: int, offset: int) -> torch.Tensor:
+    """Dropout multiplier of element ``index`` (int64): ``keep / (1 - p)`` with keep iff
+    ``unit(x) > p`` where x = component ``index & 3`` of Philox counter ``index >> 2``."""
+    x = philox4x32(seed, offset, index >> 2).gather(-1, (index & 3).unsqueeze(-1)).squeeze(-1)
+    return _keep_scale(x, p)
+
+
 def dropout_add(h: torch.Tensor, res: Optional[torch.Tensor], p: float, seed: int, offset: int) -> torch.Tensor:
-    """``res + h o Z`` with Z the element-indexed mask of ``csrc/dropout.hip``."""
-    z = dropout_scale(torch.arange(h.numel(), device=h.device), p, seed, offset).view(h.shape).to(_f(h).dtype)
+    """``res + h o Z`` with Z the element-indexed mask of ``csrc/dropout.hip`` (one Philox
+    call per 4 consecutive elements, as the kernel)."""
+    n = h.numel()
+    words = philox4x32(seed, offset, torch.arange((n + 3) // 4, device=h.device)).reshape(-1)[:n]
+    z = _keep_scale(words, p).view(h.shape).to(_f(h).dtype)
     out = _f(h) * z
     return out if res is None else out + _f(res)
 
 
 def attention_dropout_scale(n: int, n_heads: int, T: int, p: float, seed: int, offset: int) -> torch.Tensor:
     """``[n, h, T, T]`` multipliers of the attention probabilities: element (title, head, t, s)
-    is mask index ``((title * h + head) * 64 + t) * 64 + s`` (title_attn.hip, T <= 64)."""
-    pair = torch.arange(n * n_heads, dtype=torch.int64).view(n, n_heads, 1, 1)
-    t = torch.arange(T, dtype=torch.int64).view(1, 1, T, 1)
-    s = torch.arange(T, dtype=torch.int64).view(1, 1, 1, T)
-    return dropout_scale((pair * 64 + t) * 64 + s, p, seed, offset)
+    is mask index ``((title * h + head) * 64 + t) * 64 + s`` (title_attn.hip, T <= 64), i.e.
+    Philox counter ``(pair * 64 + t) * 16 + s // 4``, word ``s % 4``."""
+    g = (T + 3) // 4
+    pair = torch.arange(n * n_heads, dtype=torch.int64).view(-1, 1, 1)
+    t = torch.arange(T, dtype=torch.int64).view(1, T, 1)
+    q = torch.arange(g, dtype=torch.int64).view(1, 1, g)
+    words = philox4x32(seed, offset, (pair * 64 + t) * 16 + q).reshape(n * n_heads, T, 4 * g)[..., :T]
+    return _keep_scale(words, p).view(n, n_heads, T, T)
 
 
 # ---------------------------------------------------------------------------------------

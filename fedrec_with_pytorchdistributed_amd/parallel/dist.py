@@ -176,3 +176,26 @@ def make_secure_grad_allreduce(ctx: DistContext, frac_bits: Optional[int] = None
         return 1.0 / W
 
     return _ar
+
+
+def make_bucket_reducer(ctx: DistContext, flat, secure: bool = False, bucket_mb: Optional[float] = None,
+                        timeout_s: float = 600.0, run_id: str = "secagg-bucket"):
+    """The backward-overlapped bucketed all-reduce (:class:`.reducer.BucketReducer`) over the
+    client data group; ``secure`` = pairwise-masked int32 buckets (seeds by Diffie-Hellman
+    over the store, as :func:`make_secure_grad_allreduce`).  None for a single client."""
+    from .reducer import DEFAULT_BUCKET_MB, BucketReducer
+
+    if ctx.num_clients <= 1 or not ctx.initialized:
+        return None
+    W, k = ctx.num_clients, ctx.client_index
+    seeds_row = None
+    if secure:
+        from . import secagg
+        from .control import ControlPlane
+
+        cp = ControlPlane.from_default(run_id, timeout_s)
+        kp = secagg.KeyPair()
+        cp.set(f"pk/{k}", secagg.public_bytes(kp))
+        seeds_row = secagg.seeds_from_publics(kp, k, [cp.get(f"pk/{j}") for j in range(W)])
+    mb = float(os.environ.get("FEDREC_BUCKET_MB", bucket_mb or DEFAULT_BUCKET_MB))
+    return BucketReducer(flat, ctx.data_group, W, "secure" if secure else "mean", mb, k, seeds_row)

@@ -1,0 +1,161 @@
+"""Bucketed gradient all-reduce overlapped with the backward (the DDP reducer's job).
+
+The reference wraps its model in DDP (``Gradient_Averaging_main.py:119``), whose reducer
+all-reduces gradient buckets as the backward produces them.  Here the trainable gradients
+live in one flat fp32 buffer (:class:`..models.fedrec_model.FlatParams`); this reducer cuts
+it into contiguous buckets along parameter boundaries (~28 MB: SURVEY §5.8 item 3, 8 ranks x
+7 xGMI links x 512 KB per-peer chunk), ordered as the backward fills them (last registered
+parameter first), and on a dedicated communication stream reduces each bucket as soon as
+every one of its parameters has its gradient -- while the backward of the earlier layers
+still runs on the compute stream.
+
+* ``op="mean"``: one RCCL SUM all-reduce per bucket (the 1/W lands in Adam's grad scale).
+* ``op="secure"``: pairwise-masked fixed-point aggregation per bucket (BASELINE config 5,
+  :mod:`.secagg`): ``m = max|g|`` on the device, one scalar MAX all-reduce, the mask
+  kernel derives the fixed-point exponent from ``m`` *on the device*, one int32 SUM
+  all-reduce cancels the masks exactly, the unmask kernel writes the dequantised sum back
+  into the bucket.  No host read anywhere (the round-1 form blocked on ``m.item()`` every
+  step).  The revealed per-bucket max|g| is the one value disclosed beyond the sum.
+
+Parameters register ``post_accumulate_grad`` hooks: the hook copies the fresh gradient into
+its flat slot, re-points ``.grad`` at the slot, and counts the bucket down.  A bucket whose
+parameters got no gradient is reduced by :meth:`finish` (after ``FlatParams.end_backward``
+zero-filled them), in bucket order, so every rank issues the same collective sequence.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .collcheck import CHECK
+
+DEFAULT_BUCKET_MB = 28.0
+
+
+class BucketReducer:
+    def __init__(self, flat, group, world: int, op: str = "mean", bucket_mb: float = DEFAULT_BUCKET_MB,
+                 client_index: int = 0, seeds_row=None):
+        if op not in ("mean", "secure"):
+            raise ValueError(f"BucketReducer op {op!r}")
+        self.flat, self.group, self.W, self.op = flat, group, int(world), op
+        self.k = client_index
+        dev = flat.grad.device
+        self.device = dev
+        cap = max(1, int(bucket_mb * 2**20) // 4)
+        # parameters in backward order (reverse registration) -> contiguous flat ranges
+        order = list(range(len(flat.params)))[::-1]
+        self.buckets: List[List[int]] = []
+        cur, size = [], 0
+        for i in order:
+            n = flat.params[i].numel()
+            if cur and size + n > cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += n
+        if cur:
+            self.buckets.append(cur)
+        self.ranges = []
+        for b in self.buckets:
+            lo = min(flat.offsets[i] for i in b)
+            hi = max(flat.offsets[i] + flat.params[i].numel() for i in b)
+            self.ranges.append((lo, hi))
+        self.bucket_of = {i: bi for bi, b in enumerate(self.buckets) for i in b}
+        self.comm = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self.step = 0
+        self._pending: List[int] = []
+        self._launched: List[bool] = []
+        self._active = False
+        if op == "secure":
+            from . import secagg
+
+            peers, sd, sg = secagg._peer_arrays(self.k, seeds_row)
+            self.sd = sd.to(dev)
+            self.sg = sg.to(dev)
+            self.seeds_row = seeds_row
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(flat.params)]
+
+    # -------------------------------------------------------------------------------
+    def begin(self) -> None:
+        """Arm the reducer for one backward pass."""
+        self._pending = [len(b) for b in self.buckets]
+        self._launched = [False] * len(self.buckets)
+        self._active = True
+
+    def _make_hook(self, i: int):
+        def hook(p: torch.Tensor) -> None:
+            if not self._active:
+                return
+            off, n = self.flat.offsets[i], p.numel()
+            view = self.flat.grad[off:off + n].view_as(p)
+            if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
+                view.copy_(p.grad)
+                p.grad = view
+            b = self.bucket_of[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._launch(b)
+        return hook
+
+    def _launch(self, b: int) -> None:
+        if self._launched[b]:
+            return
+        self._launched[b] = True
+        lo, hi = self.ranges[b]
+        g = self.flat.grad[lo:hi]
+        if self.comm is None:
+            self._reduce(g, b)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.comm.wait_event(ev)
+        with torch.cuda.stream(self.comm):
+            self._reduce(g, b)
+
+    def _reduce(self, g: torch.Tensor, b: int) -> None:
+        if self.op == "mean":
+            CHECK.record("all_reduce", g, f"bucket{b}")
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
+            return
+        from . import secagg
+
+        rnd = self.step * 4096 + b  # a fresh PRG counter space per (step, bucket)
+        m = torch.nan_to_num(g.abs().amax().float().reshape(1), nan=0.0, posinf=3.0e38)
+        CHECK.record("all_reduce", m, f"secagg-max{b}")
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
+        if g.is_cuda:
+            from ..ops import native
+
+            lib = native.require_for(g)
+            q = lib.secagg_mask_dev(g.contiguous(), self.sd, self.sg, m, self.W, rnd)
+            CHECK.record("all_reduce", q, f"secagg-sum{b}")
+            dist.all_reduce(q, op=dist.ReduceOp.SUM, group=self.group)
+            lib.secagg_unmask_dev_(q, m, self.W, g)
+            return
+        # host (gloo plumbing): same exponent rule, the reference-format masks of secagg.py
+        mv = max(float(m.item()), 1e-30)
+        f = max(0, min(int(math.floor(math.log2((2.0 ** 30) / (self.W * mv)))), 56))
+        q = secagg.mask_local(g, self.k, self.W, self.seeds_row, rnd, f, mv)
+        CHECK.record("all_reduce", q, f"secagg-sum{b}")
+        dist.all_reduce(q, op=dist.ReduceOp.SUM, group=self.group)
+        g.copy_(secagg.unmask_sum(q, f).view_as(g))
+
+    def finish(self) -> float:
+        """Reduce any bucket still waiting (parameters without a gradient: zero-filled by
+        ``end_backward``), make the compute stream wait for every bucket; returns 1/W."""
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:
+                self._launch(b)
+        if self.comm is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm)
+        self._active = False
+        self.step += 1
+        return 1.0 / self.W
+
+    def close(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

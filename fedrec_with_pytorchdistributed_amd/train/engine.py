@@ -122,6 +122,9 @@ class LocalEngine:
                                        truncate=not self.q.no_history_truncation, seed=cfg.seed, rank=rank)
         # grad_allreduce(flat_grad) -> scale to apply (1/W); None = local only
         self.grad_allreduce = grad_allreduce
+        # or a BucketReducer (large trainable sets: the unfrozen backbone): buckets reduced
+        # during the backward as their gradients land (set_reducer)
+        self.reducer = None
         self.sigma: Optional[float] = None  # LDP noise multiplier (set by the client driver)
         self.noise_offset = 0
         self.epoch = 0
@@ -153,6 +156,10 @@ class LocalEngine:
         # backbone's M) no longer drains the GPU at every step start
         lookahead = device.type == "cuda" and os.environ.get("FEDREC_LOOKAHEAD", "1") != "0"
         self._prep = torch.cuda.Stream(device) if lookahead else None
+
+    def set_reducer(self, reducer) -> None:
+        """Use a backward-overlapped bucket reducer (``parallel.reducer``) for the gradients."""
+        self.reducer = reducer
 
     def state(self) -> Dict[str, int]:
         """Counters that key the engine's randomness (checkpointed with the snapshot)."""
@@ -290,6 +297,8 @@ class LocalEngine:
         if self.epoch_table or not self.cfg.backbone.frozen:
             self.sync_params()
         self.flat.begin_backward()
+        if self.reducer is not None:
+            self.reducer.begin()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True, pre=pre)
         with obs.range("user_fwd"):
             u = self.model.user_encoder(his_v, his)
@@ -366,7 +375,10 @@ class LocalEngine:
 
     def _optimizer_step(self, extra_scale: float) -> None:
         scale = extra_scale
-        if self.grad_allreduce is not None:
+        if self.reducer is not None:
+            with obs.range("allreduce_wait"):
+                scale *= self.reducer.finish()
+        elif self.grad_allreduce is not None:
             with obs.range("allreduce"):
                 scale *= self.grad_allreduce(self.flat.grad)
         self.flat.step += 1

@@ -37,7 +37,7 @@ from ..parallel import comm
 from ..parallel import secagg
 from ..parallel.collcheck import CHECK
 from ..parallel.control import ControlPlane, Heartbeat
-from ..parallel.dist import DistContext, make_grad_allreduce, make_secure_grad_allreduce
+from ..parallel.dist import DistContext, make_bucket_reducer, make_grad_allreduce, make_secure_grad_allreduce
 from ..privacy.rdp import calibrate_client_sigma
 from ..utils import obs
 from ..utils.fault import FaultInjector
@@ -150,9 +150,18 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     model = build_model(cfg, ctx.device)
     start, est = _resume(cfg, model)
     _sync_initial(model, ctx, cfg.sync == "full")
-    ar = (make_secure_grad_allreduce(ctx, timeout_s=cfg.collective_timeout_s) if cfg.secagg.enabled
-          else make_grad_allreduce(ctx))
+    # large trainable sets (unfrozen backbone: ~66-110M grads) reduce in ~28 MB buckets during the
+    # backward; the frozen backbone's 4.66 MB head + user encoder is one flat bucket per step
+    bucketed = not cfg.backbone.frozen and os.environ.get("FEDREC_BUCKETED", "1") != "0"
+    if bucketed:
+        ar = None
+    else:
+        ar = (make_secure_grad_allreduce(ctx, timeout_s=cfg.collective_timeout_s) if cfg.secagg.enabled
+              else make_grad_allreduce(ctx))
     eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=ar)
+    if bucketed:
+        eng.set_reducer(make_bucket_reducer(ctx, model.flat, secure=cfg.secagg.enabled,
+                                            timeout_s=cfg.collective_timeout_s))
     eng.sigma = _maybe_dp(cfg, eng)
     eng.load_state(est)
     eng.epoch = start

@@ -38,6 +38,24 @@ def test_grad_avg_two_ranks(tmp_path):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("secure", [False, True])
+def test_grad_avg_unfrozen_bucketed_two_ranks(tmp_path, secure):
+    """Unfrozen backbone: gradients are reduced in buckets from autograd hooks during the
+    backward (the DDP-reducer equivalent), plain or pairwise-masked; tiny buckets force many
+    of them.  Both ranks must end bit-identical (GA keeps every client in lockstep)."""
+    argv = ["Gradient_Averaging_main.py", "1", "16", "1", *TINY, "--backbone.frozen=0", "--backbone.dropout=0",
+            "--backbone.attention_dropout=0",
+            f"--secagg.enabled={int(secure)}", f"--snapshot_path={tmp_path}/s.pt"]
+    outs = run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump"), "FEDREC_BUCKET_MB": "0.05",
+                                    "FEDREC_COLL_CHECK": "1"})
+    _ok(outs)
+    a = torch.load(tmp_path / "dump" / "rank0.pt")
+    b = torch.load(tmp_path / "dump" / "rank1.pt")
+    assert a.numel() > 2_000_000  # the backbone is in the trainable set
+    assert torch.equal(a, b)
+
+
+@pytest.mark.slow
 def test_param_avg_two_ranks(tmp_path):
     argv = ["Parameter_Averaging_main.py", "2", "16", "1", *TINY, f"--snapshot_path={tmp_path}/s.pt"]
     outs = run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump")})

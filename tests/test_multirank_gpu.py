@@ -61,3 +61,20 @@ def test_bench_configs_multi_client_on_gpu(dev, config, ranks):
     r = json.loads(lines[0])
     assert r["n_gpus"] == ranks and r["config"]["baseline_config"] == config
     assert r["value"] > 0 and r["train_loss"] == r["train_loss"]
+
+
+@pytest.mark.gpu
+def test_grad_avg_unfrozen_secure_buckets_two_clients_on_gpu(tmp_path, dev):
+    """Unfrozen backbone GA with pairwise-masked buckets reduced from autograd hooks on a
+    side stream during the backward (device-side fixed-point scale, no host read): both
+    clients end bit-identical."""
+    argv = ["Gradient_Averaging_main.py", "1", "16", "1", "--data_dir=synthetic:tiny", "--backbone.frozen=0",
+            "--backbone.n_layers=2", "--secagg.enabled=1", "--round_timeout_s=300", "--collective_timeout_s=300",
+            f"--snapshot_path={tmp_path}/s.pt"]
+    env = dict(SHARE, FEDREC_DUMP_FLAT=str(tmp_path / "dump"), FEDREC_BUCKET_MB="8")
+    outs = run_ranks([argv, argv], env, timeout=500)
+    _ok(outs)
+    a = torch.load(tmp_path / "dump" / "rank0.pt")
+    b = torch.load(tmp_path / "dump" / "rank1.pt")
+    assert a.numel() > 20_000_000 and torch.isfinite(a).all()
+    assert torch.equal(a, b)

@@ -560,3 +560,16 @@ def test_snapshot_restores_adam_rng_and_engine_counters(tmp_path):
     assert torch.equal(m2.flat.flat, m.flat.flat)
     assert e2.noise_offset == 17
     assert ckpt.client_snapshot_path("/x/snapshot.pt", 3) == "/x/client3_snapshot.pt"
+
+
+def test_backbone_preset_then_field_overrides_any_order():
+    """--backbone.name=X picks the preset, other backbone.* overrides apply on top of it
+    whatever their position (round 1 silently kept DistilBERT-base shapes for
+    --backbone.name=tiny --backbone.frozen=0)."""
+    for argv in (["--backbone.name=tiny", "--backbone.frozen=0"], ["--backbone.frozen=0", "--backbone.name=tiny"]):
+        c = FedRecConfig()
+        c.apply_overrides(argv)
+        assert c.backbone.dim == 64 and c.backbone.n_layers == 2 and not c.backbone.frozen
+    c = FedRecConfig()
+    c.apply_overrides(["--backbone.name=bert-base", "--backbone.dropout=0"])
+    assert c.backbone.n_layers == 12 and c.backbone.dropout == 0.0 and not c.backbone.frozen
