@@ -268,18 +268,23 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         eng.load_state(info["engine"])
         obs.log(f"[client {k}] resumed {csnap} (round {info['round']}, Adam step {model.flat.step})")
     beat = Heartbeat(cp, f"client{k}", cfg.heartbeat_s)
+    # model sync (server.py:76-77 / client.py:261-264): client 0 alone reads the coordinator's
+    # global model from the store and broadcasts it over the client data group (RCCL over
+    # xGMI on the GPU) -- one host transfer per round instead of one per client.  With a
+    # quorum < 1 a dead client must not stall a collective, so every client reads the store.
+    bcast = ctx.initialized and ctx.num_clients > 1 and ctx.data_group is not None and cfg.quorum >= 1.0
+    if k == 0:
+        plane = {"backend": dist.get_backend(ctx.data_group) if bcast else "store",
+                 "size": dist.get_world_size(ctx.data_group) if bcast else 1}
+        cp.put_json("data_plane", plane)
+        obs.log(f"[client 0] model sync: {plane}")
     last: Dict = {}
     while True:
         flag = cp.get(f"r{r}/go").decode()
         if flag != "1":
             break
         beat(force=True)
-        g = cp.get_tensor(f"r{r}/global")
-        with torch.no_grad():
-            model.flat.flat.copy_(g.to(model.flat.flat.device))
-        if full:
-            bb = cp.get_tensor(f"r{r}/backbone")
-            _load_flat_backbone(model, bb)
+        _receive_global(cp, r, model, ctx, full, bcast)
         _backbone_synced(model, full)
         eng.sigma = _maybe_dp(cfg, eng)
         eng.epoch = 0
@@ -331,6 +336,21 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
 def _flat_backbone(model: FedRecModel) -> torch.Tensor:
     ps = [p.detach().reshape(-1).float().cpu() for p in model.parameters() if not p.requires_grad]
     return torch.cat(ps) if ps else torch.zeros(0)
+
+
+def _receive_global(cp, r: int, model: FedRecModel, ctx: DistContext, full: bool, bcast: bool) -> None:
+    """Round ``r``'s global model into ``model`` (trainable flat buffer; + frozen backbone with
+    ``sync=full``): from the store, or read by client 0 and RCCL-broadcast to the others."""
+    if not bcast or ctx.client_index == 0:
+        g = cp.get_tensor(f"r{r}/global")
+        with torch.no_grad():
+            model.flat.flat.copy_(g.to(model.flat.flat.device))
+        if full:
+            _load_flat_backbone(model, cp.get_tensor(f"r{r}/backbone"))
+    if bcast:
+        frozen = [p.data for p in model.parameters() if not p.requires_grad] if full else []
+        with obs.range("model_broadcast"):
+            comm.broadcast_([model.flat.flat, *frozen], src=ctx.client_ranks[0], group=ctx.data_group)
 
 
 def _load_flat_backbone(model: FedRecModel, flat: torch.Tensor) -> None:

@@ -97,6 +97,8 @@ def test_star_fedavg_server_plus_two_clients(tmp_path):
     for key in ("text_encoder.fc.weight", "user_encoder.additive_attention.att_fc1.weight"):
         assert torch.allclose(g[key], (r0[key] + r1[key]) / 2, atol=1e-6), key
     assert not torch.equal(r0["text_encoder.fc.weight"], r1["text_encoder.fc.weight"])
+    # model sync: client 0 read the global model once and broadcast it over the client data group
+    assert "model sync: {'backend': 'gloo', 'size': 2}" in outs[0][1] + outs[2][1]
     # every client kept its own resumable snapshot (Adam moments + step, RNG, engine counters)
     for k in (0, 1):
         cs = torch.load(tmp_path / f"client{k}_c.pt", weights_only=True)
