@@ -3,12 +3,17 @@
 Each pass is its own run of the same short bench, so counters are joined per kernel family
 (summed over that family's dispatches), not per dispatch.  Derived metrics:
 
-* ``clock_GHz``     GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time (DVFS-lowered clock)
-* ``mfma_util``     SQ_VALU_MFMA_BUSY_CYCLES / (clock cycles x 256 CUs x 4 SIMDs)
+* ``mfma_util``     SQ_VALU_MFMA_BUSY_CYCLES / (2.4 GHz peak clock x kernel wall time x 256 CUs
+                    x 4 SIMDs): a LOWER bound (at a DVFS-lowered clock the true share is higher)
+* ``gui_active_GHz`` GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time -- NOT a clock: the counter
+                    window is wider than the kernel's timestamps (short kernels read 4-6 "GHz"),
+                    kept only as a diagnostic and flagged ``gui_window_exceeds_kernel`` > 2.4
 * ``lds_conflict``  SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles per LDS-array cycle)
-* ``hbm_TBps``      (FETCH_SIZE + WRITE_SIZE) [KB] / kernel wall time
+* ``read_TBps``     FETCH_SIZE [KB] / kernel wall time of its pass (L2-miss read traffic, which
+                    includes Infinity-Cache hits: not HBM bandwidth)
+* ``write_TBps``    WRITE_SIZE [KB] / kernel wall time of its pass (same caveat)
 
-Usage: python benchmarks/pmc_summary.py gpurun_out/pmc2 > profiles/pmc_r1_cfg2.json
+Usage: python benchmarks/pmc_summary.py gpurun_out/pmc2 > profiles/pmc_<tag>.json
 """
 import csv
 import json
@@ -16,6 +21,9 @@ import os
 import re
 import sys
 from collections import defaultdict
+
+
+PEAK_GHZ = 2.4  # MI355X peak engine clock
 
 
 def family(name: str) -> str:
@@ -64,10 +72,11 @@ def main(d: str) -> None:
         r = dict(c)
         w1 = c.get("wall_ns_p1", 0)
         if w1 and "GRBM_GUI_ACTIVE" in c:
-            clk = c["GRBM_GUI_ACTIVE"] / 8 / w1  # cycles per ns = GHz
-            r["clock_GHz"] = round(clk, 3)
-            if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
-                r["mfma_util"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (clk * w1 * 256 * 4), 4)
+            g = c["GRBM_GUI_ACTIVE"] / 8 / w1
+            r["gui_active_GHz"] = round(g, 3)
+            r["gui_window_exceeds_kernel"] = g > PEAK_GHZ
+        if w1 and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+            r["mfma_util"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (PEAK_GHZ * w1 * 256 * 4), 4)
         if c.get("SQ_LDS_IDX_ACTIVE"):
             r["lds_conflict"] = round(c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"], 4)
         if "FETCH_SIZE" in c and c.get("wall_ns_p2"):
