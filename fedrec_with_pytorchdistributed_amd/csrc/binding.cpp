@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <tuple>
+#include <vector>
 
 extern "C" {
 void fr_gemm_set_variant(int v);
@@ -78,6 +79,9 @@ int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R
 int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int W, const unsigned long long* seeds,
                        const int* signs, int npeers, unsigned long long round, hipStream_t s);
 int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
+int fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds, int n,
+                  hipStream_t s);
+int fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, hipStream_t s);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
 int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
@@ -536,6 +540,93 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
   return out;
 }
 
+// ---- small fp32 GEMMs on MFMA (small_gemm.hip): up to 6 independent GEMMs per launch -------
+// ints: 13 per GEMM (M, N, K, lda, ldb, ldc, a_mode, b_mode, act, accumulate, drop_ld, drop_on, gather_on);
+// floats: (alpha, pdrop) per GEMM; seeds: (seed, offset) per GEMM.  C tensors are written.
+// elements addressable from t.data_ptr() to the end of its storage (strided operand views)
+int64_t avail(const at::Tensor& t) {
+  return (int64_t)(t.storage().nbytes() / t.element_size()) - t.storage_offset();
+}
+
+void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<at::Tensor>>& gidx,
+                const std::vector<at::Tensor>& B, const c10::List<c10::optional<at::Tensor>>& bias,
+                const std::vector<at::Tensor>& C, at::IntArrayRef ints, at::ArrayRef<double> floats,
+                at::IntArrayRef seeds) {
+  const size_t n = A.size();
+  TORCH_CHECK(n >= 1 && n <= 6 && B.size() == n && C.size() == n && gidx.size() == n && bias.size() == n &&
+                  ints.size() == 13 * n && floats.size() == 2 * n && seeds.size() == 2 * n,
+              "fedrec::small_gemm: descriptor sizes");
+  const c10::DeviceGuard g(A[0].device());
+  std::vector<const void*> ptrs(5 * n);
+  std::vector<int> iv(13 * n);
+  std::vector<float> fv(2 * n);
+  std::vector<unsigned long long> sv(2 * n);
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t* q = ints.data() + 13 * i;
+    const int64_t M = q[0], N = q[1], K = q[2], lda = q[3], ldb = q[4], ldc = q[5], am = q[6], bm = q[7];
+    for (const at::Tensor* t : {&A[i], &B[i], &C[i]}) {  // row-major views with any leading dimension
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && (t->dim() == 0 || t->stride(-1) == 1),
+                  "fedrec::small_gemm: fp32 device operands with unit inner stride");
+    }
+    // bounds of the strided accesses the kernel makes (a kernel never sees a shape it was not written for)
+    const auto gv = gidx.get(i);
+    const bool gathered = gv.has_value() && gv->defined();
+    const int64_t gather_on = q[12];
+    // a gathered operand's rows are gidx values (checked in range by the producer: dedup)
+    if (!(gathered && gather_on == 1))
+      TORCH_CHECK(avail(A[i]) >= (am == 0 ? (M - 1) * lda + K : (K - 1) * lda + M) || M == 0 || K == 0,
+                  "fedrec::small_gemm: A too small");
+    if (!(gathered && gather_on == 2))
+      TORCH_CHECK(avail(B[i]) >= (bm == 0 ? (N - 1) * ldb + K : (K - 1) * ldb + N) || N == 0 || K == 0,
+                  "fedrec::small_gemm: B too small");
+    TORCH_CHECK(gathered == (gather_on != 0), "fedrec::small_gemm: gidx given iff gather_on");
+    TORCH_CHECK(avail(C[i]) >= (M - 1) * ldc + N || M == 0 || N == 0, "fedrec::small_gemm: C too small");
+    ptrs[5 * i + 0] = A[i].data_ptr();
+    ptrs[5 * i + 1] = nullptr;
+    if (gathered) {
+      TORCH_CHECK(gv->is_cuda() && gv->scalar_type() == at::kInt && gv->numel() >= (gather_on == 1 ? M : K),
+                  "fedrec::small_gemm: gidx int32[M] (A rows) or int32[K] (B rows)");
+      ptrs[5 * i + 1] = gv->data_ptr();
+    }
+    ptrs[5 * i + 2] = B[i].data_ptr();
+    const auto bv = bias.get(i);
+    ptrs[5 * i + 3] = nullptr;
+    if (bv.has_value() && bv->defined()) {
+      TORCH_CHECK(bv->is_cuda() && bv->scalar_type() == at::kFloat && bv->numel() >= N, "fedrec::small_gemm: bias");
+      ptrs[5 * i + 3] = bv->data_ptr();
+    }
+    ptrs[5 * i + 4] = C[i].data_ptr();
+    for (int j = 0; j < 13; ++j) iv[13 * i + j] = (int)q[j];
+    fv[2 * i] = (float)floats[2 * i];
+    fv[2 * i + 1] = (float)floats[2 * i + 1];
+    sv[2 * i] = (unsigned long long)seeds[2 * i];
+    sv[2 * i + 1] = (unsigned long long)seeds[2 * i + 1];
+  }
+  check_rc(fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), (int)n, cur_stream()), "small_gemm");
+}
+
+// column sums of fp32 matrices [M, N] (row stride ld) into out[N] (accumulate: out += sums)
+void colsum_f32(const std::vector<at::Tensor>& X, const std::vector<at::Tensor>& out, at::IntArrayRef ints) {
+  const size_t n = X.size();
+  TORCH_CHECK(n >= 1 && n <= 6 && out.size() == n && ints.size() == 4 * n, "fedrec::colsum_f32: sizes");
+  const c10::DeviceGuard g(X[0].device());
+  std::vector<const float*> xs(n);
+  std::vector<float*> os(n);
+  std::vector<int> iv(4 * n);
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(X[i].is_cuda() && X[i].scalar_type() == at::kFloat && out[i].is_cuda() &&
+                    out[i].scalar_type() == at::kFloat && (X[i].dim() == 0 || X[i].stride(-1) == 1) &&
+                    (out[i].dim() == 0 || out[i].stride(-1) == 1),
+                "fedrec::colsum_f32: fp32 device");
+    const int64_t M = ints[4 * i], N = ints[4 * i + 1], ld = ints[4 * i + 2];
+    TORCH_CHECK(avail(out[i]) >= N && (M == 0 || avail(X[i]) >= (M - 1) * ld + N), "fedrec::colsum_f32: shapes");
+    xs[i] = X[i].data_ptr<float>();
+    os[i] = out[i].data_ptr<float>();
+    for (int j = 0; j < 4; ++j) iv[4 * i + j] = (int)ints[4 * i + j];
+  }
+  check_rc(fr_colsum_f32(xs.data(), os.data(), iv.data(), (int)n, cur_stream()), "colsum_f32");
+}
+
 // device-scale secure aggregation (bucketed GA): the fixed-point exponent is derived on the device
 // from m = the clients' MAX-all-reduced max|x| -- no host read, no host sync
 at::Tensor secagg_mask_dev(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs, const at::Tensor& m,
@@ -831,6 +922,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
+  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds) -> ()");
+  m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");
   m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");
   m.def("dropout_add(Tensor h, Tensor? res, float p, int seed, int offset) -> Tensor");
@@ -870,6 +963,8 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("embed_grad", &embed_grad);
   m.impl("dropout_add", &dropout_add);
   m.impl("secagg_mask_dev", &secagg_mask_dev);
+  m.impl("small_gemm", &small_gemm);
+  m.impl("colsum_f32", &colsum_f32);
   m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);

@@ -244,3 +244,85 @@ def dedup(ids: torch.Tensor, num_news: int):
     uniq, inv = torch.unique(flat.long(), sorted=True, return_inverse=True)
     perm, ptr = segments_from_inv(inv, uniq.numel())
     return uniq.to(torch.int32), inv.to(torch.int32), perm, ptr
+
+
+# ---- small fp32 GEMMs on MFMA (csrc/small_gemm.hip) ------------------------------------------
+class Gemm:
+    """One GEMM of a :func:`small_gemm` launch: ``C = act(alpha * A(m,k) B(n,k) + bias) (+C)``.
+
+    ``a_mode`` 0: A row-major [M, K] (``gather_on=1``: row m is ``A[gidx[m]]``); 1: A stored
+    [K, M].  ``b_mode`` 0: B [N, K]; 1: B stored [K, N] (``gather_on=2``: row k is
+    ``B[gidx[k]]``).  ``drop_on`` 1/2/3: Philox dropout (p, seed, offset) on A elements
+    (m, k), on B elements (k, n), or on the output (m, n), element index ``row * drop_ld +
+    col`` in the logical (gathered) matrix -- the mask of ``ops.dropout_add``."""
+
+    __slots__ = ("A", "B", "C", "M", "N", "K", "lda", "ldb", "ldc", "a_mode", "b_mode", "act", "accumulate",
+                 "alpha", "bias", "gidx", "gather_on", "pdrop", "drop_on", "drop_ld", "seed", "offset")
+
+    def __init__(self, A, B, C, M, N, K, lda, ldb, ldc, a_mode=0, b_mode=0, act=0, accumulate=False, alpha=1.0,
+                 bias=None, gidx=None, gather_on=0, pdrop=0.0, drop_on=0, drop_ld=0, seed=0, offset=0):
+        self.A, self.B, self.C = A, B, C
+        self.M, self.N, self.K, self.lda, self.ldb, self.ldc = int(M), int(N), int(K), int(lda), int(ldb), int(ldc)
+        self.a_mode, self.b_mode, self.act, self.accumulate = int(a_mode), int(b_mode), int(act), bool(accumulate)
+        self.alpha, self.bias, self.gidx, self.gather_on = float(alpha), bias, gidx, int(gather_on)
+        self.pdrop, self.drop_on, self.drop_ld = float(pdrop), int(drop_on), int(drop_ld)
+        self.seed, self.offset = int(seed), int(offset)
+
+
+def small_gemm(*gs: Gemm) -> None:
+    """Run up to 6 independent GEMMs in one launch (device only)."""
+    ints, floats, seeds = [], [], []
+    for g in gs:
+        ints += [g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.a_mode, g.b_mode, g.act, int(g.accumulate), g.drop_ld,
+                 g.drop_on, g.gather_on]
+        floats += [g.alpha, g.pdrop]
+        seeds += [g.seed, g.offset]
+    native.require_for(gs[0].A).small_gemm([g.A for g in gs], [g.gidx for g in gs], [g.B for g in gs],
+                                           [g.bias for g in gs], [g.C for g in gs], ints, floats, seeds)
+
+
+def small_gemm_ref(g: Gemm) -> torch.Tensor:
+    """fp32 torch emulation of one :class:`Gemm` (operands rounded to bf16 like the kernel)
+    -> the new ``C`` [M, N] (tests)."""
+    def rows(t, n_rows, n_cols, ld, gidx=None):  # strided view semantics of the kernel (base + r * ld + c)
+        flat = torch.as_strided(t, (t.untyped_storage().nbytes() // t.element_size() - t.storage_offset(),), (1,),
+                                t.storage_offset())
+        idx = gidx.long()[:n_rows] if gidx is not None else torch.arange(n_rows, device=t.device)
+        return flat[(idx[:, None] * ld + torch.arange(n_cols, device=t.device)[None, :]).reshape(-1)].view(
+            n_rows, n_cols).float()
+
+    def drop(x):  # logical element (r, c) -> index r * drop_ld + c
+        idx = (torch.arange(x.shape[0], device=x.device)[:, None] * g.drop_ld
+               + torch.arange(x.shape[1], device=x.device)[None, :]).cpu()
+        return x * ref.dropout_scale(idx, g.pdrop, g.seed, g.offset).to(x.device)
+
+    A = rows(g.A, g.M, g.K, g.lda, g.gidx if g.gather_on == 1 else None) if g.a_mode == 0 else rows(g.A, g.K, g.M, g.lda).t()
+    if g.drop_on == 1:
+        A = drop(A)
+    if g.b_mode == 0:
+        Bm = rows(g.B, g.N, g.K, g.ldb)  # [N, K]
+    else:
+        Bk = rows(g.B, g.K, g.N, g.ldb, g.gidx if g.gather_on == 2 else None)  # [K, N]
+        if g.drop_on == 2:
+            Bk = drop(Bk)
+        Bm = Bk.t()
+    A = A.to(torch.bfloat16).float()
+    Bm = Bm.to(torch.bfloat16).float()
+    out = g.alpha * (A @ Bm.t())
+    if g.bias is not None:
+        out = out + g.bias.float()[:g.N]
+    if g.act == 1:
+        out = torch.tanh(out)
+    if g.drop_on == 3:
+        out = drop(out)
+    if g.accumulate:
+        out = out + rows(g.C, g.M, g.N, g.ldc)
+    return out
+
+
+def colsum_f32(pairs, accumulate: bool = False) -> None:
+    """``out[:N] (+)= X[:M, :N].sum(0)`` for each ``(X, out, M, N, ld)`` (one deterministic launch)."""
+    ints = []
+    for X, out, M, N, ld in pairs:
+        ints += [int(M), int(N), int(ld), int(accumulate)]
+    native.require_for(pairs[0][0]).colsum_f32([p[0] for p in pairs], [p[1] for p in pairs], ints)
