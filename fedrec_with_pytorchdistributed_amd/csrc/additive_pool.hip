@@ -11,8 +11,9 @@
 //
 // One 256-thread block per sequence (a title for the text head: T=50, D=768, Q=384; an
 // impression for the user encoder: H=50, D=400, Q=200).  x/e are bf16 (text path) or
-// fp32 (user path); statistics and outputs are fp32.  dw2/db2 are reduced in LDS per
-// block, then one float atomic per element per block.
+// fp32 (user path); statistics and outputs are fp32.  dw2/db2 (and the text kernel's dpre
+// column sums) are reduced in LDS per block and stored to the block's own partial row; the
+// caller sums the rows with the deterministic colsum kernel (no float atomics).
 #include "common.h"
 
 namespace {
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
   __shared__ float al_s[MAXT_G];
   __shared__ float red[4];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  dw2 += (size_t)(n % R) * Q;  // R accumulator replicas: 1/R of the atomic contention
+  dw2 += (size_t)(n % R) * Q;  // this block's partial row (R == n)
   db2 += n % R;
   const TX* xe = x + (size_t)n * T * D;
   const TX* ee = e + (size_t)n * T * Q;
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
     if (lane == 0) red[0] = sd;
   }
   __syncthreads();
-  if (tid == 0) atomicAdd(db2, red[0]);
+  if (tid == 0) *db2 = red[0];
   // dpre and dw2
   for (int q = tid; q < Q; q += 256) {
     const float wq = w2[q];
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
       acc += da * ev;
       dpre[((size_t)n * T + t) * Q + q] = (TX)(da * wq * (1.0f - ev * ev));
     }
-    atomicAdd(dw2 + q, acc);
+    dw2[q] = acc;
   }
   if (dx != nullptr) {
     for (int d = tid; d < D; d += 256) {
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
   __shared__ float al_s[MAXT];
   __shared__ float part[8][256 * 8 / 4];  // per t-group dw2 partials (Q <= 512 for TG >= 4)
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  dw2 += (size_t)(n % R) * Q;  // R accumulator replicas: 1/R of the atomic contention
+  dw2 += (size_t)(n % R) * Q;  // this block's partial row (R == n)
   db2 += n % R;
   dsum += (size_t)(n % R) * Q;  // column sums of dpre (= the att_fc1 bias gradient)
   const bf16* xe = x + (size_t)n * T * D;
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
       sd += v;
     }
     sd = wave_sum(sd);
-    if (lane == 0) atomicAdd(db2, sd);
+    if (lane == 0) *db2 = sd;
   }
   __syncthreads();
   // dpre_t = da_t w2 (1 - e_t^2) (bf16x8 stores); dw2 += sum_t da_t e_t
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
   for (int q = tid; q < Q; q += 256) {
     float sacc = 0.f;
     for (int j = 0; j < TG; ++j) sacc += part[j][q];
-    atomicAdd(dw2 + q, sacc);
+    dw2[q] = sacc;
   }
   __syncthreads();
   if (tg < TG) {
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
   for (int q = tid; q < Q; q += 256) {
     float sacc = 0.f;
     for (int j = 0; j < TG; ++j) sacc += part[j][q];
-    atomicAdd(dsum + q, sacc);
+    dsum[q] = sacc;
   }
 }
 
@@ -322,14 +323,14 @@ extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w
   return 0;
 }
 
-// dw2 / db2 point at R zeroed replicas ([R, Q] / [R]); the caller sums them.
-// dsum ([R, Q] zeroed): column sums of dpre, produced only by the vectorised text-head kernel.
+// dw2 / db2 point at n partial rows ([n, Q] / [n], R must equal n); the caller sums them.
+// dsum ([n, Q]): column sums of dpre, produced only by the vectorised text-head kernel.
 // Returns 0 when dsum was produced, -1 when the generic kernel ran (caller reduces dpre),
 // > 0 on argument errors.
 extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g,
                                     float* dx, void* dpre, float* dw2, float* db2, float* dsum, int n, int T, int D,
                                     int Q, int R, int is_bf16, hipStream_t s) {
-  if (T > MAXT_G) return 1;
+  if (T > MAXT_G || R != n) return 1;
   if (n == 0) return -1;
   if (is_bf16 && T <= MAXT && dx == nullptr && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256) {
     hipLaunchKernelGGL(pool_bwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, alpha, w2, g,

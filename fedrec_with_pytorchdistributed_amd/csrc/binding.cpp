@@ -79,9 +79,9 @@ int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R
 int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int W, const unsigned long long* seeds,
                        const int* signs, int npeers, unsigned long long round, hipStream_t s);
 int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
-int fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds, int n,
-                  hipStream_t s);
-int fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, hipStream_t s);
+long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
+                   const unsigned long long* dev_off, int n, float* scratch, hipStream_t s);
+long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part, hipStream_t s);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
 int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
@@ -335,8 +335,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor dx = want_dx ? at::empty({n, T, D}, fopt) : at::empty({0}, fopt);
   auto dpre = at::empty({n, T, Q}, e.options());
-  const int64_t R = std::max<int64_t>(1, std::min<int64_t>(n, 64));  // atomic replicas
-  auto red = at::zeros({2 * R * Q + R}, fopt);  // [dw2 replicas | dpre col-sum replicas | db2 replicas]
+  const int64_t R = std::max<int64_t>(1, n);  // one partial row per block (no float atomics)
+  auto red = at::empty({2 * R * Q + R}, fopt);  // [dw2 rows | dpre col-sum rows | db2 rows]
   float* dw2p = red.data_ptr<float>();
   float* dsump = dw2p + R * Q;
   float* db2p = dsump + R * Q;
@@ -344,10 +344,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_
                                       g.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr, dpre.data_ptr(),
                                       dw2p, db2p, dsump, (int)n, (int)T, (int)D, (int)Q, (int)R, bf, cur_stream());
   TORCH_CHECK(rc <= 0, "fedrec::additive_pool_bwd: kernel launch rejected the arguments (code ", rc, ")");
-  auto parts = red.narrow(0, 0, 2 * R * Q).view({2, R, Q}).sum(1);
-  auto dw2 = parts.select(0, 0);
-  auto dsum = rc == 0 ? parts.select(0, 1) : at::empty({0}, fopt);
-  auto db2 = red.narrow(0, 2 * R * Q, R).sum().view({1});
+  // the partial rows -> sums, one deterministic colsum launch (dw2, db2 and, from the text
+  // kernel, the dpre column sums)
+  auto sums = at::empty({2 * Q + 1}, fopt);
+  const float* xs[3] = {dw2p, db2p, dsump};
+  float* os[3] = {sums.data_ptr<float>(), sums.data_ptr<float>() + Q, sums.data_ptr<float>() + Q + 1};
+  const int ints[12] = {(int)n, (int)Q, (int)Q, 0, (int)n, 1, 1, 0, (int)n, (int)Q, (int)Q, 0};
+  const int ncs = rc == 0 ? 3 : 2;
+  const long need = fr_colsum_f32(xs, os, ints, ncs, nullptr, cur_stream());
+  auto part = at::empty({std::max<long>(need, 1)}, fopt);
+  TORCH_CHECK(need >= 0 && fr_colsum_f32(xs, os, ints, ncs, part.data_ptr<float>(), cur_stream()) == 0,
+              "fedrec::additive_pool_bwd: colsum failed");
+  auto dw2 = sums.narrow(0, 0, Q);
+  auto db2 = sums.narrow(0, Q, 1);
+  auto dsum = rc == 0 ? sums.narrow(0, Q + 1, Q) : at::empty({0}, fopt);
   return {dx, dpre, dw2, db2, dsum};
 }
 
@@ -551,7 +561,7 @@ int64_t avail(const at::Tensor& t) {
 void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<at::Tensor>>& gidx,
                 const std::vector<at::Tensor>& B, const c10::List<c10::optional<at::Tensor>>& bias,
                 const std::vector<at::Tensor>& C, at::IntArrayRef ints, at::ArrayRef<double> floats,
-                at::IntArrayRef seeds) {
+                at::IntArrayRef seeds, const c10::optional<at::Tensor>& dev_off) {
   const size_t n = A.size();
   TORCH_CHECK(n >= 1 && n <= 6 && B.size() == n && C.size() == n && gidx.size() == n && bias.size() == n &&
                   ints.size() == 13 * n && floats.size() == 2 * n && seeds.size() == 2 * n,
@@ -602,7 +612,22 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
     sv[2 * i] = (unsigned long long)seeds[2 * i];
     sv[2 * i + 1] = (unsigned long long)seeds[2 * i + 1];
   }
-  check_rc(fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), (int)n, cur_stream()), "small_gemm");
+  const unsigned long long* dop = nullptr;
+  if (dev_off.has_value() && dev_off->defined()) {  // int64 device counter added to every dropout offset
+    TORCH_CHECK(dev_off->is_cuda() && dev_off->scalar_type() == at::kLong && dev_off->numel() >= 1,
+                "fedrec::small_gemm: dev_off int64[1]");
+    dop = (const unsigned long long*)dev_off->data_ptr<int64_t>();
+  }
+  // first call: validate + ask for split-K partial space; second call: launch
+  long need = fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), dop, (int)n, nullptr, cur_stream());
+  TORCH_CHECK(need >= 0, "fedrec::small_gemm: descriptor rejected (code ", need, ")");
+  at::Tensor scratch;
+  if (need > 0) {
+    scratch = at::empty({need}, A[0].options());
+    const long rc = fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), dop, (int)n,
+                                  scratch.data_ptr<float>(), cur_stream());
+    TORCH_CHECK(rc == 0, "fedrec::small_gemm: launch failed (code ", rc, ")");
+  }
 }
 
 // column sums of fp32 matrices [M, N] (row stride ld) into out[N] (accumulate: out += sums)
@@ -624,7 +649,11 @@ void colsum_f32(const std::vector<at::Tensor>& X, const std::vector<at::Tensor>&
     os[i] = out[i].data_ptr<float>();
     for (int j = 0; j < 4; ++j) iv[4 * i + j] = (int)ints[4 * i + j];
   }
-  check_rc(fr_colsum_f32(xs.data(), os.data(), iv.data(), (int)n, cur_stream()), "colsum_f32");
+  const long need = fr_colsum_f32(xs.data(), os.data(), iv.data(), (int)n, nullptr, cur_stream());
+  TORCH_CHECK(need >= 0, "fedrec::colsum_f32: descriptor rejected");
+  auto part = at::empty({std::max<long>(need, 1)}, X[0].options());
+  TORCH_CHECK(fr_colsum_f32(xs.data(), os.data(), iv.data(), (int)n, part.data_ptr<float>(), cur_stream()) == 0,
+              "fedrec::colsum_f32: launch failed");
 }
 
 // device-scale secure aggregation (bucketed GA): the fixed-point exponent is derived on the device
@@ -922,7 +951,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
-  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds) -> ()");
+  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off=None) -> ()");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");
   m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");

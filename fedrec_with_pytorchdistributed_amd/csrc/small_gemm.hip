@@ -16,15 +16,17 @@
 //   act: 0 none, 1 tanh.  drop_on: 0 none, 1 A elements (m, k), 2 B elements (k, n) of a K-major
 //      B, 3 output elements (m, n) -- the input dropout's backward fused into the dgrad
 //      epilogue.  gather_on: 0 none, 1 A rows (a_mode 0), 2 B rows (b_mode 1).
-// Tile 64 x 64 x 32, 256 threads = 4 waves in 2 x 2, each wave 32 x 32 = 2 x 2 MFMA tiles.
-// Several independent GEMMs run in ONE launch (GemmBatch: the Q/K/V projections, the three
-// weight gradients of one backward, ...): blockIdx.x walks the concatenated tile lists.
-// Deterministic: no split-K, no atomics.
+// Tile 64 x 64 x 64, 256 threads = 4 waves in 2 x 2, each wave 32 x 32 = 2 x 2 MFMA tiles;
+// 16-byte global loads where aligned.  Several independent GEMMs run in ONE launch (GemmBatch:
+// the Q/K/V projections, the weight gradients of one backward, ...): blockIdx.x walks the
+// concatenated tile lists.  Long reductions with few output tiles (weight gradients over
+// K = B*H = 3200 rows) split K over workgroups into fp32 partials that a second kernel sums in
+// split order -- deterministic, no atomics.
 #include "common.h"
 
 namespace {
 
-constexpr int TM = 64, TN = 64, TK = 32, LDT = TK + 8;  // LDS row stride 40 bf16 = 80 B
+constexpr int TM = 64, TN = 64, TK = 64, LDT = TK + 8;  // LDS row stride 72 bf16 = 144 B
 constexpr int MAXG = 6;
 
 struct GemmDesc {
@@ -33,70 +35,81 @@ struct GemmDesc {
   const float* B;
   const float* bias;
   float* C;
+  float* P;  // split-K partials [splits, M, N] (splits > 1: the reduce kernel does the epilogue)
   int M, N, K, lda, ldb, ldc;
   int a_mode, b_mode, act, accumulate;
   float alpha, pdrop;
-  int drop_ld, drop_on, gather_on, tiles_n, tile_base;
-  unsigned long long seed, offset;
+  int drop_ld, drop_on, gather_on, tiles_n, tile_base, splits, kchunk;
+  unsigned long long seed, offset;  // offset += *dev_off when dev_off is set (graph replays)
 };
 
 struct GemmBatch {
   GemmDesc d[MAXG];
+  const unsigned long long* dev_off;  // per-launch device counter added to the dropout offsets
   int n;
 };
 
-__device__ __forceinline__ void load_tile(const GemmDesc& g, bool isA, int r0, int k0, bf16 (*S)[LDT], int tid) {
+__device__ __forceinline__ void load16(const float* __restrict__ p, bool full, bool vec, int valid, float (&v)[16]) {
+  if (full && vec) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 f = *(const float4*)(p + 4 * j);
+      v[4 * j] = f.x; v[4 * j + 1] = f.y; v[4 * j + 2] = f.z; v[4 * j + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = j < valid ? p[j] : 0.f;
+  }
+}
+
+__device__ __forceinline__ void apply_drop16(float (&v)[16], unsigned long long e, const GemmDesc& g,
+                                             unsigned long long off) {  // e: element index of v[0], % 16 == 0
+  const float inv_keep = 1.0f / (1.0f - g.pdrop);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4 x = Philox::gen(g.seed, off, (e >> 2) + q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * q + j] *= drop_scale(u4_get(x, j), g.pdrop, inv_keep);
+  }
+}
+
+// one 64 x 64 operand tile (rows r0.., k0..) -> bf16 LDS [row][k]
+__device__ __forceinline__ void load_tile(const GemmDesc& g, unsigned long long off, bool isA, int r0, int k0,
+                                          int kend, bf16 (*S)[LDT], int tid) {
   const int mode = isA ? g.a_mode : g.b_mode;
   const float* P = isA ? g.A : g.B;
   const int ld = isA ? g.lda : g.ldb;
   const int R = isA ? g.M : g.N;
-  if (mode == 0) {  // [R, K] row-major: thread -> (row, 8 consecutive k)
-    const int r = tid >> 2, kk = (tid & 3) * 8;
-    const int rr = r0 + r;
-    float v[8];
+  float v[16];
+  if (mode == 0) {  // [R, K] row-major: thread -> (row, 16 consecutive k)
+    const int r = tid >> 2, kk = (tid & 3) * 16;
+    const int rr = r0 + r, k = k0 + kk;
     const bool rok = rr < R;
     const int src = rok ? ((isA && g.gather_on == 1) ? g.gidx[rr] : rr) : 0;
+    const float* p = P + (size_t)src * ld + k;
+    const int valid = rok ? min(16, kend - k) : 0;
+    load16(p, valid == 16, ((uintptr_t)p & 15) == 0, valid, v);
+    if (isA && g.drop_on == 1 && rok) apply_drop16(v, (unsigned long long)rr * g.drop_ld + k, g, off);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = k0 + kk + j;
-      v[j] = (rok && k < g.K) ? P[(size_t)src * ld + k] : 0.f;
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[8 * h + j]);
+      *(bf16x8*)&S[r][kk + 8 * h] = o;
     }
-    if (isA && g.drop_on == 1 && rok) {
-      const unsigned long long e = (unsigned long long)rr * g.drop_ld + (k0 + kk);  // multiple of 4
-      const float inv_keep = 1.0f / (1.0f - g.pdrop);
-      const uint4 x0 = Philox::gen(g.seed, g.offset, e >> 2);
-      const uint4 x1 = Philox::gen(g.seed, g.offset, (e >> 2) + 1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= drop_scale(u4_get(j < 4 ? x0 : x1, j & 3), g.pdrop, inv_keep);
-    }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-    *(bf16x8*)&S[r][kk] = o;
-  } else {  // stored [K, R]: thread -> (k, 8 consecutive rows), coalesced along the rows
-    const int k = tid >> 3, rr8 = (tid & 7) * 8;
+  } else {  // stored [K, R]: thread -> (k, 16 consecutive rows), coalesced along the rows
+    const int k = tid >> 2, rr16 = (tid & 3) * 16;
     const int kg = k0 + k;
+    const bool kok = kg < kend;
     // B in mode 1 may be the gathered + dropped-out input of the forward (the weight
     // gradient dW = dY^T X' regenerates X' = drop(X[gidx]) instead of storing it)
-    const bool gat = !isA && g.gather_on == 2;
-    const bool drop = !isA && g.drop_on == 2;
-    const size_t src = (kg < g.K) ? (size_t)(gat ? g.gidx[kg] : kg) : 0;
-    float v[8];
+    const size_t src = kok ? (size_t)((!isA && g.gather_on == 2) ? g.gidx[kg] : kg) : 0;
+    const float* p = P + src * ld + r0 + rr16;
+    const int valid = kok ? min(16, R - (r0 + rr16)) : 0;
+    load16(p, valid == 16, ((uintptr_t)p & 15) == 0, valid, v);
+    if (!isA && g.drop_on == 2 && kok) apply_drop16(v, (unsigned long long)kg * g.drop_ld + r0 + rr16, g, off);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int rr = r0 + rr8 + j;
-      v[j] = (kg < g.K && rr < R) ? P[src * ld + rr] : 0.f;
-    }
-    if (drop && kg < g.K) {
-      const unsigned long long e = (unsigned long long)kg * g.drop_ld + (r0 + rr8);  // multiple of 8
-      const float inv_keep = 1.0f / (1.0f - g.pdrop);
-      const uint4 x0 = Philox::gen(g.seed, g.offset, e >> 2);
-      const uint4 x1 = Philox::gen(g.seed, g.offset, (e >> 2) + 1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= drop_scale(u4_get(j < 4 ? x0 : x1, j & 3), g.pdrop, inv_keep);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) S[rr8 + j][k] = f2bf(v[j]);
+    for (int j = 0; j < 16; ++j) S[rr16 + j][k] = f2bf(v[j]);
   }
 }
 
@@ -108,8 +121,12 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   for (int i = 1; i < MAXG; ++i)
     if (i < batch.n && (int)blockIdx.x >= batch.d[i].tile_base) gi = i;
   const GemmDesc& g = batch.d[gi];
-  const int t = blockIdx.x - g.tile_base;
+  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+  int t = blockIdx.x - g.tile_base;
+  const int split = t % g.splits;
+  t /= g.splits;
   const int m0 = (t / g.tiles_n) * TM, n0 = (t % g.tiles_n) * TN;
+  const int kbeg = split * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   const int fr = lane & 15, fq = lane >> 4;
@@ -118,26 +135,41 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < g.K; k0 += TK) {
+  for (int k0 = kbeg; k0 < kend; k0 += TK) {
     __syncthreads();
-    load_tile(g, true, m0, k0, As, tid);
-    load_tile(g, false, n0, k0, Bs, tid);
+    load_tile(g, off, true, m0, k0, kend, As, tid);
+    load_tile(g, off, false, n0, k0, kend, Bs, tid);
     __syncthreads();
-    bf16x8 a[2], b[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) a[i] = *(const bf16x8*)&As[wm + i * 16 + fr][fq * 8];
+    for (int ks = 0; ks < TK; ks += 32) {
+      bf16x8 a[2], b[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = *(const bf16x8*)&Bs[wn + j * 16 + fr][fq * 8];
+      for (int i = 0; i < 2; ++i) a[i] = *(const bf16x8*)&As[wm + i * 16 + fr][ks + fq * 8];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j) b[j] = *(const bf16x8*)&Bs[wn + j * 16 + fr][ks + fq * 8];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
   }
   // lane holds C[m = wm + 16 i + 4 fq + r][n = wn + 16 j + fr]
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn + j * 16 + fr;
     if (n >= g.N) continue;
+    if (g.splits > 1) {  // raw partial; alpha / accumulate in splitk_reduce_kernel
+      float* pp = g.P + (size_t)split * g.M * g.N;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm + i * 16 + fq * 4 + r;
+          if (m < g.M) pp[(size_t)m * g.N + n] = acc[i][j][r];
+        }
+      continue;
+    }
     const float bn = g.bias ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -149,7 +181,7 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
         if (g.act == 1) v = tanhf(v);
         if (g.drop_on == 3) {  // dropout backward in the epilogue: element (m, n) of the dropped input
           const unsigned long long e = (unsigned long long)m * g.drop_ld + n;
-          const uint4 x = Philox::gen(g.seed, g.offset, e >> 2);
+          const uint4 x = Philox::gen(g.seed, off, e >> 2);
           v *= drop_scale(u4_get(x, (int)(e & 3)), g.pdrop, 1.0f / (1.0f - g.pdrop));
         }
         float* c = g.C + (size_t)m * g.ldc + n;
@@ -159,46 +191,95 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   }
 }
 
-// Deterministic fp32 column sums (bias gradients): block = 64 columns, 4 waves take rows
-// w, w + 4, ... and combine in a fixed order.  Several matrices per launch (ColsumBatch).
+// split-K epilogue: C = alpha * sum_s P[s] (+ C), partials summed in split order (deterministic)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batch, int total) {
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    int gi = 0, base = 0;
+    for (int i = 0; i < batch.n; ++i) {
+      const GemmDesc& d = batch.d[i];
+      const int sz = d.splits > 1 ? d.M * d.N : 0;
+      if (e < base + sz) { gi = i; break; }
+      base += sz;
+    }
+    const GemmDesc& g = batch.d[gi];
+    const int idx = e - base, m = idx / g.N, n = idx - m * g.N;
+    float s = 0.f;
+    for (int sp = 0; sp < g.splits; ++sp) s += g.P[(size_t)sp * g.M * g.N + idx];
+    float* c = g.C + (size_t)m * g.ldc + n;
+    const float v = g.alpha * s;
+    *c = g.accumulate ? *c + v : v;
+  }
+}
+
+// Deterministic fp32 column sums (bias gradients), two passes: (1) blocks of 64 columns x 128
+// rows (4 waves x 32 rows) write per-chunk partials; (2) the partials are summed in chunk order.
+constexpr int CS_ROWS = 128;
 struct ColsumDesc {
   const float* X;
   float* out;
-  int M, N, ld, col_blocks, block_base, accumulate;
+  float* part;  // [chunks, N]
+  int M, N, ld, col_blocks, chunks, block_base, block2_base, accumulate;
 };
 struct ColsumBatch {
   ColsumDesc d[MAXG];
   int n;
 };
 
-__global__ __launch_bounds__(256) void colsum_f32_kernel(const ColsumBatch batch) {
+__global__ __launch_bounds__(256) void colsum_part_kernel(const ColsumBatch batch) {
   __shared__ float part[4][64];
   int gi = 0;
 #pragma unroll
   for (int i = 1; i < MAXG; ++i)
     if (i < batch.n && (int)blockIdx.x >= batch.d[i].block_base) gi = i;
   const ColsumDesc& g = batch.d[gi];
-  const int c = (blockIdx.x - g.block_base) * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.x - g.block_base;
+  const int cb = b % g.col_blocks, ch = b / g.col_blocks;
+  const int c = cb * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
+  const int r0 = ch * CS_ROWS, r1 = min(g.M, r0 + CS_ROWS);
   float s = 0.f;
   if (c < g.N)
-    for (int m = w; m < g.M; m += 4) s += g.X[(size_t)m * g.ld + c];
+    for (int m = r0 + w; m < r1; m += 4) s += g.X[(size_t)m * g.ld + c];
   part[w][threadIdx.x & 63] = s;
   __syncthreads();
-  if (w == 0 && c < g.N) {
-    const float v = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
-    g.out[c] = g.accumulate ? g.out[c] + v : v;
-  }
+  if (w == 0 && c < g.N)
+    g.part[(size_t)ch * g.N + c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+}
+
+__global__ __launch_bounds__(64) void colsum_final_kernel(const ColsumBatch batch) {
+  int gi = 0;
+#pragma unroll
+  for (int i = 1; i < MAXG; ++i)
+    if (i < batch.n && (int)blockIdx.x >= batch.d[i].block2_base) gi = i;
+  const ColsumDesc& g = batch.d[gi];
+  const int c = (blockIdx.x - g.block2_base) * 64 + threadIdx.x;
+  if (c >= g.N) return;
+  float s = 0.f;
+  for (int ch = 0; ch < g.chunks; ++ch) s += g.part[(size_t)ch * g.N + c];
+  g.out[c] = g.accumulate ? g.out[c] + s : s;
 }
 
 }  // namespace
 
-// descs: 5 pointers + 13 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm
-extern "C" int fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats,
-                             const unsigned long long* seeds, int n, hipStream_t s) {
-  if (n < 1 || n > MAXG) return 1;
+// descs: 5 pointers + 13 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
+// scratch: split-K partial space (floats) the caller allocated; returns the floats it needs
+// when scratch is null (query mode).
+static int choose_splits(int M, int N, int K) {
+  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  if (K < 512 || tiles >= 192) return 1;
+  int s = (256 + tiles - 1) / tiles;  // about one wave of workgroups over the 256 CUs
+  s = min(s, K / 256);
+  return max(1, min(s, 16));
+}
+
+extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats,
+                              const unsigned long long* seeds, const unsigned long long* dev_off, int n, float* scratch,
+                              hipStream_t s) {
+  if (n < 1 || n > MAXG) return -1;
   GemmBatch b{};
+  b.dev_off = dev_off;
   int tiles = 0;
+  long need = 0;
+  int red_total = 0;
   for (int i = 0; i < n; ++i) {
     GemmDesc& d = b.d[i];
     d.A = (const float*)ptrs[5 * i + 0];
@@ -214,26 +295,44 @@ extern "C" int fr_small_gemm(const void* const* ptrs, const int* ints, const flo
     d.pdrop = floats[2 * i + 1];
     d.seed = seeds[2 * i];
     d.offset = seeds[2 * i + 1];
-    if (d.M < 0 || d.N < 0 || d.K < 0) return 2;
-    if (d.drop_on < 0 || d.drop_on > 3 || d.gather_on < 0 || d.gather_on > 2 || d.act < 0 || d.act > 1) return 3;
-    if (d.drop_on && (!(d.pdrop > 0.f && d.pdrop < 1.f) || d.drop_ld % 8 != 0 || (d.drop_on == 1 && d.a_mode != 0) ||
+    if (d.M < 0 || d.N < 0 || d.K < 0) return -2;
+    if (d.drop_on < 0 || d.drop_on > 3 || d.gather_on < 0 || d.gather_on > 2 || d.act < 0 || d.act > 1) return -3;
+    if (d.drop_on && (!(d.pdrop > 0.f && d.pdrop < 1.f) || d.drop_ld % 16 != 0 || (d.drop_on == 1 && d.a_mode != 0) ||
                       (d.drop_on == 2 && d.b_mode != 1)))
-      return 3;
-    if (d.gather_on && (!d.gidx || (d.gather_on == 1 && d.a_mode != 0) || (d.gather_on == 2 && d.b_mode != 1))) return 4;
+      return -3;
+    if (d.gather_on && (!d.gidx || (d.gather_on == 1 && d.a_mode != 0) || (d.gather_on == 2 && d.b_mode != 1))) return -4;
+    // split-K only for plain epilogues (no bias / act / output dropout): the reduce applies alpha + accumulate
+    d.splits = (d.bias == nullptr && d.act == 0 && d.drop_on != 3) ? choose_splits(d.M, d.N, d.K) : 1;
+    d.kchunk = d.splits > 1 ? ((d.K + d.splits - 1) / d.splits + TK - 1) / TK * TK : d.K;
+    if (d.splits > 1) d.splits = (d.K + d.kchunk - 1) / d.kchunk;
+    d.P = nullptr;
+    if (d.splits > 1) {
+      d.P = scratch ? scratch + need : nullptr;
+      need += (long)d.splits * d.M * d.N;
+      red_total += d.M * d.N;
+    }
     d.tiles_n = (d.N + TN - 1) / TN;
     d.tile_base = tiles;
-    tiles += ((d.M + TM - 1) / TM) * d.tiles_n;
+    tiles += ((d.M + TM - 1) / TM) * d.tiles_n * d.splits;
   }
   b.n = n;
+  if (scratch == nullptr && need > 0) return need;  // query: the caller allocates and calls again
   if (tiles == 0) return 0;
   hipLaunchKernelGGL(small_gemm_kernel, dim3(tiles), dim3(256), 0, s, b);
+  if (red_total > 0) {
+    const int blocks = min(2048, (red_total + 255) / 256);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, b, red_total);
+  }
   return 0;
 }
 
-extern "C" int fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, hipStream_t s) {
-  if (n < 1 || n > MAXG) return 1;
+// returns the scratch floats needed when part == nullptr (query mode), else launches
+extern "C" long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part,
+                              hipStream_t s) {
+  if (n < 1 || n > MAXG) return -1;
   ColsumBatch b{};
-  int blocks = 0;
+  int blocks = 0, blocks2 = 0;
+  long need = 0;
   for (int i = 0; i < n; ++i) {
     ColsumDesc& d = b.d[i];
     d.X = xs[i];
@@ -243,11 +342,18 @@ extern "C" int fr_colsum_f32(const float* const* xs, float* const* outs, const i
     d.ld = ints[4 * i + 2];
     d.accumulate = ints[4 * i + 3];
     d.col_blocks = (d.N + 63) / 64;
+    d.chunks = max(1, (d.M + CS_ROWS - 1) / CS_ROWS);
+    d.part = part ? part + need : nullptr;
+    need += (long)d.chunks * d.N;
     d.block_base = blocks;
-    blocks += d.col_blocks;
+    blocks += d.col_blocks * d.chunks;
+    d.block2_base = blocks2;
+    blocks2 += d.col_blocks;
   }
   b.n = n;
+  if (part == nullptr) return need;
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(colsum_f32_kernel, dim3(blocks), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(blocks), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(blocks2), dim3(64), 0, s, b);
   return 0;
 }

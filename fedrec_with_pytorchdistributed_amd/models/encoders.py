@@ -122,6 +122,8 @@ class TextEncoder(nn.Module):
         tokens from the pooling when ``mask_padding`` is on (the reference pools over them: Q7)."""
         keep = (token_mask != 0) if (self.cfg.mask_padding and token_mask is not None) else None
         pooled = self.additive_attention(hidden, keep)
+        if pooled.is_cuda:  # K07 on the small MFMA GEMM (fwd + bwd), not the vendor library
+            return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias)
         return F.linear(pooled, self.fc.weight, self.fc.bias)
 
     def forward(self, text: torch.Tensor) -> torch.Tensor:

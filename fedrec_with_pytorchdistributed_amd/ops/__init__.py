@@ -192,7 +192,9 @@ def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: floa
     """Per-news gradient reduction ``out[inv[r]] += clip(rows[r]) + N(0, noise_std)``.
 
     ``seg = (perm, seg_ptr)`` (rows grouped by output id) enables the deterministic,
-    atomic-free device kernel; it is produced by :func:`dedup`.
+    atomic-free device kernel; it is produced by :func:`dedup`.  The device kernel expects
+    the layout dedup produces: every output row has occurrences, except trailing padded rows
+    (``zero_empty``, the step graphs' padded unique lists).
     """
     if _dev(rows):
         if seg is None:
@@ -269,8 +271,9 @@ class Gemm:
         self.seed, self.offset = int(seed), int(offset)
 
 
-def small_gemm(*gs: Gemm) -> None:
-    """Run up to 6 independent GEMMs in one launch (device only)."""
+def small_gemm(*gs: Gemm, dev_off=None) -> None:
+    """Run up to 6 independent GEMMs in one launch (device only).  ``dev_off``: an int64[1]
+    device counter added to every dropout offset (HIP-graph replays draw fresh masks)."""
     ints, floats, seeds = [], [], []
     for g in gs:
         ints += [g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.a_mode, g.b_mode, g.act, int(g.accumulate), g.drop_ld,
@@ -278,7 +281,7 @@ def small_gemm(*gs: Gemm) -> None:
         floats += [g.alpha, g.pdrop]
         seeds += [g.seed, g.offset]
     native.require_for(gs[0].A).small_gemm([g.A for g in gs], [g.gidx for g in gs], [g.B for g in gs],
-                                           [g.bias for g in gs], [g.C for g in gs], ints, floats, seeds)
+                                           [g.bias for g in gs], [g.C for g in gs], ints, floats, seeds, dev_off)
 
 
 def small_gemm_ref(g: Gemm) -> torch.Tensor:

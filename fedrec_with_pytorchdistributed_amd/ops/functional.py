@@ -434,3 +434,126 @@ class EmbedLNFn(torch.autograd.Function):
         dpos = torch.zeros(ctx.shapes[1], dtype=torch.float32, device=dy.device)
         dpos[:T] = bgrad(dx0.view(n, -1)).view(T, -1)  # per-position sum over titles
         return None, dword, dpos, dw, db, None, None, None
+
+
+# ---------------------------------------------------------------------------------------
+# the device user side of a step as ONE autograd Function:
+# candidate gather -> [gather + dropout + Q|K|V projection] -> user attention -> additive
+# pool -> sigmoid-CE, and a hand-written backward.  Every GEMM is csrc/small_gemm.hip, every
+# bias gradient the deterministic colsum, the per-news reduction (+ LDP) the segment sum.
+# ---------------------------------------------------------------------------------------
+class UserStepFn(torch.autograd.Function):
+    """``loss, scores = UserStepFn(v, inv, perm, ptr, ...)`` for news vectors ``v [U, D]``.
+
+    ``inv [R]`` maps the batch's occurrences (``B*C`` candidates, then ``B*H`` history
+    slots) to rows of ``v``; ``perm / ptr`` group them per news for the segment sum.  The
+    input dropout of the user encoder (``encoder.py:50``) is the Philox mask of element
+    ``(b*H + t) * D + d`` of the gathered history matrix with offset ``drop[2] + *dev_off``
+    -- applied in the Q/K/V GEMMs' operand loads, regenerated by the weight-gradient GEMMs'
+    loads and by the dgrad's epilogue (nothing is stored)."""
+
+    @staticmethod
+    def forward(ctx, v, inv, perm, ptr, wq, bq, wk, bk, wv, bv, w1, b1, w2, b2, meta):
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded = meta
+        D = v.shape[1]
+        BC, BH = B * C, B * H
+        Qd = w1.shape[0]
+        his_idx = inv[BC:]
+        cand = v.index_select(0, inv[:BC].long()).view(B, C, D)
+        qkv = torch.empty(BH, 3 * D, device=v.device, dtype=torch.float32)
+        p, seed, off = drop
+        dkw = dict(pdrop=p, drop_on=1, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
+        ops.small_gemm(*[ops.Gemm(v, w, qkv[:, s * D:(s + 1) * D], BH, D, D, D, D, 3 * D, bias=b, gidx=his_idx,
+                                  gather_on=1, **dkw)
+                         for s, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv)))], dev_off=dev_off)
+        q3 = qkv.view(B, H, 3 * D)
+        c3, stats = ops.user_attention_fwd(q3, heads, hd)
+        e = torch.empty(BH, Qd, device=v.device, dtype=torch.float32)
+        ops.small_gemm(ops.Gemm(c3, w1, e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
+        e3 = e.view(B, H, Qd)
+        u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2)
+        loss, scores, dcand, du = ops.score_ce(cand, u, act)
+        ctx.save_for_backward(v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2)
+        ctx.meta = meta
+        ctx.mark_non_differentiable(scores)
+        return loss, scores
+
+    @staticmethod
+    def backward(ctx, gloss, gscores):
+        v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2 = ctx.saved_tensors
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded = ctx.meta
+        D = v.shape[1]
+        BC, BH = B * C, B * H
+        Qd = w1.shape[0]
+        dev = v.device
+        R = inv.numel()
+        rows = torch.empty(R, D, device=dev, dtype=torch.float32)  # per-occurrence news gradients
+        torch.mul(dcand.view(BC, D), gloss, out=rows[:BC])
+        du_g = du * gloss
+        # additive pool backward: dx_direct = alpha du, dpre = da w2 (1 - e^2), dw2, db2
+        dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du_g, True)
+        dpre2 = dpre.view(BH, Qd)
+        ops.small_gemm(ops.Gemm(dpre2, w1, dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
+        dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd).view(BH, 3 * D)
+        p, seed, off = drop
+        his_idx = inv[BC:]
+        dx = rows[BC:]
+        # dx = (dQ Wq + dK Wk + dV Wv) o Z: three accumulating passes, the dropout backward in
+        # each epilogue (linear, so drop(a + b + c) = drop(a) + drop(b) + drop(c))
+        ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
+        for s, w in enumerate((wq, wk, wv)):
+            ops.small_gemm(ops.Gemm(dqkv[:, s * D:(s + 1) * D], w, dx, BH, D, D, 3 * D, D, D, b_mode=1,
+                                    accumulate=s > 0, **ekw), dev_off=dev_off)
+        # weight gradients in one launch: dW_s = dS^T X' (X' = the gathered, dropped-out input,
+        # regenerated in the B loads) and dW1 = dpre^T ctx
+        gq, gk, gv = (torch.empty(D, D, device=dev) for _ in range(3))
+        gw1 = torch.empty(Qd, D, device=dev)
+        bkw = dict(pdrop=p, drop_on=2, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
+        ops.small_gemm(*[ops.Gemm(dqkv[:, s * D:(s + 1) * D], v, g, D, D, BH, 3 * D, D, D, a_mode=1, b_mode=1,
+                                  gidx=his_idx, gather_on=2, **bkw) for s, g in enumerate((gq, gk, gv))],
+                       ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1), dev_off=dev_off)
+        gbq, gbk, gbv = (torch.empty(D, device=dev) for _ in range(3))
+        gb1 = torch.empty(Qd, device=dev)
+        ops.colsum_f32([(dqkv[:, 0:D], gbq, BH, D, 3 * D), (dqkv[:, D:2 * D], gbk, BH, D, 3 * D),
+                        (dqkv[:, 2 * D:], gbv, BH, D, 3 * D), (dpre2, gb1, BH, Qd, Qd)])
+        clip, noise, lseed, loff = ldp
+        dv = ops.segment_sum_rows(rows, inv, v.shape[0], clip, noise, lseed, loff, seg=(perm, ptr), zero_empty=padded)
+        return (dv, None, None, None, gq, gbq, gk, gbk, gv, gbv, gw1, gb1, dw2.view(1, -1), db2.view(1), None)
+
+
+def user_step(v, inv, perm, ptr, user_encoder, B: int, C: int, H: int, act: str, drop, dev_off, ldp, padded: bool):
+    """Device user side of a step (see :class:`UserStepFn`) -> ``(loss, scores)``."""
+    mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
+    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded)
+    return UserStepFn.apply(v, inv, perm, ptr, mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias,
+                            mha.W_V.weight, mha.W_V.bias, pool.att_fc1.weight, pool.att_fc1.bias,
+                            pool.att_fc2.weight, pool.att_fc2.bias, meta)
+
+
+class HeadFCFn(torch.autograd.Function):
+    """The text head's ``fc`` (``encoder.py:22,29``: [n, 768] -> [n, 400]) on the small MFMA
+    GEMM: forward NT, backward dgrad (NN), wgrad (TN) in one launch, bias gradient by colsum."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        n, K = x.shape
+        N = w.shape[0]
+        x = x.contiguous()
+        y = torch.empty(n, N, device=x.device, dtype=torch.float32)
+        ops.small_gemm(ops.Gemm(x, w, y, n, N, K, K, K, N, bias=b))
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        n, K = x.shape
+        N = w.shape[0]
+        dy = dy.contiguous().float()
+        dx = torch.empty(n, K, device=x.device, dtype=torch.float32)
+        dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+        db = torch.empty(N, device=x.device, dtype=torch.float32)
+        ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1),
+                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1))
+        ops.colsum_f32([(dy, db, n, N, N)])
+        return dx, dw, db

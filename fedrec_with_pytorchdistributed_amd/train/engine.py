@@ -133,6 +133,15 @@ class LocalEngine:
         self.news_table: Optional[torch.Tensor] = None
         # train-mode dropout masks of the backbone (unfrozen training, Q4 replay): Philox key per client
         model.text_encoder.DistillBert.drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 1
+        # device user side as one fused autograd Function (ops.functional.UserStepFn): our GEMMs
+        # and kernels end to end; the user-input dropout mask is Philox keyed by (seed, step),
+        # the step being a device counter so HIP-graph replays draw fresh masks
+        ue = model.user_encoder
+        self.fused_user = (device.type == "cuda" and not cfg.mask_padding
+                           and ue.multihead_attention.n_heads * ue.multihead_attention.d_k == cfg.news_dim
+                           and os.environ.get("FEDREC_FUSED_USER", "1") != "0")
+        self.user_drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 2
+        self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
         self.hcache = self._make_hidden_cache()
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
@@ -291,6 +300,24 @@ class LocalEngine:
         his_v = rows[B * C:].view(B, H, -1)
         return uniq, v, cand_v, his_v
 
+    def _user_loss(self, v: torch.Tensor, dd, B: int, C: int, H: int, padded: bool, train: bool):
+        """Device user side (fused): ``(loss, scores)`` from news vectors ``v`` of the unique ids."""
+        uniq, inv, perm, ptr = dd
+        p = float(self.cfg.user_dropout) if train else 0.0
+        clip, std = self._ldp()
+        ldp = (clip, std, self.cfg.seed * 7919 + self.rank, self.noise_offset)
+        if train:
+            self.noise_offset += 1
+        return OF.user_step(v, inv, perm, ptr, self.model.user_encoder, B, C, H, self.score_act,
+                            (p, self.user_drop_seed, 0), self._rng_step, ldp, padded)
+
+    def _dedup(self, cand, his, pre):
+        if pre is not None and pre.dedup is not None:
+            if pre.ready is not None:
+                torch.cuda.current_stream(self.device).wait_event(pre.ready)
+            return pre.dedup
+        return tuple(ops.dedup(torch.cat([cand.reshape(-1), his.reshape(-1)]), self.N))
+
     def forward_backward(self, cand: torch.Tensor, his: torch.Tensor, pre: Optional[Prepared] = None) -> torch.Tensor:
         """Loss of one batch with every trainable gradient left in ``flat.grad``."""
         self.model.train()
@@ -299,6 +326,18 @@ class LocalEngine:
         self.flat.begin_backward()
         if self.reducer is not None:
             self.reducer.begin()
+        if self.fused_user:
+            dd = self._dedup(cand, his, pre)
+            with obs.range("news_encode"):
+                v = self.news_vectors(dd[0], grad=True)
+            with obs.range("user_step"):
+                loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
+                                          pre is not None and pre.padded, True)
+            with obs.range("backward"):
+                loss.backward()
+            self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
+            self.flat.end_backward()
+            return loss.detach()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True, pre=pre)
         with obs.range("user_fwd"):
             u = self.model.user_encoder(his_v, his)
@@ -416,6 +455,15 @@ class LocalEngine:
         if self.q.grad_double_last_batch:
             self.flat.grad.zero_()  # Q2: optimizer.zero_grad() each batch (client.py:75)
         self.model.text_encoder.eval()  # gen_news_vecs runs the text encoder in eval (model.py:42)
+        if self.fused_user:
+            dd = self._dedup(cand, his, pre)
+            v = self.news_vectors(dd[0], grad=False).detach().requires_grad_(True)
+            loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1], False, True)
+            loss.backward()
+            self._rng_step.add_(1)
+            self.G.index_add_(0, dd[0].long(), v.grad)
+            self.touched[dd[0].long()] = True
+            return loss.detach()
         uniq, v, cand_v, his_v = self._forward_rows(cand, his, grad_news=False, pre=pre)
         u = self.model.user_encoder(his_v, his)
         loss, _ = OF.score_ce(cand_v, u, self.score_act)
@@ -538,6 +586,16 @@ class LocalEngine:
             cand, his = self.to_device(cand_np), self.to_device(his_np)
             B, C = cand.shape
             ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
+            if self.fused_user:  # the fused device user side, forward only (eval: no dropout)
+                if table is not None:
+                    v, inv = table, ids.to(torch.int32)
+                else:
+                    uniq, inv, _, _ = ops.dedup(ids, self.N)
+                    v = self.news_vectors(uniq, grad=False)
+                loss, s = self._user_loss(v, (None, inv, inv, inv), B, C, his.shape[1], False, False)
+                losses.append(float(loss) * B)
+                scores_all.append(s.float().cpu().numpy())
+                continue
             if table is not None:
                 rows = table.index_select(0, ids.long())
             else:
