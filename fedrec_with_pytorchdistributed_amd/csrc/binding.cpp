@@ -81,6 +81,8 @@ int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int 
 int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, hipStream_t s);
+int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
+                  hipStream_t s);
 long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part, hipStream_t s);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
@@ -398,14 +400,25 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Te
   const c10::DeviceGuard g(cand.device());
   const int64_t B = cand.size(0), C = cand.size(1), D = cand.size(2);
   TORCH_CHECK(user.size(0) == B && user.size(1) == D, "fedrec::score_ce: user shape");
-  auto loss = at::empty({}, cand.options());
+  // per-impression losses, then the deterministic colsum (no float atomics: bit-reproducible loss)
+  auto lossb = at::empty({std::max<int64_t>(B, 1) + 1}, cand.options());
+  auto loss = lossb.narrow(0, B > 0 ? B : 0, 1).squeeze(0);  // 0-d view (view({}) would pick view(ScalarType))
   auto scores = at::empty({B, C}, cand.options());
   auto dcand = at::empty_like(cand);
   auto duser = at::empty_like(user);
-  check_rc(fr_score_ce(cand.data_ptr<float>(), user.data_ptr<float>(), loss.data_ptr<float>(), scores.data_ptr<float>(),
+  check_rc(fr_score_ce(cand.data_ptr<float>(), user.data_ptr<float>(), lossb.data_ptr<float>(), scores.data_ptr<float>(),
                        dcand.data_ptr<float>(), duser.data_ptr<float>(), (int)B, (int)C, (int)D, (int)act,
                        cur_stream()),
            "score_ce");
+  {
+    const float* xs[1] = {lossb.data_ptr<float>()};
+    float* os[1] = {loss.data_ptr<float>()};
+    const int ints[4] = {(int)B, 1, 1, 0};
+    const long need = fr_colsum_f32(xs, os, ints, 1, nullptr, cur_stream());
+    auto part = at::empty({std::max<long>(need, 1)}, cand.options());
+    TORCH_CHECK(need >= 0 && fr_colsum_f32(xs, os, ints, 1, part.data_ptr<float>(), cur_stream()) == 0,
+                "fedrec::score_ce: loss sum");
+  }
   return {loss, scores, dcand, duser};
 }
 
@@ -551,7 +564,8 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
 }
 
 // ---- small fp32 GEMMs on MFMA (small_gemm.hip): up to 6 independent GEMMs per launch -------
-// ints: 13 per GEMM (M, N, K, lda, ldb, ldc, a_mode, b_mode, act, accumulate, drop_ld, drop_on, gather_on);
+// ints: 14 per GEMM (M, N, K, lda, ldb, ldc, a_mode, b_mode, act, accumulate, drop_ld, drop_on, gather_on, kseg);
+// Bseg: per GEMM 0 or 2 extra [kseg, N] row blocks of a K-segmented B (kseg > 0)
 // floats: (alpha, pdrop) per GEMM; seeds: (seed, offset) per GEMM.  C tensors are written.
 // elements addressable from t.data_ptr() to the end of its storage (strided operand views)
 int64_t avail(const at::Tensor& t) {
@@ -561,18 +575,19 @@ int64_t avail(const at::Tensor& t) {
 void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<at::Tensor>>& gidx,
                 const std::vector<at::Tensor>& B, const c10::List<c10::optional<at::Tensor>>& bias,
                 const std::vector<at::Tensor>& C, at::IntArrayRef ints, at::ArrayRef<double> floats,
-                at::IntArrayRef seeds, const c10::optional<at::Tensor>& dev_off) {
+                at::IntArrayRef seeds, const c10::optional<at::Tensor>& dev_off, const std::vector<at::Tensor>& Bseg) {
   const size_t n = A.size();
   TORCH_CHECK(n >= 1 && n <= 6 && B.size() == n && C.size() == n && gidx.size() == n && bias.size() == n &&
-                  ints.size() == 13 * n && floats.size() == 2 * n && seeds.size() == 2 * n,
+                  ints.size() == 14 * n && floats.size() == 2 * n && seeds.size() == 2 * n,
               "fedrec::small_gemm: descriptor sizes");
   const c10::DeviceGuard g(A[0].device());
-  std::vector<const void*> ptrs(5 * n);
-  std::vector<int> iv(13 * n);
+  std::vector<const void*> ptrs(7 * n);
+  std::vector<int> iv(14 * n);
+  size_t seg_used = 0;
   std::vector<float> fv(2 * n);
   std::vector<unsigned long long> sv(2 * n);
   for (size_t i = 0; i < n; ++i) {
-    const int64_t* q = ints.data() + 13 * i;
+    const int64_t* q = ints.data() + 14 * i;
     const int64_t M = q[0], N = q[1], K = q[2], lda = q[3], ldb = q[4], ldc = q[5], am = q[6], bm = q[7];
     for (const at::Tensor* t : {&A[i], &B[i], &C[i]}) {  // row-major views with any leading dimension
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && (t->dim() == 0 || t->stride(-1) == 1),
@@ -586,27 +601,41 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
     if (!(gathered && gather_on == 1))
       TORCH_CHECK(avail(A[i]) >= (am == 0 ? (M - 1) * lda + K : (K - 1) * lda + M) || M == 0 || K == 0,
                   "fedrec::small_gemm: A too small");
+    const int64_t kseg = q[13];
+    const int64_t b_rows = kseg > 0 ? std::min<int64_t>(K, kseg) : K;
     if (!(gathered && gather_on == 2))
-      TORCH_CHECK(avail(B[i]) >= (bm == 0 ? (N - 1) * ldb + K : (K - 1) * ldb + N) || N == 0 || K == 0,
+      TORCH_CHECK(avail(B[i]) >= (bm == 0 ? (N - 1) * ldb + K : (b_rows - 1) * ldb + N) || N == 0 || K == 0,
                   "fedrec::small_gemm: B too small");
     TORCH_CHECK(gathered == (gather_on != 0), "fedrec::small_gemm: gidx given iff gather_on");
     TORCH_CHECK(avail(C[i]) >= (M - 1) * ldc + N || M == 0 || N == 0, "fedrec::small_gemm: C too small");
-    ptrs[5 * i + 0] = A[i].data_ptr();
-    ptrs[5 * i + 1] = nullptr;
+    ptrs[7 * i + 0] = A[i].data_ptr();
+    ptrs[7 * i + 1] = nullptr;
+    ptrs[7 * i + 5] = ptrs[7 * i + 6] = nullptr;
+    if (kseg > 0) {  // the extra row blocks of a K-segmented B come from Bseg in order
+      TORCH_CHECK(bm == 1 && seg_used + 2 <= Bseg.size(), "fedrec::small_gemm: K-segmented B needs b_mode 1 + 2 Bseg");
+      for (int j = 0; j < 2; ++j) {
+        const at::Tensor& t = Bseg[seg_used + j];
+        TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.stride(-1) == 1 &&
+                        avail(t) >= (kseg - 1) * ldb + N,
+                    "fedrec::small_gemm: Bseg block");
+        ptrs[7 * i + 5 + j] = t.data_ptr();
+      }
+      seg_used += 2;
+    }
     if (gathered) {
       TORCH_CHECK(gv->is_cuda() && gv->scalar_type() == at::kInt && gv->numel() >= (gather_on == 1 ? M : K),
                   "fedrec::small_gemm: gidx int32[M] (A rows) or int32[K] (B rows)");
-      ptrs[5 * i + 1] = gv->data_ptr();
+      ptrs[7 * i + 1] = gv->data_ptr();
     }
-    ptrs[5 * i + 2] = B[i].data_ptr();
+    ptrs[7 * i + 2] = B[i].data_ptr();
     const auto bv = bias.get(i);
-    ptrs[5 * i + 3] = nullptr;
+    ptrs[7 * i + 3] = nullptr;
     if (bv.has_value() && bv->defined()) {
       TORCH_CHECK(bv->is_cuda() && bv->scalar_type() == at::kFloat && bv->numel() >= N, "fedrec::small_gemm: bias");
-      ptrs[5 * i + 3] = bv->data_ptr();
+      ptrs[7 * i + 3] = bv->data_ptr();
     }
-    ptrs[5 * i + 4] = C[i].data_ptr();
-    for (int j = 0; j < 13; ++j) iv[13 * i + j] = (int)q[j];
+    ptrs[7 * i + 4] = C[i].data_ptr();
+    for (int j = 0; j < 14; ++j) iv[14 * i + j] = (int)q[j];
     fv[2 * i] = (float)floats[2 * i];
     fv[2 * i + 1] = (float)floats[2 * i + 1];
     sv[2 * i] = (unsigned long long)seeds[2 * i];
@@ -654,6 +683,29 @@ void colsum_f32(const std::vector<at::Tensor>& X, const std::vector<at::Tensor>&
   auto part = at::empty({std::max<long>(need, 1)}, X[0].options());
   TORCH_CHECK(fr_colsum_f32(xs.data(), os.data(), iv.data(), (int)n, part.data_ptr<float>(), cur_stream()) == 0,
               "fedrec::colsum_f32: launch failed");
+}
+
+// several small copies (+ fills of the tails) in one launch, in 4-byte words
+void multi_copy(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst, at::IntArrayRef fill) {
+  const size_t n = src.size();
+  TORCH_CHECK(n >= 1 && n <= 8 && dst.size() == n && fill.size() == n, "fedrec::multi_copy: sizes");
+  const c10::DeviceGuard g(dst[0].device());
+  std::vector<const int*> sp(n);
+  std::vector<int*> dp(n);
+  std::vector<long> ns(n), nd(n);
+  std::vector<int> fv(n);
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && dst[i].is_contiguous() &&
+                    src[i].element_size() % 4 == 0 && dst[i].element_size() == src[i].element_size(),
+                "fedrec::multi_copy: contiguous device tensors of one 4/8-byte dtype");
+    sp[i] = (const int*)src[i].data_ptr();
+    dp[i] = (int*)dst[i].data_ptr();
+    ns[i] = (long)(src[i].numel() * src[i].element_size() / 4);
+    nd[i] = (long)(dst[i].numel() * dst[i].element_size() / 4);
+    TORCH_CHECK(ns[i] <= nd[i], "fedrec::multi_copy: source larger than destination");
+    fv[i] = (int)fill[i];
+  }
+  check_rc(fr_multi_copy(sp.data(), dp.data(), ns.data(), nd.data(), fv.data(), (int)n, cur_stream()), "multi_copy");
 }
 
 // device-scale secure aggregation (bucketed GA): the fixed-point exponent is derived on the device
@@ -951,7 +1003,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
-  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off=None) -> ()");
+  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg) -> ()");
+  m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");
   m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");
@@ -994,6 +1047,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("secagg_mask_dev", &secagg_mask_dev);
   m.impl("small_gemm", &small_gemm);
   m.impl("colsum_f32", &colsum_f32);
+  m.impl("multi_copy", &multi_copy);
   m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void score_ce_kernel(const float* __restrict__
   for (int c = 0; c < C; ++c) se += __expf(s[c] - mx);
   const float lse = mx + __logf(se);
   if (lane == 0) {
-    atomicAdd(loss, (lse - s[0]) / (float)B);
+    loss[b] = (lse - s[0]) / (float)B;  // per-impression share; the caller sums in a fixed order
     for (int c = 0; c < C; ++c) scores[(size_t)b * C + c] = s[c];
   }
   float dz[MAXC];
@@ -61,7 +61,6 @@ __global__ __launch_bounds__(256) void score_ce_kernel(const float* __restrict__
 extern "C" int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand,
                            float* duser, int B, int C, int D, int sigm, hipStream_t s) {
   if (C > MAXC) return 1;
-  hipMemsetAsync(loss, 0, sizeof(float), s);
   if (B == 0) return 0;
   hipLaunchKernelGGL(score_ce_kernel, dim3((B + 3) / 4), dim3(256), 0, s, cand, user, loss, scores, dcand, duser, B,
                      C, D, sigm);

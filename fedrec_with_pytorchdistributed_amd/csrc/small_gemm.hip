@@ -33,13 +33,15 @@ struct GemmDesc {
   const float* A;
   const int* gidx;  // row gather of A (gather_on 1, a_mode 0) or of B (gather_on 2, b_mode 1)
   const float* B;
+  const float* B2;  // K-segmented B (b_mode 1): rows [kseg, 2 kseg) from B2, [2 kseg, 3 kseg) from B3
+  const float* B3;
   const float* bias;
   float* C;
   float* P;  // split-K partials [splits, M, N] (splits > 1: the reduce kernel does the epilogue)
   int M, N, K, lda, ldb, ldc;
   int a_mode, b_mode, act, accumulate;
   float alpha, pdrop;
-  int drop_ld, drop_on, gather_on, tiles_n, tile_base, splits, kchunk;
+  int drop_ld, drop_on, gather_on, tiles_n, tile_base, splits, kchunk, kseg;
   unsigned long long seed, offset;  // offset += *dev_off when dev_off is set (graph replays)
 };
 
@@ -103,7 +105,12 @@ __device__ __forceinline__ void load_tile(const GemmDesc& g, unsigned long long 
     const bool kok = kg < kend;
     // B in mode 1 may be the gathered + dropped-out input of the forward (the weight
     // gradient dW = dY^T X' regenerates X' = drop(X[gidx]) instead of storing it)
-    const size_t src = kok ? (size_t)((!isA && g.gather_on == 2) ? g.gidx[kg] : kg) : 0;
+    size_t src = kok ? (size_t)((!isA && g.gather_on == 2) ? g.gidx[kg] : kg) : 0;
+    if (!isA && g.kseg > 0 && kok) {  // one [K, N] operand stored as up to three row blocks
+      const int seg = kg / g.kseg;
+      P = seg == 0 ? g.B : (seg == 1 ? g.B2 : g.B3);
+      src = kg - seg * g.kseg;
+    }
     const float* p = P + src * ld + r0 + rr16;
     const int valid = kok ? min(16, R - (r0 + rr16)) : 0;
     load16(p, valid == 16, ((uintptr_t)p & 15) == 0, valid, v);
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(64) void colsum_final_kernel(const ColsumBatch batc
 
 }  // namespace
 
-// descs: 5 pointers + 13 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
+// descs: 7 pointers + 14 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
 // scratch: split-K partial space (floats) the caller allocated; returns the floats it needs
 // when scratch is null (query mode).
 static int choose_splits(int M, int N, int K) {
@@ -282,15 +289,19 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   int red_total = 0;
   for (int i = 0; i < n; ++i) {
     GemmDesc& d = b.d[i];
-    d.A = (const float*)ptrs[5 * i + 0];
-    d.gidx = (const int*)ptrs[5 * i + 1];
-    d.B = (const float*)ptrs[5 * i + 2];
-    d.bias = (const float*)ptrs[5 * i + 3];
-    d.C = (float*)ptrs[5 * i + 4];
-    const int* q = ints + 13 * i;
+    d.A = (const float*)ptrs[7 * i + 0];
+    d.gidx = (const int*)ptrs[7 * i + 1];
+    d.B = (const float*)ptrs[7 * i + 2];
+    d.bias = (const float*)ptrs[7 * i + 3];
+    d.C = (float*)ptrs[7 * i + 4];
+    d.B2 = (const float*)ptrs[7 * i + 5];
+    d.B3 = (const float*)ptrs[7 * i + 6];
+    const int* q = ints + 14 * i;
     d.M = q[0]; d.N = q[1]; d.K = q[2]; d.lda = q[3]; d.ldb = q[4]; d.ldc = q[5];
     d.a_mode = q[6]; d.b_mode = q[7]; d.act = q[8]; d.accumulate = q[9]; d.drop_ld = q[10];
-    d.drop_on = q[11]; d.gather_on = q[12];
+    d.drop_on = q[11]; d.gather_on = q[12]; d.kseg = q[13];
+    if (d.kseg > 0 && (d.b_mode != 1 || d.gather_on == 2 || !d.B2 || (d.K > 2 * d.kseg && !d.B3) || d.K > 3 * d.kseg))
+      return -5;
     d.alpha = floats[2 * i];
     d.pdrop = floats[2 * i + 1];
     d.seed = seeds[2 * i];

@@ -259,16 +259,19 @@ class Gemm:
     col`` in the logical (gathered) matrix -- the mask of ``ops.dropout_add``."""
 
     __slots__ = ("A", "B", "C", "M", "N", "K", "lda", "ldb", "ldc", "a_mode", "b_mode", "act", "accumulate",
-                 "alpha", "bias", "gidx", "gather_on", "pdrop", "drop_on", "drop_ld", "seed", "offset")
+                 "alpha", "bias", "gidx", "gather_on", "pdrop", "drop_on", "drop_ld", "seed", "offset", "bseg", "kseg")
 
     def __init__(self, A, B, C, M, N, K, lda, ldb, ldc, a_mode=0, b_mode=0, act=0, accumulate=False, alpha=1.0,
-                 bias=None, gidx=None, gather_on=0, pdrop=0.0, drop_on=0, drop_ld=0, seed=0, offset=0):
+                 bias=None, gidx=None, gather_on=0, pdrop=0.0, drop_on=0, drop_ld=0, seed=0, offset=0,
+                 bseg=(), kseg=0):
         self.A, self.B, self.C = A, B, C
         self.M, self.N, self.K, self.lda, self.ldb, self.ldc = int(M), int(N), int(K), int(lda), int(ldb), int(ldc)
         self.a_mode, self.b_mode, self.act, self.accumulate = int(a_mode), int(b_mode), int(act), bool(accumulate)
         self.alpha, self.bias, self.gidx, self.gather_on = float(alpha), bias, gidx, int(gather_on)
         self.pdrop, self.drop_on, self.drop_ld = float(pdrop), int(drop_on), int(drop_ld)
         self.seed, self.offset = int(seed), int(offset)
+        # K-segmented B (b_mode 1): rows [0, kseg) of B, [kseg, 2 kseg) of bseg[0], then bseg[1]
+        self.bseg, self.kseg = tuple(bseg), int(kseg)
 
 
 def small_gemm(*gs: Gemm, dev_off=None) -> None:
@@ -277,11 +280,12 @@ def small_gemm(*gs: Gemm, dev_off=None) -> None:
     ints, floats, seeds = [], [], []
     for g in gs:
         ints += [g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.a_mode, g.b_mode, g.act, int(g.accumulate), g.drop_ld,
-                 g.drop_on, g.gather_on]
+                 g.drop_on, g.gather_on, g.kseg]
         floats += [g.alpha, g.pdrop]
         seeds += [g.seed, g.offset]
     native.require_for(gs[0].A).small_gemm([g.A for g in gs], [g.gidx for g in gs], [g.B for g in gs],
-                                           [g.bias for g in gs], [g.C for g in gs], ints, floats, seeds, dev_off)
+                                           [g.bias for g in gs], [g.C for g in gs], ints, floats, seeds, dev_off,
+                                           [t for g in gs for t in g.bseg])
 
 
 def small_gemm_ref(g: Gemm) -> torch.Tensor:
@@ -304,6 +308,9 @@ def small_gemm_ref(g: Gemm) -> torch.Tensor:
         A = drop(A)
     if g.b_mode == 0:
         Bm = rows(g.B, g.N, g.K, g.ldb)  # [N, K]
+    elif g.kseg:
+        Bm = torch.cat([rows(t, min(g.kseg, g.K - i * g.kseg), g.N, g.ldb)
+                        for i, t in enumerate((g.B, *g.bseg)) if i * g.kseg < g.K]).t()
     else:
         Bk = rows(g.B, g.K, g.N, g.ldb, g.gidx if g.gather_on == 2 else None)  # [K, N]
         if g.drop_on == 2:

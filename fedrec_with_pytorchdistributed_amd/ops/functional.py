@@ -498,12 +498,11 @@ class UserStepFn(torch.autograd.Function):
         p, seed, off = drop
         his_idx = inv[BC:]
         dx = rows[BC:]
-        # dx = (dQ Wq + dK Wk + dV Wv) o Z: three accumulating passes, the dropout backward in
-        # each epilogue (linear, so drop(a + b + c) = drop(a) + drop(b) + drop(c))
+        # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the three weight blocks
+        # (K-segmented B), the dropout backward in its epilogue
         ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
-        for s, w in enumerate((wq, wk, wv)):
-            ops.small_gemm(ops.Gemm(dqkv[:, s * D:(s + 1) * D], w, dx, BH, D, D, 3 * D, D, D, b_mode=1,
-                                    accumulate=s > 0, **ekw), dev_off=dev_off)
+        ops.small_gemm(ops.Gemm(dqkv, wq, dx, BH, D, 3 * D, 3 * D, D, D, b_mode=1, bseg=(wk, wv), kseg=D, **ekw),
+                       dev_off=dev_off)
         # weight gradients in one launch: dW_s = dS^T X' (X' = the gathered, dropped-out input,
         # regenerated in the B loads) and dW1 = dpre^T ctx
         gq, gk, gv = (torch.empty(D, D, device=dev) for _ in range(3))

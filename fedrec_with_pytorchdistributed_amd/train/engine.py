@@ -43,6 +43,7 @@ from ..data.shard import Shard
 from ..eval.metrics import batch_metrics
 from ..models.fedrec_model import FedRecModel
 from ..ops import functional as OF
+from ..ops import native
 from ..utils import obs
 from .news_cache import HiddenCache
 
@@ -88,15 +89,13 @@ class _StepGraph:
             self.loss = eng.forward_backward(self.cand, self.his, static)
 
     def load(self, pre: Prepared, U: int) -> None:
+        """The batch into the static inputs: one multi-copy launch; the unique list is padded
+        with news 0 and the segment pointers with R (padded segments are empty)."""
         uniq, inv, perm, ptr = pre.dedup
-        self.cand.copy_(pre.cand)
-        self.his.copy_(pre.his)
-        self.uniq[:U].copy_(uniq)
-        self.uniq[U:].zero_()
-        self.inv.copy_(inv)
-        self.perm.copy_(perm)
-        self.ptr[:U + 1].copy_(ptr)
-        self.ptr[U + 1:].fill_(inv.numel())  # padded segments are empty
+        native.require_for(self.cand).multi_copy(
+            [pre.cand.contiguous(), pre.his.contiguous(), uniq, inv, perm, ptr],
+            [self.cand, self.his, self.uniq, self.inv, self.perm, self.ptr],
+            [0, 0, 0, 0, 0, int(inv.numel())])
 
 
 class LocalEngine:

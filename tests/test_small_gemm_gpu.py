@@ -78,3 +78,13 @@ def test_colsum_f32_deterministic(dev):
     o3 = torch.zeros(400, device=dev)
     ops.colsum_f32([(X[:, 400:], o3, 3200, 400, 1200)])
     assert torch.equal(o1, o3)
+
+
+def test_k_segmented_b_with_dropout_epilogue(dev):
+    """dx = [dQ|dK|dV] [Wq; Wk; Wv]: one GEMM over three separately stored weight blocks."""
+    torch.manual_seed(5)
+    dq = torch.randn(3200, 1200, device=dev)
+    ws = [torch.randn(400, 400, device=dev) * 0.05 for _ in range(3)]
+    C = torch.zeros(3200, 400, device=dev)
+    _check(Gemm(dq, ws[0], C, 3200, 400, 1200, 1200, 400, 400, b_mode=1, bseg=(ws[1], ws[2]), kseg=400,
+                pdrop=0.2, drop_on=3, drop_ld=400, seed=2, offset=3))

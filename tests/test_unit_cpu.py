@@ -573,3 +573,18 @@ def test_backbone_preset_then_field_overrides_any_order():
     c = FedRecConfig()
     c.apply_overrides(["--backbone.name=bert-base", "--backbone.dropout=0"])
     assert c.backbone.n_layers == 12 and c.backbone.dropout == 0.0 and not c.backbone.frozen
+
+
+def test_extension_loads_and_registers_ops():
+    """The built _C.so registers every op schema (a bad schema aborts the process at load
+    time, so this runs in a subprocess); skipped when the extension was not built here."""
+    import subprocess
+    import sys
+    from fedrec_with_pytorchdistributed_amd.ops import native
+    if not native.SO_PATH.exists():
+        pytest.skip("extension not built")
+    code = ("import torch; torch.ops.load_library(%r); f = torch.ops.fedrec; "
+            "[getattr(f, n) for n in ('small_gemm', 'colsum_f32', 'multi_copy', 'dropout_add', "
+            "'title_attention_drop', 'secagg_mask_dev', 'segment_sum_rows', 'linear')]" % str(native.SO_PATH))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
