@@ -75,14 +75,15 @@ __device__ __forceinline__ void apply_drop16(float (&v)[16], unsigned long long 
   }
 }
 
-// one 64 x 64 operand tile (rows r0.., k0..) -> bf16 LDS [row][k]
-__device__ __forceinline__ void load_tile(const GemmDesc& g, unsigned long long off, bool isA, int r0, int k0,
-                                          int kend, bf16 (*S)[LDT], int tid) {
+// one 64 x 64 operand tile (rows r0.., k0..): global -> 16 registers per thread (converted
+// and dropout-scaled), then registers -> bf16 LDS [row][k] in a separate step, so the next
+// tile's loads are in flight while the MFMAs consume the current one
+__device__ __forceinline__ void load_regs(const GemmDesc& g, unsigned long long off, bool isA, int r0, int k0,
+                                          int kend, int tid, float (&v)[16]) {
   const int mode = isA ? g.a_mode : g.b_mode;
   const float* P = isA ? g.A : g.B;
   const int ld = isA ? g.lda : g.ldb;
   const int R = isA ? g.M : g.N;
-  float v[16];
   if (mode == 0) {  // [R, K] row-major: thread -> (row, 16 consecutive k)
     const int r = tid >> 2, kk = (tid & 3) * 16;
     const int rr = r0 + r, k = k0 + kk;
@@ -92,13 +93,6 @@ __device__ __forceinline__ void load_tile(const GemmDesc& g, unsigned long long 
     const int valid = rok ? min(16, kend - k) : 0;
     load16(p, valid == 16, ((uintptr_t)p & 15) == 0, valid, v);
     if (isA && g.drop_on == 1 && rok) apply_drop16(v, (unsigned long long)rr * g.drop_ld + k, g, off);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[8 * h + j]);
-      *(bf16x8*)&S[r][kk + 8 * h] = o;
-    }
   } else {  // stored [K, R]: thread -> (k, 16 consecutive rows), coalesced along the rows
     const int k = tid >> 2, rr16 = (tid & 3) * 16;
     const int kg = k0 + k;
@@ -115,6 +109,22 @@ __device__ __forceinline__ void load_tile(const GemmDesc& g, unsigned long long 
     const int valid = kok ? min(16, R - (r0 + rr16)) : 0;
     load16(p, valid == 16, ((uintptr_t)p & 15) == 0, valid, v);
     if (!isA && g.drop_on == 2 && kok) apply_drop16(v, (unsigned long long)kg * g.drop_ld + r0 + rr16, g, off);
+  }
+}
+
+__device__ __forceinline__ void store_regs(const GemmDesc& g, bool isA, int tid, const float (&v)[16],
+                                           bf16 (*S)[LDT]) {
+  if ((isA ? g.a_mode : g.b_mode) == 0) {
+    const int r = tid >> 2, kk = (tid & 3) * 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[8 * h + j]);
+      *(bf16x8*)&S[r][kk + 8 * h] = o;
+    }
+  } else {
+    const int k = tid >> 2, rr16 = (tid & 3) * 16;
 #pragma unroll
     for (int j = 0; j < 16; ++j) S[rr16 + j][k] = f2bf(v[j]);
   }
@@ -142,11 +152,20 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float va[16], vb[16];
+  if (kbeg < kend) {
+    load_regs(g, off, true, m0, kbeg, kend, tid, va);
+    load_regs(g, off, false, n0, kbeg, kend, tid, vb);
+  }
   for (int k0 = kbeg; k0 < kend; k0 += TK) {
+    __syncthreads();  // the previous tile's fragments are consumed
+    store_regs(g, true, tid, va, As);
+    store_regs(g, false, tid, vb, Bs);
     __syncthreads();
-    load_tile(g, off, true, m0, k0, kend, As, tid);
-    load_tile(g, off, false, n0, k0, kend, Bs, tid);
-    __syncthreads();
+    if (k0 + TK < kend) {  // next tile's global loads overlap this tile's MFMAs
+      load_regs(g, off, true, m0, k0 + TK, kend, tid, va);
+      load_regs(g, off, false, n0, k0 + TK, kend, tid, vb);
+    }
 #pragma unroll
     for (int ks = 0; ks < TK; ks += 32) {
       bf16x8 a[2], b[2];
