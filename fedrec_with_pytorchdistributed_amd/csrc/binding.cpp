@@ -91,6 +91,8 @@ int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, in
 int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles,
                                      int T, int H, int D, float pdrop, unsigned long long seed,
                                      unsigned long long offset, hipStream_t s);
+long fr_wgrad_bf16(const void* dY, const void* X, float* C, float* scratch, int M, int N, int K, int accumulate,
+                   hipStream_t s);
 }
 
 namespace {
@@ -960,6 +962,30 @@ at::Tensor embed_grad(const at::Tensor& dx, const at::Tensor& sorted, const at::
   return dword;
 }
 
+// dW[N, K] = dy[M, N]^T x[M, K] in fp32 (gemm_wgrad.hip)
+at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x) {
+  check_dev(dy, "dy");
+  check_dev(x, "x");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "fedrec::wgrad: bf16 dy/x");
+  const c10::DeviceGuard g(dy.device());
+  const int64_t N = dy.size(-1), K = x.size(-1), M = dy.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(x.numel() == M * K, "fedrec::wgrad: row count mismatch");
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "fedrec::wgrad: N, K must be multiples of 8");
+  TORCH_CHECK(M < (1ll << 31), "fedrec::wgrad: too many rows");
+  auto C = at::empty({N, K}, dy.options().dtype(at::kFloat));
+  if (M == 0) return C.zero_();
+  const long need = fr_wgrad_bf16(dy.data_ptr(), x.data_ptr(), C.data_ptr<float>(), nullptr, (int)M, (int)N, (int)K, 0,
+                                  cur_stream());
+  TORCH_CHECK(need >= 0, "fedrec::wgrad: unsupported shape");
+  if (need > 0) {
+    auto scratch = at::empty({need}, C.options());
+    TORCH_CHECK(fr_wgrad_bf16(dy.data_ptr(), x.data_ptr(), C.data_ptr<float>(), scratch.data_ptr<float>(), (int)M,
+                              (int)N, (int)K, 0, cur_stream()) == 0,
+                "fedrec::wgrad: launch");
+  }
+  return C;
+}
+
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
@@ -1011,6 +1037,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("dropout_add(Tensor h, Tensor? res, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
+  m.def("wgrad(Tensor dy, Tensor x) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
@@ -1051,4 +1078,5 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);
+  m.impl("wgrad", &wgrad);
 }

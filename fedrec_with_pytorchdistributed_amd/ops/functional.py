@@ -1,8 +1,9 @@
 """Autograd wiring of the fused ops.
 
 Each ``Function`` has a hand-written forward *and* backward kernel pair (device) or the
-oracle pair (host); torch autograd only strings them together.  The small user-side
-projections (``[B*H, 400] x [400, 1200]``) and the head FC stay plain library GEMMs.
+oracle pair (host); torch autograd only strings them together.  Every GEMM of the training
+step runs on our MFMA kernels: forward / dX on the NT kernel (``gemm_bf16.hip``), dW on the TN
+kernel (``gemm_wgrad.hip``), the fp32 user side on the small-GEMM kernel (``small_gemm.hip``).
 """
 from __future__ import annotations
 
@@ -16,21 +17,23 @@ from .. import ops
 from .reference import _f
 
 
-_WGRAD_TILES = int(__import__("os").environ.get("FEDREC_WGRAD_TILES", "512"))  # split-K target (A/B runs)
+_WGRAD_TILES = int(__import__("os").environ.get("FEDREC_WGRAD_TILES", "512"))  # split-K target (lib A/B)
+_WGRAD_IMPL = __import__("os").environ.get("FEDREC_WGRAD", "ours")  # ours | lib (A/B runs)
 
 
 def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
     """``dy^T x`` in fp32 for ``dy [M, N]``, ``x [M, K]`` with a long reduction dim M.
 
-    On the device with bf16 operands this is a split-K batched MFMA GEMM: M is cut into
-    ``splits`` row chunks (free views, no copies), one fp32-output GEMM per chunk in a
-    single bmm launch, then an fp32 sum of the partials.  The library picks a handful of
-    output tiles for the un-split product ([384, 768] from 78850 rows: 18 tiles, 155 TF)."""
+    On the device with bf16 operands: our TN MFMA kernel (``csrc/gemm_wgrad.hip``: M-major
+    tiles staged as they sit in HBM, fragments by LDS transpose reads, split-K over M with a
+    fixed-order partial sum).  ``FEDREC_WGRAD=lib`` keeps the round-1 library form for A/B
+    runs: a split-K batched library GEMM over free row-chunk views, then an fp32 sum."""
     if not (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
         return _f(dy).t() @ _f(x)
+    if _WGRAD_IMPL != "lib":
+        return ops.native.require_for(dy).wgrad(dy.reshape(-1, dy.shape[-1]).contiguous(),
+                                                x.reshape(-1, x.shape[-1]).contiguous())
     M = dy.shape[0]
-    # enough split-K chunks for ~2 output tiles per CU (the library tiles 256x256), no more:
-    # every chunk adds an [N, K] fp32 partial that the final sum reads back
     tiles = -(-dy.shape[1] // 256) * -(-x.shape[1] // 256)
     splits = min(splits, max(1, -(-_WGRAD_TILES // tiles)))
     S = max(1, min(splits, M // 2048))
@@ -42,6 +45,24 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
     if M0 < M:
         out += torch.mm(dy[M0:].t(), x[M0:], out_dtype=torch.float32)
     return out
+
+
+_DGRAD_IMPL = __import__("os").environ.get("FEDREC_DGRAD", "ours")  # ours | lib (A/B runs)
+
+
+def dgrad(dy: torch.Tensor, wlow: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``dy @ wlow (+ residual)``: the input gradient of ``y = x wlow^T``.
+
+    On the device our NT MFMA GEMM runs it on ``wlow^T`` (a 1-5 MB per-step transpose of the
+    bf16 weight; the GEMM streams ~100 MB of ``dy``), with the residual gradient added in the
+    epilogue (beta = 1) -- no library GEMM in the training step.  ``FEDREC_DGRAD=lib`` keeps
+    the library ``mm`` / ``addmm_`` for A/B runs."""
+    if (dy.is_cuda and dy.dtype == torch.bfloat16 and _DGRAD_IMPL != "lib" and wlow.shape[1] % 128 == 0
+            and wlow.shape[0] % 64 == 0):
+        return ops.linear(dy, wlow.t().contiguous(), None, residual=residual)
+    if residual is not None:
+        return residual.addmm_(dy, wlow)
+    return torch.mm(dy, wlow)
 
 
 def bgrad(dy: torch.Tensor) -> torch.Tensor:
@@ -91,7 +112,7 @@ class AdditivePoolFn(torch.autograd.Function):
         dx = None
         if want_dx:
             if x2.is_cuda and x2.dtype == torch.bfloat16:
-                dxp = torch.mm(dpre2, w1.to(torch.bfloat16), out_dtype=torch.float32)
+                dxp = dgrad(dpre2.contiguous(), w1.to(torch.bfloat16))
             else:
                 dxp = _f(dpre2) @ _f(w1)
             dx = (_f(dx_dir) + dxp.reshape(n, T, D)).to(x.dtype)
@@ -207,7 +228,7 @@ def news_gather(table, inv, perm, seg_ptr, clip: float = 0.0, noise_std: float =
 # ---------------------------------------------------------------------------------------
 # training-mode backbone (unfrozen encoder, BASELINE config 5): forward on the fp32 master
 # parameters through their bf16 compute copies; backward kernels for attention / LayerNorm /
-# GELU, and library GEMMs (bf16 in, fp32 out) for dX / dW.
+# GELU, our NT GEMM for dX (``dgrad``) and our TN GEMM for dW (``wgrad``).
 # ---------------------------------------------------------------------------------------
 class LinearTFn(torch.autograd.Function):
     """``y = x @ wlow^T + b (+ residual)`` with ``wlow`` = bf16 copy of the fp32 ``w``."""
@@ -222,7 +243,7 @@ class LinearTFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, wlow = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = torch.mm(dy, wlow) if ctx.needs_input_grad[0] else None
+        dx = dgrad(dy, wlow) if ctx.needs_input_grad[0] else None
         dw = wgrad(dy, x)
         db = bgrad(dy)
         return dx, dw, db, (dy if ctx.has_res else None), None
@@ -243,7 +264,7 @@ class LinearGeluTFn(torch.autograd.Function):
     def backward(ctx, dh):
         x, wlow, z = ctx.saved_tensors
         dz = ops.native.require_for(z).gelu(z, dh.contiguous())
-        dx = torch.mm(dz, wlow) if ctx.needs_input_grad[0] else None
+        dx = dgrad(dz, wlow) if ctx.needs_input_grad[0] else None
         return dx, wgrad(dz, x), bgrad(dz), None
 
 
@@ -268,7 +289,7 @@ class DropoutFn(torch.autograd.Function):
 class AttnBlockFn(torch.autograd.Function):
     """``h = out_proj(attention(x Wqkv^T + bqkv)) + x`` (one post-LN block's attention half,
     unfrozen backbone).  One Function so the residual gradient joins the QKV input gradient
-    inside the dgrad GEMM (``dh.addmm_(dqkv, Wqkv)``: beta = 1 accumulate) instead of an
+    inside the dgrad GEMM (``dqkv Wqkv + dh`` in the GEMM epilogue: beta = 1) instead of an
     extra bf16 add pass over [M, 768] that autograd would insert for the two uses of ``x``.
     ``drop = (p, seed, offset)``: train-mode dropout of the attention probabilities (HF
     DistilBERT has no dropout after ``out_lin``)."""
@@ -290,7 +311,7 @@ class AttnBlockFn(torch.autograd.Function):
         dh = dh.contiguous()
         dbo = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN1's backward
         dwo, dbo = wgrad(dh, c), (dbo if dbo is not None else bgrad(dh))
-        dc = torch.mm(dh, wo_low)
+        dc = dgrad(dh, wo_low)
         dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
         dwqkv = wgrad(dqkv, x)
         if _QKV_BIAS_SHORTCUT and dqkv.is_cuda and ctx.drop is None:
@@ -304,7 +325,7 @@ class AttnBlockFn(torch.autograd.Function):
                                (dbo.float().unsqueeze(0) @ wo.float()).squeeze(0)])
         else:
             dbqkv = bgrad(dqkv)
-        dx = dh.addmm_(dqkv, wqkv_low)  # dh is ours (consumed above): residual + QKV dgrad
+        dx = dgrad(dqkv, wqkv_low, residual=dh)  # residual + QKV dgrad in one GEMM (beta = 1)
         return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None, None, None
 
 
@@ -313,7 +334,7 @@ class MLPBlockFn(torch.autograd.Function):
     ``drop = (p, seed, offset)`` = HF ``FFN.dropout`` in train mode, else identity).
     Backward: the GELU derivative rides in the epilogue of the GEMM that forms dF
     (``act = 3``: ``dz = (dh W2) * GELU'(z)``, z saved by the dual-store forward GEMM), and
-    the residual gradient joins the FFN1 dgrad via ``addmm_``."""
+    the residual gradient joins the FFN1 dgrad in its GEMM epilogue (beta = 1)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low, box=None, drop=None):
@@ -349,9 +370,9 @@ class MLPBlockFn(torch.autograd.Function):
         else:
             # library dF GEMM, then one streaming pass: dz = dF * GELU'(z) and its column sums
             # (the FFN1 bias gradient), deterministic partials
-            dz, db1 = lib.gelu_bwd_colsum(torch.mm(dh, w2_low), z)
+            dz, db1 = lib.gelu_bwd_colsum(dgrad(dh, w2_low), z)
         dw1 = wgrad(dz, x)
-        dx = dres.addmm_(dz, w1_low)
+        dx = dgrad(dz, w1_low, residual=dres)
         return dx, dw1, db1, dw2, db2, None, None, None, None
 
 
