@@ -6,7 +6,11 @@ the scores apart from slow learning --
 * user vectors (validation): mean |u|,
 * scores: mean |s|, and the share of impressions whose 5 scores are all equal (ties = a
   constant scorer: AUC exactly 0.5),
-* text-head FC weight / bias norms.
+* text-head FC weight / bias norms,
+* the eps-softmax cliff (``attention.py:20-22,40-42``: ``exp(s) / (sum exp(s) + 1e-8)``): per
+  user-MHSA query row and per user pooling, the max logit; below ln(1e-8) = -18.4 the 1e-8
+  term dominates and every weight shrinks as exp(max); below ~-87 they are exactly 0 in fp32
+  and so is the gradient through them (an absorbing state).
 
     python benchmarks/quality_diag.py --lr 1e-3 --score-act identity --epochs 4
 """
@@ -35,20 +39,37 @@ def diag(eng: LocalEngine, limit: int = 2048):
     V = eng.encode_all()
     m = eng.model
     m.eval()
-    us, ss = [], []
+    us, ss, mh_max, pool_max = [], [], [], []
+    ue = m.user_encoder
+    mha = ue.multihead_attention
     for cand_np, his_np in validation_batches(eng.shard.valid, 256, 4, 50, True, limit):
         cand, his = eng.to_device(cand_np), eng.to_device(his_np)
         B, C = cand.shape
         hv = V.index_select(0, his.reshape(-1).long()).view(B, his.shape[1], -1)
         cv = V.index_select(0, cand.reshape(-1).long()).view(B, C, -1)
         u = m.user_encoder(hv.float(), his)  # module path (the fused step returns no user vector)
+        x = hv.float()
+        q = torch.nn.functional.linear(x, mha.W_Q.weight, mha.W_Q.bias).view(B, -1, mha.n_heads, mha.d_k)
+        k = torch.nn.functional.linear(x, mha.W_K.weight, mha.W_K.bias).view(B, -1, mha.n_heads, mha.d_k)
+        sc = torch.einsum("bqhd,bkhd->bhqk", q, k) / mha.d_k ** 0.5
+        mh_max.append(sc.amax(-1).flatten().cpu())
+        y = mha(x)
+        ad = ue.additive_attention
+        a = torch.nn.functional.linear(torch.tanh(torch.nn.functional.linear(y, ad.att_fc1.weight, ad.att_fc1.bias)),
+                                       ad.att_fc2.weight, ad.att_fc2.bias).squeeze(-1)
+        pool_max.append(a.amax(-1).cpu())
         s = torch.bmm(cv, u.unsqueeze(-1)).squeeze(-1)
         us.append(u.norm(dim=-1).cpu())
         ss.append(s.cpu())
     S = torch.cat(ss)
     ties = float(((S.max(1).values - S.min(1).values).abs() < 1e-6).float().mean())
     fc = m.text_encoder.fc
-    return {"news_norm": float(V.norm(dim=1).mean()), "news_spread": float((V - V.mean(0)).norm(dim=1).mean()),
+    mh, pm = torch.cat(mh_max), torch.cat(pool_max)
+    cliff = float(np.log(1e-8))
+    return {"mhsa_rowmax_median": float(mh.median()), "mhsa_rows_below_cliff": float((mh < cliff).float().mean()),
+            "mhsa_rows_zero": float((mh < -87.0).float().mean()), "pool_max_median": float(pm.median()),
+            "pool_users_below_cliff": float((pm < cliff).float().mean()),
+            "news_norm": float(V.norm(dim=1).mean()), "news_spread": float((V - V.mean(0)).norm(dim=1).mean()),
             "user_norm": float(torch.cat(us).mean()), "score_abs": float(S.abs().mean()),
             "score_spread": float((S.max(1).values - S.min(1).values).mean()), "tied_share": ties,
             "fc_w": float(fc.weight.norm()), "fc_b": float(fc.bias.norm())}

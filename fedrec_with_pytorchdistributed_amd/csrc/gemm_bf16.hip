@@ -935,7 +935,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
         int gm = m0 + (rho >> 6) * 128 + h * 64 + (rho & 63);
         gm = gm < M ? gm : M - 1;
         o[h][i] = gm * K + schunk * 8;
-        o[2 + h][i] = (n0 + (rho >> 5) * 64 + h * 32 + (rho & 31)) * K + schunk * 8;
+        int wrow = n0 + (rho >> 5) * 64 + h * 32 + (rho & 31);
+        wrow = wrow < N ? wrow : N - 1;  // partial last column tile (N % 256 != 0): clamped, never stored
+        o[2 + h][i] = wrow * K + schunk * 8;
       }
     }
   };
@@ -1030,6 +1032,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
 
   int kt = 0, it = 0;
   bool after_epi = false;  // the previous step ended with a tile epilogue (its 16 stores in flight)
+  bool epi_stored = true;  // ... and this wave issued them (false: columns past a partial tile)
   for (int g = 0; g < S; ++g) {
     const char* buf = smem + (g & 1) * 4 * PP_HALF;
     const bool nx2 = kt + 2 >= nk;
@@ -1057,8 +1060,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     if (g + 2 >= S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if (DEFER && pend) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");        // 8 loads + 16 stores
     else if (DEFER && after_pend) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // + last phase's 4 stores
-    else if (!DEFER && !HAS_RES && after_epi && DUAL) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 8 + 32 stores
-    else if (!DEFER && !HAS_RES && after_epi) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 + 16 stores
+    // (a wave whose columns lay outside a partial last tile issued no stores: plain wait)
+    else if (!DEFER && !HAS_RES && after_epi && epi_stored && DUAL) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 8 + 32 stores
+    else if (!DEFER && !HAS_RES && after_epi && epi_stored) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 + 16 stores
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     after_pend = DEFER && pend;
     pend = false;
@@ -1082,6 +1086,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
       int m0, n0;
       tile_mn(it * G + c, m0, n0);
       const int nb0 = n0 + wc * 64 + fq * 4;
+      // partial last column tile (N % 256 == 64/128/192, no residual / dual / colsum: host
+      // checked): this wave's 64 columns are either all inside N or all outside
+      const bool col_ok = n0 + wc * 64 < N;
+      epi_stored = col_ok;
       f32x4 bb[2][2];
       if constexpr (HAS_BIAS) {
         // bias via opaque ds_reads (a plain read of the staging object would also drain vmcnt)
@@ -1146,8 +1154,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
               }
               a4 = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            store_pair16(C + (size_t)m * N + n0 + wc * 64 + p * 32, v[0], v[1], fq);
-            if constexpr (DUAL) store_pair16(Z + (size_t)m * N + n0 + wc * 64 + p * 32, zv[0], zv[1], fq);
+            if (col_ok) store_pair16(C + (size_t)m * N + n0 + wc * 64 + p * 32, v[0], v[1], fq);
+            if constexpr (DUAL) {
+              if (col_ok) store_pair16(Z + (size_t)m * N + n0 + wc * 64 + p * 32, zv[0], zv[1], fq);
+            }
           }
         }
       }
@@ -1200,14 +1210,19 @@ int g_gemm_variant = -1;  // -1 auto, 0 = 128x128, 1 = 256x256
 template <int ACT>
 void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, bf16* C, int M, int N, int K,
                 int c_rows, hipStream_t s) {
-  const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && N % BN2 == 0 && M >= 4096);
+  // N % 256 != 0 (the text head's N = 384): the ping-pong kernel with a partial last column
+  // tile (plain / bias / act epilogue only) -- opt-in (variant 9) only: at M = 80k, N = 384
+  // with tanh it measured 133 us vs 102 us for the 128x128 kernel (2.45 waves of 256-row
+  // tiles, a third of the MFMA work wasted on the clamped columns, tanh in the exposed epilogue)
+  const bool part_n = N % BN2 != 0 && N % 64 == 0 && R == nullptr && ACT != 3 && g_gemm_variant == 9;
+  const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && (N % BN2 == 0 || part_n) && M >= 4096);
   // auto policy (measured, profiles/gemm_bench_r1_pp.json): the ping-pong kernel (6) on every
   // N % 256 == 0 shape (with the packed-f32 GELU epilogue it also edges out variant 5 on FFN1).
   // auto: variant 9 wherever it applies (measured: profiles/gemm_bench_r1_v9.json), else 6
   const bool v9 = g_gemm_variant == 9 || g_gemm_variant == 10 || g_gemm_variant < 0;
-  if (big && N % BN2 == 0 && v9 && K >= 128 && N <= PP2_MAXN && c_rows >= ((M + 255) / 256) * 256 &&
+  if (big && (N % BN2 == 0 || part_n) && v9 && K >= 128 && N <= PP2_MAXN && c_rows >= ((M + 255) / 256) * 256 &&
       (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
-    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
+    const int tiles_n = (N + BN2 - 1) / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     if (g_num_cus == 0) {
       int dev = 0;
       (void)hipGetDevice(&dev);

@@ -33,12 +33,13 @@
 // Requirements (host-checked): N % 8 == 0, K % 8 == 0 (16-B row chunks), contiguous rows.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int TN = 256, TKO = 256, TM = 32;        // output tile n x k, reduction rows per stage
 constexpr int OP_BYTES = TM * 512;                 // one operand tile: 32 rows x 512 B
 constexpr int WSTAGE = 2 * OP_BYTES;               // 32 KB
-constexpr int NST = 4;                             // LDS stages (128 KB): 3 stages in flight
 
 __device__ __attribute__((aligned(16))) bf16 g_zero_row[256];  // zero-initialised (bss)
 
@@ -90,12 +91,15 @@ __device__ __forceinline__ bf16x8 join(s16x4 a, s16x4 b) {
 
 __device__ __forceinline__ void sync_stage(int inflight) {  // inflight younger stages may stay
   __builtin_amdgcn_sched_barrier(0);
-  if (inflight >= 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  if (inflight >= 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+  else if (inflight == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
   else if (inflight == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// NST LDS stages of 32 KB, NST - 1 in flight (4: 128 KB; 5: the whole 160 KB)
+template <int NST>
 __global__ __launch_bounds__(512, 1) void wgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
                                                        float* __restrict__ P, int M, int N, int K, int tiles_k,
                                                        int ntiles, int mchunk) {
@@ -252,8 +256,16 @@ extern "C" long fr_wgrad_bf16(const void* dY, const void* X, float* C, float* sc
   const long need = direct ? 0 : (long)S * N * K;
   if (scratch == nullptr && need > 0) return need;
   float* P = direct ? C : scratch;
-  hipLaunchKernelGGL(wgrad_kernel, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M, N,
-                     K, tiles_k, ntiles, mchunk);
+  static const int nst = [] {
+    const char* e = getenv("FEDREC_WGRAD_NST");  // A/B runs; default measured best
+    return e != nullptr && atoi(e) == 5 ? 5 : 4;
+  }();
+  if (nst == 5)
+    hipLaunchKernelGGL(wgrad_kernel<5>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M,
+                       N, K, tiles_k, ntiles, mchunk);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<4>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M,
+                       N, K, tiles_k, ntiles, mchunk);
   if (!direct) {
     const long n4 = (long)N * K / 4;
     long blocks = (n4 + 255) / 256;
