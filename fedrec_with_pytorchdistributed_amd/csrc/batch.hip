@@ -17,15 +17,20 @@ namespace {
 constexpr int MAXR = 8192;
 constexpr int NT = 1024;
 
+// KeyT = uint32 (ids < 2^19, R <= 8192: key = id << 13 | occurrence) or uint64 (id << 32 | i).
+// The 32-bit form halves the LDS image (32 KB): a step's dedup runs on the lookahead stream
+// beside the step's kernels, and a 64 KB block kept the weight-gradient GEMM's 96 KB block
+// off its CU (a one-wave grid then waits for that CU: 68 -> 120 us).
+template <typename KeyT, int SHIFT>
 __global__ __launch_bounds__(NT) void dedup_kernel(const int* __restrict__ ids, int R, int P, int* __restrict__ uniq,
                                                    int* __restrict__ inv, int* __restrict__ perm,
                                                    int* __restrict__ seg_ptr, int* __restrict__ u_count) {
-  __shared__ unsigned long long key[MAXR];
+  __shared__ KeyT key[MAXR];
   __shared__ int part[NT];
   __shared__ int wsum[NT / 64];
   const int tid = threadIdx.x;
   for (int i = tid; i < P; i += NT)
-    key[i] = i < R ? (((unsigned long long)(unsigned)ids[i]) << 32) | (unsigned)i : ~0ull;
+    key[i] = i < R ? (KeyT)((((KeyT)(unsigned)ids[i]) << SHIFT) | (KeyT)(unsigned)i) : (KeyT)~(KeyT)0;
   __syncthreads();
   // bitonic sort, ascending
   for (int k = 2; k <= P; k <<= 1) {
@@ -33,7 +38,7 @@ __global__ __launch_bounds__(NT) void dedup_kernel(const int* __restrict__ ids, 
       for (int i = tid; i < P; i += NT) {
         const int ixj = i ^ j;
         if (ixj > i) {
-          const unsigned long long a = key[i], b = key[ixj];
+          const KeyT a = key[i], b = key[ixj];
           const bool up = (i & k) == 0;
           if ((a > b) == up) {
             key[i] = b;
@@ -50,7 +55,7 @@ __global__ __launch_bounds__(NT) void dedup_kernel(const int* __restrict__ ids, 
   int cnt = 0;
   for (int e = 0; e < E; ++e) {
     const int i = b0 + e;
-    if (i < R) cnt += (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32)) ? 1 : 0;
+    if (i < R) cnt += (i == 0 || (key[i] >> SHIFT) != (key[i - 1] >> SHIFT)) ? 1 : 0;
   }
   // inclusive scan of cnt over the block
   const int lane = tid & 63, w = tid >> 6;
@@ -76,9 +81,9 @@ __global__ __launch_bounds__(NT) void dedup_kernel(const int* __restrict__ ids, 
   for (int e = 0; e < E; ++e) {
     const int i = b0 + e;
     if (i >= R) break;
-    const int id = (int)(key[i] >> 32);
-    const int r = (int)(key[i] & 0xffffffffu);
-    const bool f = (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32));
+    const int id = (int)(key[i] >> SHIFT);
+    const int r = (int)(key[i] & (KeyT)(((KeyT)1 << SHIFT) - 1));
+    const bool f = (i == 0 || (key[i] >> SHIFT) != (key[i - 1] >> SHIFT));
     if (f) {
       uniq[run] = id;
       seg_ptr[run] = i;
@@ -155,12 +160,17 @@ extern "C" int fr_sample_batch(const int* rows, const int* pos, const long long*
   return 0;
 }
 
-extern "C" int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count,
-                        hipStream_t s) {
+extern "C" int fr_dedup(const int* ids, int R, int num_news, int* uniq, int* inv, int* perm, int* seg_ptr,
+                        int* u_count, hipStream_t s) {
   if (R > MAXR || R < 1) return 1;
   int P = 1;
   while (P < R) P <<= 1;
-  hipLaunchKernelGGL(dedup_kernel, dim3(1), dim3(NT), 0, s, ids, R, P, uniq, inv, perm, seg_ptr, u_count);
+  if (num_news > 0 && num_news <= (1 << 19))  // 13 bits of occurrence index (MAXR = 8192)
+    hipLaunchKernelGGL((dedup_kernel<unsigned, 13>), dim3(1), dim3(NT), 0, s, ids, R, P, uniq, inv, perm, seg_ptr,
+                       u_count);
+  else
+    hipLaunchKernelGGL((dedup_kernel<unsigned long long, 32>), dim3(1), dim3(NT), 0, s, ids, R, P, uniq, inv, perm,
+                       seg_ptr, u_count);
   return 0;
 }
 

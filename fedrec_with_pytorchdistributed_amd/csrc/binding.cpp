@@ -52,7 +52,8 @@ int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long 
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
                     const int* his, int* cand, int* hout, int B, int npr, int H, int truncate, unsigned long long seed,
                     unsigned long long offset, hipStream_t s);
-int fr_dedup(const int* ids, int R, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count, hipStream_t s);
+int fr_dedup(const int* ids, int R, int num_news, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count,
+             hipStream_t s);
 int fr_secagg_mask(const float* x, int* out, long n, float scale, float clipv, const unsigned long long* seeds,
                    const int* signs, int npeers, unsigned long long round, hipStream_t s);
 int fr_secagg_unmask(const int* x, float* out, long n, float inv_scale, hipStream_t s);
@@ -509,8 +510,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dedup(const at::Tenso
   auto perm = at::empty({R}, opt);
   auto seg = at::empty({R + 1}, opt);
   auto ucount = at::empty({1}, opt);
-  check_rc(fr_dedup(ids.data_ptr<int>(), (int)R, uniq.data_ptr<int>(), inv.data_ptr<int>(), perm.data_ptr<int>(),
-                    seg.data_ptr<int>(), ucount.data_ptr<int>(), cur_stream()),
+  // num_news bounds the ids (the engine passes its table size): <= 2^19 selects 32-bit sort keys
+  check_rc(fr_dedup(ids.data_ptr<int>(), (int)R, (int)std::min<int64_t>(num_news, 1 << 30), uniq.data_ptr<int>(),
+                    inv.data_ptr<int>(), perm.data_ptr<int>(), seg.data_ptr<int>(), ucount.data_ptr<int>(),
+                    cur_stream()),
            "dedup");
   const int64_t U = ucount.item<int>();  // the backbone grid depends on U: one small D2H per step
   return {uniq.slice(0, 0, U), inv, perm, seg.slice(0, 0, U + 1)};

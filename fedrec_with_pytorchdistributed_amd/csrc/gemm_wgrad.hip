@@ -15,10 +15,10 @@
 // Structure:
 //   * output tile 256 (n) x 256 (k), 512 threads = 8 waves as 2 (n) x 4 (k), 128 x 64 per
 //     wave (8 x 4 MFMA tiles -> 128 accumulator VGPRs);
-//   * LDS stage = dY[32][256] + X[32][256] bf16 = 32 KB, four stages (128 KB, one block per
-//     CU), three in flight: the operand stream comes from L2 / HBM at ~1-2 us latency, one
-//     32-row step is ~0.4 us of MFMA work, so a 2-stage pipeline waits on every load
-//     (measured: 2 x 64-row stages ran at 760-800 TF);
+//   * LDS stage = dY[32][256] + X[32][256] bf16 = 32 KB, three stages by default (96 KB, one
+//     block per CU), two in flight; the fragment reads are opaque asm, so the compiler does
+//     not drain vmcnt before them (with builtin reads it waited for every in-flight stage:
+//     760-800 TF; pipelined: 974-1033 TF; 4 or 5 stages measured the same as 3);
 //   * bank-conflict swizzle: 16-B chunk c of row r is stored at chunk c ^ swz(r), swz(r) =
 //     2 * ((r & 3) | ((r >> 3) & 1) << 2); a 32-lane half of a transposed read touches rows
 //     {q, 8 + q} x one 32-B column pair, which the XOR spreads over all 64 banks (applied to
@@ -98,7 +98,7 @@ __device__ __forceinline__ void sync_stage(int inflight) {  // inflight younger 
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// NST LDS stages of 32 KB, NST - 1 in flight (4: 128 KB; 5: the whole 160 KB)
+// NST LDS stages of 32 KB, NST - 1 in flight (3: 96 KB, the default; 4: 128 KB; 5: 160 KB)
 template <int NST>
 __global__ __launch_bounds__(512, 1) void wgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
                                                        float* __restrict__ P, int M, int N, int K, int tiles_k,
@@ -257,10 +257,17 @@ extern "C" long fr_wgrad_bf16(const void* dY, const void* X, float* C, float* sc
   if (scratch == nullptr && need > 0) return need;
   float* P = direct ? C : scratch;
   static const int nst = [] {
-    const char* e = getenv("FEDREC_WGRAD_NST");  // A/B runs; default measured best
-    return e != nullptr && atoi(e) == 5 ? 5 : 4;
+    // A/B runs; default 3 (96 KB): 4 and 5 stages measured the same in isolation, and the
+    // smaller block leaves room on a CU for a lookahead-stream kernel (dedup: 32 KB) -- this
+    // grid is one wave of blocks, so a CU that cannot host its block doubles the kernel
+    const char* e = getenv("FEDREC_WGRAD_NST");
+    const int v = e != nullptr ? atoi(e) : 3;
+    return v == 4 || v == 5 ? v : 3;
   }();
-  if (nst == 5)
+  if (nst == 3)
+    hipLaunchKernelGGL(wgrad_kernel<3>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M,
+                       N, K, tiles_k, ntiles, mchunk);
+  else if (nst == 5)
     hipLaunchKernelGGL(wgrad_kernel<5>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M,
                        N, K, tiles_k, ntiles, mchunk);
   else

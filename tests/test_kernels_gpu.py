@@ -197,12 +197,16 @@ def test_score_ce(dev):
     assert rel_err(s, s2) < 1e-6 and rel_err(dc, dc2) < 1e-5 and rel_err(du, du2) < 1e-5
 
 
-def test_dedup_and_segment_sum(dev):
-    ids = torch.randint(0, 500, (64 * 55,), device=dev, dtype=torch.int32)
-    uniq, inv, perm, ptr = ops.dedup(ids, 500)
+@pytest.mark.parametrize("num_news", [500, 3 << 20])  # 32-bit sort keys / the 64-bit form (ids >= 2^19)
+def test_dedup_and_segment_sum(dev, num_news):
+    ids = torch.randint(0, num_news, (64 * 55,), device=dev, dtype=torch.int32)
+    ids[::7] = ids[3]  # repeated ids: the occurrence order inside a segment must be ascending
+    uniq, inv, perm, ptr = ops.dedup(ids, num_news)
     u_ref = torch.unique(ids.cpu())
     assert torch.equal(uniq.cpu().long(), u_ref.long())
     assert torch.equal(uniq[inv.long()], ids)
+    order = torch.sort(ids.cpu().long() * ids.numel() + torch.arange(ids.numel()), stable=True).indices
+    assert torch.equal(perm.cpu().long(), order)
     rows = torch.randn(ids.numel(), 400, device=dev)
     out = ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr))
     o_ref = ref.segment_sum_rows(rows, inv, uniq.numel())
