@@ -92,6 +92,8 @@ int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, in
 int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles,
                                      int T, int H, int D, float pdrop, unsigned long long seed,
                                      unsigned long long offset, hipStream_t s);
+int fr_gather_dropout_f32(const float* v, const int* idx, float* out, int M, int K, float p, unsigned long long seed,
+                          unsigned long long offset, const unsigned long long* dev_off, hipStream_t s);
 long fr_wgrad_bf16(const void* dY, const void* X, float* C, float* scratch, int M, int N, int K, int accumulate,
                    hipStream_t s);
 }
@@ -965,6 +967,29 @@ at::Tensor embed_grad(const at::Tensor& dx, const at::Tensor& sorted, const at::
   return dword;
 }
 
+// out[m] = v[idx[m]] * Philox dropout mask (small_gemm.hip), fp32
+at::Tensor gather_dropout(const at::Tensor& v, const at::Tensor& idx, double p, int64_t seed, int64_t offset,
+                          const c10::optional<at::Tensor>& dev_off) {
+  check_dev(v, "v");
+  check_dev(idx, "idx");
+  TORCH_CHECK(v.scalar_type() == at::kFloat && v.dim() == 2 && idx.scalar_type() == at::kInt && idx.dim() == 1,
+              "fedrec::gather_dropout: fp32 v [U, K], int32 idx [M]");
+  TORCH_CHECK(v.size(1) % 4 == 0, "fedrec::gather_dropout: K % 4");
+  const c10::DeviceGuard g(v.device());
+  const unsigned long long* dp = nullptr;
+  if (dev_off.has_value() && dev_off->defined()) {
+    check_dev(*dev_off, "dev_off");
+    TORCH_CHECK(dev_off->scalar_type() == at::kLong && dev_off->numel() >= 1, "fedrec::gather_dropout: dev_off");
+    dp = (const unsigned long long*)dev_off->data_ptr<int64_t>();
+  }
+  auto out = at::empty({idx.size(0), v.size(1)}, v.options());
+  check_rc(fr_gather_dropout_f32(v.data_ptr<float>(), idx.data_ptr<int>(), out.data_ptr<float>(), (int)idx.size(0),
+                                 (int)v.size(1), (float)p, (unsigned long long)seed, (unsigned long long)offset, dp,
+                                 cur_stream()),
+           "gather_dropout");
+  return out;
+}
+
 // dW[N, K] = dy[M, N]^T x[M, K] in fp32 (gemm_wgrad.hip)
 at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x) {
   check_dev(dy, "dy");
@@ -1041,6 +1066,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x) -> Tensor");
+  m.def("gather_dropout(Tensor v, Tensor idx, float p, int seed, int offset, Tensor? dev_off) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
@@ -1082,4 +1108,5 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);
   m.impl("wgrad", &wgrad);
+  m.impl("gather_dropout", &gather_dropout);
 }

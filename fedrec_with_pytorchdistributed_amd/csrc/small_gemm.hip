@@ -387,3 +387,45 @@ extern "C" long fr_colsum_f32(const float* const* xs, float* const* outs, const 
   hipLaunchKernelGGL(colsum_final_kernel, dim3(blocks2), dim3(64), 0, s, b);
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// X'[m, k] = v[idx[m], k] * Z(m * K + k): the user encoder's gathered, dropped-out input
+// (encoder.py:50), materialised once per step (fp32 [B*H, D], 5 MB) instead of regenerated in
+// every GEMM tile that reads it -- the Q/K/V projection's A loads (21 column tiles each redid
+// the Philox draws of their rows) and the weight-gradient GEMMs' B loads (one redo per output
+// row tile).  Same mask, same fp32 product: bitwise the values those loads computed.
+// One thread per 4 consecutive elements = one Philox draw (K % 4 == 0, host-checked).
+namespace {
+__global__ __launch_bounds__(256) void gather_dropout_kernel(const float* __restrict__ v, const int* __restrict__ idx,
+                                                             float* __restrict__ out, int M, int K, float p,
+                                                             unsigned long long seed, unsigned long long offset,
+                                                             const unsigned long long* __restrict__ dev_off) {
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index
+  const long n4 = (long)M * K / 4;
+  if (q >= n4) return;
+  const long e = q * 4;
+  const int m = (int)(e / K), k = (int)(e - (long)m * K);
+  float4 x = *(const float4*)(v + (size_t)idx[m] * K + k);
+  if (p > 0.f) {
+    const unsigned long long off = offset + (dev_off ? *dev_off : 0ull);
+    const float inv_keep = 1.0f / (1.0f - p);
+    const uint4 r = Philox::gen(seed, off, (unsigned long long)e >> 2);
+    x.x *= drop_scale(r.x, p, inv_keep);
+    x.y *= drop_scale(r.y, p, inv_keep);
+    x.z *= drop_scale(r.z, p, inv_keep);
+    x.w *= drop_scale(r.w, p, inv_keep);
+  }
+  *(float4*)(out + e) = x;
+}
+}  // namespace
+
+extern "C" int fr_gather_dropout_f32(const float* v, const int* idx, float* out, int M, int K, float p,
+                                     unsigned long long seed, unsigned long long offset,
+                                     const unsigned long long* dev_off, hipStream_t s) {
+  if (K % 4 != 0 || M < 0) return 1;
+  const long n4 = (long)M * K / 4;
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL(gather_dropout_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, v, idx, out, M, K, p,
+                     seed, offset, dev_off);
+  return 0;
+}

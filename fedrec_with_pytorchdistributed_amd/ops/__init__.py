@@ -274,6 +274,20 @@ class Gemm:
         self.bseg, self.kseg = tuple(bseg), int(kseg)
 
 
+def gather_dropout(v: torch.Tensor, idx: torch.Tensor, p: float, seed: int, offset: int, dev_off=None) -> torch.Tensor:
+    """``v[idx] * Z`` (fp32): rows of ``v`` gathered and dropped out with the counter mask of
+    element ``m * K + k`` (offset + ``*dev_off``) -- the mask ``small_gemm``'s dropout loads use."""
+    if _dev(v):
+        return native.require_for(v).gather_dropout(v.contiguous(), idx.to(torch.int32).contiguous(), float(p),
+                                                    int(seed), int(offset), dev_off)
+    x = v.index_select(0, idx.long())
+    if p > 0:
+        off = int(offset) + (int(dev_off.item()) if dev_off is not None else 0)
+        idx_e = torch.arange(x.numel(), device=x.device, dtype=torch.int64)
+        x = x * ref.dropout_scale(idx_e, p, int(seed), off).view_as(x).to(x.dtype)
+    return x
+
+
 def small_gemm(*gs: Gemm, dev_off=None) -> None:
     """Run up to 6 independent GEMMs in one launch (device only).  ``dev_off``: an int64[1]
     device counter added to every dropout offset (HIP-graph replays draw fresh masks)."""

@@ -469,9 +469,11 @@ class UserStepFn(torch.autograd.Function):
     ``inv [R]`` maps the batch's occurrences (``B*C`` candidates, then ``B*H`` history
     slots) to rows of ``v``; ``perm / ptr`` group them per news for the segment sum.  The
     input dropout of the user encoder (``encoder.py:50``) is the Philox mask of element
-    ``(b*H + t) * D + d`` of the gathered history matrix with offset ``drop[2] + *dev_off``
-    -- applied in the Q/K/V GEMMs' operand loads, regenerated by the weight-gradient GEMMs'
-    loads and by the dgrad's epilogue (nothing is stored)."""
+    ``(b*H + t) * D + d`` of the gathered history matrix with offset ``drop[2] + *dev_off``:
+    the gathered, dropped-out input X' is materialised once (``ops.gather_dropout``, 5 MB),
+    read by the Q/K/V GEMMs and the weight gradients; the dgrad regenerates the mask in its
+    epilogue.  (Round 2 first applied the mask inside every GEMM tile's operand loads; each
+    of the ~21 column tiles redid its rows' Philox draws.)"""
 
     @staticmethod
     def forward(ctx, v, inv, perm, ptr, wq, bq, wk, bk, wv, bv, w1, b1, w2, b2, meta):
@@ -483,10 +485,10 @@ class UserStepFn(torch.autograd.Function):
         cand = v.index_select(0, inv[:BC].long()).view(B, C, D)
         qkv = torch.empty(BH, 3 * D, device=v.device, dtype=torch.float32)
         p, seed, off = drop
-        dkw = dict(pdrop=p, drop_on=1, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
-        ops.small_gemm(*[ops.Gemm(v, w, qkv[:, s * D:(s + 1) * D], BH, D, D, D, D, 3 * D, bias=b, gidx=his_idx,
-                                  gather_on=1, **dkw)
-                         for s, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv)))], dev_off=dev_off)
+        # X' = drop(v[his]) once (5 MB): the Q/K/V projection and the weight gradients read it
+        xd = ops.gather_dropout(v, his_idx, p, seed, off, dev_off)
+        ops.small_gemm(*[ops.Gemm(xd, w, qkv[:, s * D:(s + 1) * D], BH, D, D, D, D, 3 * D, bias=b)
+                         for s, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv)))])
         q3 = qkv.view(B, H, 3 * D)
         c3, stats = ops.user_attention_fwd(q3, heads, hd)
         e = torch.empty(BH, Qd, device=v.device, dtype=torch.float32)
@@ -494,14 +496,14 @@ class UserStepFn(torch.autograd.Function):
         e3 = e.view(B, H, Qd)
         u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2)
         loss, scores, dcand, du = ops.score_ce(cand, u, act)
-        ctx.save_for_backward(v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2)
+        ctx.save_for_backward(v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2, xd)
         ctx.meta = meta
         ctx.mark_non_differentiable(scores)
         return loss, scores
 
     @staticmethod
     def backward(ctx, gloss, gscores):
-        v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2 = ctx.saved_tensors
+        v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2, xd = ctx.saved_tensors
         B, C, H, heads, hd, act, drop, dev_off, ldp, padded = ctx.meta
         D = v.shape[1]
         BC, BH = B * C, B * H
@@ -524,14 +526,13 @@ class UserStepFn(torch.autograd.Function):
         ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
         ops.small_gemm(ops.Gemm(dqkv, wq, dx, BH, D, 3 * D, 3 * D, D, D, b_mode=1, bseg=(wk, wv), kseg=D, **ekw),
                        dev_off=dev_off)
-        # weight gradients in one launch: dW_s = dS^T X' (X' = the gathered, dropped-out input,
-        # regenerated in the B loads) and dW1 = dpre^T ctx
+        # weight gradients in one launch: dW_s = dS^T X' (X' saved by the forward) and
+        # dW1 = dpre^T ctx
         gq, gk, gv = (torch.empty(D, D, device=dev) for _ in range(3))
         gw1 = torch.empty(Qd, D, device=dev)
-        bkw = dict(pdrop=p, drop_on=2, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
-        ops.small_gemm(*[ops.Gemm(dqkv[:, s * D:(s + 1) * D], v, g, D, D, BH, 3 * D, D, D, a_mode=1, b_mode=1,
-                                  gidx=his_idx, gather_on=2, **bkw) for s, g in enumerate((gq, gk, gv))],
-                       ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1), dev_off=dev_off)
+        ops.small_gemm(*[ops.Gemm(dqkv[:, s * D:(s + 1) * D], xd, g, D, D, BH, 3 * D, D, D, a_mode=1, b_mode=1)
+                         for s, g in enumerate((gq, gk, gv))],
+                       ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1))
         gbq, gbk, gbv = (torch.empty(D, device=dev) for _ in range(3))
         gb1 = torch.empty(Qd, device=dev)
         ops.colsum_f32([(dqkv[:, 0:D], gbq, BH, D, 3 * D), (dqkv[:, D:2 * D], gbk, BH, D, 3 * D),

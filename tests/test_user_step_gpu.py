@@ -93,3 +93,18 @@ def test_head_fc_matches_torch(dev):
     yc.backward(g)
     assert _rel(y, yc) < 5e-3
     assert _rel(x.grad, xc.grad) < 5e-3 and _rel(w.grad, wc.grad) < 5e-3 and _rel(b.grad, bc.grad) < 1e-5
+
+
+def test_gather_dropout_matches_oracle():
+    """X' = v[idx] o Z on the device == the Philox torch oracle, bit for bit (with the graph
+    replay counter dev_off added to the offset)."""
+    dev = torch.device("cuda")
+    v = torch.randn(300, 400, device=dev)
+    idx = torch.randint(0, 300, (3200,), device=dev, dtype=torch.int32)
+    dev_off = torch.tensor([7], device=dev, dtype=torch.int64)
+    x = ops.gather_dropout(v, idx, 0.2, 11, 5, dev_off)
+    xr = ops.gather_dropout(v.cpu(), idx.cpu(), 0.2, 11, 5, dev_off.cpu())
+    assert torch.equal(x.cpu(), xr)
+    keep = (x != 0).float().mean().item()
+    assert abs(keep - 0.8) < 0.01
+    assert torch.equal(ops.gather_dropout(v, idx, 0.0, 11, 5, None), v[idx.long()])
