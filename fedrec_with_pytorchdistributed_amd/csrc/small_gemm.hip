@@ -239,6 +239,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batc
 
 // Deterministic fp32 column sums (bias gradients), two passes: (1) blocks of 64 columns x 128
 // rows (4 waves x 32 rows) write per-chunk partials; (2) the partials are summed in chunk order.
+// A desc of one row chunk (M <= 128: the loss sum, the pooled-user partial rows) is final after
+// pass 1, and a launch of only such descs skips pass 2.  (A single-pass "last block sums"
+// form with agent-scope fences measured 131 us/step vs 69: each release fence writes back L2.)
 constexpr int CS_ROWS = 128;
 struct ColsumDesc {
   const float* X;
@@ -267,8 +270,13 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const ColsumBatch batc
     for (int m = r0 + w; m < r1; m += 4) s += g.X[(size_t)m * g.ld + c];
   part[w][threadIdx.x & 63] = s;
   __syncthreads();
-  if (w == 0 && c < g.N)
-    g.part[(size_t)ch * g.N + c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+  if (w == 0 && c < g.N) {
+    const float tot = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+    if (g.chunks == 1)  // one row chunk: the final value (no second pass for this desc)
+      g.out[c] = g.accumulate ? g.out[c] + tot : tot;
+    else
+      g.part[(size_t)ch * g.N + c] = tot;
+  }
 }
 
 __global__ __launch_bounds__(64) void colsum_final_kernel(const ColsumBatch batch) {
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(64) void colsum_final_kernel(const ColsumBatch batc
     if (i < batch.n && (int)blockIdx.x >= batch.d[i].block2_base) gi = i;
   const ColsumDesc& g = batch.d[gi];
   const int c = (blockIdx.x - g.block2_base) * 64 + threadIdx.x;
-  if (c >= g.N) return;
+  if (c >= g.N || g.chunks == 1) return;
   float s = 0.f;
   for (int ch = 0; ch < g.chunks; ++ch) s += g.part[(size_t)ch * g.N + c];
   g.out[c] = g.accumulate ? g.out[c] + s : s;
@@ -384,7 +392,9 @@ extern "C" long fr_colsum_f32(const float* const* xs, float* const* outs, const 
   if (part == nullptr) return need;
   if (blocks == 0) return 0;
   hipLaunchKernelGGL(colsum_part_kernel, dim3(blocks), dim3(256), 0, s, b);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(blocks2), dim3(64), 0, s, b);
+  bool second = false;  // descs of one row chunk are final after the first pass
+  for (int i = 0; i < n; ++i) second |= b.d[i].chunks > 1;
+  if (second) hipLaunchKernelGGL(colsum_final_kernel, dim3(blocks2), dim3(64), 0, s, b);
   return 0;
 }
 
