@@ -79,6 +79,24 @@ class FlatParams:
                 dst.append(view)
                 src.append(p.grad)
             p.grad = view
+        if dst and not missing and len(dst) == len(self.params):
+            # every parameter has a fresh gradient: one cat of [grad, zero gap, grad, ...] into
+            # the flat buffer (a single batched copy kernel; the multi-tensor copy took ~18 us
+            # for these 4.66 MB).  The alignment gaps get zeros, as the buffer was created.
+            if getattr(self, "_cat_parts", None) is None or self._cat_parts[0] != self.grad.device:
+                gaps = []
+                for i, (p, off) in enumerate(zip(self.params, self.offsets)):
+                    end = self.offsets[i + 1] if i + 1 < len(self.offsets) else self.numel_padded
+                    gaps.append(end - off - p.numel())
+                self._cat_parts = (self.grad.device,
+                                   [torch.zeros(g, device=self.grad.device) if g > 0 else None for g in gaps])
+            parts = []
+            for t, z in zip(src, self._cat_parts[1]):
+                parts.append(t.reshape(-1))
+                if z is not None:
+                    parts.append(z)
+            torch.cat(parts, out=self.grad)
+            return
         if dst:
             torch._foreach_copy_(dst, src)
         if missing:
