@@ -1,0 +1,73 @@
+"""User-encoder attention (20 heads x d_k 20, fp32) at the config-2 shape (B = 64 impressions,
+H = 50 clicked news): the ILP kernels (default) against the first forms, interleaved in one
+process, with an output check between them.
+
+    python benchmarks/user_attn_bench.py [--out gpurun_out/user_attn_bench.json]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from fedrec_with_pytorchdistributed_amd import ops
+from fedrec_with_pytorchdistributed_amd.ops import native
+
+
+def timeit(fn, iters=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--H", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    lib = native.lib()
+    NH, DK = 20, 20
+    g = torch.Generator(device="cpu").manual_seed(0)
+    qkv = torch.randn(a.B, a.H, 3 * NH * DK, generator=g).cuda()
+    d = torch.randn(a.B, a.H, NH * DK, generator=g).cuda()
+    outs = {}
+    for v in (0, 1):
+        lib.user_attn_set_variant(v)
+        c, st = ops.user_attention_fwd(qkv, NH, DK)
+        outs[v] = (c, st, ops.user_attention_bwd(qkv, st, d, NH, DK))
+    res = {"fwd_rel_diff": float((outs[0][0] - outs[1][0]).norm() / outs[0][0].norm()),
+           "bwd_rel_diff": float((outs[0][2] - outs[1][2]).norm() / outs[0][2].norm())}
+    print(res, flush=True)
+    times = {f"{k}_v{v}": [] for k in ("fwd", "bwd") for v in (0, 1)}
+    st = outs[1][1]
+    for _ in range(a.rounds):
+        for v in (0, 1):
+            lib.user_attn_set_variant(v)
+            times[f"fwd_v{v}"].append(timeit(lambda: ops.user_attention_fwd(qkv, NH, DK)))
+            times[f"bwd_v{v}"].append(timeit(lambda: ops.user_attention_bwd(qkv, st, d, NH, DK)))
+    lib.user_attn_set_variant(1)
+    for k, v in times.items():
+        res[k] = {"us": round(1000 * statistics.median(v), 2), "all_us": [round(1000 * x, 2) for x in v]}
+        print(k, res[k], flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

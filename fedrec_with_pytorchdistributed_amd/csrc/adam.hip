@@ -49,3 +49,75 @@ extern "C" int fr_adam_flat(float* p, const float* g, float* m, float* v, void* 
                      (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, lr / bc1, 1.0f / sqrtf(bc2), grad_scale);
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// Compute-weight refresh of the unfrozen backbone after an optimizer step: up to MCAST_SEG
+// fp32 master tensors -> their bf16 (or fp32) compute copies in ONE launch, 8 elements per
+// thread (two float4 loads, one 16-byte bf16 store).  Segment i may write into a slice of a
+// bigger destination (q / k / v weights -> the fused [3D, D] QKV weight), so the per-step
+// pack rebuild (a cat + a cast launch per weight, ~100 launches at BERT-base) becomes one
+// streaming pass.  Blocks are assigned to segments in proportion to their size
+// (MCAST_CHUNK elements per block); a block finds its segment by binary search.
+namespace {
+constexpr int MCAST_SEG = 96;
+constexpr int MCAST_CHUNK = 8192;  // 256 threads x 4 iterations x 8 elements
+
+struct MultiCast {
+  const float* src[MCAST_SEG];
+  void* dst[MCAST_SEG];
+  long n[MCAST_SEG];
+  int blk0[MCAST_SEG + 1];
+  unsigned char bf[MCAST_SEG];  // 1: bf16 destination, 0: fp32
+  int nseg;
+};
+
+__global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
+  int lo = 0, hi = mc.nseg - 1;  // last segment with blk0 <= blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (mc.blk0[mid] <= (int)blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  const int sg = lo;
+  const long base = (long)(blockIdx.x - mc.blk0[sg]) * MCAST_CHUNK;
+  const float4* s4 = (const float4*)mc.src[sg];
+  const long n = mc.n[sg];
+#pragma unroll
+  for (int it = 0; it < MCAST_CHUNK / (256 * 8); ++it) {
+    const long e = base + ((long)it * 256 + threadIdx.x) * 8;
+    if (e < n) {
+      const float4 a = s4[e >> 2], b = s4[(e >> 2) + 1];
+      if (mc.bf[sg]) {
+        *(bf16x8*)((bf16*)mc.dst[sg] + e) =
+            bf16x8{f2bf(a.x), f2bf(a.y), f2bf(a.z), f2bf(a.w), f2bf(b.x), f2bf(b.y), f2bf(b.z), f2bf(b.w)};
+      } else {
+        float4* d4 = (float4*)((float*)mc.dst[sg] + e);
+        d4[0] = a;
+        d4[1] = b;
+      }
+    }
+  }
+}
+}  // namespace
+
+// 0 ok; 1 = too many segments / bad size or alignment (the caller rebuilds the pack instead)
+extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
+                             hipStream_t s) {
+  if (nseg < 1 || nseg > MCAST_SEG) return 1;
+  MultiCast mc{};
+  mc.nseg = nseg;
+  long blk = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (n[i] <= 0 || n[i] % 8 != 0 || ((uintptr_t)src[i] & 15) != 0 || ((uintptr_t)dst[i] & 15) != 0) return 1;
+    mc.src[i] = src[i];
+    mc.dst[i] = dst[i];
+    mc.n[i] = n[i];
+    mc.bf[i] = to_bf16[i] ? 1 : 0;
+    mc.blk0[i] = (int)blk;
+    blk += (n[i] + MCAST_CHUNK - 1) / MCAST_CHUNK;
+  }
+  mc.blk0[nseg] = (int)blk;
+  if (blk >= (1L << 31)) return 1;
+  hipLaunchKernelGGL(multi_cast_kernel, dim3((unsigned)blk), dim3(256), 0, s, mc);
+  return 0;
+}

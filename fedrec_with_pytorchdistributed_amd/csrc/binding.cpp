@@ -17,11 +17,13 @@ extern "C" {
 void fr_gemm_set_variant(int v);
 void fr_title_attn_set_waves(int w);
 void fr_title_attn_bwd_set_variant(int v);
+void fr_user_attn_set_variant(int v);
 void fr_ln_set_wide(int v);
 int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K, int act,
                     int c_rows, hipStream_t s);
 int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db, int rows, int D,
-                           float eps, hipStream_t s, float* dxs);
+                           float eps, hipStream_t s, float* dxs, void* dxz, float pdrop, unsigned long long seed,
+                           unsigned long long offset);
 int fr_gelu_bf16(const void* z, const void* dh, void* out, long n, int bwd, hipStream_t s);
 int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles, int T, int H,
                                 int D, hipStream_t s);
@@ -82,13 +84,17 @@ int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int 
 int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, hipStream_t s);
+int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg, hipStream_t s);
 int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
                   hipStream_t s);
 long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part, hipStream_t s);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
 int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
-                                 float pdrop, unsigned long long seed, unsigned long long offset, hipStream_t s);
+                                 float pdrop, unsigned long long seed, unsigned long long offset, hipStream_t s,
+                                 void* zbits);
+int fr_title_attention_bwd_drop_bits_bf16(const void* qkv, const void* dout, const int* mask, const void* zbits,
+                                          void* dqkv, int n_titles, int T, int H, int D, float pdrop, hipStream_t s);
 int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles,
                                      int T, int H, int D, float pdrop, unsigned long long seed,
                                      unsigned long long offset, hipStream_t s);
@@ -174,12 +180,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_impl(c
   const int64_t D = x.size(-1);
   auto wf = w.to(at::kFloat).contiguous();
   auto dx = at::empty_like(x);
-  auto dw = at::zeros({D}, x.options().dtype(at::kFloat));
-  auto db = at::zeros({D}, x.options().dtype(at::kFloat));
-  at::Tensor dxs = want_dxsum ? at::zeros({D}, x.options().dtype(at::kFloat)) : at::Tensor();
+  // the kernel accumulates dw / db (/ dx column sums) across row blocks: one zeroed buffer,
+  // one fill launch (three at::zeros were 75 fill launches per config-5 step)
+  auto acc = at::zeros({want_dxsum ? 3 : 2, D}, x.options().dtype(at::kFloat));
+  auto dw = acc[0];
+  auto db = acc[1];
+  at::Tensor dxs = want_dxsum ? acc[2] : at::Tensor();
   check_rc(fr_layer_norm_bwd_bf16(x.data_ptr(), wf.data_ptr<float>(), dy.data_ptr(), dx.data_ptr(), dw.data_ptr<float>(),
                                   db.data_ptr<float>(), (int)(x.numel() / D), (int)D, (float)eps, cur_stream(),
-                                  want_dxsum ? dxs.data_ptr<float>() : nullptr),
+                                  want_dxsum ? dxs.data_ptr<float>() : nullptr, nullptr, 0.f, 0ull, 0ull),
            "layer_norm_bwd");
   return {dx, dw, db, dxs};
 }
@@ -195,6 +204,27 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_colsum
                                                                                  const at::Tensor& w,
                                                                                  const at::Tensor& dy, double eps) {
   return layer_norm_bwd_impl(x, w, dy, eps, true);
+}
+
+// + the dropout backward of the layer feeding the LayerNorm: (dx, dx o Z, dw, db, colsum(dx o Z))
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_drop(
+    const at::Tensor& x, const at::Tensor& w, const at::Tensor& dy, double eps, double p, int64_t seed, int64_t offset) {
+  check_dev(x, "x");
+  check_dev(dy, "dy");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "fedrec::layer_norm_bwd_drop: bf16");
+  TORCH_CHECK(x.is_contiguous() && dy.is_contiguous() && dy.numel() == x.numel(), "fedrec::layer_norm_bwd_drop: shapes");
+  const c10::DeviceGuard g(x.device());
+  const int64_t D = x.size(-1);
+  auto wf = w.to(at::kFloat).contiguous();
+  auto dx = at::empty_like(x);
+  auto dxz = at::empty_like(x);
+  auto acc = at::zeros({3, D}, x.options().dtype(at::kFloat));
+  check_rc(fr_layer_norm_bwd_bf16(x.data_ptr(), wf.data_ptr<float>(), dy.data_ptr(), dx.data_ptr(),
+                                  acc[0].data_ptr<float>(), acc[1].data_ptr<float>(), (int)(x.numel() / D), (int)D,
+                                  (float)eps, cur_stream(), acc[2].data_ptr<float>(), dxz.data_ptr(), (float)p,
+                                  (unsigned long long)seed, (unsigned long long)offset),
+           "layer_norm_bwd_drop");
+  return {dx, dxz, acc[0], acc[1], acc[2]};
 }
 
 at::Tensor gelu(const at::Tensor& z, const c10::optional<at::Tensor>& dh) {
@@ -245,6 +275,45 @@ at::Tensor dropout_add(const at::Tensor& h, const c10::optional<at::Tensor>& res
   return out;
 }
 
+// the train-mode forward that also returns the keep bits ([n*H*64] int64) for the backward
+std::tuple<at::Tensor, at::Tensor> title_attention_drop_bits(const at::Tensor& qkv, const at::Tensor& mask,
+                                                             int64_t n_heads, double p, int64_t seed, int64_t offset) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.is_contiguous(), "fedrec::title_attention_drop_bits: bf16");
+  const c10::DeviceGuard g(qkv.device());
+  auto mk = mask.to(at::kInt).contiguous();
+  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
+  TORCH_CHECK(qkv.numel() == n * T * 3 * D, "fedrec::title_attention_drop_bits: qkv shape");
+  auto out = at::empty({n * T, D}, qkv.options());
+  auto bits = at::empty({n * n_heads * 64}, qkv.options().dtype(at::kLong));
+  check_rc(fr_title_attention_drop_bf16(qkv.data_ptr(), mk.data_ptr<int>(), out.data_ptr(), (int)n, (int)T,
+                                        (int)n_heads, (int)D, (float)p, (unsigned long long)seed,
+                                        (unsigned long long)offset, cur_stream(), bits.data_ptr()),
+           "title_attention_drop_bits");
+  return {out, bits};
+}
+
+at::Tensor title_attention_bwd_drop_bits(const at::Tensor& qkv, const at::Tensor& dout, const at::Tensor& mask,
+                                         const at::Tensor& bits, int64_t n_heads, double p) {
+  check_dev(qkv, "qkv");
+  check_dev(dout, "dout");
+  check_dev(bits, "bits");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && dout.scalar_type() == at::kBFloat16 && qkv.is_contiguous() &&
+                  dout.is_contiguous(), "fedrec::title_attention_bwd_drop_bits: bf16");
+  const c10::DeviceGuard g(qkv.device());
+  auto mk = mask.to(at::kInt).contiguous();
+  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
+  TORCH_CHECK(qkv.numel() == n * T * 3 * D && dout.numel() == n * T * D, "fedrec::title_attention_bwd_drop_bits: shapes");
+  TORCH_CHECK(bits.scalar_type() == at::kLong && bits.is_contiguous() && bits.numel() == n * n_heads * 64,
+              "fedrec::title_attention_bwd_drop_bits: bits");
+  auto dqkv = at::empty_like(qkv);
+  check_rc(fr_title_attention_bwd_drop_bits_bf16(qkv.data_ptr(), dout.data_ptr(), mk.data_ptr<int>(), bits.data_ptr(),
+                                                 dqkv.data_ptr(), (int)n, (int)T, (int)n_heads, (int)D, (float)p,
+                                                 cur_stream()),
+           "title_attention_bwd_drop_bits");
+  return dqkv;
+}
+
 at::Tensor title_attention_drop(const at::Tensor& qkv, const at::Tensor& mask, int64_t n_heads, double p, int64_t seed,
                                 int64_t offset) {
   check_dev(qkv, "qkv");
@@ -256,7 +325,7 @@ at::Tensor title_attention_drop(const at::Tensor& qkv, const at::Tensor& mask, i
   auto out = at::empty({n * T, D}, qkv.options());
   check_rc(fr_title_attention_drop_bf16(qkv.data_ptr(), mk.data_ptr<int>(), out.data_ptr(), (int)n, (int)T,
                                         (int)n_heads, (int)D, (float)p, (unsigned long long)seed,
-                                        (unsigned long long)offset, cur_stream()),
+                                        (unsigned long long)offset, cur_stream(), nullptr),
            "title_attention_drop");
   return out;
 }
@@ -692,6 +761,37 @@ void colsum_f32(const std::vector<at::Tensor>& X, const std::vector<at::Tensor>&
               "fedrec::colsum_f32: launch failed");
 }
 
+// fp32 tensors -> bf16 / fp32 destinations (slices allowed) in one launch (adam.hip); false =
+// not launched (too many segments, sizes not multiples of 8, misaligned): the caller copies itself
+bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst) {
+  const size_t n = src.size();
+  TORCH_CHECK(n >= 1 && dst.size() == n, "fedrec::multi_cast: sizes");
+  const c10::DeviceGuard g(dst[0].device());
+  std::vector<const float*> sp(n);
+  std::vector<void*> dp(n);
+  std::vector<long> ne(n);
+  std::vector<int> bf(n);
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && dst[i].is_contiguous() &&
+                    src[i].scalar_type() == at::kFloat &&
+                    (dst[i].scalar_type() == at::kBFloat16 || dst[i].scalar_type() == at::kFloat) &&
+                    src[i].numel() == dst[i].numel(),
+                "fedrec::multi_cast: contiguous fp32 sources, bf16/fp32 destinations of the same size");
+    sp[i] = src[i].data_ptr<float>();
+    dp[i] = dst[i].data_ptr();
+    ne[i] = (long)src[i].numel();
+    bf[i] = dst[i].scalar_type() == at::kBFloat16 ? 1 : 0;
+  }
+  for (size_t i = 0; i < n; ++i)  // every segment is checked before anything launches
+    if (ne[i] % 8 != 0 || ((uintptr_t)sp[i] & 15) != 0 || ((uintptr_t)dp[i] & 15) != 0) return false;
+  for (size_t i0 = 0; i0 < n; i0 += 96) {  // 96 segments per launch (kernel-argument size)
+    const int k = (int)std::min<size_t>(96, n - i0);
+    TORCH_CHECK(fr_multi_cast(sp.data() + i0, dp.data() + i0, ne.data() + i0, bf.data() + i0, k, cur_stream()) == 0,
+                "fedrec::multi_cast: launch rejected");
+  }
+  return true;
+}
+
 // several small copies (+ fills of the tails) in one launch, in 4-byte words
 void multi_copy(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst, at::IntArrayRef fill) {
   const size_t n = src.size();
@@ -1017,6 +1117,7 @@ at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x) {
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
+void user_attn_set_variant(int64_t v) { fr_user_attn_set_variant((int)v); }
 void segsum_set_variant(int64_t v) { fr_segsum_set_variant((int)v); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 
@@ -1026,6 +1127,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("gemm_set_variant(int v) -> ()", &gemm_set_variant);
   m.def("title_attn_set_waves(int w) -> ()", &title_attn_set_waves);
   m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
+  m.def("user_attn_set_variant(int v) -> ()", &user_attn_set_variant);
   m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
@@ -1034,6 +1136,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual=None) -> Tensor");
   m.def("layer_norm_bwd(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layer_norm_bwd_colsum(Tensor x, Tensor w, Tensor dy, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("layer_norm_bwd_drop(Tensor x, Tensor w, Tensor dy, float eps, float p, int seed, int offset) -> "
+        "(Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("gelu(Tensor z, Tensor? dh) -> Tensor");
   m.def("title_attention_bwd(Tensor qkv, Tensor dout, Tensor mask, int n_heads) -> Tensor");
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
@@ -1059,11 +1163,14 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
   m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg) -> ()");
   m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
+  m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst) -> bool");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");
   m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");
   m.def("dropout_add(Tensor h, Tensor? res, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
+  m.def("title_attention_drop_bits(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> (Tensor, Tensor)");
+  m.def("title_attention_bwd_drop_bits(Tensor qkv, Tensor dout, Tensor mask, Tensor bits, int n_heads, float p) -> Tensor");
   m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("gather_dropout(Tensor v, Tensor idx, float p, int seed, int offset, Tensor? dev_off) -> Tensor");
@@ -1076,6 +1183,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("layer_norm", &layer_norm);
   m.impl("layer_norm_bwd", &layer_norm_bwd);
   m.impl("layer_norm_bwd_colsum", &layer_norm_bwd_colsum);
+  m.impl("layer_norm_bwd_drop", &layer_norm_bwd_drop);
   m.impl("gelu", &gelu);
   m.impl("title_attention_bwd", &title_attention_bwd);
   m.impl("embed_ln", &embed_ln);
@@ -1104,8 +1212,11 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("small_gemm", &small_gemm);
   m.impl("colsum_f32", &colsum_f32);
   m.impl("multi_copy", &multi_copy);
+  m.impl("multi_cast", &multi_cast);
   m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
   m.impl("title_attention_drop", &title_attention_drop);
+  m.impl("title_attention_drop_bits", &title_attention_drop_bits);
+  m.impl("title_attention_bwd_drop_bits", &title_attention_bwd_drop_bits);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);
   m.impl("wgrad", &wgrad);
   m.impl("gather_dropout", &gather_dropout);

@@ -317,7 +317,12 @@ bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* po
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                      const bf16* __restrict__ dy, bf16* __restrict__ dx,
                                                      float* __restrict__ dw, float* __restrict__ db, int rows, int D,
-                                                     float eps, float* __restrict__ dxs) {
+                                                     float eps, float* __restrict__ dxs, bf16* __restrict__ dxz,
+                                                     float pdrop, float inv_keep, unsigned long long seed,
+                                                     unsigned long long offset) {
+  // dxz (optional, with dxs): dx o Z, the dropout backward of the layer that fed the LN input
+  // (HF FFN.dropout, dropout.hip's element-indexed mask), written beside dx; dxs then sums
+  // dx o Z -- the lin2 bias gradient -- instead of dx
   // dxs (optional): column sums of the bf16 dx it writes -- the bias gradient of the linear
   // layer that produced the LN input (config 5 training blocks), without a separate pass
   __shared__ float red[3][4][256 * MAXC];
@@ -384,11 +389,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x,
       if (c < nc && i < D) {
         bf16x4 o;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          o[k] = f2bf(rstd * (g[c][k] - mg - v[c][k] * mgx));
-          px[c][k] += (float)o[k];
-        }
+        for (int k = 0; k < 4; ++k) o[k] = f2bf(rstd * (g[c][k] - mg - v[c][k] * mgx));
         *(bf16x4*)(dx + (size_t)row * D + i) = o;
+        if (dxz != nullptr) {
+          // element e = row * D + i + k: Philox counter e >> 2, component k (i % 4 == 0);
+          // rounded as dropout_add_kernel's own backward (bf16(dx) * Z, one rounding)
+          const uint4 r = Philox::gen(seed, offset, ((unsigned long long)row * D + i) >> 2);
+          bf16x4 oz;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            oz[k] = f2bf(__fmul_rn(bf2f(o[k]), drop_scale(u4_get(r, k), pdrop, inv_keep)));
+            px[c][k] += (float)oz[k];
+          }
+          *(bf16x4*)(dxz + (size_t)row * D + i) = oz;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) px[c][k] += (float)o[k];
+        }
       }
     }
   }
@@ -451,13 +468,15 @@ __global__ __launch_bounds__(256) void gelu_kernel(const bf16* __restrict__ z, c
 extern "C" void fr_ln_set_wide(int v) { g_ln_wide = v; }
 
 extern "C" int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void* dy, void* dx, float* dw, float* db,
-                                      int rows, int D, float eps, hipStream_t s, float* dxs) {
+                                      int rows, int D, float eps, hipStream_t s, float* dxs, void* dxz, float pdrop,
+                                      unsigned long long seed, unsigned long long offset) {
   if (D % 4 != 0 || D > 256 * MAXC) return 1;
+  if (dxz != nullptr && (dxs == nullptr || !(pdrop > 0.f && pdrop < 1.f))) return 2;
   if (rows == 0) return 0;
   int blocks = (rows + 3) / 4;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy, (bf16*)dx, dw, db,
-                     rows, D, eps, dxs);
+                     rows, D, eps, dxs, (bf16*)dxz, pdrop, dxz ? 1.0f / (1.0f - pdrop) : 1.f, seed, offset);
   return 0;
 }
 

@@ -217,7 +217,8 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   }
 }
 
-// split-K epilogue: C = alpha * sum_s P[s] (+ C), partials summed in split order (deterministic)
+// split-K epilogue: C = alpha * sum_s P[s] (x the output dropout scale, drop_on 3) (+ C),
+// partials summed in split order (deterministic)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batch, int total) {
   for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
     int gi = 0, base = 0;
@@ -232,7 +233,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batc
     float s = 0.f;
     for (int sp = 0; sp < g.splits; ++sp) s += g.P[(size_t)sp * g.M * g.N + idx];
     float* c = g.C + (size_t)m * g.ldc + n;
-    const float v = g.alpha * s;
+    float v = g.alpha * s;
+    if (g.drop_on == 3) {  // as the single-pass epilogue: element (m, n) of the dropped input
+      const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+      const unsigned long long el = (unsigned long long)m * g.drop_ld + n;
+      const uint4 x = Philox::gen(g.seed, off, el >> 2);
+      v *= drop_scale(u4_get(x, (int)(el & 3)), g.pdrop, 1.0f / (1.0f - g.pdrop));
+    }
     *c = g.accumulate ? *c + v : v;
   }
 }
@@ -299,7 +306,23 @@ __global__ __launch_bounds__(64) void colsum_final_kernel(const ColsumBatch batc
 // when scratch is null (query mode).
 static int choose_splits(int M, int N, int K) {
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-  if (K < 512 || tiles >= 192) return 1;
+  if (K < 512) return 1;
+  if (tiles >= 192) {
+    // more than ~3/4 of a wave of tiles: split only when it fixes the wave quantisation by a
+    // margin that pays for the reduce pass (the user dgrad: 350 tiles x K = 1200 = 1.37 waves
+    // of 19-step tiles -> 2 splits = 700 half-length tiles, 3 rounds of 1/2 instead of 2 of 1)
+    const int rounds1 = (tiles + 255) / 256;
+    int best = 1;
+    float bestc = (float)rounds1;
+    for (int sp = 2; sp <= 4 && sp <= K / 256; ++sp) {
+      const float c = (float)((tiles * sp + 255) / 256) / sp;
+      if (c * 1.15f < bestc) {
+        best = sp;
+        bestc = c * 1.15f;
+      }
+    }
+    return best;
+  }
   int s = (256 + tiles - 1) / tiles;  // about one wave of workgroups over the 256 CUs
   s = min(s, K / 256);
   return max(1, min(s, 16));
@@ -339,8 +362,8 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
                       (d.drop_on == 2 && d.b_mode != 1)))
       return -3;
     if (d.gather_on && (!d.gidx || (d.gather_on == 1 && d.a_mode != 0) || (d.gather_on == 2 && d.b_mode != 1))) return -4;
-    // split-K only for plain epilogues (no bias / act / output dropout): the reduce applies alpha + accumulate
-    d.splits = (d.bias == nullptr && d.act == 0 && d.drop_on != 3) ? choose_splits(d.M, d.N, d.K) : 1;
+    // split-K only for epilogues the reduce can apply: alpha, output dropout, accumulate (no bias / act)
+    d.splits = (d.bias == nullptr && d.act == 0) ? choose_splits(d.M, d.N, d.K) : 1;
     d.kchunk = d.splits > 1 ? ((d.K + d.splits - 1) / d.splits + TK - 1) / TK * TK : d.K;
     if (d.splits > 1) d.splits = (d.K + d.kchunk - 1) / d.kchunk;
     d.P = nullptr;

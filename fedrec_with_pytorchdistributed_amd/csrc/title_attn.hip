@@ -224,9 +224,17 @@ __device__ __forceinline__ void ta_load_v(TAIn& in, const bf16* __restrict__ qkv
   }
 }
 
-template <int OCC, int DEPTH>
+// DROP: the train-mode forward (attention-probability dropout, the same Philox element index as
+// title_attn_kernel<.., true>, so title_attn_bwd.hip regenerates the identical mask)
+template <int OCC, int DEPTH, bool DROP = false>
 __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __restrict__ qkv, const int* __restrict__ mask,
-                                                          bf16* __restrict__ out, int n_pairs, int T, int H, int D) {
+                                                          bf16* __restrict__ out, int n_pairs, int T, int H, int D,
+                                                          float pdrop = 0.f, unsigned long long seed = 0ull,
+                                                          unsigned long long offset = 0ull,
+                                                          unsigned long long* __restrict__ zout = nullptr) {
+  // zout (DROP, optional): the keep bits of each pair, [n_pairs][64 lanes] x 64 bits (lane's
+  // query t = 16 jq + fr, key s = 16 is + 4 fq + r at bit 16 jq + 4 is + r) -- the backward
+  // reads 8 bytes per lane instead of regenerating 16 Philox blocks
   __shared__ __attribute__((aligned(16))) bf16 vs[4][64 * DH];
   // wave index via readfirstlane: the compiler then knows pair / next are wave-uniform, so the
   // prefetch guards are scalar branches (a "divergent" guard around loads makes it drain
@@ -268,6 +276,7 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
 
     const float scale = 0.125f;
     bf16x8 pf[4][2];
+    unsigned long long zbits = 0ull;
 #pragma unroll
     for (int jq = 0; jq < 4; ++jq) {
       float m = -INFINITY;
@@ -292,6 +301,20 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
           l += e;
         }
       const float inv = 1.0f / group4_sum(l);
+      if constexpr (DROP) {
+        const float inv_keep = 1.0f / (1.0f - pdrop);
+        const int t = jq * 16 + fr;
+#pragma unroll
+        for (int is = 0; is < 4; ++is) {
+          const uint4 rnd = Philox::gen(seed, offset, ((unsigned long long)pair * 64 + t) * 16 + is * 4 + fq);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bool kp = u32_to_unit(u4_get(rnd, r)) > pdrop;  // = drop_scale's test
+            st[is][jq][r] *= kp ? inv_keep : 0.f;
+            zbits |= (kp ? 1ull : 0ull) << (jq * 16 + is * 4 + r);
+          }
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 f;
@@ -302,6 +325,9 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
         }
         pf[jq][ks] = f;
       }
+    }
+    if constexpr (DROP) {
+      if (zout != nullptr) zout[(size_t)pair * 64 + lane] = zbits;
     }
     if (next < n_pairs) ta_load_v(in, qkv, next, T, H, D, lane);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V image is in LDS
@@ -683,13 +709,27 @@ extern "C" int fr_title_attention_bf16(const void* qkv, const int* mask, void* o
   return 0;
 }
 
-// train-mode forward with attention-probability dropout (T <= 64; 2 = unsupported shape)
+// train-mode forward with attention-probability dropout (T <= 64; 2 = unsupported shape);
+// zbits (optional, [n_titles * H * 64] u64): keep bits for title_attention_bwd_drop_bits
 extern "C" int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H,
                                             int D, float pdrop, unsigned long long seed, unsigned long long offset,
-                                            hipStream_t s) {
+                                            hipStream_t s, void* zbits) {
   if (T < 1 || T > 64 || D != H * DH || !(pdrop > 0.f && pdrop < 1.f)) return 2;
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
+  if (g_ta_waves == -2 || zbits != nullptr) {  // persistent 2-deep prefetching form (default), as the eval forward
+    if (g_ta_cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_ta_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_ta_cus <= 0) g_ta_cus = 256;
+    }
+    const int need = (pairs + 3) / 4;
+    const int blocks = g_ta_cus < need ? g_ta_cus : need;
+    hipLaunchKernelGGL((title_attn_pkernel<1, 2, true>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, mask,
+                       (bf16*)out, pairs, T, H, D, pdrop, seed, offset, (unsigned long long*)zbits);
+    return 0;
+  }
   hipLaunchKernelGGL((title_attn_kernel<2, true>), dim3((pairs + 1) / 2), dim3(128), 0, s, (const bf16*)qkv, mask,
                      (bf16*)out, n_titles, T, H, D, pdrop, seed, offset);
   return 0;

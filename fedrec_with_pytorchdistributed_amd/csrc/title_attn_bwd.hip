@@ -266,13 +266,15 @@ __global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __
 struct TBIn {
   bf16x8 q[8], k[8], v[8], g[8];
   int mk;  // lane s: mask of key s (clamped row; s >= T is handled by the caller)
+  unsigned long long zb;  // the forward's dropout keep bits of this lane (zin given)
 };
 
 // element index of (row r, column c) in a swizzled [64][64] bf16 tile
 __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((((c >> 3) ^ (r & 7)) << 3) | (c & 7)); }
 
 __device__ __forceinline__ void tb_load(TBIn& in, const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                        const int* __restrict__ mask, int pair, int T, int H, int D, int lane) {
+                                        const int* __restrict__ mask, int pair, int T, int H, int D, int lane,
+                                        const unsigned long long* __restrict__ zin = nullptr) {
   const int title = pair / H, h = pair - title * H;
   const size_t row0 = (size_t)title * T;
   const int ld = 3 * D;
@@ -290,13 +292,21 @@ __device__ __forceinline__ void tb_load(TBIn& in, const bf16* __restrict__ qkv, 
     in.g[c] = *(const bf16x8*)(gb + (size_t)r * D + ch * 8);
   }
   in.mk = mask[row0 + (lane < T ? lane : T - 1)];
+  if (zin != nullptr) in.zb = zin[(size_t)pair * 64 + lane];
 }
 
+// DM 0: no dropout; 1: as title_attn_bwd_kernel<true> (the forward's Philox mask regenerated
+// per element); 2: the forward's stored keep bits (zin).  Compile-time: a kernel carrying both
+// dropout forms spills (688 B/lane vs 116).
+template <int DM>
 __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const int* __restrict__ mask,
                                                                  bf16* __restrict__ dqkv, int n_pairs, int T, int H,
-                                                                 int D) {
+                                                                 int D, float pdrop, unsigned long long seed,
+                                                                 unsigned long long offset,
+                                                                 const unsigned long long* __restrict__ zin) {
+  constexpr bool DROP = DM != 0;
   __shared__ __attribute__((aligned(16))) bf16 lds[4][4][64 * DH];  // per wave: Q, K, V (then P^T/dS^T), dO
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int stride = gridDim.x * 4;
@@ -311,7 +321,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
   const int qq = fr >> 2, pp = fr & 3;
   const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
   TBIn in;
-  tb_load(in, qkv, dout, mask, pair, T, H, D, lane);
+  tb_load(in, qkv, dout, mask, pair, T, H, D, lane, DM == 2 ? zin : nullptr);
   while (true) {
     // ---- stage the current pair (rows >= T zero) and its mask; then prefetch the next ----
 #pragma unroll
@@ -331,6 +341,25 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
     const int next = min(pair + stride, n_pairs - 1);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the staged tiles are in LDS
     __builtin_amdgcn_wave_barrier();
+    // dropout keep bits (DROP): query t = 16 jq + fr, key s = 16 is + 4 fq + r -> bit 4 is + r of
+    // zbits[jq]; the same Philox elements as the forward.  Generated here, while the LDS writes
+    // drain, and kept as 4 words (per-element scale arrays across the softmax spill)
+    unsigned zbits[4] = {0u, 0u, 0u, 0u};
+    const float inv_keep = DROP ? 1.0f / (1.0f - pdrop) : 1.f;
+    if constexpr (DM == 2) {
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq) zbits[jq] = (unsigned)(in.zb >> (jq * 16)) & 0xFFFFu;
+    } else if constexpr (DROP) {
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq)
+#pragma unroll
+        for (int is = 0; is < 4; ++is) {
+          const uint4 rnd = Philox::gen(seed, offset, ((unsigned long long)pair * 64 + jq * 16 + fr) * 16 + is * 4 + fq);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            zbits[jq] |= (u32_to_unit(u4_get(rnd, r)) > pdrop ? 1u : 0u) << (is * 4 + r);
+        }
+    }
     // ---- S^T = K Q^T and dP^T = V dO^T from LDS fragments ----
     f32x4 st[4][4], dp[4][4];
 #pragma unroll
@@ -391,19 +420,24 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
         }
       l = group4_sum(l);
       const float inv = 1.0f / l;
+      const unsigned zb = zbits[jq];
       float dsum = 0.f;
 #pragma unroll
       for (int is = 0; is < 4; ++is)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           st[is][jq][r] *= inv;
+          if constexpr (DROP) dp[is][jq][r] *= ((zb >> (is * 4 + r)) & 1u) ? inv_keep : 0.f;
           dsum += st[is][jq][r] * dp[is][jq][r];
         }
       dsum = group4_sum(dsum);
 #pragma unroll
       for (int is = 0; is < 4; ++is)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dp[is][jq][r] = keep[is][r] * st[is][jq][r] * (dp[is][jq][r] - dsum) * 0.125f;
+        for (int r = 0; r < 4; ++r) {
+          dp[is][jq][r] = keep[is][r] * st[is][jq][r] * (dp[is][jq][r] - dsum) * 0.125f;
+          if constexpr (DROP) st[is][jq][r] *= ((zb >> (is * 4 + r)) & 1u) ? inv_keep : 0.f;  // P~ for dV
+        }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 f, g;
@@ -420,7 +454,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
     }
     // the fp32 S / dP are dead: prefetch the next pair into the staging registers now (its
     // loads land during dQ, dV and dK of this pair)
-    tb_load(in, qkv, dout, mask, next, T, H, D, lane);
+    tb_load(in, qkv, dout, mask, next, T, H, D, lane, DM == 2 ? zin : nullptr);
     // ---- dQ = dS K (B = K via transposed reads of the swizzled tile) ----
     f32x4 o[4][4];
 #pragma unroll
@@ -501,6 +535,16 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
 int g_tab_variant = 1;  // 1: persistent prefetching (default), 0: one-shot
 int g_tab_cus = 0;
 
+int tab_cus() {
+  if (g_tab_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_tab_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_tab_cus <= 0) g_tab_cus = 256;
+  }
+  return g_tab_cus;
+}
+
 }  // namespace
 
 extern "C" void fr_title_attn_bwd_set_variant(int v) { g_tab_variant = v; }
@@ -515,17 +559,11 @@ extern "C" int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, co
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
   if (g_tab_variant == 1) {
-    if (g_tab_cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&g_tab_cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (g_tab_cus <= 0) g_tab_cus = 256;
-    }
-    int blocks = g_tab_cus;
+    int blocks = tab_cus();
     const int need = (pairs + 3) / 4;
     blocks = blocks < need ? blocks : need;
-    hipLaunchKernelGGL(title_attn_bwd_pkernel, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
-                       mask, (bf16*)dqkv, pairs, T, H, D);
+    hipLaunchKernelGGL(title_attn_bwd_pkernel<0>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
+                       mask, (bf16*)dqkv, pairs, T, H, D, 0.f, 0ull, 0ull, nullptr);
     return 0;
   }
   hipLaunchKernelGGL((title_attn_bwd_kernel<false>), dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s,
@@ -539,7 +577,28 @@ extern "C" int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dou
   if (T < 1 || T > 64 || D != H * DH || !(pdrop > 0.f && pdrop < 1.f)) return 2;
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
+  if (g_tab_variant == 1) {
+    const int need = (pairs + 3) / 4;
+    const int blocks = tab_cus() < need ? tab_cus() : need;
+    hipLaunchKernelGGL(title_attn_bwd_pkernel<1>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
+                       mask, (bf16*)dqkv, pairs, T, H, D, pdrop, seed, offset, nullptr);
+    return 0;
+  }
   hipLaunchKernelGGL((title_attn_bwd_kernel<true>), dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s,
                      (const bf16*)qkv, (const bf16*)dout, mask, (bf16*)dqkv, n_titles, T, H, D, pdrop, seed, offset);
+  return 0;
+}
+
+// backward from the forward's stored keep bits ([n_titles * H * 64] u64, title_attn.hip zbits)
+extern "C" int fr_title_attention_bwd_drop_bits_bf16(const void* qkv, const void* dout, const int* mask,
+                                                     const void* zbits, void* dqkv, int n_titles, int T, int H, int D,
+                                                     float pdrop, hipStream_t s) {
+  if (T < 1 || T > 64 || D != H * DH || !(pdrop > 0.f && pdrop < 1.f) || zbits == nullptr) return 2;
+  const int pairs = n_titles * H;
+  if (pairs == 0) return 0;
+  const int need = (pairs + 3) / 4;
+  const int blocks = tab_cus() < need ? tab_cus() : need;
+  hipLaunchKernelGGL(title_attn_bwd_pkernel<2>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout, mask,
+                     (bf16*)dqkv, pairs, T, H, D, pdrop, 0ull, 0ull, (const unsigned long long*)zbits);
   return 0;
 }

@@ -181,6 +181,185 @@ __global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------------------
+// ILP forms (default).  The kernels above are latency-bound, not FLOP-bound: ~1.25 waves per
+// SIMD, and every key costs a 20-deep chain of dependent FMAs (dot20) before its exp -- the
+// forward ran 35 us for 1,280 (impression, head) pairs of 50 x 50 x 20.  Here the key loops
+// are fully unrolled over MAXH with a wave-uniform guard (so independent keys interleave),
+// the dot products split into 4 partial sums (chains of 5), and the forward keeps its scores
+// in registers (one dot product per key instead of two).  Same math and outputs (fp32; only
+// the summation order inside a 20-term dot product differs).
+__device__ __forceinline__ void load_row_s(float (&x)[DK], const float* __restrict__ p, float sc) {
+#pragma unroll
+  for (int c4 = 0; c4 < DK / 4; ++c4) {
+    const float4 v = *(const float4*)(p + 4 * c4);
+    x[4 * c4] = v.x * sc;
+    x[4 * c4 + 1] = v.y * sc;
+    x[4 * c4 + 2] = v.z * sc;
+    x[4 * c4 + 3] = v.w * sc;
+  }
+}
+
+__device__ __forceinline__ float dot20x(const float (&q)[DK], const float* __restrict__ row) {
+  float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c4 = 0; c4 < DK / 4; ++c4) {
+    const float4 k = *(const float4*)(row + 4 * c4);
+    d[0] += q[4 * c4] * k.x;
+    d[1] += q[4 * c4 + 1] * k.y;
+    d[2] += q[4 * c4 + 2] * k.z;
+    d[3] += q[4 * c4 + 3] * k.w;
+  }
+  return (d[0] + d[1]) + (d[2] + d[3]);
+}
+
+__global__ __launch_bounds__(128) void user_attn_fwd_ilp_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
+                                                                float* __restrict__ stats, int B, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float ks[2][MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float vs[2][MAXH][DK];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pair = blockIdx.x * 2 + wave;
+  const bool active = pair < B * NH;
+  const int b = active ? pair / NH : 0, h = active ? pair - b * NH : 0;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  for (int i = lane; i < H * DK / 4; i += 64) {
+    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+    *(float4*)&ks[wave][r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
+    *(float4*)&vs[wave][r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
+  }
+  const int t = lane < H ? lane : H - 1;  // clamped: every lane runs the same unrolled code
+  float q[DK];
+  load_row_s(q, base + (size_t)t * ld, rsqrtf((float)DK));
+  __syncthreads();
+  if (!active) return;
+  float sc[MAXH];
+  float m = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < MAXH; ++s)
+    if (s < H) {
+      sc[s] = dot20x(q, &ks[wave][s][0]);
+      m = fmaxf(m, sc[s]);
+    }
+  float acc[DK];
+#pragma unroll
+  for (int c = 0; c < DK; ++c) acc[c] = 0.f;
+  float l = 0.f;
+#pragma unroll
+  for (int s = 0; s < MAXH; ++s)
+    if (s < H) {
+      const float p = __expf(sc[s] - m);
+      l += p;
+      axpy20(acc, p, &vs[wave][s][0]);
+    }
+  if (lane >= H) return;
+  l += 1e-8f * __expf(-m);
+  const float inv = 1.0f / l;
+  float* o = ctx + ((size_t)b * H + lane) * D + h * DK;
+#pragma unroll
+  for (int c4 = 0; c4 < DK / 4; ++c4)
+    *(float4*)(o + 4 * c4) = make_float4(acc[4 * c4] * inv, acc[4 * c4 + 1] * inv, acc[4 * c4 + 2] * inv,
+                                         acc[4 * c4 + 3] * inv);
+  float* st = stats + (((size_t)b * NH + h) * H + lane) * 2;
+  st[0] = m;
+  st[1] = inv;
+}
+
+__global__ __launch_bounds__(64) void user_attn_bwd_ilp_kernel(const float* __restrict__ qkv,
+                                                               const float* __restrict__ stats,
+                                                               const float* __restrict__ dctx, float* __restrict__ dqkv,
+                                                               int B, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float qs[MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float ks[MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float vs[MAXH][DK];
+  __shared__ __attribute__((aligned(16))) float gs[MAXH][DK];
+  __shared__ float ms[MAXH], is_[MAXH], Ds[MAXH];
+  const int lane = threadIdx.x;
+  const int pair = blockIdx.x;
+  const int b = pair / NH, h = pair - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  const float* gb = dctx + (size_t)b * H * D + h * DK;
+  for (int i = lane; i < H * DK / 4; i += 64) {
+    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+    *(float4*)&qs[r][c] = *(const float4*)(base + (size_t)r * ld + c);
+    *(float4*)&ks[r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
+    *(float4*)&vs[r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
+    *(float4*)&gs[r][c] = *(const float4*)(gb + (size_t)r * D + c);
+  }
+  const float* st = stats + ((size_t)b * NH + h) * H * 2;
+  for (int t = lane; t < H; t += 64) {
+    ms[t] = st[2 * t];
+    is_[t] = st[2 * t + 1];
+  }
+  __syncthreads();
+  const float scale = rsqrtf((float)DK);
+  float* dbase = dqkv + (size_t)b * H * ld + h * DK;
+  const int r = lane < H ? lane : H - 1;  // clamped row: uniform unrolled code, guarded stores
+  {
+    // lane = query t: D_t = sum_s A_ts dA_ts, u = sum_s A dA k_s, w = sum_s A k_s
+    const float m = ms[r], inv = is_[r];
+    float q[DK], g[DK], u[DK], w[DK];
+#pragma unroll
+    for (int c = 0; c < DK; ++c) {
+      q[c] = qs[r][c] * scale;
+      g[c] = gs[r][c];
+      u[c] = w[c] = 0.f;
+    }
+    float Dt = 0.f;
+#pragma unroll
+    for (int s = 0; s < MAXH; ++s)
+      if (s < H) {
+        const float A = __expf(dot20x(q, &ks[s][0]) - m) * inv;
+        const float dA = dot20x(g, &vs[s][0]);
+        Dt += A * dA;
+        axpy20(u, A * dA, &ks[s][0]);
+        axpy20(w, A, &ks[s][0]);
+      }
+    if (lane < H) {
+      Ds[lane] = Dt;
+      float* o = dbase + (size_t)lane * ld;
+#pragma unroll
+      for (int c4 = 0; c4 < DK / 4; ++c4) {
+        const int c = 4 * c4;
+        *(float4*)(o + c) = make_float4(scale * (u[c] - Dt * w[c]), scale * (u[c + 1] - Dt * w[c + 1]),
+                                        scale * (u[c + 2] - Dt * w[c + 2]), scale * (u[c + 3] - Dt * w[c + 3]));
+      }
+    }
+  }
+  __syncthreads();
+  {
+    // lane = key s: dk_s = sum_t dS_ts q_t, dv_s = sum_t A_ts g_t
+    float k[DK], v[DK], dk[DK], dv[DK];
+#pragma unroll
+    for (int c = 0; c < DK; ++c) {
+      k[c] = ks[r][c] * scale;
+      v[c] = vs[r][c];
+      dk[c] = dv[c] = 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < MAXH; ++t)
+      if (t < H) {
+        const float A = __expf(dot20x(k, &qs[t][0]) - ms[t]) * is_[t];
+        const float dA = dot20x(v, &gs[t][0]);
+        const float dS = A * (dA - Ds[t]) * scale;
+        axpy20(dk, dS, &qs[t][0]);
+        axpy20(dv, A, &gs[t][0]);
+      }
+    if (lane < H) {
+      float* o = dbase + (size_t)lane * ld;
+#pragma unroll
+      for (int c4 = 0; c4 < DK / 4; ++c4) {
+        const int c = 4 * c4;
+        *(float4*)(o + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
+        *(float4*)(o + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
+      }
+    }
+  }
+}
+
+int g_ua_variant = 1;  // 1: ILP forms (default), 0: the first forms
+
+// ---------------------------------------------------------------------------------------
 // Long histories (H > 64): the reference pads but never truncates (dataset.py:84, quirk Q6;
 // its shipped shard has H = 76), and SURVEY §5.7 asks for H limited only by memory.  Same
 // math, one wave per (impression, head), query rows in chunks of 64 (lane = row), keys /
@@ -354,6 +533,8 @@ __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __r
 
 }  // namespace
 
+extern "C" void fr_user_attn_set_variant(int v) { g_ua_variant = v; }
+
 extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk,
                                 hipStream_t s) {
   if (dk != DK || H > MAXL || H < 1) return 1;
@@ -361,6 +542,8 @@ extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int 
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH);
+  else if (g_ua_variant == 1)
+    hipLaunchKernelGGL(user_attn_fwd_ilp_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
   else
     hipLaunchKernelGGL(user_attn_fwd_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
   return 0;
@@ -373,6 +556,8 @@ extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const floa
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
+  else if (g_ua_variant == 1)
+    hipLaunchKernelGGL(user_attn_bwd_ilp_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   else
     hipLaunchKernelGGL(user_attn_bwd_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   return 0;

@@ -81,6 +81,7 @@ class Backbone(nn.Module):
         self.transformer = _Transformer(c)
         self._pack: Optional[Dict] = None
         self._pack_key = None
+        self._stale = True
         self.version = 0  # bumped whenever the weights may have changed (hidden-state caches key on it)
         # train-mode dropout: Philox key (the engine sets seed + rank) and a per-forward counter;
         # a forward's sites use offsets 1024 * call + {0: embeddings, 1 + 2l: attention of
@@ -107,8 +108,12 @@ class Backbone(nn.Module):
         self.invalidate()
 
     def invalidate(self) -> None:
-        self._pack = None
+        self._stale = True
         self.version += 1
+
+    @property
+    def pack_stale(self) -> bool:
+        return self._pack is None or self._stale
 
     def _load_from_state_dict(self, *args, **kwargs):  # keep the compute pack coherent
         self.invalidate()
@@ -119,7 +124,14 @@ class Backbone(nn.Module):
         dev = self.embeddings.word_embeddings.weight.device
         key = (dtype, dev)
         if self._pack is not None and self._pack_key == key:
-            return self._pack
+            if not self._stale:
+                return self._pack
+            # an optimizer step (or a load) changed the masters: refresh the existing compute
+            # copies in place, all of them in one launch (csrc/adam.hip multi_cast) instead of
+            # a cat + cast launch per weight
+            if dev.type == "cuda" and ops.native.lib().multi_cast(*self._cast_plan):
+                self._stale = False
+                return self._pack
         e = self.embeddings
         pack: Dict = {
             "word": e.word_embeddings.weight.detach().to(dtype).contiguous(),
@@ -144,7 +156,18 @@ class Backbone(nn.Module):
                 "ln2_w": blk.output_layer_norm.weight.detach().float().contiguous(),
                 "ln2_b": blk.output_layer_norm.bias.detach().float().contiguous(),
             })
-        self._pack, self._pack_key = pack, key
+        # in-place refresh plan: every master whose compute copy is not the master itself
+        src, dst = [e.word_embeddings.weight, e.position_embeddings.weight], [pack["word"], pack["pos"]]
+        for blk, L in zip(self.transformer.layer, pack["layers"]):
+            a = blk.attention
+            D = a.q_lin.weight.shape[0]
+            for i, lin in enumerate((a.q_lin, a.k_lin, a.v_lin)):
+                src += [lin.weight, lin.bias]
+                dst += [L["wqkv"][i * D:(i + 1) * D], L["bqkv"][i * D:(i + 1) * D]]
+            src += [a.out_lin.weight, blk.ffn.lin1.weight, blk.ffn.lin2.weight]
+            dst += [L["wo"], L["w1"], L["w2"]]
+        self._cast_plan = ([t.detach() for t in src], dst)
+        self._pack, self._pack_key, self._stale = pack, key, False
         return pack
 
     # -------------------------------------------------------------------------------
@@ -312,20 +335,21 @@ class Backbone(nn.Module):
             raise ValueError("FEDREC_TRAIN_BLOCKS=0 (per-op A/B path) has no dropout; use the block path")
         for blk, L, (sa, sf) in zip(self.transformer.layer, P["layers"], sites):
             a = blk.attention
-            wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
-            bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
             if blocks:  # fused block Functions (default)
                 # box: each LN backward hands its dx column sums (the bias grad of the block
                 # half feeding it) to that block's backward, which runs next
                 fuse = os.environ.get("FEDREC_LN_COLSUM", "1") != "0"
                 box1, box2 = ({}, {}) if fuse else (None, None)
-                h = OF.AttnBlockFn.apply(x, wqkv, bqkv, a.out_lin.weight, a.out_lin.bias, mask.contiguous(),
-                                         c.n_heads, L["wqkv"], L["wo"], box1, sa)
+                h = OF.AttnBlockFn.apply(x, a.q_lin.weight, a.k_lin.weight, a.v_lin.weight, a.q_lin.bias,
+                                         a.k_lin.bias, a.v_lin.bias, a.out_lin.weight, a.out_lin.bias,
+                                         mask.contiguous(), c.n_heads, L["wqkv"], L["bqkv"], L["wo"], box1, sa)
                 x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps, box1)
                 h = OF.MLPBlockFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, blk.ffn.lin2.weight,
                                         blk.ffn.lin2.bias, L["w1"], L["w2"], box2, sf)
                 x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps, box2)
                 continue
+            wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
+            bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
             qkv = OF.LinearTFn.apply(x, wqkv, bqkv, None, L["wqkv"])
             ctx = OF.TitleAttentionFn.apply(qkv, mask.contiguous(), c.n_heads)
             h = OF.LinearTFn.apply(ctx, a.out_lin.weight, a.out_lin.bias, x, L["wo"])

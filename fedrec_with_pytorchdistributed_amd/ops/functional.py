@@ -286,6 +286,9 @@ class DropoutFn(torch.autograd.Function):
         return ops.dropout_add(g.contiguous(), None, *ctx.drop), None, None, None
 
 
+_ATTN_BITS = __import__("os").environ.get("FEDREC_ATTN_BITS", "1") != "0"  # A/B switch
+
+
 class AttnBlockFn(torch.autograd.Function):
     """``h = out_proj(attention(x Wqkv^T + bqkv)) + x`` (one post-LN block's attention half,
     unfrozen backbone).  One Function so the residual gradient joins the QKV input gradient
@@ -295,11 +298,22 @@ class AttnBlockFn(torch.autograd.Function):
     DistilBERT has no dropout after ``out_lin``)."""
 
     @staticmethod
-    def forward(ctx, x, wqkv, bqkv, wo, bo, mask, heads: int, wqkv_low, wo_low, box=None, drop=None):
+    def forward(ctx, x, wq, wk, wv, bq, bk, bv, wo, bo, mask, heads: int, wqkv_low, bqkv, wo_low, box=None,
+                drop=None):
+        # wq .. bv: the fp32 masters (autograd inputs: their gradients are slices of dwqkv /
+        # dbqkv, so no per-step fp32 cat of the three weights); the GEMM runs on the fused bf16
+        # compute copy wqkv_low and the fused fp32 bias bqkv of the backbone's pack
         qkv = ops.linear(x, wqkv_low, bqkv)
-        c = ops.title_attention(qkv, mask, heads, drop)
+        bits = None
+        if drop is not None and _ATTN_BITS and qkv.is_cuda and mask.shape[1] <= 64:
+            # the keep bits leave the forward (8 B per lane and (title, head)): the backward
+            # reads them instead of regenerating 16 Philox blocks per lane
+            c, bits = ops.native.require_for(qkv).title_attention_drop_bits(qkv, mask, heads, float(drop[0]),
+                                                                            int(drop[1]), int(drop[2]))
+        else:
+            c = ops.title_attention(qkv, mask, heads, drop)
         h = ops.linear(c, wo_low, bo, residual=x)
-        ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low, wo)
+        ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low, wo, bits)
         ctx.heads = heads
         ctx.box = box
         ctx.drop = drop
@@ -307,12 +321,16 @@ class AttnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh):
-        x, qkv, c, mask, wqkv_low, wo_low, wo = ctx.saved_tensors
+        x, qkv, c, mask, wqkv_low, wo_low, wo, bits = ctx.saved_tensors
         dh = dh.contiguous()
         dbo = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN1's backward
         dwo, dbo = wgrad(dh, c), (dbo if dbo is not None else bgrad(dh))
         dc = dgrad(dh, wo_low)
-        dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
+        if bits is not None:
+            dqkv = ops.native.require_for(qkv).title_attention_bwd_drop_bits(qkv, dc, mask, bits, ctx.heads,
+                                                                            float(ctx.drop[0]))
+        else:
+            dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
         dwqkv = wgrad(dqkv, x)
         if _QKV_BIAS_SHORTCUT and dqkv.is_cuda and ctx.drop is None:
             # column sums of dQ | dK | dV without reading dK and dV: every softmax row sums to
@@ -323,10 +341,21 @@ class AttnBlockFn(torch.autograd.Function):
             dbqkv = torch.cat([ops.native.require_for(dqkv).colsum(dqkv[:, :Dm]),
                                torch.zeros(Dm, device=dqkv.device, dtype=torch.float32),
                                (dbo.float().unsqueeze(0) @ wo.float()).squeeze(0)])
+        elif _QKV_BIAS_SHORTCUT and dqkv.is_cuda:
+            # with attention dropout the key-bias gradient is still exactly zero (the dropout
+            # acts after the softmax: sum_s dS_ts = D_t - D_t sum_s P_ts = 0), but the dropped
+            # P~ rows no longer sum to one, so dV needs its own column sums
+            Dm = wo.shape[0]
+            lib = ops.native.require_for(dqkv)
+            dbqkv = torch.cat([lib.colsum(dqkv[:, :Dm]), torch.zeros(Dm, device=dqkv.device, dtype=torch.float32),
+                               lib.colsum(dqkv[:, 2 * Dm:])])
         else:
             dbqkv = bgrad(dqkv)
         dx = dgrad(dqkv, wqkv_low, residual=dh)  # residual + QKV dgrad in one GEMM (beta = 1)
-        return dx, dwqkv, dbqkv, dwo, dbo, None, None, None, None, None, None
+        Dm = dwqkv.shape[0] // 3
+        dw = [dwqkv[i * Dm:(i + 1) * Dm] for i in range(3)]
+        db = [dbqkv[i * Dm:(i + 1) * Dm] for i in range(3)]
+        return (dx, *dw, *db, dwo, dbo) + (None,) * 7
 
 
 class MLPBlockFn(torch.autograd.Function):
@@ -339,6 +368,8 @@ class MLPBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low, box=None, drop=None):
         lib = ops.native.require_for(x)
+        if box is not None and drop is not None:
+            box["drop"] = drop  # LN2's backward applies this dropout's backward in its own pass
         f, z = lib.linear_gelu_dual(x.contiguous(), w1_low, b1)
         if drop is None:
             h = ops.linear(f, w2_low, b2, residual=x)
@@ -355,7 +386,10 @@ class MLPBlockFn(torch.autograd.Function):
         lib = ops.native.require_for(x)
         dres = dh.contiguous()  # the residual branch's gradient
         db2 = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN2's backward
-        if ctx.drop is not None:  # the lin2 branch sees dh o Z; LN2's column sums are of dh itself
+        dz2 = ctx.box.pop("dxz", None) if ctx.box is not None else None
+        if ctx.drop is not None and dz2 is not None:
+            dh = dz2  # dh o Z and its column sums (db2) came out of LN2's backward pass
+        elif ctx.drop is not None:  # the lin2 branch sees dh o Z; LN2's column sums are of dh itself
             dh, db2 = ops.dropout_add(dres, None, *ctx.drop), None
         else:
             dh = dres
@@ -388,6 +422,9 @@ class GeluFn(torch.autograd.Function):
         return ops.native.require_for(z).gelu(z, dh.contiguous())
 
 
+_LN_DROP_FUSE = __import__("os").environ.get("FEDREC_LN_DROP_FUSE", "1") != "0"  # A/B switch
+
+
 class LayerNormFn(torch.autograd.Function):
     """``box`` (optional dict): the backward also leaves the column sums of its dx in
     ``box["colsum"]`` -- the bias gradient of the block Function that produced the LN input
@@ -404,7 +441,12 @@ class LayerNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         lib = ops.native.require_for(x)
-        if ctx.box is not None:
+        drop = ctx.box.pop("drop", None) if ctx.box is not None else None
+        if drop is not None and _LN_DROP_FUSE:
+            p, seed, off = drop
+            dx, ctx.box["dxz"], dw, db, ctx.box["colsum"] = lib.layer_norm_bwd_drop(
+                x.contiguous(), w, dy.contiguous(), float(ctx.eps), float(p), int(seed), int(off))
+        elif ctx.box is not None:
             dx, dw, db, ctx.box["colsum"] = lib.layer_norm_bwd_colsum(x, w, dy.contiguous(), float(ctx.eps))
         else:
             dx, dw, db = lib.layer_norm_bwd(x, w, dy.contiguous(), float(ctx.eps))

@@ -155,10 +155,14 @@ def test_additive_pool(dev, dtype, D, Q):
     assert abs(float(db2_n) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
 
 
+@pytest.mark.parametrize("variant", [1, 0])
 @pytest.mark.parametrize("H", [1, 50, 64, 65, 76, 200])
-def test_user_attention(dev, H):
+def test_user_attention(dev, H, variant):
     """H > 64 runs the long-history kernels (online softmax over 64-row LDS chunks): the
-    reference never truncates histories (Q6; its shipped shard has H = 76)."""
+    reference never truncates histories (Q6; its shipped shard has H = 76).  variant 1 = the
+    ILP kernels (default), 0 = the first forms."""
+    from fedrec_with_pytorchdistributed_amd.ops import native
+    native.lib().user_attn_set_variant(variant)
     B, NH, DK = 7, 20, 20
     qkv = torch.randn(B, H, 3 * NH * DK, device=dev)
     ctx, stats = ops.user_attention_fwd(qkv, NH, DK)
@@ -167,6 +171,7 @@ def test_user_attention(dev, H):
     d = torch.randn_like(ctx)
     dq = ops.user_attention_bwd(qkv, stats, d, NH, DK)
     dq_ref = ref.user_attention_bwd(qkv, A, d, NH, DK)
+    native.lib().user_attn_set_variant(1)
     assert rel_err(dq, dq_ref) < 1e-4
 
 
