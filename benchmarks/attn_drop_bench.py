@@ -59,33 +59,19 @@ def main():
         lib.title_attn_bwd_set_variant(v)
         return lib.title_attention_bwd_drop(qkv, dout, mask, H, p, seed, off)
 
-    def fwd_bits():
-        return lib.title_attention_drop_bits(qkv, mask, H, p, seed, off)
-
-    o_b, bits = fwd_bits()
-
-    def bwd_bits():
-        return lib.title_attention_bwd_drop_bits(qkv, dout, mask, bits, H, p)
-
     # same outputs from every form
     o_p, o_1 = fwd(-2).float(), fwd(2).float()
     g_p, g_1 = bwd(1).float(), bwd(0).float()
-    g_b = bwd_bits().float()
     res = {"fwd_max_abs_diff": float((o_p - o_1).abs().max()),
-           "fwd_bits_max_abs_diff": float((o_b.float() - o_1).abs().max()),
            "bwd_max_abs_diff": float((g_p - g_1).abs().max()),
-           "bwd_bits_max_abs_diff": float((g_b - g_1).abs().max()),
            "bwd_rel_l2": float((g_p - g_1).norm() / g_1.norm())}
     print(res, flush=True)
-    times = {"fwd_persistent": [], "fwd_oneshot": [], "fwd_bits": [], "bwd_persistent": [], "bwd_oneshot": [],
-             "bwd_bits": []}
+    times = {"fwd_persistent": [], "fwd_oneshot": [], "bwd_persistent": [], "bwd_oneshot": []}
     for _ in range(a.rounds):
         times["fwd_persistent"].append(timeit(lambda: fwd(-2)))
         times["fwd_oneshot"].append(timeit(lambda: fwd(2)))
-        times["fwd_bits"].append(timeit(fwd_bits))
         times["bwd_persistent"].append(timeit(lambda: bwd(1)))
         times["bwd_oneshot"].append(timeit(lambda: bwd(0)))
-        times["bwd_bits"].append(timeit(bwd_bits))
     lib.title_attn_set_waves(-2)
     lib.title_attn_bwd_set_variant(1)
     fbytes = M * 4 * D * 2  # read qkv, write out

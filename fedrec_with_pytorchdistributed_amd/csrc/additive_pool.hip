@@ -33,6 +33,9 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const TX* __restrict__ x,
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const TX* xe = x + (size_t)n * T * D;
   const TX* ee = e + (size_t)n * T * Q;
+  // rows interleaved 4 at a time and the t loops unrolled: these kernels are latency-bound
+  // (one block per impression, 64 blocks at B = 64), so independent loads must be in flight
+#pragma unroll 4
   for (int t = wave; t < T; t += 4) {
     float s = 0.f;
     for (int q = lane; q < Q; q += 64) s += ld(ee + (size_t)t * Q + q) * w2[q];
@@ -60,9 +63,14 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const TX* __restrict__ x,
   }
   __syncthreads();
   for (int d = tid; d < D; d += 256) {
-    float acc = 0.f;
-    for (int t = 0; t < T; ++t) acc += a_s[t] * ld(xe + (size_t)t * D + d);
-    out[(size_t)n * D + d] = acc;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int t = 0;
+#pragma unroll 2
+    for (; t + 4 <= T; t += 4)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += a_s[t + j] * ld(xe + (size_t)(t + j) * D + d);
+    for (; t < T; ++t) acc[0] += a_s[t] * ld(xe + (size_t)t * D + d);
+    out[(size_t)n * D + d] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
 }
 
@@ -83,6 +91,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
   const float* gn = g + (size_t)n * D;
   for (int t = tid; t < T; t += 256) al_s[t] = alpha[(size_t)n * T + t];
   // dalpha_t = x_t . g
+#pragma unroll 4
   for (int t = wave; t < T; t += 4) {
     float s = 0.f;
     for (int d = lane; d < D; d += 64) s += ld(xe + (size_t)t * D + d) * gn[d];
@@ -109,6 +118,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
   for (int q = tid; q < Q; q += 256) {
     const float wq = w2[q];
     float acc = 0.f;
+#pragma unroll 8
     for (int t = 0; t < T; ++t) {
       const float ev = ld(ee + (size_t)t * Q + q);
       const float da = da_s[t];
@@ -120,6 +130,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const TX* __restrict__ x,
   if (dx != nullptr) {
     for (int d = tid; d < D; d += 256) {
       const float gd = gn[d];
+#pragma unroll 8
       for (int t = 0; t < T; ++t) dx[((size_t)n * T + t) * D + d] = al_s[t] * gd;
     }
   }

@@ -91,10 +91,7 @@ long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, 
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
 int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
-                                 float pdrop, unsigned long long seed, unsigned long long offset, hipStream_t s,
-                                 void* zbits);
-int fr_title_attention_bwd_drop_bits_bf16(const void* qkv, const void* dout, const int* mask, const void* zbits,
-                                          void* dqkv, int n_titles, int T, int H, int D, float pdrop, hipStream_t s);
+                                 float pdrop, unsigned long long seed, unsigned long long offset, hipStream_t s);
 int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles,
                                      int T, int H, int D, float pdrop, unsigned long long seed,
                                      unsigned long long offset, hipStream_t s);
@@ -275,45 +272,6 @@ at::Tensor dropout_add(const at::Tensor& h, const c10::optional<at::Tensor>& res
   return out;
 }
 
-// the train-mode forward that also returns the keep bits ([n*H*64] int64) for the backward
-std::tuple<at::Tensor, at::Tensor> title_attention_drop_bits(const at::Tensor& qkv, const at::Tensor& mask,
-                                                             int64_t n_heads, double p, int64_t seed, int64_t offset) {
-  check_dev(qkv, "qkv");
-  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.is_contiguous(), "fedrec::title_attention_drop_bits: bf16");
-  const c10::DeviceGuard g(qkv.device());
-  auto mk = mask.to(at::kInt).contiguous();
-  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
-  TORCH_CHECK(qkv.numel() == n * T * 3 * D, "fedrec::title_attention_drop_bits: qkv shape");
-  auto out = at::empty({n * T, D}, qkv.options());
-  auto bits = at::empty({n * n_heads * 64}, qkv.options().dtype(at::kLong));
-  check_rc(fr_title_attention_drop_bf16(qkv.data_ptr(), mk.data_ptr<int>(), out.data_ptr(), (int)n, (int)T,
-                                        (int)n_heads, (int)D, (float)p, (unsigned long long)seed,
-                                        (unsigned long long)offset, cur_stream(), bits.data_ptr()),
-           "title_attention_drop_bits");
-  return {out, bits};
-}
-
-at::Tensor title_attention_bwd_drop_bits(const at::Tensor& qkv, const at::Tensor& dout, const at::Tensor& mask,
-                                         const at::Tensor& bits, int64_t n_heads, double p) {
-  check_dev(qkv, "qkv");
-  check_dev(dout, "dout");
-  check_dev(bits, "bits");
-  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && dout.scalar_type() == at::kBFloat16 && qkv.is_contiguous() &&
-                  dout.is_contiguous(), "fedrec::title_attention_bwd_drop_bits: bf16");
-  const c10::DeviceGuard g(qkv.device());
-  auto mk = mask.to(at::kInt).contiguous();
-  const int64_t n = mk.size(0), T = mk.size(1), D = qkv.size(-1) / 3;
-  TORCH_CHECK(qkv.numel() == n * T * 3 * D && dout.numel() == n * T * D, "fedrec::title_attention_bwd_drop_bits: shapes");
-  TORCH_CHECK(bits.scalar_type() == at::kLong && bits.is_contiguous() && bits.numel() == n * n_heads * 64,
-              "fedrec::title_attention_bwd_drop_bits: bits");
-  auto dqkv = at::empty_like(qkv);
-  check_rc(fr_title_attention_bwd_drop_bits_bf16(qkv.data_ptr(), dout.data_ptr(), mk.data_ptr<int>(), bits.data_ptr(),
-                                                 dqkv.data_ptr(), (int)n, (int)T, (int)n_heads, (int)D, (float)p,
-                                                 cur_stream()),
-           "title_attention_bwd_drop_bits");
-  return dqkv;
-}
-
 at::Tensor title_attention_drop(const at::Tensor& qkv, const at::Tensor& mask, int64_t n_heads, double p, int64_t seed,
                                 int64_t offset) {
   check_dev(qkv, "qkv");
@@ -325,7 +283,7 @@ at::Tensor title_attention_drop(const at::Tensor& qkv, const at::Tensor& mask, i
   auto out = at::empty({n * T, D}, qkv.options());
   check_rc(fr_title_attention_drop_bf16(qkv.data_ptr(), mk.data_ptr<int>(), out.data_ptr(), (int)n, (int)T,
                                         (int)n_heads, (int)D, (float)p, (unsigned long long)seed,
-                                        (unsigned long long)offset, cur_stream(), nullptr),
+                                        (unsigned long long)offset, cur_stream()),
            "title_attention_drop");
   return out;
 }
@@ -1169,8 +1127,6 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");
   m.def("dropout_add(Tensor h, Tensor? res, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
-  m.def("title_attention_drop_bits(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> (Tensor, Tensor)");
-  m.def("title_attention_bwd_drop_bits(Tensor qkv, Tensor dout, Tensor mask, Tensor bits, int n_heads, float p) -> Tensor");
   m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("gather_dropout(Tensor v, Tensor idx, float p, int seed, int offset, Tensor? dev_off) -> Tensor");
@@ -1215,8 +1171,6 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("multi_cast", &multi_cast);
   m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
   m.impl("title_attention_drop", &title_attention_drop);
-  m.impl("title_attention_drop_bits", &title_attention_drop_bits);
-  m.impl("title_attention_bwd_drop_bits", &title_attention_bwd_drop_bits);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);
   m.impl("wgrad", &wgrad);
   m.impl("gather_dropout", &gather_dropout);

@@ -230,11 +230,7 @@ template <int OCC, int DEPTH, bool DROP = false>
 __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __restrict__ qkv, const int* __restrict__ mask,
                                                           bf16* __restrict__ out, int n_pairs, int T, int H, int D,
                                                           float pdrop = 0.f, unsigned long long seed = 0ull,
-                                                          unsigned long long offset = 0ull,
-                                                          unsigned long long* __restrict__ zout = nullptr) {
-  // zout (DROP, optional): the keep bits of each pair, [n_pairs][64 lanes] x 64 bits (lane's
-  // query t = 16 jq + fr, key s = 16 is + 4 fq + r at bit 16 jq + 4 is + r) -- the backward
-  // reads 8 bytes per lane instead of regenerating 16 Philox blocks
+                                                          unsigned long long offset = 0ull) {
   __shared__ __attribute__((aligned(16))) bf16 vs[4][64 * DH];
   // wave index via readfirstlane: the compiler then knows pair / next are wave-uniform, so the
   // prefetch guards are scalar branches (a "divergent" guard around loads makes it drain
@@ -276,7 +272,6 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
 
     const float scale = 0.125f;
     bf16x8 pf[4][2];
-    unsigned long long zbits = 0ull;
 #pragma unroll
     for (int jq = 0; jq < 4; ++jq) {
       float m = -INFINITY;
@@ -308,11 +303,7 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
         for (int is = 0; is < 4; ++is) {
           const uint4 rnd = Philox::gen(seed, offset, ((unsigned long long)pair * 64 + t) * 16 + is * 4 + fq);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const bool kp = u32_to_unit(u4_get(rnd, r)) > pdrop;  // = drop_scale's test
-            st[is][jq][r] *= kp ? inv_keep : 0.f;
-            zbits |= (kp ? 1ull : 0ull) << (jq * 16 + is * 4 + r);
-          }
+          for (int r = 0; r < 4; ++r) st[is][jq][r] *= drop_scale(u4_get(rnd, r), pdrop, inv_keep);
         }
       }
 #pragma unroll
@@ -325,9 +316,6 @@ __global__ __launch_bounds__(256, OCC) void title_attn_pkernel(const bf16* __res
         }
         pf[jq][ks] = f;
       }
-    }
-    if constexpr (DROP) {
-      if (zout != nullptr) zout[(size_t)pair * 64 + lane] = zbits;
     }
     if (next < n_pairs) ta_load_v(in, qkv, next, T, H, D, lane);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V image is in LDS
@@ -709,15 +697,14 @@ extern "C" int fr_title_attention_bf16(const void* qkv, const int* mask, void* o
   return 0;
 }
 
-// train-mode forward with attention-probability dropout (T <= 64; 2 = unsupported shape);
-// zbits (optional, [n_titles * H * 64] u64): keep bits for title_attention_bwd_drop_bits
+// train-mode forward with attention-probability dropout (T <= 64; 2 = unsupported shape)
 extern "C" int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H,
                                             int D, float pdrop, unsigned long long seed, unsigned long long offset,
-                                            hipStream_t s, void* zbits) {
+                                            hipStream_t s) {
   if (T < 1 || T > 64 || D != H * DH || !(pdrop > 0.f && pdrop < 1.f)) return 2;
   const int pairs = n_titles * H;
   if (pairs == 0) return 0;
-  if (g_ta_waves == -2 || zbits != nullptr) {  // persistent 2-deep prefetching form (default), as the eval forward
+  if (g_ta_waves == -2) {  // persistent 2-deep prefetching form (default), as the eval forward
     if (g_ta_cus == 0) {
       int dev = 0;
       (void)hipGetDevice(&dev);
@@ -727,7 +714,7 @@ extern "C" int fr_title_attention_drop_bf16(const void* qkv, const int* mask, vo
     const int need = (pairs + 3) / 4;
     const int blocks = g_ta_cus < need ? g_ta_cus : need;
     hipLaunchKernelGGL((title_attn_pkernel<1, 2, true>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, mask,
-                       (bf16*)out, pairs, T, H, D, pdrop, seed, offset, (unsigned long long*)zbits);
+                       (bf16*)out, pairs, T, H, D, pdrop, seed, offset);
     return 0;
   }
   hipLaunchKernelGGL((title_attn_kernel<2, true>), dim3((pairs + 1) / 2), dim3(128), 0, s, (const bf16*)qkv, mask,

@@ -266,15 +266,13 @@ __global__ __launch_bounds__(64 * WPB) void title_attn_bwd_kernel(const bf16* __
 struct TBIn {
   bf16x8 q[8], k[8], v[8], g[8];
   int mk;  // lane s: mask of key s (clamped row; s >= T is handled by the caller)
-  unsigned long long zb;  // the forward's dropout keep bits of this lane (zin given)
 };
 
 // element index of (row r, column c) in a swizzled [64][64] bf16 tile
 __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((((c >> 3) ^ (r & 7)) << 3) | (c & 7)); }
 
 __device__ __forceinline__ void tb_load(TBIn& in, const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                        const int* __restrict__ mask, int pair, int T, int H, int D, int lane,
-                                        const unsigned long long* __restrict__ zin = nullptr) {
+                                        const int* __restrict__ mask, int pair, int T, int H, int D, int lane) {
   const int title = pair / H, h = pair - title * H;
   const size_t row0 = (size_t)title * T;
   const int ld = 3 * D;
@@ -292,21 +290,19 @@ __device__ __forceinline__ void tb_load(TBIn& in, const bf16* __restrict__ qkv, 
     in.g[c] = *(const bf16x8*)(gb + (size_t)r * D + ch * 8);
   }
   in.mk = mask[row0 + (lane < T ? lane : T - 1)];
-  if (zin != nullptr) in.zb = zin[(size_t)pair * 64 + lane];
 }
 
-// DM 0: no dropout; 1: as title_attn_bwd_kernel<true> (the forward's Philox mask regenerated
-// per element); 2: the forward's stored keep bits (zin).  Compile-time: a kernel carrying both
-// dropout forms spills (688 B/lane vs 116).
-template <int DM>
+// DROP: as title_attn_bwd_kernel<true> (the forward's Philox mask regenerated per element,
+// kept as 16-bit keep words per query: per-element scale arrays across the softmax spill).
+// Reading keep bits stored by the forward instead (8 B per lane and pair) measured slower:
+// 523 vs 437 us (profiles/r2_attn_drop_bits_bench.json) -- the bit unpacking spilled more.
+template <bool DROP>
 __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const int* __restrict__ mask,
                                                                  bf16* __restrict__ dqkv, int n_pairs, int T, int H,
                                                                  int D, float pdrop, unsigned long long seed,
-                                                                 unsigned long long offset,
-                                                                 const unsigned long long* __restrict__ zin) {
-  constexpr bool DROP = DM != 0;
+                                                                 unsigned long long offset) {
   __shared__ __attribute__((aligned(16))) bf16 lds[4][4][64 * DH];  // per wave: Q, K, V (then P^T/dS^T), dO
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int stride = gridDim.x * 4;
@@ -321,7 +317,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
   const int qq = fr >> 2, pp = fr & 3;
   const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
   TBIn in;
-  tb_load(in, qkv, dout, mask, pair, T, H, D, lane, DM == 2 ? zin : nullptr);
+  tb_load(in, qkv, dout, mask, pair, T, H, D, lane);
   while (true) {
     // ---- stage the current pair (rows >= T zero) and its mask; then prefetch the next ----
 #pragma unroll
@@ -346,10 +342,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
     // drain, and kept as 4 words (per-element scale arrays across the softmax spill)
     unsigned zbits[4] = {0u, 0u, 0u, 0u};
     const float inv_keep = DROP ? 1.0f / (1.0f - pdrop) : 1.f;
-    if constexpr (DM == 2) {
-#pragma unroll
-      for (int jq = 0; jq < 4; ++jq) zbits[jq] = (unsigned)(in.zb >> (jq * 16)) & 0xFFFFu;
-    } else if constexpr (DROP) {
+    if constexpr (DROP) {
 #pragma unroll
       for (int jq = 0; jq < 4; ++jq)
 #pragma unroll
@@ -454,7 +447,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
     }
     // the fp32 S / dP are dead: prefetch the next pair into the staging registers now (its
     // loads land during dQ, dV and dK of this pair)
-    tb_load(in, qkv, dout, mask, next, T, H, D, lane, DM == 2 ? zin : nullptr);
+    tb_load(in, qkv, dout, mask, next, T, H, D, lane);
     // ---- dQ = dS K (B = K via transposed reads of the swizzled tile) ----
     f32x4 o[4][4];
 #pragma unroll
@@ -562,8 +555,8 @@ extern "C" int fr_title_attention_bwd_bf16(const void* qkv, const void* dout, co
     int blocks = tab_cus();
     const int need = (pairs + 3) / 4;
     blocks = blocks < need ? blocks : need;
-    hipLaunchKernelGGL(title_attn_bwd_pkernel<0>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
-                       mask, (bf16*)dqkv, pairs, T, H, D, 0.f, 0ull, 0ull, nullptr);
+    hipLaunchKernelGGL(title_attn_bwd_pkernel<false>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
+                       mask, (bf16*)dqkv, pairs, T, H, D, 0.f, 0ull, 0ull);
     return 0;
   }
   hipLaunchKernelGGL((title_attn_bwd_kernel<false>), dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s,
@@ -580,8 +573,8 @@ extern "C" int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dou
   if (g_tab_variant == 1) {
     const int need = (pairs + 3) / 4;
     const int blocks = tab_cus() < need ? tab_cus() : need;
-    hipLaunchKernelGGL(title_attn_bwd_pkernel<1>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
-                       mask, (bf16*)dqkv, pairs, T, H, D, pdrop, seed, offset, nullptr);
+    hipLaunchKernelGGL(title_attn_bwd_pkernel<true>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
+                       mask, (bf16*)dqkv, pairs, T, H, D, pdrop, seed, offset);
     return 0;
   }
   hipLaunchKernelGGL((title_attn_bwd_kernel<true>), dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s,
@@ -589,16 +582,3 @@ extern "C" int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dou
   return 0;
 }
 
-// backward from the forward's stored keep bits ([n_titles * H * 64] u64, title_attn.hip zbits)
-extern "C" int fr_title_attention_bwd_drop_bits_bf16(const void* qkv, const void* dout, const int* mask,
-                                                     const void* zbits, void* dqkv, int n_titles, int T, int H, int D,
-                                                     float pdrop, hipStream_t s) {
-  if (T < 1 || T > 64 || D != H * DH || !(pdrop > 0.f && pdrop < 1.f) || zbits == nullptr) return 2;
-  const int pairs = n_titles * H;
-  if (pairs == 0) return 0;
-  const int need = (pairs + 3) / 4;
-  const int blocks = tab_cus() < need ? tab_cus() : need;
-  hipLaunchKernelGGL(title_attn_bwd_pkernel<2>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout, mask,
-                     (bf16*)dqkv, pairs, T, H, D, pdrop, 0ull, 0ull, (const unsigned long long*)zbits);
-  return 0;
-}

@@ -181,13 +181,15 @@ __global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------------------
-// ILP forms (default).  The kernels above are latency-bound, not FLOP-bound: ~1.25 waves per
+// ILP forward (default).  The kernels above are latency-bound, not FLOP-bound: ~1.25 waves per
 // SIMD, and every key costs a 20-deep chain of dependent FMAs (dot20) before its exp -- the
-// forward ran 35 us for 1,280 (impression, head) pairs of 50 x 50 x 20.  Here the key loops
+// forward ran 33 us for 1,280 (impression, head) pairs of 50 x 50 x 20.  Here the key loops
 // are fully unrolled over MAXH with a wave-uniform guard (so independent keys interleave),
-// the dot products split into 4 partial sums (chains of 5), and the forward keeps its scores
-// in registers (one dot product per key instead of two).  Same math and outputs (fp32; only
-// the summation order inside a 20-term dot product differs).
+// the dot products split into 4 partial sums (chains of 5), and the scores stay in registers
+// (one dot product per key instead of two): 20 us (profiles/r2_user_attn_ilp_bench.json).
+// Same math (fp32; only the summation order inside a 20-term dot product differs).  The same
+// treatment of the backward measured slower (63 vs 54 us: 141 VGPRs, half the occupancy) and
+// is not used.
 __device__ __forceinline__ void load_row_s(float (&x)[DK], const float* __restrict__ p, float sc) {
 #pragma unroll
   for (int c4 = 0; c4 < DK / 4; ++c4) {
@@ -264,100 +266,7 @@ __global__ __launch_bounds__(128) void user_attn_fwd_ilp_kernel(const float* __r
   st[1] = inv;
 }
 
-__global__ __launch_bounds__(64) void user_attn_bwd_ilp_kernel(const float* __restrict__ qkv,
-                                                               const float* __restrict__ stats,
-                                                               const float* __restrict__ dctx, float* __restrict__ dqkv,
-                                                               int B, int H, int NH) {
-  __shared__ __attribute__((aligned(16))) float qs[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float ks[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float vs[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float gs[MAXH][DK];
-  __shared__ float ms[MAXH], is_[MAXH], Ds[MAXH];
-  const int lane = threadIdx.x;
-  const int pair = blockIdx.x;
-  const int b = pair / NH, h = pair - b * NH;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  const float* gb = dctx + (size_t)b * H * D + h * DK;
-  for (int i = lane; i < H * DK / 4; i += 64) {
-    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
-    *(float4*)&qs[r][c] = *(const float4*)(base + (size_t)r * ld + c);
-    *(float4*)&ks[r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
-    *(float4*)&vs[r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
-    *(float4*)&gs[r][c] = *(const float4*)(gb + (size_t)r * D + c);
-  }
-  const float* st = stats + ((size_t)b * NH + h) * H * 2;
-  for (int t = lane; t < H; t += 64) {
-    ms[t] = st[2 * t];
-    is_[t] = st[2 * t + 1];
-  }
-  __syncthreads();
-  const float scale = rsqrtf((float)DK);
-  float* dbase = dqkv + (size_t)b * H * ld + h * DK;
-  const int r = lane < H ? lane : H - 1;  // clamped row: uniform unrolled code, guarded stores
-  {
-    // lane = query t: D_t = sum_s A_ts dA_ts, u = sum_s A dA k_s, w = sum_s A k_s
-    const float m = ms[r], inv = is_[r];
-    float q[DK], g[DK], u[DK], w[DK];
-#pragma unroll
-    for (int c = 0; c < DK; ++c) {
-      q[c] = qs[r][c] * scale;
-      g[c] = gs[r][c];
-      u[c] = w[c] = 0.f;
-    }
-    float Dt = 0.f;
-#pragma unroll
-    for (int s = 0; s < MAXH; ++s)
-      if (s < H) {
-        const float A = __expf(dot20x(q, &ks[s][0]) - m) * inv;
-        const float dA = dot20x(g, &vs[s][0]);
-        Dt += A * dA;
-        axpy20(u, A * dA, &ks[s][0]);
-        axpy20(w, A, &ks[s][0]);
-      }
-    if (lane < H) {
-      Ds[lane] = Dt;
-      float* o = dbase + (size_t)lane * ld;
-#pragma unroll
-      for (int c4 = 0; c4 < DK / 4; ++c4) {
-        const int c = 4 * c4;
-        *(float4*)(o + c) = make_float4(scale * (u[c] - Dt * w[c]), scale * (u[c + 1] - Dt * w[c + 1]),
-                                        scale * (u[c + 2] - Dt * w[c + 2]), scale * (u[c + 3] - Dt * w[c + 3]));
-      }
-    }
-  }
-  __syncthreads();
-  {
-    // lane = key s: dk_s = sum_t dS_ts q_t, dv_s = sum_t A_ts g_t
-    float k[DK], v[DK], dk[DK], dv[DK];
-#pragma unroll
-    for (int c = 0; c < DK; ++c) {
-      k[c] = ks[r][c] * scale;
-      v[c] = vs[r][c];
-      dk[c] = dv[c] = 0.f;
-    }
-#pragma unroll
-    for (int t = 0; t < MAXH; ++t)
-      if (t < H) {
-        const float A = __expf(dot20x(k, &qs[t][0]) - ms[t]) * is_[t];
-        const float dA = dot20x(v, &gs[t][0]);
-        const float dS = A * (dA - Ds[t]) * scale;
-        axpy20(dk, dS, &qs[t][0]);
-        axpy20(dv, A, &gs[t][0]);
-      }
-    if (lane < H) {
-      float* o = dbase + (size_t)lane * ld;
-#pragma unroll
-      for (int c4 = 0; c4 < DK / 4; ++c4) {
-        const int c = 4 * c4;
-        *(float4*)(o + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
-        *(float4*)(o + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
-      }
-    }
-  }
-}
-
-int g_ua_variant = 1;  // 1: ILP forms (default), 0: the first forms
+int g_ua_variant = 1;  // 1: ILP forward (default), 0: the first forward
 
 // ---------------------------------------------------------------------------------------
 // Long histories (H > 64): the reference pads but never truncates (dataset.py:84, quirk Q6;
@@ -556,8 +465,6 @@ extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const floa
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
-  else if (g_ua_variant == 1)
-    hipLaunchKernelGGL(user_attn_bwd_ilp_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   else
     hipLaunchKernelGGL(user_attn_bwd_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   return 0;

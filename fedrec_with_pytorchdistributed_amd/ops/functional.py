@@ -286,9 +286,6 @@ class DropoutFn(torch.autograd.Function):
         return ops.dropout_add(g.contiguous(), None, *ctx.drop), None, None, None
 
 
-_ATTN_BITS = __import__("os").environ.get("FEDREC_ATTN_BITS", "1") != "0"  # A/B switch
-
-
 class AttnBlockFn(torch.autograd.Function):
     """``h = out_proj(attention(x Wqkv^T + bqkv)) + x`` (one post-LN block's attention half,
     unfrozen backbone).  One Function so the residual gradient joins the QKV input gradient
@@ -304,16 +301,9 @@ class AttnBlockFn(torch.autograd.Function):
         # dbqkv, so no per-step fp32 cat of the three weights); the GEMM runs on the fused bf16
         # compute copy wqkv_low and the fused fp32 bias bqkv of the backbone's pack
         qkv = ops.linear(x, wqkv_low, bqkv)
-        bits = None
-        if drop is not None and _ATTN_BITS and qkv.is_cuda and mask.shape[1] <= 64:
-            # the keep bits leave the forward (8 B per lane and (title, head)): the backward
-            # reads them instead of regenerating 16 Philox blocks per lane
-            c, bits = ops.native.require_for(qkv).title_attention_drop_bits(qkv, mask, heads, float(drop[0]),
-                                                                            int(drop[1]), int(drop[2]))
-        else:
-            c = ops.title_attention(qkv, mask, heads, drop)
+        c = ops.title_attention(qkv, mask, heads, drop)
         h = ops.linear(c, wo_low, bo, residual=x)
-        ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low, wo, bits)
+        ctx.save_for_backward(x, qkv, c, mask, wqkv_low, wo_low, wo)
         ctx.heads = heads
         ctx.box = box
         ctx.drop = drop
@@ -321,16 +311,12 @@ class AttnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh):
-        x, qkv, c, mask, wqkv_low, wo_low, wo, bits = ctx.saved_tensors
+        x, qkv, c, mask, wqkv_low, wo_low, wo = ctx.saved_tensors
         dh = dh.contiguous()
         dbo = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN1's backward
         dwo, dbo = wgrad(dh, c), (dbo if dbo is not None else bgrad(dh))
         dc = dgrad(dh, wo_low)
-        if bits is not None:
-            dqkv = ops.native.require_for(qkv).title_attention_bwd_drop_bits(qkv, dc, mask, bits, ctx.heads,
-                                                                            float(ctx.drop[0]))
-        else:
-            dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
+        dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
         dwqkv = wgrad(dqkv, x)
         if _QKV_BIAS_SHORTCUT and dqkv.is_cuda and ctx.drop is None:
             # column sums of dQ | dK | dV without reading dK and dV: every softmax row sums to
@@ -541,6 +527,7 @@ class UserStepFn(torch.autograd.Function):
         ctx.save_for_backward(v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2, xd)
         ctx.meta = meta
         ctx.mark_non_differentiable(scores)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the scores (one fill launch)
         return loss, scores
 
     @staticmethod

@@ -12,7 +12,6 @@ from fedrec_with_pytorchdistributed_amd import ops
 from fedrec_with_pytorchdistributed_amd.config import BackboneConfig, FedRecConfig
 from fedrec_with_pytorchdistributed_amd.data.synthetic import make_client_shards
 from fedrec_with_pytorchdistributed_amd.models.fedrec_model import FedRecModel
-from fedrec_with_pytorchdistributed_amd.ops import native
 from fedrec_with_pytorchdistributed_amd.ops import reference as R
 from fedrec_with_pytorchdistributed_amd.train.engine import LocalEngine
 
@@ -131,33 +130,6 @@ def test_title_attention_dropout_fwd_bwd_match_oracle(dev, T):
         a = dq.float().cpu()[:, part * D:(part + 1) * D]
         b = q32.grad[:, part * D:(part + 1) * D]
         assert float((a - b).norm() / (b.norm() + 1e-12)) < 2e-2, part
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("T", [50, 64])
-def test_title_attention_drop_bits_match_regenerated_mask(dev, T):
-    """The forward that stores its keep bits (8 bytes per lane and pair) and the backward that
-    reads them give the outputs of the Philox-regenerating pair, and match the fp32 oracle."""
-    torch.manual_seed(1)
-    n, H, D = 40, 12, 768
-    lib = native.lib()
-    qkv = (torch.randn(n * T, 3 * D, device=dev) * 0.5).to(torch.bfloat16)
-    mask = torch.ones(n, T, dtype=torch.int32, device=dev)
-    mask[3, T // 3:] = 0
-    mask[5, :] = 0
-    p, seed, off = 0.1, 777, 9
-    out_b, bits = lib.title_attention_drop_bits(qkv, mask, H, p, seed, off)
-    out_r = ops.title_attention(qkv, mask, H, (p, seed, off))
-    assert torch.equal(out_b, out_r)
-    assert bits.numel() == n * H * 64
-    g = (torch.randn(n * T, D, device=dev) * 0.1).to(torch.bfloat16)
-    d_b = lib.title_attention_bwd_drop_bits(qkv, g, mask, bits, H, p)
-    d_r = ops.title_attention_bwd(qkv, g, mask, H, (p, seed, off))
-    assert float((d_b.float() - d_r.float()).norm() / d_r.float().norm()) < 1e-5
-    q32 = qkv.float().cpu().requires_grad_(True)
-    ref = R.title_attention(q32, mask.cpu(), H, (p, seed, off))
-    ref.backward(g.float().cpu())
-    assert float((d_b.float().cpu() - q32.grad).norm() / q32.grad.norm()) < 2e-2
 
 
 @pytest.mark.gpu
