@@ -121,3 +121,81 @@ extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const lo
   hipLaunchKernelGGL(multi_cast_kernel, dim3((unsigned)blk), dim3(256), 0, s, mc);
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// The same refresh into TRANSPOSED bf16 copies (unfrozen backbone: the input-gradient GEMMs
+// run on W^T, which was a `wlow.t().contiguous()` copy launch per weight and step): segment i
+// is an fp32 [R, C] master, written as bf16 dst[c * ld + r] (ld >= R: the q / k / v blocks
+// land side by side in the fused [D, 3D] transposed QKV weight).  64 x 64 tiles through LDS
+// (padded rows: conflict-free column reads), R % 64 == C % 64 == 0 (host-checked).
+namespace {
+constexpr int MCT_SEG = 96;
+
+struct MultiCastT {
+  const float* src[MCT_SEG];
+  bf16* dst[MCT_SEG];
+  int R[MCT_SEG], C[MCT_SEG], ld[MCT_SEG];
+  int blk0[MCT_SEG + 1];
+  int nseg;
+};
+
+__global__ __launch_bounds__(256) void multi_cast_t_kernel(const MultiCastT mc) {
+  __shared__ float tile[64][65];
+  int lo = 0, hi = mc.nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (mc.blk0[mid] <= (int)blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  const int sg = lo;
+  const int t = blockIdx.x - mc.blk0[sg];
+  const int ct = mc.C[sg] >> 6;
+  const int r0 = (t / ct) * 64, c0 = (t % ct) * 64;
+  const float* src = mc.src[sg];
+  const int C = mc.C[sg];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 64 rows x 16 float4
+    const int r = (tid >> 4) + 16 * i, c = (tid & 15) * 4;
+    const float4 v = *(const float4*)(src + (size_t)(r0 + r) * C + c0 + c);
+    tile[r][c] = v.x;
+    tile[r][c + 1] = v.y;
+    tile[r][c + 2] = v.z;
+    tile[r][c + 3] = v.w;
+  }
+  __syncthreads();
+  bf16* dst = mc.dst[sg];
+  const int ld = mc.ld[sg];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 64 destination rows (source columns) x 8 chunks of 8
+    const int c = (tid >> 3) + 32 * i, r = (tid & 7) * 8;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(tile[r + j][c]);
+    *(bf16x8*)(dst + (size_t)(c0 + c) * ld + r0 + r) = o;
+  }
+}
+}  // namespace
+
+extern "C" int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, const int* C, const int* ld,
+                               int nseg, hipStream_t s) {
+  if (nseg < 1 || nseg > MCT_SEG) return 1;
+  MultiCastT mc{};
+  mc.nseg = nseg;
+  long blk = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (R[i] <= 0 || C[i] <= 0 || R[i] % 64 || C[i] % 64 || ld[i] < R[i] || ld[i] % 8 || ((uintptr_t)src[i] & 15) ||
+        ((uintptr_t)dst[i] & 15))
+      return 1;
+    mc.src[i] = src[i];
+    mc.dst[i] = (bf16*)dst[i];
+    mc.R[i] = R[i];
+    mc.C[i] = C[i];
+    mc.ld[i] = ld[i];
+    mc.blk0[i] = (int)blk;
+    blk += (long)(R[i] / 64) * (C[i] / 64);
+  }
+  mc.blk0[nseg] = (int)blk;
+  hipLaunchKernelGGL(multi_cast_t_kernel, dim3((unsigned)blk), dim3(256), 0, s, mc);
+  return 0;
+}

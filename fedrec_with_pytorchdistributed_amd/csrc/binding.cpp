@@ -85,6 +85,8 @@ int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, in
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, hipStream_t s);
 int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg, hipStream_t s);
+int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, const int* C, const int* ld, int nseg,
+                    hipStream_t s);
 int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
                   hipStream_t s);
 long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part, hipStream_t s);
@@ -750,6 +752,36 @@ bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor
   return true;
 }
 
+// fp32 [R, C] masters -> transposed bf16 copies (dst: [C, ld] views, ld = row stride >= R) in one
+// launch per 96 (adam.hip); false = not launched (shape / alignment), the caller transposes itself
+bool multi_cast_t(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst) {
+  const size_t n = src.size();
+  TORCH_CHECK(n >= 1 && dst.size() == n, "fedrec::multi_cast_t: sizes");
+  const c10::DeviceGuard g(dst[0].device());
+  std::vector<const float*> sp(n);
+  std::vector<void*> dp(n);
+  std::vector<int> R(n), C(n), ld(n);
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && src[i].dim() == 2 &&
+                    dst[i].dim() == 2 && src[i].scalar_type() == at::kFloat && dst[i].scalar_type() == at::kBFloat16 &&
+                    dst[i].size(0) == src[i].size(1) && dst[i].size(1) == src[i].size(0) && dst[i].stride(1) == 1,
+                "fedrec::multi_cast_t: fp32 [R, C] sources, bf16 [C, R] row-major destinations");
+    sp[i] = src[i].data_ptr<float>();
+    dp[i] = dst[i].data_ptr();
+    R[i] = (int)src[i].size(0);
+    C[i] = (int)src[i].size(1);
+    ld[i] = (int)dst[i].stride(0);
+    if (R[i] % 64 || C[i] % 64 || ld[i] % 8 || ((uintptr_t)sp[i] & 15) || ((uintptr_t)dp[i] & 15)) return false;
+  }
+  for (size_t i0 = 0; i0 < n; i0 += 96) {
+    const int k = (int)std::min<size_t>(96, n - i0);
+    TORCH_CHECK(fr_multi_cast_t(sp.data() + i0, dp.data() + i0, R.data() + i0, C.data() + i0, ld.data() + i0, k,
+                                cur_stream()) == 0,
+                "fedrec::multi_cast_t: launch rejected");
+  }
+  return true;
+}
+
 // several small copies (+ fills of the tails) in one launch, in 4-byte words
 void multi_copy(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst, at::IntArrayRef fill) {
   const size_t n = src.size();
@@ -1122,6 +1154,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg) -> ()");
   m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
   m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst) -> bool");
+  m.def("multi_cast_t(Tensor[] src, Tensor(a!)[] dst) -> bool");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");
   m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");
@@ -1169,6 +1202,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("colsum_f32", &colsum_f32);
   m.impl("multi_copy", &multi_copy);
   m.impl("multi_cast", &multi_cast);
+  m.impl("multi_cast_t", &multi_cast_t);
   m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);

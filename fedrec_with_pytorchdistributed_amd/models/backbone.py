@@ -82,6 +82,7 @@ class Backbone(nn.Module):
         self._pack: Optional[Dict] = None
         self._pack_key = None
         self._stale = True
+        self._cast_plan_t = None
         self.version = 0  # bumped whenever the weights may have changed (hidden-state caches key on it)
         # train-mode dropout: Philox key (the engine sets seed + rank) and a per-forward counter;
         # a forward's sites use offsets 1024 * call + {0: embeddings, 1 + 2l: attention of
@@ -129,7 +130,9 @@ class Backbone(nn.Module):
             # an optimizer step (or a load) changed the masters: refresh the existing compute
             # copies in place, all of them in one launch (csrc/adam.hip multi_cast) instead of
             # a cat + cast launch per weight
-            if dev.type == "cuda" and ops.native.lib().multi_cast(*self._cast_plan):
+            lib = ops.native.lib() if dev.type == "cuda" else None
+            if lib is not None and lib.multi_cast(*self._cast_plan) and (
+                    self._cast_plan_t is None or lib.multi_cast_t(*self._cast_plan_t)):
                 self._stale = False
                 return self._pack
         e = self.embeddings
@@ -167,6 +170,25 @@ class Backbone(nn.Module):
             src += [a.out_lin.weight, blk.ffn.lin1.weight, blk.ffn.lin2.weight]
             dst += [L["wo"], L["w1"], L["w2"]]
         self._cast_plan = ([t.detach() for t in src], dst)
+        # unfrozen training: transposed bf16 copies for the input-gradient GEMMs (they run on
+        # W^T), refreshed in the same step by one transposing launch (multi_cast_t) instead of
+        # a `.t().contiguous()` copy per weight in every backward
+        self._cast_plan_t = None
+        if not self.cfg.frozen and dev.type == "cuda" and dtype == torch.bfloat16:
+            srct, dstt = [], []
+            for blk, L in zip(self.transformer.layer, pack["layers"]):
+                a = blk.attention
+                D = a.q_lin.weight.shape[0]
+                L["wqkv_t"] = L["wqkv"].t().contiguous()
+                L["wo_t"] = L["wo"].t().contiguous()
+                L["w1_t"] = L["w1"].t().contiguous()
+                L["w2_t"] = L["w2"].t().contiguous()
+                for i, lin in enumerate((a.q_lin, a.k_lin, a.v_lin)):
+                    srct.append(lin.weight)
+                    dstt.append(L["wqkv_t"][:, i * D:(i + 1) * D])
+                srct += [a.out_lin.weight, blk.ffn.lin1.weight, blk.ffn.lin2.weight]
+                dstt += [L["wo_t"], L["w1_t"], L["w2_t"]]
+            self._cast_plan_t = ([t.detach() for t in srct], dstt)
         self._pack, self._pack_key, self._stale = pack, key, False
         return pack
 
@@ -342,10 +364,11 @@ class Backbone(nn.Module):
                 box1, box2 = ({}, {}) if fuse else (None, None)
                 h = OF.AttnBlockFn.apply(x, a.q_lin.weight, a.k_lin.weight, a.v_lin.weight, a.q_lin.bias,
                                          a.k_lin.bias, a.v_lin.bias, a.out_lin.weight, a.out_lin.bias,
-                                         mask.contiguous(), c.n_heads, L["wqkv"], L["bqkv"], L["wo"], box1, sa)
+                                         mask.contiguous(), c.n_heads, L["wqkv"], L["bqkv"], L["wo"], box1, sa,
+                                         (L.get("wqkv_t"), L.get("wo_t")))
                 x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps, box1)
                 h = OF.MLPBlockFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, blk.ffn.lin2.weight,
-                                        blk.ffn.lin2.bias, L["w1"], L["w2"], box2, sf)
+                                        blk.ffn.lin2.bias, L["w1"], L["w2"], box2, sf, (L.get("w1_t"), L.get("w2_t")))
                 x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps, box2)
                 continue
             wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)

@@ -50,16 +50,18 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
 _DGRAD_IMPL = __import__("os").environ.get("FEDREC_DGRAD", "ours")  # ours | lib (A/B runs)
 
 
-def dgrad(dy: torch.Tensor, wlow: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+def dgrad(dy: torch.Tensor, wlow: torch.Tensor, residual: Optional[torch.Tensor] = None,
+          wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``dy @ wlow (+ residual)``: the input gradient of ``y = x wlow^T``.
 
     On the device our NT MFMA GEMM runs it on ``wlow^T`` (a 1-5 MB per-step transpose of the
     bf16 weight; the GEMM streams ~100 MB of ``dy``), with the residual gradient added in the
     epilogue (beta = 1) -- no library GEMM in the training step.  ``FEDREC_DGRAD=lib`` keeps
-    the library ``mm`` / ``addmm_`` for A/B runs."""
+    the library ``mm`` / ``addmm_`` for A/B runs.  ``wt``: ``wlow^T`` already materialised (the
+    unfrozen backbone's pack keeps transposed copies, refreshed once per optimizer step)."""
     if (dy.is_cuda and dy.dtype == torch.bfloat16 and _DGRAD_IMPL != "lib" and wlow.shape[1] % 128 == 0
             and wlow.shape[0] % 64 == 0):
-        return ops.linear(dy, wlow.t().contiguous(), None, residual=residual)
+        return ops.linear(dy, wt if wt is not None else wlow.t().contiguous(), None, residual=residual)
     if residual is not None:
         return residual.addmm_(dy, wlow)
     return torch.mm(dy, wlow)
@@ -296,7 +298,7 @@ class AttnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wq, wk, wv, bq, bk, bv, wo, bo, mask, heads: int, wqkv_low, bqkv, wo_low, box=None,
-                drop=None):
+                drop=None, wts=(None, None)):
         # wq .. bv: the fp32 masters (autograd inputs: their gradients are slices of dwqkv /
         # dbqkv, so no per-step fp32 cat of the three weights); the GEMM runs on the fused bf16
         # compute copy wqkv_low and the fused fp32 bias bqkv of the backbone's pack
@@ -307,15 +309,17 @@ class AttnBlockFn(torch.autograd.Function):
         ctx.heads = heads
         ctx.box = box
         ctx.drop = drop
+        ctx.wts = wts  # (Wqkv^T, Wo^T) bf16 or None: not saved tensors (refreshed in place per step)
         return h
 
     @staticmethod
     def backward(ctx, dh):
         x, qkv, c, mask, wqkv_low, wo_low, wo = ctx.saved_tensors
+        wqkv_t, wo_t = ctx.wts
         dh = dh.contiguous()
         dbo = ctx.box.pop("colsum", None) if ctx.box is not None else None  # from LN1's backward
         dwo, dbo = wgrad(dh, c), (dbo if dbo is not None else bgrad(dh))
-        dc = dgrad(dh, wo_low)
+        dc = dgrad(dh, wo_low, wt=wo_t)
         dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
         dwqkv = wgrad(dqkv, x)
         if _QKV_BIAS_SHORTCUT and dqkv.is_cuda and ctx.drop is None:
@@ -337,11 +341,11 @@ class AttnBlockFn(torch.autograd.Function):
                                lib.colsum(dqkv[:, 2 * Dm:])])
         else:
             dbqkv = bgrad(dqkv)
-        dx = dgrad(dqkv, wqkv_low, residual=dh)  # residual + QKV dgrad in one GEMM (beta = 1)
+        dx = dgrad(dqkv, wqkv_low, residual=dh, wt=wqkv_t)  # residual + QKV dgrad in one GEMM (beta = 1)
         Dm = dwqkv.shape[0] // 3
         dw = [dwqkv[i * Dm:(i + 1) * Dm] for i in range(3)]
         db = [dbqkv[i * Dm:(i + 1) * Dm] for i in range(3)]
-        return (dx, *dw, *db, dwo, dbo) + (None,) * 7
+        return (dx, *dw, *db, dwo, dbo) + (None,) * 8
 
 
 class MLPBlockFn(torch.autograd.Function):
@@ -352,7 +356,7 @@ class MLPBlockFn(torch.autograd.Function):
     the residual gradient joins the FFN1 dgrad in its GEMM epilogue (beta = 1)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low, box=None, drop=None):
+    def forward(ctx, x, w1, b1, w2, b2, w1_low, w2_low, box=None, drop=None, wts=(None, None)):
         lib = ops.native.require_for(x)
         if box is not None and drop is not None:
             box["drop"] = drop  # LN2's backward applies this dropout's backward in its own pass
@@ -364,6 +368,7 @@ class MLPBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, f, z, w1_low, w2_low)
         ctx.box = box
         ctx.drop = drop
+        ctx.wts = wts  # (W1^T, W2^T) bf16 or None
         return h
 
     @staticmethod
@@ -384,16 +389,17 @@ class MLPBlockFn(torch.autograd.Function):
             # (dh W2) * GELU'(z) and its column sums from our GEMM's epilogue in one pass (the
             # aux-input epilogue makes that GEMM 650 us vs 480 for the forward FFN1 shape; the
             # "stream" form measured the same step time: bench_r1_cfg5_dzmode_ab.jsonl)
-            dz, db1 = lib.linear_gelu_bwd(dh, w2_low.t().contiguous(), z)
+            w2t = ctx.wts[1] if ctx.wts[1] is not None else w2_low.t().contiguous()
+            dz, db1 = lib.linear_gelu_bwd(dh, w2t, z)
             if db1 is None:
                 db1 = bgrad(dz)
         else:
             # library dF GEMM, then one streaming pass: dz = dF * GELU'(z) and its column sums
             # (the FFN1 bias gradient), deterministic partials
-            dz, db1 = lib.gelu_bwd_colsum(dgrad(dh, w2_low), z)
+            dz, db1 = lib.gelu_bwd_colsum(dgrad(dh, w2_low, wt=ctx.wts[1]), z)
         dw1 = wgrad(dz, x)
-        dx = dgrad(dz, w1_low, residual=dres)
-        return dx, dw1, db1, dw2, db2, None, None, None, None
+        dx = dgrad(dz, w1_low, residual=dres, wt=ctx.wts[0])
+        return dx, dw1, db1, dw2, db2, None, None, None, None, None
 
 
 class GeluFn(torch.autograd.Function):

@@ -74,19 +74,35 @@ class _StepGraph:
         static = Prepared(self.cand, self.his, (self.uniq, self.inv, self.perm, self.ptr), None, True)
         main = torch.cuda.current_stream(dev)
         eng.sync_params()
-        # warm up on a side stream (autograd / allocator state), then capture on it
+        # two graphs: (1) the parameter-free gather of the unique titles' cached hidden states,
+        # replayed BEFORE the step waits for the previous optimizer step, so the gradient
+        # all-reduce + Adam on the side stream overlap it; (2) the rest of the forward + backward
+        eng.hcache.ensure()
         side = torch.cuda.Stream(dev)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             for _ in range(2):
-                eng.forward_backward(self.cand, self.his, static)
+                self.hid = eng.hcache.rows(self.uniq)
         main.wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        # a private memory pool per graph (~250 MB of step activations at B = 64): sharing the
-        # first graph's pool (graph.pool()) trips an allocator assert in this torch build when
-        # eager steps of other engines run between the captures
-        with torch.cuda.graph(self.graph):
-            self.loss = eng.forward_backward(self.cand, self.his, static)
+        self.hid_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.hid_graph):
+            self.hid = eng.hcache.rows(self.uniq)
+        # warm up on a side stream (autograd / allocator state), then capture on it
+        eng._pre_hid = self.hid
+        try:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    eng.forward_backward(self.cand, self.his, static)
+            main.wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            # a private memory pool per graph (~250 MB of step activations at B = 64): sharing
+            # the first graph's pool (graph.pool()) trips an allocator assert in this torch build
+            # when eager steps of other engines run between the captures
+            with torch.cuda.graph(self.graph):
+                self.loss = eng.forward_backward(self.cand, self.his, static)
+        finally:
+            eng._pre_hid = None
 
     def load(self, pre: Prepared, U: int) -> None:
         """The batch into the static inputs: one multi-copy launch; the unique list is padded
@@ -141,6 +157,8 @@ class LocalEngine:
                            and os.environ.get("FEDREC_FUSED_USER", "1") != "0")
         self.user_drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 2
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
+        # hidden states of the step's unique titles gathered ahead (the step graph's first part)
+        self._pre_hid: Optional[torch.Tensor] = None
         self.hcache = self._make_hidden_cache()
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
@@ -237,7 +255,7 @@ class LocalEngine:
         mask only when the head uses it).  From the HBM cache when it is on; otherwise the
         frozen / unfrozen backbone runs on the titles."""
         if self.hcache is not None:
-            hid = self.hcache.rows(ids)
+            hid = self._pre_hid if self._pre_hid is not None else self.hcache.rows(ids)
             mask = self.tokens.index_select(0, ids.long())[:, 1, :] if self.cfg.mask_padding else None
             return hid, mask
         text = self.tokens.index_select(0, ids.long())
@@ -391,6 +409,7 @@ class LocalEngine:
             g = _StepGraph(self, pre, ucap)
             self._graphs[key] = g
         g.load(pre, U)
+        g.hid_graph.replay()  # parameter-free: runs while the previous all-reduce + Adam finish
         self.sync_params()
         g.graph.replay()
         return g.loss.clone()

@@ -434,6 +434,49 @@ def test_layer_norm_bwd(dev):
     assert rel_err(dx, xf.grad) < 1e-2 and rel_err(dw, wf.grad) < 1e-3 and rel_err(db, bf.grad) < 1e-4
 
 
+def test_layer_norm_bwd_drop(dev):
+    """LN backward with the dropout backward of the layer that fed it (config-5 LN2 after the
+    FFN dropout): dx as the plain kernel, dx o Z bit-equal to the separate dropout pass over
+    dx, and the fused column sums are those of dx o Z (the lin2 bias gradient)."""
+    x = (torch.randn(1000, 768, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    w = torch.randn(768, device=dev)
+    dy = torch.randn(1000, 768, device=dev).to(torch.bfloat16)
+    p, seed, off = 0.1, 99, 5
+    dx, dw, db = native.lib().layer_norm_bwd(x, w, dy, 1e-12)
+    dx2, dxz, dw2, db2, cs = native.lib().layer_norm_bwd_drop(x, w, dy, 1e-12, p, seed, off)
+    assert torch.equal(dx2, dx) and rel_err(dw2, dw) < 1e-5 and rel_err(db2, db) < 1e-5
+    assert torch.equal(dxz, ops.dropout_add(dx, None, p, seed, off))
+    assert rel_err(cs, dxz.float().sum(0)) < 1e-4
+    kept = float((dxz != 0).float().mean() / (dx != 0).float().mean())
+    assert 0.87 < kept < 0.93
+
+
+def test_multi_cast(dev):
+    """One-launch refresh of compute copies: fp32 masters -> bf16 (or fp32) destinations,
+    including slices of a fused destination, equal to .to(bf16) element for element."""
+    srcs = [torch.randn(768, 768, device=dev), torch.randn(768, device=dev), torch.randn(3072, 768, device=dev),
+            torch.randn(1000, 8, device=dev)]
+    fused = torch.empty(2 * 768, 768, device=dev, dtype=torch.bfloat16)
+    dsts = [fused[:768], torch.empty(768, device=dev), torch.empty(3072, 768, device=dev, dtype=torch.bfloat16),
+            fused[768:].view(-1)[:8000].view(1000, 8)]
+    assert native.lib().multi_cast(srcs, dsts)
+    for a, b in zip(srcs, dsts):
+        assert torch.equal(b, a.to(b.dtype))
+    many_s = [torch.randn(64, device=dev) for _ in range(130)]  # > 96 segments: several launches
+    many_d = [torch.empty(64, device=dev, dtype=torch.bfloat16) for _ in range(130)]
+    assert native.lib().multi_cast(many_s, many_d)
+    assert all(torch.equal(b, a.to(torch.bfloat16)) for a, b in zip(many_s, many_d))
+    assert not native.lib().multi_cast([torch.randn(12, device=dev)], [torch.empty(12, device=dev)])  # n % 8
+    # transposed: [R, C] fp32 -> bf16 [C, R] views, side by side in a fused [C, 3R] destination
+    ws = [torch.randn(768, 768, device=dev) for _ in range(3)] + [torch.randn(3072, 768, device=dev)]
+    fused_t = torch.empty(768, 3 * 768, device=dev, dtype=torch.bfloat16)
+    w1t = torch.empty(768, 3072, device=dev, dtype=torch.bfloat16)
+    dt = [fused_t[:, i * 768:(i + 1) * 768] for i in range(3)] + [w1t]
+    assert native.lib().multi_cast_t(ws, dt)
+    assert torch.equal(fused_t, torch.cat(ws, 0).to(torch.bfloat16).t())
+    assert torch.equal(w1t, ws[3].to(torch.bfloat16).t())
+
+
 def test_gelu_fwd_bwd(dev):
     z = (torch.randn(4096, device=dev) * 3).to(torch.bfloat16)
     dh = torch.randn(4096, device=dev).to(torch.bfloat16)
