@@ -21,58 +21,37 @@ __global__ __launch_bounds__(256) void score_ce_kernel(const float* __restrict__
   if (b >= B) return;
   const float* cb = cand + (size_t)b * C * D;
   const float* ub = user + (size_t)b * D;
-  // every per-candidate array is indexed by a compile-time c (loops unrolled to MAXC with a
-  // wave-uniform c < C guard): a runtime-indexed z[] / s[] / dz[] lives in scratch memory (the
-  // kernel took 18 us for 64 impressions that way)
   float z[MAXC];
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    z[c] = 0.f;
-    if (c < C) {
-      float a = 0.f;
-      for (int d = lane; d < D; d += 64) a += cb[(size_t)c * D + d] * ub[d];
-      z[c] = a;
-    }
+  for (int c = 0; c < C; ++c) {
+    float s = 0.f;
+    for (int d = lane; d < D; d += 64) s += cb[(size_t)c * D + d] * ub[d];
+    z[c] = wave_sum(s);
   }
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c)
-    if (c < C) z[c] = wave_sum(z[c]);
   float s[MAXC], mx = -INFINITY;
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    s[c] = 0.f;
-    if (c < C) {
-      s[c] = sigm ? 1.0f / (1.0f + __expf(-z[c])) : z[c];
-      mx = fmaxf(mx, s[c]);
-    }
+  for (int c = 0; c < C; ++c) {
+    s[c] = sigm ? 1.0f / (1.0f + __expf(-z[c])) : z[c];
+    mx = fmaxf(mx, s[c]);
   }
   float se = 0.f;
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c)
-    if (c < C) se += __expf(s[c] - mx);
+  for (int c = 0; c < C; ++c) se += __expf(s[c] - mx);
   const float lse = mx + __logf(se);
   if (lane == 0) {
     loss[b] = (lse - s[0]) / (float)B;  // per-impression share; the caller sums in a fixed order
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < C) scores[(size_t)b * C + c] = s[c];
+    for (int c = 0; c < C; ++c) scores[(size_t)b * C + c] = s[c];
   }
   float dz[MAXC];
   const float invB = 1.0f / (float)B;
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    const float ds = (__expf(s[c] - mx) / se - (c == 0 ? 1.f : 0.f)) * invB;
-    dz[c] = c < C ? (sigm ? ds * s[c] * (1.f - s[c]) : ds) : 0.f;
+  for (int c = 0; c < C; ++c) {
+    float ds = (__expf(s[c] - mx) / se - (c == 0 ? 1.f : 0.f)) * invB;
+    dz[c] = sigm ? ds * s[c] * (1.f - s[c]) : ds;
   }
   for (int d = lane; d < D; d += 64) {
     const float ud = ub[d];
     float du = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < C) {
-        du += dz[c] * cb[(size_t)c * D + d];
-        dcand[((size_t)b * C + c) * D + d] = dz[c] * ud;
-      }
+    for (int c = 0; c < C; ++c) {
+      du += dz[c] * cb[(size_t)c * D + d];
+      dcand[((size_t)b * C + c) * D + d] = dz[c] * ud;
+    }
     duser[(size_t)b * D + d] = du;
   }
 }

@@ -174,7 +174,8 @@ class Backbone(nn.Module):
         # W^T), refreshed in the same step by one transposing launch (multi_cast_t) instead of
         # a `.t().contiguous()` copy per weight in every backward
         self._cast_plan_t = None
-        if not self.cfg.frozen and dev.type == "cuda" and dtype == torch.bfloat16:
+        if (not self.cfg.frozen and dev.type == "cuda" and dtype == torch.bfloat16
+                and os.environ.get("FEDREC_WT_CACHE", "1") != "0"):
             srct, dstt = [], []
             for blk, L in zip(self.transformer.layer, pack["layers"]):
                 a = blk.attention

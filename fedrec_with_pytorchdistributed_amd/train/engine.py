@@ -79,16 +79,21 @@ class _StepGraph:
         # all-reduce + Adam on the side stream overlap it; (2) the rest of the forward + backward
         eng.hcache.ensure()
         side = torch.cuda.Stream(dev)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            for _ in range(2):
+        self.hid_graph = None
+        # (on with a gradient all-reduce only: at one client there is only Adam (7 us) to hide,
+        # and the extra replay measured neutral: 66.86k vs 67.15k imp/s, r2_bench_batch6.jsonl)
+        split = os.environ.get("FEDREC_SPLIT_GRAPH", "auto")
+        if split == "on" or (split == "auto" and eng.grad_allreduce is not None):
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self.hid = eng.hcache.rows(self.uniq)
+            main.wait_stream(side)
+            self.hid_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.hid_graph):
                 self.hid = eng.hcache.rows(self.uniq)
-        main.wait_stream(side)
-        self.hid_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.hid_graph):
-            self.hid = eng.hcache.rows(self.uniq)
+            eng._pre_hid = self.hid
         # warm up on a side stream (autograd / allocator state), then capture on it
-        eng._pre_hid = self.hid
         try:
             side.wait_stream(main)
             with torch.cuda.stream(side):
@@ -409,7 +414,8 @@ class LocalEngine:
             g = _StepGraph(self, pre, ucap)
             self._graphs[key] = g
         g.load(pre, U)
-        g.hid_graph.replay()  # parameter-free: runs while the previous all-reduce + Adam finish
+        if g.hid_graph is not None:
+            g.hid_graph.replay()  # parameter-free: runs while the previous all-reduce + Adam finish
         self.sync_params()
         g.graph.replay()
         return g.loss.clone()

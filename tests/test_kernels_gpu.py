@@ -473,7 +473,7 @@ def test_multi_cast(dev):
     w1t = torch.empty(768, 3072, device=dev, dtype=torch.bfloat16)
     dt = [fused_t[:, i * 768:(i + 1) * 768] for i in range(3)] + [w1t]
     assert native.lib().multi_cast_t(ws, dt)
-    assert torch.equal(fused_t, torch.cat(ws, 0).to(torch.bfloat16).t())
+    assert torch.equal(fused_t, torch.cat(ws[:3], 0).to(torch.bfloat16).t())
     assert torch.equal(w1t, ws[3].to(torch.bfloat16).t())
 
 
