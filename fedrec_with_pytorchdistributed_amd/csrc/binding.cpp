@@ -48,7 +48,7 @@ int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, 
 int fr_segsum_chunks(int R);
 void fr_segsum_set_variant(int v);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
-                unsigned long long offset, hipStream_t s);
+                unsigned long long offset, hipStream_t s, const unsigned long long* dev_off);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
@@ -458,7 +458,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Te
 
 at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, const at::Tensor& seg_ptr, int64_t num_out,
                             double clip, double noise_std, int64_t seed, int64_t offset,
-                            const c10::optional<at::Tensor>& inv, bool zero_empty) {
+                            const c10::optional<at::Tensor>& inv, bool zero_empty,
+                            const c10::optional<at::Tensor>& dev_off) {
   check_dev(rows, "rows");
   check_dev(perm, "perm");
   check_dev(seg_ptr, "seg_ptr");
@@ -473,8 +474,14 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
   at::Tensor src = rows;
   if (clip > 0.0 || noise_std > 0.0) {  // LDP: clip + noise every occurrence first (parallel pass)
     src = at::empty_like(rows);
+    const unsigned long long* dop = nullptr;
+    if (dev_off.has_value() && dev_off->defined()) {  // device step counter (graph replays: fresh noise)
+      check_dev(*dev_off, "dev_off");
+      TORCH_CHECK(dev_off->scalar_type() == at::kLong && dev_off->numel() == 1, "fedrec::segment_sum_rows: dev_off int64[1]");
+      dop = (const unsigned long long*)dev_off->data_ptr();
+    }
     check_rc(fr_ldp_rows(rows.data_ptr<float>(), src.data_ptr<float>(), (int)(rows.numel() / D), (int)D, (float)clip,
-                         (float)noise_std, (unsigned long long)seed, (unsigned long long)offset, cur_stream()),
+                         (float)noise_std, (unsigned long long)seed, (unsigned long long)offset, cur_stream(), dop),
              "ldp_rows");
   }
   const int64_t R = perm.numel();
@@ -1137,7 +1144,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim) -> (Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False) -> Tensor");
+  m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset) -> (Tensor, Tensor)");

@@ -27,7 +27,11 @@ constexpr int UNR = 4;    // rows in flight per wave
 // Box-Muller), counter = (row, element group of 4): independent of the launch geometry.
 __global__ __launch_bounds__(256) void ldp_rows_kernel(const float* __restrict__ rows, float* __restrict__ out, int R,
                                                        int D, float clip, float noise_std, unsigned long long seed,
-                                                       unsigned long long offset) {
+                                                       unsigned long long offset,
+                                                       const unsigned long long* __restrict__ dev_off) {
+  // dev_off (optional): a device step counter added to the offset, so a captured HIP graph
+  // draws fresh noise at every replay (the host offset is frozen into the graph)
+  if (dev_off != nullptr) offset += *dev_off;
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
@@ -213,11 +217,12 @@ extern "C" void fr_segsum_set_variant(int v) { g_segsum_variant = v; }
 extern "C" int fr_segsum_chunks(int R) { return (R + SCH - 1) / SCH; }
 
 extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std,
-                           unsigned long long seed, unsigned long long offset, hipStream_t s) {
+                           unsigned long long seed, unsigned long long offset, hipStream_t s,
+                           const unsigned long long* dev_off) {
   if (D > 64 * MAXV) return 1;
   if (R == 0) return 0;
   hipLaunchKernelGGL(ldp_rows_kernel, dim3((R + 3) / 4), dim3(256), 0, s, rows, out, R, D, clip, noise_std, seed,
-                     offset);
+                     offset, dev_off);
   return 0;
 }
 

@@ -188,13 +188,15 @@ def score_ce(cand, user, act: str = "sigmoid"):
 
 
 def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: float = 0.0,
-                     seed: int = 0, offset: int = 0, generator=None, seg=None, zero_empty: bool = False):
+                     seed: int = 0, offset: int = 0, generator=None, seg=None, zero_empty: bool = False,
+                     dev_off=None):
     """Per-news gradient reduction ``out[inv[r]] += clip(rows[r]) + N(0, noise_std)``.
 
     ``seg = (perm, seg_ptr)`` (rows grouped by output id) enables the deterministic,
     atomic-free device kernel; it is produced by :func:`dedup`.  The device kernel expects
     the layout dedup produces: every output row has occurrences, except trailing padded rows
-    (``zero_empty``, the step graphs' padded unique lists).
+    (``zero_empty``, the step graphs' padded unique lists).  ``dev_off`` (device int64[1]):
+    added to ``offset`` on the device, so a captured step graph draws fresh noise per replay.
     """
     if _dev(rows):
         if seg is None:
@@ -205,7 +207,9 @@ def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: floa
         inv32 = inv32 if inv32.dtype == torch.int32 else inv32.to(torch.int32)
         return native.require_for(rows).segment_sum_rows(rows.float().contiguous(), perm, ptr, int(num_out),
                                                          float(clip), float(noise_std), int(seed), int(offset),
-                                                         inv32.contiguous(), bool(zero_empty))
+                                                         inv32.contiguous(), bool(zero_empty), dev_off)
+    if dev_off is not None:
+        offset = int(offset) + int(dev_off.reshape(-1)[0])
     if noise_std > 0 and generator is None:
         generator = torch.Generator().manual_seed((int(seed) * 1_000_003 + int(offset)) & 0x7FFFFFFFFFFF)
     return ref.segment_sum_rows(rows, inv, num_out, clip, noise_std, generator)

@@ -516,7 +516,8 @@ class UserStepFn(torch.autograd.Function):
         BC, BH = B * C, B * H
         Qd = w1.shape[0]
         his_idx = inv[BC:]
-        cand = v.index_select(0, inv[:BC].long()).view(B, C, D)
+        ci = inv[:BC]
+        cand = v.index_select(0, ci if ci.dtype in (torch.int32, torch.int64) else ci.long()).view(B, C, D)
         qkv = torch.empty(BH, 3 * D, device=v.device, dtype=torch.float32)
         p, seed, off = drop
         # X' = drop(v[his]) once (5 MB): the Q/K/V projection and the weight gradients read it
@@ -573,7 +574,9 @@ class UserStepFn(torch.autograd.Function):
         ops.colsum_f32([(dqkv[:, 0:D], gbq, BH, D, 3 * D), (dqkv[:, D:2 * D], gbk, BH, D, 3 * D),
                         (dqkv[:, 2 * D:], gbv, BH, D, 3 * D), (dpre2, gb1, BH, Qd, Qd)])
         clip, noise, lseed, loff = ldp
-        dv = ops.segment_sum_rows(rows, inv, v.shape[0], clip, noise, lseed, loff, seg=(perm, ptr), zero_empty=padded)
+        # the noise offset's step part is the device counter (dev_off): graph replays draw fresh noise
+        dv = ops.segment_sum_rows(rows, inv, v.shape[0], clip, noise, lseed, loff, seg=(perm, ptr), zero_empty=padded,
+                                  dev_off=dev_off if noise > 0 else None)
         return (dv, None, None, None, gq, gbq, gk, gbk, gv, gbv, gw1, gb1, dw2.view(1, -1), db2.view(1), None)
 
 

@@ -161,6 +161,8 @@ class LocalEngine:
                            and ue.multihead_attention.n_heads * ue.multihead_attention.d_k == cfg.news_dim
                            and os.environ.get("FEDREC_FUSED_USER", "1") != "0")
         self.user_drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 2
+        # LDP noise: its own Philox key per client (disjoint from the dropout keys above)
+        self.ldp_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 3
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
         # hidden states of the step's unique titles gathered ahead (the step graph's first part)
         self._pre_hid: Optional[torch.Tensor] = None
@@ -171,7 +173,7 @@ class LocalEngine:
         # HIP graphs of the per-step forward + backward (see _graph_step)
         sg = os.environ.get("FEDREC_STEP_GRAPH", cfg.step_graph)
         self.step_graphs = device.type == "cuda" and self.hcache is not None and (
-            sg == "on" or (sg == "auto" and not cfg.dp.enabled))
+            sg == "on" or (sg == "auto" and (self.fused_user or not cfg.dp.enabled)))
         self._graphs: Dict[tuple, "_StepGraph"] = {}
         self.last_stats: Dict[str, float] = {}
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
@@ -195,10 +197,12 @@ class LocalEngine:
     def state(self) -> Dict[str, int]:
         """Counters that key the engine's randomness (checkpointed with the snapshot)."""
         return {"noise_offset": self.noise_offset, "epoch": self.epoch,
-                "drop_calls": self.model.text_encoder.DistillBert._drop_calls}
+                "drop_calls": self.model.text_encoder.DistillBert._drop_calls,
+                "rng_step": int(self._rng_step.item())}
 
     def load_state(self, st: Dict[str, int]) -> None:
         self.noise_offset = int(st.get("noise_offset", self.noise_offset))
+        self._rng_step.fill_(int(st.get("rng_step", 0)))  # user-dropout / LDP-noise step counter
         self.epoch = int(st.get("epoch", self.epoch))
         self.model.text_encoder.DistillBert._drop_calls = int(st.get("drop_calls", 0))
 
@@ -316,7 +320,7 @@ class LocalEngine:
             v = v.detach().requires_grad_(True)
         clip, std = self._ldp()
         padded = pre is not None and pre.padded
-        rows = OF.news_gather(v, inv, perm, ptr, clip, std, self.cfg.seed * 7919 + self.rank, self.noise_offset, padded)
+        rows = OF.news_gather(v, inv, perm, ptr, clip, std, self.ldp_seed, (1 << 40) + self.noise_offset, padded)
         self.noise_offset += 1
         cand_v = rows[: B * C].view(B, C, -1)
         his_v = rows[B * C:].view(B, H, -1)
@@ -327,7 +331,11 @@ class LocalEngine:
         uniq, inv, perm, ptr = dd
         p = float(self.cfg.user_dropout) if train else 0.0
         clip, std = self._ldp()
-        ldp = (clip, std, self.cfg.seed * 7919 + self.rank, self.noise_offset)
+        # the fused path's noise offset is the device step counter alone (_rng_step, advanced once per
+        # step inside the step graph too): the host part is a constant, so eager and replayed steps
+        # never reuse an offset; the non-fused path (news_gather) keeps the host counter, offset
+        # past 2^40 so the two streams cannot meet
+        ldp = (clip, std, self.ldp_seed, 0)
         if train:
             self.noise_offset += 1
         return OF.user_step(v, inv, perm, ptr, self.model.user_encoder, B, C, H, self.score_act,
@@ -376,7 +384,10 @@ class LocalEngine:
         return loss
 
     def train_prepared(self, pre: Prepared) -> torch.Tensor:
-        if self.step_graphs and pre.dedup is not None and not (self.cfg.dp.enabled and self.sigma):
+        # LDP: the fused user step draws its noise at a device-counter offset, so it replays fresh
+        # noise; the non-fused path's host offset would be frozen into the graph
+        if self.step_graphs and pre.dedup is not None and not (self.cfg.dp.enabled and self.sigma
+                                                               and not self.fused_user):
             loss = self._graph_step(pre)
             if loss is not None:
                 self.optimizer_step(overlap=True)

@@ -82,4 +82,5 @@ class HiddenCache:
     def rows(self, ids: torch.Tensor) -> torch.Tensor:
         """Hidden states ``[n, T, D]`` of the titles ``ids [n]``."""
         self.ensure()
-        return self.table.index_select(0, ids.long())
+        # int32 / int64 ids index directly (a .long() would be one more launch per step)
+        return self.table.index_select(0, ids if ids.dtype in (torch.int32, torch.int64) else ids.long())

@@ -58,11 +58,40 @@ def test_graph_step_matches_eager(dev):
     assert float((g1 - g0).norm()) <= 2e-2 * float(g0.norm()) + 1e-8
 
 
-def test_graph_off_with_ldp_noise(dev):
+def test_graph_with_ldp_noise_draws_fresh_noise(dev):
+    """LDP under the captured step: the fused user step's noise offset is the device step
+    counter, so every replay draws fresh noise (the host offset would be frozen in the graph).
+    Two replays of the same batch give different gradients, and a graph step equals the eager
+    step at the same counter value (same Philox draws)."""
     cfg = FedRecConfig(mode="grad_avg", batch_size=8)
     cfg.backbone = BackboneConfig(name="distilbert-2l", n_layers=2)
     cfg.dp.enabled = True
-    m = FedRecModel(cfg).to(dev)
-    m.build_flat()
-    e = LocalEngine(cfg, m, make_client_shards("tiny", 1)[0], dev)
-    assert not e.step_graphs  # the LDP Philox offset advances per step on the host
+    shard = make_client_shards("tiny", 1)[0]
+    engines = []
+    for graphs in ("on", "off"):
+        torch.manual_seed(0)
+        c = copy.deepcopy(cfg)
+        c.step_graph = graphs
+        m = FedRecModel(c).to(dev)
+        m.build_flat()
+        e = LocalEngine(c, m, shard, dev)
+        e.sigma = 1.0
+        e.build_cache()
+        engines.append(e)
+    eg, ee = engines
+    assert eg.step_graphs and eg.fused_user
+    cand, his = next(iter(eg.sampler.epoch(0)))
+    torch.cuda.synchronize()
+    pre = eg.prepare(lambda: (cand, his))
+    lg = eg._graph_step(pre)
+    assert lg is not None and len(eg._graphs) == 1
+    g1 = eg.model.flat.grad.clone()
+    eg._graph_step(pre)  # same batch, next counter value: fresh noise
+    g2 = eg.model.flat.grad.clone()
+    assert float((g1 - g2).norm()) > 1e-6 * float(g1.norm())
+    # eager step at the same counter as the second replay: same noise, same gradient
+    pre2 = ee.prepare(lambda: (cand, his))
+    ee._rng_step.fill_(int(eg._rng_step.item()) - 1)
+    ee.forward_backward(pre2.cand, pre2.his, pre2)
+    ge = ee.model.flat.grad
+    assert float((ge - g2).norm()) <= 2e-2 * float(g2.norm()) + 1e-8
