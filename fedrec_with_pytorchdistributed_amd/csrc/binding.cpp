@@ -44,7 +44,7 @@ int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, fl
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
                 int C, int D, int sigm, hipStream_t s);
 int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U, int D,
-                        int R, float* scratch, hipStream_t s);
+                        int R, float* scratch, hipStream_t s, int zero_empty);
 int fr_segsum_chunks(int R);
 void fr_segsum_set_variant(int v);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
@@ -468,9 +468,9 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
   TORCH_CHECK(seg_ptr.numel() == num_out + 1, "fedrec::segment_sum_rows: seg_ptr size");
   const c10::DeviceGuard g(rows.device());
   const int64_t D = rows.size(-1);
-  // the kernels write only rows whose segment has occurrences; zero_empty (padded unique
-  // lists of the step graphs) clears the rest first
-  auto out = zero_empty ? at::zeros({num_out, D}, rows.options()) : at::empty({num_out, D}, rows.options());
+  // empty segments (padded unique lists of the step graphs) come out as zero rows: the chunked
+  // kernel writes them itself (no separate fill launch), the block-per-row form clears first
+  auto out = at::empty({num_out, D}, rows.options());
   at::Tensor src = rows;
   if (clip > 0.0 || noise_std > 0.0) {  // LDP: clip + noise every occurrence first (parallel pass)
     src = at::empty_like(rows);
@@ -494,7 +494,7 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
   }
   check_rc(fr_segment_sum_rows(src.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(), invp,
                                out.data_ptr<float>(), (int)num_out, (int)D, (int)R, scratch.data_ptr<float>(),
-                               cur_stream()),
+                               cur_stream(), zero_empty ? 1 : 0),
            "segment_sum_rows");
   return out;
 }

@@ -180,6 +180,10 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int u = blockIdx.x;
   const int beg = seg_ptr[u], end = seg_ptr[u + 1];
+  if (beg == end) {  // no occurrences (a padded unique slot of a step graph): a zero row
+    for (int d = threadIdx.x; d < D; d += 256) out[(size_t)u * D + d] = 0.f;
+    return;
+  }
   const int c0 = beg / SCH, c1 = (end - 1) / SCH;
   if (c0 == c1) return;  // written whole by the chunk pass (block-uniform exit)
   const int n = c1 - c0 + 1;
@@ -227,8 +231,10 @@ extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float cl
 }
 
 // scratch: fr_segsum_chunks(R) * 2 * D floats (chunked form); R = total occurrences = seg_ptr[U]
+// Rows of empty segments: the chunked form writes them as zeros (its fix pass); the
+// block-per-row form needs zero_empty = 1 to clear the output first.
 extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out,
-                                   int U, int D, int R, float* scratch, hipStream_t s) {
+                                   int U, int D, int R, float* scratch, hipStream_t s, int zero_empty) {
   if (D > 64 * MAXV) return 1;
   if (U == 0) return 0;
   if (g_segsum_variant == 1 && scratch != nullptr && inv != nullptr && R > 0) {
@@ -238,6 +244,7 @@ extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int
     hipLaunchKernelGGL(segsum_fix_kernel, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
     return 0;
   }
+  if (zero_empty) (void)hipMemsetAsync(out, 0, (size_t)U * D * sizeof(float), s);
   hipLaunchKernelGGL(segsum_kernel, dim3(U), dim3(1024), 0, s, rows, perm, seg_ptr, out, U, D);
   return 0;
 }

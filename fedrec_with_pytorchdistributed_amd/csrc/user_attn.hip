@@ -188,8 +188,8 @@ __global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restri
 // the dot products split into 4 partial sums (chains of 5), and the scores stay in registers
 // (one dot product per key instead of two): 20 us (profiles/r2_user_attn_ilp_bench.json).
 // Same math (fp32; only the summation order inside a 20-term dot product differs).  The same
-// treatment of the backward measured slower (63 vs 54 us: 141 VGPRs, half the occupancy) and
-// is not used.
+// treatment of the backward measured slower (63 vs 54 us), and so did an unroll-by-4 form
+// with split dot products (64 vs 56 us, 256 VGPRs); the backward keeps its first form.
 __device__ __forceinline__ void load_row_s(float (&x)[DK], const float* __restrict__ p, float sc) {
 #pragma unroll
   for (int c4 = 0; c4 < DK / 4; ++c4) {
@@ -266,95 +266,7 @@ __global__ __launch_bounds__(128) void user_attn_fwd_ilp_kernel(const float* __r
   st[1] = inv;
 }
 
-// Backward with the key / query loops unrolled by 4 and 4-way split dot products (a full
-// unroll measured slower: 63 vs 54 us, likely the ~20k-instruction body).
-__global__ __launch_bounds__(64) void user_attn_bwd_u4_kernel(const float* __restrict__ qkv, const float* __restrict__ stats,
-                                                           const float* __restrict__ dctx, float* __restrict__ dqkv,
-                                                           int B, int H, int NH) {
-  __shared__ __attribute__((aligned(16))) float qs[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float ks[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float vs[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float gs[MAXH][DK];
-  __shared__ float ms[MAXH], is_[MAXH], Ds[MAXH];
-  const int lane = threadIdx.x;
-  const int pair = blockIdx.x;
-  const int b = pair / NH, h = pair - b * NH;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  const float* gb = dctx + (size_t)b * H * D + h * DK;
-  for (int i = lane; i < H * DK / 4; i += 64) {
-    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
-    *(float4*)&qs[r][c] = *(const float4*)(base + (size_t)r * ld + c);
-    *(float4*)&ks[r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
-    *(float4*)&vs[r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
-    *(float4*)&gs[r][c] = *(const float4*)(gb + (size_t)r * D + c);
-  }
-  const float* st = stats + ((size_t)b * NH + h) * H * 2;
-  for (int t = lane; t < H; t += 64) {
-    ms[t] = st[2 * t];
-    is_[t] = st[2 * t + 1];
-  }
-  __syncthreads();
-  const float scale = rsqrtf((float)DK);
-  float* dbase = dqkv + (size_t)b * H * ld + h * DK;
-  if (lane < H) {
-    const int t = lane;
-    const float m = ms[t], inv = is_[t];
-    float q[DK], g[DK], u[DK], w[DK];
-#pragma unroll
-    for (int c = 0; c < DK; ++c) {
-      q[c] = qs[t][c] * scale;
-      g[c] = gs[t][c];
-      u[c] = w[c] = 0.f;
-    }
-    float Dt = 0.f;
-#pragma unroll 4
-    for (int s = 0; s < H; ++s) {
-      const float A = __expf(dot20x(q, &ks[s][0]) - m) * inv;
-      const float dA = dot20x(g, &vs[s][0]);
-      Dt += A * dA;
-      axpy20(u, A * dA, &ks[s][0]);
-      axpy20(w, A, &ks[s][0]);
-    }
-    Ds[t] = Dt;
-    float* o = dbase + (size_t)t * ld;
-#pragma unroll
-    for (int c4 = 0; c4 < DK / 4; ++c4) {
-      const int c = 4 * c4;
-      *(float4*)(o + c) = make_float4(scale * (u[c] - Dt * w[c]), scale * (u[c + 1] - Dt * w[c + 1]),
-                                      scale * (u[c + 2] - Dt * w[c + 2]), scale * (u[c + 3] - Dt * w[c + 3]));
-    }
-  }
-  __syncthreads();
-  if (lane < H) {
-    const int s = lane;
-    float k[DK], v[DK], dk[DK], dv[DK];
-#pragma unroll
-    for (int c = 0; c < DK; ++c) {
-      k[c] = ks[s][c] * scale;
-      v[c] = vs[s][c];
-      dk[c] = dv[c] = 0.f;
-    }
-#pragma unroll 4
-    for (int t = 0; t < H; ++t) {
-      const float A = __expf(dot20x(k, &qs[t][0]) - ms[t]) * is_[t];
-      const float dA = dot20x(v, &gs[t][0]);
-      const float dS = A * (dA - Ds[t]) * scale;
-      axpy20(dk, dS, &qs[t][0]);
-      axpy20(dv, A, &gs[t][0]);
-    }
-    float* o = dbase + (size_t)s * ld;
-#pragma unroll
-    for (int c4 = 0; c4 < DK / 4; ++c4) {
-      const int c = 4 * c4;
-      *(float4*)(o + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
-      *(float4*)(o + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
-    }
-  }
-}
-
-
-int g_ua_variant = 1;  // 1: ILP forward (default), 0: the first forward, 2: + the unroll-4 backward
+int g_ua_variant = 1;  // 1: ILP forward (default), 0: the first forward
 
 // ---------------------------------------------------------------------------------------
 // Long histories (H > 64): the reference pads but never truncates (dataset.py:84, quirk Q6;
@@ -539,7 +451,7 @@ extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int 
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH);
-  else if (g_ua_variant >= 1)
+  else if (g_ua_variant == 1)
     hipLaunchKernelGGL(user_attn_fwd_ilp_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
   else
     hipLaunchKernelGGL(user_attn_fwd_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
@@ -553,8 +465,6 @@ extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const floa
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
-  else if (g_ua_variant == 2)
-    hipLaunchKernelGGL(user_attn_bwd_u4_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   else
     hipLaunchKernelGGL(user_attn_bwd_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   return 0;

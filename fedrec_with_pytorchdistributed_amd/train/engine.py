@@ -58,6 +58,13 @@ class Prepared(NamedTuple):
     padded: bool = False  # dedup's unique list padded with rows no occurrence maps to (step graphs)
 
 
+# "thread_local": only this thread's unsafe calls are refused during a capture -- the RCCL
+# process group's watchdog thread keeps polling its work events (a multi-client run captures
+# its step graphs while collectives of other steps are tracked); "global" would turn those polls
+# into capture failures
+_CAPTURE_MODE = os.environ.get("FEDREC_CAPTURE_MODE", "thread_local")
+
+
 class _StepGraph:
     """Static inputs + the captured graph of one (batch shape, unique-title bucket)."""
 
@@ -90,7 +97,7 @@ class _StepGraph:
                     self.hid = eng.hcache.rows(self.uniq)
             main.wait_stream(side)
             self.hid_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.hid_graph):
+            with torch.cuda.graph(self.hid_graph, capture_error_mode=_CAPTURE_MODE):
                 self.hid = eng.hcache.rows(self.uniq)
             eng._pre_hid = self.hid
         # warm up on a side stream (autograd / allocator state), then capture on it
@@ -104,7 +111,7 @@ class _StepGraph:
             # a private memory pool per graph (~250 MB of step activations at B = 64): sharing
             # the first graph's pool (graph.pool()) trips an allocator assert in this torch build
             # when eager steps of other engines run between the captures
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
                 self.loss = eng.forward_backward(self.cand, self.his, static)
         finally:
             eng._pre_hid = None

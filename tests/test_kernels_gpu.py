@@ -155,7 +155,7 @@ def test_additive_pool(dev, dtype, D, Q):
     assert abs(float(db2_n) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
 
 
-@pytest.mark.parametrize("variant", [1, 0, 2])
+@pytest.mark.parametrize("variant", [1, 0])
 @pytest.mark.parametrize("H", [1, 50, 64, 65, 76, 200])
 def test_user_attention(dev, H, variant):
     """H > 64 runs the long-history kernels (online softmax over 64-row LDS chunks): the
