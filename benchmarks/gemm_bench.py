@@ -71,6 +71,8 @@ def main():
                 variants["ours-pingpong-v10-deferred"] = ours(10)
             if a.diag:
                 variants["diag-pingpong-nostore"] = ours(7)
+        elif N % 128 == 0 and N > 256:  # text head N = 384: ping-pong with a partial last column tile
+            variants["ours-pingpong-v9-partial"] = ours(9)
         bb = b.to(torch.bfloat16)
 
         def lt():
