@@ -544,6 +544,7 @@ def test_snapshot_restores_adam_rng_and_engine_counters(tmp_path):
     e = LocalEngine(cfg, m, shard, torch.device("cpu"))
     e.train_epoch(max_steps=2)
     e.noise_offset = 17
+    e._rng_step.fill_(41)  # the device step counter keying user dropout and LDP noise
     path = str(tmp_path / "client0_snapshot.pt")
     ckpt.save_snapshot(path, m, 0, round_idx=3, engine=e.state())
     after_save = torch.rand(4)
@@ -559,6 +560,7 @@ def test_snapshot_restores_adam_rng_and_engine_counters(tmp_path):
     assert torch.equal(m2.flat.m, m.flat.m) and torch.equal(m2.flat.v, m.flat.v)
     assert torch.equal(m2.flat.flat, m.flat.flat)
     assert e2.noise_offset == 17
+    assert int(e2._rng_step.item()) == 41
     assert ckpt.client_snapshot_path("/x/snapshot.pt", 3) == "/x/client3_snapshot.pt"
 
 
