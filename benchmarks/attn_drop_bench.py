@@ -55,24 +55,30 @@ def main():
         lib.title_attn_set_waves(w)
         return lib.title_attention_drop(qkv, mask, H, p, seed, off)
 
-    def bwd(v):
+    def bwd(v, split=1):
+        lib.title_attn_bwd_set_variant(10 + split)  # the dropout backward's prefetch form
         lib.title_attn_bwd_set_variant(v)
         return lib.title_attention_bwd_drop(qkv, dout, mask, H, p, seed, off)
 
     # same outputs from every form
     o_p, o_1 = fwd(-2).float(), fwd(2).float()
     g_p, g_1 = bwd(1).float(), bwd(0).float()
+    g_n = bwd(1, 0).float()
     res = {"fwd_max_abs_diff": float((o_p - o_1).abs().max()),
            "bwd_max_abs_diff": float((g_p - g_1).abs().max()),
-           "bwd_rel_l2": float((g_p - g_1).norm() / g_1.norm())}
+           "bwd_rel_l2": float((g_p - g_1).norm() / g_1.norm()),
+           "bwd_split_vs_nosplit_max_abs_diff": float((g_p - g_n).abs().max())}
     print(res, flush=True)
-    times = {"fwd_persistent": [], "fwd_oneshot": [], "bwd_persistent": [], "bwd_oneshot": []}
+    times = {"fwd_persistent": [], "fwd_oneshot": [], "bwd_persistent": [], "bwd_persistent_nosplit": [],
+             "bwd_oneshot": []}
     for _ in range(a.rounds):
         times["fwd_persistent"].append(timeit(lambda: fwd(-2)))
         times["fwd_oneshot"].append(timeit(lambda: fwd(2)))
         times["bwd_persistent"].append(timeit(lambda: bwd(1)))
+        times["bwd_persistent_nosplit"].append(timeit(lambda: bwd(1, 0)))
         times["bwd_oneshot"].append(timeit(lambda: bwd(0)))
     lib.title_attn_set_waves(-2)
+    lib.title_attn_bwd_set_variant(11)
     lib.title_attn_bwd_set_variant(1)
     fbytes = M * 4 * D * 2  # read qkv, write out
     bbytes = M * 8 * D * 2  # read qkv + dout, write dqkv

@@ -271,6 +271,7 @@ struct TBIn {
 // element index of (row r, column c) in a swizzled [64][64] bf16 tile
 __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((((c >> 3) ^ (r & 7)) << 3) | (c & 7)); }
 
+template <int PART = 0>
 __device__ __forceinline__ void tb_load(TBIn& in, const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                         const int* __restrict__ mask, int pair, int T, int H, int D, int lane) {
   const int title = pair / H, h = pair - title * H;
@@ -278,25 +279,33 @@ __device__ __forceinline__ void tb_load(TBIn& in, const bf16* __restrict__ qkv, 
   const int ld = 3 * D;
   const bf16* qb = qkv + row0 * ld + h * DH;
   const bf16* gb = dout + row0 * D + h * DH;
+  const int part = PART;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {  // unconditional (rows clamped): see title_attn.hip on vmcnt drains
     const int idx = c * 64 + lane;
     int r = idx >> 3;
     r = r < T ? r : T - 1;
     const int ch = idx & 7;
-    in.q[c] = *(const bf16x8*)(qb + (size_t)r * ld + ch * 8);
-    in.k[c] = *(const bf16x8*)(qb + D + (size_t)r * ld + ch * 8);
-    in.v[c] = *(const bf16x8*)(qb + 2 * D + (size_t)r * ld + ch * 8);
-    in.g[c] = *(const bf16x8*)(gb + (size_t)r * D + ch * 8);
+    if (part != 2) {
+      in.q[c] = *(const bf16x8*)(qb + (size_t)r * ld + ch * 8);
+      in.k[c] = *(const bf16x8*)(qb + D + (size_t)r * ld + ch * 8);
+    }
+    if (part != 1) {
+      in.v[c] = *(const bf16x8*)(qb + 2 * D + (size_t)r * ld + ch * 8);
+      in.g[c] = *(const bf16x8*)(gb + (size_t)r * D + ch * 8);
+    }
   }
-  in.mk = mask[row0 + (lane < T ? lane : T - 1)];
+  if (part != 2) in.mk = mask[row0 + (lane < T ? lane : T - 1)];
 }
 
 // DROP: as title_attn_bwd_kernel<true> (the forward's Philox mask regenerated per element,
 // kept as 16-bit keep words per query: per-element scale arrays across the softmax spill).
 // Reading keep bits stored by the forward instead (8 B per lane and pair) measured slower:
 // 523 vs 437 us (profiles/r2_attn_drop_bits_bench.json) -- the bit unpacking spilled more.
-template <bool DROP>
+// SPLIT: the next pair's Q / K are prefetched before dQ and its V / dO only after the dV pass,
+// so half the staging registers are live through dQ / dV -- with DROP the Philox keep words
+// otherwise push the kernel to 432 B/lane of spill (68 B with the split)
+template <bool DROP, bool SPLIT = false>
 __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const int* __restrict__ mask,
@@ -447,7 +456,8 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
     }
     // the fp32 S / dP are dead: prefetch the next pair into the staging registers now (its
     // loads land during dQ, dV and dK of this pair)
-    tb_load(in, qkv, dout, mask, next, T, H, D, lane);
+    if constexpr (SPLIT) tb_load<1>(in, qkv, dout, mask, next, T, H, D, lane);
+    else tb_load(in, qkv, dout, mask, next, T, H, D, lane);
     // ---- dQ = dS K (B = K via transposed reads of the swizzled tile) ----
     f32x4 o[4][4];
 #pragma unroll
@@ -518,6 +528,9 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);  // the scratch is rewritten by the next pass / pair
+      if constexpr (SPLIT) {
+        if (pass == 0) tb_load<2>(in, qkv, dout, mask, next, T, H, D, lane);  // V, dO of the next pair
+      }
       __builtin_amdgcn_wave_barrier();
     }
     pair += stride;
@@ -527,6 +540,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
 
 int g_tab_variant = 1;  // 1: persistent prefetching (default), 0: one-shot
 int g_tab_cus = 0;
+int g_tab_drop_split = 1;  // dropout backward: split prefetch (FEDREC_TAB_DROP_SPLIT=0: one block)
 
 int tab_cus() {
   if (g_tab_cus == 0) {
@@ -540,7 +554,10 @@ int tab_cus() {
 
 }  // namespace
 
-extern "C" void fr_title_attn_bwd_set_variant(int v) { g_tab_variant = v; }
+extern "C" void fr_title_attn_bwd_set_variant(int v) {
+  if (v >= 10) g_tab_drop_split = v - 10;  // 10 / 11: the dropout backward's prefetch form
+  else g_tab_variant = v;
+}
 
 extern "C" int fr_title_attention_bwd_long_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv,
                                                 int n_titles, int T, int H, int D, hipStream_t s);  // title_attn_long.hip
@@ -573,8 +590,12 @@ extern "C" int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dou
   if (g_tab_variant == 1) {
     const int need = (pairs + 3) / 4;
     const int blocks = tab_cus() < need ? tab_cus() : need;
-    hipLaunchKernelGGL(title_attn_bwd_pkernel<true>, dim3(blocks), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
-                       mask, (bf16*)dqkv, pairs, T, H, D, pdrop, seed, offset);
+    if (g_tab_drop_split)
+      hipLaunchKernelGGL((title_attn_bwd_pkernel<true, true>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv,
+                         (const bf16*)dout, mask, (bf16*)dqkv, pairs, T, H, D, pdrop, seed, offset);
+    else
+      hipLaunchKernelGGL((title_attn_bwd_pkernel<true, false>), dim3(blocks), dim3(256), 0, s, (const bf16*)qkv,
+                         (const bf16*)dout, mask, (bf16*)dqkv, pairs, T, H, D, pdrop, seed, offset);
     return 0;
   }
   hipLaunchKernelGGL((title_attn_bwd_kernel<true>), dim3((pairs + WPB - 1) / WPB), dim3(64 * WPB), 0, s,

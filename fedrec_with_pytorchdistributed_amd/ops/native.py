@@ -62,6 +62,8 @@ def _apply_env_knobs(ops) -> None:
         ops.title_attn_set_waves(int(os.environ["FEDREC_TA_WAVES"]))
     if os.environ.get("FEDREC_TAB_VARIANT"):
         ops.title_attn_bwd_set_variant(int(os.environ["FEDREC_TAB_VARIANT"]))
+    if os.environ.get("FEDREC_TAB_DROP_SPLIT"):
+        ops.title_attn_bwd_set_variant(10 + int(os.environ["FEDREC_TAB_DROP_SPLIT"]))
     if os.environ.get("FEDREC_SEGSUM_VARIANT"):
         ops.segsum_set_variant(int(os.environ["FEDREC_SEGSUM_VARIANT"]))
     if os.environ.get("FEDREC_GEMM_VARIANT"):
