@@ -173,6 +173,7 @@ class LocalEngine:
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
         # hidden states of the step's unique titles gathered ahead (the step graph's first part)
         self._pre_hid: Optional[torch.Tensor] = None
+        self._one: Optional[torch.Tensor] = None  # seed gradient of the loss (see forward_backward)
         self.hcache = self._make_hidden_cache()
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
@@ -371,7 +372,11 @@ class LocalEngine:
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
                                           pre is not None and pre.padded, True)
             with obs.range("backward"):
-                loss.backward()
+                # a persistent ones tensor as the seed gradient: no fill launch per step (the
+                # captured graph reads it in place)
+                if self._one is None or self._one.shape != loss.shape or self._one.device != loss.device:
+                    self._one = torch.ones_like(loss)
+                loss.backward(self._one)
             self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
             self.flat.end_backward()
             return loss.detach()
