@@ -1,7 +1,7 @@
 #!/bin/bash
 # small GEMM back to one tile in flight (+ split-K with the full epilogue in the reduce);
 # unroll-4 user-attention backward as variant 2: tests, micro A/B, config-2 A/B/A, profile
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check tests 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_small_gemm_gpu.py tests/test_user_step_gpu.py tests/test_kernels_gpu.py -k "small or user or gemm or colsum"
 run uabench 200 python benchmarks/user_attn_bench.py --out gpurun_out/user_attn_bench.json
 run c2_a 300 python bench.py --steps 50 --warmup 10

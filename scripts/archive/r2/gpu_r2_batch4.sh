@@ -2,7 +2,7 @@
 # config-5 glue (one-launch weight refresh, LN2 bwd + FFN dropout bwd, bias shortcut, no fp32
 # q|k|v cat, stored attention keep bits) + config-2 (ILP user attention, split-K dgrad with the
 # dropout epilogue): full GPU suite, micro A/Bs, bench A/Bs, profiles
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check gputests 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
 run attnbench 200 python benchmarks/attn_drop_bench.py --out gpurun_out/attn_drop_bench.json
 run uabench 200 python benchmarks/user_attn_bench.py --out gpurun_out/user_attn_bench.json

@@ -1,7 +1,7 @@
 #!/bin/bash
 # after dropping the keep-bits attention path and the ILP user-attention backward: GPU suite,
 # config-2 / config-5 benches (A/B of the fused LN2 + FFN-dropout backward), config-2 profile
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check gputests 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
 run uabench 200 python benchmarks/user_attn_bench.py --out gpurun_out/user_attn_bench.json
 run c2_a 300 python bench.py --steps 50 --warmup 10

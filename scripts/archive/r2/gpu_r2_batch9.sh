@@ -1,6 +1,6 @@
 #!/bin/bash
 # small GEMM: two K-tiles in flight + split-K with the whole epilogue in the reduce
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check tests 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_small_gemm_gpu.py tests/test_user_step_gpu.py tests/test_engine_gpu.py tests/test_step_graph.py
 run c2 300 python bench.py --steps 50 --warmup 10
 run c2_default 300 python bench.py

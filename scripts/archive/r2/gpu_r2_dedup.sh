@@ -1,6 +1,6 @@
 #!/bin/bash
 # 32-bit-key dedup + 3-stage wgrad: tests, wgrad stage A/B, config-2 bench + profile
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check ktests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_wgrad_gpu.py tests/test_engine_gpu.py tests/test_user_step_gpu.py -m gpu
 FEDREC_WGRAD_NST=4 run bwd4 300 python benchmarks/bwd_gemm_bench.py --rounds 5
 run bwd3 300 python benchmarks/bwd_gemm_bench.py --rounds 5

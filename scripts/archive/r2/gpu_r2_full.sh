@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-2 verification: smoke, the GPU suite, the driver's default bench, the four BASELINE
 # configs, a config-2 and a config-5 kernel profile
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 check gputests 1100 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread
 run bench_default 400 python bench.py

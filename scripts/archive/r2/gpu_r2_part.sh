@@ -1,6 +1,6 @@
 #!/bin/bash
 # partial-column-tile ping-pong GEMM: numerics, all GEMM/kernel tests, config-2 bench + profile
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check parttest 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_partial_gpu.py
 check ktests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_user_step_gpu.py tests/test_engine_gpu.py tests/test_step_graph.py -m gpu
 run bench 400 python bench.py --steps 50 --warmup 10
