@@ -57,7 +57,9 @@ extern "C" int fr_adam_flat(float* p, const float* g, float* m, float* v, void* 
 // bigger destination (q / k / v weights -> the fused [3D, D] QKV weight), so the per-step
 // pack rebuild (a cat + a cast launch per weight, ~100 launches at BERT-base) becomes one
 // streaming pass.  Blocks are assigned to segments in proportion to their size
-// (MCAST_CHUNK elements per block); a block finds its segment by binary search.
+// (MCAST_CHUNK elements per block); a block finds its segment by binary search.  Any size and
+// alignment: 16-byte aligned segments take the vector path, the rest (and ragged tails) go
+// element by element.
 namespace {
 constexpr int MCAST_SEG = 96;
 constexpr int MCAST_CHUNK = 8192;  // 256 threads x 4 iterations x 8 elements
@@ -67,7 +69,8 @@ struct MultiCast {
   void* dst[MCAST_SEG];
   long n[MCAST_SEG];
   int blk0[MCAST_SEG + 1];
-  unsigned char bf[MCAST_SEG];  // 1: bf16 destination, 0: fp32
+  unsigned char bf[MCAST_SEG];   // 1: bf16 destination, 0: fp32
+  unsigned char vec[MCAST_SEG];  // 1: 16-byte aligned (vector path), 0: element by element
   int nseg;
 };
 
@@ -85,7 +88,13 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
 #pragma unroll
   for (int it = 0; it < MCAST_CHUNK / (256 * 8); ++it) {
     const long e = base + ((long)it * 256 + threadIdx.x) * 8;
-    if (e < n) {
+    if (e < n && (!mc.vec[sg] || e + 8 > n)) {  // unaligned segment or its ragged tail
+      const float* src = mc.src[sg];
+      for (int j = 0; j < 8 && e + j < n; ++j) {
+        if (mc.bf[sg]) ((bf16*)mc.dst[sg])[e + j] = f2bf(src[e + j]);
+        else ((float*)mc.dst[sg])[e + j] = src[e + j];
+      }
+    } else if (e < n) {
       const float4 a = s4[e >> 2], b = s4[(e >> 2) + 1];
       if (mc.bf[sg]) {
         *(bf16x8*)((bf16*)mc.dst[sg] + e) =
@@ -108,7 +117,8 @@ extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const lo
   mc.nseg = nseg;
   long blk = 0;
   for (int i = 0; i < nseg; ++i) {
-    if (n[i] <= 0 || n[i] % 8 != 0 || ((uintptr_t)src[i] & 15) != 0 || ((uintptr_t)dst[i] & 15) != 0) return 1;
+    if (n[i] <= 0) return 1;
+    mc.vec[i] = (((uintptr_t)src[i] & 15) == 0 && ((uintptr_t)dst[i] & 15) == 0) ? 1 : 0;
     mc.src[i] = src[i];
     mc.dst[i] = dst[i];
     mc.n[i] = n[i];

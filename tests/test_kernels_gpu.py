@@ -466,7 +466,12 @@ def test_multi_cast(dev):
     many_d = [torch.empty(64, device=dev, dtype=torch.bfloat16) for _ in range(130)]
     assert native.lib().multi_cast(many_s, many_d)
     assert all(torch.equal(b, a.to(torch.bfloat16)) for a, b in zip(many_s, many_d))
-    assert not native.lib().multi_cast([torch.randn(12, device=dev)], [torch.empty(12, device=dev)])  # n % 8
+    # ragged sizes and 4-byte-aligned slices take the element path
+    odd_s = [torch.randn(13, device=dev), torch.randn(1, device=dev), torch.randn(1001, device=dev)[1:]]
+    odd_d = [torch.empty(13, device=dev), torch.empty(3, device=dev, dtype=torch.bfloat16)[1:2],
+             torch.empty(1000, device=dev)]
+    assert native.lib().multi_cast(odd_s, odd_d)
+    assert all(torch.equal(b, a.to(b.dtype)) for a, b in zip(odd_s, odd_d))
     # transposed: [R, C] fp32 -> bf16 [C, R] views, side by side in a fused [C, 3R] destination
     ws = [torch.randn(768, 768, device=dev) for _ in range(3)] + [torch.randn(3072, 768, device=dev)]
     fused_t = torch.empty(768, 3 * 768, device=dev, dtype=torch.bfloat16)
