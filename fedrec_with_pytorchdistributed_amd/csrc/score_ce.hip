@@ -56,13 +56,66 @@ __global__ __launch_bounds__(256) void score_ce_kernel(const float* __restrict__
   }
 }
 
+// Block-per-impression form (default): one wave per candidate computes its score, so the C
+// dot products run side by side instead of one after another in a single wave (that chain of
+// load -> reduce rounds made the wave-per-impression kernel ~18 us for B = 64).  The softmax /
+// loss / dz of the impression come from wave 0's first C lanes; dcand rows are written by
+// their own wave, du by all threads over the D columns.
+__global__ __launch_bounds__(64 * MAXC) void score_ce_block_kernel(const float* __restrict__ cand,
+                                                                   const float* __restrict__ user,
+                                                                   float* __restrict__ loss,
+                                                                   float* __restrict__ scores,
+                                                                   float* __restrict__ dcand,
+                                                                   float* __restrict__ duser, int B, int C, int D,
+                                                                   int sigm) {
+  __shared__ float zs[MAXC], dzs[MAXC];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x;
+  const float* cb = cand + (size_t)b * C * D;
+  const float* ub = user + (size_t)b * D;
+  float a = 0.f;
+  for (int d = lane; d < D; d += 64) a += cb[(size_t)w * D + d] * ub[d];
+  a = wave_sum(a);
+  if (lane == 0) zs[w] = a;
+  __syncthreads();
+  if (w == 0) {
+    const bool on = lane < C;
+    const float z = on ? zs[lane] : 0.f;
+    const float sc = sigm ? 1.0f / (1.0f + __expf(-z)) : z;
+    const float mx = wave_max(on ? sc : -INFINITY);
+    const float se = wave_sum(on ? __expf(sc - mx) : 0.f);
+    if (on) {
+      scores[(size_t)b * C + lane] = sc;
+      const float ds = (__expf(sc - mx) / se - (lane == 0 ? 1.f : 0.f)) / (float)B;
+      dzs[lane] = sigm ? ds * sc * (1.f - sc) : ds;
+      if (lane == 0) loss[b] = (mx + __logf(se) - sc) / (float)B;  // per-impression share
+    }
+  }
+  __syncthreads();
+  const float dzw = dzs[w];
+  for (int d = lane; d < D; d += 64) dcand[((size_t)b * C + w) * D + d] = dzw * ub[d];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float du = 0.f;
+    for (int c = 0; c < C; ++c) du += dzs[c] * cb[(size_t)c * D + d];
+    duser[(size_t)b * D + d] = du;
+  }
+}
+
+int g_score_variant = 1;  // 1: block per impression (default), 0: wave per impression
+
 }  // namespace
+
+extern "C" void fr_score_set_variant(int v) { g_score_variant = v; }
 
 extern "C" int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand,
                            float* duser, int B, int C, int D, int sigm, hipStream_t s) {
   if (C > MAXC) return 1;
   if (B == 0) return 0;
-  hipLaunchKernelGGL(score_ce_kernel, dim3((B + 3) / 4), dim3(256), 0, s, cand, user, loss, scores, dcand, duser, B,
-                     C, D, sigm);
+  if (g_score_variant == 1 && C <= MAXC)
+    hipLaunchKernelGGL(score_ce_block_kernel, dim3(B), dim3(64 * C), 0, s, cand, user, loss, scores, dcand, duser, B,
+                       C, D, sigm);
+  else
+    hipLaunchKernelGGL(score_ce_kernel, dim3((B + 3) / 4), dim3(256), 0, s, cand, user, loss, scores, dcand, duser, B,
+                       C, D, sigm);
   return 0;
 }

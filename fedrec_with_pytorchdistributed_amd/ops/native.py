@@ -56,6 +56,8 @@ def _apply_env_knobs(ops) -> None:
     """Kernel-variant switches for A/B runs (unset = the measured defaults)."""
     if os.environ.get("FEDREC_LN_WIDE"):
         ops.ln_set_wide(int(os.environ["FEDREC_LN_WIDE"]))
+    if os.environ.get("FEDREC_SCORE_VARIANT"):
+        ops.score_set_variant(int(os.environ["FEDREC_SCORE_VARIANT"]))
     if os.environ.get("FEDREC_UA_VARIANT"):
         ops.user_attn_set_variant(int(os.environ["FEDREC_UA_VARIANT"]))
     if os.environ.get("FEDREC_TA_WAVES"):

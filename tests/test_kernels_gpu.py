@@ -192,12 +192,16 @@ def test_additive_pool_long_fp32(dev, T):
     assert rel_err(dx, rdx) < 1e-5 and rel_err(dpre, rde * (1 - e ** 2)) < 1e-4 and rel_err(dw2, rdw2) < 1e-4
 
 
-def test_score_ce(dev):
-    B, C, D = 33, 5, 400
+@pytest.mark.parametrize("variant", [1, 0])  # 1: block per impression (default), 0: wave per impression
+@pytest.mark.parametrize("act,C", [("sigmoid", 5), ("identity", 5), ("sigmoid", 16), ("identity", 1)])
+def test_score_ce(dev, variant, act, C):
+    native.lib().score_set_variant(variant)
+    B, D = 33, 400
     cand = torch.randn(B, C, D, device=dev) * 0.1
     u = torch.randn(B, D, device=dev) * 0.1
-    loss, s, dc, du = ops.score_ce(cand, u, "sigmoid")
-    l2, s2, dc2, du2 = ref.score_ce_fwd_bwd(cand, u, "sigmoid")
+    loss, s, dc, du = ops.score_ce(cand, u, act)
+    l2, s2, dc2, du2 = ref.score_ce_fwd_bwd(cand, u, act)
+    native.lib().score_set_variant(1)
     assert abs(float(loss) - float(l2)) < 1e-5
     assert rel_err(s, s2) < 1e-6 and rel_err(dc, dc2) < 1e-5 and rel_err(du, du2) < 1e-5
 
