@@ -58,11 +58,15 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const TX* __restrict__ x,
     for (int t = lane; t < T; t += 64) {
       const float al = a_s[t] * inv;
       a_s[t] = al;
-      alpha_out[(size_t)n * T + t] = al;
+      if (blockIdx.y == 0) alpha_out[(size_t)n * T + t] = al;
     }
   }
   __syncthreads();
-  for (int d = tid; d < D; d += 256) {
+  // gridDim.y blocks share a sequence (few sequences, e.g. B = 64 impressions): each recomputes
+  // the T scores (cheap) and writes its own slice of the D output columns
+  const int dspan = (D + gridDim.y - 1) / gridDim.y;
+  const int dlo = blockIdx.y * dspan, dhi = min(D, dlo + dspan);
+  for (int d = dlo + tid; d < dhi; d += 256) {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     int t = 0;
 #pragma unroll 2
@@ -329,8 +333,8 @@ extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w
     hipLaunchKernelGGL(pool_fwd_kernel<bf16>, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, w2, b2, out,
                        alpha, T, D, Q);
   else
-    hipLaunchKernelGGL(pool_fwd_kernel<float>, dim3(n), dim3(256), 0, s, (const float*)x, (const float*)e, w2, b2,
-                       out, alpha, T, D, Q);
+    hipLaunchKernelGGL(pool_fwd_kernel<float>, dim3(n, n < 128 ? 4 : (n < 256 ? 2 : 1)), dim3(256), 0, s,
+                       (const float*)x, (const float*)e, w2, b2, out, alpha, T, D, Q);
   return 0;
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # block-per-impression score/CE: kernel tests, then config-2 A/B/A
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_kernels_gpu.py -k "score" tests/test_user_step_gpu.py tests/test_step_graph.py
 run c2_a 300 python bench.py --steps 50 --warmup 10
 run c2_old 300 env FEDREC_SCORE_VARIANT=0 python bench.py --steps 50 --warmup 10

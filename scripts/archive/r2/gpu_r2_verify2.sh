@@ -1,6 +1,6 @@
 #!/bin/bash
 # multi_cast for any size / alignment, flat-gradient gather by multi_cast: GPU suite + benches
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check gputests 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
 run c2 300 python bench.py --steps 50 --warmup 10
 run c2_default 300 python bench.py
