@@ -1,6 +1,6 @@
 #!/bin/bash
 # fp32 additive-pool forward split over several blocks per impression: tests + config-2 bench
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 check tests 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_kernels_gpu.py tests/test_user_step_gpu.py tests/test_engine_gpu.py tests/test_step_graph.py
 run c2_a 300 python bench.py --steps 50 --warmup 10
 run c2_b 300 python bench.py --steps 50 --warmup 10
