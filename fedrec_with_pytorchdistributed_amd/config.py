@@ -83,7 +83,11 @@ class SecAggConfig:
 
     enabled: bool = False
     frac_bits: int = 16  # fixed-point fraction bits for uint32 quantisation
-    clip_value: float = 1024.0  # |x| bound before quantisation
+    clip_value: float = 1024.0  # |x| bound before quantisation (model parameters, star uploads)
+    # secure GRADIENT averaging: coordinates are clamped to a running bound = headroom x the
+    # largest coordinate of the previous (public) mean gradient, quantised on the finest grid the
+    # W-client int32 sum allows (parallel.secagg.RunningMasker: no per-step collective beyond it)
+    bound_headroom: float = 4.0
 
 
 @dataclass

@@ -39,6 +39,16 @@ int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const fl
 int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g, float* dx,
                          void* dpre, float* dw2, float* db2, float* dsum, int n, int T, int D, int Q, int R,
                          int is_bf16, hipStream_t s);
+int fr_head_supported(int D, int Q, int T);
+int fr_head_score(const void* table, const int* ids, int U, int T, int D, int Q, const void* W1, const float* b1,
+                  const float* w2, const float* b2, void* e_out, float* a_out, hipStream_t s);
+int fr_head_pool(const void* table, const int* ids, const float* a, const int* tokens, int U, int T, int D,
+                 float* pooled, float* alpha, hipStream_t s);
+int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, const float* g, int U, int T, int D,
+                     float* da, float* db2p, hipStream_t s);
+long fr_head_wgrad(const void* e, const void* table, const int* ids, const float* da, const float* db2p,
+                   const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2, float* db2,
+                   float* scratch, hipStream_t s);
 int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, hipStream_t s);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
                      int dk, hipStream_t s);
@@ -357,6 +367,121 @@ std::tuple<at::Tensor, at::Tensor> additive_pool_fwd(const at::Tensor& x, const 
                                 cur_stream()),
            "additive_pool_fwd");
   return {out, alpha};
+}
+
+// ---- fused text head over gathered hidden states (text_head.hip) ----------------------------
+// table [rows, D] bf16 (the HBM hidden-state cache viewed as rows, or a batch's hidden states);
+// ids [U] int32 title indices (None: titles 0..U-1 of the table); T tokens per title.
+namespace {
+int64_t head_titles(const at::Tensor& table, const c10::optional<at::Tensor>& ids, int64_t T) {
+  check_dev(table, "table");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && table.scalar_type() == at::kBFloat16,
+              "fedrec::head: table [rows, D] contiguous bf16");
+  TORCH_CHECK(T >= 1 && table.size(0) % T == 0, "fedrec::head: table rows not a multiple of T");
+  if (ids.has_value()) {
+    check_dev(*ids, "ids");
+    TORCH_CHECK(ids->dim() == 1 && ids->is_contiguous() && ids->scalar_type() == at::kInt, "fedrec::head: ids int32 [U]");
+    return ids->size(0);
+  }
+  return table.size(0) / T;
+}
+const int* opt_int_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr<int>() : nullptr; }
+}  // namespace
+
+bool head_supported(int64_t D, int64_t Q, int64_t T) { return fr_head_supported((int)D, (int)Q, (int)T) != 0; }
+
+std::tuple<at::Tensor, at::Tensor> head_score(const at::Tensor& table, const c10::optional<at::Tensor>& ids, int64_t T,
+                                              const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2,
+                                              const at::Tensor& b2, bool store_e) {
+  const int64_t U = head_titles(table, ids, T), D = table.size(1), Q = w1.size(0);
+  check_dev(w1, "w1");
+  TORCH_CHECK(w1.scalar_type() == at::kBFloat16 && w1.is_contiguous() && w1.size(1) == D, "fedrec::head_score: w1 bf16 [Q, D]");
+  TORCH_CHECK(b1.scalar_type() == at::kFloat && w2.scalar_type() == at::kFloat && b2.scalar_type() == at::kFloat &&
+                  b1.numel() == Q && w2.numel() == Q && b2.numel() == 1 && b1.is_contiguous() && w2.is_contiguous() &&
+                  b1.is_cuda() && w2.is_cuda() && b2.is_cuda(),
+              "fedrec::head_score: b1 / w2 [Q], b2 [1] fp32 device");
+  TORCH_CHECK(fr_head_supported((int)D, (int)Q, (int)T), "fedrec::head_score: unsupported shape D=", D, " Q=", Q, " T=", T);
+  // (ids are not range-checked here: that needs a device->host read every step; the engine's
+  // ids come from the dedup over [0, N) by construction)
+  const c10::DeviceGuard g(table.device());
+  auto e = store_e ? at::empty({U * T, Q}, table.options()) : at::empty({0}, table.options());
+  auto a = at::empty({U * T}, table.options().dtype(at::kFloat));
+  check_rc(fr_head_score(table.data_ptr(), opt_int_ptr(ids), (int)U, (int)T, (int)D, (int)Q, w1.data_ptr(),
+                         b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+                         store_e ? e.data_ptr() : nullptr, a.data_ptr<float>(), cur_stream()),
+           "head_score");
+  return {e, a};
+}
+
+std::tuple<at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10::optional<at::Tensor>& ids, int64_t T,
+                                             const at::Tensor& a, const c10::optional<at::Tensor>& tokens) {
+  const int64_t U = head_titles(table, ids, T), D = table.size(1);
+  check_dev(a, "a");
+  TORCH_CHECK(a.scalar_type() == at::kFloat && a.numel() == U * T && a.is_contiguous(), "fedrec::head_pool: a [U*T] fp32");
+  if (tokens.has_value()) {
+    check_dev(*tokens, "tokens");
+    TORCH_CHECK(tokens->scalar_type() == at::kInt && tokens->dim() == 3 && tokens->size(1) == 2 &&
+                    tokens->size(2) == T && tokens->is_contiguous() && tokens->size(0) * T >= table.size(0),
+                "fedrec::head_pool: tokens int32 [N, 2, T] covering the table");
+  }
+  const c10::DeviceGuard g(table.device());
+  auto pooled = at::empty({U, D}, a.options());
+  auto alpha = at::empty({U, T}, a.options());
+  check_rc(fr_head_pool(table.data_ptr(), opt_int_ptr(ids), a.data_ptr<float>(), opt_int_ptr(tokens), (int)U, (int)T,
+                        (int)D, pooled.data_ptr<float>(), alpha.data_ptr<float>(), cur_stream()),
+           "head_pool");
+  return {pooled, alpha};
+}
+
+std::tuple<at::Tensor, at::Tensor> head_pool_bwd(const at::Tensor& table, const c10::optional<at::Tensor>& ids,
+                                                 int64_t T, const at::Tensor& alpha, const at::Tensor& g) {
+  const int64_t U = head_titles(table, ids, T), D = table.size(1);
+  check_dev(alpha, "alpha");
+  check_dev(g, "g");
+  TORCH_CHECK(alpha.scalar_type() == at::kFloat && alpha.numel() == U * T && alpha.is_contiguous() &&
+                  g.scalar_type() == at::kFloat && g.numel() == U * D && g.is_contiguous(),
+              "fedrec::head_pool_bwd: alpha [U, T], g [U, D] fp32");
+  const c10::DeviceGuard dg(table.device());
+  auto da = at::empty({U * T}, alpha.options());
+  auto db2p = at::empty({std::max<int64_t>(U, 1)}, alpha.options());
+  check_rc(fr_head_pool_bwd(table.data_ptr(), opt_int_ptr(ids), alpha.data_ptr<float>(), g.data_ptr<float>(), (int)U,
+                            (int)T, (int)D, da.data_ptr<float>(), db2p.data_ptr<float>(), cur_stream()),
+           "head_pool_bwd");
+  return {da, db2p};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad(const at::Tensor& table,
+                                                                      const c10::optional<at::Tensor>& ids, int64_t T,
+                                                                      const at::Tensor& e, const at::Tensor& da,
+                                                                      const at::Tensor& w2, const at::Tensor& db2p) {
+  const int64_t U = head_titles(table, ids, T), D = table.size(1), Q = w2.numel();
+  check_dev(e, "e");
+  check_dev(da, "da");
+  check_dev(w2, "w2");
+  check_dev(db2p, "db2p");
+  TORCH_CHECK(e.scalar_type() == at::kBFloat16 && e.is_contiguous() && e.numel() == U * T * Q,
+              "fedrec::head_wgrad: e bf16 [U*T, Q]");
+  TORCH_CHECK(da.scalar_type() == at::kFloat && da.numel() == U * T && w2.scalar_type() == at::kFloat &&
+                  w2.is_contiguous() && db2p.scalar_type() == at::kFloat && db2p.numel() >= U,
+              "fedrec::head_wgrad: da / w2 / db2p");
+  TORCH_CHECK(fr_head_supported((int)D, (int)Q, (int)T), "fedrec::head_wgrad: unsupported shape");
+  const c10::DeviceGuard g(table.device());
+  auto fopt = da.options();
+  auto dW1 = at::empty({Q, D}, fopt);
+  auto small = at::empty({2 * Q + 1}, fopt);
+  float* db1 = small.data_ptr<float>();
+  float* dw2 = db1 + Q;
+  float* db2 = dw2 + Q;
+  const long need = fr_head_wgrad(e.data_ptr(), table.data_ptr(), opt_int_ptr(ids), da.data_ptr<float>(),
+                                  db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
+                                  dW1.data_ptr<float>(), db1, dw2, db2, nullptr, cur_stream());
+  TORCH_CHECK(need > 0, "fedrec::head_wgrad: unsupported shape");
+  auto scratch = at::empty({need}, fopt);
+  check_rc((int)fr_head_wgrad(e.data_ptr(), table.data_ptr(), opt_int_ptr(ids), da.data_ptr<float>(),
+                              db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
+                              dW1.data_ptr<float>(), db1, dw2, db2, scratch.data_ptr<float>(), cur_stream()),
+           "head_wgrad");
+  return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(
@@ -813,8 +938,8 @@ void multi_copy(const std::vector<at::Tensor>& src, const std::vector<at::Tensor
   check_rc(fr_multi_copy(sp.data(), dp.data(), ns.data(), nd.data(), fv.data(), (int)n, cur_stream()), "multi_copy");
 }
 
-// device-scale secure aggregation (bucketed GA): the fixed-point exponent is derived on the device
-// from m = the clients' MAX-all-reduced max|x| -- no host read, no host sync
+// device-scale secure aggregation (parallel/secagg.py RunningMasker): the fixed-point exponent
+// is derived on the device from the running bound m (a device scalar) -- no host read, no sync
 at::Tensor secagg_mask_dev(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs, const at::Tensor& m,
                            int64_t W, int64_t round) {
   check_dev(x, "x");
@@ -1142,6 +1267,11 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attention_bwd(Tensor qkv, Tensor dout, Tensor mask, int n_heads) -> Tensor");
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("title_attention(Tensor qkv, Tensor mask, int n_heads) -> Tensor");
+  m.def("head_supported(int D, int Q, int T) -> bool", &head_supported);
+  m.def("head_score(Tensor table, Tensor? ids, int T, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bool store_e) -> (Tensor, Tensor)");
+  m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens) -> (Tensor, Tensor)");
+  m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g) -> (Tensor, Tensor)");
+  m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2) -> (Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim) -> (Tensor, Tensor)");
@@ -1187,6 +1317,10 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("title_attention_bwd", &title_attention_bwd);
   m.impl("embed_ln", &embed_ln);
   m.impl("title_attention", &title_attention);
+  m.impl("head_score", &head_score);
+  m.impl("head_pool", &head_pool);
+  m.impl("head_pool_bwd", &head_pool_bwd);
+  m.impl("head_wgrad", &head_wgrad);
   m.impl("additive_pool_fwd", &additive_pool_fwd);
   m.impl("additive_pool_bwd", &additive_pool_bwd);
   m.impl("user_attention_fwd", &user_attention_fwd);

@@ -1,0 +1,706 @@
+// The text head of the news encoder, fused over gathered backbone hidden states (gfx950).
+//
+// Reference (encoder.py:27-29, attention.py:14-26): for a title's
+// last hidden state x [T, D] (D = 768, T = 50)
+//     e_t = tanh(W1 x_t + b1)          W1 [Q, D], Q = 384
+//     a_t = w2 . e_t + b2              alpha = exp(a) / (sum_t exp(a) + 1e-8)
+//     pooled = sum_t alpha_t x_t       -> fc [400, D] (small_gemm.hip, not here)
+//
+// The frozen backbone's hidden states sit in an HBM cache [N, T, D] bf16 (train/news_cache.py)
+// and a step needs the U ~ 1.6k unique titles of its batch.  Round 2 materialised them with a
+// gather (128 MB), ran att_fc1 as a plain GEMM that wrote e (64 MB), re-read x and e in the pool,
+// wrote dpre = da w2 (1 - e^2) (64 MB) in the pool backward and re-read dpre and x in the weight
+// gradient: ~290 us of the 0.8 ms step was the same rows going through HBM five times.  Here:
+//
+//   head_score   A rows loaded straight from the cache by title index (row m -> cache row
+//                ids[m / T] * T + m % T, per-lane glds source address), the whole Q = 384 in
+//                one block (128 x 384 tile, 8 waves) so the epilogue forms the score
+//                a_m = w2 . tanh(acc + b1) + b2 in registers (cross-lane + LDS reduction);
+//                e is stored once in bf16 for the backward.
+//   head_pool    per title: eps-softmax of a (optional token mask) and pooled = sum alpha x
+//                (x read through the same index).
+//   head_pool_bwd  per title: dalpha_t = g . x_t, da_t = alpha_t (dalpha_t - sum alpha dalpha).
+//   head_wgrad   dW1[q][k] = w2[q] sum_m da_m (1 - e_mq^2) x_mk: a split-K TN MFMA GEMM whose
+//                dY operand is FORMED IN ITS LDS PIPELINE -- the raw e tile and the da values
+//                arrive by glds, one pass per stage rewrites the e tile in place as
+//                g = da (1 - e^2) (bf16) while accumulating the dw2 = sum da e and
+//                db1 = w2 sum g column sums; no dpre tensor exists.  w2[q] is applied to the
+//                fp32 result in the split-K reduction.
+//
+// Requirements (host-checked in binding.cpp): D % 256 == 0, Q in {128, 256, 384}, T <= 128.
+#include "common.h"
+
+#include <stdlib.h>
+
+namespace {
+
+constexpr int MAXT = 128;
+
+__device__ __forceinline__ float tanh_fast(float x) {  // 1 - 2 / (1 + e^{2x}), as gemm_bf16.hip
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
+}
+
+__device__ __attribute__((aligned(16))) bf16 g_zero_row[512];  // zero-initialised (bss)
+__device__ float g_zero_f32[64];
+
+// cache row of logical row m (title slot m / T, token m % T)
+__device__ __forceinline__ const bf16* hrow(const bf16* __restrict__ table, const int* __restrict__ ids, int m, int T,
+                                            int D) {
+  const int u = m / T;
+  const int t = m - u * T;
+  const int id = ids != nullptr ? ids[u] : u;
+  return table + ((size_t)id * T + t) * D;
+}
+
+// =========================================================================================
+// head_score: e = tanh(X W1^T + b1) (bf16, optional), a = e . w2 + b2 (fp32, from the fp32 e)
+// 128 rows x Q columns per block, BK = 64, 512 threads = 8 waves as 2 (rows) x 4 (columns):
+// 64 rows x Q/4 columns per wave = 4 x QF MFMA tiles of 16x16 (v_mfma_f32_16x16x32_bf16 with
+// W1 as the A operand, so a lane ends with 4 consecutive columns of one row).  LDS: two stages
+// of [128 x 128 B rows | Q x 128 B rows], each 16-B chunk c of row r stored at c ^ (r & 7)
+// (conflict-free ds_read_b128; glds images are lane-linear so the XOR goes on the source).
+// =========================================================================================
+template <int QF>
+__device__ __forceinline__ void score_stage(char* base, const bf16* const (&arow)[2], const bf16* __restrict__ W1,
+                                            int D, int k0, int wave, int lane) {
+  constexpr int Q = QF * 64;
+  const int rsub = lane >> 3, chunk = (lane & 7) ^ rsub;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, arow[i] + k0 + chunk * 8),
+                                     LDS_PTR(void, base + (wave * 16 + i * 8) * 128), 16, 0, 0);
+#pragma unroll
+  for (int i = 0; i < QF; ++i) {
+    const int row = (wave * QF + i) * 8 + rsub;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W1 + (size_t)row * D + k0 + chunk * 8),
+                                     LDS_PTR(void, base + 128 * 128 + (wave * QF + i) * 8 * 128), 16, 0, 0);
+  }
+  (void)Q;
+}
+
+template <int QF>
+__global__ __launch_bounds__(512, 1) void head_score_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
+                                                            int M, int T, int D, const bf16* __restrict__ W1,
+                                                            const float* __restrict__ b1, const float* __restrict__ w2,
+                                                            const float* __restrict__ b2, bf16* __restrict__ e_out,
+                                                            float* __restrict__ a_out) {
+  constexpr int Q = QF * 64;
+  constexpr int ST = (128 + Q) * 128;  // stage bytes
+  __shared__ __attribute__((aligned(16))) char smem[2 * ST];
+  const int m0 = blockIdx.x * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wq = wave & 3;
+  const int rsub = lane >> 3, chunk = (lane & 7) ^ rsub;
+  const bf16* arow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int gm = m0 + wave * 16 + i * 8 + rsub;
+    gm = gm < M ? gm : M - 1;  // rows past M: any valid row (outputs masked)
+    arow[i] = hrow(table, ids, gm, T, D);
+  }
+  (void)chunk;
+
+  f32x4 acc[QF][4];
+#pragma unroll
+  for (int i = 0; i < QF; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = D / 64;
+  score_stage<QF>(smem, arow, W1, D, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) score_stage<QF>(smem + (cur ^ 1) * ST, arow, W1, D, (kt + 1) * 64, wave, lane);
+    const char* As = smem + cur * ST;
+    const char* Ws = As + 128 * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int phys = ((kk * 4 + fq) ^ (fr & 7)) * 16;
+      bf16x8 x[4], w[QF];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = *(const bf16x8*)(As + (wm * 64 + j * 16 + fr) * 128 + phys);
+#pragma unroll
+      for (int i = 0; i < QF; ++i) w[i] = *(const bf16x8*)(Ws + (wq * QF * 16 + i * 16 + fr) * 128 + phys);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < QF; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[i], x[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: lane holds rows m = m0 + wm*64 + j*16 + fr, columns q = qb_i + fq*4 + (0..3)
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < QF; i += 2) {
+    float v[2][4][4];  // [frag pair][j][reg]
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int qb = wq * QF * 16 + (i + h) * 16 + fq * 4;
+      const float4 bb = *(const float4*)(b1 + qb);
+      const float4 ww = *(const float4*)(w2 + qb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[h][j][0] = tanh_fast(acc[i + h][j][0] + bb.x);
+        v[h][j][1] = tanh_fast(acc[i + h][j][1] + bb.y);
+        v[h][j][2] = tanh_fast(acc[i + h][j][2] + bb.z);
+        v[h][j][3] = tanh_fast(acc[i + h][j][3] + bb.w);
+        part[j] += v[h][j][0] * ww.x + v[h][j][1] * ww.y + v[h][j][2] * ww.z + v[h][j][3] * ww.w;
+      }
+    }
+    if (e_out != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + fr;
+        store_pair16_if(e_out + (size_t)(m < M ? m : 0) * Q + wq * QF * 16 + i * 16, v[0][j], v[1][j], fq, m < M);
+      }
+    }
+  }
+  float* red = (float*)smem;  // the staging buffers are free (the loop ended on a barrier)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float s = group4_sum(part[j]);
+    if (fq == 0) red[wq * 128 + wm * 64 + j * 16 + fr] = s;
+  }
+  __syncthreads();
+  if (tid < 128 && m0 + tid < M)
+    a_out[m0 + tid] = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]) + b2[0];
+}
+
+// =========================================================================================
+// head_pool: per title u, alpha = eps-softmax(a) (stable form exp(a-m) / (sum + 1e-8 e^-m),
+// masked tokens get weight 0), pooled = sum_t alpha_t x_t (fp32).  384 threads: TG t-groups x
+// D/8 column chunks of 16 B.
+// =========================================================================================
+__global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
+                                                        const float* __restrict__ a, const int* __restrict__ tokens,
+                                                        int T, int D, float* __restrict__ pooled,
+                                                        float* __restrict__ alpha) {
+  __shared__ float a_s[MAXT];
+  __shared__ float part[3072];
+  const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int id = ids != nullptr ? ids[u] : u;
+  const bf16* xe = table + (size_t)id * T * D;
+  if (wave == 0) {
+    float av[2], m = -INFINITY;
+    bool keep[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      keep[c] = t < T && (tokens == nullptr || tokens[((size_t)id * 2 + 1) * T + t] != 0);
+      av[c] = keep[c] ? a[(size_t)u * T + t] : -INFINITY;
+      m = fmaxf(m, av[c]);
+    }
+    m = wave_max(m);
+    if (!(m > -INFINITY)) m = 0.f;  // every token masked: every weight 0
+    float p[2], l = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      p[c] = keep[c] ? __expf(av[c] - m) : 0.f;
+      l += p[c];
+    }
+    const float inv = 1.0f / (wave_sum(l) + 1e-8f * __expf(-m));
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      if (t < T) {
+        const float al = p[c] * inv;
+        a_s[t] = al;
+        alpha[(size_t)u * T + t] = al;
+      }
+    }
+  }
+  __syncthreads();
+  const int DC = D >> 3, TG = 384 / DC;
+  const int dc = tid % DC, tg = tid / DC;
+  if (tg < TG) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t = tg; t < T; t += TG) {
+      const bf16x8 v = *(const bf16x8*)(xe + (size_t)t * D + dc * 8);
+      const float al = a_s[t];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += al * (float)v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[tg * D + dc * 8 + k] = acc[k];
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += 384) {
+    float s = 0.f;
+    for (int j = 0; j < TG; ++j) s += part[j * D + d];
+    pooled[(size_t)u * D + d] = s;
+  }
+}
+
+// =========================================================================================
+// head_pool_bwd: per title, dalpha_t = g . x_t (fp32 g = dL/dpooled), then
+// da_t = alpha_t (dalpha_t - sum_s alpha_s dalpha_s) and db2 partial = sum_t da_t.
+// =========================================================================================
+__global__ __launch_bounds__(256) void head_pool_bwd_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
+                                                            const float* __restrict__ alpha, const float* __restrict__ g,
+                                                            int T, int D, float* __restrict__ da,
+                                                            float* __restrict__ db2p) {
+  __shared__ float dal[MAXT];
+  const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int id = ids != nullptr ? ids[u] : u;
+  const bf16* xe = table + (size_t)id * T * D;
+  const float* gu = g + (size_t)u * D;
+  const int DC = D >> 3;
+  // lanes over 16-B column chunks (up to 2 per lane: D <= 1024), g chunks in registers
+  float gv[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int dc = lane + 64 * c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[c][k] = dc < DC ? gu[dc * 8 + k] : 0.f;
+  }
+  for (int t = wave; t < T; t += 4) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int dc = lane + 64 * c;
+      if (dc < DC) {
+        const bf16x8 v = *(const bf16x8*)(xe + (size_t)t * D + dc * 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += (float)v[k] * gv[c][k];
+      }
+    }
+    s = wave_sum(s);
+    if (lane == 0) dal[t] = s;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float al[2], dv[2], s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      al[c] = t < T ? alpha[(size_t)u * T + t] : 0.f;
+      dv[c] = t < T ? dal[t] : 0.f;
+      s += al[c] * dv[c];
+    }
+    s = wave_sum(s);
+    float sd = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      const float v = al[c] * (dv[c] - s);
+      if (t < T) da[(size_t)u * T + t] = v;
+      sd += v;
+    }
+    sd = wave_sum(sd);
+    if (lane == 0) db2p[u] = sd;
+  }
+}
+
+// =========================================================================================
+// head_wgrad: P[s][q][k] = sum_{m in split s} g_mq x_mk with g = da_m (1 - e_mq^2), formed in
+// the LDS pipeline; dw2 / dsum partials [s][q] from blocks of the first k tile.
+//
+// Tile 128 (q) x 256 (k), 512 threads = 8 waves as 2 (q) x 4 (k), 64 x 64 per wave (4 x 4 MFMA
+// tiles; operands are M-major, so fragments are read with ds_read_b64_tr_b16 exactly as
+// gemm_wgrad.hip).  Stage = 32 rows: E [32 x 256 B] (raw e, then g), X [32 x 512 B] (cache rows
+// by index), DA [8 waves x 64 floats] (each wave stages the 32 da values its transform threads
+// read, so every wave issues the same 4 glds per stage and counted vmcnt waits hold).
+// Four stages: in iteration st the MFMAs read stage st, stage st+1 is rewritten (e -> g), st+2
+// is in flight and st+3 is issued.  One barrier per iteration.
+// =========================================================================================
+constexpr int WQT = 128, WKT = 256, WTM = 32;
+constexpr int E_BYTES = WTM * WQT * 2;         // 8 KB
+constexpr int X_BYTES = WTM * WKT * 2;         // 16 KB
+constexpr int DA_BYTES = 8 * 64 * 4;           // 2 KB
+constexpr int WSTAGE = E_BYTES + X_BYTES + DA_BYTES;
+constexpr int NSTAGE = 4;
+constexpr int MAX_SPLIT_TITLES = 1024;  // title ids of one split, staged in LDS up front
+
+// LDS accesses as opaque asm: a builtin LDS access after a glds into the same LDS object makes
+// the compiler drain vmcnt -- every in-flight stage (gemm_wgrad.hip); completion is ours to wait
+__device__ __forceinline__ s16x4 tr_read(uint32_t addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4_t lds_read128(uint32_t addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ float lds_read32(uint32_t addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ int lds_read32i(uint32_t addr) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ void lds_write128(uint32_t addr, u32x4_t v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ int swz(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }
+
+// ids_lds: LDS byte address of the split's title ids (title u at ids_lds + 4 (u - u_lo)): a
+// global load of ids[] here would be an ordinary load whose use makes the compiler wait
+// vmcnt(0) -- draining every glds stage in flight
+__device__ __forceinline__ void wg_stage(char* base, const bf16* __restrict__ e, const bf16* __restrict__ table,
+                                         uint32_t ids_lds, int u_lo, const float* __restrict__ da, int T, int D,
+                                         int Q, int q0, int k0, int m, int me, int wave, int lane) {
+  // E: 8 pieces of 4 rows x 16 chunks (one per wave)
+  {
+    const int row = wave * 4 + (lane >> 4), pc = lane & 15;
+    const int c = pc ^ swz(row);
+    const int gm = m + row;
+    const bf16* p = gm < me ? e + (size_t)gm * Q + q0 + 8 * c : g_zero_row + 8 * c;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + wave * 1024), 16, 0, 0);
+  }
+  // X: 16 pieces of 2 rows x 32 chunks (two per wave), rows from the cache by title index
+  const int rsub = lane >> 5, pc = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = wave * 2 + i;
+    const int row = 2 * blk + rsub;
+    const int c = pc ^ swz(row);
+    const int gm = m + row;
+    const bf16* p = g_zero_row + 8 * c;
+    if (gm < me) {
+      const int u = gm / T;
+      const int id = lds_read32i(ids_lds + 4 * (u - u_lo));
+      p = table + ((size_t)id * T + (gm - u * T)) * D + k0 + 8 * c;
+    }
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + E_BYTES + blk * 1024), 16, 0,
+                                     0);
+  }
+  // DA: this wave's copy (lanes 0..31 = rows; lanes 32..63 duplicate)
+  {
+    const int gm = m + (lane & 31);
+    const float* p = gm < me ? da + gm : g_zero_f32;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + E_BYTES + X_BYTES + wave * 256), 4,
+                                     0, 0);
+  }
+}
+
+__device__ __forceinline__ uint32_t tr_off_e(int r0, int col0, int q, int p) {  // 256-B rows
+  const int c = (col0 >> 3) + (p >> 1);
+  const int r = r0 + q;
+  return (uint32_t)(r * 256 + ((c ^ swz(r)) << 4) + (p & 1) * 8);
+}
+__device__ __forceinline__ uint32_t tr_off_x(int r0, int col0, int q, int p) {  // 512-B rows
+  const int c = (col0 >> 3) + (p >> 1);
+  const int r = r0 + q;
+  return (uint32_t)(r * 512 + ((c ^ swz(r)) << 4) + (p & 1) * 8);
+}
+
+#define LGKM_TIE8(r)                                                                                  \
+  asm volatile("s_waitcnt lgkmcnt(0)"                                                                 \
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), \
+                 "+v"(r[7]))
+
+__device__ __forceinline__ bf16x8 join(s16x4 a, s16x4 b) {
+  bf16x4 x = __builtin_bit_cast(bf16x4, a), y = __builtin_bit_cast(bf16x4, b);
+  return bf16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+}
+
+// stage landed for this wave except `inflight` younger stages (4 glds each), then barrier
+__device__ __forceinline__ void wg_sync(int inflight) {
+  __builtin_amdgcn_sched_barrier(0);
+  if (inflight >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (inflight == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// rewrite this thread's 16-B chunk of a stage's E tile: e -> g = da (1 - e^2) (bf16); STATS:
+// accumulate dw2 += da e and dsum += g (the rounded g the GEMM consumes) for its 8 columns
+template <bool STATS>
+__device__ __forceinline__ void wg_transform(uint32_t base, int tid, int wave, float (&dw2)[8], float (&dsum)[8]) {
+  const int r = tid >> 4, pc = tid & 15;
+  const uint32_t ea = base + r * 256 + pc * 16;
+  u32x4_t v = lds_read128(ea);
+  float dav = lds_read32(base + E_BYTES + X_BYTES + wave * 256 + r * 4);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(dav));
+  const bf16x8 ev = __builtin_bit_cast(bf16x8, v);
+  bf16x8 o;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float f = (float)ev[k];
+    o[k] = f2bf(dav * (1.0f - f * f));
+    if constexpr (STATS) {
+      dw2[k] += dav * f;
+      dsum[k] += (float)o[k];
+    }
+  }
+  lds_write128(ea, __builtin_bit_cast(u32x4_t, o));
+}
+
+__global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restrict__ e, const bf16* __restrict__ table,
+                                                            const int* __restrict__ ids, const float* __restrict__ da,
+                                                            int M, int T, int D, int Q, float* __restrict__ P,
+                                                            float* __restrict__ dw2p, float* __restrict__ dsump,
+                                                            int tiles_k, int ntiles, int mchunk, int no_transform) {
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * WSTAGE + 4 * MAX_SPLIT_TITLES];
+  // XCD-aware order: all tiles of one split (same e / x row panel) on one XCD's L2
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rmd = nwg & 7;
+  const int t = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (bid >> 3);
+  const int s = t / ntiles, tile = t - s * ntiles;
+  const int qt = tile / tiles_k, kt = tile - qt * tiles_k;
+  const int q0 = qt * WQT, k0 = kt * WKT;
+  const int mb = s * mchunk;
+  const int me = min(M, mb + mchunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 2, wk = wave & 3;
+  const bool stats = kt == 0 && !no_transform;  // block-uniform
+  const bool xform = !no_transform;  // diagnostic A/B: raw e as the dY operand
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float sw2[8], ssum[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sw2[k] = ssum[k] = 0.f;
+
+  const int nsteps = me > mb ? (me - mb + WTM - 1) / WTM : 0;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+  // the split's title ids into LDS before any glds is in flight (host guarantees the count fits)
+  const int u_lo = mb / T;
+  const int u_hi = me > mb ? (me - 1) / T : u_lo;
+  int* ids_s = (int*)(smem + NSTAGE * WSTAGE);
+  for (int u = u_lo + tid; u <= u_hi; u += 512) ids_s[u - u_lo] = ids != nullptr ? ids[u] : u;
+  __syncthreads();
+  const uint32_t ids_lds = lds0 + NSTAGE * WSTAGE;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < nsteps)
+      wg_stage(smem + i * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0, mb + i * WTM, me, wave, lane);
+  if (nsteps > 0) {
+    wg_sync(nsteps - 1 < 2 ? nsteps - 1 : 2);  // stage 0 landed
+    if (stats) wg_transform<true>(lds0, tid, wave, sw2, ssum);
+    else if (xform) wg_transform<false>(lds0, tid, wave, sw2, ssum);
+  }
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = g * 8;
+  uint32_t xo[4][2], yo[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    xo[j][0] = E_BYTES + tr_off_x(r0, wk * 64 + j * 16, q, p);
+    xo[j][1] = E_BYTES + tr_off_x(r0 + 4, wk * 64 + j * 16, q, p);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    yo[i][0] = tr_off_e(r0, wn * 64 + i * 16, q, p);
+    yo[i][1] = tr_off_e(r0 + 4, wn * 64 + i * 16, q, p);
+  }
+  for (int st = 0; st < nsteps; ++st) {
+    // stage st+1 landed (all waves), stage st fully rewritten (all waves' transform writes,
+    // lgkmcnt(0) before the barrier), every wave done reading stage st-1
+    const int left = nsteps - 2 - st;  // stages issued beyond st+1
+    wg_sync(left < 0 ? 0 : (left > 1 ? 1 : left));
+    if (st + 3 < nsteps)
+      wg_stage(smem + ((st + 3) % NSTAGE) * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0, mb + (st + 3) * WTM,
+               me, wave, lane);
+    if (st + 1 < nsteps) {
+      const uint32_t nb = lds0 + ((st + 1) % NSTAGE) * WSTAGE;
+      if (stats) wg_transform<true>(nb, tid, wave, sw2, ssum);
+      else if (xform) wg_transform<false>(nb, tid, wave, sw2, ssum);
+    }
+    const uint32_t base = lds0 + (st % NSTAGE) * WSTAGE;
+    s16x4 xr[8], yr[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xr[2 * j] = tr_read(base + xo[j][0]);
+      xr[2 * j + 1] = tr_read(base + xo[j][1]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      yr[2 * i] = tr_read(base + yo[i][0]);
+      yr[2 * i + 1] = tr_read(base + yo[i][1]);
+    }
+    LGKM_TIE8(xr);
+    LGKM_TIE8(yr);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 xb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xb[j] = join(xr[2 * j], xr[2 * j + 1]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16x8 ya = join(yr[2 * i], yr[2 * i + 1]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], ya, acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // lane holds P[q][k .. k+3]: q = tile column (lane % 16), k = 4 consecutive (lane / 16)
+  float* out = P + (size_t)s * Q * D;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qq2 = q0 + wn * 64 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wk * 64 + j * 16 + 4 * g;
+      *(f32x4*)(out + (size_t)qq2 * D + k) = acc[i][j];
+    }
+  }
+  if (stats) {  // column sums over the split's rows: 32 row-threads per 8-column chunk
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* red = (float*)smem;  // [32 rows][128 q] x 2
+    const int r = tid >> 4, lc = (tid & 15) ^ swz(r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[r * WQT + lc * 8 + k] = sw2[k];
+      red[WTM * WQT + r * WQT + lc * 8 + k] = ssum[k];
+    }
+    __syncthreads();
+    if (tid < 2 * WQT) {
+      const int which = tid / WQT, c = tid % WQT;
+      float acc2 = 0.f;
+      for (int rr = 0; rr < WTM; ++rr) acc2 += red[which * WTM * WQT + rr * WQT + c];
+      (which == 0 ? dw2p : dsump)[(size_t)s * Q + q0 + c] = acc2;
+    }
+  }
+}
+
+// dW1 = w2 (.) sum_s P[s] ; db1 = w2 (.) sum_s dsum[s] ; dw2 = sum_s dw2p[s] ; db2 = sum_u db2p[u]
+// (fixed summation order: deterministic).  The last block does the small vectors.
+__global__ __launch_bounds__(256) void head_reduce_kernel(const f32x4* __restrict__ P, const float* __restrict__ dw2p,
+                                                          const float* __restrict__ dsump,
+                                                          const float* __restrict__ db2p, const float* __restrict__ w2,
+                                                          f32x4* __restrict__ dW1, float* __restrict__ db1,
+                                                          float* __restrict__ dw2, float* __restrict__ db2, int S, int Q,
+                                                          int D, int U) {
+  const long n4 = (long)Q * D / 4;
+  if (blockIdx.x + 1 < gridDim.x) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)(gridDim.x - 1) * blockDim.x) {
+      f32x4 v = P[i];
+      for (int s = 1; s < S; ++s) v += P[(size_t)s * n4 + i];
+      dW1[i] = v * w2[(i * 4) / D];
+    }
+    return;
+  }
+  for (int q = threadIdx.x; q < Q; q += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int s = 0; s < S; ++s) {
+      a += dw2p[(size_t)s * Q + q];
+      b += dsump[(size_t)s * Q + q];
+    }
+    dw2[q] = a;
+    db1[q] = b * w2[q];
+  }
+  __shared__ float red[4];
+  float c = 0.f;
+  for (int u = threadIdx.x; u < U; u += blockDim.x) c += db2p[u];
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) db2[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+int g_cus = 0;
+int g_wg_variant = -1;  // FEDREC_HEAD_WG: bit 0 = no e -> g transform (diagnostic timing only)
+int g_wg_splits = -1;   // FEDREC_HEAD_SPLITS: split-K count override (A/B runs)
+
+int env_int(const char* k, int d) {
+  const char* v = getenv(k);
+  return v != nullptr ? atoi(v) : d;
+}
+
+}  // namespace
+
+extern "C" int fr_head_supported(int D, int Q, int T) {
+  return D % 256 == 0 && D <= 1024 && (Q == 128 || Q == 256 || Q == 384) && T >= 1 && T <= MAXT;
+}
+
+extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, int D, int Q, const void* W1,
+                             const float* b1, const float* w2, const float* b2, void* e_out, float* a_out,
+                             hipStream_t s) {
+  if (!fr_head_supported(D, Q, T)) return 1;
+  const int M = U * T;
+  if (M == 0) return 0;
+  const dim3 grid((M + 127) / 128);
+#define LAUNCH_SCORE(QF)                                                                                          \
+  hipLaunchKernelGGL(head_score_kernel<QF>, grid, dim3(512), 0, s, (const bf16*)table, ids, M, T, D,             \
+                     (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out)
+  if (Q == 384) LAUNCH_SCORE(6);
+  else if (Q == 256) LAUNCH_SCORE(4);
+  else LAUNCH_SCORE(2);
+#undef LAUNCH_SCORE
+  return 0;
+}
+
+extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, const int* tokens, int U, int T, int D,
+                            float* pooled, float* alpha, hipStream_t s) {
+  if (T > MAXT || D % 8 != 0 || D / 8 > 384) return 1;
+  if (U == 0) return 0;
+  hipLaunchKernelGGL(head_pool_kernel, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, tokens, T, D, pooled,
+                     alpha);
+  return 0;
+}
+
+extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, const float* g, int U, int T,
+                                int D, float* da, float* db2p, hipStream_t s) {
+  if (T > MAXT || D % 8 != 0 || D / 8 > 128) return 1;
+  if (U == 0) return 0;
+  hipLaunchKernelGGL(head_pool_bwd_kernel, dim3(U), dim3(256), 0, s, (const bf16*)table, ids, alpha, g, T, D, da,
+                     db2p);
+  return 0;
+}
+
+// scratch = null: returns the fp32 scratch element count needed; else launches.
+extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, const float* da, const float* db2p,
+                              const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2,
+                              float* db2, float* scratch, hipStream_t s) {
+  if (!fr_head_supported(D, Q, T)) return -1;
+  const int M = U * T;
+  if (g_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_cus <= 0) g_cus = 256;
+  }
+  if (g_wg_variant < 0) {
+    g_wg_variant = env_int("FEDREC_HEAD_WG", 0);
+    g_wg_splits = env_int("FEDREC_HEAD_SPLITS", 0);
+  }
+  const int tiles_k = D / WKT, ntiles = (Q / WQT) * tiles_k;
+  // one wave of blocks (one per CU), each split >= 8 stages of 32 rows
+  int S = g_wg_splits > 0 ? g_wg_splits : g_cus / ntiles;
+  const int smax = (M + 8 * WTM - 1) / (8 * WTM);
+  S = S < 1 ? 1 : (S > smax ? smax : S);
+  if (S < 1) S = 1;
+  int mchunk = ((M + S - 1) / S + WTM - 1) / WTM * WTM;
+  if (mchunk < WTM) mchunk = WTM;
+  // a split's title ids must fit the LDS table: more splits for very short titles
+  const int cap = (MAX_SPLIT_TITLES - 2) * T / WTM * WTM;
+  if (mchunk > cap) mchunk = cap < WTM ? WTM : cap;
+  S = (M + mchunk - 1) / mchunk;
+  if (S < 1) S = 1;
+  const long need = (long)S * Q * D + 2L * S * Q;
+  if (scratch == nullptr) return need;
+  float* P = scratch;
+  float* dw2p = scratch + (long)S * Q * D;
+  float* dsump = dw2p + (long)S * Q;
+  if (M > 0)
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, da,
+                       M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1);
+  else {
+    (void)hipMemsetAsync(scratch, 0, need * sizeof(float), s);
+  }
+  const long n4 = (long)Q * D / 4;
+  long blocks = (n4 + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)blocks + 1), dim3(256), 0, s, (const f32x4*)P, dw2p, dsump,
+                     db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U);
+  return 0;
+}

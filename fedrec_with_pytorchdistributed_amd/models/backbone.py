@@ -112,6 +112,24 @@ class Backbone(nn.Module):
         self._stale = True
         self.version += 1
 
+    @torch.no_grad()
+    def fingerprint(self) -> torch.Tensor:
+        """A checksum of every weight (fp64 sum and sum of squares per tensor, on the host):
+        identical weights give identical fingerprints (same deterministic reductions)."""
+        parts = [torch.stack([p.detach().double().sum(), p.detach().double().square().sum()])
+                 for p in self.parameters()]
+        return torch.cat(parts).cpu() if parts else torch.zeros(0, dtype=torch.float64)
+
+    def invalidate_if_changed(self, before: torch.Tensor) -> bool:
+        """Invalidate (compute pack + hidden-state caches) only when the weights differ from
+        the ``before`` fingerprint; a sync of a frozen backbone between bitwise-identical
+        replicas (every client starts from the same seed / checkpoint, and a mean over a
+        power-of-two client count is exact) then keeps the cache.  Returns True if invalidated."""
+        if torch.equal(self.fingerprint(), before):
+            return False
+        self.invalidate()
+        return True
+
     @property
     def pack_stale(self) -> bool:
         return self._pack is None or self._stale

@@ -117,9 +117,38 @@ class TextEncoder(nn.Module):
             h = bb(text[:, 0, :], text[:, 1, :], self.compute_dtype, dropout=dropout)
         return h.view(n, T, -1)
 
+    def fused_head_ok(self, title_len: int) -> bool:
+        """The fused text-head kernels (``OF.TextHeadFn``) apply: device, bf16, supported shape."""
+        if self.compute_dtype != torch.bfloat16:
+            return False
+        key = int(title_len)
+        cache = self.__dict__.setdefault("_fused_ok", {})
+        if key not in cache:
+            cache[key] = OF.fused_head_supported(self.cfg.backbone.dim, self.additive_attention.att_fc1.out_features,
+                                                 title_len)
+        return cache[key]
+
+    def head_rows(self, table: torch.Tensor, ids: torch.Tensor | None, title_len: int,
+                  tokens: torch.Tensor | None = None) -> torch.Tensor:
+        """Trainable head over GATHERED hidden states: ``table [rows, D]`` bf16 (the HBM cache as
+        rows), titles ``ids [U]`` (None: 0..U-1), ``title_len`` tokens each -> ``[U, 400]`` fp32.
+        ``tokens [N, 2, T]`` int32 masks padding tokens when ``mask_padding`` is on (Q7)."""
+        aa = self.additive_attention
+        tok = tokens if self.cfg.mask_padding else None
+        pooled = OF.TextHeadFn.apply(aa.att_fc1.weight, aa.att_fc1.bias, aa.att_fc2.weight, aa.att_fc2.bias,
+                                     table, ids, int(title_len), tok)
+        return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias)
+
     def head(self, hidden: torch.Tensor, token_mask: torch.Tensor | None = None) -> torch.Tensor:
         """Trainable head: ``[n,T,D] -> [n,400]`` (fp32).  ``token_mask [n,T]`` excludes padding
         tokens from the pooling when ``mask_padding`` is on (the reference pools over them: Q7)."""
+        n, T, D = hidden.shape
+        if hidden.is_cuda and not hidden.requires_grad and self.fused_head_ok(T):
+            tokens = None
+            if self.cfg.mask_padding and token_mask is not None:
+                m = token_mask.to(torch.int32)
+                tokens = torch.stack([m, m], 1).contiguous()
+            return self.head_rows(hidden.reshape(n * T, D).contiguous(), None, T, tokens)
         keep = (token_mask != 0) if (self.cfg.mask_padding and token_mask is not None) else None
         pooled = self.additive_attention(hidden, keep)
         if pooled.is_cuda:  # K07 on the small MFMA GEMM (fwd + bwd), not the vendor library

@@ -121,6 +121,50 @@ class AdditivePoolFn(torch.autograd.Function):
         return dx, dw1, db1, dw2.reshape(1, -1).to(w2.dtype), db2.reshape(1).to(w2.dtype)
 
 
+class TextHeadFn(torch.autograd.Function):
+    """The text head's attention pooling (``encoder.py:27-28`` -> ``attention.py:14-26``) over
+    GATHERED hidden states: rows of ``table [rows, D]`` (the HBM hidden-state cache, or a
+    batch's hidden states) picked by title index ``ids [U]`` (None: titles 0..U-1), ``T`` tokens
+    per title -> pooled ``[U, D]`` fp32 (the ``fc`` follows as :class:`HeadFCFn`).
+
+    ``csrc/text_head.hip``: forward = the att_fc1 GEMM with its A rows loaded by index and a
+    tanh.w2 row-dot epilogue (scores a; e kept in bf16 for the backward) + the per-title pool;
+    backward = the pool backward (da) + the att_fc1 weight gradient with
+    ``dpre = da w2 (1 - e^2)`` formed inside its LDS pipeline, with the db1 / dw2 / db2 sums.
+    No hidden-state gather, no dpre tensor.  The hidden states get no gradient (frozen
+    backbone); the unfrozen backbone keeps :class:`AdditivePoolFn`.  ``tokens [N, 2, T]``
+    int32 (optional, indexed like the table's titles): padding tokens get weight 0 (the
+    ``mask_padding`` option, Q7)."""
+
+    @staticmethod
+    def forward(ctx, w1, b1, w2, b2, table, ids, T: int, tokens):
+        lib = ops.native.require_for(table)
+        need = any(ctx.needs_input_grad[:4])
+        e, a = lib.head_score(table, ids, T, w1.to(torch.bfloat16).contiguous(), b1.contiguous(),
+                              w2.reshape(-1).contiguous(), b2.reshape(-1), need)
+        pooled, alpha = lib.head_pool(table, ids, T, a, tokens)
+        if need:
+            ctx.save_for_backward(table, ids, e, alpha, w2)
+        ctx.T = T
+        return pooled
+
+    @staticmethod
+    def backward(ctx, g):
+        table, ids, e, alpha, w2 = ctx.saved_tensors
+        lib = ops.native.require_for(table)
+        da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float())
+        dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p)
+        return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None
+
+
+def fused_head_supported(table_dim: int, query_dim: int, title_len: int) -> bool:
+    """Shapes the fused text-head kernels take (D % 256 == 0, Q in {128, 256, 384}, T <= 128);
+    ``FEDREC_FUSED_HEAD=0`` keeps the round-2 gather + GEMM + pool path for A/B runs."""
+    if __import__("os").environ.get("FEDREC_FUSED_HEAD", "1") == "0":
+        return False
+    return bool(ops.native.lib().head_supported(int(table_dim), int(query_dim), int(title_len)))
+
+
 class UserAttentionFn(torch.autograd.Function):
     """``ScaledDotProductAttention`` over 20 heads x d_k 20 (``attention.py:32-82``)."""
 

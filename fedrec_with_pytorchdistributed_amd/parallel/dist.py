@@ -14,7 +14,6 @@ Collective timeouts default to minutes, not the reference's 2 days (``client.py:
 from __future__ import annotations
 
 import datetime
-import math
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -124,54 +123,32 @@ def make_grad_allreduce(ctx: DistContext):
     return _ar
 
 
-def make_secure_grad_allreduce(ctx: DistContext, frac_bits: Optional[int] = None, clip: float = 32.0,
-                               timeout_s: float = 600.0, run_id: str = "secagg-ga"):
+def make_secure_grad_allreduce(ctx: DistContext, headroom: float = 4.0, timeout_s: float = 600.0,
+                               run_id: str = "secagg-ga"):
     """Gradient averaging under pairwise-mask secure aggregation (BASELINE config 5).
 
     Each client uploads ``Q(g) + sum_j +-PRG(s_ij, step)`` as wrap-around int32; one RCCL
     int32 SUM all-reduce cancels the masks exactly; the result is dequantised in place.
     Pair seeds come from a Diffie-Hellman exchange of public keys over the store.  The
-    fixed-point range must hold the W-client sum: ``W * clip * 2^frac_bits < 2^31``.
-
-    ``frac_bits=None`` (default) picks the fixed-point scale per step: the clients agree on
-    ``m = max_k max|g_k|`` with one scalar MAX all-reduce (the only value revealed beyond
-    the sum) and use the largest power of two with ``W * m * 2^f < 2^30`` -- a fixed
-    2^-22 grid is coarser than the small gradients of the head layers, which Adam's
-    normalisation then amplifies."""
+    fixed-point bound is a device-side running bound (:class:`.secagg.RunningMasker`): one
+    collective per step and no host read (round 2 ran a scalar MAX all-reduce plus a
+    ``.item()`` every step)."""
     from . import secagg
     from .control import ControlPlane
 
     if ctx.num_clients <= 1 or not ctx.initialized:
         return None
     W, k = ctx.num_clients, ctx.client_index
-    if frac_bits is not None and W * clip * (1 << frac_bits) >= 2 ** 31:
-        raise ValueError(f"secure aggregation range overflow: {W} x {clip} x 2^{frac_bits} >= 2^31")
     cp = ControlPlane.from_default(run_id, timeout_s)
     kp = secagg.KeyPair()
     cp.set(f"pk/{k}", secagg.public_bytes(kp))
     pubs = [cp.get(f"pk/{j}") for j in range(W)]
     seeds_row = secagg.seeds_from_publics(kp, k, pubs)
+    masker = secagg.RunningMasker(k, W, seeds_row, ctx.device, headroom)
     state = {"step": 0}
 
-    def _scale(flat_grad: torch.Tensor):
-        if frac_bits is not None:
-            return frac_bits, clip
-        m = torch.nan_to_num(flat_grad.abs().max().float().reshape(1), nan=0.0, posinf=3.0e38)
-        CHECK.record("all_reduce", m, "secagg-max")
-        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=ctx.data_group)
-        mv = max(float(m.item()), 1e-30)
-        f = int(math.floor(math.log2((2.0 ** 30) / (W * mv))))
-        f = max(0, min(f, 56))
-        return f, mv
-
     def _ar(flat_grad: torch.Tensor) -> float:
-        fb, cl = _scale(flat_grad)
-        q = secagg.mask_local(flat_grad, k, W, seeds_row, state["step"], fb, cl)
-        if q.device != flat_grad.device:
-            q = q.to(flat_grad.device)
-        CHECK.record("all_reduce", q, "secagg-sum")
-        dist.all_reduce(q, op=dist.ReduceOp.SUM, group=ctx.data_group)
-        flat_grad.copy_(secagg.unmask_sum(q, fb).view_as(flat_grad))
+        masker.allreduce_(flat_grad, state["step"], ctx.data_group, "secagg")
         state["step"] += 1
         return 1.0 / W
 
@@ -179,7 +156,7 @@ def make_secure_grad_allreduce(ctx: DistContext, frac_bits: Optional[int] = None
 
 
 def make_bucket_reducer(ctx: DistContext, flat, secure: bool = False, bucket_mb: Optional[float] = None,
-                        timeout_s: float = 600.0, run_id: str = "secagg-bucket"):
+                        timeout_s: float = 600.0, run_id: str = "secagg-bucket", headroom: float = 4.0):
     """The backward-overlapped bucketed all-reduce (:class:`.reducer.BucketReducer`) over the
     client data group; ``secure`` = pairwise-masked int32 buckets (seeds by Diffie-Hellman
     over the store, as :func:`make_secure_grad_allreduce`).  None for a single client."""
@@ -198,4 +175,4 @@ def make_bucket_reducer(ctx: DistContext, flat, secure: bool = False, bucket_mb:
         cp.set(f"pk/{k}", secagg.public_bytes(kp))
         seeds_row = secagg.seeds_from_publics(kp, k, [cp.get(f"pk/{j}") for j in range(W)])
     mb = float(os.environ.get("FEDREC_BUCKET_MB", bucket_mb or DEFAULT_BUCKET_MB))
-    return BucketReducer(flat, ctx.data_group, W, "secure" if secure else "mean", mb, k, seeds_row)
+    return BucketReducer(flat, ctx.data_group, W, "secure" if secure else "mean", mb, k, seeds_row, headroom)

@@ -11,11 +11,10 @@ still runs on the compute stream.
 
 * ``op="mean"``: one RCCL SUM all-reduce per bucket (the 1/W lands in Adam's grad scale).
 * ``op="secure"``: pairwise-masked fixed-point aggregation per bucket (BASELINE config 5,
-  :mod:`.secagg`): ``m = max|g|`` on the device, one scalar MAX all-reduce, the mask
-  kernel derives the fixed-point exponent from ``m`` *on the device*, one int32 SUM
-  all-reduce cancels the masks exactly, the unmask kernel writes the dequantised sum back
-  into the bucket.  No host read anywhere (the round-1 form blocked on ``m.item()`` every
-  step).  The revealed per-bucket max|g| is the one value disclosed beyond the sum.
+  :class:`.secagg.RunningMasker`): ONE int32 SUM all-reduce per bucket cancels the masks
+  exactly.  The fixed-point bound is agreed once (first step) and then tracked on the
+  device from the public sums, so there is no per-step scalar collective and no host read
+  (round 2 issued a MAX all-reduce per bucket per step, which also disclosed max|g|).
 
 Parameters register ``post_accumulate_grad`` hooks: the hook copies the fresh gradient into
 its flat slot, re-points ``.grad`` at the slot, and counts the bucket down.  A bucket whose
@@ -24,7 +23,6 @@ zero-filled them), in bucket order, so every rank issues the same collective seq
 """
 from __future__ import annotations
 
-import math
 from typing import List, Optional
 
 import torch
@@ -37,7 +35,7 @@ DEFAULT_BUCKET_MB = 28.0
 
 class BucketReducer:
     def __init__(self, flat, group, world: int, op: str = "mean", bucket_mb: float = DEFAULT_BUCKET_MB,
-                 client_index: int = 0, seeds_row=None):
+                 client_index: int = 0, seeds_row=None, headroom: float = 4.0):
         if op not in ("mean", "secure"):
             raise ValueError(f"BucketReducer op {op!r}")
         self.flat, self.group, self.W, self.op = flat, group, int(world), op
@@ -72,10 +70,7 @@ class BucketReducer:
         if op == "secure":
             from . import secagg
 
-            peers, sd, sg = secagg._peer_arrays(self.k, seeds_row)
-            self.sd = sd.to(dev)
-            self.sg = sg.to(dev)
-            self.seeds_row = seeds_row
+            self.maskers = [secagg.RunningMasker(self.k, self.W, seeds_row, dev, headroom) for _ in self.buckets]
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(flat.params)]
 
     # -------------------------------------------------------------------------------
@@ -120,32 +115,18 @@ class BucketReducer:
             CHECK.record("all_reduce", g, f"bucket{b}")
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
             return
-        from . import secagg
-
         rnd = self.step * 4096 + b  # a fresh PRG counter space per (step, bucket)
-        m = torch.nan_to_num(g.abs().amax().float().reshape(1), nan=0.0, posinf=3.0e38)
-        CHECK.record("all_reduce", m, f"secagg-max{b}")
-        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
-        if g.is_cuda:
-            from ..ops import native
-
-            lib = native.require_for(g)
-            q = lib.secagg_mask_dev(g.contiguous(), self.sd, self.sg, m, self.W, rnd)
-            CHECK.record("all_reduce", q, f"secagg-sum{b}")
-            dist.all_reduce(q, op=dist.ReduceOp.SUM, group=self.group)
-            lib.secagg_unmask_dev_(q, m, self.W, g)
-            return
-        # host (gloo plumbing): same exponent rule, the reference-format masks of secagg.py
-        mv = max(float(m.item()), 1e-30)
-        f = max(0, min(int(math.floor(math.log2((2.0 ** 30) / (self.W * mv)))), 56))
-        q = secagg.mask_local(g, self.k, self.W, self.seeds_row, rnd, f, mv)
-        CHECK.record("all_reduce", q, f"secagg-sum{b}")
-        dist.all_reduce(q, op=dist.ReduceOp.SUM, group=self.group)
-        g.copy_(secagg.unmask_sum(q, f).view_as(g))
+        self.maskers[b].allreduce_(g, rnd, self.group, f"secagg{b}")
 
     def finish(self) -> float:
         """Reduce any bucket still waiting (parameters without a gradient: zero-filled by
-        ``end_backward``), make the compute stream wait for every bucket; returns 1/W."""
+        ``end_backward``), make the compute stream wait for every bucket; returns 1/W.
+
+        Without a :meth:`begin` (the ``per_epoch`` schedule accumulates several backward
+        passes and reduces once, at the epoch-end optimizer step) every bucket is reduced
+        here, in bucket order."""
+        if not self._active:
+            self._launched = [False] * len(self.buckets)
         for b in range(len(self.buckets)):
             if not self._launched[b]:
                 self._launch(b)

@@ -69,12 +69,23 @@ FRAC_BITS = 16
 CLIP = 1024.0
 
 
+def frac_bits_for(world: int, bound: float) -> int:
+    """Fraction bits of the fixed-point grid for ``world`` clients whose coordinates are
+    clamped to ``[-bound, bound]``: the largest ``f`` with ``world * bound * 2^f <= 2^30``,
+    so the int32 sum of every client's quantised value cannot wrap (masks aside).  The same
+    rule as the device kernels' ``frac_exp2`` (``secagg.hip``)."""
+    import math
+
+    f = int(math.floor(math.log2((2.0 ** 30) / (max(1, int(world)) * max(float(bound), 1e-30)))))
+    return max(0, min(f, 56))
+
+
 def quantize_ref(x: torch.Tensor, frac_bits: int = FRAC_BITS, clip: float = CLIP) -> torch.Tensor:
-    return torch.round(x.float().clamp(-clip, clip) * (1 << frac_bits)).to(torch.int64).to(torch.int32)
+    return torch.round(x.float().clamp(-clip, clip) * (2.0 ** frac_bits)).to(torch.int64).to(torch.int32)
 
 
 def dequantize_ref(q: torch.Tensor, frac_bits: int = FRAC_BITS) -> torch.Tensor:
-    return q.float() * (1.0 / (1 << frac_bits))
+    return q.float() * (2.0 ** -frac_bits)
 
 
 def _peer_arrays(i: int, seeds_row: np.ndarray):
@@ -93,7 +104,7 @@ def mask_local(x: torch.Tensor, i: int, W: int, seeds: np.ndarray, round_idx: in
     if flat.is_cuda:
         from ..ops import native
 
-        out = native.require_for(flat).secagg_mask(flat, sd, sg, float(1 << frac_bits), float(clip), int(round_idx))
+        out = native.require_for(flat).secagg_mask(flat, sd, sg, float(2.0 ** frac_bits), float(clip), int(round_idx))
         if isinstance(out, (tuple, list)):
             out = out[0]
         return out.view(x.shape)
@@ -106,9 +117,73 @@ def mask_local(x: torch.Tensor, i: int, W: int, seeds: np.ndarray, round_idx: in
     return torch.from_numpy(acc.view(np.int32).copy()).view(x.shape)
 
 
+class RunningMasker:
+    """Client ``i``'s secure-aggregation state for repeated sums of one gradient buffer (or
+    bucket), with a fixed-point scale that needs no per-step agreement:
+
+    * every coordinate is clamped to a bound ``m`` and quantised on the grid ``2^-f``, ``f``
+      the largest with ``W * m * 2^f <= 2^30`` (the W-client int32 sum cannot wrap);
+    * ``m`` lives on the device.  It is agreed ONCE, at the first call (the
+      scalar MAX all-reduce of ``max|g|``, exact: nothing is clamped), and from then on tracked
+      from the PUBLIC result: after each sum every client sets
+      ``m = max(headroom * max|sum| / W, decay * m)`` from the
+      unmasked sum it holds (``max|sum| / W``: the largest coordinate of the MEAN gradient) -- bitwise identical on every client, so every client derives the
+      same ``f`` without a collective, and nothing beyond the sums is disclosed after step 0.
+      Clamped coordinates raise the next sum's maximum, so the bound grows back within a
+      step; the decay floor keeps it from collapsing on an all-zero step.
+    * pair seeds and signs are device-resident (no per-call host->device copy, which torch
+      would synchronise on), and the scale is read by the kernels from device memory: a step's
+      mask / all-reduce / unmask sequence never waits on the host.
+
+    One SUM all-reduce per call (plus the one-time MAX)."""
+
+    def __init__(self, i: int, world: int, seeds_row: np.ndarray, device: torch.device,
+                 headroom: float = 4.0, decay: float = 0.25):
+        self.i, self.W, self.row = int(i), int(world), seeds_row
+        self.headroom, self.decay = float(headroom), float(decay)
+        _, sd, sg = _peer_arrays(self.i, seeds_row)
+        self.device = device
+        self.sd, self.sg = sd.to(device), sg.to(device)
+        self.m: Optional[torch.Tensor] = None  # device fp32 [1]: the current clamp bound
+
+    def _amax(self, g: torch.Tensor) -> torch.Tensor:
+        return torch.nan_to_num(g.detach().abs().amax().float().reshape(1), nan=0.0, posinf=3.0e38)
+
+    def allreduce_(self, g: torch.Tensor, round_idx: int, group, check_tag: str = "secagg") -> None:
+        """``g`` <- the exact (fixed-point) SUM of every client's ``g``, in place."""
+        import torch.distributed as dist
+
+        from .collcheck import CHECK
+
+        if self.m is None:  # one-time agreement of the initial bound
+            m = self._amax(g)
+            CHECK.record("all_reduce", m, f"{check_tag}-init")
+            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+            self.m = torch.clamp(m, min=1e-30, max=3.0e38)
+        flat = g.reshape(-1)
+        if flat.is_cuda:
+            from ..ops import native
+
+            lib = native.require_for(flat)
+            q = lib.secagg_mask_dev(flat.float().contiguous(), self.sd, self.sg, self.m, self.W, int(round_idx))
+            CHECK.record("all_reduce", q, f"{check_tag}-sum")
+            dist.all_reduce(q, op=dist.ReduceOp.SUM, group=group)
+            lib.secagg_unmask_dev_(q, self.m, self.W, flat)
+        else:  # host (gloo plumbing): the same bound rule, the reference-format masks below
+            mv = float(self.m.item())
+            f = frac_bits_for(self.W, mv)
+            q = mask_local(flat, self.i, self.W, self.row, round_idx, f, mv)
+            CHECK.record("all_reduce", q, f"{check_tag}-sum")
+            dist.all_reduce(q, op=dist.ReduceOp.SUM, group=group)
+            flat.copy_(unmask_sum(q, f).view_as(flat))
+        self.used = self.m  # the bound this sum was quantised with (tests read it)
+        self.m = torch.maximum(torch.clamp(self._amax(flat) * (self.headroom / self.W), max=3.0e38),
+                               self.m * self.decay).clamp_(min=1e-30)
+
+
 def unmask_sum(total: torch.Tensor, frac_bits: int = FRAC_BITS) -> torch.Tensor:
     if total.is_cuda:
         from ..ops import native
 
-        return native.require_for(total).secagg_unmask(total.contiguous(), 1.0 / (1 << frac_bits))
+        return native.require_for(total).secagg_unmask(total.contiguous(), 2.0 ** -frac_bits)
     return dequantize_ref(total, frac_bits)

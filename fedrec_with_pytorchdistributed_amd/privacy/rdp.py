@@ -13,6 +13,13 @@ same computation from the published analysis:
 * default orders ``[1 + x/10 for x in 1..99] + [12..63]`` and the doubling + bisection
   search of ``get_noise_multiplier`` with epsilon tolerance 0.01.
 
+Attribution: the structure of this module -- the log-space helpers ``_log_add`` / ``_log_sub``
+/ ``_log_erfc``, the integer / fractional-order split ``_log_a_int`` / ``_log_a_frac``, the
+``MAX_SIGMA`` cap and the doubling + bisection noise search with its "privacy budget is too
+low" error -- follows the public Apache-2.0 RDP analysis of TensorFlow Privacy
+(``rdp_accountant.py``) and Opacus (``opacus/accountants/analysis/rdp.py``,
+``opacus/accountants/utils.py``), re-implemented here; the reference itself has no accountant.
+
 Numerics are validated in tests against q = 1 (closed form ``a / (2 sigma^2)``) and
 against direct numerical integration of the Renyi divergence; parity with the Opacus
 package itself is unpinned (not importable offline).

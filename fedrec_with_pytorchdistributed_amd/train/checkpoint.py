@@ -98,6 +98,30 @@ def client_snapshot_path(snapshot_path: str, client: int) -> str:
     return os.path.join(d, f"client{client}_{f}")
 
 
+def save_client_state(path: str, model: FedRecModel, round_idx: int, engine: Dict[str, int]) -> None:
+    """A star client's resume state: the trainable flat parameters, Adam moments + step, RNG
+    states and engine counters -- NOT the frozen backbone (the round's global model and the
+    client's own seed / checkpoint restore that).  ~14 MB instead of a 270 MB state_dict."""
+    snap: Dict[str, Any] = {"FLAT_PARAMS": model.flat.flat.detach().cpu(), "OPTIM_STATE": model.flat.state(),
+                            "ROUND": int(round_idx), "ENGINE": {k: int(v) for k, v in engine.items()},
+                            "FLAT_NAMES": list(model.flat.names)}
+    snap.update(rng_state())
+    atomic_save(snap, path)
+
+
+def load_client_state(path: str, model: FedRecModel) -> Dict[str, Any]:
+    snap = torch.load(path, map_location="cpu", weights_only=True)
+    if "FLAT_PARAMS" not in snap:  # a full snapshot (round-2 format)
+        return load_snapshot(path, model)
+    if list(snap.get("FLAT_NAMES", model.flat.names)) != list(model.flat.names):
+        raise ValueError(f"{path}: trainable parameter set differs from the model's")
+    with torch.no_grad():
+        model.flat.flat.copy_(snap["FLAT_PARAMS"].to(model.flat.flat.device))
+    model.flat.load_state(snap["OPTIM_STATE"])
+    restore_rng(snap)
+    return {"round": snap.get("ROUND"), "engine": snap.get("ENGINE", {})}
+
+
 def save_state_dict(path: str, model: FedRecModel) -> None:
     atomic_save(cpu_state_dict(model), path)
 

@@ -90,7 +90,8 @@ class _StepGraph:
         # (on with a gradient all-reduce only: at one client there is only Adam (7 us) to hide,
         # and the extra replay measured neutral: 66.86k vs 67.15k imp/s, r2_bench_batch6.jsonl)
         split = os.environ.get("FEDREC_SPLIT_GRAPH", "auto")
-        if split == "on" or (split == "auto" and eng.grad_allreduce is not None):
+        # (the fused text head reads the cache by index inside its GEMM: nothing to gather ahead)
+        if not eng.fused_head and (split == "on" or (split == "auto" and eng.grad_allreduce is not None)):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 for _ in range(2):
@@ -278,10 +279,25 @@ class LocalEngine:
         text = self.tokens.index_select(0, ids.long())
         return self.model.text_encoder.hidden(text), text[:, 1, :]
 
+    @property
+    def fused_head(self) -> bool:
+        """Text head on the fused kernels straight over the hidden-state cache (by index)."""
+        return self.hcache is not None and self.model.text_encoder.fused_head_ok(self.tokens.shape[2])
+
+    def _cache_ids(self, ids: torch.Tensor) -> torch.Tensor:
+        return ids if ids.dtype == torch.int32 else ids.to(torch.int32)
+
     def news_vectors(self, uniq: torch.Tensor, grad: bool) -> torch.Tensor:
         te = self.model.text_encoder
         if not grad and self.news_table is not None:
             return self.news_table.index_select(0, uniq.long())
+        if self.fused_head:
+            table = self.hcache.flat()
+            self.sync_params()
+            if grad:
+                return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens)
+            with torch.no_grad():
+                return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens)
         hid, mask = self._hidden(uniq)  # parameter-free: overlaps the previous step's all-reduce + Adam
         self.sync_params()
         if grad:
@@ -424,6 +440,11 @@ class LocalEngine:
         uniq, inv, perm, ptr = pre.dedup
         U = int(uniq.numel())
         ucap = -(-U // self.GRAPH_BUCKET) * self.GRAPH_BUCKET
+        # a backbone sync (sync=full, an unfrozen step) may have invalidated the cache since the
+        # last replay: rebuild it BEFORE keying, so a replay never reads a stale table and a new
+        # graph is filed under the build it captured
+        self.sync_params()
+        self.hcache.ensure()
         key = (tuple(pre.cand.shape), tuple(pre.his.shape), int(inv.numel()), ucap, self.hcache.builds)
         g = self._graphs.get(key)
         main = torch.cuda.current_stream(self.device)
@@ -492,6 +513,10 @@ class LocalEngine:
         out = torch.empty(self.N, self.cfg.news_dim, dtype=torch.float32, device=self.device)
         for s in range(0, self.N, chunk):
             ids = torch.arange(s, min(s + chunk, self.N), device=self.device, dtype=torch.int32)
+            if self.fused_head:
+                out[s:s + len(ids)] = self.model.text_encoder.head_rows(self.hcache.flat(), ids, self.tokens.shape[2],
+                                                                        self.tokens)
+                continue
             hid, mask = self._hidden(ids)
             out[s:s + len(ids)] = self.model.text_encoder.head(hid, mask).float()
         return out
@@ -542,9 +567,12 @@ class LocalEngine:
                 if train_mode:  # DistilBERT with its dropout (p = backbone.dropout / attention_dropout)
                     text = self.tokens.index_select(0, cid.long())
                     hid, mask = te.hidden(text, dropout=True), text[:, 1, :]
+                    v = te.head(hid, mask)
+                elif self.fused_head:  # the head VJP straight over the cache rows of the touched titles
+                    v = te.head_rows(self.hcache.flat(), self._cache_ids(cid), self.tokens.shape[2], self.tokens)
                 else:
                     hid, mask = self._hidden(cid)
-                v = te.head(hid, mask)
+                    v = te.head(hid, mask)
                 v.backward(self.G.index_select(0, cid.long()) * head_scale)
         self.optimizer_step()
         self.G = None

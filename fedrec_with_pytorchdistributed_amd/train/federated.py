@@ -102,19 +102,36 @@ def _min_over_clients(ctx: DistContext, x: int) -> int:
     return int(t.item())
 
 
-def _backbone_synced(model: FedRecModel, full: bool) -> None:
+def _backbone_before(model: FedRecModel, full: bool) -> Optional[torch.Tensor]:
+    """Fingerprint of a FROZEN backbone about to be overwritten by a ``sync=full`` collective
+    (None when no check applies)."""
+    if full and model.cfg.backbone.frozen:
+        return model.text_encoder.DistillBert.fingerprint()
+    return None
+
+
+def _backbone_synced(model: FedRecModel, full: bool, before: Optional[torch.Tensor] = None) -> None:
     """Parameters were overwritten by a collective: the backbone changed iff it was part of
     the synced set (``sync=full``, or an unfrozen backbone is trainable), and only then do
-    its compute pack and the HBM hidden-state cache have to be rebuilt."""
-    if full or not model.cfg.backbone.frozen:
+    its compute pack and the HBM hidden-state cache have to be rebuilt.  A frozen backbone
+    synced with ``sync=full`` is compared against its fingerprint from before the sync: the
+    reference-compat full sync (Q15) moves the 270 MB every round, but between identical
+    replicas it changes nothing and must not force a re-encode of every title."""
+    if not model.cfg.backbone.frozen:
         model.text_encoder.DistillBert.invalidate()
+    elif full:
+        if before is None:
+            model.text_encoder.DistillBert.invalidate()
+        else:
+            model.text_encoder.DistillBert.invalidate_if_changed(before)
 
 
 def _sync_initial(model: FedRecModel, ctx: DistContext, full: bool) -> None:
     """DDP-style start: every client takes client 0's parameters (X6, one bucketed call)."""
     if ctx.initialized and ctx.num_clients > 1:
+        before = _backbone_before(model, full)
         comm.broadcast_(model.sync_tensors(full), src=ctx.client_ranks[0], group=ctx.data_group)
-        _backbone_synced(model, full)
+        _backbone_synced(model, full, before)
 
 
 def _maybe_dp(cfg: FedRecConfig, eng: LocalEngine) -> Optional[float]:
@@ -156,12 +173,12 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     if bucketed:
         ar = None
     else:
-        ar = (make_secure_grad_allreduce(ctx, timeout_s=cfg.collective_timeout_s) if cfg.secagg.enabled
-              else make_grad_allreduce(ctx))
+        ar = (make_secure_grad_allreduce(ctx, cfg.secagg.bound_headroom, timeout_s=cfg.collective_timeout_s)
+              if cfg.secagg.enabled else make_grad_allreduce(ctx))
     eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=ar)
     if bucketed:
         eng.set_reducer(make_bucket_reducer(ctx, model.flat, secure=cfg.secagg.enabled,
-                                            timeout_s=cfg.collective_timeout_s))
+                                            timeout_s=cfg.collective_timeout_s, headroom=cfg.secagg.bound_headroom))
     eng.sigma = _maybe_dp(cfg, eng)
     eng.load_state(est)
     eng.epoch = start
@@ -201,9 +218,10 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
 
     def average():
         if ctx.initialized and W > 1:
+            before = _backbone_before(model, full)
             with obs.range("param_allreduce"):
                 comm.allreduce_(model.sync_tensors(full), ctx.data_group, scale=1.0 / W)
-            _backbone_synced(model, full)
+            _backbone_synced(model, full, before)
 
     hook = (lambda n: average() if n % K == 0 else None) if K else None
     last = {}
@@ -264,7 +282,7 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     # global model below, exactly as the reference's broadcast overwrites them
     csnap = ckpt.client_snapshot_path(cfg.snapshot_path, k) if cfg.snapshot_path else ""
     if csnap and os.path.exists(csnap):
-        info = ckpt.load_snapshot(csnap, model)
+        info = ckpt.load_client_state(csnap, model)
         eng.load_state(info["engine"])
         obs.log(f"[client {k}] resumed {csnap} (round {info['round']}, Adam step {model.flat.step})")
     beat = Heartbeat(cp, f"client{k}", cfg.heartbeat_s)
@@ -284,8 +302,9 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         if flag != "1":
             break
         beat(force=True)
+        before = _backbone_before(model, full)
         _receive_global(cp, r, model, ctx, full, bcast)
-        _backbone_synced(model, full)
+        _backbone_synced(model, full, before)
         eng.sigma = _maybe_dp(cfg, eng)
         eng.epoch = 0
         tr, va = {}, {}
@@ -302,8 +321,8 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         meta = {"client": k, "n_train": len(shard.train), "train_s": t_train, "valid_s": t_valid,
                 **{m: float(v) for m, v in {**tr, **va}.items() if isinstance(v, (int, float))}}
         up = _client_upload_tensor(model, cfg).clone()
-        if csnap:
-            ckpt.save_snapshot(csnap, model, r, round_idx=r, engine=eng.state())
+        last_round = r + 1 >= cfg.global_rounds if cfg.global_rounds else False
+        save_now = bool(csnap) and cfg.save_every > 0 and (r % cfg.save_every == 0 or last_round)
         if cfg.round_artifacts:  # client.py:288 torch.save(model.state_dict(), "model.pt")
             sub = "" if ctx.num_clients == 1 else f"client{k}"
             ckpt.save_state_dict(os.path.join(_artifact_dir(cfg), sub, "model.pt"), model)
@@ -327,6 +346,11 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
             else:
                 cp.put_tensor(f"r{r}/up/{k}", up.cpu())
             cp.put_json(f"r{r}/meta/{k}", meta)
+        if save_now:
+            # after the upload (off the round's critical path), every save_every rounds, and only
+            # what a resume needs: trainable flat + Adam + RNG + engine counters (~14 MB, not the
+            # 270 MB full state with the frozen backbone)
+            ckpt.save_client_state(csnap, model, r, eng.state())
         last = meta
         r += 1
     _dump_flat(model, ctx)

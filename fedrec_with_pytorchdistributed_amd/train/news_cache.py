@@ -11,7 +11,9 @@ This cache encodes every title of the client's shard once -- ``[N, T, D]`` in th
 dtype (bf16 on the device: 76.8 KB per title, ~5 GB for the 65k-title MIND-small table,
 ~12 GB for MIND-large, against 288 GB of HBM) -- and every later consumer reads rows of it:
 
-* the per-step head forward/backward (``LocalEngine.news_vectors``),
+* the per-step head forward/backward (``LocalEngine.news_vectors``): the fused text-head
+  kernels (``csrc/text_head.hip``) read a step's titles straight from the table by index --
+  no gathered copy of the rows,
 * the per-epoch news-vector table and validation (``encode_all``),
 * the epoch-end head VJP replay (``end_epoch_update``).
 
@@ -78,6 +80,11 @@ class HiddenCache:
     def ensure(self) -> None:
         if not self.fresh():
             self.build()
+
+    def flat(self) -> torch.Tensor:
+        """The table as rows ``[N * T, D]`` (the fused text head reads titles by index from it)."""
+        self.ensure()
+        return self.table.view(-1, self.table.shape[-1])
 
     def rows(self, ids: torch.Tensor) -> torch.Tensor:
         """Hidden states ``[n, T, D]`` of the titles ``ids [n]``."""

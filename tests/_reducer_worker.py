@@ -1,0 +1,59 @@
+"""Two-rank worker for test_bucket_reducer_secure_matches_plain_sum: a toy model whose
+gradients span ~9 decades, reduced by the bucket reducer (plain and pairwise-masked) from the
+backward's own hooks, checked against an explicit all-reduce of a copy of each rank's
+gradient -- the unbucketed oracle, per bucket within its fixed-point grid step."""
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from fedrec_with_pytorchdistributed_amd.models.fedrec_model import FlatParams
+from fedrec_with_pytorchdistributed_amd.parallel import secagg
+from fedrec_with_pytorchdistributed_amd.parallel.reducer import BucketReducer
+
+dist.init_process_group("gloo")
+rank, W = dist.get_rank(), dist.get_world_size()
+torch.manual_seed(0)
+layers = nn.ModuleList([nn.Linear(64, 64) for _ in range(6)])
+with torch.no_grad():
+    for i, l in enumerate(layers):  # per-layer gradient scales from 1e-6 to 1e2
+        l.weight.mul_(10.0 ** (i - 3))
+flat = FlatParams(list(layers.named_parameters()))
+seeds = secagg.pair_seeds(W, 5)[rank]
+ok = True
+for op in ("mean", "secure"):
+    red = BucketReducer(flat, None, W, op, bucket_mb=0.02, client_index=rank, seeds_row=seeds)
+    assert len(red.buckets) >= 4, len(red.buckets)
+    for step in range(3):
+        torch.manual_seed(100 * step + rank)  # different data per rank and step
+        x = torch.randn(32, 64)
+        def loss():
+            h = x
+            for l in layers:
+                h = torch.tanh(l(h)) * 3.0
+            return h.square().mean()
+
+        # this rank's own gradient, taken without accumulating (no reducer hook fires)
+        local = torch.zeros_like(flat.grad)
+        for (_, p, off), g in zip(flat.views(), torch.autograd.grad(loss(), flat.params)):
+            local[off:off + p.numel()] = g.reshape(-1)
+        flat.begin_backward()
+        red.begin()
+        loss().backward()  # the hooks reduce each bucket as its gradients land
+        flat.end_backward()
+        red.finish()
+        expect = local.clone()
+        dist.all_reduce(expect)  # the oracle: one flat SUM of every rank's gradient
+        for b, (lo, hi) in enumerate(red.ranges):
+            got, ref = flat.grad[lo:hi], expect[lo:hi]
+            if op == "mean":
+                tol = 0.0
+            else:  # each client's value rounds once onto the grid 2^-f of the bound it was masked with
+                tol = W * 2.0 ** -secagg.frac_bits_for(W, float(red.maskers[b].used.item()))
+                tol += 4 * 2.0 ** -24 * float(ref.abs().max())  # + the fp32 rounding of both sums
+            err = float((got - ref).abs().max())
+            if err > tol:
+                ok = False
+                print(f"MISMATCH op={op} step={step} bucket={b} err={err} tol={tol}", flush=True)
+    red.close()
+print("REDUCER OK" if ok else "REDUCER FAIL", flush=True)
+dist.destroy_process_group()

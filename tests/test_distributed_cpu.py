@@ -56,6 +56,47 @@ def test_grad_avg_unfrozen_bucketed_two_ranks(tmp_path, secure):
 
 
 @pytest.mark.slow
+def test_bucketed_reducer_matches_flat_allreduce(tmp_path):
+    """The backward-overlapped bucket reducer must reduce exactly what the flat all-reduce of
+    the whole gradient reduces: same buckets summed once, scale 1/W, every bucket after all of
+    its gradients landed.  Lockstep alone (both ranks equal) would not catch a skipped or early
+    bucket; the unbucketed run is the oracle.  (The pairwise-masked op is pinned per bucket by
+    test_bucket_reducer_sums_match_flat_oracle: its fixed-point grid follows each bucket's own
+    bound, so whole runs differ by grid steps that Adam amplifies on near-zero coordinates.)"""
+    base = ["Gradient_Averaging_main.py", "1", "16", "0", *TINY, "--backbone.frozen=0", "--backbone.dropout=0",
+            "--backbone.attention_dropout=0"]
+    _ok(run_ranks([base, base], {"FEDREC_DUMP_FLAT": str(tmp_path / "flat"), "FEDREC_BUCKETED": "0"}))
+    _ok(run_ranks([base, base], {"FEDREC_DUMP_FLAT": str(tmp_path / "buck"), "FEDREC_BUCKET_MB": "0.05"}))
+    a = torch.load(tmp_path / "flat" / "rank0.pt")
+    b = torch.load(tmp_path / "buck" / "rank0.pt")
+    assert torch.equal(b, torch.load(tmp_path / "buck" / "rank1.pt"))
+    assert float((a - b).abs().max()) <= 1e-7, float((a - b).abs().max())
+
+
+@pytest.mark.slow
+def test_bucket_reducer_sums_match_flat_oracle():
+    """Reducer-level oracle: per bucket, the reduced gradient equals an explicit flat SUM
+    all-reduce of every rank's gradient -- exactly for op=mean, within the bucket's fixed-point
+    grid for op=secure -- over gradients spanning 8 decades and several steps."""
+    outs = run_ranks([["tests/_reducer_worker.py"]] * 2, timeout=120)
+    _ok(outs)
+    for _, out in outs:
+        assert "REDUCER OK" in out, out[-2000:]
+
+
+@pytest.mark.slow
+def test_grad_avg_per_epoch_unfrozen_two_ranks(tmp_path):
+    """grad_avg with the per-epoch schedule and an unfrozen backbone: the bucket reducer is
+    installed but no backward arms it (several accumulated batches, one epoch-end step), so
+    finish() must reduce every bucket itself."""
+    argv = ["Gradient_Averaging_main.py", "1", "8", "0", *TINY, "--backbone.frozen=0", "--backbone.dropout=0",
+            "--backbone.attention_dropout=0", "--local_update=per_epoch"]
+    _ok(run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump"), "FEDREC_BUCKET_MB": "0.05"}))
+    a = torch.load(tmp_path / "dump" / "rank0.pt")
+    assert torch.equal(a, torch.load(tmp_path / "dump" / "rank1.pt"))
+
+
+@pytest.mark.slow
 def test_param_avg_two_ranks(tmp_path):
     argv = ["Parameter_Averaging_main.py", "2", "16", "1", *TINY, f"--snapshot_path={tmp_path}/s.pt"]
     outs = run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump")})
@@ -201,9 +242,11 @@ def test_grad_avg_secure_aggregation_matches_plain(tmp_path):
     assert torch.equal(b, c)
     # Adam normalises each coordinate, so a gradient near the fixed-point step can move its
     # parameter by up to lr per step either way: bound the bulk tightly, the tail by lr * steps
+    # (the running bound -- 4x the previous public mean's max, so no per-step MAX collective --
+    # puts the grid ~2 bits coarser than an exact per-step max|g| would)
     d = (a - b).abs()
-    assert float(torch.quantile(d.float(), 0.999)) < 1e-6
-    assert float((d > 1e-6).float().mean()) < 1e-4
+    assert float(torch.quantile(d.float(), 0.999)) < 4e-6
+    assert float((d > 1e-6).float().mean()) < 4e-3
     assert float(d.max()) < 5e-5 * 40  # lr x (an upper bound on the epoch's steps)
 
 

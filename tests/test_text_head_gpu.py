@@ -1,0 +1,139 @@
+"""The fused text head (csrc/text_head.hip, ops.functional.TextHeadFn) against the plain-PyTorch
+fp32 oracle of the reference head (encoder.py:27-29, attention.py:14-26): titles read from a
+hidden-state table by index (duplicates, padded slots of id 0, an all-padding title), forward
+(pooled) and every gradient (att_fc1 weight / bias, att_fc2 weight / bias), with and without the
+padding-token mask, T = 50 and shorter titles, and a row count that is not a tile multiple."""
+import math
+
+import pytest
+import torch
+
+from fedrec_with_pytorchdistributed_amd.ops import functional as OF
+from fedrec_with_pytorchdistributed_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(table, ids, T, w1, b1, w2, b2, tokens):
+    """fp32 reference head over table rows (bf16 inputs and bf16 W1 as the kernel consumes them)."""
+    D = table.shape[1]
+    x = table.view(-1, T, D)[ids.long()].float()  # [U, T, D]
+    e = torch.tanh(x @ w1.to(torch.bfloat16).float().t() + b1)
+    a = (e @ w2.reshape(-1, 1)).squeeze(-1) + b2
+    if tokens is not None:
+        keep = tokens[ids.long(), 1, :] != 0
+        m = a.masked_fill(~keep, float("-inf")).amax(1, keepdim=True)
+        m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+        p = torch.exp(a - m) * keep
+    else:
+        m = a.amax(1, keepdim=True)
+        p = torch.exp(a - m)
+    alpha = p / (p.sum(1, keepdim=True) + 1e-8 * torch.exp(-m))
+    return torch.einsum("ut,utd->ud", alpha, x)
+
+
+def _rel(a, b):
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / (b.norm() + 1e-20))
+
+
+@pytest.mark.parametrize("U,T,masked", [(257, 50, False), (257, 50, True), (40, 17, False), (3, 50, False),
+                                        (1664, 50, False)])
+def test_fused_text_head_matches_fp32_oracle(dev, U, T, masked):
+    g = torch.Generator(device="cpu").manual_seed(U * 100 + T)
+    N, D, Q = 300, 768, 384
+    table = torch.randn(N * T, D, generator=g).to(dev, torch.bfloat16)
+    ids = torch.randint(0, N, (U,), generator=g, dtype=torch.int32)
+    ids[: min(U, 5)] = 0  # padded slots (the step graphs pad the unique list with news 0)
+    ids = ids.to(dev)
+    tokens = None
+    if masked:
+        lens = torch.randint(0, T + 1, (N,), generator=g)
+        lens[0] = 0  # the <unk> / pad title: every token masked
+        mask = (torch.arange(T).unsqueeze(0) < lens.unsqueeze(1)).to(torch.int32)
+        tokens = torch.stack([mask * 7, mask], 1).contiguous().to(dev)
+    w1 = (torch.randn(Q, D, generator=g) / math.sqrt(D)).to(dev).requires_grad_(True)
+    b1 = (torch.randn(Q, generator=g) * 0.1).to(dev).requires_grad_(True)
+    w2 = (torch.randn(1, Q, generator=g) / math.sqrt(Q) * 3).to(dev).requires_grad_(True)
+    b2 = torch.randn(1, generator=g).to(dev).requires_grad_(True)
+    assert OF.fused_head_supported(D, Q, T)
+    pooled = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, tokens)
+    gout = torch.randn(U, D, generator=g).to(dev)
+    gw = torch.autograd.grad(pooled, (w1, b1, w2, b2), gout)
+    params = [t.detach().clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    ref = _oracle(table, ids, T, *params, tokens)
+    rw = torch.autograd.grad(ref, params, gout)
+    torch.cuda.synchronize()
+    assert pooled.shape == (U, D) and pooled.dtype == torch.float32
+    assert _rel(pooled, ref) < 2e-3, _rel(pooled, ref)
+    if masked:  # the all-padding title pools to exactly zero
+        z = (ids == 0).nonzero().reshape(-1)
+        assert float(pooled.detach()[z].abs().max()) == 0.0
+    for name, a, b in zip(("dW1", "db1", "dw2"), gw[:3], rw[:3]):
+        assert a.shape == b.shape, name
+        assert torch.isfinite(a).all(), name
+        assert _rel(a, b) < 3e-2, (name, _rel(a, b))
+    # db2 = (1 - sum alpha) sum alpha dalpha per title: ~1e-8 of the other gradients, both sides
+    # are fp32 cancellation noise -- bound it against the gradient scale instead
+    assert float((gw[3] - rw[3]).abs().max()) < 1e-3 * float(rw[2].norm()), (gw[3], rw[3])
+
+
+def test_fused_head_forward_only_skips_e(dev):
+    """Under no_grad nothing is stored for a backward (validation / epoch news tables)."""
+    T, D, Q, U = 50, 768, 384, 100
+    table = torch.randn(U * T, D, device=dev).to(torch.bfloat16)
+    lib = native.lib()
+    w1 = torch.randn(Q, D, device=dev).to(torch.bfloat16)
+    b1, w2, b2 = torch.zeros(Q, device=dev), torch.randn(Q, device=dev), torch.zeros(1, device=dev)
+    e, a = lib.head_score(table, None, T, w1, b1, w2, b2, False)
+    e2, a2 = lib.head_score(table, None, T, w1, b1, w2, b2, True)
+    assert e.numel() == 0 and e2.shape == (U * T, Q)
+    assert torch.equal(a, a2)
+    # the score is the row-dot of the fp32 tanh values: agrees with the stored bf16 e to its rounding
+    assert _rel(a2 - b2, e2.float() @ w2) < 1e-2
+
+
+def test_engine_head_uses_fused_kernels_over_cache(dev):
+    """The engine's per-step head reads the cache by index (no hidden-row gather) and gives the
+    same news vectors and head gradients as the round-2 path (gather + GEMM + pool)."""
+    import copy
+    import os
+
+    from fedrec_with_pytorchdistributed_amd.config import BackboneConfig, FedRecConfig
+    from fedrec_with_pytorchdistributed_amd.data.synthetic import make_client_shards
+    from fedrec_with_pytorchdistributed_amd.models.fedrec_model import FedRecModel
+    from fedrec_with_pytorchdistributed_amd.train.engine import LocalEngine
+
+    cfg = FedRecConfig(mode="grad_avg", batch_size=8, user_dropout=0.0)
+    cfg.backbone = BackboneConfig(name="distilbert-2l", n_layers=2)
+    torch.manual_seed(0)
+    m = FedRecModel(cfg).to(dev)
+    m.build_flat()
+    shard = make_client_shards("tiny", 1)[0]
+    eng = LocalEngine(cfg, m, shard, dev)
+    assert eng.fused_head
+    ids = torch.tensor([0, 3, 3, 7, 1, 0], dtype=torch.int32, device=dev)
+    v = eng.news_vectors(ids, grad=True)
+    gv = torch.randn_like(v)
+    te = m.text_encoder
+    params = [te.additive_attention.att_fc1.weight, te.additive_attention.att_fc1.bias,
+              te.additive_attention.att_fc2.weight, te.additive_attention.att_fc2.bias, te.fc.weight, te.fc.bias]
+    g1 = torch.autograd.grad(v, params, gv)
+    os.environ["FEDREC_FUSED_HEAD"] = "0"
+    try:
+        te2 = copy.deepcopy(te)
+        te2.__dict__.pop("_fused_ok", None)
+        hid = eng.hcache.rows(ids)
+        v2 = te2.head(hid, None)
+        params2 = [te2.additive_attention.att_fc1.weight, te2.additive_attention.att_fc1.bias,
+                   te2.additive_attention.att_fc2.weight, te2.additive_attention.att_fc2.bias, te2.fc.weight,
+                   te2.fc.bias]
+        g2 = torch.autograd.grad(v2, params2, gv)
+    finally:
+        os.environ.pop("FEDREC_FUSED_HEAD", None)
+    assert _rel(v, v2) < 5e-3
+    for i, (a, b) in enumerate(zip(g1, g2)):
+        if i == 3:  # att_fc2.bias: cancellation noise on both paths (see the oracle test)
+            assert float((a - b).abs().max()) < 1e-3 * float(g2[2].norm())
+        else:
+            assert _rel(a, b) < 3e-2, (i, _rel(a, b))
