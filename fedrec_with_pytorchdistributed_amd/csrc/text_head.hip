@@ -316,7 +316,6 @@ constexpr int E_BYTES = WTM * WQT * 2;         // 8 KB
 constexpr int X_BYTES = WTM * WKT * 2;         // 16 KB
 constexpr int DA_BYTES = 8 * 64 * 4;           // 2 KB
 constexpr int WSTAGE = E_BYTES + X_BYTES + DA_BYTES;
-constexpr int NSTAGE = 4;
 constexpr int MAX_SPLIT_TITLES = 1024;  // title ids of one split, staged in LDS up front
 
 // LDS accesses as opaque asm: a builtin LDS access after a glds into the same LDS object makes
@@ -412,7 +411,9 @@ __device__ __forceinline__ bf16x8 join(s16x4 a, s16x4 b) {
 // stage landed for this wave except `inflight` younger stages (4 glds each), then barrier
 __device__ __forceinline__ void wg_sync(int inflight) {
   __builtin_amdgcn_sched_barrier(0);
-  if (inflight >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (inflight >= 4) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (inflight == 3) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (inflight == 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (inflight == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -441,6 +442,7 @@ __device__ __forceinline__ void wg_transform(uint32_t base, int tid, int wave, f
   lds_write128(ea, __builtin_bit_cast(u32x4_t, o));
 }
 
+template <int NSTAGE>
 __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restrict__ e, const bf16* __restrict__ table,
                                                             const int* __restrict__ ids, const float* __restrict__ da,
                                                             int M, int T, int D, int Q, float* __restrict__ P,
@@ -479,12 +481,13 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
   for (int u = u_lo + tid; u <= u_hi; u += 512) ids_s[u - u_lo] = ids != nullptr ? ids[u] : u;
   __syncthreads();
   const uint32_t ids_lds = lds0 + NSTAGE * WSTAGE;
+  // NSTAGE buffers: MFMAs read stage st, stage st+1 is being rewritten, NSTAGE-2 are in flight
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < NSTAGE - 1; ++i)
     if (i < nsteps)
       wg_stage(smem + i * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0, mb + i * WTM, me, wave, lane);
   if (nsteps > 0) {
-    wg_sync(nsteps - 1 < 2 ? nsteps - 1 : 2);  // stage 0 landed
+    wg_sync(nsteps - 1 < NSTAGE - 2 ? nsteps - 1 : NSTAGE - 2);  // stage 0 landed
     if (stats) wg_transform<true>(lds0, tid, wave, sw2, ssum);
     else if (xform) wg_transform<false>(lds0, tid, wave, sw2, ssum);
   }
@@ -505,10 +508,10 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
     // stage st+1 landed (all waves), stage st fully rewritten (all waves' transform writes,
     // lgkmcnt(0) before the barrier), every wave done reading stage st-1
     const int left = nsteps - 2 - st;  // stages issued beyond st+1
-    wg_sync(left < 0 ? 0 : (left > 1 ? 1 : left));
-    if (st + 3 < nsteps)
-      wg_stage(smem + ((st + 3) % NSTAGE) * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0, mb + (st + 3) * WTM,
-               me, wave, lane);
+    wg_sync(left < 0 ? 0 : (left > NSTAGE - 3 ? NSTAGE - 3 : left));
+    if (st + NSTAGE - 1 < nsteps)
+      wg_stage(smem + ((st + NSTAGE - 1) % NSTAGE) * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0,
+               mb + (st + NSTAGE - 1) * WTM, me, wave, lane);
     if (st + 1 < nsteps) {
       const uint32_t nb = lds0 + ((st + 1) % NSTAGE) * WSTAGE;
       if (stats) wg_transform<true>(nb, tid, wave, sw2, ssum);
@@ -572,37 +575,286 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
   }
 }
 
+// -----------------------------------------------------------------------------------------
+// head_wgrad, 64-row stages (the default): twice the MFMA work per barrier of the 32-row form
+// (32 v_mfma_f32_16x16x32_bf16 per wave per stage), and no per-row index math in the loop: the
+// block's cache-row indices are resolved once into an LDS table laid out so one ds_read_b128
+// gives a lane the rows of its four X glds of a stage.  Stage = E [64 x 256 B] | X [64 x 512 B] |
+// DA [64 floats] (every wave DMAs the same 256 B: identical bytes, so the writes are benign and
+// every wave issues the same 7 glds per stage).  Three buffers: MFMAs on stage st, stage st+1
+// rewritten e -> g, stage st+2 in flight.
+// -----------------------------------------------------------------------------------------
+constexpr int W64_TM = 64;
+constexpr int W64_E = W64_TM * WQT * 2;   // 16 KB
+constexpr int W64_X = W64_TM * WKT * 2;   // 32 KB
+constexpr int W64_STAGE = W64_E + W64_X + 256;
+constexpr int W64_NST = 3;
+constexpr int W64_MAX_ROWS = 2816;        // per split (host-checked): rows table 11 KB
+
+__device__ __forceinline__ u32x4_t lds_read128w(uint32_t addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+__device__ __forceinline__ void w64_stage(char* base, const bf16* __restrict__ e, const bf16* __restrict__ table,
+                                          uint32_t rows_lds, const float* __restrict__ da, int D, int Q, int q0,
+                                          int k0, int st, int m, int me, int wave, int lane) {
+  // E: 16 pieces of 4 rows x 16 chunks (pieces 2w, 2w+1)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pc4 = wave * 2 + i;
+    const int row = pc4 * 4 + (lane >> 4), pc = lane & 15;
+    const int c = pc ^ swz(row);
+    const int gm = m + row;
+    const bf16* p = gm < me ? e + (size_t)gm * Q + q0 + 8 * c : g_zero_row + 8 * c;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + pc4 * 1024), 16, 0, 0);
+  }
+  // X: 32 pieces of 2 rows x 32 chunks (pieces 4w..4w+3); this lane's rows 8w + rsub + 2i
+  const int rsub = lane >> 5, pc = lane & 31;
+  const u32x4_t rr = lds_read128w(rows_lds + (uint32_t)(st * 64 + wave * 8 + rsub * 4) * 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = wave * 4 + i;
+    const int row = 2 * blk + rsub;
+    const int c = pc ^ swz(row);
+    const int cr = (int)rr[i];
+    const bf16* p = cr >= 0 ? table + (size_t)cr * D + k0 + 8 * c : g_zero_row + 8 * c;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + W64_E + blk * 1024), 16, 0, 0);
+  }
+  {
+    const int gm = m + lane;
+    const float* p = gm < me ? da + gm : g_zero_f32;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + W64_E + W64_X), 4, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void w64_sync(int inflight) {  // 7 glds per stage
+  __builtin_amdgcn_sched_barrier(0);
+  if (inflight >= 1) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// rewrite this thread's two 16-B chunks (rows r and r + 32) of a stage's E tile
+template <bool STATS>
+__device__ __forceinline__ void w64_transform(uint32_t base, int tid, float (&dw2)[8], float (&dsum)[8]) {
+  const int r = tid >> 4, pc = tid & 15;
+  const uint32_t ea0 = base + r * 256 + pc * 16, ea1 = ea0 + 32 * 256;
+  u32x4_t v0 = lds_read128(ea0), v1 = lds_read128(ea1);
+  float d0 = lds_read32(base + W64_E + W64_X + r * 4), d1 = lds_read32(base + W64_E + W64_X + (r + 32) * 4);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v0), "+v"(v1), "+v"(d0), "+v"(d1));
+  const bf16x8 e0 = __builtin_bit_cast(bf16x8, v0), e1 = __builtin_bit_cast(bf16x8, v1);
+  bf16x8 o0, o1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float f0 = (float)e0[k], f1 = (float)e1[k];
+    o0[k] = f2bf(d0 * (1.0f - f0 * f0));
+    o1[k] = f2bf(d1 * (1.0f - f1 * f1));
+    if constexpr (STATS) {
+      dw2[k] += d0 * f0 + d1 * f1;
+      dsum[k] += (float)o0[k] + (float)o1[k];
+    }
+  }
+  lds_write128(ea0, __builtin_bit_cast(u32x4_t, o0));
+  lds_write128(ea1, __builtin_bit_cast(u32x4_t, o1));
+}
+
+__global__ __launch_bounds__(512, 1) void head_wgrad64_kernel(const bf16* __restrict__ e,
+                                                              const bf16* __restrict__ table,
+                                                              const int* __restrict__ ids,
+                                                              const float* __restrict__ da, int M, int T, int D, int Q,
+                                                              float* __restrict__ P, float* __restrict__ dw2p,
+                                                              float* __restrict__ dsump, int tiles_k, int ntiles,
+                                                              int mchunk) {
+  __shared__ __attribute__((aligned(16))) char smem[W64_NST * W64_STAGE + 4 * W64_MAX_ROWS];
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rmd = nwg & 7;
+  const int t = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (bid >> 3);
+  const int s = t / ntiles, tile = t - s * ntiles;
+  const int qt = tile / tiles_k, kt = tile - qt * tiles_k;
+  const int q0 = qt * WQT, k0 = kt * WKT;
+  const int mb = s * mchunk;
+  const int me = min(M, mb + mchunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 2, wk = wave & 3;
+  const bool stats = kt == 0;
+
+  const int nsteps = me > mb ? (me - mb + W64_TM - 1) / W64_TM : 0;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+  // cache-row table, permuted: entry st*64 + 8w + 4 rsub + i <-> local row st*64 + 8w + rsub + 2i
+  int* rows_s = (int*)(smem + W64_NST * W64_STAGE);
+  for (int j = tid; j < nsteps * 64; j += 512) {
+    const int st = j >> 6, rp = j & 63;
+    const int w = rp >> 3, rsub = (rp >> 2) & 1, i = rp & 3;
+    const int gm = mb + st * 64 + 8 * w + rsub + 2 * i;
+    int cr = -1;
+    if (gm < me) {
+      const int u = gm / T;
+      cr = (ids != nullptr ? ids[u] : u) * T + (gm - u * T);
+    }
+    rows_s[j] = cr;
+  }
+  __syncthreads();
+  const uint32_t rows_lds = lds0 + W64_NST * W64_STAGE;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float sw2[8], ssum[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sw2[k] = ssum[k] = 0.f;
+
+#pragma unroll
+  for (int i = 0; i < W64_NST - 1; ++i)
+    if (i < nsteps) w64_stage(smem + i * W64_STAGE, e, table, rows_lds, da, D, Q, q0, k0, i, mb + i * W64_TM, me, wave,
+                              lane);
+  if (nsteps > 0) {
+    w64_sync(nsteps > 1 ? 1 : 0);
+    if (stats) w64_transform<true>(lds0, tid, sw2, ssum);
+    else w64_transform<false>(lds0, tid, sw2, ssum);
+  }
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  uint32_t xo[2][4][2], yo[2][4][2];  // [k32 half][frag][row half]
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r0 = h * 32 + g * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xo[h][j][0] = W64_E + tr_off_x(r0, wk * 64 + j * 16, q, p);
+      xo[h][j][1] = W64_E + tr_off_x(r0 + 4, wk * 64 + j * 16, q, p);
+      yo[h][j][0] = tr_off_e(r0, wn * 64 + j * 16, q, p);
+      yo[h][j][1] = tr_off_e(r0 + 4, wn * 64 + j * 16, q, p);
+    }
+  }
+  for (int st = 0; st < nsteps; ++st) {
+    w64_sync(st + 2 < nsteps ? 1 : 0);  // stage st+1 landed, stage st rewritten, stage st-1 read
+    if (st + 2 < nsteps)
+      w64_stage(smem + ((st + 2) % W64_NST) * W64_STAGE, e, table, rows_lds, da, D, Q, q0, k0, st + 2,
+                mb + (st + 2) * W64_TM, me, wave, lane);
+    if (st + 1 < nsteps) {
+      const uint32_t nb = lds0 + ((st + 1) % W64_NST) * W64_STAGE;
+      if (stats) w64_transform<true>(nb, tid, sw2, ssum);
+      else w64_transform<false>(nb, tid, sw2, ssum);
+    }
+    const uint32_t base = lds0 + (st % W64_NST) * W64_STAGE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      s16x4 xr[8], yr[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xr[2 * j] = tr_read(base + xo[h][j][0]);
+        xr[2 * j + 1] = tr_read(base + xo[h][j][1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        yr[2 * i] = tr_read(base + yo[h][i][0]);
+        yr[2 * i + 1] = tr_read(base + yo[h][i][1]);
+      }
+      LGKM_TIE8(xr);
+      LGKM_TIE8(yr);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 xb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xb[j] = join(xr[2 * j], xr[2 * j + 1]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 ya = join(yr[2 * i], yr[2 * i + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], ya, acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float* out = P + (size_t)s * Q * D;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qq2 = q0 + wn * 64 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wk * 64 + j * 16 + 4 * g;
+      *(f32x4*)(out + (size_t)qq2 * D + k) = acc[i][j];
+    }
+  }
+  if (stats) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* red = (float*)smem;  // [32 row-threads][128 q] x 2
+    const int r = tid >> 4, lc = (tid & 15) ^ swz(r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[r * WQT + lc * 8 + k] = sw2[k];
+      red[32 * WQT + r * WQT + lc * 8 + k] = ssum[k];
+    }
+    __syncthreads();
+    if (tid < 2 * WQT) {
+      const int which = tid / WQT, c = tid % WQT;
+      float acc2 = 0.f;
+      for (int rr = 0; rr < 32; ++rr) acc2 += red[which * 32 * WQT + rr * WQT + c];
+      (which == 0 ? dw2p : dsump)[(size_t)s * Q + q0 + c] = acc2;
+    }
+  }
+}
+
 // dW1 = w2 (.) sum_s P[s] ; db1 = w2 (.) sum_s dsum[s] ; dw2 = sum_s dw2p[s] ; db2 = sum_u db2p[u]
-// (fixed summation order: deterministic).  The last block does the small vectors.
+// (fixed summation order: deterministic).  A block owns 64 float4 of dW1: its 4 waves sum the
+// split partials s = w, w+4, ... (independent 16-B loads in flight per lane), then wave 0 adds
+// the 4 wave sums in order.  Then Q/64 blocks do dw2 / db1 the same way, the last block db2.
 __global__ __launch_bounds__(256) void head_reduce_kernel(const f32x4* __restrict__ P, const float* __restrict__ dw2p,
                                                           const float* __restrict__ dsump,
                                                           const float* __restrict__ db2p, const float* __restrict__ w2,
                                                           f32x4* __restrict__ dW1, float* __restrict__ db1,
                                                           float* __restrict__ dw2, float* __restrict__ db2, int S, int Q,
                                                           int D, int U) {
+  __shared__ f32x4 part[4][64];
+  __shared__ float red[4];
   const long n4 = (long)Q * D / 4;
-  if (blockIdx.x + 1 < gridDim.x) {
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)(gridDim.x - 1) * blockDim.x) {
-      f32x4 v = P[i];
-      for (int s = 1; s < S; ++s) v += P[(size_t)s * n4 + i];
-      dW1[i] = v * w2[(i * 4) / D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((long)blockIdx.x * 64 < n4) {
+    const long i = (long)blockIdx.x * 64 + lane;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+      int s = wave;
+#pragma unroll 4
+      for (; s + 12 < S; s += 16) {
+        const f32x4 a0 = P[(size_t)s * n4 + i], a1 = P[(size_t)(s + 4) * n4 + i];
+        const f32x4 a2 = P[(size_t)(s + 8) * n4 + i], a3 = P[(size_t)(s + 12) * n4 + i];
+        v += ((a0 + a1) + (a2 + a3));
+      }
+      for (; s < S; s += 4) v += P[(size_t)s * n4 + i];
+    }
+    part[wave][lane] = v;
+    __syncthreads();
+    if (wave == 0 && i < n4) dW1[i] = ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) * w2[(i * 4) / D];
+    return;
+  }
+  const int nmain = (int)((n4 + 63) / 64), nvec = (Q + 63) / 64;
+  if ((int)blockIdx.x < nmain + nvec) {  // 64 columns of dw2 / db1, the splits over 4 waves
+    const int q = ((int)blockIdx.x - nmain) * 64 + lane;
+    float a = 0.f, b = 0.f;
+    if (q < Q)
+#pragma unroll 4
+      for (int s = wave; s < S; s += 4) {
+        a += dw2p[(size_t)s * Q + q];
+        b += dsump[(size_t)s * Q + q];
+      }
+    float* pa = (float*)&part[0][0];
+    pa[wave * 64 + lane] = a;
+    pa[256 + wave * 64 + lane] = b;
+    __syncthreads();
+    if (wave == 0 && q < Q) {
+      dw2[q] = (pa[lane] + pa[64 + lane]) + (pa[128 + lane] + pa[192 + lane]);
+      db1[q] = ((pa[256 + lane] + pa[320 + lane]) + (pa[384 + lane] + pa[448 + lane])) * w2[q];
     }
     return;
   }
-  for (int q = threadIdx.x; q < Q; q += blockDim.x) {
-    float a = 0.f, b = 0.f;
-    for (int s = 0; s < S; ++s) {
-      a += dw2p[(size_t)s * Q + q];
-      b += dsump[(size_t)s * Q + q];
-    }
-    dw2[q] = a;
-    db1[q] = b * w2[q];
-  }
-  __shared__ float red[4];
   float c = 0.f;
   for (int u = threadIdx.x; u < U; u += blockDim.x) c += db2p[u];
   c = wave_sum(c);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  if (lane == 0) red[wave] = c;
   __syncthreads();
   if (threadIdx.x == 0) db2[0] = (red[0] + red[1]) + (red[2] + red[3]);
 }
@@ -674,16 +926,19 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
     g_wg_splits = env_int("FEDREC_HEAD_SPLITS", 0);
   }
   const int tiles_k = D / WKT, ntiles = (Q / WQT) * tiles_k;
-  // one wave of blocks (one per CU), each split >= 8 stages of 32 rows
-  int S = g_wg_splits > 0 ? g_wg_splits : g_cus / ntiles;
+  // one wave of blocks (one per CU), each split >= 8 stages of 32 rows.  A few CUs are left
+  // out: in the training step the next batch's sampler / dedup run on the lookahead stream
+  // meanwhile, and a block that cannot be placed beside them would start only after them --
+  // the whole grid then waits for one late block (measured 168 us in the step vs 117 alone)
+  int S = g_wg_splits > 0 ? g_wg_splits : (g_cus - 16) / ntiles;
   const int smax = (M + 8 * WTM - 1) / (8 * WTM);
   S = S < 1 ? 1 : (S > smax ? smax : S);
   if (S < 1) S = 1;
   int mchunk = ((M + S - 1) / S + WTM - 1) / WTM * WTM;
   if (mchunk < WTM) mchunk = WTM;
-  // a split's title ids must fit the LDS table: more splits for very short titles
-  const int cap = (MAX_SPLIT_TITLES - 2) * T / WTM * WTM;
-  if (mchunk > cap) mchunk = cap < WTM ? WTM : cap;
+  // a split's title ids (32-row forms) / cache-row table (64-row form) must fit in LDS
+  const int cap = ((g_wg_variant >> 1) & 3) == 3 ? W64_MAX_ROWS : (MAX_SPLIT_TITLES - 2) * T / WTM * WTM;
+  if (mchunk > cap) mchunk = cap < 64 ? 64 : cap / 64 * 64;
   S = (M + mchunk - 1) / mchunk;
   if (S < 1) S = 1;
   const long need = (long)S * Q * D + 2L * S * Q;
@@ -691,16 +946,26 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
   float* P = scratch;
   float* dw2p = scratch + (long)S * Q * D;
   float* dsump = dw2p + (long)S * Q;
-  if (M > 0)
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, da,
-                       M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1);
-  else {
+  // FEDREC_HEAD_WG bits 1-2: 0 -> 32-row stages x4 (default: 139 us at U = 1600 vs 146 / 149
+  // for x5 / x6 and 183 for the 64-row form, benchmarks/head_bench.py), 1 -> x5, 2 -> x6, 3 -> 64-row
+  const int nst = (g_wg_variant >> 1) & 3;
+  if (M > 0 && nst == 3) {
+    hipLaunchKernelGGL(head_wgrad64_kernel, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids,
+                       da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk);
+  } else if (M > 0) {
+#define LAUNCH_WG(N)                                                                                                 \
+  hipLaunchKernelGGL(head_wgrad_kernel<N>, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, \
+                     da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1)
+    if (nst == 1) LAUNCH_WG(5);
+    else if (nst == 2) LAUNCH_WG(6);
+    else LAUNCH_WG(4);  // (FEDREC_HEAD_WG bit 0 = no e -> g transform: diagnostic timing only)
+#undef LAUNCH_WG
+  } else {
     (void)hipMemsetAsync(scratch, 0, need * sizeof(float), s);
   }
   const long n4 = (long)Q * D / 4;
-  long blocks = (n4 + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)blocks + 1), dim3(256), 0, s, (const f32x4*)P, dw2p, dsump,
+  const long blocks = (n4 + 63) / 64 + (Q + 63) / 64 + 1;  // dW1 | dw2, db1 | db2
+  hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)P, dw2p, dsump,
                      db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U);
   return 0;
 }

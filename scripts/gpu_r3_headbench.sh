@@ -1,6 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+export PYTHONPATH=$GRAFT_REPO_ROOT:$PYTHONPATH
 run() { echo "== $*"; timeout -k 10 120 "$@" || exit 1; }
 run python -u benchmarks/head_bench.py --iters 30
 FEDREC_HEAD_WG=1 run python -u benchmarks/head_bench.py --iters 30
