@@ -96,6 +96,9 @@ def main() -> int:
     dev = ctx.device
     if dev.type == "cuda":
         native.lib()  # hard requirement on the GPU path
+    # N > 1: exact all-reduce self-check of the data group (RCCL on the node) before anything is
+    # timed; a wrong sum raises here and the run exits non-zero
+    selfcheck = fdist.selfcheck(ctx, log=lambda m: print(m, file=sys.stderr, flush=True))
 
     from fedrec_with_pytorchdistributed_amd.config import BackboneConfig
     from fedrec_with_pytorchdistributed_amd.parallel import comm
@@ -312,6 +315,7 @@ def main() -> int:
             "valid_auc": None if auc is None else round(auc, 4),
             "data_group": None if not (ctx.initialized and ctx.data_group is not None) else
             {"backend": dist.get_backend(ctx.data_group), "size": dist.get_world_size(ctx.data_group)},
+            "data_plane_selfcheck": selfcheck or None,
         }
         if rnd is not None:
             out.update(rnd)

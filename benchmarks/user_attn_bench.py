@@ -46,21 +46,24 @@ def main():
     qkv = torch.randn(a.B, a.H, 3 * NH * DK, generator=g).cuda()
     d = torch.randn(a.B, a.H, NH * DK, generator=g).cuda()
     outs = {}
-    for v in (0, 1):
+    for v in (0, 1, 2, 3):
         lib.user_attn_set_variant(v)
         c, st = ops.user_attention_fwd(qkv, NH, DK)
         outs[v] = (c, st, ops.user_attention_bwd(qkv, st, d, NH, DK))
-    res = {"fwd_rel_diff": float((outs[0][0] - outs[1][0]).norm() / outs[0][0].norm()),
-           "bwd_rel_diff": float((outs[0][2] - outs[1][2]).norm() / outs[0][2].norm())}
+    res = {"fwd_rel_diff_v3_v1": float((outs[3][0] - outs[1][0]).norm() / outs[1][0].norm()),
+           "bwd_rel_diff_v3_v1": float((outs[3][2] - outs[1][2]).norm() / outs[1][2].norm())}
     print(res, flush=True)
-    times = {f"{k}_v{v}": [] for k in ("fwd", "bwd") for v in (0, 1)}
-    st = outs[1][1]
+    times = {f"{k}_v{v}": [] for k in ("fwd", "bwd") for v in (0, 1, 2, 3)}
     for _ in range(a.rounds):
-        for v in (0, 1):
+        for v in (0, 1, 2, 3):
             lib.user_attn_set_variant(v)
+            st = outs[v][1]
             times[f"fwd_v{v}"].append(timeit(lambda: ops.user_attention_fwd(qkv, NH, DK)))
             times[f"bwd_v{v}"].append(timeit(lambda: ops.user_attention_bwd(qkv, st, d, NH, DK)))
-    lib.user_attn_set_variant(1)
+    for v in (10, 11):  # diagnostic partial forwards of the MFMA kernel
+        lib.user_attn_set_variant(v)
+        times[f"fwd_v{v}"] = [timeit(lambda: ops.user_attention_fwd(qkv, NH, DK)) for _ in range(a.rounds)]
+    lib.user_attn_set_variant(3)
     for k, v in times.items():
         res[k] = {"us": round(1000 * statistics.median(v), 2), "all_us": [round(1000 * x, 2) for x in v]}
         print(k, res[k], flush=True)

@@ -2,9 +2,10 @@
 //
 //   S = Q K^T / sqrt(d_k),  A = exp(S) / (rowsum exp(S) + 1e-8),  ctx = A V
 //
-// 20 heads x d_k 20 over H <= 64 clicked news, fp32 (the user side is tiny: ~0.5 MFLOP per
-// impression and head; it is latency-, not FLOP-bound, so it runs on the VALU with K/V
-// broadcast from LDS).  The eps softmax is evaluated stably:
+// 20 heads x d_k 20 over the clicked news, fp32.  H <= 64 runs on the matrix cores in fp32
+// (v_mfma_f32_16x16x4_f32, the "matrix-core forms" below -- the default); the VALU forms stay
+// for A/B runs (FEDREC_UA_VARIANT=1/0) and long histories (H > 64).  The eps softmax is
+// evaluated stably:
 // A = exp(S - m) / (sum exp(S - m) + 1e-8 exp(-m)).  No mask (Q7), like the reference.
 //
 // Forward: one wave per (impression, head), lane = query row; saves (m, l) per row.
@@ -266,7 +267,542 @@ __global__ __launch_bounds__(128) void user_attn_fwd_ilp_kernel(const float* __r
   st[1] = inv;
 }
 
-int g_ua_variant = 1;  // 1: ILP forward (default), 0: the first forward
+// ---------------------------------------------------------------------------------------
+// Matrix-core forms (default for H <= 64): every product of the attention runs on
+// v_mfma_f32_16x16x4_f32 -- fp32 in, fp32 accumulate, one rounding per product, so the numerics
+// are the fp32 reference's (attention.py:38-44) up to summation order.  d_k = 20 is exactly 5
+// k-steps of 4; the H <= 64 rows pad to 16-row tiles (rows >= H read as zeros, keys >= H get
+// probability 0).  One wave per (impression, head); Q, K, V (and dctx) rows are staged in LDS
+// as [64][20] fp32 (80-B rows: a 16 x 4 operand read hits 64 distinct banks), the probability /
+// dS tile goes through a [64][68] LDS image to change its lane layout between products.
+//
+// v_mfma_f32_16x16x4_f32 lane maps (cdna_hip_programming.md §3): A[i][k] from lane
+// (i = l & 15, k = l >> 4); B[k][j] from lane (k = l >> 4, j = l & 15); C[row][col] in lane
+// (col = l & 15, row = 4 (l >> 4) + reg).
+//
+// forward:  S = Q K^T (80 MFMA), row softmax on the C layout (xor-shuffles over the 16 lanes
+//           of a row), ctx = P V (P through LDS; <= 128 MFMA), saves (m, 1/l) per row.
+// backward: S again -> P; dP = dctx V^T (80); D_t = sum_s P dP; dS = P (dP - D) / sqrt(d_k);
+//           dV = P^T dctx, dQ = dS K, dK = dS^T Q (<= 128 each, P / dS through LDS).
+// ---------------------------------------------------------------------------------------
+constexpr int PLD = 68;  // LDS row stride of the [64 x 64] P / dS image (conflict-free both ways)
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// rows [0, 16 NT) of NOP [H, DK] head slices (row stride ld each) into xs[o][64][DK], zero rows
+// >= H.  Every load of every slice is issued before the first LDS store (5 NT / 4 float4 per
+// lane and slice in flight), the row index is clamped and the padded rows zeroed by a select:
+// a load guarded by a per-lane condition compiles to a branch around it with a vmcnt(0) wait
+// per load (cdna_hip_programming.md §5 trap (c)), and staging the slices one after the other
+// waited out one load latency per slice
+template <int NT, int NOP>
+__device__ __forceinline__ void stage_heads(float (*const (&xs)[NOP])[DK], const float* const (&src)[NOP],
+                                            const size_t (&ld)[NOP], int H, int lane) {
+  constexpr int N4 = NT * 16 * (DK / 4);  // float4 chunks of one padded slice
+  constexpr int IT = (N4 + 63) / 64;
+  float4 v[NOP][IT];
+#pragma unroll
+  for (int o = 0; o < NOP; ++o)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = lane + 64 * it;
+      const int r = min(i / (DK / 4), H - 1), c = (i % (DK / 4)) * 4;
+      v[o][it] = *(const float4*)(src[o] + (size_t)r * ld[o] + c);
+    }
+#pragma unroll
+  for (int o = 0; o < NOP; ++o)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = lane + 64 * it;
+      const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+      const bool z = r >= H;
+      const float4 w = make_float4(z ? 0.f : v[o][it].x, z ? 0.f : v[o][it].y, z ? 0.f : v[o][it].z,
+                                   z ? 0.f : v[o][it].w);
+      if (i < N4) *(float4*)&xs[o][r][c] = w;
+    }
+}
+
+// C[i][j] += X Y^T over d_k for 16-row tiles i, j < NT (X, Y: [64][DK] in LDS)
+template <int NT>
+__device__ __forceinline__ void mm_xyT(f32x4 (&c)[4][4], float (*X)[DK], float (*Y)[DK], int fr, int fq) {
+#pragma unroll
+  for (int kk = 0; kk < DK / 4; ++kk) {
+    float a[NT], b[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) a[i] = X[i * 16 + fr][4 * kk + fq];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) b[j] = Y[j * 16 + fr][4 * kk + fq];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) c[i][j] = mfma4(a[i], b[j], c[i][j]);
+  }
+}
+
+// out[i][dj] = sum_k A(i*16 + fr, k) * Y[k][dj*16 + fr'] over k < KS*4, A read from the
+// [64][PLD] image P either as P[row][k] (TRANS = false) or P[k][row] (TRANS = true)
+template <int NT, bool TRANS>
+__device__ __forceinline__ void mm_pY(f32x4 (&o)[4][2], const float* __restrict__ P, float (*Y)[DK], int KS, int fr,
+                                      int fq) {
+#pragma unroll
+  for (int kk = 0; kk < NT * 4; ++kk) {  // unrolled to the tile bound: LDS reads hoist over MFMAs
+    if (kk >= KS) break;
+    const int k = 4 * kk + fq;
+    // (column 16 + fr >= DK reads the next row -- the arrays carry a 16-float tail -- and is
+    // zeroed by the select: no branch around the LDS read)
+    const float y0 = Y[k][fr], y1r = Y[k][16 + fr], y1 = fr < DK - 16 ? y1r : 0.f;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const float a = TRANS ? P[k * PLD + i * 16 + fr] : P[(i * 16 + fr) * PLD + k];
+      o[i][0] = mfma4(a, y0, o[i][0]);
+      o[i][1] = mfma4(a, y1, o[i][1]);
+    }
+  }
+}
+
+// store rows (tile i: 4 fq + r) x columns (dj*16 + fr < DK) of o, scaled per row by rs[i][r]
+template <int NT>
+__device__ __forceinline__ void store_head(float* __restrict__ dst, size_t ld, const f32x4 (&o)[4][2],
+                                           const float (*rs)[4], int H, int fr, int fq) {
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i * 16 + fq * 4 + r;
+      if (row >= H) continue;
+      const float sc = rs != nullptr ? rs[i][r] : 1.f;
+      dst[(size_t)row * ld + fr] = o[i][0][r] * sc;
+      if (fr < DK - 16) dst[(size_t)row * ld + 16 + fr] = o[i][1][r] * sc;
+    }
+}
+
+// reductions over the 16 lanes of a DPP row (= one C-layout row of a 16x16 tile): four DPP
+// butterflies (quad_perm xor 1, xor 2, row_half_mirror, row_mirror) -- VALU-speed lane moves,
+// where __shfl_xor is a ds_bpermute round trip through the LDS crossbar per step
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+constexpr int DPP_XOR1 = 0xB1;       // quad_perm [1, 0, 3, 2]
+constexpr int DPP_XOR2 = 0x4E;       // quad_perm [2, 3, 0, 1]
+constexpr int DPP_HALF_MIRROR = 0x141;
+constexpr int DPP_MIRROR = 0x140;
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp<DPP_XOR1>(v));
+  v = fmaxf(v, dpp<DPP_XOR2>(v));
+  v = fmaxf(v, dpp<DPP_HALF_MIRROR>(v));
+  return fmaxf(v, dpp<DPP_MIRROR>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp<DPP_XOR1>(v);
+  v += dpp<DPP_XOR2>(v);
+  v += dpp<DPP_HALF_MIRROR>(v);
+  return v + dpp<DPP_MIRROR>(v);
+}
+
+template <int NT, int DBG = 0>
+__global__ __launch_bounds__(64) void user_attn_fwd_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
+                                                                float* __restrict__ stats, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float qs[65][DK];  // row 64: the tail of mm_pY's column reads
+  __shared__ __attribute__((aligned(16))) float ks[65][DK];
+  __shared__ __attribute__((aligned(16))) float vs[65][DK];
+  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
+  const int lane = threadIdx.x, fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  {
+    float (*const xs[3])[DK] = {qs, ks, vs};
+    const float* const src[3] = {base, base + D, base + 2 * D};
+    const size_t lds[3] = {(size_t)ld, (size_t)ld, (size_t)ld};
+    stage_heads<NT, 3>(xs, src, lds, H, lane);
+  }
+  __syncthreads();
+  if constexpr (DBG == 1) {  // diagnostic timing: staging only
+    if (lane == 0) ctx[(size_t)b * H * NH * DK + h] = qs[1][1] + ks[2][2] + vs[3][3];
+    return;
+  }
+  f32x4 s[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mm_xyT<NT>(s, qs, ks, fr, fq);
+  const float scale = rsqrtf((float)DK);
+  float inv[4][4], mrow[4][4];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const float v = j * 16 + fr < H ? s[i][j][r] * scale : -INFINITY;
+        s[i][j][r] = v;
+        m = fmaxf(m, v);
+      }
+      m = row16_max(m);
+      float l = 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const float p = __expf(s[i][j][r] - m);  // exp(-inf) = 0 for the padded keys
+        s[i][j][r] = p;
+        l += p;
+        ps[(i * 16 + fq * 4 + r) * PLD + j * 16 + fr] = p;
+      }
+      l = row16_sum(l) + 1e-8f * __expf(-m);
+      inv[i][r] = 1.0f / l;
+      mrow[i][r] = m;
+    }
+  __syncthreads();
+  if constexpr (DBG == 2) {  // diagnostic timing: staging + S + softmax
+    if (lane == 0) ctx[(size_t)b * H * NH * DK + h] = inv[0][0] + ps[5];
+    return;
+  }
+  f32x4 o[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mm_pY<NT, false>(o, ps, vs, (H + 3) / 4, fr, fq);
+  store_head<NT>(ctx + (size_t)b * H * D + h * DK, D, o, inv, H, fr, fq);
+  if (fr == 0) {
+    float* st = stats + ((size_t)b * NH + h) * H * 2;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        if (row < H) {
+          st[2 * row] = mrow[i][r];
+          st[2 * row + 1] = inv[i][r];
+        }
+      }
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(64) void user_attn_bwd_mfma_kernel(const float* __restrict__ qkv,
+                                                                const float* __restrict__ stats,
+                                                                const float* __restrict__ dctx,
+                                                                float* __restrict__ dqkv, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float qs[65][DK];  // row 64: the tail of mm_pY's column reads
+  __shared__ __attribute__((aligned(16))) float ks[65][DK];
+  __shared__ __attribute__((aligned(16))) float vs[65][DK];
+  __shared__ __attribute__((aligned(16))) float gs[65][DK];
+  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
+  const int lane = threadIdx.x, fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  {
+    float (*const xs[4])[DK] = {qs, ks, vs, gs};
+    const float* const src[4] = {base, base + D, base + 2 * D, dctx + (size_t)b * H * D + h * DK};
+    const size_t lds[4] = {(size_t)ld, (size_t)ld, (size_t)ld, (size_t)D};
+    stage_heads<NT, 4>(xs, src, lds, H, lane);
+  }
+  const float* st = stats + ((size_t)b * NH + h) * H * 2;
+  float mrow[4][4], inv[4][4];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i * 16 + fq * 4 + r, rc = min(row, H - 1);
+      const float mv = st[2 * rc], iv = st[2 * rc + 1];  // unconditional loads (see stage_head)
+      mrow[i][r] = row < H ? mv : 0.f;
+      inv[i][r] = row < H ? iv : 0.f;
+    }
+  __syncthreads();
+  f32x4 p[4][4], dp[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[i][j] = dp[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mm_xyT<NT>(p, qs, ks, fr, fq);
+  mm_xyT<NT>(dp, gs, vs, fr, fq);
+  const float scale = rsqrtf((float)DK);
+  // P = exp(S scale - m) / l; D_t = sum_s P dP; dS = P (dP - D) scale (kept in dp)
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float Dt = 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const float pv = j * 16 + fr < H ? __expf(p[i][j][r] * scale - mrow[i][r]) * inv[i][r] : 0.f;
+        p[i][j][r] = pv;
+        Dt += pv * dp[i][j][r];
+        ps[(i * 16 + fq * 4 + r) * PLD + j * 16 + fr] = pv;
+      }
+      Dt = row16_sum(Dt);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) dp[i][j][r] = p[i][j][r] * (dp[i][j][r] - Dt) * scale;
+    }
+  __syncthreads();
+  float* dbase = dqkv + (size_t)b * H * ld + h * DK;
+  const int KS = (H + 3) / 4;
+  f32x4 o[4][2];
+  // dV = P^T dctx (rows = keys)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mm_pY<NT, true>(o, ps, gs, KS, fr, fq);
+  store_head<NT>(dbase + 2 * D, ld, o, nullptr, H, fr, fq);
+  __syncthreads();  // every lane done reading P before it is overwritten by dS
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) ps[(i * 16 + fq * 4 + r) * PLD + j * 16 + fr] = dp[i][j][r];
+  __syncthreads();
+  // dQ = dS K (rows = queries), dK = dS^T Q (rows = keys)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mm_pY<NT, false>(o, ps, ks, KS, fr, fq);
+  store_head<NT>(dbase, ld, o, nullptr, H, fr, fq);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mm_pY<NT, true>(o, ps, qs, KS, fr, fq);
+  store_head<NT>(dbase + D, ld, o, nullptr, H, fr, fq);
+}
+
+// Four-wave forms (the default): one workgroup per (impression, head), wave w owns query tile
+// w (rows 16w..16w+15) -- S row tile, softmax and ctx rows; in the backward also dQ of its rows,
+// then (after one barrier, P and dS complete in LDS) key tile w -- dK and dV of its keys.  A wave
+// has a quarter of the one-wave form's serial MFMA / softmax work and the CU 4x the waves to
+// hide the staging latency.
+__global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* __restrict__ qkv,
+                                                                  float* __restrict__ ctx, float* __restrict__ stats,
+                                                                  int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float qs[65][DK];
+  __shared__ __attribute__((aligned(16))) float ks[65][DK];
+  __shared__ __attribute__((aligned(16))) float vs[65][DK];
+  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  {  // 3 x 320 float4 chunks over 256 threads, every load in flight before the stores
+    float4 v[3][2];
+#pragma unroll
+    for (int o = 0; o < 3; ++o)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int i = tid + 256 * it;
+        const int r = min(min(i, 319) / (DK / 4), H - 1), c = (i % (DK / 4)) * 4;
+        v[o][it] = *(const float4*)(base + (size_t)o * D + (size_t)r * ld + c);
+      }
+    float (*const xs[3])[DK] = {qs, ks, vs};
+#pragma unroll
+    for (int o = 0; o < 3; ++o)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int i = tid + 256 * it;
+        const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+        const bool z = r >= H;
+        const float4 w = make_float4(z ? 0.f : v[o][it].x, z ? 0.f : v[o][it].y, z ? 0.f : v[o][it].z,
+                                     z ? 0.f : v[o][it].w);
+        if (i < 320) *(float4*)&xs[o][r][c] = w;
+      }
+  }
+  __syncthreads();
+  const int i0 = wave * 16;
+  if (i0 >= H) return;  // wave-uniform; no barrier follows
+  const int NT = (H + 15) / 16;
+  f32x4 s[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < DK / 4; ++kk) {
+    const float a = qs[i0 + fr][4 * kk + fq];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < NT) s[j] = mfma4(a, ks[j * 16 + fr][4 * kk + fq], s[j]);
+  }
+  const float scale = rsqrtf((float)DK);
+  float* pw = ps + wave * 16 * PLD;  // this wave's 16 rows of P
+  float inv[4], mrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = (j < NT && j * 16 + fr < H) ? s[j][r] * scale : -INFINITY;
+      s[j][r] = v;
+      m = fmaxf(m, v);
+    }
+    m = row16_max(m);
+    float l = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float p = __expf(s[j][r] - m);
+      l += p;
+      pw[(fq * 4 + r) * PLD + j * 16 + fr] = p;
+    }
+    l = row16_sum(l) + 1e-8f * __expf(-m);
+    inv[r] = 1.0f / l;
+    mrow[r] = m;
+  }
+  f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
+  const int KS = (H + 3) / 4;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    if (kk >= KS) break;
+    const int k = 4 * kk + fq;
+    const float a = pw[fr * PLD + k];
+    const float y0 = vs[k][fr], y1r = vs[k][16 + fr], y1 = fr < DK - 16 ? y1r : 0.f;
+    o0 = mfma4(a, y0, o0);
+    o1 = mfma4(a, y1, o1);
+  }
+  float* dst = ctx + (size_t)b * H * D + h * DK;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = i0 + fq * 4 + r;
+    if (row >= H) continue;
+    dst[(size_t)row * D + fr] = o0[r] * inv[r];
+    if (fr < DK - 16) dst[(size_t)row * D + 16 + fr] = o1[r] * inv[r];
+    if (fr == 0) {
+      float* st = stats + (((size_t)b * NH + h) * H + row) * 2;
+      st[0] = mrow[r];
+      st[1] = inv[r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* __restrict__ qkv,
+                                                                  const float* __restrict__ stats,
+                                                                  const float* __restrict__ dctx,
+                                                                  float* __restrict__ dqkv, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) float qs[65][DK];
+  __shared__ __attribute__((aligned(16))) float ks[65][DK];
+  __shared__ __attribute__((aligned(16))) float vs[65][DK];
+  __shared__ __attribute__((aligned(16))) float gs[65][DK];
+  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
+  __shared__ __attribute__((aligned(16))) float dss[64 * PLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  const float* gbase = dctx + (size_t)b * H * D + h * DK;
+  {
+    float4 v[4][2];
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int i = tid + 256 * it;
+        const int r = min(min(i, 319) / (DK / 4), H - 1), c = (i % (DK / 4)) * 4;
+        v[o][it] = o < 3 ? *(const float4*)(base + (size_t)o * D + (size_t)r * ld + c)
+                         : *(const float4*)(gbase + (size_t)r * D + c);
+      }
+    float (*const xs[4])[DK] = {qs, ks, vs, gs};
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int i = tid + 256 * it;
+        const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+        const bool z = r >= H;
+        const float4 w = make_float4(z ? 0.f : v[o][it].x, z ? 0.f : v[o][it].y, z ? 0.f : v[o][it].z,
+                                     z ? 0.f : v[o][it].w);
+        if (i < 320) *(float4*)&xs[o][r][c] = w;
+      }
+  }
+  const int i0 = wave * 16;
+  const int NT = (H + 15) / 16;
+  const float* st = stats + ((size_t)b * NH + h) * H * 2;
+  float mrow[4], inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = i0 + fq * 4 + r, rc = min(row, H - 1);
+    const float mv = st[2 * rc], iv = st[2 * rc + 1];
+    mrow[r] = row < H ? mv : 0.f;
+    inv[r] = row < H ? iv : 0.f;
+  }
+  __syncthreads();
+  const float scale = rsqrtf((float)DK);
+  float* dst = dqkv + (size_t)b * H * ld + h * DK;
+  const int KS = (H + 3) / 4;
+  if (i0 < H) {  // query tile: P, dP, D, dS rows into LDS; dQ
+    f32x4 p[4], dp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < DK / 4; ++kk) {
+      const float a = qs[i0 + fr][4 * kk + fq], g = gs[i0 + fr][4 * kk + fq];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < NT) {
+          p[j] = mfma4(a, ks[j * 16 + fr][4 * kk + fq], p[j]);
+          dp[j] = mfma4(g, vs[j * 16 + fr][4 * kk + fq], dp[j]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float Dt = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float pv = (j < NT && j * 16 + fr < H) ? __expf(p[j][r] * scale - mrow[r]) * inv[r] : 0.f;
+        p[j][r] = pv;
+        Dt += pv * dp[j][r];
+      }
+      Dt = row16_sum(Dt);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int idx = (i0 + fq * 4 + r) * PLD + j * 16 + fr;
+        ps[idx] = p[j][r];
+        dss[idx] = p[j][r] * (dp[j][r] - Dt) * scale;
+      }
+    }
+    // dQ rows of this tile = dS K (this wave's own dS rows)
+    f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      if (kk >= KS) break;
+      const int k = 4 * kk + fq;
+      const float a = dss[(i0 + fr) * PLD + k];
+      const float y0 = ks[k][fr], y1r = ks[k][16 + fr], y1 = fr < DK - 16 ? y1r : 0.f;
+      o0 = mfma4(a, y0, o0);
+      o1 = mfma4(a, y1, o1);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i0 + fq * 4 + r;
+      if (row >= H) continue;
+      dst[(size_t)row * ld + fr] = o0[r];
+      if (fr < DK - 16) dst[(size_t)row * ld + 16 + fr] = o1[r];
+    }
+  }
+  __syncthreads();  // every P / dS row in LDS
+  if (i0 >= H) return;
+  // key tile i0: dV = P^T dctx, dK = dS^T Q (sums over every query)
+  f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0, k0 = v0, k1 = v0;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    if (kk >= KS) break;
+    const int t = 4 * kk + fq;
+    const float pa = ps[t * PLD + i0 + fr], da = dss[t * PLD + i0 + fr];
+    const float g0 = gs[t][fr], g1r = gs[t][16 + fr], g1 = fr < DK - 16 ? g1r : 0.f;
+    const float q0 = qs[t][fr], q1r = qs[t][16 + fr], q1 = fr < DK - 16 ? q1r : 0.f;
+    v0 = mfma4(pa, g0, v0);
+    v1 = mfma4(pa, g1, v1);
+    k0 = mfma4(da, q0, k0);
+    k1 = mfma4(da, q1, k1);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = i0 + fq * 4 + r;
+    if (row >= H) continue;
+    dst[(size_t)row * ld + D + fr] = k0[r];
+    dst[(size_t)row * ld + 2 * D + fr] = v0[r];
+    if (fr < DK - 16) {
+      dst[(size_t)row * ld + D + 16 + fr] = k1[r];
+      dst[(size_t)row * ld + 2 * D + 16 + fr] = v1[r];
+    }
+  }
+}
+
+int g_ua_variant = 3;  // 3: four-wave MFMA (default), 2: one-wave MFMA, 1: VALU ILP forward, 0: first VALU forward
 
 // ---------------------------------------------------------------------------------------
 // Long histories (H > 64): the reference pads but never truncates (dataset.py:84, quirk Q6;
@@ -451,7 +987,18 @@ extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int 
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH);
-  else if (g_ua_variant == 1)
+  else if (g_ua_variant >= 10) {  // diagnostic partial forwards (timing only): 10 staging, 11 + S/softmax
+    if (g_ua_variant == 10) hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 1>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
+    else hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 2>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
+  } else if (g_ua_variant == 3) {
+    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH);
+  } else if (g_ua_variant == 2) {
+    const int nt = (H + 15) / 16;
+    if (nt == 1) hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<1>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
+    else if (nt == 2) hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<2>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
+    else if (nt == 3) hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<3>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
+    else hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<4>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
+  } else if (g_ua_variant == 1)
     hipLaunchKernelGGL(user_attn_fwd_ilp_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
   else
     hipLaunchKernelGGL(user_attn_fwd_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
@@ -465,7 +1012,18 @@ extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const floa
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
-  else
+  else if (g_ua_variant == 3)
+    hipLaunchKernelGGL(user_attn_bwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH);
+  else if (g_ua_variant == 2) {
+    const int nt = (H + 15) / 16;
+#define UA_BWD(N) \
+  hipLaunchKernelGGL(user_attn_bwd_mfma_kernel<N>, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, H, NH)
+    if (nt == 1) UA_BWD(1);
+    else if (nt == 2) UA_BWD(2);
+    else if (nt == 3) UA_BWD(3);
+    else UA_BWD(4);
+#undef UA_BWD
+  } else
     hipLaunchKernelGGL(user_attn_bwd_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   return 0;
 }

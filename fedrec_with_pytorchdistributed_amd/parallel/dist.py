@@ -101,6 +101,44 @@ def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0, g
     return ctx
 
 
+def selfcheck(ctx: DistContext, nbytes: int = 4 << 20, log=None) -> dict:
+    """Data-plane self-check before any timed / training work at N > 1 clients: every client
+    all-reduces (a) its client index + 1 as an exact int64 scalar and (b) a ``nbytes`` fp32
+    buffer of ones over the DATA group (RCCL over xGMI on the GPU), and the sums must be exact
+    (W (W + 1) / 2 and W everywhere).  A misconfigured group, a wrong device mapping or a
+    transport fault fails loudly here instead of as a silently wrong average later.  Returns
+    ``{backend, size, us_4MB}``; raises RuntimeError on a mismatch."""
+    import time
+
+    if not ctx.initialized or ctx.num_clients <= 1 or ctx.client_index < 0:
+        return {}
+    W, k = ctx.num_clients, ctx.client_index
+    dev = ctx.device
+    t = torch.tensor([k + 1], dtype=torch.int64, device=dev)
+    buf = torch.ones(max(1, nbytes // 4), dtype=torch.float32, device=dev)
+    dist.all_reduce(t, group=ctx.data_group)
+    dist.all_reduce(buf, group=ctx.data_group)  # warm-up / connection set-up
+    buf.fill_(1.0)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    dist.all_reduce(buf, group=ctx.data_group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    us = (time.perf_counter() - t0) * 1e6
+    got_ids = int(t.item())
+    ok_ids = got_ids == W * (W + 1) // 2
+    bad = int((buf != float(W)).sum().item())
+    info = {"backend": dist.get_backend(ctx.data_group), "size": dist.get_world_size(ctx.data_group),
+            "device": str(dev), "us_4MB": round(us, 1), "ok": ok_ids and bad == 0}
+    if log is not None:
+        log(f"[client {k}] data-plane self-check: {info}")
+    if not info["ok"]:
+        raise RuntimeError(f"data-plane self-check FAILED on client {k}: id sum {got_ids} (expected "
+                           f"{W * (W + 1) // 2}), {bad} wrong elements of {buf.numel()} (expected {W})")
+    return info
+
+
 def shutdown(ctx: DistContext) -> None:
     if ctx.initialized and dist.is_initialized():
         try:

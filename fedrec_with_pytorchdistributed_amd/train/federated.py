@@ -37,7 +37,8 @@ from ..parallel import comm
 from ..parallel import secagg
 from ..parallel.collcheck import CHECK
 from ..parallel.control import ControlPlane, Heartbeat
-from ..parallel.dist import DistContext, make_bucket_reducer, make_grad_allreduce, make_secure_grad_allreduce
+from ..parallel.dist import (DistContext, make_bucket_reducer, make_grad_allreduce, make_secure_grad_allreduce,
+                             selfcheck)
 from ..privacy.rdp import calibrate_client_sigma
 from ..utils import obs
 from ..utils.fault import FaultInjector
@@ -163,6 +164,7 @@ def _resume(cfg: FedRecConfig, model: FedRecModel) -> Tuple[int, Dict]:
 
 # ---------------------------------------------------------------------------------------
 def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
+    selfcheck(ctx, log=obs.log)
     shard = load_client_shard(cfg, ctx)
     model = build_model(cfg, ctx.device)
     start, est = _resume(cfg, model)
@@ -201,6 +203,7 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
 
 
 def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
+    selfcheck(ctx, log=obs.log)
     shard = load_client_shard(cfg, ctx)
     model = build_model(cfg, ctx.device)
     start, est = _resume(cfg, model)
@@ -291,6 +294,8 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     # xGMI on the GPU) -- one host transfer per round instead of one per client.  With a
     # quorum < 1 a dead client must not stall a collective, so every client reads the store.
     bcast = ctx.initialized and ctx.num_clients > 1 and ctx.data_group is not None and cfg.quorum >= 1.0
+    if bcast or agg == "allreduce":
+        selfcheck(ctx, log=obs.log)  # every client, before round 0 (the coordinator is not in the data group)
     if k == 0:
         plane = {"backend": dist.get_backend(ctx.data_group) if bcast else "store",
                  "size": dist.get_world_size(ctx.data_group) if bcast else 1}
