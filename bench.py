@@ -217,7 +217,7 @@ def main() -> int:
 
     # untimed: the data-plane share of a step -- the same flat-bucket RCCL all-reduce the GA
     # step issues, alone, averaged over 20 calls (bus bandwidth = 2 (W-1)/W x bytes / time)
-    comm_ms = busbw = None
+    comm_ms = busbw = ipc_info = None
     if ctx.initialized and world > 1 and dev.type == "cuda" and args.config in (2, 4):
         g = torch.zeros_like(model.flat.grad)
         for _ in range(3):
@@ -232,6 +232,32 @@ def main() -> int:
         dist.all_reduce(ct, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
         comm_ms = 1000.0 * float(ct.item())
         busbw = 2.0 * (world - 1) / world * g.numel() * g.element_size() / (comm_ms / 1000.0) / 1e9
+        # the custom IPC all-reduce (one-shot over xGMI) on the same bucket, for comparison; its
+        # result is checked against RCCL's first.  A failure is reported, not fatal.
+        try:
+            ipc = fdist.make_ipc_allreduce(ctx)
+            a = torch.randn_like(g)
+            b = a.clone()
+            dist.all_reduce(a, group=ctx.data_group)
+            ipc.allreduce_(b)
+            sync()
+            ok = torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+            for _ in range(3):
+                ipc.allreduce_(g)
+            sync()
+            dist.barrier(group=ctx.ctrl_group)
+            t1 = time.perf_counter()
+            for _ in range(20):
+                ipc.allreduce_(g)
+            sync()
+            ct = torch.tensor([(time.perf_counter() - t1) / 20], dtype=torch.float64)
+            dist.all_reduce(ct, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
+            ipc_ms = 1000.0 * float(ct.item())
+            ipc_info = {"ms": round(ipc_ms, 4), "matches_rccl": bool(ok), "status": ipc.status(),
+                        "busbw_GBps": round(2.0 * (world - 1) / world * g.numel() * 4 / (ipc_ms / 1000.0) / 1e9, 2)}
+            ipc.close()
+        except Exception as e:  # pragma: no cover - depends on the node
+            ipc_info = {"error": repr(e)[:300]}
 
     def reduce_valid(m):
         vals = np.array([m["valid_auc"] * m["n_valid"], m["n_valid"]], dtype=np.float64)
@@ -316,6 +342,7 @@ def main() -> int:
             "data_group": None if not (ctx.initialized and ctx.data_group is not None) else
             {"backend": dist.get_backend(ctx.data_group), "size": dist.get_world_size(ctx.data_group)},
             "data_plane_selfcheck": selfcheck or None,
+            "ipc_allreduce": ipc_info,
         }
         if rnd is not None:
             out.update(rnd)

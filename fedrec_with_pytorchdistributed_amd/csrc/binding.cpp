@@ -49,6 +49,14 @@ int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, cons
 long fr_head_wgrad(const void* e, const void* table, const int* ids, const float* da, const float* db2p,
                    const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2, float* db2,
                    float* scratch, hipStream_t s);
+int fr_ipc_create(long cap, void* handle_out);
+int fr_ipc_open(int id, const void* handles, int me, int W, const long long* local_ptrs);
+long long fr_ipc_region(int id);
+int* fr_ipc_status(int id);
+int fr_ipc_allreduce(int id, void* x, long n, int is_int, long long epoch, int mode, int blocks, hipStream_t s);
+int fr_ipc_destroy(int id);
+int fr_ipc_allreduce_local(const int* ids, void* const* xs, int W, long n, int is_int, long long epoch, int mode,
+                           int blocks, hipStream_t s);
 int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, hipStream_t s);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
                      int dk, hipStream_t s);
@@ -387,6 +395,70 @@ int64_t head_titles(const at::Tensor& table, const c10::optional<at::Tensor>& id
 }
 const int* opt_int_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr<int>() : nullptr; }
 }  // namespace
+
+// ---- peer-to-peer all-reduce over IPC-mapped buffers (ipc_allreduce.hip) --------------------
+std::tuple<int64_t, at::Tensor> ipc_create(int64_t cap) {
+  auto h = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  const int id = fr_ipc_create((long)cap, h.data_ptr());
+  TORCH_CHECK(id >= 0, "fedrec::ipc_create failed (code ", id, ")");
+  return {id, h};
+}
+
+void ipc_open(int64_t id, const at::Tensor& handles, int64_t me, int64_t W, const c10::optional<at::Tensor>& local) {
+  TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.numel() == 64 * W &&
+                  handles.is_contiguous(),
+              "fedrec::ipc_open: handles uint8 [W*64] on the host");
+  const long long* lp = nullptr;
+  at::Tensor lc;
+  if (local.has_value()) {
+    lc = local->to(at::kLong).contiguous();
+    TORCH_CHECK(!lc.is_cuda() && lc.numel() == W, "fedrec::ipc_open: local_ptrs int64 [W] on the host");
+    lp = (const long long*)lc.data_ptr<int64_t>();
+  }
+  const int rc = fr_ipc_open((int)id, handles.data_ptr(), (int)me, (int)W, lp);
+  TORCH_CHECK(rc == 0, "fedrec::ipc_open failed (code ", rc, ")");
+}
+
+int64_t ipc_region(int64_t id) { return (int64_t)fr_ipc_region((int)id); }
+
+int64_t ipc_status(int64_t id) {  // device -> host read (tests / diagnostics only)
+  int* st = fr_ipc_status((int)id);
+  TORCH_CHECK(st != nullptr, "fedrec::ipc_status: bad id");
+  int v = 0;
+  TORCH_CHECK(hipMemcpy(&v, st, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess, "fedrec::ipc_status: copy");
+  return v;
+}
+
+void ipc_allreduce_(int64_t id, at::Tensor x, int64_t epoch, int64_t mode, int64_t blocks) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kInt) && x.numel() % 4 == 0,
+              "fedrec::ipc_allreduce_: contiguous fp32 / int32, numel % 4 == 0");
+  const c10::DeviceGuard g(x.device());
+  check_rc(fr_ipc_allreduce((int)id, x.data_ptr(), (long)x.numel(), x.scalar_type() == at::kInt ? 1 : 0,
+                            (long long)epoch, (int)mode, (int)blocks, cur_stream()),
+           "ipc_allreduce_");
+}
+
+void ipc_destroy(int64_t id) { (void)fr_ipc_destroy((int)id); }
+
+// single-process rehearsal: every rank's context + tensor, one launch playing all ranks
+void ipc_allreduce_local_(at::IntArrayRef ids, at::TensorList xs, int64_t epoch, int64_t mode, int64_t blocks) {
+  TORCH_CHECK(ids.size() == xs.size() && !xs.empty() && xs.size() <= 16, "fedrec::ipc_allreduce_local_: W tensors");
+  std::vector<int> iv(ids.begin(), ids.end());
+  std::vector<void*> pv;
+  for (const auto& x : xs) {
+    check_dev(x, "x");
+    TORCH_CHECK(x.is_contiguous() && x.scalar_type() == xs[0].scalar_type() && x.numel() == xs[0].numel() &&
+                    (x.scalar_type() == at::kFloat || x.scalar_type() == at::kInt) && x.numel() % 4 == 0,
+                "fedrec::ipc_allreduce_local_: contiguous fp32 / int32 tensors of one size, numel % 4 == 0");
+    pv.push_back(x.data_ptr());
+  }
+  const c10::DeviceGuard g(xs[0].device());
+  check_rc(fr_ipc_allreduce_local(iv.data(), pv.data(), (int)xs.size(), (long)xs[0].numel(),
+                                  xs[0].scalar_type() == at::kInt ? 1 : 0, (long long)epoch, (int)mode, (int)blocks,
+                                  cur_stream()),
+           "ipc_allreduce_local_");
+}
 
 bool head_supported(int64_t D, int64_t Q, int64_t T) { return fr_head_supported((int)D, (int)Q, (int)T) != 0; }
 
@@ -1268,6 +1340,13 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("title_attention(Tensor qkv, Tensor mask, int n_heads) -> Tensor");
   m.def("head_supported(int D, int Q, int T) -> bool", &head_supported);
+  m.def("ipc_create(int cap) -> (int, Tensor)", &ipc_create);
+  m.def("ipc_open(int id, Tensor handles, int me, int W, Tensor? local_ptrs) -> ()", &ipc_open);
+  m.def("ipc_region(int id) -> int", &ipc_region);
+  m.def("ipc_status(int id) -> int", &ipc_status);
+  m.def("ipc_destroy(int id) -> ()", &ipc_destroy);
+  m.def("ipc_allreduce_(int id, Tensor(a!) x, int epoch, int mode, int blocks) -> ()");
+  m.def("ipc_allreduce_local_(int[] ids, Tensor(a!)[] xs, int epoch, int mode, int blocks) -> ()");
   m.def("head_score(Tensor table, Tensor? ids, int T, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bool store_e) -> (Tensor, Tensor)");
   m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens) -> (Tensor, Tensor)");
   m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g) -> (Tensor, Tensor)");
@@ -1317,6 +1396,8 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("title_attention_bwd", &title_attention_bwd);
   m.impl("embed_ln", &embed_ln);
   m.impl("title_attention", &title_attention);
+  m.impl("ipc_allreduce_", &ipc_allreduce_);
+  m.impl("ipc_allreduce_local_", &ipc_allreduce_local_);
   m.impl("head_score", &head_score);
   m.impl("head_pool", &head_pool);
   m.impl("head_pool_bwd", &head_pool_bwd);

@@ -34,6 +34,7 @@ class DistContext:
     roles: List[str] = field(default_factory=lambda: ["client"])
     ctrl_group: Optional[object] = None  # gloo, everybody
     data_group: Optional[object] = None  # RCCL (or gloo on CPU), clients only
+    client_ctrl_group: Optional[object] = None  # gloo, clients only (IPC handle exchange)
     client_ranks: List[int] = field(default_factory=lambda: [0])
     initialized: bool = False
 
@@ -98,6 +99,7 @@ def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0, g
     data_backend = os.environ.get("FEDREC_DATA_BACKEND") or ("nccl" if gpu_job else "gloo")
     # every rank must call new_group, members or not
     ctx.data_group = dist.new_group(ranks=ctx.client_ranks, backend=data_backend, timeout=timeout)
+    ctx.client_ctrl_group = dist.new_group(ranks=ctx.client_ranks, backend="gloo", timeout=timeout)
     return ctx
 
 
@@ -147,11 +149,32 @@ def shutdown(ctx: DistContext) -> None:
             pass
 
 
+def make_ipc_allreduce(ctx: DistContext):
+    """The custom peer-to-peer all-reduce over IPC-mapped buffers among the client GPUs
+    (:mod:`.ipc_allreduce`), or None (one client, no GPU)."""
+    if ctx.num_clients <= 1 or not ctx.initialized or ctx.device.type != "cuda" or ctx.client_index < 0:
+        return None
+    from .ipc_allreduce import IpcAllReduce
+
+    return IpcAllReduce(ctx.client_ctrl_group, ctx.client_index, ctx.num_clients, ctx.device)
+
+
 def make_grad_allreduce(ctx: DistContext):
-    """Sum the flat gradient over the client data group; returns the 1/W scale Adam applies."""
+    """Sum the flat gradient over the client data group; returns the 1/W scale Adam applies.
+    ``FEDREC_ALLREDUCE=ipc``: the custom IPC all-reduce instead of RCCL (same sum; every rank
+    gets the bitwise-same result)."""
     if ctx.num_clients <= 1 or not ctx.initialized:
         return None
     W = ctx.num_clients
+    if os.environ.get("FEDREC_ALLREDUCE", "rccl") == "ipc" and ctx.device.type == "cuda":
+        ipc = make_ipc_allreduce(ctx)
+
+        def _ar_ipc(flat_grad: torch.Tensor) -> float:
+            CHECK.record("all_reduce", flat_grad, "grad-ipc")
+            ipc.allreduce_(flat_grad)
+            return 1.0 / W
+
+        return _ar_ipc
 
     def _ar(flat_grad: torch.Tensor) -> float:
         CHECK.record("all_reduce", flat_grad, "grad")

@@ -1,0 +1,128 @@
+"""Custom peer-to-peer all-reduce over IPC-mapped device buffers (``csrc/ipc_allreduce.hip``).
+
+SURVEY §5.8.2 / §7.3 P6: the data plane's gradient and parameter buckets (4.66 MB trainable set;
+~28 MB buckets of the unfrozen config) are small enough that a ring all-reduce is latency-bound
+on a node whose GPUs are fully connected by xGMI.  Here every client exports one uncached
+device region (hipIpcGetMemHandle), the handles travel over the gloo control group, and each
+call runs ONE kernel per rank:
+
+* ``one-shot`` (buckets up to ``one_shot_max``): publish the input, one cross-rank barrier
+  (release / acquire flags in the peers' regions), every rank reads all W inputs over xGMI and
+  sums them in rank order -- every rank gets the bitwise-same result.
+* ``two-shot`` (larger buckets): reduce-scatter of 1/W slices, barrier, all-gather of the
+  reduced slices: 2 (W-1)/W of the bucket read per rank instead of (W-1).
+
+fp32 SUM and int32 wrap-around SUM (the pairwise-masked fixed point of secure aggregation).
+RCCL stays the default data plane; ``FEDREC_ALLREDUCE=ipc`` selects this one, and the bench
+reports both at N > 1.  The barrier waits are bounded: a missing peer makes the kernel record a
+timeout in its status word and exit instead of hanging the GPU.
+
+Reference call sites this replaces: ``Gradient_Averaging_main.py:119`` (DDP reducer),
+``Parameter_Averaging_main.py:144-148`` (per-tensor parameter all-reduce).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import native
+
+DEFAULT_CAP = 32 << 20  # bytes per slot (two slots + flags per rank)
+
+
+class IpcAllReduce:
+    """One rank's end of the IPC all-reduce among the ``world`` clients of ``ctrl_group``."""
+
+    def __init__(self, ctrl_group, rank: int, world: int, device: torch.device, cap: int = DEFAULT_CAP,
+                 one_shot_max: int = int(os.environ.get("FEDREC_IPC_ONE_SHOT_MAX", 8 << 20)),
+                 blocks: int = int(os.environ.get("FEDREC_IPC_BLOCKS", 32))):
+        self.lib = native.lib()
+        self.rank, self.world, self.device = int(rank), int(world), device
+        self.cap, self.one_shot_max, self.blocks = int(cap), int(one_shot_max), int(blocks)
+        with torch.cuda.device(device):
+            self.id, h = self.lib.ipc_create(self.cap)
+        handles: List[Optional[bytes]] = [None] * self.world
+        dist.all_gather_object(handles, bytes(h.numpy().tobytes()), group=ctrl_group)
+        flat = torch.frombuffer(bytearray(b"".join(handles)), dtype=torch.uint8)
+        with torch.cuda.device(device):
+            self.lib.ipc_open(self.id, flat, self.rank, self.world, None)
+        dist.barrier(group=ctrl_group)  # every rank opened every region before the first call
+        self.epoch = 0
+
+    def allreduce_(self, t: torch.Tensor, mode: Optional[str] = None) -> torch.Tensor:
+        """In-place SUM of ``t`` (fp32 or int32, on this rank's device) over the ranks."""
+        return _allreduce(self, t, mode)
+
+    def status(self) -> int:
+        """0 = every call completed; 1 = a barrier timed out (a peer never arrived).  Reads the
+        device (tests and diagnostics only)."""
+        return int(self.lib.ipc_status(self.id))
+
+    def close(self) -> None:
+        if self.id is not None:
+            torch.cuda.synchronize(self.device)
+            self.lib.ipc_destroy(self.id)
+            self.id = None
+
+
+def _allreduce(g, t: torch.Tensor, mode: Optional[str]) -> torch.Tensor:
+    if t.dtype not in (torch.float32, torch.int32):
+        raise TypeError(f"IPC all-reduce: fp32 / int32 only, got {t.dtype}")
+    nbytes = t.numel() * 4
+    if nbytes > g.cap:
+        # larger than one slot: consecutive chunks (each call a full barrier-protected epoch)
+        flat = t.view(-1)
+        step = (g.cap // 16) * 4
+        for s in range(0, flat.numel(), step):
+            _allreduce(g, flat[s:s + step], mode)
+        return t
+    work = t if (t.is_contiguous() and t.numel() % 4 == 0) else None
+    if work is None:  # pad to whole 16-byte chunks (the kernel moves float4 / int4)
+        work = torch.zeros(-(-t.numel() // 4) * 4, dtype=t.dtype, device=t.device)
+        work[:t.numel()].copy_(t.reshape(-1))
+    m = mode or ("one" if nbytes <= g.one_shot_max else "two")
+    g.epoch += 1
+    g.lib.ipc_allreduce_(g.id, work.view(-1), g.epoch, 0 if m == "one" else 1, g.blocks)
+    if work is not t:
+        t.view(-1).copy_(work[:t.numel()])
+    return t
+
+
+class LocalIpcGroup:
+    """Single-process rehearsal of the protocol: ``world`` ranks' regions on ONE device and ONE
+    launch whose blocks play every rank (rank = block / blocks-per-rank), synchronising through
+    the same per-rank flags, slots and barriers as the per-process kernels -- co-resident by
+    construction (one kernel per rank on separate streams depends on the streams landing on
+    distinct hardware queues).  Used by the 1-GPU tests; the multi-process form is
+    :class:`IpcAllReduce`."""
+
+    def __init__(self, world: int, device: torch.device, cap: int = 4 << 20, blocks: int = 8):
+        lib = native.lib()
+        self.lib, self.world, self.device, self.cap, self.blocks = lib, int(world), device, int(cap), int(blocks)
+        self.one_shot_max = 1 << 62
+        with torch.cuda.device(device):
+            made = [lib.ipc_create(self.cap) for _ in range(self.world)]
+        self.ids = [m[0] for m in made]
+        regions = torch.tensor([lib.ipc_region(i) for i in self.ids], dtype=torch.int64)
+        handles = torch.cat([m[1] for m in made])
+        for r, i in enumerate(self.ids):
+            lib.ipc_open(i, handles, r, self.world, regions)
+        self.epoch = 0
+
+    def allreduce_(self, ts: List[torch.Tensor], mode: str = "one") -> None:
+        """``ts[r]`` = rank r's tensor; every one is replaced by the sum."""
+        self.epoch += 1
+        self.lib.ipc_allreduce_local_(self.ids, [t.view(-1) for t in ts], self.epoch, 0 if mode == "one" else 1,
+                                      self.blocks)
+
+    def status(self) -> List[int]:
+        return [int(self.lib.ipc_status(i)) for i in self.ids]
+
+    def close(self) -> None:
+        torch.cuda.synchronize(self.device)
+        for i in self.ids:
+            self.lib.ipc_destroy(i)
+        self.ids = []

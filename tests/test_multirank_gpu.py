@@ -42,6 +42,29 @@ def test_bench_two_clients_on_gpu(dev):
     r = json.loads(lines[0][0])
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["value"] > 0
     assert r["dtype"] == "bf16" and r["train_loss"] == r["train_loss"]  # not NaN
+    # the data-plane self-check ran, and the custom IPC all-reduce matched the group's sum
+    assert r["data_plane_selfcheck"]["ok"] and r["data_plane_selfcheck"]["size"] == 2
+    ipc = r["ipc_allreduce"]
+    assert ipc.get("matches_rccl") is True and ipc.get("status") == 0, ipc
+
+
+@pytest.mark.gpu
+def test_grad_avg_two_clients_ipc_allreduce(tmp_path, dev):
+    """GA with the gradient bucket summed by the custom IPC all-reduce (FEDREC_ALLREDUCE=ipc,
+    real IPC handles between the two processes): both clients bit-identical, and the same
+    parameters as the gloo data plane up to summation order."""
+    base = ["Gradient_Averaging_main.py", "1", "32", "0", "--data_dir=synthetic:tiny", "--round_timeout_s=300",
+            "--collective_timeout_s=300", "--user_dropout=0"]
+    outs = run_ranks([base, base], dict(SHARE, FEDREC_DUMP_FLAT=str(tmp_path / "gloo")), timeout=400)
+    _ok(outs)
+    outs = run_ranks([base, base], dict(SHARE, FEDREC_DUMP_FLAT=str(tmp_path / "ipc"), FEDREC_ALLREDUCE="ipc"),
+                     timeout=400)
+    _ok(outs)
+    a = torch.load(tmp_path / "ipc" / "rank0.pt")
+    assert torch.equal(a, torch.load(tmp_path / "ipc" / "rank1.pt"))
+    ref = torch.load(tmp_path / "gloo" / "rank0.pt")
+    d = (a - ref).abs()
+    assert float(torch.quantile(d, 0.999)) < 1e-5 and float(d.max()) < 5e-5 * 40
 
 
 @pytest.mark.gpu
