@@ -102,7 +102,7 @@ int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int 
                        const int* signs, int npeers, unsigned long long round, hipStream_t s);
 int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
-                   const unsigned long long* dev_off, int n, float* scratch, hipStream_t s);
+                   const unsigned long long* dev_off, int n, float* scratch, int tile, hipStream_t s);
 int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg, hipStream_t s);
 int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, const int* C, const int* ld, int nseg,
                     hipStream_t s);
@@ -116,8 +116,9 @@ int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, in
 int fr_title_attention_bwd_drop_bf16(const void* qkv, const void* dout, const int* mask, void* dqkv, int n_titles,
                                      int T, int H, int D, float pdrop, unsigned long long seed,
                                      unsigned long long offset, hipStream_t s);
-int fr_gather_dropout_f32(const float* v, const int* idx, float* out, int M, int K, float p, unsigned long long seed,
-                          unsigned long long offset, const unsigned long long* dev_off, hipStream_t s);
+int fr_gather_dropout(const float* v, const int* idx, void* out, int out_bf16, int M, int K, float p,
+                      unsigned long long seed, unsigned long long offset, const unsigned long long* dev_off,
+                      hipStream_t s);
 long fr_wgrad_bf16(const void* dY, const void* X, float* C, float* scratch, int M, int N, int K, int accumulate,
                    hipStream_t s);
 }
@@ -804,8 +805,10 @@ at::Tensor secagg_unmask(const at::Tensor& x, double inv_scale) {
   return out;
 }
 
-// ---- small fp32 GEMMs on MFMA (small_gemm.hip): up to 6 independent GEMMs per launch -------
+// ---- small GEMMs on MFMA (small_gemm.hip): up to 6 independent GEMMs per launch ------------
 // ints: 14 per GEMM (M, N, K, lda, ldb, ldc, a_mode, b_mode, act, accumulate, drop_ld, drop_on, gather_on, kseg);
+// A / B fp32 or bf16 (the kernel takes the dtype flags from the tensors), C fp32;
+// tile: 0 = the launcher's choice, 1..4 = 64x64 / 128x64 / 64x128 / 128x128 (benchmarks);
 // Bseg: per GEMM 0 or 2 extra [kseg, N] row blocks of a K-segmented B (kseg > 0)
 // floats: (alpha, pdrop) per GEMM; seeds: (seed, offset) per GEMM.  C tensors are written.
 // elements addressable from t.data_ptr() to the end of its storage (strided operand views)
@@ -816,14 +819,15 @@ int64_t avail(const at::Tensor& t) {
 void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<at::Tensor>>& gidx,
                 const std::vector<at::Tensor>& B, const c10::List<c10::optional<at::Tensor>>& bias,
                 const std::vector<at::Tensor>& C, at::IntArrayRef ints, at::ArrayRef<double> floats,
-                at::IntArrayRef seeds, const c10::optional<at::Tensor>& dev_off, const std::vector<at::Tensor>& Bseg) {
+                at::IntArrayRef seeds, const c10::optional<at::Tensor>& dev_off, const std::vector<at::Tensor>& Bseg,
+                int64_t tile) {
   const size_t n = A.size();
   TORCH_CHECK(n >= 1 && n <= 6 && B.size() == n && C.size() == n && gidx.size() == n && bias.size() == n &&
                   ints.size() == 14 * n && floats.size() == 2 * n && seeds.size() == 2 * n,
               "fedrec::small_gemm: descriptor sizes");
   const c10::DeviceGuard g(A[0].device());
   std::vector<const void*> ptrs(7 * n);
-  std::vector<int> iv(14 * n);
+  std::vector<int> iv(16 * n);
   size_t seg_used = 0;
   std::vector<float> fv(2 * n);
   std::vector<unsigned long long> sv(2 * n);
@@ -831,8 +835,9 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
     const int64_t* q = ints.data() + 14 * i;
     const int64_t M = q[0], N = q[1], K = q[2], lda = q[3], ldb = q[4], ldc = q[5], am = q[6], bm = q[7];
     for (const at::Tensor* t : {&A[i], &B[i], &C[i]}) {  // row-major views with any leading dimension
-      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && (t->dim() == 0 || t->stride(-1) == 1),
-                  "fedrec::small_gemm: fp32 device operands with unit inner stride");
+      TORCH_CHECK(t->is_cuda() && (t->scalar_type() == at::kFloat || (t != &C[i] && t->scalar_type() == at::kBFloat16)) &&
+                      (t->dim() == 0 || t->stride(-1) == 1),
+                  "fedrec::small_gemm: fp32 / bf16 device operands (fp32 C) with unit inner stride");
     }
     // bounds of the strided accesses the kernel makes (a kernel never sees a shape it was not written for)
     const auto gv = gidx.get(i);
@@ -856,7 +861,7 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
       TORCH_CHECK(bm == 1 && seg_used + 2 <= Bseg.size(), "fedrec::small_gemm: K-segmented B needs b_mode 1 + 2 Bseg");
       for (int j = 0; j < 2; ++j) {
         const at::Tensor& t = Bseg[seg_used + j];
-        TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.stride(-1) == 1 &&
+        TORCH_CHECK(t.is_cuda() && t.scalar_type() == B[i].scalar_type() && t.stride(-1) == 1 &&
                         avail(t) >= (kseg - 1) * ldb + N,
                     "fedrec::small_gemm: Bseg block");
         ptrs[7 * i + 5 + j] = t.data_ptr();
@@ -876,7 +881,9 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
       ptrs[7 * i + 3] = bv->data_ptr();
     }
     ptrs[7 * i + 4] = C[i].data_ptr();
-    for (int j = 0; j < 14; ++j) iv[14 * i + j] = (int)q[j];
+    for (int j = 0; j < 14; ++j) iv[16 * i + j] = (int)q[j];
+    iv[16 * i + 14] = A[i].scalar_type() == at::kBFloat16;
+    iv[16 * i + 15] = B[i].scalar_type() == at::kBFloat16;
     fv[2 * i] = (float)floats[2 * i];
     fv[2 * i + 1] = (float)floats[2 * i + 1];
     sv[2 * i] = (unsigned long long)seeds[2 * i];
@@ -889,13 +896,13 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
     dop = (const unsigned long long*)dev_off->data_ptr<int64_t>();
   }
   // first call: validate + ask for split-K partial space; second call: launch
-  long need = fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), dop, (int)n, nullptr, cur_stream());
+  long need = fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), dop, (int)n, nullptr, (int)tile, cur_stream());
   TORCH_CHECK(need >= 0, "fedrec::small_gemm: descriptor rejected (code ", need, ")");
   at::Tensor scratch;
   if (need > 0) {
-    scratch = at::empty({need}, A[0].options());
+    scratch = at::empty({need}, A[0].options().dtype(at::kFloat));
     const long rc = fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), dop, (int)n,
-                                  scratch.data_ptr<float>(), cur_stream());
+                                  scratch.data_ptr<float>(), (int)tile, cur_stream());
     TORCH_CHECK(rc == 0, "fedrec::small_gemm: launch failed (code ", rc, ")");
   }
 }
@@ -1262,9 +1269,9 @@ at::Tensor embed_grad(const at::Tensor& dx, const at::Tensor& sorted, const at::
   return dword;
 }
 
-// out[m] = v[idx[m]] * Philox dropout mask (small_gemm.hip), fp32
+// out[m] = v[idx[m]] * Philox dropout mask (small_gemm.hip), fp32 or bf16 (bf16_out)
 at::Tensor gather_dropout(const at::Tensor& v, const at::Tensor& idx, double p, int64_t seed, int64_t offset,
-                          const c10::optional<at::Tensor>& dev_off) {
+                          const c10::optional<at::Tensor>& dev_off, bool bf16_out) {
   check_dev(v, "v");
   check_dev(idx, "idx");
   TORCH_CHECK(v.scalar_type() == at::kFloat && v.dim() == 2 && idx.scalar_type() == at::kInt && idx.dim() == 1,
@@ -1277,10 +1284,10 @@ at::Tensor gather_dropout(const at::Tensor& v, const at::Tensor& idx, double p, 
     TORCH_CHECK(dev_off->scalar_type() == at::kLong && dev_off->numel() >= 1, "fedrec::gather_dropout: dev_off");
     dp = (const unsigned long long*)dev_off->data_ptr<int64_t>();
   }
-  auto out = at::empty({idx.size(0), v.size(1)}, v.options());
-  check_rc(fr_gather_dropout_f32(v.data_ptr<float>(), idx.data_ptr<int>(), out.data_ptr<float>(), (int)idx.size(0),
-                                 (int)v.size(1), (float)p, (unsigned long long)seed, (unsigned long long)offset, dp,
-                                 cur_stream()),
+  auto out = at::empty({idx.size(0), v.size(1)}, v.options().dtype(bf16_out ? at::kBFloat16 : at::kFloat));
+  check_rc(fr_gather_dropout(v.data_ptr<float>(), idx.data_ptr<int>(), out.data_ptr(), bf16_out ? 1 : 0,
+                             (int)idx.size(0), (int)v.size(1), (float)p, (unsigned long long)seed,
+                             (unsigned long long)offset, dp, cur_stream()),
            "gather_dropout");
   return out;
 }
@@ -1370,7 +1377,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
-  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg) -> ()");
+  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg, int tile=0) -> ()");
   m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
   m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst) -> bool");
   m.def("multi_cast_t(Tensor[] src, Tensor(a!)[] dst) -> bool");
@@ -1381,7 +1388,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x) -> Tensor");
-  m.def("gather_dropout(Tensor v, Tensor idx, float p, int seed, int offset, Tensor? dev_off) -> Tensor");
+  m.def("gather_dropout(Tensor v, Tensor idx, float p, int seed, int offset, Tensor? dev_off, bool bf16_out=False) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {

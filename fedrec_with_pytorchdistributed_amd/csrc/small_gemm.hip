@@ -1,40 +1,48 @@
-// Small fp32-in / fp32-out GEMMs on MFMA for the user encoder and the text head's FC
-// (round-1 these were hipBLASLt fp32 calls plus torch glue).
+// Small GEMMs on MFMA for the user encoder and the text head's FC (SURVEY §2.3 K07, K10, K14;
+// round-1 these were hipBLASLt fp32 calls plus torch glue).
 //
 //   C[m, n] = act(alpha * sum_k A(m, k) * B(n, k) + bias[n])  (+ C[m, n] when accumulating)
 //
 // Shapes are the user side's: M = B*H = 3200 history rows (or U titles), N / K in {200, 400,
-// 768, 1200}, none of them multiples of the big GEMM's 128/64 tiling -- every edge is masked.
-// Operands are converted fp32 -> bf16 on their way into LDS and multiplied with
-// v_mfma_f32_16x16x32_bf16 (fp32 accumulate).  Layouts:
+// 768, 1200}, none of them multiples of a power-of-two tiling -- every edge is masked.
+// Operands are fp32 or bf16 per operand (a_bf16 / b_bf16); fp32 ones are converted to bf16 on
+// their way into LDS, so an operand its producer already wrote in bf16 gives the bitwise same
+// product at half the bytes.  v_mfma_f32_16x16x32_bf16, fp32 accumulate.  Layouts:
 //   A: a_mode 0 = row-major [M, K] (optionally with a row gather m -> gidx[m] and a Philox
-//      dropout on the gathered elements, index m * drop_ld + k: the user encoder's input
-//      dropout fused into the QKV projection, K09), a_mode 1 = stored transposed [K, M]
-//      (weight gradients dW = dY^T X);
+//      dropout on the gathered elements, index m * drop_ld + k), a_mode 1 = stored transposed
+//      [K, M] (weight gradients dW = dY^T X);
 //   B: b_mode 0 = [N, K] (nn.Linear weight: y = x W^T), b_mode 1 = [K, N] (dgrad dx = dy W;
-//      or, with gidx / dropout, the forward's gathered dropped-out input X' for dW = dY^T X').
+//      or, with gidx / dropout, a gathered dropped-out input for dW = dY^T X').
 //   act: 0 none, 1 tanh.  drop_on: 0 none, 1 A elements (m, k), 2 B elements (k, n) of a K-major
-//      B, 3 output elements (m, n) -- the input dropout's backward fused into the dgrad
-//      epilogue.  gather_on: 0 none, 1 A rows (a_mode 0), 2 B rows (b_mode 1).
-// Tile 64 x 64 x 64, 256 threads = 4 waves in 2 x 2, each wave 32 x 32 = 2 x 2 MFMA tiles;
-// 16-byte global loads where aligned.  Several independent GEMMs run in ONE launch (GemmBatch:
-// the Q/K/V projections, the weight gradients of one backward, ...): blockIdx.x walks the
-// concatenated tile lists.  Long reductions with few output tiles (weight gradients over
-// K = B*H = 3200 rows) split K over workgroups into fp32 partials that a second kernel sums in
-// split order -- deterministic, no atomics.
+//      B (both fp32 operands only), 3 output elements (m, n) -- the input dropout's backward
+//      fused into the dgrad epilogue.  gather_on: 0 none, 1 A rows (a_mode 0), 2 B rows (b_mode 1).
+//
+// Tiles: TM x TN x 64 with TM = 32 FM, TN = 32 FN (FM, FN in {2, 4}: 64 / 128), 256 threads =
+// 4 waves in 2 x 2, each wave (TM/2) x (TN/2) = FM x FN MFMA tiles.  The K loop keeps the next
+// k-tile's global loads in flight in registers (raw bits, converted when stored to LDS) while
+// the MFMAs consume the current one.  These GEMMs are L2-bandwidth bound at 64 x 64 (each
+// operand re-read once per tile of the other dimension: the Q|K|V projection moved ~235 MB
+// through L2 for 3 GFLOP), so the host picks the biggest tile that still fills the chip.
+// Several independent GEMMs run in ONE launch (GemmBatch: the weight gradients of one
+// backward, ...): the XCD-remapped blockIdx walks the concatenated tile lists, consecutive
+// tiles (the column tiles of one row panel, the splits of one tile) on one XCD's L2.  Long
+// reductions with few output tiles split K over workgroups into fp32 partials that a second
+// kernel sums in split order -- deterministic, no atomics.
 #include "common.h"
+
+#include <stdlib.h>
 
 namespace {
 
-constexpr int TM = 64, TN = 64, TK = 64, LDT = TK + 8;  // LDS row stride 72 bf16 = 144 B
+constexpr int TK = 64, LDT = TK + 8;  // LDS row stride 72 bf16 = 144 B
 constexpr int MAXG = 6;
 
 struct GemmDesc {
-  const float* A;
+  const void* A;
   const int* gidx;  // row gather of A (gather_on 1, a_mode 0) or of B (gather_on 2, b_mode 1)
-  const float* B;
-  const float* B2;  // K-segmented B (b_mode 1): rows [kseg, 2 kseg) from B2, [2 kseg, 3 kseg) from B3
-  const float* B3;
+  const void* B;
+  const void* B2;  // K-segmented B (b_mode 1): rows [kseg, 2 kseg) from B2, [2 kseg, 3 kseg) from B3
+  const void* B3;
   const float* bias;
   float* C;
   float* P;  // split-K partials [splits, M, N] (splits > 1: the reduce kernel does the epilogue)
@@ -42,6 +50,7 @@ struct GemmDesc {
   int a_mode, b_mode, act, accumulate;
   float alpha, pdrop;
   int drop_ld, drop_on, gather_on, tiles_n, tile_base, splits, kchunk, kseg;
+  int a_bf16, b_bf16;
   unsigned long long seed, offset;  // offset += *dev_off when dev_off is set (graph replays)
 };
 
@@ -51,16 +60,32 @@ struct GemmBatch {
   int n;
 };
 
-__device__ __forceinline__ void load16(const float* __restrict__ p, bool full, bool vec, int valid, float (&v)[16]) {
-  if (full && vec) {
+// 16 consecutive elements -> raw register bits (fp32: 16 words; bf16: 8 words, 2 per word)
+__device__ __forceinline__ void load16_f32(const float* __restrict__ p, int valid, uint32_t (&v)[16]) {
+  if (valid == 16 && ((uintptr_t)p & 15) == 0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float4 f = *(const float4*)(p + 4 * j);
+      const uint4 f = *(const uint4*)(p + 4 * j);
       v[4 * j] = f.x; v[4 * j + 1] = f.y; v[4 * j + 2] = f.z; v[4 * j + 3] = f.w;
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = j < valid ? p[j] : 0.f;
+    for (int j = 0; j < 16; ++j) v[j] = j < valid ? __float_as_uint(p[j]) : 0u;
+  }
+}
+__device__ __forceinline__ void load16_bf16(const unsigned short* __restrict__ p, int valid, uint32_t (&v)[16]) {
+  if (valid == 16 && ((uintptr_t)p & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint4 f = *(const uint4*)(p + 8 * j);
+      v[4 * j] = f.x; v[4 * j + 1] = f.y; v[4 * j + 2] = f.z; v[4 * j + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t lo = 2 * j < valid ? p[2 * j] : 0u, hi = 2 * j + 1 < valid ? p[2 * j + 1] : 0u;
+      v[j] = lo | (hi << 16);
+    }
   }
 }
 
@@ -75,147 +100,313 @@ __device__ __forceinline__ void apply_drop16(float (&v)[16], unsigned long long 
   }
 }
 
-// one 64 x 64 operand tile (rows r0.., k0..): global -> 16 registers per thread (converted
-// and dropout-scaled), then registers -> bf16 LDS [row][k] in a separate step, so the next
-// tile's loads are in flight while the MFMAs consume the current one
-__device__ __forceinline__ void load_regs(const GemmDesc& g, unsigned long long off, bool isA, int r0, int k0,
-                                          int kend, int tid, float (&v)[16]) {
+// chunk c of a TR x 64 operand tile: mode 0 ([R, K] row-major) -> (row c / 4, 16 k from
+// 16 (c % 4)); mode 1 (stored [K, R]) -> (k c / (TR/16), 16 rows from 16 (c % (TR/16)))
+template <int TR>
+__device__ __forceinline__ void load_raw(const GemmDesc& g, bool isA, int r0, int k0, int kend, int tid,
+                                         uint32_t (&raw)[TR / 64][16]) {
   const int mode = isA ? g.a_mode : g.b_mode;
-  const float* P = isA ? g.A : g.B;
+  const bool h = isA ? g.a_bf16 : g.b_bf16;
   const int ld = isA ? g.lda : g.ldb;
   const int R = isA ? g.M : g.N;
-  if (mode == 0) {  // [R, K] row-major: thread -> (row, 16 consecutive k)
-    const int r = tid >> 2, kk = (tid & 3) * 16;
-    const int rr = r0 + r, k = k0 + kk;
-    const bool rok = rr < R;
-    const int src = rok ? ((isA && g.gather_on == 1) ? g.gidx[rr] : rr) : 0;
-    const float* p = P + (size_t)src * ld + k;
-    const int valid = rok ? min(16, kend - k) : 0;
-    load16(p, valid == 16, ((uintptr_t)p & 15) == 0, valid, v);
-    if (isA && g.drop_on == 1 && rok) apply_drop16(v, (unsigned long long)rr * g.drop_ld + k, g, off);
-  } else {  // stored [K, R]: thread -> (k, 16 consecutive rows), coalesced along the rows
-    const int k = tid >> 2, rr16 = (tid & 3) * 16;
-    const int kg = k0 + k;
-    const bool kok = kg < kend;
-    // B in mode 1 may be the gathered + dropped-out input of the forward (the weight
-    // gradient dW = dY^T X' regenerates X' = drop(X[gidx]) instead of storing it)
-    size_t src = kok ? (size_t)((!isA && g.gather_on == 2) ? g.gidx[kg] : kg) : 0;
-    if (!isA && g.kseg > 0 && kok) {  // one [K, N] operand stored as up to three row blocks
-      const int seg = kg / g.kseg;
-      P = seg == 0 ? g.B : (seg == 1 ? g.B2 : g.B3);
-      src = kg - seg * g.kseg;
+#pragma unroll
+  for (int i = 0; i < TR / 64; ++i) {
+    const int c = tid + 256 * i;
+    const void* base = isA ? g.A : g.B;
+    size_t src;
+    int valid;
+    if (mode == 0) {
+      const int r = c >> 2, kk = (c & 3) * 16;
+      const int rr = r0 + r, k = k0 + kk;
+      const bool rok = rr < R;
+      const int row = rok ? ((isA && g.gather_on == 1) ? g.gidx[rr] : rr) : 0;
+      src = (size_t)row * ld + k;
+      valid = rok ? min(16, kend - k) : 0;
+    } else {
+      constexpr int CPR = TR / 16;
+      const int k = c / CPR, rr16 = (c % CPR) * 16;
+      const int kg = k0 + k;
+      const bool kok = kg < kend;
+      size_t row = kok ? (size_t)((!isA && g.gather_on == 2) ? g.gidx[kg] : kg) : 0;
+      if (!isA && g.kseg > 0 && kok) {  // one [K, N] operand stored as up to three row blocks
+        const int seg = kg / g.kseg;
+        base = seg == 0 ? g.B : (seg == 1 ? g.B2 : g.B3);
+        row = kg - seg * g.kseg;
+      }
+      src = row * ld + r0 + rr16;
+      valid = kok ? min(16, R - (r0 + rr16)) : 0;
     }
-    const float* p = P + src * ld + r0 + rr16;
-    const int valid = kok ? min(16, R - (r0 + rr16)) : 0;
-    load16(p, valid == 16, ((uintptr_t)p & 15) == 0, valid, v);
-    if (!isA && g.drop_on == 2 && kok) apply_drop16(v, (unsigned long long)kg * g.drop_ld + r0 + rr16, g, off);
+    if (h)
+      load16_bf16((const unsigned short*)base + src, valid, raw[i]);
+    else
+      load16_f32((const float*)base + src, valid, raw[i]);
   }
 }
 
-__device__ __forceinline__ void store_regs(const GemmDesc& g, bool isA, int tid, const float (&v)[16],
-                                           bf16 (*S)[LDT]) {
-  if ((isA ? g.a_mode : g.b_mode) == 0) {
-    const int r = tid >> 2, kk = (tid & 3) * 16;
+// The same tile with no data-dependent branches around loads (FAST launches: every contiguous extent a
+// multiple of 8 elements, 16-byte aligned rows): each 8-element half of a chunk is one
+// unconditional load from its address or -- when it lies outside the operand -- from the
+// operand's first row, and `vm` records which halves are real; the zeroing select waits until
+// the chunk is stored to LDS, after the MFMAs.  (With per-lane branches around the loads the
+// compiler joins the paths right after them and waits for the data there: every k-tile's
+// loads became synchronous -- the 128-row tiles measured 2-4x SLOWER than 64-row ones.)
+// (1) offsets: every chunk's two half byte offsets into its operand -- any row-gather index
+// load happens here, before the first data load is issued, so its wait drains nothing else;
+// a half outside the operand gets an offset past the descriptor's range, which the buffer
+// unit answers with zeros; (2) the data loads, buffer_load_dwordx4 through a per-operand
+// descriptor built from wave-uniform values.  (Plain pointer loads here compile to FLAT loads
+// -- the operand pointers come out of the kernel-argument struct as generic pointers -- and a
+// flat load also counts in lgkmcnt: the LDS-read wait before the MFMAs then waited for the
+// next tile's prefetch as well, serialising the pipeline.)
+constexpr uint32_t OOB = 0x80000000u;  // past num_records: the load returns zeros
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
+}
+
+template <int TR, bool H>
+__device__ __forceinline__ void chunk_offs(const GemmDesc& g, bool isA, int r0, int k0, int kend, int tid,
+                                           uint32_t (&ol)[TR / 64], uint32_t (&oh)[TR / 64]) {
+  const int mode = isA ? g.a_mode : g.b_mode;
+  constexpr uint32_t ES = H ? 2 : 4;
+  const int ld = isA ? g.lda : g.ldb;
+  const int R = isA ? g.M : g.N;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[8 * h + j]);
-      *(bf16x8*)&S[r][kk + 8 * h] = o;
+  for (int i = 0; i < TR / 64; ++i) {
+    const int c = tid + 256 * i;
+    uint32_t src;
+    int valid;
+    if (mode == 0) {
+      const int r = c >> 2, kk = (c & 3) * 16;
+      const int rr = r0 + r, k = k0 + kk;
+      const bool rok = rr < R;
+      const int row = rok ? ((isA && g.gather_on == 1) ? g.gidx[rr] : rr) : 0;
+      src = (uint32_t)row * ld + k;
+      valid = rok ? kend - k : 0;
+    } else {
+      constexpr int CPR = TR / 16;
+      const int k = c / CPR, rr16 = (c % CPR) * 16;
+      const int kg = k0 + k;
+      const bool kok = kg < kend;
+      const uint32_t row = kok ? (uint32_t)((!isA && g.gather_on == 2) ? g.gidx[kg] : kg) : 0u;
+      src = row * ld + r0 + rr16;
+      valid = kok ? R - (r0 + rr16) : 0;
     }
-  } else {
-    const int k = tid >> 2, rr16 = (tid & 3) * 16;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) S[rr16 + j][k] = f2bf(v[j]);
+    ol[i] = valid >= 8 ? src * ES : OOB;
+    oh[i] = valid >= 16 ? src * ES + 8 * ES : OOB;
   }
 }
 
-__global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) bf16 As[TM][LDT];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[TN][LDT];
-  int gi = 0;
+template <int TR, bool H>
+__device__ __forceinline__ void issue_loads(__amdgpu_buffer_rsrc_t rs, const uint32_t (&ol)[TR / 64],
+                                            const uint32_t (&oh)[TR / 64], uint32_t (&raw)[TR / 64][16]) {
+#pragma unroll
+  for (int i = 0; i < TR / 64; ++i) {
+    if (H) {  // 8 bf16 per half: one 16-byte load each
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, ol[i], 0, 0);
+      const auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, oh[i], 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        raw[i][q] = a[q];
+        raw[i][4 + q] = b[q];
+      }
+    } else {  // 8 floats per half: two
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, ol[i] + 16 * j, 0, 0);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, oh[i] + 16 * j, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          raw[i][4 * j + q] = a[q];
+          raw[i][8 + 4 * j + q] = b[q];
+        }
+      }
+    }
+  }
+}
+
+// raw chunk -> 16 bf16 (fp32 operands: dropout-scaled first when it applies)
+__device__ __forceinline__ void to_bf16x16(const uint32_t (&raw)[16], bool h, bool drop, unsigned long long e,
+                                           const GemmDesc& g, unsigned long long off, bf16x8 (&o)[2]) {
+  if (h) {
+    o[0] = __builtin_bit_cast(bf16x8, uint4{raw[0], raw[1], raw[2], raw[3]});
+    o[1] = __builtin_bit_cast(bf16x8, uint4{raw[4], raw[5], raw[6], raw[7]});
+    return;
+  }
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = __uint_as_float(raw[j]);
+  if (drop) apply_drop16(v, e, g, off);
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[hh][j] = f2bf(v[8 * hh + j]);
+}
+
+template <int TR>
+__device__ __forceinline__ void store_lds(const GemmDesc& g, bool isA, int r0, int k0, int tid,
+                                          const uint32_t (&raw)[TR / 64][16], unsigned long long off,
+                                          bf16 (*S)[LDT], bool h) {
+  const int mode = isA ? g.a_mode : g.b_mode;
+#pragma unroll
+  for (int i = 0; i < TR / 64; ++i) {
+    const int c = tid + 256 * i;
+    bf16x8 o[2];
+    if (mode == 0) {
+      const int r = c >> 2, kk = (c & 3) * 16;
+      to_bf16x16(raw[i], h, isA && g.drop_on == 1, (unsigned long long)(r0 + r) * g.drop_ld + k0 + kk, g, off, o);
+      *(bf16x8*)&S[r][kk] = o[0];
+      *(bf16x8*)&S[r][kk + 8] = o[1];
+    } else {
+      constexpr int CPR = TR / 16;
+      const int k = c / CPR, rr16 = (c % CPR) * 16;
+      to_bf16x16(raw[i], h, !isA && g.drop_on == 2, (unsigned long long)(k0 + k) * g.drop_ld + r0 + rr16, g, off, o);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) S[rr16 + j][k] = o[j >> 3][j & 7];
+    }
+  }
+}
+
+// dropout-backward scale of output element (m, n) (drop_on 3): element m * drop_ld + n of the
+// dropped input
+__device__ __forceinline__ float drop3(const GemmDesc& g, unsigned long long off, int m, int n) {
+  const unsigned long long e = (unsigned long long)m * g.drop_ld + n;
+  const uint4 x = Philox::gen(g.seed, off, e >> 2);
+  return drop_scale(u4_get(x, (int)(e & 3)), g.pdrop, 1.0f / (1.0f - g.pdrop));
+}
+
+// FAST: branch-free operand loads with the operand dtypes fixed per launch (AH / BH: A / B
+// bf16); generic: any alignment, per-desc dtypes, the dropout prologues
+// tile index tg of the launch -> (desc, split, m0, n0); XCD-aware order: blocks bid = x, x + 8,
+// ... (one XCD) take consecutive tiles (the column tiles of one row panel share its A rows)
+__device__ __forceinline__ int tile_of_block(const GemmBatch& batch, int& gi) {
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rmd = nwg & 7;
+  const int tg = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (bid >> 3);
+  gi = 0;
 #pragma unroll
   for (int i = 1; i < MAXG; ++i)
-    if (i < batch.n && (int)blockIdx.x >= batch.d[i].tile_base) gi = i;
-  const GemmDesc& g = batch.d[gi];
-  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
-  int t = blockIdx.x - g.tile_base;
+    if (i < batch.n && tg >= batch.d[i].tile_base) gi = i;
+  return tg - batch.d[gi].tile_base;
+}
+
+template <int FM, int FN, bool FAST, bool AH, bool BH>
+__device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long off, int t,
+                                          bf16 (*As)[LDT], bf16 (*Bs)[LDT]) {
+  constexpr int TM = 32 * FM, TN = 32 * FN;
   const int split = t % g.splits;
   t /= g.splits;
   const int m0 = (t / g.tiles_n) * TM, n0 = (t % g.tiles_n) * TN;
   const int kbeg = split * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int wm = (wave >> 1) * (TM / 2), wn = (wave & 1) * (TN / 2);
   const int fr = lane & 15, fq = lane >> 4;
-  f32x4 acc[2][2];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // one K-tile in flight in registers (two in flight measured slower: 132 VGPRs cost the
-  // bigger grids an occupancy step -- QKV 33 -> 38 us, weight gradients 33 -> 39 us)
-  float va[16], vb[16];
-  if (kbeg < kend) {
-    load_regs(g, off, true, m0, kbeg, kend, tid, va);
-    load_regs(g, off, false, n0, kbeg, kend, tid, vb);
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t ra[TM / 64][16], rb[TN / 64][16];
+  __amdgpu_buffer_rsrc_t rsa, rsb;
+  if (FAST) {
+    rsa = rsrc_of(g.A);
+    rsb = rsrc_of(g.B);
   }
+  auto load = [&](int k) {
+    if (FAST) {
+      uint32_t oal[TM / 64], oah[TM / 64], obl[TN / 64], obh[TN / 64];
+      chunk_offs<TM, AH>(g, true, m0, k, kend, tid, oal, oah);
+      chunk_offs<TN, BH>(g, false, n0, k, kend, tid, obl, obh);
+      issue_loads<TM, AH>(rsa, oal, oah, ra);
+      issue_loads<TN, BH>(rsb, obl, obh, rb);
+    } else {
+      load_raw<TM>(g, true, m0, k, kend, tid, ra);
+      load_raw<TN>(g, false, n0, k, kend, tid, rb);
+    }
+  };
+  if (kbeg < kend) load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += TK) {
     __syncthreads();  // the previous tile's fragments are consumed
-    store_regs(g, true, tid, va, As);
-    store_regs(g, false, tid, vb, Bs);
+    store_lds<TM>(g, true, m0, k0, tid, ra, off, As, FAST ? AH : (bool)g.a_bf16);
+    store_lds<TN>(g, false, n0, k0, tid, rb, off, Bs, FAST ? BH : (bool)g.b_bf16);
     __syncthreads();
-    if (k0 + TK < kend) {  // next tile's global loads overlap this tile's MFMAs
-      load_regs(g, off, true, m0, k0 + TK, kend, tid, va);
-      load_regs(g, off, false, n0, k0 + TK, kend, tid, vb);
-    }
+    if (k0 + TK < kend) load(k0 + TK);  // next tile's global loads overlap this tile's MFMAs
 #pragma unroll
     for (int ks = 0; ks < TK; ks += 32) {
-      bf16x8 a[2], b[2];
+      bf16x8 a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = *(const bf16x8*)&As[wm + i * 16 + fr][ks + fq * 8];
+      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)&As[wm + i * 16 + fr][ks + fq * 8];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = *(const bf16x8*)&Bs[wn + j * 16 + fr][ks + fq * 8];
+      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)&Bs[wn + j * 16 + fr][ks + fq * 8];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
-  // lane holds C[m = wm + 16 i + 4 fq + r][n = wn + 16 j + fr]
+  // lane holds C[m = wm + 16 i + 4 fq + r][n = wn + 16 j + fr]; every loop fully unrolled
+  // (static accumulator indices: the earlier form, with the split-K store inside the loop
+  // nest, stayed rolled at 128-row tiles and kept the accumulators in scratch)
+  const bool part = g.splits > 1;
+  float* const dst = part ? g.P + (size_t)split * g.M * g.N : g.C;
+  const int ldd = part ? g.N : g.ldc;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn + j * 16 + fr;
-    if (n >= g.N) continue;
-    if (g.splits > 1) {  // raw partial; alpha / accumulate in splitk_reduce_kernel
-      float* pp = g.P + (size_t)split * g.M * g.N;
+    const bool nok = n < g.N;
+    const float bn = (!part && nok && g.bias) ? g.bias[n] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm + i * 16 + fq * 4 + r;
-          if (m < g.M) pp[(size_t)m * g.N + n] = acc[i][j][r];
-        }
-      continue;
-    }
-    const float bn = g.bias ? g.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm + i * 16 + fq * 4 + r;
-        if (m >= g.M) continue;
-        float v = g.alpha * acc[i][j][r] + bn;
-        if (g.act == 1) v = tanhf(v);
-        if (g.drop_on == 3) {  // dropout backward in the epilogue: element (m, n) of the dropped input
-          const unsigned long long e = (unsigned long long)m * g.drop_ld + n;
-          const uint4 x = Philox::gen(g.seed, off, e >> 2);
-          v *= drop_scale(u4_get(x, (int)(e & 3)), g.pdrop, 1.0f / (1.0f - g.pdrop));
+        if (!nok || m >= g.M) continue;
+        float v = acc[i][j][r];
+        float* c = dst + (size_t)m * ldd + n;
+        if (!part) {  // raw partial otherwise: alpha / bias / act / accumulate in splitk_reduce_kernel
+          v = g.alpha * v + bn;
+          if (g.act == 1) v = tanhf(v);
+          if (g.drop_on == 3) v *= drop3(g, off, m, n);
+          if (g.accumulate) v += *c;
         }
-        float* c = g.C + (size_t)m * g.ldc + n;
-        if (g.accumulate) v += *c;
         *c = v;
       }
+  }
+}
+
+template <int FM, int FN, bool FAST, bool AH, bool BH>
+__global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) bf16 As[32 * FM][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[32 * FN][LDT];
+  int gi;
+  const int t = tile_of_block(batch, gi);
+  const GemmDesc& g = batch.d[gi];
+  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+  gemm_tile<FM, FN, FAST, AH, BH>(g, off, t, As, Bs);
+}
+
+// FAST loads with the operand dtypes per desc: a block-uniform switch into the four typed
+// bodies (one launch for, e.g., a backward's weight gradients over bf16 and fp32 inputs)
+__global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
+  int gi;
+  const int t = tile_of_block(batch, gi);
+  const GemmDesc& g = batch.d[gi];
+  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+  if (g.a_bf16) {
+    if (g.b_bf16)
+      gemm_tile<2, 2, true, true, true>(g, off, t, As, Bs);
+    else
+      gemm_tile<2, 2, true, true, false>(g, off, t, As, Bs);
+  } else {
+    if (g.b_bf16)
+      gemm_tile<2, 2, true, false, true>(g, off, t, As, Bs);
+    else
+      gemm_tile<2, 2, true, false, false>(g, off, t, As, Bs);
   }
 }
 
@@ -247,17 +438,20 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batc
   }
 }
 
-// Deterministic fp32 column sums (bias gradients), two passes: (1) blocks of 64 columns x 128
-// rows (4 waves x 32 rows) write per-chunk partials; (2) the partials are summed in chunk order.
-// A desc of one row chunk (M <= 128: the loss sum, the pooled-user partial rows) is final after
-// pass 1, and a launch of only such descs skips pass 2.  (A single-pass "last block sums"
-// form with agent-scope fences measured 131 us/step vs 69: each release fence writes back L2.)
-constexpr int CS_ROWS = 128;
+// Deterministic fp32 column sums (bias gradients), two passes: (1) blocks of CS_ROWS rows x
+// (256 columns as float4 per lane when the matrix allows 16-byte loads, else 64 columns)
+// write per-chunk partials, 4 waves x CS_ROWS/4 rows each, 8 row loads in flight per lane;
+// (2) the partials are summed in chunk order.  A desc of one row chunk (the loss sum, the
+// pooled-user partial rows) is final after pass 1, and a launch of only such descs skips
+// pass 2.  (A single-pass "last block sums" form with agent-scope fences measured 131 us/step
+// vs 69: each release fence writes back L2.  The scalar form -- one float per lane, 128 rows
+// per block -- took 32 us for the user step's 18 MB of gradients.)
+constexpr int CS_ROWS = 64;
 struct ColsumDesc {
   const float* X;
   float* out;
   float* part;  // [chunks, N]
-  int M, N, ld, col_blocks, chunks, block_base, block2_base, accumulate;
+  int M, N, ld, col_blocks, chunks, block_base, block2_base, accumulate, vec;
 };
 struct ColsumBatch {
   ColsumDesc d[MAXG];
@@ -265,7 +459,7 @@ struct ColsumBatch {
 };
 
 __global__ __launch_bounds__(256) void colsum_part_kernel(const ColsumBatch batch) {
-  __shared__ float part[4][64];
+  __shared__ float4 part[4][64];
   int gi = 0;
 #pragma unroll
   for (int i = 1; i < MAXG; ++i)
@@ -273,19 +467,44 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const ColsumBatch batc
   const ColsumDesc& g = batch.d[gi];
   const int b = blockIdx.x - g.block_base;
   const int cb = b % g.col_blocks, ch = b / g.col_blocks;
-  const int c = cb * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r0 = ch * CS_ROWS, r1 = min(g.M, r0 + CS_ROWS);
-  float s = 0.f;
-  if (c < g.N)
-    for (int m = r0 + w; m < r1; m += 4) s += g.X[(size_t)m * g.ld + c];
-  part[w][threadIdx.x & 63] = s;
+  constexpr int RW = CS_ROWS / 4;  // rows per wave (contiguous)
+  const int ra = r0 + w * RW, rb = min(r1, ra + RW);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g.vec) {
+    const int c = cb * 256 + 4 * l;
+    if (c < g.N) {
+      const float* x = g.X + c;
+#pragma unroll 8
+      for (int m = ra; m < rb; ++m) {
+        const float4 v = *(const float4*)(x + (size_t)m * g.ld);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+    }
+  } else {
+    const int c = cb * 64 + l;
+    if (c < g.N) {
+#pragma unroll 8
+      for (int m = ra; m < rb; ++m) s.x += g.X[(size_t)m * g.ld + c];
+    }
+  }
+  part[w][l] = s;
   __syncthreads();
-  if (w == 0 && c < g.N) {
-    const float tot = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+  if (w != 0) return;
+  const float4 a = part[0][l], bq = part[1][l], cq = part[2][l], d = part[3][l];
+  const float tot[4] = {(a.x + bq.x) + (cq.x + d.x), (a.y + bq.y) + (cq.y + d.y), (a.z + bq.z) + (cq.z + d.z),
+                        (a.w + bq.w) + (cq.w + d.w)};
+  const int nc = g.vec ? 4 : 1;
+  const int c0 = g.vec ? cb * 256 + 4 * l : cb * 64 + l;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + q;
+    if (q >= nc || c >= g.N) break;
     if (g.chunks == 1)  // one row chunk: the final value (no second pass for this desc)
-      g.out[c] = g.accumulate ? g.out[c] + tot : tot;
+      g.out[c] = g.accumulate ? g.out[c] + tot[q] : tot[q];
     else
-      g.part[(size_t)ch * g.N + c] = tot;
+      g.part[(size_t)ch * g.N + c] = tot[q];
   }
 }
 
@@ -304,55 +523,87 @@ __global__ __launch_bounds__(64) void colsum_final_kernel(const ColsumBatch batc
 
 }  // namespace
 
-// descs: 7 pointers + 14 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
+// descs: 7 pointers + 16 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
 // scratch: split-K partial space (floats) the caller allocated; returns the floats it needs
 // when scratch is null (query mode).
-static int choose_splits(int M, int N, int K) {
-  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+static int choose_splits(int tiles, int K) {
+  // a workgroup's k-steps are a chain of dependent global-load latencies (one k-tile in
+  // flight): a long reduction over few output tiles is latency bound, not bandwidth bound.
+  // Split K until the launch has ~2 workgroups per CU, keeping >= 6 k-tiles per split
+  // (measured: the 1200 x 400 x 3200 weight gradient in 133 tiles -- 2 splits 69 us, four
+  // 400-row descs in 6 splits 49 us; the 3200 x 400 x 1200 dgrad in 350 tiles -- 2 splits
+  // 38.6 us, 3 splits 44.5: the partials' write + reduce outweigh the shorter chains).
   if (K < 512) return 1;
-  if (tiles >= 192) {
-    // more than ~3/4 of a wave of tiles: split only when it fixes the wave quantisation by a
-    // margin that pays for the reduce pass (the user dgrad: 350 tiles x K = 1200 = 1.37 waves
-    // of 19-step tiles -> 2 splits = 700 half-length tiles, 3 rounds of 1/2 instead of 2 of 1)
-    const int rounds1 = (tiles + 255) / 256;
-    int best = 1;
-    float bestc = (float)rounds1;
-    for (int sp = 2; sp <= 4 && sp <= K / 256; ++sp) {
-      const float c = (float)((tiles * sp + 255) / 256) / sp;
-      if (c * 1.15f < bestc) {
-        best = sp;
-        bestc = c * 1.15f;
-      }
-    }
-    return best;
-  }
-  int s = (256 + tiles - 1) / tiles;  // about one wave of workgroups over the 256 CUs
-  s = min(s, K / 256);
+  const int want = (512 + tiles - 1) / tiles;
+  int s = min(want, K / 384);
   return max(1, min(s, 16));
+}
+
+// tile variants: 1 = 64 x 64, 2 = 128 x 64, 3 = 64 x 128, 4 = 128 x 128 (TM x TN)
+static void tile_dims(int v, int& tm, int& tn) {
+  tm = (v == 2 || v == 4) ? 128 : 64;
+  tn = (v == 3 || v == 4) ? 128 : 64;
+}
+
+// auto: 64 x 64 unless the launch has >= 8 tiles of it per CU.  Per k-tile the bigger tiles
+// cost the same (bandwidth-bound: fewer bytes, fewer waves), but a launch of ~1 tile per CU
+// exposes each workgroup's serial prologue -> k-steps -> epilogue chain: at K = 64 the
+// 128 x 128 form took 18.7 us vs 9.4 (3200 x 1200), and only caught up at >= 4 tiles per CU
+// and K >= 512 (benchmarks/sg_latency_probe.py, profiles/r3_small_gemm_bench.json).
+static int choose_tile(const GemmBatch& b) {
+  static const int forced = [] {
+    const char* e = getenv("FEDREC_SG_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced >= 1 && forced <= 4) return forced;
+  long tiles = 0;
+  for (int i = 0; i < b.n; ++i) tiles += (long)((b.d[i].M + 63) / 64) * ((b.d[i].N + 63) / 64);
+  return tiles >= 2048 ? 4 : 1;
+}
+
+// can the launch take the FAST kernels (branch-free buffer loads, dtypes fixed per launch)?
+static bool fast_ok(const GemmBatch& b) {
+  bool fast = true;  // every operand's contiguous extent in whole 16-byte halves of a chunk
+  for (int i = 0; i < b.n; ++i) {
+    const GemmDesc& d = b.d[i];
+    const int ea = d.a_bf16 ? 8 : 4, eb = d.b_bf16 ? 8 : 4;  // elements per 16 bytes
+    const int ca = d.a_mode == 0 ? d.K : d.M, cb = d.b_mode == 0 ? d.K : d.N;  // contiguous extents
+    // byte extents the 32-bit buffer offsets address
+    const double ext_a = (double)(d.a_mode == 0 ? d.M : d.K) * d.lda * (d.a_bf16 ? 2 : 4);
+    const double ext_b = (double)(d.b_mode == 0 ? d.N : d.K) * d.ldb * (d.b_bf16 ? 2 : 4);
+    fast = fast && ca % 8 == 0 && cb % 8 == 0 && d.K % 8 == 0 && d.lda % ea == 0 && d.ldb % eb == 0 &&
+           ((uintptr_t)d.A & 15) == 0 && ((uintptr_t)d.B & 15) == 0 && d.kseg == 0 && d.gather_on == 0 &&
+           d.drop_on != 1 && d.drop_on != 2 && ext_a < 2.0e9 && ext_b < 2.0e9;
+  }
+  static const bool no_fast = getenv("FEDREC_SG_GENERIC") != nullptr;
+  return fast && !no_fast;
+}
+
+static bool mixed_dtypes(const GemmBatch& b) {
+  for (int i = 1; i < b.n; ++i)
+    if (b.d[i].a_bf16 != b.d[0].a_bf16 || b.d[i].b_bf16 != b.d[0].b_bf16) return true;
+  return false;
 }
 
 extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats,
                               const unsigned long long* seeds, const unsigned long long* dev_off, int n, float* scratch,
-                              hipStream_t s) {
+                              int tile, hipStream_t s) {
   if (n < 1 || n > MAXG) return -1;
   GemmBatch b{};
   b.dev_off = dev_off;
-  int tiles = 0;
-  long need = 0;
-  int red_total = 0;
   for (int i = 0; i < n; ++i) {
     GemmDesc& d = b.d[i];
-    d.A = (const float*)ptrs[7 * i + 0];
+    d.A = ptrs[7 * i + 0];
     d.gidx = (const int*)ptrs[7 * i + 1];
-    d.B = (const float*)ptrs[7 * i + 2];
+    d.B = ptrs[7 * i + 2];
     d.bias = (const float*)ptrs[7 * i + 3];
     d.C = (float*)ptrs[7 * i + 4];
-    d.B2 = (const float*)ptrs[7 * i + 5];
-    d.B3 = (const float*)ptrs[7 * i + 6];
-    const int* q = ints + 14 * i;
+    d.B2 = ptrs[7 * i + 5];
+    d.B3 = ptrs[7 * i + 6];
+    const int* q = ints + 16 * i;
     d.M = q[0]; d.N = q[1]; d.K = q[2]; d.lda = q[3]; d.ldb = q[4]; d.ldc = q[5];
     d.a_mode = q[6]; d.b_mode = q[7]; d.act = q[8]; d.accumulate = q[9]; d.drop_ld = q[10];
-    d.drop_on = q[11]; d.gather_on = q[12]; d.kseg = q[13];
+    d.drop_on = q[11]; d.gather_on = q[12]; d.kseg = q[13]; d.a_bf16 = q[14] != 0; d.b_bf16 = q[15] != 0;
     if (d.kseg > 0 && (d.b_mode != 1 || d.gather_on == 2 || !d.B2 || (d.K > 2 * d.kseg && !d.B3) || d.K > 3 * d.kseg))
       return -5;
     d.alpha = floats[2 * i];
@@ -361,12 +612,26 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     d.offset = seeds[2 * i + 1];
     if (d.M < 0 || d.N < 0 || d.K < 0) return -2;
     if (d.drop_on < 0 || d.drop_on > 3 || d.gather_on < 0 || d.gather_on > 2 || d.act < 0 || d.act > 1) return -3;
-    if (d.drop_on && (!(d.pdrop > 0.f && d.pdrop < 1.f) || d.drop_ld % 16 != 0 || (d.drop_on == 1 && d.a_mode != 0) ||
-                      (d.drop_on == 2 && d.b_mode != 1)))
+    if (d.drop_on && (!(d.pdrop > 0.f && d.pdrop < 1.f) || d.drop_ld % 16 != 0 ||
+                      (d.drop_on == 1 && (d.a_mode != 0 || d.a_bf16)) || (d.drop_on == 2 && (d.b_mode != 1 || d.b_bf16))))
       return -3;
     if (d.gather_on && (!d.gidx || (d.gather_on == 1 && d.a_mode != 0) || (d.gather_on == 2 && d.b_mode != 1))) return -4;
+  }
+  b.n = n;
+  const bool fast = fast_ok(b), mixed = mixed_dtypes(b);
+  int v = (tile >= 1 && tile <= 4) ? tile : choose_tile(b);
+  if (!fast || mixed) v = 1;  // the generic (any alignment) and mixed-dtype kernels: 64 x 64
+  int tm, tn;
+  tile_dims(v, tm, tn);
+  int tiles = 0;
+  long need = 0;
+  int red_total = 0;
+  for (int i = 0; i < n; ++i) {
+    GemmDesc& d = b.d[i];
+    d.tiles_n = (d.N + tn - 1) / tn;
+    const int t = ((d.M + tm - 1) / tm) * d.tiles_n;
     // split-K: the reduce applies the whole epilogue (alpha, bias, tanh, output dropout, accumulate)
-    d.splits = choose_splits(d.M, d.N, d.K);
+    d.splits = choose_splits(t, d.K);
     d.kchunk = d.splits > 1 ? ((d.K + d.splits - 1) / d.splits + TK - 1) / TK * TK : d.K;
     if (d.splits > 1) d.splits = (d.K + d.kchunk - 1) / d.kchunk;
     d.P = nullptr;
@@ -375,14 +640,34 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
       need += (long)d.splits * d.M * d.N;
       red_total += d.M * d.N;
     }
-    d.tiles_n = (d.N + TN - 1) / TN;
     d.tile_base = tiles;
-    tiles += ((d.M + TM - 1) / TM) * d.tiles_n * d.splits;
+    tiles += t * d.splits;
   }
-  b.n = n;
   if (scratch == nullptr && need > 0) return need;  // query: the caller allocates and calls again
   if (tiles == 0) return 0;
-  hipLaunchKernelGGL(small_gemm_kernel, dim3(tiles), dim3(256), 0, s, b);
+  const int dt = (b.d[0].a_bf16 ? 2 : 0) | (b.d[0].b_bf16 ? 1 : 0);
+#define SG_LAUNCH(FM, FN)                                                                                  \
+  do {                                                                                                     \
+    if (dt == 0)                                                                                           \
+      hipLaunchKernelGGL((small_gemm_kernel<FM, FN, true, false, false>), dim3(tiles), dim3(256), 0, s, b);  \
+    else if (dt == 1)                                                                                      \
+      hipLaunchKernelGGL((small_gemm_kernel<FM, FN, true, false, true>), dim3(tiles), dim3(256), 0, s, b);   \
+    else if (dt == 2)                                                                                      \
+      hipLaunchKernelGGL((small_gemm_kernel<FM, FN, true, true, false>), dim3(tiles), dim3(256), 0, s, b);   \
+    else                                                                                                   \
+      hipLaunchKernelGGL((small_gemm_kernel<FM, FN, true, true, true>), dim3(tiles), dim3(256), 0, s, b);    \
+  } while (0)
+  if (!fast)
+    hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);
+  else if (mixed)
+    hipLaunchKernelGGL(small_gemm_mixed_kernel, dim3(tiles), dim3(256), 0, s, b);
+  else switch (v) {
+    case 2: SG_LAUNCH(4, 2); break;
+    case 3: SG_LAUNCH(2, 4); break;
+    case 4: SG_LAUNCH(4, 4); break;
+    default: SG_LAUNCH(2, 2); break;
+  }
+#undef SG_LAUNCH
   if (red_total > 0) {
     const int blocks = min(2048, (red_total + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, b, red_total);
@@ -405,14 +690,15 @@ extern "C" long fr_colsum_f32(const float* const* xs, float* const* outs, const 
     d.N = ints[4 * i + 1];
     d.ld = ints[4 * i + 2];
     d.accumulate = ints[4 * i + 3];
-    d.col_blocks = (d.N + 63) / 64;
+    d.vec = (d.N % 4 == 0 && d.ld % 4 == 0 && ((uintptr_t)d.X & 15) == 0) ? 1 : 0;
+    d.col_blocks = d.vec ? (d.N + 255) / 256 : (d.N + 63) / 64;
     d.chunks = max(1, (d.M + CS_ROWS - 1) / CS_ROWS);
     d.part = part ? part + need : nullptr;
     need += (long)d.chunks * d.N;
     d.block_base = blocks;
     blocks += d.col_blocks * d.chunks;
     d.block2_base = blocks2;
-    blocks2 += d.col_blocks;
+    blocks2 += (d.N + 63) / 64;
   }
   b.n = n;
   if (part == nullptr) return need;
@@ -426,14 +712,18 @@ extern "C" long fr_colsum_f32(const float* const* xs, float* const* outs, const 
 
 // ---------------------------------------------------------------------------------------
 // X'[m, k] = v[idx[m], k] * Z(m * K + k): the user encoder's gathered, dropped-out input
-// (encoder.py:50), materialised once per step (fp32 [B*H, D], 5 MB) instead of regenerated in
-// every GEMM tile that reads it -- the Q/K/V projection's A loads (21 column tiles each redid
-// the Philox draws of their rows) and the weight-gradient GEMMs' B loads (one redo per output
-// row tile).  Same mask, same fp32 product: bitwise the values those loads computed.
-// One thread per 4 consecutive elements = one Philox draw (K % 4 == 0, host-checked).
+// (encoder.py:50), materialised once per step ([B*H, D], fp32 or -- when every reader is a
+// bf16-operand GEMM -- bf16, 2.5 MB) instead of regenerated in every GEMM tile that reads it.
+// Same mask, same fp32 product; the bf16 form is exactly what the GEMMs' fp32 loads rounded
+// the fp32 form to.  One thread per 4 consecutive elements = one Philox draw (K % 4 == 0).
 namespace {
+__device__ __forceinline__ void store4(float* out, long e, float4 x) { *(float4*)(out + e) = x; }
+__device__ __forceinline__ void store4(bf16* out, long e, float4 x) {
+  *(bf16x4*)(out + e) = bf16x4{f2bf(x.x), f2bf(x.y), f2bf(x.z), f2bf(x.w)};
+}
+template <typename OutT>
 __global__ __launch_bounds__(256) void gather_dropout_kernel(const float* __restrict__ v, const int* __restrict__ idx,
-                                                             float* __restrict__ out, int M, int K, float p,
+                                                             OutT* __restrict__ out, int M, int K, float p,
                                                              unsigned long long seed, unsigned long long offset,
                                                              const unsigned long long* __restrict__ dev_off) {
   const long q = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index
@@ -451,17 +741,22 @@ __global__ __launch_bounds__(256) void gather_dropout_kernel(const float* __rest
     x.z *= drop_scale(r.z, p, inv_keep);
     x.w *= drop_scale(r.w, p, inv_keep);
   }
-  *(float4*)(out + e) = x;
+  store4(out, e, x);
 }
 }  // namespace
 
-extern "C" int fr_gather_dropout_f32(const float* v, const int* idx, float* out, int M, int K, float p,
-                                     unsigned long long seed, unsigned long long offset,
-                                     const unsigned long long* dev_off, hipStream_t s) {
+extern "C" int fr_gather_dropout(const float* v, const int* idx, void* out, int out_bf16, int M, int K, float p,
+                                 unsigned long long seed, unsigned long long offset, const unsigned long long* dev_off,
+                                 hipStream_t s) {
   if (K % 4 != 0 || M < 0) return 1;
   const long n4 = (long)M * K / 4;
   if (n4 == 0) return 0;
-  hipLaunchKernelGGL(gather_dropout_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, v, idx, out, M, K, p,
-                     seed, offset, dev_off);
+  const dim3 grid((unsigned)((n4 + 255) / 256));
+  if (out_bf16)
+    hipLaunchKernelGGL(gather_dropout_kernel<bf16>, grid, dim3(256), 0, s, v, idx, (bf16*)out, M, K, p, seed, offset,
+                       dev_off);
+  else
+    hipLaunchKernelGGL(gather_dropout_kernel<float>, grid, dim3(256), 0, s, v, idx, (float*)out, M, K, p, seed, offset,
+                       dev_off);
   return 0;
 }

@@ -278,23 +278,27 @@ class Gemm:
         self.bseg, self.kseg = tuple(bseg), int(kseg)
 
 
-def gather_dropout(v: torch.Tensor, idx: torch.Tensor, p: float, seed: int, offset: int, dev_off=None) -> torch.Tensor:
-    """``v[idx] * Z`` (fp32): rows of ``v`` gathered and dropped out with the counter mask of
-    element ``m * K + k`` (offset + ``*dev_off``) -- the mask ``small_gemm``'s dropout loads use."""
+def gather_dropout(v: torch.Tensor, idx: torch.Tensor, p: float, seed: int, offset: int, dev_off=None,
+                   bf16_out: bool = False) -> torch.Tensor:
+    """``v[idx] * Z``: rows of ``v`` gathered and dropped out with the counter mask of element
+    ``m * K + k`` (offset + ``*dev_off``) -- the mask ``small_gemm``'s dropout loads use.  fp32,
+    or bf16 (``bf16_out``: the fp32 product rounded once, as a bf16-operand GEMM would)."""
     if _dev(v):
         return native.require_for(v).gather_dropout(v.contiguous(), idx.to(torch.int32).contiguous(), float(p),
-                                                    int(seed), int(offset), dev_off)
+                                                    int(seed), int(offset), dev_off, bool(bf16_out))
     x = v.index_select(0, idx.long())
     if p > 0:
         off = int(offset) + (int(dev_off.item()) if dev_off is not None else 0)
         idx_e = torch.arange(x.numel(), device=x.device, dtype=torch.int64)
         x = x * ref.dropout_scale(idx_e, p, int(seed), off).view_as(x).to(x.dtype)
-    return x
+    return x.to(torch.bfloat16) if bf16_out else x
 
 
-def small_gemm(*gs: Gemm, dev_off=None) -> None:
+def small_gemm(*gs: Gemm, dev_off=None, tile: int = 0) -> None:
     """Run up to 6 independent GEMMs in one launch (device only).  ``dev_off``: an int64[1]
-    device counter added to every dropout offset (HIP-graph replays draw fresh masks)."""
+    device counter added to every dropout offset (HIP-graph replays draw fresh masks).
+    Operands A / B may be fp32 or bf16 (C fp32).  ``tile``: 0 = the launcher's choice, 1..4 =
+    64x64 / 128x64 / 64x128 / 128x128 (benchmarks)."""
     ints, floats, seeds = [], [], []
     for g in gs:
         ints += [g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.a_mode, g.b_mode, g.act, int(g.accumulate), g.drop_ld,
@@ -303,7 +307,7 @@ def small_gemm(*gs: Gemm, dev_off=None) -> None:
         seeds += [g.seed, g.offset]
     native.require_for(gs[0].A).small_gemm([g.A for g in gs], [g.gidx for g in gs], [g.B for g in gs],
                                            [g.bias for g in gs], [g.C for g in gs], ints, floats, seeds, dev_off,
-                                           [t for g in gs for t in g.bseg])
+                                           [t for g in gs for t in g.bseg], int(tile))
 
 
 def small_gemm_ref(g: Gemm) -> torch.Tensor:

@@ -548,7 +548,7 @@ class UserStepFn(torch.autograd.Function):
     slots) to rows of ``v``; ``perm / ptr`` group them per news for the segment sum.  The
     input dropout of the user encoder (``encoder.py:50``) is the Philox mask of element
     ``(b*H + t) * D + d`` of the gathered history matrix with offset ``drop[2] + *dev_off``:
-    the gathered, dropped-out input X' is materialised once (``ops.gather_dropout``, 5 MB),
+    the gathered, dropped-out input X' is materialised once (``ops.gather_dropout``, bf16, 2.5 MB),
     read by the Q/K/V GEMMs and the weight gradients; the dgrad regenerates the mask in its
     epilogue.  (Round 2 first applied the mask inside every GEMM tile's operand loads; each
     of the ~21 column tiles redid its rows' Philox draws.)"""
@@ -562,20 +562,28 @@ class UserStepFn(torch.autograd.Function):
         his_idx = inv[BC:]
         ci = inv[:BC]
         cand = v.index_select(0, ci if ci.dtype in (torch.int32, torch.int64) else ci.long()).view(B, C, D)
-        qkv = torch.empty(BH, 3 * D, device=v.device, dtype=torch.float32)
+        D3 = 3 * D
+        qkv = torch.empty(BH, D3, device=v.device, dtype=torch.float32)
+        # the GEMMs' weight operands in bf16 ([Wq; Wk; Wv; W1], what their fp32 loads rounded
+        # to) and the concatenated Q|K|V bias, one cast launch per step
+        wb = torch.empty(D3 + Qd, D, device=v.device, dtype=torch.bfloat16)
+        bqkv = torch.empty(D3, device=v.device, dtype=torch.float32)
+        ops.native.require_for(v).multi_cast([wq, wk, wv, w1, bq, bk, bv],
+                                             [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D],
+                                              bqkv[2 * D:]])
         p, seed, off = drop
-        # X' = drop(v[his]) once (5 MB): the Q/K/V projection and the weight gradients read it
-        xd = ops.gather_dropout(v, his_idx, p, seed, off, dev_off)
-        ops.small_gemm(*[ops.Gemm(xd, w, qkv[:, s * D:(s + 1) * D], BH, D, D, D, D, 3 * D, bias=b)
-                         for s, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv)))])
-        q3 = qkv.view(B, H, 3 * D)
+        # X' = drop(v[his]) once, in bf16 (2.5 MB): the Q|K|V projection and the weight
+        # gradients read it
+        xd = ops.gather_dropout(v, his_idx, p, seed, off, dev_off, bf16_out=True)
+        ops.small_gemm(ops.Gemm(xd, wb[:D3], qkv, BH, D3, D, D, D, D3, bias=bqkv))  # one N = 3D GEMM
+        q3 = qkv.view(B, H, D3)
         c3, stats = ops.user_attention_fwd(q3, heads, hd)
         e = torch.empty(BH, Qd, device=v.device, dtype=torch.float32)
-        ops.small_gemm(ops.Gemm(c3, w1, e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
+        ops.small_gemm(ops.Gemm(c3, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
         e3 = e.view(B, H, Qd)
         u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2)
         loss, scores, dcand, du = ops.score_ce(cand, u, act)
-        ctx.save_for_backward(v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2, xd)
+        ctx.save_for_backward(v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wb, w2, xd)
         ctx.meta = meta
         ctx.mark_non_differentiable(scores)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the scores (one fill launch)
@@ -583,11 +591,12 @@ class UserStepFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss, gscores):
-        v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wq, wk, wv, w1, w2, xd = ctx.saved_tensors
+        v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wb, w2, xd = ctx.saved_tensors
         B, C, H, heads, hd, act, drop, dev_off, ldp, padded = ctx.meta
         D = v.shape[1]
         BC, BH = B * C, B * H
-        Qd = w1.shape[0]
+        D3 = 3 * D
+        Qd = wb.shape[0] - D3
         dev = v.device
         R = inv.numel()
         rows = torch.empty(R, D, device=dev, dtype=torch.float32)  # per-occurrence news gradients
@@ -596,22 +605,22 @@ class UserStepFn(torch.autograd.Function):
         # additive pool backward: dx_direct = alpha du, dpre = da w2 (1 - e^2), dw2, db2
         dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du_g, True)
         dpre2 = dpre.view(BH, Qd)
-        ops.small_gemm(ops.Gemm(dpre2, w1, dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
+        ops.small_gemm(ops.Gemm(dpre2, wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
         dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd).view(BH, 3 * D)
         p, seed, off = drop
         his_idx = inv[BC:]
         dx = rows[BC:]
-        # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the three weight blocks
-        # (K-segmented B), the dropout backward in its epilogue
+        # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,
+        # the dropout backward in its epilogue
         ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
-        ops.small_gemm(ops.Gemm(dqkv, wq, dx, BH, D, 3 * D, 3 * D, D, D, b_mode=1, bseg=(wk, wv), kseg=D, **ekw),
-                       dev_off=dev_off)
-        # weight gradients in one launch: dW_s = dS^T X' (X' saved by the forward) and
-        # dW1 = dpre^T ctx
-        gq, gk, gv = (torch.empty(D, D, device=dev) for _ in range(3))
+        ops.small_gemm(ops.Gemm(dqkv, wb[:D3], dx, BH, D, D3, D3, D, D, b_mode=1, **ekw), dev_off=dev_off)
+        # weight gradients in one launch: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM;
+        # X' saved by the forward, bf16) and dW1 = dpre^T ctx (fp32 operands: the
+        # mixed-dtype kernel)
+        gqkv = torch.empty(D3, D, device=dev)
+        gq, gk, gv = gqkv[:D], gqkv[D:2 * D], gqkv[2 * D:]
         gw1 = torch.empty(Qd, D, device=dev)
-        ops.small_gemm(*[ops.Gemm(dqkv[:, s * D:(s + 1) * D], xd, g, D, D, BH, 3 * D, D, D, a_mode=1, b_mode=1)
-                         for s, g in enumerate((gq, gk, gv))],
+        ops.small_gemm(ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1),
                        ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1))
         gbq, gbk, gbv = (torch.empty(D, device=dev) for _ in range(3))
         gb1 = torch.empty(Qd, device=dev)

@@ -79,7 +79,8 @@ def init(role: str = "client", device: str = "auto", timeout_s: float = 600.0, g
         dev = torch.device("cuda", gi)
     else:
         dev = torch.device("cpu")
-    ctx = DistContext(rank, world, local_rank, dev, role, [role], None, None, [0], False)
+    ctx = DistContext(rank=rank, world=world, local_rank=local_rank, device=dev, role=role, roles=[role],
+                      client_ranks=[0], initialized=False)
     if world == 1:
         return ctx
     timeout = datetime.timedelta(seconds=timeout_s)

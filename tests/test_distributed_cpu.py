@@ -302,3 +302,14 @@ def test_grad_avg_with_collective_checker(tmp_path):
         argv = [script, "2", "16", "1", *TINY, f"--snapshot_path={snap}"]
         outs = run_ranks([argv, argv], {"FEDREC_COLL_CHECK": "1"})
         _ok(outs)
+
+
+def test_single_process_context_is_one_client(monkeypatch):
+    """world == 1 (the bench's N=1 path): a one-client context with no process groups."""
+    from fedrec_with_pytorchdistributed_amd.parallel import dist as fdist
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    ctx = fdist.init(device="cpu")
+    assert ctx.world == 1 and ctx.num_clients == 1 and ctx.client_index == 0 and not ctx.initialized
+    assert ctx.client_ctrl_group is None and ctx.data_group is None
+    assert fdist.make_grad_allreduce(ctx) is None or callable(fdist.make_grad_allreduce(ctx))

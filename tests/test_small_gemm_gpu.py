@@ -14,14 +14,18 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
 
 
-def _check(g, tol=2e-3):
+TILES = [1, 2, 3, 4]  # 64x64, 128x64, 64x128, 128x128
+
+
+def _check(g, tol=2e-3, tile=0):
     want = ops.small_gemm_ref(g)
-    ops.small_gemm(g)
+    ops.small_gemm(g, tile=tile)
     got = g.C.reshape(-1)[: g.M * g.ldc].view(g.M, g.ldc)[:, : g.N]
     assert _rel(got, want) < tol, _rel(got, want)
 
 
-def test_nt_gather_dropout_bias_tanh(dev):
+@pytest.mark.parametrize("tile", TILES)
+def test_nt_gather_dropout_bias_tanh(dev, tile):
     torch.manual_seed(0)
     x = torch.randn(900, 400, device=dev)
     gidx = torch.randint(0, 900, (3200,), device=dev, dtype=torch.int32)
@@ -29,29 +33,32 @@ def test_nt_gather_dropout_bias_tanh(dev):
     b = torch.randn(200, device=dev)
     C = torch.zeros(3200, 200, device=dev)
     _check(Gemm(x, w, C, 3200, 200, 400, 400, 400, 200, bias=b, act=1, gidx=gidx, gather_on=1,
-                pdrop=0.2, drop_on=1, drop_ld=400, seed=5, offset=9))
+                pdrop=0.2, drop_on=1, drop_ld=400, seed=5, offset=9), tile=tile)
 
 
-def test_tn_wgrad_with_gathered_dropped_input(dev):
+@pytest.mark.parametrize("tile", TILES)
+def test_tn_wgrad_with_gathered_dropped_input(dev, tile):
     torch.manual_seed(1)
     dy = torch.randn(3200, 1200, device=dev)  # stored [K, M]: dY, column slice = one projection
     x = torch.randn(700, 400, device=dev)
     gidx = torch.randint(0, 700, (3200,), device=dev, dtype=torch.int32)
     C = torch.zeros(400, 400, device=dev)
     _check(Gemm(dy[:, 400:], x, C, 400, 400, 3200, 1200, 400, 400, a_mode=1, b_mode=1, gidx=gidx, gather_on=2,
-                pdrop=0.2, drop_on=2, drop_ld=400, seed=3, offset=4))
+                pdrop=0.2, drop_on=2, drop_ld=400, seed=3, offset=4), tile=tile)
 
 
-def test_nn_dgrad_dropout_epilogue_accumulate(dev):
+@pytest.mark.parametrize("tile", TILES)
+def test_nn_dgrad_dropout_epilogue_accumulate(dev, tile):
     torch.manual_seed(2)
     dy = torch.randn(3200, 400, device=dev)
     w = torch.randn(400, 400, device=dev) * 0.05
     C = torch.randn(3200, 400, device=dev)
     _check(Gemm(dy, w, C, 3200, 400, 400, 400, 400, 400, b_mode=1, accumulate=True, pdrop=0.2, drop_on=3,
-                drop_ld=400, seed=1, offset=2))
+                drop_ld=400, seed=1, offset=2), tile=tile)
 
 
-def test_grouped_launch_and_odd_shapes(dev):
+@pytest.mark.parametrize("tile", [0] + TILES)
+def test_grouped_launch_and_odd_shapes(dev, tile):
     torch.manual_seed(3)
     gs, wants = [], []
     for (M, N, K) in ((17, 33, 5), (64, 64, 64), (1565, 400, 768), (3, 200, 1200)):
@@ -61,7 +68,7 @@ def test_grouped_launch_and_odd_shapes(dev):
         g = Gemm(A, B, C, M, N, K, K, K, N, alpha=0.5)
         gs.append(g)
         wants.append(ops.small_gemm_ref(g))
-    ops.small_gemm(*gs)
+    ops.small_gemm(*gs, tile=tile)
     for g, w in zip(gs, wants):
         assert _rel(g.C, w) < 2e-3
 
@@ -80,11 +87,74 @@ def test_colsum_f32_deterministic(dev):
     assert torch.equal(o1, o3)
 
 
-def test_k_segmented_b_with_dropout_epilogue(dev):
+@pytest.mark.parametrize("tile", TILES)
+def test_k_segmented_b_with_dropout_epilogue(dev, tile):
     """dx = [dQ|dK|dV] [Wq; Wk; Wv]: one GEMM over three separately stored weight blocks."""
     torch.manual_seed(5)
     dq = torch.randn(3200, 1200, device=dev)
     ws = [torch.randn(400, 400, device=dev) * 0.05 for _ in range(3)]
     C = torch.zeros(3200, 400, device=dev)
     _check(Gemm(dq, ws[0], C, 3200, 400, 1200, 1200, 400, 400, b_mode=1, bseg=(ws[1], ws[2]), kseg=400,
-                pdrop=0.2, drop_on=3, drop_ld=400, seed=2, offset=3))
+                pdrop=0.2, drop_on=3, drop_ld=400, seed=2, offset=3), tile=tile)
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("a_mode,b_mode", [(0, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("dt", ["a", "b", "ab"])
+def test_bf16_operands_match_fp32_operands_bitwise(dev, tile, a_mode, b_mode, dt):
+    """A bf16 operand is what the kernel's fp32 loads round to: the product is bitwise the one
+    of the fp32 operand (same tile, same order), for every layout and tile."""
+    torch.manual_seed(6)
+    M, N, K = 1000, 300, 456
+    A = torch.randn(M, K, device=dev) if a_mode == 0 else torch.randn(K, M, device=dev)
+    B = torch.randn(N, K, device=dev) if b_mode == 0 else torch.randn(K, N, device=dev)
+    bias = torch.randn(N, device=dev)
+    lda, ldb = (K if a_mode == 0 else M), (K if b_mode == 0 else N)
+    C32 = torch.zeros(M, N, device=dev)
+    ops.small_gemm(Gemm(A, B, C32, M, N, K, lda, ldb, N, a_mode=a_mode, b_mode=b_mode, bias=bias, act=1), tile=tile)
+    Ah = A.to(torch.bfloat16) if "a" in dt else A
+    Bh = B.to(torch.bfloat16) if "b" in dt else B
+    C16 = torch.zeros(M, N, device=dev)
+    g = Gemm(Ah, Bh, C16, M, N, K, lda, ldb, N, a_mode=a_mode, b_mode=b_mode, bias=bias, act=1)
+    ops.small_gemm(g, tile=tile)
+    assert torch.equal(C32, C16)
+    assert _rel(C16, ops.small_gemm_ref(g)) < 2e-3
+
+
+@pytest.mark.parametrize("tile", TILES)
+def test_bf16_unaligned_and_odd_edges(dev, tile):
+    """bf16 operands whose rows are not 16-byte aligned (odd K / odd offsets): the scalar
+    edge path, every element once."""
+    torch.manual_seed(7)
+    M, N, K = 77, 45, 131
+    A = torch.randn(M * K + 1, device=dev).to(torch.bfloat16)[1:].view(M, K)
+    B = torch.randn(K, N, device=dev).to(torch.bfloat16)
+    C = torch.zeros(M, N, device=dev)
+    _check(Gemm(A, B, C, M, N, K, K, N, N, b_mode=1), tile=tile)
+
+
+def test_gather_dropout_bf16_is_rounded_fp32(dev):
+    torch.manual_seed(8)
+    v = torch.randn(500, 400, device=dev)
+    idx = torch.randint(0, 500, (3200,), device=dev, dtype=torch.int32)
+    off = torch.tensor([7], device=dev, dtype=torch.int64)
+    x32 = ops.gather_dropout(v, idx, 0.2, 11, 3, off)
+    x16 = ops.gather_dropout(v, idx, 0.2, 11, 3, off, bf16_out=True)
+    assert x16.dtype == torch.bfloat16 and torch.equal(x16, x32.to(torch.bfloat16))
+
+
+def test_colsum_f32_scalar_and_vector_paths(dev):
+    torch.manual_seed(9)
+    X = torch.randn(3201, 1204, device=dev)
+    Z = torch.randn(3201, 1203, device=dev)
+    outs = [torch.zeros(n, device=dev) for n in (33, 400, 1203)]
+    # a misaligned view (scalar path), an aligned float4 view, and an odd-width matrix (scalar)
+    ops.colsum_f32([(X[:, 1:], outs[0], 3201, 33, 1204), (X[:, 400:], outs[1], 3200, 400, 1204),
+                    (Z, outs[2], 3201, 1203, 1203)])
+    assert torch.allclose(outs[0], X[:, 1:34].sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(outs[1], X[:3200, 400:800].sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(outs[2], Z.sum(0), rtol=1e-4, atol=1e-3)
+    Y = torch.randn(4096, 800, device=dev)
+    o = torch.zeros(800, device=dev)
+    ops.colsum_f32([(Y, o, 4096, 800, 800)])
+    assert torch.allclose(o, Y.double().sum(0).float(), rtol=1e-5, atol=1e-3)
