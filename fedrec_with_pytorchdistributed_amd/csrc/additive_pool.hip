@@ -24,11 +24,15 @@ constexpr int MAXT_G = 2048;  // generic kernels: long user histories (Q6: never
 template <typename T>
 __device__ __forceinline__ float ld(const T* p) { return (float)*p; }
 
+// keep (optional, [n, T] int32): position t of sequence n is pooled iff keep[n T + t] != 0 (the
+// mask_padding option): its score becomes -inf, so its weight is exactly 0; a sequence with every
+// position masked pools to 0 (m := 0), as the torch oracle's masked eps-softmax.  The backward
+// needs no mask: it reads the (zero) weights.
 template <typename TX>
 __global__ __launch_bounds__(256) void pool_fwd_kernel(const TX* __restrict__ x, const TX* __restrict__ e,
                                                        const float* __restrict__ w2, const float* __restrict__ b2,
                                                        float* __restrict__ out, float* __restrict__ alpha_out, int T,
-                                                       int D, int Q) {
+                                                       int D, int Q, const int* __restrict__ keep) {
   __shared__ float a_s[MAXT_G];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const TX* xe = x + (size_t)n * T * D;
@@ -40,13 +44,14 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const TX* __restrict__ x,
     float s = 0.f;
     for (int q = lane; q < Q; q += 64) s += ld(ee + (size_t)t * Q + q) * w2[q];
     s = wave_sum(s);
-    if (lane == 0) a_s[t] = s + b2[0];
+    if (lane == 0) a_s[t] = (keep == nullptr || keep[(size_t)n * T + t] != 0) ? s + b2[0] : -INFINITY;
   }
   __syncthreads();
   if (wave == 0) {
     float m = -INFINITY;
     for (int t = lane; t < T; t += 64) m = fmaxf(m, a_s[t]);
     m = wave_max(m);
+    if (m == -INFINITY) m = 0.f;
     float l = 0.f;
     for (int t = lane; t < T; t += 64) {
       const float p = __expf(a_s[t] - m);
@@ -151,7 +156,7 @@ __device__ __forceinline__ void unpack8(const bf16x8 v, float (&f)[8]) {
 __global__ __launch_bounds__(256) void pool_fwd16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ e,
                                                          const float* __restrict__ w2, const float* __restrict__ b2,
                                                          float* __restrict__ out, float* __restrict__ alpha_out, int T,
-                                                         int D, int Q) {
+                                                         int D, int Q, const int* __restrict__ keep) {
   __shared__ float a_s[MAXT];
   __shared__ float part[2][1024];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -179,13 +184,14 @@ __global__ __launch_bounds__(256) void pool_fwd16_kernel(const bf16* __restrict_
       }
     }
     sacc = wave_sum(sacc);
-    if (lane == 0) a_s[t] = sacc + b2[0];
+    if (lane == 0) a_s[t] = (keep == nullptr || keep[(size_t)n * T + t] != 0) ? sacc + b2[0] : -INFINITY;
   }
   __syncthreads();
   if (wave == 0) {
     float m = -INFINITY;
     for (int t = lane; t < T; t += 64) m = fmaxf(m, a_s[t]);
     m = wave_max(m);
+    if (m == -INFINITY) m = 0.f;
     float l = 0.f;
     for (int t = lane; t < T; t += 64) {
       const float p = __expf(a_s[t] - m);
@@ -320,21 +326,194 @@ __global__ __launch_bounds__(256) void pool_bwd16_kernel(const bf16* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// fp32 short-sequence forms (the user encoder's pool: n = B impressions, T = H <= 64, D = 400,
+// Q = 200).  The generic kernels above run one block per impression -- 64 blocks at B = 64 --
+// and walk rows with a wave-sum per row: ~13 dependent load + reduce rounds per wave, 20 us
+// (fwd) / 24 us (bwd) for 7.7 MB.  Here each impression gets US blocks (column / row slices)
+// and every phase issues all of a lane's loads at once: row-parallel partial dots (lane =
+// (row, quarter of the row)) reduced through LDS, then the weighted sums over t-groups.
+constexpr int UT = 64;  // max T
+constexpr int US = 4;   // blocks per sequence
+
+// a_t = w2 . e_t + b2 for t < T -> a_s (masked: -inf); lane (t = tid / 4, part = tid % 4)
+__device__ __forceinline__ void upool_scores(const float* __restrict__ ee, const float* __restrict__ w2, float b2,
+                                             const int* __restrict__ keep_n, int T, int Q, float* a_s,
+                                             float (*part)[4]) {
+  const int tid = threadIdx.x, t = tid >> 2, pq = tid & 3;
+  const int Q4 = Q >> 2, per = (Q4 + 3) >> 2;
+  float acc = 0.f;
+  if (t < T) {
+    const float4* er = (const float4*)(ee + (size_t)t * Q);
+    const float4* wr = (const float4*)w2;
+#pragma unroll 7
+    for (int c = pq * per; c < min(Q4, (pq + 1) * per); ++c) {
+      const float4 v = er[c], w = wr[c];
+      acc += v.x * w.x + v.y * w.y + v.z * w.z + v.w * w.w;
+    }
+  }
+  part[t][pq] = acc;
+  __syncthreads();
+  if (tid < T) {
+    const float a = (part[tid][0] + part[tid][1]) + (part[tid][2] + part[tid][3]) + b2;
+    a_s[tid] = (keep_n == nullptr || keep_n[tid] != 0) ? a : -INFINITY;
+  }
+  __syncthreads();
+}
+
+// in wave 0: a_s -> alpha (eps-softmax, stable form; every position masked -> all 0)
+__device__ __forceinline__ void upool_softmax(float* a_s, int T) {
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x >= 64) return;
+  const float a = lane < T ? a_s[lane] : -INFINITY;
+  float m = wave_max(a);
+  if (m == -INFINITY) m = 0.f;
+  const float p = lane < T ? __expf(a - m) : 0.f;
+  const float inv = 1.0f / (wave_sum(p) + 1e-8f * __expf(-m));
+  if (lane < T) a_s[lane] = p * inv;
+}
+
+__global__ __launch_bounds__(256) void upool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ e,
+                                                        const float* __restrict__ w2, const float* __restrict__ b2,
+                                                        float* __restrict__ out, float* __restrict__ alpha_out, int T,
+                                                        int D, int Q, const int* __restrict__ keep) {
+  __shared__ float a_s[UT];
+  __shared__ float part[UT][4];
+  __shared__ float4 red[10][32];
+  const int n = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  upool_scores(e + (size_t)n * T * Q, w2, b2[0], keep ? keep + (size_t)n * T : nullptr, T, Q, a_s, part);
+  upool_softmax(a_s, T);
+  __syncthreads();
+  if (y == 0 && tid < T) alpha_out[(size_t)n * T + tid] = a_s[tid];
+  // out[d] for this block's slice of float4 columns: lane (t-group tg of 10, column c)
+  const int D4 = D >> 2, span = (D4 + US - 1) / US, c0 = y * span, nc = min(span, D4 - c0);
+  const int tg = tid / 32, c = tid % 32;  // 8 t-groups x 32 columns (span <= 32)
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < nc) {
+    const float4* xr = (const float4*)(x + (size_t)n * T * D) + c0 + c;
+#pragma unroll 4
+    for (int t = tg; t < T; t += 8) {
+      const float4 v = xr[(size_t)t * D4];
+      const float al = a_s[t];
+      acc.x += al * v.x; acc.y += al * v.y; acc.z += al * v.z; acc.w += al * v.w;
+    }
+  }
+  red[tg][c] = acc;
+  __syncthreads();
+  if (tid < 32 && c < nc) {
+    float4 s = red[0][c];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      s.x += red[j][c].x; s.y += red[j][c].y; s.z += red[j][c].z; s.w += red[j][c].w;
+    }
+    ((float4*)(out + (size_t)n * D))[c0 + c] = s;
+  }
+}
+
+// grid (n, US): every block forms da (full x . g dots), then its quarter of the rows: dpre,
+// the dw2 partial of those rows (partial row n US + y), dx_direct; db2 from block 0 (others 0)
+__global__ __launch_bounds__(256) void upool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ e,
+                                                        const float* __restrict__ alpha, const float* __restrict__ w2,
+                                                        const float* __restrict__ g, float* __restrict__ dx,
+                                                        float* __restrict__ dpre, float* __restrict__ dw2,
+                                                        float* __restrict__ db2, int T, int D, int Q) {
+  __shared__ float da_s[UT], al_s[UT];
+  __shared__ float part[UT][4];
+  __shared__ float4 red[4][64];
+  const int n = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  const float* xe = x + (size_t)n * T * D;
+  const float* gn = g + (size_t)n * D;
+  if (tid < T) al_s[tid] = alpha[(size_t)n * T + tid];
+  {  // dalpha_t = x_t . g: lane (t, quarter)
+    const int t = tid >> 2, pq = tid & 3, D4 = D >> 2, per = (D4 + 3) >> 2;
+    float acc = 0.f;
+    if (t < T) {
+      const float4* xr = (const float4*)(xe + (size_t)t * D);
+      const float4* gr = (const float4*)gn;
+#pragma unroll 5
+      for (int c = pq * per; c < min(D4, (pq + 1) * per); ++c) {
+        const float4 v = xr[c], w = gr[c];
+        acc += v.x * w.x + v.y * w.y + v.z * w.z + v.w * w.w;
+      }
+    }
+    part[t][pq] = acc;
+  }
+  __syncthreads();
+  if (tid < 64) {  // wave 0: da_t = alpha_t (dalpha_t - sum alpha dalpha); db2
+    const int lane = tid;
+    const float dal = lane < T ? (part[lane][0] + part[lane][1]) + (part[lane][2] + part[lane][3]) : 0.f;
+    const float al = lane < T ? al_s[lane] : 0.f;
+    const float s = wave_sum(al * dal);
+    const float da = al * (dal - s);
+    if (lane < T) da_s[lane] = da;
+    const float sd = wave_sum(da);
+    if (lane == 0) db2[(size_t)n * US + y] = y == 0 ? sd : 0.f;
+  }
+  __syncthreads();
+  const int rspan = (T + US - 1) / US, r0 = y * rspan, r1 = min(T, r0 + rspan);
+  {  // dpre rows [r0, r1) and their dw2 partial: lane (t-group of 4, float4 column q)
+    const int Q4 = Q >> 2, tg = tid >> 6, qc = tid & 63;  // Q4 <= 64
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (qc < Q4) {
+      const float4 w = ((const float4*)w2)[qc];
+      for (int t = r0 + tg; t < r1; t += 4) {
+        const float4 v = ((const float4*)(e + ((size_t)n * T + t) * Q))[qc];
+        const float da = da_s[t];
+        acc.x += da * v.x; acc.y += da * v.y; acc.z += da * v.z; acc.w += da * v.w;
+        ((float4*)(dpre + ((size_t)n * T + t) * Q))[qc] =
+            make_float4(da * w.x * (1.f - v.x * v.x), da * w.y * (1.f - v.y * v.y), da * w.z * (1.f - v.z * v.z),
+                        da * w.w * (1.f - v.w * v.w));
+      }
+    }
+    red[tg][qc] = acc;
+    __syncthreads();
+    if (tid < Q4) {
+      float4 s = red[0][tid];
+#pragma unroll
+      for (int j = 1; j < 4; ++j) {
+        s.x += red[j][tid].x; s.y += red[j][tid].y; s.z += red[j][tid].z; s.w += red[j][tid].w;
+      }
+      ((float4*)(dw2 + ((size_t)n * US + y) * Q))[tid] = s;
+    }
+  }
+  if (dx != nullptr) {  // dx_direct rows [r0, r1) = alpha_t g
+    const int D4 = D >> 2;
+    const float4* gr = (const float4*)gn;
+    for (int i = tid; i < (r1 - r0) * D4; i += 256) {
+      const int t = r0 + i / D4, c = i % D4;
+      const float4 gv = gr[c];
+      const float al = al_s[t];
+      ((float4*)(dx + ((size_t)n * T + t) * D))[c] = make_float4(al * gv.x, al * gv.y, al * gv.z, al * gv.w);
+    }
+  }
+}
+
+// the fp32 short-sequence kernels apply (16-byte rows, T <= 64, a block's column slice <= 32
+// float4, Q / 4 <= 64)
+__host__ __device__ inline bool upool_ok(int T, int D, int Q, int is_bf16) {
+  return !is_bf16 && T >= 1 && T <= UT && D % 4 == 0 && Q % 4 == 0 && (D / 4 + US - 1) / US <= 32 && Q / 4 <= 64;
+}
+
 }  // namespace
 
 extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const float* b2, float* out,
-                                    float* alpha, int n, int T, int D, int Q, int is_bf16, hipStream_t s) {
+                                    float* alpha, int n, int T, int D, int Q, int is_bf16, const int* keep,
+                                    hipStream_t s) {
   if (T > MAXT_G) return 1;
   if (n == 0) return 0;
-  if (is_bf16 && T <= MAXT && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256)
+  if (upool_ok(T, D, Q, is_bf16) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)e & 15) == 0 && ((uintptr_t)w2 & 15) == 0 &&
+      ((uintptr_t)out & 15) == 0)
+    hipLaunchKernelGGL(upool_fwd_kernel, dim3(n, US), dim3(256), 0, s, (const float*)x, (const float*)e, w2, b2, out,
+                       alpha, T, D, Q, keep);
+  else if (is_bf16 && T <= MAXT && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256)
     hipLaunchKernelGGL(pool_fwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, w2, b2, out, alpha,
-                       T, D, Q);
+                       T, D, Q, keep);
   else if (is_bf16)
     hipLaunchKernelGGL(pool_fwd_kernel<bf16>, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, w2, b2, out,
-                       alpha, T, D, Q);
+                       alpha, T, D, Q, keep);
   else
     hipLaunchKernelGGL(pool_fwd_kernel<float>, dim3(n, n < 128 ? 4 : (n < 256 ? 2 : 1)), dim3(256), 0, s,
-                       (const float*)x, (const float*)e, w2, b2, out, alpha, T, D, Q);
+                       (const float*)x, (const float*)e, w2, b2, out, alpha, T, D, Q, keep);
   return 0;
 }
 
@@ -342,11 +521,24 @@ extern "C" int fr_additive_pool_fwd(const void* x, const void* e, const float* w
 // dsum ([n, Q]): column sums of dpre, produced only by the vectorised text-head kernel.
 // Returns 0 when dsum was produced, -1 when the generic kernel ran (caller reduces dpre),
 // > 0 on argument errors.
+// partial rows of dw2 / db2 per sequence the backward writes (the caller sizes R = n * this)
+extern "C" int fr_additive_pool_rows(int T, int D, int Q, int is_bf16) { return upool_ok(T, D, Q, is_bf16) ? US : 1; }
+
 extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g,
                                     float* dx, void* dpre, float* dw2, float* db2, float* dsum, int n, int T, int D,
                                     int Q, int R, int is_bf16, hipStream_t s) {
-  if (T > MAXT_G || R != n) return 1;
+  if (T > MAXT_G) return 1;
   if (n == 0) return -1;
+  if (upool_ok(T, D, Q, is_bf16)) {
+    if (R != n * US) return 1;
+    const uintptr_t al = (uintptr_t)x | (uintptr_t)e | (uintptr_t)w2 | (uintptr_t)g | (uintptr_t)dpre |
+                         (uintptr_t)(dx ? dx : g);
+    if (al & 15) return 3;  // 16-byte rows (fresh tensors and 256-B aligned parameter views)
+    hipLaunchKernelGGL(upool_bwd_kernel, dim3(n, US), dim3(256), 0, s, (const float*)x, (const float*)e, alpha, w2, g, dx,
+                       (float*)dpre, dw2, db2, T, D, Q);
+    return -1;
+  }
+  if (R != n) return 1;
   if (is_bf16 && T <= MAXT && dx == nullptr && D % 8 == 0 && Q % 8 == 0 && D <= 1024 && Q <= 512 && Q >= 256) {
     hipLaunchKernelGGL(pool_bwd16_kernel, dim3(n), dim3(256), 0, s, (const bf16*)x, (const bf16*)e, alpha, w2, g,
                        (bf16*)dpre, dw2, db2, dsum, T, D, Q, R);

@@ -35,7 +35,8 @@ int fr_embed_ln_bf16(const int* tokens, const void* word, const void* pos, const
 int fr_title_attention_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
                             hipStream_t s);
 int fr_additive_pool_fwd(const void* x, const void* e, const float* w2, const float* b2, float* out, float* alpha,
-                         int n, int T, int D, int Q, int is_bf16, hipStream_t s);
+                         int n, int T, int D, int Q, int is_bf16, const int* keep, hipStream_t s);
+int fr_additive_pool_rows(int T, int D, int Q, int is_bf16);
 int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const float* w2, const float* g, float* dx,
                          void* dpre, float* dw2, float* db2, float* dsum, int n, int T, int D, int Q, int R,
                          int is_bf16, hipStream_t s);
@@ -57,9 +58,10 @@ int fr_ipc_allreduce(int id, void* x, long n, int is_int, long long epoch, int m
 int fr_ipc_destroy(int id);
 int fr_ipc_allreduce_local(const int* ids, void* const* xs, int W, long n, int is_int, long long epoch, int mode,
                            int blocks, hipStream_t s);
-int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, hipStream_t s);
+int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, const int* keep,
+                     hipStream_t s);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
-                     int dk, hipStream_t s);
+                     int dk, const int* keep, hipStream_t s);
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
                 int C, int D, int sigm, hipStream_t s);
 int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U, int D,
@@ -360,8 +362,17 @@ at::Tensor title_attention(const at::Tensor& qkv, const at::Tensor& mask, int64_
   return out;
 }
 
+// keep: optional [B, H] int32 mask (nonzero = attend / pool), the mask_padding option
+const int* key_mask_ptr(const c10::optional<at::Tensor>& keep, int64_t B, int64_t H, const char* what) {
+  if (!keep.has_value() || !keep->defined()) return nullptr;
+  check_dev(*keep, "keep");
+  TORCH_CHECK(keep->scalar_type() == at::kInt && keep->is_contiguous() && keep->numel() == B * H, "fedrec::", what,
+              ": keep int32 [B, H]");
+  return keep->data_ptr<int>();
+}
+
 std::tuple<at::Tensor, at::Tensor> additive_pool_fwd(const at::Tensor& x, const at::Tensor& e, const at::Tensor& w2,
-                                                     const at::Tensor& b2) {
+                                                     const at::Tensor& b2, const c10::optional<at::Tensor>& keep) {
   check_dev(x, "x");
   check_dev(e, "e");
   TORCH_CHECK(x.dim() == 3 && e.dim() == 3 && x.scalar_type() == e.scalar_type(), "fedrec::additive_pool_fwd");
@@ -373,7 +384,7 @@ std::tuple<at::Tensor, at::Tensor> additive_pool_fwd(const at::Tensor& x, const 
   auto alpha = at::empty({n, T}, x.options().dtype(at::kFloat));
   check_rc(fr_additive_pool_fwd(x.data_ptr(), e.data_ptr(), w2.data_ptr<float>(), b2.data_ptr<float>(),
                                 out.data_ptr<float>(), alpha.data_ptr<float>(), (int)n, (int)T, (int)D, (int)Q, bf,
-                                cur_stream()),
+                                key_mask_ptr(keep, n, T, "additive_pool_fwd"), cur_stream()),
            "additive_pool_fwd");
   return {out, alpha};
 }
@@ -570,7 +581,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor dx = want_dx ? at::empty({n, T, D}, fopt) : at::empty({0}, fopt);
   auto dpre = at::empty({n, T, Q}, e.options());
-  const int64_t R = std::max<int64_t>(1, n);  // one partial row per block (no float atomics)
+  // partial rows, one per block (no float atomics)
+  const int64_t R = std::max<int64_t>(1, n * fr_additive_pool_rows((int)T, (int)D, (int)Q, bf ? 1 : 0));
   auto red = at::empty({2 * R * Q + R}, fopt);  // [dw2 rows | dpre col-sum rows | db2 rows]
   float* dw2p = red.data_ptr<float>();
   float* dsump = dw2p + R * Q;
@@ -584,7 +596,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_
   auto sums = at::empty({2 * Q + 1}, fopt);
   const float* xs[3] = {dw2p, db2p, dsump};
   float* os[3] = {sums.data_ptr<float>(), sums.data_ptr<float>() + Q, sums.data_ptr<float>() + Q + 1};
-  const int ints[12] = {(int)n, (int)Q, (int)Q, 0, (int)n, 1, 1, 0, (int)n, (int)Q, (int)Q, 0};
+  const int ints[12] = {(int)R, (int)Q, (int)Q, 0, (int)R, 1, 1, 0, (int)R, (int)Q, (int)Q, 0};
   const int ncs = rc == 0 ? 3 : 2;
   const long need = fr_colsum_f32(xs, os, ints, ncs, nullptr, cur_stream());
   auto part = at::empty({std::max<long>(need, 1)}, fopt);
@@ -596,7 +608,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_
   return {dx, dpre, dw2, db2, dsum};
 }
 
-std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int64_t heads, int64_t head_dim) {
+std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int64_t heads, int64_t head_dim,
+                                                      const c10::optional<at::Tensor>& keep) {
   check_dev(qkv, "qkv");
   TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.dim() == 3, "fedrec::user_attention_fwd: fp32 [B,H,3D]");
   const c10::DeviceGuard g(qkv.device());
@@ -605,13 +618,13 @@ std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int
   auto ctx = at::empty({B, H, heads * head_dim}, qkv.options());
   auto stats = at::empty({B, heads, H, 2}, qkv.options());
   check_rc(fr_user_attn_fwd(qkv.data_ptr<float>(), ctx.data_ptr<float>(), stats.data_ptr<float>(), (int)B, (int)H,
-                            (int)heads, (int)head_dim, cur_stream()),
+                            (int)heads, (int)head_dim, key_mask_ptr(keep, B, H, "user_attention_fwd"), cur_stream()),
            "user_attention_fwd");
   return {ctx, stats};
 }
 
 at::Tensor user_attention_bwd(const at::Tensor& qkv, const at::Tensor& stats, const at::Tensor& dctx, int64_t heads,
-                              int64_t head_dim) {
+                              int64_t head_dim, const c10::optional<at::Tensor>& keep) {
   check_dev(qkv, "qkv");
   check_dev(stats, "stats");
   check_dev(dctx, "dctx");
@@ -620,7 +633,8 @@ at::Tensor user_attention_bwd(const at::Tensor& qkv, const at::Tensor& stats, co
   auto d = dctx.to(at::kFloat).contiguous();
   auto dqkv = at::empty_like(qkv);
   check_rc(fr_user_attn_bwd(qkv.data_ptr<float>(), stats.data_ptr<float>(), d.data_ptr<float>(), dqkv.data_ptr<float>(),
-                            (int)B, (int)H, (int)heads, (int)head_dim, cur_stream()),
+                            (int)B, (int)H, (int)heads, (int)head_dim, key_mask_ptr(keep, B, H, "user_attention_bwd"),
+                            cur_stream()),
            "user_attention_bwd");
   return dqkv;
 }
@@ -1358,10 +1372,10 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens) -> (Tensor, Tensor)");
   m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g) -> (Tensor, Tensor)");
   m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2) -> (Tensor, Tensor)");
+  m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep=None) -> (Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
-  m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim) -> (Tensor, Tensor)");
-  m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim) -> Tensor");
+  m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None) -> (Tensor, Tensor)");
+  m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");

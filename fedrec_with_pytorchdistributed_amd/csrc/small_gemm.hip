@@ -51,6 +51,7 @@ struct GemmDesc {
   float alpha, pdrop;
   int drop_ld, drop_on, gather_on, tiles_n, tile_base, splits, kchunk, kseg;
   int a_bf16, b_bf16;
+  int red_base;  // first block of this desc's split-K reduction
   unsigned long long seed, offset;  // offset += *dev_off when dev_off is set (graph replays)
 };
 
@@ -411,42 +412,72 @@ __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch b
 }
 
 // split-K epilogue: C = act(alpha * sum_s P[s] + bias) (x the output dropout scale, drop_on 3)
-// (+ C), partials summed in split order (deterministic) -- the single-pass epilogue's order
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batch, int total) {
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
-    int gi = 0, base = 0;
-    for (int i = 0; i < batch.n; ++i) {
-      const GemmDesc& d = batch.d[i];
-      const int sz = d.splits > 1 ? d.M * d.N : 0;
-      if (e < base + sz) { gi = i; break; }
-      base += sz;
-    }
-    const GemmDesc& g = batch.d[gi];
-    const int idx = e - base, m = idx / g.N, n = idx - m * g.N;
-    float s = 0.f;
-    for (int sp = 0; sp < g.splits; ++sp) s += g.P[(size_t)sp * g.M * g.N + idx];
-    float* c = g.C + (size_t)m * g.ldc + n;
-    float v = g.alpha * s + (g.bias ? g.bias[n] : 0.f);
-    if (g.act == 1) v = tanhf(v);
-    if (g.drop_on == 3) {  // as the single-pass epilogue: element (m, n) of the dropped input
-      const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
-      const unsigned long long el = (unsigned long long)m * g.drop_ld + n;
-      const uint4 x = Philox::gen(g.seed, off, el >> 2);
-      v *= drop_scale(u4_get(x, (int)(el & 3)), g.pdrop, 1.0f / (1.0f - g.pdrop));
-    }
-    *c = g.accumulate ? *c + v : v;
+// (+ C), partials summed in split order (deterministic) -- the single-pass epilogue's order.
+// Each desc owns a block range (red_base); a lane takes 4 consecutive columns of one row: 16-B
+// partial loads, one Philox draw for the 4 dropout scales (drop_ld % 16 == 0, n % 4 == 0).
+// N % 4 == 0 for every split desc (host-checked); C / bias / accumulate fall back to scalar
+// accesses when a row of C is not 16-byte aligned.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batch) {
+  int gi = 0;
+#pragma unroll
+  for (int i = 1; i < MAXG; ++i)
+    if (i < batch.n && batch.d[i].splits > 1 && (int)blockIdx.x >= batch.d[i].red_base) gi = i;
+  const GemmDesc& g = batch.d[gi];
+  if (g.splits <= 1) return;
+  const long q = (long)(blockIdx.x - g.red_base) * 256 + threadIdx.x;
+  const long MN = (long)g.M * g.N;
+  const long e = 4 * q;
+  if (e >= MN) return;
+  const int m = (int)(e / g.N), n = (int)(e - (long)m * g.N);
+  float4 sum = *(const float4*)(g.P + e);
+  for (int sp = 1; sp < g.splits; ++sp) {
+    const float4 t = *(const float4*)(g.P + (size_t)sp * MN + e);
+    sum.x += t.x; sum.y += t.y; sum.z += t.z; sum.w += t.w;
   }
+  float v[4] = {sum.x, sum.y, sum.z, sum.w};
+  float sc[4] = {1.f, 1.f, 1.f, 1.f};
+  if (g.drop_on == 3) {  // as the single-pass epilogue: elements (m, n..n+3) of the dropped input
+    const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+    const uint4 x = Philox::gen(g.seed, off, ((unsigned long long)m * g.drop_ld + n) >> 2);
+    const float inv_keep = 1.0f / (1.0f - g.pdrop);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sc[r] = drop_scale(u4_get(x, r), g.pdrop, inv_keep);
+  }
+  float* c = g.C + (size_t)m * g.ldc + n;
+  const bool vec = ((uintptr_t)c & 15) == 0;
+  float cv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.accumulate) {
+    if (vec) {
+      const float4 t = *(const float4*)c;
+      cv[0] = t.x; cv[1] = t.y; cv[2] = t.z; cv[3] = t.w;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cv[r] = c[r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float x = g.alpha * v[r] + (g.bias ? g.bias[n + r] : 0.f);
+    if (g.act == 1) x = tanhf(x);
+    x *= sc[r];
+    v[r] = g.accumulate ? cv[r] + x : x;
+  }
+  if (vec)
+    *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
+  else
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = v[r];
 }
 
 // Deterministic fp32 column sums (bias gradients), two passes: (1) blocks of CS_ROWS rows x
 // (256 columns as float4 per lane when the matrix allows 16-byte loads, else 64 columns)
 // write per-chunk partials, 4 waves x CS_ROWS/4 rows each, 8 row loads in flight per lane;
-// (2) the partials are summed in chunk order.  A desc of one row chunk (the loss sum, the
+// (2) the partials are summed in a fixed order, 4 waves per 64 columns.  A desc of one row chunk (the loss sum, the
 // pooled-user partial rows) is final after pass 1, and a launch of only such descs skips
 // pass 2.  (A single-pass "last block sums" form with agent-scope fences measured 131 us/step
 // vs 69: each release fence writes back L2.  The scalar form -- one float per lane, 128 rows
 // per block -- took 32 us for the user step's 18 MB of gradients.)
-constexpr int CS_ROWS = 64;
+constexpr int CS_ROWS = 128;
 struct ColsumDesc {
   const float* X;
   float* out;
@@ -508,17 +539,28 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const ColsumBatch batc
   }
 }
 
-__global__ __launch_bounds__(64) void colsum_final_kernel(const ColsumBatch batch) {
+// pass 2: 64 columns per block, wave w sums chunks w, w + 4, ... (independent loads in flight),
+// wave 0 adds the four wave sums in order (deterministic)
+__global__ __launch_bounds__(256) void colsum_final_kernel(const ColsumBatch batch) {
+  __shared__ float ws[4][64];
   int gi = 0;
 #pragma unroll
   for (int i = 1; i < MAXG; ++i)
     if (i < batch.n && (int)blockIdx.x >= batch.d[i].block2_base) gi = i;
   const ColsumDesc& g = batch.d[gi];
-  const int c = (blockIdx.x - g.block2_base) * 64 + threadIdx.x;
-  if (c >= g.N || g.chunks == 1) return;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blockIdx.x - g.block2_base) * 64 + l;
+  if (g.chunks == 1) return;  // block-uniform
   float s = 0.f;
-  for (int ch = 0; ch < g.chunks; ++ch) s += g.part[(size_t)ch * g.N + c];
-  g.out[c] = g.accumulate ? g.out[c] + s : s;
+  if (c < g.N)
+#pragma unroll 4
+    for (int ch = w; ch < g.chunks; ch += 4) s += g.part[(size_t)ch * g.N + c];
+  ws[w][l] = s;
+  __syncthreads();
+  if (w == 0 && c < g.N) {
+    const float t = (ws[0][l] + ws[1][l]) + (ws[2][l] + ws[3][l]);
+    g.out[c] = g.accumulate ? g.out[c] + t : t;
+  }
 }
 
 }  // namespace
@@ -625,7 +667,7 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   tile_dims(v, tm, tn);
   int tiles = 0;
   long need = 0;
-  int red_total = 0;
+  int red_blocks = 0;
   for (int i = 0; i < n; ++i) {
     GemmDesc& d = b.d[i];
     d.tiles_n = (d.N + tn - 1) / tn;
@@ -634,11 +676,16 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     d.splits = choose_splits(t, d.K);
     d.kchunk = d.splits > 1 ? ((d.K + d.splits - 1) / d.splits + TK - 1) / TK * TK : d.K;
     if (d.splits > 1) d.splits = (d.K + d.kchunk - 1) / d.kchunk;
+    if (d.splits > 1 && d.N % 4 != 0) {  // the reduction takes 4 columns per lane
+      d.splits = 1;
+      d.kchunk = d.K;
+    }
     d.P = nullptr;
+    d.red_base = red_blocks;
     if (d.splits > 1) {
       d.P = scratch ? scratch + need : nullptr;
       need += (long)d.splits * d.M * d.N;
-      red_total += d.M * d.N;
+      red_blocks += (int)(((long)d.M * d.N / 4 + 255) / 256);
     }
     d.tile_base = tiles;
     tiles += t * d.splits;
@@ -668,10 +715,7 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     default: SG_LAUNCH(2, 2); break;
   }
 #undef SG_LAUNCH
-  if (red_total > 0) {
-    const int blocks = min(2048, (red_total + 255) / 256);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, b, red_total);
-  }
+  if (red_blocks > 0) hipLaunchKernelGGL(splitk_reduce_kernel, dim3(red_blocks), dim3(256), 0, s, b);
   return 0;
 }
 
@@ -706,7 +750,7 @@ extern "C" long fr_colsum_f32(const float* const* xs, float* const* outs, const 
   hipLaunchKernelGGL(colsum_part_kernel, dim3(blocks), dim3(256), 0, s, b);
   bool second = false;  // descs of one row chunk are final after the first pass
   for (int i = 0; i < n; ++i) second |= b.d[i].chunks > 1;
-  if (second) hipLaunchKernelGGL(colsum_final_kernel, dim3(blocks2), dim3(64), 0, s, b);
+  if (second) hipLaunchKernelGGL(colsum_final_kernel, dim3(blocks2), dim3(256), 0, s, b);
   return 0;
 }
 

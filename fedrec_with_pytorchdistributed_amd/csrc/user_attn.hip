@@ -571,9 +571,16 @@ __global__ __launch_bounds__(64) void user_attn_bwd_mfma_kernel(const float* __r
 // then (after one barrier, P and dS complete in LDS) key tile w -- dK and dV of its keys.  A wave
 // has a quarter of the one-wave form's serial MFMA / softmax work and the CU 4x the waves to
 // hide the staging latency.
+// keep (optional, [B, H] int32): key t of impression b takes part iff keep[b H + t] != 0 (the
+// mask_padding option's key mask, attention.py:76-78: masked keys get weight exactly 0; a row
+// with every key masked gives ctx = 0, as the torch oracle's eps-softmax)
+__device__ __forceinline__ bool key_kept(const int* __restrict__ keep, int b, int H, int t) {
+  return keep == nullptr || keep[(size_t)b * H + t] != 0;
+}
+
 __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   float* __restrict__ ctx, float* __restrict__ stats,
-                                                                  int H, int NH) {
+                                                                  int H, int NH, const int* __restrict__ keep) {
   __shared__ __attribute__((aligned(16))) float qs[65][DK];
   __shared__ __attribute__((aligned(16))) float ks[65][DK];
   __shared__ __attribute__((aligned(16))) float vs[65][DK];
@@ -609,6 +616,9 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
   const int i0 = wave * 16;
   if (i0 >= H) return;  // wave-uniform; no barrier follows
   const int NT = (H + 15) / 16;
+  bool kept[4];  // this lane's key columns j * 16 + fr
+#pragma unroll
+  for (int j = 0; j < 4; ++j) kept[j] = j * 16 + fr < H && key_kept(keep, b, H, min(j * 16 + fr, H - 1));
   f32x4 s[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -627,11 +637,12 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
     float m = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float v = (j < NT && j * 16 + fr < H) ? s[j][r] * scale : -INFINITY;
+      const float v = (j < NT && kept[j]) ? s[j][r] * scale : -INFINITY;
       s[j][r] = v;
       m = fmaxf(m, v);
     }
     m = row16_max(m);
+    if (m == -INFINITY) m = 0.f;  // every key masked: weights 0, ctx 0
     float l = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -672,7 +683,8 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
 __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   const float* __restrict__ stats,
                                                                   const float* __restrict__ dctx,
-                                                                  float* __restrict__ dqkv, int H, int NH) {
+                                                                  float* __restrict__ dqkv, int H, int NH,
+                                                                  const int* __restrict__ keep) {
   __shared__ __attribute__((aligned(16))) float qs[65][DK];
   __shared__ __attribute__((aligned(16))) float ks[65][DK];
   __shared__ __attribute__((aligned(16))) float vs[65][DK];
@@ -724,6 +736,9 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   float* dst = dqkv + (size_t)b * H * ld + h * DK;
   const int KS = (H + 3) / 4;
   if (i0 < H) {  // query tile: P, dP, D, dS rows into LDS; dQ
+    bool kept[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kept[j] = j * 16 + fr < H && key_kept(keep, b, H, min(j * 16 + fr, H - 1));
     f32x4 p[4], dp[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) p[j] = dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -742,7 +757,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
       float Dt = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float pv = (j < NT && j * 16 + fr < H) ? __expf(p[j][r] * scale - mrow[r]) * inv[r] : 0.f;
+        const float pv = (j < NT && kept[j]) ? __expf(p[j][r] * scale - mrow[r]) * inv[r] : 0.f;
         p[j][r] = pv;
         Dt += pv * dp[j][r];
       }
@@ -835,7 +850,8 @@ __device__ __forceinline__ void load_row(float (&x)[DK], const float* __restrict
 }
 
 __global__ __launch_bounds__(64) void user_attn_fwd_long_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
-                                                                float* __restrict__ stats, int B, int H, int NH) {
+                                                                float* __restrict__ stats, int B, int H, int NH,
+                                                                const int* __restrict__ keep) {
   __shared__ __attribute__((aligned(16))) float ks[CH][DK];
   __shared__ __attribute__((aligned(16))) float vs[CH][DK];
   const int lane = threadIdx.x;
@@ -858,12 +874,16 @@ __global__ __launch_bounds__(64) void user_attn_fwd_long_kernel(const float* __r
       stage_rows(vs, base + 2 * D, ld, s0, n, lane);
       __syncthreads();
       float mc = m;
-      for (int s = 0; s < n; ++s) mc = fmaxf(mc, dot20(q, &ks[s][0]));
-      const float alpha = __expf(m - mc);  // 0 on the first chunk (m = -inf)
+      for (int s = 0; s < n; ++s)
+        if (key_kept(keep, b, H, s0 + s)) mc = fmaxf(mc, dot20(q, &ks[s][0]));
+      // 0 on the first chunk with a kept key (m = -inf); a chunk before any kept key leaves
+      // l = acc = 0, whatever the factor
+      const float alpha = mc == -INFINITY ? 0.f : __expf(m - mc);
       l *= alpha;
 #pragma unroll
       for (int c = 0; c < DK; ++c) acc[c] *= alpha;
       for (int s = 0; s < n; ++s) {
+        if (!key_kept(keep, b, H, s0 + s)) continue;  // key index: the same for every lane
         const float p = __expf(dot20(q, &ks[s][0]) - mc);
         l += p;
         axpy20(acc, p, &vs[s][0]);
@@ -871,6 +891,7 @@ __global__ __launch_bounds__(64) void user_attn_fwd_long_kernel(const float* __r
       m = mc;
     }
     if (!valid) continue;
+    if (m == -INFINITY) m = 0.f;  // every key masked: weights 0, ctx 0
     l += 1e-8f * __expf(-m);
     const float inv = 1.0f / l;
     float* o = ctx + ((size_t)b * H + t) * D + h * DK;
@@ -887,7 +908,8 @@ __global__ __launch_bounds__(64) void user_attn_fwd_long_kernel(const float* __r
 __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __restrict__ qkv,
                                                                 const float* __restrict__ stats,
                                                                 const float* __restrict__ dctx,
-                                                                float* __restrict__ dqkv, int B, int H, int NH) {
+                                                                float* __restrict__ dqkv, int B, int H, int NH,
+                                                                const int* __restrict__ keep) {
   __shared__ __attribute__((aligned(16))) float xs[CH][DK];  // keys (pass A) / queries (pass B)
   __shared__ __attribute__((aligned(16))) float ys[CH][DK];  // values (pass A) / dctx rows (pass B)
   __shared__ float ms[MAXL], is_[MAXL], Ds[MAXL];
@@ -923,6 +945,7 @@ __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __r
       stage_rows(ys, base + 2 * D, ld, s0, n, lane);
       __syncthreads();
       for (int s = 0; s < n; ++s) {
+        if (!key_kept(keep, b, H, s0 + s)) continue;
         const float A = __expf(dot20(q, &xs[s][0]) - m) * inv;
         const float dA = dot20(g, &ys[s][0]);
         Dt += A * dA;
@@ -948,6 +971,7 @@ __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __r
     float k[DK], v[DK], dk[DK], dv[DK];
     load_row(k, base + (size_t)sc * ld + D, scale);
     load_row(v, base + (size_t)sc * ld + 2 * D, 1.f);
+    const float kf = key_kept(keep, b, H, sc) ? 1.f : 0.f;  // a masked key gets no gradient
 #pragma unroll
     for (int c = 0; c < DK; ++c) dk[c] = dv[c] = 0.f;
     for (int t0 = 0; t0 < H; t0 += CH) {
@@ -958,7 +982,7 @@ __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __r
       __syncthreads();
       for (int j = 0; j < n; ++j) {
         const int t = t0 + j;
-        const float A = __expf(dot20(k, &xs[j][0]) - ms[t]) * is_[t];
+        const float A = kf * __expf(dot20(k, &xs[j][0]) - ms[t]) * is_[t];
         const float dA = dot20(v, &ys[j][0]);
         const float dS = A * (dA - Ds[t]) * scale;
         axpy20(dk, dS, &xs[j][0]);
@@ -980,18 +1004,20 @@ __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __r
 
 extern "C" void fr_user_attn_set_variant(int v) { g_ua_variant = v; }
 
+// keep: optional [B, H] int32 key mask (mask_padding); the default four-wave and the long
+// kernels take it, the diagnostic variants do not (a masked call always runs one of those two)
 extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk,
-                                hipStream_t s) {
+                                const int* keep, hipStream_t s) {
   if (dk != DK || H > MAXL || H < 1) return 1;
   const int pairs = B * NH;
   if (pairs == 0) return 0;
   if (H > MAXH)
-    hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH);
+    hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH, keep);
+  else if (keep != nullptr || g_ua_variant == 3)
+    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
   else if (g_ua_variant >= 10) {  // diagnostic partial forwards (timing only): 10 staging, 11 + S/softmax
     if (g_ua_variant == 10) hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 1>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
     else hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 2>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
-  } else if (g_ua_variant == 3) {
-    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH);
   } else if (g_ua_variant == 2) {
     const int nt = (H + 15) / 16;
     if (nt == 1) hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<1>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
@@ -1006,14 +1032,14 @@ extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int 
 }
 
 extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H,
-                                int NH, int dk, hipStream_t s) {
+                                int NH, int dk, const int* keep, hipStream_t s) {
   if (dk != DK || H > MAXL || H < 1) return 1;
   const int pairs = B * NH;
   if (pairs == 0) return 0;
   if (H > MAXH)
-    hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
-  else if (g_ua_variant == 3)
-    hipLaunchKernelGGL(user_attn_bwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH);
+    hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH, keep);
+  else if (keep != nullptr || g_ua_variant == 3)
+    hipLaunchKernelGGL(user_attn_bwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH, keep);
   else if (g_ua_variant == 2) {
     const int nt = (H + 15) / 16;
 #define UA_BWD(N) \

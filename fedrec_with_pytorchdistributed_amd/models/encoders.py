@@ -25,7 +25,8 @@ from .backbone import Backbone
 
 
 class AdditiveAttention(nn.Module):
-    """``attention.py:8-26``; the pooling has no padding mask (Q7)."""
+    """``attention.py:8-26``; the reference pools without a padding mask (Q7), ``keep`` is the
+    mask_padding option."""
 
     def __init__(self, d_h: int, hidden_size: int = 200):
         super().__init__()
@@ -33,13 +34,12 @@ class AdditiveAttention(nn.Module):
         self.att_fc2 = nn.Linear(hidden_size, 1)
 
     def forward(self, x: torch.Tensor, keep: torch.Tensor | None = None) -> torch.Tensor:
-        if keep is not None:  # mask_padding (Q7 option)
-            return OF.masked_additive_pool(x, self.att_fc1, self.att_fc2, keep)
-        return OF.additive_pool(x, self.att_fc1, self.att_fc2)
+        return OF.additive_pool(x, self.att_fc1, self.att_fc2, keep)  # keep: mask_padding (Q7 option)
 
 
 class MultiHeadAttention(nn.Module):
-    """``attention.py:50-82`` (no output projection, no mask)."""
+    """``attention.py:50-82`` (no output projection; the reference passes no mask, ``keep`` is
+    the mask_padding option)."""
 
     def __init__(self, d_model: int, n_heads: int, d_k: int, d_v: int):
         super().__init__()
@@ -54,10 +54,13 @@ class MultiHeadAttention(nn.Module):
     def forward(self, x: torch.Tensor, keep: torch.Tensor | None = None) -> torch.Tensor:
         w = torch.cat([self.W_Q.weight, self.W_K.weight, self.W_V.weight], 0)
         b = torch.cat([self.W_Q.bias, self.W_K.bias, self.W_V.bias], 0)
-        qkv = F.linear(x, w, b)  # one [B*H, 400] x [400, 1200] GEMM
-        if keep is not None:  # mask_padding (Q7 option): attention.py:76-78 key mask
-            return OF.masked_user_attention(qkv, self.n_heads, self.d_k, keep)
-        return OF.user_attention(qkv, self.n_heads, self.d_k)
+        if x.is_cuda:  # one [B*H, 400] x [400, 1200] GEMM on the small MFMA kernel
+            B, H, D = x.shape
+            qkv = OF.HeadFCFn.apply(x.reshape(B * H, D).float(), w, b).view(B, H, -1)
+        else:
+            qkv = F.linear(x, w, b)
+        # keep: mask_padding (Q7 option), the attention.py:76-78 key mask
+        return OF.user_attention(qkv, self.n_heads, self.d_k, keep)
 
 
 class UserEncoder(nn.Module):
@@ -73,8 +76,12 @@ class UserEncoder(nn.Module):
         """``clicked [B,H,400]``; ``his_ids [B,H]`` (0 = padding) masks the padded history
         slots when ``mask_padding`` is on (the reference attends over them: Q7)."""
         keep = (his_ids != 0) if (self.mask_padding and his_ids is not None) else None
-        x = F.dropout(clicked, p=self.dropout_rate, training=self.training)
-        y = self.multihead_attention(x, keep)
+        mha = self.multihead_attention
+        if clicked.is_cuda and mha.n_heads * mha.d_k == clicked.shape[-1]:
+            # the training step's kernels (Philox input dropout, small GEMMs, MHSA, pool)
+            return OF.user_encoder_device(self, clicked, keep)
+        x = F.dropout(clicked, p=self.dropout_rate, training=self.training)  # host path
+        y = mha(x, keep)
         return self.additive_attention(y, keep)
 
 

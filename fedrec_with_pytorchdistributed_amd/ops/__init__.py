@@ -60,14 +60,6 @@ def linear(x, w, b=None, act: str = "none", residual=None, out_dtype=None):
     return y.to(out_dtype or x.dtype)
 
 
-def linear_lib(x, w, b=None, act: str = "none"):
-    """fp32 ``act(x @ w^T + b)`` through the vendor GEMM (hipBLASLt on the device).  Used by
-    the user encoder's additive-attention projection, which runs in fp32 like the reference
-    (its [B*H, 400] x [400, 200] shape is below the bf16 MFMA kernel's N % 128 tiling)."""
-    y = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
-    return torch.tanh(y) if act == "tanh" else (torch.nn.functional.gelu(y) if act == "gelu" else y)
-
-
 def layer_norm(x, w, b, eps: float, dtype=None, residual=None):
     """``LN(x [+ residual]) * w + b`` (the residual add is fused into the LN kernel)."""
     if _dev(x):
@@ -140,13 +132,18 @@ def layer_norm_scatter(x, w, b, eps: float, residual, dst):
     return native.require_for(x).layer_norm_scatter(x, w, b, float(eps), residual, dst)
 
 
-def additive_pool_fwd(x, e, w2, b2) -> Tuple[torch.Tensor, torch.Tensor]:
-    """-> ``(pooled fp32 [n,D], alpha fp32 [n,T])``."""
+def additive_pool_fwd(x, e, w2, b2, keep=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """-> ``(pooled fp32 [n,D], alpha fp32 [n,T])``; ``keep [n,T]`` int (nonzero = pooled):
+    the mask_padding position mask."""
     if _dev(x):
         return tuple(native.require_for(x).additive_pool_fwd(x.contiguous(), e.contiguous(),
                                                              w2.reshape(-1).float().contiguous(),
-                                                             b2.reshape(-1).float().contiguous()))
-    return ref.additive_pool_fwd(x, e, w2, b2)
+                                                             b2.reshape(-1).float().contiguous(), _mask32(keep)))
+    return ref.additive_pool_fwd(x, e, w2, b2, keep=keep)
+
+
+def _mask32(keep):
+    return None if keep is None else keep.to(torch.int32).contiguous()
 
 
 def additive_pool_bwd(x, e, alpha, w2, g, want_dx: bool, want_colsum: bool = False):
@@ -165,18 +162,19 @@ def additive_pool_bwd(x, e, alpha, w2, g, want_dx: bool, want_colsum: bool = Fal
     return out + (None,) if want_colsum else out
 
 
-def user_attention_fwd(qkv, heads: int, head_dim: int):
-    """-> ``(ctx [B,H,h*d], saved)``; ``saved`` is whatever the backward needs."""
+def user_attention_fwd(qkv, heads: int, head_dim: int, keep=None):
+    """-> ``(ctx [B,H,h*d], saved)``; ``saved`` is whatever the backward needs.  ``keep [B,H]``
+    int (nonzero = attend): the mask_padding key mask."""
     if _dev(qkv):
-        return tuple(native.require_for(qkv).user_attention_fwd(qkv.contiguous(), heads, head_dim))
-    return ref.user_attention_fwd(qkv, heads, head_dim)
+        return tuple(native.require_for(qkv).user_attention_fwd(qkv.contiguous(), heads, head_dim, _mask32(keep)))
+    return ref.user_attention_fwd(qkv, heads, head_dim, keep=keep)
 
 
-def user_attention_bwd(qkv, saved, dctx, heads: int, head_dim: int):
+def user_attention_bwd(qkv, saved, dctx, heads: int, head_dim: int, keep=None):
     if _dev(qkv):
         return native.require_for(qkv).user_attention_bwd(qkv.contiguous(), saved, dctx.contiguous(),
-                                                          heads, head_dim)
-    return ref.user_attention_bwd(qkv, saved, dctx, heads, head_dim)
+                                                          heads, head_dim, _mask32(keep))
+    return ref.user_attention_bwd(qkv, saved, dctx, heads, head_dim)  # the saved weights hold the mask
 
 
 def score_ce(cand, user, act: str = "sigmoid"):

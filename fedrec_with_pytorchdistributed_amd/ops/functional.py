@@ -81,20 +81,26 @@ class AdditivePoolFn(torch.autograd.Function):
     Forward: ``e = tanh(x W1^T + b1)`` (GEMM with a tanh epilogue), then the fused
     score / eps-softmax / weighted-sum kernel.  Backward: the fused kernel yields
     ``alpha g`` and ``dpre = da w2 (1 - e^2)``; ``dW1 = dpre^T x``, ``dx += dpre W1``.
+    Device GEMMs: the bf16 NT / TN kernels (text head of the unfrozen backbone) or the
+    small-GEMM kernel (fp32 inputs).  ``keep [n,T]`` (optional, nonzero = pooled): the
+    mask_padding position mask (masked positions get weight 0).
     """
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, keep=None):
         n, T, D = x.shape
         x2 = x.reshape(n * T, D)
         if x.dtype == torch.bfloat16:  # text head on the device: MFMA GEMM + tanh epilogue
             e = ops.linear(x2, w1.to(x.dtype), b1.float(), act="tanh")
-        elif x.is_cuda:  # user encoder (fp32): explicit vendor GEMM, see ops.linear_lib
-            e = ops.linear_lib(x2, w1, b1, act="tanh")
+        elif x.is_cuda:  # fp32 on the device: the small MFMA GEMM with a tanh epilogue
+            x2 = x2.float().contiguous()
+            Q = w1.shape[0]
+            e = torch.empty(n * T, Q, device=x.device, dtype=torch.float32)
+            ops.small_gemm(ops.Gemm(x2, w1.contiguous(), e, n * T, Q, D, D, D, Q, bias=b1.contiguous(), act=1))
         else:
             e = ops.linear(x2, w1, b1, act="tanh")
         e = e.reshape(n, T, -1)
-        pooled, alpha = ops.additive_pool_fwd(x, e, w2, b2)
+        pooled, alpha = ops.additive_pool_fwd(x, e, w2, b2, keep)
         ctx.save_for_backward(x, e, alpha, w1, w2)
         return pooled
 
@@ -107,18 +113,38 @@ class AdditivePoolFn(torch.autograd.Function):
         dpre2 = dpre.reshape(n * T, -1)
         x2 = x.reshape(n * T, D)
         dw1 = db1 = None
+        small = x2.is_cuda and x2.dtype == torch.float32  # fp32 device: the small MFMA GEMM
+        Q = w1.shape[0]
+        if small:
+            dpre2 = dpre2.contiguous()
+            x2 = x2.contiguous()
         if ctx.needs_input_grad[1]:
-            dw1 = wgrad(dpre2, x2)  # reduced over all n*T tokens (split-K on the device)
+            if small:
+                dw1 = torch.empty(Q, D, device=x.device, dtype=torch.float32)
+                ops.small_gemm(ops.Gemm(dpre2, x2, dw1, Q, D, n * T, Q, D, D, a_mode=1, b_mode=1))
+            else:
+                dw1 = wgrad(dpre2, x2)  # reduced over all n*T tokens (split-K on the device)
         if ctx.needs_input_grad[2]:
-            db1 = dsum if dsum is not None else bgrad(dpre2)
+            if dsum is not None:
+                db1 = dsum
+            elif small:
+                db1 = torch.empty(Q, device=x.device, dtype=torch.float32)
+                ops.colsum_f32([(dpre2, db1, n * T, Q, Q)])
+            else:
+                db1 = bgrad(dpre2)
         dx = None
         if want_dx:
-            if x2.is_cuda and x2.dtype == torch.bfloat16:
-                dxp = dgrad(dpre2.contiguous(), w1.to(torch.bfloat16))
+            if small:  # dx = alpha g + dpre W1, the GEMM accumulating onto the direct term
+                dx = dx_dir.float().contiguous()
+                ops.small_gemm(ops.Gemm(dpre2, w1.contiguous(), dx.view(n * T, D), n * T, D, Q, Q, D, D, b_mode=1,
+                                        accumulate=True))
             else:
-                dxp = _f(dpre2) @ _f(w1)
-            dx = (_f(dx_dir) + dxp.reshape(n, T, D)).to(x.dtype)
-        return dx, dw1, db1, dw2.reshape(1, -1).to(w2.dtype), db2.reshape(1).to(w2.dtype)
+                if x2.is_cuda and x2.dtype == torch.bfloat16:
+                    dxp = dgrad(dpre2.contiguous(), w1.to(torch.bfloat16))
+                else:
+                    dxp = _f(dpre2) @ _f(w1)
+                dx = (_f(dx_dir) + dxp.reshape(n, T, D)).to(x.dtype)
+        return dx, dw1, db1, dw2.reshape(1, -1).to(w2.dtype), db2.reshape(1).to(w2.dtype), None
 
 
 class TextHeadFn(torch.autograd.Function):
@@ -166,19 +192,20 @@ def fused_head_supported(table_dim: int, query_dim: int, title_len: int) -> bool
 
 
 class UserAttentionFn(torch.autograd.Function):
-    """``ScaledDotProductAttention`` over 20 heads x d_k 20 (``attention.py:32-82``)."""
+    """``ScaledDotProductAttention`` over 20 heads x d_k 20 (``attention.py:32-82``); ``keep
+    [B,H]`` (optional, nonzero = attend): the mask_padding key mask."""
 
     @staticmethod
-    def forward(ctx, qkv, heads: int, head_dim: int):
-        out, saved = ops.user_attention_fwd(qkv, heads, head_dim)
+    def forward(ctx, qkv, heads: int, head_dim: int, keep=None):
+        out, saved = ops.user_attention_fwd(qkv, heads, head_dim, keep)
         ctx.save_for_backward(qkv, saved)
-        ctx.heads, ctx.head_dim = heads, head_dim
+        ctx.heads, ctx.head_dim, ctx.keep = heads, head_dim, keep
         return out
 
     @staticmethod
     def backward(ctx, dctx):
         qkv, saved = ctx.saved_tensors
-        return ops.user_attention_bwd(qkv, saved, dctx, ctx.heads, ctx.head_dim), None, None
+        return ops.user_attention_bwd(qkv, saved, dctx, ctx.heads, ctx.head_dim, ctx.keep), None, None, None
 
 
 class ScoreCEFn(torch.autograd.Function):
@@ -222,44 +249,19 @@ class NewsGatherFn(torch.autograd.Function):
         return d, None, None, None, None, None, None, None, None
 
 
-def additive_pool(x, lin1: torch.nn.Linear, lin2: torch.nn.Linear):
-    return AdditivePoolFn.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+def additive_pool(x, lin1: torch.nn.Linear, lin2: torch.nn.Linear, keep=None):
+    return AdditivePoolFn.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias, keep)
 
 
-def user_attention(qkv, heads: int, head_dim: int):
-    return UserAttentionFn.apply(qkv, heads, head_dim)
+def user_attention(qkv, heads: int, head_dim: int, keep=None):
+    return UserAttentionFn.apply(qkv, heads, head_dim, keep)
 
 
-# ---------------------------------------------------------------------------------------
 # padding masks (config mask_padding): the reference passes mask=None everywhere,
 # but its AdditiveAttention / ScaledDotProductAttention take an optional mask that multiplies
-# exp(score) before the +1e-8 normalisation (attention.py:20-22, 40-42).  Opt-in, plain
-# autograd (not a hot path of any BASELINE config); stable form exp(a - m) with the 1e-8
-# term scaled by e^{-m}, exactly as the fused kernels treat the unmasked case.
-# ---------------------------------------------------------------------------------------
-def _masked_eps_softmax(a: torch.Tensor, keep: torch.Tensor, dim: int) -> torch.Tensor:
-    m = a.masked_fill(~keep, float("-inf")).amax(dim=dim, keepdim=True)
-    m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))  # all masked: every weight is 0
-    e = torch.exp(a - m) * keep
-    return e / (e.sum(dim=dim, keepdim=True) + 1e-8 * torch.exp(-m))
-
-
-def masked_additive_pool(x, lin1: torch.nn.Linear, lin2: torch.nn.Linear, keep: torch.Tensor):
-    """``x [n,T,D]``, ``keep [n,T]`` (bool) -> ``[n,D]`` fp32."""
-    xf = x.float()
-    e = torch.tanh(torch.nn.functional.linear(xf, lin1.weight, lin1.bias))
-    a = torch.nn.functional.linear(e, lin2.weight, lin2.bias).squeeze(-1)
-    alpha = _masked_eps_softmax(a, keep, dim=1)
-    return torch.einsum("nt,ntd->nd", alpha, xf)
-
-
-def masked_user_attention(qkv, heads: int, head_dim: int, keep: torch.Tensor):
-    """``qkv [B,H,3*h*d]``, key mask ``keep [B,H]`` -> ``ctx [B,H,h*d]``."""
-    B, H, _ = qkv.shape
-    q, k, v = qkv.float().view(B, H, 3, heads, head_dim).permute(2, 0, 3, 1, 4)
-    s = q @ k.transpose(-1, -2) / math.sqrt(head_dim)
-    A = _masked_eps_softmax(s, keep.view(B, 1, 1, H), dim=-1)
-    return (A @ v).permute(0, 2, 1, 3).reshape(B, H, heads * head_dim)
+# exp(score) before the +1e-8 normalisation (attention.py:20-22, 40-42).  Every pool /
+# attention above takes it as ``keep`` (kernels on the device, ops/reference.py on the host):
+# masked positions get weight exactly 0, a fully masked row gives 0.
 
 
 def score_ce(cand, user, act: str = "sigmoid") -> Tuple[torch.Tensor, torch.Tensor]:
@@ -541,49 +543,92 @@ class EmbedLNFn(torch.autograd.Function):
 # pool -> sigmoid-CE, and a hand-written backward.  Every GEMM is csrc/small_gemm.hip, every
 # bias gradient the deterministic colsum, the per-news reduction (+ LDP) the segment sum.
 # ---------------------------------------------------------------------------------------
+def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
+    """Device user encoder forward over history rows ``src[idx]`` (``src [*, D]`` fp32, ``idx``
+    int32 [B*H]) -> ``(u [B, D] fp32, saved)``.
+
+    The input dropout (``encoder.py:50``) is the Philox mask of element ``(b*H + t) * D + d`` of
+    the gathered history matrix with offset ``drop[2] + *dev_off``: X' = drop(src[idx]) is
+    materialised once in bf16 (``ops.gather_dropout``, 2.5 MB at config 2) and read by the
+    Q|K|V GEMM and the weight gradients; the dgrad regenerates the mask in its epilogue.  The
+    GEMM weights go through one bf16 stack [Wq; Wk; Wv; W1] (one cast launch; what the GEMMs'
+    fp32 loads rounded to).  ``keep [B, H]`` int32 (nonzero = real history slot, or None): the
+    mask_padding key mask of the attention and the pool (attention.py:76-78)."""
+    wq, bq, wk, bk, wv, bv, w1, b1, w2, b2 = wts
+    D = src.shape[1]
+    BH, D3, Qd = B * H, 3 * D, w1.shape[0]
+    dev = src.device
+    wb = torch.empty(D3 + Qd, D, device=dev, dtype=torch.bfloat16)
+    bqkv = torch.empty(D3, device=dev, dtype=torch.float32)
+    ops.native.require_for(src).multi_cast([wq, wk, wv, w1, bq, bk, bv],
+                                           [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D],
+                                            bqkv[2 * D:]])
+    p, seed, off = drop
+    xd = ops.gather_dropout(src, idx, p, seed, off, dev_off, bf16_out=True)
+    qkv = torch.empty(BH, D3, device=dev, dtype=torch.float32)
+    ops.small_gemm(ops.Gemm(xd, wb[:D3], qkv, BH, D3, D, D, D, D3, bias=bqkv))  # one N = 3D GEMM
+    q3 = qkv.view(B, H, D3)
+    c3, stats = ops.user_attention_fwd(q3, heads, hd, keep)
+    e = torch.empty(BH, Qd, device=dev, dtype=torch.float32)
+    ops.small_gemm(ops.Gemm(c3, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
+    e3 = e.view(B, H, Qd)
+    u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2, keep)
+    return u, [q3, stats, c3, e3, alpha, wb, w2, xd]
+
+
+def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
+    """Backward of :func:`_user_enc_fwd` for ``du [B, D]``: the input gradient goes into ``dx
+    [B*H, D]`` (the dropout backward in the dgrad epilogue) -> the ten weight gradients."""
+    q3, stats, c3, e3, alpha, wb, w2, xd = saved
+    D = c3.shape[-1]
+    BH, D3 = B * H, 3 * D
+    Qd = wb.shape[0] - D3
+    dev = c3.device
+    # additive pool backward: dx_direct = alpha du, dpre = da w2 (1 - e^2), dw2, db2
+    dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
+    dpre2 = dpre.view(BH, Qd)
+    ops.small_gemm(ops.Gemm(dpre2, wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
+    dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep).view(BH, D3)
+    p, seed, off = drop
+    # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,
+    # the dropout backward in its epilogue
+    ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
+    ops.small_gemm(ops.Gemm(dqkv, wb[:D3], dx, BH, D, D3, D3, D, D, b_mode=1, **ekw), dev_off=dev_off)
+    # weight gradients in one launch: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM; X'
+    # bf16) and dW1 = dpre^T ctx (fp32 operands: the mixed-dtype kernel)
+    gqkv = torch.empty(D3, D, device=dev)
+    gw1 = torch.empty(Qd, D, device=dev)
+    ops.small_gemm(ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1),
+                   ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1))
+    gbq, gbk, gbv = (torch.empty(D, device=dev) for _ in range(3))
+    gb1 = torch.empty(Qd, device=dev)
+    ops.colsum_f32([(dqkv[:, 0:D], gbq, BH, D, D3), (dqkv[:, D:2 * D], gbk, BH, D, D3),
+                    (dqkv[:, 2 * D:], gbv, BH, D, D3), (dpre2, gb1, BH, Qd, Qd)])
+    return gqkv[:D], gbq, gqkv[D:2 * D], gbk, gqkv[2 * D:], gbv, gw1, gb1, dw2.view(1, -1), db2.view(1)
+
+
 class UserStepFn(torch.autograd.Function):
-    """``loss, scores = UserStepFn(v, inv, perm, ptr, ...)`` for news vectors ``v [U, D]``.
+    """``loss, scores = UserStepFn(v, inv, perm, ptr, ...)`` for news vectors ``v [U, D]``: the
+    device user side of a training / validation step.
 
     ``inv [R]`` maps the batch's occurrences (``B*C`` candidates, then ``B*H`` history
-    slots) to rows of ``v``; ``perm / ptr`` group them per news for the segment sum.  The
-    input dropout of the user encoder (``encoder.py:50``) is the Philox mask of element
-    ``(b*H + t) * D + d`` of the gathered history matrix with offset ``drop[2] + *dev_off``:
-    the gathered, dropped-out input X' is materialised once (``ops.gather_dropout``, bf16, 2.5 MB),
-    read by the Q/K/V GEMMs and the weight gradients; the dgrad regenerates the mask in its
-    epilogue.  (Round 2 first applied the mask inside every GEMM tile's operand loads; each
-    of the ~21 column tiles redid its rows' Philox draws.)"""
+    slots) to rows of ``v``; ``perm / ptr`` group them per news for the segment sum (+ LDP).
+    The user encoder is :func:`_user_enc_fwd` / :func:`_user_enc_bwd`; ``meta[-1]`` is the
+    mask_padding key mask (the batch's history ids, int32 [B, H], or None).  (Round 2 first
+    applied the input-dropout mask inside every GEMM tile's operand loads; each of the ~21
+    column tiles redid its rows' Philox draws.)"""
 
     @staticmethod
     def forward(ctx, v, inv, perm, ptr, wq, bq, wk, bk, wv, bv, w1, b1, w2, b2, meta):
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded = meta
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep = meta
         D = v.shape[1]
-        BC, BH = B * C, B * H
-        Qd = w1.shape[0]
-        his_idx = inv[BC:]
+        BC = B * C
         ci = inv[:BC]
         cand = v.index_select(0, ci if ci.dtype in (torch.int32, torch.int64) else ci.long()).view(B, C, D)
-        D3 = 3 * D
-        qkv = torch.empty(BH, D3, device=v.device, dtype=torch.float32)
-        # the GEMMs' weight operands in bf16 ([Wq; Wk; Wv; W1], what their fp32 loads rounded
-        # to) and the concatenated Q|K|V bias, one cast launch per step
-        wb = torch.empty(D3 + Qd, D, device=v.device, dtype=torch.bfloat16)
-        bqkv = torch.empty(D3, device=v.device, dtype=torch.float32)
-        ops.native.require_for(v).multi_cast([wq, wk, wv, w1, bq, bk, bv],
-                                             [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D],
-                                              bqkv[2 * D:]])
-        p, seed, off = drop
-        # X' = drop(v[his]) once, in bf16 (2.5 MB): the Q|K|V projection and the weight
-        # gradients read it
-        xd = ops.gather_dropout(v, his_idx, p, seed, off, dev_off, bf16_out=True)
-        ops.small_gemm(ops.Gemm(xd, wb[:D3], qkv, BH, D3, D, D, D, D3, bias=bqkv))  # one N = 3D GEMM
-        q3 = qkv.view(B, H, D3)
-        c3, stats = ops.user_attention_fwd(q3, heads, hd)
-        e = torch.empty(BH, Qd, device=v.device, dtype=torch.float32)
-        ops.small_gemm(ops.Gemm(c3, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
-        e3 = e.view(B, H, Qd)
-        u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2)
+        u, saved = _user_enc_fwd(v, inv[BC:], (wq, bq, wk, bk, wv, bv, w1, b1, w2, b2), B, H, heads, hd, drop,
+                                 dev_off, keep)
         loss, scores, dcand, du = ops.score_ce(cand, u, act)
-        ctx.save_for_backward(v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wb, w2, xd)
+        ctx.save_for_backward(v, inv, perm, ptr, dcand, du, *saved)
         ctx.meta = meta
         ctx.mark_non_differentiable(scores)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the scores (one fill launch)
@@ -591,55 +636,83 @@ class UserStepFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss, gscores):
-        v, inv, perm, ptr, q3, stats, c3, e3, alpha, dcand, du, wb, w2, xd = ctx.saved_tensors
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded = ctx.meta
+        v, inv, perm, ptr, dcand, du, *saved = ctx.saved_tensors
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep = ctx.meta
         D = v.shape[1]
-        BC, BH = B * C, B * H
-        D3 = 3 * D
-        Qd = wb.shape[0] - D3
-        dev = v.device
-        R = inv.numel()
-        rows = torch.empty(R, D, device=dev, dtype=torch.float32)  # per-occurrence news gradients
+        BC = B * C
+        rows = torch.empty(inv.numel(), D, device=v.device, dtype=torch.float32)  # per-occurrence news gradients
         torch.mul(dcand.view(BC, D), gloss, out=rows[:BC])
-        du_g = du * gloss
-        # additive pool backward: dx_direct = alpha du, dpre = da w2 (1 - e^2), dw2, db2
-        dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du_g, True)
-        dpre2 = dpre.view(BH, Qd)
-        ops.small_gemm(ops.Gemm(dpre2, wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
-        dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd).view(BH, 3 * D)
-        p, seed, off = drop
-        his_idx = inv[BC:]
-        dx = rows[BC:]
-        # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,
-        # the dropout backward in its epilogue
-        ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
-        ops.small_gemm(ops.Gemm(dqkv, wb[:D3], dx, BH, D, D3, D3, D, D, b_mode=1, **ekw), dev_off=dev_off)
-        # weight gradients in one launch: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM;
-        # X' saved by the forward, bf16) and dW1 = dpre^T ctx (fp32 operands: the
-        # mixed-dtype kernel)
-        gqkv = torch.empty(D3, D, device=dev)
-        gq, gk, gv = gqkv[:D], gqkv[D:2 * D], gqkv[2 * D:]
-        gw1 = torch.empty(Qd, D, device=dev)
-        ops.small_gemm(ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1),
-                       ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1))
-        gbq, gbk, gbv = (torch.empty(D, device=dev) for _ in range(3))
-        gb1 = torch.empty(Qd, device=dev)
-        ops.colsum_f32([(dqkv[:, 0:D], gbq, BH, D, 3 * D), (dqkv[:, D:2 * D], gbk, BH, D, 3 * D),
-                        (dqkv[:, 2 * D:], gbv, BH, D, 3 * D), (dpre2, gb1, BH, Qd, Qd)])
+        grads = _user_enc_bwd(saved, du * gloss, rows[BC:], B, H, heads, hd, drop, dev_off, keep)
         clip, noise, lseed, loff = ldp
         # the noise offset's step part is the device counter (dev_off): graph replays draw fresh noise
         dv = ops.segment_sum_rows(rows, inv, v.shape[0], clip, noise, lseed, loff, seg=(perm, ptr), zero_empty=padded,
                                   dev_off=dev_off if noise > 0 else None)
-        return (dv, None, None, None, gq, gbq, gk, gbk, gv, gbv, gw1, gb1, dw2.view(1, -1), db2.view(1), None)
+        return (dv, None, None, None) + grads + (None,)
 
 
-def user_step(v, inv, perm, ptr, user_encoder, B: int, C: int, H: int, act: str, drop, dev_off, ldp, padded: bool):
-    """Device user side of a step (see :class:`UserStepFn`) -> ``(loss, scores)``."""
+def user_step(v, inv, perm, ptr, user_encoder, B: int, C: int, H: int, act: str, drop, dev_off, ldp, padded: bool,
+              keep=None):
+    """Device user side of a step (see :class:`UserStepFn`) -> ``(loss, scores)``.  ``keep``:
+    the mask_padding key mask (history ids [B, H], nonzero = real slot) or None."""
     mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
-    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded)
+    if keep is not None:
+        keep = keep.reshape(B, H)
+        keep = keep if keep.dtype == torch.int32 and keep.is_contiguous() else keep.to(torch.int32).contiguous()
+    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded, keep)
     return UserStepFn.apply(v, inv, perm, ptr, mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias,
                             mha.W_V.weight, mha.W_V.bias, pool.att_fc1.weight, pool.att_fc1.bias,
                             pool.att_fc2.weight, pool.att_fc2.bias, meta)
+
+
+_ARANGE: dict = {}
+
+
+class UserEncoderFn(torch.autograd.Function):
+    """The user encoder as a module call on the device (``encoder.py:36-56``: input dropout ->
+    MHSA -> additive pool): ``clicked [B, H, D] -> u [B, D]`` on the same kernels as the
+    training step (:func:`_user_enc_fwd` / :func:`_user_enc_bwd`), with autograd for the
+    clicked-news rows and the ten weights.  No vendor GEMM, no torch dropout."""
+
+    @staticmethod
+    def forward(ctx, clicked, wq, bq, wk, bk, wv, bv, w1, b1, w2, b2, meta):
+        heads, hd, drop, keep = meta
+        B, H, D = clicked.shape
+        key = (B * H, clicked.device)
+        if key not in _ARANGE:
+            _ARANGE[key] = torch.arange(B * H, device=clicked.device, dtype=torch.int32)
+        u, saved = _user_enc_fwd(clicked.reshape(B * H, D).float().contiguous(), _ARANGE[key],
+                                 (wq, bq, wk, bk, wv, bv, w1, b1, w2, b2), B, H, heads, hd, drop, None, keep)
+        ctx.save_for_backward(*saved)
+        ctx.meta = meta
+        ctx.shape = (B, H, D)
+        return u
+
+    @staticmethod
+    def backward(ctx, du):
+        heads, hd, drop, keep = ctx.meta
+        B, H, D = ctx.shape
+        dx = torch.empty(B * H, D, device=du.device, dtype=torch.float32)
+        grads = _user_enc_bwd(list(ctx.saved_tensors), du.float().contiguous(), dx, B, H, heads, hd, drop, None, keep)
+        return (dx.view(B, H, D),) + grads + (None,)
+
+
+_MODULE_DROP_STEP = [0]
+
+
+def user_encoder_device(user_encoder, clicked, keep=None):
+    """``UserEncoder.forward`` on the device (see :class:`UserEncoderFn`).  Train-mode input
+    dropout draws a Philox mask keyed by the module's seed and a per-call counter."""
+    mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
+    p = float(user_encoder.dropout_rate) if user_encoder.training else 0.0
+    drop = (p, 0x5EED0001, 0)
+    if p > 0:
+        _MODULE_DROP_STEP[0] += 1
+        drop = (p, 0x5EED0001, _MODULE_DROP_STEP[0])
+    if keep is not None:
+        keep = keep.to(torch.int32).contiguous()
+    return UserEncoderFn.apply(clicked, mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight,
+                               mha.W_V.bias, pool.att_fc1.weight, pool.att_fc1.bias, pool.att_fc2.weight,
+                               pool.att_fc2.bias, (mha.n_heads, mha.d_k, drop, keep))
 
 
 class HeadFCFn(torch.autograd.Function):

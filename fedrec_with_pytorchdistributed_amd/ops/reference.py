@@ -36,7 +36,17 @@ def _f(t: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------
 # eps-softmax helpers
 # ---------------------------------------------------------------------------------------
-def eps_softmax(s: torch.Tensor, dim: int, eps: float = EPS_SOFTMAX, literal: bool = False) -> torch.Tensor:
+def eps_softmax(s: torch.Tensor, dim: int, eps: float = EPS_SOFTMAX, literal: bool = False,
+                keep: torch.Tensor | None = None) -> torch.Tensor:
+    """``exp(s) / (sum exp(s) + eps)`` in the stable form.  ``keep`` (bool, broadcastable to
+    ``s``): masked entries get weight exactly 0; a slice with every entry masked is all 0
+    (max taken as 0) -- the kernels' mask_padding semantics."""
+    if keep is not None:
+        s = s.masked_fill(~keep, float("-inf"))
+        m = s.amax(dim, keepdim=True)
+        m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+        e = torch.exp(s - m)
+        return e / (e.sum(dim, keepdim=True) + eps * torch.exp(-m))
     if literal:
         e = torch.exp(s)
         return e / (e.sum(dim, keepdim=True) + eps)
@@ -185,10 +195,11 @@ def backbone_forward(tokens: torch.Tensor, mask: torch.Tensor, params: dict, n_l
 # additive attention pooling (text head and user encoder)
 # ---------------------------------------------------------------------------------------
 def additive_pool_fwd(x: torch.Tensor, e: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
-                      literal: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
-    """``x [n,T,D]``, ``e = tanh(W1 x + b1) [n,T,Q]`` -> ``(pooled [n,D], alpha [n,T])``."""
+                      literal: bool = False, keep: torch.Tensor | None = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``x [n,T,D]``, ``e = tanh(W1 x + b1) [n,T,Q]`` -> ``(pooled [n,D], alpha [n,T])``;
+    ``keep [n,T]`` (nonzero = pooled) masks positions (mask_padding)."""
     a = _f(e) @ _f(w2).reshape(-1) + _f(b2).reshape(())
-    alpha = eps_softmax(a, dim=1, literal=literal)
+    alpha = eps_softmax(a, dim=1, literal=literal, keep=None if keep is None else keep != 0)
     pooled = torch.einsum("nt,ntd->nd", alpha, _f(x))
     return pooled, alpha
 
@@ -214,12 +225,13 @@ def additive_pool_bwd(x: torch.Tensor, e: torch.Tensor, alpha: torch.Tensor, w2:
 # user-side multi-head attention (attention.py:32-82)
 # ---------------------------------------------------------------------------------------
 def user_attention_fwd(qkv: torch.Tensor, n_heads: int, head_dim: int,
-                       literal: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
-    """``qkv [B,H,3*h*d]`` -> ``(ctx [B,H,h*d], A [B,h,H,H])``."""
+                       literal: bool = False, keep: torch.Tensor | None = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``qkv [B,H,3*h*d]`` -> ``(ctx [B,H,h*d], A [B,h,H,H])``; ``keep [B,H]`` (nonzero =
+    attend) masks keys (mask_padding, attention.py:76-78)."""
     B, H, _ = qkv.shape
     q, k, v = _f(qkv).view(B, H, 3, n_heads, head_dim).permute(2, 0, 3, 1, 4)
     s = q @ k.transpose(-1, -2) / math.sqrt(head_dim)
-    A = eps_softmax(s, dim=-1, literal=literal)
+    A = eps_softmax(s, dim=-1, literal=literal, keep=None if keep is None else (keep != 0).view(B, 1, 1, H))
     ctx = (A @ v).permute(0, 2, 1, 3).reshape(B, H, n_heads * head_dim)
     return ctx, A
 

@@ -165,7 +165,7 @@ class LocalEngine:
         # and kernels end to end; the user-input dropout mask is Philox keyed by (seed, step),
         # the step being a device counter so HIP-graph replays draw fresh masks
         ue = model.user_encoder
-        self.fused_user = (device.type == "cuda" and not cfg.mask_padding
+        self.fused_user = (device.type == "cuda"
                            and ue.multihead_attention.n_heads * ue.multihead_attention.d_k == cfg.news_dim
                            and os.environ.get("FEDREC_FUSED_USER", "1") != "0")
         self.user_drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 2
@@ -350,8 +350,10 @@ class LocalEngine:
         his_v = rows[B * C:].view(B, H, -1)
         return uniq, v, cand_v, his_v
 
-    def _user_loss(self, v: torch.Tensor, dd, B: int, C: int, H: int, padded: bool, train: bool):
-        """Device user side (fused): ``(loss, scores)`` from news vectors ``v`` of the unique ids."""
+    def _user_loss(self, v: torch.Tensor, dd, B: int, C: int, H: int, padded: bool, train: bool,
+                   his: Optional[torch.Tensor] = None):
+        """Device user side (fused): ``(loss, scores)`` from news vectors ``v`` of the unique ids.
+        ``his [B, H]``: the batch's history ids, the key mask when ``mask_padding`` is on."""
         uniq, inv, perm, ptr = dd
         p = float(self.cfg.user_dropout) if train else 0.0
         clip, std = self._ldp()
@@ -362,8 +364,9 @@ class LocalEngine:
         ldp = (clip, std, self.ldp_seed, 0)
         if train:
             self.noise_offset += 1
+        keep = his if (self.cfg.mask_padding and his is not None) else None
         return OF.user_step(v, inv, perm, ptr, self.model.user_encoder, B, C, H, self.score_act,
-                            (p, self.user_drop_seed, 0), self._rng_step, ldp, padded)
+                            (p, self.user_drop_seed, 0), self._rng_step, ldp, padded, keep)
 
     def _dedup(self, cand, his, pre):
         if pre is not None and pre.dedup is not None:
@@ -386,7 +389,7 @@ class LocalEngine:
                 v = self.news_vectors(dd[0], grad=True)
             with obs.range("user_step"):
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
-                                          pre is not None and pre.padded, True)
+                                          pre is not None and pre.padded, True, his)
             with obs.range("backward"):
                 # a persistent ones tensor as the seed gradient: no fill launch per step (the
                 # captured graph reads it in place)
@@ -530,7 +533,7 @@ class LocalEngine:
         if self.fused_user:
             dd = self._dedup(cand, his, pre)
             v = self.news_vectors(dd[0], grad=False).detach().requires_grad_(True)
-            loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1], False, True)
+            loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1], False, True, his)
             loss.backward()
             self._rng_step.add_(1)
             self.G.index_add_(0, dd[0].long(), v.grad)
@@ -667,7 +670,7 @@ class LocalEngine:
                 else:
                     uniq, inv, _, _ = ops.dedup(ids, self.N)
                     v = self.news_vectors(uniq, grad=False)
-                loss, s = self._user_loss(v, (None, inv, inv, inv), B, C, his.shape[1], False, False)
+                loss, s = self._user_loss(v, (None, inv, inv, inv), B, C, his.shape[1], False, False, his)
                 losses.append(float(loss) * B)
                 scores_all.append(s.float().cpu().numpy())
                 continue

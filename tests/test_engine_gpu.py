@@ -19,12 +19,26 @@ def _cfg():
     return cfg
 
 
-@pytest.mark.parametrize("untruncated", [False, True])
-def test_step_matches_cpu_oracle(dev, untruncated):
+_ORACLE_ERRS: dict = {}
+
+
+@pytest.mark.parametrize("untruncated,mask", [(False, False), (True, False), (False, True), (True, True)])
+def test_step_matches_cpu_oracle(dev, untruncated, mask):
     """``untruncated``: the reference's Q6 (histories padded, never truncated) -- batches of the
-    tiny shard then carry histories > 64, the long-history user attention / pool kernels."""
+    tiny shard then carry histories > 64, the long-history user attention / pool kernels.
+    ``mask``: the mask_padding option (masked user attention keys / pool positions, masked title
+    tokens in the text pool).
+
+    Bounds from bf16 rounding: the device step rounds the frozen backbone's activations, the
+    hidden-state cache and every GEMM operand to bf16 (unit roundoff u = 2^-8), so a gradient
+    is the oracle's up to a few u of relative error per bf16 stage it went through -- at most
+    ~5 stages here (backbone output, head GEMM operands, news vector, user GEMM operands):
+    per tensor err <= 8 u ||a|| (3.1e-2), plus 2e-4 of the whole gradient's norm for tensors
+    that are a near-cancellation (tiny against the rest).  The measured errors are written to
+    ``FEDREC_ORACLE_ERRS`` (json) when set."""
     cfg = _cfg()
     cfg.compat.no_history_truncation = untruncated
+    cfg.mask_padding = mask
     torch.manual_seed(0)
     m_cpu = FedRecModel(cfg)
     m_gpu = copy.deepcopy(m_cpu).to(dev)
@@ -52,7 +66,13 @@ def test_step_matches_cpu_oracle(dev, untruncated):
         # relative for well-conditioned tensors; tensors whose gradient is a near-cancellation
         # (tiny vs the whole-model gradient) are held to an absolute bound instead
         err = float((a - b).norm())
-        assert err <= 5e-2 * float(a.norm()) + 2e-3 * total, (name, err, float(a.norm()), total)
+        _ORACLE_ERRS[f"{untruncated}/{mask}/{name}"] = (err / max(float(a.norm()), 1e-30), float(a.norm()) / total)
+        assert err <= 8 * 2.0 ** -8 * float(a.norm()) + 2e-4 * total, (name, err, float(a.norm()), total)
+    out = __import__("os").environ.get("FEDREC_ORACLE_ERRS")
+    if out:
+        import json
+        with open(out, "w") as f:
+            json.dump(_ORACLE_ERRS, f, indent=1)
 
 
 def test_training_reduces_loss_on_gpu(dev):

@@ -21,10 +21,22 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-12))
 
 
-@pytest.mark.parametrize("p", [0.0, 0.2])
-def test_user_step_matches_module_oracle(dev, p):
+def _his_ids(B, H, dev):
+    """History ids with padded slots (0): impression b keeps its first H - 6 b slots, the
+    last impression none (a fully masked row)."""
+    ids = torch.randint(1, 300, (B, H), dtype=torch.int32)
+    for b in range(B):
+        ids[b, max(0, H - 6 * b):] = 0
+    ids[-1] = 0
+    return ids.to(dev)
+
+
+@pytest.mark.parametrize("p,mask", [(0.0, False), (0.2, False), (0.2, True)])
+def test_user_step_matches_module_oracle(dev, p, mask):
+    """``mask``: the mask_padding option -- the padded history slots are masked keys of the
+    attention and masked positions of the pool (kernels vs the host oracle's masked softmax)."""
     torch.manual_seed(0)
-    cfg = FedRecConfig(mode="grad_avg")
+    cfg = FedRecConfig(mode="grad_avg", mask_padding=mask)
     model = FedRecModel(cfg)
     ue_c = model.user_encoder
     ue_g = copy.deepcopy(ue_c).to(dev)
@@ -35,8 +47,9 @@ def test_user_step_matches_module_oracle(dev, p):
     v = (torch.randn(U, D) * 0.05).to(dev).requires_grad_(True)
     seed, off, step = 1234, 7, 3
     rng = torch.tensor([step], dtype=torch.int64, device=dev)
+    his_ids = _his_ids(B, H, dev) if mask else None
     loss, scores = OF.user_step(v, inv, perm, ptr, ue_g, B, C, H, "sigmoid", (p, seed, off), rng, (0.0, 0.0, 0, 0),
-                                False)
+                                False, his_ids)
     loss.backward()
     # oracle: fp32 CPU, the same gathered rows and the same mask (offset off + step)
     vc = v.detach().cpu().requires_grad_(True)
@@ -46,7 +59,7 @@ def test_user_step_matches_module_oracle(dev, p):
         idx = torch.arange(B * H)[:, None] * D + torch.arange(D)[None, :]
         his = his * R.dropout_scale(idx, p, seed, off + step)
     ue_c.eval()  # the mask is applied above; the module's own dropout stays off
-    u = ue_c(his.view(B, H, D))
+    u = ue_c(his.view(B, H, D), None if his_ids is None else his_ids.cpu())
     loss_c, s_c, _, _ = R.score_ce_fwd_bwd(cand, u, "sigmoid")
     # score_ce_fwd_bwd returns analytic grads; recompute the loss under autograd for the backward
     sc = torch.sigmoid(torch.bmm(cand, u.unsqueeze(-1)).squeeze(-1))
@@ -108,3 +121,35 @@ def test_gather_dropout_matches_oracle():
     keep = (x != 0).float().mean().item()
     assert abs(keep - 0.8) < 0.01
     assert torch.equal(ops.gather_dropout(v, idx, 0.0, 11, 5, None), v[idx.long()])
+
+
+@pytest.mark.parametrize("mask", [False, True])
+def test_user_encoder_module_on_device_matches_cpu(dev, mask):
+    """``UserEncoder.forward`` on the device (OF.UserEncoderFn: the step's kernels, no vendor
+    GEMM / torch dropout) against the host module: the user vector and every gradient."""
+    torch.manual_seed(3)
+    cfg = FedRecConfig(mode="grad_avg", mask_padding=mask)
+    ue_c = FedRecModel(cfg).user_encoder
+    ue_g = copy.deepcopy(ue_c).to(dev)
+    ue_c.eval()
+    ue_g.eval()
+    B, H, D = 6, 50, 400
+    x = torch.randn(B, H, D)  # unit scale: peaky attention, so the pool gradients do not cancel
+    his_ids = _his_ids(B, H, dev) if mask else None
+    xg = x.to(dev).requires_grad_(True)
+    xc = x.clone().requires_grad_(True)
+    ug = ue_g(xg, his_ids)
+    uc = ue_c(xc, None if his_ids is None else his_ids.cpu())
+    g = torch.randn(B, D)
+    ug.backward(g.to(dev))
+    uc.backward(g)
+    assert _rel(ug, uc) < 1e-2, _rel(ug, uc)
+    if mask:
+        assert float(ug[-1].abs().max()) == 0.0  # every slot padded: the pooled user vector is 0
+    assert _rel(xg.grad, xc.grad) < 3e-2
+    top = max(float(p.grad.norm()) for p in ue_c.parameters())
+    for (n, pg), (_, pc) in zip(ue_g.named_parameters(), ue_c.named_parameters()):
+        if float(pc.grad.norm()) < 1e-6 * top:  # a near-cancellation (e.g. the key bias): rounding noise
+            assert float(pg.grad.norm()) < 1e-4 * top, n
+            continue
+        assert _rel(pg.grad, pc.grad) < 4e-2, (n, _rel(pg.grad, pc.grad))
