@@ -63,7 +63,7 @@ int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, i
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
                      int dk, const int* keep, hipStream_t s);
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
-                int C, int D, int sigm, hipStream_t s);
+                int C, int D, int sigm, const int* ci, hipStream_t s);
 int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U, int D,
                         int R, float* scratch, hipStream_t s, int zero_empty);
 int fr_segsum_chunks(int R);
@@ -639,23 +639,47 @@ at::Tensor user_attention_bwd(const at::Tensor& qkv, const at::Tensor& stats, co
   return dqkv;
 }
 
+// ci (optional): candidates as rows of a table -- cand is then [U, D], candidate (b, c) its row
+// ci[b C + c]; dcand_out (optional): a [B C, D] fp32 buffer the candidate gradient is written to
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Tensor& cand, const at::Tensor& user,
-                                                                    int64_t act) {
+                                                                    int64_t act, const c10::optional<at::Tensor>& ci,
+                                                                    const c10::optional<at::Tensor>& dcand_out) {
   check_dev(cand, "cand");
   check_dev(user, "user");
-  TORCH_CHECK(cand.scalar_type() == at::kFloat && user.scalar_type() == at::kFloat, "fedrec::score_ce: fp32");
+  TORCH_CHECK(cand.scalar_type() == at::kFloat && user.scalar_type() == at::kFloat && cand.is_contiguous() &&
+                  user.is_contiguous(),
+              "fedrec::score_ce: contiguous fp32");
   const c10::DeviceGuard g(cand.device());
-  const int64_t B = cand.size(0), C = cand.size(1), D = cand.size(2);
-  TORCH_CHECK(user.size(0) == B && user.size(1) == D, "fedrec::score_ce: user shape");
+  const bool gathered = ci.has_value() && ci->defined();
+  const int64_t B = user.size(0), D = user.size(1);
+  int64_t C;
+  if (gathered) {
+    check_dev(*ci, "ci");
+    TORCH_CHECK(cand.dim() == 2 && cand.size(1) == D && ci->scalar_type() == at::kInt && ci->is_contiguous() &&
+                    B > 0 && ci->numel() % B == 0,
+                "fedrec::score_ce: table [U, D] + int32 ci [B C]");
+    C = ci->numel() / B;  // ci values index the table: produced by dedup (in range by construction)
+  } else {
+    TORCH_CHECK(cand.dim() == 3 && cand.size(0) == B && cand.size(2) == D, "fedrec::score_ce: cand [B, C, D]");
+    C = cand.size(1);
+  }
   // per-impression losses, then the deterministic colsum (no float atomics: bit-reproducible loss)
   auto lossb = at::empty({std::max<int64_t>(B, 1) + 1}, cand.options());
   auto loss = lossb.narrow(0, B > 0 ? B : 0, 1).squeeze(0);  // 0-d view (view({}) would pick view(ScalarType))
   auto scores = at::empty({B, C}, cand.options());
-  auto dcand = at::empty_like(cand);
+  at::Tensor dcand;
+  if (dcand_out.has_value() && dcand_out->defined()) {
+    check_dev(*dcand_out, "dcand_out");
+    TORCH_CHECK(dcand_out->scalar_type() == at::kFloat && dcand_out->is_contiguous() && dcand_out->numel() == B * C * D,
+                "fedrec::score_ce: dcand_out fp32 [B C, D]");
+    dcand = *dcand_out;
+  } else {
+    dcand = at::empty({B, C, D}, cand.options());
+  }
   auto duser = at::empty_like(user);
   check_rc(fr_score_ce(cand.data_ptr<float>(), user.data_ptr<float>(), lossb.data_ptr<float>(), scores.data_ptr<float>(),
                        dcand.data_ptr<float>(), duser.data_ptr<float>(), (int)B, (int)C, (int)D, (int)act,
-                       cur_stream()),
+                       gathered ? ci->data_ptr<int>() : nullptr, cur_stream()),
            "score_ce");
   {
     const float* xs[1] = {lossb.data_ptr<float>()};
@@ -666,6 +690,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Te
     TORCH_CHECK(need >= 0 && fr_colsum_f32(xs, os, ints, 1, part.data_ptr<float>(), cur_stream()) == 0,
                 "fedrec::score_ce: loss sum");
   }
+  // with dcand_out the gradient lives in the caller's buffer (no output aliasing an input)
+  if (dcand_out.has_value() && dcand_out->defined()) return {loss, scores, at::empty({0}, cand.options()), duser};
   return {loss, scores, dcand, duser};
 }
 
@@ -1376,7 +1402,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None) -> (Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None) -> Tensor");
-  m.def("score_ce(Tensor cand, Tensor user, int act) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("score_ce(Tensor cand, Tensor user, int act, Tensor? ci=None, Tensor(a!)? dcand_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");

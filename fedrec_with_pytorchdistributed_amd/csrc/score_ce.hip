@@ -60,21 +60,26 @@ __global__ __launch_bounds__(256) void score_ce_kernel(const float* __restrict__
 // dot products run side by side instead of one after another in a single wave (that chain of
 // load -> reduce rounds made the wave-per-impression kernel ~18 us for B = 64).  The softmax /
 // loss / dz of the impression come from wave 0's first C lanes; dcand rows are written by
-// their own wave, du by all threads over the D columns.
+// their own wave, du by all threads over the D columns.  ci (optional): candidate (b, c) is
+// row ci[b C + c] of a news-vector table (the training step's rows, no gathered copy).
 __global__ __launch_bounds__(64 * MAXC) void score_ce_block_kernel(const float* __restrict__ cand,
                                                                    const float* __restrict__ user,
                                                                    float* __restrict__ loss,
                                                                    float* __restrict__ scores,
                                                                    float* __restrict__ dcand,
                                                                    float* __restrict__ duser, int B, int C, int D,
-                                                                   int sigm) {
+                                                                   int sigm, const int* __restrict__ ci) {
   __shared__ float zs[MAXC], dzs[MAXC];
+  __shared__ const float* rowp[MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x;
-  const float* cb = cand + (size_t)b * C * D;
+  if (threadIdx.x < C)
+    rowp[threadIdx.x] = cand + (size_t)(ci ? ci[(size_t)b * C + threadIdx.x] : b * C + threadIdx.x) * D;
+  __syncthreads();
   const float* ub = user + (size_t)b * D;
   float a = 0.f;
-  for (int d = lane; d < D; d += 64) a += cb[(size_t)w * D + d] * ub[d];
+  const float* cw = rowp[w];
+  for (int d = lane; d < D; d += 64) a += cw[d] * ub[d];
   a = wave_sum(a);
   if (lane == 0) zs[w] = a;
   __syncthreads();
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(64 * MAXC) void score_ce_block_kernel(const float* 
   for (int d = lane; d < D; d += 64) dcand[((size_t)b * C + w) * D + d] = dzw * ub[d];
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     float du = 0.f;
-    for (int c = 0; c < C; ++c) du += dzs[c] * cb[(size_t)c * D + d];
+    for (int c = 0; c < C; ++c) du += dzs[c] * rowp[c][d];
     duser[(size_t)b * D + d] = du;
   }
 }
@@ -108,12 +113,12 @@ int g_score_variant = 1;  // 1: block per impression (default), 0: wave per impr
 extern "C" void fr_score_set_variant(int v) { g_score_variant = v; }
 
 extern "C" int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand,
-                           float* duser, int B, int C, int D, int sigm, hipStream_t s) {
+                           float* duser, int B, int C, int D, int sigm, const int* ci, hipStream_t s) {
   if (C > MAXC) return 1;
   if (B == 0) return 0;
-  if (g_score_variant == 1 && C <= MAXC)
+  if (ci != nullptr || (g_score_variant == 1 && C <= MAXC))
     hipLaunchKernelGGL(score_ce_block_kernel, dim3(B), dim3(64 * C), 0, s, cand, user, loss, scores, dcand, duser, B,
-                       C, D, sigm);
+                       C, D, sigm, ci);
   else
     hipLaunchKernelGGL(score_ce_kernel, dim3((B + 3) / 4), dim3(256), 0, s, cand, user, loss, scores, dcand, duser, B,
                        C, D, sigm);

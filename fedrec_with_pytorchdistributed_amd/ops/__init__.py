@@ -185,6 +185,20 @@ def score_ce(cand, user, act: str = "sigmoid"):
     return ref.score_ce_fwd_bwd(cand, user, act)
 
 
+def score_ce_rows(table, ci, user, act: str, dcand_out):
+    """:func:`score_ce` with candidate ``(b, c)`` = row ``ci[b C + c]`` of ``table [U, D]`` and its
+    gradient written into ``dcand_out [B C, D]`` -> ``(loss, scores, duser)``."""
+    B = user.shape[0]
+    if _dev(table):
+        loss, scores, _, du = native.require_for(table).score_ce(table, user.contiguous(), 1 if act == "sigmoid" else 0,
+                                                                 ci, dcand_out)
+        return loss, scores, du
+    loss, scores, dcand, du = ref.score_ce_fwd_bwd(table.index_select(0, ci.long()).view(B, -1, table.shape[1]), user,
+                                                   act)
+    dcand_out.copy_(dcand.reshape(dcand_out.shape))
+    return loss, scores, du
+
+
 def segment_sum_rows(rows, inv, num_out: int, clip: float = 0.0, noise_std: float = 0.0,
                      seed: int = 0, offset: int = 0, generator=None, seg=None, zero_empty: bool = False,
                      dev_off=None):

@@ -620,15 +620,17 @@ class UserStepFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, v, inv, perm, ptr, wq, bq, wk, bk, wv, bv, w1, b1, w2, b2, meta):
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep = meta
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one = meta
         D = v.shape[1]
         BC = B * C
-        ci = inv[:BC]
-        cand = v.index_select(0, ci if ci.dtype in (torch.int32, torch.int64) else ci.long()).view(B, C, D)
         u, saved = _user_enc_fwd(v, inv[BC:], (wq, bq, wk, bk, wv, bv, w1, b1, w2, b2), B, H, heads, hd, drop,
                                  dev_off, keep)
-        loss, scores, dcand, du = ops.score_ce(cand, u, act)
-        ctx.save_for_backward(v, inv, perm, ptr, dcand, du, *saved)
+        # per-occurrence news gradients: the candidate rows come straight from the scoring
+        # kernel (candidates read from v by index: no gathered copy), the history rows from the
+        # user encoder's dgrad in the backward
+        rows = torch.empty(inv.numel(), D, device=v.device, dtype=torch.float32)
+        loss, scores, du = ops.score_ce_rows(v, inv[:BC], u, act, rows[:BC])
+        ctx.save_for_backward(v, inv, perm, ptr, rows, du, *saved)
         ctx.meta = meta
         ctx.mark_non_differentiable(scores)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the scores (one fill launch)
@@ -636,13 +638,13 @@ class UserStepFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss, gscores):
-        v, inv, perm, ptr, dcand, du, *saved = ctx.saved_tensors
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep = ctx.meta
-        D = v.shape[1]
+        v, inv, perm, ptr, rows, du, *saved = ctx.saved_tensors
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one = ctx.meta
         BC = B * C
-        rows = torch.empty(inv.numel(), D, device=v.device, dtype=torch.float32)  # per-occurrence news gradients
-        torch.mul(dcand.view(BC, D), gloss, out=rows[:BC])
-        grads = _user_enc_bwd(saved, du * gloss, rows[BC:], B, H, heads, hd, drop, dev_off, keep)
+        if gloss is not one:  # the engine seeds the backward with its persistent ones tensor: no scale
+            rows[:BC].mul_(gloss)
+            du = du * gloss
+        grads = _user_enc_bwd(saved, du, rows[BC:], B, H, heads, hd, drop, dev_off, keep)
         clip, noise, lseed, loff = ldp
         # the noise offset's step part is the device counter (dev_off): graph replays draw fresh noise
         dv = ops.segment_sum_rows(rows, inv, v.shape[0], clip, noise, lseed, loff, seg=(perm, ptr), zero_empty=padded,
@@ -651,14 +653,16 @@ class UserStepFn(torch.autograd.Function):
 
 
 def user_step(v, inv, perm, ptr, user_encoder, B: int, C: int, H: int, act: str, drop, dev_off, ldp, padded: bool,
-              keep=None):
+              keep=None, one=None):
     """Device user side of a step (see :class:`UserStepFn`) -> ``(loss, scores)``.  ``keep``:
-    the mask_padding key mask (history ids [B, H], nonzero = real slot) or None."""
+    the mask_padding key mask (history ids [B, H], nonzero = real slot) or None.  ``one``: the
+    tensor the caller will seed ``loss.backward`` with when it is a ones tensor (the backward
+    then skips the scale by the incoming gradient)."""
     mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
     if keep is not None:
         keep = keep.reshape(B, H)
         keep = keep if keep.dtype == torch.int32 and keep.is_contiguous() else keep.to(torch.int32).contiguous()
-    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded, keep)
+    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded, keep, one)
     return UserStepFn.apply(v, inv, perm, ptr, mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias,
                             mha.W_V.weight, mha.W_V.bias, pool.att_fc1.weight, pool.att_fc1.bias,
                             pool.att_fc2.weight, pool.att_fc2.bias, meta)

@@ -366,7 +366,14 @@ class LocalEngine:
             self.noise_offset += 1
         keep = his if (self.cfg.mask_padding and his is not None) else None
         return OF.user_step(v, inv, perm, ptr, self.model.user_encoder, B, C, H, self.score_act,
-                            (p, self.user_drop_seed, 0), self._rng_step, ldp, padded, keep)
+                            (p, self.user_drop_seed, 0), self._rng_step, ldp, padded, keep, self._seed_one())
+
+    def _seed_one(self) -> torch.Tensor:
+        """The persistent ones tensor every fused backward is seeded with (no fill launch per
+        step; the captured graph reads it in place, and UserStepFn skips the scale by it)."""
+        if self._one is None or self._one.device != self.device:
+            self._one = torch.ones((), device=self.device, dtype=torch.float32)
+        return self._one
 
     def _dedup(self, cand, his, pre):
         if pre is not None and pre.dedup is not None:
@@ -391,11 +398,7 @@ class LocalEngine:
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
                                           pre is not None and pre.padded, True, his)
             with obs.range("backward"):
-                # a persistent ones tensor as the seed gradient: no fill launch per step (the
-                # captured graph reads it in place)
-                if self._one is None or self._one.shape != loss.shape or self._one.device != loss.device:
-                    self._one = torch.ones_like(loss)
-                loss.backward(self._one)
+                loss.backward(self._seed_one())
             self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
             self.flat.end_backward()
             return loss.detach()
@@ -534,7 +537,7 @@ class LocalEngine:
             dd = self._dedup(cand, his, pre)
             v = self.news_vectors(dd[0], grad=False).detach().requires_grad_(True)
             loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1], False, True, his)
-            loss.backward()
+            loss.backward(self._seed_one())
             self._rng_step.add_(1)
             self.G.index_add_(0, dd[0].long(), v.grad)
             self.touched[dd[0].long()] = True
