@@ -860,13 +860,14 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
                 const std::vector<at::Tensor>& B, const c10::List<c10::optional<at::Tensor>>& bias,
                 const std::vector<at::Tensor>& C, at::IntArrayRef ints, at::ArrayRef<double> floats,
                 at::IntArrayRef seeds, const c10::optional<at::Tensor>& dev_off, const std::vector<at::Tensor>& Bseg,
-                int64_t tile) {
+                int64_t tile, const c10::List<c10::optional<at::Tensor>>& asum) {
   const size_t n = A.size();
   TORCH_CHECK(n >= 1 && n <= 6 && B.size() == n && C.size() == n && gidx.size() == n && bias.size() == n &&
+                  asum.size() == n &&
                   ints.size() == 14 * n && floats.size() == 2 * n && seeds.size() == 2 * n,
               "fedrec::small_gemm: descriptor sizes");
   const c10::DeviceGuard g(A[0].device());
-  std::vector<const void*> ptrs(7 * n);
+  std::vector<const void*> ptrs(8 * n);
   std::vector<int> iv(16 * n);
   size_t seg_used = 0;
   std::vector<float> fv(2 * n);
@@ -894,9 +895,9 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
                   "fedrec::small_gemm: B too small");
     TORCH_CHECK(gathered == (gather_on != 0), "fedrec::small_gemm: gidx given iff gather_on");
     TORCH_CHECK(avail(C[i]) >= (M - 1) * ldc + N || M == 0 || N == 0, "fedrec::small_gemm: C too small");
-    ptrs[7 * i + 0] = A[i].data_ptr();
-    ptrs[7 * i + 1] = nullptr;
-    ptrs[7 * i + 5] = ptrs[7 * i + 6] = nullptr;
+    ptrs[8 * i + 0] = A[i].data_ptr();
+    ptrs[8 * i + 1] = nullptr;
+    ptrs[8 * i + 5] = ptrs[8 * i + 6] = nullptr;
     if (kseg > 0) {  // the extra row blocks of a K-segmented B come from Bseg in order
       TORCH_CHECK(bm == 1 && seg_used + 2 <= Bseg.size(), "fedrec::small_gemm: K-segmented B needs b_mode 1 + 2 Bseg");
       for (int j = 0; j < 2; ++j) {
@@ -904,23 +905,31 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
         TORCH_CHECK(t.is_cuda() && t.scalar_type() == B[i].scalar_type() && t.stride(-1) == 1 &&
                         avail(t) >= (kseg - 1) * ldb + N,
                     "fedrec::small_gemm: Bseg block");
-        ptrs[7 * i + 5 + j] = t.data_ptr();
+        ptrs[8 * i + 5 + j] = t.data_ptr();
       }
       seg_used += 2;
     }
     if (gathered) {
       TORCH_CHECK(gv->is_cuda() && gv->scalar_type() == at::kInt && gv->numel() >= (gather_on == 1 ? M : K),
                   "fedrec::small_gemm: gidx int32[M] (A rows) or int32[K] (B rows)");
-      ptrs[7 * i + 1] = gv->data_ptr();
+      ptrs[8 * i + 1] = gv->data_ptr();
     }
-    ptrs[7 * i + 2] = B[i].data_ptr();
+    ptrs[8 * i + 2] = B[i].data_ptr();
     const auto bv = bias.get(i);
-    ptrs[7 * i + 3] = nullptr;
+    ptrs[8 * i + 3] = nullptr;
     if (bv.has_value() && bv->defined()) {
       TORCH_CHECK(bv->is_cuda() && bv->scalar_type() == at::kFloat && bv->numel() >= N, "fedrec::small_gemm: bias");
-      ptrs[7 * i + 3] = bv->data_ptr();
+      ptrs[8 * i + 3] = bv->data_ptr();
     }
-    ptrs[7 * i + 4] = C[i].data_ptr();
+    ptrs[8 * i + 4] = C[i].data_ptr();
+    ptrs[8 * i + 7] = nullptr;
+    const auto av = asum.get(i);
+    if (av.has_value() && av->defined()) {  // column sums of A (a_mode 1): fp32 [M], contiguous
+      TORCH_CHECK(av->is_cuda() && av->scalar_type() == at::kFloat && av->is_contiguous() && av->numel() >= M &&
+                      am == 1,
+                  "fedrec::small_gemm: asum fp32 [M] (a_mode 1)");
+      ptrs[8 * i + 7] = av->data_ptr();
+    }
     for (int j = 0; j < 14; ++j) iv[16 * i + j] = (int)q[j];
     iv[16 * i + 14] = A[i].scalar_type() == at::kBFloat16;
     iv[16 * i + 15] = B[i].scalar_type() == at::kBFloat16;
@@ -1417,7 +1426,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
-  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg, int tile=0) -> ()");
+  m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg, int tile, Tensor?[] asum) -> ()");
   m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
   m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst) -> bool");
   m.def("multi_cast_t(Tensor[] src, Tensor(a!)[] dst) -> bool");

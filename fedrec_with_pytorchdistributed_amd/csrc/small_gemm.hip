@@ -46,12 +46,15 @@ struct GemmDesc {
   const float* bias;
   float* C;
   float* P;  // split-K partials [splits, M, N] (splits > 1: the reduce kernel does the epilogue)
+  float* asum;  // optional (a_mode 1): asum[m] = sum_k A(m, k) in fp32 -- a weight gradient's bias
+  float* AP;    // gradient dY^T 1 from the dY tiles the GEMM streams; partials [splits, M] if split
   int M, N, K, lda, ldb, ldc;
   int a_mode, b_mode, act, accumulate;
   float alpha, pdrop;
   int drop_ld, drop_on, gather_on, tiles_n, tile_base, splits, kchunk, kseg;
   int a_bf16, b_bf16;
-  int red_base;  // first block of this desc's split-K reduction
+  int red_base;   // first block of this desc's split-K reduction
+  int ared_base;  // first block of its asum partial reduction (split asum descs)
   unsigned long long seed, offset;  // offset += *dev_off when dev_off is set (graph replays)
 };
 
@@ -327,9 +330,24 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
       load_raw<TN>(g, false, n0, k, kend, tid, rb);
     }
   };
+  // asum: the column-0 tiles of an a_mode-1 desc also sum the raw A values they stage (chunk
+  // = 16 consecutive m of one k), per lane, then across lanes / waves after the loop
+  const bool do_as = g.asum != nullptr && n0 == 0;
+  const bool ah = FAST ? AH : (bool)g.a_bf16;
+  float as_[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) as_[j] = 0.f;
   if (kbeg < kend) load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += TK) {
     __syncthreads();  // the previous tile's fragments are consumed
+    if (do_as) {
+#pragma unroll
+      for (int i = 0; i < TM / 64; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          as_[j] += ah ? __uint_as_float((j & 1 ? ra[i][j >> 1] & 0xFFFF0000u : ra[i][j >> 1] << 16))
+                       : __uint_as_float(ra[i][j]);
+    }
     store_lds<TM>(g, true, m0, k0, tid, ra, off, As, FAST ? AH : (bool)g.a_bf16);
     store_lds<TN>(g, false, n0, k0, tid, rb, off, Bs, FAST ? BH : (bool)g.b_bf16);
     __syncthreads();
@@ -346,6 +364,28 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  if (do_as) {  // lanes of one m group (tid % CPR) hold the same 16 m: xor-shuffle, then waves in order
+    constexpr int CPR = TM / 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) as_[j] += __shfl_xor(as_[j], o, 64);
+    }
+    __syncthreads();  // the LDS tiles are free: reuse As as [4 waves][TM] floats
+    float* red = (float*)&As[0][0];
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) red[wave * TM + lane * 16 + j] = as_[j];
+    }
+    __syncthreads();
+    if (tid < TM && m0 + tid < g.M) {
+      const float v = (red[tid] + red[TM + tid]) + (red[2 * TM + tid] + red[3 * TM + tid]);
+      if (g.splits > 1)
+        g.AP[(size_t)split * g.M + m0 + tid] = v;
+      else
+        g.asum[m0 + tid] = v;
     }
   }
   // lane holds C[m = wm + 16 i + 4 fq + r][n = wn + 16 j + fr]; every loop fully unrolled
@@ -417,7 +457,21 @@ __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch b
 // partial loads, one Philox draw for the 4 dropout scales (drop_ld % 16 == 0, n % 4 == 0).
 // N % 4 == 0 for every split desc (host-checked); C / bias / accumulate fall back to scalar
 // accesses when a row of C is not 16-byte aligned.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batch) {
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batch, int c_blocks) {
+  if ((int)blockIdx.x >= c_blocks) {  // the asum partials of split descs: asum[m] = sum_s AP[s][m]
+    int ai = -1;
+#pragma unroll
+    for (int i = 0; i < MAXG; ++i)
+      if (i < batch.n && batch.d[i].AP != nullptr && (int)blockIdx.x >= batch.d[i].ared_base) ai = i;
+    if (ai < 0) return;
+    const GemmDesc& a = batch.d[ai];
+    const int m = (blockIdx.x - a.ared_base) * 256 + threadIdx.x;
+    if (m >= a.M) return;
+    float v = a.AP[m];
+    for (int sp = 1; sp < a.splits; ++sp) v += a.AP[(size_t)sp * a.M + m];
+    a.asum[m] = v;
+    return;
+  }
   int gi = 0;
 #pragma unroll
   for (int i = 1; i < MAXG; ++i)
@@ -565,7 +619,7 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const ColsumBatch bat
 
 }  // namespace
 
-// descs: 7 pointers + 16 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
+// descs: 8 pointers + 16 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
 // scratch: split-K partial space (floats) the caller allocated; returns the floats it needs
 // when scratch is null (query mode).
 static int choose_splits(int tiles, int K) {
@@ -635,13 +689,14 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   b.dev_off = dev_off;
   for (int i = 0; i < n; ++i) {
     GemmDesc& d = b.d[i];
-    d.A = ptrs[7 * i + 0];
-    d.gidx = (const int*)ptrs[7 * i + 1];
-    d.B = ptrs[7 * i + 2];
-    d.bias = (const float*)ptrs[7 * i + 3];
-    d.C = (float*)ptrs[7 * i + 4];
-    d.B2 = ptrs[7 * i + 5];
-    d.B3 = ptrs[7 * i + 6];
+    d.A = ptrs[8 * i + 0];
+    d.gidx = (const int*)ptrs[8 * i + 1];
+    d.B = ptrs[8 * i + 2];
+    d.bias = (const float*)ptrs[8 * i + 3];
+    d.C = (float*)ptrs[8 * i + 4];
+    d.B2 = ptrs[8 * i + 5];
+    d.B3 = ptrs[8 * i + 6];
+    d.asum = (float*)ptrs[8 * i + 7];
     const int* q = ints + 16 * i;
     d.M = q[0]; d.N = q[1]; d.K = q[2]; d.lda = q[3]; d.ldb = q[4]; d.ldc = q[5];
     d.a_mode = q[6]; d.b_mode = q[7]; d.act = q[8]; d.accumulate = q[9]; d.drop_ld = q[10];
@@ -658,6 +713,7 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
                       (d.drop_on == 1 && (d.a_mode != 0 || d.a_bf16)) || (d.drop_on == 2 && (d.b_mode != 1 || d.b_bf16))))
       return -3;
     if (d.gather_on && (!d.gidx || (d.gather_on == 1 && d.a_mode != 0) || (d.gather_on == 2 && d.b_mode != 1))) return -4;
+    if (d.asum && d.a_mode != 1) return -6;  // column sums of a stored-transposed A only
   }
   b.n = n;
   const bool fast = fast_ok(b), mixed = mixed_dtypes(b);
@@ -681,11 +737,16 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
       d.kchunk = d.K;
     }
     d.P = nullptr;
+    d.AP = nullptr;
     d.red_base = red_blocks;
     if (d.splits > 1) {
       d.P = scratch ? scratch + need : nullptr;
       need += (long)d.splits * d.M * d.N;
       red_blocks += (int)(((long)d.M * d.N / 4 + 255) / 256);
+      if (d.asum) {
+        d.AP = scratch ? scratch + need : nullptr;
+        need += (long)d.splits * d.M;
+      }
     }
     d.tile_base = tiles;
     tiles += t * d.splits;
@@ -715,7 +776,14 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     default: SG_LAUNCH(2, 2); break;
   }
 #undef SG_LAUNCH
-  if (red_blocks > 0) hipLaunchKernelGGL(splitk_reduce_kernel, dim3(red_blocks), dim3(256), 0, s, b);
+  int ared_blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    GemmDesc& d = b.d[i];
+    d.ared_base = red_blocks + ared_blocks;
+    if (d.splits > 1 && d.asum) ared_blocks += (d.M + 255) / 256;
+  }
+  if (red_blocks + ared_blocks > 0)
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(red_blocks + ared_blocks), dim3(256), 0, s, b, red_blocks);
   return 0;
 }
 

@@ -275,11 +275,12 @@ class Gemm:
     col`` in the logical (gathered) matrix -- the mask of ``ops.dropout_add``."""
 
     __slots__ = ("A", "B", "C", "M", "N", "K", "lda", "ldb", "ldc", "a_mode", "b_mode", "act", "accumulate",
-                 "alpha", "bias", "gidx", "gather_on", "pdrop", "drop_on", "drop_ld", "seed", "offset", "bseg", "kseg")
+                 "alpha", "bias", "gidx", "gather_on", "pdrop", "drop_on", "drop_ld", "seed", "offset", "bseg", "kseg",
+                 "asum")
 
     def __init__(self, A, B, C, M, N, K, lda, ldb, ldc, a_mode=0, b_mode=0, act=0, accumulate=False, alpha=1.0,
                  bias=None, gidx=None, gather_on=0, pdrop=0.0, drop_on=0, drop_ld=0, seed=0, offset=0,
-                 bseg=(), kseg=0):
+                 bseg=(), kseg=0, asum=None):
         self.A, self.B, self.C = A, B, C
         self.M, self.N, self.K, self.lda, self.ldb, self.ldc = int(M), int(N), int(K), int(lda), int(ldb), int(ldc)
         self.a_mode, self.b_mode, self.act, self.accumulate = int(a_mode), int(b_mode), int(act), bool(accumulate)
@@ -288,6 +289,9 @@ class Gemm:
         self.seed, self.offset = int(seed), int(offset)
         # K-segmented B (b_mode 1): rows [0, kseg) of B, [kseg, 2 kseg) of bseg[0], then bseg[1]
         self.bseg, self.kseg = tuple(bseg), int(kseg)
+        # a_mode 1 only: asum[m] = sum_k A(m, k) in fp32 from the raw A values the GEMM stages
+        # (a weight gradient's bias gradient dY^T 1 in the same launch)
+        self.asum = asum
 
 
 def gather_dropout(v: torch.Tensor, idx: torch.Tensor, p: float, seed: int, offset: int, dev_off=None,
@@ -319,7 +323,7 @@ def small_gemm(*gs: Gemm, dev_off=None, tile: int = 0) -> None:
         seeds += [g.seed, g.offset]
     native.require_for(gs[0].A).small_gemm([g.A for g in gs], [g.gidx for g in gs], [g.B for g in gs],
                                            [g.bias for g in gs], [g.C for g in gs], ints, floats, seeds, dev_off,
-                                           [t for g in gs for t in g.bseg], int(tile))
+                                           [t for g in gs for t in g.bseg], int(tile), [g.asum for g in gs])
 
 
 def small_gemm_ref(g: Gemm) -> torch.Tensor:

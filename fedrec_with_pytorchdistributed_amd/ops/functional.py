@@ -119,12 +119,13 @@ class AdditivePoolFn(torch.autograd.Function):
             dpre2 = dpre2.contiguous()
             x2 = x2.contiguous()
         if ctx.needs_input_grad[1]:
-            if small:
+            if small:  # with the bias gradient (column sums of dpre) from the same launch
                 dw1 = torch.empty(Q, D, device=x.device, dtype=torch.float32)
-                ops.small_gemm(ops.Gemm(dpre2, x2, dw1, Q, D, n * T, Q, D, D, a_mode=1, b_mode=1))
+                db1 = torch.empty(Q, device=x.device, dtype=torch.float32)
+                ops.small_gemm(ops.Gemm(dpre2, x2, dw1, Q, D, n * T, Q, D, D, a_mode=1, b_mode=1, asum=db1))
             else:
                 dw1 = wgrad(dpre2, x2)  # reduced over all n*T tokens (split-K on the device)
-        if ctx.needs_input_grad[2]:
+        if ctx.needs_input_grad[2] and db1 is None:
             if dsum is not None:
                 db1 = dsum
             elif small:
@@ -595,16 +596,16 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
     ops.small_gemm(ops.Gemm(dqkv, wb[:D3], dx, BH, D, D3, D3, D, D, b_mode=1, **ekw), dev_off=dev_off)
     # weight gradients in one launch: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM; X'
-    # bf16) and dW1 = dpre^T ctx (fp32 operands: the mixed-dtype kernel)
+    # bf16) and dW1 = dpre^T ctx (fp32 operands: the mixed-dtype kernel); the bias gradients
+    # (column sums of dQ|dK|dV and dpre, fp32) come out of the same launch (asum)
     gqkv = torch.empty(D3, D, device=dev)
     gw1 = torch.empty(Qd, D, device=dev)
-    ops.small_gemm(ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1),
-                   ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1))
-    gbq, gbk, gbv = (torch.empty(D, device=dev) for _ in range(3))
+    gbqkv = torch.empty(D3, device=dev)
     gb1 = torch.empty(Qd, device=dev)
-    ops.colsum_f32([(dqkv[:, 0:D], gbq, BH, D, D3), (dqkv[:, D:2 * D], gbk, BH, D, D3),
-                    (dqkv[:, 2 * D:], gbv, BH, D, D3), (dpre2, gb1, BH, Qd, Qd)])
-    return gqkv[:D], gbq, gqkv[D:2 * D], gbk, gqkv[2 * D:], gbv, gw1, gb1, dw2.view(1, -1), db2.view(1)
+    ops.small_gemm(ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
+                   ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
+    return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1, gb1, dw2.view(1, -1),
+            db2.view(1))
 
 
 class UserStepFn(torch.autograd.Function):
@@ -742,7 +743,7 @@ class HeadFCFn(torch.autograd.Function):
         dx = torch.empty(n, K, device=x.device, dtype=torch.float32)
         dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
         db = torch.empty(N, device=x.device, dtype=torch.float32)
+        # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one launch
         ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1),
-                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1))
-        ops.colsum_f32([(dy, db, n, N, N)])
+                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db))
         return dx, dw, db

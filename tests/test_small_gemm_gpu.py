@@ -158,3 +158,28 @@ def test_colsum_f32_scalar_and_vector_paths(dev):
     o = torch.zeros(800, device=dev)
     ops.colsum_f32([(Y, o, 4096, 800, 800)])
     assert torch.allclose(o, Y.double().sum(0).float(), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("ah", [False, True])
+def test_asum_column_sums_of_a(dev, tile, ah):
+    """asum (a_mode 1): the fp32 column sums of the stored-transposed A -- a weight gradient's
+    bias gradient -- from the same launch, split-K and not, next to a second desc."""
+    torch.manual_seed(10)
+    outs = []
+    gs = []
+    for (M, N, K) in ((1200, 400, 3200), (200, 400, 3200), (400, 768, 1664), (72, 40, 300)):
+        A = torch.randn(K, M, device=dev)
+        if ah:
+            A = A.to(torch.bfloat16)
+        Bm = torch.randn(K, N, device=dev).to(torch.bfloat16)
+        C = torch.zeros(M, N, device=dev)
+        a_s = torch.full((M,), float("nan"), device=dev)
+        gs.append(Gemm(A, Bm, C, M, N, K, M, N, N, a_mode=1, b_mode=1, asum=a_s))
+        outs.append((A, a_s, ops.small_gemm_ref(gs[-1])))
+    ops.small_gemm(gs[0], gs[1], tile=tile)
+    ops.small_gemm(gs[2], gs[3], tile=tile)
+    for g, (A, a_s, want) in zip(gs, outs):
+        assert _rel(g.C, want) < 2e-3
+        ref = A.double().sum(0)
+        assert torch.allclose(a_s.double(), ref, rtol=1e-5, atol=1e-3), float((a_s.double() - ref).abs().max())
