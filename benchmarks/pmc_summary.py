@@ -30,7 +30,8 @@ def family(name: str) -> str:
     m = re.search(r"gemm_nt_pp2_kernel<(\d)", name)
     if m:
         return {"0": "gemm_pp2 (QKV / out-proj / FFN2, bias)", "1": "gemm_pp2 + GELU (FFN1)"}.get(m.group(1), "gemm_pp2")
-    for key, fam in (("ln16p_kernel", "layernorm (persistent, + residual)"),
+    for key, fam in (("head_pool_bwd", "head_pool_bwd"), ("head_pool", "head_pool"), ("upool_", "user pool"),
+                     ("ln16p_kernel", "layernorm (persistent, + residual)"),
                      ("title_attn_packed_kernel", "title attention (packed)"),
                      ("gemm_nt_kernel", "gemm_nt 128x128 (text head)"),
                      ("dedup_kernel", "dedup (lookahead)"), ("sample_kernel", "sample (lookahead)"),
@@ -42,7 +43,12 @@ def family(name: str) -> str:
                      ("segsum_kernel", "news-grad segment sum")):
         if key in name:
             return fam
-    return "other"
+    # any other kernel: its name without the argument list (templates kept: they name variants)
+    short = name.replace("(anonymous namespace)::", "")
+    short = short[5:] if short.startswith("void ") else short
+    short = short.split("(")[0]
+    m = re.search(r"_GLOBAL__N_1\d+(\w+?)(I|E)", short)  # anonymous-namespace mangled names
+    return m.group(1) if m else short[:80]
 
 
 def load(path: str):

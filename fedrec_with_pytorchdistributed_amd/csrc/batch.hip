@@ -12,6 +12,8 @@
 // larger batches take the sort-based torch path on the host side of the binding.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int MAXR = 8192;
@@ -100,6 +102,145 @@ __global__ __launch_bounds__(NT) void dedup_kernel(const int* __restrict__ ids, 
   (void)part;
 }
 
+// ---------------------------------------------------------------------------------------
+// Register form (the default).  The kernel above runs all log2(P)(log2(P)+1)/2 compare-exchange
+// stages through LDS with a barrier each: 78 barriered stages at P = 4096, 56 us per step on the
+// lookahead stream.  Here thread t holds elements t + NT e (e < E) in registers, so the partner
+// i ^ j of a stage is
+//   j <  64:  lane t ^ j of the same wave, same slot  -> one shuffle, no barrier (57 of 78 stages)
+//   j >= NT:  the same thread, slot e ^ (j / NT)       -> registers (3 stages)
+//   else:     another wave                              -> LDS, double-buffered: one barrier
+// P is padded to at least NT (every thread holds E >= 1 elements; pads sort last).
+// ---------------------------------------------------------------------------------------
+template <typename KeyT>
+__device__ __forceinline__ KeyT shfl_xor_key(KeyT v, int j) {
+  if constexpr (sizeof(KeyT) == 4) {
+    return (KeyT)__shfl_xor((int)v, j, 64);
+  } else {
+    const int lo = __shfl_xor((int)(unsigned)(v & 0xffffffffull), j, 64);
+    const int hi = __shfl_xor((int)(unsigned)(v >> 32), j, 64);
+    return ((KeyT)(unsigned)hi << 32) | (KeyT)(unsigned)lo;
+  }
+}
+
+template <typename KeyT, int SHIFT, int E>
+__global__ __launch_bounds__(NT) void dedup2_kernel(const int* __restrict__ ids, int R, int* __restrict__ uniq,
+                                                    int* __restrict__ inv, int* __restrict__ perm,
+                                                    int* __restrict__ seg_ptr, int* __restrict__ u_count) {
+  constexpr int P = NT * E;
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  KeyT* buf0 = (KeyT*)dsm;
+  KeyT* buf1 = buf0 + P;
+  __shared__ int wsum[NT / 64];
+  const int tid = threadIdx.x;
+  KeyT k_[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = tid + NT * e;
+    k_[e] = i < R ? (KeyT)((((KeyT)(unsigned)ids[i]) << SHIFT) | (KeyT)(unsigned)i) : (KeyT)~(KeyT)0;
+  }
+  int pb = 0;  // LDS buffer parity
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= NT) {
+        // slot partner e ^ js with js a compile-time constant per branch (no dynamic register index)
+#pragma unroll
+        for (int js = 1; js < E; js <<= 1) {
+          if (j == NT * js) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const int ep = e ^ js;
+              if (ep > e) {
+                const int i = tid + NT * e;
+                const bool up = (i & k) == 0;
+                const KeyT a = k_[e], b = k_[ep];
+                const bool sw = (a > b) == up;
+                k_[e] = sw ? b : a;
+                k_[ep] = sw ? a : b;
+              }
+            }
+          }
+        }
+      } else if (j >= 64) {
+        KeyT* bs = pb ? buf1 : buf0;
+        pb ^= 1;
+#pragma unroll
+        for (int e = 0; e < E; ++e) bs[tid + NT * e] = k_[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = tid + NT * e;
+          const KeyT b = bs[i ^ j];
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          k_[e] = keep_min ? (b < k_[e] ? b : k_[e]) : (b > k_[e] ? b : k_[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = tid + NT * e;
+          const KeyT b = shfl_xor_key(k_[e], j);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          k_[e] = keep_min ? (b < k_[e] ? b : k_[e]) : (b > k_[e] ? b : k_[e]);
+        }
+      }
+    }
+  }
+  KeyT* key = pb ? buf1 : buf0;  // a buffer no thread can still be reading (the last LDS stage used the other)
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E; ++e) key[tid + NT * e] = k_[e];
+  __syncthreads();
+  // flags + block scan over contiguous runs, as dedup_kernel
+  const int EC = (R + NT - 1) / NT;
+  const int b0 = tid * EC;
+  int cnt = 0;
+  for (int e = 0; e < EC; ++e) {
+    const int i = b0 + e;
+    if (i < R) cnt += (i == 0 || (key[i] >> SHIFT) != (key[i - 1] >> SHIFT)) ? 1 : 0;
+  }
+  const int lane = tid & 63, w = tid >> 6;
+  int x = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (w == 0) {
+    int s = lane < NT / 64 ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(s, o, 64);
+      if (lane >= o) s += y;
+    }
+    if (lane < NT / 64) wsum[lane] = s;
+  }
+  __syncthreads();
+  int run = x - cnt + (w > 0 ? wsum[w - 1] : 0);
+  for (int e = 0; e < EC; ++e) {
+    const int i = b0 + e;
+    if (i >= R) break;
+    const int id = (int)(key[i] >> SHIFT);
+    const int r = (int)(key[i] & (KeyT)(((KeyT)1 << SHIFT) - 1));
+    const bool f = (i == 0 || (key[i] >> SHIFT) != (key[i - 1] >> SHIFT));
+    if (f) {
+      uniq[run] = id;
+      seg_ptr[run] = i;
+      ++run;
+    }
+    perm[i] = r;
+    inv[r] = run - 1;
+  }
+  if (tid == NT - 1) {
+    const int U = wsum[NT / 64 - 1];
+    *u_count = U;
+    seg_ptr[U] = R;
+  }
+}
+
+int g_dedup_variant = -1;  // FEDREC_DEDUP: 1 = register bitonic (default), 0 = the LDS form
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -165,6 +306,30 @@ extern "C" int fr_dedup(const int* ids, int R, int num_news, int* uniq, int* inv
   if (R > MAXR || R < 1) return 1;
   int P = 1;
   while (P < R) P <<= 1;
+  if (g_dedup_variant < 0) {
+    const char* e = getenv("FEDREC_DEDUP");
+    g_dedup_variant = e != nullptr ? atoi(e) : 1;
+  }
+  const bool narrow = num_news > 0 && num_news <= (1 << 19);
+  const int E = P <= NT ? 1 : P / NT;
+  const size_t lds = 2 * (size_t)NT * E * (narrow ? 4 : 8);  // two key buffers
+  if (g_dedup_variant != 0 && lds <= 65536) {
+#define DEDUP2(KT, SH, EE)                                                                                    \
+  hipLaunchKernelGGL((dedup2_kernel<KT, SH, EE>), dim3(1), dim3(NT), lds, s, ids, R, uniq, inv, perm, seg_ptr, \
+                     u_count)
+#define DEDUP2_E(KT, SH)        \
+  do {                          \
+    if (E == 1) DEDUP2(KT, SH, 1); \
+    else if (E == 2) DEDUP2(KT, SH, 2); \
+    else if (E == 4) DEDUP2(KT, SH, 4); \
+    else DEDUP2(KT, SH, 8);     \
+  } while (0)
+    if (narrow) DEDUP2_E(unsigned, 13);
+    else DEDUP2_E(unsigned long long, 32);
+#undef DEDUP2_E
+#undef DEDUP2
+    return 0;
+  }
   if (num_news > 0 && num_news <= (1 << 19))  // 13 bits of occurrence index (MAXR = 8192)
     hipLaunchKernelGGL((dedup_kernel<unsigned, 13>), dim3(1), dim3(NT), 0, s, ids, R, P, uniq, inv, perm, seg_ptr,
                        u_count);

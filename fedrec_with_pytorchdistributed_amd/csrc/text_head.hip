@@ -53,6 +53,15 @@ __device__ __forceinline__ const bf16* hrow(const bf16* __restrict__ table, cons
   return table + ((size_t)id * T + t) * D;
 }
 
+// LDS accesses as opaque asm: a builtin LDS access after a glds into the same LDS object makes
+// the compiler drain vmcnt -- every in-flight stage (gemm_wgrad.hip); completion is ours to wait
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4_t lds_read128(uint32_t addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
 // =========================================================================================
 // head_score: e = tanh(X W1^T + b1) (bf16, optional), a = e . w2 + b2 (fp32, from the fp32 e)
 // 128 rows x Q columns per block, BK = 64, 512 threads = 8 waves as 2 (rows) x 4 (columns):
@@ -172,6 +181,169 @@ __global__ __launch_bounds__(512, 1) void head_score_kernel(const bf16* __restri
   __syncthreads();
   if (tid < 128 && m0 + tid < M)
     a_out[m0 + tid] = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]) + b2[0];
+}
+
+// -----------------------------------------------------------------------------------------
+// head_score2: the same product with the row tile (32 RF rows), the k-tile (BK) and the depth
+// of the LDS pipeline (NST stages, NST - 2 in flight while the MFMAs read one) as parameters.
+// A stage is XP + WP "pieces" of one wave-instruction each (64 lanes x 16 B = RPP rows of BK
+// bf16); wave w issues pieces w, w + 8, ... and pads to PPW pieces with duplicates of the
+// first ones (identical bytes to the same LDS address), so every wave counts the same glds per
+// stage and the waits are counted (vmcnt) rather than drains.  LDS reads are opaque asm (a
+// builtin LDS read after a glds makes the compiler drain vmcnt).  Rows of BK = 32 stages are
+// 64 B: chunk c of row r at c ^ ((r >> 2) & 3) keeps a 16-lane ds_read_b128 group on 64
+// distinct banks; BK = 64 keeps the 128-B rows and c ^ (r & 7) of head_score_kernel.
+// -----------------------------------------------------------------------------------------
+template <int BK>
+__device__ __forceinline__ int hs_swz(int r) {
+  return BK == 64 ? (r & 7) : ((r >> 2) & 3);
+}
+
+template <int N>
+__device__ __forceinline__ void hs_wait_sync() {  // this wave's stage landed except N younger glds, then barrier
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int QF, int RF, int BK, int NST>
+__global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
+                                                             int M, int T, int D, const bf16* __restrict__ W1,
+                                                             const float* __restrict__ b1, const float* __restrict__ w2,
+                                                             const float* __restrict__ b2, bf16* __restrict__ e_out,
+                                                             float* __restrict__ a_out) {
+  constexpr int Q = QF * 64;
+  constexpr int MR = 32 * RF;       // rows per block
+  constexpr int RB = BK * 2;        // LDS row bytes
+  constexpr int CPR = BK / 8;       // 16-B chunks per row
+  constexpr int RPP = 64 / CPR;     // rows per piece
+  constexpr int XP = MR / RPP, PT = XP + Q / RPP;
+  constexpr int PPW = (PT + 7) / 8;
+  constexpr int ST = (MR + Q) * RB;
+  constexpr int KS = BK / 32;       // MFMA k-steps per stage
+  static_assert(MR % RPP == 0 && Q % RPP == 0 && PT >= 8, "piece tiling");
+  __shared__ __attribute__((aligned(16))) char smem[NST * ST];
+  const int m0 = blockIdx.x * MR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wq = wave & 3;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+
+  const bf16* src[PPW];
+  uint32_t dst[PPW];
+  {
+    const int lr = lane / CPR, pc = lane % CPR;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int p = wave + 8 * i;
+      p = p < PT ? p : p - PT;
+      if (p < XP) {
+        const int r = p * RPP + lr;
+        int gm = m0 + r;
+        gm = gm < M ? gm : M - 1;  // rows past M: any valid row (outputs masked)
+        src[i] = hrow(table, ids, gm, T, D) + (pc ^ hs_swz<BK>(r)) * 8;
+        dst[i] = (uint32_t)(p * RPP * RB);
+      } else {
+        const int r = (p - XP) * RPP + lr;
+        src[i] = W1 + (size_t)r * D + (pc ^ hs_swz<BK>(r)) * 8;
+        dst[i] = (uint32_t)((MR + (p - XP) * RPP) * RB);
+      }
+    }
+  }
+  auto issue = [&](int stage, int k0) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src[i] + k0),
+                                       LDS_PTR(void, smem + stage * ST + dst[i]), 16, 0, 0);
+  };
+
+  f32x4 acc[QF][RF];
+#pragma unroll
+  for (int i = 0; i < QF; ++i)
+#pragma unroll
+    for (int j = 0; j < RF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = D / BK;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, s * BK);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed (every wave), every wave done with stage kt - 1
+    const int younger = nk - 1 - kt;  // stages issued after kt, at most NST - 2
+    if (NST >= 4 && younger >= 2) hs_wait_sync<(NST >= 4 ? 2 * PPW : 0)>();
+    else if (NST >= 3 && younger >= 1) hs_wait_sync<(NST >= 3 ? PPW : 0)>();
+    else hs_wait_sync<0>();
+    if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, (kt + NST - 1) * BK);
+    const uint32_t As = lds0 + (kt % NST) * ST, Ws = As + MR * RB;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int lc = kk * 4 + fq;
+      u32x4_t xr[RF], wr[QF];
+#pragma unroll
+      for (int j = 0; j < RF; ++j) {
+        const int r = wm * 16 * RF + j * 16 + fr;
+        xr[j] = lds_read128(As + r * RB + ((lc ^ hs_swz<BK>(r)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < QF; ++i) {
+        const int r = wq * QF * 16 + i * 16 + fr;
+        wr[i] = lds_read128(Ws + r * RB + ((lc ^ hs_swz<BK>(r)) << 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < RF; ++j) asm volatile("" : "+v"(xr[j]));  // uses stay after the wait
+#pragma unroll
+      for (int i = 0; i < QF; ++i) asm volatile("" : "+v"(wr[i]));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < QF; ++i)
+#pragma unroll
+        for (int j = 0; j < RF; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wr[i]),
+                                                              __builtin_bit_cast(bf16x8, xr[j]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  __syncthreads();  // every wave done reading the last stage before the reduction buffer reuses it
+
+  float part[RF];
+#pragma unroll
+  for (int j = 0; j < RF; ++j) part[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < QF; i += 2) {
+    float v[2][RF][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int qb = wq * QF * 16 + (i + h) * 16 + fq * 4;
+      const float4 bb = *(const float4*)(b1 + qb);
+      const float4 ww = *(const float4*)(w2 + qb);
+#pragma unroll
+      for (int j = 0; j < RF; ++j) {
+        v[h][j][0] = tanh_fast(acc[i + h][j][0] + bb.x);
+        v[h][j][1] = tanh_fast(acc[i + h][j][1] + bb.y);
+        v[h][j][2] = tanh_fast(acc[i + h][j][2] + bb.z);
+        v[h][j][3] = tanh_fast(acc[i + h][j][3] + bb.w);
+        part[j] += v[h][j][0] * ww.x + v[h][j][1] * ww.y + v[h][j][2] * ww.z + v[h][j][3] * ww.w;
+      }
+    }
+    if (e_out != nullptr) {
+#pragma unroll
+      for (int j = 0; j < RF; ++j) {
+        const int m = m0 + wm * 16 * RF + j * 16 + fr;
+        store_pair16_if(e_out + (size_t)(m < M ? m : 0) * Q + wq * QF * 16 + i * 16, v[0][j], v[1][j], fq, m < M);
+      }
+    }
+  }
+  float* red = (float*)smem;
+#pragma unroll
+  for (int j = 0; j < RF; ++j) {
+    const float s = group4_sum(part[j]);
+    if (fq == 0) red[wq * MR + wm * 16 * RF + j * 16 + fr] = s;
+  }
+  __syncthreads();
+  if (tid < MR && m0 + tid < M)
+    a_out[m0 + tid] = (red[tid] + red[MR + tid]) + (red[2 * MR + tid] + red[3 * MR + tid]) + b2[0];
 }
 
 // =========================================================================================
@@ -299,6 +471,157 @@ __global__ __launch_bounds__(256) void head_pool_bwd_kernel(const bf16* __restri
   }
 }
 
+// -----------------------------------------------------------------------------------------
+// Load-first forms of the two pool kernels (the default).  The kernels above start streaming a
+// title's 76.8 KB only after a serial prologue (the softmax behind a barrier; the g . x_t wave
+// sums one token after another), so a block keeps a few 16-B loads in flight at a time: 26 and
+// 31 us per step for what is one 121 MB sweep each.  Here every thread issues ALL of its X
+// chunks first (TPT / TPW registers of 16 B), then works on them:
+//   head_pool2      the softmax runs in every wave (no barrier before the weights), a token's
+//                   weight reaches the lanes by ds_bpermute; then the t-group sums via LDS.
+//   head_pool_bwd2  six waves over tokens t = w, w + 6, ...; the per-token wave sums are
+//                   independent chains the compiler interleaves.
+// Both keep the summation orders of the forms above (bit-identical outputs).
+// -----------------------------------------------------------------------------------------
+template <int TPT>
+__global__ __launch_bounds__(384) void head_pool2_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
+                                                         const float* __restrict__ a, const int* __restrict__ tokens,
+                                                         int T, int D, float* __restrict__ pooled,
+                                                         float* __restrict__ alpha) {
+  __shared__ float part[3072];
+  const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int id = ids != nullptr ? ids[u] : u;
+  const bf16* xe = table + (size_t)id * T * D;
+  const int DC = D >> 3, TG = 384 / DC;
+  const int dc = tid % DC, tgr = tid / DC;
+  const int tg = tgr < TG ? tgr : TG - 1;  // spare threads (384 % DC != 0) load a valid row, store nothing
+  bf16x8 v[TPT];
+#pragma unroll
+  for (int i = 0; i < TPT; ++i) {
+    const int t = tg + TG * i;
+    v[i] = *(const bf16x8*)(xe + (size_t)(t < T ? t : T - 1) * D + dc * 8);
+  }
+  float av[2], m = -INFINITY;
+  bool keep[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int t = lane + 64 * c;
+    keep[c] = t < T && (tokens == nullptr || tokens[((size_t)id * 2 + 1) * T + t] != 0);
+    av[c] = keep[c] ? a[(size_t)u * T + t] : -INFINITY;
+    m = fmaxf(m, av[c]);
+  }
+  m = wave_max(m);
+  if (!(m > -INFINITY)) m = 0.f;
+  float p[2], l = 0.f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    p[c] = keep[c] ? __expf(av[c] - m) : 0.f;
+    l += p[c];
+  }
+  const float inv = 1.0f / (wave_sum(l) + 1e-8f * __expf(-m));
+  const float al0 = p[0] * inv, al1 = p[1] * inv;
+  if (wave == 0) {
+    if (lane < T) alpha[(size_t)u * T + lane] = al0;
+    if (lane + 64 < T) alpha[(size_t)u * T + lane + 64] = al1;
+  }
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < TPT; ++i) {
+    const int t = tg + TG * i;
+    const float w0 = __shfl(al0, t & 63, 64), w1 = __shfl(al1, t & 63, 64);
+    const float w = t < T ? (t < 64 ? w0 : w1) : 0.f;
+    if (t < T) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += w * (float)v[i][k];
+    }
+  }
+  if (tgr < TG) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[tg * D + dc * 8 + k] = acc[k];
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += 384) {
+    float s = 0.f;
+    for (int j = 0; j < TG; ++j) s += part[j * D + d];
+    pooled[(size_t)u * D + d] = s;
+  }
+}
+
+template <int TPW>
+__global__ __launch_bounds__(384) void head_pool_bwd2_kernel(const bf16* __restrict__ table,
+                                                             const int* __restrict__ ids,
+                                                             const float* __restrict__ alpha,
+                                                             const float* __restrict__ g, int T, int D,
+                                                             float* __restrict__ da, float* __restrict__ db2p) {
+  __shared__ float dal[MAXT];
+  const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int id = ids != nullptr ? ids[u] : u;
+  const bf16* xe = table + (size_t)id * T * D;
+  const float* gu = g + (size_t)u * D;
+  const int DC = D >> 3;
+  bf16x8 v[TPW][2];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = wave + 6 * i;
+    const bf16* row = xe + (size_t)(t < T ? t : T - 1) * D;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int dc = lane + 64 * c;
+      v[i][c] = *(const bf16x8*)(row + (dc < DC ? dc : 0) * 8);
+    }
+  }
+  float gv[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int dc = lane + 64 * c;
+    const float4 g0 = dc < DC ? *(const float4*)(gu + dc * 8) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g1 = dc < DC ? *(const float4*)(gu + dc * 8 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
+    gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
+  }
+  float s[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    s[i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (lane + 64 * c < DC) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[i] += (float)v[i][c][k] * gv[c][k];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) s[i] = wave_sum(s[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i)
+      if (wave + 6 * i < T) dal[wave + 6 * i] = s[i];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float al[2], dv[2], sm = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      al[c] = t < T ? alpha[(size_t)u * T + t] : 0.f;
+      dv[c] = t < T ? dal[t] : 0.f;
+      sm += al[c] * dv[c];
+    }
+    sm = wave_sum(sm);
+    float sd = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      const float val = al[c] * (dv[c] - sm);
+      if (t < T) da[(size_t)u * T + t] = val;
+      sd += val;
+    }
+    sd = wave_sum(sd);
+    if (lane == 0) db2p[u] = sd;
+  }
+}
+
 // =========================================================================================
 // head_wgrad: P[s][q][k] = sum_{m in split s} g_mq x_mk with g = da_m (1 - e_mq^2), formed in
 // the LDS pipeline; dw2 / dsum partials [s][q] from blocks of the first k tile.
@@ -318,17 +641,10 @@ constexpr int DA_BYTES = 8 * 64 * 4;           // 2 KB
 constexpr int WSTAGE = E_BYTES + X_BYTES + DA_BYTES;
 constexpr int MAX_SPLIT_TITLES = 1024;  // title ids of one split, staged in LDS up front
 
-// LDS accesses as opaque asm: a builtin LDS access after a glds into the same LDS object makes
-// the compiler drain vmcnt -- every in-flight stage (gemm_wgrad.hip); completion is ours to wait
+// (more opaque LDS accesses, see lds_read128)
 __device__ __forceinline__ s16x4 tr_read(uint32_t addr) {
   s16x4 v;
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4_t lds_read128(uint32_t addr) {
-  u32x4_t v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
   return v;
 }
 __device__ __forceinline__ float lds_read32(uint32_t addr) {
@@ -862,6 +1178,8 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const f32x4* __restric
 int g_cus = 0;
 int g_wg_variant = -1;  // FEDREC_HEAD_WG: bit 0 = no e -> g transform (diagnostic timing only)
 int g_wg_splits = -1;   // FEDREC_HEAD_SPLITS: split-K count override (A/B runs)
+int g_score_variant = -1;  // FEDREC_HEAD_SCORE: head_score2 tilings (A/B), 0 = head_score_kernel
+int g_pool_variant = -1;  // FEDREC_HEAD_POOL: 1 = load-first pool kernels (default), 0 = the first forms
 
 int env_int(const char* k, int d) {
   const char* v = getenv(k);
@@ -880,6 +1198,20 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   if (!fr_head_supported(D, Q, T)) return 1;
   const int M = U * T;
   if (M == 0) return 0;
+  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 0);
+  // FEDREC_HEAD_SCORE (Q = 384): 1 -> 128 rows, BK 32, 4 stages; 2 -> 192 rows, BK 64, 2 stages;
+  // 3 -> 128 rows, BK 64, 2 stages (head_score2 form of the default); 4 -> 192 rows, BK 32, 3 stages
+  if (Q == 384 && g_score_variant > 0) {
+#define LAUNCH_S2(RF, BK, NST)                                                                                   \
+  hipLaunchKernelGGL((head_score2_kernel<6, RF, BK, NST>), dim3((M + 32 * RF - 1) / (32 * RF)), dim3(512), 0, s, \
+                     (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out)
+    if (g_score_variant == 1) LAUNCH_S2(4, 32, 4);
+    else if (g_score_variant == 2) LAUNCH_S2(6, 64, 2);
+    else if (g_score_variant == 3) LAUNCH_S2(4, 64, 2);
+    else LAUNCH_S2(6, 32, 3);
+#undef LAUNCH_S2
+    return 0;
+  }
   const dim3 grid((M + 127) / 128);
 #define LAUNCH_SCORE(QF)                                                                                          \
   hipLaunchKernelGGL(head_score_kernel<QF>, grid, dim3(512), 0, s, (const bf16*)table, ids, M, T, D,             \
@@ -895,6 +1227,18 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, c
                             float* pooled, float* alpha, hipStream_t s) {
   if (T > MAXT || D % 8 != 0 || D / 8 > 384) return 1;
   if (U == 0) return 0;
+  if (g_pool_variant < 0) g_pool_variant = env_int("FEDREC_HEAD_POOL", 1);
+  const int TG = 384 / (D / 8), tpt = (T + TG - 1) / TG;
+  if (g_pool_variant != 0 && D <= 3072 && tpt <= 32) {
+#define LAUNCH_POOL2(N)                                                                                          \
+  hipLaunchKernelGGL(head_pool2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, tokens, T, D, \
+                     pooled, alpha)
+    if (tpt <= 13) LAUNCH_POOL2(13);
+    else if (tpt <= 16) LAUNCH_POOL2(16);
+    else LAUNCH_POOL2(32);
+#undef LAUNCH_POOL2
+    return 0;
+  }
   hipLaunchKernelGGL(head_pool_kernel, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, tokens, T, D, pooled,
                      alpha);
   return 0;
@@ -904,6 +1248,18 @@ extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* 
                                 int D, float* da, float* db2p, hipStream_t s) {
   if (T > MAXT || D % 8 != 0 || D / 8 > 128) return 1;
   if (U == 0) return 0;
+  if (g_pool_variant < 0) g_pool_variant = env_int("FEDREC_HEAD_POOL", 1);
+  const int tpw = (T + 5) / 6;
+  if (g_pool_variant != 0 && tpw <= 22) {
+#define LAUNCH_PBWD2(N)                                                                                           \
+  hipLaunchKernelGGL(head_pool_bwd2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, alpha, g, T, D, \
+                     da, db2p)
+    if (tpw <= 9) LAUNCH_PBWD2(9);
+    else if (tpw <= 11) LAUNCH_PBWD2(11);
+    else LAUNCH_PBWD2(22);
+#undef LAUNCH_PBWD2
+    return 0;
+  }
   hipLaunchKernelGGL(head_pool_bwd_kernel, dim3(U), dim3(256), 0, s, (const bf16*)table, ids, alpha, g, T, D, da,
                      db2p);
   return 0;

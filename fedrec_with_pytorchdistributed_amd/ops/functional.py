@@ -544,6 +544,9 @@ class EmbedLNFn(torch.autograd.Function):
 # pool -> sigmoid-CE, and a hand-written backward.  Every GEMM is csrc/small_gemm.hip, every
 # bias gradient the deterministic colsum, the per-news reduction (+ LDP) the segment sum.
 # ---------------------------------------------------------------------------------------
+_USER_BWD_SPLIT = __import__("os").environ.get("FEDREC_USER_BWD_SPLIT", "0") == "1"  # A/B switch
+
+
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
     """Device user encoder forward over history rows ``src[idx]`` (``src [*, D]`` fp32, ``idx``
     int32 [B*H]) -> ``(u [B, D] fp32, saved)``.
@@ -594,16 +597,22 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,
     # the dropout backward in its epilogue
     ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
-    ops.small_gemm(ops.Gemm(dqkv, wb[:D3], dx, BH, D, D3, D3, D, D, b_mode=1, **ekw), dev_off=dev_off)
-    # weight gradients in one launch: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM; X'
-    # bf16) and dW1 = dpre^T ctx (fp32 operands: the mixed-dtype kernel); the bias gradients
-    # (column sums of dQ|dK|dV and dpre, fp32) come out of the same launch (asum)
+    dgrad = ops.Gemm(dqkv, wb[:D3], dx, BH, D, D3, D3, D, D, b_mode=1, **ekw)
+    # weight gradients: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM; X' bf16) and dW1 =
+    # dpre^T ctx (fp32 operands: the mixed-dtype kernel); the bias gradients (column sums of
+    # dQ|dK|dV and dpre, fp32) come out of the same launch (asum).  The input gradient has no
+    # dependence on them: all three share ONE launch (FEDREC_USER_BWD_SPLIT=1: two launches)
     gqkv = torch.empty(D3, D, device=dev)
     gw1 = torch.empty(Qd, D, device=dev)
     gbqkv = torch.empty(D3, device=dev)
     gb1 = torch.empty(Qd, device=dev)
-    ops.small_gemm(ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
-                   ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
+    wg = (ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
+          ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
+    if _USER_BWD_SPLIT:
+        ops.small_gemm(dgrad, dev_off=dev_off)
+        ops.small_gemm(*wg)
+    else:
+        ops.small_gemm(dgrad, *wg, dev_off=dev_off)
     return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1, gb1, dw2.view(1, -1),
             db2.view(1))
 

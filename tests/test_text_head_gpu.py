@@ -38,7 +38,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("U,T,masked", [(257, 50, False), (257, 50, True), (40, 17, False), (3, 50, False),
-                                        (1664, 50, False)])
+                                        (1664, 50, False), (40, 64, False), (30, 100, True), (20, 128, False)])
 def test_fused_text_head_matches_fp32_oracle(dev, U, T, masked):
     g = torch.Generator(device="cpu").manual_seed(U * 100 + T)
     N, D, Q = 300, 768, 384
