@@ -43,7 +43,8 @@ int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const
 int fr_head_supported(int D, int Q, int T);
 int fr_head_score(const void* table, const int* ids, int U, int T, int D, int Q, const void* W1, const float* b1,
                   const float* w2, const float* b2, void* e_out, float* a_out, hipStream_t s);
-int fr_head_pool(const void* table, const int* ids, const float* a, const int* tokens, int U, int T, int D,
+int fr_head_score_slices(int Q);
+int fr_head_pool(const void* table, const int* ids, const float* a, int slices, const int* tokens, int U, int T, int D,
                  float* pooled, float* alpha, hipStream_t s);
 int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, const float* g, int U, int T, int D,
                      float* da, float* db2p, hipStream_t s);
@@ -489,7 +490,10 @@ std::tuple<at::Tensor, at::Tensor> head_score(const at::Tensor& table, const c10
   // ids come from the dedup over [0, N) by construction)
   const c10::DeviceGuard g(table.device());
   auto e = store_e ? at::empty({U * T, Q}, table.options()) : at::empty({0}, table.options());
-  auto a = at::empty({U * T}, table.options().dtype(at::kFloat));
+  // [slices, U*T]: partial scores per Q slice of the tiling (summed by head_pool); 1 slice -> [U*T]
+  const int slices = fr_head_score_slices((int)Q);
+  auto a = slices > 1 ? at::empty({slices, U * T}, table.options().dtype(at::kFloat))
+                      : at::empty({U * T}, table.options().dtype(at::kFloat));
   check_rc(fr_head_score(table.data_ptr(), opt_int_ptr(ids), (int)U, (int)T, (int)D, (int)Q, w1.data_ptr(),
                          b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
                          store_e ? e.data_ptr() : nullptr, a.data_ptr<float>(), cur_stream()),
@@ -501,7 +505,9 @@ std::tuple<at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10:
                                              const at::Tensor& a, const c10::optional<at::Tensor>& tokens) {
   const int64_t U = head_titles(table, ids, T), D = table.size(1);
   check_dev(a, "a");
-  TORCH_CHECK(a.scalar_type() == at::kFloat && a.numel() == U * T && a.is_contiguous(), "fedrec::head_pool: a [U*T] fp32");
+  TORCH_CHECK(a.scalar_type() == at::kFloat && (a.numel() == U * T || (a.dim() == 2 && a.size(0) == 2 && a.size(1) == U * T)) &&
+                  a.is_contiguous(),
+              "fedrec::head_pool: a [U*T] (or [2, U*T] score partials) fp32");
   if (tokens.has_value()) {
     check_dev(*tokens, "tokens");
     TORCH_CHECK(tokens->scalar_type() == at::kInt && tokens->dim() == 3 && tokens->size(1) == 2 &&
@@ -511,7 +517,8 @@ std::tuple<at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10:
   const c10::DeviceGuard g(table.device());
   auto pooled = at::empty({U, D}, a.options());
   auto alpha = at::empty({U, T}, a.options());
-  check_rc(fr_head_pool(table.data_ptr(), opt_int_ptr(ids), a.data_ptr<float>(), opt_int_ptr(tokens), (int)U, (int)T,
+  check_rc(fr_head_pool(table.data_ptr(), opt_int_ptr(ids), a.data_ptr<float>(), a.dim() == 2 ? (int)a.size(0) : 1,
+                        opt_int_ptr(tokens), (int)U, (int)T,
                         (int)D, pooled.data_ptr<float>(), alpha.data_ptr<float>(), cur_stream()),
            "head_pool");
   return {pooled, alpha};

@@ -207,13 +207,27 @@ __device__ __forceinline__ void hs_wait_sync() {  // this wave's stage landed ex
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int QF, int RF, int BK, int NST>
+//
+// Q slices (gridDim.y > 1): block (x, y) computes columns [y Q, (y + 1) Q) of e (row stride ldq)
+// and the partial score sum_{q in slice} w2_q tanh(.) into a_out[y M + m] (b2 in slice 0); the
+// pool adds the slices.  Halving the W1 panel per block (192 of 384 columns) frees the LDS for a
+// third stage: two stages in flight while the MFMAs read one.
+template <int QF, int RF, int BK, int NST, int WQ = 4>
 __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
                                                              int M, int T, int D, const bf16* __restrict__ W1,
                                                              const float* __restrict__ b1, const float* __restrict__ w2,
                                                              const float* __restrict__ b2, bf16* __restrict__ e_out,
-                                                             float* __restrict__ a_out) {
+                                                             float* __restrict__ a_out, int ldq) {
   constexpr int Q = QF * 64;
+  {
+    const int qs = blockIdx.y;
+    W1 += (size_t)qs * Q * D;
+    b1 += qs * Q;
+    w2 += qs * Q;
+    if (e_out != nullptr) e_out += qs * Q;
+    a_out += (size_t)qs * M;
+  }
+  const float b2v = blockIdx.y == 0 ? b2[0] : 0.f;
   constexpr int MR = 32 * RF;       // rows per block
   constexpr int RB = BK * 2;        // LDS row bytes
   constexpr int CPR = BK / 8;       // 16-B chunks per row
@@ -222,11 +236,15 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
   constexpr int PPW = (PT + 7) / 8;
   constexpr int ST = (MR + Q) * RB;
   constexpr int KS = BK / 32;       // MFMA k-steps per stage
+  constexpr int WMN = 8 / WQ;       // waves along the rows
+  constexpr int QFW = Q / 16 / WQ;  // 16-column fragments per wave
+  constexpr int RFW = MR / 16 / WMN;  // 16-row fragments per wave
+  static_assert(QFW % 2 == 0 && QFW * 16 * WQ == Q && RFW * 16 * WMN == MR, "wave tiling");
   static_assert(MR % RPP == 0 && Q % RPP == 0 && PT >= 8, "piece tiling");
   __shared__ __attribute__((aligned(16))) char smem[NST * ST];
   const int m0 = blockIdx.x * MR;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wq = wave & 3;
+  const int wm = wave / WQ, wq = wave % WQ;
   const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
 
   const bf16* src[PPW];
@@ -257,11 +275,11 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
                                        LDS_PTR(void, smem + stage * ST + dst[i]), 16, 0, 0);
   };
 
-  f32x4 acc[QF][RF];
+  f32x4 acc[QFW][RFW];
 #pragma unroll
-  for (int i = 0; i < QF; ++i)
+  for (int i = 0; i < QFW; ++i)
 #pragma unroll
-    for (int j = 0; j < RF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < RFW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = D / BK;
 #pragma unroll
@@ -279,27 +297,27 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       const int lc = kk * 4 + fq;
-      u32x4_t xr[RF], wr[QF];
+      u32x4_t xr[RFW], wr[QFW];
 #pragma unroll
-      for (int j = 0; j < RF; ++j) {
-        const int r = wm * 16 * RF + j * 16 + fr;
+      for (int j = 0; j < RFW; ++j) {
+        const int r = wm * 16 * RFW + j * 16 + fr;
         xr[j] = lds_read128(As + r * RB + ((lc ^ hs_swz<BK>(r)) << 4));
       }
 #pragma unroll
-      for (int i = 0; i < QF; ++i) {
-        const int r = wq * QF * 16 + i * 16 + fr;
+      for (int i = 0; i < QFW; ++i) {
+        const int r = wq * QFW * 16 + i * 16 + fr;
         wr[i] = lds_read128(Ws + r * RB + ((lc ^ hs_swz<BK>(r)) << 4));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int j = 0; j < RF; ++j) asm volatile("" : "+v"(xr[j]));  // uses stay after the wait
+      for (int j = 0; j < RFW; ++j) asm volatile("" : "+v"(xr[j]));  // uses stay after the wait
 #pragma unroll
-      for (int i = 0; i < QF; ++i) asm volatile("" : "+v"(wr[i]));
+      for (int i = 0; i < QFW; ++i) asm volatile("" : "+v"(wr[i]));
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < QF; ++i)
+      for (int i = 0; i < QFW; ++i)
 #pragma unroll
-        for (int j = 0; j < RF; ++j)
+        for (int j = 0; j < RFW; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wr[i]),
                                                               __builtin_bit_cast(bf16x8, xr[j]), acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
@@ -307,19 +325,19 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
   }
   __syncthreads();  // every wave done reading the last stage before the reduction buffer reuses it
 
-  float part[RF];
+  float part[RFW];
 #pragma unroll
-  for (int j = 0; j < RF; ++j) part[j] = 0.f;
+  for (int j = 0; j < RFW; ++j) part[j] = 0.f;
 #pragma unroll
-  for (int i = 0; i < QF; i += 2) {
-    float v[2][RF][4];
+  for (int i = 0; i < QFW; i += 2) {
+    float v[2][RFW][4];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int qb = wq * QF * 16 + (i + h) * 16 + fq * 4;
+      const int qb = wq * QFW * 16 + (i + h) * 16 + fq * 4;
       const float4 bb = *(const float4*)(b1 + qb);
       const float4 ww = *(const float4*)(w2 + qb);
 #pragma unroll
-      for (int j = 0; j < RF; ++j) {
+      for (int j = 0; j < RFW; ++j) {
         v[h][j][0] = tanh_fast(acc[i + h][j][0] + bb.x);
         v[h][j][1] = tanh_fast(acc[i + h][j][1] + bb.y);
         v[h][j][2] = tanh_fast(acc[i + h][j][2] + bb.z);
@@ -329,21 +347,25 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
     }
     if (e_out != nullptr) {
 #pragma unroll
-      for (int j = 0; j < RF; ++j) {
-        const int m = m0 + wm * 16 * RF + j * 16 + fr;
-        store_pair16_if(e_out + (size_t)(m < M ? m : 0) * Q + wq * QF * 16 + i * 16, v[0][j], v[1][j], fq, m < M);
+      for (int j = 0; j < RFW; ++j) {
+        const int m = m0 + wm * 16 * RFW + j * 16 + fr;
+        store_pair16_if(e_out + (size_t)(m < M ? m : 0) * ldq + wq * QFW * 16 + i * 16, v[0][j], v[1][j], fq, m < M);
       }
     }
   }
   float* red = (float*)smem;
 #pragma unroll
-  for (int j = 0; j < RF; ++j) {
+  for (int j = 0; j < RFW; ++j) {
     const float s = group4_sum(part[j]);
-    if (fq == 0) red[wq * MR + wm * 16 * RF + j * 16 + fr] = s;
+    if (fq == 0) red[wq * MR + wm * 16 * RFW + j * 16 + fr] = s;
   }
   __syncthreads();
-  if (tid < MR && m0 + tid < M)
-    a_out[m0 + tid] = (red[tid] + red[MR + tid]) + (red[2 * MR + tid] + red[3 * MR + tid]) + b2[0];
+  if (tid < MR && m0 + tid < M) {
+    float sa;
+    if constexpr (WQ == 4) sa = (red[tid] + red[MR + tid]) + (red[2 * MR + tid] + red[3 * MR + tid]);
+    else sa = red[tid] + red[MR + tid];
+    a_out[m0 + tid] = sa + b2v;
+  }
 }
 
 // =========================================================================================
@@ -352,7 +374,8 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
 // D/8 column chunks of 16 B.
 // =========================================================================================
 __global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
-                                                        const float* __restrict__ a, const int* __restrict__ tokens,
+                                                        const float* __restrict__ a, const float* __restrict__ a2,
+                                                        const int* __restrict__ tokens,
                                                         int T, int D, float* __restrict__ pooled,
                                                         float* __restrict__ alpha) {
   __shared__ float a_s[MAXT];
@@ -367,7 +390,7 @@ __global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__
     for (int c = 0; c < 2; ++c) {
       const int t = lane + 64 * c;
       keep[c] = t < T && (tokens == nullptr || tokens[((size_t)id * 2 + 1) * T + t] != 0);
-      av[c] = keep[c] ? a[(size_t)u * T + t] : -INFINITY;
+      av[c] = keep[c] ? (a2 != nullptr ? a[(size_t)u * T + t] + a2[(size_t)u * T + t] : a[(size_t)u * T + t]) : -INFINITY;
       m = fmaxf(m, av[c]);
     }
     m = wave_max(m);
@@ -485,7 +508,8 @@ __global__ __launch_bounds__(256) void head_pool_bwd_kernel(const bf16* __restri
 // -----------------------------------------------------------------------------------------
 template <int TPT>
 __global__ __launch_bounds__(384) void head_pool2_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
-                                                         const float* __restrict__ a, const int* __restrict__ tokens,
+                                                         const float* __restrict__ a, const float* __restrict__ a2,
+                                                         const int* __restrict__ tokens,
                                                          int T, int D, float* __restrict__ pooled,
                                                          float* __restrict__ alpha) {
   __shared__ float part[3072];
@@ -507,7 +531,7 @@ __global__ __launch_bounds__(384) void head_pool2_kernel(const bf16* __restrict_
   for (int c = 0; c < 2; ++c) {
     const int t = lane + 64 * c;
     keep[c] = t < T && (tokens == nullptr || tokens[((size_t)id * 2 + 1) * T + t] != 0);
-    av[c] = keep[c] ? a[(size_t)u * T + t] : -INFINITY;
+    av[c] = keep[c] ? (a2 != nullptr ? a[(size_t)u * T + t] + a2[(size_t)u * T + t] : a[(size_t)u * T + t]) : -INFINITY;
     m = fmaxf(m, av[c]);
   }
   m = wave_max(m);
@@ -758,7 +782,12 @@ __device__ __forceinline__ void wg_transform(uint32_t base, int tid, int wave, f
   lds_write128(ea, __builtin_bit_cast(u32x4_t, o));
 }
 
-template <int NSTAGE>
+// IL (the default): the e -> g rewrite of stage st+1 no longer runs as its own LDS round trip
+// in front of stage st's MFMAs (25 us of the 128 in isolation: FEDREC_HEAD_WG=1 measured 104);
+// its two LDS reads join the fragment reads, one wait covers both, and its VALU work is spread
+// between the MFMA groups (the MFMAs do not depend on it), its write after them.  The column
+// sums dw2 / db1 accumulate in every block (a few FMAs) and only the k-tile-0 blocks store them.
+template <int NSTAGE, bool IL = false>
 __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restrict__ e, const bf16* __restrict__ table,
                                                             const int* __restrict__ ids, const float* __restrict__ da,
                                                             int M, int T, int D, int Q, float* __restrict__ P,
@@ -804,7 +833,7 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
       wg_stage(smem + i * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0, mb + i * WTM, me, wave, lane);
   if (nsteps > 0) {
     wg_sync(nsteps - 1 < NSTAGE - 2 ? nsteps - 1 : NSTAGE - 2);  // stage 0 landed
-    if (stats) wg_transform<true>(lds0, tid, wave, sw2, ssum);
+    if (stats || (IL && xform)) wg_transform<true>(lds0, tid, wave, sw2, ssum);
     else if (xform) wg_transform<false>(lds0, tid, wave, sw2, ssum);
   }
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
@@ -828,6 +857,54 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
     if (st + NSTAGE - 1 < nsteps)
       wg_stage(smem + ((st + NSTAGE - 1) % NSTAGE) * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0,
                mb + (st + NSTAGE - 1) * WTM, me, wave, lane);
+    if constexpr (IL) {
+      const bool tr = st + 1 < nsteps && xform;  // block-uniform
+      const uint32_t base = lds0 + (st % NSTAGE) * WSTAGE;
+      const uint32_t nb = lds0 + ((st + 1) % NSTAGE) * WSTAGE;
+      const uint32_t ea = nb + (tid >> 4) * 256 + (tid & 15) * 16;
+      s16x4 xr[8], yr[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xr[2 * j] = tr_read(base + xo[j][0]);
+        xr[2 * j + 1] = tr_read(base + xo[j][1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        yr[2 * i] = tr_read(base + yo[i][0]);
+        yr[2 * i + 1] = tr_read(base + yo[i][1]);
+      }
+      u32x4_t ev4 = u32x4_t{0u, 0u, 0u, 0u};
+      float dav = 0.f;
+      if (tr) {
+        ev4 = lds_read128(ea);
+        dav = lds_read32(nb + E_BYTES + X_BYTES + wave * 256 + (tid >> 4) * 4);
+      }
+      LGKM_TIE8(xr);
+      LGKM_TIE8(yr);
+      asm volatile("" : "+v"(ev4), "+v"(dav));
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 ev = __builtin_bit_cast(bf16x8, ev4);
+      bf16x8 o;
+      bf16x8 xb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xb[j] = join(xr[2 * j], xr[2 * j + 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 ya = join(yr[2 * i], yr[2 * i + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], ya, acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int k = 2 * i; k < 2 * i + 2; ++k) {  // two of the eight transform elements per MFMA group
+          const float f = (float)ev[k];
+          o[k] = f2bf(dav * (1.0f - f * f));
+          sw2[k] += dav * f;
+          ssum[k] += (float)o[k];
+        }
+      }
+      if (tr) lds_write128(ea, __builtin_bit_cast(u32x4_t, o));
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
     if (st + 1 < nsteps) {
       const uint32_t nb = lds0 + ((st + 1) % NSTAGE) * WSTAGE;
       if (stats) wg_transform<true>(nb, tid, wave, sw2, ssum);
@@ -1198,17 +1275,21 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   if (!fr_head_supported(D, Q, T)) return 1;
   const int M = U * T;
   if (M == 0) return 0;
-  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 0);
-  // FEDREC_HEAD_SCORE (Q = 384): 1 -> 128 rows, BK 32, 4 stages; 2 -> 192 rows, BK 64, 2 stages;
-  // 3 -> 128 rows, BK 64, 2 stages (head_score2 form of the default); 4 -> 192 rows, BK 32, 3 stages
+  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 2);
+  // FEDREC_HEAD_SCORE (Q = 384): 2 (default) -> 192 rows, BK 64, 2 stages (bench A/B/A: steady
+  // step 0.5925 / 0.5859 / 0.5921 ms vs the 128-row form); 1 -> 128 rows, BK 32, 4 stages;
+  // 3 -> 128 rows, BK 64, 2 stages; 4 -> 192 rows, BK 32, 3 stages; 5 -> two Q slices of 192
+  // columns, 192 rows, BK 64, 3 stages (partial scores, see head_score2_kernel); 0 ->
+  // head_score_kernel
   if (Q == 384 && g_score_variant > 0) {
-#define LAUNCH_S2(RF, BK, NST)                                                                                   \
-  hipLaunchKernelGGL((head_score2_kernel<6, RF, BK, NST>), dim3((M + 32 * RF - 1) / (32 * RF)), dim3(512), 0, s, \
-                     (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out)
-    if (g_score_variant == 1) LAUNCH_S2(4, 32, 4);
-    else if (g_score_variant == 2) LAUNCH_S2(6, 64, 2);
-    else if (g_score_variant == 3) LAUNCH_S2(4, 64, 2);
-    else LAUNCH_S2(6, 32, 3);
+#define LAUNCH_S2(QF, RF, BK, NST, WQ, NS)                                                                     \
+  hipLaunchKernelGGL((head_score2_kernel<QF, RF, BK, NST, WQ>), dim3((M + 32 * RF - 1) / (32 * RF), NS), dim3(512), \
+                     0, s, (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q)
+    if (g_score_variant == 1) LAUNCH_S2(6, 4, 32, 4, 4, 1);
+    else if (g_score_variant == 3) LAUNCH_S2(6, 4, 64, 2, 4, 1);
+    else if (g_score_variant == 4) LAUNCH_S2(6, 6, 32, 3, 4, 1);
+    else if (g_score_variant == 5) LAUNCH_S2(3, 6, 64, 3, 2, 2);
+    else LAUNCH_S2(6, 6, 64, 2, 4, 1);
 #undef LAUNCH_S2
     return 0;
   }
@@ -1223,15 +1304,22 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   return 0;
 }
 
-extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, const int* tokens, int U, int T, int D,
-                            float* pooled, float* alpha, hipStream_t s) {
+// score partials per row: head_score writes a[slices][M] (the pool sums the slices)
+extern "C" int fr_head_score_slices(int Q) {
+  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 2);
+  return Q == 384 && g_score_variant == 5 ? 2 : 1;
+}
+
+extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, int slices, const int* tokens, int U,
+                            int T, int D, float* pooled, float* alpha, hipStream_t s) {
+  const float* a2 = slices == 2 ? a + (size_t)U * T : nullptr;
   if (T > MAXT || D % 8 != 0 || D / 8 > 384) return 1;
   if (U == 0) return 0;
   if (g_pool_variant < 0) g_pool_variant = env_int("FEDREC_HEAD_POOL", 1);
   const int TG = 384 / (D / 8), tpt = (T + TG - 1) / TG;
   if (g_pool_variant != 0 && D <= 3072 && tpt <= 32) {
 #define LAUNCH_POOL2(N)                                                                                          \
-  hipLaunchKernelGGL(head_pool2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, tokens, T, D, \
+  hipLaunchKernelGGL(head_pool2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, \
                      pooled, alpha)
     if (tpt <= 13) LAUNCH_POOL2(13);
     else if (tpt <= 16) LAUNCH_POOL2(16);
@@ -1239,7 +1327,7 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, c
 #undef LAUNCH_POOL2
     return 0;
   }
-  hipLaunchKernelGGL(head_pool_kernel, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, tokens, T, D, pooled,
+  hipLaunchKernelGGL(head_pool_kernel, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, pooled,
                      alpha);
   return 0;
 }
@@ -1309,12 +1397,13 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
     hipLaunchKernelGGL(head_wgrad64_kernel, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids,
                        da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk);
   } else if (M > 0) {
-#define LAUNCH_WG(N)                                                                                                 \
-  hipLaunchKernelGGL(head_wgrad_kernel<N>, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, \
+#define LAUNCH_WG(N, IL)                                                                                             \
+  hipLaunchKernelGGL((head_wgrad_kernel<N, IL>), dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, \
                      da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1)
-    if (nst == 1) LAUNCH_WG(5);
-    else if (nst == 2) LAUNCH_WG(6);
-    else LAUNCH_WG(4);  // (FEDREC_HEAD_WG bit 0 = no e -> g transform: diagnostic timing only)
+    if (nst == 1) LAUNCH_WG(5, false);
+    else if (nst == 2) LAUNCH_WG(6, false);
+    else if (g_wg_variant & 8) LAUNCH_WG(4, false);  // bit 3: the transform as its own LDS pass
+    else LAUNCH_WG(4, true);  // (FEDREC_HEAD_WG bit 0 = no e -> g transform: diagnostic timing only)
 #undef LAUNCH_WG
   } else {
     (void)hipMemsetAsync(scratch, 0, need * sizeof(float), s);

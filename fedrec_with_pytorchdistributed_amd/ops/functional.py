@@ -547,6 +547,71 @@ class EmbedLNFn(torch.autograd.Function):
 _USER_BWD_SPLIT = __import__("os").environ.get("FEDREC_USER_BWD_SPLIT", "0") == "1"  # A/B switch
 
 
+class side_grads:
+    """Weight gradients that only the optimizer reads, off the backward's critical path.
+
+    Inside ``with side_grads(dev):`` (the engine wraps ``loss.backward()`` in it) the user
+    encoder's and the text FC's weight-gradient GEMMs launch on a side stream that forks from
+    the backward after their inputs exist; the input-gradient chain (segment sum -> text FC
+    dgrad -> head pool backward -> head weight gradient) runs on meanwhile.  Autograd takes the
+    returned gradient tensors without a kernel (``FlatParams.begin_backward`` leaves ``.grad``
+    None), and the block's exit joins the side stream into the current one before anything
+    (``FlatParams.end_backward``'s gather) reads them.  Works under HIP-graph capture: the fork
+    and join are event edges of the captured graph.
+
+    OFF by default (``FEDREC_SIDE_GRADS=1`` enables it): measured SLOWER at config 2 -- steady
+    step 0.644-0.670 ms against 0.578 inline (``profiles/r3_ab_side_score_wgrad.txt``).  The
+    side-stream GEMM blocks take CU slots while the head weight gradient launches; that kernel
+    is sized to one block per CU, so a block that cannot be placed starts a wave late and the
+    whole grid waits for it."""
+
+    enabled = __import__("os").environ.get("FEDREC_SIDE_GRADS", "0") == "1"
+    _active = None  # (device, side stream, [events]) while a block is open
+    _streams: dict = {}
+
+    def __init__(self, dev):
+        self.dev = torch.device(dev)
+
+    def __enter__(self):
+        if side_grads.enabled and self.dev.type == "cuda" and side_grads._active is None:
+            st = side_grads._streams.get(self.dev)
+            if st is None:
+                st = side_grads._streams[self.dev] = torch.cuda.Stream(self.dev)
+            side_grads._active = (self.dev, st, [])
+            self.owner = True
+        else:
+            self.owner = False
+        return self
+
+    def __exit__(self, *exc):
+        if self.owner:
+            dev, _, evs = side_grads._active
+            side_grads._active = None
+            main = torch.cuda.current_stream(dev)
+            for ev in evs:
+                main.wait_event(ev)
+        return False
+
+    @staticmethod
+    def launch(fn, inputs):
+        """Run ``fn()`` (kernel launches + allocations of its outputs) on the side stream when
+        a block is open, else inline.  ``inputs``: tensors of the current stream ``fn`` reads."""
+        act = side_grads._active
+        if act is None:
+            return fn()
+        dev, side, evs = act
+        main = torch.cuda.current_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            out = fn()
+        for t in inputs:
+            t.record_stream(side)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        evs.append(ev)
+        return out
+
+
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
     """Device user encoder forward over history rows ``src[idx]`` (``src [*, D]`` fp32, ``idx``
     int32 [B*H]) -> ``(u [B, D] fp32, saved)``.
@@ -602,19 +667,34 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     # dpre^T ctx (fp32 operands: the mixed-dtype kernel); the bias gradients (column sums of
     # dQ|dK|dV and dpre, fp32) come out of the same launch (asum).  The input gradient has no
     # dependence on them: all three share ONE launch (FEDREC_USER_BWD_SPLIT=1: two launches)
-    gqkv = torch.empty(D3, D, device=dev)
-    gw1 = torch.empty(Qd, D, device=dev)
-    gbqkv = torch.empty(D3, device=dev)
-    gb1 = torch.empty(Qd, device=dev)
-    wg = (ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
-          ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
-    if _USER_BWD_SPLIT:
+    # (under side_grads the weight gradients run on the side stream beside the input gradient)
+    def wgrads():
+        gqkv = torch.empty(D3, D, device=dev)
+        gw1 = torch.empty(Qd, D, device=dev)
+        gbqkv = torch.empty(D3, device=dev)
+        gb1 = torch.empty(Qd, device=dev)
+        wg = (ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
+              ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
+        return gqkv, gw1, gbqkv, gb1, wg
+
+    if side_grads._active is not None:
+        gqkv, gw1, gbqkv, gb1 = side_grads.launch(lambda: _run_wgrads(wgrads), (dqkv, xd, dpre2, c3))
+        ops.small_gemm(dgrad, dev_off=dev_off)
+    elif _USER_BWD_SPLIT:
+        gqkv, gw1, gbqkv, gb1, wg = wgrads()
         ops.small_gemm(dgrad, dev_off=dev_off)
         ops.small_gemm(*wg)
     else:
+        gqkv, gw1, gbqkv, gb1, wg = wgrads()
         ops.small_gemm(dgrad, *wg, dev_off=dev_off)
     return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1, gb1, dw2.view(1, -1),
             db2.view(1))
+
+
+def _run_wgrads(make):
+    gqkv, gw1, gbqkv, gb1, wg = make()
+    ops.small_gemm(*wg)
+    return gqkv, gw1, gbqkv, gb1
 
 
 class UserStepFn(torch.autograd.Function):
@@ -750,9 +830,22 @@ class HeadFCFn(torch.autograd.Function):
         N = w.shape[0]
         dy = dy.contiguous().float()
         dx = torch.empty(n, K, device=x.device, dtype=torch.float32)
-        dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
-        db = torch.empty(N, device=x.device, dtype=torch.float32)
+
+        def wgrad():
+            dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+            db = torch.empty(N, device=x.device, dtype=torch.float32)
+            return dw, db, ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db)
+
+        dgrad = ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1)
+        if side_grads._active is not None:  # the weight gradient beside the head's backward
+            def run():
+                dw, db, g = wgrad()
+                ops.small_gemm(g)
+                return dw, db
+            dw, db = side_grads.launch(run, (dy, x))
+            ops.small_gemm(dgrad)
+            return dx, dw, db
         # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one launch
-        ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1),
-                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db))
+        dw, db, g = wgrad()
+        ops.small_gemm(dgrad, g)
         return dx, dw, db

@@ -397,7 +397,7 @@ class LocalEngine:
             with obs.range("user_step"):
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
                                           pre is not None and pre.padded, True, his)
-            with obs.range("backward"):
+            with obs.range("backward"), OF.side_grads(self.device):
                 loss.backward(self._seed_one())
             self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
             self.flat.end_backward()
