@@ -188,11 +188,16 @@ def main() -> int:
     t0 = time.perf_counter()
     losses = []
     uniq = []  # unique titles per step (the backbone's work; it varies by batch and client)
+    host_step = host_next = 0.0  # host time spent launching steps / preparing batches (diagnostic)
     for _ in range(args.steps):
         if pre.dedup is not None:
             uniq.append(int(pre.dedup[0].numel()))
+        h0 = time.perf_counter()
         losses.append(step(pre))
+        h1 = time.perf_counter()
         pre = next_batch()  # the batch of the step after this one (K prepares per K steps)
+        host_step += h1 - h0
+        host_next += time.perf_counter() - h1
     sync()
     if ctx.initialized:
         dist.barrier(group=ctx.ctrl_group)
@@ -333,6 +338,8 @@ def main() -> int:
             "cache_build_ms": None if cache_s is None else round(1000.0 * cache_s, 2),
             "steps_per_epoch": steps_per_epoch,
             "steady_ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "host_ms_per_step": {"launch": round(1000.0 * host_step / args.steps, 4),
+                                 "next_batch": round(1000.0 * host_next / args.steps, 4)},
             "cache_amortized_ms_per_step": round(1000.0 * amort / args.steps, 4),
             "fastest_rank_ms_per_step": round(1000.0 * fastest / args.steps, 3),
             "unique_titles_per_step": None if u_mean is None else round(u_mean, 1),

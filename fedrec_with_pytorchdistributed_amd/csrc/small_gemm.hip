@@ -36,6 +36,9 @@ namespace {
 
 constexpr int TK = 64, LDT = TK + 8;  // LDS row stride 72 bf16 = 144 B
 constexpr int MAXG = 6;
+#ifndef SG_NQ
+#define SG_NQ 1
+#endif
 
 struct GemmDesc {
   const void* A;
@@ -312,22 +315,27 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint32_t ra[TM / 64][16], rb[TN / 64][16];
+  // NQ k-tiles of operand loads in flight, in registers (a rotating queue, statically indexed by
+  // unrolling the k loop NQ times): these GEMMs are short (K = 200..1200: 4-19 k-tiles) and
+  // latency-bound -- with one k-tile in flight each k-step waited out a global-load latency
+  // behind its 8 MFMAs per wave (15 us for the 0.5 GFLOP att_fc1 GEMM, 7 k-steps)
+  constexpr int NQ = SG_NQ;
+  uint32_t ra[NQ][TM / 64][16], rb[NQ][TN / 64][16];
   __amdgpu_buffer_rsrc_t rsa, rsb;
   if (FAST) {
     rsa = rsrc_of(g.A);
     rsb = rsrc_of(g.B);
   }
-  auto load = [&](int k) {
+  auto load = [&](int k, uint32_t (&qa)[TM / 64][16], uint32_t (&qb)[TN / 64][16]) {
     if (FAST) {
       uint32_t oal[TM / 64], oah[TM / 64], obl[TN / 64], obh[TN / 64];
       chunk_offs<TM, AH>(g, true, m0, k, kend, tid, oal, oah);
       chunk_offs<TN, BH>(g, false, n0, k, kend, tid, obl, obh);
-      issue_loads<TM, AH>(rsa, oal, oah, ra);
-      issue_loads<TN, BH>(rsb, obl, obh, rb);
+      issue_loads<TM, AH>(rsa, oal, oah, qa);
+      issue_loads<TN, BH>(rsb, obl, obh, qb);
     } else {
-      load_raw<TM>(g, true, m0, k, kend, tid, ra);
-      load_raw<TN>(g, false, n0, k, kend, tid, rb);
+      load_raw<TM>(g, true, m0, k, kend, tid, qa);
+      load_raw<TN>(g, false, n0, k, kend, tid, qb);
     }
   };
   // asum: the column-0 tiles of an a_mode-1 desc also sum the raw A values they stage (chunk
@@ -337,21 +345,22 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
   float as_[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) as_[j] = 0.f;
-  if (kbeg < kend) load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += TK) {
+  // one k-step: the queued tile into LDS, then its MFMAs; the slot is refilled with the tile NQ
+  // steps ahead right after its registers were stored
+  auto step = [&](int k0, uint32_t (&qa)[TM / 64][16], uint32_t (&qb)[TN / 64][16]) {
     __syncthreads();  // the previous tile's fragments are consumed
     if (do_as) {
 #pragma unroll
       for (int i = 0; i < TM / 64; ++i)
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-          as_[j] += ah ? __uint_as_float((j & 1 ? ra[i][j >> 1] & 0xFFFF0000u : ra[i][j >> 1] << 16))
-                       : __uint_as_float(ra[i][j]);
+          as_[j] += ah ? __uint_as_float((j & 1 ? qa[i][j >> 1] & 0xFFFF0000u : qa[i][j >> 1] << 16))
+                       : __uint_as_float(qa[i][j]);
     }
-    store_lds<TM>(g, true, m0, k0, tid, ra, off, As, FAST ? AH : (bool)g.a_bf16);
-    store_lds<TN>(g, false, n0, k0, tid, rb, off, Bs, FAST ? BH : (bool)g.b_bf16);
+    store_lds<TM>(g, true, m0, k0, tid, qa, off, As, FAST ? AH : (bool)g.a_bf16);
+    store_lds<TN>(g, false, n0, k0, tid, qb, off, Bs, FAST ? BH : (bool)g.b_bf16);
     __syncthreads();
-    if (k0 + TK < kend) load(k0 + TK);  // next tile's global loads overlap this tile's MFMAs
+    if (k0 + NQ * TK < kend) load(k0 + NQ * TK, qa, qb);  // overlaps this and the next NQ-1 steps
 #pragma unroll
     for (int ks = 0; ks < TK; ks += 32) {
       bf16x8 a[FM], b[FN];
@@ -364,6 +373,20 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    if (kbeg + q * TK < kend) load(kbeg + q * TK, ra[q], rb[q]);
+  for (int k0 = kbeg; k0 < kend; k0 += NQ * TK) {
+    step(k0, ra[0], rb[0]);
+    if constexpr (NQ > 1) {
+      if (k0 + TK >= kend) break;
+      step(k0 + TK, ra[1], rb[1]);
+    }
+    if constexpr (NQ > 2) {
+      if (k0 + 2 * TK >= kend) break;
+      step(k0 + 2 * TK, ra[2], rb[2]);
     }
   }
   if (do_as) {  // lanes of one m group (tid % CPR) hold the same 16 m: xor-shuffle, then waves in order
@@ -432,6 +455,42 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
 // FAST loads with the operand dtypes per desc: a block-uniform switch into the four typed
 // bodies (one launch for, e.g., a backward's weight gradients over bf16 and fp32 inputs)
 __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
+  int gi;
+  const int t = tile_of_block(batch, gi);
+  const GemmDesc& g = batch.d[gi];
+  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+  if (g.a_bf16) {
+    if (g.b_bf16)
+      gemm_tile<2, 2, true, true, true>(g, off, t, As, Bs);
+    else
+      gemm_tile<2, 2, true, true, false>(g, off, t, As, Bs);
+  } else {
+    if (g.b_bf16)
+      gemm_tile<2, 2, true, false, true>(g, off, t, As, Bs);
+    else
+      gemm_tile<2, 2, true, false, false>(g, off, t, As, Bs);
+  }
+}
+
+// The same 64 x 64 bodies compiled for 5 waves per SIMD (<= 96 VGPRs, a few spilled words)
+// instead of 4: these GEMMs are latency-bound and hide it across co-resident blocks (a deeper
+// in-block register queue, SG_NQ = 3, measured slower: 2 waves per SIMD).  FEDREC_SG_OCC=5.
+template <bool AH, bool BH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void small_gemm_occ5_kernel(
+    const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
+  int gi;
+  const int t = tile_of_block(batch, gi);
+  const GemmDesc& g = batch.d[gi];
+  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+  gemm_tile<2, 2, true, AH, BH>(g, off, t, As, Bs);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void small_gemm_mixed_occ5_kernel(
+    const GemmBatch batch) {
   __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
   __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
   int gi;
@@ -765,10 +824,22 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     else                                                                                                   \
       hipLaunchKernelGGL((small_gemm_kernel<FM, FN, true, true, true>), dim3(tiles), dim3(256), 0, s, b);    \
   } while (0)
+  static const int occ = [] {
+    const char* e = getenv("FEDREC_SG_OCC");
+    return e ? atoi(e) : 0;
+  }();
   if (!fast)
     hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);
+  else if (mixed && occ == 5)
+    hipLaunchKernelGGL(small_gemm_mixed_occ5_kernel, dim3(tiles), dim3(256), 0, s, b);
   else if (mixed)
     hipLaunchKernelGGL(small_gemm_mixed_kernel, dim3(tiles), dim3(256), 0, s, b);
+  else if (occ == 5 && v == 1) {
+    if (dt == 0) hipLaunchKernelGGL((small_gemm_occ5_kernel<false, false>), dim3(tiles), dim3(256), 0, s, b);
+    else if (dt == 1) hipLaunchKernelGGL((small_gemm_occ5_kernel<false, true>), dim3(tiles), dim3(256), 0, s, b);
+    else if (dt == 2) hipLaunchKernelGGL((small_gemm_occ5_kernel<true, false>), dim3(tiles), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((small_gemm_occ5_kernel<true, true>), dim3(tiles), dim3(256), 0, s, b);
+  }
   else switch (v) {
     case 2: SG_LAUNCH(4, 2); break;
     case 3: SG_LAUNCH(2, 4); break;
