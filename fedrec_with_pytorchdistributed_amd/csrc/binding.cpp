@@ -42,15 +42,15 @@ int fr_additive_pool_bwd(const void* x, const void* e, const float* alpha, const
                          int is_bf16, hipStream_t s);
 int fr_head_supported(int D, int Q, int T);
 int fr_head_score(const void* table, const int* ids, int U, int T, int D, int Q, const void* W1, const float* b1,
-                  const float* w2, const float* b2, void* e_out, float* a_out, hipStream_t s);
+                  const float* w2, const float* b2, void* e_out, float* a_out, const int* nreal, hipStream_t s);
 int fr_head_score_slices(int Q);
 int fr_head_pool(const void* table, const int* ids, const float* a, int slices, const int* tokens, int U, int T, int D,
-                 float* pooled, float* alpha, hipStream_t s);
+                 float* pooled, float* alpha, const int* nreal, hipStream_t s);
 int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, const float* g, int U, int T, int D,
-                     float* da, float* db2p, hipStream_t s);
+                     float* da, float* db2p, const int* nreal, hipStream_t s);
 long fr_head_wgrad(const void* e, const void* table, const int* ids, const float* da, const float* db2p,
                    const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2, float* db2,
-                   float* scratch, hipStream_t s);
+                   float* scratch, const int* nreal, hipStream_t s);
 int fr_ipc_create(long cap, void* handle_out);
 int fr_ipc_open(int id, const void* handles, int me, int W, const long long* local_ptrs);
 long long fr_ipc_region(int id);
@@ -407,6 +407,15 @@ int64_t head_titles(const at::Tensor& table, const c10::optional<at::Tensor>& id
   return table.size(0) / T;
 }
 const int* opt_int_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr<int>() : nullptr; }
+
+// the text-head ops' optional device count of REAL titles (a padded step graph: titles past it
+// are skipped, their outputs zero): int32 [1] on the table's device
+const int* opt_nreal(const c10::optional<at::Tensor>& t, const at::Tensor& table) {
+  if (!t.has_value()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kInt && t->numel() == 1 && t->device() == table.device(),
+              "fedrec::head_*: nreal int32 [1] on the table's device");
+  return t->data_ptr<int>();
+}
 }  // namespace
 
 // ---- peer-to-peer all-reduce over IPC-mapped buffers (ipc_allreduce.hip) --------------------
@@ -477,7 +486,8 @@ bool head_supported(int64_t D, int64_t Q, int64_t T) { return fr_head_supported(
 
 std::tuple<at::Tensor, at::Tensor> head_score(const at::Tensor& table, const c10::optional<at::Tensor>& ids, int64_t T,
                                               const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2,
-                                              const at::Tensor& b2, bool store_e) {
+                                              const at::Tensor& b2, bool store_e,
+                                              const c10::optional<at::Tensor>& nreal) {
   const int64_t U = head_titles(table, ids, T), D = table.size(1), Q = w1.size(0);
   check_dev(w1, "w1");
   TORCH_CHECK(w1.scalar_type() == at::kBFloat16 && w1.is_contiguous() && w1.size(1) == D, "fedrec::head_score: w1 bf16 [Q, D]");
@@ -496,13 +506,14 @@ std::tuple<at::Tensor, at::Tensor> head_score(const at::Tensor& table, const c10
                       : at::empty({U * T}, table.options().dtype(at::kFloat));
   check_rc(fr_head_score(table.data_ptr(), opt_int_ptr(ids), (int)U, (int)T, (int)D, (int)Q, w1.data_ptr(),
                          b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
-                         store_e ? e.data_ptr() : nullptr, a.data_ptr<float>(), cur_stream()),
+                         store_e ? e.data_ptr() : nullptr, a.data_ptr<float>(), opt_nreal(nreal, table), cur_stream()),
            "head_score");
   return {e, a};
 }
 
 std::tuple<at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10::optional<at::Tensor>& ids, int64_t T,
-                                             const at::Tensor& a, const c10::optional<at::Tensor>& tokens) {
+                                             const at::Tensor& a, const c10::optional<at::Tensor>& tokens,
+                                             const c10::optional<at::Tensor>& nreal) {
   const int64_t U = head_titles(table, ids, T), D = table.size(1);
   check_dev(a, "a");
   TORCH_CHECK(a.scalar_type() == at::kFloat && (a.numel() == U * T || (a.dim() == 2 && a.size(0) == 2 && a.size(1) == U * T)) &&
@@ -519,13 +530,14 @@ std::tuple<at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10:
   auto alpha = at::empty({U, T}, a.options());
   check_rc(fr_head_pool(table.data_ptr(), opt_int_ptr(ids), a.data_ptr<float>(), a.dim() == 2 ? (int)a.size(0) : 1,
                         opt_int_ptr(tokens), (int)U, (int)T,
-                        (int)D, pooled.data_ptr<float>(), alpha.data_ptr<float>(), cur_stream()),
+                        (int)D, pooled.data_ptr<float>(), alpha.data_ptr<float>(), opt_nreal(nreal, table), cur_stream()),
            "head_pool");
   return {pooled, alpha};
 }
 
 std::tuple<at::Tensor, at::Tensor> head_pool_bwd(const at::Tensor& table, const c10::optional<at::Tensor>& ids,
-                                                 int64_t T, const at::Tensor& alpha, const at::Tensor& g) {
+                                                 int64_t T, const at::Tensor& alpha, const at::Tensor& g,
+                                                 const c10::optional<at::Tensor>& nreal) {
   const int64_t U = head_titles(table, ids, T), D = table.size(1);
   check_dev(alpha, "alpha");
   check_dev(g, "g");
@@ -536,7 +548,8 @@ std::tuple<at::Tensor, at::Tensor> head_pool_bwd(const at::Tensor& table, const 
   auto da = at::empty({U * T}, alpha.options());
   auto db2p = at::empty({std::max<int64_t>(U, 1)}, alpha.options());
   check_rc(fr_head_pool_bwd(table.data_ptr(), opt_int_ptr(ids), alpha.data_ptr<float>(), g.data_ptr<float>(), (int)U,
-                            (int)T, (int)D, da.data_ptr<float>(), db2p.data_ptr<float>(), cur_stream()),
+                            (int)T, (int)D, da.data_ptr<float>(), db2p.data_ptr<float>(), opt_nreal(nreal, table),
+                            cur_stream()),
            "head_pool_bwd");
   return {da, db2p};
 }
@@ -544,7 +557,8 @@ std::tuple<at::Tensor, at::Tensor> head_pool_bwd(const at::Tensor& table, const 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad(const at::Tensor& table,
                                                                       const c10::optional<at::Tensor>& ids, int64_t T,
                                                                       const at::Tensor& e, const at::Tensor& da,
-                                                                      const at::Tensor& w2, const at::Tensor& db2p) {
+                                                                      const at::Tensor& w2, const at::Tensor& db2p,
+                                                                      const c10::optional<at::Tensor>& nreal) {
   const int64_t U = head_titles(table, ids, T), D = table.size(1), Q = w2.numel();
   check_dev(e, "e");
   check_dev(da, "da");
@@ -565,12 +579,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad(const at::
   float* db2 = dw2 + Q;
   const long need = fr_head_wgrad(e.data_ptr(), table.data_ptr(), opt_int_ptr(ids), da.data_ptr<float>(),
                                   db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
-                                  dW1.data_ptr<float>(), db1, dw2, db2, nullptr, cur_stream());
+                                  dW1.data_ptr<float>(), db1, dw2, db2, nullptr, nullptr, cur_stream());
   TORCH_CHECK(need > 0, "fedrec::head_wgrad: unsupported shape");
   auto scratch = at::empty({need}, fopt);
   check_rc((int)fr_head_wgrad(e.data_ptr(), table.data_ptr(), opt_int_ptr(ids), da.data_ptr<float>(),
                               db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
-                              dW1.data_ptr<float>(), db1, dw2, db2, scratch.data_ptr<float>(), cur_stream()),
+                              dW1.data_ptr<float>(), db1, dw2, db2, scratch.data_ptr<float>(), opt_nreal(nreal, table),
+                              cur_stream()),
            "head_wgrad");
   return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
 }
@@ -1410,10 +1425,10 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("ipc_destroy(int id) -> ()", &ipc_destroy);
   m.def("ipc_allreduce_(int id, Tensor(a!) x, int epoch, int mode, int blocks) -> ()");
   m.def("ipc_allreduce_local_(int[] ids, Tensor(a!)[] xs, int epoch, int mode, int blocks) -> ()");
-  m.def("head_score(Tensor table, Tensor? ids, int T, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bool store_e) -> (Tensor, Tensor)");
-  m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens) -> (Tensor, Tensor)");
-  m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g) -> (Tensor, Tensor)");
-  m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("head_score(Tensor table, Tensor? ids, int T, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bool store_e, Tensor? nreal=None) -> (Tensor, Tensor)");
+  m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens, Tensor? nreal=None) -> (Tensor, Tensor)");
+  m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor? nreal=None) -> (Tensor, Tensor)");
+  m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep=None) -> (Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None) -> (Tensor, Tensor)");

@@ -93,11 +93,12 @@ __global__ __launch_bounds__(512, 1) void head_score_kernel(const bf16* __restri
                                                             int M, int T, int D, const bf16* __restrict__ W1,
                                                             const float* __restrict__ b1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, bf16* __restrict__ e_out,
-                                                            float* __restrict__ a_out) {
+                                                            float* __restrict__ a_out, const int* __restrict__ nreal) {
   constexpr int Q = QF * 64;
   constexpr int ST = (128 + Q) * 128;  // stage bytes
   __shared__ __attribute__((aligned(16))) char smem[2 * ST];
   const int m0 = blockIdx.x * 128;
+  if (nreal != nullptr && m0 >= min(M, nreal[0] * T)) return;  // only padded titles' rows (never read)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wq = wave & 3;
   const int rsub = lane >> 3, chunk = (lane & 7) ^ rsub;
@@ -217,7 +218,8 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
                                                              int M, int T, int D, const bf16* __restrict__ W1,
                                                              const float* __restrict__ b1, const float* __restrict__ w2,
                                                              const float* __restrict__ b2, bf16* __restrict__ e_out,
-                                                             float* __restrict__ a_out, int ldq) {
+                                                             float* __restrict__ a_out, int ldq,
+                                                             const int* __restrict__ nreal) {
   constexpr int Q = QF * 64;
   {
     const int qs = blockIdx.y;
@@ -243,6 +245,7 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
   static_assert(MR % RPP == 0 && Q % RPP == 0 && PT >= 8, "piece tiling");
   __shared__ __attribute__((aligned(16))) char smem[NST * ST];
   const int m0 = blockIdx.x * MR;
+  if (nreal != nullptr && m0 >= min(M, nreal[0] * T)) return;  // only padded titles' rows (never read)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WQ, wq = wave % WQ;
   const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
@@ -377,10 +380,15 @@ __global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__
                                                         const float* __restrict__ a, const float* __restrict__ a2,
                                                         const int* __restrict__ tokens,
                                                         int T, int D, float* __restrict__ pooled,
-                                                        float* __restrict__ alpha) {
+                                                        float* __restrict__ alpha, const int* __restrict__ nreal) {
   __shared__ float a_s[MAXT];
   __shared__ float part[3072];
   const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (nreal != nullptr && u >= nreal[0]) {  // a padded title of a step graph: exact zeros
+    for (int d = tid; d < D; d += blockDim.x) pooled[(size_t)u * D + d] = 0.f;
+    for (int t = tid; t < T; t += blockDim.x) alpha[(size_t)u * T + t] = 0.f;
+    return;
+  }
   const int id = ids != nullptr ? ids[u] : u;
   const bf16* xe = table + (size_t)id * T * D;
   if (wave == 0) {
@@ -441,9 +449,14 @@ __global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__
 __global__ __launch_bounds__(256) void head_pool_bwd_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
                                                             const float* __restrict__ alpha, const float* __restrict__ g,
                                                             int T, int D, float* __restrict__ da,
-                                                            float* __restrict__ db2p) {
+                                                            float* __restrict__ db2p, const int* __restrict__ nreal) {
   __shared__ float dal[MAXT];
   const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (nreal != nullptr && u >= nreal[0]) {  // a padded title: no gradient
+    for (int t = tid; t < T; t += blockDim.x) da[(size_t)u * T + t] = 0.f;
+    if (tid == 0) db2p[u] = 0.f;
+    return;
+  }
   const int id = ids != nullptr ? ids[u] : u;
   const bf16* xe = table + (size_t)id * T * D;
   const float* gu = g + (size_t)u * D;
@@ -511,9 +524,14 @@ __global__ __launch_bounds__(384) void head_pool2_kernel(const bf16* __restrict_
                                                          const float* __restrict__ a, const float* __restrict__ a2,
                                                          const int* __restrict__ tokens,
                                                          int T, int D, float* __restrict__ pooled,
-                                                         float* __restrict__ alpha) {
+                                                         float* __restrict__ alpha, const int* __restrict__ nreal) {
   __shared__ float part[3072];
   const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (nreal != nullptr && u >= nreal[0]) {  // a padded title of a step graph: exact zeros
+    for (int d = tid; d < D; d += blockDim.x) pooled[(size_t)u * D + d] = 0.f;
+    for (int t = tid; t < T; t += blockDim.x) alpha[(size_t)u * T + t] = 0.f;
+    return;
+  }
   const int id = ids != nullptr ? ids[u] : u;
   const bf16* xe = table + (size_t)id * T * D;
   const int DC = D >> 3, TG = 384 / DC;
@@ -576,9 +594,15 @@ __global__ __launch_bounds__(384) void head_pool_bwd2_kernel(const bf16* __restr
                                                              const int* __restrict__ ids,
                                                              const float* __restrict__ alpha,
                                                              const float* __restrict__ g, int T, int D,
-                                                             float* __restrict__ da, float* __restrict__ db2p) {
+                                                             float* __restrict__ da, float* __restrict__ db2p,
+                                                             const int* __restrict__ nreal) {
   __shared__ float dal[MAXT];
   const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (nreal != nullptr && u >= nreal[0]) {  // a padded title: no gradient
+    for (int t = tid; t < T; t += blockDim.x) da[(size_t)u * T + t] = 0.f;
+    if (tid == 0) db2p[u] = 0.f;
+    return;
+  }
   const int id = ids != nullptr ? ids[u] : u;
   const bf16* xe = table + (size_t)id * T * D;
   const float* gu = g + (size_t)u * D;
@@ -792,7 +816,8 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
                                                             const int* __restrict__ ids, const float* __restrict__ da,
                                                             int M, int T, int D, int Q, float* __restrict__ P,
                                                             float* __restrict__ dw2p, float* __restrict__ dsump,
-                                                            int tiles_k, int ntiles, int mchunk, int no_transform) {
+                                                            int tiles_k, int ntiles, int mchunk, int no_transform,
+                                                            const int* __restrict__ nreal) {
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * WSTAGE + 4 * MAX_SPLIT_TITLES];
   // XCD-aware order: all tiles of one split (same e / x row panel) on one XCD's L2
   const int bid = blockIdx.x, nwg = gridDim.x;
@@ -801,6 +826,14 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
   const int s = t / ntiles, tile = t - s * ntiles;
   const int qt = tile / tiles_k, kt = tile - qt * tiles_k;
   const int q0 = qt * WQT, k0 = kt * WKT;
+  // a padded step graph: rows past the real titles' carry no gradient -- re-split the real rows
+  // over the same grid (no split grows past the host's chunk, so the LDS id table still fits)
+  if (nreal != nullptr) {
+    M = min(M, nreal[0] * T);
+    const int S = nwg / ntiles;
+    const int c = ((M + S - 1) / S + WTM - 1) / WTM * WTM;
+    mchunk = max(WTM, min(mchunk, c));
+  }
   const int mb = s * mchunk;
   const int me = min(M, mb + mchunk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1059,7 +1092,7 @@ __global__ __launch_bounds__(512, 1) void head_wgrad64_kernel(const bf16* __rest
                                                               const float* __restrict__ da, int M, int T, int D, int Q,
                                                               float* __restrict__ P, float* __restrict__ dw2p,
                                                               float* __restrict__ dsump, int tiles_k, int ntiles,
-                                                              int mchunk) {
+                                                              int mchunk, const int* __restrict__ nreal) {
   __shared__ __attribute__((aligned(16))) char smem[W64_NST * W64_STAGE + 4 * W64_MAX_ROWS];
   const int bid = blockIdx.x, nwg = gridDim.x;
   const int xcd = bid & 7, qq = nwg >> 3, rmd = nwg & 7;
@@ -1067,6 +1100,12 @@ __global__ __launch_bounds__(512, 1) void head_wgrad64_kernel(const bf16* __rest
   const int s = t / ntiles, tile = t - s * ntiles;
   const int qt = tile / tiles_k, kt = tile - qt * tiles_k;
   const int q0 = qt * WQT, k0 = kt * WKT;
+  if (nreal != nullptr) {  // as head_wgrad_kernel
+    M = min(M, nreal[0] * T);
+    const int S = nwg / ntiles;
+    const int c = ((M + S - 1) / S + W64_TM - 1) / W64_TM * W64_TM;
+    mchunk = max(W64_TM, min(mchunk, c));
+  }
   const int mb = s * mchunk;
   const int me = min(M, mb + mchunk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1271,7 +1310,7 @@ extern "C" int fr_head_supported(int D, int Q, int T) {
 
 extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, int D, int Q, const void* W1,
                              const float* b1, const float* w2, const float* b2, void* e_out, float* a_out,
-                             hipStream_t s) {
+                             const int* nreal, hipStream_t s) {
   if (!fr_head_supported(D, Q, T)) return 1;
   const int M = U * T;
   if (M == 0) return 0;
@@ -1284,11 +1323,12 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   if (Q == 384 && g_score_variant > 0) {
 #define LAUNCH_S2(QF, RF, BK, NST, WQ, NS)                                                                     \
   hipLaunchKernelGGL((head_score2_kernel<QF, RF, BK, NST, WQ>), dim3((M + 32 * RF - 1) / (32 * RF), NS), dim3(512), \
-                     0, s, (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q)
+                     0, s, (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal)
     if (g_score_variant == 1) LAUNCH_S2(6, 4, 32, 4, 4, 1);
     else if (g_score_variant == 3) LAUNCH_S2(6, 4, 64, 2, 4, 1);
     else if (g_score_variant == 4) LAUNCH_S2(6, 6, 32, 3, 4, 1);
     else if (g_score_variant == 5) LAUNCH_S2(3, 6, 64, 3, 2, 2);
+    else if (g_score_variant == 6) LAUNCH_S2(6, 5, 64, 2, 4, 1);  // 160 rows: ~491 tiles = 1.9 waves of 256 CUs
     else LAUNCH_S2(6, 6, 64, 2, 4, 1);
 #undef LAUNCH_S2
     return 0;
@@ -1296,7 +1336,7 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   const dim3 grid((M + 127) / 128);
 #define LAUNCH_SCORE(QF)                                                                                          \
   hipLaunchKernelGGL(head_score_kernel<QF>, grid, dim3(512), 0, s, (const bf16*)table, ids, M, T, D,             \
-                     (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out)
+                     (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, nreal)
   if (Q == 384) LAUNCH_SCORE(6);
   else if (Q == 256) LAUNCH_SCORE(4);
   else LAUNCH_SCORE(2);
@@ -1311,7 +1351,7 @@ extern "C" int fr_head_score_slices(int Q) {
 }
 
 extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, int slices, const int* tokens, int U,
-                            int T, int D, float* pooled, float* alpha, hipStream_t s) {
+                            int T, int D, float* pooled, float* alpha, const int* nreal, hipStream_t s) {
   const float* a2 = slices == 2 ? a + (size_t)U * T : nullptr;
   if (T > MAXT || D % 8 != 0 || D / 8 > 384) return 1;
   if (U == 0) return 0;
@@ -1320,7 +1360,7 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, i
   if (g_pool_variant != 0 && D <= 3072 && tpt <= 32) {
 #define LAUNCH_POOL2(N)                                                                                          \
   hipLaunchKernelGGL(head_pool2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, \
-                     pooled, alpha)
+                     pooled, alpha, nreal)
     if (tpt <= 13) LAUNCH_POOL2(13);
     else if (tpt <= 16) LAUNCH_POOL2(16);
     else LAUNCH_POOL2(32);
@@ -1328,12 +1368,12 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, i
     return 0;
   }
   hipLaunchKernelGGL(head_pool_kernel, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, pooled,
-                     alpha);
+                     alpha, nreal);
   return 0;
 }
 
 extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, const float* g, int U, int T,
-                                int D, float* da, float* db2p, hipStream_t s) {
+                                int D, float* da, float* db2p, const int* nreal, hipStream_t s) {
   if (T > MAXT || D % 8 != 0 || D / 8 > 128) return 1;
   if (U == 0) return 0;
   if (g_pool_variant < 0) g_pool_variant = env_int("FEDREC_HEAD_POOL", 1);
@@ -1341,7 +1381,7 @@ extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* 
   if (g_pool_variant != 0 && tpw <= 22) {
 #define LAUNCH_PBWD2(N)                                                                                           \
   hipLaunchKernelGGL(head_pool_bwd2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, alpha, g, T, D, \
-                     da, db2p)
+                     da, db2p, nreal)
     if (tpw <= 9) LAUNCH_PBWD2(9);
     else if (tpw <= 11) LAUNCH_PBWD2(11);
     else LAUNCH_PBWD2(22);
@@ -1349,14 +1389,14 @@ extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* 
     return 0;
   }
   hipLaunchKernelGGL(head_pool_bwd_kernel, dim3(U), dim3(256), 0, s, (const bf16*)table, ids, alpha, g, T, D, da,
-                     db2p);
+                     db2p, nreal);
   return 0;
 }
 
 // scratch = null: returns the fp32 scratch element count needed; else launches.
 extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, const float* da, const float* db2p,
                               const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2,
-                              float* db2, float* scratch, hipStream_t s) {
+                              float* db2, float* scratch, const int* nreal, hipStream_t s) {
   if (!fr_head_supported(D, Q, T)) return -1;
   const int M = U * T;
   if (g_cus == 0) {
@@ -1395,11 +1435,11 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
   const int nst = (g_wg_variant >> 1) & 3;
   if (M > 0 && nst == 3) {
     hipLaunchKernelGGL(head_wgrad64_kernel, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids,
-                       da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk);
+                       da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, nreal);
   } else if (M > 0) {
 #define LAUNCH_WG(N, IL)                                                                                             \
   hipLaunchKernelGGL((head_wgrad_kernel<N, IL>), dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, \
-                     da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1)
+                     da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1, nreal)
     if (nst == 1) LAUNCH_WG(5, false);
     else if (nst == 2) LAUNCH_WG(6, false);
     else if (g_wg_variant & 8) LAUNCH_WG(4, false);  // bit 3: the transform as its own LDS pass

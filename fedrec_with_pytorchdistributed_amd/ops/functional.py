@@ -164,24 +164,26 @@ class TextHeadFn(torch.autograd.Function):
     ``mask_padding`` option, Q7)."""
 
     @staticmethod
-    def forward(ctx, w1, b1, w2, b2, table, ids, T: int, tokens):
+    def forward(ctx, w1, b1, w2, b2, table, ids, T: int, tokens, nreal=None):
+        # nreal (device int32 [1], optional): titles past it are padding of a step graph's unique
+        # list -- every kernel skips them (pooled / da exactly 0, no rows in the weight gradient)
         lib = ops.native.require_for(table)
         need = any(ctx.needs_input_grad[:4])
         e, a = lib.head_score(table, ids, T, w1.to(torch.bfloat16).contiguous(), b1.contiguous(),
-                              w2.reshape(-1).contiguous(), b2.reshape(-1), need)
-        pooled, alpha = lib.head_pool(table, ids, T, a, tokens)
+                              w2.reshape(-1).contiguous(), b2.reshape(-1), need, nreal)
+        pooled, alpha = lib.head_pool(table, ids, T, a, tokens, nreal)
         if need:
-            ctx.save_for_backward(table, ids, e, alpha, w2)
+            ctx.save_for_backward(table, ids, e, alpha, w2, nreal)
         ctx.T = T
         return pooled
 
     @staticmethod
     def backward(ctx, g):
-        table, ids, e, alpha, w2 = ctx.saved_tensors
+        table, ids, e, alpha, w2, nreal = ctx.saved_tensors
         lib = ops.native.require_for(table)
-        da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float())
-        dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p)
-        return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None
+        da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
+        dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p, nreal)
+        return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None, None
 
 
 def fused_head_supported(table_dim: int, query_dim: int, title_len: int) -> bool:

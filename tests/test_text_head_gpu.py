@@ -138,3 +138,32 @@ def test_engine_head_uses_fused_kernels_over_cache(dev):
             assert float((a - b).abs().max()) < 1e-3 * float(g2[2].norm())
         else:
             assert _rel(a, b) < 3e-2, (i, _rel(a, b))
+
+
+def test_fused_head_skips_padded_titles(dev):
+    """A step graph pads its unique-title list; with the device count ``nreal`` the head kernels
+    skip the padded titles: their pooled rows are exactly 0 and they add nothing to the weight
+    gradients (which equal the oracle over the real titles alone, whatever gradient arrives for
+    the padded rows)."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    N, D, Q, T, U, R = 400, 768, 384, 50, 300, 213  # R real titles, U - R padding (id 0)
+    table = torch.randn(N * T, D, generator=g).to(dev, torch.bfloat16)
+    ids = torch.randint(1, N, (U,), generator=g, dtype=torch.int32)
+    ids[R:] = 0
+    ids = ids.to(dev)
+    nreal = torch.tensor([R], dtype=torch.int32, device=dev)
+    w1 = (torch.randn(Q, D, generator=g) / math.sqrt(D)).to(dev).requires_grad_(True)
+    b1 = (torch.randn(Q, generator=g) * 0.1).to(dev).requires_grad_(True)
+    w2 = (torch.randn(1, Q, generator=g) / math.sqrt(Q) * 3).to(dev).requires_grad_(True)
+    b2 = torch.randn(1, generator=g).to(dev).requires_grad_(True)
+    pooled = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, None, nreal)
+    gout = torch.randn(U, D, generator=g).to(dev)  # padded rows get a nonzero gradient too
+    gw = torch.autograd.grad(pooled, (w1, b1, w2, b2), gout)
+    params = [t.detach().clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    ref = _oracle(table, ids[:R], T, *params, None)
+    rw = torch.autograd.grad(ref, params, gout[:R])
+    torch.cuda.synchronize()
+    assert float(pooled.detach()[R:].abs().max()) == 0.0
+    assert _rel(pooled[:R], ref) < 2e-3
+    for name, a, b in zip(("dW1", "db1", "dw2"), gw[:3], rw[:3]):
+        assert _rel(a, b) < 3e-2, (name, _rel(a, b))
