@@ -4,6 +4,7 @@ source "$(dirname "$0")/gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 check tests_pad 400 $T tests/test_text_head_gpu.py tests/test_step_graph.py tests/test_engine_gpu.py tests/test_user_step_gpu.py tests/test_no_library_kernels_gpu.py tests/test_news_cache.py
+check tests_dedup 200 $T tests/test_kernels_gpu.py -k dedup
 B="python -u bench.py --steps 50 --warmup 10 --round off --no-valid"
 run bench_pad 200 $B
 FEDREC_SKIP_PADDED=0 run bench_nopad 200 $B

@@ -209,8 +209,10 @@ def test_score_ce(dev, variant, act, C):
 
 
 @pytest.mark.parametrize("num_news", [500, 3 << 20])  # 32-bit sort keys / the 64-bit form (ids >= 2^19)
-def test_dedup_and_segment_sum(dev, num_news):
-    ids = torch.randint(0, num_news, (64 * 55,), device=dev, dtype=torch.int32)
+@pytest.mark.parametrize("R", [64 * 55, 37, 1024, 128 * 55, 8192])  # register-bitonic slots E = 4, 1, 1, 8, 8
+def test_dedup_and_segment_sum(dev, num_news, R):
+    # (64-bit keys at P = 8192 would need a 128 KB two-buffer key image: the LDS form runs those)
+    ids = torch.randint(0, num_news, (R,), device=dev, dtype=torch.int32)
     ids[::7] = ids[3]  # repeated ids: the occurrence order inside a segment must be ascending
     uniq, inv, perm, ptr = ops.dedup(ids, num_news)
     u_ref = torch.unique(ids.cpu())
