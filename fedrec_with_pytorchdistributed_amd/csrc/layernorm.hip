@@ -10,6 +10,8 @@
 // biased variance and eps inside the sqrt (eps = 1e-12).
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int MAXC = 4;  // D <= 1024
@@ -314,6 +316,7 @@ bool launch_ln16(const bf16* x, const int* tok, const bf16* word, const bf16* po
 //   dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 //   dw = sum_rows dy * xhat, db = sum_rows dy   (per-lane partials over a grid-stride of
 //   rows, reduced across the block's waves in LDS, one atomic per column per block)
+template <bool PF>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                      const bf16* __restrict__ dy, bf16* __restrict__ dx,
                                                      float* __restrict__ dw, float* __restrict__ db, int rows, int D,
@@ -333,15 +336,40 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x,
   for (int c = 0; c < MAXC; ++c)
 #pragma unroll
     for (int k = 0; k < 4; ++k) pw[c][k] = pb[c][k] = px[c][k] = 0.f;
-  for (int row = blockIdx.x * 4 + wv; row < rows; row += gridDim.x * 4) {
+  // the next row's x / dy are loaded while this row is reduced and written (one row in flight
+  // ahead per wave: the row loop was a chain of load latencies, ~3 TB/s at 78850 x 768)
+  const int stride = gridDim.x * 4;
+  bf16x4 xa[MAXC], xd[MAXC];
+  auto load_row = [&](int r) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int i = c * 256 + lane * 4;
+      const bool ok = c < nc && i < D;
+      const size_t src = ok ? (size_t)r * D + i : 0;  // masked lanes read row 0 (discarded below)
+      xa[c] = *(const bf16x4*)(x + src);
+      xd[c] = *(const bf16x4*)(dy + src);
+    }
+  };
+  if (blockIdx.x * 4 + wv < rows) load_row(blockIdx.x * 4 + wv);
+  for (int row = blockIdx.x * 4 + wv; row < rows; row += stride) {
     float v[MAXC][4], g[MAXC][4], dyv[MAXC][4];
+    bf16x4 ca[MAXC], cd[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      ca[c] = xa[c];
+      cd[c] = xd[c];
+    }
+    if (PF && row + stride < rows) load_row(row + stride);  // wave-uniform
+    if (!PF && row + stride < rows) {  // A/B form: the next row only after this one is written
+      __builtin_amdgcn_sched_barrier(0);
+    }
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int i = c * 256 + lane * 4;
       const bool ok = c < nc && i < D;
-      bf16x4 a = ok ? *(const bf16x4*)(x + (size_t)row * D + i) : bf16x4{0, 0, 0, 0};
-      bf16x4 d = ok ? *(const bf16x4*)(dy + (size_t)row * D + i) : bf16x4{0, 0, 0, 0};
+      bf16x4 a = ok ? ca[c] : bf16x4{0, 0, 0, 0};
+      bf16x4 d = ok ? cd[c] : bf16x4{0, 0, 0, 0};
       float4 ww = ok ? *(const float4*)(w + i) : make_float4(0.f, 0.f, 0.f, 0.f);
       const float wa[4] = {ww.x, ww.y, ww.z, ww.w};
 #pragma unroll
@@ -408,6 +436,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ x,
         }
       }
     }
+    if (!PF && row + stride < rows) load_row(row + stride);
   }
 #pragma unroll
   for (int c = 0; c < MAXC; ++c)
@@ -475,8 +504,18 @@ extern "C" int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void*
   if (rows == 0) return 0;
   int blocks = (rows + 3) / 4;
   if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy, (bf16*)dx, dw, db,
-                     rows, D, eps, dxs, (bf16*)dxz, pdrop, dxz ? 1.0f / (1.0f - pdrop) : 1.f, seed, offset);
+  static const bool pf = [] {  // FEDREC_LN_BWD_PF=0: the row-serial form (A/B runs)
+    const char* e = getenv("FEDREC_LN_BWD_PF");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (pf)
+    hipLaunchKernelGGL(ln_bwd_kernel<true>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy,
+                       (bf16*)dx, dw, db, rows, D, eps, dxs, (bf16*)dxz, pdrop, dxz ? 1.0f / (1.0f - pdrop) : 1.f,
+                       seed, offset);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<false>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy,
+                       (bf16*)dx, dw, db, rows, D, eps, dxs, (bf16*)dxz, pdrop, dxz ? 1.0f / (1.0f - pdrop) : 1.f,
+                       seed, offset);
   return 0;
 }
 
