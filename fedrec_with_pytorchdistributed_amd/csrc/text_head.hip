@@ -1410,11 +1410,13 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
     g_wg_splits = env_int("FEDREC_HEAD_SPLITS", 0);
   }
   const int tiles_k = D / WKT, ntiles = (Q / WQT) * tiles_k;
-  // one wave of blocks (one per CU), each split >= 8 stages of 32 rows.  A few CUs are left
-  // out: in the training step the next batch's sampler / dedup run on the lookahead stream
-  // meanwhile, and a block that cannot be placed beside them would start only after them --
-  // the whole grid then waits for one late block (measured 168 us in the step vs 117 alone)
-  int S = g_wg_splits > 0 ? g_wg_splits : (g_cus - 16) / ntiles;
+  // one wave of blocks (one per CU), each split >= 8 stages of 32 rows.  The first form left
+  // 16 CUs out for the lookahead stream's sampler / dedup, which then still ran beside this
+  // kernel (a block that could not be placed beside them started a wave late: 168 vs 117 us).
+  // The register-bitonic dedup (30 us) finishes before this kernel starts, so every CU gets a
+  // block: 28 splits vs 26 measured 0.5709 / 0.5707 vs 0.5780 / 0.5791 ms per step (A/B/A/B,
+  // profiles/r3_ab_wgrad_splits.txt)
+  int S = g_wg_splits > 0 ? g_wg_splits : g_cus / ntiles;
   const int smax = (M + 8 * WTM - 1) / (8 * WTM);
   S = S < 1 ? 1 : (S > smax ? smax : S);
   if (S < 1) S = 1;
