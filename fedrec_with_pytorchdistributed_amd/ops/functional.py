@@ -164,12 +164,13 @@ class TextHeadFn(torch.autograd.Function):
     ``mask_padding`` option, Q7)."""
 
     @staticmethod
-    def forward(ctx, w1, b1, w2, b2, table, ids, T: int, tokens, nreal=None):
+    def forward(ctx, w1, b1, w2, b2, table, ids, T: int, tokens, nreal=None, w1b=None):
         # nreal (device int32 [1], optional): titles past it are padding of a step graph's unique
         # list -- every kernel skips them (pooled / da exactly 0, no rows in the weight gradient)
         lib = ops.native.require_for(table)
         need = any(ctx.needs_input_grad[:4])
-        e, a = lib.head_score(table, ids, T, w1.to(torch.bfloat16).contiguous(), b1.contiguous(),
+        w1c = w1b if w1b is not None else w1.to(torch.bfloat16).contiguous()  # w1b: the step's cast
+        e, a = lib.head_score(table, ids, T, w1c, b1.contiguous(),
                               w2.reshape(-1).contiguous(), b2.reshape(-1), need, nreal)
         pooled, alpha = lib.head_pool(table, ids, T, a, tokens, nreal)
         if need:
@@ -183,7 +184,7 @@ class TextHeadFn(torch.autograd.Function):
         lib = ops.native.require_for(table)
         da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
         dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p, nreal)
-        return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None, None
+        return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None, None, None
 
 
 def fused_head_supported(table_dim: int, query_dim: int, title_len: int) -> bool:
@@ -549,6 +550,37 @@ class EmbedLNFn(torch.autograd.Function):
 _USER_BWD_SPLIT = __import__("os").environ.get("FEDREC_USER_BWD_SPLIT", "0") == "1"  # A/B switch
 
 
+def _user_weight_bufs(wts, dev):
+    """The user step's compute copies: the bf16 stack [Wq; Wk; Wv; W1] and the fp32 [bq | bk | bv]."""
+    wq, w1, D = wts[0], wts[6], wts[0].shape[1]
+    return (torch.empty(3 * wq.shape[0] + w1.shape[0], D, device=dev, dtype=torch.bfloat16),
+            torch.empty(3 * wq.shape[0], device=dev, dtype=torch.float32))
+
+
+def _user_cast_lists(wts, wb, bqkv):
+    wq, bq, wk, bk, wv, bv, w1 = wts[:7]
+    D, D3 = wq.shape[1], 3 * wq.shape[0]
+    return ([wq, wk, wv, w1, bq, bk, bv],
+            [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D], bqkv[2 * D:]])
+
+
+def step_weight_casts(text_encoder, user_encoder):
+    """Every compute copy a fused training step needs, in ONE cast launch: the text head's att_fc1
+    weight in bf16 (the head_score operand) and the user encoder's bf16 weight stack + fp32 Q|K|V
+    bias (the user step's GEMM operands).  Returns ``(w1_bf16, (wb, bqkv))``; the two were a cast
+    kernel each (4.7 + 6.2 us per step)."""
+    aa = text_encoder.additive_attention
+    mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
+    wts = (mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight, mha.W_V.bias,
+           pool.att_fc1.weight)
+    w = aa.att_fc1.weight
+    w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+    wb, bqkv = _user_weight_bufs(wts, w.device)
+    src, dst = _user_cast_lists(wts, wb, bqkv)
+    ops.native.require_for(w).multi_cast([w.detach()] + [t.detach() for t in src], [w1b] + dst)
+    return w1b, (wb, bqkv)
+
+
 class side_grads:
     """Weight gradients that only the optimizer reads, off the backward's critical path.
 
@@ -614,7 +646,7 @@ class side_grads:
         return out
 
 
-def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
+def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None):
     """Device user encoder forward over history rows ``src[idx]`` (``src [*, D]`` fp32, ``idx``
     int32 [B*H]) -> ``(u [B, D] fp32, saved)``.
 
@@ -629,11 +661,11 @@ def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_
     D = src.shape[1]
     BH, D3, Qd = B * H, 3 * D, w1.shape[0]
     dev = src.device
-    wb = torch.empty(D3 + Qd, D, device=dev, dtype=torch.bfloat16)
-    bqkv = torch.empty(D3, device=dev, dtype=torch.float32)
-    ops.native.require_for(src).multi_cast([wq, wk, wv, w1, bq, bk, bv],
-                                           [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D],
-                                            bqkv[2 * D:]])
+    if casts is not None:  # the step's one cast launch made them already (step_weight_casts)
+        wb, bqkv = casts
+    else:
+        wb, bqkv = _user_weight_bufs(wts, dev)
+        ops.native.require_for(src).multi_cast(*_user_cast_lists(wts, wb, bqkv))
     p, seed, off = drop
     xd = ops.gather_dropout(src, idx, p, seed, off, dev_off, bf16_out=True)
     qkv = torch.empty(BH, D3, device=dev, dtype=torch.float32)
@@ -712,11 +744,11 @@ class UserStepFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, v, inv, perm, ptr, wq, bq, wk, bk, wv, bv, w1, b1, w2, b2, meta):
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one = meta
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one, casts = meta
         D = v.shape[1]
         BC = B * C
         u, saved = _user_enc_fwd(v, inv[BC:], (wq, bq, wk, bk, wv, bv, w1, b1, w2, b2), B, H, heads, hd, drop,
-                                 dev_off, keep)
+                                 dev_off, keep, casts)
         # per-occurrence news gradients: the candidate rows come straight from the scoring
         # kernel (candidates read from v by index: no gathered copy), the history rows from the
         # user encoder's dgrad in the backward
@@ -731,7 +763,7 @@ class UserStepFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gloss, gscores):
         v, inv, perm, ptr, rows, du, *saved = ctx.saved_tensors
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one = ctx.meta
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one, _ = ctx.meta
         BC = B * C
         if gloss is not one:  # the engine seeds the backward with its persistent ones tensor: no scale
             rows[:BC].mul_(gloss)
@@ -745,7 +777,7 @@ class UserStepFn(torch.autograd.Function):
 
 
 def user_step(v, inv, perm, ptr, user_encoder, B: int, C: int, H: int, act: str, drop, dev_off, ldp, padded: bool,
-              keep=None, one=None):
+              keep=None, one=None, casts=None):
     """Device user side of a step (see :class:`UserStepFn`) -> ``(loss, scores)``.  ``keep``:
     the mask_padding key mask (history ids [B, H], nonzero = real slot) or None.  ``one``: the
     tensor the caller will seed ``loss.backward`` with when it is a ones tensor (the backward
@@ -754,7 +786,7 @@ def user_step(v, inv, perm, ptr, user_encoder, B: int, C: int, H: int, act: str,
     if keep is not None:
         keep = keep.reshape(B, H)
         keep = keep if keep.dtype == torch.int32 and keep.is_contiguous() else keep.to(torch.int32).contiguous()
-    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded, keep, one)
+    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded, keep, one, casts)
     return UserStepFn.apply(v, inv, perm, ptr, mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias,
                             mha.W_V.weight, mha.W_V.bias, pool.att_fc1.weight, pool.att_fc1.bias,
                             pool.att_fc2.weight, pool.att_fc2.bias, meta)

@@ -67,6 +67,7 @@ _CAPTURE_MODE = os.environ.get("FEDREC_CAPTURE_MODE", "thread_local")
 
 
 _SKIP_PADDED = os.environ.get("FEDREC_SKIP_PADDED", "1") != "0"  # A/B switch
+_STEP_CASTS = os.environ.get("FEDREC_STEP_CASTS", "1") != "0"  # A/B switch (0: a cast launch per consumer)
 
 
 class _StepGraph:
@@ -296,7 +297,8 @@ class LocalEngine:
     def _cache_ids(self, ids: torch.Tensor) -> torch.Tensor:
         return ids if ids.dtype == torch.int32 else ids.to(torch.int32)
 
-    def news_vectors(self, uniq: torch.Tensor, grad: bool, nreal: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def news_vectors(self, uniq: torch.Tensor, grad: bool, nreal: Optional[torch.Tensor] = None,
+                     w1b: Optional[torch.Tensor] = None) -> torch.Tensor:
         """News vectors of titles ``uniq``; ``nreal`` (device int32 [1], fused head only): rows
         past it are padding of a step graph's unique list and come out as the fc bias."""
         te = self.model.text_encoder
@@ -306,7 +308,7 @@ class LocalEngine:
             table = self.hcache.flat()
             self.sync_params()
             if grad:
-                return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens, nreal)
+                return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens, nreal, w1b)
             with torch.no_grad():
                 return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens)
         hid, mask = self._hidden(uniq)  # parameter-free: overlaps the previous step's all-reduce + Adam
@@ -362,7 +364,7 @@ class LocalEngine:
         return uniq, v, cand_v, his_v
 
     def _user_loss(self, v: torch.Tensor, dd, B: int, C: int, H: int, padded: bool, train: bool,
-                   his: Optional[torch.Tensor] = None):
+                   his: Optional[torch.Tensor] = None, casts=None):
         """Device user side (fused): ``(loss, scores)`` from news vectors ``v`` of the unique ids.
         ``his [B, H]``: the batch's history ids, the key mask when ``mask_padding`` is on."""
         uniq, inv, perm, ptr = dd
@@ -377,7 +379,7 @@ class LocalEngine:
             self.noise_offset += 1
         keep = his if (self.cfg.mask_padding and his is not None) else None
         return OF.user_step(v, inv, perm, ptr, self.model.user_encoder, B, C, H, self.score_act,
-                            (p, self.user_drop_seed, 0), self._rng_step, ldp, padded, keep, self._seed_one())
+                            (p, self.user_drop_seed, 0), self._rng_step, ldp, padded, keep, self._seed_one(), casts)
 
     def _seed_one(self) -> torch.Tensor:
         """The persistent ones tensor every fused backward is seeded with (no fill launch per
@@ -403,11 +405,17 @@ class LocalEngine:
             self.reducer.begin()
         if self.fused_user:
             dd = self._dedup(cand, his, pre)
+            casts = None
+            if self.fused_head and _STEP_CASTS:  # every compute copy of the step's weights in one cast launch
+                self.sync_params()
+                casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder)
             with obs.range("news_encode"):
-                v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None)
+                v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
+                                      w1b=casts[0] if casts is not None else None)
             with obs.range("user_step"):
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
-                                          pre is not None and pre.padded, True, his)
+                                          pre is not None and pre.padded, True, his,
+                                          casts=casts[1] if casts is not None else None)
             with obs.range("backward"), OF.side_grads(self.device):
                 loss.backward(self._seed_one())
             self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
