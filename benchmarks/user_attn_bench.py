@@ -46,16 +46,16 @@ def main():
     qkv = torch.randn(a.B, a.H, 3 * NH * DK, generator=g).cuda()
     d = torch.randn(a.B, a.H, NH * DK, generator=g).cuda()
     outs = {}
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2, 3, 4):
         lib.user_attn_set_variant(v)
         c, st = ops.user_attention_fwd(qkv, NH, DK)
         outs[v] = (c, st, ops.user_attention_bwd(qkv, st, d, NH, DK))
     res = {"fwd_rel_diff_v3_v1": float((outs[3][0] - outs[1][0]).norm() / outs[1][0].norm()),
            "bwd_rel_diff_v3_v1": float((outs[3][2] - outs[1][2]).norm() / outs[1][2].norm())}
     print(res, flush=True)
-    times = {f"{k}_v{v}": [] for k in ("fwd", "bwd") for v in (0, 1, 2, 3)}
+    times = {f"{k}_v{v}": [] for k in ("fwd", "bwd") for v in (0, 1, 2, 3, 4)}
     for _ in range(a.rounds):
-        for v in (0, 1, 2, 3):
+        for v in (0, 1, 2, 3, 4):
             lib.user_attn_set_variant(v)
             st = outs[v][1]
             times[f"fwd_v{v}"].append(timeit(lambda: ops.user_attention_fwd(qkv, NH, DK)))

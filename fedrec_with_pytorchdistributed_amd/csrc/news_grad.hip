@@ -15,6 +15,8 @@
 // per-occurrence clip+noise pass is embarrassingly parallel; the segment sum is skewed.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int MAXV = 8;   // D <= 512
@@ -117,8 +119,10 @@ __global__ __launch_bounds__(1024) void segsum_kernel(const float* __restrict__ 
 // partial in scratch[chunk][slot] (slot 0: started before the chunk, slot 1: ends after it).
 // A second pass sums the partials of every crossing segment in chunk order.  The chunk grid
 // is fixed by R alone, so the result is deterministic, and no float atomics are used.
-constexpr int SCH = 16;
-
+// SCH: chunk length, a template parameter: 16 (default) or 8 (FEDREC_SEGSUM_SCH=8: half the
+// per-wave row registers -- 89 vs 161 VGPRs -- and twice the waves; measured neutral, 0.5694 /
+// 0.5668 vs 0.5665 / 0.5702 ms per step, profiles/r3_ab_segsum_ua.txt)
+template <int SCH>
 __global__ __launch_bounds__(256) void segsum_chunk_kernel(const float* __restrict__ rows, const int* __restrict__ perm,
                                                            const int* __restrict__ seg_ptr, const int* __restrict__ inv,
                                                            float* __restrict__ out, float* __restrict__ scratch, int U,
@@ -171,6 +175,7 @@ __global__ __launch_bounds__(256) void segsum_chunk_kernel(const float* __restri
   }
 }
 
+template <int SCH>
 __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__ seg_ptr, float* __restrict__ out,
                                                          const float* __restrict__ scratch, int U, int D) {
   // partials of a crossing segment: [scratch[c0][1], scratch[c0+1][0], ..., scratch[c1][0]];
@@ -214,11 +219,20 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__
 }
 
 int g_segsum_variant = 1;  // 1: chunked (default), 0: one block per output row
+int g_segsum_sch = 0;      // chunk length of the chunked form (FEDREC_SEGSUM_SCH: 16 default, or 8)
+
+int segsum_sch() {
+  if (g_segsum_sch == 0) {
+    const char* e = getenv("FEDREC_SEGSUM_SCH");
+    g_segsum_sch = (e != nullptr && atoi(e) == 8) ? 8 : 16;
+  }
+  return g_segsum_sch;
+}
 
 }  // namespace
 
 extern "C" void fr_segsum_set_variant(int v) { g_segsum_variant = v; }
-extern "C" int fr_segsum_chunks(int R) { return (R + SCH - 1) / SCH; }
+extern "C" int fr_segsum_chunks(int R) { return (R + segsum_sch() - 1) / segsum_sch(); }
 
 extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std,
                            unsigned long long seed, unsigned long long offset, hipStream_t s,
@@ -238,10 +252,17 @@ extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int
   if (D > 64 * MAXV) return 1;
   if (U == 0) return 0;
   if (g_segsum_variant == 1 && scratch != nullptr && inv != nullptr && R > 0) {
-    const int nch = (R + SCH - 1) / SCH;
-    hipLaunchKernelGGL(segsum_chunk_kernel, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out, scratch,
-                       U, R, D);
-    hipLaunchKernelGGL(segsum_fix_kernel, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
+    const int sch = segsum_sch();
+    const int nch = (R + sch - 1) / sch;
+    if (sch == 16) {
+      hipLaunchKernelGGL(segsum_chunk_kernel<16>, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out,
+                         scratch, U, R, D);
+      hipLaunchKernelGGL(segsum_fix_kernel<16>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
+    } else {
+      hipLaunchKernelGGL(segsum_chunk_kernel<8>, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out,
+                         scratch, U, R, D);
+      hipLaunchKernelGGL(segsum_fix_kernel<8>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
+    }
     return 0;
   }
   if (zero_empty) (void)hipMemsetAsync(out, 0, (size_t)U * D * sizeof(float), s);

@@ -578,12 +578,17 @@ __device__ __forceinline__ bool key_kept(const int* __restrict__ keep, int b, in
   return keep == nullptr || keep[(size_t)b * H + t] != 0;
 }
 
+// SR = 65 (default, 33,008 B of LDS, four blocks per CU) or SR = 64 (FEDREC_UA_VARIANT=4: 64-row
+// operand stages -- rows 64.. are never read -- 32,768 B, five blocks per CU, all 1,280
+// (impression, head) blocks of B = 64 in one wave of the chip): measured neutral (fwd 20.5 vs
+// 20.0 us, steady step 0.5652 / 0.5862 vs 0.5663 / 0.5660 ms, profiles/r3_ab_segsum_ua.txt)
+template <int SR>
 __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   float* __restrict__ ctx, float* __restrict__ stats,
                                                                   int H, int NH, const int* __restrict__ keep) {
-  __shared__ __attribute__((aligned(16))) float qs[65][DK];
-  __shared__ __attribute__((aligned(16))) float ks[65][DK];
-  __shared__ __attribute__((aligned(16))) float vs[65][DK];
+  __shared__ __attribute__((aligned(16))) float qs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float ks[SR][DK];
+  __shared__ __attribute__((aligned(16))) float vs[SR][DK];
   __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
@@ -680,17 +685,21 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
   }
 }
 
+// Backward LDS: 55,616 B with PLDB = 68 and 65-row stages (default, two blocks per CU); with
+// PLDB = 66 and 64-row stages (FEDREC_UA_VARIANT=4) 54,272 B, three blocks per CU, at the cost
+// of 2-way conflicts on the row-major P / dS reads: measured neutral (34.4 vs 34.2 us)
+template <int SR, int PLDB>
 __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   const float* __restrict__ stats,
                                                                   const float* __restrict__ dctx,
                                                                   float* __restrict__ dqkv, int H, int NH,
                                                                   const int* __restrict__ keep) {
-  __shared__ __attribute__((aligned(16))) float qs[65][DK];
-  __shared__ __attribute__((aligned(16))) float ks[65][DK];
-  __shared__ __attribute__((aligned(16))) float vs[65][DK];
-  __shared__ __attribute__((aligned(16))) float gs[65][DK];
-  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
-  __shared__ __attribute__((aligned(16))) float dss[64 * PLD];
+  __shared__ __attribute__((aligned(16))) float qs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float ks[SR][DK];
+  __shared__ __attribute__((aligned(16))) float vs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float gs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float ps[64 * PLDB];
+  __shared__ __attribute__((aligned(16))) float dss[64 * PLDB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
   const int ld = 3 * NH * DK, D = NH * DK;
@@ -764,7 +773,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
       Dt = row16_sum(Dt);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int idx = (i0 + fq * 4 + r) * PLD + j * 16 + fr;
+        const int idx = (i0 + fq * 4 + r) * PLDB + j * 16 + fr;
         ps[idx] = p[j][r];
         dss[idx] = p[j][r] * (dp[j][r] - Dt) * scale;
       }
@@ -775,7 +784,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
     for (int kk = 0; kk < 16; ++kk) {
       if (kk >= KS) break;
       const int k = 4 * kk + fq;
-      const float a = dss[(i0 + fr) * PLD + k];
+      const float a = dss[(i0 + fr) * PLDB + k];
       const float y0 = ks[k][fr], y1r = ks[k][16 + fr], y1 = fr < DK - 16 ? y1r : 0.f;
       o0 = mfma4(a, y0, o0);
       o1 = mfma4(a, y1, o1);
@@ -796,7 +805,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   for (int kk = 0; kk < 16; ++kk) {
     if (kk >= KS) break;
     const int t = 4 * kk + fq;
-    const float pa = ps[t * PLD + i0 + fr], da = dss[t * PLD + i0 + fr];
+    const float pa = ps[t * PLDB + i0 + fr], da = dss[t * PLDB + i0 + fr];
     const float g0 = gs[t][fr], g1r = gs[t][16 + fr], g1 = fr < DK - 16 ? g1r : 0.f;
     const float q0 = qs[t][fr], q1r = qs[t][16 + fr], q1 = fr < DK - 16 ? q1r : 0.f;
     v0 = mfma4(pa, g0, v0);
@@ -817,7 +826,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   }
 }
 
-int g_ua_variant = 3;  // 3: four-wave MFMA (default), 2: one-wave MFMA, 1: VALU ILP forward, 0: first VALU forward
+int g_ua_variant = 3;  // 3: four-wave MFMA (default), 4: the same with smaller LDS stages, 2: one-wave MFMA, 1: VALU ILP forward, 0: first VALU forward
 
 // ---------------------------------------------------------------------------------------
 // Long histories (H > 64): the reference pads but never truncates (dataset.py:84, quirk Q6;
@@ -1013,8 +1022,10 @@ extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int 
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH, keep);
+  else if (g_ua_variant == 4)
+    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<64>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
   else if (keep != nullptr || g_ua_variant == 3)
-    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
+    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<65>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
   else if (g_ua_variant >= 10) {  // diagnostic partial forwards (timing only): 10 staging, 11 + S/softmax
     if (g_ua_variant == 10) hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 1>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
     else hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 2>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
@@ -1038,8 +1049,12 @@ extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const floa
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH, keep);
+  else if (g_ua_variant == 4)
+    hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<64, 66>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH,
+                       keep);
   else if (keep != nullptr || g_ua_variant == 3)
-    hipLaunchKernelGGL(user_attn_bwd_mfma4_kernel, dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH, keep);
+    hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<65, 68>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH,
+                       keep);
   else if (g_ua_variant == 2) {
     const int nt = (H + 15) / 16;
 #define UA_BWD(N) \

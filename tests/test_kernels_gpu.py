@@ -155,7 +155,7 @@ def test_additive_pool(dev, dtype, D, Q):
     assert abs(float(db2_n) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
 
 
-@pytest.mark.parametrize("variant", [3, 2, 1, 0])
+@pytest.mark.parametrize("variant", [3, 4, 2, 1, 0])
 @pytest.mark.parametrize("H", [1, 17, 33, 50, 64, 65, 76, 200])
 def test_user_attention(dev, H, variant):
     """variants 3 (default, four waves per head) / 2 (one wave) = the fp32 matrix-core kernels
