@@ -252,11 +252,28 @@ __device__ __forceinline__ void to_bf16x16(const uint32_t (&raw)[16], bool h, bo
     for (int j = 0; j < 8; ++j) o[hh][j] = f2bf(v[8 * hh + j]);
 }
 
-template <int TR>
+// TRI (transposed-image) form of a stored-transposed operand (mode 1, TR = 64): the tile stays
+// as it sits in memory, [64 k rows][64 cols] bf16 (128-B rows), 16-B chunk c of row k at
+// c ^ tsw(k), written with two ds_write_b128 per chunk of 16 columns instead of 16 scalar
+// 2-byte stores into the k-contiguous image; the MFMA fragments (8 consecutive k of one
+// column) come back with two ds_read_b64_tr_b16.  tsw spreads the 4 rows x 2 chunks a
+// 16-lane group reads -- rows {8g + q}, g = lane / 16 -- over distinct 8-bank quarters
+__device__ __forceinline__ int tsw(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }
+
+template <int TR, bool TRI = false>
 __device__ __forceinline__ void store_lds(const GemmDesc& g, bool isA, int r0, int k0, int tid,
                                           const uint32_t (&raw)[TR / 64][16], unsigned long long off,
                                           bf16 (*S)[LDT], bool h) {
   const int mode = isA ? g.a_mode : g.b_mode;
+  if (TRI && TR == 64 && mode == 1) {  // block-uniform
+    bf16* img = &S[0][0];
+    const int k = tid >> 2, c0 = (tid & 3) * 2;  // 16 columns = chunks c0, c0 + 1 of row k
+    bf16x8 o[2];
+    to_bf16x16(raw[0], h, !isA && g.drop_on == 2, (unsigned long long)(k0 + k) * g.drop_ld + r0 + c0 * 8, g, off, o);
+    *(bf16x8*)(img + k * 64 + ((c0 ^ tsw(k)) << 3)) = o[0];
+    *(bf16x8*)(img + k * 64 + (((c0 + 1) ^ tsw(k)) << 3)) = o[1];
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TR / 64; ++i) {
     const int c = tid + 256 * i;
@@ -274,6 +291,21 @@ __device__ __forceinline__ void store_lds(const GemmDesc& g, bool isA, int r0, i
       for (int j = 0; j < 16; ++j) S[rr16 + j][k] = o[j >> 3][j & 7];
     }
   }
+}
+
+// MFMA operand fragment (8 consecutive k of column col0 + lane % 16, k from 8 (lane / 16)) of a
+// TRI image: two transposed 8-byte reads of 4 rows each
+__device__ __forceinline__ bf16x8 tri_frag(const bf16* img, int ks, int col0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  bf16x4 v[2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const int r = ks + 8 * g + 4 * hf + q;
+    const int c = (col0 >> 3) + (p >> 1);
+    const bf16* a = img + r * 64 + ((c ^ tsw(r)) << 3) + (p & 1) * 4;
+    v[hf] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a)));
+  }
+  return bf16x8{v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
 }
 
 // dropout-backward scale of output element (m, n) (drop_on 3): element m * drop_ld + n of the
@@ -299,7 +331,7 @@ __device__ __forceinline__ int tile_of_block(const GemmBatch& batch, int& gi) {
   return tg - batch.d[gi].tile_base;
 }
 
-template <int FM, int FN, bool FAST, bool AH, bool BH>
+template <int FM, int FN, bool FAST, bool AH, bool BH, bool TRI = false>
 __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long off, int t,
                                           bf16 (*As)[LDT], bf16 (*Bs)[LDT]) {
   constexpr int TM = 32 * FM, TN = 32 * FN;
@@ -357,17 +389,20 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
           as_[j] += ah ? __uint_as_float((j & 1 ? qa[i][j >> 1] & 0xFFFF0000u : qa[i][j >> 1] << 16))
                        : __uint_as_float(qa[i][j]);
     }
-    store_lds<TM>(g, true, m0, k0, tid, qa, off, As, FAST ? AH : (bool)g.a_bf16);
-    store_lds<TN>(g, false, n0, k0, tid, qb, off, Bs, FAST ? BH : (bool)g.b_bf16);
+    store_lds<TM, TRI>(g, true, m0, k0, tid, qa, off, As, FAST ? AH : (bool)g.a_bf16);
+    store_lds<TN, TRI>(g, false, n0, k0, tid, qb, off, Bs, FAST ? BH : (bool)g.b_bf16);
     __syncthreads();
     if (k0 + NQ * TK < kend) load(k0 + NQ * TK, qa, qb);  // overlaps this and the next NQ-1 steps
 #pragma unroll
     for (int ks = 0; ks < TK; ks += 32) {
       bf16x8 a[FM], b[FN];
+      const bool ta = TRI && TM == 64 && g.a_mode == 1, tb = TRI && TN == 64 && g.b_mode == 1;  // block-uniform
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)&As[wm + i * 16 + fr][ks + fq * 8];
+      for (int i = 0; i < FM; ++i)
+        a[i] = ta ? tri_frag(&As[0][0], ks, wm + i * 16, lane) : *(const bf16x8*)&As[wm + i * 16 + fr][ks + fq * 8];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)&Bs[wn + j * 16 + fr][ks + fq * 8];
+      for (int j = 0; j < FN; ++j)
+        b[j] = tb ? tri_frag(&Bs[0][0], ks, wn + j * 16, lane) : *(const bf16x8*)&Bs[wn + j * 16 + fr][ks + fq * 8];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -441,7 +476,7 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
   }
 }
 
-template <int FM, int FN, bool FAST, bool AH, bool BH>
+template <int FM, int FN, bool FAST, bool AH, bool BH, bool TRI = false>
 __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) {
   __shared__ __attribute__((aligned(16))) bf16 As[32 * FM][LDT];
   __shared__ __attribute__((aligned(16))) bf16 Bs[32 * FN][LDT];
@@ -449,11 +484,12 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   const int t = tile_of_block(batch, gi);
   const GemmDesc& g = batch.d[gi];
   const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
-  gemm_tile<FM, FN, FAST, AH, BH>(g, off, t, As, Bs);
+  gemm_tile<FM, FN, FAST, AH, BH, TRI>(g, off, t, As, Bs);
 }
 
 // FAST loads with the operand dtypes per desc: a block-uniform switch into the four typed
 // bodies (one launch for, e.g., a backward's weight gradients over bf16 and fp32 inputs)
+template <bool TRI = false>
 __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch batch) {
   __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
   __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
@@ -463,14 +499,14 @@ __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch b
   const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
   if (g.a_bf16) {
     if (g.b_bf16)
-      gemm_tile<2, 2, true, true, true>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, true, true, TRI>(g, off, t, As, Bs);
     else
-      gemm_tile<2, 2, true, true, false>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, true, false, TRI>(g, off, t, As, Bs);
   } else {
     if (g.b_bf16)
-      gemm_tile<2, 2, true, false, true>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, false, true, TRI>(g, off, t, As, Bs);
     else
-      gemm_tile<2, 2, true, false, false>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, false, false, TRI>(g, off, t, As, Bs);
   }
 }
 
@@ -828,12 +864,27 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     const char* e = getenv("FEDREC_SG_OCC");
     return e ? atoi(e) : 0;
   }();
+  // stored-transposed operands of the 64x64 tiles as TRI images (FEDREC_SG_TR=0: the
+  // k-contiguous image with scalar transposed stores; the TRI form measured 0.5715 -> 0.5566 ms
+  // per config-2 step, profiles/r3_ab_sg_tri.txt)
+  static const bool tri = [] {
+    const char* e = getenv("FEDREC_SG_TR");
+    return e == nullptr || atoi(e) != 0;
+  }();
   if (!fast)
     hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);
   else if (mixed && occ == 5)
     hipLaunchKernelGGL(small_gemm_mixed_occ5_kernel, dim3(tiles), dim3(256), 0, s, b);
+  else if (mixed && tri)
+    hipLaunchKernelGGL(small_gemm_mixed_kernel<true>, dim3(tiles), dim3(256), 0, s, b);
   else if (mixed)
-    hipLaunchKernelGGL(small_gemm_mixed_kernel, dim3(tiles), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(small_gemm_mixed_kernel<false>, dim3(tiles), dim3(256), 0, s, b);
+  else if (tri && v == 1) {
+    if (dt == 0) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, false, true>), dim3(tiles), dim3(256), 0, s, b);
+    else if (dt == 1) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
+    else if (dt == 2) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, false, true>), dim3(tiles), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, true, true>), dim3(tiles), dim3(256), 0, s, b);
+  }
   else if (occ == 5 && v == 1) {
     if (dt == 0) hipLaunchKernelGGL((small_gemm_occ5_kernel<false, false>), dim3(tiles), dim3(256), 0, s, b);
     else if (dt == 1) hipLaunchKernelGGL((small_gemm_occ5_kernel<false, true>), dim3(tiles), dim3(256), 0, s, b);
