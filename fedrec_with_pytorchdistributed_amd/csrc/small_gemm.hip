@@ -28,6 +28,11 @@
 // tiles (the column tiles of one row panel, the splits of one tile) on one XCD's L2.  Long
 // reductions with few output tiles split K over workgroups into fp32 partials that a second
 // kernel sums in split order -- deterministic, no atomics.
+// Stored-transposed operands (mode 1) of the 64 x 64 tiles stay k-major in LDS (TRI images,
+// see tsw) and come back as MFMA fragments through ds_read_b64_tr_b16; the k-contiguous image
+// needed 16 scalar 2-byte stores per chunk (LDS bank conflicts at 0.5-0.66 of the LDS busy
+// cycles).  A register queue two k-tiles deep (SG_NQ = 2) measured slower on every launch of
+// the config-2 step, even the ones with fewer tiles than CUs (profiles/r3_ab_sg_nq2.txt).
 #include "common.h"
 
 #include <stdlib.h>

@@ -2,7 +2,7 @@
 # Small GEMM with stored-transposed operands staged as TRI images (default; FEDREC_SG_TR=0 = the
 # scalar-transposed-store image): numerics (small-GEMM, user-step, step-graph, text-head tests),
 # then bench arms A/B/A/B.  Recorded in profiles/r3_ab_sg_tri.txt (run while TRI was opt-in).
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
 check t_tr 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_small_gemm_gpu.py tests/test_user_step_gpu.py tests/test_step_graph.py tests/test_text_head_gpu.py
