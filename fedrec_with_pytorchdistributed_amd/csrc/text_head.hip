@@ -811,7 +811,13 @@ __device__ __forceinline__ void wg_transform(uint32_t base, int tid, int wave, f
 // its two LDS reads join the fragment reads, one wait covers both, and its VALU work is spread
 // between the MFMA groups (the MFMAs do not depend on it), its write after them.  The column
 // sums dw2 / db1 accumulate in every block (a few FMAs) and only the k-tile-0 blocks store them.
-template <int NSTAGE, bool IL = false>
+//
+// SW (staged waits, with IL): the stage's LDS reads go out in the order the MFMA groups consume
+// them -- the transform's e chunk and da first, the 8 X fragment halves, then g fragment i --
+// and each group waits only for its own reads (lgkmcnt 6 / 4 / 2 / 0: LDS reads retire in
+// order), so group 0's MFMAs start while the reads of groups 1-3 are still in the LDS queue
+// (the 8 waves leave one barrier together and all want the LDS at once).
+template <int NSTAGE, bool IL = false, bool SW = false>
 __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restrict__ e, const bf16* __restrict__ table,
                                                             const int* __restrict__ ids, const float* __restrict__ da,
                                                             int M, int T, int D, int Q, float* __restrict__ P,
@@ -890,6 +896,58 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
     if (st + NSTAGE - 1 < nsteps)
       wg_stage(smem + ((st + NSTAGE - 1) % NSTAGE) * WSTAGE, e, table, ids_lds, u_lo, da, T, D, Q, q0, k0,
                mb + (st + NSTAGE - 1) * WTM, me, wave, lane);
+    if constexpr (IL && SW) {
+      const bool tr = st + 1 < nsteps && xform;  // block-uniform
+      const uint32_t base = lds0 + (st % NSTAGE) * WSTAGE;
+      const uint32_t nb = lds0 + ((st + 1) % NSTAGE) * WSTAGE;
+      const uint32_t ea = nb + (tid >> 4) * 256 + (tid & 15) * 16;
+      // 18 reads whatever tr is (stage st+1's buffer is always a valid LDS address), so the
+      // counted waits are immediates
+      u32x4_t ev4 = lds_read128(ea);
+      float dav = lds_read32(nb + E_BYTES + X_BYTES + wave * 256 + (tid >> 4) * 4);
+      s16x4 xr[8], yr[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xr[2 * j] = tr_read(base + xo[j][0]);
+        xr[2 * j + 1] = tr_read(base + xo[j][1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        yr[2 * i] = tr_read(base + yo[i][0]);
+        yr[2 * i + 1] = tr_read(base + yo[i][1]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(6)"
+                   : "+v"(ev4), "+v"(dav), "+v"(xr[0]), "+v"(xr[1]), "+v"(xr[2]), "+v"(xr[3]), "+v"(xr[4]),
+                     "+v"(xr[5]), "+v"(xr[6]), "+v"(xr[7]), "+v"(yr[0]), "+v"(yr[1]));
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 ev = __builtin_bit_cast(bf16x8, ev4);
+      bf16x8 o;
+      bf16x8 xb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xb[j] = join(xr[2 * j], xr[2 * j + 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i == 1) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(yr[2]), "+v"(yr[3]));
+        if (i == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(yr[4]), "+v"(yr[5]));
+        if (i == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(yr[6]), "+v"(yr[7]));
+        const bf16x8 ya = join(yr[2 * i], yr[2 * i + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], ya, acc[i][j], 0, 0, 0);
+        if (tr) {
+#pragma unroll
+          for (int k = 2 * i; k < 2 * i + 2; ++k) {
+            const float f = (float)ev[k];
+            o[k] = f2bf(dav * (1.0f - f * f));
+            sw2[k] += dav * f;
+            ssum[k] += (float)o[k];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (tr) lds_write128(ea, __builtin_bit_cast(u32x4_t, o));
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
     if constexpr (IL) {
       const bool tr = st + 1 < nsteps && xform;  // block-uniform
       const uint32_t base = lds0 + (st % NSTAGE) * WSTAGE;
@@ -1439,12 +1497,13 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
     hipLaunchKernelGGL(head_wgrad64_kernel, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids,
                        da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, nreal);
   } else if (M > 0) {
-#define LAUNCH_WG(N, IL)                                                                                             \
-  hipLaunchKernelGGL((head_wgrad_kernel<N, IL>), dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, \
+#define LAUNCH_WG(N, IL, ...)                                                                                        \
+  hipLaunchKernelGGL((head_wgrad_kernel<N, IL, ##__VA_ARGS__>), dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, \
                      da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1, nreal)
     if (nst == 1) LAUNCH_WG(5, false);
     else if (nst == 2) LAUNCH_WG(6, false);
     else if (g_wg_variant & 8) LAUNCH_WG(4, false);  // bit 3: the transform as its own LDS pass
+    else if (g_wg_variant & 16) LAUNCH_WG(4, true, true);  // bit 4: staged LDS waits
     else LAUNCH_WG(4, true);  // (FEDREC_HEAD_WG bit 0 = no e -> g transform: diagnostic timing only)
 #undef LAUNCH_WG
   } else {

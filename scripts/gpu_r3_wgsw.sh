@@ -1,0 +1,19 @@
+#!/bin/bash
+# head_wgrad with staged LDS waits (FEDREC_HEAD_WG=16) vs the default: text-head tests under
+# the switch, then bench arms A/B/A/B.
+source "$(dirname "$0")/gpu_lib.sh"
+export PYTHONPATH=$PWD:$PYTHONPATH
+FEDREC_HEAD_WG=16 check t_sw 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_text_head_gpu.py tests/test_step_graph.py
+B="python -u bench.py --steps 50 --warmup 10 --round off --no-valid"
+run b_def 200 $B
+FEDREC_HEAD_WG=16 run b_sw 200 $B
+run b_def2 200 $B
+FEDREC_HEAD_WG=16 run b_sw2 200 $B
+for f in b_def b_sw b_def2 b_sw2; do echo "$f $(tail -1 gpurun_out/$f.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["steady_ms_per_step"])')"; done
+O=$PWD/gpurun_out/prof_sw
+rm -rf $O; mkdir -p $O
+FEDREC_HEAD_WG=16 run prof_sw 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o sw -- python -u bench.py --steps 30 --warmup 5 --round off --no-valid
+f=$(find $O -name "*kernel_trace.csv" | head -1)
+python benchmarks/step_breakdown.py "$f" --steps 20 > gpurun_out/breakdown_sw.txt 2>&1
+head -8 gpurun_out/breakdown_sw.txt
