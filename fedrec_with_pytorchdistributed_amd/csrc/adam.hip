@@ -72,6 +72,7 @@ struct MultiCast {
   unsigned char bf[MCAST_SEG];   // 1: bf16 destination, 0: fp32
   unsigned char vec[MCAST_SEG];  // 1: 16-byte aligned (vector path), 0: element by element
   int nseg;
+  long long* bump;  // optional: a device step counter advanced by one (block 0, lane 0)
 };
 
 __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
@@ -82,6 +83,7 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
     else hi = mid - 1;
   }
   const int sg = lo;
+  if (mc.bump != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *mc.bump += 1;
   const long base = (long)(blockIdx.x - mc.blk0[sg]) * MCAST_CHUNK;
   const float4* s4 = (const float4*)mc.src[sg];
   const long n = mc.n[sg];
@@ -109,12 +111,15 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
 }
 }  // namespace
 
-// 0 ok; 1 = too many segments / bad size or alignment (the caller rebuilds the pack instead)
+// 0 ok; 1 = too many segments / bad size or alignment (the caller rebuilds the pack instead).
+// bump (optional): an int64 device counter the launch advances by one -- the training step's
+// dropout / noise offset rides in the step's cast launch instead of a launch of its own
 extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                             hipStream_t s) {
+                             long long* bump, hipStream_t s) {
   if (nseg < 1 || nseg > MCAST_SEG) return 1;
   MultiCast mc{};
   mc.nseg = nseg;
+  mc.bump = bump;
   long blk = 0;
   for (int i = 0; i < nseg; ++i) {
     if (n[i] <= 0) return 1;

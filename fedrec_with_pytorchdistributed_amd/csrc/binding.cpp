@@ -106,7 +106,8 @@ int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int 
 int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, int tile, hipStream_t s);
-int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg, hipStream_t s);
+int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
+                  long long* bump, hipStream_t s);
 int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, const int* C, const int* ld, int nseg,
                     hipStream_t s);
 int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
@@ -1005,11 +1006,20 @@ void colsum_f32(const std::vector<at::Tensor>& X, const std::vector<at::Tensor>&
 }
 
 // fp32 tensors -> bf16 / fp32 destinations (contiguous slices allowed) in one launch per 96
-// (adam.hip), any size / alignment; false = not launched (an empty segment)
-bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst) {
+// (adam.hip), any size / alignment; false = not launched (an empty segment).  bump (optional
+// int64 [1] on the same device): advanced by one by the first launch
+bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst,
+                const c10::optional<at::Tensor>& bump) {
   const size_t n = src.size();
   TORCH_CHECK(n >= 1 && dst.size() == n, "fedrec::multi_cast: sizes");
   const c10::DeviceGuard g(dst[0].device());
+  long long* bp = nullptr;
+  if (bump.has_value() && bump->defined()) {
+    TORCH_CHECK(bump->device() == dst[0].device() && bump->scalar_type() == at::kLong && bump->numel() == 1 &&
+                    bump->is_contiguous(),
+                "fedrec::multi_cast: bump must be an int64 [1] tensor on the destinations' device");
+    bp = (long long*)bump->data_ptr<int64_t>();
+  }
   std::vector<const float*> sp(n);
   std::vector<void*> dp(n);
   std::vector<long> ne(n);
@@ -1029,7 +1039,8 @@ bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor
     if (ne[i] <= 0) return false;
   for (size_t i0 = 0; i0 < n; i0 += 96) {  // 96 segments per launch (kernel-argument size)
     const int k = (int)std::min<size_t>(96, n - i0);
-    TORCH_CHECK(fr_multi_cast(sp.data() + i0, dp.data() + i0, ne.data() + i0, bf.data() + i0, k, cur_stream()) == 0,
+    TORCH_CHECK(fr_multi_cast(sp.data() + i0, dp.data() + i0, ne.data() + i0, bf.data() + i0, k, i0 == 0 ? bp : nullptr,
+                              cur_stream()) == 0,
                 "fedrec::multi_cast: launch rejected");
   }
   return true;
@@ -1450,7 +1461,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
   m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg, int tile, Tensor?[] asum) -> ()");
   m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
-  m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst) -> bool");
+  m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst, Tensor(b!)? bump=None) -> bool");
   m.def("multi_cast_t(Tensor[] src, Tensor(a!)[] dst) -> bool");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");

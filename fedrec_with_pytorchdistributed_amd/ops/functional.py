@@ -564,11 +564,13 @@ def _user_cast_lists(wts, wb, bqkv):
             [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D], bqkv[2 * D:]])
 
 
-def step_weight_casts(text_encoder, user_encoder):
+def step_weight_casts(text_encoder, user_encoder, bump=None):
     """Every compute copy a fused training step needs, in ONE cast launch: the text head's att_fc1
     weight in bf16 (the head_score operand) and the user encoder's bf16 weight stack + fp32 Q|K|V
     bias (the user step's GEMM operands).  Returns ``(w1_bf16, (wb, bqkv))``; the two were a cast
-    kernel each (4.7 + 6.2 us per step)."""
+    kernel each (4.7 + 6.2 us per step).  ``bump`` (int64 [1] device counter, optional): advanced
+    by one in the same launch -- the step's dropout / noise offset (a torch ``add_`` of its own
+    cost 4.8 us at the end of every step)."""
     aa = text_encoder.additive_attention
     mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
     wts = (mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight, mha.W_V.bias,
@@ -577,7 +579,9 @@ def step_weight_casts(text_encoder, user_encoder):
     w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
     wb, bqkv = _user_weight_bufs(wts, w.device)
     src, dst = _user_cast_lists(wts, wb, bqkv)
-    ops.native.require_for(w).multi_cast([w.detach()] + [t.detach() for t in src], [w1b] + dst)
+    launched = ops.native.require_for(w).multi_cast([w.detach()] + [t.detach() for t in src], [w1b] + dst, bump)
+    if bump is not None and not launched:
+        bump.add_(1)
     return w1b, (wb, bqkv)
 
 

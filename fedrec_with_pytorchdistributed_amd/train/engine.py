@@ -68,6 +68,8 @@ _CAPTURE_MODE = os.environ.get("FEDREC_CAPTURE_MODE", "thread_local")
 
 _SKIP_PADDED = os.environ.get("FEDREC_SKIP_PADDED", "1") != "0"  # A/B switch
 _STEP_CASTS = os.environ.get("FEDREC_STEP_CASTS", "1") != "0"  # A/B switch (0: a cast launch per consumer)
+# the step counter advanced inside that cast launch (0: a torch add_ after the backward)
+_STEP_BUMP = os.environ.get("FEDREC_STEP_BUMP", "1") != "0"
 
 
 class _StepGraph:
@@ -406,9 +408,10 @@ class LocalEngine:
         if self.fused_user:
             dd = self._dedup(cand, his, pre)
             casts = None
-            if self.fused_head and _STEP_CASTS:  # every compute copy of the step's weights in one cast launch
-                self.sync_params()
-                casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder)
+            if self.fused_head and _STEP_CASTS:  # every compute copy of the step's weights in one cast launch,
+                self.sync_params()  # which also advances the dropout / noise step counter this step reads
+                casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder,
+                                             bump=self._rng_step if _STEP_BUMP else None)
             with obs.range("news_encode"):
                 v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
                                       w1b=casts[0] if casts is not None else None)
@@ -418,7 +421,8 @@ class LocalEngine:
                                           casts=casts[1] if casts is not None else None)
             with obs.range("backward"), OF.side_grads(self.device):
                 loss.backward(self._seed_one())
-            self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
+            if casts is None or not _STEP_BUMP:
+                self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
             self.flat.end_backward()
             return loss.detach()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True, pre=pre)

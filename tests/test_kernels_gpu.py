@@ -474,6 +474,11 @@ def test_multi_cast(dev):
     many_d = [torch.empty(64, device=dev, dtype=torch.bfloat16) for _ in range(130)]
     assert native.lib().multi_cast(many_s, many_d)
     assert all(torch.equal(b, a.to(torch.bfloat16)) for a, b in zip(many_s, many_d))
+    # the optional step-counter bump: +1 per call, however many launches the call takes
+    ctr = torch.full((1,), 41, device=dev, dtype=torch.int64)
+    assert native.lib().multi_cast(many_s, many_d, ctr)
+    assert native.lib().multi_cast(srcs, dsts, ctr)
+    assert int(ctr.item()) == 43
     # ragged sizes and 4-byte-aligned slices take the element path
     odd_s = [torch.randn(13, device=dev), torch.randn(1, device=dev), torch.randn(1001, device=dev)[1:]]
     odd_d = [torch.empty(13, device=dev), torch.empty(3, device=dev, dtype=torch.bfloat16)[1:2],
