@@ -812,7 +812,7 @@ __device__ __forceinline__ void wg_transform(uint32_t base, int tid, int wave, f
 // between the MFMA groups (the MFMAs do not depend on it), its write after them.  The column
 // sums dw2 / db1 accumulate in every block (a few FMAs) and only the k-tile-0 blocks store them.
 //
-// SW (staged waits, with IL): the stage's LDS reads go out in the order the MFMA groups consume
+// SW (staged waits, with IL; the default): the stage's LDS reads go out in the order the MFMA groups consume
 // them -- the transform's e chunk and da first, the 8 X fragment halves, then g fragment i --
 // and each group waits only for its own reads (lgkmcnt 6 / 4 / 2 / 0: LDS reads retire in
 // order), so group 0's MFMAs start while the reads of groups 1-3 are still in the LDS queue
@@ -1503,8 +1503,10 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
     if (nst == 1) LAUNCH_WG(5, false);
     else if (nst == 2) LAUNCH_WG(6, false);
     else if (g_wg_variant & 8) LAUNCH_WG(4, false);  // bit 3: the transform as its own LDS pass
-    else if (g_wg_variant & 16) LAUNCH_WG(4, true, true);  // bit 4: staged LDS waits
-    else LAUNCH_WG(4, true);  // (FEDREC_HEAD_WG bit 0 = no e -> g transform: diagnostic timing only)
+    else if (g_wg_variant & 16) LAUNCH_WG(4, true, false);  // bit 4: one LDS wait for all fragment reads
+    // default: staged LDS waits -- steady step 0.5498-0.5529 vs 0.5509-0.5534 ms over two calls
+    // (profiles/r3_ab_wgrad_sw_bump.txt).  (FEDREC_HEAD_WG bit 0 = no e -> g transform: diagnostic)
+    else LAUNCH_WG(4, true, true);
 #undef LAUNCH_WG
   } else {
     (void)hipMemsetAsync(scratch, 0, need * sizeof(float), s);

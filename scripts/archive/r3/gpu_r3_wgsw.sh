@@ -1,7 +1,8 @@
 #!/bin/bash
+# (run while the staged waits were opt-in; FEDREC_HEAD_WG=16 now selects the single-wait form)
 # head_wgrad with staged LDS waits (FEDREC_HEAD_WG=16) vs the default: text-head tests under
 # the switch, then bench arms A/B/A/B.
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
 FEDREC_HEAD_WG=16 check t_sw 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_text_head_gpu.py tests/test_step_graph.py

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Wave-state counters of the config-2 step (two --pmc passes of 8 SQ counters each, each pass
 # its own run of the same short bench) -> benchmarks/pmc_stalls.py; then the staged-wait
-# head_wgrad (FEDREC_HEAD_WG=16) bench arms again, and the step counter advanced in the cast
+# head_wgrad (FEDREC_HEAD_WG=16 = then the staged waits; since their adoption the single-wait form) bench arms again, and the step counter advanced in the cast
 # launch (default) vs a torch add_ (FEDREC_STEP_BUMP=0).
 source "$(dirname "$0")/gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
