@@ -213,7 +213,26 @@ __device__ __forceinline__ void hs_wait_sync() {  // this wave's stage landed ex
 // and the partial score sum_{q in slice} w2_q tanh(.) into a_out[y M + m] (b2 in slice 0); the
 // pool adds the slices.  Halving the W1 panel per block (192 of 384 columns) frees the LDS for a
 // third stage: two stages in flight while the MFMAs read one.
-template <int QF, int RF, int BK, int NST, int WQ = 4>
+// SW: staged LDS waits -- the X fragments first, then the W1 fragments in MFMA-row order, and
+// row i of the MFMAs waits only for W1 fragment i (lgkmcnt QFW - 1 - i), as head_wgrad's SW.
+template <int N>
+__device__ __forceinline__ void lgkm_tie(u32x4_t& r) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(r) : "n"(N));
+}
+__device__ __forceinline__ void lgkm_tie_rt(int n, u32x4_t& r) {  // n folds to a constant once unrolled
+  switch (n) {
+    case 0: lgkm_tie<0>(r); break;
+    case 1: lgkm_tie<1>(r); break;
+    case 2: lgkm_tie<2>(r); break;
+    case 3: lgkm_tie<3>(r); break;
+    case 4: lgkm_tie<4>(r); break;
+    case 5: lgkm_tie<5>(r); break;
+    case 6: lgkm_tie<6>(r); break;
+    default: lgkm_tie<7>(r); break;
+  }
+}
+
+template <int QF, int RF, int BK, int NST, int WQ = 4, bool SW = false>
 __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
                                                              int M, int T, int D, const bf16* __restrict__ W1,
                                                              const float* __restrict__ b1, const float* __restrict__ w2,
@@ -310,6 +329,24 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
       for (int i = 0; i < QFW; ++i) {
         const int r = wq * QFW * 16 + i * 16 + fr;
         wr[i] = lds_read128(Ws + r * RB + ((lc ^ hs_swz<BK>(r)) << 4));
+      }
+      if constexpr (SW) {
+        static_assert(QFW <= 8, "lgkmcnt staging");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < QFW; ++i) {
+          lgkm_tie_rt(QFW - 1 - i, wr[i]);  // X fragments (issued first) and W1 fragment i landed
+          if (i == 0) {
+#pragma unroll
+            for (int j = 0; j < RFW; ++j) asm volatile("" : "+v"(xr[j]));
+          }
+#pragma unroll
+          for (int j = 0; j < RFW; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wr[i]),
+                                                                __builtin_bit_cast(bf16x8, xr[j]), acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        continue;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1379,14 +1416,15 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   // columns, 192 rows, BK 64, 3 stages (partial scores, see head_score2_kernel); 0 ->
   // head_score_kernel
   if (Q == 384 && g_score_variant > 0) {
-#define LAUNCH_S2(QF, RF, BK, NST, WQ, NS)                                                                     \
-  hipLaunchKernelGGL((head_score2_kernel<QF, RF, BK, NST, WQ>), dim3((M + 32 * RF - 1) / (32 * RF), NS), dim3(512), \
+#define LAUNCH_S2(QF, RF, BK, NST, WQ, NS, ...)                                                                \
+  hipLaunchKernelGGL((head_score2_kernel<QF, RF, BK, NST, WQ, ##__VA_ARGS__>), dim3((M + 32 * RF - 1) / (32 * RF), NS), dim3(512), \
                      0, s, (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal)
     if (g_score_variant == 1) LAUNCH_S2(6, 4, 32, 4, 4, 1);
     else if (g_score_variant == 3) LAUNCH_S2(6, 4, 64, 2, 4, 1);
     else if (g_score_variant == 4) LAUNCH_S2(6, 6, 32, 3, 4, 1);
     else if (g_score_variant == 5) LAUNCH_S2(3, 6, 64, 3, 2, 2);
     else if (g_score_variant == 6) LAUNCH_S2(6, 5, 64, 2, 4, 1);  // 160 rows: ~491 tiles = 1.9 waves of 256 CUs
+    else if (g_score_variant == 7) LAUNCH_S2(6, 6, 64, 2, 4, 1, true);  // the default tiling, staged LDS waits
     else LAUNCH_S2(6, 6, 64, 2, 4, 1);
 #undef LAUNCH_S2
     return 0;
