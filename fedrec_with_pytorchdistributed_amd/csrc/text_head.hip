@@ -1409,9 +1409,11 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   if (!fr_head_supported(D, Q, T)) return 1;
   const int M = U * T;
   if (M == 0) return 0;
-  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 2);
-  // FEDREC_HEAD_SCORE (Q = 384): 2 (default) -> 192 rows, BK 64, 2 stages (bench A/B/A: steady
-  // step 0.5925 / 0.5859 / 0.5921 ms vs the 128-row form); 1 -> 128 rows, BK 32, 4 stages;
+  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 7);
+  // FEDREC_HEAD_SCORE (Q = 384): 7 (default) -> 192 rows, BK 64, 2 stages, staged LDS waits
+  // (steady step 0.5452-0.5473 vs 0.5477-0.5520 ms, three A/B pairs, profiles/r3_ab_score_sw.txt);
+  // 2 -> the same with one wait for all fragment reads (bench A/B/A: steady step 0.5925 / 0.5859
+  // / 0.5921 ms vs the 128-row form); 1 -> 128 rows, BK 32, 4 stages;
   // 3 -> 128 rows, BK 64, 2 stages; 4 -> 192 rows, BK 32, 3 stages; 5 -> two Q slices of 192
   // columns, 192 rows, BK 64, 3 stages (partial scores, see head_score2_kernel); 0 ->
   // head_score_kernel

@@ -1,7 +1,8 @@
 #!/bin/bash
-# head_score2 with staged LDS waits (FEDREC_HEAD_SCORE=7) vs the default tiling: text-head tests
+# head_score2 with staged LDS waits (FEDREC_HEAD_SCORE=7, since adopted as the default) vs the tiling
+# without them (then the default, now FEDREC_HEAD_SCORE=2): text-head tests
 # under the switch, then bench arms A/B/A/B.
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
 FEDREC_HEAD_SCORE=7 check t_hs 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_text_head_gpu.py tests/test_step_graph.py
