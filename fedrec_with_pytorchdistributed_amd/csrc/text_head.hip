@@ -1399,6 +1399,12 @@ int env_int(const char* k, int d) {
 
 }  // namespace
 
+// one default for every reader (fr_head_score_slices runs first: the binding sizes the score
+// buffer with it)
+static void score_variant_init() {
+  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 7);
+}
+
 extern "C" int fr_head_supported(int D, int Q, int T) {
   return D % 256 == 0 && D <= 1024 && (Q == 128 || Q == 256 || Q == 384) && T >= 1 && T <= MAXT;
 }
@@ -1409,7 +1415,7 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   if (!fr_head_supported(D, Q, T)) return 1;
   const int M = U * T;
   if (M == 0) return 0;
-  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 7);
+  score_variant_init();
   // FEDREC_HEAD_SCORE (Q = 384): 7 (default) -> 192 rows, BK 64, 2 stages, staged LDS waits
   // (steady step 0.5452-0.5473 vs 0.5477-0.5520 ms, three A/B pairs, profiles/r3_ab_score_sw.txt);
   // 2 -> the same with one wait for all fragment reads (bench A/B/A: steady step 0.5925 / 0.5859
@@ -1444,7 +1450,7 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
 
 // score partials per row: head_score writes a[slices][M] (the pool sums the slices)
 extern "C" int fr_head_score_slices(int Q) {
-  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 2);
+  score_variant_init();
   return Q == 384 && g_score_variant == 5 ? 2 : 1;
 }
 

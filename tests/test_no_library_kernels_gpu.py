@@ -60,3 +60,29 @@ def test_step_and_validation_use_only_our_kernels(dev, mask):
     assert any("small_gemm" in n for n in names) and any("user_attn" in n for n in names)
     bad = library_kernels(names)
     assert not bad, sorted(set(bad))
+
+
+def test_default_text_head_kernels(dev):
+    """The default step runs the staged-wait forms of the text-head GEMMs (head_score2 with
+    SW = true, head_wgrad <4, IL, SW>): guards the knob defaults of csrc/text_head.hip, which are
+    read once per process by whichever entry point runs first."""
+    cfg = FedRecConfig(mode="grad_avg", batch_size=16)  # the headline backbone (Q = 384 head)
+    torch.manual_seed(0)
+    m = FedRecModel(cfg).to(dev)
+    m.build_flat()
+    eng = LocalEngine(cfg, m, make_client_shards("tiny", 1)[0], dev)
+    if not eng.fused_head:
+        pytest.skip("this configuration does not take the fused text head")
+    batches = [tuple(eng.to_device(a) for a in b) for _, b in zip(range(2), eng.sampler.epoch(0))]
+    eng.train_step(*batches[0])
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        eng.train_step(*batches[1])
+        torch.cuda.synchronize()
+    names = _kernel_names(prof)
+    hs = [n for n in names if "head_score2_kernel" in n]
+    wg = [n for n in names if "head_wgrad_kernel" in n]
+    assert hs and wg, sorted(set(n for n in names if "head" in n))
+    # bool template arguments: mangled "Lb1E" or demangled "true>" (the last template argument)
+    assert all("Lb1EE" in n or n.split(">")[0].rstrip().endswith("true") for n in hs), sorted(set(hs))
+    assert all("Lb1ELb1EE" in n or "<4, true, true>" in n for n in wg), sorted(set(wg))
