@@ -729,9 +729,15 @@ static int choose_splits(int tiles, int K) {
   // (measured: the 1200 x 400 x 3200 weight gradient in 133 tiles -- 2 splits 69 us, four
   // 400-row descs in 6 splits 49 us; the 3200 x 400 x 1200 dgrad in 350 tiles -- 2 splits
   // 38.6 us, 3 splits 44.5: the partials' write + reduce outweigh the shorter chains).
+  static const int mink = [] {  // FEDREC_SG_MINK: fewest K per split (A/B; 384 = 6 k-tiles measured best of 192-768,
+    // profiles/r3_ab_sg_mink.txt)
+    const char* e = getenv("FEDREC_SG_MINK");
+    const int v = e ? atoi(e) : 384;
+    return v >= 64 ? v : 384;
+  }();
   if (K < 512) return 1;
   const int want = (512 + tiles - 1) / tiles;
-  int s = min(want, K / 384);
+  int s = min(want, K / mink);
   return max(1, min(s, 16));
 }
 
