@@ -336,9 +336,14 @@ __device__ __forceinline__ int tile_of_block(const GemmBatch& batch, int& gi) {
   return tg - batch.d[gi].tile_base;
 }
 
-template <int FM, int FN, bool FAST, bool AH, bool BH, bool TRI = false>
+// DB: two LDS buffers -- step s stores its tile into buffer s % 2, issues the next loads and
+// meets ONE barrier before its MFMAs (the single-buffer step needs a second barrier in front,
+// so no wave overwrites a tile another wave still reads); buffer s % 2 was last read by step
+// s - 2, which every wave finished before passing step s - 1's barrier.
+template <int FM, int FN, bool FAST, bool AH, bool BH, bool TRI = false, bool DB = false>
 __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long off, int t,
-                                          bf16 (*As)[LDT], bf16 (*Bs)[LDT]) {
+                                          bf16 (*As)[LDT], bf16 (*Bs)[LDT], bf16 (*As2)[LDT] = nullptr,
+                                          bf16 (*Bs2)[LDT] = nullptr) {
   constexpr int TM = 32 * FM, TN = 32 * FN;
   const int split = t % g.splits;
   t /= g.splits;
@@ -385,7 +390,10 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
   // one k-step: the queued tile into LDS, then its MFMAs; the slot is refilled with the tile NQ
   // steps ahead right after its registers were stored
   auto step = [&](int k0, uint32_t (&qa)[TM / 64][16], uint32_t (&qb)[TN / 64][16]) {
-    __syncthreads();  // the previous tile's fragments are consumed
+    const bool alt = DB && ((((k0 - kbeg) / TK) & 1) != 0);  // block-uniform
+    bf16 (*const Ab)[LDT] = alt ? As2 : As;
+    bf16 (*const Bb)[LDT] = alt ? Bs2 : Bs;
+    if (!DB) __syncthreads();  // the previous tile's fragments are consumed
     if (do_as) {
 #pragma unroll
       for (int i = 0; i < TM / 64; ++i)
@@ -394,20 +402,25 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
           as_[j] += ah ? __uint_as_float((j & 1 ? qa[i][j >> 1] & 0xFFFF0000u : qa[i][j >> 1] << 16))
                        : __uint_as_float(qa[i][j]);
     }
-    store_lds<TM, TRI>(g, true, m0, k0, tid, qa, off, As, FAST ? AH : (bool)g.a_bf16);
-    store_lds<TN, TRI>(g, false, n0, k0, tid, qb, off, Bs, FAST ? BH : (bool)g.b_bf16);
-    __syncthreads();
-    if (k0 + NQ * TK < kend) load(k0 + NQ * TK, qa, qb);  // overlaps this and the next NQ-1 steps
+    store_lds<TM, TRI>(g, true, m0, k0, tid, qa, off, Ab, FAST ? AH : (bool)g.a_bf16);
+    store_lds<TN, TRI>(g, false, n0, k0, tid, qb, off, Bb, FAST ? BH : (bool)g.b_bf16);
+    if (DB) {
+      if (k0 + NQ * TK < kend) load(k0 + NQ * TK, qa, qb);
+      __syncthreads();
+    } else {
+      __syncthreads();
+      if (k0 + NQ * TK < kend) load(k0 + NQ * TK, qa, qb);  // overlaps this and the next NQ-1 steps
+    }
 #pragma unroll
     for (int ks = 0; ks < TK; ks += 32) {
       bf16x8 a[FM], b[FN];
       const bool ta = TRI && TM == 64 && g.a_mode == 1, tb = TRI && TN == 64 && g.b_mode == 1;  // block-uniform
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        a[i] = ta ? tri_frag(&As[0][0], ks, wm + i * 16, lane) : *(const bf16x8*)&As[wm + i * 16 + fr][ks + fq * 8];
+        a[i] = ta ? tri_frag(&Ab[0][0], ks, wm + i * 16, lane) : *(const bf16x8*)&Ab[wm + i * 16 + fr][ks + fq * 8];
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        b[j] = tb ? tri_frag(&Bs[0][0], ks, wn + j * 16, lane) : *(const bf16x8*)&Bs[wn + j * 16 + fr][ks + fq * 8];
+        b[j] = tb ? tri_frag(&Bb[0][0], ks, wn + j * 16, lane) : *(const bf16x8*)&Bb[wn + j * 16 + fr][ks + fq * 8];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -481,37 +494,37 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
   }
 }
 
-template <int FM, int FN, bool FAST, bool AH, bool BH, bool TRI = false>
+template <int FM, int FN, bool FAST, bool AH, bool BH, bool TRI = false, bool DB = false>
 __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) bf16 As[32 * FM][LDT];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[32 * FN][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 As[DB ? 2 : 1][32 * FM][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[DB ? 2 : 1][32 * FN][LDT];
   int gi;
   const int t = tile_of_block(batch, gi);
   const GemmDesc& g = batch.d[gi];
   const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
-  gemm_tile<FM, FN, FAST, AH, BH, TRI>(g, off, t, As, Bs);
+  gemm_tile<FM, FN, FAST, AH, BH, TRI, DB>(g, off, t, As[0], Bs[0], As[DB ? 1 : 0], Bs[DB ? 1 : 0]);
 }
 
 // FAST loads with the operand dtypes per desc: a block-uniform switch into the four typed
 // bodies (one launch for, e.g., a backward's weight gradients over bf16 and fp32 inputs)
-template <bool TRI = false>
+template <bool TRI = false, bool DB = false>
 __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 As[DB ? 2 : 1][64][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[DB ? 2 : 1][64][LDT];
   int gi;
   const int t = tile_of_block(batch, gi);
   const GemmDesc& g = batch.d[gi];
   const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
   if (g.a_bf16) {
     if (g.b_bf16)
-      gemm_tile<2, 2, true, true, true, TRI>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, true, true, TRI, DB>(g, off, t, As[0], Bs[0], As[DB ? 1 : 0], Bs[DB ? 1 : 0]);
     else
-      gemm_tile<2, 2, true, true, false, TRI>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, true, false, TRI, DB>(g, off, t, As[0], Bs[0], As[DB ? 1 : 0], Bs[DB ? 1 : 0]);
   } else {
     if (g.b_bf16)
-      gemm_tile<2, 2, true, false, true, TRI>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, false, true, TRI, DB>(g, off, t, As[0], Bs[0], As[DB ? 1 : 0], Bs[DB ? 1 : 0]);
     else
-      gemm_tile<2, 2, true, false, false, TRI>(g, off, t, As, Bs);
+      gemm_tile<2, 2, true, false, false, TRI, DB>(g, off, t, As[0], Bs[0], As[DB ? 1 : 0], Bs[DB ? 1 : 0]);
   }
 }
 
@@ -882,14 +895,26 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     const char* e = getenv("FEDREC_SG_TR");
     return e == nullptr || atoi(e) != 0;
   }();
+  static const bool db = [] {  // FEDREC_SG_DB=1: two LDS buffers, one barrier per k-step (TRI kernels)
+    const char* e = getenv("FEDREC_SG_DB");
+    return e != nullptr && atoi(e) == 1;
+  }();
   if (!fast)
     hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);
   else if (mixed && occ == 5)
     hipLaunchKernelGGL(small_gemm_mixed_occ5_kernel, dim3(tiles), dim3(256), 0, s, b);
+  else if (mixed && tri && db)
+    hipLaunchKernelGGL((small_gemm_mixed_kernel<true, true>), dim3(tiles), dim3(256), 0, s, b);
   else if (mixed && tri)
     hipLaunchKernelGGL(small_gemm_mixed_kernel<true>, dim3(tiles), dim3(256), 0, s, b);
   else if (mixed)
     hipLaunchKernelGGL(small_gemm_mixed_kernel<false>, dim3(tiles), dim3(256), 0, s, b);
+  else if (tri && v == 1 && db) {
+    if (dt == 0) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
+    else if (dt == 1) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, true, true, true>), dim3(tiles), dim3(256), 0, s, b);
+    else if (dt == 2) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, true, true, true>), dim3(tiles), dim3(256), 0, s, b);
+  }
   else if (tri && v == 1) {
     if (dt == 0) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, false, true>), dim3(tiles), dim3(256), 0, s, b);
     else if (dt == 1) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
