@@ -895,9 +895,11 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     const char* e = getenv("FEDREC_SG_TR");
     return e == nullptr || atoi(e) != 0;
   }();
-  static const bool db = [] {  // FEDREC_SG_DB=1: two LDS buffers, one barrier per k-step (TRI kernels)
+  // two LDS buffers, one barrier per k-step on the TRI kernels (FEDREC_SG_DB=0: one buffer, two
+  // barriers): steady step 0.5484-0.5493 vs 0.5494-0.5520 ms, three A/B pairs (r3_ab_sg_db.txt)
+  static const bool db = [] {
     const char* e = getenv("FEDREC_SG_DB");
-    return e != nullptr && atoi(e) == 1;
+    return e == nullptr || atoi(e) != 0;
   }();
   if (!fast)
     hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);

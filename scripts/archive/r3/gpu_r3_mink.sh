@@ -1,7 +1,7 @@
 #!/bin/bash
 # Small-GEMM split-K granularity: fewest K per split (FEDREC_SG_MINK, arms via MINKS) vs 384 (default):
 # small-GEMM tests under the switch, bench arms, and the kernel breakdown of the 256 arm.
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
 FEDREC_SG_MINK=192 check t_mink 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_small_gemm_gpu.py tests/test_user_step_gpu.py

@@ -1,7 +1,8 @@
 #!/bin/bash
+# (run while the two buffers were opt-in; they are the default now, FEDREC_SG_DB=0 = one buffer)
 # Small GEMM with two LDS buffers and one barrier per k-step (FEDREC_SG_DB=1) vs the default:
 # numerics under the switch, then bench arms A/B/A/B.
-source "$(dirname "$0")/gpu_lib.sh"
+source "$(dirname "$0")/../../gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
 FEDREC_SG_DB=1 check t_db 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_small_gemm_gpu.py tests/test_user_step_gpu.py tests/test_step_graph.py tests/test_engine_gpu.py

@@ -77,11 +77,13 @@ def test_grouped_launch_and_odd_shapes(dev, tile):
         assert _rel(g.C, w) < 2e-3
 
 
-def test_scalar_transposed_store_form():
-    """FEDREC_SG_TR=0 (read once per process): the stored-transposed operands of the 64x64 tiles
-    through the k-contiguous image instead of the default TRI image -- the mode-1 cases again in a
-    child process"""
-    env = dict(os.environ, FEDREC_SG_TR="0")
+@pytest.mark.parametrize("knob", ["FEDREC_SG_TR", "FEDREC_SG_DB"])
+def test_scalar_transposed_store_form(knob):
+    """The non-default staging forms (knobs read once per process), the mode-1 cases again in a
+    child process: FEDREC_SG_TR=0 -- the stored-transposed operands of the 64x64 tiles through the
+    k-contiguous image instead of the TRI image; FEDREC_SG_DB=0 -- one LDS buffer and two
+    barriers per k-step instead of two buffers and one"""
+    env = dict(os.environ, **{knob: "0"})
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__, "-k",
            "(tn_wgrad or nn_dgrad or grouped) and not scalar_transposed"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300,
