@@ -135,6 +135,7 @@ def main() -> int:
         cfg.dp.enabled, cfg.dp.epsilon = True, args.dp_epsilon
         eng.sigma = calibrate_client_sigma(cfg.dp.epsilon, cfg.dp.delta, cfg.batch_size, len(shard.train), cfg.dp.epochs)
     pa_state = {"n": 0}
+    pa_ipc = fdist.data_ipc(ctx) if (args.config == 3 and dev.type == "cuda") else None
 
     def sync():
         if dev.type == "cuda":
@@ -160,7 +161,7 @@ def main() -> int:
         if args.config == 3:
             pa_state["n"] += 1
             if world > 1 and pa_state["n"] % args.pa_every == 0:
-                comm.allreduce_(model.sync_tensors(False), ctx.data_group, scale=1.0 / world)
+                comm.allreduce_(model.sync_tensors(False), ctx.data_group, scale=1.0 / world, ipc=pa_ipc)
         return loss
 
     # batches: sampled on the device inside the timed loop, one step ahead -- the next batch's
@@ -220,46 +221,49 @@ def main() -> int:
         from fedrec_with_pytorchdistributed_amd.parallel.collcheck import CHECK
         CHECK.verify(ctx.ctrl_group, "bench")
 
-    # untimed: the data-plane share of a step -- the same flat-bucket RCCL all-reduce the GA
-    # step issues, alone, averaged over 20 calls (bus bandwidth = 2 (W-1)/W x bytes / time)
+    # untimed: the data-plane share of a step -- the bucket the step all-reduces, alone, RCCL
+    # vs the custom IPC all-reduce (bus bandwidth = 2 (W-1)/W x bytes / time): configs 2-4 the
+    # flat fp32 4.66 MB bucket, config 5 one 28 MB int32 (masked) bucket of the reducer
     comm_ms = busbw = ipc_info = None
-    if ctx.initialized and world > 1 and dev.type == "cuda" and args.config in (2, 4):
-        g = torch.zeros_like(model.flat.grad)
-        for _ in range(3):
-            dist.all_reduce(g, group=ctx.data_group)
-        sync()
-        dist.barrier(group=ctx.ctrl_group)
-        t1 = time.perf_counter()
-        for _ in range(20):
-            dist.all_reduce(g, group=ctx.data_group)
-        sync()
-        ct = torch.tensor([(time.perf_counter() - t1) / 20], dtype=torch.float64)
-        dist.all_reduce(ct, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
-        comm_ms = 1000.0 * float(ct.item())
-        busbw = 2.0 * (world - 1) / world * g.numel() * g.element_size() / (comm_ms / 1000.0) / 1e9
-        # the custom IPC all-reduce (one-shot over xGMI) on the same bucket, for comparison; its
-        # result is checked against RCCL's first.  A failure is reported, not fatal.
+    if ctx.initialized and world > 1 and dev.type == "cuda":
+        if args.config == 5:
+            g = torch.zeros(7 << 20, dtype=torch.int32, device=dev)
+        else:
+            g = torch.zeros_like(model.flat.grad)
+        nbytes = g.numel() * g.element_size()
+
+        def timed(fn, reps=20):
+            for _ in range(3):
+                fn(g)
+            sync()
+            dist.barrier(group=ctx.ctrl_group)
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                fn(g)
+            sync()
+            ct = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64)
+            dist.all_reduce(ct, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
+            return 1000.0 * float(ct.item())
+
+        comm_ms = timed(lambda x: dist.all_reduce(x, group=ctx.data_group))
+        busbw = 2.0 * (world - 1) / world * nbytes / (comm_ms / 1000.0) / 1e9
+        # the custom IPC all-reduce (one-shot / two-shot over xGMI) on the same bucket; its result
+        # is checked against RCCL's first.  A failure is reported, not fatal.
         try:
             ipc = fdist.make_ipc_allreduce(ctx)
-            a = torch.randn_like(g)
+            if g.dtype == torch.int32:
+                a = torch.randint(-2**30, 2**30, g.shape, dtype=torch.int32, device=dev)
+            else:
+                a = torch.randn_like(g)
             b = a.clone()
             dist.all_reduce(a, group=ctx.data_group)
             ipc.allreduce_(b)
             sync()
-            ok = torch.allclose(a, b, rtol=1e-5, atol=1e-6)
-            for _ in range(3):
-                ipc.allreduce_(g)
-            sync()
-            dist.barrier(group=ctx.ctrl_group)
-            t1 = time.perf_counter()
-            for _ in range(20):
-                ipc.allreduce_(g)
-            sync()
-            ct = torch.tensor([(time.perf_counter() - t1) / 20], dtype=torch.float64)
-            dist.all_reduce(ct, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
-            ipc_ms = 1000.0 * float(ct.item())
-            ipc_info = {"ms": round(ipc_ms, 4), "matches_rccl": bool(ok), "status": ipc.status(),
-                        "busbw_GBps": round(2.0 * (world - 1) / world * g.numel() * 4 / (ipc_ms / 1000.0) / 1e9, 2)}
+            ok = bool(torch.equal(a, b)) if g.dtype == torch.int32 else bool(torch.allclose(a, b, rtol=1e-5, atol=1e-6))
+            ipc_ms = timed(ipc.allreduce_)
+            ipc_info = {"bucket_MB": round(nbytes / 2**20, 2), "dtype": str(g.dtype).split(".")[-1],
+                        "ms": round(ipc_ms, 4), "matches_rccl": ok, "status": ipc.status(),
+                        "busbw_GBps": round(2.0 * (world - 1) / world * nbytes / (ipc_ms / 1000.0) / 1e9, 2)}
             ipc.close()
         except Exception as e:  # pragma: no cover - depends on the node
             ipc_info = {"error": repr(e)[:300]}
@@ -286,7 +290,8 @@ def main() -> int:
         t1 = time.perf_counter()
         hook = None
         if args.config == 3 and world > 1:
-            hook = (lambda n: comm.allreduce_(model.sync_tensors(False), ctx.data_group, scale=1.0 / world)
+            hook = (lambda n: comm.allreduce_(model.sync_tensors(False), ctx.data_group, scale=1.0 / world,
+                                              ipc=pa_ipc)
                     if n % args.pa_every == 0 else None)
         st = eng.train_epoch(max_steps=steps_per_epoch, step_hook=hook)
         t2 = time.perf_counter()
@@ -330,7 +335,8 @@ def main() -> int:
                 "seq_len": cfg.title_len,
                 "history_len": cfg.max_his_len,
                 "parallelism": f"dp{world}",
-                "mode": MODES[args.config].format(k=args.pa_every),
+                "mode": (MODES[args.config].format(k=args.pa_every) if world > 1 else
+                         MODES[args.config].split(" (")[0] + " (1 client: no all-reduce issued)"),
                 "baseline_config": args.config,
             },
             "train_loss": round(loss, 5),

@@ -84,10 +84,8 @@ class SecAggConfig:
     enabled: bool = False
     frac_bits: int = 16  # fixed-point fraction bits for uint32 quantisation
     clip_value: float = 1024.0  # |x| bound before quantisation (model parameters, star uploads)
-    # secure GRADIENT averaging: coordinates are clamped to a running bound = headroom x the
-    # largest coordinate of the previous (public) mean gradient, quantised on the finest grid the
-    # W-client int32 sum allows (parallel.secagg.RunningMasker: no per-step collective beyond it)
-    bound_headroom: float = 4.0
+    # (secure GRADIENT averaging needs no setting: parallel.secagg.ExactMasker agrees on the bound
+    # per sum with a masked exponent histogram, so no coordinate is ever clamped)
 
 
 @dataclass

@@ -251,19 +251,25 @@ int g_dedup_variant = -1;  // FEDREC_DEDUP: 1 = register bitonic (default), 0 = 
 //   his[b]  = the last min(len, H) history ids, zero padded (truncate) / first H (compat)
 // Randomness: Philox(seed, offset = step) with counter (impression, draw): reproducible and
 // independent of the launch geometry.
+// valid = 1: the validation batch of client.py:158-165 -- cand[b] = [pos] + the LAST
+// min(n, npr) negatives (negs[-4:]), zero padded; no randomness (data/sampler.valid_candidates).
 __global__ __launch_bounds__(256) void sample_kernel(const int* __restrict__ rows, const int* __restrict__ pos,
                                                      const long long* __restrict__ neg_ptr, const int* __restrict__ negs,
                                                      const long long* __restrict__ his_ptr, const int* __restrict__ his,
                                                      int* __restrict__ cand, int* __restrict__ hout, int B, int npr,
                                                      int H, int truncate, unsigned long long seed,
-                                                     unsigned long long offset) {
+                                                     unsigned long long offset, int valid) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const int r = rows[b];
   const long long n0 = neg_ptr[r], n = neg_ptr[r + 1] - n0;
   int* cb = cand + (size_t)b * (npr + 1);
-  if (lane == 0) {
+  if (valid) {
+    if (lane == 0) cb[0] = pos[r];
+    const long long take = n < npr ? n : npr;
+    if (lane < npr) cb[1 + lane] = lane < take ? negs[n0 + n - take + lane] : 0;
+  } else if (lane == 0) {
     cb[0] = pos[r];
     if (n < npr) {
       for (int j = 0; j < npr; ++j) cb[1 + j] = j < n ? negs[n0 + j] : 0;
@@ -293,11 +299,12 @@ __global__ __launch_bounds__(256) void sample_kernel(const int* __restrict__ row
 
 extern "C" int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs,
                                const long long* his_ptr, const int* his, int* cand, int* hout, int B, int npr, int H,
-                               int truncate, unsigned long long seed, unsigned long long offset, hipStream_t s) {
+                               int truncate, unsigned long long seed, unsigned long long offset, int valid,
+                               hipStream_t s) {
   if (npr > 16 || B < 0) return 1;
   if (B == 0) return 0;
   hipLaunchKernelGGL(sample_kernel, dim3((B + 3) / 4), dim3(256), 0, s, rows, pos, neg_ptr, negs, his_ptr, his, cand,
-                     hout, B, npr, H, truncate, seed, offset);
+                     hout, B, npr, H, truncate, seed, offset, valid);
   return 0;
 }
 

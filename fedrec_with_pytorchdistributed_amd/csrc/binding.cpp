@@ -55,10 +55,11 @@ int fr_ipc_create(long cap, void* handle_out);
 int fr_ipc_open(int id, const void* handles, int me, int W, const long long* local_ptrs);
 long long fr_ipc_region(int id);
 int* fr_ipc_status(int id);
-int fr_ipc_allreduce(int id, void* x, long n, int is_int, long long epoch, int mode, int blocks, hipStream_t s);
+int fr_ipc_allreduce(int id, void* x, long n, int is_int, long long epoch, int mode, int blocks, double timeout_s,
+                     hipStream_t s);
 int fr_ipc_destroy(int id);
 int fr_ipc_allreduce_local(const int* ids, void* const* xs, int W, long n, int is_int, long long epoch, int mode,
-                           int blocks, hipStream_t s);
+                           int blocks, double timeout_s, hipStream_t s);
 int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, const int* keep,
                      hipStream_t s);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
@@ -75,7 +76,7 @@ int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long 
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
                     const int* his, int* cand, int* hout, int B, int npr, int H, int truncate, unsigned long long seed,
-                    unsigned long long offset, hipStream_t s);
+                    unsigned long long offset, int valid, hipStream_t s);
 int fr_dedup(const int* ids, int R, int num_news, int* uniq, int* inv, int* perm, int* seg_ptr, int* u_count,
              hipStream_t s);
 int fr_secagg_mask(const float* x, int* out, long n, float scale, float clipv, const unsigned long long* seeds,
@@ -101,9 +102,11 @@ int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* 
                          int c_rows, hipStream_t s);
 int fr_embed_grad_bf16(const void* dx, const int* sorted, const int* perm, int R, int D, float* dword, int* scratch,
                        hipStream_t s);
-int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int W, const unsigned long long* seeds,
-                       const int* signs, int npeers, unsigned long long round, hipStream_t s);
-int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s);
+int fr_secagg_hist(const float* x, long n, unsigned* scratch, int* out, const unsigned long long* seeds,
+                   const int* signs, int npeers, unsigned long long round, hipStream_t s);
+int fr_secagg_mask_exact(const float* x, int* out, long n, const int* H, int W, const unsigned long long* seeds,
+                         const int* signs, int npeers, unsigned long long round, hipStream_t s);
+int fr_secagg_unmask_exact(const int* x, float* out, long n, const int* H, int W, hipStream_t s);
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, int tile, hipStream_t s);
 int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
@@ -452,20 +455,21 @@ int64_t ipc_status(int64_t id) {  // device -> host read (tests / diagnostics on
   return v;
 }
 
-void ipc_allreduce_(int64_t id, at::Tensor x, int64_t epoch, int64_t mode, int64_t blocks) {
+void ipc_allreduce_(int64_t id, at::Tensor x, int64_t epoch, int64_t mode, int64_t blocks, double timeout_s) {
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kInt) && x.numel() % 4 == 0,
               "fedrec::ipc_allreduce_: contiguous fp32 / int32, numel % 4 == 0");
   const c10::DeviceGuard g(x.device());
   check_rc(fr_ipc_allreduce((int)id, x.data_ptr(), (long)x.numel(), x.scalar_type() == at::kInt ? 1 : 0,
-                            (long long)epoch, (int)mode, (int)blocks, cur_stream()),
+                            (long long)epoch, (int)mode, (int)blocks, timeout_s, cur_stream()),
            "ipc_allreduce_");
 }
 
 void ipc_destroy(int64_t id) { (void)fr_ipc_destroy((int)id); }
 
 // single-process rehearsal: every rank's context + tensor, one launch playing all ranks
-void ipc_allreduce_local_(at::IntArrayRef ids, at::TensorList xs, int64_t epoch, int64_t mode, int64_t blocks) {
+void ipc_allreduce_local_(at::IntArrayRef ids, at::TensorList xs, int64_t epoch, int64_t mode, int64_t blocks,
+                          double timeout_s) {
   TORCH_CHECK(ids.size() == xs.size() && !xs.empty() && xs.size() <= 16, "fedrec::ipc_allreduce_local_: W tensors");
   std::vector<int> iv(ids.begin(), ids.end());
   std::vector<void*> pv;
@@ -479,7 +483,7 @@ void ipc_allreduce_local_(at::IntArrayRef ids, at::TensorList xs, int64_t epoch,
   const c10::DeviceGuard g(xs[0].device());
   check_rc(fr_ipc_allreduce_local(iv.data(), pv.data(), (int)xs.size(), (long)xs[0].numel(),
                                   xs[0].scalar_type() == at::kInt ? 1 : 0, (long long)epoch, (int)mode, (int)blocks,
-                                  cur_stream()),
+                                  timeout_s, cur_stream()),
            "ipc_allreduce_local_");
 }
 
@@ -822,7 +826,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dedup(const at::Tenso
 std::tuple<at::Tensor, at::Tensor> sample_batch(const at::Tensor& rows, const at::Tensor& pos, const at::Tensor& neg_ptr,
                                                 const at::Tensor& negs, const at::Tensor& his_ptr, const at::Tensor& his,
                                                 int64_t npratio, int64_t H, bool truncate, int64_t seed,
-                                                int64_t offset) {
+                                                int64_t offset, bool valid) {
   for (auto* t : {&rows, &pos, &negs, &his}) {
     check_dev(*t, "sample_batch input");
     TORCH_CHECK(t->scalar_type() == at::kInt, "fedrec::sample_batch: int32 ids");
@@ -838,7 +842,7 @@ std::tuple<at::Tensor, at::Tensor> sample_batch(const at::Tensor& rows, const at
   check_rc(fr_sample_batch(rows.data_ptr<int>(), pos.data_ptr<int>(), (const long long*)neg_ptr.data_ptr<int64_t>(),
                            negs.data_ptr<int>(), (const long long*)his_ptr.data_ptr<int64_t>(), his.data_ptr<int>(),
                            cand.data_ptr<int>(), hout.data_ptr<int>(), (int)B, (int)npratio, (int)H, truncate ? 1 : 0,
-                           (unsigned long long)seed, (unsigned long long)offset, cur_stream()),
+                           (unsigned long long)seed, (unsigned long long)offset, valid ? 1 : 0, cur_stream()),
            "sample_batch");
   return {cand, hout};
 }
@@ -1099,36 +1103,55 @@ void multi_copy(const std::vector<at::Tensor>& src, const std::vector<at::Tensor
   check_rc(fr_multi_copy(sp.data(), dp.data(), ns.data(), nd.data(), fv.data(), (int)n, cur_stream()), "multi_copy");
 }
 
-// device-scale secure aggregation (parallel/secagg.py RunningMasker): the fixed-point exponent
-// is derived on the device from the running bound m (a device scalar) -- no host read, no sync
-at::Tensor secagg_mask_dev(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs, const at::Tensor& m,
-                           int64_t W, int64_t round) {
+// exact secure aggregation (parallel/secagg.py ExactMasker): a masked exponent histogram agrees on
+// the fixed-point bound (one tiny all-reduce), then the masked payload -- no host read, no sync
+at::Tensor secagg_hist(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs, int64_t round) {
   check_dev(x, "x");
   check_dev(seeds, "seeds");
   check_dev(signs, "signs");
-  check_dev(m, "m");
-  TORCH_CHECK(x.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && seeds.scalar_type() == at::kLong &&
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && seeds.scalar_type() == at::kLong &&
                   signs.scalar_type() == at::kInt && seeds.numel() == signs.numel(),
-              "fedrec::secagg_mask_dev: dtypes");
+              "fedrec::secagg_hist: dtypes");
   const c10::DeviceGuard g(x.device());
-  auto out = at::empty(x.sizes(), x.options().dtype(at::kInt));
-  check_rc(fr_secagg_mask_dev(x.data_ptr<float>(), out.data_ptr<int>(), (long)x.numel(), m.data_ptr<float>(), (int)W,
-                              (const unsigned long long*)seeds.data_ptr<int64_t>(), signs.data_ptr<int>(),
-                              (int)seeds.numel(), (unsigned long long)round, cur_stream()),
-           "secagg_mask_dev");
+  auto scratch = at::zeros({2}, x.options().dtype(at::kInt));
+  auto out = at::empty({256}, x.options().dtype(at::kInt));
+  check_rc(fr_secagg_hist(x.data_ptr<float>(), (long)x.numel(), (unsigned*)scratch.data_ptr<int>(), out.data_ptr<int>(),
+                          (const unsigned long long*)seeds.data_ptr<int64_t>(), signs.data_ptr<int>(),
+                          (int)seeds.numel(), (unsigned long long)round, cur_stream()),
+           "secagg_hist");
   return out;
 }
 
-void secagg_unmask_dev_(const at::Tensor& q, const at::Tensor& m, int64_t W, at::Tensor out) {
+at::Tensor secagg_mask_exact(const at::Tensor& x, const at::Tensor& seeds, const at::Tensor& signs,
+                             const at::Tensor& hist, int64_t W, int64_t round) {
+  check_dev(x, "x");
+  check_dev(seeds, "seeds");
+  check_dev(signs, "signs");
+  check_dev(hist, "hist");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && hist.scalar_type() == at::kInt &&
+                  hist.numel() == 256 && seeds.scalar_type() == at::kLong && signs.scalar_type() == at::kInt &&
+                  seeds.numel() == signs.numel(),
+              "fedrec::secagg_mask_exact: dtypes");
+  const c10::DeviceGuard g(x.device());
+  auto out = at::empty(x.sizes(), x.options().dtype(at::kInt));
+  check_rc(fr_secagg_mask_exact(x.data_ptr<float>(), out.data_ptr<int>(), (long)x.numel(), hist.data_ptr<int>(),
+                                (int)W, (const unsigned long long*)seeds.data_ptr<int64_t>(), signs.data_ptr<int>(),
+                                (int)seeds.numel(), (unsigned long long)round, cur_stream()),
+           "secagg_mask_exact");
+  return out;
+}
+
+void secagg_unmask_exact_(const at::Tensor& q, const at::Tensor& hist, int64_t W, at::Tensor out) {
   check_dev(q, "q");
-  check_dev(m, "m");
+  check_dev(hist, "hist");
   check_dev(out, "out");
-  TORCH_CHECK(q.scalar_type() == at::kInt && out.scalar_type() == at::kFloat && q.numel() == out.numel(),
-              "fedrec::secagg_unmask_dev_");
+  TORCH_CHECK(q.scalar_type() == at::kInt && out.scalar_type() == at::kFloat && q.numel() == out.numel() &&
+                  hist.scalar_type() == at::kInt && hist.numel() == 256 && out.is_contiguous(),
+              "fedrec::secagg_unmask_exact_");
   const c10::DeviceGuard g(q.device());
-  check_rc(fr_secagg_unmask_dev(q.data_ptr<int>(), out.data_ptr<float>(), (long)q.numel(), m.data_ptr<float>(), (int)W,
-                                cur_stream()),
-           "secagg_unmask_dev_");
+  check_rc(fr_secagg_unmask_exact(q.data_ptr<int>(), out.data_ptr<float>(), (long)q.numel(), hist.data_ptr<int>(),
+                                  (int)W, cur_stream()),
+           "secagg_unmask_exact_");
 }
 
 // ---- packed title rows (frozen backbone forward; title_attn.hip) ----------------------------
@@ -1434,8 +1457,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("ipc_region(int id) -> int", &ipc_region);
   m.def("ipc_status(int id) -> int", &ipc_status);
   m.def("ipc_destroy(int id) -> ()", &ipc_destroy);
-  m.def("ipc_allreduce_(int id, Tensor(a!) x, int epoch, int mode, int blocks) -> ()");
-  m.def("ipc_allreduce_local_(int[] ids, Tensor(a!)[] xs, int epoch, int mode, int blocks) -> ()");
+  m.def("ipc_allreduce_(int id, Tensor(a!) x, int epoch, int mode, int blocks, float timeout_s=60.) -> ()");
+  m.def("ipc_allreduce_local_(int[] ids, Tensor(a!)[] xs, int epoch, int mode, int blocks, float timeout_s=60.) -> ()");
   m.def("head_score(Tensor table, Tensor? ids, int T, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bool store_e, Tensor? nreal=None) -> (Tensor, Tensor)");
   m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens, Tensor? nreal=None) -> (Tensor, Tensor)");
   m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor? nreal=None) -> (Tensor, Tensor)");
@@ -1448,7 +1471,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset) -> (Tensor, Tensor)");
+  m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset, bool valid=False) -> (Tensor, Tensor)");
   m.def("secagg_mask(Tensor x, Tensor seeds, Tensor signs, float scale, float clipv, int round) -> (Tensor)");
   m.def("secagg_unmask(Tensor x, float inv_scale) -> Tensor");
   m.def("title_plan(Tensor mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
@@ -1464,8 +1487,9 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst, Tensor(b!)? bump=None) -> bool");
   m.def("multi_cast_t(Tensor[] src, Tensor(a!)[] dst) -> bool");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
-  m.def("secagg_mask_dev(Tensor x, Tensor seeds, Tensor signs, Tensor m, int W, int round) -> Tensor");
-  m.def("secagg_unmask_dev_(Tensor q, Tensor m, int W, Tensor(a!) out) -> ()");
+  m.def("secagg_hist(Tensor x, Tensor seeds, Tensor signs, int round) -> Tensor");
+  m.def("secagg_mask_exact(Tensor x, Tensor seeds, Tensor signs, Tensor hist, int W, int round) -> Tensor");
+  m.def("secagg_unmask_exact_(Tensor q, Tensor hist, int W, Tensor(a!) out) -> ()");
   m.def("dropout_add(Tensor h, Tensor? res, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_drop(Tensor qkv, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
   m.def("title_attention_bwd_drop(Tensor qkv, Tensor dout, Tensor mask, int n_heads, float p, int seed, int offset) -> Tensor");
@@ -1511,13 +1535,14 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("linear_gelu_dual", &linear_gelu_dual);
   m.impl("embed_grad", &embed_grad);
   m.impl("dropout_add", &dropout_add);
-  m.impl("secagg_mask_dev", &secagg_mask_dev);
+  m.impl("secagg_hist", &secagg_hist);
+  m.impl("secagg_mask_exact", &secagg_mask_exact);
   m.impl("small_gemm", &small_gemm);
   m.impl("colsum_f32", &colsum_f32);
   m.impl("multi_copy", &multi_copy);
   m.impl("multi_cast", &multi_cast);
   m.impl("multi_cast_t", &multi_cast_t);
-  m.impl("secagg_unmask_dev_", &secagg_unmask_dev_);
+  m.impl("secagg_unmask_exact_", &secagg_unmask_exact_);
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);
   m.impl("wgrad", &wgrad);

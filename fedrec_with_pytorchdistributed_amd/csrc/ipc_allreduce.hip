@@ -21,10 +21,12 @@
 // epoch e + 1, which every peer entered only after finishing its reads of epoch e.
 // Types: fp32 SUM, int32 wrap-around SUM (secure aggregation's masked fixed point).
 //
-// Liveness: the waits are bounded (spin limit, then a status word records the timeout and the
-// kernel exits), so a missing peer cannot hang the GPU; the host checks the status word when
-// it synchronises anyway (tests, the bench's self-check).  All flag traffic is vector stores /
-// loads with system-scope ordering.
+// Liveness: the waits are bounded by a wall-clock deadline (the caller's collective timeout);
+// then a status word records the timeout, the output is poisoned (NaN / INT_MIN) and the
+// kernel exits, so a missing peer cannot hang the GPU and cannot yield a silently wrong sum;
+// the host raises on the status word at its next check (IpcAllReduce.check: the GA step wrapper
+// at every epoch end, the bench).  All flag traffic is vector stores / loads with system-scope
+// ordering.
 #include "common.h"
 
 #include <stdint.h>
@@ -45,21 +47,30 @@ __device__ __forceinline__ long long* flag_ptr(char* region, int phase, int r, i
 
 // grid-wide barrier among the W ranks for `phase` / `epoch`: this block publishes (its writes,
 // then flag[phase][me][block] := epoch in every rank's region), then waits until every block of
-// every rank has published.  Returns false on timeout (status recorded, kernel exits).
+// every rank has published.  Publication order: EVERY thread makes its own slot stores visible
+// at system scope (release fence + drained vmcnt) before the workgroup barrier, and only then
+// do lanes < W store the flags -- a workgroup-scope barrier alone orders other waves' stores
+// for this CU, not for a remote agent.  The inline vmcnt(0) after the fences is deliberate: the
+// compiler may drop the wait after the L2 write-back when it believes vmcnt is already empty.
+// Waits are bounded by a wall-clock deadline (s_memrealtime, 100 MHz): on timeout the status
+// word is set and the caller poisons its output; returns false then.
 __device__ bool rank_barrier(const Peers& P, int me, int W, int phase, long long epoch, int* status, int blk,
-                             int nb) {
-  __syncthreads();  // this block's writes precede its publication
+                             int nb, unsigned long long deadline_ticks) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope, every thread: its own stores first
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave of this block has published its stores
   if (threadIdx.x < (unsigned)W) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: visible to the peers first
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(flag_ptr(P.base[threadIdx.x], phase, me, blk), epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
   bool ok = true;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (int j = threadIdx.x; j < W * nb; j += blockDim.x) {
     long long* f = flag_ptr(P.base[me], phase, j / nb, j % nb);
-    long spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      if (++spins > (1L << 24)) {  // ~seconds: a peer never arrived
+      if (__builtin_amdgcn_s_memrealtime() - t0 > deadline_ticks) {  // a peer never arrived
         ok = false;
         __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -69,6 +80,20 @@ __device__ bool rank_barrier(const Peers& P, int me, int W, int phase, long long
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   return __syncthreads_and(ok);
+}
+
+// a timed-out call leaves this block's part of x poisoned (fp32: NaN, int32: INT_MIN, a value
+// no masked sum depends on being), so a caller that misses the status word still fails loudly
+template <typename T>
+__device__ void poison(T* __restrict__ x, long n4, long t0, long stride) {
+  const T v = __is_same(T, int) ? (T)(-2147483647 - 1) : (T)__builtin_nanf("");
+  for (long i = t0; i < n4; i += stride) {
+    T* p = x + 4 * i;
+    p[0] = v;
+    p[1] = v;
+    p[2] = v;
+    p[3] = v;
+  }
 }
 
 template <typename T>
@@ -101,7 +126,7 @@ struct Xs {
 template <typename T>
 __global__ __launch_bounds__(AR_THREADS) void ipc_allreduce_kernel(Xs<T> xs, long n, Peers P, int me_arg, int W,
                                                                   long long epoch, long cap, int mode, int nb,
-                                                                  int multi) {
+                                                                  int multi, unsigned long long deadline) {
   const int me = multi ? (int)blockIdx.x / nb : me_arg;
   const int blk = multi ? (int)blockIdx.x % nb : (int)blockIdx.x;
   T* __restrict__ x = xs.x[multi ? me : 0];
@@ -111,8 +136,16 @@ __global__ __launch_bounds__(AR_THREADS) void ipc_allreduce_kernel(Xs<T> xs, lon
   const long n4 = n / 4;
   const long stride = (long)nb * blockDim.x;
   const long t0 = (long)blk * blockDim.x + threadIdx.x;
+  // a previous call timed out: the peers' epochs no longer line up -- fail fast (poisoned)
+  if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+    poison(x, n4, t0, stride);
+    return;
+  }
   for (long i = t0; i < n4; i += stride) *(float4*)(mine + 4 * i) = *(const float4*)(x + 4 * i);
-  if (!rank_barrier(P, me, W, 0, epoch, status, blk, nb)) return;
+  if (!rank_barrier(P, me, W, 0, epoch, status, blk, nb, deadline)) {
+    poison(x, n4, t0, stride);
+    return;
+  }
   if (mode == 0) {
     for (long i = t0; i < n4; i += stride) {
       T acc[4] = {0, 0, 0, 0};
@@ -129,7 +162,10 @@ __global__ __launch_bounds__(AR_THREADS) void ipc_allreduce_kernel(Xs<T> xs, lon
     for (int p = 0; p < W; ++p) add4(acc, (const T*)(P.base[p] + slot_off) + 4 * i);
     *(float4*)(mine + 4 * i) = __builtin_bit_cast(float4, acc);  // own slice of own slot: reduced
   }
-  if (!rank_barrier(P, me, W, 1, epoch, status, blk, nb)) return;
+  if (!rank_barrier(P, me, W, 1, epoch, status, blk, nb, deadline)) {
+    poison(x, n4, t0, stride);
+    return;
+  }
   for (long i = t0; i < n4; i += stride) {
     const int owner = (int)(i / per);
     *(float4*)(x + 4 * i) = *(const float4*)((const T*)(P.base[owner] + slot_off) + 4 * i);
@@ -219,25 +255,27 @@ extern "C" int* fr_ipc_status(int id) { return (id >= 0 && id < 64 && g_ctx[id])
 
 // x: device pointer of n elements (is_int: int32 wrap-around sum, else fp32); n % 4 == 0 and
 // n * 4 <= cap (host-checked by the caller)
+// timeout_s: bound of every barrier wait (wall clock; the status word records a timeout)
 extern "C" int fr_ipc_allreduce(int id, void* x, long n, int is_int, long long epoch, int mode, int blocks,
-                                hipStream_t s) {
+                                double timeout_s, hipStream_t s) {
   if (id < 0 || id >= 64 || g_ctx[id] == nullptr) return -1;
   Ctx* c = g_ctx[id];
   if (n % 4 != 0 || n * 4 > c->cap || c->W < 1) return -2;
   if (n == 0) return 0;
   const int nb = blocks > 0 ? (blocks < MAXB ? blocks : MAXB) : AR_BLOCKS;
+  const unsigned long long dl = (unsigned long long)((timeout_s > 0 ? timeout_s : 60.0) * 1e8);
   if (is_int) {
     Xs<int> xs{};
     xs.x[0] = (int*)x;
     xs.status[0] = c->status;
     hipLaunchKernelGGL(ipc_allreduce_kernel<int>, dim3(nb), dim3(AR_THREADS), 0, s, xs, n, c->P, c->me, c->W, epoch,
-                       c->cap, mode, nb, 0);
+                       c->cap, mode, nb, 0, dl);
   } else {
     Xs<float> xs{};
     xs.x[0] = (float*)x;
     xs.status[0] = c->status;
     hipLaunchKernelGGL(ipc_allreduce_kernel<float>, dim3(nb), dim3(AR_THREADS), 0, s, xs, n, c->P, c->me, c->W,
-                       epoch, c->cap, mode, nb, 0);
+                       epoch, c->cap, mode, nb, 0, dl);
   }
   return 0;
 }
@@ -245,7 +283,7 @@ extern "C" int fr_ipc_allreduce(int id, void* x, long n, int is_int, long long e
 // single-process rehearsal: ids[W] contexts of this process (opened with local_ptrs), xs[W] their
 // inputs; one launch plays every rank
 extern "C" int fr_ipc_allreduce_local(const int* ids, void* const* xs_in, int W, long n, int is_int, long long epoch,
-                                      int mode, int blocks, hipStream_t s) {
+                                      int mode, int blocks, double timeout_s, hipStream_t s) {
   if (W < 1 || W > MAXW) return -1;
   for (int r = 0; r < W; ++r)
     if (ids[r] < 0 || ids[r] >= 64 || g_ctx[ids[r]] == nullptr || g_ctx[ids[r]]->me != r) return -1;
@@ -253,6 +291,7 @@ extern "C" int fr_ipc_allreduce_local(const int* ids, void* const* xs_in, int W,
   if (n % 4 != 0 || n * 4 > c->cap) return -2;
   if (n == 0) return 0;
   const int nb = blocks > 0 ? (blocks < MAXB ? blocks : MAXB) : AR_BLOCKS;
+  const unsigned long long dl = (unsigned long long)((timeout_s > 0 ? timeout_s : 60.0) * 1e8);
   if (is_int) {
     Xs<int> xs{};
     for (int r = 0; r < W; ++r) {
@@ -260,7 +299,7 @@ extern "C" int fr_ipc_allreduce_local(const int* ids, void* const* xs_in, int W,
       xs.status[r] = g_ctx[ids[r]]->status;
     }
     hipLaunchKernelGGL(ipc_allreduce_kernel<int>, dim3(nb * W), dim3(AR_THREADS), 0, s, xs, n, c->P, 0, W, epoch,
-                       c->cap, mode, nb, 1);
+                       c->cap, mode, nb, 1, dl);
   } else {
     Xs<float> xs{};
     for (int r = 0; r < W; ++r) {
@@ -268,7 +307,7 @@ extern "C" int fr_ipc_allreduce_local(const int* ids, void* const* xs_in, int W,
       xs.status[r] = g_ctx[ids[r]]->status;
     }
     hipLaunchKernelGGL(ipc_allreduce_kernel<float>, dim3(nb * W), dim3(AR_THREADS), 0, s, xs, n, c->P, 0, W, epoch,
-                       c->cap, mode, nb, 1);
+                       c->cap, mode, nb, 1, dl);
   }
   return 0;
 }

@@ -41,42 +41,115 @@ __global__ __launch_bounds__(256) void unmask_kernel(const int* __restrict__ x, 
     out[i] = (float)x[i] * inv_scale;
 }
 
-// ---- device-scale variants (bucketed gradient averaging, no host sync) ---------------------
-// The fixed-point exponent comes from m = max_k max|x_k| (a device scalar, MAX all-reduced
-// over the clients): f = clamp(floor(log2(2^30 / (W m))), 0, 56) so the W-client sum of
-// |Q(x)| <= 2^30 fits int32.  Every client derives the same f from the same bits of m.  One
-// Philox call masks 4 consecutive elements (counter = element / 4, word = element % 4).
-__device__ __forceinline__ float frac_exp2(const float* __restrict__ mdev, int W, float sign) {
-  float m = mdev[0];
-  if (!(m > 1e-30f)) m = 1e-30f;  // also NaN
-  if (!(m < 3.0e38f)) m = 3.0e38f;
-  float f = floorf(log2f(1073741824.0f / ((float)W * m)));
-  f = fminf(fmaxf(f, 0.f), 56.f);
-  return exp2f(sign * f);
+// ---- exact device variants (bucketed gradient averaging, no host sync) ----------------------
+// Per sum, a PRE-PASS agrees on a bound every client's values fit: each client adds a one-hot of
+// the binary exponent of its own max|x| (plus its count of non-finite coordinates) into a masked
+// int32 histogram of HB slots, one tiny SUM all-reduce of it, and every client reads the largest
+// occupied slot: m = 2^E >= max_k max|x_k|.  Nothing is ever clamped, so the fixed-point sum is
+// the plain sum to within the grid; the histogram discloses only how many clients have their
+// maximum in each power-of-two range (the masks hide whose).
+//   slot 0: max|x| = 0;  slot 1: non-finite count;  slot s >= 2: max|x| in [2^(s-128), 2^(s-127))
+//   (exponent field e of the fp32 max -> s = max(e, 1) + 1; subnormals share slot 2).
+// f = 30 - ceil(log2 W) - E (W m 2^f <= 2^30: the W-client int32 sum cannot wrap), clamped to
+// [-120, 60].  One Philox call masks 4 consecutive elements (counter = element / 4).
+constexpr int HB = 256;
+
+__device__ __forceinline__ int ceil_log2(int W) {
+  int c = 0;
+  while ((1 << c) < W) ++c;
+  return c;
 }
 
-__global__ __launch_bounds__(256) void mask_dev_kernel(const float* __restrict__ x, int* __restrict__ out, long n,
-                                                       const float* __restrict__ mdev, int W,
-                                                       const unsigned long long* __restrict__ seeds,
-                                                       const int* __restrict__ signs, int npeers,
-                                                       unsigned long long round) {
+// every thread of the block (blockDim >= HB) returns 2^f (sign > 0) or 2^-f; *bad = non-finite seen
+__device__ float hist_scale(const int* __restrict__ H, int W, float sign, bool* bad) {
+  __shared__ int smax, snf;
+  if (threadIdx.x == 0) {
+    smax = 0;
+    snf = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x < HB) {
+    const int h = H[threadIdx.x];
+    if (threadIdx.x >= 2 && h != 0) atomicMax(&smax, (int)threadIdx.x);
+    if (threadIdx.x == 1 && h != 0) snf = 1;
+  }
+  __syncthreads();
+  *bad = snf != 0;
+  if (smax == 0) return 1.f;  // every coordinate of every client is 0
+  int f = 30 - ceil_log2(W) - (smax - 127);
+  f = f < -120 ? -120 : (f > 60 ? 60 : f);
+  return ldexpf(1.f, sign > 0.f ? f : -f);
+}
+
+// scratch[0] |= max over finite |x| (fp32 bits: ordered as unsigned), scratch[1] += non-finite count
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long n, unsigned* __restrict__ scratch) {
+  unsigned mx = 0, nf = 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = fabsf(x[i]);
+    if (v <= 3.4028234663852886e38f)
+      mx = mx > __float_as_uint(v) ? mx : __float_as_uint(v);
+    else
+      ++nf;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned m2 = __shfl_xor(mx, o, 64);
+    mx = mx > m2 ? mx : m2;
+    nf += __shfl_xor(nf, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (mx) atomicMax(&scratch[0], mx);
+    if (nf) atomicAdd(&scratch[1], nf);
+  }
+}
+
+// one block of HB / 4 threads: this client's masked histogram
+__global__ __launch_bounds__(64) void hist_kernel(const unsigned* __restrict__ scratch, int* __restrict__ out,
+                                                  const unsigned long long* __restrict__ seeds,
+                                                  const int* __restrict__ signs, int npeers,
+                                                  unsigned long long round) {
+  const unsigned bits = scratch[0], nf = scratch[1];
+  const int e = (int)(bits >> 23);
+  const int slot = bits == 0 ? 0 : (e > 1 ? e : 1) + 1;
+  const int g = threadIdx.x;
+  uint32_t acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int s = 4 * g + j;
+    acc[j] = (s == slot ? 1u : 0u) + (s == 1 ? nf : 0u);
+  }
+  for (int p = 0; p < npeers; ++p) {
+    const uint4 r = Philox::gen(seeds[p], round, (unsigned long long)g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t rr = u4_get(r, j);
+      acc[j] += signs[p] > 0 ? rr : (uint32_t)(0u - rr);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[4 * g + j] = (int32_t)acc[j];
+}
+
+__global__ __launch_bounds__(256) void mask_exact_kernel(const float* __restrict__ x, int* __restrict__ out, long n,
+                                                         const int* __restrict__ H, int W,
+                                                         const unsigned long long* __restrict__ seeds,
+                                                         const int* __restrict__ signs, int npeers,
+                                                         unsigned long long round) {
   __shared__ unsigned long long sd[MAXP];
   __shared__ int sg[MAXP];
   for (int i = threadIdx.x; i < npeers; i += blockDim.x) {
     sd[i] = seeds[i];
     sg[i] = signs[i];
   }
-  __syncthreads();
-  const float scale = frac_exp2(mdev, W, 1.f);
-  float clipv = mdev[0];
-  if (!(clipv >= 0.f)) clipv = 0.f;
+  bool bad;
+  const float scale = hist_scale(H, W, 1.f, &bad);  // (its barriers also cover sd / sg)
   const long n4 = (n + 3) >> 2;
   for (long g = blockIdx.x * (long)blockDim.x + threadIdx.x; g < n4; g += (long)gridDim.x * blockDim.x) {
     uint32_t acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long i = g * 4 + j;
-      const float v = i < n ? fminf(fmaxf(x[i], -clipv), clipv) : 0.f;
+      float v = i < n ? x[i] : 0.f;
+      if (!(fabsf(v) <= 3.4028234663852886e38f)) v = 0.f;  // counted in the histogram instead
       acc[j] = (uint32_t)(int32_t)rintf(v * scale);
     }
     for (int p = 0; p < npeers; ++p) {
@@ -93,11 +166,15 @@ __global__ __launch_bounds__(256) void mask_dev_kernel(const float* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void unmask_dev_kernel(const int* __restrict__ x, float* __restrict__ out, long n,
-                                                         const float* __restrict__ mdev, int W) {
-  const float inv = frac_exp2(mdev, W, -1.f);
+// the sum, dequantised; NaN everywhere if any client had a non-finite coordinate (as the plain
+// sum would have been non-finite)
+__global__ __launch_bounds__(256) void unmask_exact_kernel(const int* __restrict__ x, float* __restrict__ out, long n,
+                                                           const int* __restrict__ H, int W) {
+  bool bad;
+  const float inv = hist_scale(H, W, -1.f, &bad);
+  const float nan = __builtin_nanf("");
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    out[i] = (float)x[i] * inv;
+    out[i] = bad ? nan : (float)x[i] * inv;
 }
 
 unsigned grid_for(long n) {
@@ -122,19 +199,28 @@ extern "C" int fr_secagg_unmask(const int* x, float* out, long n, float inv_scal
   return 0;
 }
 
-extern "C" int fr_secagg_mask_dev(const float* x, int* out, long n, const float* mdev, int W,
-                                  const unsigned long long* seeds, const int* signs, int npeers,
-                                  unsigned long long round, hipStream_t s) {
+// x [n] fp32 -> masked histogram out [HB] int32 (scratch: 2 zeroed uint32)
+extern "C" int fr_secagg_hist(const float* x, long n, unsigned* scratch, int* out, const unsigned long long* seeds,
+                              const int* signs, int npeers, unsigned long long round, hipStream_t s) {
+  if (npeers > MAXP) return 1;
+  if (n > 0) hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, scratch);
+  hipLaunchKernelGGL(hist_kernel, dim3(1), dim3(HB / 4), 0, s, scratch, out, seeds, signs, npeers, round);
+  return 0;
+}
+
+extern "C" int fr_secagg_mask_exact(const float* x, int* out, long n, const int* H, int W,
+                                    const unsigned long long* seeds, const int* signs, int npeers,
+                                    unsigned long long round, hipStream_t s) {
   if (npeers > MAXP || W < 1) return 1;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(mask_dev_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, x, out, n, mdev, W, seeds, signs,
+  hipLaunchKernelGGL(mask_exact_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, x, out, n, H, W, seeds, signs,
                      npeers, round);
   return 0;
 }
 
-extern "C" int fr_secagg_unmask_dev(const int* x, float* out, long n, const float* mdev, int W, hipStream_t s) {
+extern "C" int fr_secagg_unmask_exact(const int* x, float* out, long n, const int* H, int W, hipStream_t s) {
   if (W < 1) return 1;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(unmask_dev_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, out, n, mdev, W);
+  hipLaunchKernelGGL(unmask_exact_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, out, n, H, W);
   return 0;
 }

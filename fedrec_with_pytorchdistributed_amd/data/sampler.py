@@ -154,3 +154,18 @@ class DeviceSampler:
             self.step += 1
             yield lib.sample_batch(rows, self.pos, self.neg_ptr, self.negs, self.his_ptr, self.his, self.npratio,
                                    self.H, self.truncate, seed, self.step)
+
+    def valid_batches(self, batch_size: int, limit: Optional[int] = None):
+        """The validation batches of :func:`validation_batches` assembled on the device
+        (``[pos] + negs[-4:]``, the same history rule), in row order: ``(cand, his)`` device
+        tensors, no host work and no H2D copy per batch."""
+        import torch
+
+        from ..ops import native
+
+        lib = native.lib()
+        n = self.n if limit is None else min(limit, self.n)
+        rows = torch.arange(n, dtype=torch.int32, device=self.device)
+        for s in range(0, n, batch_size):
+            yield lib.sample_batch(rows[s:s + batch_size], self.pos, self.neg_ptr, self.negs, self.his_ptr, self.his,
+                                   self.npratio, self.H, self.truncate, 0, 0, True)

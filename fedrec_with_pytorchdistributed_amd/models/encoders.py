@@ -67,6 +67,10 @@ class UserEncoder(nn.Module):
     def __init__(self, cfg: FedRecConfig):
         super().__init__()
         self.dropout_rate = cfg.user_dropout
+        # device path's train-mode input dropout: Philox key (the engine sets it from the config
+        # seed and the client rank) and a per-forward counter (checkpointed via engine.state())
+        self.drop_seed = (int(cfg.seed) << 20) + 2
+        self.drop_calls = 0
         self.multihead_attention = MultiHeadAttention(cfg.news_dim, cfg.user_heads, cfg.user_head_dim,
                                                       cfg.user_head_dim)
         self.additive_attention = AdditiveAttention(cfg.news_dim, cfg.user_query_dim)

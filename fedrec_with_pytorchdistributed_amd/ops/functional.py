@@ -828,18 +828,17 @@ class UserEncoderFn(torch.autograd.Function):
         return (dx.view(B, H, D),) + grads + (None,)
 
 
-_MODULE_DROP_STEP = [0]
-
-
 def user_encoder_device(user_encoder, clicked, keep=None):
     """``UserEncoder.forward`` on the device (see :class:`UserEncoderFn`).  Train-mode input
-    dropout draws a Philox mask keyed by the module's seed and a per-call counter."""
+    dropout draws a Philox mask keyed by the module's ``drop_seed`` (config seed + client rank)
+    and its per-call counter ``drop_calls`` (in the engine's checkpointed state)."""
     mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
     p = float(user_encoder.dropout_rate) if user_encoder.training else 0.0
-    drop = (p, 0x5EED0001, 0)
+    seed = int(getattr(user_encoder, "drop_seed", 0))
+    drop = (p, seed, 0)
     if p > 0:
-        _MODULE_DROP_STEP[0] += 1
-        drop = (p, 0x5EED0001, _MODULE_DROP_STEP[0])
+        user_encoder.drop_calls = int(getattr(user_encoder, "drop_calls", 0)) + 1
+        drop = (p, seed, user_encoder.drop_calls)
     if keep is not None:
         keep = keep.to(torch.int32).contiguous()
     return UserEncoderFn.apply(clicked, mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight,

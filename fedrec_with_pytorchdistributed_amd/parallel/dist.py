@@ -150,31 +150,45 @@ def shutdown(ctx: DistContext) -> None:
             pass
 
 
-def make_ipc_allreduce(ctx: DistContext):
+def make_ipc_allreduce(ctx: DistContext, timeout_s: float = 600.0):
     """The custom peer-to-peer all-reduce over IPC-mapped buffers among the client GPUs
     (:mod:`.ipc_allreduce`), or None (one client, no GPU)."""
     if ctx.num_clients <= 1 or not ctx.initialized or ctx.device.type != "cuda" or ctx.client_index < 0:
         return None
     from .ipc_allreduce import IpcAllReduce
 
-    return IpcAllReduce(ctx.client_ctrl_group, ctx.client_index, ctx.num_clients, ctx.device)
+    return IpcAllReduce(ctx.client_ctrl_group, ctx.client_index, ctx.num_clients, ctx.device, timeout_s=timeout_s)
 
 
-def make_grad_allreduce(ctx: DistContext):
+def data_ipc(ctx: DistContext, timeout_s: float = 600.0):
+    """The data plane's IPC all-reduce when ``FEDREC_ALLREDUCE=ipc`` selects it (one instance
+    per context, shared by the GA bucket, the bucket reducer and parameter averaging), else
+    None (RCCL).  Every client must make the same choice (the environment of the launch)."""
+    if os.environ.get("FEDREC_ALLREDUCE", "rccl") != "ipc":
+        return None
+    ipc = getattr(ctx, "_ipc", None)
+    if ipc is None:
+        ipc = make_ipc_allreduce(ctx, timeout_s)
+        ctx._ipc = ipc
+    return ipc
+
+
+def make_grad_allreduce(ctx: DistContext, timeout_s: float = 600.0):
     """Sum the flat gradient over the client data group; returns the 1/W scale Adam applies.
     ``FEDREC_ALLREDUCE=ipc``: the custom IPC all-reduce instead of RCCL (same sum; every rank
-    gets the bitwise-same result)."""
+    gets the bitwise-same result); its ``check`` (run by the engine at every epoch end) raises
+    if a peer timed out."""
     if ctx.num_clients <= 1 or not ctx.initialized:
         return None
     W = ctx.num_clients
-    if os.environ.get("FEDREC_ALLREDUCE", "rccl") == "ipc" and ctx.device.type == "cuda":
-        ipc = make_ipc_allreduce(ctx)
-
+    ipc = data_ipc(ctx, timeout_s) if ctx.device.type == "cuda" else None
+    if ipc is not None:
         def _ar_ipc(flat_grad: torch.Tensor) -> float:
             CHECK.record("all_reduce", flat_grad, "grad-ipc")
             ipc.allreduce_(flat_grad)
             return 1.0 / W
 
+        _ar_ipc.check = ipc.check
         return _ar_ipc
 
     def _ar(flat_grad: torch.Tensor) -> float:
@@ -185,16 +199,14 @@ def make_grad_allreduce(ctx: DistContext):
     return _ar
 
 
-def make_secure_grad_allreduce(ctx: DistContext, headroom: float = 4.0, timeout_s: float = 600.0,
-                               run_id: str = "secagg-ga"):
+def make_secure_grad_allreduce(ctx: DistContext, timeout_s: float = 600.0, run_id: str = "secagg-ga"):
     """Gradient averaging under pairwise-mask secure aggregation (BASELINE config 5).
 
     Each client uploads ``Q(g) + sum_j +-PRG(s_ij, step)`` as wrap-around int32; one RCCL
     int32 SUM all-reduce cancels the masks exactly; the result is dequantised in place.
     Pair seeds come from a Diffie-Hellman exchange of public keys over the store.  The
-    fixed-point bound is a device-side running bound (:class:`.secagg.RunningMasker`): one
-    collective per step and no host read (round 2 ran a scalar MAX all-reduce plus a
-    ``.item()`` every step)."""
+    fixed-point bound is agreed per step by a masked exponent histogram
+    (:class:`.secagg.ExactMasker`): nothing is clamped, no host read."""
     from . import secagg
     from .control import ControlPlane
 
@@ -206,19 +218,22 @@ def make_secure_grad_allreduce(ctx: DistContext, headroom: float = 4.0, timeout_
     cp.set(f"pk/{k}", secagg.public_bytes(kp))
     pubs = [cp.get(f"pk/{j}") for j in range(W)]
     seeds_row = secagg.seeds_from_publics(kp, k, pubs)
-    masker = secagg.RunningMasker(k, W, seeds_row, ctx.device, headroom)
+    masker = secagg.ExactMasker(k, W, seeds_row, ctx.device)
+    ipc = data_ipc(ctx, timeout_s) if ctx.device.type == "cuda" else None
     state = {"step": 0}
 
     def _ar(flat_grad: torch.Tensor) -> float:
-        masker.allreduce_(flat_grad, state["step"], ctx.data_group, "secagg")
+        masker.allreduce_(flat_grad, state["step"], ctx.data_group, "secagg", ipc=ipc)
         state["step"] += 1
         return 1.0 / W
 
+    if ipc is not None:
+        _ar.check = ipc.check
     return _ar
 
 
 def make_bucket_reducer(ctx: DistContext, flat, secure: bool = False, bucket_mb: Optional[float] = None,
-                        timeout_s: float = 600.0, run_id: str = "secagg-bucket", headroom: float = 4.0):
+                        timeout_s: float = 600.0, run_id: str = "secagg-bucket"):
     """The backward-overlapped bucketed all-reduce (:class:`.reducer.BucketReducer`) over the
     client data group; ``secure`` = pairwise-masked int32 buckets (seeds by Diffie-Hellman
     over the store, as :func:`make_secure_grad_allreduce`).  None for a single client."""
@@ -237,4 +252,5 @@ def make_bucket_reducer(ctx: DistContext, flat, secure: bool = False, bucket_mb:
         cp.set(f"pk/{k}", secagg.public_bytes(kp))
         seeds_row = secagg.seeds_from_publics(kp, k, [cp.get(f"pk/{j}") for j in range(W)])
     mb = float(os.environ.get("FEDREC_BUCKET_MB", bucket_mb or DEFAULT_BUCKET_MB))
-    return BucketReducer(flat, ctx.data_group, W, "secure" if secure else "mean", mb, k, seeds_row, headroom)
+    ipc = data_ipc(ctx, timeout_s) if ctx.device.type == "cuda" else None
+    return BucketReducer(flat, ctx.data_group, W, "secure" if secure else "mean", mb, k, seeds_row, ipc=ipc)

@@ -13,9 +13,11 @@ call runs ONE kernel per rank:
   reduced slices: 2 (W-1)/W of the bucket read per rank instead of (W-1).
 
 fp32 SUM and int32 wrap-around SUM (the pairwise-masked fixed point of secure aggregation).
-RCCL stays the default data plane; ``FEDREC_ALLREDUCE=ipc`` selects this one, and the bench
-reports both at N > 1.  The barrier waits are bounded: a missing peer makes the kernel record a
-timeout in its status word and exit instead of hanging the GPU.
+RCCL stays the default data plane; ``FEDREC_ALLREDUCE=ipc`` selects this one for the GA flat
+bucket, the unfrozen / secure bucket reducer and parameter averaging, and the bench reports both
+at N > 1.  The barrier waits are bounded by the collective timeout: a missing peer makes the
+kernel record a timeout in its status word, poison its output and exit instead of hanging the
+GPU, and :meth:`IpcAllReduce.check` (run by the engine at every epoch end) raises on it.
 
 Reference call sites this replaces: ``Gradient_Averaging_main.py:119`` (DDP reducer),
 ``Parameter_Averaging_main.py:144-148`` (per-tensor parameter all-reduce).
@@ -37,16 +39,25 @@ class IpcAllReduce:
     """One rank's end of the IPC all-reduce among the ``world`` clients of ``ctrl_group``."""
 
     def __init__(self, ctrl_group, rank: int, world: int, device: torch.device, cap: int = DEFAULT_CAP,
-                 one_shot_max: int = int(os.environ.get("FEDREC_IPC_ONE_SHOT_MAX", 8 << 20)),
-                 blocks: int = int(os.environ.get("FEDREC_IPC_BLOCKS", 32))):
+                 one_shot_max: Optional[int] = None, blocks: Optional[int] = None, timeout_s: float = 600.0):
         self.lib = native.lib()
         self.rank, self.world, self.device = int(rank), int(world), device
+        if one_shot_max is None:
+            one_shot_max = int(os.environ.get("FEDREC_IPC_ONE_SHOT_MAX", 8 << 20))
+        if blocks is None:
+            blocks = int(os.environ.get("FEDREC_IPC_BLOCKS", 32))
         self.cap, self.one_shot_max, self.blocks = int(cap), int(one_shot_max), int(blocks)
+        self.timeout_s = float(timeout_s)
         with torch.cuda.device(device):
             self.id, h = self.lib.ipc_create(self.cap)
-        handles: List[Optional[bytes]] = [None] * self.world
-        dist.all_gather_object(handles, bytes(h.numpy().tobytes()), group=ctrl_group)
-        flat = torch.frombuffer(bytearray(b"".join(handles)), dtype=torch.uint8)
+        # every rank must run the same protocol geometry (the barrier waits on blocks x ranks
+        # flags; a different one-shot threshold would split one call into different modes)
+        geo = (self.cap, self.one_shot_max, self.blocks)
+        handles: List[Optional[tuple]] = [None] * self.world
+        dist.all_gather_object(handles, (bytes(h.numpy().tobytes()), geo), group=ctrl_group)
+        if any(g[1] != geo for g in handles):
+            raise RuntimeError(f"IPC all-reduce: ranks disagree on (cap, one_shot_max, blocks): {[g[1] for g in handles]}")
+        flat = torch.frombuffer(bytearray(b"".join(g[0] for g in handles)), dtype=torch.uint8)
         with torch.cuda.device(device):
             self.lib.ipc_open(self.id, flat, self.rank, self.world, None)
         dist.barrier(group=ctrl_group)  # every rank opened every region before the first call
@@ -58,8 +69,15 @@ class IpcAllReduce:
 
     def status(self) -> int:
         """0 = every call completed; 1 = a barrier timed out (a peer never arrived).  Reads the
-        device (tests and diagnostics only)."""
+        device (synchronises with it)."""
         return int(self.lib.ipc_status(self.id))
+
+    def check(self) -> None:
+        """Raise if any call since the start timed out (its output was poisoned); one device
+        read -- the engine calls it at every epoch end, where it synchronises anyway."""
+        if self.id is not None and self.status() != 0:
+            raise RuntimeError(f"IPC all-reduce on client {self.rank}: a peer did not arrive within "
+                               f"{self.timeout_s:.0f} s (the reduced gradients of that call are invalid)")
 
     def close(self) -> None:
         if self.id is not None:
@@ -74,10 +92,13 @@ def _allreduce(g, t: torch.Tensor, mode: Optional[str]) -> torch.Tensor:
     nbytes = t.numel() * 4
     if nbytes > g.cap:
         # larger than one slot: consecutive chunks (each call a full barrier-protected epoch)
-        flat = t.view(-1)
+        src = t if t.is_contiguous() else t.contiguous()
+        flat = src.reshape(-1)
         step = (g.cap // 16) * 4
         for s in range(0, flat.numel(), step):
             _allreduce(g, flat[s:s + step], mode)
+        if src is not t:
+            t.copy_(src)
         return t
     work = t if (t.is_contiguous() and t.numel() % 4 == 0) else None
     if work is None:  # pad to whole 16-byte chunks (the kernel moves float4 / int4)
@@ -85,7 +106,7 @@ def _allreduce(g, t: torch.Tensor, mode: Optional[str]) -> torch.Tensor:
         work[:t.numel()].copy_(t.reshape(-1))
     m = mode or ("one" if nbytes <= g.one_shot_max else "two")
     g.epoch += 1
-    g.lib.ipc_allreduce_(g.id, work.view(-1), g.epoch, 0 if m == "one" else 1, g.blocks)
+    g.lib.ipc_allreduce_(g.id, work.view(-1), g.epoch, 0 if m == "one" else 1, g.blocks, g.timeout_s)
     if work is not t:
         t.view(-1).copy_(work[:t.numel()])
     return t
@@ -99,8 +120,10 @@ class LocalIpcGroup:
     distinct hardware queues).  Used by the 1-GPU tests; the multi-process form is
     :class:`IpcAllReduce`."""
 
-    def __init__(self, world: int, device: torch.device, cap: int = 4 << 20, blocks: int = 8):
+    def __init__(self, world: int, device: torch.device, cap: int = 4 << 20, blocks: int = 8,
+                 timeout_s: float = 60.0):
         lib = native.lib()
+        self.timeout_s = float(timeout_s)
         self.lib, self.world, self.device, self.cap, self.blocks = lib, int(world), device, int(cap), int(blocks)
         self.one_shot_max = 1 << 62
         with torch.cuda.device(device):
@@ -116,7 +139,7 @@ class LocalIpcGroup:
         """``ts[r]`` = rank r's tensor; every one is replaced by the sum."""
         self.epoch += 1
         self.lib.ipc_allreduce_local_(self.ids, [t.view(-1) for t in ts], self.epoch, 0 if mode == "one" else 1,
-                                      self.blocks)
+                                      self.blocks, self.timeout_s)
 
     def status(self) -> List[int]:
         return [int(self.lib.ipc_status(i)) for i in self.ids]

@@ -11,10 +11,10 @@ still runs on the compute stream.
 
 * ``op="mean"``: one RCCL SUM all-reduce per bucket (the 1/W lands in Adam's grad scale).
 * ``op="secure"``: pairwise-masked fixed-point aggregation per bucket (BASELINE config 5,
-  :class:`.secagg.RunningMasker`): ONE int32 SUM all-reduce per bucket cancels the masks
-  exactly.  The fixed-point bound is agreed once (first step) and then tracked on the
-  device from the public sums, so there is no per-step scalar collective and no host read
-  (round 2 issued a MAX all-reduce per bucket per step, which also disclosed max|g|).
+  :class:`.secagg.ExactMasker`): a 1 KB masked exponent histogram agrees on a bound every
+  client's values fit (nothing is clamped, at any number of clients), then ONE int32 SUM
+  all-reduce of the bucket cancels the masks exactly.  Both run on the communication stream
+  with no host read.
 
 Parameters register ``post_accumulate_grad`` hooks: the hook copies the fresh gradient into
 its flat slot, re-points ``.grad`` at the slot, and counts the bucket down.  A bucket whose
@@ -35,10 +35,11 @@ DEFAULT_BUCKET_MB = 28.0
 
 class BucketReducer:
     def __init__(self, flat, group, world: int, op: str = "mean", bucket_mb: float = DEFAULT_BUCKET_MB,
-                 client_index: int = 0, seeds_row=None, headroom: float = 4.0):
+                 client_index: int = 0, seeds_row=None, ipc=None):
         if op not in ("mean", "secure"):
             raise ValueError(f"BucketReducer op {op!r}")
         self.flat, self.group, self.W, self.op = flat, group, int(world), op
+        self.ipc = ipc  # parallel.ipc_allreduce.IpcAllReduce (FEDREC_ALLREDUCE=ipc), else RCCL / gloo
         self.k = client_index
         dev = flat.grad.device
         self.device = dev
@@ -70,7 +71,7 @@ class BucketReducer:
         if op == "secure":
             from . import secagg
 
-            self.maskers = [secagg.RunningMasker(self.k, self.W, seeds_row, dev, headroom) for _ in self.buckets]
+            self.maskers = [secagg.ExactMasker(self.k, self.W, seeds_row, dev) for _ in self.buckets]
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(flat.params)]
 
     # -------------------------------------------------------------------------------
@@ -113,10 +114,18 @@ class BucketReducer:
     def _reduce(self, g: torch.Tensor, b: int) -> None:
         if self.op == "mean":
             CHECK.record("all_reduce", g, f"bucket{b}")
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
+            if self.ipc is not None:
+                self.ipc.allreduce_(g)
+            else:
+                dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
             return
         rnd = self.step * 4096 + b  # a fresh PRG counter space per (step, bucket)
-        self.maskers[b].allreduce_(g, rnd, self.group, f"secagg{b}")
+        self.maskers[b].allreduce_(g, rnd, self.group, f"secagg{b}", ipc=self.ipc)
+
+    def check(self) -> None:
+        """Raise if an IPC all-reduce of this reducer timed out (engine: every epoch end)."""
+        if self.ipc is not None:
+            self.ipc.check()
 
     def finish(self) -> float:
         """Reduce any bucket still waiting (parameters without a gradient: zero-filled by

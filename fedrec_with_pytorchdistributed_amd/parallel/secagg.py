@@ -11,13 +11,18 @@ classic pairwise-masking protocol (Bonawitz et al. 2017, without dropout recover
 3. **Aggregation**: an ordinary int32 SUM all-reduce (RCCL over xGMI); masks cancel
    exactly, leaving ``sum_i Q(x_i)``; then dequantise and divide by ``W``.
 
+Gradient buckets (:class:`ExactMasker`) agree on the fixed-point bound per sum through a
+masked exponent histogram, so no value is ever clamped at any number of clients; model
+uploads of the star mode (:func:`mask_local`) use a fixed grid (``SecAggConfig``).
+
 Fixed-point arithmetic is what makes cancellation bit-exact.
 """
 from __future__ import annotations
 
 import hashlib
+import math
 import secrets
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -117,68 +122,136 @@ def mask_local(x: torch.Tensor, i: int, W: int, seeds: np.ndarray, round_idx: in
     return torch.from_numpy(acc.view(np.int32).copy()).view(x.shape)
 
 
-class RunningMasker:
-    """Client ``i``'s secure-aggregation state for repeated sums of one gradient buffer (or
-    bucket), with a fixed-point scale that needs no per-step agreement:
+HIST_SLOTS = 256
+_HIST_ROUND = 1 << 62  # PRG counter space of the exponent histograms (disjoint from the payloads')
 
-    * every coordinate is clamped to a bound ``m`` and quantised on the grid ``2^-f``, ``f``
-      the largest with ``W * m * 2^f <= 2^30`` (the W-client int32 sum cannot wrap);
-    * ``m`` lives on the device.  It is agreed ONCE, at the first call (the
-      scalar MAX all-reduce of ``max|g|``, exact: nothing is clamped), and from then on tracked
-      from the PUBLIC result: after each sum every client sets
-      ``m = max(headroom * max|sum| / W, decay * m)`` from the
-      unmasked sum it holds (``max|sum| / W``: the largest coordinate of the MEAN gradient) -- bitwise identical on every client, so every client derives the
-      same ``f`` without a collective, and nothing beyond the sums is disclosed after step 0.
-      Clamped coordinates raise the next sum's maximum, so the bound grows back within a
-      step; the decay floor keeps it from collapsing on an all-zero step.
-    * pair seeds and signs are device-resident (no per-call host->device copy, which torch
-      would synchronise on), and the scale is read by the kernels from device memory: a step's
-      mask / all-reduce / unmask sequence never waits on the host.
 
-    One SUM all-reduce per call (plus the one-time MAX)."""
+def hist_slot(max_abs: float) -> int:
+    """Histogram slot of a client's largest finite ``|x|`` (the device kernels' rule): 0 for 0,
+    else ``max(e, 1) + 1`` with ``e`` the fp32 exponent field, so slot ``s`` means
+    ``max|x| < 2^(s - 127)``."""
+    bits = int(np.array([max_abs], dtype=np.float32).view(np.uint32)[0])
+    if bits == 0:
+        return 0
+    return max(bits >> 23, 1) + 1
 
-    def __init__(self, i: int, world: int, seeds_row: np.ndarray, device: torch.device,
-                 headroom: float = 4.0, decay: float = 0.25):
+
+def hist_local(x: torch.Tensor) -> np.ndarray:
+    """This client's UNMASKED histogram: a one-hot at :func:`hist_slot` of its max|x| and, in
+    slot 1, its count of non-finite coordinates."""
+    v = x.detach().reshape(-1).float().abs()
+    fin = torch.isfinite(v)
+    h = np.zeros(HIST_SLOTS, dtype=np.int64)
+    h[hist_slot(float(v[fin].max()) if bool(fin.any()) else 0.0)] += 1
+    h[1] += int((~fin).sum())
+    return h
+
+
+def hist_frac_bits(H, world: int) -> Tuple[int, bool]:
+    """``(f, non_finite)`` from a SUMMED histogram: the bound is ``2^E`` of the largest occupied
+    slot and ``f = 30 - ceil(log2 W) - E`` (clamped to [-120, 60]) -- the W-client int32 sum of
+    values within the bound cannot wrap, and no client's value exceeds it."""
+    H = np.asarray(H).reshape(-1)
+    occ = [s for s in range(2, HIST_SLOTS) if H[s] != 0]
+    bad = bool(H[1] != 0)
+    if not occ:
+        return 0, bad
+    E = max(occ) - 127
+    f = 30 - int(math.ceil(math.log2(max(1, int(world))))) - E
+    return max(-120, min(60, f)), bad
+
+
+def _add_masks(acc: np.ndarray, seeds_row: np.ndarray, i: int, round_idx: int) -> np.ndarray:
+    """uint32 wrap-around ``acc + sum_j sign_ij PRG(s_ij, round)`` (host PRG: PCG64)."""
+    peers, sd, sg = _peer_arrays(i, seeds_row)
+    for s, g in zip(sd.tolist(), sg.tolist()):
+        r = np.random.Generator(np.random.PCG64([s & 0xFFFFFFFFFFFFFFFF, round_idx])).integers(
+            0, 1 << 32, acc.size, dtype=np.uint64).astype(np.uint32)
+        acc = (acc + r) if g > 0 else (acc - r)
+    return acc
+
+
+class ExactMasker:
+    """Client ``i``'s end of an EXACT secure sum of a gradient buffer (or bucket), any number
+    of clients, no host synchronisation on the device:
+
+    1. **bound agreement** -- a masked exponent histogram (:data:`HIST_SLOTS` int32): each
+       client adds a one-hot at the binary exponent of its own ``max|g|`` (and its count of
+       non-finite coordinates); one SUM all-reduce of 1 KB; every client reads the largest
+       occupied slot, a power of two ``m >= max_k max|g_k|``.  The masks hide which client
+       holds which exponent: the sum discloses only how many clients have their maximum in
+       each power-of-two range.
+    2. **payload** -- ``Q(g) = round(g 2^f)`` with ``f = 30 - ceil(log2 W) - log2 m`` (the
+       W-client sum cannot wrap int32), pairwise masks, one int32 SUM all-reduce; the masks
+       cancel exactly and the dequantised sum is the plain sum to within ``W 2^(-f-1)``.
+
+    Nothing is clamped, so there is no running bound to collapse or to lag a gradient spike
+    (round 3's ``RunningMasker``).  A non-finite coordinate anywhere makes every output NaN,
+    as the plain sum would be non-finite.  Two collectives per call, both on the caller's
+    stream."""
+
+    def __init__(self, i: int, world: int, seeds_row: np.ndarray, device: torch.device):
         self.i, self.W, self.row = int(i), int(world), seeds_row
-        self.headroom, self.decay = float(headroom), float(decay)
         _, sd, sg = _peer_arrays(self.i, seeds_row)
         self.device = device
         self.sd, self.sg = sd.to(device), sg.to(device)
-        self.m: Optional[torch.Tensor] = None  # device fp32 [1]: the current clamp bound
+        self.hist: Optional[torch.Tensor] = None  # the last summed histogram (tests read it)
 
-    def _amax(self, g: torch.Tensor) -> torch.Tensor:
-        return torch.nan_to_num(g.detach().abs().amax().float().reshape(1), nan=0.0, posinf=3.0e38)
+    def frac_bits(self) -> int:
+        """Fraction bits of the last sum (reads the device histogram: tests / diagnostics)."""
+        return hist_frac_bits(self.hist.cpu().numpy(), self.W)[0]
 
-    def allreduce_(self, g: torch.Tensor, round_idx: int, group, check_tag: str = "secagg") -> None:
-        """``g`` <- the exact (fixed-point) SUM of every client's ``g``, in place."""
+    def allreduce_(self, g: torch.Tensor, round_idx: int, group, check_tag: str = "secagg", ipc=None) -> None:
+        """``g`` <- the exact (fixed-point) SUM of every client's ``g``, in place.  ``ipc``: an
+        :class:`.ipc_allreduce.IpcAllReduce` moves both int32 buffers instead of ``group``."""
         import torch.distributed as dist
 
         from .collcheck import CHECK
 
-        if self.m is None:  # one-time agreement of the initial bound
-            m = self._amax(g)
-            CHECK.record("all_reduce", m, f"{check_tag}-init")
-            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
-            self.m = torch.clamp(m, min=1e-30, max=3.0e38)
         flat = g.reshape(-1)
+        hround = _HIST_ROUND | int(round_idx)
         if flat.is_cuda:
             from ..ops import native
 
             lib = native.require_for(flat)
-            q = lib.secagg_mask_dev(flat.float().contiguous(), self.sd, self.sg, self.m, self.W, int(round_idx))
+            x = flat if (flat.dtype == torch.float32 and flat.is_contiguous()) else flat.float().contiguous()
+            h = lib.secagg_hist(x, self.sd, self.sg, hround)
+            CHECK.record("all_reduce", h, f"{check_tag}-hist")
+            if ipc is not None:
+                ipc.allreduce_(h)
+            else:
+                dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            q = lib.secagg_mask_exact(x, self.sd, self.sg, h, self.W, int(round_idx))
             CHECK.record("all_reduce", q, f"{check_tag}-sum")
-            dist.all_reduce(q, op=dist.ReduceOp.SUM, group=group)
-            lib.secagg_unmask_dev_(q, self.m, self.W, flat)
-        else:  # host (gloo plumbing): the same bound rule, the reference-format masks below
-            mv = float(self.m.item())
-            f = frac_bits_for(self.W, mv)
-            q = mask_local(flat, self.i, self.W, self.row, round_idx, f, mv)
-            CHECK.record("all_reduce", q, f"{check_tag}-sum")
-            dist.all_reduce(q, op=dist.ReduceOp.SUM, group=group)
-            flat.copy_(unmask_sum(q, f).view_as(flat))
-        self.used = self.m  # the bound this sum was quantised with (tests read it)
-        self.m = torch.maximum(torch.clamp(self._amax(flat) * (self.headroom / self.W), max=3.0e38),
-                               self.m * self.decay).clamp_(min=1e-30)
+            if ipc is not None:
+                ipc.allreduce_(q)
+            else:
+                dist.all_reduce(q, op=dist.ReduceOp.SUM, group=group)
+            if x is flat:
+                lib.secagg_unmask_exact_(q, h, self.W, flat)
+            else:
+                out = torch.empty_like(x)
+                lib.secagg_unmask_exact_(q, h, self.W, out)
+                flat.copy_(out)
+            self.hist = h
+            return
+        # host (gloo plumbing): the same protocol with the host PRG
+        hl = _add_masks(hist_local(flat).astype(np.uint32), self.row, self.i, hround)
+        h = torch.from_numpy(hl.view(np.int32).copy())
+        CHECK.record("all_reduce", h, f"{check_tag}-hist")
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        f, bad = hist_frac_bits(h.numpy(), self.W)
+        v = flat.detach().float()
+        v = torch.where(torch.isfinite(v), v, torch.zeros_like(v))
+        qv = torch.round(v.double() * (2.0 ** f)).to(torch.int64).numpy().astype(np.uint32)
+        q = torch.from_numpy(_add_masks(qv, self.row, self.i, int(round_idx)).view(np.int32).copy())
+        CHECK.record("all_reduce", q, f"{check_tag}-sum")
+        dist.all_reduce(q, op=dist.ReduceOp.SUM, group=group)
+        out = q.double() * (2.0 ** -f)
+        if bad:
+            out.fill_(float("nan"))
+        flat.copy_(out.to(flat.dtype).view_as(flat))
+        self.hist = h
 
 
 def unmask_sum(total: torch.Tensor, frac_bits: int = FRAC_BITS) -> torch.Tensor:

@@ -181,6 +181,7 @@ class LocalEngine:
                            and ue.multihead_attention.n_heads * ue.multihead_attention.d_k == cfg.news_dim
                            and os.environ.get("FEDREC_FUSED_USER", "1") != "0")
         self.user_drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 2
+        ue.drop_seed = self.user_drop_seed  # the module-level device path (user_encoder_device) too
         # LDP noise: its own Philox key per client (disjoint from the dropout keys above)
         self.ldp_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 3
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
@@ -215,10 +216,20 @@ class LocalEngine:
         """Use a backward-overlapped bucket reducer (``parallel.reducer``) for the gradients."""
         self.reducer = reducer
 
+    def check_data_plane(self) -> None:
+        """Raise if a gradient all-reduce failed silently on the device (the IPC all-reduce
+        records a peer timeout in a status word and poisons that call's output); one device
+        read, at every epoch end."""
+        for obj in (self.grad_allreduce, self.reducer):
+            chk = getattr(obj, "check", None)
+            if chk is not None:
+                chk()
+
     def state(self) -> Dict[str, int]:
         """Counters that key the engine's randomness (checkpointed with the snapshot)."""
         return {"noise_offset": self.noise_offset, "epoch": self.epoch,
                 "drop_calls": self.model.text_encoder.DistillBert._drop_calls,
+                "user_drop_calls": int(getattr(self.model.user_encoder, "drop_calls", 0)),
                 "rng_step": int(self._rng_step.item())}
 
     def load_state(self, st: Dict[str, int]) -> None:
@@ -226,6 +237,7 @@ class LocalEngine:
         self._rng_step.fill_(int(st.get("rng_step", 0)))  # user-dropout / LDP-noise step counter
         self.epoch = int(st.get("epoch", self.epoch))
         self.model.text_encoder.DistillBert._drop_calls = int(st.get("drop_calls", 0))
+        self.model.user_encoder.drop_calls = int(st.get("user_drop_calls", 0))
 
     def _make_hidden_cache(self) -> Optional[HiddenCache]:
         """The HBM hidden-state cache when the config asks for it and it fits."""
@@ -657,6 +669,7 @@ class LocalEngine:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
+        self.check_data_plane()
         self.epoch += 1
         mean_loss = float(torch.stack(losses).float().mean()) if losses else float("nan")
         sum_loss = float(torch.stack(losses).float().sum()) if losses else float("nan")
@@ -666,8 +679,12 @@ class LocalEngine:
         return self.last_stats
 
     @torch.no_grad()
-    def validate(self, batch_size: int = 256, limit: Optional[int] = None) -> Dict[str, float]:
-        """Corpus-mean AUC/MRR/nDCG over the validation impressions (fix of Q9)."""
+    def validate(self, batch_size: int = 256, limit: Optional[int] = None,
+                 device_batches: Optional[bool] = None) -> Dict[str, float]:
+        """Corpus-mean AUC/MRR/nDCG over the validation impressions (fix of Q9).
+        ``device_batches`` (None = auto: the fused device user side with truncated histories):
+        the batches are assembled and scored on the device with no host step per batch
+        (:meth:`_validate_device`); False = the host-batched loop."""
         self.sync_params()
         self.model.eval()
         scores_all, losses = [], []
@@ -677,6 +694,11 @@ class LocalEngine:
         # ONCE into a table and gather -- per-title results are the same either way (every
         # kernel computes a title's rows independently of the rest of the batch)
         n_imp = len(self.shard.valid) if limit is None else min(limit, len(self.shard.valid))
+        if device_batches is None:
+            device_batches = self.fused_user and self.device.type == "cuda" and not self.q.no_history_truncation
+        if device_batches and n_imp > 0:
+            S, loss_sum = self._validate_device(batch_size, limit, n_imp)
+            return self._valid_metrics(S, loss_sum)
         table = None
         if self.news_table is not None:
             table = self.news_table
@@ -715,9 +737,38 @@ class LocalEngine:
         if not scores_all:
             return {"validation_loss": float("nan"), "valid_auc": float("nan"), "valid_mrr": float("nan"),
                     "val_ndcg@5": float("nan"), "val_ndcg@10": float("nan"), "n_valid": 0}
-        S = np.concatenate(scores_all, 0)
+        return self._valid_metrics(np.concatenate(scores_all, 0), sum(losses))
+
+    def _validate_device(self, batch_size: int, limit: Optional[int], n_imp: int) -> Tuple[np.ndarray, float]:
+        """The validation pass with no host work per batch: the batches are assembled by the
+        device sampler's validation mode (``[pos] + negs[-4:]``, client.py:158-165), the news
+        vectors come from one encode of the whole table (the parameters are constant during
+        validation, so every title's vector is), scores and the loss sum accumulate in device
+        buffers, and ONE copy brings them back.  Same values as the host-batched path
+        (``test_device_validation_matches_host_batches``)."""
+        if getattr(self, "_vsampler", None) is None:
+            self._vsampler = DeviceSampler(self.shard.valid, batch_size, self.device, self.cfg.npratio,
+                                           self.cfg.max_his_len, truncate=True, seed=self.cfg.seed, rank=self.rank,
+                                           shuffle=False)
+        table = self.news_table if self.news_table is not None else self.encode_all(grad=False)
+        self.model.eval()
+        C = self.cfg.npratio + 1
+        S = torch.empty(n_imp, C, dtype=torch.float32, device=self.device)
+        lsum = torch.zeros((), dtype=torch.float32, device=self.device)
+        s0 = 0
+        for cand, his in self._vsampler.valid_batches(batch_size, limit):
+            B = cand.shape[0]
+            ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
+            loss, s = self._user_loss(table, (None, ids, ids, ids), B, C, his.shape[1], False, False, his)
+            S[s0:s0 + B].copy_(s)
+            lsum.add_(loss.float(), alpha=float(B))
+            s0 += B
+        host = torch.cat([S.reshape(-1), lsum.reshape(1)]).cpu().numpy()  # the one copy back
+        return host[:-1].reshape(n_imp, C), float(host[-1])
+
+    def _valid_metrics(self, S: np.ndarray, loss_sum: float) -> Dict[str, float]:
         m = batch_metrics(S)
-        out = {"validation_loss": sum(losses) / S.shape[0], "valid_auc": m["auc"], "valid_mrr": m["mrr"],
+        out = {"validation_loss": loss_sum / S.shape[0], "valid_auc": m["auc"], "valid_mrr": m["mrr"],
                "val_ndcg@5": m["ndcg5"], "val_ndcg@10": m["ndcg10"], "n_valid": S.shape[0],
                "last_valid_auc": m["last_auc"], "last_valid_mrr": m["last_mrr"]}
         if self.q.validate_last_only:  # Q9 compat: the reference returns the last impression's values

@@ -37,7 +37,7 @@ from ..parallel import comm
 from ..parallel import secagg
 from ..parallel.collcheck import CHECK
 from ..parallel.control import ControlPlane, Heartbeat
-from ..parallel.dist import (DistContext, make_bucket_reducer, make_grad_allreduce, make_secure_grad_allreduce,
+from ..parallel.dist import (DistContext, data_ipc, make_bucket_reducer, make_grad_allreduce, make_secure_grad_allreduce,
                              selfcheck)
 from ..privacy.rdp import calibrate_client_sigma
 from ..utils import obs
@@ -175,12 +175,12 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     if bucketed:
         ar = None
     else:
-        ar = (make_secure_grad_allreduce(ctx, cfg.secagg.bound_headroom, timeout_s=cfg.collective_timeout_s)
-              if cfg.secagg.enabled else make_grad_allreduce(ctx))
+        ar = (make_secure_grad_allreduce(ctx, timeout_s=cfg.collective_timeout_s)
+              if cfg.secagg.enabled else make_grad_allreduce(ctx, cfg.collective_timeout_s))
     eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=ar)
     if bucketed:
         eng.set_reducer(make_bucket_reducer(ctx, model.flat, secure=cfg.secagg.enabled,
-                                            timeout_s=cfg.collective_timeout_s, headroom=cfg.secagg.bound_headroom))
+                                            timeout_s=cfg.collective_timeout_s))
     eng.sigma = _maybe_dp(cfg, eng)
     eng.load_state(est)
     eng.epoch = start
@@ -219,11 +219,13 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     K = cfg.param_avg_every if sched == "per_step" else 0
     steps = _min_over_clients(ctx, eng.sampler.num_batches()) if K else None
 
+    ipc = data_ipc(ctx, cfg.collective_timeout_s) if ctx.device.type == "cuda" else None
+
     def average():
         if ctx.initialized and W > 1:
             before = _backbone_before(model, full)
             with obs.range("param_allreduce"):
-                comm.allreduce_(model.sync_tensors(full), ctx.data_group, scale=1.0 / W)
+                comm.allreduce_(model.sync_tensors(full), ctx.data_group, scale=1.0 / W, ipc=ipc)
             _backbone_synced(model, full, before)
 
     hook = (lambda n: average() if n % K == 0 else None) if K else None
@@ -232,6 +234,8 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
         tr = eng.train_epoch(max_steps=steps, step_hook=hook)
         if not K or (steps or 0) % K:
             average()  # once per epoch (Parameter_Averaging_main.py:144-148)
+        if ipc is not None:
+            ipc.check()  # a timed-out IPC all-reduce poisoned its bucket: fail loudly
         va = eng.validate()
         CHECK.verify(ctx.ctrl_group, f"param_avg epoch {epoch}")
         last = _reduce_metrics(ctx, tr, va)
@@ -326,8 +330,6 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         meta = {"client": k, "n_train": len(shard.train), "train_s": t_train, "valid_s": t_valid,
                 **{m: float(v) for m, v in {**tr, **va}.items() if isinstance(v, (int, float))}}
         up = _client_upload_tensor(model, cfg).clone()
-        last_round = r + 1 >= cfg.global_rounds if cfg.global_rounds else False
-        save_now = bool(csnap) and cfg.save_every > 0 and (r % cfg.save_every == 0 or last_round)
         if cfg.round_artifacts:  # client.py:288 torch.save(model.state_dict(), "model.pt")
             sub = "" if ctx.num_clients == 1 else f"client{k}"
             ckpt.save_state_dict(os.path.join(_artifact_dir(cfg), sub, "model.pt"), model)
@@ -337,7 +339,10 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
             w = float(len(shard.train)) if cfg.weighted_fedavg else 1.0
             wt = torch.tensor([w], device=up.device, dtype=torch.float32)
             up.mul_(wt)
-            comm.allreduce_([up, wt], ctx.data_group)
+            ipc = data_ipc(ctx, cfg.collective_timeout_s) if ctx.device.type == "cuda" else None
+            comm.allreduce_([up, wt], ctx.data_group, ipc=ipc)
+            if ipc is not None:
+                ipc.check()
             up.div_(wt)
             if k == 0:
                 cp.put_tensor(f"r{r}/avg", up.cpu())
@@ -351,10 +356,12 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
             else:
                 cp.put_tensor(f"r{r}/up/{k}", up.cpu())
             cp.put_json(f"r{r}/meta/{k}", meta)
-        if save_now:
-            # after the upload (off the round's critical path), every save_every rounds, and only
-            # what a resume needs: trainable flat + Adam + RNG + engine counters (~14 MB, not the
-            # 270 MB full state with the frozen backbone)
+        if csnap:
+            # after the upload (off the round's critical path), EVERY round, and only what a
+            # resume needs: trainable flat + Adam + RNG + engine counters (~14 MB, not the 270 MB
+            # full state with the frozen backbone).  Every round, not every save_every: a resume
+            # from an older round would redraw the LDP noise / dropout of the rounds in between
+            # at the same offsets, and noise that was already uploaded must never be reused
             ckpt.save_client_state(csnap, model, r, eng.state())
         last = meta
         r += 1

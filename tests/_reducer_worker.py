@@ -48,7 +48,7 @@ for op in ("mean", "secure"):
             if op == "mean":
                 tol = 0.0
             else:  # each client's value rounds once onto the grid 2^-f of the bound it was masked with
-                tol = W * 2.0 ** -secagg.frac_bits_for(W, float(red.maskers[b].used.item()))
+                tol = W * 2.0 ** -red.maskers[b].frac_bits()
                 tol += 4 * 2.0 ** -24 * float(ref.abs().max())  # + the fp32 rounding of both sums
             err = float((got - ref).abs().max())
             if err > tol:

@@ -74,6 +74,19 @@ def test_bucketed_reducer_matches_flat_allreduce(tmp_path):
 
 
 @pytest.mark.slow
+def test_secure_sum_exact_eight_clients():
+    """Secure aggregation at W = 8 (BASELINE config 5's client count): the masked sum equals
+    the plain sum within the fixed-point grid at every step -- an all-zero first step, single-
+    client largest coordinates with the holder alternating and a 10x jump per step, cancelling
+    opposite signs, tiny values -- so no coordinate is ever clamped; a non-finite value on one
+    client makes the result NaN."""
+    outs = run_ranks([["tests/_secagg_worker.py"]] * 8, timeout=180)
+    _ok(outs)
+    for _, out in outs:
+        assert "SECAGG OK" in out, out[-2000:]
+
+
+@pytest.mark.slow
 def test_bucket_reducer_sums_match_flat_oracle():
     """Reducer-level oracle: per bucket, the reduced gradient equals an explicit flat SUM
     all-reduce of every rank's gradient -- exactly for op=mean, within the bucket's fixed-point

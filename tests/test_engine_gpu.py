@@ -233,10 +233,30 @@ def test_validation_news_table_matches_per_batch(dev, monkeypatch):
     m.build_flat()
     eng = LocalEngine(cfg, m, make_client_shards("tiny", 1)[0], dev)
     monkeypatch.setenv("FEDREC_VALID_TABLE", "0")
-    a = eng.validate(batch_size=64)
+    a = eng.validate(batch_size=64, device_batches=False)
     monkeypatch.setenv("FEDREC_VALID_TABLE", "2")
-    b = eng.validate(batch_size=64)
+    b = eng.validate(batch_size=64, device_batches=False)
     assert a["n_valid"] == b["n_valid"] > 0
     for k in ("valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):
         assert abs(a[k] - b[k]) < 1e-4, (k, a[k], b[k])
     assert abs(a["validation_loss"] - b["validation_loss"]) < 1e-4
+
+
+@pytest.mark.parametrize("mask,last_only,limit", [(False, False, None), (True, False, 77), (False, True, None)])
+def test_device_validation_matches_host_batches(dev, mask, last_only, limit):
+    """The device-assembled validation (sampler validation mode, scores and loss accumulated on
+    the device, one copy back) equals the host-batched loop (numpy batches, a sync per batch):
+    same impressions, same candidates [pos] + negs[-4:], same metrics -- with the padding mask,
+    a partial last batch, and the reference's last-impression metrics (Q9 compat)."""
+    cfg = _cfg()
+    cfg.mask_padding = mask
+    cfg.compat.validate_last_only = last_only
+    torch.manual_seed(0)
+    m = FedRecModel(cfg).to(dev)
+    m.build_flat()
+    eng = LocalEngine(cfg, m, make_client_shards("tiny", 1)[0], dev)
+    a = eng.validate(batch_size=32, limit=limit, device_batches=True)
+    b = eng.validate(batch_size=32, limit=limit, device_batches=False)
+    assert a["n_valid"] == b["n_valid"] > 0
+    for k in ("valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10", "validation_loss"):
+        assert abs(a[k] - b[k]) < 1e-5, (k, a[k], b[k])

@@ -38,6 +38,27 @@ def test_ipc_allreduce_local_ranks(dev, W, mode):
         g.close()
 
 
+def test_ipc_allreduce_local_28mb_int32_buckets(dev):
+    """The secure reducer's bucket size: 28 MB of int32 (masked fixed point) per call, two-shot
+    and one-shot, wrap-around sum exact and bitwise-identical on every rank."""
+    from fedrec_with_pytorchdistributed_amd.parallel.ipc_allreduce import LocalIpcGroup
+
+    W, n = 4, 7 << 20
+    g = LocalIpcGroup(W, dev, cap=32 << 20, blocks=16)
+    try:
+        for mode in ("two", "one"):
+            qi = [torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device=dev, dtype=torch.int64).to(torch.int32)
+                  for _ in range(W)]
+            qe = torch.stack([q.to(torch.int64) for q in qi]).sum(0)
+            qe = ((qe + (1 << 31)) % (1 << 32) - (1 << 31)).to(torch.int32)
+            g.allreduce_(qi, mode)
+            torch.cuda.synchronize()
+            assert all(torch.equal(q, qe) for q in qi), mode
+        assert g.status() == [0] * W
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("W", [2, 4])
 def test_ipc_allreduce_multiprocess(W):
     import torch as _t

@@ -164,16 +164,18 @@ def test_user_attention(dev, H, variant):
     kernels (online softmax over 64-row LDS chunks): the reference never truncates histories
     (Q6; its shipped shard has H = 76).  variant 1 = the VALU ILP kernels, 0 = the first forms."""
     from fedrec_with_pytorchdistributed_amd.ops import native
-    native.lib().user_attn_set_variant(variant)
     B, NH, DK = 7, 20, 20
     qkv = torch.randn(B, H, 3 * NH * DK, device=dev)
-    ctx, stats = ops.user_attention_fwd(qkv, NH, DK)
+    native.lib().user_attn_set_variant(variant)
+    try:  # the variant is process-global: restored even when an assert fails
+        ctx, stats = ops.user_attention_fwd(qkv, NH, DK)
+        d = torch.randn_like(ctx)
+        dq = ops.user_attention_bwd(qkv, stats, d, NH, DK)
+    finally:
+        native.lib().user_attn_set_variant(3)
     c_ref, A = ref.user_attention_fwd(qkv, NH, DK)
     assert rel_err(ctx, c_ref) < 1e-5
-    d = torch.randn_like(ctx)
-    dq = ops.user_attention_bwd(qkv, stats, d, NH, DK)
     dq_ref = ref.user_attention_bwd(qkv, A, d, NH, DK)
-    native.lib().user_attn_set_variant(3)
     assert rel_err(dq, dq_ref) < (1e-5 if variant >= 2 and H <= 64 else 1e-4)
 
 
@@ -197,13 +199,15 @@ def test_additive_pool_long_fp32(dev, T):
 @pytest.mark.parametrize("variant", [1, 0])  # 1: block per impression (default), 0: wave per impression
 @pytest.mark.parametrize("act,C", [("sigmoid", 5), ("identity", 5), ("sigmoid", 16), ("identity", 1)])
 def test_score_ce(dev, variant, act, C):
-    native.lib().score_set_variant(variant)
     B, D = 33, 400
     cand = torch.randn(B, C, D, device=dev) * 0.1
     u = torch.randn(B, D, device=dev) * 0.1
-    loss, s, dc, du = ops.score_ce(cand, u, act)
+    native.lib().score_set_variant(variant)
+    try:  # process-global: restored even when the call fails
+        loss, s, dc, du = ops.score_ce(cand, u, act)
+    finally:
+        native.lib().score_set_variant(1)
     l2, s2, dc2, du2 = ref.score_ce_fwd_bwd(cand, u, act)
-    native.lib().score_set_variant(1)
     assert abs(float(loss) - float(l2)) < 1e-5
     assert rel_err(s, s2) < 1e-6 and rel_err(dc, dc2) < 1e-5 and rel_err(du, du2) < 1e-5
 
@@ -331,6 +335,40 @@ def test_secagg_cancels_exactly(dev):
     q = [secagg.quantize_ref(x) for x in xs]
     exp = sum(q[1:], q[0].clone())
     assert torch.equal(got, secagg.dequantize_ref(exp))
+
+
+def test_secagg_exact_kernels_match_host(dev):
+    """The exact secure sum's device kernels against the host protocol, one client's view with
+    no peers (no masks): the exponent histogram equals the host one-hot (+ non-finite count),
+    and mask -> unmask is round(x 2^f) 2^-f with the host's f."""
+    import numpy as np
+
+    from fedrec_with_pytorchdistributed_amd.ops import native
+    from fedrec_with_pytorchdistributed_amd.parallel import secagg
+
+    lib = native.lib()
+    sd = torch.zeros(0, dtype=torch.int64, device=dev)
+    sg = torch.zeros(0, dtype=torch.int32, device=dev)
+    for scale in (0.0, 1e-30, 3e-3, 1.0, 7.5e5):
+        x = torch.randn(50_001, device=dev) * scale
+        x[17] = 2.0 * scale  # a known maximum
+        h = lib.secagg_hist(x, sd, sg, 5).cpu().numpy()
+        assert np.array_equal(h, secagg.hist_local(x.cpu()).astype(np.int32)), scale
+        for W in (1, 3, 8):
+            f, bad = secagg.hist_frac_bits(h, W)
+            q = lib.secagg_mask_exact(x, sd, sg, torch.from_numpy(h).to(dev), W, 5)
+            exp = torch.round(x.double().cpu() * 2.0 ** f)
+            assert torch.equal(q.cpu().double(), exp), (scale, W)
+            out = torch.empty_like(x)
+            lib.secagg_unmask_exact_(q, torch.from_numpy(h).to(dev), W, out)
+            assert torch.equal(out.cpu(), (exp * 2.0 ** -f).float()) and not bad
+    x = torch.zeros(1000, device=dev)
+    x[3], x[9] = float("nan"), float("inf")
+    h = lib.secagg_hist(x, sd, sg, 5)
+    assert int(h[1]) == 2 and int(h[0]) == 1
+    out = torch.empty_like(x)
+    lib.secagg_unmask_exact_(lib.secagg_mask_exact(x, sd, sg, h, 2, 5), h, 2, out)
+    assert bool(torch.isnan(out).all())
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10])

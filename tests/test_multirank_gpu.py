@@ -89,15 +89,44 @@ def test_bench_configs_multi_client_on_gpu(dev, config, ranks):
 @pytest.mark.gpu
 def test_grad_avg_unfrozen_secure_buckets_two_clients_on_gpu(tmp_path, dev):
     """Unfrozen backbone GA with pairwise-masked buckets reduced from autograd hooks on a
-    side stream during the backward (device-side fixed-point scale, no host read): both
-    clients end bit-identical."""
+    side stream during the backward (device-side histogram bound, no host read): both
+    clients end bit-identical -- over the gloo data plane and over the custom IPC all-reduce
+    (FEDREC_ALLREDUCE=ipc, real IPC handles), and the two transports agree BITWISE (the
+    masked fixed-point sums are exact integer sums, whatever moves them)."""
     argv = ["Gradient_Averaging_main.py", "1", "16", "1", "--data_dir=synthetic:tiny", "--backbone.frozen=0",
             "--backbone.n_layers=2", "--secagg.enabled=1", "--round_timeout_s=300", "--collective_timeout_s=300",
             f"--snapshot_path={tmp_path}/s.pt"]
-    env = dict(SHARE, FEDREC_DUMP_FLAT=str(tmp_path / "dump"), FEDREC_BUCKET_MB="8")
-    outs = run_ranks([argv, argv], env, timeout=500)
+    got = {}
+    for plane in ("gloo", "ipc"):
+        env = dict(SHARE, FEDREC_DUMP_FLAT=str(tmp_path / plane), FEDREC_BUCKET_MB="8")
+        if plane == "ipc":
+            env["FEDREC_ALLREDUCE"] = "ipc"
+        outs = run_ranks([argv, argv], env, timeout=500)
+        _ok(outs)
+        a = torch.load(tmp_path / plane / "rank0.pt")
+        b = torch.load(tmp_path / plane / "rank1.pt")
+        assert a.numel() > 20_000_000 and torch.isfinite(a).all()
+        assert torch.equal(a, b), plane
+        got[plane] = a
+    assert torch.equal(got["gloo"], got["ipc"])
+
+
+@pytest.mark.gpu
+def test_secure_sum_exact_four_clients_device_kernels(dev):
+    """The W-client exact secure sum through the HIP histogram / mask / unmask kernels (four
+    client processes on the one card, gloo moving the int32 buffers): equal to the plain sum
+    within the fixed-point grid at every step of tests/_secagg_worker.py."""
+    outs = run_ranks([["tests/_secagg_worker.py", "--device", "cuda"]] * 4, SHARE, timeout=300)
     _ok(outs)
-    a = torch.load(tmp_path / "dump" / "rank0.pt")
-    b = torch.load(tmp_path / "dump" / "rank1.pt")
-    assert a.numel() > 20_000_000 and torch.isfinite(a).all()
-    assert torch.equal(a, b)
+    for _, out in outs:
+        assert "SECAGG OK" in out, out[-2000:]
+
+
+@pytest.mark.gpu
+def test_ipc_allreduce_dead_peer_raises(dev):
+    """A client that vanishes makes the surviving client's IPC all-reduce time out within the
+    configured bound, poison its output and raise at check() -- a wrong gradient sum is never
+    returned silently; later calls fail fast."""
+    outs = run_ranks([["tests/_ipc_peer_worker.py"]] * 2, SHARE, timeout=120)
+    _ok(outs)
+    assert "PEER OK" in outs[0][1], outs[0][1][-2000:]

@@ -587,6 +587,6 @@ def test_extension_loads_and_registers_ops():
         pytest.skip("extension not built")
     code = ("import torch; torch.ops.load_library(%r); f = torch.ops.fedrec; "
             "[getattr(f, n) for n in ('small_gemm', 'colsum_f32', 'multi_copy', 'dropout_add', "
-            "'title_attention_drop', 'secagg_mask_dev', 'segment_sum_rows', 'linear')]" % str(native.SO_PATH))
+            "'title_attention_drop', 'secagg_mask_exact', 'segment_sum_rows', 'linear')]" % str(native.SO_PATH))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
