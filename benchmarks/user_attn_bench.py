@@ -1,6 +1,6 @@
 """User-encoder attention (20 heads x d_k 20, fp32) at the config-2 shape (B = 64 impressions,
-H = 50 clicked news): the ILP kernels (default) against the first forms, interleaved in one
-process, with an output check between them.
+H = 50 clicked news): forward and backward of the four-wave matrix-core kernels (median of
+--rounds timings).
 
     python benchmarks/user_attn_bench.py [--out gpurun_out/user_attn_bench.json]
 """
@@ -45,25 +45,12 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     qkv = torch.randn(a.B, a.H, 3 * NH * DK, generator=g).cuda()
     d = torch.randn(a.B, a.H, NH * DK, generator=g).cuda()
-    outs = {}
-    for v in (0, 1, 2, 3, 4):
-        lib.user_attn_set_variant(v)
-        c, st = ops.user_attention_fwd(qkv, NH, DK)
-        outs[v] = (c, st, ops.user_attention_bwd(qkv, st, d, NH, DK))
-    res = {"fwd_rel_diff_v3_v1": float((outs[3][0] - outs[1][0]).norm() / outs[1][0].norm()),
-           "bwd_rel_diff_v3_v1": float((outs[3][2] - outs[1][2]).norm() / outs[1][2].norm())}
-    print(res, flush=True)
-    times = {f"{k}_v{v}": [] for k in ("fwd", "bwd") for v in (0, 1, 2, 3, 4)}
+    c, st = ops.user_attention_fwd(qkv, NH, DK)
+    res = {}
+    times = {"fwd": [], "bwd": []}
     for _ in range(a.rounds):
-        for v in (0, 1, 2, 3, 4):
-            lib.user_attn_set_variant(v)
-            st = outs[v][1]
-            times[f"fwd_v{v}"].append(timeit(lambda: ops.user_attention_fwd(qkv, NH, DK)))
-            times[f"bwd_v{v}"].append(timeit(lambda: ops.user_attention_bwd(qkv, st, d, NH, DK)))
-    for v in (10, 11):  # diagnostic partial forwards of the MFMA kernel
-        lib.user_attn_set_variant(v)
-        times[f"fwd_v{v}"] = [timeit(lambda: ops.user_attention_fwd(qkv, NH, DK)) for _ in range(a.rounds)]
-    lib.user_attn_set_variant(3)
+        times["fwd"].append(timeit(lambda: ops.user_attention_fwd(qkv, NH, DK)))
+        times["bwd"].append(timeit(lambda: ops.user_attention_bwd(qkv, st, d, NH, DK)))
     for k, v in times.items():
         res[k] = {"us": round(1000 * statistics.median(v), 2), "all_us": [round(1000 * x, 2) for x in v]}
         print(k, res[k], flush=True)

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(NT) void dedup2_kernel(const int* __restrict__ ids,
   }
 }
 
-int g_dedup_variant = -1;  // FEDREC_DEDUP: 1 = register bitonic (default), 0 = the LDS form
+// the register-bitonic form (dedup2) where its key image fits 64 KB of LDS, else the LDS form
 
 }  // namespace
 
@@ -313,14 +313,10 @@ extern "C" int fr_dedup(const int* ids, int R, int num_news, int* uniq, int* inv
   if (R > MAXR || R < 1) return 1;
   int P = 1;
   while (P < R) P <<= 1;
-  if (g_dedup_variant < 0) {
-    const char* e = getenv("FEDREC_DEDUP");
-    g_dedup_variant = e != nullptr ? atoi(e) : 1;
-  }
   const bool narrow = num_news > 0 && num_news <= (1 << 19);
   const int E = P <= NT ? 1 : P / NT;
   const size_t lds = 2 * (size_t)NT * E * (narrow ? 4 : 8);  // two key buffers
-  if (g_dedup_variant != 0 && lds <= 65536) {
+  if (lds <= 65536) {
 #define DEDUP2(KT, SH, EE)                                                                                    \
   hipLaunchKernelGGL((dedup2_kernel<KT, SH, EE>), dim3(1), dim3(NT), lds, s, ids, R, uniq, inv, perm, seg_ptr, \
                      u_count)

@@ -17,7 +17,6 @@ extern "C" {
 void fr_gemm_set_variant(int v);
 void fr_title_attn_set_waves(int w);
 void fr_title_attn_bwd_set_variant(int v);
-void fr_user_attn_set_variant(int v);
 void fr_score_set_variant(int v);
 void fr_ln_set_wide(int v);
 int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, const void* R, void* C, int M, int N, int K, int act,
@@ -1424,7 +1423,6 @@ at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x) {
 void gemm_set_variant(int64_t v) { fr_gemm_set_variant((int)v); }
 void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
-void user_attn_set_variant(int64_t v) { fr_user_attn_set_variant((int)v); }
 void score_set_variant(int64_t v) { fr_score_set_variant((int)v); }
 void segsum_set_variant(int64_t v) { fr_segsum_set_variant((int)v); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
@@ -1435,7 +1433,6 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("gemm_set_variant(int v) -> ()", &gemm_set_variant);
   m.def("title_attn_set_waves(int w) -> ()", &title_attn_set_waves);
   m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
-  m.def("user_attn_set_variant(int v) -> ()", &user_attn_set_variant);
   m.def("score_set_variant(int v) -> ()", &score_set_variant);
   m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);

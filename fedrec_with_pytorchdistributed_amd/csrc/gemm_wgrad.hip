@@ -256,23 +256,11 @@ extern "C" long fr_wgrad_bf16(const void* dY, const void* X, float* C, float* sc
   const long need = direct ? 0 : (long)S * N * K;
   if (scratch == nullptr && need > 0) return need;
   float* P = direct ? C : scratch;
-  static const int nst = [] {
-    // A/B runs; default 3 (96 KB): 4 and 5 stages measured the same in isolation, and the
-    // smaller block leaves room on a CU for a lookahead-stream kernel (dedup: 32 KB) -- this
-    // grid is one wave of blocks, so a CU that cannot host its block doubles the kernel
-    const char* e = getenv("FEDREC_WGRAD_NST");
-    const int v = e != nullptr ? atoi(e) : 3;
-    return v == 4 || v == 5 ? v : 3;
-  }();
-  if (nst == 3)
-    hipLaunchKernelGGL(wgrad_kernel<3>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M,
-                       N, K, tiles_k, ntiles, mchunk);
-  else if (nst == 5)
-    hipLaunchKernelGGL(wgrad_kernel<5>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M,
-                       N, K, tiles_k, ntiles, mchunk);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<4>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M,
-                       N, K, tiles_k, ntiles, mchunk);
+  // three LDS stages (96 KB): 4 and 5 measured the same in isolation, and the smaller block
+  // leaves room on a CU for a lookahead-stream kernel (dedup: 32 KB) -- this grid is one wave of
+  // blocks, so a CU that cannot host its block doubles the kernel
+  hipLaunchKernelGGL(wgrad_kernel<3>, dim3(S * ntiles), dim3(512), 0, stream, (const bf16*)dY, (const bf16*)X, P, M, N,
+                     K, tiles_k, ntiles, mchunk);
   if (!direct) {
     const long n4 = (long)N * K / 4;
     long blocks = (n4 + 255) / 256;

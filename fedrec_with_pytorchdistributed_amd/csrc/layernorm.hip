@@ -504,18 +504,9 @@ extern "C" int fr_layer_norm_bwd_bf16(const void* x, const float* w, const void*
   if (rows == 0) return 0;
   int blocks = (rows + 3) / 4;
   if (blocks > 1024) blocks = 1024;
-  static const bool pf = [] {  // FEDREC_LN_BWD_PF=0: the row-serial form (A/B runs)
-    const char* e = getenv("FEDREC_LN_BWD_PF");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  if (pf)
-    hipLaunchKernelGGL(ln_bwd_kernel<true>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy,
-                       (bf16*)dx, dw, db, rows, D, eps, dxs, (bf16*)dxz, pdrop, dxz ? 1.0f / (1.0f - pdrop) : 1.f,
-                       seed, offset);
-  else
-    hipLaunchKernelGGL(ln_bwd_kernel<false>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy,
-                       (bf16*)dx, dw, db, rows, D, eps, dxs, (bf16*)dxz, pdrop, dxz ? 1.0f / (1.0f - pdrop) : 1.f,
-                       seed, offset);
+  hipLaunchKernelGGL(ln_bwd_kernel<true>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, w, (const bf16*)dy,
+                     (bf16*)dx, dw, db, rows, D, eps, dxs, (bf16*)dxz, pdrop, dxz ? 1.0f / (1.0f - pdrop) : 1.f,
+                     seed, offset);
   return 0;
 }
 

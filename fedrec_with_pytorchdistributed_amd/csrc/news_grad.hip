@@ -119,9 +119,9 @@ __global__ __launch_bounds__(1024) void segsum_kernel(const float* __restrict__ 
 // partial in scratch[chunk][slot] (slot 0: started before the chunk, slot 1: ends after it).
 // A second pass sums the partials of every crossing segment in chunk order.  The chunk grid
 // is fixed by R alone, so the result is deterministic, and no float atomics are used.
-// SCH: chunk length, a template parameter: 16 (default) or 8 (FEDREC_SEGSUM_SCH=8: half the
-// per-wave row registers -- 89 vs 161 VGPRs -- and twice the waves; measured neutral, 0.5694 /
-// 0.5668 vs 0.5665 / 0.5702 ms per step, profiles/r3_ab_segsum_ua.txt)
+// SCH: chunk length (16; 8 -- half the per-wave row registers, 89 vs 161 VGPRs, twice the
+// waves -- measured neutral: 0.5694 / 0.5668 vs 0.5665 / 0.5702 ms per step,
+// profiles/r3_ab_segsum_ua.txt)
 template <int SCH>
 __global__ __launch_bounds__(256) void segsum_chunk_kernel(const float* __restrict__ rows, const int* __restrict__ perm,
                                                            const int* __restrict__ seg_ptr, const int* __restrict__ inv,
@@ -218,21 +218,13 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__
   for (int d = threadIdx.x; d < D; d += 256) out[(size_t)u * D + d] = ((part[0][d] + part[1][d]) + part[2][d]) + part[3][d];
 }
 
-int g_segsum_variant = 1;  // 1: chunked (default), 0: one block per output row
-int g_segsum_sch = 0;      // chunk length of the chunked form (FEDREC_SEGSUM_SCH: 16 default, or 8)
-
-int segsum_sch() {
-  if (g_segsum_sch == 0) {
-    const char* e = getenv("FEDREC_SEGSUM_SCH");
-    g_segsum_sch = (e != nullptr && atoi(e) == 8) ? 8 : 16;
-  }
-  return g_segsum_sch;
-}
+int g_segsum_variant = 1;  // 1: chunked (default), 0: one block per output row (the no-scratch form)
+constexpr int SCH = 16;    // chunk length (8-occurrence chunks measured neutral, r3_ab_segsum_ua.txt)
 
 }  // namespace
 
 extern "C" void fr_segsum_set_variant(int v) { g_segsum_variant = v; }
-extern "C" int fr_segsum_chunks(int R) { return (R + segsum_sch() - 1) / segsum_sch(); }
+extern "C" int fr_segsum_chunks(int R) { return (R + SCH - 1) / SCH; }
 
 extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std,
                            unsigned long long seed, unsigned long long offset, hipStream_t s,
@@ -252,17 +244,10 @@ extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int
   if (D > 64 * MAXV) return 1;
   if (U == 0) return 0;
   if (g_segsum_variant == 1 && scratch != nullptr && inv != nullptr && R > 0) {
-    const int sch = segsum_sch();
-    const int nch = (R + sch - 1) / sch;
-    if (sch == 16) {
-      hipLaunchKernelGGL(segsum_chunk_kernel<16>, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out,
-                         scratch, U, R, D);
-      hipLaunchKernelGGL(segsum_fix_kernel<16>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
-    } else {
-      hipLaunchKernelGGL(segsum_chunk_kernel<8>, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out,
-                         scratch, U, R, D);
-      hipLaunchKernelGGL(segsum_fix_kernel<8>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
-    }
+    const int nch = (R + SCH - 1) / SCH;
+    hipLaunchKernelGGL(segsum_chunk_kernel<SCH>, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out,
+                       scratch, U, R, D);
+    hipLaunchKernelGGL(segsum_fix_kernel<SCH>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
     return 0;
   }
   if (zero_empty) (void)hipMemsetAsync(out, 0, (size_t)U * D * sizeof(float), s);

@@ -528,41 +528,6 @@ __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch b
   }
 }
 
-// The same 64 x 64 bodies compiled for 5 waves per SIMD (<= 96 VGPRs, a few spilled words)
-// instead of 4: these GEMMs are latency-bound and hide it across co-resident blocks (a deeper
-// in-block register queue, SG_NQ = 3, measured slower: 2 waves per SIMD).  FEDREC_SG_OCC=5.
-template <bool AH, bool BH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void small_gemm_occ5_kernel(
-    const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
-  int gi;
-  const int t = tile_of_block(batch, gi);
-  const GemmDesc& g = batch.d[gi];
-  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
-  gemm_tile<2, 2, true, AH, BH>(g, off, t, As, Bs);
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void small_gemm_mixed_occ5_kernel(
-    const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) bf16 As[64][LDT];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[64][LDT];
-  int gi;
-  const int t = tile_of_block(batch, gi);
-  const GemmDesc& g = batch.d[gi];
-  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
-  if (g.a_bf16) {
-    if (g.b_bf16)
-      gemm_tile<2, 2, true, true, true>(g, off, t, As, Bs);
-    else
-      gemm_tile<2, 2, true, true, false>(g, off, t, As, Bs);
-  } else {
-    if (g.b_bf16)
-      gemm_tile<2, 2, true, false, true>(g, off, t, As, Bs);
-    else
-      gemm_tile<2, 2, true, false, false>(g, off, t, As, Bs);
-  }
-}
 
 // split-K epilogue: C = act(alpha * sum_s P[s] + bias) (x the output dropout scale, drop_on 3)
 // (+ C), partials summed in split order (deterministic) -- the single-pass epilogue's order.
@@ -742,12 +707,8 @@ static int choose_splits(int tiles, int K) {
   // (measured: the 1200 x 400 x 3200 weight gradient in 133 tiles -- 2 splits 69 us, four
   // 400-row descs in 6 splits 49 us; the 3200 x 400 x 1200 dgrad in 350 tiles -- 2 splits
   // 38.6 us, 3 splits 44.5: the partials' write + reduce outweigh the shorter chains).
-  static const int mink = [] {  // FEDREC_SG_MINK: fewest K per split (A/B; 384 = 6 k-tiles measured best of 192-768,
-    // profiles/r3_ab_sg_mink.txt)
-    const char* e = getenv("FEDREC_SG_MINK");
-    const int v = e ? atoi(e) : 384;
-    return v >= 64 ? v : 384;
-  }();
+  // fewest K per split: 384 (6 k-tiles) measured best of 192-768 (profiles/r3_ab_sg_mink.txt)
+  constexpr int mink = 384;
   if (K < 512) return 1;
   const int want = (512 + tiles - 1) / tiles;
   int s = min(want, K / mink);
@@ -766,11 +727,6 @@ static void tile_dims(int v, int& tm, int& tn) {
 // 128 x 128 form took 18.7 us vs 9.4 (3200 x 1200), and only caught up at >= 4 tiles per CU
 // and K >= 512 (benchmarks/sg_latency_probe.py, profiles/r3_small_gemm_bench.json).
 static int choose_tile(const GemmBatch& b) {
-  static const int forced = [] {
-    const char* e = getenv("FEDREC_SG_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced >= 1 && forced <= 4) return forced;
   long tiles = 0;
   for (int i = 0; i < b.n; ++i) tiles += (long)((b.d[i].M + 63) / 64) * ((b.d[i].N + 63) / 64);
   return tiles >= 2048 ? 4 : 1;
@@ -790,8 +746,7 @@ static bool fast_ok(const GemmBatch& b) {
            ((uintptr_t)d.A & 15) == 0 && ((uintptr_t)d.B & 15) == 0 && d.kseg == 0 && d.gather_on == 0 &&
            d.drop_on != 1 && d.drop_on != 2 && ext_a < 2.0e9 && ext_b < 2.0e9;
   }
-  static const bool no_fast = getenv("FEDREC_SG_GENERIC") != nullptr;
-  return fast && !no_fast;
+  return fast;
 }
 
 static bool mixed_dtypes(const GemmBatch& b) {
@@ -884,50 +839,19 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     else                                                                                                   \
       hipLaunchKernelGGL((small_gemm_kernel<FM, FN, true, true, true>), dim3(tiles), dim3(256), 0, s, b);    \
   } while (0)
-  static const int occ = [] {
-    const char* e = getenv("FEDREC_SG_OCC");
-    return e ? atoi(e) : 0;
-  }();
-  // stored-transposed operands of the 64x64 tiles as TRI images (FEDREC_SG_TR=0: the
-  // k-contiguous image with scalar transposed stores; the TRI form measured 0.5715 -> 0.5566 ms
-  // per config-2 step, profiles/r3_ab_sg_tri.txt)
-  static const bool tri = [] {
-    const char* e = getenv("FEDREC_SG_TR");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  // two LDS buffers, one barrier per k-step on the TRI kernels (FEDREC_SG_DB=0: one buffer, two
-  // barriers): steady step 0.5484-0.5493 vs 0.5494-0.5520 ms, three A/B pairs (r3_ab_sg_db.txt)
-  static const bool db = [] {
-    const char* e = getenv("FEDREC_SG_DB");
-    return e == nullptr || atoi(e) != 0;
-  }();
+  // stored-transposed operands of the 64x64 tiles staged as TRI images (0.5715 -> 0.5566 ms per
+  // config-2 step, profiles/r3_ab_sg_tri.txt) with two LDS buffers and one barrier per k-step
+  // (0.5484-0.5493 vs 0.5494-0.5520 ms, r3_ab_sg_db.txt); the 128-row / -column tiles keep the
+  // k-contiguous image (their launches have >= 8 tiles per CU: bandwidth-, not latency-bound)
   if (!fast)
     hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);
-  else if (mixed && occ == 5)
-    hipLaunchKernelGGL(small_gemm_mixed_occ5_kernel, dim3(tiles), dim3(256), 0, s, b);
-  else if (mixed && tri && db)
-    hipLaunchKernelGGL((small_gemm_mixed_kernel<true, true>), dim3(tiles), dim3(256), 0, s, b);
-  else if (mixed && tri)
-    hipLaunchKernelGGL(small_gemm_mixed_kernel<true>, dim3(tiles), dim3(256), 0, s, b);
   else if (mixed)
-    hipLaunchKernelGGL(small_gemm_mixed_kernel<false>, dim3(tiles), dim3(256), 0, s, b);
-  else if (tri && v == 1 && db) {
+    hipLaunchKernelGGL((small_gemm_mixed_kernel<true, true>), dim3(tiles), dim3(256), 0, s, b);
+  else if (v == 1) {
     if (dt == 0) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
     else if (dt == 1) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, true, true, true>), dim3(tiles), dim3(256), 0, s, b);
     else if (dt == 2) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
     else hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, true, true, true>), dim3(tiles), dim3(256), 0, s, b);
-  }
-  else if (tri && v == 1) {
-    if (dt == 0) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, false, true>), dim3(tiles), dim3(256), 0, s, b);
-    else if (dt == 1) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
-    else if (dt == 2) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, false, true>), dim3(tiles), dim3(256), 0, s, b);
-    else hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, true, true, true>), dim3(tiles), dim3(256), 0, s, b);
-  }
-  else if (occ == 5 && v == 1) {
-    if (dt == 0) hipLaunchKernelGGL((small_gemm_occ5_kernel<false, false>), dim3(tiles), dim3(256), 0, s, b);
-    else if (dt == 1) hipLaunchKernelGGL((small_gemm_occ5_kernel<false, true>), dim3(tiles), dim3(256), 0, s, b);
-    else if (dt == 2) hipLaunchKernelGGL((small_gemm_occ5_kernel<true, false>), dim3(tiles), dim3(256), 0, s, b);
-    else hipLaunchKernelGGL((small_gemm_occ5_kernel<true, true>), dim3(tiles), dim3(256), 0, s, b);
   }
   else switch (v) {
     case 2: SG_LAUNCH(4, 2); break;

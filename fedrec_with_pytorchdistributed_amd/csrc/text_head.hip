@@ -408,6 +408,197 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
   }
 }
 
+// -----------------------------------------------------------------------------------------
+// head_score3: the att_fc1 product with ONLY the gathered X rows in the LDS pipeline.
+// head_score2 stages X (192 rows) AND the whole W1 k-slice (384 rows) per k-step: 72 KB a stage,
+// two stages, so one stage is in flight while the MFMAs read the other, and a k-step waits out
+// the full LDS-DMA latency of 72 KB (the wave-state counters' dependency waits).  Here:
+//   * X: 128 rows x 64 k per stage = 16 KB, NST-deep ring (NST - 1 stages in flight);
+//   * W1: each wave owns Q / 8 columns (QFW 16-column fragments) and loads its MFMA A fragments
+//     straight from L2 into registers (one 16-B global load per lane = one fragment), NST - 1
+//     k-steps ahead -- W1 (590 KB) is L2-resident and every block reads each byte once, the
+//     same bytes head_score2 moved through the LDS, without the LDS write + read;
+//   * every wave multiplies its QFW column fragments by all 8 row fragments of the stage
+//     (acc 8 x QFW f32x4), so X fragments are read from LDS by all 8 waves (8 x 16 KB per
+//     stage: 1/3 of what the LDS serves per MFMA in head_score2's 2 x 4 layout).
+// Issue order per iteration: the glds of stage kt + NST - 1, then (after a compiler memory fence,
+// so the order holds) the W1 loads of k-step kt + NST - 1; waiting for k-step kt's W1 loads
+// therefore also covers its stage.  The k loop is fully unrolled (NK = D / 64 k-steps), so the
+// counted waits are immediates.  Epilogue as head_score2 (tanh, w2 row-dot, bf16 e).
+// -----------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void vm_wait_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void vm_wait_barrier_rt(int n) {  // n folds to a constant once unrolled
+  switch (n) {
+    case 0: vm_wait_barrier<0>(); break;
+    case 8: vm_wait_barrier<8>(); break;
+    case 16: vm_wait_barrier<16>(); break;
+    case 24: vm_wait_barrier<24>(); break;
+    case 6: vm_wait_barrier<6>(); break;
+    case 12: vm_wait_barrier<12>(); break;
+    case 18: vm_wait_barrier<18>(); break;
+    case 4: vm_wait_barrier<4>(); break;
+    case 10: vm_wait_barrier<10>(); break;
+    case 20: vm_wait_barrier<20>(); break;
+    case 30: vm_wait_barrier<30>(); break;
+    case 32: vm_wait_barrier<32>(); break;
+    case 40: vm_wait_barrier<40>(); break;
+    default: vm_wait_barrier<0>(); break;
+  }
+}
+
+template <int QFW, int NST, int NK, int PW>
+__global__ __launch_bounds__(512, 1) void head_score3_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
+                                                             int M, int T, const bf16* __restrict__ W1,
+                                                             const float* __restrict__ b1, const float* __restrict__ w2,
+                                                             const float* __restrict__ b2, bf16* __restrict__ e_out,
+                                                             float* __restrict__ a_out, const int* __restrict__ nreal) {
+  constexpr int D = NK * 64, Q = QFW * 128, MR = 128, RB = 128, ST = MR * RB, PX = NST - 1;
+  static_assert(PW >= 1 && PW <= PX, "W1 prefetch distance within the X ring's");
+  __shared__ __attribute__((aligned(16))) char smem[NST * ST];
+  const int m0 = blockIdx.x * MR;
+  if (nreal != nullptr && m0 >= min(M, nreal[0] * T)) return;  // only padded titles' rows (never read)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+  // X pieces: 16 per stage (8 rows x 128 B each); wave w issues pieces w and w + 8
+  const bf16* xsrc[2];
+  uint32_t xdst[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = wave + 8 * i, r = p * 8 + (lane >> 3);
+    int gm = m0 + r;
+    gm = gm < M ? gm : M - 1;  // rows past M: any valid row (outputs masked)
+    xsrc[i] = hrow(table, ids, gm, T, D) + ((lane & 7) ^ (r & 7)) * 8;
+    xdst[i] = (uint32_t)(p * 8 * RB);
+  }
+  // this lane's W1 fragment rows: q = wave * 16 QFW + 16 i + fr, k chunk fq (+ 32 for substep 1)
+  const bf16* wsrc = W1 + (size_t)(wave * 16 * QFW + fr) * D + fq * 8;
+  u32x4_t wreg[PW][2][QFW];
+  // iteration j issues the X stage of k-step j + PX, then the W1 fragments of k-step j + PW
+  auto issue_x = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, xsrc[i] + kt * 64),
+                                       LDS_PTR(void, smem + (kt % NST) * ST + xdst[i]), 16, 0, 0);
+    asm volatile("" ::: "memory");  // later loads stay behind this stage's glds
+  };
+  // one substep's fragments; a k-step's substep-kk registers are refilled right after the MFMAs
+  // that read them (no extra register slot for the load in flight)
+  auto issue_w = [&](int kt, int kk) {
+#pragma unroll
+    for (int i = 0; i < QFW; ++i)
+      wreg[kt % PW][kk][i] = *(const u32x4_t*)(wsrc + (size_t)i * 16 * D + kt * 64 + kk * 32);
+    asm volatile("" ::: "memory");
+  };
+  f32x4 acc[QFW][8];
+#pragma unroll
+  for (int i = 0; i < QFW; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // prologue, in the loop's issue order
+#pragma unroll
+  for (int kt = 0; kt < PX; ++kt) {
+    if (kt < NK) issue_x(kt);
+    if (kt + PW - PX >= 0 && kt + PW - PX < NK) {
+      issue_w(kt + PW - PX, 0);
+      issue_w(kt + PW - PX, 1);
+    }
+  }
+#pragma unroll
+  for (int kt = 0; kt < NK; ++kt) {
+    // k-step kt's W1 fragments landed (issued in iteration kt - PW, after the glds of its stage,
+    // which was issued earlier still): the younger ops are those of iterations kt - PW + 1 .. kt - 1
+    int younger = 0;
+#pragma unroll
+    for (int j = kt - PW + 1; j < kt; ++j) {
+      if (j + PX < NK) younger += 2;
+      if (j + PW < NK) younger += 2 * QFW;
+    }
+    vm_wait_barrier_rt(younger);
+    if (kt + PX < NK) issue_x(kt + PX);
+    const uint32_t As = lds0 + (kt % NST) * ST;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int lc = kk * 4 + fq;
+      u32x4_t xr[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = j * 16 + fr;
+        xr[j] = lds_read128(As + r * RB + ((lc ^ (r & 7)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        lgkm_tie_rt(7 - j, xr[j]);
+#pragma unroll
+        for (int i = 0; i < QFW; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wreg[kt % PW][kk][i]),
+                                                              __builtin_bit_cast(bf16x8, xr[j]), acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);  // the refill stays after the MFMAs that read these registers
+      if (kt + PW < NK) issue_w(kt + PW, kk);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();  // every wave done with the last stage: the reduction buffer reuses it
+  const float b2v = b2[0];
+  float part[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < QFW; ++i) {
+    const int qb = wave * 16 * QFW + i * 16 + fq * 4;
+    const float4 bb = *(const float4*)(b1 + qb);
+    const float4 ww = *(const float4*)(w2 + qb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v[4];
+      v[0] = tanh_fast(acc[i][j][0] + bb.x);
+      v[1] = tanh_fast(acc[i][j][1] + bb.y);
+      v[2] = tanh_fast(acc[i][j][2] + bb.z);
+      v[3] = tanh_fast(acc[i][j][3] + bb.w);
+      part[j] += v[0] * ww.x + v[1] * ww.y + v[2] * ww.z + v[3] * ww.w;
+      acc[i][j] = f32x4{v[0], v[1], v[2], v[3]};
+    }
+  }
+  if (e_out != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + j * 16 + fr;
+      bf16* crow = e_out + (size_t)(m < M ? m : 0) * Q + wave * 16 * QFW;
+#pragma unroll
+      for (int i = 0; i + 1 < QFW; i += 2) {
+        const float v0[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        const float v1[4] = {acc[i + 1][j][0], acc[i + 1][j][1], acc[i + 1][j][2], acc[i + 1][j][3]};
+        store_pair16_if(crow + i * 16, v0, v1, fq, m < M);
+      }
+      if constexpr (QFW % 2 == 1) {
+        const int i = QFW - 1;
+        const bf16x4 o = {f2bf(acc[i][j][0]), f2bf(acc[i][j][1]), f2bf(acc[i][j][2]), f2bf(acc[i][j][3])};
+        if (m < M) *(bf16x4*)(crow + i * 16 + fq * 4) = o;
+      }
+    }
+  }
+  float* red = (float*)smem;  // [8 waves][128 rows]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float sv = group4_sum(part[j]);
+    if (fq == 0) red[wave * MR + j * 16 + fr] = sv;
+  }
+  __syncthreads();
+  if (tid < MR && m0 + tid < M) {
+    const float sa = ((red[tid] + red[MR + tid]) + (red[2 * MR + tid] + red[3 * MR + tid])) +
+                     ((red[4 * MR + tid] + red[5 * MR + tid]) + (red[6 * MR + tid] + red[7 * MR + tid]));
+    a_out[m0 + tid] = sa + b2v;
+  }
+}
+
 // =========================================================================================
 // head_pool: per title u, alpha = eps-softmax(a) (stable form exp(a-m) / (sum + 1e-8 e^-m),
 // masked tokens get weight 0), pooled = sum_t alpha_t x_t (fp32).  384 threads: TG t-groups x
@@ -1423,6 +1614,17 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   // 3 -> 128 rows, BK 64, 2 stages; 4 -> 192 rows, BK 32, 3 stages; 5 -> two Q slices of 192
   // columns, 192 rows, BK 64, 3 stages (partial scores, see head_score2_kernel); 0 ->
   // head_score_kernel
+  if (g_score_variant == 8 && D == 768) {  // head_score3: X-only LDS ring, W1 fragments from L2
+    const dim3 grid((M + 127) / 128);
+#define LAUNCH_S3(QFW)                                                                                       \
+  hipLaunchKernelGGL((head_score3_kernel<QFW, 4, 12, 2>), grid, dim3(512), 0, s, (const bf16*)table, ids, M, T, \
+                     (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, nreal)
+    if (Q == 384) LAUNCH_S3(3);
+    else if (Q == 256) LAUNCH_S3(2);
+    else LAUNCH_S3(1);
+#undef LAUNCH_S3
+    return 0;
+  }
   if (Q == 384 && g_score_variant > 0) {
 #define LAUNCH_S2(QF, RF, BK, NST, WQ, NS, ...)                                                                \
   hipLaunchKernelGGL((head_score2_kernel<QF, RF, BK, NST, WQ, ##__VA_ARGS__>), dim3((M + 32 * RF - 1) / (32 * RF), NS), dim3(512), \

@@ -3,8 +3,9 @@
 //   S = Q K^T / sqrt(d_k),  A = exp(S) / (rowsum exp(S) + 1e-8),  ctx = A V
 //
 // 20 heads x d_k 20 over the clicked news, fp32.  H <= 64 runs on the matrix cores in fp32
-// (v_mfma_f32_16x16x4_f32, the "matrix-core forms" below -- the default); the VALU forms stay
-// for A/B runs (FEDREC_UA_VARIANT=1/0) and long histories (H > 64).  The eps softmax is
+// (v_mfma_f32_16x16x4_f32, the "matrix-core forms" below); long histories (H > 64) on the
+// VALU kernels at the end (online softmax over 64-row chunks).  (The round-2 VALU forms and a
+// one-wave MFMA form measured slower at H <= 64 and were removed in round 4.)  The eps softmax is
 // evaluated stably:
 // A = exp(S - m) / (sum exp(S - m) + 1e-8 exp(-m)).  No mask (Q7), like the reference.
 //
@@ -41,230 +42,6 @@ __device__ __forceinline__ void axpy20(float (&acc)[DK], float a, const float* _
     acc[4 * c4 + 2] += a * v.z;
     acc[4 * c4 + 3] += a * v.w;
   }
-}
-
-__global__ __launch_bounds__(128) void user_attn_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
-                                                            float* __restrict__ stats, int B, int H, int NH) {
-  __shared__ __attribute__((aligned(16))) float ks[2][MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float vs[2][MAXH][DK];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pair = blockIdx.x * 2 + wave;
-  const bool active = pair < B * NH;
-  const int b = active ? pair / NH : 0, h = active ? pair - b * NH : 0;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  for (int i = lane; i < H * DK / 4; i += 64) {  // 16-B chunks (DK % 4 == 0, rows 16-B aligned)
-    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
-    *(float4*)&ks[wave][r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
-    *(float4*)&vs[wave][r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
-  }
-  __syncthreads();
-  if (!active || lane >= H) return;
-  float q[DK];
-#pragma unroll
-  for (int c4 = 0; c4 < DK / 4; ++c4) {
-    const float4 v = *(const float4*)(base + (size_t)lane * ld + 4 * c4);
-    q[4 * c4] = v.x;
-    q[4 * c4 + 1] = v.y;
-    q[4 * c4 + 2] = v.z;
-    q[4 * c4 + 3] = v.w;
-  }
-  const float scale = rsqrtf((float)DK);
-#pragma unroll
-  for (int c = 0; c < DK; ++c) q[c] *= scale;
-  float m = -INFINITY;
-  for (int s = 0; s < H; ++s) m = fmaxf(m, dot20(q, &ks[wave][s][0]));
-  float acc[DK];
-#pragma unroll
-  for (int c = 0; c < DK; ++c) acc[c] = 0.f;
-  float l = 0.f;
-  for (int s = 0; s < H; ++s) {
-    const float p = __expf(dot20(q, &ks[wave][s][0]) - m);
-    l += p;
-    axpy20(acc, p, &vs[wave][s][0]);
-  }
-  l += 1e-8f * __expf(-m);
-  const float inv = 1.0f / l;
-  float* o = ctx + ((size_t)b * H + lane) * D + h * DK;
-#pragma unroll
-  for (int c4 = 0; c4 < DK / 4; ++c4)
-    *(float4*)(o + 4 * c4) = make_float4(acc[4 * c4] * inv, acc[4 * c4 + 1] * inv, acc[4 * c4 + 2] * inv,
-                                         acc[4 * c4 + 3] * inv);
-  float* st = stats + (((size_t)b * NH + h) * H + lane) * 2;
-  st[0] = m;
-  st[1] = inv;
-}
-
-// Backward, 2 passes over the keys (was 3): lane = query t accumulates
-//   u = sum_s A_ts dA_ts k_s, w = sum_s A_ts k_s, D_t = sum_s A_ts dA_ts
-// in ONE pass and forms dq_t = scale (u - D_t w); lane = key s then accumulates dk_s, dv_s.
-__global__ __launch_bounds__(64) void user_attn_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ stats,
-                                                           const float* __restrict__ dctx, float* __restrict__ dqkv,
-                                                           int B, int H, int NH) {
-  __shared__ __attribute__((aligned(16))) float qs[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float ks[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float vs[MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float gs[MAXH][DK];
-  __shared__ float ms[MAXH], is_[MAXH], Ds[MAXH];
-  const int lane = threadIdx.x;
-  const int pair = blockIdx.x;
-  const int b = pair / NH, h = pair - b * NH;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  const float* gb = dctx + (size_t)b * H * D + h * DK;
-  for (int i = lane; i < H * DK / 4; i += 64) {
-    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
-    *(float4*)&qs[r][c] = *(const float4*)(base + (size_t)r * ld + c);
-    *(float4*)&ks[r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
-    *(float4*)&vs[r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
-    *(float4*)&gs[r][c] = *(const float4*)(gb + (size_t)r * D + c);
-  }
-  const float* st = stats + ((size_t)b * NH + h) * H * 2;
-  for (int t = lane; t < H; t += 64) {
-    ms[t] = st[2 * t];
-    is_[t] = st[2 * t + 1];
-  }
-  __syncthreads();
-  const float scale = rsqrtf((float)DK);
-  float* dbase = dqkv + (size_t)b * H * ld + h * DK;
-  if (lane < H) {
-    const int t = lane;
-    const float m = ms[t], inv = is_[t];
-    float q[DK], g[DK], u[DK], w[DK];
-#pragma unroll
-    for (int c = 0; c < DK; ++c) {
-      q[c] = qs[t][c] * scale;
-      g[c] = gs[t][c];
-      u[c] = w[c] = 0.f;
-    }
-    float Dt = 0.f;
-    for (int s = 0; s < H; ++s) {
-      const float A = __expf(dot20(q, &ks[s][0]) - m) * inv;
-      const float dA = dot20(g, &vs[s][0]);
-      Dt += A * dA;
-      axpy20(u, A * dA, &ks[s][0]);
-      axpy20(w, A, &ks[s][0]);
-    }
-    Ds[t] = Dt;
-    float* o = dbase + (size_t)t * ld;
-#pragma unroll
-    for (int c4 = 0; c4 < DK / 4; ++c4) {
-      const int c = 4 * c4;
-      *(float4*)(o + c) = make_float4(scale * (u[c] - Dt * w[c]), scale * (u[c + 1] - Dt * w[c + 1]),
-                                      scale * (u[c + 2] - Dt * w[c + 2]), scale * (u[c + 3] - Dt * w[c + 3]));
-    }
-  }
-  __syncthreads();
-  if (lane < H) {
-    const int s = lane;
-    float k[DK], v[DK], dk[DK], dv[DK];
-#pragma unroll
-    for (int c = 0; c < DK; ++c) {
-      k[c] = ks[s][c] * scale;
-      v[c] = vs[s][c];
-      dk[c] = dv[c] = 0.f;
-    }
-    for (int t = 0; t < H; ++t) {
-      const float A = __expf(dot20(k, &qs[t][0]) - ms[t]) * is_[t];
-      const float dA = dot20(v, &gs[t][0]);
-      const float dS = A * (dA - Ds[t]) * scale;
-      axpy20(dk, dS, &qs[t][0]);
-      axpy20(dv, A, &gs[t][0]);
-    }
-    float* o = dbase + (size_t)s * ld;
-#pragma unroll
-    for (int c4 = 0; c4 < DK / 4; ++c4) {
-      const int c = 4 * c4;
-      *(float4*)(o + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
-      *(float4*)(o + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// ILP forward (default).  The kernels above are latency-bound, not FLOP-bound: ~1.25 waves per
-// SIMD, and every key costs a 20-deep chain of dependent FMAs (dot20) before its exp -- the
-// forward ran 33 us for 1,280 (impression, head) pairs of 50 x 50 x 20.  Here the key loops
-// are fully unrolled over MAXH with a wave-uniform guard (so independent keys interleave),
-// the dot products split into 4 partial sums (chains of 5), and the scores stay in registers
-// (one dot product per key instead of two): 20 us (profiles/r2_user_attn_ilp_bench.json).
-// Same math (fp32; only the summation order inside a 20-term dot product differs).  The same
-// treatment of the backward measured slower (63 vs 54 us), and so did an unroll-by-4 form
-// with split dot products (64 vs 56 us, 256 VGPRs); the backward keeps its first form.
-__device__ __forceinline__ void load_row_s(float (&x)[DK], const float* __restrict__ p, float sc) {
-#pragma unroll
-  for (int c4 = 0; c4 < DK / 4; ++c4) {
-    const float4 v = *(const float4*)(p + 4 * c4);
-    x[4 * c4] = v.x * sc;
-    x[4 * c4 + 1] = v.y * sc;
-    x[4 * c4 + 2] = v.z * sc;
-    x[4 * c4 + 3] = v.w * sc;
-  }
-}
-
-__device__ __forceinline__ float dot20x(const float (&q)[DK], const float* __restrict__ row) {
-  float d[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c4 = 0; c4 < DK / 4; ++c4) {
-    const float4 k = *(const float4*)(row + 4 * c4);
-    d[0] += q[4 * c4] * k.x;
-    d[1] += q[4 * c4 + 1] * k.y;
-    d[2] += q[4 * c4 + 2] * k.z;
-    d[3] += q[4 * c4 + 3] * k.w;
-  }
-  return (d[0] + d[1]) + (d[2] + d[3]);
-}
-
-__global__ __launch_bounds__(128) void user_attn_fwd_ilp_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
-                                                                float* __restrict__ stats, int B, int H, int NH) {
-  __shared__ __attribute__((aligned(16))) float ks[2][MAXH][DK];
-  __shared__ __attribute__((aligned(16))) float vs[2][MAXH][DK];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pair = blockIdx.x * 2 + wave;
-  const bool active = pair < B * NH;
-  const int b = active ? pair / NH : 0, h = active ? pair - b * NH : 0;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  for (int i = lane; i < H * DK / 4; i += 64) {
-    const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
-    *(float4*)&ks[wave][r][c] = *(const float4*)(base + (size_t)r * ld + D + c);
-    *(float4*)&vs[wave][r][c] = *(const float4*)(base + (size_t)r * ld + 2 * D + c);
-  }
-  const int t = lane < H ? lane : H - 1;  // clamped: every lane runs the same unrolled code
-  float q[DK];
-  load_row_s(q, base + (size_t)t * ld, rsqrtf((float)DK));
-  __syncthreads();
-  if (!active) return;
-  float sc[MAXH];
-  float m = -INFINITY;
-#pragma unroll
-  for (int s = 0; s < MAXH; ++s)
-    if (s < H) {
-      sc[s] = dot20x(q, &ks[wave][s][0]);
-      m = fmaxf(m, sc[s]);
-    }
-  float acc[DK];
-#pragma unroll
-  for (int c = 0; c < DK; ++c) acc[c] = 0.f;
-  float l = 0.f;
-#pragma unroll
-  for (int s = 0; s < MAXH; ++s)
-    if (s < H) {
-      const float p = __expf(sc[s] - m);
-      l += p;
-      axpy20(acc, p, &vs[wave][s][0]);
-    }
-  if (lane >= H) return;
-  l += 1e-8f * __expf(-m);
-  const float inv = 1.0f / l;
-  float* o = ctx + ((size_t)b * H + lane) * D + h * DK;
-#pragma unroll
-  for (int c4 = 0; c4 < DK / 4; ++c4)
-    *(float4*)(o + 4 * c4) = make_float4(acc[4 * c4] * inv, acc[4 * c4 + 1] * inv, acc[4 * c4 + 2] * inv,
-                                         acc[4 * c4 + 3] * inv);
-  float* st = stats + (((size_t)b * NH + h) * H + lane) * 2;
-  st[0] = m;
-  st[1] = inv;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -402,186 +179,14 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v + dpp<DPP_MIRROR>(v);
 }
 
-template <int NT, int DBG = 0>
-__global__ __launch_bounds__(64) void user_attn_fwd_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
-                                                                float* __restrict__ stats, int H, int NH) {
-  __shared__ __attribute__((aligned(16))) float qs[65][DK];  // row 64: the tail of mm_pY's column reads
-  __shared__ __attribute__((aligned(16))) float ks[65][DK];
-  __shared__ __attribute__((aligned(16))) float vs[65][DK];
-  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
-  const int lane = threadIdx.x, fr = lane & 15, fq = lane >> 4;
-  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  {
-    float (*const xs[3])[DK] = {qs, ks, vs};
-    const float* const src[3] = {base, base + D, base + 2 * D};
-    const size_t lds[3] = {(size_t)ld, (size_t)ld, (size_t)ld};
-    stage_heads<NT, 3>(xs, src, lds, H, lane);
-  }
-  __syncthreads();
-  if constexpr (DBG == 1) {  // diagnostic timing: staging only
-    if (lane == 0) ctx[(size_t)b * H * NH * DK + h] = qs[1][1] + ks[2][2] + vs[3][3];
-    return;
-  }
-  f32x4 s[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mm_xyT<NT>(s, qs, ks, fr, fq);
-  const float scale = rsqrtf((float)DK);
-  float inv[4][4], mrow[4][4];
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float m = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const float v = j * 16 + fr < H ? s[i][j][r] * scale : -INFINITY;
-        s[i][j][r] = v;
-        m = fmaxf(m, v);
-      }
-      m = row16_max(m);
-      float l = 0.f;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const float p = __expf(s[i][j][r] - m);  // exp(-inf) = 0 for the padded keys
-        s[i][j][r] = p;
-        l += p;
-        ps[(i * 16 + fq * 4 + r) * PLD + j * 16 + fr] = p;
-      }
-      l = row16_sum(l) + 1e-8f * __expf(-m);
-      inv[i][r] = 1.0f / l;
-      mrow[i][r] = m;
-    }
-  __syncthreads();
-  if constexpr (DBG == 2) {  // diagnostic timing: staging + S + softmax
-    if (lane == 0) ctx[(size_t)b * H * NH * DK + h] = inv[0][0] + ps[5];
-    return;
-  }
-  f32x4 o[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mm_pY<NT, false>(o, ps, vs, (H + 3) / 4, fr, fq);
-  store_head<NT>(ctx + (size_t)b * H * D + h * DK, D, o, inv, H, fr, fq);
-  if (fr == 0) {
-    float* st = stats + ((size_t)b * NH + h) * H * 2;
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i * 16 + fq * 4 + r;
-        if (row < H) {
-          st[2 * row] = mrow[i][r];
-          st[2 * row + 1] = inv[i][r];
-        }
-      }
-  }
-}
-
-template <int NT>
-__global__ __launch_bounds__(64) void user_attn_bwd_mfma_kernel(const float* __restrict__ qkv,
-                                                                const float* __restrict__ stats,
-                                                                const float* __restrict__ dctx,
-                                                                float* __restrict__ dqkv, int H, int NH) {
-  __shared__ __attribute__((aligned(16))) float qs[65][DK];  // row 64: the tail of mm_pY's column reads
-  __shared__ __attribute__((aligned(16))) float ks[65][DK];
-  __shared__ __attribute__((aligned(16))) float vs[65][DK];
-  __shared__ __attribute__((aligned(16))) float gs[65][DK];
-  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
-  const int lane = threadIdx.x, fr = lane & 15, fq = lane >> 4;
-  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  {
-    float (*const xs[4])[DK] = {qs, ks, vs, gs};
-    const float* const src[4] = {base, base + D, base + 2 * D, dctx + (size_t)b * H * D + h * DK};
-    const size_t lds[4] = {(size_t)ld, (size_t)ld, (size_t)ld, (size_t)D};
-    stage_heads<NT, 4>(xs, src, lds, H, lane);
-  }
-  const float* st = stats + ((size_t)b * NH + h) * H * 2;
-  float mrow[4][4], inv[4][4];
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = i * 16 + fq * 4 + r, rc = min(row, H - 1);
-      const float mv = st[2 * rc], iv = st[2 * rc + 1];  // unconditional loads (see stage_head)
-      mrow[i][r] = row < H ? mv : 0.f;
-      inv[i][r] = row < H ? iv : 0.f;
-    }
-  __syncthreads();
-  f32x4 p[4][4], dp[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) p[i][j] = dp[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mm_xyT<NT>(p, qs, ks, fr, fq);
-  mm_xyT<NT>(dp, gs, vs, fr, fq);
-  const float scale = rsqrtf((float)DK);
-  // P = exp(S scale - m) / l; D_t = sum_s P dP; dS = P (dP - D) scale (kept in dp)
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float Dt = 0.f;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const float pv = j * 16 + fr < H ? __expf(p[i][j][r] * scale - mrow[i][r]) * inv[i][r] : 0.f;
-        p[i][j][r] = pv;
-        Dt += pv * dp[i][j][r];
-        ps[(i * 16 + fq * 4 + r) * PLD + j * 16 + fr] = pv;
-      }
-      Dt = row16_sum(Dt);
-#pragma unroll
-      for (int j = 0; j < NT; ++j) dp[i][j][r] = p[i][j][r] * (dp[i][j][r] - Dt) * scale;
-    }
-  __syncthreads();
-  float* dbase = dqkv + (size_t)b * H * ld + h * DK;
-  const int KS = (H + 3) / 4;
-  f32x4 o[4][2];
-  // dV = P^T dctx (rows = keys)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mm_pY<NT, true>(o, ps, gs, KS, fr, fq);
-  store_head<NT>(dbase + 2 * D, ld, o, nullptr, H, fr, fq);
-  __syncthreads();  // every lane done reading P before it is overwritten by dS
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) ps[(i * 16 + fq * 4 + r) * PLD + j * 16 + fr] = dp[i][j][r];
-  __syncthreads();
-  // dQ = dS K (rows = queries), dK = dS^T Q (rows = keys)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mm_pY<NT, false>(o, ps, ks, KS, fr, fq);
-  store_head<NT>(dbase, ld, o, nullptr, H, fr, fq);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mm_pY<NT, true>(o, ps, qs, KS, fr, fq);
-  store_head<NT>(dbase + D, ld, o, nullptr, H, fr, fq);
-}
-
-// Four-wave forms (the default): one workgroup per (impression, head), wave w owns query tile
-// w (rows 16w..16w+15) -- S row tile, softmax and ctx rows; in the backward also dQ of its rows,
-// then (after one barrier, P and dS complete in LDS) key tile w -- dK and dV of its keys.  A wave
-// has a quarter of the one-wave form's serial MFMA / softmax work and the CU 4x the waves to
-// hide the staging latency.
-// keep (optional, [B, H] int32): key t of impression b takes part iff keep[b H + t] != 0 (the
 // mask_padding option's key mask, attention.py:76-78: masked keys get weight exactly 0; a row
 // with every key masked gives ctx = 0, as the torch oracle's eps-softmax)
 __device__ __forceinline__ bool key_kept(const int* __restrict__ keep, int b, int H, int t) {
   return keep == nullptr || keep[(size_t)b * H + t] != 0;
 }
 
-// SR = 65 (default, 33,008 B of LDS, four blocks per CU) or SR = 64 (FEDREC_UA_VARIANT=4: 64-row
-// operand stages -- rows 64.. are never read -- 32,768 B, five blocks per CU, all 1,280
-// (impression, head) blocks of B = 64 in one wave of the chip): measured neutral (fwd 20.5 vs
-// 20.0 us, steady step 0.5652 / 0.5862 vs 0.5663 / 0.5660 ms, profiles/r3_ab_segsum_ua.txt)
+// SR = 65: 33,008 B of LDS, four blocks per CU (64-row stages, five blocks per CU, measured
+// neutral: profiles/r3_ab_segsum_ua.txt)
 template <int SR>
 __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   float* __restrict__ ctx, float* __restrict__ stats,
@@ -685,9 +290,9 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
   }
 }
 
-// Backward LDS: 55,616 B with PLDB = 68 and 65-row stages (default, two blocks per CU); with
-// PLDB = 66 and 64-row stages (FEDREC_UA_VARIANT=4) 54,272 B, three blocks per CU, at the cost
-// of 2-way conflicts on the row-major P / dS reads: measured neutral (34.4 vs 34.2 us)
+// Backward LDS: 55,616 B with PLDB = 68 and 65-row stages (two blocks per CU); PLDB = 66 with
+// 64-row stages (three blocks per CU, 2-way conflicts on the row-major P / dS reads) measured
+// neutral (34.4 vs 34.2 us)
 template <int SR, int PLDB>
 __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   const float* __restrict__ stats,
@@ -826,7 +431,6 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   }
 }
 
-int g_ua_variant = 3;  // 3: four-wave MFMA (default), 4: the same with smaller LDS stages, 2: one-wave MFMA, 1: VALU ILP forward, 0: first VALU forward
 
 // ---------------------------------------------------------------------------------------
 // Long histories (H > 64): the reference pads but never truncates (dataset.py:84, quirk Q6;
@@ -1011,10 +615,7 @@ __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __r
 
 }  // namespace
 
-extern "C" void fr_user_attn_set_variant(int v) { g_ua_variant = v; }
-
-// keep: optional [B, H] int32 key mask (mask_padding); the default four-wave and the long
-// kernels take it, the diagnostic variants do not (a masked call always runs one of those two)
+// keep: optional [B, H] int32 key mask (mask_padding)
 extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk,
                                 const int* keep, hipStream_t s) {
   if (dk != DK || H > MAXL || H < 1) return 1;
@@ -1022,23 +623,8 @@ extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int 
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH, keep);
-  else if (g_ua_variant == 4)
-    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<64>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
-  else if (keep != nullptr || g_ua_variant == 3)
-    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<65>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
-  else if (g_ua_variant >= 10) {  // diagnostic partial forwards (timing only): 10 staging, 11 + S/softmax
-    if (g_ua_variant == 10) hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 1>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
-    else hipLaunchKernelGGL((user_attn_fwd_mfma_kernel<4, 2>), dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
-  } else if (g_ua_variant == 2) {
-    const int nt = (H + 15) / 16;
-    if (nt == 1) hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<1>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
-    else if (nt == 2) hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<2>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
-    else if (nt == 3) hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<3>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
-    else hipLaunchKernelGGL(user_attn_fwd_mfma_kernel<4>, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, H, NH);
-  } else if (g_ua_variant == 1)
-    hipLaunchKernelGGL(user_attn_fwd_ilp_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
   else
-    hipLaunchKernelGGL(user_attn_fwd_kernel, dim3((pairs + 1) / 2), dim3(128), 0, s, qkv, ctx, stats, B, H, NH);
+    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<65>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
   return 0;
 }
 
@@ -1049,22 +635,8 @@ extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const floa
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH, keep);
-  else if (g_ua_variant == 4)
-    hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<64, 66>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH,
-                       keep);
-  else if (keep != nullptr || g_ua_variant == 3)
+  else
     hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<65, 68>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH,
                        keep);
-  else if (g_ua_variant == 2) {
-    const int nt = (H + 15) / 16;
-#define UA_BWD(N) \
-  hipLaunchKernelGGL(user_attn_bwd_mfma_kernel<N>, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, H, NH)
-    if (nt == 1) UA_BWD(1);
-    else if (nt == 2) UA_BWD(2);
-    else if (nt == 3) UA_BWD(3);
-    else UA_BWD(4);
-#undef UA_BWD
-  } else
-    hipLaunchKernelGGL(user_attn_bwd_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH);
   return 0;
 }

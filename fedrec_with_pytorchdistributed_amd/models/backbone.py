@@ -192,8 +192,7 @@ class Backbone(nn.Module):
         # W^T), refreshed in the same step by one transposing launch (multi_cast_t) instead of
         # a `.t().contiguous()` copy per weight in every backward
         self._cast_plan_t = None
-        if (not self.cfg.frozen and dev.type == "cuda" and dtype == torch.bfloat16
-                and os.environ.get("FEDREC_WT_CACHE", "1") != "0"):
+        if not self.cfg.frozen and dev.type == "cuda" and dtype == torch.bfloat16:
             srct, dstt = [], []
             for blk, L in zip(self.transformer.layer, pack["layers"]):
                 a = blk.attention
@@ -278,43 +277,15 @@ class Backbone(nn.Module):
         in title order, so the output is identical in layout (and, up to fp32 summation
         order, in value) to the unpacked path.
 
-        ``FEDREC_BACKBONE_STREAMS=2``: the titles are split in two halves that run on two
-        HIP streams, interleaved layer by layer, so one half's LayerNorm / attention and the
-        tail of its persistent GEMMs can overlap the other half's kernels."""
-        ns = int(os.environ.get("FEDREC_BACKBONE_STREAMS", "1"))
-        n = tokens.shape[0]
-        if ns < 2 or n < 64:
-            out = [None]
-            for _ in self._packed_stages(tokens, mask, P, out, 0):
-                pass
-            return out[0]
-        main = torch.cuda.current_stream(tokens.device)
-        if getattr(self, "_streams", None) is None or len(self._streams) != ns:
-            self._streams = [torch.cuda.Stream(tokens.device) for _ in range(ns)]
-        bounds = [round(i * n / ns) for i in range(ns + 1)]
-        gens, outs = [], []
-        for i, st in enumerate(self._streams):
-            st.wait_stream(main)
-            with torch.cuda.stream(st):
-                gens.append(self._packed_stages(tokens[bounds[i]:bounds[i + 1]], mask[bounds[i]:bounds[i + 1]], P,
-                                                holder=outs, slot=i))
-        outs.extend([None] * ns)
-        live = list(range(ns))
-        while live:
-            for i in list(live):
-                with torch.cuda.stream(self._streams[i]):
-                    try:
-                        next(gens[i])
-                    except StopIteration:
-                        live.remove(i)
-        for st in self._streams:
-            main.wait_stream(st)
-        for t, st in zip(outs, self._streams):
-            t.record_stream(main)
-        return torch.cat(outs, 0)
+        (Splitting the titles over two streams interleaved layer by layer measured no gain:
+        profiles/r1/bench_r1_backbone_streams_ab.jsonl.)"""
+        out = [None]
+        for _ in self._packed_stages(tokens, mask, P, out, 0):
+            pass
+        return out[0]
 
     def _packed_stages(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict, holder: list, slot: int):
-        """Generator: one ``yield`` per transformer layer (lets two halves interleave)."""
+        """Generator: one ``yield`` per transformer layer."""
         c = self.cfg
         rowmap, src, kv_start, kv_len, qstart, n_kv = ops.title_plan(mask)
         x = ops.embed_ln_rows(tokens, src, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps)
@@ -371,34 +342,19 @@ class Backbone(nn.Module):
                                e.LayerNorm.weight, e.LayerNorm.bias, c.ln_eps, P["word"], P["pos"])
         if emb is not None:
             x = OF.DropoutFn.apply(x, *emb)
-        blocks = os.environ.get("FEDREC_TRAIN_BLOCKS", "1") != "0"
-        if not blocks and dropout:
-            raise ValueError("FEDREC_TRAIN_BLOCKS=0 (per-op A/B path) has no dropout; use the block path")
         for blk, L, (sa, sf) in zip(self.transformer.layer, P["layers"], sites):
             a = blk.attention
-            if blocks:  # fused block Functions (default)
-                # box: each LN backward hands its dx column sums (the bias grad of the block
-                # half feeding it) to that block's backward, which runs next
-                fuse = os.environ.get("FEDREC_LN_COLSUM", "1") != "0"
-                box1, box2 = ({}, {}) if fuse else (None, None)
-                h = OF.AttnBlockFn.apply(x, a.q_lin.weight, a.k_lin.weight, a.v_lin.weight, a.q_lin.bias,
-                                         a.k_lin.bias, a.v_lin.bias, a.out_lin.weight, a.out_lin.bias,
-                                         mask.contiguous(), c.n_heads, L["wqkv"], L["bqkv"], L["wo"], box1, sa,
-                                         (L.get("wqkv_t"), L.get("wo_t")))
-                x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps, box1)
-                h = OF.MLPBlockFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, blk.ffn.lin2.weight,
-                                        blk.ffn.lin2.bias, L["w1"], L["w2"], box2, sf, (L.get("w1_t"), L.get("w2_t")))
-                x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps, box2)
-                continue
-            wqkv = torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight], 0)
-            bqkv = torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias], 0)
-            qkv = OF.LinearTFn.apply(x, wqkv, bqkv, None, L["wqkv"])
-            ctx = OF.TitleAttentionFn.apply(qkv, mask.contiguous(), c.n_heads)
-            h = OF.LinearTFn.apply(ctx, a.out_lin.weight, a.out_lin.bias, x, L["wo"])
-            x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps)
-            f = OF.LinearGeluTFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, L["w1"])
-            h = OF.LinearTFn.apply(f, blk.ffn.lin2.weight, blk.ffn.lin2.bias, x, L["w2"])
-            x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps)
+            # fused block Functions; box: each LN backward hands its dx column sums (the bias grad
+            # of the block half feeding it) to that block's backward, which runs next
+            box1, box2 = {}, {}
+            h = OF.AttnBlockFn.apply(x, a.q_lin.weight, a.k_lin.weight, a.v_lin.weight, a.q_lin.bias,
+                                     a.k_lin.bias, a.v_lin.bias, a.out_lin.weight, a.out_lin.bias,
+                                     mask.contiguous(), c.n_heads, L["wqkv"], L["bqkv"], L["wo"], box1, sa,
+                                     (L.get("wqkv_t"), L.get("wo_t")))
+            x = OF.LayerNormFn.apply(h, blk.sa_layer_norm.weight, blk.sa_layer_norm.bias, c.ln_eps, box1)
+            h = OF.MLPBlockFn.apply(x, blk.ffn.lin1.weight, blk.ffn.lin1.bias, blk.ffn.lin2.weight,
+                                    blk.ffn.lin2.bias, L["w1"], L["w2"], box2, sf, (L.get("w1_t"), L.get("w2_t")))
+            x = OF.LayerNormFn.apply(h, blk.output_layer_norm.weight, blk.output_layer_norm.bias, c.ln_eps, box2)
         return x
 
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:

@@ -17,37 +17,16 @@ from .. import ops
 from .reference import _f
 
 
-_WGRAD_TILES = int(__import__("os").environ.get("FEDREC_WGRAD_TILES", "512"))  # split-K target (lib A/B)
-_WGRAD_IMPL = __import__("os").environ.get("FEDREC_WGRAD", "ours")  # ours | lib (A/B runs)
-
-
-def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 32) -> torch.Tensor:
+def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """``dy^T x`` in fp32 for ``dy [M, N]``, ``x [M, K]`` with a long reduction dim M.
 
     On the device with bf16 operands: our TN MFMA kernel (``csrc/gemm_wgrad.hip``: M-major
     tiles staged as they sit in HBM, fragments by LDS transpose reads, split-K over M with a
-    fixed-order partial sum).  ``FEDREC_WGRAD=lib`` keeps the round-1 library form for A/B
-    runs: a split-K batched library GEMM over free row-chunk views, then an fp32 sum."""
+    fixed-order partial sum)."""
     if not (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
         return _f(dy).t() @ _f(x)
-    if _WGRAD_IMPL != "lib":
-        return ops.native.require_for(dy).wgrad(dy.reshape(-1, dy.shape[-1]).contiguous(),
-                                                x.reshape(-1, x.shape[-1]).contiguous())
-    M = dy.shape[0]
-    tiles = -(-dy.shape[1] // 256) * -(-x.shape[1] // 256)
-    splits = min(splits, max(1, -(-_WGRAD_TILES // tiles)))
-    S = max(1, min(splits, M // 2048))
-    if S == 1:
-        return torch.mm(dy.t(), x, out_dtype=torch.float32)
-    c = M // S
-    M0 = S * c
-    out = torch.bmm(dy[:M0].view(S, c, -1).transpose(1, 2), x[:M0].view(S, c, -1), out_dtype=torch.float32).sum(0)
-    if M0 < M:
-        out += torch.mm(dy[M0:].t(), x[M0:], out_dtype=torch.float32)
-    return out
-
-
-_DGRAD_IMPL = __import__("os").environ.get("FEDREC_DGRAD", "ours")  # ours | lib (A/B runs)
+    return ops.native.require_for(dy).wgrad(dy.reshape(-1, dy.shape[-1]).contiguous(),
+                                            x.reshape(-1, x.shape[-1]).contiguous())
 
 
 def dgrad(dy: torch.Tensor, wlow: torch.Tensor, residual: Optional[torch.Tensor] = None,
@@ -56,10 +35,9 @@ def dgrad(dy: torch.Tensor, wlow: torch.Tensor, residual: Optional[torch.Tensor]
 
     On the device our NT MFMA GEMM runs it on ``wlow^T`` (a 1-5 MB per-step transpose of the
     bf16 weight; the GEMM streams ~100 MB of ``dy``), with the residual gradient added in the
-    epilogue (beta = 1) -- no library GEMM in the training step.  ``FEDREC_DGRAD=lib`` keeps
-    the library ``mm`` / ``addmm_`` for A/B runs.  ``wt``: ``wlow^T`` already materialised (the
+    epilogue (beta = 1) -- no library GEMM in the training step.  ``wt``: ``wlow^T`` already materialised (the
     unfrozen backbone's pack keeps transposed copies, refreshed once per optimizer step)."""
-    if (dy.is_cuda and dy.dtype == torch.bfloat16 and _DGRAD_IMPL != "lib" and wlow.shape[1] % 128 == 0
+    if (dy.is_cuda and dy.dtype == torch.bfloat16 and wlow.shape[1] % 128 == 0
             and wlow.shape[0] % 64 == 0):
         return ops.linear(dy, wt if wt is not None else wlow.t().contiguous(), None, residual=residual)
     if residual is not None:
@@ -282,48 +260,6 @@ def news_gather(table, inv, perm, seg_ptr, clip: float = 0.0, noise_std: float =
 # parameters through their bf16 compute copies; backward kernels for attention / LayerNorm /
 # GELU, our NT GEMM for dX (``dgrad``) and our TN GEMM for dW (``wgrad``).
 # ---------------------------------------------------------------------------------------
-class LinearTFn(torch.autograd.Function):
-    """``y = x @ wlow^T + b (+ residual)`` with ``wlow`` = bf16 copy of the fp32 ``w``."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, residual, wlow):
-        ctx.save_for_backward(x, wlow)
-        ctx.has_res = residual is not None
-        return ops.linear(x, wlow, b, residual=residual)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, wlow = ctx.saved_tensors
-        dy = dy.contiguous()
-        dx = dgrad(dy, wlow) if ctx.needs_input_grad[0] else None
-        dw = wgrad(dy, x)
-        db = bgrad(dy)
-        return dx, dw, db, (dy if ctx.has_res else None), None
-
-
-class LinearGeluTFn(torch.autograd.Function):
-    """``h = GELU(x @ wlow^T + b)`` (training FFN1).  One GEMM pass stores both ``h`` and the
-    pre-activation ``z`` the backward needs (dual-store epilogue), instead of GEMM -> z ->
-    a separate GELU pass reading z back."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, wlow):
-        h, z = ops.native.require_for(x).linear_gelu_dual(x.contiguous(), wlow, b)
-        ctx.save_for_backward(x, wlow, z)
-        return h
-
-    @staticmethod
-    def backward(ctx, dh):
-        x, wlow, z = ctx.saved_tensors
-        dz = ops.native.require_for(z).gelu(z, dh.contiguous())
-        dx = dgrad(dz, wlow) if ctx.needs_input_grad[0] else None
-        return dx, wgrad(dz, x), bgrad(dz), None
-
-
-_DZ_MODE = __import__("os").environ.get("FEDREC_DZ_MODE", "gemm")  # gemm | stream (A/B runs)
-_QKV_BIAS_SHORTCUT = __import__("os").environ.get("FEDREC_QKV_BIAS_SHORTCUT", "1") != "0"
-
-
 class DropoutFn(torch.autograd.Function):
     """Train-mode dropout with the counter-based mask (``ops.dropout_add``): the backward
     regenerates Z from (seed, offset) instead of storing it."""
@@ -372,7 +308,7 @@ class AttnBlockFn(torch.autograd.Function):
         dc = dgrad(dh, wo_low, wt=wo_t)
         dqkv = ops.title_attention_bwd(qkv, dc, mask, ctx.heads, ctx.drop)
         dwqkv = wgrad(dqkv, x)
-        if _QKV_BIAS_SHORTCUT and dqkv.is_cuda and ctx.drop is None:
+        if dqkv.is_cuda and ctx.drop is None:
             # column sums of dQ | dK | dV without reading dK and dV: every softmax row sums to
             # one, so sum_s dV_s = sum_t dctx_t = dbo Wo; and sum_s dS_ts = 0 for every query
             # (shift invariance), so the key-bias gradient is identically zero.  (Not with
@@ -381,7 +317,7 @@ class AttnBlockFn(torch.autograd.Function):
             dbqkv = torch.cat([ops.native.require_for(dqkv).colsum(dqkv[:, :Dm]),
                                torch.zeros(Dm, device=dqkv.device, dtype=torch.float32),
                                (dbo.float().unsqueeze(0) @ wo.float()).squeeze(0)])
-        elif _QKV_BIAS_SHORTCUT and dqkv.is_cuda:
+        elif dqkv.is_cuda:
             # with attention dropout the key-bias gradient is still exactly zero (the dropout
             # acts after the softmax: sum_s dS_ts = D_t - D_t sum_s P_ts = 0), but the dropped
             # P~ rows no longer sum to one, so dV needs its own column sums
@@ -435,36 +371,16 @@ class MLPBlockFn(torch.autograd.Function):
         else:
             dh = dres
         dw2, db2 = wgrad(dh, f), (db2 if db2 is not None else bgrad(dh))
-        if _DZ_MODE == "gemm":
-            # (dh W2) * GELU'(z) and its column sums from our GEMM's epilogue in one pass (the
-            # aux-input epilogue makes that GEMM 650 us vs 480 for the forward FFN1 shape; the
-            # "stream" form measured the same step time: bench_r1_cfg5_dzmode_ab.jsonl)
-            w2t = ctx.wts[1] if ctx.wts[1] is not None else w2_low.t().contiguous()
-            dz, db1 = lib.linear_gelu_bwd(dh, w2t, z)
-            if db1 is None:
-                db1 = bgrad(dz)
-        else:
-            # library dF GEMM, then one streaming pass: dz = dF * GELU'(z) and its column sums
-            # (the FFN1 bias gradient), deterministic partials
-            dz, db1 = lib.gelu_bwd_colsum(dgrad(dh, w2_low, wt=ctx.wts[1]), z)
+        # (dh W2) * GELU'(z) and its column sums from our GEMM's epilogue in one pass (the
+        # aux-input epilogue makes that GEMM 650 us vs 480 for the forward FFN1 shape; a separate
+        # streaming pass measured the same step time: bench_r1_cfg5_dzmode_ab.jsonl)
+        w2t = ctx.wts[1] if ctx.wts[1] is not None else w2_low.t().contiguous()
+        dz, db1 = lib.linear_gelu_bwd(dh, w2t, z)
+        if db1 is None:
+            db1 = bgrad(dz)
         dw1 = wgrad(dz, x)
         dx = dgrad(dz, w1_low, residual=dres, wt=ctx.wts[0])
         return dx, dw1, db1, dw2, db2, None, None, None, None, None
-
-
-class GeluFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, z):
-        ctx.save_for_backward(z)
-        return ops.native.require_for(z).gelu(z, None)
-
-    @staticmethod
-    def backward(ctx, dh):
-        (z,) = ctx.saved_tensors
-        return ops.native.require_for(z).gelu(z, dh.contiguous())
-
-
-_LN_DROP_FUSE = __import__("os").environ.get("FEDREC_LN_DROP_FUSE", "1") != "0"  # A/B switch
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -484,7 +400,7 @@ class LayerNormFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         lib = ops.native.require_for(x)
         drop = ctx.box.pop("drop", None) if ctx.box is not None else None
-        if drop is not None and _LN_DROP_FUSE:
+        if drop is not None:
             p, seed, off = drop
             dx, ctx.box["dxz"], dw, db, ctx.box["colsum"] = lib.layer_norm_bwd_drop(
                 x.contiguous(), w, dy.contiguous(), float(ctx.eps), float(p), int(seed), int(off))
@@ -493,19 +409,6 @@ class LayerNormFn(torch.autograd.Function):
         else:
             dx, dw, db = lib.layer_norm_bwd(x, w, dy.contiguous(), float(ctx.eps))
         return dx, dw, db, None, None
-
-
-class TitleAttentionFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, qkv, mask, heads: int):
-        ctx.save_for_backward(qkv, mask)
-        ctx.heads = heads
-        return ops.title_attention(qkv, mask, heads)
-
-    @staticmethod
-    def backward(ctx, dout):
-        qkv, mask = ctx.saved_tensors
-        return ops.native.require_for(qkv).title_attention_bwd(qkv, dout.contiguous(), mask, ctx.heads), None, None
 
 
 class EmbedLNFn(torch.autograd.Function):
@@ -547,7 +450,6 @@ class EmbedLNFn(torch.autograd.Function):
 # pool -> sigmoid-CE, and a hand-written backward.  Every GEMM is csrc/small_gemm.hip, every
 # bias gradient the deterministic colsum, the per-news reduction (+ LDP) the segment sum.
 # ---------------------------------------------------------------------------------------
-_USER_BWD_SPLIT = __import__("os").environ.get("FEDREC_USER_BWD_SPLIT", "0") == "1"  # A/B switch
 
 
 def _user_weight_bufs(wts, dev):
@@ -583,71 +485,6 @@ def step_weight_casts(text_encoder, user_encoder, bump=None):
     if bump is not None and not launched:
         bump.add_(1)
     return w1b, (wb, bqkv)
-
-
-class side_grads:
-    """Weight gradients that only the optimizer reads, off the backward's critical path.
-
-    Inside ``with side_grads(dev):`` (the engine wraps ``loss.backward()`` in it) the user
-    encoder's and the text FC's weight-gradient GEMMs launch on a side stream that forks from
-    the backward after their inputs exist; the input-gradient chain (segment sum -> text FC
-    dgrad -> head pool backward -> head weight gradient) runs on meanwhile.  Autograd takes the
-    returned gradient tensors without a kernel (``FlatParams.begin_backward`` leaves ``.grad``
-    None), and the block's exit joins the side stream into the current one before anything
-    (``FlatParams.end_backward``'s gather) reads them.  Works under HIP-graph capture: the fork
-    and join are event edges of the captured graph.
-
-    OFF by default (``FEDREC_SIDE_GRADS=1`` enables it): measured SLOWER at config 2 -- steady
-    step 0.644-0.670 ms against 0.578 inline (``profiles/r3_ab_side_score_wgrad.txt``).  The
-    side-stream GEMM blocks take CU slots while the head weight gradient launches; that kernel
-    is sized to one block per CU, so a block that cannot be placed starts a wave late and the
-    whole grid waits for it."""
-
-    enabled = __import__("os").environ.get("FEDREC_SIDE_GRADS", "0") == "1"
-    _active = None  # (device, side stream, [events]) while a block is open
-    _streams: dict = {}
-
-    def __init__(self, dev):
-        self.dev = torch.device(dev)
-
-    def __enter__(self):
-        if side_grads.enabled and self.dev.type == "cuda" and side_grads._active is None:
-            st = side_grads._streams.get(self.dev)
-            if st is None:
-                st = side_grads._streams[self.dev] = torch.cuda.Stream(self.dev)
-            side_grads._active = (self.dev, st, [])
-            self.owner = True
-        else:
-            self.owner = False
-        return self
-
-    def __exit__(self, *exc):
-        if self.owner:
-            dev, _, evs = side_grads._active
-            side_grads._active = None
-            main = torch.cuda.current_stream(dev)
-            for ev in evs:
-                main.wait_event(ev)
-        return False
-
-    @staticmethod
-    def launch(fn, inputs):
-        """Run ``fn()`` (kernel launches + allocations of its outputs) on the side stream when
-        a block is open, else inline.  ``inputs``: tensors of the current stream ``fn`` reads."""
-        act = side_grads._active
-        if act is None:
-            return fn()
-        dev, side, evs = act
-        main = torch.cuda.current_stream(dev)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            out = fn()
-        for t in inputs:
-            t.record_stream(side)
-        ev = torch.cuda.Event()
-        ev.record(side)
-        evs.append(ev)
-        return out
 
 
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None):
@@ -704,35 +541,17 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     # weight gradients: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM; X' bf16) and dW1 =
     # dpre^T ctx (fp32 operands: the mixed-dtype kernel); the bias gradients (column sums of
     # dQ|dK|dV and dpre, fp32) come out of the same launch (asum).  The input gradient has no
-    # dependence on them: all three share ONE launch (FEDREC_USER_BWD_SPLIT=1: two launches)
-    # (under side_grads the weight gradients run on the side stream beside the input gradient)
-    def wgrads():
-        gqkv = torch.empty(D3, D, device=dev)
-        gw1 = torch.empty(Qd, D, device=dev)
-        gbqkv = torch.empty(D3, device=dev)
-        gb1 = torch.empty(Qd, device=dev)
-        wg = (ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
-              ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
-        return gqkv, gw1, gbqkv, gb1, wg
-
-    if side_grads._active is not None:
-        gqkv, gw1, gbqkv, gb1 = side_grads.launch(lambda: _run_wgrads(wgrads), (dqkv, xd, dpre2, c3))
-        ops.small_gemm(dgrad, dev_off=dev_off)
-    elif _USER_BWD_SPLIT:
-        gqkv, gw1, gbqkv, gb1, wg = wgrads()
-        ops.small_gemm(dgrad, dev_off=dev_off)
-        ops.small_gemm(*wg)
-    else:
-        gqkv, gw1, gbqkv, gb1, wg = wgrads()
-        ops.small_gemm(dgrad, *wg, dev_off=dev_off)
+    # dependence on them: all three share ONE launch (weight gradients on a side stream beside
+    # the input gradient measured slower: profiles/r3_ab_side_score_wgrad.txt)
+    gqkv = torch.empty(D3, D, device=dev)
+    gw1 = torch.empty(Qd, D, device=dev)
+    gbqkv = torch.empty(D3, device=dev)
+    gb1 = torch.empty(Qd, device=dev)
+    wg = (ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
+          ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
+    ops.small_gemm(dgrad, *wg, dev_off=dev_off)
     return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1, gb1, dw2.view(1, -1),
             db2.view(1))
-
-
-def _run_wgrads(make):
-    gqkv, gw1, gbqkv, gb1, wg = make()
-    ops.small_gemm(*wg)
-    return gqkv, gw1, gbqkv, gb1
 
 
 class UserStepFn(torch.autograd.Function):
@@ -868,21 +687,9 @@ class HeadFCFn(torch.autograd.Function):
         dy = dy.contiguous().float()
         dx = torch.empty(n, K, device=x.device, dtype=torch.float32)
 
-        def wgrad():
-            dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
-            db = torch.empty(N, device=x.device, dtype=torch.float32)
-            return dw, db, ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db)
-
-        dgrad = ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1)
-        if side_grads._active is not None:  # the weight gradient beside the head's backward
-            def run():
-                dw, db, g = wgrad()
-                ops.small_gemm(g)
-                return dw, db
-            dw, db = side_grads.launch(run, (dy, x))
-            ops.small_gemm(dgrad)
-            return dx, dw, db
+        dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+        db = torch.empty(N, device=x.device, dtype=torch.float32)
         # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one launch
-        dw, db, g = wgrad()
-        ops.small_gemm(dgrad, g)
+        ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1),
+                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db))
         return dx, dw, db

@@ -48,28 +48,7 @@ def lib():
                 _error = RuntimeError(f"failed to load {SO_PATH}: {e}")
                 raise _error
             _loaded = True
-            _apply_env_knobs(torch.ops.fedrec)
     return torch.ops.fedrec
-
-
-def _apply_env_knobs(ops) -> None:
-    """Kernel-variant switches for A/B runs (unset = the measured defaults)."""
-    if os.environ.get("FEDREC_LN_WIDE"):
-        ops.ln_set_wide(int(os.environ["FEDREC_LN_WIDE"]))
-    if os.environ.get("FEDREC_SCORE_VARIANT"):
-        ops.score_set_variant(int(os.environ["FEDREC_SCORE_VARIANT"]))
-    if os.environ.get("FEDREC_UA_VARIANT"):
-        ops.user_attn_set_variant(int(os.environ["FEDREC_UA_VARIANT"]))
-    if os.environ.get("FEDREC_TA_WAVES"):
-        ops.title_attn_set_waves(int(os.environ["FEDREC_TA_WAVES"]))
-    if os.environ.get("FEDREC_TAB_VARIANT"):
-        ops.title_attn_bwd_set_variant(int(os.environ["FEDREC_TAB_VARIANT"]))
-    if os.environ.get("FEDREC_TAB_DROP_SPLIT"):
-        ops.title_attn_bwd_set_variant(10 + int(os.environ["FEDREC_TAB_DROP_SPLIT"]))
-    if os.environ.get("FEDREC_SEGSUM_VARIANT"):
-        ops.segsum_set_variant(int(os.environ["FEDREC_SEGSUM_VARIANT"]))
-    if os.environ.get("FEDREC_GEMM_VARIANT"):
-        ops.gemm_set_variant(int(os.environ["FEDREC_GEMM_VARIANT"]))
 
 
 def require_for(t: torch.Tensor):

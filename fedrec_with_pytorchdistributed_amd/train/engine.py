@@ -63,13 +63,7 @@ class Prepared(NamedTuple):
 # process group's watchdog thread keeps polling its work events (a multi-client run captures
 # its step graphs while collectives of other steps are tracked); "global" would turn those polls
 # into capture failures
-_CAPTURE_MODE = os.environ.get("FEDREC_CAPTURE_MODE", "thread_local")
-
-
-_SKIP_PADDED = os.environ.get("FEDREC_SKIP_PADDED", "1") != "0"  # A/B switch
-_STEP_CASTS = os.environ.get("FEDREC_STEP_CASTS", "1") != "0"  # A/B switch (0: a cast launch per consumer)
-# the step counter advanced inside that cast launch (0: a torch add_ after the backward)
-_STEP_BUMP = os.environ.get("FEDREC_STEP_BUMP", "1") != "0"
+_CAPTURE_MODE = "thread_local"
 
 
 class _StepGraph:
@@ -90,7 +84,7 @@ class _StepGraph:
         self._none = torch.empty(0, dtype=torch.int32, device=dev)
         self.load(pre, int(uniq.numel()))
         static = Prepared(self.cand, self.his, (self.uniq, self.inv, self.perm, self.ptr), None, True,
-                          self.nreal if _SKIP_PADDED else None)
+                          self.nreal)
         main = torch.cuda.current_stream(dev)
         eng.sync_params()
         # two graphs: (1) the parameter-free gather of the unique titles' cached hidden states,
@@ -101,9 +95,8 @@ class _StepGraph:
         self.hid_graph = None
         # (on with a gradient all-reduce only: at one client there is only Adam (7 us) to hide,
         # and the extra replay measured neutral: 66.86k vs 67.15k imp/s, r2_bench_batch6.jsonl)
-        split = os.environ.get("FEDREC_SPLIT_GRAPH", "auto")
         # (the fused text head reads the cache by index inside its GEMM: nothing to gather ahead)
-        if not eng.fused_head and (split == "on" or (split == "auto" and eng.grad_allreduce is not None)):
+        if not eng.fused_head and eng.grad_allreduce is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 for _ in range(2):
@@ -178,8 +171,7 @@ class LocalEngine:
         # the step being a device counter so HIP-graph replays draw fresh masks
         ue = model.user_encoder
         self.fused_user = (device.type == "cuda"
-                           and ue.multihead_attention.n_heads * ue.multihead_attention.d_k == cfg.news_dim
-                           and os.environ.get("FEDREC_FUSED_USER", "1") != "0")
+                           and ue.multihead_attention.n_heads * ue.multihead_attention.d_k == cfg.news_dim)
         self.user_drop_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 2
         ue.drop_seed = self.user_drop_seed  # the module-level device path (user_encoder_device) too
         # LDP noise: its own Philox key per client (disjoint from the dropout keys above)
@@ -193,7 +185,7 @@ class LocalEngine:
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
         self.replay_chunk = 4096 if self.hcache is not None else 1024
         # HIP graphs of the per-step forward + backward (see _graph_step)
-        sg = os.environ.get("FEDREC_STEP_GRAPH", cfg.step_graph)
+        sg = cfg.step_graph
         self.step_graphs = device.type == "cuda" and self.hcache is not None and (
             sg == "on" or (sg == "auto" and (self.fused_user or not cfg.dp.enabled)))
         self._graphs: Dict[tuple, "_StepGraph"] = {}
@@ -201,7 +193,7 @@ class LocalEngine:
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
         # trainable parameters; everything that does calls sync_params() first
-        ov = os.environ.get("FEDREC_OVERLAP_OPTIMIZER", cfg.overlap_optimizer)  # env: A/B runs
+        ov = cfg.overlap_optimizer
         self.overlap = device.type == "cuda" and cfg.backbone.frozen and (
             ov == "on" or (ov == "auto" and grad_allreduce is not None))
         self._side = torch.cuda.Stream(device) if self.overlap else None
@@ -209,8 +201,7 @@ class LocalEngine:
         # batch lookahead (GPU): the next batch is sampled and de-duplicated on its own stream
         # while the current step runs, so the dedup's host read of the unique count (the
         # backbone's M) no longer drains the GPU at every step start
-        lookahead = device.type == "cuda" and os.environ.get("FEDREC_LOOKAHEAD", "1") != "0"
-        self._prep = torch.cuda.Stream(device) if lookahead else None
+        self._prep = torch.cuda.Stream(device) if device.type == "cuda" else None
 
     def set_reducer(self, reducer) -> None:
         """Use a backward-overlapped bucket reducer (``parallel.reducer``) for the gradients."""
@@ -420,10 +411,10 @@ class LocalEngine:
         if self.fused_user:
             dd = self._dedup(cand, his, pre)
             casts = None
-            if self.fused_head and _STEP_CASTS:  # every compute copy of the step's weights in one cast launch,
+            if self.fused_head:  # every compute copy of the step's weights in one cast launch,
                 self.sync_params()  # which also advances the dropout / noise step counter this step reads
                 casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder,
-                                             bump=self._rng_step if _STEP_BUMP else None)
+                                             bump=self._rng_step)
             with obs.range("news_encode"):
                 v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
                                       w1b=casts[0] if casts is not None else None)
@@ -431,9 +422,9 @@ class LocalEngine:
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
                                           pre is not None and pre.padded, True, his,
                                           casts=casts[1] if casts is not None else None)
-            with obs.range("backward"), OF.side_grads(self.device):
+            with obs.range("backward"):
                 loss.backward(self._seed_one())
-            if casts is None or not _STEP_BUMP:
+            if casts is None:
                 self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
             self.flat.end_backward()
             return loss.detach()

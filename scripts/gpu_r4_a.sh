@@ -9,3 +9,4 @@ check t_ipc 400 $T tests/test_ipc_allreduce_gpu.py
 check t_multi 900 $T tests/test_multirank_gpu.py -k "secure or ipc"
 run bench 300 python -u bench.py
 run bench_c5 300 python -u bench.py --config 5 --steps 6 --warmup 3
+bash scripts/gpu_r4_hosttrace.sh

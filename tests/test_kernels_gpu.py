@@ -155,28 +155,21 @@ def test_additive_pool(dev, dtype, D, Q):
     assert abs(float(db2_n) - float(rdb2)) < 1e-3 * (abs(float(rdb2)) + 1)
 
 
-@pytest.mark.parametrize("variant", [3, 4, 2, 1, 0])
 @pytest.mark.parametrize("H", [1, 17, 33, 50, 64, 65, 76, 200])
-def test_user_attention(dev, H, variant):
-    """variants 3 (default, four waves per head) / 2 (one wave) = the fp32 matrix-core kernels
-    (v_mfma_f32_16x16x4_f32) for H <= 64,
-    held to 1e-5 against the fp32 oracle forward AND backward; H > 64 runs the long-history
-    kernels (online softmax over 64-row LDS chunks): the reference never truncates histories
-    (Q6; its shipped shard has H = 76).  variant 1 = the VALU ILP kernels, 0 = the first forms."""
-    from fedrec_with_pytorchdistributed_amd.ops import native
+def test_user_attention(dev, H):
+    """H <= 64: the fp32 matrix-core kernels (v_mfma_f32_16x16x4_f32, four waves per head), held
+    to 1e-5 against the fp32 oracle forward AND backward; H > 64 runs the long-history kernels
+    (online softmax over 64-row LDS chunks): the reference never truncates histories (Q6; its
+    shipped shard has H = 76)."""
     B, NH, DK = 7, 20, 20
     qkv = torch.randn(B, H, 3 * NH * DK, device=dev)
-    native.lib().user_attn_set_variant(variant)
-    try:  # the variant is process-global: restored even when an assert fails
-        ctx, stats = ops.user_attention_fwd(qkv, NH, DK)
-        d = torch.randn_like(ctx)
-        dq = ops.user_attention_bwd(qkv, stats, d, NH, DK)
-    finally:
-        native.lib().user_attn_set_variant(3)
+    ctx, stats = ops.user_attention_fwd(qkv, NH, DK)
+    d = torch.randn_like(ctx)
+    dq = ops.user_attention_bwd(qkv, stats, d, NH, DK)
     c_ref, A = ref.user_attention_fwd(qkv, NH, DK)
     assert rel_err(ctx, c_ref) < 1e-5
     dq_ref = ref.user_attention_bwd(qkv, A, d, NH, DK)
-    assert rel_err(dq, dq_ref) < (1e-5 if variant >= 2 and H <= 64 else 1e-4)
+    assert rel_err(dq, dq_ref) < (1e-5 if H <= 64 else 1e-4)
 
 
 @pytest.mark.parametrize("T", [76, 300])

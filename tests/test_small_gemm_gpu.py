@@ -1,9 +1,6 @@
 """csrc/small_gemm.hip against an fp32 torch emulation (operands rounded to bf16 as the kernel
 does): every layout, the fused row gather / Philox dropout prologues, the dropout epilogue,
 bias / tanh / accumulate, and several GEMMs per launch; plus the deterministic fp32 colsum."""
-import os
-import subprocess
-import sys
 
 import pytest
 import torch
@@ -75,21 +72,6 @@ def test_grouped_launch_and_odd_shapes(dev, tile):
     ops.small_gemm(*gs, tile=tile)
     for g, w in zip(gs, wants):
         assert _rel(g.C, w) < 2e-3
-
-
-@pytest.mark.parametrize("knob", ["FEDREC_SG_TR", "FEDREC_SG_DB"])
-def test_scalar_transposed_store_form(knob):
-    """The non-default staging forms (knobs read once per process), the mode-1 cases again in a
-    child process: FEDREC_SG_TR=0 -- the stored-transposed operands of the 64x64 tiles through the
-    k-contiguous image instead of the TRI image; FEDREC_SG_DB=0 -- one LDS buffer and two
-    barriers per k-step instead of two buffers and one"""
-    env = dict(os.environ, **{knob: "0"})
-    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__, "-k",
-           "(tn_wgrad or nn_dgrad or grouped) and not scalar_transposed"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300,
-                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout
 
 
 def test_colsum_f32_deterministic(dev):
