@@ -51,6 +51,73 @@ extern "C" int fr_adam_flat(float* p, const float* g, float* m, float* v, void* 
 }
 
 // ---------------------------------------------------------------------------------------
+// The same step with the step count on the device, for a HIP graph that captures the whole
+// training step (forward, backward, Adam) when no gradient all-reduce sits between the
+// backward and the optimizer (one client): every block reads t = step + 1 and forms the bias
+// corrections itself (in double, then rounded as the host path rounds them); block 0 also
+// copies this step's loss into slot (t - 1) % ring of a loss ring (no per-step clone launch);
+// the block that takes the last ticket advances the step and re-arms the ticket.  Every block
+// reads the step before it takes its ticket, so the last one writes after all reads.
+namespace {
+__global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, const float4* __restrict__ g,
+                                                       float4* __restrict__ m, float4* __restrict__ v,
+                                                       bf16x4* __restrict__ plow, long n4, float lr, float b1, float b2,
+                                                       float eps, float gs, long long* __restrict__ step,
+                                                       unsigned* __restrict__ ticket, const float* __restrict__ loss,
+                                                       float* __restrict__ ring, int ring_n) {
+  __shared__ long long t_s;
+  if (threadIdx.x == 0) t_s = __hip_atomic_load(step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  const long long t = t_s;
+  const float bc1 = (float)(1.0 - pow((double)b1, (double)t));
+  const float bc2 = (float)(1.0 - pow((double)b2, (double)t));
+  const float step_size = lr / bc1, inv_sqrt_bc2 = 1.0f / sqrtf(bc2);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    float* pa = (float*)&pp;
+    float* ga = (float*)&gg;
+    float* ma = (float*)&mm;
+    float* va = (float*)&vv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x = ga[k] * gs;
+      ma[k] = b1 * ma[k] + (1.f - b1) * x;
+      va[k] = b2 * va[k] + (1.f - b2) * x * x;
+      const float denom = sqrtf(va[k]) * inv_sqrt_bc2 + eps;
+      pa[k] -= step_size * ma[k] / denom;
+    }
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+    if (plow) plow[i] = bf16x4{f2bf(pa[0]), f2bf(pa[1]), f2bf(pa[2]), f2bf(pa[3])};
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ring != nullptr) ring[(t - 1) % ring_n] = loss[0];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned k = atomicAdd(ticket, 1u);
+    if (k == gridDim.x - 1) {
+      __hip_atomic_store(step, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int fr_adam_dev(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1,
+                           float b2, float eps, float grad_scale, long long* step, unsigned* ticket, const float* loss,
+                           float* ring, int ring_n, hipStream_t s) {
+  if (n % 4 != 0 || (ring != nullptr && (loss == nullptr || ring_n < 1))) return 1;
+  const long n4 = n / 4;
+  long blocks = (n4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (float4*)p, (const float4*)g, (float4*)m,
+                     (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, grad_scale, step, ticket, loss, ring, ring_n);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
 // Compute-weight refresh of the unfrozen backbone after an optimizer step: up to MCAST_SEG
 // fp32 master tensors -> their bf16 (or fp32) compute copies in ONE launch, 8 elements per
 // thread (two float4 loads, one 16-byte bf16 store).  Segment i may write into a slice of a

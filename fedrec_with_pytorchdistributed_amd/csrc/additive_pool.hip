@@ -416,7 +416,8 @@ __global__ __launch_bounds__(256) void upool_bwd_kernel(const float* __restrict_
                                                         const float* __restrict__ alpha, const float* __restrict__ w2,
                                                         const float* __restrict__ g, float* __restrict__ dx,
                                                         float* __restrict__ dpre, float* __restrict__ dw2,
-                                                        float* __restrict__ db2, int T, int D, int Q) {
+                                                        float* __restrict__ db2, int T, int D, int Q,
+                                                        float* __restrict__ da8) {
   __shared__ float da_s[UT], al_s[UT];
   __shared__ float part[UT][4];
   __shared__ float4 red[4][64];
@@ -446,8 +447,16 @@ __global__ __launch_bounds__(256) void upool_bwd_kernel(const float* __restrict_
     const float s = wave_sum(al * dal);
     const float da = al * (dal - s);
     if (lane < T) da_s[lane] = da;
-    const float sd = wave_sum(da);
-    if (lane == 0) db2[(size_t)n * US + y] = y == 0 ? sd : 0.f;
+    if (da8 != nullptr) {  // da as column 0 of [n T, 8] (the weight-gradient launch reduces it)
+      if (y == 0 && lane < T) {
+        float4* o = (float4*)(da8 + ((size_t)n * T + lane) * 8);
+        o[0] = make_float4(da, 0.f, 0.f, 0.f);
+        o[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
+      const float sd = wave_sum(da);
+      if (lane == 0) db2[(size_t)n * US + y] = y == 0 ? sd : 0.f;
+    }
   }
   __syncthreads();
   const int rspan = (T + US - 1) / US, r0 = y * rspan, r1 = min(T, r0 + rspan);
@@ -465,15 +474,17 @@ __global__ __launch_bounds__(256) void upool_bwd_kernel(const float* __restrict_
                         da * w.w * (1.f - v.w * v.w));
       }
     }
-    red[tg][qc] = acc;
-    __syncthreads();
-    if (tid < Q4) {
-      float4 s = red[0][tid];
+    if (dw2 != nullptr) {  // block-uniform
+      red[tg][qc] = acc;
+      __syncthreads();
+      if (tid < Q4) {
+        float4 s = red[0][tid];
 #pragma unroll
-      for (int j = 1; j < 4; ++j) {
-        s.x += red[j][tid].x; s.y += red[j][tid].y; s.z += red[j][tid].z; s.w += red[j][tid].w;
+        for (int j = 1; j < 4; ++j) {
+          s.x += red[j][tid].x; s.y += red[j][tid].y; s.z += red[j][tid].z; s.w += red[j][tid].w;
+        }
+        ((float4*)(dw2 + ((size_t)n * US + y) * Q))[tid] = s;
       }
-      ((float4*)(dw2 + ((size_t)n * US + y) * Q))[tid] = s;
     }
   }
   if (dx != nullptr) {  // dx_direct rows [r0, r1) = alpha_t g
@@ -535,7 +546,7 @@ extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* a
                          (uintptr_t)(dx ? dx : g);
     if (al & 15) return 3;  // 16-byte rows (fresh tensors and 256-B aligned parameter views)
     hipLaunchKernelGGL(upool_bwd_kernel, dim3(n, US), dim3(256), 0, s, (const float*)x, (const float*)e, alpha, w2, g, dx,
-                       (float*)dpre, dw2, db2, T, D, Q);
+                       (float*)dpre, dw2, db2, T, D, Q, nullptr);
     return -1;
   }
   if (R != n) return 1;
@@ -551,4 +562,20 @@ extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* a
     hipLaunchKernelGGL(pool_bwd_kernel<float>, dim3(n), dim3(256), 0, s, (const float*)x, (const float*)e, alpha, w2,
                        g, dx, (float*)dpre, dw2, db2, T, D, Q, R);
   return -1;
+}
+
+// The user pool's backward without the dw2 / db2 partial rows: da goes out as column 0 of
+// da8 [n T, 8] (zeros elsewhere) and the caller adds dw2 = e^T da, db2 = sum da to its weight-
+// gradient launch (a small-GEMM desc with M = 8; db2 from that desc's column sums) -- two
+// deterministic colsum launches fewer per step.  fp32 short-sequence shapes only (upool_ok).
+extern "C" int fr_upool_bwd_da(const float* x, const float* e, const float* alpha, const float* w2, const float* g,
+                               float* dx, float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s) {
+  if (!upool_ok(T, D, Q, 0)) return 1;
+  const uintptr_t al = (uintptr_t)x | (uintptr_t)e | (uintptr_t)w2 | (uintptr_t)g | (uintptr_t)dpre |
+                       (uintptr_t)(dx ? dx : g) | (uintptr_t)da8;
+  if (al & 15) return 3;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(upool_bwd_kernel, dim3(n, US), dim3(256), 0, s, x, e, alpha, w2, g, dx, dpre, nullptr, nullptr, T,
+                     D, Q, da8);
+  return 0;
 }

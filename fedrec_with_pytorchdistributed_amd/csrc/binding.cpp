@@ -64,13 +64,16 @@ int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, i
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
                      int dk, const int* keep, hipStream_t s);
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
-                int C, int D, int sigm, const int* ci, hipStream_t s);
+                int C, int D, int sigm, const int* ci, float* loss_total, hipStream_t s);
 int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U, int D,
                         int R, float* scratch, hipStream_t s, int zero_empty);
 int fr_segsum_chunks(int R);
 void fr_segsum_set_variant(int v);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
                 unsigned long long offset, hipStream_t s, const unsigned long long* dev_off);
+int fr_adam_dev(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
+                float eps, float grad_scale, long long* step, unsigned* ticket, const float* loss, float* ring,
+                int ring_n, hipStream_t s);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
@@ -115,6 +118,8 @@ int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, con
 int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
                   hipStream_t s);
 long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part, hipStream_t s);
+int fr_upool_bwd_da(const float* x, const float* e, const float* alpha, const float* w2, const float* g, float* dx,
+                    float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
 int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
@@ -594,6 +599,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad(const at::
   return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
 }
 
+// user pool backward with da out (column 0 of [n T, 8]) instead of dw2 / db2 (fr_upool_bwd_da)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> upool_bwd_da(const at::Tensor& x, const at::Tensor& e,
+                                                            const at::Tensor& alpha, const at::Tensor& w2,
+                                                            const at::Tensor& g) {
+  for (auto* t : {&x, &e, &alpha, &w2, &g}) {
+    check_dev(*t, "upool_bwd_da input");
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "fedrec::upool_bwd_da: contiguous fp32");
+  }
+  const c10::DeviceGuard dg(x.device());
+  const int64_t n = x.size(0), T = x.size(1), D = x.size(2), Q = e.size(2);
+  TORCH_CHECK(e.size(0) == n && e.size(1) == T && alpha.numel() == n * T && w2.numel() == Q && g.numel() == n * D,
+              "fedrec::upool_bwd_da: shapes");
+  auto dx = at::empty({n, T, D}, x.options());
+  auto dpre = at::empty({n, T, Q}, x.options());
+  auto da8 = at::empty({n * T, 8}, x.options());
+  check_rc(fr_upool_bwd_da(x.data_ptr<float>(), e.data_ptr<float>(), alpha.data_ptr<float>(), w2.data_ptr<float>(),
+                           g.data_ptr<float>(), dx.data_ptr<float>(), dpre.data_ptr<float>(), da8.data_ptr<float>(),
+                           (int)n, (int)T, (int)D, (int)Q, cur_stream()),
+           "upool_bwd_da");
+  return {dx, dpre, da8};
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(
     const at::Tensor& x, const at::Tensor& e, const at::Tensor& alpha, const at::Tensor& w2, const at::Tensor& g,
     bool want_dx) {
@@ -703,11 +730,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Te
     dcand = at::empty({B, C, D}, cand.options());
   }
   auto duser = at::empty_like(user);
-  check_rc(fr_score_ce(cand.data_ptr<float>(), user.data_ptr<float>(), lossb.data_ptr<float>(), scores.data_ptr<float>(),
-                       dcand.data_ptr<float>(), duser.data_ptr<float>(), (int)B, (int)C, (int)D, (int)act,
-                       gathered ? ci->data_ptr<int>() : nullptr, cur_stream()),
-           "score_ce");
-  {
+  // the batch loss is summed inside the launch by its last block (impression order); the
+  // wave-per-impression form leaves it to a deterministic colsum
+  const int rc = fr_score_ce(cand.data_ptr<float>(), user.data_ptr<float>(), lossb.data_ptr<float>(),
+                             scores.data_ptr<float>(), dcand.data_ptr<float>(), duser.data_ptr<float>(), (int)B, (int)C,
+                             (int)D, (int)act, gathered ? ci->data_ptr<int>() : nullptr, loss.data_ptr<float>(),
+                             cur_stream());
+  if (rc == 2) {
+    check_rc(fr_score_ce(cand.data_ptr<float>(), user.data_ptr<float>(), lossb.data_ptr<float>(),
+                         scores.data_ptr<float>(), dcand.data_ptr<float>(), duser.data_ptr<float>(), (int)B, (int)C,
+                         (int)D, (int)act, gathered ? ci->data_ptr<int>() : nullptr, nullptr, cur_stream()),
+             "score_ce");
     const float* xs[1] = {lossb.data_ptr<float>()};
     float* os[1] = {loss.data_ptr<float>()};
     const int ints[4] = {(int)B, 1, 1, 0};
@@ -715,6 +748,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> score_ce(const at::Te
     auto part = at::empty({std::max<long>(need, 1)}, cand.options());
     TORCH_CHECK(need >= 0 && fr_colsum_f32(xs, os, ints, 1, part.data_ptr<float>(), cur_stream()) == 0,
                 "fedrec::score_ce: loss sum");
+  } else {
+    check_rc(rc, "score_ce");
   }
   // with dcand_out the gradient lives in the caller's buffer (no output aliasing an input)
   if (dcand_out.has_value() && dcand_out->defined()) return {loss, scores, at::empty({0}, cand.options()), duser};
@@ -762,6 +797,38 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
                                cur_stream(), zero_empty ? 1 : 0),
            "segment_sum_rows");
   return out;
+}
+
+// Adam with the step count (and the per-step loss ring) on the device: capturable in a graph
+void adam_dev(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at::Tensor step, at::Tensor ticket,
+              const at::Tensor& loss, at::Tensor ring, double lr, double b1, double b2, double eps, double grad_scale) {
+  for (auto* t : {&p, &m, &v}) check_dev(*t, "adam_dev buffer");
+  check_dev(g, "g");
+  check_dev(step, "step");
+  check_dev(ticket, "ticket");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
+                  v.scalar_type() == at::kFloat && p.numel() == g.numel() && p.numel() == m.numel() &&
+                  p.numel() == v.numel() && p.is_contiguous() && g.is_contiguous() && m.is_contiguous() &&
+                  v.is_contiguous(),
+              "fedrec::adam_dev: fp32 flat buffers of one size");
+  TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() == 1 && ticket.scalar_type() == at::kInt &&
+                  ticket.numel() == 1,
+              "fedrec::adam_dev: int64 step [1], int32 ticket [1]");
+  const bool has_ring = ring.numel() > 0;
+  if (has_ring) {
+    check_dev(loss, "loss");
+    check_dev(ring, "ring");
+    TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.numel() == 1 && ring.scalar_type() == at::kFloat &&
+                    ring.is_contiguous(),
+                "fedrec::adam_dev: fp32 loss [1] and ring");
+  }
+  const c10::DeviceGuard dg(p.device());
+  check_rc(fr_adam_dev(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), nullptr,
+                       (long)p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale,
+                       (long long*)step.data_ptr<int64_t>(), (unsigned*)ticket.data_ptr<int>(),
+                       has_ring ? loss.data_ptr<float>() : nullptr, has_ring ? ring.data_ptr<float>() : nullptr,
+                       (int)ring.numel(), cur_stream()),
+           "adam_dev");
 }
 
 void adam_flat(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, const c10::optional<at::Tensor>& plow,
@@ -1461,11 +1528,13 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor? nreal=None) -> (Tensor, Tensor)");
   m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep=None) -> (Tensor, Tensor)");
+  m.def("upool_bwd_da(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g) -> (Tensor, Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None) -> (Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act, Tensor? ci=None, Tensor(a!)? dcand_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
+  m.def("adam_dev(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!) step, Tensor(e!) ticket, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale) -> ()");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset, bool valid=False) -> (Tensor, Tensor)");
@@ -1514,11 +1583,13 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("head_wgrad", &head_wgrad);
   m.impl("additive_pool_fwd", &additive_pool_fwd);
   m.impl("additive_pool_bwd", &additive_pool_bwd);
+  m.impl("upool_bwd_da", &upool_bwd_da);
   m.impl("user_attention_fwd", &user_attention_fwd);
   m.impl("user_attention_bwd", &user_attention_bwd);
   m.impl("score_ce", &score_ce);
   m.impl("segment_sum_rows", &segment_sum_rows);
   m.impl("adam_flat", &adam_flat);
+  m.impl("adam_dev", &adam_dev);
   m.impl("dedup", &dedup);
   m.impl("sample_batch", &sample_batch);
   m.impl("secagg_mask", &secagg_mask);

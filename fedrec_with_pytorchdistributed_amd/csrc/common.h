@@ -119,3 +119,31 @@ static __device__ __forceinline__ void store_pair16_if(bf16* __restrict__ crow, 
   typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
   if (store) *GLOBAL_PTR(u32x4_t, crow + (fq & 1) * 16 + (fq >> 1) * 8) = u32x4_t{a.x, a.y, b.x, b.y};
 }
+
+// ---------------------------------------------------------------------------------------
+// Last-arriver hand-off between the workgroups of one launch (split-K seams, partial-row
+// sums): MI355X_MICROARCH.md "Valid forms" table row 1 -- the producers' data stored
+// write-through (st_sc1: relaxed agent-scope stores = global_store sc1), every storing wave's
+// vmcnt(0), a workgroup barrier, ONE agent-scope ticket add per workgroup; the workgroup whose
+// add returns total - 1 reads the data with ld_sc1 (relaxed agent-scope loads) and re-arms the
+// ticket for the next launch.  No release / acquire fences (a release writes back the XCD's
+// whole L2: a fenced last-block column sum measured 131 vs 69 us per step).
+static __device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static __device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every thread of the workgroup; true in the workgroup that arrived last
+static __device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned total) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = k == total - 1;
+    if (s_last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_last != 0;
+}

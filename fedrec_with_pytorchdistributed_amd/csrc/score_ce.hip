@@ -68,7 +68,9 @@ __global__ __launch_bounds__(64 * MAXC) void score_ce_block_kernel(const float* 
                                                                    float* __restrict__ scores,
                                                                    float* __restrict__ dcand,
                                                                    float* __restrict__ duser, int B, int C, int D,
-                                                                   int sigm, const int* __restrict__ ci) {
+                                                                   int sigm, const int* __restrict__ ci,
+                                                                   float* __restrict__ loss_total,
+                                                                   unsigned* __restrict__ cnt) {
   __shared__ float zs[MAXC], dzs[MAXC];
   __shared__ const float* rowp[MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -93,7 +95,11 @@ __global__ __launch_bounds__(64 * MAXC) void score_ce_block_kernel(const float* 
       scores[(size_t)b * C + lane] = sc;
       const float ds = (__expf(sc - mx) / se - (lane == 0 ? 1.f : 0.f)) / (float)B;
       dzs[lane] = sigm ? ds * sc * (1.f - sc) : ds;
-      if (lane == 0) loss[b] = (mx + __logf(se) - sc) / (float)B;  // per-impression share
+      if (lane == 0) {  // per-impression share
+        const float lb = (mx + __logf(se) - sc) / (float)B;
+        if (cnt != nullptr) st_sc1(loss + b, lb);
+        else loss[b] = lb;
+      }
     }
   }
   __syncthreads();
@@ -104,7 +110,15 @@ __global__ __launch_bounds__(64 * MAXC) void score_ce_block_kernel(const float* 
     for (int c = 0; c < C; ++c) du += dzs[c] * rowp[c][d];
     duser[(size_t)b * D + d] = du;
   }
+  // the batch loss: the last impression block to finish sums the shares in impression order
+  if (cnt != nullptr && last_arrival(cnt, gridDim.x) && threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < B; ++i) t += ld_sc1(loss + i);
+    loss_total[0] = t;
+  }
 }
+
+__device__ unsigned g_score_cnt[1];  // zero-initialised; every launch leaves it zero
 
 int g_score_variant = 1;  // 1: block per impression (default), 0: wave per impression
 
@@ -112,13 +126,24 @@ int g_score_variant = 1;  // 1: block per impression (default), 0: wave per impr
 
 extern "C" void fr_score_set_variant(int v) { g_score_variant = v; }
 
+// loss_total (optional): the batch loss sum_b loss[b], formed by the last block (block form only;
+// else the caller sums loss[])
 extern "C" int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand,
-                           float* duser, int B, int C, int D, int sigm, const int* ci, hipStream_t s) {
+                           float* duser, int B, int C, int D, int sigm, const int* ci, float* loss_total,
+                           hipStream_t s) {
   if (C > MAXC) return 1;
   if (B == 0) return 0;
-  if (ci != nullptr || (g_score_variant == 1 && C <= MAXC))
+  if (ci != nullptr || (g_score_variant == 1 && C <= MAXC)) {
+    static unsigned* cnt = [] {
+      unsigned* p = nullptr;
+      (void)hipGetSymbolAddress((void**)&p, HIP_SYMBOL(g_score_cnt));
+      return p;
+    }();
     hipLaunchKernelGGL(score_ce_block_kernel, dim3(B), dim3(64 * C), 0, s, cand, user, loss, scores, dcand, duser, B,
-                       C, D, sigm, ci);
+                       C, D, sigm, ci, loss_total, loss_total != nullptr ? cnt : nullptr);
+    return 0;
+  }
+  if (loss_total != nullptr) return 2;
   else
     hipLaunchKernelGGL(score_ce_kernel, dim3((B + 3) / 4), dim3(256), 0, s, cand, user, loss, scores, dcand, duser, B,
                        C, D, sigm);

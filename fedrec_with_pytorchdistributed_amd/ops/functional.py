@@ -528,8 +528,16 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     BH, D3 = B * H, 3 * D
     Qd = wb.shape[0] - D3
     dev = c3.device
-    # additive pool backward: dx_direct = alpha du, dpre = da w2 (1 - e^2), dw2, db2
-    dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
+    # additive pool backward: dx_direct = alpha du, dpre = da w2 (1 - e^2); dw2 = e^T da and
+    # db2 = sum da join the weight-gradient launch below (da as column 0 of [BH, 8]: a small-GEMM
+    # desc with M = 8, db2 from its column sums) -- no partial rows, no colsum launches
+    lib = ops.native.require_for(c3)
+    da8 = None
+    if H <= 64 and c3.dtype == torch.float32 and e3.dtype == torch.float32:
+        dctx, dpre, da8 = lib.upool_bwd_da(c3.contiguous(), e3.contiguous(), alpha.contiguous(),
+                                           w2.reshape(-1).float().contiguous(), du.float().contiguous())
+    else:
+        dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
     dpre2 = dpre.view(BH, Qd)
     ops.small_gemm(ops.Gemm(dpre2, wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
     dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep).view(BH, D3)
@@ -549,6 +557,11 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     gb1 = torch.empty(Qd, device=dev)
     wg = (ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
           ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
+    if da8 is not None:
+        dw2 = torch.empty(8, Qd, device=dev)
+        db2 = torch.empty(8, device=dev)
+        wg += (ops.Gemm(da8, e3.reshape(BH, Qd), dw2, 8, Qd, BH, 8, Qd, Qd, a_mode=1, b_mode=1, asum=db2),)
+        dw2, db2 = dw2[0], db2[:1]
     ops.small_gemm(dgrad, *wg, dev_off=dev_off)
     return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1, gb1, dw2.view(1, -1),
             db2.view(1))

@@ -69,8 +69,9 @@ _CAPTURE_MODE = "thread_local"
 class _StepGraph:
     """Static inputs + the captured graph of one (batch shape, unique-title bucket)."""
 
-    def __init__(self, eng: "LocalEngine", pre: Prepared, ucap: int):
+    def __init__(self, eng: "LocalEngine", pre: Prepared, ucap: int, with_adam: bool = False):
         uniq, inv, perm, ptr = pre.dedup
+        self.adam = with_adam
         dev = eng.device
         self.cand = torch.zeros_like(pre.cand)
         self.his = torch.zeros_like(pre.his)
@@ -119,6 +120,8 @@ class _StepGraph:
             # when eager steps of other engines run between the captures
             with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
                 self.loss = eng.forward_backward(self.cand, self.his, static)
+                if with_adam:  # no all-reduce between backward and optimizer: the step in one graph
+                    eng._adam_dev(self.loss)
         finally:
             eng._pre_hid = None
 
@@ -448,17 +451,31 @@ class LocalEngine:
         # noise; the non-fused path's host offset would be frozen into the graph
         if self.step_graphs and pre.dedup is not None and not (self.cfg.dp.enabled and self.sigma
                                                                and not self.fused_user):
-            loss = self._graph_step(pre)
+            with_adam = self.grad_allreduce is None and self.reducer is None
+            loss = self._graph_step(pre, with_adam)
             if loss is not None:
-                self.optimizer_step(overlap=True)
+                if not with_adam:
+                    self.optimizer_step(overlap=True)
                 return loss
         return self.train_step(pre.cand, pre.his, pre)
+
+    # ---- Adam inside the step graph (no gradient all-reduce: one client) ----------------
+    LOSS_RING = 4096  # per-step losses live here until read (train_epoch folds every LOSS_RING / 2)
+
+    def _adam_dev(self, loss: torch.Tensor) -> None:
+        """Adam with its step count on the device (csrc/adam.hip adam_dev_kernel), capturable:
+        also copies the step's loss into the loss ring.  The host mirror ``flat.step`` is
+        advanced by the caller per replay."""
+        c = self.cfg
+        native.require_for(loss).adam_dev(self.flat.flat, self.flat.grad, self.flat.m, self.flat.v, self._adam_step_dev,
+                                          self._adam_ticket, loss.reshape(1).float(), self._loss_ring, c.lr,
+                                          c.adam_beta1, c.adam_beta2, c.adam_eps, 1.0)
 
     # ---- HIP graph of the per-step forward + backward ------------------------------------
     GRAPH_BUCKET = 128  # unique titles are padded up to a multiple of this (padded rows: id 0)
     MAX_GRAPHS = 16
 
-    def _graph_step(self, pre: Prepared) -> Optional[torch.Tensor]:
+    def _graph_step(self, pre: Prepared, with_adam: bool = False) -> Optional[torch.Tensor]:
         """Forward + backward of one step by replaying a captured HIP graph.
 
         The step's only data-dependent shape is the number U of unique titles: it is padded to
@@ -467,8 +484,10 @@ class LocalEngine:
         occurrences) is 0, so the trainable gradient is the eager step's (up to fp32
         summation order in the split-K weight gradients).  One graph per (batch shape, bucket,
         cache build); the batch is copied into the graph's static inputs, then one replay
-        runs ~60 kernels with no host in between.  Returns None when a new graph is not
-        allowed (the caller runs the step eagerly)."""
+        runs ~60 kernels with no host in between.  ``with_adam`` (no gradient all-reduce): the
+        graph ends with the device-step Adam and the loss goes to the loss ring -- no eager
+        launch between two steps' graphs.  Returns None when a new graph is not allowed (the
+        caller runs the step eagerly)."""
         uniq, inv, perm, ptr = pre.dedup
         U = int(uniq.numel())
         ucap = -(-U // self.GRAPH_BUCKET) * self.GRAPH_BUCKET
@@ -477,7 +496,7 @@ class LocalEngine:
         # graph is filed under the build it captured
         self.sync_params()
         self.hcache.ensure()
-        key = (tuple(pre.cand.shape), tuple(pre.his.shape), int(inv.numel()), ucap, self.hcache.builds)
+        key = (tuple(pre.cand.shape), tuple(pre.his.shape), int(inv.numel()), ucap, with_adam, self.hcache.builds)
         g = self._graphs.get(key)
         main = torch.cuda.current_stream(self.device)
         if pre.ready is not None:
@@ -487,12 +506,25 @@ class LocalEngine:
                 return None
             if any(k[-1] != self.hcache.builds for k in self._graphs):  # a rebuilt cache: old graphs are stale
                 self._graphs = {k: v for k, v in self._graphs.items() if k[-1] == self.hcache.builds}
-            g = _StepGraph(self, pre, ucap)
+            if with_adam and getattr(self, "_adam_step_dev", None) is None:  # (outside any capture)
+                self._adam_step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+                self._adam_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+                self._loss_ring = torch.zeros(self.LOSS_RING, dtype=torch.float32, device=self.device)
+                self._adam_mirror = -1
+            g = _StepGraph(self, pre, ucap, with_adam)
             self._graphs[key] = g
         g.load(pre, U)
         if g.hid_graph is not None:
             g.hid_graph.replay()  # parameter-free: runs while the previous all-reduce + Adam finish
         self.sync_params()
+        if g.adam:
+            if self._adam_mirror != self.flat.step:  # an eager step / a resume moved the host count
+                self._adam_step_dev.fill_(self.flat.step)
+                self._adam_mirror = self.flat.step
+            g.graph.replay()
+            self.flat.step += 1
+            self._adam_mirror += 1
+            return self._loss_ring[(self.flat.step - 1) % self.LOSS_RING]
         g.graph.replay()
         return g.loss.clone()
 
@@ -629,7 +661,7 @@ class LocalEngine:
         runs after every step (parameter averaging every K steps)."""
         sched = self.cfg.resolved_local_update()
         t0 = time.perf_counter()
-        losses = []
+        losses, folded = [], []
         n = 0
         if sched == "per_epoch":
             self._begin_epoch_accumulate()
@@ -647,6 +679,9 @@ class LocalEngine:
             last = max_steps is not None and n + 1 >= max_steps
             nxt = None if last else self._next_prepared(it)
             losses.append(loss)
+            if len(losses) >= self.LOSS_RING // 2:  # fold before the loss ring wraps
+                folded.append(torch.stack(losses).float().sum())
+                losses = []
             n += 1
             if step_hook is not None:
                 self.sync_params()  # hooks (parameter averaging every K steps) read the parameters
@@ -662,8 +697,9 @@ class LocalEngine:
         dt = time.perf_counter() - t0
         self.check_data_plane()
         self.epoch += 1
-        mean_loss = float(torch.stack(losses).float().mean()) if losses else float("nan")
-        sum_loss = float(torch.stack(losses).float().sum()) if losses else float("nan")
+        parts = folded + ([torch.stack(losses).float().sum()] if losses else [])
+        sum_loss = float(torch.stack(parts).sum()) if parts else float("nan")
+        mean_loss = sum_loss / n if n else float("nan")
         imps = min(n * self.cfg.batch_size, len(self.shard.train))
         self.last_stats = {"training_loss": mean_loss, "training_loss_sum": sum_loss, "steps": n,
                            "impressions": imps, "epoch_s": dt, "impressions_per_s": imps / max(dt, 1e-9)}

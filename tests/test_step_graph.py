@@ -53,6 +53,21 @@ def test_graph_step_matches_eager(dev):
     p0, p1 = e0.model.flat.flat, e1.model.flat.flat
     rel = float((p1 - p0).norm() / p0.norm())
     assert rel < 1e-5, rel
+    # one client: Adam ran inside the replayed graphs with its step count on the device
+    assert any(k[-2] for k in e1._graphs), "the step graphs should carry the optimizer (no all-reduce)"
+    assert e1.model.flat.step == e0.model.flat.step == len(batches)
+    assert int(e1._adam_step_dev.item()) == e1.model.flat.step
+    # an eager step in between (e.g. a graph-cache miss) keeps the device count in step
+    cand, his = batches[0]
+    for e in (e0, e1):
+        e.train_step(*(t for t in e.prepare(lambda: (cand, his))[:2]))
+    p2 = e1.prepare(lambda: (cand, his))
+    q2 = e0.prepare(lambda: (cand, his))
+    assert abs(float(e0.train_prepared(q2)) - float(e1.train_prepared(p2))) < 1e-4
+    torch.cuda.synchronize()
+    assert int(e1._adam_step_dev.item()) == e1.model.flat.step == e0.model.flat.step
+    rel = float((e1.model.flat.flat - e0.model.flat.flat).norm() / e0.model.flat.flat.norm())
+    assert rel < 5e-5, rel  # two more Adam steps of bf16-rounding differences
     # the replayed graph wrote the gradient of the LAST step into the same flat buffer
     g0, g1 = e0.model.flat.grad, e1.model.flat.grad
     assert float((g1 - g0).norm()) <= 2e-2 * float(g0.norm()) + 1e-8
