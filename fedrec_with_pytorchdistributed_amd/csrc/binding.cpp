@@ -1310,7 +1310,8 @@ at::Tensor title_attention_packed(const at::Tensor& qkv, const at::Tensor& rowma
 }
 
 at::Tensor layer_norm_scatter(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps,
-                              const c10::optional<at::Tensor>& residual, const at::Tensor& dst) {
+                              const c10::optional<at::Tensor>& residual, const at::Tensor& dst,
+                              const c10::optional<at::Tensor>& out) {
   check_dev(x, "x");
   check_dev(dst, "dst");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "fedrec::layer_norm_scatter: bf16");
@@ -1326,7 +1327,16 @@ at::Tensor layer_norm_scatter(const at::Tensor& x, const at::Tensor& w, const at
                 "fedrec::layer_norm_scatter: residual must match x (bf16)");
     rp = residual->data_ptr();
   }
-  auto y = at::empty_like(x);
+  // out (optional): the destination rows in place (the hidden-state cache's chunk) -- no copy
+  at::Tensor y;
+  if (out.has_value() && out->defined()) {
+    check_dev(*out, "out");
+    TORCH_CHECK(out->scalar_type() == at::kBFloat16 && out->is_contiguous() && out->numel() == x.numel(),
+                "fedrec::layer_norm_scatter: out bf16 contiguous, x's size");
+    y = *out;
+  } else {
+    y = at::empty_like(x);
+  }
   check_rc(fr_layer_norm_scatter_bf16(x.data_ptr(), wf.data_ptr<float>(), bf.data_ptr<float>(), y.data_ptr(), (int)rows,
                                       (int)D, (float)eps, rp, dst.data_ptr<int>(), cur_stream()),
            "layer_norm_scatter");
@@ -1544,7 +1554,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_ln_rows(Tensor tokens, Tensor src, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("linear_split(Tensor x, Tensor w, Tensor? b, Tensor full_rows, int n_partial) -> Tensor");
   m.def("title_attention_packed(Tensor qkv, Tensor rowmap, Tensor kv_start, Tensor kv_len, Tensor qstart, int n_heads) -> Tensor");
-  m.def("layer_norm_scatter(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual, Tensor dst) -> Tensor");
+  m.def("layer_norm_scatter(Tensor x, Tensor w, Tensor b, float eps, Tensor? residual, Tensor dst, Tensor(a!)? out=None) -> Tensor");
   m.def("colsum(Tensor x) -> Tensor");
   m.def("linear_gelu_dual(Tensor x, Tensor w, Tensor b) -> (Tensor, Tensor)");
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");

@@ -225,16 +225,19 @@ class Backbone(nn.Module):
                                     for i in range(c.n_layers)]
 
     @torch.no_grad()
-    def forward(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype, dropout: bool = False) -> torch.Tensor:
+    def forward(self, tokens: torch.Tensor, mask: torch.Tensor, dtype: torch.dtype, dropout: bool = False,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``tokens, mask [n, T]`` -> last hidden state ``[n*T, D]`` in ``dtype`` (eval mode;
-        ``dropout`` = HF train-mode dropout, used by the reference-compat replay Q4)."""
+        ``dropout`` = HF train-mode dropout, used by the reference-compat replay Q4).  ``out``
+        (packed device path): the last LayerNorm writes straight into it (e.g. the hidden-state
+        cache's rows); other paths copy into it."""
         c = self.cfg
         P = self.compute_weights(dtype)
         if dropout:
-            return self._forward_dropout(tokens, mask, P)
+            return _into(self._forward_dropout(tokens, mask, P), out)
         if (tokens.is_cuda and dtype == torch.bfloat16 and c.dim % 256 == 0 and c.n_layers > 0
                 and tokens.shape[1] <= 64 and os.environ.get("FEDREC_TITLE_PACK", "1") != "0"):
-            return self._forward_packed(tokens, mask, P)
+            return self._forward_packed(tokens, mask, P, out)
         x = ops.embed_ln(tokens, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps, dtype)
         for L in P["layers"]:
             qkv = ops.linear(x, L["wqkv"], L["bqkv"], out_dtype=dtype)
@@ -246,7 +249,7 @@ class Backbone(nn.Module):
             f = ops.linear(x, L["w1"], L["b1"], act="gelu", out_dtype=dtype)
             h = ops.linear(f, L["w2"], L["b2"], out_dtype=dtype)
             x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, dtype, residual=x)
-        return x
+        return _into(x, out)
 
     def _forward_dropout(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict) -> torch.Tensor:
         """Train-mode forward without gradients (frozen backbone, Q4 replay): the unpacked
@@ -269,7 +272,8 @@ class Backbone(nn.Module):
                 x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, residual=x)
         return x
 
-    def _forward_packed(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict) -> torch.Tensor:
+    def _forward_packed(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """The same forward over the packed row order of ``ops.title_plan``: the rows read as
         keys/values (real tokens) come first, so the fused QKV GEMM skips the K and V columns
         of every padding row (~2/3 of MIND title rows) and the attention skips key tiles past
@@ -279,12 +283,13 @@ class Backbone(nn.Module):
 
         (Splitting the titles over two streams interleaved layer by layer measured no gain:
         profiles/r1/bench_r1_backbone_streams_ab.jsonl.)"""
-        out = [None]
-        for _ in self._packed_stages(tokens, mask, P, out, 0):
+        holder = [None]
+        for _ in self._packed_stages(tokens, mask, P, holder, 0, out):
             pass
-        return out[0]
+        return holder[0]
 
-    def _packed_stages(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict, holder: list, slot: int):
+    def _packed_stages(self, tokens: torch.Tensor, mask: torch.Tensor, P: Dict, holder: list, slot: int,
+                       out: Optional[torch.Tensor] = None):
         """Generator: one ``yield`` per transformer layer."""
         c = self.cfg
         rowmap, src, kv_start, kv_len, qstart, n_kv = ops.title_plan(mask)
@@ -298,7 +303,7 @@ class Backbone(nn.Module):
             f = ops.linear(x, L["w1"], L["b1"], act="gelu")
             h = ops.linear(f, L["w2"], L["b2"])
             if li == last:
-                x = ops.layer_norm_scatter(h, L["ln2_w"], L["ln2_b"], c.ln_eps, x, src)
+                x = ops.layer_norm_scatter(h, L["ln2_w"], L["ln2_b"], c.ln_eps, x, src, out)
             else:
                 x = ops.layer_norm(h, L["ln2_w"], L["ln2_b"], c.ln_eps, residual=x)
             yield li
@@ -360,6 +365,13 @@ class Backbone(nn.Module):
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
         """Keys as HF ``DistilBertModel`` names them (for parity tests)."""
         return {k: v for k, v in self.state_dict().items()}
+
+
+def _into(x: torch.Tensor, out: Optional[torch.Tensor]) -> torch.Tensor:
+    if out is None:
+        return x
+    out.view_as(x).copy_(x)
+    return out
 
 
 def param_names(c: BackboneConfig) -> List[str]:

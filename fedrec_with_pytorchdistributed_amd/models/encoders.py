@@ -109,14 +109,15 @@ class TextEncoder(nn.Module):
             return torch.bfloat16
         return torch.float32
 
-    def hidden(self, text: torch.Tensor, dropout: bool | None = None) -> torch.Tensor:
+    def hidden(self, text: torch.Tensor, dropout: bool | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
         """``text [n,2,T]`` -> last hidden state ``[n,T,D]``: no-grad inference for the frozen
         backbone (the reference, model.py:25-26); a differentiable forward when unfrozen.
 
         ``dropout``: HF train-mode dropout in the backbone.  None = on for the unfrozen
         backbone's training forward in train mode; the frozen backbone's news vectors are
         eval-mode as in ``gen_news_vecs`` (model.py:42) unless the caller asks for it (the
-        reference's train-mode replay, model.py:73 -- Q4)."""
+        reference's train-mode replay, model.py:73 -- Q4).  ``out`` (no-grad paths): the result
+        is written there (the packed device forward stores its last LayerNorm into it)."""
         n, _, T = text.shape
         bb = self.DistillBert
         train = not bb.cfg.frozen and torch.is_grad_enabled()
@@ -125,7 +126,7 @@ class TextEncoder(nn.Module):
         if train:
             h = bb.forward_train(text[:, 0, :].contiguous(), text[:, 1, :].contiguous(), self.compute_dtype, dropout)
         else:
-            h = bb(text[:, 0, :], text[:, 1, :], self.compute_dtype, dropout=dropout)
+            h = bb(text[:, 0, :], text[:, 1, :], self.compute_dtype, dropout=dropout, out=out)
         return h.view(n, T, -1)
 
     def fused_head_ok(self, title_len: int) -> bool:

@@ -127,9 +127,9 @@ def title_attention_packed(qkv, rowmap, kv_start, kv_len, qstart, n_heads: int):
     return native.require_for(qkv).title_attention_packed(qkv, rowmap, kv_start, kv_len, qstart, int(n_heads))
 
 
-def layer_norm_scatter(x, w, b, eps: float, residual, dst):
-    """``LN(x + residual)`` with row r stored at output row ``dst[r]``."""
-    return native.require_for(x).layer_norm_scatter(x, w, b, float(eps), residual, dst)
+def layer_norm_scatter(x, w, b, eps: float, residual, dst, out=None):
+    """``LN(x + residual)`` with row r stored at output row ``dst[r]`` (of ``out`` when given)."""
+    return native.require_for(x).layer_norm_scatter(x, w, b, float(eps), residual, dst, out)
 
 
 def additive_pool_fwd(x, e, w2, b2, keep=None) -> Tuple[torch.Tensor, torch.Tensor]:
