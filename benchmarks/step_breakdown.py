@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--marker", default="adam_kernel")
+    ap.add_argument("--marker", default="adam")  # adam_kernel (eager) or adam_dev_kernel (in the step graph)
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))

@@ -65,12 +65,19 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, c
                                                        float eps, float gs, long long* __restrict__ step,
                                                        unsigned* __restrict__ ticket, const float* __restrict__ loss,
                                                        float* __restrict__ ring, int ring_n) {
+  // the step count and the bias corrections once per block (double pow, as the host computes
+  // them for the eager kernel: a per-thread double pow made this launch 3x the eager one)
   __shared__ long long t_s;
-  if (threadIdx.x == 0) t_s = __hip_atomic_load(step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __shared__ float bc_s[2];
+  if (threadIdx.x == 0) {
+    const long long t0 = __hip_atomic_load(step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    t_s = t0;
+    bc_s[0] = (float)(1.0 - pow((double)b1, (double)t0));
+    bc_s[1] = (float)(1.0 - pow((double)b2, (double)t0));
+  }
   __syncthreads();
   const long long t = t_s;
-  const float bc1 = (float)(1.0 - pow((double)b1, (double)t));
-  const float bc2 = (float)(1.0 - pow((double)b2, (double)t));
+  const float bc1 = bc_s[0], bc2 = bc_s[1];
   const float step_size = lr / bc1, inv_sqrt_bc2 = 1.0f / sqrtf(bc2);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];

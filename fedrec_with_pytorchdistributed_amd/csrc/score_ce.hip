@@ -110,11 +110,15 @@ __global__ __launch_bounds__(64 * MAXC) void score_ce_block_kernel(const float* 
     for (int c = 0; c < C; ++c) du += dzs[c] * rowp[c][d];
     duser[(size_t)b * D + d] = du;
   }
-  // the batch loss: the last impression block to finish sums the shares in impression order
-  if (cnt != nullptr && last_arrival(cnt, gridDim.x) && threadIdx.x == 0) {
+  // the batch loss: the last impression block to finish sums the shares -- wave 0, every lane's
+  // loads in flight at once (a one-lane loop pays a memory round trip per impression), then a
+  // fixed-order shuffle tree (deterministic)
+  if (cnt != nullptr && last_arrival(cnt, gridDim.x) && threadIdx.x < 64) {
     float t = 0.f;
-    for (int i = 0; i < B; ++i) t += ld_sc1(loss + i);
-    loss_total[0] = t;
+    for (int i = threadIdx.x; i < B; i += 64) t += ld_sc1(loss + i);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (threadIdx.x == 0) loss_total[0] = t;
   }
 }
 

@@ -63,7 +63,6 @@ struct GemmDesc {
   int a_bf16, b_bf16;
   int red_base;   // first block of this desc's split-K reduction
   int ared_base;  // first block of its asum partial reduction (split asum descs)
-  unsigned* cnt;  // split-K in the GEMM launch: arrival tickets, one per output tile (else null)
   unsigned long long seed, offset;  // offset += *dev_off when dev_off is set (graph replays)
 };
 
@@ -337,87 +336,6 @@ __device__ __forceinline__ int tile_of_block(const GemmBatch& batch, int& gi) {
   return tg - batch.d[gi].tile_base;
 }
 
-// ---- split-K seam inside the GEMM launch ---------------------------------------------------
-// The splits of an output tile hand their fp32 partials to the LAST of them to finish, which
-// sums them in split order (the separate reduce kernel's order: bitwise-identical results) and
-// applies the epilogue.  Hand-off as MI355X_MICROARCH.md "Valid forms" table row 1: partials
-// stored write-through (sc1: relaxed agent-scope stores), every storing wave's vmcnt(0), a
-// workgroup barrier, ONE agent-scope ticket add per block; the block whose add returns
-// splits - 1 loads the partials with sc1 loads (relaxed agent-scope atomics) and re-arms the
-// ticket.  No release / acquire fences: each release writes back the XCD's L2 (a fenced
-// "last block" column sum measured 131 vs 69 us per step).
-__device__ unsigned g_sk_cnt[8192];  // zero-initialised; every launch leaves it zero
-constexpr int SK_CNT = 8192;
-
-__device__ __forceinline__ bool sk_last_arrival(unsigned* cnt, int splits) {
-  return last_arrival(cnt, (unsigned)splits);
-}
-
-// the epilogue of 4 consecutive columns (m, n..n+3) of a split desc from their summed partials v
-__device__ __forceinline__ void sk_finish4(const GemmDesc& g, unsigned long long off, int m, int n, float (&v)[4]) {
-  float sc[4] = {1.f, 1.f, 1.f, 1.f};
-  if (g.drop_on == 3) {  // as the single-pass epilogue: elements (m, n..n+3) of the dropped input
-    const uint4 x = Philox::gen(g.seed, off, ((unsigned long long)m * g.drop_ld + n) >> 2);
-    const float inv_keep = 1.0f / (1.0f - g.pdrop);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sc[r] = drop_scale(u4_get(x, r), g.pdrop, inv_keep);
-  }
-  float* c = g.C + (size_t)m * g.ldc + n;
-  const bool vec = ((uintptr_t)c & 15) == 0;
-  float cv[4] = {0.f, 0.f, 0.f, 0.f};
-  if (g.accumulate) {
-    if (vec) {
-      const float4 t = *(const float4*)c;
-      cv[0] = t.x; cv[1] = t.y; cv[2] = t.z; cv[3] = t.w;
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cv[r] = c[r];
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float x = g.alpha * v[r] + (g.bias ? g.bias[n + r] : 0.f);
-    if (g.act == 1) x = tanhf(x);
-    x *= sc[r];
-    v[r] = g.accumulate ? cv[r] + x : x;
-  }
-  if (vec)
-    *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
-  else
-#pragma unroll
-    for (int r = 0; r < 4; ++r) c[r] = v[r];
-}
-
-// the last split of output tile (m0, n0): sum every split's partials (split order) + epilogue,
-// and the asum rows of a column-0 tile
-template <int TM, int TN>
-__device__ void sk_reduce_tile(const GemmDesc& g, unsigned long long off, int m0, int n0, bool do_as) {
-  const size_t MN = (size_t)g.M * g.N;
-  for (int q = threadIdx.x; q < TM * TN / 4; q += 256) {
-    const int m = m0 + q / (TN / 4), n = n0 + (q % (TN / 4)) * 4;
-    if (m >= g.M || n >= g.N) continue;  // N % 4 == 0 for split descs: a 4-column group is whole
-    const float* p = g.P + (size_t)m * g.N + n;
-    float v[4] = {ld_sc1(p), ld_sc1(p + 1), ld_sc1(p + 2), ld_sc1(p + 3)};
-    for (int sp = 1; sp < g.splits; ++sp) {
-      const float* ps = p + sp * MN;
-      v[0] += ld_sc1(ps);
-      v[1] += ld_sc1(ps + 1);
-      v[2] += ld_sc1(ps + 2);
-      v[3] += ld_sc1(ps + 3);
-    }
-    sk_finish4(g, off, m, n, v);
-  }
-  if (do_as && g.AP != nullptr) {
-    for (int r = threadIdx.x; r < TM; r += 256) {
-      const int m = m0 + r;
-      if (m >= g.M) continue;
-      float v = ld_sc1(g.AP + m);
-      for (int sp = 1; sp < g.splits; ++sp) v += ld_sc1(g.AP + (size_t)sp * g.M + m);
-      g.asum[m] = v;
-    }
-  }
-}
-
 // DB: two LDS buffers -- step s stores its tile into buffer s % 2, issues the next loads and
 // meets ONE barrier before its MFMAs (the single-buffer step needs a second barrier in front,
 // so no wave overwrites a tile another wave still reads); buffer s % 2 was last read by step
@@ -540,9 +458,7 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
     __syncthreads();
     if (tid < TM && m0 + tid < g.M) {
       const float v = (red[tid] + red[TM + tid]) + (red[2 * TM + tid] + red[3 * TM + tid]);
-      if (g.splits > 1 && g.cnt != nullptr)
-        st_sc1(g.AP + (size_t)split * g.M + m0 + tid, v);
-      else if (g.splits > 1)
+      if (g.splits > 1)
         g.AP[(size_t)split * g.M + m0 + tid] = v;
       else
         g.asum[m0 + tid] = v;
@@ -567,21 +483,15 @@ __device__ __forceinline__ void gemm_tile(const GemmDesc& g, unsigned long long 
         if (!nok || m >= g.M) continue;
         float v = acc[i][j][r];
         float* c = dst + (size_t)m * ldd + n;
-        if (!part) {  // raw partial otherwise: alpha / bias / act / accumulate by the last split
+        if (!part) {  // raw partial otherwise: alpha / bias / act / accumulate in splitk_reduce_kernel
           v = g.alpha * v + bn;
           if (g.act == 1) v = tanhf(v);
           if (g.drop_on == 3) v *= drop3(g, off, m, n);
           if (g.accumulate) v += *c;
-          *c = v;
-        } else if (g.cnt != nullptr) {
-          st_sc1(c, v);
-        } else {
-          *c = v;
         }
+        *c = v;
       }
   }
-  if (part && g.cnt != nullptr && sk_last_arrival(g.cnt + t, g.splits))
-    sk_reduce_tile<TM, TN>(g, off, m0, n0, do_as);
 }
 
 template <int FM, int FN, bool FAST, bool AH, bool BH, bool TRI = false, bool DB = false>
@@ -902,7 +812,6 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     }
     d.P = nullptr;
     d.AP = nullptr;
-    d.cnt = nullptr;
     d.red_base = red_blocks;
     if (d.splits > 1) {
       d.P = scratch ? scratch + need : nullptr;
@@ -915,27 +824,6 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     }
     d.tile_base = tiles;
     tiles += t * d.splits;
-  }
-  // split-K in the launch itself when every split desc's tiles get a ticket (see sk_reduce_tile)
-  {
-    int need_cnt = 0;
-    for (int i = 0; i < n; ++i)
-      if (b.d[i].splits > 1) need_cnt += (b.d[i].M + tm - 1) / tm * b.d[i].tiles_n;
-    if (need_cnt <= SK_CNT) {
-      static unsigned* base = [] {
-        unsigned* p = nullptr;
-        (void)hipGetSymbolAddress((void**)&p, HIP_SYMBOL(g_sk_cnt));
-        return p;
-      }();
-      int c = 0;
-      for (int i = 0; i < n; ++i) {
-        GemmDesc& d = b.d[i];
-        if (d.splits <= 1) continue;
-        d.cnt = base + c;
-        c += (d.M + tm - 1) / tm * d.tiles_n;
-      }
-      red_blocks = 0;  // no reduce launch
-    }
   }
   if (scratch == nullptr && need > 0) return need;  // query: the caller allocates and calls again
   if (tiles == 0) return 0;
@@ -976,7 +864,7 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   for (int i = 0; i < n; ++i) {
     GemmDesc& d = b.d[i];
     d.ared_base = red_blocks + ared_blocks;
-    if (d.splits > 1 && d.asum && d.cnt == nullptr) ared_blocks += (d.M + 255) / 256;
+    if (d.splits > 1 && d.asum) ared_blocks += (d.M + 255) / 256;
   }
   if (red_blocks + ared_blocks > 0)
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(red_blocks + ared_blocks), dim3(256), 0, s, b, red_blocks);

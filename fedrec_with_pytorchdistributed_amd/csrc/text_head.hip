@@ -408,197 +408,6 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
   }
 }
 
-// -----------------------------------------------------------------------------------------
-// head_score3: the att_fc1 product with ONLY the gathered X rows in the LDS pipeline.
-// head_score2 stages X (192 rows) AND the whole W1 k-slice (384 rows) per k-step: 72 KB a stage,
-// two stages, so one stage is in flight while the MFMAs read the other, and a k-step waits out
-// the full LDS-DMA latency of 72 KB (the wave-state counters' dependency waits).  Here:
-//   * X: 128 rows x 64 k per stage = 16 KB, NST-deep ring (NST - 1 stages in flight);
-//   * W1: each wave owns Q / 8 columns (QFW 16-column fragments) and loads its MFMA A fragments
-//     straight from L2 into registers (one 16-B global load per lane = one fragment), NST - 1
-//     k-steps ahead -- W1 (590 KB) is L2-resident and every block reads each byte once, the
-//     same bytes head_score2 moved through the LDS, without the LDS write + read;
-//   * every wave multiplies its QFW column fragments by all 8 row fragments of the stage
-//     (acc 8 x QFW f32x4), so X fragments are read from LDS by all 8 waves (8 x 16 KB per
-//     stage: 1/3 of what the LDS serves per MFMA in head_score2's 2 x 4 layout).
-// Issue order per iteration: the glds of stage kt + NST - 1, then (after a compiler memory fence,
-// so the order holds) the W1 loads of k-step kt + NST - 1; waiting for k-step kt's W1 loads
-// therefore also covers its stage.  The k loop is fully unrolled (NK = D / 64 k-steps), so the
-// counted waits are immediates.  Epilogue as head_score2 (tanh, w2 row-dot, bf16 e).
-// -----------------------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void vm_wait_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-__device__ __forceinline__ void vm_wait_barrier_rt(int n) {  // n folds to a constant once unrolled
-  switch (n) {
-    case 0: vm_wait_barrier<0>(); break;
-    case 8: vm_wait_barrier<8>(); break;
-    case 16: vm_wait_barrier<16>(); break;
-    case 24: vm_wait_barrier<24>(); break;
-    case 6: vm_wait_barrier<6>(); break;
-    case 12: vm_wait_barrier<12>(); break;
-    case 18: vm_wait_barrier<18>(); break;
-    case 4: vm_wait_barrier<4>(); break;
-    case 10: vm_wait_barrier<10>(); break;
-    case 20: vm_wait_barrier<20>(); break;
-    case 30: vm_wait_barrier<30>(); break;
-    case 32: vm_wait_barrier<32>(); break;
-    case 40: vm_wait_barrier<40>(); break;
-    default: vm_wait_barrier<0>(); break;
-  }
-}
-
-template <int QFW, int NST, int NK, int PW>
-__global__ __launch_bounds__(512, 1) void head_score3_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
-                                                             int M, int T, const bf16* __restrict__ W1,
-                                                             const float* __restrict__ b1, const float* __restrict__ w2,
-                                                             const float* __restrict__ b2, bf16* __restrict__ e_out,
-                                                             float* __restrict__ a_out, const int* __restrict__ nreal) {
-  constexpr int D = NK * 64, Q = QFW * 128, MR = 128, RB = 128, ST = MR * RB, PX = NST - 1;
-  static_assert(PW >= 1 && PW <= PX, "W1 prefetch distance within the X ring's");
-  __shared__ __attribute__((aligned(16))) char smem[NST * ST];
-  const int m0 = blockIdx.x * MR;
-  if (nreal != nullptr && m0 >= min(M, nreal[0] * T)) return;  // only padded titles' rows (never read)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
-  // X pieces: 16 per stage (8 rows x 128 B each); wave w issues pieces w and w + 8
-  const bf16* xsrc[2];
-  uint32_t xdst[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int p = wave + 8 * i, r = p * 8 + (lane >> 3);
-    int gm = m0 + r;
-    gm = gm < M ? gm : M - 1;  // rows past M: any valid row (outputs masked)
-    xsrc[i] = hrow(table, ids, gm, T, D) + ((lane & 7) ^ (r & 7)) * 8;
-    xdst[i] = (uint32_t)(p * 8 * RB);
-  }
-  // this lane's W1 fragment rows: q = wave * 16 QFW + 16 i + fr, k chunk fq (+ 32 for substep 1)
-  const bf16* wsrc = W1 + (size_t)(wave * 16 * QFW + fr) * D + fq * 8;
-  u32x4_t wreg[PW][2][QFW];
-  // iteration j issues the X stage of k-step j + PX, then the W1 fragments of k-step j + PW
-  auto issue_x = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, xsrc[i] + kt * 64),
-                                       LDS_PTR(void, smem + (kt % NST) * ST + xdst[i]), 16, 0, 0);
-    asm volatile("" ::: "memory");  // later loads stay behind this stage's glds
-  };
-  // one substep's fragments; a k-step's substep-kk registers are refilled right after the MFMAs
-  // that read them (no extra register slot for the load in flight)
-  auto issue_w = [&](int kt, int kk) {
-#pragma unroll
-    for (int i = 0; i < QFW; ++i)
-      wreg[kt % PW][kk][i] = *(const u32x4_t*)(wsrc + (size_t)i * 16 * D + kt * 64 + kk * 32);
-    asm volatile("" ::: "memory");
-  };
-  f32x4 acc[QFW][8];
-#pragma unroll
-  for (int i = 0; i < QFW; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // prologue, in the loop's issue order
-#pragma unroll
-  for (int kt = 0; kt < PX; ++kt) {
-    if (kt < NK) issue_x(kt);
-    if (kt + PW - PX >= 0 && kt + PW - PX < NK) {
-      issue_w(kt + PW - PX, 0);
-      issue_w(kt + PW - PX, 1);
-    }
-  }
-#pragma unroll
-  for (int kt = 0; kt < NK; ++kt) {
-    // k-step kt's W1 fragments landed (issued in iteration kt - PW, after the glds of its stage,
-    // which was issued earlier still): the younger ops are those of iterations kt - PW + 1 .. kt - 1
-    int younger = 0;
-#pragma unroll
-    for (int j = kt - PW + 1; j < kt; ++j) {
-      if (j + PX < NK) younger += 2;
-      if (j + PW < NK) younger += 2 * QFW;
-    }
-    vm_wait_barrier_rt(younger);
-    if (kt + PX < NK) issue_x(kt + PX);
-    const uint32_t As = lds0 + (kt % NST) * ST;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int lc = kk * 4 + fq;
-      u32x4_t xr[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = j * 16 + fr;
-        xr[j] = lds_read128(As + r * RB + ((lc ^ (r & 7)) << 4));
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        lgkm_tie_rt(7 - j, xr[j]);
-#pragma unroll
-        for (int i = 0; i < QFW; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wreg[kt % PW][kk][i]),
-                                                              __builtin_bit_cast(bf16x8, xr[j]), acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);  // the refill stays after the MFMAs that read these registers
-      if (kt + PW < NK) issue_w(kt + PW, kk);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  __syncthreads();  // every wave done with the last stage: the reduction buffer reuses it
-  const float b2v = b2[0];
-  float part[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) part[j] = 0.f;
-#pragma unroll
-  for (int i = 0; i < QFW; ++i) {
-    const int qb = wave * 16 * QFW + i * 16 + fq * 4;
-    const float4 bb = *(const float4*)(b1 + qb);
-    const float4 ww = *(const float4*)(w2 + qb);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v[4];
-      v[0] = tanh_fast(acc[i][j][0] + bb.x);
-      v[1] = tanh_fast(acc[i][j][1] + bb.y);
-      v[2] = tanh_fast(acc[i][j][2] + bb.z);
-      v[3] = tanh_fast(acc[i][j][3] + bb.w);
-      part[j] += v[0] * ww.x + v[1] * ww.y + v[2] * ww.z + v[3] * ww.w;
-      acc[i][j] = f32x4{v[0], v[1], v[2], v[3]};
-    }
-  }
-  if (e_out != nullptr) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = m0 + j * 16 + fr;
-      bf16* crow = e_out + (size_t)(m < M ? m : 0) * Q + wave * 16 * QFW;
-#pragma unroll
-      for (int i = 0; i + 1 < QFW; i += 2) {
-        const float v0[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        const float v1[4] = {acc[i + 1][j][0], acc[i + 1][j][1], acc[i + 1][j][2], acc[i + 1][j][3]};
-        store_pair16_if(crow + i * 16, v0, v1, fq, m < M);
-      }
-      if constexpr (QFW % 2 == 1) {
-        const int i = QFW - 1;
-        const bf16x4 o = {f2bf(acc[i][j][0]), f2bf(acc[i][j][1]), f2bf(acc[i][j][2]), f2bf(acc[i][j][3])};
-        if (m < M) *(bf16x4*)(crow + i * 16 + fq * 4) = o;
-      }
-    }
-  }
-  float* red = (float*)smem;  // [8 waves][128 rows]
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float sv = group4_sum(part[j]);
-    if (fq == 0) red[wave * MR + j * 16 + fr] = sv;
-  }
-  __syncthreads();
-  if (tid < MR && m0 + tid < M) {
-    const float sa = ((red[tid] + red[MR + tid]) + (red[2 * MR + tid] + red[3 * MR + tid])) +
-                     ((red[4 * MR + tid] + red[5 * MR + tid]) + (red[6 * MR + tid] + red[7 * MR + tid]));
-    a_out[m0 + tid] = sa + b2v;
-  }
-}
-
 // =========================================================================================
 // head_pool: per title u, alpha = eps-softmax(a) (stable form exp(a-m) / (sum + 1e-8 e^-m),
 // masked tokens get weight 0), pooled = sum_t alpha_t x_t (fp32).  384 threads: TG t-groups x
@@ -1287,236 +1096,6 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
   }
 }
 
-// -----------------------------------------------------------------------------------------
-// head_wgrad, 64-row stages (the default): twice the MFMA work per barrier of the 32-row form
-// (32 v_mfma_f32_16x16x32_bf16 per wave per stage), and no per-row index math in the loop: the
-// block's cache-row indices are resolved once into an LDS table laid out so one ds_read_b128
-// gives a lane the rows of its four X glds of a stage.  Stage = E [64 x 256 B] | X [64 x 512 B] |
-// DA [64 floats] (every wave DMAs the same 256 B: identical bytes, so the writes are benign and
-// every wave issues the same 7 glds per stage).  Three buffers: MFMAs on stage st, stage st+1
-// rewritten e -> g, stage st+2 in flight.
-// -----------------------------------------------------------------------------------------
-constexpr int W64_TM = 64;
-constexpr int W64_E = W64_TM * WQT * 2;   // 16 KB
-constexpr int W64_X = W64_TM * WKT * 2;   // 32 KB
-constexpr int W64_STAGE = W64_E + W64_X + 256;
-constexpr int W64_NST = 3;
-constexpr int W64_MAX_ROWS = 2816;        // per split (host-checked): rows table 11 KB
-
-__device__ __forceinline__ u32x4_t lds_read128w(uint32_t addr) {
-  u32x4_t v;
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr));
-  return v;
-}
-
-__device__ __forceinline__ void w64_stage(char* base, const bf16* __restrict__ e, const bf16* __restrict__ table,
-                                          uint32_t rows_lds, const float* __restrict__ da, int D, int Q, int q0,
-                                          int k0, int st, int m, int me, int wave, int lane) {
-  // E: 16 pieces of 4 rows x 16 chunks (pieces 2w, 2w+1)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int pc4 = wave * 2 + i;
-    const int row = pc4 * 4 + (lane >> 4), pc = lane & 15;
-    const int c = pc ^ swz(row);
-    const int gm = m + row;
-    const bf16* p = gm < me ? e + (size_t)gm * Q + q0 + 8 * c : g_zero_row + 8 * c;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + pc4 * 1024), 16, 0, 0);
-  }
-  // X: 32 pieces of 2 rows x 32 chunks (pieces 4w..4w+3); this lane's rows 8w + rsub + 2i
-  const int rsub = lane >> 5, pc = lane & 31;
-  const u32x4_t rr = lds_read128w(rows_lds + (uint32_t)(st * 64 + wave * 8 + rsub * 4) * 4);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = wave * 4 + i;
-    const int row = 2 * blk + rsub;
-    const int c = pc ^ swz(row);
-    const int cr = (int)rr[i];
-    const bf16* p = cr >= 0 ? table + (size_t)cr * D + k0 + 8 * c : g_zero_row + 8 * c;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + W64_E + blk * 1024), 16, 0, 0);
-  }
-  {
-    const int gm = m + lane;
-    const float* p = gm < me ? da + gm : g_zero_f32;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, p), LDS_PTR(void, base + W64_E + W64_X), 4, 0, 0);
-  }
-}
-
-__device__ __forceinline__ void w64_sync(int inflight) {  // 7 glds per stage
-  __builtin_amdgcn_sched_barrier(0);
-  if (inflight >= 1) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// rewrite this thread's two 16-B chunks (rows r and r + 32) of a stage's E tile
-template <bool STATS>
-__device__ __forceinline__ void w64_transform(uint32_t base, int tid, float (&dw2)[8], float (&dsum)[8]) {
-  const int r = tid >> 4, pc = tid & 15;
-  const uint32_t ea0 = base + r * 256 + pc * 16, ea1 = ea0 + 32 * 256;
-  u32x4_t v0 = lds_read128(ea0), v1 = lds_read128(ea1);
-  float d0 = lds_read32(base + W64_E + W64_X + r * 4), d1 = lds_read32(base + W64_E + W64_X + (r + 32) * 4);
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v0), "+v"(v1), "+v"(d0), "+v"(d1));
-  const bf16x8 e0 = __builtin_bit_cast(bf16x8, v0), e1 = __builtin_bit_cast(bf16x8, v1);
-  bf16x8 o0, o1;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float f0 = (float)e0[k], f1 = (float)e1[k];
-    o0[k] = f2bf(d0 * (1.0f - f0 * f0));
-    o1[k] = f2bf(d1 * (1.0f - f1 * f1));
-    if constexpr (STATS) {
-      dw2[k] += d0 * f0 + d1 * f1;
-      dsum[k] += (float)o0[k] + (float)o1[k];
-    }
-  }
-  lds_write128(ea0, __builtin_bit_cast(u32x4_t, o0));
-  lds_write128(ea1, __builtin_bit_cast(u32x4_t, o1));
-}
-
-__global__ __launch_bounds__(512, 1) void head_wgrad64_kernel(const bf16* __restrict__ e,
-                                                              const bf16* __restrict__ table,
-                                                              const int* __restrict__ ids,
-                                                              const float* __restrict__ da, int M, int T, int D, int Q,
-                                                              float* __restrict__ P, float* __restrict__ dw2p,
-                                                              float* __restrict__ dsump, int tiles_k, int ntiles,
-                                                              int mchunk, const int* __restrict__ nreal) {
-  __shared__ __attribute__((aligned(16))) char smem[W64_NST * W64_STAGE + 4 * W64_MAX_ROWS];
-  const int bid = blockIdx.x, nwg = gridDim.x;
-  const int xcd = bid & 7, qq = nwg >> 3, rmd = nwg & 7;
-  const int t = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (bid >> 3);
-  const int s = t / ntiles, tile = t - s * ntiles;
-  const int qt = tile / tiles_k, kt = tile - qt * tiles_k;
-  const int q0 = qt * WQT, k0 = kt * WKT;
-  if (nreal != nullptr) {  // as head_wgrad_kernel
-    M = min(M, nreal[0] * T);
-    const int S = nwg / ntiles;
-    const int c = ((M + S - 1) / S + W64_TM - 1) / W64_TM * W64_TM;
-    mchunk = max(W64_TM, min(mchunk, c));
-  }
-  const int mb = s * mchunk;
-  const int me = min(M, mb + mchunk);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave >> 2, wk = wave & 3;
-  const bool stats = kt == 0;
-
-  const int nsteps = me > mb ? (me - mb + W64_TM - 1) / W64_TM : 0;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
-  // cache-row table, permuted: entry st*64 + 8w + 4 rsub + i <-> local row st*64 + 8w + rsub + 2i
-  int* rows_s = (int*)(smem + W64_NST * W64_STAGE);
-  for (int j = tid; j < nsteps * 64; j += 512) {
-    const int st = j >> 6, rp = j & 63;
-    const int w = rp >> 3, rsub = (rp >> 2) & 1, i = rp & 3;
-    const int gm = mb + st * 64 + 8 * w + rsub + 2 * i;
-    int cr = -1;
-    if (gm < me) {
-      const int u = gm / T;
-      cr = (ids != nullptr ? ids[u] : u) * T + (gm - u * T);
-    }
-    rows_s[j] = cr;
-  }
-  __syncthreads();
-  const uint32_t rows_lds = lds0 + W64_NST * W64_STAGE;
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float sw2[8], ssum[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) sw2[k] = ssum[k] = 0.f;
-
-#pragma unroll
-  for (int i = 0; i < W64_NST - 1; ++i)
-    if (i < nsteps) w64_stage(smem + i * W64_STAGE, e, table, rows_lds, da, D, Q, q0, k0, i, mb + i * W64_TM, me, wave,
-                              lane);
-  if (nsteps > 0) {
-    w64_sync(nsteps > 1 ? 1 : 0);
-    if (stats) w64_transform<true>(lds0, tid, sw2, ssum);
-    else w64_transform<false>(lds0, tid, sw2, ssum);
-  }
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  uint32_t xo[2][4][2], yo[2][4][2];  // [k32 half][frag][row half]
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int r0 = h * 32 + g * 8;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      xo[h][j][0] = W64_E + tr_off_x(r0, wk * 64 + j * 16, q, p);
-      xo[h][j][1] = W64_E + tr_off_x(r0 + 4, wk * 64 + j * 16, q, p);
-      yo[h][j][0] = tr_off_e(r0, wn * 64 + j * 16, q, p);
-      yo[h][j][1] = tr_off_e(r0 + 4, wn * 64 + j * 16, q, p);
-    }
-  }
-  for (int st = 0; st < nsteps; ++st) {
-    w64_sync(st + 2 < nsteps ? 1 : 0);  // stage st+1 landed, stage st rewritten, stage st-1 read
-    if (st + 2 < nsteps)
-      w64_stage(smem + ((st + 2) % W64_NST) * W64_STAGE, e, table, rows_lds, da, D, Q, q0, k0, st + 2,
-                mb + (st + 2) * W64_TM, me, wave, lane);
-    if (st + 1 < nsteps) {
-      const uint32_t nb = lds0 + ((st + 1) % W64_NST) * W64_STAGE;
-      if (stats) w64_transform<true>(nb, tid, sw2, ssum);
-      else w64_transform<false>(nb, tid, sw2, ssum);
-    }
-    const uint32_t base = lds0 + (st % W64_NST) * W64_STAGE;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      s16x4 xr[8], yr[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        xr[2 * j] = tr_read(base + xo[h][j][0]);
-        xr[2 * j + 1] = tr_read(base + xo[h][j][1]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        yr[2 * i] = tr_read(base + yo[h][i][0]);
-        yr[2 * i + 1] = tr_read(base + yo[h][i][1]);
-      }
-      LGKM_TIE8(xr);
-      LGKM_TIE8(yr);
-      __builtin_amdgcn_sched_barrier(0);
-      bf16x8 xb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) xb[j] = join(xr[2 * j], xr[2 * j + 1]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bf16x8 ya = join(yr[2 * i], yr[2 * i + 1]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], ya, acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  float* out = P + (size_t)s * Q * D;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int qq2 = q0 + wn * 64 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + wk * 64 + j * 16 + 4 * g;
-      *(f32x4*)(out + (size_t)qq2 * D + k) = acc[i][j];
-    }
-  }
-  if (stats) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    float* red = (float*)smem;  // [32 row-threads][128 q] x 2
-    const int r = tid >> 4, lc = (tid & 15) ^ swz(r);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      red[r * WQT + lc * 8 + k] = sw2[k];
-      red[32 * WQT + r * WQT + lc * 8 + k] = ssum[k];
-    }
-    __syncthreads();
-    if (tid < 2 * WQT) {
-      const int which = tid / WQT, c = tid % WQT;
-      float acc2 = 0.f;
-      for (int rr = 0; rr < 32; ++rr) acc2 += red[which * 32 * WQT + rr * WQT + c];
-      (which == 0 ? dw2p : dsump)[(size_t)s * Q + q0 + c] = acc2;
-    }
-  }
-}
-
 // dW1 = w2 (.) sum_s P[s] ; db1 = w2 (.) sum_s dsum[s] ; dw2 = sum_s dw2p[s] ; db2 = sum_u db2p[u]
 // (fixed summation order: deterministic).  A block owns 64 float4 of dW1: its 4 waves sum the
 // split partials s = w, w+4, ... (independent 16-B loads in flight per lane), then wave 0 adds
@@ -1578,23 +1157,8 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const f32x4* __restric
 }
 
 int g_cus = 0;
-int g_wg_variant = -1;  // FEDREC_HEAD_WG: bit 0 = no e -> g transform (diagnostic timing only)
-int g_wg_splits = -1;   // FEDREC_HEAD_SPLITS: split-K count override (A/B runs)
-int g_score_variant = -1;  // FEDREC_HEAD_SCORE: head_score2 tilings (A/B), 0 = head_score_kernel
-int g_pool_variant = -1;  // FEDREC_HEAD_POOL: 1 = load-first pool kernels (default), 0 = the first forms
-
-int env_int(const char* k, int d) {
-  const char* v = getenv(k);
-  return v != nullptr ? atoi(v) : d;
-}
 
 }  // namespace
-
-// one default for every reader (fr_head_score_slices runs first: the binding sizes the score
-// buffer with it)
-static void score_variant_init() {
-  if (g_score_variant < 0) g_score_variant = env_int("FEDREC_HEAD_SCORE", 7);
-}
 
 extern "C" int fr_head_supported(int D, int Q, int T) {
   return D % 256 == 0 && D <= 1024 && (Q == 128 || Q == 256 || Q == 384) && T >= 1 && T <= MAXT;
@@ -1606,37 +1170,12 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   if (!fr_head_supported(D, Q, T)) return 1;
   const int M = U * T;
   if (M == 0) return 0;
-  score_variant_init();
-  // FEDREC_HEAD_SCORE (Q = 384): 7 (default) -> 192 rows, BK 64, 2 stages, staged LDS waits
-  // (steady step 0.5452-0.5473 vs 0.5477-0.5520 ms, three A/B pairs, profiles/r3_ab_score_sw.txt);
-  // 2 -> the same with one wait for all fragment reads (bench A/B/A: steady step 0.5925 / 0.5859
-  // / 0.5921 ms vs the 128-row form); 1 -> 128 rows, BK 32, 4 stages;
-  // 3 -> 128 rows, BK 64, 2 stages; 4 -> 192 rows, BK 32, 3 stages; 5 -> two Q slices of 192
-  // columns, 192 rows, BK 64, 3 stages (partial scores, see head_score2_kernel); 0 ->
-  // head_score_kernel
-  if (g_score_variant == 8 && D == 768) {  // head_score3: X-only LDS ring, W1 fragments from L2
-    const dim3 grid((M + 127) / 128);
-#define LAUNCH_S3(QFW)                                                                                       \
-  hipLaunchKernelGGL((head_score3_kernel<QFW, 4, 12, 2>), grid, dim3(512), 0, s, (const bf16*)table, ids, M, T, \
-                     (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, nreal)
-    if (Q == 384) LAUNCH_S3(3);
-    else if (Q == 256) LAUNCH_S3(2);
-    else LAUNCH_S3(1);
-#undef LAUNCH_S3
-    return 0;
-  }
-  if (Q == 384 && g_score_variant > 0) {
-#define LAUNCH_S2(QF, RF, BK, NST, WQ, NS, ...)                                                                \
-  hipLaunchKernelGGL((head_score2_kernel<QF, RF, BK, NST, WQ, ##__VA_ARGS__>), dim3((M + 32 * RF - 1) / (32 * RF), NS), dim3(512), \
-                     0, s, (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal)
-    if (g_score_variant == 1) LAUNCH_S2(6, 4, 32, 4, 4, 1);
-    else if (g_score_variant == 3) LAUNCH_S2(6, 4, 64, 2, 4, 1);
-    else if (g_score_variant == 4) LAUNCH_S2(6, 6, 32, 3, 4, 1);
-    else if (g_score_variant == 5) LAUNCH_S2(3, 6, 64, 3, 2, 2);
-    else if (g_score_variant == 6) LAUNCH_S2(6, 5, 64, 2, 4, 1);  // 160 rows: ~491 tiles = 1.9 waves of 256 CUs
-    else if (g_score_variant == 7) LAUNCH_S2(6, 6, 64, 2, 4, 1, true);  // the default tiling, staged LDS waits
-    else LAUNCH_S2(6, 6, 64, 2, 4, 1);
-#undef LAUNCH_S2
+  // Q = 384 (the DistilBERT head): 192-row tiles, BK 64, 2 stages, staged LDS waits (steady step
+  // 0.5452-0.5473 vs 0.5477-0.5520 ms for one wait, profiles/r3_ab_score_sw.txt; the X-only
+  // LDS ring with W1 fragments from L2 ran 100 vs 75 us, profiles/r4_ab_head_score3.txt)
+  if (Q == 384) {
+    hipLaunchKernelGGL((head_score2_kernel<6, 6, 64, 2, 4, true>), dim3((M + 191) / 192), dim3(512), 0, s,
+                       (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
     return 0;
   }
   const dim3 grid((M + 127) / 128);
@@ -1650,10 +1189,11 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   return 0;
 }
 
-// score partials per row: head_score writes a[slices][M] (the pool sums the slices)
+// score partials per row: head_score writes a[slices][M] (the pool sums the slices); every
+// current tiling writes whole scores
 extern "C" int fr_head_score_slices(int Q) {
-  score_variant_init();
-  return Q == 384 && g_score_variant == 5 ? 2 : 1;
+  (void)Q;
+  return 1;
 }
 
 extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, int slices, const int* tokens, int U,
@@ -1661,9 +1201,8 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, i
   const float* a2 = slices == 2 ? a + (size_t)U * T : nullptr;
   if (T > MAXT || D % 8 != 0 || D / 8 > 384) return 1;
   if (U == 0) return 0;
-  if (g_pool_variant < 0) g_pool_variant = env_int("FEDREC_HEAD_POOL", 1);
   const int TG = 384 / (D / 8), tpt = (T + TG - 1) / TG;
-  if (g_pool_variant != 0 && D <= 3072 && tpt <= 32) {
+  if (D <= 3072 && tpt <= 32) {  // load-first form; the first form takes the shapes past it
 #define LAUNCH_POOL2(N)                                                                                          \
   hipLaunchKernelGGL(head_pool2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, \
                      pooled, alpha, nreal)
@@ -1682,9 +1221,8 @@ extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* 
                                 int D, float* da, float* db2p, const int* nreal, hipStream_t s) {
   if (T > MAXT || D % 8 != 0 || D / 8 > 128) return 1;
   if (U == 0) return 0;
-  if (g_pool_variant < 0) g_pool_variant = env_int("FEDREC_HEAD_POOL", 1);
   const int tpw = (T + 5) / 6;
-  if (g_pool_variant != 0 && tpw <= 22) {
+  if (tpw <= 22) {
 #define LAUNCH_PBWD2(N)                                                                                           \
   hipLaunchKernelGGL(head_pool_bwd2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, alpha, g, T, D, \
                      da, db2p, nreal)
@@ -1711,10 +1249,6 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
     (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (g_cus <= 0) g_cus = 256;
   }
-  if (g_wg_variant < 0) {
-    g_wg_variant = env_int("FEDREC_HEAD_WG", 0);
-    g_wg_splits = env_int("FEDREC_HEAD_SPLITS", 0);
-  }
   const int tiles_k = D / WKT, ntiles = (Q / WQT) * tiles_k;
   // one wave of blocks (one per CU), each split >= 8 stages of 32 rows.  The first form left
   // 16 CUs out for the lookahead stream's sampler / dedup, which then still ran beside this
@@ -1722,14 +1256,14 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
   // The register-bitonic dedup (30 us) finishes before this kernel starts, so every CU gets a
   // block: 28 splits vs 26 measured 0.5709 / 0.5707 vs 0.5780 / 0.5791 ms per step (A/B/A/B,
   // profiles/r3_ab_wgrad_splits.txt)
-  int S = g_wg_splits > 0 ? g_wg_splits : g_cus / ntiles;
+  int S = g_cus / ntiles;
   const int smax = (M + 8 * WTM - 1) / (8 * WTM);
   S = S < 1 ? 1 : (S > smax ? smax : S);
   if (S < 1) S = 1;
   int mchunk = ((M + S - 1) / S + WTM - 1) / WTM * WTM;
   if (mchunk < WTM) mchunk = WTM;
   // a split's title ids (32-row forms) / cache-row table (64-row form) must fit in LDS
-  const int cap = ((g_wg_variant >> 1) & 3) == 3 ? W64_MAX_ROWS : (MAX_SPLIT_TITLES - 2) * T / WTM * WTM;
+  const int cap = (MAX_SPLIT_TITLES - 2) * T / WTM * WTM;
   if (mchunk > cap) mchunk = cap < 64 ? 64 : cap / 64 * 64;
   S = (M + mchunk - 1) / mchunk;
   if (S < 1) S = 1;
@@ -1738,24 +1272,12 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
   float* P = scratch;
   float* dw2p = scratch + (long)S * Q * D;
   float* dsump = dw2p + (long)S * Q;
-  // FEDREC_HEAD_WG bits 1-2: 0 -> 32-row stages x4 (default: 139 us at U = 1600 vs 146 / 149
-  // for x5 / x6 and 183 for the 64-row form, benchmarks/head_bench.py), 1 -> x5, 2 -> x6, 3 -> 64-row
-  const int nst = (g_wg_variant >> 1) & 3;
-  if (M > 0 && nst == 3) {
-    hipLaunchKernelGGL(head_wgrad64_kernel, dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids,
-                       da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, nreal);
-  } else if (M > 0) {
-#define LAUNCH_WG(N, IL, ...)                                                                                        \
-  hipLaunchKernelGGL((head_wgrad_kernel<N, IL, ##__VA_ARGS__>), dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e, (const bf16*)table, ids, \
-                     da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, g_wg_variant & 1, nreal)
-    if (nst == 1) LAUNCH_WG(5, false);
-    else if (nst == 2) LAUNCH_WG(6, false);
-    else if (g_wg_variant & 8) LAUNCH_WG(4, false);  // bit 3: the transform as its own LDS pass
-    else if (g_wg_variant & 16) LAUNCH_WG(4, true, false);  // bit 4: one LDS wait for all fragment reads
-    // default: staged LDS waits -- steady step 0.5498-0.5529 vs 0.5509-0.5534 ms over two calls
-    // (profiles/r3_ab_wgrad_sw_bump.txt).  (FEDREC_HEAD_WG bit 0 = no e -> g transform: diagnostic)
-    else LAUNCH_WG(4, true, true);
-#undef LAUNCH_WG
+  // 32-row stages x4 with staged LDS waits: 139 us at U = 1600 vs 146 / 149 for x5 / x6 and
+  // 183 for a 64-row form (benchmarks/head_bench.py); staged waits: steady step 0.5498-0.5529
+  // vs 0.5509-0.5534 ms over two calls (profiles/r3_ab_wgrad_sw_bump.txt)
+  if (M > 0) {
+    hipLaunchKernelGGL((head_wgrad_kernel<4, true, true>), dim3(S * ntiles), dim3(512), 0, s, (const bf16*)e,
+                       (const bf16*)table, ids, da, M, T, D, Q, P, dw2p, dsump, tiles_k, ntiles, mchunk, 0, nreal);
   } else {
     (void)hipMemsetAsync(scratch, 0, need * sizeof(float), s);
   }

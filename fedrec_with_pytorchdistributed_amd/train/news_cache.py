@@ -30,11 +30,16 @@ import torch
 
 
 class HiddenCache:
-    def __init__(self, text_encoder, tokens: torch.Tensor, chunk: int = 16384):
+    def __init__(self, text_encoder, tokens: torch.Tensor, chunk: int = 8192):
         """``tokens [N, 2, T]`` (int, on the compute device): the client's news table."""
         self.te = text_encoder
         self.tokens = tokens
-        self.chunk = chunk
+        # the ping-pong GEMM indexes its operands with 32-bit offsets: a chunk's widest
+        # activation (FFN1 output / FFN2 input, [chunk * T, hidden]) must stay below 2^31
+        # elements, or FFN2 leaves the persistent kernel (16k MIND titles: 2.5e9)
+        c = self.backbone.cfg
+        widest = max(c.dim, getattr(c, "hidden_dim", 4 * c.dim)) * tokens.shape[-1]
+        self.chunk = max(1, min(chunk, (2 ** 31 - 1) // widest))
         self.table: Optional[torch.Tensor] = None  # [N, T, D]
         self.version = -1
         self.build_s = 0.0  # wall time of the last build (device-synchronised)
@@ -66,8 +71,8 @@ class HiddenCache:
         N, _, T = self.tokens.shape
         D = self.backbone.cfg.dim
         table = torch.empty(N, T, D, dtype=self.te.compute_dtype, device=dev)
-        # chunks of 16k titles (~10 GB of activations at DistilBERT widths: fewer, larger GEMM
-        # launches); the last LayerNorm of each chunk writes straight into the table's rows
+        # chunks of 8k titles (409,600 token rows, ~5 GB of activations at DistilBERT widths);
+        # the last LayerNorm of each chunk writes straight into the table's rows
         for s in range(0, N, self.chunk):
             e = min(s + self.chunk, N)
             self.te.hidden(self.tokens[s:e], out=table[s:e])

@@ -129,15 +129,24 @@ def test_unfrozen_backbone_grads_match_cpu(dev):
     assert abs(float(l_cpu) - float(l_gpu)) < 3e-3
     gc, gg = m_cpu.flat.grad, m_gpu.flat.grad.cpu()
     total = float(gc.norm())
-    checked = 0
+    # per tensor, embeddings included: the bf16 compute path (bf16 weights and activations,
+    # fp32 accumulation) keeps every backbone gradient within a few bf16 ulps-worth of
+    # relative error of the fp32 CPU autograd; tensors whose gradient is tiny against the
+    # whole vector get an absolute bound instead
+    checked, worst = 0, []
     for name, p, off in m_cpu.flat.views():
-        if "DistillBert" not in name or name.endswith("position_embeddings.weight"):
+        if "DistillBert" not in name:
             continue
         a, b = gc[off:off + p.numel()], gg[off:off + p.numel()]
-        err = float((a - b).norm())
-        assert err <= 8e-2 * float(a.norm()) + 2e-3 * total, (name, err, float(a.norm()), total)
+        err, an = float((a - b).norm()), float(a.norm())
+        worst.append((err / max(an, 1e-30), name, an / total))
+        if an >= 1e-3 * total:
+            assert err <= 3e-2 * an, (name, err, an, total)
+        else:
+            assert err <= 3e-5 * total, (name, err, an, total)
         checked += 1
     assert checked > 20
+    print("worst per-tensor relative errors:", sorted(worst, reverse=True)[:6])
     # one optimizer step invalidates the bf16 compute copies of the backbone, and the next
     # pack carries the updated weights
     w1_before = m_gpu.text_encoder.DistillBert.compute_weights(torch.bfloat16)["layers"][0]["w1"].clone()
