@@ -2,10 +2,14 @@
 
 Interleaves every variant in ONE process (cdna_hip_programming.md §5.4 rule 24) on random
 data (rule 25) and reports the median TFLOP/s per variant:
-  ours-128  : 128x128x64 tile, 4 waves, glds double buffer
-  ours-256  : 256x256x64 tile, 8 waves, glds double buffer
-  ours-256p : the same, persistent (next tile's first K-tile overlaps the epilogue)
-  hipblaslt : torch.nn.functional.linear (bias fused), the library baseline
+  ours-128   : 128x128x64 tile, 4 waves, glds double buffer
+  ours-pp-v6 : 256x256x64 persistent ping-pong (row-predicated stores)
+  ours-pp-v9 : ping-pong with the store-tolerant stage schedule (padded C rows)
+  ours-pp-v12: v9 + bias-armed accumulators (the auto form)
+  ours-pp-v13: v12 with non-temporal output stores
+  hipblaslt  : torch.nn.functional.linear (bias fused) + the eager activation, the library baseline
+The default shapes are the backbone forward as it runs (residual adds live in the LayerNorm
+kernel, so out-proj / FFN2 carry bias only); ``--shapes res`` adds the residual-epilogue forms.
 """
 import argparse
 import os
@@ -26,15 +30,16 @@ def main():
     ap.add_argument("--M", type=int, default=78850)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--out", default="")
-    ap.add_argument("--diag", action="store_true", help="add the no-store diagnostic variant (timing only)")
     ap.add_argument("--only-shape", default="", help="run just this shape name (profiling)")
     ap.add_argument("--only-variants", default="", help="comma list of variant names to keep (profiling)")
     ap.add_argument("--shapes", default="model", help="model | square (8192^3 / 4096^3, no epilogue)")
     a = ap.parse_args()
     lib = native.lib()
     dev = torch.device("cuda")
-    shapes = [("qkv", 2304, 768, 0, False), ("out_proj+res", 768, 768, 0, True), ("ffn1+gelu", 3072, 768, 1, False),
-              ("ffn2+res", 768, 3072, 0, True), ("head_fc1+tanh", 384, 768, 2, False)]
+    shapes = [("qkv", 2304, 768, 0, False), ("out_proj", 768, 768, 0, False), ("ffn1+gelu", 3072, 768, 1, False),
+              ("ffn2", 768, 3072, 0, False), ("head_fc1+tanh", 384, 768, 2, False)]
+    if a.shapes == "res":
+        shapes = [("out_proj+res", 768, 768, 0, True), ("ffn2+res", 768, 3072, 0, True)]
     if a.shapes == "nores":  # the residual shapes without their residual (LN-side residual study)
         shapes = [("out_proj", 768, 768, 0, False), ("out_proj+res", 768, 768, 0, True),
                   ("ffn2", 768, 3072, 0, False), ("ffn2+res", 768, 3072, 0, True)]
@@ -60,19 +65,15 @@ def main():
 
         variants["ours-128"] = ours(0)
         if N % 256 == 0:
-            variants["ours-256"] = ours(1)
-            variants["ours-256p"] = ours(2)
-            variants["ours-256s"] = ours(3)
-            variants["ours-256p-split"] = ours(4)
-            variants["ours-256p-split-pipe"] = ours(5)
-            variants["ours-pingpong"] = ours(6)
+            variants["ours-pp-v6"] = ours(6)
             if N <= 3072:
-                variants["ours-pingpong-v9"] = ours(9)
-                variants["ours-pingpong-v10-deferred"] = ours(10)
-            if a.diag:
-                variants["diag-pingpong-nostore"] = ours(7)
+                variants["ours-pp-v9"] = ours(9)
+                if not has_res:
+                    variants["ours-pp-v12"] = ours(12)
+                    variants["ours-pp-v13-nt"] = ours(13)
         elif N % 128 == 0 and N > 256:  # text head N = 384: ping-pong with a partial last column tile
-            variants["ours-pingpong-v9-partial"] = ours(9)
+            variants["ours-pp-v9-partial"] = ours(9)
+        variants["ours-auto"] = ours(-1)
         bb = b.to(torch.bfloat16)
 
         def lt():

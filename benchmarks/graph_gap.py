@@ -52,8 +52,29 @@ def main():
         y.add_(1.0)
         g.replay()
 
+    other = torch.cuda.Stream()
+    z = torch.zeros(4096, device=dev)
+
+    def replay_xstream():  # the engine's pattern: a lookahead-stream kernel + event, main waits
+        with torch.cuda.stream(other):
+            z.add_(1.0)
+            ev = torch.cuda.Event()
+            ev.record(other)
+        torch.cuda.current_stream().wait_event(ev)
+        y.add_(1.0)
+        g.replay()
+
+    done = torch.cuda.Event()
+    done.record(other)
+
+    def replay_wait_done():  # waiting on an event that completed long ago
+        torch.cuda.current_stream().wait_event(done)
+        y.add_(1.0)
+        g.replay()
+
     out = {"one_kernel_us": timed(one, 2000), "eager_20_us": timed(eager), "replay_20_us": timed(replay),
-           "eager1_plus_replay_20_us": timed(replay_plus_eager)}
+           "eager1_plus_replay_20_us": timed(replay_plus_eager), "xstream_wait_replay_20_us": timed(replay_xstream),
+           "done_event_wait_replay_20_us": timed(replay_wait_done)}
     out["replay_seam_us"] = out["replay_20_us"] - K * out["one_kernel_us"]
     print(json.dumps({k: round(v, 2) for k, v in out.items()}), flush=True)
 

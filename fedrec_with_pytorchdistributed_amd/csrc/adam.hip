@@ -145,6 +145,7 @@ struct MultiCast {
   int blk0[MCAST_SEG + 1];
   unsigned char bf[MCAST_SEG];   // 1: bf16 destination, 0: fp32
   unsigned char vec[MCAST_SEG];  // 1: 16-byte aligned (vector path), 0: element by element
+  int trc[MCAST_SEG];            // > 0: transposed segment -- source [n / trc, trc] -> dst [trc, n / trc]
   int nseg;
   long long* bump;  // optional: a device step counter advanced by one (block 0, lane 0)
 };
@@ -161,6 +162,18 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
   const long base = (long)(blockIdx.x - mc.blk0[sg]) * MCAST_CHUNK;
   const float4* s4 = (const float4*)mc.src[sg];
   const long n = mc.n[sg];
+  if (mc.trc[sg] > 0) {  // transposed (small weights: element stores, strided)
+    const int C = mc.trc[sg];
+    const long R = n / C;
+    for (int it = 0; it < MCAST_CHUNK / (256 * 8); ++it) {
+      const long e = base + ((long)it * 256 + threadIdx.x) * 8;
+      for (int j = 0; j < 8 && e + j < n; ++j) {
+        const long r = (e + j) / C, c = (e + j) - r * C;
+        ((bf16*)mc.dst[sg])[c * R + r] = f2bf(mc.src[sg][e + j]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < MCAST_CHUNK / (256 * 8); ++it) {
     const long e = base + ((long)it * 256 + threadIdx.x) * 8;
@@ -189,7 +202,7 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
 // bump (optional): an int64 device counter the launch advances by one -- the training step's
 // dropout / noise offset rides in the step's cast launch instead of a launch of its own
 extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                             long long* bump, hipStream_t s) {
+                             long long* bump, hipStream_t s, const int* trc) {
   if (nseg < 1 || nseg > MCAST_SEG) return 1;
   MultiCast mc{};
   mc.nseg = nseg;
@@ -202,6 +215,8 @@ extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const lo
     mc.dst[i] = dst[i];
     mc.n[i] = n[i];
     mc.bf[i] = to_bf16[i] ? 1 : 0;
+    mc.trc[i] = trc != nullptr ? trc[i] : 0;
+    if (mc.trc[i] > 0 && (!mc.bf[i] || n[i] % mc.trc[i] != 0)) return 1;
     mc.blk0[i] = (int)blk;
     blk += (n[i] + MCAST_CHUNK - 1) / MCAST_CHUNK;
   }

@@ -22,11 +22,13 @@
 // Requirements (checked on the host): N % 128 == 0, K % 64 == 0; any M (rows clamped on
 // load, masked on store).
 //
-// Variants (fr_gemm_set_variant; -1 = auto): 0 the 128x128 kernel above; 1 256x256; 2 its
-// persistent form; 3 BK=32 four-stage; 4/5 persistent with split staging (+ register-
-// pipelined fragments); 6 persistent 256x256 ping-pong (two wave rows half a phase apart).
-// 9 = ping-pong with a store-tolerant stage schedule.  Auto: 9 for N % 256 == 0, N <= 3072,
-// K >= 128 (row-padded C); 6 for other N % 256 == 0; 0 otherwise (benchmarks/gemm_bench.py).
+// Variants (fr_gemm_set_variant; -1 = auto): 0 the 128x128 kernel above; 6 the persistent
+// 256x256 ping-pong (two wave rows half a phase apart, row-predicated stores); 9 the ping-pong
+// with a store-tolerant stage schedule (padded C rows; also the residual / GELU-backward /
+// dual-output epilogues); 12 = 9 with bias-armed accumulators; 13 = 12 with non-temporal
+// stores.  Auto: 13 for no-residual N % 256 == 0 shapes with padded C and K < 2048, 9 for the
+// residual forms and K >= 2048, 6 outside the padded-C domain, 0 otherwise
+// (benchmarks/gemm_bench.py, profiles/r4_gemm_bench.json).
 #include "common.h"
 
 namespace {
@@ -240,388 +242,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const bf16* __restrict_
 // per CU.  Twice the FLOP per staged byte of the 128x128 tile (128 vs 64 FLOP/B), which is
 // what the L2 can feed at MFMA rate (~34 TB/s aggregate L2 vs ~39 TB/s the small tile needs).
 constexpr int BM2 = 256, BN2 = 256;
-constexpr int STAGE2 = (BM2 + BN2) * BK * 2;  // 64 KB
-
-__device__ __forceinline__ void stage_tile2(char* smem, int st, const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                            int M, int K, int m0, int n0, int k0, int wave, int lane) {
-  char* base = smem + st * STAGE2;
-  const int rsub = lane >> 3;
-  const int chunk = (lane & 7) ^ rsub;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wave * 32 + i * 8 + rsub;  // 0..255
-    int gm = m0 + row;
-    gm = gm < M ? gm : M - 1;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, A + (size_t)gm * K + k0 + chunk * 8),
-                                     LDS_PTR(void, base + (wave * 32 + i * 8) * 128), 16, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wave * 32 + i * 8 + rsub;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W + (size_t)(n0 + row) * K + k0 + chunk * 8),
-                                     LDS_PTR(void, base + BM2 * 128 + (wave * 32 + i * 8) * 128), 16, 0, 0);
-  }
-}
-
-// one quarter of stage_tile2 (2 of its 8 glds): q = 0,1 -> A rows, q = 2,3 -> W rows
-__device__ __forceinline__ void stage_quarter2(char* smem, int st, int q, const bf16* __restrict__ A,
-                                               const bf16* __restrict__ W, int M, int K, int m0, int n0, int k0,
-                                               int wave, int lane) {
-  char* base = smem + st * STAGE2;
-  const int rsub = lane >> 3;
-  const int chunk = (lane & 7) ^ rsub;
-#pragma unroll
-  for (int i2 = 0; i2 < 2; ++i2) {
-    const int i = (q & 1) * 2 + i2;
-    const int row = wave * 32 + i * 8 + rsub;
-    if (q < 2) {
-      int gm = m0 + row;
-      gm = gm < M ? gm : M - 1;
-      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, A + (size_t)gm * K + k0 + chunk * 8),
-                                       LDS_PTR(void, base + (wave * 32 + i * 8) * 128), 16, 0, 0);
-    } else {
-      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W + (size_t)(n0 + row) * K + k0 + chunk * 8),
-                                       LDS_PTR(void, base + BM2 * 128 + (wave * 32 + i * 8) * 128), 16, 0, 0);
-    }
-  }
-}
-
-template <int ACT, bool HAS_BIAS, bool HAS_RES>
-__global__ __launch_bounds__(512, 1) void gemm_nt_256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                                             const float* __restrict__ bias,
-                                                             const bf16* __restrict__ R, bf16* __restrict__ C, int M,
-                                                             int N, int K, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE2];
-  const int bid = blockIdx.x, nwg = gridDim.x;
-  const int xcd = bid & 7, q = nwg >> 3, rmd = nwg & 7;
-  const int tile = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + (bid >> 3);
-  const int mt = tile / tiles_n, nt = tile - mt * tiles_n;
-  const int m0 = mt * BM2, n0 = nt * BN2;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-  stage_tile2(smem, 0, A, W, M, K, m0, n0, 0, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage_tile2(smem, cur ^ 1, A, W, M, K, m0, n0, (kt + 1) * BK, wave, lane);
-    const char* As = smem + cur * STAGE2;
-    const char* Bs = As + BM2 * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int phys = ((kk * 4 + fq) ^ (fr & 7)) * 16;
-      bf16x8 b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *(const bf16x8*)(Bs + (wn * 64 + j * 16 + fr) * 128 + phys);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x8 a[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(As + (wm * 128 + (h * 4 + i) * 16 + fr) * 128 + phys);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[h * 4 + i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + fr;
-    if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nb = n0 + wn * 64 + j * 16 + fq * 4;
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      if constexpr (HAS_BIAS) {
-        const float4 bb = *(const float4*)(bias + nb);
-        v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
-      }
-      act4<ACT>(v0, v1, v2, v3);
-      if constexpr (HAS_RES) {
-        const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
-        res4<ACT>(v0, v1, v2, v3, (float)rr[0], (float)rr[1], (float)rr[2], (float)rr[3]);
-      }
-      bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-      *(bf16x4*)(C + (size_t)m * N + nb) = o;
-    }
-  }
-}
-
-// Persistent form of the 256x256 kernel: one block per CU walks the tiles; the first K-tile
-// of the NEXT tile is issued before the current tile's epilogue, so tile prologue latency
-// and the epilogue (bias/act/residual/stores) overlap instead of idling the matrix cores.
-// Tile order: iteration `it` covers tiles [it*G, it*G+G); XCD x (blocks b % 8 == x) takes a
-// contiguous run of G/8 of them, so concurrently running tiles of one XCD share A panels.
-template <int ACT, bool HAS_BIAS, bool HAS_RES, bool SPLIT, bool PIPE = false>
-__global__ __launch_bounds__(512, 1) void gemm_nt_256p_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                                              const float* __restrict__ bias,
-                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
-                                                              int N, int K, int tiles_n, int ntiles) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE2];
-  const int G = gridDim.x, b = blockIdx.x;
-  const bool xcd_map = (G % 8) == 0;
-  auto map = [&](int it) -> int { return it * G + (xcd_map ? (b & 7) * (G >> 3) + (b >> 3) : b); };
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int nk = K / BK;
-  int it = 0;
-  int t = map(0);
-  if (t >= ntiles) return;
-  {
-    const int mt = t / tiles_n;
-    stage_tile2(smem, 0, A, W, M, K, mt * BM2, (t - mt * tiles_n) * BN2, 0, wave, lane);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int buf = 0;
-  while (true) {
-    const int mt = t / tiles_n, nt = t - mt * tiles_n;
-    const int m0 = mt * BM2, n0 = nt * BN2;
-    const int tn = map(it + 1);
-    const bool has_next = tn < ntiles;
-    const int mtn = tn / tiles_n;
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool st_next = (kt + 1 < nk) || has_next;
-      const int sm0 = (kt + 1 < nk) ? m0 : mtn * BM2;
-      const int sn0 = (kt + 1 < nk) ? n0 : (tn - mtn * tiles_n) * BN2;
-      const int sk0 = (kt + 1 < nk) ? (kt + 1) * BK : 0;
-      if (!SPLIT && st_next) stage_tile2(smem, buf ^ 1, A, W, M, K, sm0, sn0, sk0, wave, lane);
-      const char* As = smem + buf * STAGE2;
-      const char* Bs = As + BM2 * 128;
-      if constexpr (PIPE) {
-        // fragments for group g+1 are read while group g's 16 MFMAs issue (register double buffer)
-        const char* arow = As + (wm * 128 + fr) * 128;
-        const char* brow = Bs + (wn * 64 + fr) * 128;
-        auto physk = [&](int kk) { return ((kk * 4 + fq) ^ (fr & 7)) * 16; };
-        bf16x8 a0[4], a1[4], b0[4], b1[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b0[j] = *(const bf16x8*)(brow + j * 16 * 128 + physk(0));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a0[i] = *(const bf16x8*)(arow + i * 16 * 128 + physk(0));
-#define FR_GROUP(G, ACUR, ANXT, BCUR)                                                                  \
-  {                                                                                                    \
-    if (G < 3) {                                                                                       \
-      const int kn = (G + 1) >> 1, hn = (G + 1) & 1;                                                   \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i) ANXT[i] =                                          \
-          *(const bf16x8*)(arow + (hn * 4 + i) * 16 * 128 + physk(kn));                                \
-      if (G == 1) {                                                                                    \
-        _Pragma("unroll") for (int j = 0; j < 4; ++j) b1[j] = *(const bf16x8*)(brow + j * 16 * 128 + physk(1)); \
-      }                                                                                                \
-    }                                                                                                  \
-    if (SPLIT && st_next) stage_quarter2(smem, buf ^ 1, G, A, W, M, K, sm0, sn0, sk0, wave, lane);     \
-    __builtin_amdgcn_s_setprio(1);                                                                     \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j)        \
-        acc[(G & 1) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BCUR[j], ACUR[i], acc[(G & 1) * 4 + i][j], 0, 0, 0); \
-    __builtin_amdgcn_s_setprio(0);                                                                     \
-  }
-        FR_GROUP(0, a0, a1, b0)
-        FR_GROUP(1, a1, a0, b0)
-        FR_GROUP(2, a0, a1, b1)
-        FR_GROUP(3, a1, a0, b1)
-#undef FR_GROUP
-      } else
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int phys = ((kk * 4 + fq) ^ (fr & 7)) * 16;
-        bf16x8 bfr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * 64 + j * 16 + fr) * 128 + phys);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          if (SPLIT && st_next) stage_quarter2(smem, buf ^ 1, kk * 2 + h, A, W, M, K, sm0, sn0, sk0, wave, lane);
-          bf16x8 a[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(As + (wm * 128 + (h * 4 + i) * 16 + fr) * 128 + phys);
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], a[i], acc[h * 4 + i][j], 0, 0, 0);
-          __builtin_amdgcn_s_setprio(0);
-        }
-      }
-      if (kt + 1 < nk) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();  // last k-tile: everyone is done reading `buf` before it is restaged
-      buf ^= 1;
-    }
-    // epilogue of tile t while tile tn's first K-tile is in flight
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wm * 128 + i * 16 + fr;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nb = n0 + wn * 64 + j * 16 + fq * 4;
-        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-        if constexpr (HAS_BIAS) {
-          const float4 bb = *(const float4*)(bias + nb);
-          v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
-        }
-        act4<ACT>(v0, v1, v2, v3);
-        if constexpr (HAS_RES) {
-          const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
-          res4<ACT>(v0, v1, v2, v3, (float)rr[0], (float)rr[1], (float)rr[2], (float)rr[3]);
-        }
-        bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-        *(bf16x4*)(C + (size_t)m * N + nb) = o;
-      }
-    }
-    if (!has_next) break;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    t = tn;
-    ++it;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Variant 3: 256x256 tile, BK = 32, FOUR LDS stages (32 KB each) and a load stream that runs
-// three K-steps ahead of the MFMAs -- continuously, across tile boundaries (persistent).
-// The per-step sync is `s_waitcnt vmcnt(8) lgkmcnt(0); s_barrier` in one asm statement:
-// it retires only the OLDEST outstanding step (each step is 4 glds per thread), so two
-// steps stay in flight across every barrier (cdna_hip_programming.md §5 "Pipelining across
-// barriers": __syncthreads() would drain vmcnt to 0 here).  LDS rows are 64 B; the 16-B
-// chunk c of row r is stored at c ^ ((r >> 2) & 3), which spreads the 16 rows a ds_read_b128
-// lane group touches over all 16 slots of a 256-B bank row.
-constexpr int BK3 = 32;
-constexpr int STAGE3 = (BM2 + BN2) * BK3 * 2;  // 32 KB
-constexpr int NST3 = 4;
-
-__device__ __forceinline__ void stage_tile3(char* smem, int st, const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                            int M, int K, int m0, int n0, int k0, int wave, int lane) {
-  char* base = smem + st * STAGE3;
-  const int rsub = lane >> 2;                     // row within the 16-row piece
-  const int chunk = (lane & 3) ^ ((lane >> 4) & 3);  // logical chunk fetched into physical slot lane & 3
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wave * 2 + i) * 16 + rsub;  // 0..255
-    int gm = m0 + row;
-    gm = gm < M ? gm : M - 1;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, A + (size_t)gm * K + k0 + chunk * 8),
-                                     LDS_PTR(void, base + (wave * 2 + i) * 16 * 64), 16, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wave * 2 + i) * 16 + rsub;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W + (size_t)(n0 + row) * K + k0 + chunk * 8),
-                                     LDS_PTR(void, base + BM2 * 64 + (wave * 2 + i) * 16 * 64), 16, 0, 0);
-  }
-}
-
-template <int ACT, bool HAS_BIAS, bool HAS_RES>
-__global__ __launch_bounds__(512, 1) void gemm_nt_256s_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                                              const float* __restrict__ bias,
-                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
-                                                              int N, int K, int tiles_n, int ntiles) {
-  __shared__ __attribute__((aligned(16))) char smem[NST3 * STAGE3];
-  const int G = gridDim.x, b = blockIdx.x;
-  const bool xcd_map = (G % 8) == 0;
-  const int slot = xcd_map ? (b & 7) * (G >> 3) + (b >> 3) : b;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int nk = K / BK3;
-  const int my_tiles = slot < ntiles ? (ntiles - 1 - slot) / G + 1 : 0;
-  const int total = my_tiles * nk;  // this block's (tile, k-step) sequence
-  if (total == 0) return;
-  // loader cursor: global step index -> (tile, k)
-  auto issue = [&](int gs) {
-    const int ti = gs / nk, kk = gs - ti * nk;
-    const int t = ti * G + slot;
-    const int mt = t / tiles_n;
-    stage_tile3(smem, gs & (NST3 - 1), A, W, M, K, mt * BM2, (t - mt * tiles_n) * BN2, kk * BK3, wave, lane);
-  };
-  // prologue: three steps in flight (pad with real issues only)
-  issue(0);
-  if (total > 1) issue(1);
-  if (total > 2) issue(2);
-  if (total > 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-
-  int gs = 0;
-  for (int ti = 0; ti < my_tiles; ++ti) {
-    const int t = ti * G + slot;
-    const int mt = t / tiles_n, nt = t - mt * tiles_n;
-    const int m0 = mt * BM2, n0 = nt * BN2;
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < nk; ++k, ++gs) {
-      const bool more = gs + 3 < total;
-      if (more) issue(gs + 3);
-      const char* As = smem + (gs & (NST3 - 1)) * STAGE3;
-      const char* Bs = As + BM2 * 64;
-      const int rsw = (fr >> 2) & 3;
-      const int phys = ((fq ^ rsw)) * 16;
-      bf16x8 bfr[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * 64 + j * 16 + fr) * 64 + phys);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x8 a[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(As + (wm * 128 + (h * 4 + i) * 16 + fr) * 64 + phys);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], a[i], acc[h * 4 + i][j], 0, 0, 0);
-      }
-      // retire step gs+1 (the oldest in flight); keep the younger ones flying
-      if (more) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (gs + 2 < total) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wm * 128 + i * 16 + fr;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nb = n0 + wn * 64 + j * 16 + fq * 4;
-        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-        if constexpr (HAS_BIAS) {
-          const float4 bb = *(const float4*)(bias + nb);
-          v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
-        }
-        act4<ACT>(v0, v1, v2, v3);
-        if constexpr (HAS_RES) {
-          const bf16x4 rr = *(const bf16x4*)(R + (size_t)m * N + nb);
-          res4<ACT>(v0, v1, v2, v3, (float)rr[0], (float)rr[1], (float)rr[2], (float)rr[3]);
-        }
-        bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-        *(bf16x4*)(C + (size_t)m * N + nb) = o;
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // Variant 6: 256x256x64 persistent "ping-pong" GEMM (cdna_hip_programming.md §5, 256² 8-phase
 // template), 512 threads = 8 waves (2 along M x 4 along N), 128x64 outputs per wave.
@@ -654,7 +274,7 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int ACT, bool HAS_BIAS, bool HAS_RES, int EPI = 0>  // EPI 1: diagnostic build, stores suppressed
+template <int ACT, bool HAS_BIAS, bool HAS_RES>
 __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                             const float* __restrict__ bias,
                                                             const bf16* __restrict__ R, bf16* __restrict__ C, int M,
@@ -819,7 +439,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restri
                 res4<ACT>(v0, v1, v2, v3, (float)rr[i][p][j][0], (float)rr[i][p][j][1], (float)rr[i][p][j][2],
                           (float)rr[i][p][j][3]);
               }
-              if (m < M && (EPI == 0 || v0 == 1234.5f)) {
+              if (m < M) {
                 bf16x4 o = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
                 *(bf16x4*)(C + (size_t)m * N + nb0 + p * 32 + j * 16) = o;
               }
@@ -845,6 +465,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(const bf16* __restri
 // dword pair gives every lane 8 contiguous columns -- fq 0: 0-7, 1: 16-23, 2: 8-15,
 // 3: 24-31 -- so the group goes out as ONE 16-byte store per lane instead of two 8-byte
 // ones (cdna_hip_programming.md T21).
+template <bool NT = false>
 __device__ __forceinline__ void store_pair16(bf16* __restrict__ crow, const float (&v0)[4], const float (&v1)[4],
                                              int fq) {
   const bf16x4 o0 = {f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3])};
@@ -857,7 +478,10 @@ __device__ __forceinline__ void store_pair16(bf16* __restrict__ crow, const floa
   a.y = r[0];
   b.y = r[1];
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  *GLOBAL_PTR(u32x4, crow + (fq & 1) * 16 + (fq >> 1) * 8) = u32x4{a.x, a.y, b.x, b.y};
+  if constexpr (NT)  // streaming store: the output is not re-read by this kernel
+    __builtin_nontemporal_store(u32x4{a.x, a.y, b.x, b.y}, GLOBAL_PTR(u32x4, crow + (fq & 1) * 16 + (fq >> 1) * 8));
+  else
+    *GLOBAL_PTR(u32x4, crow + (fq & 1) * 16 + (fq >> 1) * 8) = u32x4{a.x, a.y, b.x, b.y};
 }
 
 // ---------------------------------------------------------------------------------------
@@ -873,11 +497,9 @@ __device__ __forceinline__ void store_pair16(bf16* __restrict__ crow, const floa
 // its loads would break the count, so HAS_RES keeps vmcnt(8)).  One more half-tile is in
 // flight per wait than in variant 6.  WAR: every half is restaged >= 1 phase after its last
 // read (A_h1 is read in phase 2 and restaged in phase 3).
-// DEFER (variant 10, no residual): a finished tile's epilogue is spread over the next tile's
-// first K-step -- quadrant q is stored in the load section of the phase whose MFMAs next write
-// it (4 x 16-B stores per phase), so each wave row's epilogue overlaps the other row's MFMAs
-// instead of stalling it at a barrier.
-template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DEFER = false, bool DUAL = false>
+// (Spreading a tile's epilogue over the load sections of the next tile's first K-step measured
+// slower: 815 vs 964 TF on QKV, profiles/r4_gemm_bench_base.json.)
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DUAL = false>
 __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                              const float* __restrict__ bias,
                                                              const bf16* __restrict__ R, bf16* __restrict__ C, int M,
@@ -1010,34 +632,6 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     pp_barrier();                                                                                       \
   }
 
-  // deferred epilogue: store quadrant (QM, QN) of the pending tile (pm0, pn0), then zero it
-  int pm0 = 0, pn0 = 0;
-  bool pend = false, after_pend = false;
-  const uint32_t bias_lds = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + 8 * PP_HALF;
-#define PP2_STORE_Q(QM, QN)                                                                         \
-  {                                                                                                 \
-    const int nq = pn0 + wc * 64 + QN * 32;                                                         \
-    f32x4 bq0 = f32x4{0.f, 0.f, 0.f, 0.f}, bq1 = f32x4{0.f, 0.f, 0.f, 0.f};                         \
-    if constexpr (HAS_BIAS) {                                                                       \
-      const uint32_t ba = bias_lds + (nq + fq * 4) * 4;                                             \
-      asm volatile("ds_read_b128 %0, %1" : "=v"(bq0) : "v"(ba));                                   \
-      asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(bq1) : "v"(ba));                         \
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bq0), "+v"(bq1));                                 \
-    }                                                                                               \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
-      float v0[4], v1[4];                                                                           \
-      _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                              \
-        v0[e] = acc[QM][i][QN][0][e] + bq0[e];                                                      \
-        v1[e] = acc[QM][i][QN][1][e] + bq1[e];                                                      \
-      }                                                                                             \
-      act4<ACT>(v0[0], v0[1], v0[2], v0[3]);                                                        \
-      act4<ACT>(v1[0], v1[1], v1[2], v1[3]);                                                        \
-      store_pair16(C + (size_t)(pm0 + wr * 128 + QM * 64 + i * 16 + fr) * N + nq, v0, v1, fq);     \
-      acc[QM][i][QN][0] = f32x4{0.f, 0.f, 0.f, 0.f};                                                \
-      acc[QM][i][QN][1] = f32x4{0.f, 0.f, 0.f, 0.f};                                                \
-    }                                                                                               \
-  }
-
   int kt = 0, it = 0;
   bool after_epi = false;  // the previous step ended with a tile epilogue (its 16 stores in flight)
   bool epi_stored = true;  // ... and this wave issued them (false: columns past a partial tile)
@@ -1048,49 +642,27 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     // phase 0: quadrant (0,0)
     read_a(buf);
     read_b(buf + 2 * PP_HALF, b0);
-    if (DEFER && pend) PP2_STORE_Q(0, 0)
     PP_MFMA(0, 0, b0)
     // phase 1: quadrant (0,1)
     read_b(buf + 3 * PP_HALF, b1);
     stage(g + 2, 0, k2, nx2);
-    if (DEFER && pend) PP2_STORE_Q(0, 1)
     PP_MFMA(0, 1, b1)
     // phase 2: quadrant (1,1)
     read_a(buf + PP_HALF);
     stage(g + 2, 2, k2, nx2);
-    if (DEFER && pend) PP2_STORE_Q(1, 1)
     PP_MFMA(1, 1, b1)
     // phase 3: quadrant (1,0); stage the rest of g+2, retire step g+1 (issued during step g-1,
     // so everything of this step may stay in flight: its 8 loads and, deferred, 16 stores)
     stage(g + 2, 3, k2, nx2);
     stage(g + 2, 1, k2, nx2);
-    if (DEFER && pend) PP2_STORE_Q(1, 0)
     if (g + 2 >= S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (DEFER && pend) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");        // 8 loads + 16 stores
-    else if (DEFER && after_pend) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // + last phase's 4 stores
     // (a wave whose columns lay outside a partial last tile issued no stores: plain wait)
-    else if (!DEFER && !HAS_RES && after_epi && epi_stored && DUAL) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 8 + 32 stores
-    else if (!DEFER && !HAS_RES && after_epi && epi_stored) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 + 16 stores
+    else if (!HAS_RES && after_epi && epi_stored && DUAL) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 8 + 32 stores
+    else if (!HAS_RES && after_epi && epi_stored) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 8 + 16 stores
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    after_pend = DEFER && pend;
-    pend = false;
     after_epi = false;
     PP_MFMA(1, 0, b0)
-    if (DEFER && ++kt == nk) {
-      tile_mn(it * G + c, pm0, pn0);
-      if (g + 1 < S) {
-        pend = true;
-      } else {
-        PP2_STORE_Q(0, 0) PP2_STORE_Q(0, 1) PP2_STORE_Q(1, 1) PP2_STORE_Q(1, 0)
-      }
-      kt = 0;
-      ++it;
-#pragma unroll
-      for (int h = 0; h < 4; ++h)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) ocur[h][i] = onxt[h][i];
-      tile_offs(it + 1, onxt);
-    } else if (!DEFER && ++kt == nk) {
+    if (++kt == nk) {
       int m0, n0;
       tile_mn(it * G + c, m0, n0);
       const int nb0 = n0 + wc * 64 + fq * 4;
@@ -1207,13 +779,243 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp2_kernel(const bf16* __restr
     }
   }
 #undef PP_MFMA
-#undef PP2_STORE_Q
+  if (wr == 0) pp_barrier();
+}
+
+// ---------------------------------------------------------------------------------------
+// Variants 12 / 13 (13 = auto on no-residual shapes with N % 256 == 0 and K < 2048): the variant-9 ping-pong
+// schedule with bias-armed accumulators -- once the tile epilogue has stored a quadrant, its
+// accumulators are set to the NEXT tile's bias (0 without a bias) instead of zero, so the
+// epilogue has no bias add and no separate zeroing.  (Storing each quadrant inside the next
+// phase's MFMA section instead -- 4 stores per phase -- needs ~40 more VGPRs than 2 waves / SIMD
+// leave: it spilled, and re-reading B_h0 to free them races its restaging in phase 2.)
+// NT (variant 13): non-temporal output stores (the C tile is not re-read by this launch).
+template <int ACT, bool HAS_BIAS, bool DUAL, bool NT = false>
+__global__ __launch_bounds__(512, 1) void gemm_nt_pp3_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                             const float* __restrict__ bias, bf16* __restrict__ C,
+                                                             int M, int N, int K, int tiles_n, int ntiles,
+                                                             const int* __restrict__ full_rows = nullptr,
+                                                             int tiles_np = 0, bf16* __restrict__ Z = nullptr) {
+  // ONE __shared__ object (staging halves + the bias vector), as variant 9
+  __shared__ __attribute__((aligned(16))) char smem[8 * PP_HALF + (HAS_BIAS ? PP2_MAXN * 4 : 0)];
+  float* bias_s = (float*)(smem + 8 * PP_HALF);
+  const int G = gridDim.x, b = blockIdx.x;
+  const int c = (G % 8 == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
+  int full_t = ntiles;
+  if (full_rows != nullptr) {  // row-split tile list (fr_gemm_nt_bf16_split), as variant 9
+    const int tiles_m = (M + 255) >> 8;
+    int fm = (*full_rows + 255) >> 8;
+    fm = fm < tiles_m ? fm : tiles_m;
+    full_t = fm * tiles_n;
+    ntiles = full_t + (tiles_m - fm) * tiles_np;
+  }
+  auto tile_mn = [&](int t, int& m0_, int& n0_) {
+    int mt_, nt_;
+    if (t < full_t) {
+      mt_ = t / tiles_n;
+      nt_ = t - mt_ * tiles_n;
+    } else {
+      const int u = t - full_t, q = u / tiles_np;
+      mt_ = full_t / tiles_n + q;
+      nt_ = u - q * tiles_np;
+    }
+    m0_ = mt_ * 256;
+    n0_ = nt_ * 256;
+  };
+  if (c >= ntiles) return;
+  const int nk = K >> 6;
+  const int S = ((ntiles - c + G - 1) / G) * nk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rsub = lane >> 3, schunk = (lane & 7) ^ rsub;
+  if constexpr (HAS_BIAS) {  // complete before the first tile's accumulators read it
+    for (int i = tid; i < N; i += 512) bias_s[i] = bias[i];
+    __syncthreads();
+  }
+  // staging addresses from the (scalar) tile origins: row r0 + 8 i + rsub of half h, r0
+  // wave-uniform; A rows past M clamp to M - 1 (their products land in C's padding rows)
+  int cm0, cn0, nm0, nn0;  // current / next tile of this block's stream
+  auto tile_at = [&](int itile, int& m0_, int& n0_) {
+    int t = itile * G + c;
+    tile_mn(t < ntiles ? t : c, m0_, n0_);
+  };
+  auto stage = [&](int g, int h, int kts, bool nx) {
+    if (g >= S) return;
+    char* dst = smem + ((g & 1) * 4 + h) * PP_HALF;
+    const int r0 = h < 2 ? (nx ? nm0 : cm0) + (wave >> 2) * 128 + h * 64 + (wave & 3) * 16
+                         : (nx ? nn0 : cn0) + (wave >> 1) * 64 + (h - 2) * 32 + (wave & 1) * 16;
+    const bf16* base = (h < 2 ? A : W) + kts * 64 + schunk * 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int row = r0 + i * 8 + rsub;
+      if (h < 2) row = row < M ? row : M - 1;
+      __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, base + row * K),
+                                       LDS_PTR(void, dst + (wave * 16 + i * 8) * 128), 16, 0, 0);
+    }
+  };
+  tile_at(0, cm0, cn0);
+  tile_at(1, nm0, nn0);
+  const bool nx_1 = nk < 2;
+  stage(0, 0, 0, false); stage(0, 2, 0, false); stage(0, 3, 0, false); stage(0, 1, 0, false);
+  stage(1, 0, 1, nx_1); stage(1, 2, 1, nx_1); stage(1, 3, 1, nx_1); stage(1, 1, 1, nx_1);
+  if (S > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (wr == 1) pp_barrier();
+
+  f32x4 acc[2][4][2][2];
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = (wr * 64 + fr) * 128, brow = (wc * 32 + fr) * 128;
+  const int ph0 = ((0 * 4 + fq) ^ (fr & 7)) * 16, ph1 = ((1 * 4 + fq) ^ (fr & 7)) * 16;
+  auto read_a = [&](const char* hb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *(const bf16x8*)(hb + arow + i * 16 * 128 + ph0);
+      af[i][1] = *(const bf16x8*)(hb + arow + i * 16 * 128 + ph1);
+    }
+  };
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf[j][0] = *(const bf16x8*)(hb + brow + j * 16 * 128 + ph0);
+      bf[j][1] = *(const bf16x8*)(hb + brow + j * 16 * 128 + ph1);
+    }
+  };
+  const uint32_t bias_lds = (uint32_t)(uintptr_t)LDS_PTR(char, smem) + 8 * PP_HALF;
+  // bias of columns n0 + wc*64 + qn*32 + j*16 + 4fq + e (j = 0, 1) via opaque ds_reads (a plain
+  // read of the staging object would also drain vmcnt); tie_bias waits for them
+  auto read_bias = [&](int n0, int qn, f32x4 (&bv)[2]) {
+    if constexpr (HAS_BIAS) {
+      const uint32_t ba = bias_lds + (n0 + wc * 64 + qn * 32 + fq * 4) * 4;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(bv[0]) : "v"(ba));
+      asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(bv[1]) : "v"(ba));
+    } else {
+      bv[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bv[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto tie_bias = [&](f32x4 (&bv)[2]) {
+    if constexpr (HAS_BIAS) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bv[0]), "+v"(bv[1]));
+  };
+  {  // the first tile's accumulators start at its bias
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      f32x4 bv[2];
+      read_bias(cn0, p, bv);
+      tie_bias(bv);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[q][i][p][j] = bv[j];
+    }
+  }
+  f32x4 bn[2];  // the bias that re-arms the quadrant an epilogue phase stores
+#define PP3_MF(QM, QN, BF)                                                                              \
+  {                                                                                                     \
+    pp_barrier();                                                                                       \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                \
+    __builtin_amdgcn_s_setprio(1);                                                                      \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) _Pragma("unroll") for (int i = 0; i < 4; ++i)      \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[QM][i][QN][j] =                               \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[j][kk], af[i][kk], acc[QM][i][QN][j], 0, 0, 0);  \
+    __builtin_amdgcn_s_setprio(0);                                                                      \
+    pp_barrier();                                                                                       \
+  }
+#define PP3_EPI(QM, QN)                                                                                 \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                      \
+    float v0[4], v1[4];                                                                                 \
+    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                    \
+      v0[e] = acc[QM][i][QN][0][e];                                                                     \
+      v1[e] = acc[QM][i][QN][1][e];                                                                     \
+    }                                                                                                   \
+    const size_t o_ = (size_t)(pm0 + wr * 128 + QM * 64 + i * 16 + fr) * N + pn0 + wc * 64 + QN * 32;  \
+    if constexpr (DUAL) store_pair16<NT>(Z + o_, v0, v1, fq);                                           \
+    act4<ACT>(v0[0], v0[1], v0[2], v0[3]);                                                              \
+    act4<ACT>(v1[0], v1[1], v1[2], v1[3]);                                                              \
+    store_pair16<NT>(C + o_, v0, v1, fq);                                                               \
+    acc[QM][i][QN][0] = bn[0];                                                                          \
+    acc[QM][i][QN][1] = bn[1];                                                                          \
+  }
+  int kt = 0, it = 0, pm0 = 0, pn0 = 0;
+  for (int g = 0; g < S; ++g) {
+    const char* buf = smem + (g & 1) * 4 * PP_HALF;
+    const bool nx2 = kt + 2 >= nk;
+    const int k2 = nx2 ? kt + 2 - nk : kt + 2;
+    const bool last = kt == nk - 1;
+    const bool epi0 = kt == 0 && it > 0;  // the step after a tile epilogue
+    if (last) {  // the tile this step's epilogue stores
+      pm0 = cm0;
+      pn0 = cn0;
+    }
+    // phase 0: quadrant (0,0)
+    read_a(buf);
+    read_b(buf + 2 * PP_HALF, b0);
+    PP3_MF(0, 0, b0)
+    // phase 1: quadrant (0,1)
+    read_b(buf + 3 * PP_HALF, b1);
+    stage(g + 2, 0, k2, nx2);
+    PP3_MF(0, 1, b1)
+    // phase 2: quadrant (1,1)
+    read_a(buf + PP_HALF);
+    stage(g + 2, 2, k2, nx2);
+    PP3_MF(1, 1, b1)
+    // phase 3: quadrant (1,0); stage the rest of g+2, retire step g+1 (after a tile epilogue its
+    // stores are younger than step g+1's loads and may stay in flight)
+    stage(g + 2, 3, k2, nx2);
+    stage(g + 2, 1, k2, nx2);
+    if (g + 2 >= S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (epi0 && DUAL) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 8 loads + 32 stores
+    else if (epi0) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");          // 8 loads + 16 stores
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    PP3_MF(1, 0, b0)
+    if (last) {  // the tile epilogue; the quadrants are re-armed with the next tile's bias
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      read_bias(nn0, 0, bn);
+      tie_bias(bn);
+      PP3_EPI(0, 0) PP3_EPI(1, 0)
+      read_bias(nn0, 1, bn);
+      tie_bias(bn);
+      PP3_EPI(0, 1) PP3_EPI(1, 1)
+    }
+    if (last) {
+      kt = 0;
+      ++it;
+      cm0 = nm0;
+      cn0 = nn0;
+      tile_at(it + 1, nm0, nn0);
+    } else {
+      ++kt;
+    }
+  }
+#undef PP3_MF
+#undef PP3_EPI
   if (wr == 0) pp_barrier();
 }
 
 int g_num_cus = 0;
 
-int g_gemm_variant = -1;  // -1 auto, 0 = 128x128, 1 = 256x256
+int g_gemm_variant = -1;  // -1 auto; 0 = 128x128, 6 / 9 / 12 / 13 = the ping-pong forms (A/B runs)
+
+static int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
+// the ping-pong kernels' domain: 256x256 tiles (a partial last column tile only in variant 9),
+// C rows padded to a multiple of 256 (unpredicated stores), 32-bit operand offsets
+static bool pp_domain(int M, int N, int K, int c_rows) {
+  return K >= 128 && N <= PP2_MAXN && c_rows >= ((M + 255) / 256) * 256 && (long long)M * K < (1ll << 31) &&
+         (long long)N * K < (1ll << 31);
+}
 
 template <int ACT>
 void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, bf16* C, int M, int N, int K,
@@ -1223,31 +1025,40 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
   // with tanh it measured 133 us vs 102 us for the 128x128 kernel (2.45 waves of 256-row
   // tiles, a third of the MFMA work wasted on the clamped columns, tanh in the exposed epilogue)
   const bool part_n = N % BN2 != 0 && N % 64 == 0 && R == nullptr && ACT != 3 && g_gemm_variant == 9;
-  const bool big = (g_gemm_variant >= 1) || (g_gemm_variant < 0 && (N % BN2 == 0 || part_n) && M >= 4096);
-  // auto policy (measured, profiles/gemm_bench_r1_pp.json): the ping-pong kernel (6) on every
-  // N % 256 == 0 shape (with the packed-f32 GELU epilogue it also edges out variant 5 on FFN1).
-  // auto: variant 9 wherever it applies (measured: profiles/gemm_bench_r1_v9.json), else 6
-  const bool v9 = g_gemm_variant == 9 || g_gemm_variant == 10 || g_gemm_variant < 0;
-  if (big && (N % BN2 == 0 || part_n) && v9 && K >= 128 && N <= PP2_MAXN && c_rows >= ((M + 255) / 256) * 256 &&
-      (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
+  const bool auto_v = g_gemm_variant < 0;
+  const bool big = (auto_v && N % BN2 == 0 && M >= 4096) || (g_gemm_variant >= 6 && (N % BN2 == 0 || part_n));
+  if (big && (auto_v || g_gemm_variant == 9 || g_gemm_variant >= 12) && pp_domain(M, N, K, c_rows)) {
     const int tiles_n = (N + BN2 - 1) / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
-    if (g_num_cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (g_num_cus <= 0) g_num_cus = 256;
+    const int G = ntiles < num_cus() ? ntiles : num_cus();
+    // auto: variant 13 (bias-armed accumulators, non-temporal stores) on the no-residual shapes
+    // with K < 2048; variant 9 for the rest (residual / GELU-backward epilogues, FFN2)
+    if constexpr (ACT != 3) {
+      if (R == nullptr && N % BN2 == 0 && g_gemm_variant != 9) {
+        // non-temporal output stores (variant 13) by default where K < 2048: QKV 1025 vs 930 TF,
+        // FFN1 + GELU 868 vs 796, out-proj 916 vs 911; FFN2 (K = 3072) keeps variant 9
+        // (1159 vs 1106), profiles/r4_gemm_bench.json
+        if (auto_v && K >= 2048) {
+          if (bias) hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, true, false>), dim3(G), dim3(512), 0, s, A, W, bias, R, C,
+                                       M, N, K, tiles_n, ntiles);
+          else hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, false, false>), dim3(G), dim3(512), 0, s, A, W, bias, R, C,
+                                  M, N, K, tiles_n, ntiles);
+          return;
+        }
+        const bool nt = g_gemm_variant == 13 || auto_v;
+#define LPP3(HB, NT)                                                                                               \
+  hipLaunchKernelGGL((gemm_nt_pp3_kernel<ACT, HB, false, NT>), dim3(G), dim3(512), 0, s, A, W, bias, C, M, N, K, tiles_n, \
+                     ntiles)
+        if (bias && nt) LPP3(true, true);
+        else if (bias) LPP3(true, false);
+        else if (nt) LPP3(false, true);
+        else LPP3(false, false);
+#undef LPP3
+        return;
+      }
     }
-    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
-    dim3 grid(G), block(512);
 #define LPP2(HB, HR)                                                                                          \
-  do {                                                                                                        \
-    if (!HR && g_gemm_variant == 10)                                                                          \
-      hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, HB, false, true>), grid, block, 0, s, A, W, bias, R, C, M, N, \
-                         K, tiles_n, ntiles);                                                                 \
-    else                                                                                                      \
-      hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K,       \
-                         tiles_n, ntiles);                                                                    \
-  } while (0)
+  hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, HB, HR>), dim3(G), dim3(512), 0, s, A, W, bias, R, C, M, N, K, tiles_n, \
+                     ntiles)
     if (bias && R) LPP2(true, true);
     else if (bias) LPP2(true, false);
     else if (R) LPP2(false, true);
@@ -1255,89 +1066,19 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
 #undef LPP2
     return;
   }
-  const bool pp = g_gemm_variant == 6 || g_gemm_variant == 7 || g_gemm_variant < 0;
-  if (big && N % BN2 == 0 && pp && K >= 128 && (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
+  // outside that domain (unpadded C, offsets past 2^31 elements): variant 6 (row-predicated
+  // stores) while the 32-bit offsets hold, else the 128x128 kernel (64-bit addressing)
+  if (big && N % BN2 == 0 && K >= 128 && (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
     const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
-    if (g_num_cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (g_num_cus <= 0) g_num_cus = 256;
-    }
-    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
-    dim3 grid(G), block(512);
-#define LPP(HB, HR)                                                                                       \
-  do {                                                                                                    \
-    if (g_gemm_variant == 7) /* diagnostic: no stores (timing only, output undefined) */                  \
-      hipLaunchKernelGGL((gemm_nt_pp_kernel<ACT, HB, HR, 1>), grid, block, 0, s, A, W, bias, R, C, M, N, K, \
-                         tiles_n, ntiles);                                                                \
-    else                                                                                                  \
-      hipLaunchKernelGGL((gemm_nt_pp_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K,    \
-                         tiles_n, ntiles);                                                                \
-  } while (0)
+    const int G = ntiles < num_cus() ? ntiles : num_cus();
+#define LPP(HB, HR)                                                                                        \
+  hipLaunchKernelGGL((gemm_nt_pp_kernel<ACT, HB, HR>), dim3(G), dim3(512), 0, s, A, W, bias, R, C, M, N, K, tiles_n, \
+                     ntiles)
     if (bias && R) LPP(true, true);
     else if (bias) LPP(true, false);
     else if (R) LPP(false, true);
     else LPP(false, false);
 #undef LPP
-    return;
-  }
-  if (big && N % BN2 == 0 && g_gemm_variant == 3 && K % BK3 == 0) {
-    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
-    if (g_num_cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (g_num_cus <= 0) g_num_cus = 256;
-    }
-    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
-    dim3 grid(G), block(512);
-#define LS(HB, HR) hipLaunchKernelGGL((gemm_nt_256s_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n, ntiles)
-    if (bias && R) LS(true, true);
-    else if (bias) LS(true, false);
-    else if (R) LS(false, true);
-    else LS(false, false);
-#undef LS
-    return;
-  }
-  if (big && N % BN2 == 0 && g_gemm_variant != 1) {
-    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
-    if (g_num_cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (g_num_cus <= 0) g_num_cus = 256;
-    }
-    int G = ntiles < g_num_cus ? ntiles : g_num_cus;
-    dim3 grid(G), block(512);
-#define LP(HB, HR)                                                                                          \
-  do {                                                                                                      \
-    if (g_gemm_variant == 4)                                                                                \
-      hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR, true>), grid, block, 0, s, A, W, bias, R, C, M, N, K, \
-                         tiles_n, ntiles);                                                                   \
-    else if (g_gemm_variant == 5 || g_gemm_variant < 0)                                                      \
-      hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR, true, true>), grid, block, 0, s, A, W, bias, R, C, M, N, \
-                         K, tiles_n, ntiles);                                                                \
-    else                                                                                                    \
-      hipLaunchKernelGGL((gemm_nt_256p_kernel<ACT, HB, HR, false>), grid, block, 0, s, A, W, bias, R, C, M, N,   \
-                         K, tiles_n, ntiles);                                                                \
-  } while (0)
-    if (bias && R) LP(true, true);
-    else if (bias) LP(true, false);
-    else if (R) LP(false, true);
-    else LP(false, false);
-#undef LP
-    return;
-  }
-  if (big && N % BN2 == 0) {
-    const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2;
-    dim3 grid(tiles_m * tiles_n), block(512);
-#define L2(HB, HR) hipLaunchKernelGGL((gemm_nt_256_kernel<ACT, HB, HR>), grid, block, 0, s, A, W, bias, R, C, M, N, K, tiles_n)
-    if (bias && R) L2(true, true);
-    else if (bias) L2(true, false);
-    else if (R) L2(false, true);
-    else L2(false, false);
-#undef L2
     return;
   }
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
@@ -1382,22 +1123,23 @@ extern "C" int fr_gemm_nt_bf16(const void* A, const void* W, const float* bias, 
 extern "C" int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,
                                      int c_rows, const int* full_rows, int n_partial, hipStream_t s) {
   if (N % BN != 0 || K % BK != 0 || M <= 0) return 1;
-  const bool ok = (g_gemm_variant == 9 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 && N <= PP2_MAXN &&
-                  K >= 128 && n_partial % BN2 == 0 && n_partial > 0 && n_partial <= N &&
-                  c_rows >= ((M + 255) / 256) * 256 && (long long)M * K < (1ll << 31) &&
-                  (long long)N * K < (1ll << 31);
+  const bool ok = (g_gemm_variant == 9 || g_gemm_variant >= 12 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 &&
+                  n_partial % BN2 == 0 && n_partial > 0 && n_partial <= N && pp_domain(M, N, K, c_rows);
   if (!ok) return fr_gemm_nt_bf16(A, W, bias, nullptr, C, M, N, K, 0, c_rows, s);
   const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles_max = tiles_m * tiles_n;
-  if (g_num_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_num_cus <= 0) g_num_cus = 256;
-  }
-  const int G = ntiles_max < g_num_cus ? ntiles_max : g_num_cus;
+  const int G = ntiles_max < num_cus() ? ntiles_max : num_cus();
   const bf16* a = (const bf16*)A;
   const bf16* w = (const bf16*)W;
   bf16* c = (bf16*)C;
+  if (g_gemm_variant != 9) {
+    if (bias)
+      hipLaunchKernelGGL((gemm_nt_pp3_kernel<0, true, false, true>), dim3(G), dim3(512), 0, s, a, w, bias, c, M, N, K,
+                         tiles_n, ntiles_max, full_rows, n_partial / BN2);
+    else
+      hipLaunchKernelGGL((gemm_nt_pp3_kernel<0, false, false, true>), dim3(G), dim3(512), 0, s, a, w, bias, c, M, N,
+                         K, tiles_n, ntiles_max, full_rows, n_partial / BN2);
+    return 0;
+  }
   if (bias)
     hipLaunchKernelGGL((gemm_nt_pp2_kernel<0, true, false>), dim3(G), dim3(512), 0, s, a, w, bias, nullptr, c, M, N, K,
                        tiles_n, ntiles_max, full_rows, n_partial / BN2);
@@ -1414,18 +1156,11 @@ extern "C" int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* 
 // the host side in a fixed order).  Variant-9 kernel only: returns 3 outside its domain.
 extern "C" int fr_gemm_gelu_bwd_colpart(const void* A, const void* W, const void* Z, void* C, float* colpart, int M,
                                         int N, int K, int c_rows, hipStream_t s) {
-  const bool ok = (g_gemm_variant == 9 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 && N <= PP2_MAXN &&
-                  K >= 128 && K % BK == 0 && c_rows >= ((M + 255) / 256) * 256 &&
-                  (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31);
+  const bool ok = (g_gemm_variant == 9 || g_gemm_variant >= 12 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 &&
+                  K % BK == 0 && pp_domain(M, N, K, c_rows);
   if (!ok) return 3;
   const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
-  if (g_num_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_num_cus <= 0) g_num_cus = 256;
-  }
-  const int G = ntiles < g_num_cus ? ntiles : g_num_cus;
+  const int G = ntiles < num_cus() ? ntiles : num_cus();
   hipLaunchKernelGGL((gemm_nt_pp2_kernel<3, false, true>), dim3(G), dim3(512), 0, s, (const bf16*)A, (const bf16*)W,
                      nullptr, (const bf16*)Z, (bf16*)C, M, N, K, tiles_n, ntiles, nullptr, 0, nullptr, colpart);
   return 0;
@@ -1433,19 +1168,17 @@ extern "C" int fr_gemm_gelu_bwd_colpart(const void* A, const void* W, const void
 
 extern "C" int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* bias, void* C, void* Z, int M, int N, int K,
                                     int c_rows, hipStream_t s) {
-  const bool ok = (g_gemm_variant == 9 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 && N <= PP2_MAXN &&
-                  K >= 128 && K % BK == 0 && bias != nullptr && c_rows >= ((M + 255) / 256) * 256 &&
-                  (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31);
+  const bool ok = (g_gemm_variant == 9 || g_gemm_variant >= 12 || g_gemm_variant < 0) && M >= 4096 && N % BN2 == 0 &&
+                  K % BK == 0 && bias != nullptr && pp_domain(M, N, K, c_rows);
   if (!ok) return 3;
   const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
-  if (g_num_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_num_cus <= 0) g_num_cus = 256;
+  const int G = ntiles < num_cus() ? ntiles : num_cus();
+  if (g_gemm_variant != 9) {
+    hipLaunchKernelGGL((gemm_nt_pp3_kernel<1, true, true, true>), dim3(G), dim3(512), 0, s, (const bf16*)A, (const bf16*)W,
+                       bias, (bf16*)C, M, N, K, tiles_n, ntiles, nullptr, 0, (bf16*)Z);
+    return 0;
   }
-  const int G = ntiles < g_num_cus ? ntiles : g_num_cus;
-  hipLaunchKernelGGL((gemm_nt_pp2_kernel<1, true, false, false, true>), dim3(G), dim3(512), 0, s, (const bf16*)A,
+  hipLaunchKernelGGL((gemm_nt_pp2_kernel<1, true, false, true>), dim3(G), dim3(512), 0, s, (const bf16*)A,
                      (const bf16*)W, bias, nullptr, (bf16*)C, M, N, K, tiles_n, ntiles, nullptr, 0, (bf16*)Z);
   return 0;
 }

@@ -327,6 +327,8 @@ class LocalEngine:
             return te.head(hid, mask)
 
     # -------------------------------------------------------------------------------
+    DEDUP_SYNC_MAX = 8192  # csrc dedup (one kernel chain, then the count read) up to this many ids
+
     def prepare(self, batch_fn: Callable[[], Tuple]) -> Prepared:
         """Sample a batch (``batch_fn() -> (cand, his)``) and de-duplicate its news ids.  On the
         GPU both run on the lookahead stream: the only host wait (the unique count) waits for
@@ -343,10 +345,17 @@ class LocalEngine:
             c, h = self.to_device(c), self.to_device(h)
             ids = torch.cat([c.reshape(-1), h.reshape(-1)])
             dd = ops.dedup(ids, self.N)
-            ev = torch.cuda.Event()
-            ev.record(self._prep)
+            ev = None
+            if ids.numel() > self.DEDUP_SYNC_MAX:  # the sort path queues work after its count read
+                ev = torch.cuda.Event()
+                ev.record(self._prep)
         for t in (c, h, *dd):
             t.record_stream(main)
+        # otherwise no event for the main stream to wait on: the dedup's unique count is a host
+        # read on the lookahead stream, the last work queued there for this batch, so when it
+        # returns every lookahead kernel of the batch has completed (kernel completion publishes
+        # its writes at agent scope).  A per-step hipStreamWaitEvent measured ~33 us of device
+        # idle between steps (profiles/r4_graph_gap.json).
         return Prepared(c, h, tuple(dd), ev)
 
     def _forward_rows(self, cand: torch.Tensor, his: torch.Tensor, grad_news: bool, pre: Optional[Prepared] = None):
