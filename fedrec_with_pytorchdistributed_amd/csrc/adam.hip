@@ -53,30 +53,27 @@ extern "C" int fr_adam_flat(float* p, const float* g, float* m, float* v, void* 
 // ---------------------------------------------------------------------------------------
 // The same step with the step count on the device, for a HIP graph that captures the whole
 // training step (forward, backward, Adam) when no gradient all-reduce sits between the
-// backward and the optimizer (one client): every block reads t = step + 1 and forms the bias
-// corrections itself (in double, then rounded as the host path rounds them); block 0 also
-// copies this step's loss into slot (t - 1) % ring of a loss ring (no per-step clone launch);
-// the block that takes the last ticket advances the step and re-arms the ticket.  Every block
-// reads the step before it takes its ticket, so the last one writes after all reads.
+// backward and the optimizer (one client): every block reads t (the step's cast launch -- the
+// graph's first kernel -- advanced the counter) and forms the bias corrections itself (in
+// double, then rounded as the host path rounds them); block 0 also copies this step's loss
+// into slot (t - 1) % ring of a loss ring (no per-step clone launch).
 namespace {
 __global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                        float4* __restrict__ m, float4* __restrict__ v,
                                                        bf16x4* __restrict__ plow, long n4, float lr, float b1, float b2,
-                                                       float eps, float gs, long long* __restrict__ step,
-                                                       unsigned* __restrict__ ticket, const float* __restrict__ loss,
-                                                       float* __restrict__ ring, int ring_n) {
-  // the step count and the bias corrections once per block (double pow, as the host computes
-  // them for the eager kernel: a per-thread double pow made this launch 3x the eager one)
-  __shared__ long long t_s;
+                                                       float eps, float gs, const long long* __restrict__ step,
+                                                       const float* __restrict__ loss, float* __restrict__ ring,
+                                                       int ring_n) {
+  // t = the device step count, already advanced for this step by the step's cast launch (an
+  // earlier kernel of the same stream): no read-modify-write here (a same-address ticket per
+  // block made this launch 20 us, against 7 for the eager kernel)
   __shared__ float bc_s[2];
-  if (threadIdx.x == 0) {
-    const long long t0 = __hip_atomic_load(step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    t_s = t0;
-    bc_s[0] = (float)(1.0 - pow((double)b1, (double)t0));
-    bc_s[1] = (float)(1.0 - pow((double)b2, (double)t0));
+  const long long t = step[0];
+  if (threadIdx.x == 0) {  // double pow once per block, as the host computes them for the eager kernel
+    bc_s[0] = (float)(1.0 - pow((double)b1, (double)t));
+    bc_s[1] = (float)(1.0 - pow((double)b2, (double)t));
   }
   __syncthreads();
-  const long long t = t_s;
   const float bc1 = bc_s[0], bc2 = bc_s[1];
   const float step_size = lr / bc1, inv_sqrt_bc2 = 1.0f / sqrtf(bc2);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
@@ -99,31 +96,22 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, c
     if (plow) plow[i] = bf16x4{f2bf(pa[0]), f2bf(pa[1]), f2bf(pa[2]), f2bf(pa[3])};
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && ring != nullptr) ring[(t - 1) % ring_n] = loss[0];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned k = atomicAdd(ticket, 1u);
-    if (k == gridDim.x - 1) {
-      __hip_atomic_store(step, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 }  // namespace
 
 extern "C" int fr_adam_dev(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1,
-                           float b2, float eps, float grad_scale, long long* step, unsigned* ticket, const float* loss,
-                           float* ring, int ring_n, hipStream_t s) {
+                           float b2, float eps, float grad_scale, const long long* step, const float* loss, float* ring,
+                           int ring_n, hipStream_t s) {
   if (n % 4 != 0 || (ring != nullptr && (loss == nullptr || ring_n < 1))) return 1;
   const long n4 = n / 4;
   long blocks = (n4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (float4*)p, (const float4*)g, (float4*)m,
-                     (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, grad_scale, step, ticket, loss, ring, ring_n);
+                     (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, grad_scale, step, loss, ring, ring_n);
   return 0;
 }
-
 // ---------------------------------------------------------------------------------------
 // Compute-weight refresh of the unfrozen backbone after an optimizer step: up to MCAST_SEG
 // fp32 master tensors -> their bf16 (or fp32) compute copies in ONE launch, 8 elements per
@@ -145,9 +133,9 @@ struct MultiCast {
   int blk0[MCAST_SEG + 1];
   unsigned char bf[MCAST_SEG];   // 1: bf16 destination, 0: fp32
   unsigned char vec[MCAST_SEG];  // 1: 16-byte aligned (vector path), 0: element by element
-  int trc[MCAST_SEG];            // > 0: transposed segment -- source [n / trc, trc] -> dst [trc, n / trc]
   int nseg;
-  long long* bump;  // optional: a device step counter advanced by one (block 0, lane 0)
+  long long* bump;   // optional: a device step counter advanced by one (block 0, lane 0)
+  long long* bump2;  // optional: a second one (the in-graph Adam's step count)
 };
 
 __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
@@ -158,22 +146,13 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
     else hi = mid - 1;
   }
   const int sg = lo;
-  if (mc.bump != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *mc.bump += 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (mc.bump != nullptr) *mc.bump += 1;
+    if (mc.bump2 != nullptr) *mc.bump2 += 1;
+  }
   const long base = (long)(blockIdx.x - mc.blk0[sg]) * MCAST_CHUNK;
   const float4* s4 = (const float4*)mc.src[sg];
   const long n = mc.n[sg];
-  if (mc.trc[sg] > 0) {  // transposed (small weights: element stores, strided)
-    const int C = mc.trc[sg];
-    const long R = n / C;
-    for (int it = 0; it < MCAST_CHUNK / (256 * 8); ++it) {
-      const long e = base + ((long)it * 256 + threadIdx.x) * 8;
-      for (int j = 0; j < 8 && e + j < n; ++j) {
-        const long r = (e + j) / C, c = (e + j) - r * C;
-        ((bf16*)mc.dst[sg])[c * R + r] = f2bf(mc.src[sg][e + j]);
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int it = 0; it < MCAST_CHUNK / (256 * 8); ++it) {
     const long e = base + ((long)it * 256 + threadIdx.x) * 8;
@@ -202,11 +181,12 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
 // bump (optional): an int64 device counter the launch advances by one -- the training step's
 // dropout / noise offset rides in the step's cast launch instead of a launch of its own
 extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                             long long* bump, hipStream_t s, const int* trc) {
+                             long long* bump, hipStream_t s, long long* bump2) {
   if (nseg < 1 || nseg > MCAST_SEG) return 1;
   MultiCast mc{};
   mc.nseg = nseg;
   mc.bump = bump;
+  mc.bump2 = bump2;
   long blk = 0;
   for (int i = 0; i < nseg; ++i) {
     if (n[i] <= 0) return 1;
@@ -215,8 +195,6 @@ extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const lo
     mc.dst[i] = dst[i];
     mc.n[i] = n[i];
     mc.bf[i] = to_bf16[i] ? 1 : 0;
-    mc.trc[i] = trc != nullptr ? trc[i] : 0;
-    if (mc.trc[i] > 0 && (!mc.bf[i] || n[i] % mc.trc[i] != 0)) return 1;
     mc.blk0[i] = (int)blk;
     blk += (n[i] + MCAST_CHUNK - 1) / MCAST_CHUNK;
   }

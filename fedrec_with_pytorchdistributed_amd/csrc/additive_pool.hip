@@ -579,298 +579,3 @@ extern "C" int fr_upool_bwd_da(const float* x, const float* e, const float* alph
                      D, Q, da8);
   return 0;
 }
-
-// ---------------------------------------------------------------------------------------
-// The user encoder's att_fc1 + additive pool in ONE launch (reference attention.py:14-26 over
-// the MHSA output): per impression n (one block), for its T <= 64 rows x_t of
-// ctx [n, T, D] (fp32, D <= 512):
-//     e_t = tanh(W1 x_t + b1)  (W1 [Q, D] bf16 stack slice, Q <= 256; stored fp32 for the backward)
-//     a_t = w2 . e_t + b2,  alpha = eps-softmax(a) (masked keys: 0),  u = sum_t alpha_t x_t.
-// The product runs on v_mfma_f32_16x16x32_bf16 with the x rows rounded to bf16 in LDS and W1
-// fragments loaded straight from L2 (each wave owns every fourth 16-column tile of Q, so the
-// block reads W1 once); operands, k order and epilogue are the small-GEMM launch's, so e is
-// bitwise the two-launch path's.  The score is reduced from the accumulators (lane rows x its
-// wave's columns, then 16 lanes, then the 4 waves through LDS), alpha and u as upool_fwd.
-// Replaces the att_fc1 small GEMM (15 us) + upool_fwd (7.6 us) of the config-2 step.
-constexpr int UF_KP = 512 + 8;  // LDS row stride of the bf16 x image (bf16 elements)
-constexpr int UF_PF = 2;        // W1 k-steps in flight ahead of the MFMAs
-
-__global__ __launch_bounds__(256) void upool_fc_fwd_kernel(const float* __restrict__ x, const bf16* __restrict__ W1,
-                                                           const float* __restrict__ b1, const float* __restrict__ w2,
-                                                           const float* __restrict__ b2, float* __restrict__ e_out,
-                                                           float* __restrict__ out, float* __restrict__ alpha_out,
-                                                           int T, int D, int Q, const int* __restrict__ keep) {
-  __shared__ __attribute__((aligned(16))) bf16 xs[UT][UF_KP];
-  __shared__ float part[4][UT];
-  __shared__ float a_s[UT];
-  __shared__ float4 red[8][32];
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const float* xn = x + (size_t)n * T * D;
-  const int KS = (D + 31) >> 5, D4 = D >> 2;
-  // x rows -> bf16 image (rows >= T and k in [D, 32 KS) zero)
-  for (int i = tid; i < UT * (KS * 8); i += 256) {
-    const int r = i / (KS * 8), c4 = i - r * (KS * 8);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < T && c4 < D4) v = ((const float4*)(xn + (size_t)r * D))[c4];
-    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-    *(bf16x4_t*)&xs[r][c4 * 4] = bf16x4_t{f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
-  }
-  // this wave's 16-column tiles of Q: j = wave + 4 s (s < NS)
-  const int NT = (Q + 15) >> 4;
-  constexpr int NS = 4;  // Q <= 256
-  f32x4 acc[4][NS];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int s = 0; s < NS; ++s) acc[i][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 wb[UF_PF + 1][NS];
-  auto load_w = [&](int ks, bf16x8 (&dst)[NS]) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int j = wave + 4 * s, row = j * 16 + fr, k = ks * 32 + fq * 8;
-      bf16x8 v = {};
-      if (j < NT && row < Q && ks < KS) {
-        if (k + 8 <= D) {
-          v = *(const bf16x8*)(W1 + (size_t)row * D + k);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = k + q < D ? W1[(size_t)row * D + k + q] : (__bf16)0.f;
-        }
-      }
-      dst[s] = v;
-    }
-  };
-#pragma unroll
-  for (int p = 0; p < UF_PF; ++p) load_w(p, wb[p]);
-  __syncthreads();  // the x image is complete
-  for (int ks = 0; ks < KS; ++ks) {
-    bf16x8 cur[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) cur[s] = wb[0][s];
-#pragma unroll
-    for (int p = 0; p < UF_PF - 1; ++p)
-#pragma unroll
-      for (int s = 0; s < NS; ++s) wb[p][s] = wb[p + 1][s];
-    load_w(ks + UF_PF, wb[UF_PF - 1]);
-    bf16x8 a[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)&xs[i * 16 + fr][ks * 32 + fq * 8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < NS; ++s) acc[i][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], cur[s], acc[i][s], 0, 0, 0);
-  }
-  // epilogue: lane holds C[m = 16 i + 4 fq + r][q = 16 (wave + 4 s) + fr]
-  float rs[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rs[i][r] = 0.f;
-  float* en = e_out + (size_t)n * T * Q;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int q = (wave + 4 * s) * 16 + fr;
-    const bool qok = q < Q;
-    const float bq = qok ? b1[q] : 0.f, wq = qok ? w2[q] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = i * 16 + fq * 4 + r;
-        const float v = tanhf(acc[i][s][r] + bq);
-        if (qok && m < T) en[(size_t)m * Q + q] = v;
-        rs[i][r] += wq * v;
-      }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = rs[i][r];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      if (fr == 0) part[wave][i * 16 + fq * 4 + r] = v;
-    }
-  __syncthreads();
-  if (tid < T) {
-    const float a = ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid])) + b2[0];
-    a_s[tid] = (keep == nullptr || keep[(size_t)n * T + tid] != 0) ? a : -INFINITY;
-  }
-  __syncthreads();
-  upool_softmax(a_s, T);
-  __syncthreads();
-  if (tid < T) alpha_out[(size_t)n * T + tid] = a_s[tid];
-  // u = sum_t alpha_t x_t (fp32 x, L2-hot): 8 t-groups x 32 float4 columns per pass
-  const int tg = tid >> 5, c = tid & 31;
-  for (int c0 = 0; c0 < D4; c0 += 32) {
-    float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c0 + c < D4) {
-      const float4* xr = (const float4*)xn + c0 + c;
-      for (int t = tg; t < T; t += 8) {
-        const float4 v = xr[(size_t)t * D4];
-        const float al = a_s[t];
-        s4.x += al * v.x; s4.y += al * v.y; s4.z += al * v.z; s4.w += al * v.w;
-      }
-    }
-    red[tg][c] = s4;
-    __syncthreads();
-    if (tid < 32 && c0 + tid < D4) {
-      float4 s = red[0][tid];
-#pragma unroll
-      for (int j = 1; j < 8; ++j) {
-        s.x += red[j][tid].x; s.y += red[j][tid].y; s.z += red[j][tid].z; s.w += red[j][tid].w;
-      }
-      ((float4*)(out + (size_t)n * D))[c0 + tid] = s;
-    }
-    __syncthreads();
-  }
-}
-
-extern "C" int fr_upool_fc_fwd(const float* x, const void* W1, const float* b1, const float* w2, const float* b2,
-                               float* e, float* out, float* alpha, int n, int T, int D, int Q, const int* keep,
-                               hipStream_t s) {
-  if (T < 1 || T > UT || D % 16 != 0 || D > 512 || Q % 4 != 0 || Q > 256 || Q < 16) return 1;
-  const uintptr_t al = (uintptr_t)x | (uintptr_t)W1 | (uintptr_t)out;
-  if (al & 15) return 3;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(upool_fc_fwd_kernel, dim3(n), dim3(256), 0, s, x, (const bf16*)W1, b1, w2, b2, e, out, alpha, T, D,
-                     Q, keep);
-  return 0;
-}
-
-// ---------------------------------------------------------------------------------------
-// Its backward in ONE launch: per impression n, with du = g [D]:
-//     dalpha_t = x_t . g,  da_t = alpha_t (dalpha_t - sum alpha dalpha)   (da8: column 0 of [n T, 8])
-//     dpre_t = da_t w2 (.) (1 - e_t^2)                                     (fp32, for dW1 = dpre^T x)
-//     dx_t = alpha_t g + dpre_t W1                                         (the MHSA output's gradient)
-// dpre W1 on v_mfma_f32_16x16x32_bf16: dpre rounded to bf16 in LDS (A), W1 fragments from the
-// transposed bf16 compute copy W1t [D, Q] in L2 (B: 8 consecutive q of one d per lane); the same
-// operands and k order as the small-GEMM accumulate launch it replaces, with upool_bwd's da.
-// Replaces upool_bwd (8.3 us) + the dctx small GEMM (15 us) of the config-2 step.
-constexpr int UF_QP = 256 + 8;  // LDS row stride of the bf16 dpre image
-
-__global__ __launch_bounds__(256) void upool_fc_bwd_kernel(const float* __restrict__ x, const float* __restrict__ e,
-                                                           const float* __restrict__ alpha, const float* __restrict__ w2,
-                                                           const float* __restrict__ g, const bf16* __restrict__ W1t,
-                                                           float* __restrict__ dx, float* __restrict__ dpre,
-                                                           float* __restrict__ da8, int T, int D, int Q) {
-  __shared__ __attribute__((aligned(16))) bf16 ps[UT][UF_QP];
-  __shared__ float da_s[UT], al_s[UT];
-  __shared__ float part[UT][4];
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const float* xe = x + (size_t)n * T * D;
-  const float* gn = g + (size_t)n * D;
-  if (tid < T) al_s[tid] = alpha[(size_t)n * T + tid];
-  {  // dalpha_t = x_t . g: lane (t, quarter) -- upool_bwd_kernel's order
-    const int t = tid >> 2, pq = tid & 3, D4 = D >> 2, per = (D4 + 3) >> 2;
-    float acc = 0.f;
-    if (t < T) {
-      const float4* xr = (const float4*)(xe + (size_t)t * D);
-      const float4* gr = (const float4*)gn;
-#pragma unroll 5
-      for (int c = pq * per; c < min(D4, (pq + 1) * per); ++c) {
-        const float4 v = xr[c], w = gr[c];
-        acc += v.x * w.x + v.y * w.y + v.z * w.z + v.w * w.w;
-      }
-    }
-    part[t][pq] = acc;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    const float dal = tid < T ? (part[tid][0] + part[tid][1]) + (part[tid][2] + part[tid][3]) : 0.f;
-    const float al = tid < T ? al_s[tid] : 0.f;
-    const float s = wave_sum(al * dal);
-    const float da = al * (dal - s);
-    if (tid < T) {
-      da_s[tid] = da;
-      float4* o = (float4*)(da8 + ((size_t)n * T + tid) * 8);
-      o[0] = make_float4(da, 0.f, 0.f, 0.f);
-      o[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  __syncthreads();
-  const int KQ = (Q + 31) & ~31, Q4 = Q >> 2;
-  {  // dpre rows (fp32 out) + the bf16 image (rows >= T and columns >= Q zero)
-    const int tg = tid >> 6, qc = tid & 63;  // 4 row groups x 64 float4 columns (Q4 <= 64)
-    const float4 w = qc < Q4 ? ((const float4*)w2)[qc] : make_float4(0.f, 0.f, 0.f, 0.f);
-    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-    for (int t = tg; t < UT; t += 4) {
-      if (qc * 4 >= KQ) continue;
-      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (t < T && qc < Q4) {
-        const float4 v = ((const float4*)(e + ((size_t)n * T + t) * Q))[qc];
-        const float da = da_s[t];
-        d = make_float4(da * w.x * (1.f - v.x * v.x), da * w.y * (1.f - v.y * v.y), da * w.z * (1.f - v.z * v.z),
-                        da * w.w * (1.f - v.w * v.w));
-        ((float4*)(dpre + ((size_t)n * T + t) * Q))[qc] = d;
-      }
-      *(bf16x4_t*)&ps[t][qc * 4] = bf16x4_t{f2bf(d.x), f2bf(d.y), f2bf(d.z), f2bf(d.w)};
-    }
-  }
-  __syncthreads();
-  // dpre W1: wave w owns the 16-column tiles j = w + 4 s of D
-  constexpr int NS = 8;  // D <= 512
-  const int NT = (D + 15) >> 4, KS = KQ >> 5;
-  f32x4 acc[4][NS];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int s = 0; s < NS; ++s) acc[i][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto load_w = [&](int ks, bf16x8 (&dst)[NS]) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int j = wave + 4 * s, d = j * 16 + fr, q = ks * 32 + fq * 8;
-      bf16x8 v = {};
-      if (j < NT && d < D && ks < KS && q < Q) v = *(const bf16x8*)(W1t + (size_t)d * Q + q);  // Q % 8 == 0
-      dst[s] = v;
-    }
-  };
-  bf16x8 wnext[NS];
-  load_w(0, wnext);
-  for (int ks = 0; ks < KS; ++ks) {
-    bf16x8 cur[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) cur[s] = wnext[s];
-    load_w(ks + 1, wnext);
-    bf16x8 a[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)&ps[i * 16 + fr][ks * 32 + fq * 8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if (wave + 4 * s < NT) acc[i][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], cur[s], acc[i][s], 0, 0, 0);
-  }
-  // dx[m][d] = acc + alpha_m g_d (the small-GEMM accumulate epilogue: v = acc, then + dx_direct)
-  float* dxn = dx + (size_t)n * T * D;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int d = (wave + 4 * s) * 16 + fr;
-    if (wave + 4 * s >= NT || d >= D) continue;
-    const float gd = gn[d];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = i * 16 + fq * 4 + r;
-        if (m < T) dxn[(size_t)m * D + d] = acc[i][s][r] + al_s[m] * gd;
-      }
-  }
-}
-
-extern "C" int fr_upool_fc_bwd(const float* x, const float* e, const float* alpha, const float* w2, const float* g,
-                               const void* W1t, float* dx, float* dpre, float* da8, int n, int T, int D, int Q,
-                               hipStream_t s) {
-  if (T < 1 || T > UT || D % 16 != 0 || D > 512 || Q % 8 != 0 || Q > 256 || Q < 16) return 1;
-  const uintptr_t al = (uintptr_t)x | (uintptr_t)e | (uintptr_t)w2 | (uintptr_t)g | (uintptr_t)W1t | (uintptr_t)dpre |
-                       (uintptr_t)da8;
-  if (al & 15) return 3;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(upool_fc_bwd_kernel, dim3(n), dim3(256), 0, s, x, e, alpha, w2, g, (const bf16*)W1t, dx, dpre, da8,
-                     T, D, Q);
-  return 0;
-}

@@ -72,8 +72,8 @@ void fr_segsum_set_variant(int v);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
                 unsigned long long offset, hipStream_t s, const unsigned long long* dev_off);
 int fr_adam_dev(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
-                float eps, float grad_scale, long long* step, unsigned* ticket, const float* loss, float* ring,
-                int ring_n, hipStream_t s);
+                float eps, float grad_scale, const long long* step, const float* loss, float* ring, int ring_n,
+                hipStream_t s);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
@@ -112,17 +112,12 @@ int fr_secagg_unmask_exact(const int* x, float* out, long n, const int* H, int W
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, int tile, hipStream_t s);
 int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                  long long* bump, hipStream_t s,
-                  const int* trc);
+                  long long* bump, hipStream_t s, long long* bump2);
 int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, const int* C, const int* ld, int nseg,
                     hipStream_t s);
 int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
                   hipStream_t s);
 long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part, hipStream_t s);
-int fr_upool_fc_fwd(const float* x, const void* W1, const float* b1, const float* w2, const float* b2, float* e,
-                    float* out, float* alpha, int n, int T, int D, int Q, const int* keep, hipStream_t s);
-int fr_upool_fc_bwd(const float* x, const float* e, const float* alpha, const float* w2, const float* g, const void* W1t,
-                    float* dx, float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s);
 int fr_upool_bwd_da(const float* x, const float* e, const float* alpha, const float* w2, const float* g, float* dx,
                     float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
@@ -604,63 +599,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad(const at::
   return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
 }
 
-// user att_fc1 + tanh + additive pool forward in one launch (fr_upool_fc_fwd): x [n, T, D]
-// fp32 (the MHSA output), W1 [Q, D] bf16 -> (u [n, D], e [n, T, Q], alpha [n, T])
-std::tuple<at::Tensor, at::Tensor, at::Tensor> upool_fc_fwd(const at::Tensor& x, const at::Tensor& W1,
-                                                            const at::Tensor& b1, const at::Tensor& w2,
-                                                            const at::Tensor& b2, const c10::optional<at::Tensor>& keep) {
-  for (auto* t : {&x, &W1, &b1, &w2, &b2}) check_dev(*t, "upool_fc_fwd input");
-  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 3, "fedrec::upool_fc_fwd: x fp32 [n, T, D]");
-  TORCH_CHECK(W1.scalar_type() == at::kBFloat16 && W1.is_contiguous() && W1.dim() == 2, "fedrec::upool_fc_fwd: W1 bf16 [Q, D]");
-  for (auto* t : {&b1, &w2, &b2})
-    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "fedrec::upool_fc_fwd: fp32 b1 / w2 / b2");
-  const c10::DeviceGuard dg(x.device());
-  const int64_t n = x.size(0), T = x.size(1), D = x.size(2), Q = W1.size(0);
-  TORCH_CHECK(W1.size(1) == D && b1.numel() == Q && w2.numel() == Q && b2.numel() == 1, "fedrec::upool_fc_fwd: shapes");
-  const int* kp = nullptr;
-  if (keep.has_value() && keep->defined()) {
-    check_dev(*keep, "keep");
-    TORCH_CHECK(keep->scalar_type() == at::kInt && keep->is_contiguous() && keep->numel() == n * T,
-                "fedrec::upool_fc_fwd: keep int32 [n, T]");
-    kp = keep->data_ptr<int>();
-  }
-  auto u = at::empty({n, D}, x.options());
-  auto e = at::empty({n, T, Q}, x.options());
-  auto alpha = at::empty({n, T}, x.options());
-  check_rc(fr_upool_fc_fwd(x.data_ptr<float>(), W1.data_ptr(), b1.data_ptr<float>(), w2.data_ptr<float>(),
-                           b2.data_ptr<float>(), e.data_ptr<float>(), u.data_ptr<float>(), alpha.data_ptr<float>(),
-                           (int)n, (int)T, (int)D, (int)Q, kp, cur_stream()),
-           "upool_fc_fwd");
-  return {u, e, alpha};
-}
-
-// its backward in one launch (fr_upool_fc_bwd): -> (dx [n, T, D] = alpha g + dpre W1, dpre [n, T, Q],
-// da8 [n T, 8]); W1t = the transposed bf16 compute copy [D, Q]
-std::tuple<at::Tensor, at::Tensor, at::Tensor> upool_fc_bwd(const at::Tensor& x, const at::Tensor& e,
-                                                            const at::Tensor& alpha, const at::Tensor& w2,
-                                                            const at::Tensor& g, const at::Tensor& W1t) {
-  for (auto* t : {&x, &e, &alpha, &w2, &g}) {
-    check_dev(*t, "upool_fc_bwd input");
-    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "fedrec::upool_fc_bwd: contiguous fp32");
-  }
-  check_dev(W1t, "W1t");
-  TORCH_CHECK(W1t.scalar_type() == at::kBFloat16 && W1t.is_contiguous() && W1t.dim() == 2,
-              "fedrec::upool_fc_bwd: W1t bf16 [D, Q]");
-  const c10::DeviceGuard dg(x.device());
-  const int64_t n = x.size(0), T = x.size(1), D = x.size(2), Q = e.size(2);
-  TORCH_CHECK(e.size(0) == n && e.size(1) == T && alpha.numel() == n * T && w2.numel() == Q && g.numel() == n * D &&
-                  W1t.size(0) == D && W1t.size(1) == Q,
-              "fedrec::upool_fc_bwd: shapes");
-  auto dx = at::empty({n, T, D}, x.options());
-  auto dpre = at::empty({n, T, Q}, x.options());
-  auto da8 = at::empty({n * T, 8}, x.options());
-  check_rc(fr_upool_fc_bwd(x.data_ptr<float>(), e.data_ptr<float>(), alpha.data_ptr<float>(), w2.data_ptr<float>(),
-                           g.data_ptr<float>(), W1t.data_ptr(), dx.data_ptr<float>(), dpre.data_ptr<float>(),
-                           da8.data_ptr<float>(), (int)n, (int)T, (int)D, (int)Q, cur_stream()),
-           "upool_fc_bwd");
-  return {dx, dpre, da8};
-}
-
 // user pool backward with da out (column 0 of [n T, 8]) instead of dw2 / db2 (fr_upool_bwd_da)
 std::tuple<at::Tensor, at::Tensor, at::Tensor> upool_bwd_da(const at::Tensor& x, const at::Tensor& e,
                                                             const at::Tensor& alpha, const at::Tensor& w2,
@@ -861,21 +799,19 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
   return out;
 }
 
-// Adam with the step count (and the per-step loss ring) on the device: capturable in a graph
-void adam_dev(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at::Tensor step, at::Tensor ticket,
+// Adam with the step count (and the per-step loss ring) on the device: capturable in a graph.
+// step: int64 [1], already advanced for this step (the step's cast launch, multi_cast bump2)
+void adam_dev(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, const at::Tensor& step,
               const at::Tensor& loss, at::Tensor ring, double lr, double b1, double b2, double eps, double grad_scale) {
   for (auto* t : {&p, &m, &v}) check_dev(*t, "adam_dev buffer");
   check_dev(g, "g");
   check_dev(step, "step");
-  check_dev(ticket, "ticket");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
                   v.scalar_type() == at::kFloat && p.numel() == g.numel() && p.numel() == m.numel() &&
                   p.numel() == v.numel() && p.is_contiguous() && g.is_contiguous() && m.is_contiguous() &&
                   v.is_contiguous(),
               "fedrec::adam_dev: fp32 flat buffers of one size");
-  TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() == 1 && ticket.scalar_type() == at::kInt &&
-                  ticket.numel() == 1,
-              "fedrec::adam_dev: int64 step [1], int32 ticket [1]");
+  TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() == 1, "fedrec::adam_dev: int64 step [1]");
   const bool has_ring = ring.numel() > 0;
   if (has_ring) {
     check_dev(loss, "loss");
@@ -887,9 +823,8 @@ void adam_dev(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at:
   const c10::DeviceGuard dg(p.device());
   check_rc(fr_adam_dev(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), nullptr,
                        (long)p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale,
-                       (long long*)step.data_ptr<int64_t>(), (unsigned*)ticket.data_ptr<int>(),
-                       has_ring ? loss.data_ptr<float>() : nullptr, has_ring ? ring.data_ptr<float>() : nullptr,
-                       (int)ring.numel(), cur_stream()),
+                       (const long long*)step.data_ptr<int64_t>(), has_ring ? loss.data_ptr<float>() : nullptr,
+                       has_ring ? ring.data_ptr<float>() : nullptr, (int)ring.numel(), cur_stream()),
            "adam_dev");
 }
 
@@ -1141,7 +1076,7 @@ void colsum_f32(const std::vector<at::Tensor>& X, const std::vector<at::Tensor>&
 // (adam.hip), any size / alignment; false = not launched (an empty segment).  bump (optional
 // int64 [1] on the same device): advanced by one by the first launch
 bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst,
-                const c10::optional<at::Tensor>& bump) {
+                const c10::optional<at::Tensor>& bump, const c10::optional<at::Tensor>& bump2) {
   const size_t n = src.size();
   TORCH_CHECK(n >= 1 && dst.size() == n, "fedrec::multi_cast: sizes");
   const c10::DeviceGuard g(dst[0].device());
@@ -1152,32 +1087,34 @@ bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor
                 "fedrec::multi_cast: bump must be an int64 [1] tensor on the destinations' device");
     bp = (long long*)bump->data_ptr<int64_t>();
   }
+  long long* bp2 = nullptr;
+  if (bump2.has_value() && bump2->defined()) {
+    TORCH_CHECK(bump2->device() == dst[0].device() && bump2->scalar_type() == at::kLong && bump2->numel() == 1 &&
+                    bump2->is_contiguous(),
+                "fedrec::multi_cast: bump2 must be an int64 [1] tensor on the destinations' device");
+    bp2 = (long long*)bump2->data_ptr<int64_t>();
+  }
   std::vector<const float*> sp(n);
   std::vector<void*> dp(n);
   std::vector<long> ne(n);
-  std::vector<int> bf(n), trc(n, 0);
+  std::vector<int> bf(n);
   for (size_t i = 0; i < n; ++i) {
-    // a transposed destination: dst = T.t() of a contiguous bf16 T [C, R] for a source [R, C]
-    const bool tr = dst[i].dim() == 2 && src[i].dim() == 2 && !dst[i].is_contiguous() && dst[i].stride(0) == 1 &&
-                    dst[i].stride(1) == dst[i].size(0) && dst[i].sizes() == src[i].sizes();
-    TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && (dst[i].is_contiguous() || tr) &&
+    TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && dst[i].is_contiguous() &&
                     src[i].scalar_type() == at::kFloat &&
-                    (dst[i].scalar_type() == at::kBFloat16 || (dst[i].scalar_type() == at::kFloat && !tr)) &&
+                    (dst[i].scalar_type() == at::kBFloat16 || dst[i].scalar_type() == at::kFloat) &&
                     src[i].numel() == dst[i].numel(),
-                "fedrec::multi_cast: contiguous fp32 sources, bf16/fp32 destinations of the same size (or the "
-                "transposed view of a contiguous bf16 tensor)");
+                "fedrec::multi_cast: contiguous fp32 sources, bf16/fp32 destinations of the same size");
     sp[i] = src[i].data_ptr<float>();
     dp[i] = dst[i].data_ptr();
     ne[i] = (long)src[i].numel();
     bf[i] = dst[i].scalar_type() == at::kBFloat16 ? 1 : 0;
-    trc[i] = tr ? (int)src[i].size(1) : 0;
   }
   for (size_t i = 0; i < n; ++i)
     if (ne[i] <= 0) return false;
   for (size_t i0 = 0; i0 < n; i0 += 96) {  // 96 segments per launch (kernel-argument size)
     const int k = (int)std::min<size_t>(96, n - i0);
     TORCH_CHECK(fr_multi_cast(sp.data() + i0, dp.data() + i0, ne.data() + i0, bf.data() + i0, k, i0 == 0 ? bp : nullptr,
-                              cur_stream(), trc.data() + i0) == 0,
+                              cur_stream(), i0 == 0 ? bp2 : nullptr) == 0,
                 "fedrec::multi_cast: launch rejected");
   }
   return true;
@@ -1606,14 +1543,12 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep=None) -> (Tensor, Tensor)");
   m.def("upool_bwd_da(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g) -> (Tensor, Tensor, Tensor)");
-  m.def("upool_fc_fwd(Tensor x, Tensor W1, Tensor b1, Tensor w2, Tensor b2, Tensor? keep) -> (Tensor, Tensor, Tensor)");
-  m.def("upool_fc_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, Tensor W1t) -> (Tensor, Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None) -> (Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act, Tensor? ci=None, Tensor(a!)? dcand_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
-  m.def("adam_dev(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!) step, Tensor(e!) ticket, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale) -> ()");
+  m.def("adam_dev(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale) -> ()");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset, bool valid=False) -> (Tensor, Tensor)");
@@ -1629,7 +1564,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_grad(Tensor dx, Tensor sorted, Tensor perm, int num_rows) -> Tensor");
   m.def("small_gemm(Tensor[] A, Tensor?[] gidx, Tensor[] B, Tensor?[] bias, Tensor(a!)[] C, int[] ints, float[] floats, int[] seeds, Tensor? dev_off, Tensor[] Bseg, int tile, Tensor?[] asum) -> ()");
   m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
-  m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst, Tensor(b!)? bump=None) -> bool");
+  m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst, Tensor(b!)? bump=None, Tensor(c!)? bump2=None) -> bool");
   m.def("multi_cast_t(Tensor[] src, Tensor(a!)[] dst) -> bool");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_hist(Tensor x, Tensor seeds, Tensor signs, int round) -> Tensor");
@@ -1663,8 +1598,6 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("additive_pool_fwd", &additive_pool_fwd);
   m.impl("additive_pool_bwd", &additive_pool_bwd);
   m.impl("upool_bwd_da", &upool_bwd_da);
-  m.impl("upool_fc_fwd", &upool_fc_fwd);
-  m.impl("upool_fc_bwd", &upool_fc_bwd);
   m.impl("user_attention_fwd", &user_attention_fwd);
   m.impl("user_attention_bwd", &user_attention_bwd);
   m.impl("score_ce", &score_ce);

@@ -26,8 +26,9 @@
 // 256x256 ping-pong (two wave rows half a phase apart, row-predicated stores); 9 the ping-pong
 // with a store-tolerant stage schedule (padded C rows; also the residual / GELU-backward /
 // dual-output epilogues); 12 = 9 with bias-armed accumulators; 13 = 12 with non-temporal
-// stores.  Auto: 13 for no-residual N % 256 == 0 shapes with padded C and K < 2048, 9 for the
-// residual forms and K >= 2048, 6 outside the padded-C domain, 0 otherwise
+// stores.  Auto: 13 for no-residual N % 256 == 0 shapes with padded C, K < 2048 and M < 256k,
+// 9 for the residual forms, K >= 2048 and M >= 256k (the cache build), 6 outside the padded-C
+// domain, 0 otherwise
 // (benchmarks/gemm_bench.py, profiles/r4_gemm_bench.json).
 #include "common.h"
 
@@ -1024,9 +1025,12 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
   // tile (plain / bias / act epilogue only) -- opt-in (variant 9) only: at M = 80k, N = 384
   // with tanh it measured 133 us vs 102 us for the 128x128 kernel (2.45 waves of 256-row
   // tiles, a third of the MFMA work wasted on the clamped columns, tanh in the exposed epilogue)
-  const bool part_n = N % BN2 != 0 && N % 64 == 0 && R == nullptr && ACT != 3 && g_gemm_variant == 9;
   const bool auto_v = g_gemm_variant < 0;
-  const bool big = (auto_v && N % BN2 == 0 && M >= 4096) || (g_gemm_variant >= 6 && (N % BN2 == 0 || part_n));
+  // (at M >= 256k rows the partial tile wins: 770 vs 612 TF for N = 384 + tanh at M = 409,600,
+  // profiles/r4_gemm_bench_M409600.json)
+  const bool part_n = N % BN2 != 0 && N % 64 == 0 && R == nullptr && ACT != 3 &&
+                      (g_gemm_variant == 9 || (auto_v && M >= (1 << 18)));
+  const bool big = (auto_v && (N % BN2 == 0 || part_n) && M >= 4096) || (g_gemm_variant >= 6 && (N % BN2 == 0 || part_n));
   if (big && (auto_v || g_gemm_variant == 9 || g_gemm_variant >= 12) && pp_domain(M, N, K, c_rows)) {
     const int tiles_n = (N + BN2 - 1) / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
     const int G = ntiles < num_cus() ? ntiles : num_cus();
@@ -1034,10 +1038,11 @@ void launch_act(const bf16* A, const bf16* W, const float* bias, const bf16* R, 
     // with K < 2048; variant 9 for the rest (residual / GELU-backward epilogues, FFN2)
     if constexpr (ACT != 3) {
       if (R == nullptr && N % BN2 == 0 && g_gemm_variant != 9) {
-        // non-temporal output stores (variant 13) by default where K < 2048: QKV 1025 vs 930 TF,
-        // FFN1 + GELU 868 vs 796, out-proj 916 vs 911; FFN2 (K = 3072) keeps variant 9
-        // (1159 vs 1106), profiles/r4_gemm_bench.json
-        if (auto_v && K >= 2048) {
+        // variant 13 (non-temporal stores) by default where K < 2048 and M < 256k: at M = 78,850
+        // QKV 1029 vs 952 TF (v9), FFN1 + GELU 867 vs 842; FFN2 (K = 3072) 1070 vs 1150; at the
+        // cache build's M = 409,600 variant 9 wins every shape (QKV 1007 vs 948, out-proj 979 vs
+        // 929, FFN1 871 vs 842): profiles/r4_gemm_bench.json, r4_gemm_bench_M409600.json
+        if (auto_v && (K >= 2048 || M >= (1 << 18))) {
           if (bias) hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, true, false>), dim3(G), dim3(512), 0, s, A, W, bias, R, C,
                                        M, N, K, tiles_n, ntiles);
           else hipLaunchKernelGGL((gemm_nt_pp2_kernel<ACT, false, false>), dim3(G), dim3(512), 0, s, A, W, bias, R, C,
@@ -1131,7 +1136,7 @@ extern "C" int fr_gemm_nt_bf16_split(const void* A, const void* W, const float* 
   const bf16* a = (const bf16*)A;
   const bf16* w = (const bf16*)W;
   bf16* c = (bf16*)C;
-  if (g_gemm_variant != 9) {
+  if (g_gemm_variant != 9 && (g_gemm_variant >= 12 || M < (1 << 18))) {
     if (bias)
       hipLaunchKernelGGL((gemm_nt_pp3_kernel<0, true, false, true>), dim3(G), dim3(512), 0, s, a, w, bias, c, M, N, K,
                          tiles_n, ntiles_max, full_rows, n_partial / BN2);
@@ -1173,7 +1178,7 @@ extern "C" int fr_gemm_nt_bf16_dual(const void* A, const void* W, const float* b
   if (!ok) return 3;
   const int tiles_n = N / BN2, tiles_m = (M + BM2 - 1) / BM2, ntiles = tiles_m * tiles_n;
   const int G = ntiles < num_cus() ? ntiles : num_cus();
-  if (g_gemm_variant != 9) {
+  if (g_gemm_variant != 9 && (g_gemm_variant >= 12 || M < (1 << 18))) {
     hipLaunchKernelGGL((gemm_nt_pp3_kernel<1, true, true, true>), dim3(G), dim3(512), 0, s, (const bf16*)A, (const bf16*)W,
                        bias, (bf16*)C, M, N, K, tiles_n, ntiles, nullptr, 0, (bf16*)Z);
     return 0;

@@ -453,40 +453,41 @@ class EmbedLNFn(torch.autograd.Function):
 
 
 def _user_weight_bufs(wts, dev):
-    """The user step's compute copies: the bf16 stack [Wq; Wk; Wv; W1], the fp32 [bq | bk | bv]
-    and W1 transposed in bf16 ([D, Qd]: the fused pool backward's dpre W1 operand)."""
+    """The user step's compute copies: the bf16 stack [Wq; Wk; Wv; W1] and the fp32 [bq | bk | bv]."""
     wq, w1, D = wts[0], wts[6], wts[0].shape[1]
     return (torch.empty(3 * wq.shape[0] + w1.shape[0], D, device=dev, dtype=torch.bfloat16),
-            torch.empty(3 * wq.shape[0], device=dev, dtype=torch.float32),
-            torch.empty(D, w1.shape[0], device=dev, dtype=torch.bfloat16))
+            torch.empty(3 * wq.shape[0], device=dev, dtype=torch.float32))
 
 
-def _user_cast_lists(wts, wb, bqkv, w1t):
+def _user_cast_lists(wts, wb, bqkv):
     wq, bq, wk, bk, wv, bv, w1 = wts[:7]
     D, D3 = wq.shape[1], 3 * wq.shape[0]
-    return ([wq, wk, wv, w1, bq, bk, bv, w1],
-            [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D], bqkv[2 * D:], w1t.t()])
+    return ([wq, wk, wv, w1, bq, bk, bv],
+            [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D], bqkv[2 * D:]])
 
 
-def step_weight_casts(text_encoder, user_encoder, bump=None):
+def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     """Every compute copy a fused training step needs, in ONE cast launch: the text head's att_fc1
     weight in bf16 (the head_score operand) and the user encoder's bf16 weight stack + fp32 Q|K|V
     bias (the user step's GEMM operands).  Returns ``(w1_bf16, (wb, bqkv))``; the two were a cast
     kernel each (4.7 + 6.2 us per step).  ``bump`` (int64 [1] device counter, optional): advanced
     by one in the same launch -- the step's dropout / noise offset (a torch ``add_`` of its own
-    cost 4.8 us at the end of every step)."""
+    cost 4.8 us at the end of every step).  ``bump2``: a second counter advanced the same way (the
+    in-graph Adam's step count: adam_dev then only reads it)."""
     aa = text_encoder.additive_attention
     mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
     wts = (mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight, mha.W_V.bias,
            pool.att_fc1.weight)
     w = aa.att_fc1.weight
     w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
-    wb, bqkv, w1t = _user_weight_bufs(wts, w.device)
-    src, dst = _user_cast_lists(wts, wb, bqkv, w1t)
-    launched = ops.native.require_for(w).multi_cast([w.detach()] + [t.detach() for t in src], [w1b] + dst, bump)
-    if bump is not None and not launched:
-        bump.add_(1)
-    return w1b, (wb, bqkv, w1t)
+    wb, bqkv = _user_weight_bufs(wts, w.device)
+    src, dst = _user_cast_lists(wts, wb, bqkv)
+    launched = ops.native.require_for(w).multi_cast([w.detach()] + [t.detach() for t in src], [w1b] + dst, bump, bump2)
+    if not launched:
+        for b in (bump, bump2):
+            if b is not None:
+                b.add_(1)
+    return w1b, (wb, bqkv)
 
 
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None):
@@ -505,34 +506,27 @@ def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_
     BH, D3, Qd = B * H, 3 * D, w1.shape[0]
     dev = src.device
     if casts is not None:  # the step's one cast launch made them already (step_weight_casts)
-        wb, bqkv, w1t = casts
+        wb, bqkv = casts
     else:
-        wb, bqkv, w1t = _user_weight_bufs(wts, dev)
-        ops.native.require_for(src).multi_cast(*_user_cast_lists(wts, wb, bqkv, w1t))
+        wb, bqkv = _user_weight_bufs(wts, dev)
+        ops.native.require_for(src).multi_cast(*_user_cast_lists(wts, wb, bqkv))
     p, seed, off = drop
     xd = ops.gather_dropout(src, idx, p, seed, off, dev_off, bf16_out=True)
     qkv = torch.empty(BH, D3, device=dev, dtype=torch.float32)
     ops.small_gemm(ops.Gemm(xd, wb[:D3], qkv, BH, D3, D, D, D, D3, bias=bqkv))  # one N = 3D GEMM
     q3 = qkv.view(B, H, D3)
     c3, stats = ops.user_attention_fwd(q3, heads, hd, keep)
-    if c3.dtype == torch.float32 and H <= 64 and D % 16 == 0 and D <= 512 and Qd % 4 == 0 and 16 <= Qd <= 256:
-        # att_fc1 + tanh + additive pool in one launch (csrc/additive_pool.hip upool_fc_fwd_kernel:
-        # e bitwise the small-GEMM path's; 15 + 7.6 us -> one kernel)
-        u, e3, alpha = ops.native.require_for(c3).upool_fc_fwd(
-            c3.contiguous(), wb[D3:], b1.float().contiguous(), w2.reshape(-1).float().contiguous(),
-            b2.reshape(-1).float().contiguous(), None if keep is None else keep.reshape(B, H).to(torch.int32).contiguous())
-        return u, [q3, stats, c3, e3, alpha, wb, w2, xd, w1t]
     e = torch.empty(BH, Qd, device=dev, dtype=torch.float32)
     ops.small_gemm(ops.Gemm(c3, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
     e3 = e.view(B, H, Qd)
     u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2, keep)
-    return u, [q3, stats, c3, e3, alpha, wb, w2, xd, w1t]
+    return u, [q3, stats, c3, e3, alpha, wb, w2, xd]
 
 
 def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
     """Backward of :func:`_user_enc_fwd` for ``du [B, D]``: the input gradient goes into ``dx
     [B*H, D]`` (the dropout backward in the dgrad epilogue) -> the ten weight gradients."""
-    q3, stats, c3, e3, alpha, wb, w2, xd, w1t = saved
+    q3, stats, c3, e3, alpha, wb, w2, xd = saved
     D = c3.shape[-1]
     BH, D3 = B * H, 3 * D
     Qd = wb.shape[0] - D3
@@ -542,20 +536,13 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     # desc with M = 8, db2 from its column sums) -- no partial rows, no colsum launches
     lib = ops.native.require_for(c3)
     da8 = None
-    f32 = c3.dtype == torch.float32 and e3.dtype == torch.float32
-    if f32 and H <= 64 and D % 16 == 0 and D <= 512 and Qd % 8 == 0 and 16 <= Qd <= 256:
-        # pool backward + dctx += dpre W1 in one launch (csrc/additive_pool.hip upool_fc_bwd_kernel)
-        dctx, dpre, da8 = lib.upool_fc_bwd(c3.contiguous(), e3.contiguous(), alpha.contiguous(),
-                                           w2.reshape(-1).float().contiguous(), du.float().contiguous(), w1t)
-        dpre2 = dpre.view(BH, Qd)
+    if H <= 64 and c3.dtype == torch.float32 and e3.dtype == torch.float32:
+        dctx, dpre, da8 = lib.upool_bwd_da(c3.contiguous(), e3.contiguous(), alpha.contiguous(),
+                                           w2.reshape(-1).float().contiguous(), du.float().contiguous())
     else:
-        if H <= 64 and f32:
-            dctx, dpre, da8 = lib.upool_bwd_da(c3.contiguous(), e3.contiguous(), alpha.contiguous(),
-                                               w2.reshape(-1).float().contiguous(), du.float().contiguous())
-        else:
-            dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
-        dpre2 = dpre.view(BH, Qd)
-        ops.small_gemm(ops.Gemm(dpre2, wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
+        dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
+    dpre2 = dpre.view(BH, Qd)
+    ops.small_gemm(ops.Gemm(dpre2, wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
     dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep).view(BH, D3)
     p, seed, off = drop
     # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,

@@ -118,12 +118,15 @@ class _StepGraph:
             # a private memory pool per graph (~250 MB of step activations at B = 64): sharing
             # the first graph's pool (graph.pool()) trips an allocator assert in this torch build
             # when eager steps of other engines run between the captures
+            # in-graph Adam: the step's cast launch (its first kernel) advances the device step count
+            eng._adam_bump = eng._adam_step_dev if with_adam else None
             with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
                 self.loss = eng.forward_backward(self.cand, self.his, static)
                 if with_adam:  # no all-reduce between backward and optimizer: the step in one graph
                     eng._adam_dev(self.loss)
         finally:
             eng._pre_hid = None
+            eng._adam_bump = None
 
     def load(self, pre: Prepared, U: int) -> None:
         """The batch into the static inputs: one multi-copy launch; the unique list is padded
@@ -180,6 +183,7 @@ class LocalEngine:
         # LDP noise: its own Philox key per client (disjoint from the dropout keys above)
         self.ldp_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 3
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
+        self._adam_bump = None  # set while capturing a step graph with Adam in it (see _StepGraph)
         # hidden states of the step's unique titles gathered ahead (the step graph's first part)
         self._pre_hid: Optional[torch.Tensor] = None
         self._one: Optional[torch.Tensor] = None  # seed gradient of the loss (see forward_backward)
@@ -426,7 +430,7 @@ class LocalEngine:
             if self.fused_head:  # every compute copy of the step's weights in one cast launch,
                 self.sync_params()  # which also advances the dropout / noise step counter this step reads
                 casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder,
-                                             bump=self._rng_step)
+                                             bump=self._rng_step, bump2=self._adam_bump)
             with obs.range("news_encode"):
                 v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
                                       w1b=casts[0] if casts is not None else None)
@@ -460,7 +464,8 @@ class LocalEngine:
         # noise; the non-fused path's host offset would be frozen into the graph
         if self.step_graphs and pre.dedup is not None and not (self.cfg.dp.enabled and self.sigma
                                                                and not self.fused_user):
-            with_adam = self.grad_allreduce is None and self.reducer is None
+            # (the device step count rides in the fused step's cast launch)
+            with_adam = self.grad_allreduce is None and self.reducer is None and self.fused_user and self.fused_head
             loss = self._graph_step(pre, with_adam)
             if loss is not None:
                 if not with_adam:
@@ -477,8 +482,8 @@ class LocalEngine:
         advanced by the caller per replay."""
         c = self.cfg
         native.require_for(loss).adam_dev(self.flat.flat, self.flat.grad, self.flat.m, self.flat.v, self._adam_step_dev,
-                                          self._adam_ticket, loss.reshape(1).float(), self._loss_ring, c.lr,
-                                          c.adam_beta1, c.adam_beta2, c.adam_eps, 1.0)
+                                          loss.reshape(1).float(), self._loss_ring, c.lr, c.adam_beta1, c.adam_beta2,
+                                          c.adam_eps, 1.0)
 
     # ---- HIP graph of the per-step forward + backward ------------------------------------
     GRAPH_BUCKET = 128  # unique titles are padded up to a multiple of this (padded rows: id 0)
@@ -517,7 +522,6 @@ class LocalEngine:
                 self._graphs = {k: v for k, v in self._graphs.items() if k[-1] == self.hcache.builds}
             if with_adam and getattr(self, "_adam_step_dev", None) is None:  # (outside any capture)
                 self._adam_step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
-                self._adam_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
                 self._loss_ring = torch.zeros(self.LOSS_RING, dtype=torch.float32, device=self.device)
                 self._adam_mirror = -1
             g = _StepGraph(self, pre, ucap, with_adam)

@@ -676,72 +676,3 @@ def test_device_ops_refuse_non_bf16(dev):
     with pytest.raises(RuntimeError, match="no HIP kernel"):
         O.layer_norm(x, torch.ones(768, device=dev), torch.zeros(768, device=dev), 1e-12)
 
-
-@pytest.mark.parametrize("H,masked", [(50, False), (50, True), (64, False), (7, True)])
-def test_upool_fc_fwd_matches_two_launch_path(dev, H, masked):
-    """The fused user att_fc1 + tanh + additive pool (one launch) against the two-launch path it
-    replaces (small-GEMM att_fc1 with tanh, then upool_fwd) and the fp32 oracle: e agrees to the
-    last bit or so (same bf16 operands, same k order), alpha / u to fp32 summation order."""
-    B, D, Q = 33, 400, 200
-    g = torch.Generator(device="cpu").manual_seed(H)
-    c3 = (torch.randn(B, H, D, generator=g) * 0.5).to(dev)
-    W1 = (torch.randn(Q, D, generator=g) / 20).to(dev, torch.bfloat16)
-    b1 = (torch.randn(Q, generator=g) * 0.1).to(dev)
-    w2 = (torch.randn(Q, generator=g) * 0.3).to(dev)
-    b2 = torch.randn(1, generator=g).to(dev)
-    keep = None
-    if masked:
-        keep = (torch.rand(B, H, generator=g) > 0.3).to(torch.int32).to(dev)
-        keep[0] = 0  # an impression with every slot masked: alpha = 0, u = 0
-    lib = native.lib()
-    u, e, a = lib.upool_fc_fwd(c3, W1, b1, w2, b2, keep)
-    e_ref = torch.empty(B * H, Q, device=dev)
-    ops.small_gemm(ops.Gemm(c3.view(B * H, D), W1, e_ref, B * H, Q, D, D, D, Q, bias=b1, act=1))
-    u_ref, a_ref = ops.additive_pool_fwd(c3, e_ref.view(B, H, Q), w2, b2, keep)
-    assert float((e - e_ref.view(B, H, Q)).abs().max()) <= 1e-6
-    assert rel_err(a, a_ref) < 1e-5 and rel_err(u, u_ref) < 1e-5
-    # fp32 oracle over the bf16-rounded x rows
-    eo = torch.tanh(c3.to(torch.bfloat16).float() @ W1.float().t() + b1)
-    ao = eo @ w2 + b2
-    if keep is not None:
-        ao = ao.masked_fill(keep == 0, float("-inf"))
-    m = ao.max(dim=1, keepdim=True).values.clamp_min(-1e30)
-    m = torch.where(torch.isinf(m), torch.zeros_like(m), m)
-    p = torch.exp(ao - m)
-    al = p / (p.sum(dim=1, keepdim=True) + 1e-8 * torch.exp(-m))
-    assert rel_err(e, eo) < 1e-5 and rel_err(a, al) < 1e-5
-    assert rel_err(u, torch.einsum("bt,btd->bd", al, c3)) < 1e-5
-
-
-@pytest.mark.parametrize("H", [50, 64, 7])
-def test_upool_fc_bwd_matches_two_launch_path(dev, H):
-    """The fused user pool backward + dctx (one launch) against upool_bwd_da + the accumulate
-    small GEMM it replaces, and the fp32 autograd oracle of the pool + att_fc1 backward."""
-    B, D, Q = 33, 400, 200
-    g = torch.Generator(device="cpu").manual_seed(100 + H)
-    c3 = (torch.randn(B, H, D, generator=g) * 0.5).to(dev)
-    W1 = (torch.randn(Q, D, generator=g) / 20).to(dev, torch.bfloat16)
-    b1 = (torch.randn(Q, generator=g) * 0.1).to(dev)
-    w2 = (torch.randn(Q, generator=g) * 0.3).to(dev)
-    b2 = torch.randn(1, generator=g).to(dev)
-    du = torch.randn(B, D, generator=g).to(dev)
-    lib = native.lib()
-    u, e, a = lib.upool_fc_fwd(c3, W1, b1, w2, b2, None)
-    W1t = W1.t().contiguous()
-    dx, dpre, da8 = lib.upool_fc_bwd(c3, e, a, w2, du, W1t)
-    dx_r, dpre_r, da8_r = lib.upool_bwd_da(c3, e, a, w2, du)
-    ops.small_gemm(ops.Gemm(dpre_r.view(B * H, Q), W1, dx_r.view(B * H, D), B * H, D, Q, Q, D, D, b_mode=1,
-                            accumulate=True))
-    assert rel_err(da8, da8_r) < 1e-6 and rel_err(dpre, dpre_r) < 1e-6
-    assert float((dx - dx_r).abs().max()) <= 1e-6 * float(dx_r.abs().max()) + 1e-7
-    # oracle: autograd through tanh(x W1^T + b1) . w2 -> eps-softmax -> pool, with the GEMM's
-    # bf16 rounding of x and dpre emulated
-    x = c3.clone().requires_grad_(True)
-    ee = torch.tanh(x.to(torch.bfloat16).float() @ W1.float().t() + b1)
-    aa = ee @ w2 + b2
-    m = aa.max(dim=1, keepdim=True).values.detach()
-    p = torch.exp(aa - m)
-    al = p / (p.sum(dim=1, keepdim=True) + 1e-8 * torch.exp(-m))
-    uo = torch.einsum("bt,btd->bd", al, x)
-    uo.backward(du)
-    assert rel_err(dx, x.grad) < 5e-3  # dpre rounded to bf16 for the dpre W1 product
