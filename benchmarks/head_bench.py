@@ -46,7 +46,7 @@ def main():
     lib = native.lib()
     M = U * T
     e, sc = lib.head_score(table, ids, T, w1, b1, w2, b2, True)
-    pooled, alpha = lib.head_pool(table, ids, T, sc, None)
+    pooled, alpha, _ = lib.head_pool(table, ids, T, sc, None)
     gout = torch.randn(U, D, device=dev, generator=g)
     da, db2p = lib.head_pool_bwd(table, ids, T, alpha, gout)
     out = []

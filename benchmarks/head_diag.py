@@ -51,7 +51,7 @@ def main():
     tag = {k: v for k, v in os.environ.items() if k.startswith("FEDREC_HEAD")}
     for name, tab, ix in (("gather", table, ids), ("contig", hid, None)):
         e, sc = lib.head_score(tab, ix, T, w1, b1, w2, b2, True)
-        pooled, alpha = lib.head_pool(tab, ix, T, sc, None)
+        pooled, alpha, _ = lib.head_pool(tab, ix, T, sc, None)
         gout = torch.randn(U, D, device=dev, generator=g)
         da, db2p = lib.head_pool_bwd(tab, ix, T, alpha, gout)
         res = {"src": name, "env": tag}

@@ -44,7 +44,8 @@ int fr_head_score(const void* table, const int* ids, int U, int T, int D, int Q,
                   const float* w2, const float* b2, void* e_out, float* a_out, const int* nreal, hipStream_t s);
 int fr_head_score_slices(int Q);
 int fr_head_pool(const void* table, const int* ids, const float* a, int slices, const int* tokens, int U, int T, int D,
-                 float* pooled, float* alpha, const int* nreal, hipStream_t s);
+                 float* pooled, float* alpha, const int* nreal, hipStream_t s,
+                 void* pooled_b);
 int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, const float* g, int U, int T, int D,
                      float* da, float* db2p, const int* nreal, hipStream_t s);
 long fr_head_wgrad(const void* e, const void* table, const int* ids, const float* da, const float* db2p,
@@ -520,9 +521,11 @@ std::tuple<at::Tensor, at::Tensor> head_score(const at::Tensor& table, const c10
   return {e, a};
 }
 
-std::tuple<at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10::optional<at::Tensor>& ids, int64_t T,
-                                             const at::Tensor& a, const c10::optional<at::Tensor>& tokens,
-                                             const c10::optional<at::Tensor>& nreal) {
+// want_bf16: also the pooled rows rounded to bf16 (the fc GEMM's operand; empty otherwise)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10::optional<at::Tensor>& ids,
+                                                         int64_t T, const at::Tensor& a,
+                                                         const c10::optional<at::Tensor>& tokens,
+                                                         const c10::optional<at::Tensor>& nreal, bool want_bf16) {
   const int64_t U = head_titles(table, ids, T), D = table.size(1);
   check_dev(a, "a");
   TORCH_CHECK(a.scalar_type() == at::kFloat && (a.numel() == U * T || (a.dim() == 2 && a.size(0) == 2 && a.size(1) == U * T)) &&
@@ -537,11 +540,13 @@ std::tuple<at::Tensor, at::Tensor> head_pool(const at::Tensor& table, const c10:
   const c10::DeviceGuard g(table.device());
   auto pooled = at::empty({U, D}, a.options());
   auto alpha = at::empty({U, T}, a.options());
+  auto pooled_b = at::empty({want_bf16 ? U : 0, D}, a.options().dtype(at::kBFloat16));
   check_rc(fr_head_pool(table.data_ptr(), opt_int_ptr(ids), a.data_ptr<float>(), a.dim() == 2 ? (int)a.size(0) : 1,
                         opt_int_ptr(tokens), (int)U, (int)T,
-                        (int)D, pooled.data_ptr<float>(), alpha.data_ptr<float>(), opt_nreal(nreal, table), cur_stream()),
+                        (int)D, pooled.data_ptr<float>(), alpha.data_ptr<float>(), opt_nreal(nreal, table), cur_stream(),
+                        want_bf16 ? pooled_b.data_ptr() : nullptr),
            "head_pool");
-  return {pooled, alpha};
+  return {pooled, alpha, pooled_b};
 }
 
 std::tuple<at::Tensor, at::Tensor> head_pool_bwd(const at::Tensor& table, const c10::optional<at::Tensor>& ids,
@@ -1538,7 +1543,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("ipc_allreduce_(int id, Tensor(a!) x, int epoch, int mode, int blocks, float timeout_s=60.) -> ()");
   m.def("ipc_allreduce_local_(int[] ids, Tensor(a!)[] xs, int epoch, int mode, int blocks, float timeout_s=60.) -> ()");
   m.def("head_score(Tensor table, Tensor? ids, int T, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bool store_e, Tensor? nreal=None) -> (Tensor, Tensor)");
-  m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens, Tensor? nreal=None) -> (Tensor, Tensor)");
+  m.def("head_pool(Tensor table, Tensor? ids, int T, Tensor a, Tensor? tokens, Tensor? nreal=None, bool want_bf16=False) -> (Tensor, Tensor, Tensor)");
   m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor? nreal=None) -> (Tensor, Tensor)");
   m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep=None) -> (Tensor, Tensor)");

@@ -417,12 +417,16 @@ __global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__
                                                         const float* __restrict__ a, const float* __restrict__ a2,
                                                         const int* __restrict__ tokens,
                                                         int T, int D, float* __restrict__ pooled,
-                                                        float* __restrict__ alpha, const int* __restrict__ nreal) {
+                                                        float* __restrict__ alpha, const int* __restrict__ nreal,
+                                                        bf16* __restrict__ pooled_b) {
   __shared__ float a_s[MAXT];
   __shared__ float part[3072];
   const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (nreal != nullptr && u >= nreal[0]) {  // a padded title of a step graph: exact zeros
-    for (int d = tid; d < D; d += blockDim.x) pooled[(size_t)u * D + d] = 0.f;
+    for (int d = tid; d < D; d += blockDim.x) {
+      pooled[(size_t)u * D + d] = 0.f;
+      if (pooled_b != nullptr) pooled_b[(size_t)u * D + d] = f2bf(0.f);
+    }
     for (int t = tid; t < T; t += blockDim.x) alpha[(size_t)u * T + t] = 0.f;
     return;
   }
@@ -476,6 +480,7 @@ __global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__
     float s = 0.f;
     for (int j = 0; j < TG; ++j) s += part[j * D + d];
     pooled[(size_t)u * D + d] = s;
+    if (pooled_b != nullptr) pooled_b[(size_t)u * D + d] = f2bf(s);  // the fc GEMM's operand rounding
   }
 }
 
@@ -561,11 +566,15 @@ __global__ __launch_bounds__(384) void head_pool2_kernel(const bf16* __restrict_
                                                          const float* __restrict__ a, const float* __restrict__ a2,
                                                          const int* __restrict__ tokens,
                                                          int T, int D, float* __restrict__ pooled,
-                                                         float* __restrict__ alpha, const int* __restrict__ nreal) {
+                                                         float* __restrict__ alpha, const int* __restrict__ nreal,
+                                                         bf16* __restrict__ pooled_b) {
   __shared__ float part[3072];
   const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (nreal != nullptr && u >= nreal[0]) {  // a padded title of a step graph: exact zeros
-    for (int d = tid; d < D; d += blockDim.x) pooled[(size_t)u * D + d] = 0.f;
+    for (int d = tid; d < D; d += blockDim.x) {
+      pooled[(size_t)u * D + d] = 0.f;
+      if (pooled_b != nullptr) pooled_b[(size_t)u * D + d] = f2bf(0.f);
+    }
     for (int t = tid; t < T; t += blockDim.x) alpha[(size_t)u * T + t] = 0.f;
     return;
   }
@@ -623,6 +632,7 @@ __global__ __launch_bounds__(384) void head_pool2_kernel(const bf16* __restrict_
     float s = 0.f;
     for (int j = 0; j < TG; ++j) s += part[j * D + d];
     pooled[(size_t)u * D + d] = s;
+    if (pooled_b != nullptr) pooled_b[(size_t)u * D + d] = f2bf(s);  // the fc GEMM's operand rounding
   }
 }
 
@@ -1197,7 +1207,8 @@ extern "C" int fr_head_score_slices(int Q) {
 }
 
 extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, int slices, const int* tokens, int U,
-                            int T, int D, float* pooled, float* alpha, const int* nreal, hipStream_t s) {
+                            int T, int D, float* pooled, float* alpha, const int* nreal, hipStream_t s,
+                            void* pooled_b) {
   const float* a2 = slices == 2 ? a + (size_t)U * T : nullptr;
   if (T > MAXT || D % 8 != 0 || D / 8 > 384) return 1;
   if (U == 0) return 0;
@@ -1205,7 +1216,7 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, i
   if (D <= 3072 && tpt <= 32) {  // load-first form; the first form takes the shapes past it
 #define LAUNCH_POOL2(N)                                                                                          \
   hipLaunchKernelGGL(head_pool2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, \
-                     pooled, alpha, nreal)
+                     pooled, alpha, nreal, (bf16*)pooled_b)
     if (tpt <= 13) LAUNCH_POOL2(13);
     else if (tpt <= 16) LAUNCH_POOL2(16);
     else LAUNCH_POOL2(32);
@@ -1213,7 +1224,7 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, i
     return 0;
   }
   hipLaunchKernelGGL(head_pool_kernel, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, pooled,
-                     alpha, nreal);
+                     alpha, nreal, (bf16*)pooled_b);
   return 0;
 }
 

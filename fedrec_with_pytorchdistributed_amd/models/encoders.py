@@ -142,17 +142,21 @@ class TextEncoder(nn.Module):
 
     def head_rows(self, table: torch.Tensor, ids: torch.Tensor | None, title_len: int,
                   tokens: torch.Tensor | None = None, nreal: torch.Tensor | None = None,
-                  w1b: torch.Tensor | None = None) -> torch.Tensor:
+                  w1b: torch.Tensor | None = None, fcb: torch.Tensor | None = None) -> torch.Tensor:
         """Trainable head over GATHERED hidden states: ``table [rows, D]`` bf16 (the HBM cache as
         rows), titles ``ids [U]`` (None: 0..U-1), ``title_len`` tokens each -> ``[U, 400]`` fp32.
         ``tokens [N, 2, T]`` int32 masks padding tokens when ``mask_padding`` is on (Q7).
         ``nreal`` (device int32 [1]): titles past it are padding (pooled = 0, no gradient).
-        ``w1b``: att_fc1's weight already cast to bf16 this step (one cast launch per step)."""
+        ``w1b`` / ``fcb``: att_fc1's / fc's weight already cast to bf16 this step (one cast launch
+        per step); with ``fcb`` the pool also emits its rows in bf16 for the fc GEMMs."""
         aa = self.additive_attention
         tok = tokens if self.cfg.mask_padding else None
-        pooled = OF.TextHeadFn.apply(aa.att_fc1.weight, aa.att_fc1.bias, aa.att_fc2.weight, aa.att_fc2.bias,
-                                     table, ids, int(title_len), tok, nreal, w1b)
-        return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias)
+        pooled, pooled_b = OF.TextHeadFn.apply(aa.att_fc1.weight, aa.att_fc1.bias, aa.att_fc2.weight,
+                                               aa.att_fc2.bias, table, ids, int(title_len), tok, nreal, w1b,
+                                               fcb is not None)
+        if fcb is None:
+            return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias)
+        return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias, pooled_b, fcb)
 
     def head(self, hidden: torch.Tensor, token_mask: torch.Tensor | None = None) -> torch.Tensor:
         """Trainable head: ``[n,T,D] -> [n,400]`` (fp32).  ``token_mask [n,T]`` excludes padding

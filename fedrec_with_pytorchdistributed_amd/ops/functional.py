@@ -142,27 +142,30 @@ class TextHeadFn(torch.autograd.Function):
     ``mask_padding`` option, Q7)."""
 
     @staticmethod
-    def forward(ctx, w1, b1, w2, b2, table, ids, T: int, tokens, nreal=None, w1b=None):
+    def forward(ctx, w1, b1, w2, b2, table, ids, T: int, tokens, nreal=None, w1b=None, want_bf16=False):
         # nreal (device int32 [1], optional): titles past it are padding of a step graph's unique
-        # list -- every kernel skips them (pooled / da exactly 0, no rows in the weight gradient)
+        # list -- every kernel skips them (pooled / da exactly 0, no rows in the weight gradient).
+        # want_bf16: also returns pooled rounded to bf16 (non-differentiable) -- the fc GEMMs'
+        # operand, the rounding they would apply to the fp32 rows themselves
         lib = ops.native.require_for(table)
         need = any(ctx.needs_input_grad[:4])
         w1c = w1b if w1b is not None else w1.to(torch.bfloat16).contiguous()  # w1b: the step's cast
         e, a = lib.head_score(table, ids, T, w1c, b1.contiguous(),
                               w2.reshape(-1).contiguous(), b2.reshape(-1), need, nreal)
-        pooled, alpha = lib.head_pool(table, ids, T, a, tokens, nreal)
+        pooled, alpha, pooled_b = lib.head_pool(table, ids, T, a, tokens, nreal, bool(want_bf16))
         if need:
             ctx.save_for_backward(table, ids, e, alpha, w2, nreal)
         ctx.T = T
-        return pooled
+        ctx.mark_non_differentiable(pooled_b)
+        return pooled, pooled_b
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, g_b=None):
         table, ids, e, alpha, w2, nreal = ctx.saved_tensors
         lib = ops.native.require_for(table)
         da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
         dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p, nreal)
-        return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None, None, None
+        return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None, None, None, None
 
 
 def fused_head_supported(table_dim: int, query_dim: int, title_len: int) -> bool:
@@ -468,8 +471,9 @@ def _user_cast_lists(wts, wb, bqkv):
 
 def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     """Every compute copy a fused training step needs, in ONE cast launch: the text head's att_fc1
-    weight in bf16 (the head_score operand) and the user encoder's bf16 weight stack + fp32 Q|K|V
-    bias (the user step's GEMM operands).  Returns ``(w1_bf16, (wb, bqkv))``; the two were a cast
+    weight in bf16 (the head_score operand), its fc weight in bf16 (the fc GEMMs' operand) and the
+    user encoder's bf16 weight stack + fp32 Q|K|V bias (the user step's GEMM operands).  Returns
+    ``(w1_bf16, (wb, bqkv), fc_bf16)``; the att_fc1 and user casts were a cast
     kernel each (4.7 + 6.2 us per step).  ``bump`` (int64 [1] device counter, optional): advanced
     by one in the same launch -- the step's dropout / noise offset (a torch ``add_`` of its own
     cost 4.8 us at the end of every step).  ``bump2``: a second counter advanced the same way (the
@@ -478,16 +482,18 @@ def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
     wts = (mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight, mha.W_V.bias,
            pool.att_fc1.weight)
-    w = aa.att_fc1.weight
+    w, wf = aa.att_fc1.weight, text_encoder.fc.weight
     w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+    fcb = torch.empty(wf.shape, device=w.device, dtype=torch.bfloat16)
     wb, bqkv = _user_weight_bufs(wts, w.device)
     src, dst = _user_cast_lists(wts, wb, bqkv)
-    launched = ops.native.require_for(w).multi_cast([w.detach()] + [t.detach() for t in src], [w1b] + dst, bump, bump2)
+    launched = ops.native.require_for(w).multi_cast([w.detach(), wf.detach()] + [t.detach() for t in src],
+                                                    [w1b, fcb] + dst, bump, bump2)
     if not launched:
         for b in (bump, bump2):
             if b is not None:
                 b.add_(1)
-    return w1b, (wb, bqkv)
+    return w1b, (wb, bqkv), fcb
 
 
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None):
@@ -686,13 +692,18 @@ class HeadFCFn(torch.autograd.Function):
     GEMM: forward NT, backward dgrad (NN), wgrad (TN) in one launch, bias gradient by colsum."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, xb=None, wb=None):
+        """``xb`` / ``wb`` (optional): x and w already rounded to bf16 (the pool's second output,
+        the step's cast launch) -- the GEMMs round their fp32 operands to bf16 on the way into LDS
+        anyway, so the products are the same, at half the bytes and on the bf16 fast path."""
         n, K = x.shape
         N = w.shape[0]
         x = x.contiguous()
+        xg = xb if xb is not None else x
+        wg = wb if wb is not None else w
         y = torch.empty(n, N, device=x.device, dtype=torch.float32)
-        ops.small_gemm(ops.Gemm(x, w, y, n, N, K, K, K, N, bias=b))
-        ctx.save_for_backward(x, w)
+        ops.small_gemm(ops.Gemm(xg, wg, y, n, N, K, K, K, N, bias=b))
+        ctx.save_for_backward(xg, wg)
         return y
 
     @staticmethod
@@ -708,4 +719,4 @@ class HeadFCFn(torch.autograd.Function):
         # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one launch
         ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1),
                        ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db))
-        return dx, dw, db
+        return dx, dw, db, None, None

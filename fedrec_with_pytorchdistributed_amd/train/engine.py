@@ -28,6 +28,7 @@ Two update schedules (Q3):
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import time
@@ -57,6 +58,7 @@ class Prepared(NamedTuple):
     ready: Optional[torch.cuda.Event]
     padded: bool = False  # dedup's unique list padded with rows no occurrence maps to (step graphs)
     nreal: Optional[torch.Tensor] = None  # device int32 [1]: the real titles of a padded list
+    held: bool = False  # lifetime kept by LocalEngine._retire (no per-tensor record_stream)
 
 
 # "thread_local": only this thread's unsafe calls are refused during a capture -- the RCCL
@@ -184,6 +186,8 @@ class LocalEngine:
         self.ldp_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 3
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
         self._adam_bump = None  # set while capturing a step graph with Adam in it (see _StepGraph)
+        self._inflight = collections.deque()  # (held batch, end event or None), see _retire
+        self._held_n = 0
         # hidden states of the step's unique titles gathered ahead (the step graph's first part)
         self._pre_hid: Optional[torch.Tensor] = None
         self._one: Optional[torch.Tensor] = None  # seed gradient of the loss (see forward_backward)
@@ -310,7 +314,7 @@ class LocalEngine:
         return ids if ids.dtype == torch.int32 else ids.to(torch.int32)
 
     def news_vectors(self, uniq: torch.Tensor, grad: bool, nreal: Optional[torch.Tensor] = None,
-                     w1b: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     w1b: Optional[torch.Tensor] = None, fcb: Optional[torch.Tensor] = None) -> torch.Tensor:
         """News vectors of titles ``uniq``; ``nreal`` (device int32 [1], fused head only): rows
         past it are padding of a step graph's unique list and come out as the fc bias."""
         te = self.model.text_encoder
@@ -320,7 +324,7 @@ class LocalEngine:
             table = self.hcache.flat()
             self.sync_params()
             if grad:
-                return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens, nreal, w1b)
+                return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens, nreal, w1b, fcb)
             with torch.no_grad():
                 return te.head_rows(table, self._cache_ids(uniq), self.tokens.shape[2], self.tokens)
         hid, mask = self._hidden(uniq)  # parameter-free: overlaps the previous step's all-reduce + Adam
@@ -333,7 +337,7 @@ class LocalEngine:
     # -------------------------------------------------------------------------------
     DEDUP_SYNC_MAX = 8192  # csrc dedup (one kernel chain, then the count read) up to this many ids
 
-    def prepare(self, batch_fn: Callable[[], Tuple]) -> Prepared:
+    def prepare(self, batch_fn: Callable[[], Tuple], held: bool = False) -> Prepared:
         """Sample a batch (``batch_fn() -> (cand, his)``) and de-duplicate its news ids.  On the
         GPU both run on the lookahead stream: the only host wait (the unique count) waits for
         that stream alone, so a step's dedup overlaps the previous step's kernels.
@@ -353,14 +357,15 @@ class LocalEngine:
             if ids.numel() > self.DEDUP_SYNC_MAX:  # the sort path queues work after its count read
                 ev = torch.cuda.Event()
                 ev.record(self._prep)
-        for t in (c, h, *dd):
-            t.record_stream(main)
+        if not held:  # (held: the training loop keeps the batch alive -- see _retire)
+            for t in (c, h, *dd):
+                t.record_stream(main)
         # otherwise no event for the main stream to wait on: the dedup's unique count is a host
         # read on the lookahead stream, the last work queued there for this batch, so when it
         # returns every lookahead kernel of the batch has completed (kernel completion publishes
         # its writes at agent scope).  A per-step hipStreamWaitEvent measured ~33 us of device
         # idle between steps (profiles/r4_graph_gap.json).
-        return Prepared(c, h, tuple(dd), ev)
+        return Prepared(c, h, tuple(dd), ev, held=held)
 
     def _forward_rows(self, cand: torch.Tensor, his: torch.Tensor, grad_news: bool, pre: Optional[Prepared] = None):
         B, C = cand.shape
@@ -433,7 +438,8 @@ class LocalEngine:
                                              bump=self._rng_step, bump2=self._adam_bump)
             with obs.range("news_encode"):
                 v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
-                                      w1b=casts[0] if casts is not None else None)
+                                      w1b=casts[0] if casts is not None else None,
+                                      fcb=casts[2] if casts is not None else None)
             with obs.range("user_step"):
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
                                           pre is not None and pre.padded, True, his,
@@ -470,8 +476,11 @@ class LocalEngine:
             if loss is not None:
                 if not with_adam:
                     self.optimizer_step(overlap=True)
+                self._retire(pre)
                 return loss
-        return self.train_step(pre.cand, pre.his, pre)
+        loss = self.train_step(pre.cand, pre.his, pre)
+        self._retire(pre)
+        return loss
 
     # ---- Adam inside the step graph (no gradient all-reduce: one client) ----------------
     LOSS_RING = 4096  # per-step losses live here until read (train_epoch folds every LOSS_RING / 2)
@@ -664,7 +673,34 @@ class LocalEngine:
             return None if b is None else Prepared(self.to_device(b[0]), self.to_device(b[1]), None, None)
         with torch.cuda.stream(self._prep):  # the device sampler's kernel runs on the lookahead stream
             b = next(it, None)
-        return None if b is None else self.prepare(lambda: b)
+        return None if b is None else self.prepare(lambda: b, held=True)
+
+    INFLIGHT = 8  # held batches kept alive after their step was queued (bounds the host run-ahead)
+    EVENT_EVERY = 4  # one end-of-step event per this many steps
+
+    def _retire(self, pre: Optional[Prepared]) -> None:
+        """Keep a held batch's lookahead tensors alive until the main stream has run its step.
+        record_stream on the six tensors made the caching allocator queue six event records on
+        the main stream per step when they were freed -- ~30 us of device idle between two step
+        graphs (steady step 0.548 -> 0.529 ms without them; the bare replay loop,
+        benchmarks/graph_seam.py, has an 8.6 us seam).  Here one event every EVENT_EVERY steps
+        marks a step's end; a batch is released once INFLIGHT later steps are queued and an event
+        recorded at or after its step has completed (the host then runs at most INFLIGHT steps
+        ahead of the device, far more than the ~0.15 ms of host work per step needs)."""
+        if pre is None or not pre.held or self._prep is None:
+            return
+        self._held_n += 1
+        ev = None
+        if self._held_n % self.EVENT_EVERY == 0:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        self._inflight.append((pre, ev))
+        while len(self._inflight) > self.INFLIGHT:
+            _, old = self._inflight.popleft()
+            if old is None:  # covered by the next event queued after it
+                old = next((e for _, e in self._inflight if e is not None), None)
+            if old is not None:
+                old.synchronize()
 
     # -------------------------------------------------------------------------------
     def train_epoch(self, max_steps: Optional[int] = None, log_every: int = 0,
@@ -688,6 +724,7 @@ class LocalEngine:
                 loss = self.train_prepared(pre)
             else:
                 loss = self.accumulate_step(pre.cand, pre.his, pre)
+                self._retire(pre)
             # sample + dedup the next batch while this step's kernels run (both schedules)
             last = max_steps is not None and n + 1 >= max_steps
             nxt = None if last else self._next_prepared(it)
@@ -707,6 +744,7 @@ class LocalEngine:
             self.end_epoch_update(n)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+        self._inflight.clear()  # every held batch's step has completed
         dt = time.perf_counter() - t0
         self.check_data_plane()
         self.epoch += 1

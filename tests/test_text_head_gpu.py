@@ -57,7 +57,7 @@ def test_fused_text_head_matches_fp32_oracle(dev, U, T, masked):
     w2 = (torch.randn(1, Q, generator=g) / math.sqrt(Q) * 3).to(dev).requires_grad_(True)
     b2 = torch.randn(1, generator=g).to(dev).requires_grad_(True)
     assert OF.fused_head_supported(D, Q, T)
-    pooled = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, tokens)
+    pooled, _ = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, tokens)
     gout = torch.randn(U, D, generator=g).to(dev)
     gw = torch.autograd.grad(pooled, (w1, b1, w2, b2), gout)
     params = [t.detach().clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
@@ -156,7 +156,7 @@ def test_fused_head_skips_padded_titles(dev):
     b1 = (torch.randn(Q, generator=g) * 0.1).to(dev).requires_grad_(True)
     w2 = (torch.randn(1, Q, generator=g) / math.sqrt(Q) * 3).to(dev).requires_grad_(True)
     b2 = torch.randn(1, generator=g).to(dev).requires_grad_(True)
-    pooled = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, None, nreal)
+    pooled, _ = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, None, nreal)
     gout = torch.randn(U, D, generator=g).to(dev)  # padded rows get a nonzero gradient too
     gw = torch.autograd.grad(pooled, (w1, b1, w2, b2), gout)
     params = [t.detach().clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
@@ -167,3 +167,29 @@ def test_fused_head_skips_padded_titles(dev):
     assert _rel(pooled[:R], ref) < 2e-3
     for name, a, b in zip(("dW1", "db1", "dw2"), gw[:3], rw[:3]):
         assert _rel(a, b) < 3e-2, (name, _rel(a, b))
+
+
+def test_fc_on_bf16_operands_matches_fp32_operands(dev):
+    """The fc GEMMs on the pool's bf16 rows and the cast fc weight give the same products as on
+    the fp32 pooled rows / fp32 weight (the GEMMs round fp32 operands to bf16 themselves): forward
+    and every gradient bitwise."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    U, D, N = 333, 768, 400
+    x = torch.randn(U, D, generator=g).to(dev).requires_grad_(True)
+    w = (torch.randn(N, D, generator=g) / 30).to(dev).requires_grad_(True)
+    b = torch.randn(N, generator=g).to(dev).requires_grad_(True)
+    dy = torch.randn(U, N, generator=g).to(dev)
+    y0 = OF.HeadFCFn.apply(x, w, b)
+    gx0, gw0, gb0 = torch.autograd.grad(y0, (x, w, b), dy)
+    y1 = OF.HeadFCFn.apply(x, w, b, x.detach().to(torch.bfloat16), w.detach().to(torch.bfloat16))
+    gx1, gw1, gb1 = torch.autograd.grad(y1, (x, w, b), dy)
+    assert torch.equal(y0, y1)
+    assert torch.equal(gx0, gx1) and torch.equal(gw0, gw1) and torch.equal(gb0, gb1)
+    # the pool's bf16 output is the fp32 pooled rows rounded
+    lib = native.lib()
+    T = 50
+    table = torch.randn(40 * T, D, generator=g).to(dev, torch.bfloat16)
+    ids = torch.randint(0, 40, (17,), generator=g).to(dev, torch.int32)
+    a = torch.randn(17 * T, generator=g).to(dev)
+    pooled, _, pb = lib.head_pool(table, ids, T, a, None, None, True)
+    assert torch.equal(pb, pooled.to(torch.bfloat16))
