@@ -290,9 +290,10 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
   }
 }
 
-// Backward LDS: 55,616 B with PLDB = 68 and 65-row stages (two blocks per CU); PLDB = 66 with
-// 64-row stages (three blocks per CU, 2-way conflicts on the row-major P / dS reads) measured
-// neutral (34.4 vs 34.2 us)
+// Backward LDS: 38,208 B with PLDB = 68 and 65-row stages -- four blocks per CU.  P and dS share
+// one [64][PLDB] image: P first (dV = P^T dctx reads it), then, after a barrier, dS (dQ and
+// dK = dS^T Q); the dS values wait in registers (16 per lane) meanwhile.  (The first form kept
+// both images, 55,616 B: two blocks per CU, 2.5 rounds of the 1,280 (impression, head) blocks.)
 template <int SR, int PLDB>
 __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   const float* __restrict__ stats,
@@ -303,8 +304,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   __shared__ __attribute__((aligned(16))) float ks[SR][DK];
   __shared__ __attribute__((aligned(16))) float vs[SR][DK];
   __shared__ __attribute__((aligned(16))) float gs[SR][DK];
-  __shared__ __attribute__((aligned(16))) float ps[64 * PLDB];
-  __shared__ __attribute__((aligned(16))) float dss[64 * PLDB];
+  __shared__ __attribute__((aligned(16))) float pd[64 * PLDB];  // P, then dS
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
   const int ld = 3 * NH * DK, D = NH * DK;
@@ -349,7 +349,9 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   const float scale = rsqrtf((float)DK);
   float* dst = dqkv + (size_t)b * H * ld + h * DK;
   const int KS = (H + 3) / 4;
-  if (i0 < H) {  // query tile: P, dP, D, dS rows into LDS; dQ
+  const bool act = i0 < H;  // this wave's query / key tile holds real rows (wave-uniform)
+  float dsv[4][4];          // this wave's dS rows (registers while P is read from LDS)
+  if (act) {  // query tile: P, dP, D; P into LDS, dS kept
     bool kept[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) kept[j] = j * 16 + fr < H && key_kept(keep, b, H, min(j * 16 + fr, H - 1));
@@ -378,18 +380,44 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
       Dt = row16_sum(Dt);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int idx = (i0 + fq * 4 + r) * PLDB + j * 16 + fr;
-        ps[idx] = p[j][r];
-        dss[idx] = p[j][r] * (dp[j][r] - Dt) * scale;
+        pd[(i0 + fq * 4 + r) * PLDB + j * 16 + fr] = p[j][r];
+        dsv[j][r] = p[j][r] * (dp[j][r] - Dt) * scale;
       }
     }
-    // dQ rows of this tile = dS K (this wave's own dS rows)
+  }
+  __syncthreads();  // every P row in LDS
+  if (act) {  // key tile i0: dV = P^T dctx (sums over every query)
+    f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      if (kk >= KS) break;
+      const int t = 4 * kk + fq;
+      const float pa = pd[t * PLDB + i0 + fr];
+      const float g0 = gs[t][fr], g1r = gs[t][16 + fr], g1 = fr < DK - 16 ? g1r : 0.f;
+      v0 = mfma4(pa, g0, v0);
+      v1 = mfma4(pa, g1, v1);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i0 + fq * 4 + r;
+      if (row >= H) continue;
+      dst[(size_t)row * ld + 2 * D + fr] = v0[r];
+      if (fr < DK - 16) dst[(size_t)row * ld + 2 * D + 16 + fr] = v1[r];
+    }
+  }
+  __syncthreads();  // every wave done reading P: the image takes dS
+  if (act) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pd[(i0 + fq * 4 + r) * PLDB + j * 16 + fr] = dsv[j][r];
+    // dQ rows of this tile = dS K (this wave's own dS rows: written by this wave, in order)
     f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       if (kk >= KS) break;
       const int k = 4 * kk + fq;
-      const float a = dss[(i0 + fr) * PLDB + k];
+      const float a = pd[(i0 + fr) * PLDB + k];
       const float y0 = ks[k][fr], y1r = ks[k][16 + fr], y1 = fr < DK - 16 ? y1r : 0.f;
       o0 = mfma4(a, y0, o0);
       o1 = mfma4(a, y1, o1);
@@ -402,19 +430,16 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
       if (fr < DK - 16) dst[(size_t)row * ld + 16 + fr] = o1[r];
     }
   }
-  __syncthreads();  // every P / dS row in LDS
-  if (i0 >= H) return;
-  // key tile i0: dV = P^T dctx, dK = dS^T Q (sums over every query)
-  f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0, k0 = v0, k1 = v0;
+  __syncthreads();  // every dS row in LDS
+  if (!act) return;
+  // key tile i0: dK = dS^T Q
+  f32x4 k0 = f32x4{0.f, 0.f, 0.f, 0.f}, k1 = k0;
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
     if (kk >= KS) break;
     const int t = 4 * kk + fq;
-    const float pa = ps[t * PLDB + i0 + fr], da = dss[t * PLDB + i0 + fr];
-    const float g0 = gs[t][fr], g1r = gs[t][16 + fr], g1 = fr < DK - 16 ? g1r : 0.f;
+    const float da = pd[t * PLDB + i0 + fr];
     const float q0 = qs[t][fr], q1r = qs[t][16 + fr], q1 = fr < DK - 16 ? q1r : 0.f;
-    v0 = mfma4(pa, g0, v0);
-    v1 = mfma4(pa, g1, v1);
     k0 = mfma4(da, q0, k0);
     k1 = mfma4(da, q1, k1);
   }
@@ -423,11 +448,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
     const int row = i0 + fq * 4 + r;
     if (row >= H) continue;
     dst[(size_t)row * ld + D + fr] = k0[r];
-    dst[(size_t)row * ld + 2 * D + fr] = v0[r];
-    if (fr < DK - 16) {
-      dst[(size_t)row * ld + D + 16 + fr] = k1[r];
-      dst[(size_t)row * ld + 2 * D + 16 + fr] = v1[r];
-    }
+    if (fr < DK - 16) dst[(size_t)row * ld + D + 16 + fr] = k1[r];
   }
 }
 

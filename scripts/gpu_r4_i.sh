@@ -5,6 +5,7 @@ source "$(dirname "$0")/gpu_lib.sh"
 export PYTHONPATH=$PWD:$PYTHONPATH
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 check t_i 500 $T tests/test_step_graph.py tests/test_engine_gpu.py tests/test_text_head_gpu.py tests/test_user_step_gpu.py
+check t_ua 200 $T tests/test_kernels_gpu.py -k "user_attention or score_ce or segment"
 run bench 300 python -u bench.py
 run bench50 300 python -u bench.py --steps 50
 O=$PWD/gpurun_out/prof_c2i
