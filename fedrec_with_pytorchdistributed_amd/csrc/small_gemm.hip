@@ -505,6 +505,132 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   gemm_tile<FM, FN, FAST, AH, BH, TRI, DB>(g, off, t, As[0], Bs[0], As[DB ? 1 : 0], Bs[DB ? 1 : 0]);
 }
 
+// ---- bf16 x bf16, both operands K-contiguous (a_mode 0, b_mode 0): an LDS-DMA ring ------------
+// The register-queue tile above keeps one k-tile in flight (a deeper queue costs VGPRs and
+// measured slower), so a tile's k-steps are a chain of global-load latencies.
+// Here every k-tile goes global -> LDS by buffer_load ... lds (16 B per lane, no VGPR round
+// trip, out-of-range rows / k answered with zeros by the buffer descriptor), NSTG stages deep:
+// NSTG - 1 k-tiles in flight while the MFMAs read one.  64 x 64 tile, 4 waves in 2 x 2 (32 x 32
+// each = 2 x 2 MFMA fragments); LDS rows of 64 k (128 B), chunk c of row r at c ^ (r & 7) (the
+// swizzle goes on the source address: DMA images are lane-linear).  Same operands, k order and
+// epilogue as gemm_tile: results are bitwise those of the FAST bf16 kernel.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int DMA_STAGE = 2 * 64 * 128;  // A and B, 64 rows x 128 B each
+
+__device__ __forceinline__ u32x4 dma_read128(uint32_t addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+template <int DMA_NSTG>
+__device__ __forceinline__ void gemm_tile_dma(const GemmDesc& g, unsigned long long off, int t, char* smem) {
+  const int split = t % g.splits;
+  t /= g.splits;
+  const int m0 = (t / g.tiles_n) * 64, n0 = (t % g.tiles_n) * 64;
+  const int kbeg = split * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int fr = lane & 15, fq = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rsa = rsrc_of(g.A), rsb = rsrc_of(g.B);
+  // this lane's rows of the two 8-row pieces per operand (wave w: rows 16 w .. 16 w + 15)
+  const int prow = lane >> 3, pch = lane & 7;
+  auto stage = [&](int st, int k0) {
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      const bool isA = op == 0;
+      const int R = isA ? g.M : g.N, r0 = isA ? m0 : n0, ld = isA ? g.lda : g.ldb;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int row = wave * 16 + p * 8 + prow;
+        const int k = k0 + ((pch ^ (row & 7)) << 3);
+        const uint32_t o = (r0 + row < R && k < kend) ? (uint32_t)((r0 + row) * ld + k) * 2u : OOB;
+        char* dst = smem + st * DMA_STAGE + op * 64 * 128 + (wave * 16 + p * 8) * 128;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsa : rsb, LDS_PTR(void, dst), 16, o, 0, 0, 0);
+      }
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + 63) >> 6;
+#pragma unroll
+  for (int s = 0; s < DMA_NSTG - 1; ++s)
+    if (s < nk) stage(s, kbeg + s * 64);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed for this wave (its younger stages -- at most NSTG - 2, 4 pieces each -- may
+    // stay in flight), then every wave's: the barrier; the buffer refilled below was read at kt - 1
+    const int younger = min(nk - 1 - kt, DMA_NSTG - 2);
+    if (DMA_NSTG >= 4 && younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (DMA_NSTG >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // a bare barrier: __syncthreads' release fence would wait for every LDS-DMA load (vmcnt(0))
+    asm volatile("s_barrier" ::: "memory");
+    if (kt + DMA_NSTG - 1 < nk) stage((kt + DMA_NSTG - 1) % DMA_NSTG, kbeg + (kt + DMA_NSTG - 1) * 64);
+    const uint32_t As = lds0 + (kt % DMA_NSTG) * DMA_STAGE, Bs = As + 64 * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm + i * 16 + fr;
+        a[i] = dma_read128(As + r * 128 + (((ks * 4 + fq) ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn + j * 16 + fr;
+        b[j] = dma_read128(Bs + r * 128 + (((ks * 4 + fq) ^ (r & 7)) << 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i]),
+                                                              __builtin_bit_cast(bf16x8, b[j]), acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue as gemm_tile: lane holds C[m = wm + 16 i + 4 fq + r][n = wn + 16 j + fr]
+  const bool part = g.splits > 1;
+  float* const dst = part ? g.P + (size_t)split * g.M * g.N : g.C;
+  const int ldd = part ? g.N : g.ldc;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn + j * 16 + fr;
+    const bool nok = n < g.N;
+    const float bn = (!part && nok && g.bias) ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + i * 16 + fq * 4 + r;
+        if (!nok || m >= g.M) continue;
+        float v = acc[i][j][r];
+        float* c = dst + (size_t)m * ldd + n;
+        if (!part) {
+          v = g.alpha * v + bn;
+          if (g.act == 1) v = tanhf(v);
+          if (g.drop_on == 3) v *= drop3(g, off, m, n);
+          if (g.accumulate) v += *c;
+        }
+        *c = v;
+      }
+  }
+}
+
+template <int NSTG>
+__global__ __launch_bounds__(256) void small_gemm_dma_kernel(const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) char smem[NSTG * DMA_STAGE];
+  int gi;
+  const int t = tile_of_block(batch, gi);
+  const GemmDesc& g = batch.d[gi];
+  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+  gemm_tile_dma<NSTG>(g, off, t, smem);
+}
+
 // FAST loads with the operand dtypes per desc: a block-uniform switch into the four typed
 // bodies (one launch for, e.g., a backward's weight gradients over bf16 and fp32 inputs)
 template <bool TRI = false, bool DB = false>
@@ -749,6 +875,14 @@ static bool fast_ok(const GemmBatch& b) {
   return fast;
 }
 
+// the LDS-DMA ring: both operands k-contiguous (16-B chunks straight into the LDS image), no
+// column sums (FAST already holds: no gather / operand dropout / kseg, 16-B aligned extents)
+static bool dma_ok(const GemmBatch& b) {
+  for (int i = 0; i < b.n; ++i)
+    if (b.d[i].a_mode != 0 || b.d[i].b_mode != 0 || b.d[i].asum) return false;
+  return true;
+}
+
 static bool mixed_dtypes(const GemmBatch& b) {
   for (int i = 1; i < b.n; ++i)
     if (b.d[i].a_bf16 != b.d[0].a_bf16 || b.d[i].b_bf16 != b.d[0].b_bf16) return true;
@@ -791,7 +925,11 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   }
   b.n = n;
   const bool fast = fast_ok(b), mixed = mixed_dtypes(b);
-  int v = (tile >= 1 && tile <= 4) ? tile : choose_tile(b);
+  // benchmarks / tests: 5 = the 64 x 64 register-queue form (never the DMA ring), 6 / 7 / 8 =
+  // the DMA ring with 2 / 3 / 4 stages where it applies
+  const bool regq = tile == 5;
+  const int force_stg = (tile >= 6 && tile <= 8) ? tile - 4 : 0;
+  int v = (tile >= 1 && tile <= 4) ? tile : (regq || force_stg) ? 1 : choose_tile(b);
   if (!fast || mixed) v = 1;  // the generic (any alignment) and mixed-dtype kernels: 64 x 64
   int tm, tn;
   tile_dims(v, tm, tn);
@@ -847,6 +985,14 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);
   else if (mixed)
     hipLaunchKernelGGL((small_gemm_mixed_kernel<true, true>), dim3(tiles), dim3(256), 0, s, b);
+  else if (v == 1 && dt == 3 && !regq && dma_ok(b)) {
+    // two stages by default: a third / fourth measured slower on every config-2 shape (LDS per
+    // block caps the blocks per CU; profiles/r4_sg_step_shapes.json)
+    const int stg = force_stg ? force_stg : 2;
+    if (stg == 2) hipLaunchKernelGGL(small_gemm_dma_kernel<2>, dim3(tiles), dim3(256), 0, s, b);
+    else if (stg == 3) hipLaunchKernelGGL(small_gemm_dma_kernel<3>, dim3(tiles), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL(small_gemm_dma_kernel<4>, dim3(tiles), dim3(256), 0, s, b);
+  }
   else if (v == 1) {
     if (dt == 0) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, false, true, true>), dim3(tiles), dim3(256), 0, s, b);
     else if (dt == 1) hipLaunchKernelGGL((small_gemm_kernel<2, 2, true, false, true, true, true>), dim3(tiles), dim3(256), 0, s, b);

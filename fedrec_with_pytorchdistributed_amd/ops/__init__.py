@@ -314,7 +314,8 @@ def small_gemm(*gs: Gemm, dev_off=None, tile: int = 0) -> None:
     """Run up to 6 independent GEMMs in one launch (device only).  ``dev_off``: an int64[1]
     device counter added to every dropout offset (HIP-graph replays draw fresh masks).
     Operands A / B may be fp32 or bf16 (C fp32).  ``tile``: 0 = the launcher's choice, 1..4 =
-    64x64 / 128x64 / 64x128 / 128x128 (benchmarks)."""
+    64x64 / 128x64 / 64x128 / 128x128, 5 = 64x64 without the LDS-DMA ring of the bf16 x bf16
+    k-contiguous launches (benchmarks / tests)."""
     ints, floats, seeds = [], [], []
     for g in gs:
         ints += [g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.a_mode, g.b_mode, g.act, int(g.accumulate), g.drop_ld,

@@ -184,3 +184,29 @@ def test_asum_column_sums_of_a(dev, tile, ah):
         assert _rel(g.C, want) < 2e-3
         ref = A.double().sum(0)
         assert torch.allclose(a_s.double(), ref, rtol=1e-5, atol=1e-3), float((a_s.double() - ref).abs().max())
+
+
+@pytest.mark.parametrize("MNK", [(3200, 1200, 400), (1565, 400, 768), (77, 45, 136), (64, 64, 64), (3, 200, 1200),
+                                 (200, 400, 3200), (5000, 72, 8)])
+def test_dma_ring_matches_register_queue_bitwise(dev, MNK):
+    """bf16 x bf16 k-contiguous launches take the LDS-DMA ring (tile 0 / 1); tile 5 forces the
+    register-queue 64 x 64 kernel: same tiles, same k order -> bitwise equal C, with row / column
+    / k tails, split-K partials, bias + tanh, the dropout epilogue and accumulate."""
+    torch.manual_seed(11)
+    M, N, K = MNK
+    A = (torch.randn(M, K + 8, device=dev)).to(torch.bfloat16)  # ld > K: a strided view of rows
+    B = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    C0 = torch.randn(M, N, device=dev)
+    kw = dict(bias=bias, act=1) if K < 1000 else dict(accumulate=True, pdrop=0.2, drop_on=3, drop_ld=N - N % 16 + 16,
+                                                     seed=4, offset=5)
+    outs = []
+    for tile in (5, 0, 1):
+        C = C0.clone()
+        g = Gemm(A, B, C, M, N, K, K + 8, K, N, **kw)
+        if tile == 5:
+            want = ops.small_gemm_ref(g)
+        ops.small_gemm(g, tile=tile)
+        outs.append(C)
+    assert _rel(outs[0], want) < 2e-3
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
