@@ -412,12 +412,17 @@ __global__ __launch_bounds__(256) void upool_fwd_kernel(const float* __restrict_
 
 // grid (n, US): every block forms da (full x . g dots), then its quarter of the rows: dpre,
 // the dw2 partial of those rows (partial row n US + y), dx_direct; db2 from block 0 (others 0)
+// dpre_b (optional): dpre rounded to bf16 as well -- the operand of the bf16 input-gradient GEMM
+// dctx += dpre W1 (the weight gradient keeps the fp32 dpre: its column sums are att_fc1's bias
+// gradient, which cancels to a few per cent of the terms' size -- bf16 terms measured 6 % off)
+template <bool BF = false>
 __global__ __launch_bounds__(256) void upool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ e,
                                                         const float* __restrict__ alpha, const float* __restrict__ w2,
                                                         const float* __restrict__ g, float* __restrict__ dx,
-                                                        float* __restrict__ dpre, float* __restrict__ dw2,
+                                                        void* __restrict__ dpre_, float* __restrict__ dw2,
                                                         float* __restrict__ db2, int T, int D, int Q,
-                                                        float* __restrict__ da8) {
+                                                        float* __restrict__ da8, bf16* __restrict__ dpre_b = nullptr) {
+  float* const dpre = (float*)dpre_;
   __shared__ float da_s[UT], al_s[UT];
   __shared__ float part[UT][4];
   __shared__ float4 red[4][64];
@@ -469,9 +474,11 @@ __global__ __launch_bounds__(256) void upool_bwd_kernel(const float* __restrict_
         const float4 v = ((const float4*)(e + ((size_t)n * T + t) * Q))[qc];
         const float da = da_s[t];
         acc.x += da * v.x; acc.y += da * v.y; acc.z += da * v.z; acc.w += da * v.w;
-        ((float4*)(dpre + ((size_t)n * T + t) * Q))[qc] =
-            make_float4(da * w.x * (1.f - v.x * v.x), da * w.y * (1.f - v.y * v.y), da * w.z * (1.f - v.z * v.z),
-                        da * w.w * (1.f - v.w * v.w));
+        const float4 dp = make_float4(da * w.x * (1.f - v.x * v.x), da * w.y * (1.f - v.y * v.y),
+                                      da * w.z * (1.f - v.z * v.z), da * w.w * (1.f - v.w * v.w));
+        ((float4*)(dpre + ((size_t)n * T + t) * Q))[qc] = dp;
+        if constexpr (BF)
+          *(bf16x4*)(dpre_b + ((size_t)n * T + t) * Q + 4 * qc) = bf16x4{f2bf(dp.x), f2bf(dp.y), f2bf(dp.z), f2bf(dp.w)};
       }
     }
     if (dw2 != nullptr) {  // block-uniform
@@ -545,8 +552,8 @@ extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* a
     const uintptr_t al = (uintptr_t)x | (uintptr_t)e | (uintptr_t)w2 | (uintptr_t)g | (uintptr_t)dpre |
                          (uintptr_t)(dx ? dx : g);
     if (al & 15) return 3;  // 16-byte rows (fresh tensors and 256-B aligned parameter views)
-    hipLaunchKernelGGL(upool_bwd_kernel, dim3(n, US), dim3(256), 0, s, (const float*)x, (const float*)e, alpha, w2, g, dx,
-                       (float*)dpre, dw2, db2, T, D, Q, nullptr);
+    hipLaunchKernelGGL(upool_bwd_kernel<false>, dim3(n, US), dim3(256), 0, s, (const float*)x, (const float*)e, alpha, w2,
+                       g, dx, dpre, dw2, db2, T, D, Q, nullptr, nullptr);
     return -1;
   }
   if (R != n) return 1;
@@ -568,14 +575,20 @@ extern "C" int fr_additive_pool_bwd(const void* x, const void* e, const float* a
 // da8 [n T, 8] (zeros elsewhere) and the caller adds dw2 = e^T da, db2 = sum da to its weight-
 // gradient launch (a small-GEMM desc with M = 8; db2 from that desc's column sums) -- two
 // deterministic colsum launches fewer per step.  fp32 short-sequence shapes only (upool_ok).
+// dpre_b != nullptr: dpre rounded to bf16 as well (8-byte aligned rows: Q % 4 == 0)
 extern "C" int fr_upool_bwd_da(const float* x, const float* e, const float* alpha, const float* w2, const float* g,
-                               float* dx, float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s) {
+                               float* dx, float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s,
+                               void* dpre_b) {
   if (!upool_ok(T, D, Q, 0)) return 1;
   const uintptr_t al = (uintptr_t)x | (uintptr_t)e | (uintptr_t)w2 | (uintptr_t)g | (uintptr_t)dpre |
-                       (uintptr_t)(dx ? dx : g) | (uintptr_t)da8;
+                       (uintptr_t)(dx ? dx : g) | (uintptr_t)da8 | (uintptr_t)(dpre_b ? dpre_b : dpre);
   if (al & 15) return 3;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(upool_bwd_kernel, dim3(n, US), dim3(256), 0, s, x, e, alpha, w2, g, dx, dpre, nullptr, nullptr, T,
-                     D, Q, da8);
+  if (dpre_b != nullptr)
+    hipLaunchKernelGGL(upool_bwd_kernel<true>, dim3(n, US), dim3(256), 0, s, x, e, alpha, w2, g, dx, dpre, nullptr,
+                       nullptr, T, D, Q, da8, (bf16*)dpre_b);
+  else
+    hipLaunchKernelGGL(upool_bwd_kernel<false>, dim3(n, US), dim3(256), 0, s, x, e, alpha, w2, g, dx, dpre, nullptr,
+                       nullptr, T, D, Q, da8, nullptr);
   return 0;
 }

@@ -61,9 +61,9 @@ int fr_ipc_destroy(int id);
 int fr_ipc_allreduce_local(const int* ids, void* const* xs, int W, long n, int is_int, long long epoch, int mode,
                            int blocks, double timeout_s, hipStream_t s);
 int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, const int* keep,
-                     hipStream_t s);
-int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H, int NH,
-                     int dk, const int* keep, hipStream_t s);
+                     hipStream_t s, void* ctx_b);
+int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, void* dqkv, int B, int H, int NH,
+                     int dk, const int* keep, hipStream_t s, int out_bf16);
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
                 int C, int D, int sigm, const int* ci, float* loss_total, hipStream_t s);
 int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U, int D,
@@ -120,7 +120,7 @@ int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, cons
                   hipStream_t s);
 long fr_colsum_f32(const float* const* xs, float* const* outs, const int* ints, int n, float* part, hipStream_t s);
 int fr_upool_bwd_da(const float* x, const float* e, const float* alpha, const float* w2, const float* g, float* dx,
-                    float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s);
+                    float* dpre, float* da8, int n, int T, int D, int Q, hipStream_t s, void* dpre_b);
 int fr_dropout_add_bf16(const void* h, const void* res, void* out, long n, float p, unsigned long long seed,
                         unsigned long long offset, hipStream_t s);
 int fr_title_attention_drop_bf16(const void* qkv, const int* mask, void* out, int n_titles, int T, int H, int D,
@@ -605,9 +605,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad(const at::
 }
 
 // user pool backward with da out (column 0 of [n T, 8]) instead of dw2 / db2 (fr_upool_bwd_da)
-std::tuple<at::Tensor, at::Tensor, at::Tensor> upool_bwd_da(const at::Tensor& x, const at::Tensor& e,
-                                                            const at::Tensor& alpha, const at::Tensor& w2,
-                                                            const at::Tensor& g) {
+// bf16_out: dpre rounded to bf16 as a fourth output (the bf16 dctx GEMM's operand); otherwise
+// the fourth output is empty
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> upool_bwd_da(const at::Tensor& x, const at::Tensor& e,
+                                                                        const at::Tensor& alpha, const at::Tensor& w2,
+                                                                        const at::Tensor& g, bool bf16_out) {
   for (auto* t : {&x, &e, &alpha, &w2, &g}) {
     check_dev(*t, "upool_bwd_da input");
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "fedrec::upool_bwd_da: contiguous fp32");
@@ -619,11 +621,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> upool_bwd_da(const at::Tensor& x,
   auto dx = at::empty({n, T, D}, x.options());
   auto dpre = at::empty({n, T, Q}, x.options());
   auto da8 = at::empty({n * T, 8}, x.options());
+  auto dpre_b = at::empty({bf16_out ? n : 0, T, Q}, x.options().dtype(at::kBFloat16));
   check_rc(fr_upool_bwd_da(x.data_ptr<float>(), e.data_ptr<float>(), alpha.data_ptr<float>(), w2.data_ptr<float>(),
                            g.data_ptr<float>(), dx.data_ptr<float>(), dpre.data_ptr<float>(), da8.data_ptr<float>(),
-                           (int)n, (int)T, (int)D, (int)Q, cur_stream()),
+                           (int)n, (int)T, (int)D, (int)Q, cur_stream(), bf16_out ? dpre_b.data_ptr() : nullptr),
            "upool_bwd_da");
-  return {dx, dpre, da8};
+  return {dx, dpre, da8, dpre_b};
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_pool_bwd(
@@ -666,8 +669,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> additive_
   return {dx, dpre, dw2, db2, dsum};
 }
 
+// ctx_b (optional, bf16 [B, H, heads * head_dim], written): ctx rounded to bf16 as well
 std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int64_t heads, int64_t head_dim,
-                                                      const c10::optional<at::Tensor>& keep) {
+                                                      const c10::optional<at::Tensor>& keep,
+                                                      const c10::optional<at::Tensor>& ctx_b) {
   check_dev(qkv, "qkv");
   TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.dim() == 3, "fedrec::user_attention_fwd: fp32 [B,H,3D]");
   const c10::DeviceGuard g(qkv.device());
@@ -675,26 +680,36 @@ std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int
   TORCH_CHECK(qkv.size(2) == 3 * heads * head_dim, "fedrec::user_attention_fwd: width");
   auto ctx = at::empty({B, H, heads * head_dim}, qkv.options());
   auto stats = at::empty({B, heads, H, 2}, qkv.options());
+  void* cb = nullptr;
+  if (ctx_b.has_value()) {
+    check_dev(*ctx_b, "ctx_b");
+    TORCH_CHECK(ctx_b->scalar_type() == at::kBFloat16 && ctx_b->numel() == ctx.numel(),
+                "fedrec::user_attention_fwd: ctx_b bf16 like ctx");
+    cb = H <= 64 ? ctx_b->data_ptr() : nullptr;  // long histories: converted below
+  }
   check_rc(fr_user_attn_fwd(qkv.data_ptr<float>(), ctx.data_ptr<float>(), stats.data_ptr<float>(), (int)B, (int)H,
-                            (int)heads, (int)head_dim, key_mask_ptr(keep, B, H, "user_attention_fwd"), cur_stream()),
+                            (int)heads, (int)head_dim, key_mask_ptr(keep, B, H, "user_attention_fwd"), cur_stream(), cb),
            "user_attention_fwd");
+  if (ctx_b.has_value() && cb == nullptr) ctx_b->copy_(ctx.view_as(*ctx_b));
   return {ctx, stats};
 }
 
+// bf16_out: dqkv in bf16 (the input / weight gradient GEMMs' operand)
 at::Tensor user_attention_bwd(const at::Tensor& qkv, const at::Tensor& stats, const at::Tensor& dctx, int64_t heads,
-                              int64_t head_dim, const c10::optional<at::Tensor>& keep) {
+                              int64_t head_dim, const c10::optional<at::Tensor>& keep, bool bf16_out) {
   check_dev(qkv, "qkv");
   check_dev(stats, "stats");
   check_dev(dctx, "dctx");
   const c10::DeviceGuard g(qkv.device());
   const int64_t B = qkv.size(0), H = qkv.size(1);
   auto d = dctx.to(at::kFloat).contiguous();
-  auto dqkv = at::empty_like(qkv);
-  check_rc(fr_user_attn_bwd(qkv.data_ptr<float>(), stats.data_ptr<float>(), d.data_ptr<float>(), dqkv.data_ptr<float>(),
+  const bool bf = bf16_out && H <= 64;  // long histories: converted below
+  auto dqkv = at::empty_like(qkv, bf ? qkv.options().dtype(at::kBFloat16) : qkv.options());
+  check_rc(fr_user_attn_bwd(qkv.data_ptr<float>(), stats.data_ptr<float>(), d.data_ptr<float>(), dqkv.data_ptr(),
                             (int)B, (int)H, (int)heads, (int)head_dim, key_mask_ptr(keep, B, H, "user_attention_bwd"),
-                            cur_stream()),
+                            cur_stream(), bf ? 1 : 0),
            "user_attention_bwd");
-  return dqkv;
+  return bf16_out && !bf ? dqkv.to(at::kBFloat16) : dqkv;
 }
 
 // ci (optional): candidates as rows of a table -- cand is then [U, D], candidate (b, c) its row
@@ -1547,10 +1562,10 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("head_pool_bwd(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor? nreal=None) -> (Tensor, Tensor)");
   m.def("head_wgrad(Tensor table, Tensor? ids, int T, Tensor e, Tensor da, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_fwd(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep=None) -> (Tensor, Tensor)");
-  m.def("upool_bwd_da(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g) -> (Tensor, Tensor, Tensor)");
+  m.def("upool_bwd_da(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool bf16_out=False) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
-  m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None) -> (Tensor, Tensor)");
-  m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None) -> Tensor");
+  m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None, Tensor(a!)? ctx_b=None) -> (Tensor, Tensor)");
+  m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None, bool bf16_out=False) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act, Tensor? ci=None, Tensor(a!)? dcand_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
   m.def("adam_dev(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale) -> ()");

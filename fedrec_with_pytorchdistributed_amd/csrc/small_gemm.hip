@@ -505,22 +505,53 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmBatch batch) 
   gemm_tile<FM, FN, FAST, AH, BH, TRI, DB>(g, off, t, As[0], Bs[0], As[DB ? 1 : 0], Bs[DB ? 1 : 0]);
 }
 
-// ---- bf16 x bf16, both operands K-contiguous (a_mode 0, b_mode 0): an LDS-DMA ring ------------
+// ---- bf16 x bf16 launches: an LDS-DMA ring ---------------------------------------------------
 // The register-queue tile above keeps one k-tile in flight (a deeper queue costs VGPRs and
-// measured slower), so a tile's k-steps are a chain of global-load latencies.
-// Here every k-tile goes global -> LDS by buffer_load ... lds (16 B per lane, no VGPR round
-// trip, out-of-range rows / k answered with zeros by the buffer descriptor), NSTG stages deep:
-// NSTG - 1 k-tiles in flight while the MFMAs read one.  64 x 64 tile, 4 waves in 2 x 2 (32 x 32
-// each = 2 x 2 MFMA fragments); LDS rows of 64 k (128 B), chunk c of row r at c ^ (r & 7) (the
-// swizzle goes on the source address: DMA images are lane-linear).  Same operands, k order and
-// epilogue as gemm_tile: results are bitwise those of the FAST bf16 kernel.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// measured slower), so a tile's k-steps are a chain of global-load latencies.  Here every
+// k-tile goes global -> LDS by buffer_load ... lds (16 B per lane, no VGPR round trip,
+// out-of-range rows / k answered with zeros by the buffer descriptor), NSTG stages deep.  64 x
+// 64 tile, 4 waves in 2 x 2 (32 x 32 each = 2 x 2 MFMA fragments).  Each operand's stage is 64
+// LDS rows of 128 B as it sits in memory: k-contiguous (mode 0) -> [64 rows][64 k], chunk c of
+// row r at c ^ (r & 7), fragments by ds_read_b128; stored transposed (mode 1) -> [64 k][64
+// rows], chunk c of row k at c ^ tsw(k) (the TRI image), fragments by two ds_read_b64_tr_b16.
+// The swizzle goes on the source address (DMA images are lane-linear).  Column sums of a
+// mode-1 A (asum, a weight gradient's bias gradient) come from one more MFMA per fragment
+// against a ones operand, in the column-0 tiles.  Same operands, k order and epilogue as
+// gemm_tile: C is bitwise that of the register-queue bf16 kernel.
 constexpr int DMA_STAGE = 2 * 64 * 128;  // A and B, 64 rows x 128 B each
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ u32x4 dma_read128(uint32_t addr) {
   u32x4 v;
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
   return v;
+}
+__device__ __forceinline__ s16x4 dma_read_tr(uint32_t addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+// MFMA fragment of rows col0 + lane % 16, k = ks + 8 (lane / 16) .. + 7, from a 128-B-row image
+// (opaque reads: a builtin LDS read after the DMA into the same array makes the compiler wait
+// for every load in flight).  TR: the image is [k][rows] (tri_frag's addressing).
+template <bool TR>
+__device__ __forceinline__ u32x4 dma_frag(uint32_t img, int ks, int col0, int lane) {
+  if constexpr (!TR) {
+    const int r = col0 + (lane & 15);
+    return dma_read128(img + r * 128 + ((((ks >> 3) + (lane >> 4)) ^ (r & 7)) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int c = (col0 >> 3) + (p >> 1);
+    s16x4 v[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int r = ks + 8 * g + 4 * hf + q;
+      v[hf] = dma_read_tr(img + r * 128 + ((c ^ tsw(r)) << 4) + (p & 1) * 8);
+    }
+    return u32x4{__builtin_bit_cast(uint2, v[0]).x, __builtin_bit_cast(uint2, v[0]).y,
+                 __builtin_bit_cast(uint2, v[1]).x, __builtin_bit_cast(uint2, v[1]).y};
+  }
 }
 
 template <int DMA_NSTG>
@@ -533,18 +564,26 @@ __device__ __forceinline__ void gemm_tile_dma(const GemmDesc& g, unsigned long l
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   const int fr = lane & 15, fq = lane >> 4;
   const __amdgpu_buffer_rsrc_t rsa = rsrc_of(g.A), rsb = rsrc_of(g.B);
-  // this lane's rows of the two 8-row pieces per operand (wave w: rows 16 w .. 16 w + 15)
+  const bool ta = g.a_mode == 1, tb = g.b_mode == 1;  // block-uniform
+  // this lane's rows of the two 8-row pieces per operand (wave w: LDS rows 16 w .. 16 w + 15)
   const int prow = lane >> 3, pch = lane & 7;
   auto stage = [&](int st, int k0) {
 #pragma unroll
     for (int op = 0; op < 2; ++op) {
       const bool isA = op == 0;
+      const bool tr = isA ? ta : tb;
       const int R = isA ? g.M : g.N, r0 = isA ? m0 : n0, ld = isA ? g.lda : g.ldb;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int row = wave * 16 + p * 8 + prow;
-        const int k = k0 + ((pch ^ (row & 7)) << 3);
-        const uint32_t o = (r0 + row < R && k < kend) ? (uint32_t)((r0 + row) * ld + k) * 2u : OOB;
+        uint32_t o;
+        if (!tr) {  // row = an output row / column, chunk = 8 k
+          const int k = k0 + ((pch ^ (row & 7)) << 3);
+          o = (r0 + row < R && k < kend) ? (uint32_t)((r0 + row) * ld + k) * 2u : OOB;
+        } else {  // row = a k, chunk = 8 output rows / columns
+          const int c = r0 + ((pch ^ tsw(row)) << 3);
+          o = (k0 + row < kend && c < R) ? (uint32_t)((k0 + row) * ld + c) * 2u : OOB;
+        }
         char* dst = smem + st * DMA_STAGE + op * 64 * 128 + (wave * 16 + p * 8) * 128;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsa : rsb, LDS_PTR(void, dst), 16, o, 0, 0, 0);
       }
@@ -555,6 +594,10 @@ __device__ __forceinline__ void gemm_tile_dma(const GemmDesc& g, unsigned long l
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // asum: the column-0 tiles' n-wave 0 also multiplies its A fragments by ones
+  const bool do_as = g.asum != nullptr && n0 == 0 && wn == 0;  // wave-uniform
+  f32x4 as_[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const bf16x8 ones = bf16x8{(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
   const int nk = (kend - kbeg + 63) >> 6;
 #pragma unroll
   for (int s = 0; s < DMA_NSTG - 1; ++s)
@@ -572,18 +615,12 @@ __device__ __forceinline__ void gemm_tile_dma(const GemmDesc& g, unsigned long l
     if (kt + DMA_NSTG - 1 < nk) stage((kt + DMA_NSTG - 1) % DMA_NSTG, kbeg + (kt + DMA_NSTG - 1) * 64);
     const uint32_t As = lds0 + (kt % DMA_NSTG) * DMA_STAGE, Bs = As + 64 * 128;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < 64; ks += 32) {
       u32x4 a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = wm + i * 16 + fr;
-        a[i] = dma_read128(As + r * 128 + (((ks * 4 + fq) ^ (r & 7)) << 4));
-      }
+      for (int i = 0; i < 2; ++i) a[i] = ta ? dma_frag<true>(As, ks, wm + i * 16, lane) : dma_frag<false>(As, ks, wm + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wn + j * 16 + fr;
-        b[j] = dma_read128(Bs + r * 128 + (((ks * 4 + fq) ^ (r & 7)) << 4));
-      }
+      for (int j = 0; j < 2; ++j) b[j] = tb ? dma_frag<true>(Bs, ks, wn + j * 16, lane) : dma_frag<false>(Bs, ks, wn + j * 16, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -591,10 +628,27 @@ __device__ __forceinline__ void gemm_tile_dma(const GemmDesc& g, unsigned long l
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i]),
                                                               __builtin_bit_cast(bf16x8, b[j]), acc[i][j], 0, 0, 0);
+      if (do_as) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          as_[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i]), ones, as_[i], 0, 0, 0);
+      }
     }
   }
-  // epilogue as gemm_tile: lane holds C[m = wm + 16 i + 4 fq + r][n = wn + 16 j + fr]
   const bool part = g.splits > 1;
+  if (do_as && fr == 0) {  // lanes of column 0 hold the row sums of rows wm + 16 i + 4 fq + r
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + i * 16 + fq * 4 + r;
+        if (m < g.M) {
+          if (part) g.AP[(size_t)split * g.M + m] = as_[i][r];
+          else g.asum[m] = as_[i][r];
+        }
+      }
+  }
+  // epilogue as gemm_tile: lane holds C[m = wm + 16 i + 4 fq + r][n = wn + 16 j + fr]
   float* const dst = part ? g.P + (size_t)split * g.M * g.N : g.C;
   const int ldd = part ? g.N : g.ldc;
 #pragma unroll
@@ -875,11 +929,12 @@ static bool fast_ok(const GemmBatch& b) {
   return fast;
 }
 
-// the LDS-DMA ring: both operands k-contiguous (16-B chunks straight into the LDS image), no
-// column sums (FAST already holds: no gather / operand dropout / kseg, 16-B aligned extents)
+// the LDS-DMA ring takes every bf16 x bf16 FAST launch (no gather / operand dropout / kseg,
+// 16-B aligned extents); M and N multiples of 8 where the operand is stored transposed (its
+// 16-B chunks run along them)
 static bool dma_ok(const GemmBatch& b) {
   for (int i = 0; i < b.n; ++i)
-    if (b.d[i].a_mode != 0 || b.d[i].b_mode != 0 || b.d[i].asum) return false;
+    if ((b.d[i].a_mode == 1 && b.d[i].M % 8) || (b.d[i].b_mode == 1 && b.d[i].N % 8)) return false;
   return true;
 }
 

@@ -187,10 +187,12 @@ __device__ __forceinline__ bool key_kept(const int* __restrict__ keep, int b, in
 
 // SR = 65: 33,008 B of LDS, four blocks per CU (64-row stages, five blocks per CU, measured
 // neutral: profiles/r3_ab_segsum_ua.txt)
+// ctx_b (optional): ctx rounded to bf16 as well (the att_fc1 GEMM's operand)
 template <int SR>
 __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   float* __restrict__ ctx, float* __restrict__ stats,
-                                                                  int H, int NH, const int* __restrict__ keep) {
+                                                                  int H, int NH, const int* __restrict__ keep,
+                                                                  bf16* __restrict__ ctx_b) {
   __shared__ __attribute__((aligned(16))) float qs[SR][DK];
   __shared__ __attribute__((aligned(16))) float ks[SR][DK];
   __shared__ __attribute__((aligned(16))) float vs[SR][DK];
@@ -282,6 +284,11 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
     if (row >= H) continue;
     dst[(size_t)row * D + fr] = o0[r] * inv[r];
     if (fr < DK - 16) dst[(size_t)row * D + 16 + fr] = o1[r] * inv[r];
+    if (ctx_b != nullptr) {
+      bf16* db = ctx_b + ((size_t)b * H + row) * D + h * DK;
+      db[fr] = f2bf(o0[r] * inv[r]);
+      if (fr < DK - 16) db[16 + fr] = f2bf(o1[r] * inv[r]);
+    }
     if (fr == 0) {
       float* st = stats + (((size_t)b * NH + h) * H + row) * 2;
       st[0] = mrow[r];
@@ -294,11 +301,15 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
 // one [64][PLDB] image: P first (dV = P^T dctx reads it), then, after a barrier, dS (dQ and
 // dK = dS^T Q); the dS values wait in registers (16 per lane) meanwhile.  (The first form kept
 // both images, 55,616 B: two blocks per CU, 2.5 rounds of the 1,280 (impression, head) blocks.)
-template <int SR, int PLDB>
+// OT: the dqkv element type (bf16: the input / weight gradient GEMMs' operand, rounded once here)
+__device__ __forceinline__ float cvt_out(float v, float*) { return v; }
+__device__ __forceinline__ bf16 cvt_out(float v, bf16*) { return f2bf(v); }
+
+template <int SR, int PLDB, typename OT = float>
 __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   const float* __restrict__ stats,
                                                                   const float* __restrict__ dctx,
-                                                                  float* __restrict__ dqkv, int H, int NH,
+                                                                  OT* __restrict__ dqkv, int H, int NH,
                                                                   const int* __restrict__ keep) {
   __shared__ __attribute__((aligned(16))) float qs[SR][DK];
   __shared__ __attribute__((aligned(16))) float ks[SR][DK];
@@ -347,7 +358,7 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   }
   __syncthreads();
   const float scale = rsqrtf((float)DK);
-  float* dst = dqkv + (size_t)b * H * ld + h * DK;
+  OT* dst = dqkv + (size_t)b * H * ld + h * DK;
   const int KS = (H + 3) / 4;
   const bool act = i0 < H;  // this wave's query / key tile holds real rows (wave-uniform)
   float dsv[4][4];          // this wave's dS rows (registers while P is read from LDS)
@@ -401,8 +412,8 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
     for (int r = 0; r < 4; ++r) {
       const int row = i0 + fq * 4 + r;
       if (row >= H) continue;
-      dst[(size_t)row * ld + 2 * D + fr] = v0[r];
-      if (fr < DK - 16) dst[(size_t)row * ld + 2 * D + 16 + fr] = v1[r];
+      dst[(size_t)row * ld + 2 * D + fr] = cvt_out(v0[r], dst);
+      if (fr < DK - 16) dst[(size_t)row * ld + 2 * D + 16 + fr] = cvt_out(v1[r], dst);
     }
   }
   __syncthreads();  // every wave done reading P: the image takes dS
@@ -426,8 +437,8 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
     for (int r = 0; r < 4; ++r) {
       const int row = i0 + fq * 4 + r;
       if (row >= H) continue;
-      dst[(size_t)row * ld + fr] = o0[r];
-      if (fr < DK - 16) dst[(size_t)row * ld + 16 + fr] = o1[r];
+      dst[(size_t)row * ld + fr] = cvt_out(o0[r], dst);
+      if (fr < DK - 16) dst[(size_t)row * ld + 16 + fr] = cvt_out(o1[r], dst);
     }
   }
   __syncthreads();  // every dS row in LDS
@@ -447,8 +458,8 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
   for (int r = 0; r < 4; ++r) {
     const int row = i0 + fq * 4 + r;
     if (row >= H) continue;
-    dst[(size_t)row * ld + D + fr] = k0[r];
-    if (fr < DK - 16) dst[(size_t)row * ld + D + 16 + fr] = k1[r];
+    dst[(size_t)row * ld + D + fr] = cvt_out(k0[r], dst);
+    if (fr < DK - 16) dst[(size_t)row * ld + D + 16 + fr] = cvt_out(k1[r], dst);
   }
 }
 
@@ -637,27 +648,37 @@ __global__ __launch_bounds__(64) void user_attn_bwd_long_kernel(const float* __r
 }  // namespace
 
 // keep: optional [B, H] int32 key mask (mask_padding)
+// ctx_b (optional, bf16 [B, H, NH dk]): ctx rounded to bf16 too -- short histories only (H <= 64;
+// returns 2 otherwise, before launching anything)
 extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk,
-                                const int* keep, hipStream_t s) {
+                                const int* keep, hipStream_t s, void* ctx_b) {
   if (dk != DK || H > MAXL || H < 1) return 1;
+  if (ctx_b != nullptr && H > MAXH) return 2;
   const int pairs = B * NH;
   if (pairs == 0) return 0;
   if (H > MAXH)
     hipLaunchKernelGGL(user_attn_fwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, ctx, stats, B, H, NH, keep);
   else
-    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<65>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep);
+    hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<65>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep,
+                       (bf16*)ctx_b);
   return 0;
 }
 
-extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, float* dqkv, int B, int H,
-                                int NH, int dk, const int* keep, hipStream_t s) {
+// out_bf16: dqkv is bf16 (short histories only; 2 otherwise, nothing launched)
+extern "C" int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, void* dqkv, int B, int H,
+                                int NH, int dk, const int* keep, hipStream_t s, int out_bf16) {
   if (dk != DK || H > MAXL || H < 1) return 1;
+  if (out_bf16 && H > MAXH) return 2;
   const int pairs = B * NH;
   if (pairs == 0) return 0;
   if (H > MAXH)
-    hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, dqkv, B, H, NH, keep);
-  else
-    hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<65, 68>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx, dqkv, H, NH,
+    hipLaunchKernelGGL(user_attn_bwd_long_kernel, dim3(pairs), dim3(64), 0, s, qkv, stats, dctx, (float*)dqkv, B, H, NH,
                        keep);
+  else if (out_bf16)
+    hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<65, 68, bf16>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx,
+                       (bf16*)dqkv, H, NH, keep);
+  else
+    hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<65, 68>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx,
+                       (float*)dqkv, H, NH, keep);
   return 0;
 }

@@ -162,19 +162,26 @@ def additive_pool_bwd(x, e, alpha, w2, g, want_dx: bool, want_colsum: bool = Fal
     return out + (None,) if want_colsum else out
 
 
-def user_attention_fwd(qkv, heads: int, head_dim: int, keep=None):
+def user_attention_fwd(qkv, heads: int, head_dim: int, keep=None, ctx_b=None):
     """-> ``(ctx [B,H,h*d], saved)``; ``saved`` is whatever the backward needs.  ``keep [B,H]``
-    int (nonzero = attend): the mask_padding key mask."""
+    int (nonzero = attend): the mask_padding key mask.  ``ctx_b`` (bf16, like ctx, device
+    only): also written with ctx rounded to bf16 (a GEMM operand)."""
     if _dev(qkv):
-        return tuple(native.require_for(qkv).user_attention_fwd(qkv.contiguous(), heads, head_dim, _mask32(keep)))
-    return ref.user_attention_fwd(qkv, heads, head_dim, keep=keep)
+        return tuple(native.require_for(qkv).user_attention_fwd(qkv.contiguous(), heads, head_dim, _mask32(keep),
+                                                                ctx_b))
+    out = ref.user_attention_fwd(qkv, heads, head_dim, keep=keep)
+    if ctx_b is not None:
+        ctx_b.copy_(out[0].reshape(ctx_b.shape))
+    return out
 
 
-def user_attention_bwd(qkv, saved, dctx, heads: int, head_dim: int, keep=None):
+def user_attention_bwd(qkv, saved, dctx, heads: int, head_dim: int, keep=None, bf16_out: bool = False):
+    """-> ``dqkv`` like qkv (bf16 with ``bf16_out``: the gradient GEMMs' operand)."""
     if _dev(qkv):
         return native.require_for(qkv).user_attention_bwd(qkv.contiguous(), saved, dctx.contiguous(),
-                                                          heads, head_dim, _mask32(keep))
-    return ref.user_attention_bwd(qkv, saved, dctx, heads, head_dim)  # the saved weights hold the mask
+                                                          heads, head_dim, _mask32(keep), bool(bf16_out))
+    d = ref.user_attention_bwd(qkv, saved, dctx, heads, head_dim)  # the saved weights hold the mask
+    return d.to(torch.bfloat16) if bf16_out else d
 
 
 def score_ce(cand, user, act: str = "sigmoid"):

@@ -157,12 +157,17 @@ class TextHeadFn(torch.autograd.Function):
             ctx.save_for_backward(table, ids, e, alpha, w2, nreal)
         ctx.T = T
         ctx.mark_non_differentiable(pooled_b)
+        # no zero tensor for pooled_b's (never used) gradient: autograd would otherwise fill one
+        # [U, D] bf16 buffer per backward (a 5.5 us fill launch in every config-2 step)
+        ctx.set_materialize_grads(False)
         return pooled, pooled_b
 
     @staticmethod
     def backward(ctx, g, g_b=None):
         table, ids, e, alpha, w2, nreal = ctx.saved_tensors
         lib = ops.native.require_for(table)
+        if g is None:
+            g = torch.zeros(ids.numel(), table.shape[-1], device=table.device)
         da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
         dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p, nreal)
         return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None, None, None, None
@@ -521,18 +526,21 @@ def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_
     qkv = torch.empty(BH, D3, device=dev, dtype=torch.float32)
     ops.small_gemm(ops.Gemm(xd, wb[:D3], qkv, BH, D3, D, D, D, D3, bias=bqkv))  # one N = 3D GEMM
     q3 = qkv.view(B, H, D3)
-    c3, stats = ops.user_attention_fwd(q3, heads, hd, keep)
+    # the attention also writes ctx rounded to bf16 -- what the att_fc1 GEMM and dW1 would round
+    # it to on their loads -- so both run as bf16 x bf16 launches (the LDS-DMA small GEMM)
+    c3b = torch.empty(B, H, D, device=dev, dtype=torch.bfloat16)
+    c3, stats = ops.user_attention_fwd(q3, heads, hd, keep, c3b)
     e = torch.empty(BH, Qd, device=dev, dtype=torch.float32)
-    ops.small_gemm(ops.Gemm(c3, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
+    ops.small_gemm(ops.Gemm(c3b, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
     e3 = e.view(B, H, Qd)
     u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2, keep)
-    return u, [q3, stats, c3, e3, alpha, wb, w2, xd]
+    return u, [q3, stats, c3, c3b, e3, alpha, wb, w2, xd]
 
 
 def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
     """Backward of :func:`_user_enc_fwd` for ``du [B, D]``: the input gradient goes into ``dx
     [B*H, D]`` (the dropout backward in the dgrad epilogue) -> the ten weight gradients."""
-    q3, stats, c3, e3, alpha, wb, w2, xd = saved
+    q3, stats, c3, c3b, e3, alpha, wb, w2, xd = saved
     D = c3.shape[-1]
     BH, D3 = B * H, 3 * D
     Qd = wb.shape[0] - D3
@@ -540,16 +548,23 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     # additive pool backward: dx_direct = alpha du, dpre = da w2 (1 - e^2); dw2 = e^T da and
     # db2 = sum da join the weight-gradient launch below (da as column 0 of [BH, 8]: a small-GEMM
     # desc with M = 8, db2 from its column sums) -- no partial rows, no colsum launches
+    # The producers also round their outputs to bf16 where a GEMM only consumes them (the values
+    # the GEMM's own fp32 loads rounded to): dpre for dctx += dpre W1 and dQ|dK|dV for the input
+    # and Q|K|V weight gradients -- bf16 x bf16 launches run on the LDS-DMA small GEMM.  The
+    # att_fc1 weight gradient keeps the fp32 dpre (its bias gradient is a near-cancelling column
+    # sum: from bf16 terms it measured 6 % off the fp32 oracle)
     lib = ops.native.require_for(c3)
     da8 = None
     if H <= 64 and c3.dtype == torch.float32 and e3.dtype == torch.float32:
-        dctx, dpre, da8 = lib.upool_bwd_da(c3.contiguous(), e3.contiguous(), alpha.contiguous(),
-                                           w2.reshape(-1).float().contiguous(), du.float().contiguous())
+        dctx, dpre, da8, dpre_b = lib.upool_bwd_da(c3.contiguous(), e3.contiguous(), alpha.contiguous(),
+                                                   w2.reshape(-1).float().contiguous(), du.float().contiguous(), True)
     else:
         dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
+        dpre_b = dpre.to(torch.bfloat16)
     dpre2 = dpre.view(BH, Qd)
-    ops.small_gemm(ops.Gemm(dpre2, wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1, accumulate=True))  # += dpre W1
-    dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep).view(BH, D3)
+    ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1,
+                            accumulate=True))  # += dpre W1
+    dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep, True).view(BH, D3)
     p, seed, off = drop
     # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,
     # the dropout backward in its epilogue
@@ -565,7 +580,7 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     gbqkv = torch.empty(D3, device=dev)
     gb1 = torch.empty(Qd, device=dev)
     wg = (ops.Gemm(dqkv, xd, gqkv, D3, D, BH, D3, D, D, a_mode=1, b_mode=1, asum=gbqkv),
-          ops.Gemm(dpre2, c3, gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
+          ops.Gemm(dpre2, c3b.view(BH, D), gw1, Qd, D, BH, Qd, D, D, a_mode=1, b_mode=1, asum=gb1))
     if da8 is not None:
         dw2 = torch.empty(8, Qd, device=dev)
         db2 = torch.empty(8, device=dev)

@@ -210,3 +210,31 @@ def test_dma_ring_matches_register_queue_bitwise(dev, MNK):
         outs.append(C)
     assert _rel(outs[0], want) < 2e-3
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("a_mode,b_mode", [(0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("MNK", [(3200, 400, 1200), (1200, 400, 3200), (72, 40, 300), (400, 768, 1568)])
+def test_dma_ring_transposed_operands_and_asum(dev, a_mode, b_mode, MNK):
+    """The DMA ring with stored-transposed operands (ds_read_b64_tr_b16 fragments) is bitwise the
+    register-queue kernel (tile 5), split-K or not; a transposed A's column sums (asum) come from
+    the ring's ones-MFMA and match a float64 sum of the same bf16 values."""
+    torch.manual_seed(12)
+    M, N, K = MNK
+    A = (torch.randn(M, K, device=dev) if a_mode == 0 else torch.randn(K, M, device=dev)).to(torch.bfloat16)
+    B = (torch.randn(N, K, device=dev) if b_mode == 0 else torch.randn(K, N, device=dev)).to(torch.bfloat16)
+    lda, ldb = (K if a_mode == 0 else M), (K if b_mode == 0 else N)
+    outs, sums = [], []
+    for tile in (5, 0):
+        C = torch.zeros(M, N, device=dev)
+        s = torch.full((M,), float("nan"), device=dev) if a_mode == 1 else None
+        g = Gemm(A, B, C, M, N, K, lda, ldb, N, a_mode=a_mode, b_mode=b_mode, asum=s)
+        if tile == 5:
+            want = ops.small_gemm_ref(g)
+        ops.small_gemm(g, tile=tile)
+        outs.append(C)
+        sums.append(s)
+    assert _rel(outs[1], want) < 2e-3
+    assert torch.equal(outs[0], outs[1])
+    if a_mode == 1:
+        ref = A.double().sum(0)
+        assert torch.allclose(sums[1].double(), ref, rtol=1e-5, atol=1e-3), float((sums[1].double() - ref).abs().max())

@@ -53,8 +53,11 @@ def test_graph_step_matches_eager(dev):
     p0, p1 = e0.model.flat.flat, e1.model.flat.flat
     rel = float((p1 - p0).norm() / p0.norm())
     # seven Adam steps over gradients that differ in fp32 summation order (the graph pads the
-    # unique-title list: other split-K partitions); Adam's normalisation carries that to ~1e-5
-    assert rel < 2e-5, rel
+    # unique-title list: other split-K partitions); Adam's normalisation carries that to ~1e-5,
+    # and the bf16 rounding of the user side's dQ|dK|dV (a GEMM operand, rounded once by its
+    # producer) turns some of those last-bit differences into bf16-ulp ones in the Q|K|V bias
+    # gradients: 2.5e-5 measured
+    assert rel < 5e-5, rel
     # one client: Adam ran inside the replayed graphs with its step count on the device
     assert any(k[-2] for k in e1._graphs), "the step graphs should carry the optimizer (no all-reduce)"
     assert e1.model.flat.step == e0.model.flat.step == len(batches)
