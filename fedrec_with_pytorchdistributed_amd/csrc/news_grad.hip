@@ -15,6 +15,8 @@
 // per-occurrence clip+noise pass is embarrassingly parallel; the segment sum is skewed.
 #include "common.h"
 
+#include <algorithm>
+
 #include <stdlib.h>
 
 namespace {
@@ -218,7 +220,66 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__
   for (int d = threadIdx.x; d < D; d += 256) out[(size_t)u * D + d] = ((part[0][d] + part[1][d]) + part[2][d]) + part[3][d];
 }
 
-int g_segsum_variant = 1;  // 1: chunked (default), 0: one block per output row (the no-scratch form)
+// float4 form of the chunked pass (D % 4 == 0, 16-B aligned rows; variant 2): a lane holds
+// columns 4 lane + 256 k (two float4 at D = 400) -- 2 loads per row instead of 7 scalar ones.
+// Same chunk grid and scratch slots as segsum_chunk_kernel (segsum_fix_kernel finishes both).
+constexpr int MAXV4 = 2;  // D <= 512
+template <int SC>
+__global__ __launch_bounds__(256) void segsum_chunk4_kernel(const float4* __restrict__ rows,
+                                                            const int* __restrict__ perm,
+                                                            const int* __restrict__ seg_ptr,
+                                                            const int* __restrict__ inv, float4* __restrict__ out,
+                                                            float4* __restrict__ scratch, int U, int R, int D4) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int p0 = c * SC;
+  if (p0 >= R) return;
+  const int p1 = min(p0 + SC, R);
+  int rr[SC];
+#pragma unroll
+  for (int j = 0; j < SC; ++j) rr[j] = perm[min(p0 + j, p1 - 1)];
+  int u = inv[rr[0]];  // segment of position p0
+  int s_beg = seg_ptr[u], s_end = seg_ptr[u + 1];
+  float4 v[SC][MAXV4];
+#pragma unroll
+  for (int j = 0; j < SC; ++j)
+#pragma unroll
+    for (int k = 0; k < MAXV4; ++k) {
+      const int d = lane + 64 * k;
+      v[j][k] = d < D4 ? rows[(size_t)rr[j] * D4 + d] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  float4 acc[MAXV4];
+#pragma unroll
+  for (int k = 0; k < MAXV4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < SC; ++j) {
+    const int pp = p0 + j;
+    if (pp < p1) {
+#pragma unroll
+      for (int k = 0; k < MAXV4; ++k) {
+        acc[k].x += v[j][k].x; acc[k].y += v[j][k].y; acc[k].z += v[j][k].z; acc[k].w += v[j][k].w;
+      }
+      if (pp + 1 == s_end || pp + 1 == p1) {  // flush the run of segment u
+        float4* dst;
+        if (s_beg >= p0 && s_end <= p1) dst = out + (size_t)u * D4;
+        else dst = scratch + ((size_t)c * 2 + (s_beg < p0 ? 0 : 1)) * D4;
+#pragma unroll
+        for (int k = 0; k < MAXV4; ++k) {
+          const int d = lane + 64 * k;
+          if (d < D4) dst[d] = acc[k];
+          acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (pp + 1 == s_end && pp + 1 < p1) {
+          ++u;
+          s_beg = s_end;
+          s_end = seg_ptr[u + 1];
+        }
+      }
+    }
+  }
+}
+
+int g_segsum_variant = 2;  // 2: chunked, float4 rows (default); 1: chunked, scalar; 0: one block per output row
 constexpr int SCH = 16;    // chunk length (8-occurrence chunks measured neutral, r3_ab_segsum_ua.txt)
 
 }  // namespace
@@ -243,7 +304,15 @@ extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int
                                    int U, int D, int R, float* scratch, hipStream_t s, int zero_empty) {
   if (D > 64 * MAXV) return 1;
   if (U == 0) return 0;
-  if (g_segsum_variant == 1 && scratch != nullptr && inv != nullptr && R > 0) {
+  if (g_segsum_variant == 2 && scratch != nullptr && inv != nullptr && R > 0 && D % 4 == 0 && D <= 256 * MAXV4 &&
+      (((uintptr_t)rows | (uintptr_t)out | (uintptr_t)scratch) & 15) == 0) {
+    const int nch = (R + SCH - 1) / SCH;
+    hipLaunchKernelGGL(segsum_chunk4_kernel<SCH>, dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows, perm,
+                       seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4);
+    hipLaunchKernelGGL(segsum_fix_kernel<SCH>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
+    return 0;
+  }
+  if (g_segsum_variant >= 1 && scratch != nullptr && inv != nullptr && R > 0) {
     const int nch = (R + SCH - 1) / SCH;
     hipLaunchKernelGGL(segsum_chunk_kernel<SCH>, dim3((nch + 3) / 4), dim3(256), 0, s, rows, perm, seg_ptr, inv, out,
                        scratch, U, R, D);

@@ -227,12 +227,13 @@ def test_dedup_and_segment_sum(dev, num_news, R):
     assert rel_err(out_c, oc_ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [1, 0])
-@pytest.mark.parametrize("R,D", [(3521, 400), (37, 400), (16, 64), (2000, 512)])
+@pytest.mark.parametrize("variant", [2, 1, 0])
+@pytest.mark.parametrize("R,D", [(3521, 400), (37, 400), (16, 64), (2000, 512), (300, 36)])
 def test_segment_sum_skewed(dev, variant, R, D):
     """Segment sums with a MIND-like skew (a ~30 % pad-row segment, Zipf-popular ids, many
     singletons; R not a multiple of the 16-row chunk): chunked form (1, default) and the
-    block-per-row form (0) against an fp64 index_add, bitwise reproducible run to run."""
+    block-per-row form (0) against an fp64 index_add, bitwise reproducible run to run; the float4
+    chunk pass (2, default) is bitwise the scalar one (1)."""
     g = torch.Generator().manual_seed(R + D)
     ids = torch.multinomial(1.0 / torch.arange(1, 600, dtype=torch.float64), R, replacement=True, generator=g)
     ids[torch.rand(R, generator=g) < 0.3] = 0
@@ -244,8 +245,11 @@ def test_segment_sum_skewed(dev, variant, R, D):
     try:
         out = ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr))
         assert torch.equal(ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr)), out)
+        if variant == 2:
+            lib.segsum_set_variant(1)
+            assert torch.equal(ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr)), out)
     finally:
-        lib.segsum_set_variant(1)
+        lib.segsum_set_variant(2)
     o_ref = torch.zeros(uniq.numel(), D, dtype=torch.float64).index_add_(0, inv.long().cpu(), rows.double().cpu())
     assert rel_err(out, o_ref) < 1e-6
 
