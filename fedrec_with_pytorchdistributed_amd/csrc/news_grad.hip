@@ -181,8 +181,9 @@ template <int SCH>
 __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__ seg_ptr, float* __restrict__ out,
                                                          const float* __restrict__ scratch, int U, int D) {
   // partials of a crossing segment: [scratch[c0][1], scratch[c0+1][0], ..., scratch[c1][0]];
-  // wave w sums entries w, w+4, w+8, ... (4 loads in flight), then the 4 sums add in order --
-  // a fixed partition, so the result does not depend on timing
+  // wave w sums entries w, w+4, w+8, ... (8 loads in flight: the pad row's ~120 partials are a
+  // chain of load rounds), then the 4 sums add in order -- a fixed partition, so the result
+  // does not depend on timing
   __shared__ float part[4][64 * MAXV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int u = blockIdx.x;
@@ -197,10 +198,10 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__
   float acc[MAXV];
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) acc[k] = 0.f;
-  for (int i0 = w; i0 < n; i0 += 16) {
-    float v[4][MAXV];
+  for (int i0 = w; i0 < n; i0 += 32) {
+    float v[8][MAXV];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 8; ++j) {
       const int i = i0 + 4 * j;
       const size_t slot = i == 0 ? (size_t)c0 * 2 + 1 : (size_t)(c0 + i) * 2;
 #pragma unroll
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int k = 0; k < MAXV; ++k) acc[k] += v[j][k];
   }

@@ -284,10 +284,14 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
     if (row >= H) continue;
     dst[(size_t)row * D + fr] = o0[r] * inv[r];
     if (fr < DK - 16) dst[(size_t)row * D + 16 + fr] = o1[r] * inv[r];
-    if (ctx_b != nullptr) {
+    if (ctx_b != nullptr) {  // lane pairs (fr, fr ^ 1) -> one 4-byte bf16x2 store by the even lane
       bf16* db = ctx_b + ((size_t)b * H + row) * D + h * DK;
-      db[fr] = f2bf(o0[r] * inv[r]);
-      if (fr < DK - 16) db[16 + fr] = f2bf(o1[r] * inv[r]);
+      const float c0 = o0[r] * inv[r], c1 = o1[r] * inv[r];
+      const float n0 = dpp<DPP_XOR1>(c0), n1 = dpp<DPP_XOR1>(c1);
+      if ((fr & 1) == 0) {
+        *(bf16x2*)(db + fr) = bf16x2{f2bf(c0), f2bf(n0)};
+        if (fr < DK - 16) *(bf16x2*)(db + 16 + fr) = bf16x2{f2bf(c1), f2bf(n1)};
+      }
     }
     if (fr == 0) {
       float* st = stats + (((size_t)b * NH + h) * H + row) * 2;
