@@ -35,7 +35,7 @@ torch.manual_seed(0)
 out = []
 
 
-def run(name, make, tiles=(0, 5, 6, 7, 8)):
+def run(name, make, tiles=(0, 5, 6, 9)):
     for dt in ("f32", "bf16"):
         gs = make(dt)
         if gs is None:
@@ -51,7 +51,7 @@ def cvt(x, dt):
     return x.to(bf) if dt == "bf16" else x
 
 
-BH, D, D3, Qd, U, TD = 3200, 400, 1200, 200, 1565, 768
+BH, D, D3, Qd, U, TD = 3200, 400, 1200, 200, 1600, 768  # U: the step graph pads the unique titles
 x_b = torch.randn(BH, D, device=dev).to(bf)
 wqkv_b = (torch.randn(D3 + Qd, D, device=dev) * 0.05).to(bf)
 w1t_b = wqkv_b[D3:].t().contiguous()  # [D, Qd]
@@ -78,7 +78,24 @@ run("dgrad_nt_on_wt", lambda dt: [Gemm(cvt(dqkv, dt), wqkvt_b, torch.empty(BH, D
 run("wgrads_tn", lambda dt: [Gemm(cvt(dqkv, dt), x_b, torch.empty(D3, D, device=dev), D3, D, BH, D3, D, D, a_mode=1,
                                   b_mode=1, asum=torch.empty(D3, device=dev)),
                              Gemm(cvt(dpre, dt), cvt(c3, dt), torch.empty(Qd, D, device=dev), Qd, D, BH, Qd, D, D,
-                                  a_mode=1, b_mode=1, asum=torch.empty(Qd, device=dev))], tiles=(0,))
+                                  a_mode=1, b_mode=1, asum=torch.empty(Qd, device=dev))], tiles=(0, 9))
+# the user backward's weight-gradient launch as the step issues it (dgrad + Q|K|V weight gradient
+# on bf16 dQ|dK|dV, dW1 on the fp32 dpre: the mixed kernel) and its all-bf16 part alone
+dqkv_b, c3b = dqkv.to(bf), c3.to(bf)
+da8 = torch.randn(BH, 8, device=dev)
+e3 = torch.randn(BH, Qd, device=dev)
+run("user_wg_launch", lambda dt: [Gemm(dqkv_b, wqkv_b[:D3], torch.empty(BH, D, device=dev), BH, D, D3, D3, D, D, b_mode=1),
+                                  Gemm(dqkv_b, x_b, torch.empty(D3, D, device=dev), D3, D, BH, D3, D, D, a_mode=1,
+                                       b_mode=1, asum=torch.empty(D3, device=dev)),
+                                  Gemm(dpre, c3b, torch.empty(Qd, D, device=dev), Qd, D, BH, Qd, D, D, a_mode=1,
+                                       b_mode=1, asum=torch.empty(Qd, device=dev)),
+                                  Gemm(da8, e3, torch.empty(8, Qd, device=dev), 8, Qd, BH, 8, Qd, Qd, a_mode=1, b_mode=1,
+                                       asum=torch.empty(8, device=dev))] if dt == "bf16" else None, tiles=(0,))
+run("user_wg_bf16_part", lambda dt: [Gemm(dqkv_b, wqkv_b[:D3], torch.empty(BH, D, device=dev), BH, D, D3, D3, D, D,
+                                          b_mode=1),
+                                     Gemm(dqkv_b, x_b, torch.empty(D3, D, device=dev), D3, D, BH, D3, D, D, a_mode=1,
+                                          b_mode=1, asum=torch.empty(D3, device=dev))] if dt == "bf16" else None,
+    tiles=(0, 9))
 run("fc_fwd", lambda dt: [Gemm(pooled_b, fc_b, torch.empty(U, D, device=dev), U, D, TD, TD, TD, D)]
     if dt == "bf16" else None)
 run("fc_dgrad_nn", lambda dt: [Gemm(cvt(dnews, dt), fc_b, torch.empty(U, TD, device=dev), U, TD, D, D, TD, TD,

@@ -880,7 +880,7 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const ColsumBatch bat
 // descs: 8 pointers + 16 ints + 2 floats + 2 u64 per GEMM, packed by binding.cpp small_gemm.
 // scratch: split-K partial space (floats) the caller allocated; returns the floats it needs
 // when scratch is null (query mode).
-static int choose_splits(int tiles, int K) {
+static int choose_splits(int tiles, int K, bool dma) {
   // a workgroup's k-steps are a chain of dependent global-load latencies (one k-tile in
   // flight): a long reduction over few output tiles is latency bound, not bandwidth bound.
   // Split K until the launch has ~2 workgroups per CU, keeping >= 6 k-tiles per split
@@ -888,7 +888,11 @@ static int choose_splits(int tiles, int K) {
   // 400-row descs in 6 splits 49 us; the 3200 x 400 x 1200 dgrad in 350 tiles -- 2 splits
   // 38.6 us, 3 splits 44.5: the partials' write + reduce outweigh the shorter chains).
   // fewest K per split: 384 (6 k-tiles) measured best of 192-768 (profiles/r3_ab_sg_mink.txt)
-  constexpr int mink = 384;
+  // The LDS-DMA ring keeps a k-tile in flight behind the MFMAs, so its k-steps are cheap: it
+  // splits only above 1,024 per split (the 3200 x 400 x 1200 dgrad 19.9 vs 22.4 us with 2
+  // splits, the text fc 13.6 vs 15.0; the K = 3200 weight gradients still want theirs:
+  // profiles/r4_sg_step_shapes_r.json)
+  const int mink = dma ? 1024 : 384;
   if (K < 512) return 1;
   const int want = (512 + tiles - 1) / tiles;
   int s = min(want, K / mink);
@@ -981,13 +985,19 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   b.n = n;
   const bool fast = fast_ok(b), mixed = mixed_dtypes(b);
   // benchmarks / tests: 5 = the 64 x 64 register-queue form (never the DMA ring), 6 / 7 / 8 =
-  // the DMA ring with 2 / 3 / 4 stages where it applies
+  // the DMA ring with 2 / 3 / 4 stages where it applies, 9 = 2 stages and no split-K
   const bool regq = tile == 5;
-  const int force_stg = (tile >= 6 && tile <= 8) ? tile - 4 : 0;
+  const int force_stg = (tile >= 6 && tile <= 8) ? tile - 4 : (tile == 9 ? 2 : 0);
+  const bool nosplit = tile == 9;  // benchmarks: the 2-stage DMA ring without split-K
   int v = (tile >= 1 && tile <= 4) ? tile : (regq || force_stg) ? 1 : choose_tile(b);
   if (!fast || mixed) v = 1;  // the generic (any alignment) and mixed-dtype kernels: 64 x 64
   int tm, tn;
   tile_dims(v, tm, tn);
+  const int dt = (b.d[0].a_bf16 ? 2 : 0) | (b.d[0].b_bf16 ? 1 : 0);
+  // a DMA-ring launch (its split-K rule also applies to the register-queue form of the same
+  // launch, tile 5, so the two stay bitwise comparable)
+  const bool dma_shape = fast && !mixed && v == 1 && dt == 3 && dma_ok(b);
+  const bool dma = dma_shape && !regq;
   int tiles = 0;
   long need = 0;
   int red_blocks = 0;
@@ -996,7 +1006,7 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     d.tiles_n = (d.N + tn - 1) / tn;
     const int t = ((d.M + tm - 1) / tm) * d.tiles_n;
     // split-K: the reduce applies the whole epilogue (alpha, bias, tanh, output dropout, accumulate)
-    d.splits = choose_splits(t, d.K);
+    d.splits = nosplit ? 1 : choose_splits(t, d.K, dma_shape);
     d.kchunk = d.splits > 1 ? ((d.K + d.splits - 1) / d.splits + TK - 1) / TK * TK : d.K;
     if (d.splits > 1) d.splits = (d.K + d.kchunk - 1) / d.kchunk;
     if (d.splits > 1 && d.N % 4 != 0) {  // the reduction takes 4 columns per lane
@@ -1020,7 +1030,6 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   }
   if (scratch == nullptr && need > 0) return need;  // query: the caller allocates and calls again
   if (tiles == 0) return 0;
-  const int dt = (b.d[0].a_bf16 ? 2 : 0) | (b.d[0].b_bf16 ? 1 : 0);
 #define SG_LAUNCH(FM, FN)                                                                                  \
   do {                                                                                                     \
     if (dt == 0)                                                                                           \
@@ -1040,7 +1049,7 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     hipLaunchKernelGGL((small_gemm_kernel<2, 2, false, false, false>), dim3(tiles), dim3(256), 0, s, b);
   else if (mixed)
     hipLaunchKernelGGL((small_gemm_mixed_kernel<true, true>), dim3(tiles), dim3(256), 0, s, b);
-  else if (v == 1 && dt == 3 && !regq && dma_ok(b)) {
+  else if (dma) {
     // two stages by default: a third / fourth measured slower on every config-2 shape (LDS per
     // block caps the blocks per CU; profiles/r4_sg_step_shapes.json)
     const int stg = force_stg ? force_stg : 2;
