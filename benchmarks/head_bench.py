@@ -52,6 +52,11 @@ def main():
     out = []
     t = timeit(lambda: lib.head_score(table, ids, T, w1, b1, w2, b2, True), a.iters)
     out.append({"kernel": "head_score", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1)})
+    for rows in (192, 160):  # the row tile forced (the default picks by the rounds rule)
+        lib.head_score_set_rows(rows)
+        t = timeit(lambda: lib.head_score(table, ids, T, w1, b1, w2, b2, True), a.iters)
+        out.append({"kernel": f"head_score_{rows}rows", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1)})
+    lib.head_score_set_rows(0)
     t = timeit(lambda: lib.head_pool(table, ids, T, sc, None), a.iters)
     out.append({"kernel": "head_pool", "us": round(t, 1), "TBs": round(M * D * 2 / t / 1e6, 2)})
     t = timeit(lambda: lib.head_pool_bwd(table, ids, T, alpha, gout), a.iters)

@@ -70,6 +70,7 @@ int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, 
                         int R, float* scratch, hipStream_t s, int zero_empty);
 int fr_segsum_chunks(int R);
 void fr_segsum_set_variant(int v);
+void fr_head_score_set_rows(int r);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
                 unsigned long long offset, hipStream_t s, const unsigned long long* dev_off);
 int fr_adam_dev(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
@@ -1526,6 +1527,7 @@ void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
 void score_set_variant(int64_t v) { fr_score_set_variant((int)v); }
 void segsum_set_variant(int64_t v) { fr_segsum_set_variant((int)v); }
+void head_score_set_rows(int64_t r) { fr_head_score_set_rows((int)r); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 
 }  // namespace
@@ -1536,6 +1538,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
   m.def("score_set_variant(int v) -> ()", &score_set_variant);
   m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
+  m.def("head_score_set_rows(int r) -> ()", &head_score_set_rows);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("linear_gelu_bwd(Tensor x, Tensor w, Tensor z) -> (Tensor, Tensor)");

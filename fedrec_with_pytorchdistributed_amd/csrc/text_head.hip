@@ -1167,8 +1167,11 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const f32x4* __restric
 }
 
 int g_cus = 0;
+int g_score_rows = 0;  // head_score2 row tile: 0 = by the rounds rule, 160 / 192 forced (benchmarks)
 
 }  // namespace
+
+extern "C" void fr_head_score_set_rows(int r) { g_score_rows = r; }
 
 extern "C" int fr_head_supported(int D, int Q, int T) {
   return D % 256 == 0 && D <= 1024 && (Q == 128 || Q == 256 || Q == 384) && T >= 1 && T <= MAXT;
@@ -1183,9 +1186,25 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
   // Q = 384 (the DistilBERT head): 192-row tiles, BK 64, 2 stages, staged LDS waits (steady step
   // 0.5452-0.5473 vs 0.5477-0.5520 ms for one wait, profiles/r3_ab_score_sw.txt; the X-only
   // LDS ring with W1 fragments from L2 ran 100 vs 75 us, profiles/r4_ab_head_score3.txt)
+  // Row tile: one block per CU, so the grid runs in ceil(blocks / CUs) rounds, each as long as
+  // its block's stages ((rows + 384) x 128 B per k-tile): 160-row tiles when that gives fewer
+  // stage bytes over the rounds than 192 (M = 80,000 on 256 CUs: 500 blocks in 2 rounds of 544
+  // vs 417 in 2 rounds of 576)
   if (Q == 384) {
-    hipLaunchKernelGGL((head_score2_kernel<6, 6, 64, 2, 4, true>), dim3((M + 191) / 192), dim3(512), 0, s,
-                       (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
+    if (g_cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_cus <= 0) g_cus = 256;
+    }
+    const long rounds192 = ((M + 191) / 192 + g_cus - 1) / g_cus, rounds160 = ((M + 159) / 160 + g_cus - 1) / g_cus;
+    const bool r160 = g_score_rows == 160 || (g_score_rows == 0 && rounds160 * (160 + 384) < rounds192 * (192 + 384));
+    if (r160)
+      hipLaunchKernelGGL((head_score2_kernel<6, 5, 64, 2, 4, true>), dim3((M + 159) / 160), dim3(512), 0, s,
+                         (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
+    else
+      hipLaunchKernelGGL((head_score2_kernel<6, 6, 64, 2, 4, true>), dim3((M + 191) / 192), dim3(512), 0, s,
+                         (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
     return 0;
   }
   const dim3 grid((M + 127) / 128);
