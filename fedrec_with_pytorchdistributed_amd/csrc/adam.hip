@@ -58,12 +58,44 @@ extern "C" int fr_adam_flat(float* p, const float* g, float* m, float* v, void* 
 // double, then rounded as the host path rounds them); block 0 also copies this step's loss
 // into slot (t - 1) % ring of a loss ring (no per-step clone launch).
 namespace {
-__global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, const float4* __restrict__ g,
+// Gradient segments (optional): the fresh per-parameter gradient tensors where autograd left
+// them -- segment j covers flat elements [off[j], off[j] + n[j]) (off 4-aligned: the flat
+// buffer aligns every parameter to 64 elements) and reads src[j]; the flat elements between
+// segments (alignment gaps) are 0.  The kernel writes each gathered value into the flat
+// gradient as it goes, so the flat buffer ends the step as the separate copy launch
+// (FlatParams.end_backward's multi_cast) left it.
+constexpr int ADAM_SEG = 48;
+struct AdamSegs {
+  const float* src[ADAM_SEG];
+  long off[ADAM_SEG];
+  long n[ADAM_SEG];
+  int nseg;
+};
+
+__device__ __forceinline__ float4 seg_grad4(const AdamSegs& sg, long e) {  // flat elements e .. e + 3
+  int lo = 0, hi = sg.nseg - 1;  // last segment with off <= e
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (sg.off[mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  const long r = e - sg.off[lo];
+  const float* src = sg.src[lo];
+  const long n = sg.n[lo];
+  if (src == nullptr || r < 0 || r >= n) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if (r + 4 <= n && (((uintptr_t)(src + r)) & 15) == 0) return *(const float4*)(src + r);
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  float* oa = (float*)&o;
+  for (int k = 0; k < 4 && r + k < n; ++k) oa[k] = src[r + k];
+  return o;
+}
+
+__global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, float4* __restrict__ g,
                                                        float4* __restrict__ m, float4* __restrict__ v,
                                                        bf16x4* __restrict__ plow, long n4, float lr, float b1, float b2,
                                                        float eps, float gs, const long long* __restrict__ step,
                                                        const float* __restrict__ loss, float* __restrict__ ring,
-                                                       int ring_n) {
+                                                       int ring_n, const AdamSegs segs) {
   // t = the device step count, already advanced for this step by the step's cast launch (an
   // earlier kernel of the same stream): no read-modify-write here (a same-address ticket per
   // block made this launch 20 us, against 7 for the eager kernel)
@@ -77,7 +109,14 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, c
   const float bc1 = bc_s[0], bc2 = bc_s[1];
   const float step_size = lr / bc1, inv_sqrt_bc2 = 1.0f / sqrtf(bc2);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    float4 gg;
+    if (segs.nseg > 0) {  // block-uniform
+      gg = seg_grad4(segs, 4 * i);
+      g[i] = gg;
+    } else {
+      gg = g[i];
+    }
+    float4 pp = p[i], mm = m[i], vv = v[i];
     float* pa = (float*)&pp;
     float* ga = (float*)&gg;
     float* ma = (float*)&mm;
@@ -100,16 +139,28 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, c
 
 }  // namespace
 
-extern "C" int fr_adam_dev(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1,
+// nseg > 0: the gradient is gathered from the segments (gsrc / goff / gn, sorted by offset;
+// a null source = no gradient) and written into g
+extern "C" int fr_adam_dev(float* p, float* g, float* m, float* v, void* plow, long n, float lr, float b1,
                            float b2, float eps, float grad_scale, const long long* step, const float* loss, float* ring,
-                           int ring_n, hipStream_t s) {
+                           int ring_n, hipStream_t s, int nseg, const float* const* gsrc, const long* goff,
+                           const long* gn) {
   if (n % 4 != 0 || (ring != nullptr && (loss == nullptr || ring_n < 1))) return 1;
+  if (nseg < 0 || nseg > ADAM_SEG) return 2;
+  AdamSegs segs{};
+  segs.nseg = nseg;
+  for (int j = 0; j < nseg; ++j) {
+    if (goff[j] % 4 != 0 || (j > 0 && goff[j] < goff[j - 1] + gn[j - 1]) || goff[j] + gn[j] > n) return 3;
+    segs.src[j] = gsrc[j];
+    segs.off[j] = goff[j];
+    segs.n[j] = gn[j];
+  }
   const long n4 = n / 4;
   long blocks = (n4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(adam_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (float4*)p, (const float4*)g, (float4*)m,
-                     (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, grad_scale, step, loss, ring, ring_n);
+  hipLaunchKernelGGL(adam_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (float4*)p, (float4*)g, (float4*)m,
+                     (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, grad_scale, step, loss, ring, ring_n, segs);
   return 0;
 }
 // ---------------------------------------------------------------------------------------

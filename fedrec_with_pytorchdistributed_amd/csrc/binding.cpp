@@ -73,9 +73,9 @@ void fr_segsum_set_variant(int v);
 void fr_head_score_set_rows(int r);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
                 unsigned long long offset, hipStream_t s, const unsigned long long* dev_off);
-int fr_adam_dev(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
-                float eps, float grad_scale, const long long* step, const float* loss, float* ring, int ring_n,
-                hipStream_t s);
+int fr_adam_dev(float* p, float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2, float eps,
+                float grad_scale, const long long* step, const float* loss, float* ring, int ring_n, hipStream_t s,
+                int nseg, const float* const* gsrc, const long* goff, const long* gn);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
@@ -822,8 +822,12 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
 
 // Adam with the step count (and the per-step loss ring) on the device: capturable in a graph.
 // step: int64 [1], already advanced for this step (the step's cast launch, multi_cast bump2)
-void adam_dev(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, const at::Tensor& step,
-              const at::Tensor& loss, at::Tensor ring, double lr, double b1, double b2, double eps, double grad_scale) {
+// gsrc / goff (optional): the step's per-parameter gradient tensors and their flat offsets --
+// Adam gathers the gradient from them and writes it into g (no separate copy launch)
+void adam_dev(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const at::Tensor& step,
+              const at::Tensor& loss, at::Tensor ring, double lr, double b1, double b2, double eps, double grad_scale,
+              const c10::optional<std::vector<c10::optional<at::Tensor>>>& gsrc,
+              const c10::optional<std::vector<int64_t>>& goff) {
   for (auto* t : {&p, &m, &v}) check_dev(*t, "adam_dev buffer");
   check_dev(g, "g");
   check_dev(step, "step");
@@ -842,10 +846,26 @@ void adam_dev(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, con
                 "fedrec::adam_dev: fp32 loss [1] and ring");
   }
   const c10::DeviceGuard dg(p.device());
+  std::vector<const float*> sp;
+  std::vector<long> so, sn;
+  if (gsrc.has_value()) {
+    TORCH_CHECK(goff.has_value() && goff->size() == gsrc->size(), "fedrec::adam_dev: gsrc / goff sizes");
+    for (size_t j = 0; j < gsrc->size(); ++j) {
+      const auto& t = (*gsrc)[j];
+      if (t.has_value()) {
+        check_dev(*t, "adam_dev gradient segment");
+        TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "fedrec::adam_dev: fp32 contiguous grads");
+      }
+      sp.push_back(t.has_value() ? t->data_ptr<float>() : nullptr);
+      so.push_back((long)(*goff)[j]);
+      sn.push_back(t.has_value() ? (long)t->numel() : 0L);
+    }
+  }
   check_rc(fr_adam_dev(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), nullptr,
                        (long)p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale,
                        (const long long*)step.data_ptr<int64_t>(), has_ring ? loss.data_ptr<float>() : nullptr,
-                       has_ring ? ring.data_ptr<float>() : nullptr, (int)ring.numel(), cur_stream()),
+                       has_ring ? ring.data_ptr<float>() : nullptr, (int)ring.numel(), cur_stream(), (int)sp.size(),
+                       sp.data(), so.data(), sn.data()),
            "adam_dev");
 }
 
@@ -1571,7 +1591,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None, bool bf16_out=False) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act, Tensor? ci=None, Tensor(a!)? dcand_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
-  m.def("adam_dev(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale) -> ()");
+  m.def("adam_dev(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale, Tensor?[]? gsrc=None, int[]? goff=None) -> ()");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset, bool valid=False) -> (Tensor, Tensor)");

@@ -32,6 +32,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace {
 
 constexpr int MAXT = 128;
@@ -1197,7 +1199,10 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
       (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (g_cus <= 0) g_cus = 256;
     }
-    const long rounds192 = ((M + 191) / 192 + g_cus - 1) / g_cus, rounds160 = ((M + 159) / 160 + g_cus - 1) / g_cus;
+    // a padded step graph (nreal given): blocks past the real titles exit at once, and the real
+    // count is the padded one less up to a bucket (128 titles) -- judge the rounds at mid-bucket
+    const long Me = nreal != nullptr ? std::max<long>((long)M - 64L * T, (long)T) : (long)M;
+    const long rounds192 = ((Me + 191) / 192 + g_cus - 1) / g_cus, rounds160 = ((Me + 159) / 160 + g_cus - 1) / g_cus;
     const bool r160 = g_score_rows == 160 || (g_score_rows == 0 && rounds160 * (160 + 384) < rounds192 * (192 + 384));
     if (r160)
       hipLaunchKernelGGL((head_score2_kernel<6, 5, 64, 2, 4, true>), dim3((M + 159) / 160), dim3(512), 0, s,

@@ -67,9 +67,27 @@ class FlatParams:
         for p in self.params:
             p.grad = None
 
-    def end_backward(self) -> None:
+    def end_backward(self, copy: bool = True):
         """Gather the fresh gradients into the flat buffer (one multi-tensor copy launch;
-        parameters that got no gradient are zeroed) and re-point ``.grad`` at it."""
+        parameters that got no gradient are zeroed) and re-point ``.grad`` at it.
+
+        ``copy=False`` (the in-graph Adam, which gathers them itself -- csrc/adam.hip gradient
+        segments): no copy launch; returns each parameter's gradient source in parameter
+        order -- the fresh tensor, its flat slot when the gradient already sits there, or None
+        (no gradient: Adam writes zeros) -- for the caller to hand to Adam, which writes them
+        into the flat buffer.  The caller keeps the list alive until Adam is queued."""
+        if not copy:
+            srcs = []
+            for p, off in zip(self.params, self.offsets):
+                view = self.grad[off:off + p.numel()].view_as(p)
+                gr = p.grad
+                if gr is not None and gr.data_ptr() != view.data_ptr() and (gr.dtype != torch.float32
+                                                                           or not gr.is_contiguous()):
+                    view.copy_(gr)  # (not expected on the fused step: every gradient is fresh fp32)
+                    gr = view
+                srcs.append(gr)
+                p.grad = view
+            return srcs
         dst, src, missing = [], [], []
         for p, off in zip(self.params, self.offsets):
             view = self.grad[off:off + p.numel()].view_as(p)

@@ -122,6 +122,9 @@ class _StepGraph:
             # when eager steps of other engines run between the captures
             # in-graph Adam: the step's cast launch (its first kernel) advances the device step count
             eng._adam_bump = eng._adam_step_dev if with_adam else None
+            # the in-graph Adam gathers the step's gradients from where autograd left them and
+            # writes them into the flat buffer itself: no separate copy launch (6 us per step)
+            eng._adam_gathers = with_adam
             with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
                 self.loss = eng.forward_backward(self.cand, self.his, static)
                 if with_adam:  # no all-reduce between backward and optimizer: the step in one graph
@@ -129,6 +132,8 @@ class _StepGraph:
         finally:
             eng._pre_hid = None
             eng._adam_bump = None
+            eng._adam_gathers = False
+            eng._grad_srcs = None
 
     def load(self, pre: Prepared, U: int) -> None:
         """The batch into the static inputs: one multi-copy launch; the unique list is padded
@@ -186,6 +191,8 @@ class LocalEngine:
         self.ldp_seed = (int(cfg.seed) << 20) + 7919 * int(rank) + 3
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
         self._adam_bump = None  # set while capturing a step graph with Adam in it (see _StepGraph)
+        self._adam_gathers = False  # ... and then Adam gathers the gradients (no end_backward copy)
+        self._grad_srcs = None
         self._inflight = collections.deque()  # (held batch, end event or None), see _retire
         self._held_n = 0
         # hidden states of the step's unique titles gathered ahead (the step graph's first part)
@@ -448,7 +455,10 @@ class LocalEngine:
                 loss.backward(self._seed_one())
             if casts is None:
                 self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
-            self.flat.end_backward()
+            if self._adam_gathers:  # the in-graph Adam reads the fresh gradients where they are
+                self._grad_srcs = self.flat.end_backward(copy=False)
+            else:
+                self.flat.end_backward()
             return loss.detach()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True, pre=pre)
         with obs.range("user_fwd"):
@@ -490,9 +500,10 @@ class LocalEngine:
         also copies the step's loss into the loss ring.  The host mirror ``flat.step`` is
         advanced by the caller per replay."""
         c = self.cfg
+        srcs, self._grad_srcs = self._grad_srcs, None
         native.require_for(loss).adam_dev(self.flat.flat, self.flat.grad, self.flat.m, self.flat.v, self._adam_step_dev,
                                           loss.reshape(1).float(), self._loss_ring, c.lr, c.adam_beta1, c.adam_beta2,
-                                          c.adam_eps, 1.0)
+                                          c.adam_eps, 1.0, srcs, list(self.flat.offsets) if srcs is not None else None)
 
     # ---- HIP graph of the per-step forward + backward ------------------------------------
     GRAPH_BUCKET = 128  # unique titles are padded up to a multiple of this (padded rows: id 0)
