@@ -73,7 +73,8 @@ def test_graph_step_matches_eager(dev):
     assert int(e1._adam_step_dev.item()) == e1.model.flat.step == e0.model.flat.step
     rel = float((e1.model.flat.flat - e0.model.flat.flat).norm() / e0.model.flat.flat.norm())
     assert rel < 5e-5, rel  # two more Adam steps of bf16-rounding differences
-    # the replayed graph wrote the gradient of the LAST step into the same flat buffer
+    # the replayed graph wrote the gradient of the LAST step into the same flat buffer (the
+    # in-graph Adam gathers it from the step's gradient tensors: no separate copy launch)
     g0, g1 = e0.model.flat.grad, e1.model.flat.grad
     assert float((g1 - g0).norm()) <= 2e-2 * float(g0.norm()) + 1e-8
 
