@@ -70,6 +70,10 @@ int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, 
                         int R, float* scratch, hipStream_t s, int zero_empty);
 int fr_segsum_chunks(int R);
 void fr_segsum_set_variant(int v);
+int fr_user_pool_score(const float* x, const float* e, const float* w2, const float* b2, const int* keep,
+                       const float* cand, const int* ci, int B, int T, int D, int Q, int C, int sigm, float* lossb,
+                       float* scores, float* dcand, float* loss_total, float* dctx, float* dpre, void* dpre_b,
+                       float* da8, hipStream_t s);
 void fr_head_score_set_rows(int r);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
                 unsigned long long offset, hipStream_t s, const unsigned long long* dev_off);
@@ -711,6 +715,56 @@ at::Tensor user_attention_bwd(const at::Tensor& qkv, const at::Tensor& stats, co
                             cur_stream(), bf ? 1 : 0),
            "user_attention_bwd");
   return bf16_out && !bf ? dqkv.to(at::kBFloat16) : dqkv;
+}
+
+// The user side's tail in one launch (csrc/score_ce.hip user_pool_score_kernel): the additive
+// pool of ctx [B, T, D] with scores from e [B, T, Q], the candidate scores + CE against rows
+// ci of the table, their gradients into dcand_out [B C, D], and (want_bwd) the pool's backward
+// for du.  -> (loss, scores, dctx, dpre, dpre_b, da8); an empty loss when the shape is outside
+// the kernel's domain (the caller takes the separate kernels).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> user_pool_score(
+    const at::Tensor& x, const at::Tensor& e, const at::Tensor& w2, const at::Tensor& b2,
+    const c10::optional<at::Tensor>& keep, const at::Tensor& table, const at::Tensor& ci, int64_t act,
+    at::Tensor dcand_out, bool want_bwd) {
+  for (const at::Tensor* t : {&x, &e, &w2, &b2, &table, &ci}) check_dev(*t, "user_pool_score input");
+  check_dev(dcand_out, "dcand_out");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && e.scalar_type() == at::kFloat && w2.scalar_type() == at::kFloat &&
+                  b2.scalar_type() == at::kFloat && table.scalar_type() == at::kFloat &&
+                  ci.scalar_type() == at::kInt && dcand_out.scalar_type() == at::kFloat && x.dim() == 3 &&
+                  e.dim() == 3 && table.dim() == 2,
+              "fedrec::user_pool_score: fp32 x [B,T,D], e [B,T,Q], table [U,D]; int32 ci");
+  const c10::DeviceGuard g(x.device());
+  const int64_t B = x.size(0), T = x.size(1), D = x.size(2), Q = e.size(2);
+  TORCH_CHECK(e.size(0) == B && e.size(1) == T && w2.numel() == Q && table.size(1) == D && B > 0 &&
+                  ci.numel() % B == 0 && dcand_out.numel() == ci.numel() * D,
+              "fedrec::user_pool_score: shapes");
+  const int64_t C = ci.numel() / B;
+  auto fo = x.options();
+  auto lossb = at::empty({B + 1}, fo);
+  auto loss = lossb.narrow(0, B, 1).squeeze(0);
+  auto scores = at::empty({B, C}, fo);
+  const int64_t nb = want_bwd ? B : 0;
+  auto dctx = at::empty({nb, T, D}, fo);
+  auto dpre = at::empty({nb, T, Q}, fo);
+  auto dpre_b = at::empty({nb, T, Q}, fo.dtype(at::kBFloat16));
+  auto da8 = at::empty({nb * T, 8}, fo);
+  const int* kp = nullptr;
+  at::Tensor k32;
+  if (keep.has_value() && keep->defined()) {
+    k32 = keep->to(at::kInt).contiguous();
+    TORCH_CHECK(k32.numel() == B * T, "fedrec::user_pool_score: keep [B, T]");
+    kp = k32.data_ptr<int>();
+  }
+  const int rc = fr_user_pool_score(x.contiguous().data_ptr<float>(), e.contiguous().data_ptr<float>(),
+                                    w2.contiguous().data_ptr<float>(), b2.data_ptr<float>(), kp, table.data_ptr<float>(),
+                                    ci.data_ptr<int>(), (int)B, (int)T, (int)D, (int)Q, (int)C, (int)act,
+                                    lossb.data_ptr<float>(), scores.data_ptr<float>(), dcand_out.data_ptr<float>(),
+                                    loss.data_ptr<float>(), want_bwd ? dctx.data_ptr<float>() : nullptr,
+                                    want_bwd ? dpre.data_ptr<float>() : nullptr,
+                                    want_bwd ? dpre_b.data_ptr() : nullptr, want_bwd ? da8.data_ptr<float>() : nullptr,
+                                    cur_stream());
+  if (rc != 0) return {at::empty({0}, fo), scores, dctx, dpre, dpre_b, da8};
+  return {loss, scores, dctx, dpre, dpre_b, da8};
 }
 
 // ci (optional): candidates as rows of a table -- cand is then [U, D], candidate (b, c) its row
@@ -1558,6 +1612,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
   m.def("score_set_variant(int v) -> ()", &score_set_variant);
   m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
+  m.def("user_pool_score(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep, Tensor table, Tensor ci, int act, Tensor(a!) dcand_out, bool want_bwd) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("head_score_set_rows(int r) -> ()", &head_score_set_rows);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
@@ -1644,6 +1699,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("user_attention_fwd", &user_attention_fwd);
   m.impl("user_attention_bwd", &user_attention_bwd);
   m.impl("score_ce", &score_ce);
+  m.impl("user_pool_score", &user_pool_score);
   m.impl("segment_sum_rows", &segment_sum_rows);
   m.impl("adam_flat", &adam_flat);
   m.impl("adam_dev", &adam_dev);

@@ -501,7 +501,8 @@ def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     return w1b, (wb, bqkv), fcb
 
 
-def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None):
+def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None,
+                  pool: bool = True):
     """Device user encoder forward over history rows ``src[idx]`` (``src [*, D]`` fp32, ``idx``
     int32 [B*H]) -> ``(u [B, D] fp32, saved)``.
 
@@ -533,11 +534,13 @@ def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_
     e = torch.empty(BH, Qd, device=dev, dtype=torch.float32)
     ops.small_gemm(ops.Gemm(c3b, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
     e3 = e.view(B, H, Qd)
+    if not pool:  # the caller runs the pool fused with the scores (UserStepFn)
+        return None, [q3, stats, c3, c3b, e3, None, wb, w2, xd]
     u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2, keep)
     return u, [q3, stats, c3, c3b, e3, alpha, wb, w2, xd]
 
 
-def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep):
+def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, pre=None):
     """Backward of :func:`_user_enc_fwd` for ``du [B, D]``: the input gradient goes into ``dx
     [B*H, D]`` (the dropout backward in the dgrad epilogue) -> the ten weight gradients."""
     q3, stats, c3, c3b, e3, alpha, wb, w2, xd = saved
@@ -555,7 +558,9 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
     # sum: from bf16 terms it measured 6 % off the fp32 oracle)
     lib = ops.native.require_for(c3)
     da8 = None
-    if H <= 64 and c3.dtype == torch.float32 and e3.dtype == torch.float32:
+    if pre is not None:  # the pool's backward ran fused with the forward (user_pool_score)
+        dctx, dpre, dpre_b, da8 = pre
+    elif H <= 64 and c3.dtype == torch.float32 and e3.dtype == torch.float32:
         dctx, dpre, da8, dpre_b = lib.upool_bwd_da(c3.contiguous(), e3.contiguous(), alpha.contiguous(),
                                                    w2.reshape(-1).float().contiguous(), du.float().contiguous(), True)
     else:
@@ -604,17 +609,35 @@ class UserStepFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, v, inv, perm, ptr, wq, bq, wk, bk, wv, bv, w1, b1, w2, b2, meta):
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one, casts = meta
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one, casts, grad_on = meta
         D = v.shape[1]
         BC = B * C
+        # the pool, the scores / loss and the pool's backward in one launch (user_pool_score)
+        # where its domain holds; the separate kernels otherwise
+        fuse = v.is_cuda and H <= 64 and C <= 16 and 256 <= D <= 512 and D % 4 == 0
         u, saved = _user_enc_fwd(v, inv[BC:], (wq, bq, wk, bk, wv, bv, w1, b1, w2, b2), B, H, heads, hd, drop,
-                                 dev_off, keep, casts)
+                                 dev_off, keep, casts, pool=not fuse)
         # per-occurrence news gradients: the candidate rows come straight from the scoring
         # kernel (candidates read from v by index: no gathered copy), the history rows from the
         # user encoder's dgrad in the backward
         rows = torch.empty(inv.numel(), D, device=v.device, dtype=torch.float32)
-        loss, scores, du = ops.score_ce_rows(v, inv[:BC], u, act, rows[:BC])
-        ctx.save_for_backward(v, inv, perm, ptr, rows, du, *saved)
+        tail = ()
+        if fuse:
+            c3, e3 = saved[2], saved[4]
+            want_bwd = grad_on and any(ctx.needs_input_grad)  # (validation: forward only)
+            loss, scores, *tail = ops.native.require_for(v).user_pool_score(
+                c3, e3, w2.reshape(-1).float().contiguous(), b2.reshape(-1).float().contiguous(), keep, v,
+                inv[:BC], 1 if act == "sigmoid" else 0, rows[:BC], want_bwd)
+            if loss.numel() == 0:  # outside the fused kernel's domain after all
+                fuse, tail = False, ()
+                u, saved[5] = ops.additive_pool_fwd(c3, e3, w2, b2, keep)
+            elif not want_bwd:
+                tail = ()
+            du = None
+        if not fuse:
+            loss, scores, du = ops.score_ce_rows(v, inv[:BC], u, act, rows[:BC])
+        ctx.n_tail = len(tail)
+        ctx.save_for_backward(v, inv, perm, ptr, rows, du, *saved, *tail)
         ctx.meta = meta
         ctx.mark_non_differentiable(scores)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the scores (one fill launch)
@@ -623,12 +646,19 @@ class UserStepFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gloss, gscores):
         v, inv, perm, ptr, rows, du, *saved = ctx.saved_tensors
-        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one, _ = ctx.meta
+        pre = None
+        if ctx.n_tail:
+            saved, pre = saved[:-ctx.n_tail], list(saved[-ctx.n_tail:])
+        B, C, H, heads, hd, act, drop, dev_off, ldp, padded, keep, one, _, _ = ctx.meta
         BC = B * C
         if gloss is not one:  # the engine seeds the backward with its persistent ones tensor: no scale
             rows[:BC].mul_(gloss)
-            du = du * gloss
-        grads = _user_enc_bwd(saved, du, rows[BC:], B, H, heads, hd, drop, dev_off, keep)
+            if pre is not None:  # the fused tail's backward pieces are linear in the loss gradient
+                for t in pre:
+                    t.mul_(gloss)
+            else:
+                du = du * gloss
+        grads = _user_enc_bwd(saved, du, rows[BC:], B, H, heads, hd, drop, dev_off, keep, pre)
         clip, noise, lseed, loff = ldp
         # the noise offset's step part is the device counter (dev_off): graph replays draw fresh noise
         dv = ops.segment_sum_rows(rows, inv, v.shape[0], clip, noise, lseed, loff, seg=(perm, ptr), zero_empty=padded,
@@ -646,7 +676,7 @@ def user_step(v, inv, perm, ptr, user_encoder, B: int, C: int, H: int, act: str,
     if keep is not None:
         keep = keep.reshape(B, H)
         keep = keep if keep.dtype == torch.int32 and keep.is_contiguous() else keep.to(torch.int32).contiguous()
-    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded, keep, one, casts)
+    meta = (B, C, H, mha.n_heads, mha.d_k, act, drop, dev_off, ldp, padded, keep, one, casts, torch.is_grad_enabled())
     return UserStepFn.apply(v, inv, perm, ptr, mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias,
                             mha.W_V.weight, mha.W_V.bias, pool.att_fc1.weight, pool.att_fc1.bias,
                             pool.att_fc2.weight, pool.att_fc2.bias, meta)
