@@ -995,8 +995,11 @@ std::tuple<at::Tensor, at::Tensor> sample_batch(const at::Tensor& rows, const at
   TORCH_CHECK(neg_ptr.numel() == pos.numel() + 1 && his_ptr.numel() == pos.numel() + 1, "fedrec::sample_batch: CSR");
   const c10::DeviceGuard g(rows.device());
   const int64_t B = rows.numel();
-  auto cand = at::empty({B, npratio + 1}, rows.options());
-  auto hout = at::empty({B, H}, rows.options());
+  // cand and his side by side in one buffer: the dedup reads [cand | his] as one id list without
+  // a concatenating copy (LocalEngine.prepare)
+  auto both = at::empty({B * (npratio + 1) + B * H}, rows.options());
+  auto cand = both.narrow(0, 0, B * (npratio + 1)).view({B, npratio + 1});
+  auto hout = both.narrow(0, B * (npratio + 1), B * H).view({B, H});
   check_rc(fr_sample_batch(rows.data_ptr<int>(), pos.data_ptr<int>(), (const long long*)neg_ptr.data_ptr<int64_t>(),
                            negs.data_ptr<int>(), (const long long*)his_ptr.data_ptr<int64_t>(), his.data_ptr<int>(),
                            cand.data_ptr<int>(), hout.data_ptr<int>(), (int)B, (int)npratio, (int)H, truncate ? 1 : 0,

@@ -49,6 +49,17 @@ from ..utils import obs
 from .news_cache import HiddenCache
 
 
+def _adjacent_ids(c: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """``[cand | his]`` flattened: a view when the device sampler wrote them side by side in one
+    buffer (no concatenating copy launch), else a cat."""
+    if (c.is_contiguous() and h.is_contiguous() and c.dtype == h.dtype and c.device == h.device
+            and c.untyped_storage().data_ptr() == h.untyped_storage().data_ptr()
+            and h.storage_offset() == c.storage_offset() + c.numel()):
+        return torch.empty(0, dtype=c.dtype, device=c.device).set_(c.untyped_storage(), c.storage_offset(),
+                                                                   (c.numel() + h.numel(),), (1,))
+    return torch.cat([c.reshape(-1), h.reshape(-1)])
+
+
 class Prepared(NamedTuple):
     """A sampled batch with its dedup done ahead of time (``LocalEngine.prepare``)."""
 
@@ -358,7 +369,7 @@ class LocalEngine:
         with torch.cuda.stream(self._prep):
             c, h = batch_fn()
             c, h = self.to_device(c), self.to_device(h)
-            ids = torch.cat([c.reshape(-1), h.reshape(-1)])
+            ids = _adjacent_ids(c, h)
             dd = ops.dedup(ids, self.N)
             ev = None
             if ids.numel() > self.DEDUP_SYNC_MAX:  # the sort path queues work after its count read
@@ -382,7 +393,7 @@ class LocalEngine:
                 torch.cuda.current_stream(self.device).wait_event(pre.ready)
             uniq, inv, perm, ptr = pre.dedup
         else:
-            ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
+            ids = _adjacent_ids(cand, his)
             uniq, inv, perm, ptr = ops.dedup(ids, self.N)
         with obs.range("news_encode"):
             v = self.news_vectors(uniq, grad=grad_news)
@@ -426,7 +437,7 @@ class LocalEngine:
             if pre.ready is not None:
                 torch.cuda.current_stream(self.device).wait_event(pre.ready)
             return pre.dedup
-        return tuple(ops.dedup(torch.cat([cand.reshape(-1), his.reshape(-1)]), self.N))
+        return tuple(ops.dedup(_adjacent_ids(cand, his), self.N))
 
     def forward_backward(self, cand: torch.Tensor, his: torch.Tensor, pre: Optional[Prepared] = None) -> torch.Tensor:
         """Loss of one batch with every trainable gradient left in ``flat.grad``."""
@@ -800,7 +811,7 @@ class LocalEngine:
                                                   limit):
             cand, his = self.to_device(cand_np), self.to_device(his_np)
             B, C = cand.shape
-            ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
+            ids = _adjacent_ids(cand, his)
             if self.fused_user:  # the fused device user side, forward only (eval: no dropout)
                 if table is not None:
                     v, inv = table, ids.to(torch.int32)
@@ -847,7 +858,7 @@ class LocalEngine:
         s0 = 0
         for cand, his in self._vsampler.valid_batches(batch_size, limit):
             B = cand.shape[0]
-            ids = torch.cat([cand.reshape(-1), his.reshape(-1)])
+            ids = _adjacent_ids(cand, his)
             loss, s = self._user_loss(table, (None, ids, ids, ids), B, C, his.shape[1], False, False, his)
             S[s0:s0 + B].copy_(s)
             lsum.add_(loss.float(), alpha=float(B))
