@@ -501,6 +501,31 @@ def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     return w1b, (wb, bqkv), fcb
 
 
+# Weight-gradient GEMMs of the user backward held back to ride in a later launch of the same
+# backward (HeadFCFn's: one launch and one split-K reduce fewer per step); an autograd
+# end-of-backward callback runs whatever is still pending, so a backward without that launch
+# still gets its gradients.  The tensors they write are returned to autograd right away (the
+# optimizer / end_backward read them only after the whole backward was queued).
+_PENDING_GEMMS: list = []
+
+
+def _flush_pending_gemms() -> None:
+    if _PENDING_GEMMS:
+        gs = list(_PENDING_GEMMS)
+        _PENDING_GEMMS.clear()
+        ops.small_gemm(*gs)
+
+
+def take_pending_gemms(room: int) -> list:
+    """Up to ``room`` pending weight-gradient GEMMs for a launch of the caller's (all of them or
+    none: they share a launch)."""
+    if not _PENDING_GEMMS or len(_PENDING_GEMMS) > room:
+        return []
+    gs = list(_PENDING_GEMMS)
+    _PENDING_GEMMS.clear()
+    return gs
+
+
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None,
                   pool: bool = True):
     """Device user encoder forward over history rows ``src[idx]`` (``src [*, D]`` fp32, ``idx``
@@ -540,7 +565,8 @@ def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_
     return u, [q3, stats, c3, c3b, e3, alpha, wb, w2, xd]
 
 
-def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, pre=None):
+def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, pre=None,
+                  defer: bool = False):
     """Backward of :func:`_user_enc_fwd` for ``du [B, D]``: the input gradient goes into ``dx
     [B*H, D]`` (the dropout backward in the dgrad epilogue) -> the ten weight gradients."""
     q3, stats, c3, c3b, e3, alpha, wb, w2, xd = saved
@@ -591,9 +617,20 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
         db2 = torch.empty(8, device=dev)
         wg += (ops.Gemm(da8, e3.reshape(BH, Qd), dw2, 8, Qd, BH, 8, Qd, Qd, a_mode=1, b_mode=1, asum=db2),)
         dw2, db2 = dw2[0], db2[:1]
-    ops.small_gemm(dgrad, *wg, dev_off=dev_off)
-    return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1, gb1, dw2.view(1, -1),
-            db2.view(1))
+    if defer and dx.is_cuda:
+        # the input gradient now (the news-gradient segment sum reads it next; bf16 x bf16: the
+        # LDS-DMA ring, unsplit), the weight gradients with the text fc's backward launch
+        ops.small_gemm(dgrad, dev_off=dev_off)
+        _PENDING_GEMMS.clear()  # (left over only by a backward that raised: its tensors are gone)
+        _PENDING_GEMMS.extend(wg)
+        torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_gemms)
+    else:
+        ops.small_gemm(dgrad, *wg, dev_off=dev_off)
+    # every gradient returned as a fresh view: autograd keeps a returned gradient as .grad only
+    # when nothing else references it and clones it otherwise -- a held-back GEMM still holds
+    # gw1 / gb1 (its output), and a clone now would copy them before that GEMM wrote them
+    return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1.view_as(gw1),
+            gb1.view_as(gb1), dw2.view(1, -1), db2.view(1))
 
 
 class UserStepFn(torch.autograd.Function):
@@ -658,7 +695,7 @@ class UserStepFn(torch.autograd.Function):
                     t.mul_(gloss)
             else:
                 du = du * gloss
-        grads = _user_enc_bwd(saved, du, rows[BC:], B, H, heads, hd, drop, dev_off, keep, pre)
+        grads = _user_enc_bwd(saved, du, rows[BC:], B, H, heads, hd, drop, dev_off, keep, pre, defer=True)
         clip, noise, lseed, loff = ldp
         # the noise offset's step part is the device counter (dev_off): graph replays draw fresh noise
         dv = ops.segment_sum_rows(rows, inv, v.shape[0], clip, noise, lseed, loff, seg=(perm, ptr), zero_empty=padded,
@@ -761,7 +798,9 @@ class HeadFCFn(torch.autograd.Function):
 
         dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
         db = torch.empty(N, device=x.device, dtype=torch.float32)
-        # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one launch
+        # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
+        # launch -- with the user encoder's weight gradients when its backward held them back
         ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1),
-                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db))
+                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db),
+                       *take_pending_gemms(4))
         return dx, dw, db, None, None
