@@ -190,6 +190,7 @@ extern "C" int fr_adam_dev(float* p, float* g, float* m, float* v, void* plow, l
 namespace {
 constexpr int MCAST_SEG = 96;
 constexpr int MCAST_CHUNK = 8192;  // 256 threads x 4 iterations x 8 elements
+constexpr int MCAST_FILL = 8;
 
 struct MultiCast {
   const float* src[MCAST_SEG];
@@ -201,6 +202,11 @@ struct MultiCast {
   int nseg;
   long long* bump;   // optional: a device step counter advanced by one (block 0, lane 0)
   long long* bump2;  // optional: a second one (the in-graph Adam's step count)
+  // up to MCAST_FILL copy segments (fp32 destination, 4-byte words of any type) may be longer
+  // than their source: words past nsrc get the fill bits (a step graph's padded static inputs)
+  signed char fslot[MCAST_SEG];  // -1: none, else index into nsrc / fill
+  long nsrc[MCAST_FILL];
+  int fill[MCAST_FILL];
 };
 
 __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
@@ -218,14 +224,16 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
   const long base = (long)(blockIdx.x - mc.blk0[sg]) * MCAST_CHUNK;
   const float4* s4 = (const float4*)mc.src[sg];
   const long n = mc.n[sg];
+  const int fs = mc.fslot[sg];
+  const long ns = fs >= 0 ? mc.nsrc[fs] : n;  // words read from the source (the rest: fill)
 #pragma unroll
   for (int it = 0; it < MCAST_CHUNK / (256 * 8); ++it) {
     const long e = base + ((long)it * 256 + threadIdx.x) * 8;
-    if (e < n && (!mc.vec[sg] || e + 8 > n)) {  // unaligned segment or its ragged tail
+    if (e < n && (!mc.vec[sg] || e + 8 > ns)) {  // unaligned segment, its ragged tail or fill
       const float* src = mc.src[sg];
       for (int j = 0; j < 8 && e + j < n; ++j) {
         if (mc.bf[sg]) ((bf16*)mc.dst[sg])[e + j] = f2bf(src[e + j]);
-        else ((float*)mc.dst[sg])[e + j] = src[e + j];
+        else ((int*)mc.dst[sg])[e + j] = e + j < ns ? ((const int*)src)[e + j] : mc.fill[fs];  // bits
       }
     } else if (e < n) {
       const float4 a = s4[e >> 2], b = s4[(e >> 2) + 1];
@@ -245,13 +253,26 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
 // 0 ok; 1 = too many segments / bad size or alignment (the caller rebuilds the pack instead).
 // bump (optional): an int64 device counter the launch advances by one -- the training step's
 // dropout / noise offset rides in the step's cast launch instead of a launch of its own
+// nsrc (optional): per segment, the source words (< n[i]: fp32 / copy segments only; the
+// rest of the destination gets fill[i]) -- at most MCAST_FILL such segments per launch
 extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                             long long* bump, hipStream_t s, long long* bump2) {
+                             long long* bump, hipStream_t s, long long* bump2, const long* nsrc, const int* fill) {
   if (nseg < 1 || nseg > MCAST_SEG) return 1;
   MultiCast mc{};
   mc.nseg = nseg;
   mc.bump = bump;
   mc.bump2 = bump2;
+  int nf = 0;
+  for (int i = 0; i < nseg; ++i) {
+    mc.fslot[i] = -1;
+    if (nsrc != nullptr && nsrc[i] != n[i]) {
+      if (nsrc[i] < 0 || nsrc[i] > n[i] || to_bf16[i] || nf == MCAST_FILL || fill == nullptr) return 1;
+      mc.fslot[i] = (signed char)nf;
+      mc.nsrc[nf] = nsrc[i];
+      mc.fill[nf] = fill[i];
+      ++nf;
+    }
+  }
   long blk = 0;
   for (int i = 0; i < nseg; ++i) {
     if (n[i] <= 0) return 1;

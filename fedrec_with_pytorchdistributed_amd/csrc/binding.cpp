@@ -118,7 +118,7 @@ int fr_secagg_unmask_exact(const int* x, float* out, long n, const int* H, int W
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, int tile, hipStream_t s);
 int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                  long long* bump, hipStream_t s, long long* bump2);
+                  long long* bump, hipStream_t s, long long* bump2, const long* nsrc, const int* fill);
 int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, const int* C, const int* ld, int nseg,
                     hipStream_t s);
 int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
@@ -1212,9 +1212,67 @@ bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor
   for (size_t i0 = 0; i0 < n; i0 += 96) {  // 96 segments per launch (kernel-argument size)
     const int k = (int)std::min<size_t>(96, n - i0);
     TORCH_CHECK(fr_multi_cast(sp.data() + i0, dp.data() + i0, ne.data() + i0, bf.data() + i0, k, i0 == 0 ? bp : nullptr,
-                              cur_stream(), i0 == 0 ? bp2 : nullptr) == 0,
+                              cur_stream(), i0 == 0 ? bp2 : nullptr, nullptr, nullptr) == 0,
                 "fedrec::multi_cast: launch rejected");
   }
+  return true;
+}
+
+// A step graph's per-replay launch: the batch into the graph's static inputs (copies of 4-byte
+// words; a destination longer than its source gets the fill word past it) and the step's weight
+// casts + counter bumps (multi_cast), ONE launch instead of a copy launch and an in-graph cast
+// launch.  false = nothing launched (an empty cast segment).
+bool copy_cast(const std::vector<at::Tensor>& csrc, const std::vector<at::Tensor>& cdst, at::IntArrayRef fill,
+               const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst,
+               const c10::optional<at::Tensor>& bump, const c10::optional<at::Tensor>& bump2) {
+  const size_t nc = csrc.size(), n = src.size();
+  TORCH_CHECK(cdst.size() == nc && fill.size() == nc && dst.size() == n && nc + n >= 1 && nc + n <= 96,
+              "fedrec::copy_cast: sizes");
+  const at::Tensor& ref = nc ? cdst[0] : dst[0];
+  const c10::DeviceGuard g(ref.device());
+  auto bptr = [&](const c10::optional<at::Tensor>& b) -> long long* {
+    if (!b.has_value() || !b->defined()) return nullptr;
+    TORCH_CHECK(b->device() == ref.device() && b->scalar_type() == at::kLong && b->numel() == 1 && b->is_contiguous(),
+                "fedrec::copy_cast: bumps must be int64 [1] tensors on the destinations' device");
+    return (long long*)b->data_ptr<int64_t>();
+  };
+  long long* bp = bptr(bump);
+  long long* bp2 = bptr(bump2);
+  std::vector<const float*> sp;
+  std::vector<void*> dp;
+  std::vector<long> ne, ns;
+  std::vector<int> bf, fv;
+  for (size_t i = 0; i < nc; ++i) {
+    TORCH_CHECK(csrc[i].is_cuda() && cdst[i].is_cuda() && csrc[i].is_contiguous() && cdst[i].is_contiguous() &&
+                    csrc[i].element_size() == 4 && cdst[i].scalar_type() == csrc[i].scalar_type() &&
+                    csrc[i].numel() <= cdst[i].numel(),
+                "fedrec::copy_cast: copies are contiguous device tensors of one 4-byte dtype, source <= destination");
+    if (cdst[i].numel() == 0) continue;
+    sp.push_back((const float*)csrc[i].data_ptr());
+    dp.push_back(cdst[i].data_ptr());
+    ne.push_back((long)cdst[i].numel());
+    ns.push_back((long)csrc[i].numel());
+    bf.push_back(0);
+    fv.push_back((int)fill[i]);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && dst[i].is_contiguous() &&
+                    src[i].scalar_type() == at::kFloat &&
+                    (dst[i].scalar_type() == at::kBFloat16 || dst[i].scalar_type() == at::kFloat) &&
+                    src[i].numel() == dst[i].numel(),
+                "fedrec::copy_cast: contiguous fp32 cast sources, bf16/fp32 destinations of the same size");
+    if (src[i].numel() == 0) return false;
+    sp.push_back(src[i].data_ptr<float>());
+    dp.push_back(dst[i].data_ptr());
+    ne.push_back((long)src[i].numel());
+    ns.push_back((long)src[i].numel());
+    bf.push_back(dst[i].scalar_type() == at::kBFloat16 ? 1 : 0);
+    fv.push_back(0);
+  }
+  if (sp.empty()) return false;
+  TORCH_CHECK(fr_multi_cast(sp.data(), dp.data(), ne.data(), bf.data(), (int)sp.size(), bp, cur_stream(), bp2,
+                            ns.data(), fv.data()) == 0,
+              "fedrec::copy_cast: launch rejected (more than 8 padded copies?)");
   return true;
 }
 
@@ -1667,6 +1725,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("multi_copy(Tensor[] src, Tensor(a!)[] dst, int[] fill) -> ()");
   m.def("multi_cast(Tensor[] src, Tensor(a!)[] dst, Tensor(b!)? bump=None, Tensor(c!)? bump2=None) -> bool");
   m.def("multi_cast_t(Tensor[] src, Tensor(a!)[] dst) -> bool");
+  m.def("copy_cast(Tensor[] csrc, Tensor(a!)[] cdst, int[] fill, Tensor[] src, Tensor(b!)[] dst, Tensor(c!)? bump=None, "
+        "Tensor(d!)? bump2=None) -> bool");
   m.def("colsum_f32(Tensor[] X, Tensor(a!)[] out, int[] ints) -> ()");
   m.def("secagg_hist(Tensor x, Tensor seeds, Tensor signs, int round) -> Tensor");
   m.def("secagg_mask_exact(Tensor x, Tensor seeds, Tensor signs, Tensor hist, int W, int round) -> Tensor");
@@ -1726,6 +1786,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("multi_copy", &multi_copy);
   m.impl("multi_cast", &multi_cast);
   m.impl("multi_cast_t", &multi_cast_t);
+  m.impl("copy_cast", &copy_cast);
   m.impl("secagg_unmask_exact_", &secagg_unmask_exact_);
   m.impl("title_attention_drop", &title_attention_drop);
   m.impl("title_attention_bwd_drop", &title_attention_bwd_drop);

@@ -474,6 +474,30 @@ def _user_cast_lists(wts, wb, bqkv):
             [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D], bqkv[2 * D:]])
 
 
+def _step_cast_weights(text_encoder, user_encoder):
+    aa = text_encoder.additive_attention
+    mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
+    wts = (mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight, mha.W_V.bias,
+           pool.att_fc1.weight)
+    return aa.att_fc1.weight, text_encoder.fc.weight, wts
+
+
+def step_cast_buffers(text_encoder, user_encoder):
+    """The compute copies :func:`step_weight_casts` fills: ``(w1_bf16, (wb, bqkv), fc_bf16)``."""
+    w, wf, wts = _step_cast_weights(text_encoder, user_encoder)
+    w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+    fcb = torch.empty(wf.shape, device=w.device, dtype=torch.bfloat16)
+    return w1b, _user_weight_bufs(wts, w.device), fcb
+
+
+def step_cast_lists(text_encoder, user_encoder, bufs):
+    """``(sources, destinations)`` of the step's weight casts into ``bufs`` (step_cast_buffers)."""
+    w, wf, wts = _step_cast_weights(text_encoder, user_encoder)
+    w1b, (wb, bqkv), fcb = bufs
+    src, dst = _user_cast_lists(wts, wb, bqkv)
+    return [w.detach(), wf.detach()] + [t.detach() for t in src], [w1b, fcb] + dst
+
+
 def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     """Every compute copy a fused training step needs, in ONE cast launch: the text head's att_fc1
     weight in bf16 (the head_score operand), its fc weight in bf16 (the fc GEMMs' operand) and the
@@ -482,23 +506,16 @@ def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     kernel each (4.7 + 6.2 us per step).  ``bump`` (int64 [1] device counter, optional): advanced
     by one in the same launch -- the step's dropout / noise offset (a torch ``add_`` of its own
     cost 4.8 us at the end of every step).  ``bump2``: a second counter advanced the same way (the
-    in-graph Adam's step count: adam_dev then only reads it)."""
-    aa = text_encoder.additive_attention
-    mha, pool = user_encoder.multihead_attention, user_encoder.additive_attention
-    wts = (mha.W_Q.weight, mha.W_Q.bias, mha.W_K.weight, mha.W_K.bias, mha.W_V.weight, mha.W_V.bias,
-           pool.att_fc1.weight)
-    w, wf = aa.att_fc1.weight, text_encoder.fc.weight
-    w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
-    fcb = torch.empty(wf.shape, device=w.device, dtype=torch.bfloat16)
-    wb, bqkv = _user_weight_bufs(wts, w.device)
-    src, dst = _user_cast_lists(wts, wb, bqkv)
-    launched = ops.native.require_for(w).multi_cast([w.detach(), wf.detach()] + [t.detach() for t in src],
-                                                    [w1b, fcb] + dst, bump, bump2)
+    in-graph Adam's step count: adam_dev then only reads it).  A captured step graph takes these
+    copies from persistent buffers its replay's input launch fills instead (engine _StepGraph)."""
+    bufs = step_cast_buffers(text_encoder, user_encoder)
+    src, dst = step_cast_lists(text_encoder, user_encoder, bufs)
+    launched = ops.native.require_for(dst[0]).multi_cast(src, dst, bump, bump2)
     if not launched:
         for b in (bump, bump2):
             if b is not None:
                 b.add_(1)
-    return w1b, (wb, bqkv), fcb
+    return bufs
 
 
 # Weight-gradient GEMMs of the user backward held back to ride in a later launch of the same

@@ -85,6 +85,7 @@ class _StepGraph:
     def __init__(self, eng: "LocalEngine", pre: Prepared, ucap: int, with_adam: bool = False):
         uniq, inv, perm, ptr = pre.dedup
         self.adam = with_adam
+        self.eng = eng
         dev = eng.device
         self.cand = torch.zeros_like(pre.cand)
         self.his = torch.zeros_like(pre.his)
@@ -96,7 +97,10 @@ class _StepGraph:
         # (their rows carry no gradient; outputs exact zeros) -- ~5 % of the head's work at B = 64
         self.nreal = torch.zeros(1, dtype=torch.int32, device=dev)
         self._none = torch.empty(0, dtype=torch.int32, device=dev)
-        self.load(pre, int(uniq.numel()))
+        # the step's weight casts + counter bumps ride in each replay's input launch (load):
+        # the graph reads the compute copies from persistent buffers, no cast launch of its own
+        self.precast = eng.fused_user and eng.fused_head
+        self.load(pre, int(uniq.numel()), cast=False)
         static = Prepared(self.cand, self.his, (self.uniq, self.inv, self.perm, self.ptr), None, True,
                           self.nreal)
         main = torch.cuda.current_stream(dev)
@@ -136,6 +140,7 @@ class _StepGraph:
             # the in-graph Adam gathers the step's gradients from where autograd left them and
             # writes them into the flat buffer itself: no separate copy launch (6 us per step)
             eng._adam_gathers = with_adam
+            eng._precast = eng.step_cast_bufs() if self.precast else None
             with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
                 self.loss = eng.forward_backward(self.cand, self.his, static)
                 if with_adam:  # no all-reduce between backward and optimizer: the step in one graph
@@ -145,15 +150,25 @@ class _StepGraph:
             eng._adam_bump = None
             eng._adam_gathers = False
             eng._grad_srcs = None
+            eng._precast = None
 
-    def load(self, pre: Prepared, U: int) -> None:
-        """The batch into the static inputs: one multi-copy launch; the unique list is padded
-        with news 0 and the segment pointers with R (padded segments are empty)."""
+    def load(self, pre: Prepared, U: int, cast: bool = True) -> None:
+        """The batch into the static inputs: one launch; the unique list is padded with news 0
+        and the segment pointers with R (padded segments are empty).  ``cast`` (a replay of a
+        graph captured with persistent compute copies): the same launch casts the step's weights
+        into them and advances the step counters (csrc/adam.hip multi_cast, copy segments) --
+        the separate in-graph cast launch was 5 us per step."""
         uniq, inv, perm, ptr = pre.dedup
-        native.require_for(self.cand).multi_copy(
-            [pre.cand.contiguous(), pre.his.contiguous(), uniq, inv, perm, ptr, self._none],
-            [self.cand, self.his, self.uniq, self.inv, self.perm, self.ptr, self.nreal],
-            [0, 0, 0, 0, 0, int(inv.numel()), U])
+        src = [pre.cand.contiguous(), pre.his.contiguous(), uniq, inv, perm, ptr, self._none]
+        dst = [self.cand, self.his, self.uniq, self.inv, self.perm, self.ptr, self.nreal]
+        fill = [0, 0, 0, 0, 0, int(inv.numel()), U]
+        lib = native.require_for(self.cand)
+        if cast and self.precast:
+            eng = self.eng
+            csrc, cdst = eng.step_cast_lists()
+            lib.copy_cast(src, dst, fill, csrc, cdst, eng._rng_step, eng._adam_step_dev if self.adam else None)
+        else:
+            lib.multi_copy(src, dst, fill)
 
 
 class LocalEngine:
@@ -203,6 +218,9 @@ class LocalEngine:
         self._rng_step = torch.zeros(1, dtype=torch.int64, device=device)
         self._adam_bump = None  # set while capturing a step graph with Adam in it (see _StepGraph)
         self._adam_gathers = False  # ... and then Adam gathers the gradients (no end_backward copy)
+        self._precast = None  # set while capturing: the step's compute copies, filled before each replay
+        self._cast_bufs = None
+        self._cast_lists = None
         self._grad_srcs = None
         self._inflight = collections.deque()  # (held batch, end event or None), see _retire
         self._held_n = 0
@@ -305,6 +323,23 @@ class LocalEngine:
         if self.device.type == "cuda":
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t
+
+    def step_cast_bufs(self):
+        """Persistent compute copies of the step's weights (shared by every step graph)."""
+        if self._cast_bufs is None:
+            self._cast_bufs = OF.step_cast_buffers(self.model.text_encoder, self.model.user_encoder)
+        return self._cast_bufs
+
+    def step_cast_lists(self):
+        """``(sources, destinations)`` of the weight casts into :meth:`step_cast_bufs`."""
+        te, ue = self.model.text_encoder, self.model.user_encoder
+        # (cached: rebuilding the slices costs ~50 us of host time per step; keyed on where the
+        # weights live, so a re-bound parameter is never cast from its old storage)
+        key = (te.fc.weight.data_ptr(), te.additive_attention.att_fc1.weight.data_ptr(),
+               ue.multihead_attention.W_Q.weight.data_ptr())
+        if self._cast_lists is None or self._cast_lists[0] != key:
+            self._cast_lists = (key, OF.step_cast_lists(te, ue, self.step_cast_bufs()))
+        return self._cast_lists[1]
 
     def sync_params(self) -> None:
         """Make the current stream wait for a pending overlapped optimizer step."""
@@ -452,8 +487,11 @@ class LocalEngine:
             casts = None
             if self.fused_head:  # every compute copy of the step's weights in one cast launch,
                 self.sync_params()  # which also advances the dropout / noise step counter this step reads
-                casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder,
-                                             bump=self._rng_step, bump2=self._adam_bump)
+                if self._precast is not None:  # a step graph: its replay's input launch casts them
+                    casts = self._precast
+                else:
+                    casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder,
+                                                 bump=self._rng_step, bump2=self._adam_bump)
             with obs.range("news_encode"):
                 v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
                                       w1b=casts[0] if casts is not None else None,
@@ -557,14 +595,17 @@ class LocalEngine:
                 self._adam_mirror = -1
             g = _StepGraph(self, pre, ucap, with_adam)
             self._graphs[key] = g
-        g.load(pre, U)
+        if not g.precast:
+            g.load(pre, U)
         if g.hid_graph is not None:
             g.hid_graph.replay()  # parameter-free: runs while the previous all-reduce + Adam finish
         self.sync_params()
+        if g.adam and self._adam_mirror != self.flat.step:  # an eager step / a resume moved the host count
+            self._adam_step_dev.fill_(self.flat.step)
+            self._adam_mirror = self.flat.step
+        if g.precast:  # after the parameters' last update: this launch casts them (and bumps the counters)
+            g.load(pre, U)
         if g.adam:
-            if self._adam_mirror != self.flat.step:  # an eager step / a resume moved the host count
-                self._adam_step_dev.fill_(self.flat.step)
-                self._adam_mirror = self.flat.step
             g.graph.replay()
             self.flat.step += 1
             self._adam_mirror += 1

@@ -525,6 +525,38 @@ def test_multi_cast(dev):
              torch.empty(1000, device=dev)]
     assert native.lib().multi_cast(odd_s, odd_d)
     assert all(torch.equal(b, a.to(b.dtype)) for a, b in zip(odd_s, odd_d))
+
+
+@pytest.mark.gpu
+def test_copy_cast(dev):
+    """A step graph's input launch: int32 batch copies whose destinations are padded with a fill
+    word (bit patterns kept: negative ids look like NaN floats), empty sources (fill only),
+    weight casts to bf16 / fp32 and both counter bumps -- one launch, equal to the separate ops."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    cand = torch.randint(-5, 65000, (64, 5), generator=g, dtype=torch.int32).to(dev)
+    ptr = torch.arange(0, 1601 * 3, 3, dtype=torch.int32).to(dev)
+    odd = torch.randint(-(2 ** 31), 2 ** 31 - 1, (37,), generator=g, dtype=torch.int64).to(torch.int32).to(dev)
+    none = torch.empty(0, dtype=torch.int32, device=dev)
+    c_dst = torch.full((64, 5), 7, dtype=torch.int32, device=dev)
+    p_dst = torch.full((1793,), 7, dtype=torch.int32, device=dev)
+    o_dst = torch.full((41,), 7, dtype=torch.int32, device=dev)
+    n_dst = torch.full((1,), 7, dtype=torch.int32, device=dev)
+    w = torch.randn(384, 768, device=dev)
+    b = torch.randn(1200, device=dev)
+    wb = torch.empty(384, 768, device=dev, dtype=torch.bfloat16)
+    bf = torch.empty(1200, device=dev)
+    c1 = torch.full((1,), 10, device=dev, dtype=torch.int64)
+    c2 = torch.full((1,), 20, device=dev, dtype=torch.int64)
+    assert native.lib().copy_cast([cand, ptr, odd[1:], none], [c_dst, p_dst, o_dst, n_dst], [0, 4800, -1, 1565],
+                                  [w, b], [wb, bf], c1, c2)
+    assert torch.equal(c_dst, cand)
+    assert torch.equal(p_dst[:1601], ptr) and bool((p_dst[1601:] == 4800).all())
+    assert torch.equal(o_dst[:36], odd[1:]) and bool((o_dst[36:] == -1).all())
+    assert int(n_dst.item()) == 1565
+    assert torch.equal(wb, w.to(torch.bfloat16)) and torch.equal(bf, b)
+    assert int(c1.item()) == 11 and int(c2.item()) == 21
+    # no casts: copies alone, no bumps
+    assert native.lib().copy_cast([cand], [c_dst], [0], [], [], None, None)
     # transposed: [R, C] fp32 -> bf16 [C, R] views, side by side in a fused [C, 3R] destination
     ws = [torch.randn(768, 768, device=dev) for _ in range(3)] + [torch.randn(3072, 768, device=dev)]
     fused_t = torch.empty(768, 3 * 768, device=dev, dtype=torch.bfloat16)
