@@ -69,6 +69,8 @@ def main() -> int:
     ap.add_argument("--dp-epsilon", type=float, default=10.0)
     ap.add_argument("--valid-limit", type=int, default=2048)
     ap.add_argument("--no-valid", action="store_true")
+    ap.add_argument("--cache-warm", type=int, default=512,
+                    help="titles run through the backbone (result dropped) before the timed cache build")
     ap.add_argument("--profile-phases", action="store_true")
     ap.add_argument("--news-cache", default="auto", choices=["auto", "hidden", "none"],
                     help="HBM hidden-state cache of the frozen backbone (none = re-encode every step)")
@@ -150,6 +152,8 @@ def main() -> int:
 
     # the HBM hidden-state cache, built once before warm-up and timed on its own (every
     # client builds its own in parallel; the slowest one counts)
+    if eng.hcache is not None and args.cache_warm > 0:  # untimed, like the warm-up steps
+        eng.hcache.warm(args.cache_warm)
     cache_s = eng.build_cache()
     if cache_s is not None:
         cache_s = max_over_ranks(cache_s)
@@ -342,6 +346,7 @@ def main() -> int:
             "train_loss": round(loss, 5),
             "news_cache": "hidden" if eng.hcache is not None else "none",
             "cache_build_ms": None if cache_s is None else round(1000.0 * cache_s, 2),
+            "cache_warm_titles": args.cache_warm if cache_s is not None else None,
             "steps_per_epoch": steps_per_epoch,
             "steady_ms_per_step": round(1000.0 * elapsed / args.steps, 4),
             "host_ms_per_step": {"launch": round(1000.0 * host_step / args.steps, 4),

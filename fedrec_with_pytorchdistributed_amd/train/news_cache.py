@@ -84,6 +84,17 @@ class HiddenCache:
         self.builds += 1
         return self.build_s
 
+    @torch.no_grad()
+    def warm(self, n: int = 512) -> None:
+        """Run the first ``n`` titles through the backbone and drop the result: the build's
+        kernels loaded and the device out of idle before a timed :meth:`build` (the warm-up
+        steps' counterpart for the one-off cache build)."""
+        n = min(n, self.tokens.shape[0])
+        if n > 0:
+            self.te.hidden(self.tokens[:n])
+            if self.tokens.device.type == "cuda":
+                torch.cuda.synchronize(self.tokens.device)
+
     def ensure(self) -> None:
         if not self.fresh():
             self.build()
