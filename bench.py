@@ -8,7 +8,9 @@ Before anything is timed, every client encodes all titles of its shard once with
 frozen 6-layer DistilBERT (hand-written MFMA kernels) into an HBM-resident hidden-state
 cache ``[N, 50, 768]`` bf16 (``--news-cache none`` = the round-1 path that
 re-encodes the batch's unique titles every step).  The build is timed on its own
-(``cache_build_ms``).
+(``cache_build_ms``), after an untimed pass of ``--cache-warm`` titles (512) through the
+same backbone -- the warm-up steps' counterpart: the kernels' first launches in a process
+(~25 ms) are not part of the build's work.
 
 One timed *step* = one synchronous federated gradient-averaging step on every client:
 sample a batch of ``--batch`` impressions from the client's private synthetic MIND shard
