@@ -131,13 +131,23 @@ def main() -> int:
     elif args.config == 3:
         ar = None
     else:
-        ar = fdist.make_grad_allreduce(ctx)
+        # N > 1: "auto" = the device-epoch IPC all-reduce inside the step graph when it checks
+        # out against RCCL on this node (and is not slower in isolation), else RCCL, eager
+        ar = fdist.make_grad_allreduce(ctx, choice=os.environ.get("FEDREC_ALLREDUCE", "auto"),
+                                       log=lambda m: print(m, file=sys.stderr, flush=True),
+                                       nelem=model.flat.grad.numel())
     eng = LocalEngine(cfg, model, shard, dev, rank=ctx.rank, grad_allreduce=ar)
     if args.config == 5:
         eng.set_reducer(fdist.make_bucket_reducer(ctx, model.flat, secure=True))
     if args.config == 4:
         cfg.dp.enabled, cfg.dp.epsilon = True, args.dp_epsilon
         eng.sigma = calibrate_client_sigma(cfg.dp.epsilon, cfg.dp.delta, cfg.batch_size, len(shard.train), cfg.dp.epochs)
+    # N > 1: the clients build the hidden-state cache cooperatively -- each encodes 1/W of the
+    # public catalog and the shares are all-gathered over the data plane (parallel/catalog.py);
+    # the plan's id exchange is charged with the build
+    from fedrec_with_pytorchdistributed_amd.parallel import catalog
+
+    plan = catalog.attach(eng, ctx)
     pa_state = {"n": 0}
     pa_ipc = fdist.data_ipc(ctx) if (args.config == 3 and dev.type == "cuda") else None
 
@@ -157,7 +167,12 @@ def main() -> int:
     if eng.hcache is not None and args.cache_warm > 0:  # untimed, like the warm-up steps
         eng.hcache.warm(args.cache_warm)
     cache_s = eng.build_cache()
+    cache_info = None
     if cache_s is not None:
+        cache_info = {k: (round(1000.0 * v, 2) if k.endswith("_s") else v) for k, v in eng.hcache.build_info.items()}
+        cache_info = {(k[:-2] + "_ms") if k.endswith("_s") else k: v for k, v in cache_info.items()}
+        if plan is not None:
+            cache_s += plan.plan_s  # one-off per run, charged like the build
         cache_s = max_over_ranks(cache_s)
     steps_per_epoch = -(-len(shard.train) // args.batch)
     steps_per_epoch = int(max_over_ranks(steps_per_epoch, dist.ReduceOp.MIN if ctx.initialized else None))
@@ -333,6 +348,9 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / REF_IMPRESSIONS_PER_S, 2),
+            "vs_baseline_note": ("value / 1.87 imp/s: the reference code measured on an 8-core CPU in fp32 "
+                                 "(BASELINE.md table 2; the reference publishes no throughput) -- a hardware + "
+                                 "design ratio, not a like-for-like speedup"),
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": f"synthetic ({args.preset} MIND-format shard per client, random-init weights)",
             "config": {
@@ -349,6 +367,7 @@ def main() -> int:
             "news_cache": "hidden" if eng.hcache is not None else "none",
             "cache_build_ms": None if cache_s is None else round(1000.0 * cache_s, 2),
             "cache_warm_titles": args.cache_warm if cache_s is not None else None,
+            "cache_build": cache_info,  # rank 0's breakdown (cooperative at N > 1: 1/W encoded + gather)
             "steps_per_epoch": steps_per_epoch,
             "steady_ms_per_step": round(1000.0 * elapsed / args.steps, 4),
             "host_ms_per_step": {"launch": round(1000.0 * host_step / args.steps, 4),
@@ -356,6 +375,10 @@ def main() -> int:
             "cache_amortized_ms_per_step": round(1000.0 * amort / args.steps, 4),
             "fastest_rank_ms_per_step": round(1000.0 * fastest / args.steps, 3),
             "unique_titles_per_step": None if u_mean is None else round(u_mean, 1),
+            "grad_allreduce": None if ar is None else {"kind": ar.kind, "in_step_graph": bool(ar.capturable),
+                                                       "probe": getattr(ar, "probe", None),
+                                                       "replays_with_optimizer": eng.counts["replays_with_optimizer"],
+                                                       "eager_optimizer_steps": eng.counts["eager_optimizer_steps"]},
             "grad_allreduce_ms": None if comm_ms is None else round(comm_ms, 4),
             "grad_allreduce_busbw_GBps": None if busbw is None else round(busbw, 2),
             "valid_auc": None if auc is None else round(auc, 4),

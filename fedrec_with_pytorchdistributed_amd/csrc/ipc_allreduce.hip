@@ -20,6 +20,12 @@
 // Slot reuse: slot e & 1 is rewritten at epoch e + 2, after this rank passed the barrier of
 // epoch e + 1, which every peer entered only after finishing its reads of epoch e.
 // Types: fp32 SUM, int32 wrap-around SUM (secure aggregation's masked fixed point).
+// Device epochs (a context created for capture, epoch argument 0): the epoch is NOT a launch
+// argument but the context's device counter + 1, so a launch captured once in a HIP graph runs
+// a fresh epoch on every replay.  Every block reads the counter first; a block that passed the
+// phase-0 barrier knows every block of every rank has started (and read it), so it stores the
+// new value back (the same value from every block; a vector store) -- the next launch on the
+// stream reads it after this one completed.
 //
 // Liveness: the waits are bounded by a wall-clock deadline (the caller's collective timeout);
 // then a status word records the timeout, the output is poisoned (NaN / INT_MIN) and the
@@ -126,11 +132,13 @@ struct Xs {
 template <typename T>
 __global__ __launch_bounds__(AR_THREADS) void ipc_allreduce_kernel(Xs<T> xs, long n, Peers P, int me_arg, int W,
                                                                   long long epoch, long cap, int mode, int nb,
-                                                                  int multi, unsigned long long deadline) {
+                                                                  int multi, unsigned long long deadline,
+                                                                  long long* __restrict__ dev_epoch) {
   const int me = multi ? (int)blockIdx.x / nb : me_arg;
   const int blk = multi ? (int)blockIdx.x % nb : (int)blockIdx.x;
   T* __restrict__ x = xs.x[multi ? me : 0];
   int* status = xs.status[multi ? me : 0];
+  if (dev_epoch != nullptr) epoch = __hip_atomic_load(dev_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   const long slot_off = FLAG_BYTES + (long)(epoch & 1) * cap;
   T* mine = (T*)(P.base[me] + slot_off);
   const long n4 = n / 4;
@@ -146,6 +154,8 @@ __global__ __launch_bounds__(AR_THREADS) void ipc_allreduce_kernel(Xs<T> xs, lon
     poison(x, n4, t0, stride);
     return;
   }
+  if (dev_epoch != nullptr && threadIdx.x == 0)
+    __hip_atomic_store(dev_epoch, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (mode == 0) {
     for (long i = t0; i < n4; i += stride) {
       T acc[4] = {0, 0, 0, 0};
@@ -166,7 +176,19 @@ __global__ __launch_bounds__(AR_THREADS) void ipc_allreduce_kernel(Xs<T> xs, lon
     poison(x, n4, t0, stride);
     return;
   }
-  for (long i = t0; i < n4; i += stride) {
+  // gather: four independent remote loads in flight per thread (xGMI latency)
+  long i = t0;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long j = i + u * stride;
+      v[u] = *(const float4*)((const T*)(P.base[(int)(j / per)] + slot_off) + 4 * j);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *(float4*)(x + 4 * (i + u * stride)) = v[u];
+  }
+  for (; i < n4; i += stride) {
     const int owner = (int)(i / per);
     *(float4*)(x + 4 * i) = *(const float4*)((const T*)(P.base[owner] + slot_off) + 4 * i);
   }
@@ -179,6 +201,7 @@ struct Ctx {
   Peers P{};
   bool opened[MAXW] = {};
   int* status = nullptr;
+  long long* dev_epoch = nullptr;  // device epochs (epoch argument 0)
 };
 
 Ctx* g_ctx[64] = {};
@@ -203,8 +226,12 @@ extern "C" int fr_ipc_create(long cap, void* handle_out) {
     return -2;
   }
   if (hipMemset(c->region, 0, FLAG_BYTES) != hipSuccess || hipMalloc((void**)&c->status, sizeof(int)) != hipSuccess ||
-      hipMemset(c->status, 0, sizeof(int)) != hipSuccess) {
+      hipMemset(c->status, 0, sizeof(int)) != hipSuccess ||
+      hipMalloc((void**)&c->dev_epoch, sizeof(long long)) != hipSuccess ||
+      hipMemset(c->dev_epoch, 0, sizeof(long long)) != hipSuccess) {
     (void)hipFree(c->region);
+    if (c->status) (void)hipFree(c->status);
+    if (c->dev_epoch) (void)hipFree(c->dev_epoch);
     delete c;
     return -3;
   }
@@ -212,6 +239,7 @@ extern "C" int fr_ipc_create(long cap, void* handle_out) {
   if (hipIpcGetMemHandle(&h, c->region) != hipSuccess) {
     (void)hipFree(c->region);
     (void)hipFree(c->status);
+    (void)hipFree(c->dev_epoch);
     delete c;
     return -4;
   }
@@ -256,26 +284,28 @@ extern "C" int* fr_ipc_status(int id) { return (id >= 0 && id < 64 && g_ctx[id])
 // x: device pointer of n elements (is_int: int32 wrap-around sum, else fp32); n % 4 == 0 and
 // n * 4 <= cap (host-checked by the caller)
 // timeout_s: bound of every barrier wait (wall clock; the status word records a timeout)
+// epoch 0: the context's device epoch (capturable); a context must use one kind only
 extern "C" int fr_ipc_allreduce(int id, void* x, long n, int is_int, long long epoch, int mode, int blocks,
                                 double timeout_s, hipStream_t s) {
   if (id < 0 || id >= 64 || g_ctx[id] == nullptr) return -1;
   Ctx* c = g_ctx[id];
-  if (n % 4 != 0 || n * 4 > c->cap || c->W < 1) return -2;
+  if (n % 4 != 0 || n * 4 > c->cap || c->W < 1 || epoch < 0) return -2;
   if (n == 0) return 0;
   const int nb = blocks > 0 ? (blocks < MAXB ? blocks : MAXB) : AR_BLOCKS;
   const unsigned long long dl = (unsigned long long)((timeout_s > 0 ? timeout_s : 60.0) * 1e8);
+  long long* de = epoch == 0 ? c->dev_epoch : nullptr;
   if (is_int) {
     Xs<int> xs{};
     xs.x[0] = (int*)x;
     xs.status[0] = c->status;
     hipLaunchKernelGGL(ipc_allreduce_kernel<int>, dim3(nb), dim3(AR_THREADS), 0, s, xs, n, c->P, c->me, c->W, epoch,
-                       c->cap, mode, nb, 0, dl);
+                       c->cap, mode, nb, 0, dl, de);
   } else {
     Xs<float> xs{};
     xs.x[0] = (float*)x;
     xs.status[0] = c->status;
     hipLaunchKernelGGL(ipc_allreduce_kernel<float>, dim3(nb), dim3(AR_THREADS), 0, s, xs, n, c->P, c->me, c->W,
-                       epoch, c->cap, mode, nb, 0, dl);
+                       epoch, c->cap, mode, nb, 0, dl, de);
   }
   return 0;
 }
@@ -299,7 +329,7 @@ extern "C" int fr_ipc_allreduce_local(const int* ids, void* const* xs_in, int W,
       xs.status[r] = g_ctx[ids[r]]->status;
     }
     hipLaunchKernelGGL(ipc_allreduce_kernel<int>, dim3(nb * W), dim3(AR_THREADS), 0, s, xs, n, c->P, 0, W, epoch,
-                       c->cap, mode, nb, 1, dl);
+                       c->cap, mode, nb, 1, dl, (long long*)nullptr);
   } else {
     Xs<float> xs{};
     for (int r = 0; r < W; ++r) {
@@ -307,7 +337,7 @@ extern "C" int fr_ipc_allreduce_local(const int* ids, void* const* xs_in, int W,
       xs.status[r] = g_ctx[ids[r]]->status;
     }
     hipLaunchKernelGGL(ipc_allreduce_kernel<float>, dim3(nb * W), dim3(AR_THREADS), 0, s, xs, n, c->P, 0, W, epoch,
-                       c->cap, mode, nb, 1, dl);
+                       c->cap, mode, nb, 1, dl, (long long*)nullptr);
   }
   return 0;
 }
@@ -320,6 +350,7 @@ extern "C" int fr_ipc_destroy(int id) {
     if (c->opened[p]) (void)hipIpcCloseMemHandle(c->P.base[p]);
   (void)hipFree(c->region);
   (void)hipFree(c->status);
+  (void)hipFree(c->dev_epoch);
   delete c;
   g_ctx[id] = nullptr;
   return 0;

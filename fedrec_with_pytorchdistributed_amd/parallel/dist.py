@@ -150,14 +150,16 @@ def shutdown(ctx: DistContext) -> None:
             pass
 
 
-def make_ipc_allreduce(ctx: DistContext, timeout_s: float = 600.0):
+def make_ipc_allreduce(ctx: DistContext, timeout_s: float = 600.0, device_epoch: bool = False):
     """The custom peer-to-peer all-reduce over IPC-mapped buffers among the client GPUs
-    (:mod:`.ipc_allreduce`), or None (one client, no GPU)."""
+    (:mod:`.ipc_allreduce`), or None (one client, no GPU).  ``device_epoch``: a capturable
+    context (epochs counted on the device)."""
     if ctx.num_clients <= 1 or not ctx.initialized or ctx.device.type != "cuda" or ctx.client_index < 0:
         return None
     from .ipc_allreduce import IpcAllReduce
 
-    return IpcAllReduce(ctx.client_ctrl_group, ctx.client_index, ctx.num_clients, ctx.device, timeout_s=timeout_s)
+    return IpcAllReduce(ctx.client_ctrl_group, ctx.client_index, ctx.num_clients, ctx.device, timeout_s=timeout_s,
+                        device_epoch=device_epoch)
 
 
 def data_ipc(ctx: DistContext, timeout_s: float = 600.0):
@@ -173,30 +175,117 @@ def data_ipc(ctx: DistContext, timeout_s: float = 600.0):
     return ipc
 
 
-def make_grad_allreduce(ctx: DistContext, timeout_s: float = 600.0):
-    """Sum the flat gradient over the client data group; returns the 1/W scale Adam applies.
-    ``FEDREC_ALLREDUCE=ipc``: the custom IPC all-reduce instead of RCCL (same sum; every rank
-    gets the bitwise-same result); its ``check`` (run by the engine at every epoch end) raises
-    if a peer timed out."""
-    if ctx.num_clients <= 1 or not ctx.initialized:
-        return None
-    W = ctx.num_clients
-    ipc = data_ipc(ctx, timeout_s) if ctx.device.type == "cuda" else None
-    if ipc is not None:
-        def _ar_ipc(flat_grad: torch.Tensor) -> float:
-            CHECK.record("all_reduce", flat_grad, "grad-ipc")
-            ipc.allreduce_(flat_grad)
-            return 1.0 / W
+def _ipc_grad_fn(ctx: DistContext, ipc, W: int):
+    def _ar_ipc(flat_grad: torch.Tensor) -> float:
+        CHECK.record("all_reduce", flat_grad, "grad-ipc")
+        ipc.allreduce_(flat_grad)
+        return 1.0 / W
 
-        _ar_ipc.check = ipc.check
-        return _ar_ipc
+    _ar_ipc.check = ipc.check
+    _ar_ipc.kind = "ipc"
+    # device epochs: the launch is capturable -- the engine puts it inside the step graph, between
+    # the backward and the device-step Adam (one replay per step at N > 1, as at N = 1)
+    _ar_ipc.capturable = os.environ.get("FEDREC_GRAPH_AR", "1") != "0"
+    _ar_ipc.ipc = ipc
+    return _ar_ipc
 
+
+def _rccl_grad_fn(ctx: DistContext, W: int):
     def _ar(flat_grad: torch.Tensor) -> float:
         CHECK.record("all_reduce", flat_grad, "grad")
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=ctx.data_group)
         return 1.0 / W
 
+    _ar.kind = "rccl" if ctx.device.type == "cuda" else dist.get_backend(ctx.data_group)
+    # RCCL inside a captured graph is opt-in (FEDREC_GRAPH_RCCL=1): the eager call on the optimizer
+    # side stream is the default for the library path
+    _ar.capturable = ctx.device.type == "cuda" and os.environ.get("FEDREC_GRAPH_RCCL", "0") == "1"
     return _ar
+
+
+def probe_ipc_grad(ctx: DistContext, nelem: int, timeout_s: float = 600.0, check_timeout_s: float = 20.0,
+                   reps: int = 10, log=None) -> dict:
+    """Set up the device-epoch IPC all-reduce for the gradient bucket and check it against the
+    data group's sum (RCCL on the node) on an ``nelem`` fp32 bucket, timing both (eager, ``reps``
+    calls).  The verdict is agreed by every client (gloo MIN / MAX).  Returns ``{"ok", "ipc_ms",
+    "group_ms", "ipc": IpcAllReduce or None}``; a failure (an exception, a wrong sum, a peer that
+    never arrives within ``check_timeout_s``) gives ok False and no context."""
+    import time
+
+    info = {"ok": False, "ipc_ms": None, "group_ms": None, "ipc": None}
+    ipc = None
+    ok = 1
+    ms = [0.0, 0.0]
+    try:
+        ipc = make_ipc_allreduce(ctx, timeout_s=check_timeout_s, device_epoch=True)
+        dev = ctx.device
+        a = torch.randn(nelem, device=dev, generator=torch.Generator(dev).manual_seed(1234 + ctx.client_index))
+        b = a.clone()
+        dist.all_reduce(a, group=ctx.data_group)
+        ipc.allreduce_(b)
+        torch.cuda.synchronize(dev)
+        ok = int(ipc.status() == 0 and bool(torch.allclose(a, b, rtol=1e-5, atol=1e-5)))
+        for k, fn in enumerate((lambda x: ipc.allreduce_(x), lambda x: dist.all_reduce(x, group=ctx.data_group))):
+            if not ok:
+                break
+            fn(b)
+            torch.cuda.synchronize(dev)
+            dist.barrier(group=ctx.client_ctrl_group)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn(b)
+            torch.cuda.synchronize(dev)
+            ms[k] = 1000.0 * (time.perf_counter() - t0) / reps
+        ok = int(ok and ipc.status() == 0)
+    except Exception as e:  # pragma: no cover - depends on the node
+        ok = 0
+        if log is not None:
+            log(f"[client {ctx.client_index}] IPC all-reduce probe failed: {e!r}"[:400])
+    t = torch.tensor([ok], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.client_ctrl_group)
+    tm = torch.tensor(ms, dtype=torch.float64)
+    dist.all_reduce(tm, op=dist.ReduceOp.MAX, group=ctx.client_ctrl_group)
+    info["ok"] = bool(t.item())
+    info["ipc_ms"], info["group_ms"] = round(float(tm[0]), 4), round(float(tm[1]), 4)
+    if info["ok"]:
+        ipc.timeout_s = float(timeout_s)  # the run's collective timeout from here on
+        info["ipc"] = ipc
+    elif ipc is not None:
+        try:
+            ipc.close()
+        except Exception:  # pragma: no cover
+            pass
+    return info
+
+
+def make_grad_allreduce(ctx: DistContext, timeout_s: float = 600.0, choice: Optional[str] = None, log=None,
+                        nelem: int = 1 << 20):
+    """Sum the flat gradient over the client data group; returns the 1/W scale Adam applies.
+
+    ``choice`` (default: ``FEDREC_ALLREDUCE``, else ``rccl``):
+      * ``rccl`` -- ``dist.all_reduce`` on the data group (RCCL over xGMI; gloo on the CPU);
+      * ``ipc``  -- the custom IPC all-reduce with device epochs: capturable, so the engine runs
+        it INSIDE the step graph (every rank gets the bitwise-same sum); its ``check`` (run by
+        the engine at every epoch end) raises if a peer timed out;
+      * ``auto`` -- ``ipc`` when :func:`probe_ipc_grad` finds it correct on this node and not
+        slower than the data group's all-reduce by more than 25 % (isolated, eager), else ``rccl``.
+    ``nelem``: the bucket the probe checks and times (the flat gradient's size).  The returned
+    callable carries ``kind``, ``capturable`` and (auto) ``probe``."""
+    if ctx.num_clients <= 1 or not ctx.initialized:
+        return None
+    W = ctx.num_clients
+    choice = choice or os.environ.get("FEDREC_ALLREDUCE", "rccl")
+    if ctx.device.type != "cuda" or choice not in ("ipc", "auto"):
+        return _rccl_grad_fn(ctx, W)
+    if choice == "ipc":
+        return _ipc_grad_fn(ctx, make_ipc_allreduce(ctx, timeout_s, device_epoch=True), W)
+    probe = probe_ipc_grad(ctx, int(nelem), timeout_s=timeout_s, log=log)
+    use = probe["ok"] and probe["ipc_ms"] <= 1.25 * probe["group_ms"]
+    fn = _ipc_grad_fn(ctx, probe["ipc"], W) if use else _rccl_grad_fn(ctx, W)
+    if not use and probe["ipc"] is not None:
+        probe["ipc"].close()
+    fn.probe = {k: v for k, v in probe.items() if k != "ipc"}
+    return fn
 
 
 def make_secure_grad_allreduce(ctx: DistContext, timeout_s: float = 600.0, run_id: str = "secagg-ga"):

@@ -39,11 +39,18 @@ class IpcAllReduce:
     """One rank's end of the IPC all-reduce among the ``world`` clients of ``ctrl_group``."""
 
     def __init__(self, ctrl_group, rank: int, world: int, device: torch.device, cap: int = DEFAULT_CAP,
-                 one_shot_max: Optional[int] = None, blocks: Optional[int] = None, timeout_s: float = 600.0):
+                 one_shot_max: Optional[int] = None, blocks: Optional[int] = None, timeout_s: float = 600.0,
+                 device_epoch: bool = False):
+        """``device_epoch``: every call's epoch comes from a device counter of the context (the
+        launch is capturable in a HIP graph: each replay runs the next epoch); such a context
+        takes device-epoch calls only."""
         self.lib = native.lib()
         self.rank, self.world, self.device = int(rank), int(world), device
+        self.device_epoch = bool(device_epoch)
         if one_shot_max is None:
-            one_shot_max = int(os.environ.get("FEDREC_IPC_ONE_SHOT_MAX", 8 << 20))
+            # one-shot reads (W - 1) buckets per rank, two-shot 2 (W - 1) / W of one plus a second
+            # barrier: one-shot for two ranks, two-shot for larger groups past 512 KB
+            one_shot_max = int(os.environ.get("FEDREC_IPC_ONE_SHOT_MAX", (8 << 20) if world <= 2 else (512 << 10)))
         if blocks is None:
             blocks = int(os.environ.get("FEDREC_IPC_BLOCKS", 32))
         self.cap, self.one_shot_max, self.blocks = int(cap), int(one_shot_max), int(blocks)
@@ -105,8 +112,9 @@ def _allreduce(g, t: torch.Tensor, mode: Optional[str]) -> torch.Tensor:
         work = torch.zeros(-(-t.numel() // 4) * 4, dtype=t.dtype, device=t.device)
         work[:t.numel()].copy_(t.reshape(-1))
     m = mode or ("one" if nbytes <= g.one_shot_max else "two")
-    g.epoch += 1
-    g.lib.ipc_allreduce_(g.id, work.view(-1), g.epoch, 0 if m == "one" else 1, g.blocks, g.timeout_s)
+    g.epoch += 1  # (a device-epoch context passes 0: the kernel takes its own counter + 1)
+    g.lib.ipc_allreduce_(g.id, work.view(-1), 0 if getattr(g, "device_epoch", False) else g.epoch,
+                         0 if m == "one" else 1, g.blocks, g.timeout_s)
     if work is not t:
         t.view(-1).copy_(work[:t.numel()])
     return t

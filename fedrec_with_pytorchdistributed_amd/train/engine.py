@@ -138,13 +138,16 @@ class _StepGraph:
             # in-graph Adam: the step's cast launch (its first kernel) advances the device step count
             eng._adam_bump = eng._adam_step_dev if with_adam else None
             # the in-graph Adam gathers the step's gradients from where autograd left them and
-            # writes them into the flat buffer itself: no separate copy launch (6 us per step)
-            eng._adam_gathers = with_adam
+            # writes them into the flat buffer itself: no separate copy launch (6 us per step) --
+            # unless a gradient all-reduce sits between them (N > 1): it needs the flat buffer
+            ar = eng.grad_allreduce if with_adam else None
+            eng._adam_gathers = with_adam and ar is None
             eng._precast = eng.step_cast_bufs() if self.precast else None
             with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
                 self.loss = eng.forward_backward(self.cand, self.his, static)
-                if with_adam:  # no all-reduce between backward and optimizer: the step in one graph
-                    eng._adam_dev(self.loss)
+                if with_adam:  # the step in one graph: backward, [all-reduce,] Adam
+                    scale = ar(eng.flat.grad) if ar is not None else 1.0
+                    eng._adam_dev(self.loss, scale)
         finally:
             eng._pre_hid = None
             eng._adam_bump = None
@@ -228,6 +231,8 @@ class LocalEngine:
         self._pre_hid: Optional[torch.Tensor] = None
         self._one: Optional[torch.Tensor] = None  # seed gradient of the loss (see forward_backward)
         self.hcache = self._make_hidden_cache()
+        self.catalog = None  # (CatalogPlan, data group): cooperative cache builds (set_catalog)
+        self._catalog_ctrl = None
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
         self.replay_chunk = 4096 if self.hcache is not None else 1024
@@ -237,6 +242,9 @@ class LocalEngine:
             sg == "on" or (sg == "auto" and (self.fused_user or not cfg.dp.enabled)))
         self._graphs: Dict[tuple, "_StepGraph"] = {}
         self.last_stats: Dict[str, float] = {}
+        # step counters (tests / bench): graph replays, replays that ran the all-reduce + Adam
+        # inside the graph, and optimizer steps issued eagerly from the host
+        self.counts = {"replays": 0, "replays_with_optimizer": 0, "eager_optimizer_steps": 0, "eager_steps": 0}
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
         # trainable parameters; everything that does calls sync_params() first
@@ -296,12 +304,40 @@ class LocalEngine:
             raise ValueError(f"news_cache={mode!r}: expected auto | hidden | none | vectors")
         return HiddenCache(te, self.tokens)
 
+    def set_catalog(self, plan, data_group, ctrl_group=None) -> None:
+        """Cooperative cache builds (:mod:`..parallel.catalog`): :meth:`build_cache` encodes this
+        client's 1/W share of the catalog and all-gathers the rest over ``data_group``.  Every
+        client of the group must then call :meth:`build_cache` at the same points; the lazy
+        rebuild of a stale cache inside a step (:meth:`HiddenCache.ensure`) stays a local build."""
+        self.catalog = (plan, data_group) if plan is not None else None
+        self._catalog_ctrl = ctrl_group
+
     def build_cache(self) -> Optional[float]:
-        """(Re)build the hidden-state cache now; returns its build time in seconds (None: no cache)."""
+        """(Re)build the hidden-state cache now; returns its build time in seconds (None: no cache).
+        With a catalog plan (:meth:`set_catalog`) this is a collective over the clients."""
         if self.hcache is None:
             return None
         self.sync_params()
+        if self.catalog is not None:
+            return self.hcache.build(*self.catalog)
         return self.hcache.build()
+
+    def ensure_cache(self) -> None:
+        """Collective point of the round drivers: rebuild a stale cache now (cooperatively when a
+        catalog plan is set) instead of lazily inside the first step."""
+        if self.hcache is None:
+            return
+        stale = not self.hcache.fresh()
+        if self.catalog is not None and self._catalog_ctrl is not None:
+            # the clients agree first (one gloo MAX): any stale cache -> every client rebuilds, so
+            # the cooperative gather never waits for a client that thought its table was fresh
+            import torch.distributed as dist
+
+            t = torch.tensor([1 if stale else 0], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._catalog_ctrl)
+            stale = bool(t.item())
+        if stale:
+            self.build_cache()
 
     # -------------------------------------------------------------------------------
     @property
@@ -529,14 +565,17 @@ class LocalEngine:
         # noise; the non-fused path's host offset would be frozen into the graph
         if self.step_graphs and pre.dedup is not None and not (self.cfg.dp.enabled and self.sigma
                                                                and not self.fused_user):
-            # (the device step count rides in the fused step's cast launch)
-            with_adam = self.grad_allreduce is None and self.reducer is None and self.fused_user and self.fused_head
+            # (the device step count rides in the fused step's cast launch); a capturable gradient
+            # all-reduce (the device-epoch IPC one) joins them: one replay per step at N > 1 too
+            ar_ok = self.grad_allreduce is None or getattr(self.grad_allreduce, "capturable", False)
+            with_adam = ar_ok and self.reducer is None and self.fused_user and self.fused_head
             loss = self._graph_step(pre, with_adam)
             if loss is not None:
                 if not with_adam:
                     self.optimizer_step(overlap=True)
                 self._retire(pre)
                 return loss
+        self.counts["eager_steps"] += 1
         loss = self.train_step(pre.cand, pre.his, pre)
         self._retire(pre)
         return loss
@@ -544,7 +583,7 @@ class LocalEngine:
     # ---- Adam inside the step graph (no gradient all-reduce: one client) ----------------
     LOSS_RING = 4096  # per-step losses live here until read (train_epoch folds every LOSS_RING / 2)
 
-    def _adam_dev(self, loss: torch.Tensor) -> None:
+    def _adam_dev(self, loss: torch.Tensor, scale: float = 1.0) -> None:
         """Adam with its step count on the device (csrc/adam.hip adam_dev_kernel), capturable:
         also copies the step's loss into the loss ring.  The host mirror ``flat.step`` is
         advanced by the caller per replay."""
@@ -552,7 +591,8 @@ class LocalEngine:
         srcs, self._grad_srcs = self._grad_srcs, None
         native.require_for(loss).adam_dev(self.flat.flat, self.flat.grad, self.flat.m, self.flat.v, self._adam_step_dev,
                                           loss.reshape(1).float(), self._loss_ring, c.lr, c.adam_beta1, c.adam_beta2,
-                                          c.adam_eps, 1.0, srcs, list(self.flat.offsets) if srcs is not None else None)
+                                          c.adam_eps, float(scale), srcs,
+                                          list(self.flat.offsets) if srcs is not None else None)
 
     # ---- HIP graph of the per-step forward + backward ------------------------------------
     GRAPH_BUCKET = 128  # unique titles are padded up to a multiple of this (padded rows: id 0)
@@ -605,8 +645,10 @@ class LocalEngine:
             self._adam_mirror = self.flat.step
         if g.precast:  # after the parameters' last update: this launch casts them (and bumps the counters)
             g.load(pre, U)
+        self.counts["replays"] += 1
         if g.adam:
             g.graph.replay()
+            self.counts["replays_with_optimizer"] += 1
             self.flat.step += 1
             self._adam_mirror += 1
             return self._loss_ring[(self.flat.step - 1) % self.LOSS_RING]
@@ -630,6 +672,7 @@ class LocalEngine:
         self._optimizer_step(extra_scale)
 
     def _optimizer_step(self, extra_scale: float) -> None:
+        self.counts["eager_optimizer_steps"] += 1
         scale = extra_scale
         if self.reducer is not None:
             with obs.range("allreduce_wait"):

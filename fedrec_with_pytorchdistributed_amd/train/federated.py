@@ -33,7 +33,7 @@ from ..config import FedRecConfig
 from ..data.shard import Shard
 from ..data.synthetic import SynthSpec, SyntheticCorpus
 from ..models.fedrec_model import FedRecModel
-from ..parallel import comm
+from ..parallel import catalog, comm
 from ..parallel import secagg
 from ..parallel.collcheck import CHECK
 from ..parallel.control import ControlPlane, Heartbeat
@@ -184,10 +184,12 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     eng.sigma = _maybe_dp(cfg, eng)
     eng.load_state(est)
     eng.epoch = start
+    catalog.attach(eng, ctx)  # cooperative hidden-state cache builds over the clients
     writer = _metrics_writer(cfg, ctx.client_index == 0)
     steps = _min_over_clients(ctx, eng.sampler.num_batches())  # every rank issues the same all-reduces
     last = {}
     for epoch in range(start, cfg.total_epochs):
+        eng.ensure_cache()  # a collective point: every client rebuilds a stale cache together
         tr = eng.train_epoch(max_steps=steps)
         va = eng.validate()
         CHECK.verify(ctx.ctrl_group, f"grad_avg epoch {epoch}")
@@ -213,6 +215,7 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     eng.sigma = _maybe_dp(cfg, eng)
     eng.load_state(est)
     eng.epoch = start
+    catalog.attach(eng, ctx)
     writer = _metrics_writer(cfg, ctx.client_index == 0)
     W = ctx.num_clients
     sched = cfg.resolved_local_update()
@@ -231,6 +234,7 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     hook = (lambda n: average() if n % K == 0 else None) if K else None
     last = {}
     for epoch in range(start, cfg.total_epochs):
+        eng.ensure_cache()
         tr = eng.train_epoch(max_steps=steps, step_hook=hook)
         if not K or (steps or 0) % K:
             average()  # once per epoch (Parameter_Averaging_main.py:144-148)
@@ -300,6 +304,8 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     bcast = ctx.initialized and ctx.num_clients > 1 and ctx.data_group is not None and cfg.quorum >= 1.0
     if bcast or agg == "allreduce":
         selfcheck(ctx, log=obs.log)  # every client, before round 0 (the coordinator is not in the data group)
+    if bcast:  # every client is in every round: the cache can be built cooperatively
+        catalog.attach(eng, ctx)
     if k == 0:
         plane = {"backend": dist.get_backend(ctx.data_group) if bcast else "store",
                  "size": dist.get_world_size(ctx.data_group) if bcast else 1}
@@ -314,6 +320,7 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         before = _backbone_before(model, full)
         _receive_global(cp, r, model, ctx, full, bcast)
         _backbone_synced(model, full, before)
+        eng.ensure_cache()  # after the broadcast every client is here: the collective build point
         eng.sigma = _maybe_dp(cfg, eng)
         eng.epoch = 0
         tr, va = {}, {}

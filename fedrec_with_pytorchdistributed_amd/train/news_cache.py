@@ -44,6 +44,7 @@ class HiddenCache:
         self.version = -1
         self.build_s = 0.0  # wall time of the last build (device-synchronised)
         self.builds = 0
+        self.build_info: dict = {}  # the last build's breakdown (cooperative builds)
 
     @staticmethod
     def nbytes_for(num_news: int, title_len: int, dim: int, dtype: torch.dtype) -> int:
@@ -61,13 +62,26 @@ class HiddenCache:
         self.version = -1
 
     @torch.no_grad()
-    def build(self) -> float:
-        """Encode every title once; returns the build time in seconds."""
+    def build(self, plan=None, data_group=None) -> float:
+        """Encode every title once; returns the build time in seconds.  ``plan`` (a
+        :class:`..parallel.catalog.CatalogPlan`, with the clients' ``data_group``): the
+        cooperative build -- this client encodes its 1/W share of the catalog and the shares are
+        all-gathered (a collective: every client of the group calls it together)."""
         dev = self.tokens.device
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         self.table = None  # free the stale table before allocating the new one
+        if plan is not None:
+            from ..parallel.catalog import cooperative_build
+
+            self.table, self.build_info = cooperative_build(self.te, self.tokens, plan, data_group,
+                                                            self.te.compute_dtype, self.chunk)
+            self.version = self.backbone.version
+            self.build_s = time.perf_counter() - t0
+            self.build_info["build_s"] = self.build_s
+            self.builds += 1
+            return self.build_s
         N, _, T = self.tokens.shape
         D = self.backbone.cfg.dim
         table = torch.empty(N, T, D, dtype=self.te.compute_dtype, device=dev)
@@ -81,6 +95,7 @@ class HiddenCache:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         self.build_s = time.perf_counter() - t0
+        self.build_info = {"build_s": self.build_s, "titles_encoded": N}
         self.builds += 1
         return self.build_s
 

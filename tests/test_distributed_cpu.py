@@ -326,3 +326,28 @@ def test_single_process_context_is_one_client(monkeypatch):
     assert ctx.world == 1 and ctx.num_clients == 1 and ctx.client_index == 0 and not ctx.initialized
     assert ctx.client_ctrl_group is None and ctx.data_group is None
     assert fdist.make_grad_allreduce(ctx) is None or callable(fdist.make_grad_allreduce(ctx))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 4])
+def test_cooperative_cache_matches_local_build(world):
+    """Cooperative catalog encode (parallel/catalog.py): W clients each encode 1/W of the
+    union of their news tables, all-gather the shares over the data plane, and place their own
+    rows; every client's table equals the one it builds alone, bitwise, and every catalog title
+    is encoded exactly once (several gather pieces, uneven shares)."""
+    outs = run_ranks([["tests/_catalog_worker.py"]] * world, timeout=240)
+    _ok(outs)
+    for _, out in outs:
+        assert "CATALOG OK 0.0" in out, out[-2000:]
+
+
+@pytest.mark.slow
+def test_grad_avg_cooperative_cache_same_trajectory(tmp_path):
+    """GA with the hidden-state cache on: the cooperative build (default at W > 1) and per-client
+    builds (FEDREC_COOP_CACHE=0) give bit-identical final parameters."""
+    argv = ["Gradient_Averaging_main.py", "1", "16", "0", *TINY, "--news_cache=hidden"]
+    _ok(run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "coop")}))
+    _ok(run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "local"), "FEDREC_COOP_CACHE": "0"}))
+    a = torch.load(tmp_path / "coop" / "rank0.pt")
+    assert torch.equal(a, torch.load(tmp_path / "coop" / "rank1.pt"))
+    assert torch.equal(a, torch.load(tmp_path / "local" / "rank0.pt"))

@@ -130,3 +130,17 @@ def test_ipc_allreduce_dead_peer_raises(dev):
     outs = run_ranks([["tests/_ipc_peer_worker.py"]] * 2, SHARE, timeout=120)
     _ok(outs)
     assert "PEER OK" in outs[0][1], outs[0][1][-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_graph_allreduce_one_replay_per_step(dev, ranks):
+    """N > 1 as one graph replay per step: the device-epoch IPC all-reduce of the flat gradient
+    and the device-step Adam run inside the captured step graph (engine counters: every step a
+    replay with the optimizer in it, no eager optimizer step); clients bit-identical; the same
+    trajectory as the eager all-reduce + Adam path within fp32 summation order.  The hidden-
+    state cache is built cooperatively over the (gloo) data plane."""
+    outs = run_ranks([["tests/_graph_ar_worker.py"]] * ranks, SHARE, timeout=400)
+    _ok(outs)
+    for _, out in outs:
+        assert "GRAPH_AR OK" in out, out[-2000:]
