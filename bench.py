@@ -50,9 +50,10 @@ METRIC = "impressions/sec/node per FedAvg round + MIND AUC, 8 client-GPUs"
 _DB = "DistilBERT-base text encoder (6L/768/12H, frozen, random init) + additive head + 20-head user encoder"
 MODELS = {2: _DB, 3: _DB, 4: _DB,
           5: "BERT-base-shaped text encoder (12L/768/12H, UNFROZEN, random init) + additive head + 20-head user encoder"}
-MODES = {2: "Gradient_Averaging (RCCL all-reduce of flat 4.66 MB grad bucket per step)",
+MODES = {2: "Gradient_Averaging (all-reduce of the flat 4.66 MB grad bucket per step: {ar})",
          3: "Parameter_Averaging (local Adam steps, RCCL all-reduce of the parameters every {k} steps)",
-         4: "Gradient_Averaging + LDP (fused per-occurrence clip C=2 + Gaussian noise, eps=10 calibrated)",
+         4: "Gradient_Averaging + LDP (fused per-occurrence clip C=2 + Gaussian noise, eps=10 calibrated; "
+            "grad all-reduce: {ar})",
          5: "Gradient_Averaging with secure aggregation (pairwise-masked int32 RCCL all-reduce of all 110M grads "
             "in 28 MB buckets during the backward)"}
 
@@ -336,6 +337,10 @@ def main() -> int:
     charged = elapsed + amort
     imps = args.batch * args.steps * world
     value = imps / charged
+    ar_desc = "none"
+    if ar is not None:
+        ar_desc = ("device-epoch IPC over xGMI inside the step graph" if ar.kind == "ipc" and ar.capturable else
+                   f"{ar.kind}, " + ("inside the step graph" if ar.capturable else "eager on the optimizer stream"))
     if ctx.rank == 0:
         out = {
             "metric": METRIC,
@@ -359,7 +364,7 @@ def main() -> int:
                 "seq_len": cfg.title_len,
                 "history_len": cfg.max_his_len,
                 "parallelism": f"dp{world}",
-                "mode": (MODES[args.config].format(k=args.pa_every) if world > 1 else
+                "mode": (MODES[args.config].format(k=args.pa_every, ar=ar_desc) if world > 1 else
                          MODES[args.config].split(" (")[0] + " (1 client: no all-reduce issued)"),
                 "baseline_config": args.config,
             },

@@ -51,6 +51,14 @@ int fr_head_pool_bwd(const void* table, const int* ids, const float* alpha, cons
 long fr_head_wgrad(const void* e, const void* table, const int* ids, const float* da, const float* db2p,
                    const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2, float* db2,
                    float* scratch, const int* nreal, hipStream_t s);
+int fr_head_g_supported(int D, int Q, int T);
+int fr_head_pool_bwd_g(const void* table, const int* ids, const float* alpha, const float* g, int U, int T, int D,
+                       int Q, float* da, float* db2p, void* e, float* cs, const int* nreal, hipStream_t s);
+long fr_head_wgrad_g(const void* G, const void* table, const int* ids, const float* cs, const float* db2p,
+                     const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2, float* db2,
+                     float* scratch, const int* nreal, hipStream_t s);
+int fr_head_g_rewrite(const float* da, int U, int T, int Q, void* e, float* cs, const int* nreal, hipStream_t s);
+void fr_head_wgrad_g_set_kt(int kt);
 int fr_ipc_create(long cap, void* handle_out);
 int fr_ipc_open(int id, const void* handles, int me, int W, const long long* local_ptrs);
 long long fr_ipc_region(int id);
@@ -606,6 +614,100 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad(const at::
                               dW1.data_ptr<float>(), db1, dw2, db2, scratch.data_ptr<float>(), opt_nreal(nreal, table),
                               cur_stream()),
            "head_wgrad");
+  return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
+}
+
+// the G path: the pool backward also rewrites e (bf16 [U*T, Q], in place) into g = da (1 - e^2)
+// and writes the per-title column partials cs [2, U, Q]; the weight gradient is then a plain
+// TN GEMM over g (head_wgrad_g).  Q = 384 only (head_g_supported).
+bool head_g_supported(int64_t D, int64_t Q, int64_t T) { return fr_head_g_supported((int)D, (int)Q, (int)T) != 0; }
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> head_pool_bwd_g(const at::Tensor& table,
+                                                               const c10::optional<at::Tensor>& ids, int64_t T,
+                                                               const at::Tensor& alpha, const at::Tensor& g,
+                                                               at::Tensor e, const c10::optional<at::Tensor>& nreal) {
+  const int64_t U = head_titles(table, ids, T), D = table.size(1);
+  check_dev(alpha, "alpha");
+  check_dev(g, "g");
+  check_dev(e, "e");
+  TORCH_CHECK(alpha.scalar_type() == at::kFloat && alpha.numel() == U * T && alpha.is_contiguous() &&
+                  g.scalar_type() == at::kFloat && g.numel() == U * D && g.is_contiguous(),
+              "fedrec::head_pool_bwd_g: alpha [U, T], g [U, D] fp32");
+  TORCH_CHECK(e.scalar_type() == at::kBFloat16 && e.is_contiguous() && U > 0 && e.numel() % (U * T) == 0,
+              "fedrec::head_pool_bwd_g: e bf16 [U*T, Q]");
+  const int64_t Q = U > 0 ? e.numel() / (U * T) : 0;
+  TORCH_CHECK(fr_head_g_supported((int)D, (int)Q, (int)T), "fedrec::head_pool_bwd_g: unsupported shape");
+  const c10::DeviceGuard dg(table.device());
+  auto da = at::empty({U * T}, alpha.options());
+  auto db2p = at::empty({std::max<int64_t>(U, 1)}, alpha.options());
+  auto cs = at::empty({2, U, Q}, alpha.options());
+  check_rc(fr_head_pool_bwd_g(table.data_ptr(), opt_int_ptr(ids), alpha.data_ptr<float>(), g.data_ptr<float>(),
+                              (int)U, (int)T, (int)D, (int)Q, da.data_ptr<float>(), db2p.data_ptr<float>(),
+                              e.data_ptr(), cs.data_ptr<float>(), opt_nreal(nreal, table), cur_stream()),
+           "head_pool_bwd_g");
+  return {da, db2p, cs};
+}
+
+// the g rewrite alone (after head_pool_bwd): e [U*T, Q] bf16 -> g in place; returns cs [2, U, Q]
+at::Tensor head_g_rewrite(const at::Tensor& da, int64_t T, at::Tensor e, const c10::optional<at::Tensor>& nreal) {
+  check_dev(da, "da");
+  check_dev(e, "e");
+  TORCH_CHECK(da.scalar_type() == at::kFloat && da.is_contiguous() && da.numel() % T == 0,
+              "fedrec::head_g_rewrite: da fp32 [U*T]");
+  const int64_t U = da.numel() / T;
+  TORCH_CHECK(e.scalar_type() == at::kBFloat16 && e.is_contiguous() && U > 0 && e.numel() % (U * T) == 0,
+              "fedrec::head_g_rewrite: e bf16 [U*T, Q]");
+  const int64_t Q = e.numel() / (U * T);
+  const int* nr = nullptr;
+  if (nreal.has_value()) {
+    TORCH_CHECK(nreal->scalar_type() == at::kInt && nreal->numel() == 1 && nreal->device() == da.device(),
+                "fedrec::head_g_rewrite: nreal int32 [1] on da's device");
+    nr = nreal->data_ptr<int>();
+  }
+  const c10::DeviceGuard dg(da.device());
+  auto cs = at::empty({2, U, Q}, da.options());
+  check_rc(fr_head_g_rewrite(da.data_ptr<float>(), (int)U, (int)T, (int)Q, e.data_ptr(), cs.data_ptr<float>(), nr,
+                             cur_stream()),
+           "head_g_rewrite");
+  return cs;
+}
+
+void head_wgrad_g_set_kt(int64_t kt) { fr_head_wgrad_g_set_kt((int)kt); }
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad_g(const at::Tensor& table,
+                                                                        const c10::optional<at::Tensor>& ids, int64_t T,
+                                                                        const at::Tensor& G, const at::Tensor& cs,
+                                                                        const at::Tensor& w2, const at::Tensor& db2p,
+                                                                        const c10::optional<at::Tensor>& nreal) {
+  const int64_t U = head_titles(table, ids, T), D = table.size(1), Q = w2.numel();
+  check_dev(G, "G");
+  check_dev(cs, "cs");
+  check_dev(w2, "w2");
+  check_dev(db2p, "db2p");
+  TORCH_CHECK(G.scalar_type() == at::kBFloat16 && G.is_contiguous() && G.numel() == U * T * Q,
+              "fedrec::head_wgrad_g: G bf16 [U*T, Q]");
+  TORCH_CHECK(cs.scalar_type() == at::kFloat && cs.is_contiguous() && cs.numel() == 2 * U * Q &&
+                  w2.scalar_type() == at::kFloat && w2.is_contiguous() && db2p.scalar_type() == at::kFloat &&
+                  db2p.numel() >= U,
+              "fedrec::head_wgrad_g: cs [2, U, Q] / w2 / db2p");
+  TORCH_CHECK(fr_head_g_supported((int)D, (int)Q, (int)T), "fedrec::head_wgrad_g: unsupported shape");
+  const c10::DeviceGuard g(table.device());
+  auto fopt = cs.options();
+  auto dW1 = at::empty({Q, D}, fopt);
+  auto small = at::empty({2 * Q + 1}, fopt);
+  float* db1 = small.data_ptr<float>();
+  float* dw2 = db1 + Q;
+  float* db2 = dw2 + Q;
+  const long need = fr_head_wgrad_g(G.data_ptr(), table.data_ptr(), opt_int_ptr(ids), cs.data_ptr<float>(),
+                                    db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
+                                    dW1.data_ptr<float>(), db1, dw2, db2, nullptr, nullptr, cur_stream());
+  TORCH_CHECK(need > 0, "fedrec::head_wgrad_g: unsupported shape");
+  auto scratch = at::empty({need}, fopt);
+  check_rc((int)fr_head_wgrad_g(G.data_ptr(), table.data_ptr(), opt_int_ptr(ids), cs.data_ptr<float>(),
+                                db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
+                                dW1.data_ptr<float>(), db1, dw2, db2, scratch.data_ptr<float>(),
+                                opt_nreal(nreal, table), cur_stream()),
+           "head_wgrad_g");
   return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
 }
 
@@ -1689,6 +1791,11 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("title_attention(Tensor qkv, Tensor mask, int n_heads) -> Tensor");
   m.def("head_supported(int D, int Q, int T) -> bool", &head_supported);
+  m.def("head_g_supported(int D, int Q, int T) -> bool", &head_g_supported);
+  m.def("head_wgrad_g_set_kt(int kt) -> ()", &head_wgrad_g_set_kt);
+  m.def("head_g_rewrite(Tensor da, int T, Tensor(a!) e, Tensor? nreal=None) -> Tensor");
+  m.def("head_pool_bwd_g(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor(a!) e, Tensor? nreal=None) -> (Tensor, Tensor, Tensor)");
+  m.def("head_wgrad_g(Tensor table, Tensor? ids, int T, Tensor G, Tensor cs, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("ipc_create(int cap) -> (int, Tensor)", &ipc_create);
   m.def("ipc_open(int id, Tensor handles, int me, int W, Tensor? local_ptrs) -> ()", &ipc_open);
   m.def("ipc_region(int id) -> int", &ipc_region);
@@ -1756,6 +1863,9 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("head_pool", &head_pool);
   m.impl("head_pool_bwd", &head_pool_bwd);
   m.impl("head_wgrad", &head_wgrad);
+  m.impl("head_pool_bwd_g", &head_pool_bwd_g);
+  m.impl("head_g_rewrite", &head_g_rewrite);
+  m.impl("head_wgrad_g", &head_wgrad_g);
   m.impl("additive_pool_fwd", &additive_pool_fwd);
   m.impl("additive_pool_bwd", &additive_pool_bwd);
   m.impl("upool_bwd_da", &upool_bwd_da);

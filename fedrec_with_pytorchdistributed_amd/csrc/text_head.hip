@@ -1168,6 +1168,438 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const f32x4* __restric
   if (threadIdx.x == 0) db2[0] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// =========================================================================================
+// The G path (round 5): the e -> g = da (1 - e^2) rewrite leaves the weight-gradient GEMM.
+// head_wgrad rewrote each E tile in all three K-tile blocks of a split (10 VALU instructions per
+// MFMA, 26 % of its wave time; profiles/r4_pmc_stalls_cfg2.json).  Here the pool backward, which
+// forms da, also reads the title's e rows once, writes g (bf16, in place over e) and the title's
+// column partials dw2_u = sum_t da_t e_tq and dsum_u = sum_t g_tq (the rounded g the GEMM
+// consumes); the weight gradient is then a pure TN MFMA stream over G and the cached X rows.
+// =========================================================================================
+
+// head_pool_bwd3: head_pool_bwd2 + the g rewrite of title u's e rows + its column partials
+// cs[0][u][q] (dw2) and cs[1][u][q] (dsum).  e chunks: Q/8 16-B chunks per row, 384 / (Q/8)
+// row groups, ETP rows per thread (loaded first: in flight with the X rows).
+template <int TPW, int ETP>
+__global__ __launch_bounds__(384) void head_pool_bwd3_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
+                                                             const float* __restrict__ alpha,
+                                                             const float* __restrict__ g, int T, int D, int Q,
+                                                             float* __restrict__ da, float* __restrict__ db2p,
+                                                             bf16* __restrict__ e, float* __restrict__ cs, int U,
+                                                             const int* __restrict__ nreal) {
+  __shared__ float dal[MAXT];
+  __shared__ float dat[MAXT];
+  __shared__ float red[2][3072];
+  const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* cs0 = cs + (size_t)u * Q;
+  float* cs1 = cs + ((size_t)U + u) * Q;
+  if (nreal != nullptr && u >= nreal[0]) {  // a padded title: no gradient (its rows are never read)
+    for (int t = tid; t < T; t += blockDim.x) da[(size_t)u * T + t] = 0.f;
+    for (int q = tid; q < Q; q += blockDim.x) {
+      cs0[q] = 0.f;
+      cs1[q] = 0.f;
+    }
+    if (tid == 0) db2p[u] = 0.f;
+    return;
+  }
+  // e rows of this title, in flight first
+  const int EC = Q >> 3, EG = 384 / EC;
+  const int ec = tid % EC, egr = tid / EC;
+  const bool eact = egr < EG;
+  const int eg = eact ? egr : 0;
+  bf16* eu = e + (size_t)u * T * Q;
+  bf16x8 ev[ETP];
+#pragma unroll
+  for (int i = 0; i < ETP; ++i) {
+    const int t = eg + EG * i;
+    ev[i] = *(const bf16x8*)(eu + (size_t)(t < T ? t : T - 1) * Q + ec * 8);
+  }
+  const int id = ids != nullptr ? ids[u] : u;
+  const bf16* xe = table + (size_t)id * T * D;
+  const float* gu = g + (size_t)u * D;
+  const int DC = D >> 3;
+  bf16x8 v[TPW][2];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = wave + 6 * i;
+    const bf16* row = xe + (size_t)(t < T ? t : T - 1) * D;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int dc = lane + 64 * c;
+      v[i][c] = *(const bf16x8*)(row + (dc < DC ? dc : 0) * 8);
+    }
+  }
+  float gv[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int dc = lane + 64 * c;
+    const float4 g0 = dc < DC ? *(const float4*)(gu + dc * 8) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g1 = dc < DC ? *(const float4*)(gu + dc * 8 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
+    gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
+  }
+  float s[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    s[i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (lane + 64 * c < DC) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[i] += (float)v[i][c][k] * gv[c][k];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) s[i] = wave_sum(s[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i)
+      if (wave + 6 * i < T) dal[wave + 6 * i] = s[i];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float al[2], dv[2], sm = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      al[c] = t < T ? alpha[(size_t)u * T + t] : 0.f;
+      dv[c] = t < T ? dal[t] : 0.f;
+      sm += al[c] * dv[c];
+    }
+    sm = wave_sum(sm);
+    float sd = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int t = lane + 64 * c;
+      const float val = al[c] * (dv[c] - sm);
+      if (t < T) {
+        da[(size_t)u * T + t] = val;
+        dat[t] = val;
+      }
+      sd += val;
+    }
+    sd = wave_sum(sd);
+    if (lane == 0) db2p[u] = sd;
+  }
+  __syncthreads();
+  // g = da (1 - e^2) in place, column partials over this thread's rows
+  float sw2[8], ssum[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sw2[k] = ssum[k] = 0.f;
+#pragma unroll
+  for (int i = 0; i < ETP; ++i) {
+    const int t = eg + EG * i;
+    if (eact && t < T) {
+      const float dav = dat[t];
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float f = (float)ev[i][k];
+        o[k] = f2bf(dav * (1.0f - f * f));
+        sw2[k] += dav * f;
+        ssum[k] += (float)o[k];
+      }
+      *(bf16x8*)(eu + (size_t)t * Q + ec * 8) = o;
+    }
+  }
+  if (eact) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[0][eg * Q + ec * 8 + k] = sw2[k];
+      red[1][eg * Q + ec * 8 + k] = ssum[k];
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < Q; q += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int j = 0; j < EG; ++j) {
+      a0 += red[0][j * Q + q];
+      a1 += red[1][j * Q + q];
+    }
+    cs0[q] = a0;
+    cs1[q] = a1;
+  }
+}
+
+// head_g_rewrite: the g rewrite alone, after head_pool_bwd2 formed da: title u's e rows -> g
+// (in place) and its column partials cs[0][u] (dw2) / cs[1][u] (dsum).  384 threads: Q/8 chunks
+// x 384/(Q/8) row groups, every e chunk in flight before da is read.
+template <int ETP>
+__global__ __launch_bounds__(384) void head_g_rewrite_kernel(const float* __restrict__ da, int T, int Q,
+                                                             bf16* __restrict__ e, float* __restrict__ cs, int U,
+                                                             const int* __restrict__ nreal) {
+  __shared__ float red[2][3072];
+  const int u = blockIdx.x, tid = threadIdx.x;
+  float* cs0 = cs + (size_t)u * Q;
+  float* cs1 = cs + ((size_t)U + u) * Q;
+  if (nreal != nullptr && u >= nreal[0]) {
+    for (int q = tid; q < Q; q += blockDim.x) {
+      cs0[q] = 0.f;
+      cs1[q] = 0.f;
+    }
+    return;
+  }
+  const int EC = Q >> 3, EG = 384 / EC;
+  const int ec = tid % EC, egr = tid / EC;
+  const bool eact = egr < EG;
+  const int eg = eact ? egr : 0;
+  bf16* eu = e + (size_t)u * T * Q;
+  bf16x8 ev[ETP];
+  float dv[ETP];
+#pragma unroll
+  for (int i = 0; i < ETP; ++i) {
+    const int t = eg + EG * i;
+    const int tc = t < T ? t : T - 1;
+    ev[i] = *(const bf16x8*)(eu + (size_t)tc * Q + ec * 8);
+    dv[i] = da[(size_t)u * T + tc];
+  }
+  float sw2[8], ssum[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sw2[k] = ssum[k] = 0.f;
+#pragma unroll
+  for (int i = 0; i < ETP; ++i) {
+    const int t = eg + EG * i;
+    if (eact && t < T) {
+      const float dav = dv[i];
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float f = (float)ev[i][k];
+        o[k] = f2bf(dav * (1.0f - f * f));
+        sw2[k] += dav * f;
+        ssum[k] += (float)o[k];
+      }
+      *(bf16x8*)(eu + (size_t)t * Q + ec * 8) = o;
+    }
+  }
+  if (eact) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[0][eg * Q + ec * 8 + k] = sw2[k];
+      red[1][eg * Q + ec * 8 + k] = ssum[k];
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < Q; q += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int j = 0; j < EG; ++j) {
+      a0 += red[0][j * Q + q];
+      a1 += red[1][j * Q + q];
+    }
+    cs0[q] = a0;
+    cs1[q] = a1;
+  }
+}
+
+// head_wgrad_g: P[s][q][k] = sum_{m in split s} g_mq x_mk -- a plain TN MFMA GEMM (the g tile
+// arrives ready in bf16).  Tile 384 (q: the whole head width) x KT (k), 512 threads = 8 waves:
+//   KT = 128: 4 (q) x 2 (k) waves of 96 x 64 (6 x 4 MFMA tiles, 96 accumulators), 4 stages;
+//   KT = 256: 2 (q) x 4 (k) waves of 192 x 64 (12 x 4 tiles, 192 accumulators), 3 stages --
+//             G read by 3 k-tile blocks instead of 6 (3,840 instead of 6,144 B per row from L2).
+// Stage = 32 rows: G [32 x 768 B] (3 glds per wave), X [32 x 2 KT B] (cache rows by title
+// index, KT / 128 glds per wave); both read back with ds_read_b64_tr_b16 (M-major operands),
+// 16-B chunks swizzled by swz(row) within aligned 16-chunk groups (256-B multiples).  The G
+// fragments are read a pair at a time, one pair ahead of the MFMAs that use it.
+// Splits are whole titles (the column partials are per title): the k-tile blocks of split s
+// each sum a 1 / tiles_k share of the 2 Q columns of cs over the split's titles into dw2p /
+// dsump[s] after their GEMM.
+constexpr int GQT = 384;
+constexpr int G_BYTES = WTM * GQT * 2;  // 24 KB
+
+__device__ __forceinline__ uint32_t tr_off_pitch(int pitch, int r0, int col0, int q, int p) {
+  const int c = (col0 >> 3) + (p >> 1);
+  const int r = r0 + q;
+  return (uint32_t)(r * pitch + ((c ^ swz(r)) << 4) + (p & 1) * 8);
+}
+
+template <int KT>
+__device__ __forceinline__ void wgg_stage(char* base, const bf16* __restrict__ G, const bf16* __restrict__ table,
+                                          uint32_t ids_lds, int u_lo, int T, int D, int k0, int m, int me, int wave,
+                                          int lane) {
+  // G: 24 pieces of 1 KB, 3 per wave (lane-linear LDS, swizzle on the source)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int p = wave * 3 + i;
+    const int off = p * 1024 + lane * 16;
+    const int row = off / 768, pc = (off % 768) >> 4;
+    const int c = pc ^ swz(row);
+    const int gm = m + row;
+    const bf16* src = gm < me ? G + (size_t)gm * GQT + 8 * c : g_zero_row + 8 * c;
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src), LDS_PTR(void, base + p * 1024), 16, 0, 0);
+  }
+  // X: 32 rows of 2 KT bytes in KT / 128 pieces per wave
+  constexpr int CPR = KT / 8, RPP = 64 / CPR;  // 16-B chunks per row, rows per piece
+#pragma unroll
+  for (int i = 0; i < KT / 128; ++i) {
+    const int piece = wave * (KT / 128) + i;
+    const int row = piece * RPP + lane / CPR, pc = lane % CPR;
+    const int c = pc ^ swz(row);
+    const int gm = m + row;
+    const bf16* src = g_zero_row + 8 * c;
+    if (gm < me) {
+      const int uu = gm / T;
+      const int id = lds_read32i(ids_lds + 4 * (uu - u_lo));
+      src = table + ((size_t)id * T + (gm - uu * T)) * D + k0 + 8 * c;
+    }
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src), LDS_PTR(void, base + G_BYTES + piece * 1024), 16, 0,
+                                     0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void lgkm_tie4(s16x4 (&r)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : "n"(N));
+}
+
+template <int KT, int NSTAGE>
+__global__ __launch_bounds__(512, 1) void head_wgrad_g_kernel(const bf16* __restrict__ G, const bf16* __restrict__ table,
+                                                              const int* __restrict__ ids, const float* __restrict__ cs,
+                                                              int U, int T, int D, float* __restrict__ P,
+                                                              float* __restrict__ dw2p, float* __restrict__ dsump,
+                                                              int tiles_k, int tps, const int* __restrict__ nreal) {
+  constexpr int X_BYTES_ = WTM * KT * 2;
+  constexpr int STB = G_BYTES + X_BYTES_;
+  constexpr int WQN = KT == 128 ? 4 : 2;  // waves along q
+  constexpr int QF = GQT / 16 / WQN;      // 16-column G fragments per wave (6 / 12)
+  constexpr int GPW = 3 + KT / 128;       // glds per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STB + 4 * MAX_SPLIT_TITLES];
+  constexpr int Q = GQT;
+  // XCD-aware order: the k-tiles of one split (same G / X row panel) on one XCD's L2
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rmd = nwg & 7;
+  const int t = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (bid >> 3);
+  const int s = t / tiles_k, kt = t - s * tiles_k;
+  const int k0 = kt * KT;
+  int Ur = U;
+  if (nreal != nullptr) {  // a padded step graph: the real titles re-split over the same grid
+    Ur = min(U, nreal[0]);
+    const int S = nwg / tiles_k;
+    tps = max(1, min(tps, (Ur + S - 1) / S));
+  }
+  const int u_lo = min(Ur, s * tps), u_hi = min(Ur, u_lo + tps);  // titles [u_lo, u_hi)
+  const int mb = u_lo * T, me = u_hi * T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wq = wave / (8 / WQN), wk = wave % (8 / WQN);
+
+  f32x4 acc[QF][4];
+#pragma unroll
+  for (int i = 0; i < QF; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = me > mb ? (me - mb + WTM - 1) / WTM : 0;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+  int* ids_s = (int*)(smem + NSTAGE * STB);
+  for (int u = u_lo + tid; u < u_hi; u += 512) ids_s[u - u_lo] = ids != nullptr ? ids[u] : u;
+  __syncthreads();
+  const uint32_t ids_lds = lds0 + NSTAGE * STB;
+#pragma unroll
+  for (int i = 0; i < NSTAGE - 1; ++i)
+    if (i < nsteps) wgg_stage<KT>(smem + i * STB, G, table, ids_lds, u_lo, T, D, k0, mb + i * WTM, me, wave, lane);
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = g * 8;
+  uint32_t xo[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    xo[j][0] = G_BYTES + tr_off_pitch(2 * KT, r0, wk * 64 + j * 16, q, p);
+    xo[j][1] = G_BYTES + tr_off_pitch(2 * KT, r0 + 4, wk * 64 + j * 16, q, p);
+  }
+  const uint32_t yo0 = tr_off_pitch(768, r0, wq * QF * 16, q, p), yo1 = tr_off_pitch(768, r0 + 4, wq * QF * 16, q, p);
+  // fragment i of this wave: columns + 16 i = chunk + 2 i (the swizzle XORs within 16-chunk
+  // groups, and 2 i never carries into bit 4 for i < 8 ... so the offset is recomputed per i)
+  auto yoff = [&](int i, int h) -> uint32_t {
+    return tr_off_pitch(768, r0 + 4 * h, wq * QF * 16 + i * 16, q, p);
+  };
+  (void)yo0;
+  (void)yo1;
+  for (int st = 0; st < nsteps; ++st) {
+    // stage st landed (this wave's GPW glds, then every wave's); every wave is done with st - 1
+    const int left = nsteps - 1 - st;
+    const int inflight = left < NSTAGE - 2 ? left : NSTAGE - 2;
+    __builtin_amdgcn_sched_barrier(0);
+    if (inflight >= 2) {
+      if constexpr (GPW == 4) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (inflight == 1) {
+      if constexpr (GPW == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + NSTAGE - 1 < nsteps)
+      wgg_stage<KT>(smem + ((st + NSTAGE - 1) % NSTAGE) * STB, G, table, ids_lds, u_lo, T, D, k0,
+                    mb + (st + NSTAGE - 1) * WTM, me, wave, lane);
+    const uint32_t base = lds0 + (st % NSTAGE) * STB;
+    s16x4 xr[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xr[2 * j] = tr_read(base + xo[j][0]);
+      xr[2 * j + 1] = tr_read(base + xo[j][1]);
+    }
+    s16x4 yr[2][4];  // a pair of G fragments (2 reads each), one pair ahead
+#pragma unroll
+    for (int h = 0; h < 4; ++h) yr[0][h] = tr_read(base + yoff(h >> 1, h & 1));
+    bf16x8 xb[4];
+#pragma unroll
+    for (int ip = 0; ip < QF / 2; ++ip) {
+      const int cur = ip & 1;
+      if (ip + 1 < QF / 2) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) yr[cur ^ 1][h] = tr_read(base + yoff(2 * (ip + 1) + (h >> 1), h & 1));
+        lgkm_tie4<4>(yr[cur]);
+      } else {
+        lgkm_tie4<0>(yr[cur]);
+      }
+      if (ip == 0) {
+        asm volatile("" : "+v"(xr[0]), "+v"(xr[1]), "+v"(xr[2]), "+v"(xr[3]), "+v"(xr[4]), "+v"(xr[5]), "+v"(xr[6]),
+                     "+v"(xr[7]));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xb[j] = join(xr[2 * j], xr[2 * j + 1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const bf16x8 ya = join(yr[cur][2 * f], yr[cur][2 * f + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[2 * ip + f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], ya, acc[2 * ip + f][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float* out = P + (size_t)s * Q * D;
+#pragma unroll
+  for (int i = 0; i < QF; ++i) {
+    const int qq2 = wq * QF * 16 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wk * 64 + j * 16 + 4 * g;
+      *(f32x4*)(out + (size_t)qq2 * D + k) = acc[i][j];
+    }
+  }
+  // column partials: this k-tile's slice of the 2 Q columns (dw2 | dsum) over the split's titles
+  const int per = (2 * Q + tiles_k - 1) / tiles_k;
+  const int c = kt * per + tid;
+  if (tid < per && c < 2 * Q) {
+    const int which = c / Q, qc = c - which * Q;
+    const float* src = cs + ((size_t)which * U) * Q + qc;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int u = u_lo;
+    for (; u + 3 < u_hi; u += 4) {
+      a0 += src[(size_t)u * Q];
+      a1 += src[(size_t)(u + 1) * Q];
+      a2 += src[(size_t)(u + 2) * Q];
+      a3 += src[(size_t)(u + 3) * Q];
+    }
+    for (; u < u_hi; ++u) a0 += src[(size_t)u * Q];
+    (which == 0 ? dw2p : dsump)[(size_t)s * Q + qc] = (a0 + a1) + (a2 + a3);
+  }
+}
+
 int g_cus = 0;
 int g_score_rows = 0;  // head_score2 row tile: 0 = by the rounds rule, 160 / 192 forced (benchmarks)
 
@@ -1318,6 +1750,93 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
   }
   const long n4 = (long)Q * D / 4;
   const long blocks = (n4 + 63) / 64 + (Q + 63) / 64 + 1;  // dW1 | dw2, db1 | db2
+  hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)P, dw2p, dsump,
+                     db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U);
+  return 0;
+}
+
+// ---- the G path (round 5) -------------------------------------------------------------------
+extern "C" int fr_head_g_supported(int D, int Q, int T) {
+  return Q == GQT && D % 128 == 0 && D <= 1024 && T >= 1 && T <= MAXT && fr_head_supported(D, Q, T);
+}
+
+// pool backward + g rewrite (e in place) + per-title column partials cs [2][U][Q]
+extern "C" int fr_head_pool_bwd_g(const void* table, const int* ids, const float* alpha, const float* g, int U, int T,
+                                  int D, int Q, float* da, float* db2p, void* e, float* cs, const int* nreal,
+                                  hipStream_t s) {
+  if (!fr_head_g_supported(D, Q, T) || D / 8 > 128) return 1;
+  if (U == 0) return 0;
+  const int tpw = (T + 5) / 6;
+  const int EG = 384 / (Q / 8), etp = (T + EG - 1) / EG;
+  if (tpw > 22 || etp > 16) return 1;
+#define LAUNCH_PBWD3(N, E)                                                                                         \
+  hipLaunchKernelGGL((head_pool_bwd3_kernel<N, E>), dim3(U), dim3(384), 0, s, (const bf16*)table, ids, alpha, g, T, \
+                     D, Q, da, db2p, (bf16*)e, cs, U, nreal)
+  if (tpw <= 9 && etp <= 7) LAUNCH_PBWD3(9, 7);
+  else if (tpw <= 11 && etp <= 8) LAUNCH_PBWD3(11, 8);
+  else LAUNCH_PBWD3(22, 16);
+#undef LAUNCH_PBWD3
+  return 0;
+}
+
+// g rewrite alone (after fr_head_pool_bwd): e -> g in place + per-title column partials
+extern "C" int fr_head_g_rewrite(const float* da, int U, int T, int Q, void* e, float* cs, const int* nreal,
+                                 hipStream_t s) {
+  if (Q % 8 != 0 || Q / 8 > 384 || T > MAXT) return 1;
+  if (U == 0) return 0;
+  const int EG = 384 / (Q / 8), etp = (T + EG - 1) / EG;
+#define LAUNCH_GRW(E) \
+  hipLaunchKernelGGL((head_g_rewrite_kernel<E>), dim3(U), dim3(384), 0, s, da, T, Q, (bf16*)e, cs, U, nreal)
+  if (etp <= 7) LAUNCH_GRW(7);
+  else if (etp <= 16) LAUNCH_GRW(16);
+  else return 1;
+#undef LAUNCH_GRW
+  return 0;
+}
+
+static int g_wgg_kt = 0;  // head_wgrad_g k-tile: 0 = default (128), 128 / 256 forced (benchmarks)
+extern "C" void fr_head_wgrad_g_set_kt(int kt) { g_wgg_kt = kt; }
+
+// scratch = null: returns the fp32 scratch element count needed; else launches.  G = the g rows
+// (the e buffer after the rewrite), cs its column partials.
+extern "C" long fr_head_wgrad_g(const void* G, const void* table, const int* ids, const float* cs, const float* db2p,
+                                const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2,
+                                float* db2, float* scratch, const int* nreal, hipStream_t s) {
+  if (!fr_head_g_supported(D, Q, T)) return -1;
+  if (g_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_cus <= 0) g_cus = 256;
+  }
+  // KT = 256 needs 192 accumulators per lane at two waves per SIMD: it spills (39 VGPRs) and ran
+  // 214 vs 84 us (profiles/r5_head_bench.jsonl) -- kept as a forced variant for measurements
+  const int KT = (g_wgg_kt == 256 && D % 256 == 0) ? 256 : 128;
+  const int tiles_k = D / KT;
+  // one block per CU: S splits of whole titles
+  int S = g_cus / tiles_k;
+  if (S < 1) S = 1;
+  int tps = (U + S - 1) / S;
+  if (tps < 1) tps = 1;
+  if (tps > MAX_SPLIT_TITLES - 2) tps = MAX_SPLIT_TITLES - 2;
+  S = U > 0 ? (U + tps - 1) / tps : 1;
+  const long need = (long)S * Q * D + 2L * S * Q;
+  if (scratch == nullptr) return need;
+  float* P = scratch;
+  float* dw2p = scratch + (long)S * Q * D;
+  float* dsump = dw2p + (long)S * Q;
+  if (U > 0) {
+    if (KT == 256)
+      hipLaunchKernelGGL((head_wgrad_g_kernel<256, 3>), dim3(S * tiles_k), dim3(512), 0, s, (const bf16*)G,
+                         (const bf16*)table, ids, cs, U, T, D, P, dw2p, dsump, tiles_k, tps, nreal);
+    else
+      hipLaunchKernelGGL((head_wgrad_g_kernel<128, 4>), dim3(S * tiles_k), dim3(512), 0, s, (const bf16*)G,
+                         (const bf16*)table, ids, cs, U, T, D, P, dw2p, dsump, tiles_k, tps, nreal);
+  } else {
+    (void)hipMemsetAsync(scratch, 0, need * sizeof(float), s);
+  }
+  const long n4 = (long)Q * D / 4;
+  const long blocks = (n4 + 63) / 64 + (Q + 63) / 64 + 1;
   hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)P, dw2p, dsump,
                      db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U);
   return 0;

@@ -168,9 +168,35 @@ class TextHeadFn(torch.autograd.Function):
         lib = ops.native.require_for(table)
         if g is None:
             g = torch.zeros(ids.numel(), table.shape[-1], device=table.device)
-        da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
-        dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p, nreal)
+        if _head_g_path(table.shape[-1], w2.numel(), ctx.T):
+            # the G path: the pool backward also turns e into g = da (1 - e^2) (in place) with the
+            # per-title column sums, and the weight gradient is a plain TN GEMM over g
+            if _HEAD_G_FUSED:
+                da, db2p, cs = lib.head_pool_bwd_g(table, ids, ctx.T, alpha, g.contiguous().float(), e, nreal)
+            else:
+                da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
+                cs = lib.head_g_rewrite(da, ctx.T, e, nreal)
+            dw1, db1, dw2, db2 = lib.head_wgrad_g(table, ids, ctx.T, e, cs, w2.reshape(-1).contiguous(), db2p, nreal)
+        else:
+            da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
+            dw1, db1, dw2, db2 = lib.head_wgrad(table, ids, ctx.T, e, da, w2.reshape(-1).contiguous(), db2p, nreal)
         return dw1, db1, dw2.view(1, -1), db2.view(1), None, None, None, None, None, None, None
+
+
+_HEAD_G: dict = {}
+_HEAD_G_FUSED = __import__("os").environ.get("FEDREC_HEAD_G_FUSED", "0") == "1"
+
+
+def _head_g_path(D: int, Q: int, T: int) -> bool:
+    """The text head's backward on the G path (``head_pool_bwd_g`` + ``head_wgrad_g``): the
+    default where the shape allows (Q = 384, the DistilBERT head); ``FEDREC_HEAD_G=0`` keeps the
+    round-4 path (the e -> g rewrite inside head_wgrad) for A/B runs."""
+    import os
+
+    key = (int(D), int(Q), int(T), os.environ.get("FEDREC_HEAD_G", "1"))
+    if key not in _HEAD_G:
+        _HEAD_G[key] = key[3] != "0" and bool(ops.native.lib().head_g_supported(key[0], key[1], key[2]))
+    return _HEAD_G[key]
 
 
 def fused_head_supported(table_dim: int, query_dim: int, title_len: int) -> bool:

@@ -216,3 +216,40 @@ def test_score_row_tiles_agree_bitwise(dev, U, T):
     finally:
         lib.head_score_set_rows(0)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("U,T,padded", [(1577, 50, True), (257, 50, False), (40, 17, False), (30, 100, True)])
+def test_head_g_path_matches_round4_path(dev, U, T, padded):
+    """The G path (pool backward writes g = da (1 - e^2) and the per-title column sums, the weight
+    gradient is a plain TN GEMM over g: head_pool_bwd_g + head_wgrad_g) against the round-4 path
+    (the rewrite inside head_wgrad's LDS pipeline).  Both consume the same bf16 g values, so the
+    gradients agree to fp32 summation order; padded titles (nreal) are skipped on both."""
+    import os
+
+    g = torch.Generator(device="cpu").manual_seed(U + T)
+    N, D, Q = 2000, 768, 384
+    table = torch.randn(N * T, D, generator=g).to(dev, torch.bfloat16)
+    ids = torch.randint(1, N, (U,), generator=g, dtype=torch.int32)
+    R = U - 37 if padded else U
+    ids[R:] = 0
+    ids = ids.to(dev)
+    nreal = torch.tensor([R], dtype=torch.int32, device=dev) if padded else None
+    w1 = (torch.randn(Q, D, generator=g) / math.sqrt(D)).to(dev).requires_grad_(True)
+    b1 = (torch.randn(Q, generator=g) * 0.1).to(dev).requires_grad_(True)
+    w2 = (torch.randn(1, Q, generator=g) / math.sqrt(Q) * 3).to(dev).requires_grad_(True)
+    b2 = torch.randn(1, generator=g).to(dev).requires_grad_(True)
+    gout = torch.randn(U, D, generator=g).to(dev)
+    assert native.lib().head_g_supported(D, Q, T)
+    out = {}
+    for path in ("1", "0"):
+        os.environ["FEDREC_HEAD_G"] = path
+        try:
+            pooled, _ = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, None, nreal)
+            out[path] = torch.autograd.grad(pooled, (w1, b1, w2, b2), gout)
+        finally:
+            os.environ.pop("FEDREC_HEAD_G", None)
+    torch.cuda.synchronize()
+    for name, a, b in zip(("dW1", "db1", "dw2"), out["1"][:3], out["0"][:3]):
+        assert torch.isfinite(a).all(), name
+        assert _rel(a, b) < 1e-4, (name, _rel(a, b))
+    assert float((out["1"][3] - out["0"][3]).abs().max()) <= 1e-6 * float(out["0"][2].norm()) + 1e-7
