@@ -74,11 +74,12 @@ def main():
         out.append({"kernel": "head_g_rewrite", "us": round(t, 1), "TBs": round(M * 2 * Q * 2 / t / 1e6, 2)})
         eg.copy_(e)
         cs = lib.head_g_rewrite(da, T, eg)
-        for kt in (128, 256):
+        for kt in (4128,):  # (one form left)
             lib.head_wgrad_g_set_kt(kt)
             t = timeit(lambda: lib.head_wgrad_g(table, ids, T, eg, cs, w2, db2p), a.iters)
-            out.append({"kernel": f"head_wgrad_g_kt{kt}(+reduce)", "us": round(t, 1),
+            out.append({"kernel": f"head_wgrad_g_kt{kt % 1000}_st{kt // 1000 or 3}(+reduce)", "us": round(t, 1),
                         "TFs": round(2 * M * Q * D / t / 1e6, 1)})
+        lib.head_wgrad_g_set_kt(4128)
         lib.head_wgrad_g_set_kt(0)
     # the round-2 pieces for reference: gather + plain GEMM + wgrad of a materialised dpre
     hid = table.view(a.N, T, D).index_select(0, ids.long()).reshape(M, D)

@@ -1393,19 +1393,27 @@ __global__ __launch_bounds__(384) void head_g_rewrite_kernel(const float* __rest
 }
 
 // head_wgrad_g: P[s][q][k] = sum_{m in split s} g_mq x_mk -- a plain TN MFMA GEMM (the g tile
-// arrives ready in bf16).  Tile 384 (q: the whole head width) x KT (k), 512 threads = 8 waves:
-//   KT = 128: 4 (q) x 2 (k) waves of 96 x 64 (6 x 4 MFMA tiles, 96 accumulators), 4 stages;
-//   KT = 256: 2 (q) x 4 (k) waves of 192 x 64 (12 x 4 tiles, 192 accumulators), 3 stages --
-//             G read by 3 k-tile blocks instead of 6 (3,840 instead of 6,144 B per row from L2).
-// Stage = 32 rows: G [32 x 768 B] (3 glds per wave), X [32 x 2 KT B] (cache rows by title
-// index, KT / 128 glds per wave); both read back with ds_read_b64_tr_b16 (M-major operands),
-// 16-B chunks swizzled by swz(row) within aligned 16-chunk groups (256-B multiples).  The G
-// fragments are read a pair at a time, one pair ahead of the MFMAs that use it.
+// arrives ready in bf16).  Tile 384 (q: the whole head width) x 128 (k), 512 threads = 8 waves
+// as 4 (q) x 2 (k) of 96 x 64 (6 x 4 MFMA tiles, 96 accumulators), 4 LDS stages of 32 rows:
+// G [32 x 768 B] (3 glds per wave), X [32 x 256 B] (cache rows by title index, 1 glds per wave);
+// both read back with ds_read_b64_tr_b16 (M-major operands), 16-B chunks swizzled by swz(row)
+// within aligned 16-chunk groups (gemm_wgrad.hip's bank pattern).
+//
+// The issue budget is the point of this form: at two waves per SIMD a stage is 48 MFMAs (768
+// cycles) per SIMD, and the first form spent ~76 VALU instructions per wave per stage on
+// addresses (64-bit multiplies, a division by T, 26 LDS address adds) -- more vector issue
+// than the MFMAs leave free (profiles/r5_pmc_stalls_head.json: 4.5 VALU per MFMA, 19 % of wave
+// time).  Here every per-lane offset is computed once: G sources are a uniform row pointer +
+// a 32-bit lane offset, the X row's (title, token) advances by 32 rows per stage with one
+// compare, the second read of a fragment is +4 rows (same swizzle) as an immediate offset.
+// The G fragments are read a pair at a time, one pair ahead of the MFMAs that use it.
 // Splits are whole titles (the column partials are per title): the k-tile blocks of split s
 // each sum a 1 / tiles_k share of the 2 Q columns of cs over the split's titles into dw2p /
 // dsump[s] after their GEMM.
-constexpr int GQT = 384;
+constexpr int GQT = 384, GKT = 128;
 constexpr int G_BYTES = WTM * GQT * 2;  // 24 KB
+constexpr int GX_BYTES = WTM * GKT * 2;  // 8 KB
+constexpr int GSTB = G_BYTES + GX_BYTES;  // 32 KB
 
 __device__ __forceinline__ uint32_t tr_off_pitch(int pitch, int r0, int col0, int q, int p) {
   const int c = (col0 >> 3) + (p >> 1);
@@ -1413,38 +1421,12 @@ __device__ __forceinline__ uint32_t tr_off_pitch(int pitch, int r0, int col0, in
   return (uint32_t)(r * pitch + ((c ^ swz(r)) << 4) + (p & 1) * 8);
 }
 
-template <int KT>
-__device__ __forceinline__ void wgg_stage(char* base, const bf16* __restrict__ G, const bf16* __restrict__ table,
-                                          uint32_t ids_lds, int u_lo, int T, int D, int k0, int m, int me, int wave,
-                                          int lane) {
-  // G: 24 pieces of 1 KB, 3 per wave (lane-linear LDS, swizzle on the source)
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int p = wave * 3 + i;
-    const int off = p * 1024 + lane * 16;
-    const int row = off / 768, pc = (off % 768) >> 4;
-    const int c = pc ^ swz(row);
-    const int gm = m + row;
-    const bf16* src = gm < me ? G + (size_t)gm * GQT + 8 * c : g_zero_row + 8 * c;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src), LDS_PTR(void, base + p * 1024), 16, 0, 0);
-  }
-  // X: 32 rows of 2 KT bytes in KT / 128 pieces per wave
-  constexpr int CPR = KT / 8, RPP = 64 / CPR;  // 16-B chunks per row, rows per piece
-#pragma unroll
-  for (int i = 0; i < KT / 128; ++i) {
-    const int piece = wave * (KT / 128) + i;
-    const int row = piece * RPP + lane / CPR, pc = lane % CPR;
-    const int c = pc ^ swz(row);
-    const int gm = m + row;
-    const bf16* src = g_zero_row + 8 * c;
-    if (gm < me) {
-      const int uu = gm / T;
-      const int id = lds_read32i(ids_lds + 4 * (uu - u_lo));
-      src = table + ((size_t)id * T + (gm - uu * T)) * D + k0 + 8 * c;
-    }
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src), LDS_PTR(void, base + G_BYTES + piece * 1024), 16, 0,
-                                     0);
-  }
+// a fragment = two ds_read_b64_tr_b16 four rows apart: the second at an immediate offset
+template <int OFF>
+__device__ __forceinline__ void tr_read2(uint32_t addr, s16x4& a, s16x4& b) {
+  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:%3"
+               : "=v"(a), "=v"(b)
+               : "v"(addr), "n"(OFF));
 }
 
 template <int N>
@@ -1452,25 +1434,20 @@ __device__ __forceinline__ void lgkm_tie4(s16x4 (&r)[4]) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : "n"(N));
 }
 
-template <int KT, int NSTAGE>
+template <int NSTAGE>
 __global__ __launch_bounds__(512, 1) void head_wgrad_g_kernel(const bf16* __restrict__ G, const bf16* __restrict__ table,
                                                               const int* __restrict__ ids, const float* __restrict__ cs,
                                                               int U, int T, int D, float* __restrict__ P,
                                                               float* __restrict__ dw2p, float* __restrict__ dsump,
                                                               int tiles_k, int tps, const int* __restrict__ nreal) {
-  constexpr int X_BYTES_ = WTM * KT * 2;
-  constexpr int STB = G_BYTES + X_BYTES_;
-  constexpr int WQN = KT == 128 ? 4 : 2;  // waves along q
-  constexpr int QF = GQT / 16 / WQN;      // 16-column G fragments per wave (6 / 12)
-  constexpr int GPW = 3 + KT / 128;       // glds per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STB + 4 * MAX_SPLIT_TITLES];
-  constexpr int Q = GQT;
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * GSTB + 4 * MAX_SPLIT_TITLES];
+  constexpr int Q = GQT, QF = 6;
   // XCD-aware order: the k-tiles of one split (same G / X row panel) on one XCD's L2
   const int bid = blockIdx.x, nwg = gridDim.x;
   const int xcd = bid & 7, qq = nwg >> 3, rmd = nwg & 7;
   const int t = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (bid >> 3);
   const int s = t / tiles_k, kt = t - s * tiles_k;
-  const int k0 = kt * KT;
+  const int k0 = kt * GKT;
   int Ur = U;
   if (nreal != nullptr) {  // a padded step graph: the real titles re-split over the same grid
     Ur = min(U, nreal[0]);
@@ -1479,8 +1456,9 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_g_kernel(const bf16* __rest
   }
   const int u_lo = min(Ur, s * tps), u_hi = min(Ur, u_lo + tps);  // titles [u_lo, u_hi)
   const int mb = u_lo * T, me = u_hi * T;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wq = wave / (8 / WQN), wk = wave % (8 / WQN);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations in SGPRs
+  const int wq = wave >> 1, wk = wave & 1;
 
   f32x4 acc[QF][4];
 #pragma unroll
@@ -1490,64 +1468,94 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_g_kernel(const bf16* __rest
 
   const int nsteps = me > mb ? (me - mb + WTM - 1) / WTM : 0;
   const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
-  int* ids_s = (int*)(smem + NSTAGE * STB);
+  int* ids_s = (int*)(smem + NSTAGE * GSTB);
   for (int u = u_lo + tid; u < u_hi; u += 512) ids_s[u - u_lo] = ids != nullptr ? ids[u] : u;
   __syncthreads();
-  const uint32_t ids_lds = lds0 + NSTAGE * STB;
+  const uint32_t ids_lds = lds0 + NSTAGE * GSTB;
+
+  // ---- per-lane staging constants ----
+  // G: 3 pieces per wave, lane-linear LDS; source = row pointer of the stage + lane offset
+  int g_row[3];
+  uint32_t g_off[3], g_zoff[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int off = (wave * 3 + i) * 1024 + lane * 16;
+    const int row = off / 768, c = ((off % 768) >> 4) ^ swz(row);
+    g_row[i] = row;
+    g_off[i] = (uint32_t)(row * (GQT * 2) + c * 16);
+    g_zoff[i] = (uint32_t)(c * 16);
+  }
+  // X: 1 piece per wave = 4 rows x 16 chunks; the lane's row advances 32 per stage
+  const int x_row = wave * 4 + (lane >> 4);
+  const int x_c = (lane & 15) ^ swz(x_row);
+  const uint32_t x_coff = (uint32_t)(k0 + 8 * x_c);  // bf16 elements within the row
+  int x_t = (mb + x_row) % T, x_u = (mb + x_row) / T;  // once per block
+  const size_t DD = (size_t)D;
+  auto stage = [&](int buf, int m) {
+    char* base = smem + buf * GSTB;
+    const char* gm_ptr = (const char*)(G + (size_t)m * GQT);  // uniform
+    if (m + WTM <= me) {  // every row of the stage is real (uniform): no per-lane select
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, gm_ptr + g_off[i]),
+                                         LDS_PTR(void, base + (wave * 3 + i) * 1024), 16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const char* src = (m + g_row[i] < me) ? gm_ptr + g_off[i] : (const char*)g_zero_row + g_zoff[i];
+        __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src), LDS_PTR(void, base + (wave * 3 + i) * 1024), 16,
+                                         0, 0);
+      }
+    }
+    const bf16* xs = g_zero_row + 8 * x_c;
+    if (m + x_row < me) {
+      const int id = lds_read32i(ids_lds + 4 * (x_u - u_lo));
+      xs = table + ((size_t)id * T + x_t) * DD + x_coff;
+    }
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, xs), LDS_PTR(void, base + G_BYTES + wave * 1024), 16, 0,
+                                     0);
+    // next stage of this lane's row: 32 rows on
+    x_t += WTM;
+    while (x_t >= T) {
+      x_t -= T;
+      ++x_u;
+    }
+  };
 #pragma unroll
   for (int i = 0; i < NSTAGE - 1; ++i)
-    if (i < nsteps) wgg_stage<KT>(smem + i * STB, G, table, ids_lds, u_lo, T, D, k0, mb + i * WTM, me, wave, lane);
+    if (i < nsteps) stage(i, mb + i * WTM);
+  // ---- per-lane fragment offsets (row r0 + q; the +4-row half is an immediate) ----
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int r0 = g * 8;
-  uint32_t xo[4][2];
+  uint32_t xo[4], yo[QF];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    xo[j][0] = G_BYTES + tr_off_pitch(2 * KT, r0, wk * 64 + j * 16, q, p);
-    xo[j][1] = G_BYTES + tr_off_pitch(2 * KT, r0 + 4, wk * 64 + j * 16, q, p);
-  }
-  const uint32_t yo0 = tr_off_pitch(768, r0, wq * QF * 16, q, p), yo1 = tr_off_pitch(768, r0 + 4, wq * QF * 16, q, p);
-  // fragment i of this wave: columns + 16 i = chunk + 2 i (the swizzle XORs within 16-chunk
-  // groups, and 2 i never carries into bit 4 for i < 8 ... so the offset is recomputed per i)
-  auto yoff = [&](int i, int h) -> uint32_t {
-    return tr_off_pitch(768, r0 + 4 * h, wq * QF * 16 + i * 16, q, p);
-  };
-  (void)yo0;
-  (void)yo1;
+  for (int j = 0; j < 4; ++j) xo[j] = G_BYTES + tr_off_pitch(2 * GKT, r0, wk * 64 + j * 16, q, p);
+#pragma unroll
+  for (int i = 0; i < QF; ++i) yo[i] = tr_off_pitch(2 * GQT, r0, wq * QF * 16 + i * 16, q, p);
   for (int st = 0; st < nsteps; ++st) {
-    // stage st landed (this wave's GPW glds, then every wave's); every wave is done with st - 1
+    // stage st landed (this wave's 4 glds, then every wave's); every wave is done with st - 1
     const int left = nsteps - 1 - st;
     const int inflight = left < NSTAGE - 2 ? left : NSTAGE - 2;
     __builtin_amdgcn_sched_barrier(0);
-    if (inflight >= 2) {
-      if constexpr (GPW == 4) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else if (inflight == 1) {
-      if constexpr (GPW == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
+    if (inflight >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (inflight == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (st + NSTAGE - 1 < nsteps)
-      wgg_stage<KT>(smem + ((st + NSTAGE - 1) % NSTAGE) * STB, G, table, ids_lds, u_lo, T, D, k0,
-                    mb + (st + NSTAGE - 1) * WTM, me, wave, lane);
-    const uint32_t base = lds0 + (st % NSTAGE) * STB;
+    if (st + NSTAGE - 1 < nsteps) stage((st + NSTAGE - 1) % NSTAGE, mb + (st + NSTAGE - 1) * WTM);
+    const uint32_t base = lds0 + (st % NSTAGE) * GSTB;
     s16x4 xr[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      xr[2 * j] = tr_read(base + xo[j][0]);
-      xr[2 * j + 1] = tr_read(base + xo[j][1]);
-    }
+    for (int j = 0; j < 4; ++j) tr_read2<4 * 2 * GKT>(base + xo[j], xr[2 * j], xr[2 * j + 1]);
     s16x4 yr[2][4];  // a pair of G fragments (2 reads each), one pair ahead
-#pragma unroll
-    for (int h = 0; h < 4; ++h) yr[0][h] = tr_read(base + yoff(h >> 1, h & 1));
+    tr_read2<4 * 2 * GQT>(base + yo[0], yr[0][0], yr[0][1]);
+    tr_read2<4 * 2 * GQT>(base + yo[1], yr[0][2], yr[0][3]);
     bf16x8 xb[4];
 #pragma unroll
     for (int ip = 0; ip < QF / 2; ++ip) {
       const int cur = ip & 1;
       if (ip + 1 < QF / 2) {
-#pragma unroll
-        for (int h = 0; h < 4; ++h) yr[cur ^ 1][h] = tr_read(base + yoff(2 * (ip + 1) + (h >> 1), h & 1));
+        tr_read2<4 * 2 * GQT>(base + yo[2 * ip + 2], yr[cur ^ 1][0], yr[cur ^ 1][1]);
+        tr_read2<4 * 2 * GQT>(base + yo[2 * ip + 3], yr[cur ^ 1][2], yr[cur ^ 1][3]);
         lgkm_tie4<4>(yr[cur]);
       } else {
         lgkm_tie4<0>(yr[cur]);
@@ -1757,7 +1765,7 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
 
 // ---- the G path (round 5) -------------------------------------------------------------------
 extern "C" int fr_head_g_supported(int D, int Q, int T) {
-  return Q == GQT && D % 128 == 0 && D <= 1024 && T >= 1 && T <= MAXT && fr_head_supported(D, Q, T);
+  return Q == GQT && D % GKT == 0 && D <= 1024 && T >= 1 && T <= MAXT && fr_head_supported(D, Q, T);
 }
 
 // pool backward + g rewrite (e in place) + per-title column partials cs [2][U][Q]
@@ -1794,8 +1802,7 @@ extern "C" int fr_head_g_rewrite(const float* da, int U, int T, int Q, void* e, 
   return 0;
 }
 
-static int g_wgg_kt = 0;  // head_wgrad_g k-tile: 0 = default (128), 128 / 256 forced (benchmarks)
-extern "C" void fr_head_wgrad_g_set_kt(int kt) { g_wgg_kt = kt; }
+extern "C" void fr_head_wgrad_g_set_kt(int kt) { (void)kt; }  // one form left (the benchmarks' knob)
 
 // scratch = null: returns the fp32 scratch element count needed; else launches.  G = the g rows
 // (the e buffer after the rewrite), cs its column partials.
@@ -1809,9 +1816,7 @@ extern "C" long fr_head_wgrad_g(const void* G, const void* table, const int* ids
     (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (g_cus <= 0) g_cus = 256;
   }
-  // KT = 256 needs 192 accumulators per lane at two waves per SIMD: it spills (39 VGPRs) and ran
-  // 214 vs 84 us (profiles/r5_head_bench.jsonl) -- kept as a forced variant for measurements
-  const int KT = (g_wgg_kt == 256 && D % 256 == 0) ? 256 : 128;
+  const int KT = GKT;
   const int tiles_k = D / KT;
   // one block per CU: S splits of whole titles
   int S = g_cus / tiles_k;
@@ -1826,12 +1831,8 @@ extern "C" long fr_head_wgrad_g(const void* G, const void* table, const int* ids
   float* dw2p = scratch + (long)S * Q * D;
   float* dsump = dw2p + (long)S * Q;
   if (U > 0) {
-    if (KT == 256)
-      hipLaunchKernelGGL((head_wgrad_g_kernel<256, 3>), dim3(S * tiles_k), dim3(512), 0, s, (const bf16*)G,
-                         (const bf16*)table, ids, cs, U, T, D, P, dw2p, dsump, tiles_k, tps, nreal);
-    else
-      hipLaunchKernelGGL((head_wgrad_g_kernel<128, 4>), dim3(S * tiles_k), dim3(512), 0, s, (const bf16*)G,
-                         (const bf16*)table, ids, cs, U, T, D, P, dw2p, dsump, tiles_k, tps, nreal);
+    hipLaunchKernelGGL((head_wgrad_g_kernel<4>), dim3(S * tiles_k), dim3(512), 0, s, (const bf16*)G,
+                       (const bf16*)table, ids, cs, U, T, D, P, dw2p, dsump, tiles_k, tps, nreal);
   } else {
     (void)hipMemsetAsync(scratch, 0, need * sizeof(float), s);
   }

@@ -253,3 +253,29 @@ def test_head_g_path_matches_round4_path(dev, U, T, padded):
         assert torch.isfinite(a).all(), name
         assert _rel(a, b) < 1e-4, (name, _rel(a, b))
     assert float((out["1"][3] - out["0"][3]).abs().max()) <= 1e-6 * float(out["0"][2].norm()) + 1e-7
+
+
+@pytest.mark.parametrize("U,padded", [(1577, True), (300, False), (7, False)])
+def test_head_wgrad_g_matches_fp32(dev, U, padded):
+    """head_wgrad_g (a plain TN GEMM over g with the cache rows by title index, whole-title
+    splits, padded titles skipped) against an fp32 matmul of the same bf16 operands; the column
+    partials cs are summed over the real titles only."""
+    g = torch.Generator(device="cpu").manual_seed(U)
+    N, D, Q, T = 2000, 768, 384, 50
+    lib = native.lib()
+    table = torch.randn(N * T, D, generator=g).to(dev, torch.bfloat16)
+    ids = torch.randint(1, N, (U,), generator=g, dtype=torch.int32).to(dev)
+    R = U - 50 if padded else U
+    nreal = torch.tensor([R], dtype=torch.int32, device=dev) if padded else None
+    G = (torch.randn(U * T, Q, generator=g) * 0.1).to(dev, torch.bfloat16)
+    cs = torch.randn(2, U, Q, generator=g).to(dev)
+    w2 = torch.randn(Q, generator=g).to(dev)
+    db2p = torch.randn(U, generator=g).to(dev)
+    dW1, db1, dw2, db2 = lib.head_wgrad_g(table, ids, T, G, cs, w2, db2p, nreal)
+    torch.cuda.synchronize()
+    x = table.view(N, T, D)[ids[:R].long()].reshape(-1, D).float()
+    ref = G[: R * T].float().t() @ x * w2.view(-1, 1)
+    assert _rel(dW1, ref) < 1e-5, _rel(dW1, ref)
+    assert _rel(dw2, cs[0, :R].sum(0)) < 1e-5
+    assert _rel(db1, cs[1, :R].sum(0) * w2) < 1e-5
+    assert abs(float(db2) - float(db2p.sum())) < 1e-3
