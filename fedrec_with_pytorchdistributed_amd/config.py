@@ -82,10 +82,9 @@ class SecAggConfig:
     """Pairwise-mask secure aggregation (README.md:56,65 describes it; never implemented there)."""
 
     enabled: bool = False
-    frac_bits: int = 16  # fixed-point fraction bits for uint32 quantisation
-    clip_value: float = 1024.0  # |x| bound before quantisation (model parameters, star uploads)
-    # (secure GRADIENT averaging needs no setting: parallel.secagg.ExactMasker agrees on the bound
-    # per sum with a masked exponent histogram, so no coordinate is ever clamped)
+    # no grid settings: every secure sum agrees its fixed-point bound through a masked exponent
+    # histogram (gradients: parallel.secagg.ExactMasker; star uploads: StarSecureUpload, which
+    # quantises the weighted model delta), so no coordinate is ever clamped
 
 
 @dataclass

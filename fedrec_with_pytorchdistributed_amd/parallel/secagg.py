@@ -12,8 +12,11 @@ classic pairwise-masking protocol (Bonawitz et al. 2017, without dropout recover
    exactly, leaving ``sum_i Q(x_i)``; then dequantise and divide by ``W``.
 
 Gradient buckets (:class:`ExactMasker`) agree on the fixed-point bound per sum through a
-masked exponent histogram, so no value is ever clamped at any number of clients; model
-uploads of the star mode (:func:`mask_local`) use a fixed grid (``SecAggConfig``).
+masked exponent histogram, so no value is ever clamped at any number of clients.  The star
+mode's model uploads do the same through the store (:class:`StarSecureUpload`): each client
+uploads its weighted model DELTA ``(w_k / sum w) (theta_k - theta_global)`` on the grid the
+masked histogram agrees, and the coordinator's unmasked sum is the (weighted) FedAvg update to
+within ``W 2^(-f-1)`` per coordinate.
 
 Fixed-point arithmetic is what makes cancellation bit-exact.
 """
@@ -252,6 +255,75 @@ class ExactMasker:
             out.fill_(float("nan"))
         flat.copy_(out.to(flat.dtype).view_as(flat))
         self.hist = h
+
+
+def masked_hist_host(x: torch.Tensor, i: int, seeds_row: np.ndarray, round_idx: int) -> torch.Tensor:
+    """Client ``i``'s masked exponent histogram of ``x`` (:func:`hist_local` + the pairwise
+    masks of counter ``_HIST_ROUND | round_idx``), int32 [HIST_SLOTS] on the host."""
+    h = _add_masks(hist_local(x).astype(np.uint32), seeds_row, i, _HIST_ROUND | int(round_idx))
+    return torch.from_numpy(h.view(np.int32).copy())
+
+
+def sum_wrap(ts: List[torch.Tensor]) -> torch.Tensor:
+    """uint32 wrap-around sum of int32 tensors (the masks cancel in it), on the host."""
+    acc = ts[0].reshape(-1).numpy().astype(np.uint32).copy()
+    for t in ts[1:]:
+        acc += t.reshape(-1).numpy().astype(np.uint32)
+    return torch.from_numpy(acc.view(np.int32).copy()).view(ts[0].shape)
+
+
+class StarSecureUpload:
+    """The star (FedAvg) mode's exact secure upload, over the store control plane.
+
+    Round ``r``, client ``k`` with the round's global model ``theta_g`` and its trained
+    ``theta_k``:
+
+    1. weights: ``w_k`` (1, or the sample count under ``weighted_fedavg``) is published --
+       the coordinator already receives it in the round's metadata -- and every client reads
+       ``sum w``;
+    2. ``u_k = (w_k / sum w) (theta_k - theta_g)``: the weight is applied BEFORE quantising and
+       the delta (a few Adam steps) is what goes on the grid, not the parameters;
+    3. bound agreement: the masked exponent histogram of ``u_k`` goes to the store; every
+       client (and the coordinator) sums the W blobs, the masks cancel, and the largest
+       occupied slot gives ``m = 2^E >= max_k max|u_k|`` and ``f = 30 - ceil(log2 W) - E``;
+    4. payload: ``round(u_k 2^f)`` (nothing clamped: ``|u_k| <= m``) + pairwise masks.
+
+    The coordinator's wrap-around sum of the W payloads unmasks to ``sum_k u_k`` within
+    ``W 2^(-f-1)``; the new global model is ``theta_g + sum_k u_k`` = the (weighted) mean of
+    the ``theta_k``, as ``server.py:46-50`` computes it in the clear.  Disclosed beyond the
+    sum: the weights (already in the metadata) and how many clients have their largest
+    ``|u_k|`` in each power-of-two range (the summed histogram)."""
+
+    def __init__(self, cp, k: int, world: int, seeds_row: np.ndarray):
+        self.cp, self.k, self.W, self.row = cp, int(k), int(world), seeds_row
+
+    def upload(self, r: int, theta_k: torch.Tensor, theta_g: torch.Tensor, weight: float) -> dict:
+        cp, k, W = self.cp, self.k, self.W
+        cp.put_json(f"r{r}/w/{k}", {"w": float(weight)})
+        ws = [float(cp.get_json(f"r{r}/w/{j}")["w"]) for j in range(W)]
+        u = (theta_k.float() - theta_g.float()) * float(weight / sum(ws))
+        cp.put_tensor(f"r{r}/hist/{k}", masked_hist_host(u, k, self.row, r))
+        H = sum_wrap([cp.get_tensor(f"r{r}/hist/{j}") for j in range(W)])
+        f, bad = hist_frac_bits(H.numpy(), W)
+        occ = [s for s in range(2, HIST_SLOTS) if int(H[s]) != 0]
+        bound = 2.0 ** (max(occ) - 127) if occ else 1.0
+        if bad:  # a non-finite coordinate somewhere: upload zeros; the coordinator rejects the round
+            u = torch.zeros_like(u)
+        masked = mask_local(u, k, W, self.row, r, f, bound)
+        cp.put_tensor(f"r{r}/up/{k}", masked.cpu())
+        return {"frac_bits": f, "non_finite": bad, "sum_w": sum(ws)}
+
+
+def star_secure_aggregate(cp, r: int, world: int, ups: List[torch.Tensor], theta_g: torch.Tensor):
+    """Coordinator side of :class:`StarSecureUpload`: ``(new global, frac_bits)`` from the W
+    masked uploads of round ``r`` (None when a client reported a non-finite coordinate)."""
+    H = sum_wrap([cp.get_tensor(f"r{r}/hist/{j}") for j in range(world)])
+    f, bad = hist_frac_bits(H.numpy(), world)
+    if bad:
+        return None, f
+    tot = sum_wrap([u.cpu() for u in ups])
+    upd = tot.double() * (2.0 ** -f)
+    return (theta_g.double().cpu() + upd.view(theta_g.shape)).float(), f
 
 
 def unmask_sum(total: torch.Tensor, frac_bits: int = FRAC_BITS) -> torch.Tensor:

@@ -281,12 +281,13 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     full = cfg.sync == "full"
     writer = _metrics_writer(cfg, False)
     # secure aggregation: pairwise seeds by Diffie-Hellman over the control plane
-    seeds_row = None
+    seeds_row = secure = None
     if cfg.secagg.enabled:
         kp = secagg.KeyPair()
         cp.set(f"pk/{k}", secagg.public_bytes(kp))
         pubs = [cp.get(f"pk/{j}") for j in range(ctx.num_clients)]
         seeds_row = secagg.seeds_from_publics(kp, k, pubs)
+        secure = secagg.StarSecureUpload(cp, k, ctx.num_clients, seeds_row)
     r = int(cp.get("start").decode())  # the coordinator may be resuming at a later round
     # the client's own snapshot (client.py:125-127 auto-loads snapshot.pt): Adam moments + step,
     # RNG states and engine counters; the trainable parameters are overwritten by the round's
@@ -320,6 +321,7 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         before = _backbone_before(model, full)
         _receive_global(cp, r, model, ctx, full, bcast)
         _backbone_synced(model, full, before)
+        theta_g = model.flat.flat.detach().clone() if secure is not None else None  # the round's global model
         eng.ensure_cache()  # after the broadcast every client is here: the collective build point
         eng.sigma = _maybe_dp(cfg, eng)
         eng.epoch = 0
@@ -355,11 +357,10 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                 cp.put_tensor(f"r{r}/avg", up.cpu())
             cp.put_json(f"r{r}/meta/{k}", meta)
         else:
-            if cfg.secagg.enabled:
+            if secure is not None:
+                # exact: the weighted delta on the grid the masked exponent histogram agrees
                 w = float(len(shard.train)) if cfg.weighted_fedavg else 1.0
-                masked = secagg.mask_local(up * w, k, ctx.num_clients, seeds_row, r, cfg.secagg.frac_bits,
-                                           cfg.secagg.clip_value)
-                cp.put_tensor(f"r{r}/up/{k}", masked.cpu())
+                meta.update(secure.upload(r, up, theta_g, w))
             else:
                 cp.put_tensor(f"r{r}/up/{k}", up.cpu())
             cp.put_json(f"r{r}/meta/{k}", meta)
@@ -463,12 +464,12 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                 raise RuntimeError(f"round {r}: quorum not reached ({len(accepted)}/{W} < {need}); aborting")
             weights = [float(m["n_train"]) if cfg.weighted_fedavg else 1.0 for m in metas]
             if cfg.secagg.enabled:
-                tot = ups[0].clone()
-                for t in ups[1:]:
-                    tot = (tot.view(torch.int32).numpy().astype(np.uint32) +
-                           t.view(torch.int32).numpy().astype(np.uint32)).view(np.int32)
-                    tot = torch.from_numpy(tot.copy())
-                new = secagg.unmask_sum(tot, cfg.secagg.frac_bits) / sum(weights)
+                # the clients uploaded (w_k / sum w)(theta_k - theta_g) on the agreed grid: the
+                # unmasked sum IS the FedAvg update (secagg.StarSecureUpload)
+                new, fb = secagg.star_secure_aggregate(cp, r, W, ups, model.flat.flat.detach())
+                if new is None:
+                    obs.log(f"[server] round {r}: a client's update is non-finite; the global model is kept")
+                    new = model.flat.flat.detach().clone()
             else:
                 acc = torch.zeros_like(ups[0], dtype=torch.float64)
                 for t, w in zip(ups, weights):

@@ -206,26 +206,57 @@ def test_star_rejects_nan_upload(tmp_path):
     assert all(torch.isfinite(v).all() for v in g.values())
 
 
-@pytest.mark.slow
-def test_star_secure_aggregation(tmp_path):
-    server = ["server.py", "1", *TINY, "--secagg.enabled=1", f"--snapshot_path={tmp_path}/s.pt"]
-    client = ["client.py", "1", "16", "1", "0", "c", *TINY, "--secagg.enabled=1"]
-    outs = run_ranks([server, client, client], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump")})
+def _star_round0(tmp_path, tag, weighted, secure, W=4):
+    """One star round (1 coordinator + W clients, tiny shards); returns (global after round 0,
+    every client's final parameters, the round-0 global broadcast) -- clients train exactly one
+    round, so their dumped parameters are what they uploaded."""
+    d = tmp_path / tag
+    flags = [f"--weighted_fedavg={int(weighted)}", f"--secagg.enabled={int(secure)}"]
+    server = ["server.py", "1", *TINY, *flags, f"--snapshot_path={d}/s.pt"]
+    client = ["client.py", "1", "16", "1", "0", "c", *TINY, *flags]
+    outs = run_ranks([server] + [client] * W, {"FEDREC_DUMP_FLAT": str(d / "dump"), "FEDREC_STAR_AGG": "upload"},
+                     timeout=300)
     _ok(outs)
-    c1 = torch.load(tmp_path / "dump" / "rank1.pt")
-    c2 = torch.load(tmp_path / "dump" / "rank2.pt")
-    g = torch.load(tmp_path / "global_model_round0.pt", weights_only=True)
-    # rebuild the expected mean of the fixed-point uploads and compare one head tensor
+    g = torch.load(d / "global_model_round0.pt", weights_only=True)
+    cl = [torch.load(d / "dump" / f"rank{i}.pt") for i in range(1, W + 1)]
+    return g, cl, outs
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("weighted", [False, True])
+def test_star_secure_aggregation_is_the_plain_mean(tmp_path, weighted):
+    """Secure aggregation in the star mode (1 coordinator + 4 clients): the clients upload their
+    WEIGHTED model deltas on the fixed-point grid a masked exponent histogram agrees
+    (parallel.secagg.StarSecureUpload), so the coordinator's global model is the plain
+    (weighted) FedAvg mean of the client models -- server.py:46-50 -- to fp32 rounding; nothing
+    is clamped.  The same round without secure aggregation gives the same global model, and the
+    weighted mean differs from the unweighted one (the shards differ in size)."""
     from fedrec_with_pytorchdistributed_amd.config import BackboneConfig, FedRecConfig
+    from fedrec_with_pytorchdistributed_amd.data.synthetic import SynthSpec, SyntheticCorpus
     from fedrec_with_pytorchdistributed_amd.models.fedrec_model import FedRecModel
+
+    gs, cs, _ = _star_round0(tmp_path, "secure", weighted, True)
+    gp, cp_, _ = _star_round0(tmp_path, "plain", weighted, False)
+    W = len(cs)
+    corpus = SyntheticCorpus(SynthSpec.preset("tiny"))
+    n = [len(corpus.client_shard(k, W).train) for k in range(W)]
+    w = torch.tensor([float(x) if weighted else 1.0 for x in n], dtype=torch.float64)
     cfg = FedRecConfig()
     cfg.backbone = BackboneConfig.preset("tiny")
-    m = FedRecModel(cfg)
-    fl = m.build_flat()
-    q = lambda t: torch.round(t.clamp(-1024, 1024) * 65536)
-    mean = (q(c1) + q(c2)) / 65536 / 2
-    name, p, off = [v for v in fl.views() if v[0] == "text_encoder.fc.weight"][0]
-    assert torch.allclose(g[name].reshape(-1), mean[off:off + p.numel()], atol=1e-6)
+    fl = FedRecModel(cfg).build_flat()
+    for name, p, off in fl.views():
+        sl = slice(off, off + p.numel())
+        mean = sum(wk * c[sl].double() for wk, c in zip(w, cs)) / w.sum()
+        assert torch.allclose(gs[name].reshape(-1).double(), mean, atol=2e-6, rtol=0), name
+        mean_p = sum(wk * c[sl].double() for wk, c in zip(w, cp_)) / w.sum()
+        assert torch.allclose(gp[name].reshape(-1).double(), mean_p, atol=2e-6, rtol=0), name
+    # the two runs trained the same clients from the same start: same uploads, same global model
+    for a, b in zip(cs, cp_):
+        assert torch.equal(a, b)
+    for k in gs:
+        assert torch.allclose(gs[k], gp[k], atol=2e-6, rtol=0), k
+    if weighted:
+        assert len(set(n)) > 1
 
 
 @pytest.mark.slow
