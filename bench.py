@@ -305,6 +305,7 @@ def main() -> int:
     rnd = None
     auc = None
     if do_round:
+        eng.prepare_validation(256)  # the validation split's device arrays: setup, like the cache
         eng.sync_params()
         sync()
         if ctx.initialized:

@@ -131,7 +131,7 @@ class FedRecConfig:
     adam_eps: float = 1e-8
     batch_size: int = 16
     total_epochs: int = 1
-    save_every: int = 1
+    save_every: int = 1  # GA / PA snapshots every N epochs; star-mode CLIENT snapshots are written every round
     global_rounds: int = 1
 
     # --- federation ------------------------------------------------------------------

@@ -103,7 +103,15 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, f
                                                        bf16x4* __restrict__ plow, long n4, float lr, float b1, float b2,
                                                        float eps, float gs, const long long* __restrict__ step,
                                                        const float* __restrict__ loss, float* __restrict__ ring,
-                                                       int ring_n, const AdamSegs segs) {
+                                                       int ring_n, const AdamSegs segs,
+                                                       const int* __restrict__ skip) {
+  // skip (optional): the gradient all-reduce's status word (the IPC all-reduce sets it when a
+  // peer timed out and poisons that call's output) -- then no update at all, and the step's loss
+  // slot gets NaN, so the epoch's loss reads back non-finite and the engine's check raises
+  if (skip != nullptr && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ring != nullptr) ring[(step[0] - 1) % ring_n] = __builtin_nanf("");
+    return;
+  }
   // t = the device step count, already advanced for this step by the step's cast launch (an
   // earlier kernel of the same stream): no read-modify-write here (a same-address ticket per
   // block made this launch 20 us, against 7 for the eager kernel)
@@ -158,7 +166,7 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float4* __restrict__ p, f
 extern "C" int fr_adam_dev(float* p, float* g, float* m, float* v, void* plow, long n, float lr, float b1,
                            float b2, float eps, float grad_scale, const long long* step, const float* loss, float* ring,
                            int ring_n, hipStream_t s, int nseg, const float* const* gsrc, const long* goff,
-                           const long* gn) {
+                           const long* gn, const int* skip) {
   if (n % 4 != 0 || (ring != nullptr && (loss == nullptr || ring_n < 1))) return 1;
   if (nseg < 0 || nseg > ADAM_SEG) return 2;
   AdamSegs segs{};
@@ -174,7 +182,7 @@ extern "C" int fr_adam_dev(float* p, float* g, float* m, float* v, void* plow, l
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (float4*)p, (float4*)g, (float4*)m,
-                     (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, grad_scale, step, loss, ring, ring_n, segs);
+                     (float4*)v, (bf16x4*)plow, n4, lr, b1, b2, eps, grad_scale, step, loss, ring, ring_n, segs, skip);
   return 0;
 }
 // ---------------------------------------------------------------------------------------

@@ -83,11 +83,14 @@ int fr_user_pool_score(const float* x, const float* e, const float* w2, const fl
                        float* scores, float* dcand, float* loss_total, float* dctx, float* dpre, void* dpre_b,
                        float* da8, hipStream_t s);
 void fr_head_score_set_rows(int r);
+int fr_segment_sum_rows_ldp(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U,
+                            int D, int R, float* scratch, float clip, float noise_std, unsigned long long seed,
+                            unsigned long long offset, const unsigned long long* dev_off, hipStream_t s);
 int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std, unsigned long long seed,
                 unsigned long long offset, hipStream_t s, const unsigned long long* dev_off);
 int fr_adam_dev(float* p, float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2, float eps,
                 float grad_scale, const long long* step, const float* loss, float* ring, int ring_n, hipStream_t s,
-                int nseg, const float* const* gsrc, const long* goff, const long* gn);
+                int nseg, const float* const* gsrc, const long* goff, const long* gn, const int* skip);
 int fr_adam_flat(float* p, const float* g, float* m, float* v, void* plow, long n, float lr, float b1, float b2,
                  float eps, float bc1, float bc2, float grad_scale, hipStream_t s);
 int fr_sample_batch(const int* rows, const int* pos, const long long* neg_ptr, const int* negs, const long long* his_ptr,
@@ -464,6 +467,17 @@ void ipc_open(int64_t id, const at::Tensor& handles, int64_t me, int64_t W, cons
 }
 
 int64_t ipc_region(int64_t id) { return (int64_t)fr_ipc_region((int)id); }
+
+// the context's status word as a device tensor view (no ownership; valid until ipc_destroy):
+// the in-graph Adam reads it to skip the update of a step whose all-reduce timed out
+at::Tensor ipc_status_word(int64_t id) {
+  int* st = fr_ipc_status((int)id);
+  TORCH_CHECK(st != nullptr, "fedrec::ipc_status_word: bad id");
+  int dev = 0;
+  TORCH_CHECK(hipPointerGetAttribute(&dev, HIP_POINTER_ATTRIBUTE_DEVICE_ORDINAL, (hipDeviceptr_t)st) == hipSuccess,
+              "fedrec::ipc_status_word: pointer attribute");
+  return at::from_blob(st, {1}, at::TensorOptions().dtype(at::kInt).device(at::Device(at::kCUDA, dev)));
+}
 
 int64_t ipc_status(int64_t id) {  // device -> host read (tests / diagnostics only)
   int* st = fr_ipc_status((int)id);
@@ -949,18 +963,6 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
   // kernel writes them itself (no separate fill launch), the block-per-row form clears first
   auto out = at::empty({num_out, D}, rows.options());
   at::Tensor src = rows;
-  if (clip > 0.0 || noise_std > 0.0) {  // LDP: clip + noise every occurrence first (parallel pass)
-    src = at::empty_like(rows);
-    const unsigned long long* dop = nullptr;
-    if (dev_off.has_value() && dev_off->defined()) {  // device step counter (graph replays: fresh noise)
-      check_dev(*dev_off, "dev_off");
-      TORCH_CHECK(dev_off->scalar_type() == at::kLong && dev_off->numel() == 1, "fedrec::segment_sum_rows: dev_off int64[1]");
-      dop = (const unsigned long long*)dev_off->data_ptr();
-    }
-    check_rc(fr_ldp_rows(rows.data_ptr<float>(), src.data_ptr<float>(), (int)(rows.numel() / D), (int)D, (float)clip,
-                         (float)noise_std, (unsigned long long)seed, (unsigned long long)offset, cur_stream(), dop),
-             "ldp_rows");
-  }
   const int64_t R = perm.numel();
   auto scratch = at::empty({(int64_t)fr_segsum_chunks((int)R) * 2 * D}, rows.options());
   const int* invp = nullptr;
@@ -968,6 +970,25 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
     check_dev(*inv, "inv");
     TORCH_CHECK(inv->scalar_type() == at::kInt && inv->numel() == R, "fedrec::segment_sum_rows: inv int32[R]");
     invp = inv->data_ptr<int>();
+  }
+  if (clip > 0.0 || noise_std > 0.0) {  // LDP: clip + noise every occurrence
+    const unsigned long long* dop = nullptr;
+    if (dev_off.has_value() && dev_off->defined()) {  // device step counter (graph replays: fresh noise)
+      check_dev(*dev_off, "dev_off");
+      TORCH_CHECK(dev_off->scalar_type() == at::kLong && dev_off->numel() == 1, "fedrec::segment_sum_rows: dev_off int64[1]");
+      dop = (const unsigned long long*)dev_off->data_ptr();
+    }
+    TORCH_CHECK(rows.numel() / D == R, "fedrec::segment_sum_rows: rows / perm sizes");
+    // fused into the chunk pass when the layout allows (K16 + K17 in one launch)
+    if (fr_segment_sum_rows_ldp(rows.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(), invp,
+                                out.data_ptr<float>(), (int)num_out, (int)D, (int)R, scratch.data_ptr<float>(),
+                                (float)clip, (float)noise_std, (unsigned long long)seed, (unsigned long long)offset, dop,
+                                cur_stream()) == 0)
+      return out;
+    src = at::empty_like(rows);  // the parallel clip + noise pass first, then the plain sum
+    check_rc(fr_ldp_rows(rows.data_ptr<float>(), src.data_ptr<float>(), (int)(rows.numel() / D), (int)D, (float)clip,
+                         (float)noise_std, (unsigned long long)seed, (unsigned long long)offset, cur_stream(), dop),
+             "ldp_rows");
   }
   check_rc(fr_segment_sum_rows(src.data_ptr<float>(), perm.data_ptr<int>(), seg_ptr.data_ptr<int>(), invp,
                                out.data_ptr<float>(), (int)num_out, (int)D, (int)R, scratch.data_ptr<float>(),
@@ -983,8 +1004,15 @@ at::Tensor segment_sum_rows(const at::Tensor& rows, const at::Tensor& perm, cons
 void adam_dev(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const at::Tensor& step,
               const at::Tensor& loss, at::Tensor ring, double lr, double b1, double b2, double eps, double grad_scale,
               const c10::optional<std::vector<c10::optional<at::Tensor>>>& gsrc,
-              const c10::optional<std::vector<int64_t>>& goff) {
+              const c10::optional<std::vector<int64_t>>& goff, const c10::optional<at::Tensor>& skip) {
   for (auto* t : {&p, &m, &v}) check_dev(*t, "adam_dev buffer");
+  const int* skp = nullptr;
+  if (skip.has_value() && skip->defined()) {  // the gradient all-reduce's status word (int32 [1])
+    check_dev(*skip, "skip");
+    TORCH_CHECK(skip->scalar_type() == at::kInt && skip->numel() == 1 && skip->device() == p.device(),
+                "fedrec::adam_dev: skip int32 [1] on p's device");
+    skp = skip->data_ptr<int>();
+  }
   check_dev(g, "g");
   check_dev(step, "step");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
@@ -1021,7 +1049,7 @@ void adam_dev(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const at::
                        (long)p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale,
                        (const long long*)step.data_ptr<int64_t>(), has_ring ? loss.data_ptr<float>() : nullptr,
                        has_ring ? ring.data_ptr<float>() : nullptr, (int)ring.numel(), cur_stream(), (int)sp.size(),
-                       sp.data(), so.data(), sn.data()),
+                       sp.data(), so.data(), sn.data(), skp),
            "adam_dev");
 }
 
@@ -1046,13 +1074,18 @@ void adam_flat(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, co
            "adam_flat");
 }
 
+// the dedup's one-kernel-chain path covers up to this many ids; past it the sort path queues
+// work after its unique-count read (the engine then waits on an event: dedup_sync_max())
+constexpr int64_t kDedupKernelMax = 8192;
+int64_t dedup_sync_max() { return kDedupKernelMax; }
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dedup(const at::Tensor& ids, int64_t num_news) {
   check_dev(ids, "ids");
   TORCH_CHECK(ids.scalar_type() == at::kInt && ids.dim() == 1, "fedrec::dedup: int32 [R]");
   const c10::DeviceGuard g(ids.device());
   const int64_t R = ids.numel();
   auto opt = ids.options();
-  if (R == 0 || R > 8192) {  // large batches: sort-based path (still on the device)
+  if (R == 0 || R > kDedupKernelMax) {  // large batches: sort-based path (still on the device)
     auto sorted = at::sort(ids.to(at::kLong), /*stable=*/true, 0, false);
     auto sid = std::get<0>(sorted);
     auto perm = std::get<1>(sorted).to(at::kInt);
@@ -1791,6 +1824,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("embed_ln(Tensor tokens, Tensor word, Tensor pos, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("title_attention(Tensor qkv, Tensor mask, int n_heads) -> Tensor");
   m.def("head_supported(int D, int Q, int T) -> bool", &head_supported);
+  m.def("dedup_sync_max() -> int", &dedup_sync_max);
   m.def("head_g_supported(int D, int Q, int T) -> bool", &head_g_supported);
   m.def("head_wgrad_g_set_kt(int kt) -> ()", &head_wgrad_g_set_kt);
   m.def("head_g_rewrite(Tensor da, int T, Tensor(a!) e, Tensor? nreal=None) -> Tensor");
@@ -1800,6 +1834,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("ipc_open(int id, Tensor handles, int me, int W, Tensor? local_ptrs) -> ()", &ipc_open);
   m.def("ipc_region(int id) -> int", &ipc_region);
   m.def("ipc_status(int id) -> int", &ipc_status);
+  m.def("ipc_status_word(int id) -> Tensor", &ipc_status_word);
   m.def("ipc_destroy(int id) -> ()", &ipc_destroy);
   m.def("ipc_allreduce_(int id, Tensor(a!) x, int epoch, int mode, int blocks, float timeout_s=60.) -> ()");
   m.def("ipc_allreduce_local_(int[] ids, Tensor(a!)[] xs, int epoch, int mode, int blocks, float timeout_s=60.) -> ()");
@@ -1814,7 +1849,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None, bool bf16_out=False) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act, Tensor? ci=None, Tensor(a!)? dcand_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
-  m.def("adam_dev(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale, Tensor?[]? gsrc=None, int[]? goff=None) -> ()");
+  m.def("adam_dev(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor loss, Tensor(f!) ring, float lr, float b1, float b2, float eps, float grad_scale, Tensor?[]? gsrc=None, int[]? goff=None, Tensor? skip=None) -> ()");
   m.def("adam_flat(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? p_lowp, float lr, float b1, float b2, float eps, float bc1, float bc2, float grad_scale) -> ()");
   m.def("dedup(Tensor ids, int num_news) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_batch(Tensor rows, Tensor pos, Tensor neg_ptr, Tensor negs, Tensor his_ptr, Tensor his, int npratio, int H, bool truncate, int seed, int offset, bool valid=False) -> (Tensor, Tensor)");

@@ -8,6 +8,13 @@
 
 Incremental: objects are rebuilt only when a source or ``common.h`` is newer.
 Usage: ``python -m fedrec_with_pytorchdistributed_amd.csrc.build [--force] [--verbose]``.
+
+``--sanitize`` builds ``_C_san.so`` instead: the HOST code of every file
+(binding.cpp's argument checks and op glue, the IPC context table and handle plumbing of
+ipc_allreduce.hip, every launcher) under AddressSanitizer + UndefinedBehaviorSanitizer, with
+clang for every object so one sanitizer runtime serves them all (device code is not
+instrumented: ``-Xarch_host``).  It is never loaded by default; ``tests/test_sanitize_host.py``
+loads it in a child process with the ASan runtime preloaded and drives the validation paths.
 """
 from __future__ import annotations
 
@@ -61,25 +68,49 @@ def _run(cmd, verbose: bool):
     return r
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> Path:
-    BUILD.mkdir(exist_ok=True)
+SAN = ["-fsanitize=address", "-fsanitize=undefined"]
+# binding.cpp only: no global-variable instrumentation -- its string literals were registered
+# twice at load (a false odr-violation report that ASAN_OPTIONS could not silence); heap, stack
+# and UB checks stay on (the .hip host objects keep the full instrumentation)
+SAN_CC = ["-mllvm", "-asan-globals=0"]
+OUT_SAN = PKG / "_C_san.so"
+
+
+def _clangxx() -> str:
+    return str(Path(_rocm()) / "lib/llvm/bin/clang++")
+
+
+def asan_runtime() -> str:
+    """The clang ASan runtime the sanitized build links against (LD_PRELOAD it)."""
+    return subprocess.run([_clangxx(), "-print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True,
+                          text=True).stdout.strip()
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int = 8, sanitize: bool = False) -> Path:
+    bdir = BUILD / "san" if sanitize else BUILD
+    out = OUT_SAN if sanitize else OUT
+    bdir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     tinc, tlib, abi = _torch_paths()
     common = [HERE / "common.h"]
     kernels = sorted(HERE.glob("*.hip"))
     jobs_list = []
     objs = []
+    # host-only sanitizers: each -fsanitize= right after -Xarch_host (device code uninstrumented)
+    hsan = [a for f in SAN for a in ("-Xarch_host", f)] + ["-Xarch_host", "-fno-omit-frame-pointer"] if sanitize else []
     for src in kernels:
-        obj = BUILD / (src.stem + ".o")
+        obj = bdir / (src.stem + ".o")
         objs.append(obj)
         if force or _newer(obj, [src, *common]):
-            jobs_list.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
-                              "-c", str(src), "-o", str(obj)])
+            jobs_list.append([hipcc, f"--offload-arch={ARCH}", "-O3" if not sanitize else "-O1", "-fPIC", "-std=c++17",
+                              "-munsafe-fp-atomics", *hsan, "-c", str(src), "-o", str(obj)])
     bsrc = HERE / "binding.cpp"
-    bobj = BUILD / "binding.o"
+    bobj = bdir / "binding.o"
     objs.append(bobj)
     if force or _newer(bobj, [bsrc]):
-        jobs_list.append(["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+        cxx, extra = ("g++", ["-O2"]) if not sanitize else (_clangxx(), ["-O1", *SAN, *SAN_CC,
+                                                                          "-fno-omit-frame-pointer"])
+        jobs_list.append([cxx, *extra, "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
                           f"-I{_rocm()}/include",
                           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{tinc}", f"-I{tinc / 'torch/csrc/api/include'}",
                           f"-I{sysconfig.get_paths()['include']}", "-c", str(bsrc), "-o", str(bobj)])
@@ -87,12 +118,13 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> Path:
         with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(jobs_list)))) as ex:
             for f in [ex.submit(_run, c, verbose) for c in jobs_list]:
                 f.result()
-    if force or jobs_list or _newer(OUT, objs):
-        tmp = OUT.with_suffix(".so.tmp")
-        _run(["g++", "-shared", "-o", str(tmp), *map(str, objs), f"-L{tlib}", "-lamdhip64", "-lc10", "-lc10_hip",
-              "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{tlib}"], verbose)
-        os.replace(tmp, OUT)
-    return OUT
+    if force or jobs_list or _newer(out, objs):
+        tmp = out.with_suffix(".so.tmp")
+        link = ["g++", "-shared"] if not sanitize else [_clangxx(), "-shared", *SAN, "-shared-libsan"]
+        _run([*link, "-o", str(tmp), *map(str, objs), f"-L{tlib}", "-lamdhip64", "-lc10", "-lc10_hip", "-ltorch_cpu",
+              "-ltorch_hip", f"-Wl,-rpath,{tlib}"], verbose)
+        os.replace(tmp, out)
+    return out
 
 
 def main(argv=None) -> int:
@@ -100,8 +132,9 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--sanitize", action="store_true", help="host ASan + UBSan build -> _C_san.so")
     a = ap.parse_args(argv)
-    p = build(a.force, a.verbose, a.j)
+    p = build(a.force, a.verbose, a.j, a.sanitize)
     print(p)
     return 0
 

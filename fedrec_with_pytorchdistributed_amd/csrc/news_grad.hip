@@ -11,8 +11,9 @@
 // LDP: per-occurrence L2 clip to C (clip > 0), then Gaussian noise N(0, std) with
 // std = sigma * C (default) or sigma (reference quirk Q10: no clip, std = sigma).  Noise
 // comes from Philox-4x32-10 keyed by (seed, offset=step) with a counter derived from the
-// occurrence row, so it does not depend on which wave processes it.  Two passes: the
-// per-occurrence clip+noise pass is embarrassingly parallel; the segment sum is skewed.
+// occurrence row, so it does not depend on which wave processes it.  The default float4 chunk
+// pass applies the clip + noise as it loads each occurrence row (one launch + the edge fix-up);
+// the separate per-occurrence pass (ldp_rows_kernel) remains for the other forms.
 #include "common.h"
 
 #include <algorithm>
@@ -224,13 +225,22 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(const int* __restrict__
 // float4 form of the chunked pass (D % 4 == 0, 16-B aligned rows; variant 2): a lane holds
 // columns 4 lane + 256 k (two float4 at D = 400) -- 2 loads per row instead of 7 scalar ones.
 // Same chunk grid and scratch slots as segsum_chunk_kernel (segsum_fix_kernel finishes both).
+//
+// LDP = true (K16 fused into K17): every occurrence row is clipped to L2 norm C and
+// gets N(0, std) noise as it is loaded -- no separate clip + noise pass over the rows and no
+// second copy of them.  Noise of elements 4L .. 4L+3 of occurrence row r comes from Philox
+// counter (r << 16) | L (4 uniforms -> 4 normals), keyed by (seed, offset + *dev_off): a pure
+// function of the occurrence, whatever chunk / wave sums it.
 constexpr int MAXV4 = 2;  // D <= 512
-template <int SC>
+template <int SC, bool LDP = false>
 __global__ __launch_bounds__(256) void segsum_chunk4_kernel(const float4* __restrict__ rows,
                                                             const int* __restrict__ perm,
                                                             const int* __restrict__ seg_ptr,
                                                             const int* __restrict__ inv, float4* __restrict__ out,
-                                                            float4* __restrict__ scratch, int U, int R, int D4) {
+                                                            float4* __restrict__ scratch, int U, int R, int D4,
+                                                            float clip = 0.f, float noise_std = 0.f,
+                                                            unsigned long long seed = 0, unsigned long long offset = 0,
+                                                            const unsigned long long* __restrict__ dev_off = nullptr) {
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int p0 = c * SC;
@@ -249,6 +259,32 @@ __global__ __launch_bounds__(256) void segsum_chunk4_kernel(const float4* __rest
       const int d = lane + 64 * k;
       v[j][k] = d < D4 ? rows[(size_t)rr[j] * D4 + d] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  if constexpr (LDP) {
+    const unsigned long long off = offset + (dev_off != nullptr ? *dev_off : 0ull);
+#pragma unroll
+    for (int j = 0; j < SC; ++j) {
+      float f = 1.0f;
+      if (clip > 0.f) {
+        float sq = 0.f;
+#pragma unroll
+        for (int k = 0; k < MAXV4; ++k)
+          sq += v[j][k].x * v[j][k].x + v[j][k].y * v[j][k].y + v[j][k].z * v[j][k].z + v[j][k].w * v[j][k].w;
+        f = fminf(1.0f, clip / (sqrtf(wave_sum(sq)) + 1e-12f));
+      }
+#pragma unroll
+      for (int k = 0; k < MAXV4; ++k) {
+        const int d = lane + 64 * k;
+        float4 nz = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (noise_std > 0.f && d < D4) {
+          const uint4 rnd = Philox::gen(seed, off, ((unsigned long long)rr[j] << 16) | (unsigned)d);
+          const float2 a = box_muller(rnd.x, rnd.y), b = box_muller(rnd.z, rnd.w);
+          nz = make_float4(a.x, a.y, b.x, b.y);
+        }
+        v[j][k] = make_float4(v[j][k].x * f + noise_std * nz.x, v[j][k].y * f + noise_std * nz.y,
+                              v[j][k].z * f + noise_std * nz.z, v[j][k].w * f + noise_std * nz.w);
+      }
+    }
+  }
   float4 acc[MAXV4];
 #pragma unroll
   for (int k = 0; k < MAXV4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -301,6 +337,23 @@ extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float cl
 // scratch: fr_segsum_chunks(R) * 2 * D floats (chunked form); R = total occurrences = seg_ptr[U]
 // Rows of empty segments: the chunked form writes them as zeros (its fix pass); the
 // block-per-row form needs zero_empty = 1 to clear the output first.
+// clip + noise fused into the float4 chunk pass (one launch fewer, no clipped copy of the rows);
+// returns 1 when the shape / alignment does not take the fused form (the caller runs the two passes)
+extern "C" int fr_segment_sum_rows_ldp(const float* rows, const int* perm, const int* seg_ptr, const int* inv,
+                                       float* out, int U, int D, int R, float* scratch, float clip, float noise_std,
+                                       unsigned long long seed, unsigned long long offset,
+                                       const unsigned long long* dev_off, hipStream_t s) {
+  if (U == 0) return 0;
+  if (g_segsum_variant != 2 || scratch == nullptr || inv == nullptr || R <= 0 || D % 4 != 0 || D > 256 * MAXV4 ||
+      (((uintptr_t)rows | (uintptr_t)out | (uintptr_t)scratch) & 15) != 0 || (D / 4) > 65535)
+    return 1;
+  const int nch = (R + SCH - 1) / SCH;
+  hipLaunchKernelGGL((segsum_chunk4_kernel<SCH, true>), dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows, perm,
+                     seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4, clip, noise_std, seed, offset, dev_off);
+  hipLaunchKernelGGL(segsum_fix_kernel<SCH>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
+  return 0;
+}
+
 extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out,
                                    int U, int D, int R, float* scratch, hipStream_t s, int zero_empty) {
   if (D > 64 * MAXV) return 1;
@@ -308,8 +361,9 @@ extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int
   if (g_segsum_variant == 2 && scratch != nullptr && inv != nullptr && R > 0 && D % 4 == 0 && D <= 256 * MAXV4 &&
       (((uintptr_t)rows | (uintptr_t)out | (uintptr_t)scratch) & 15) == 0) {
     const int nch = (R + SCH - 1) / SCH;
-    hipLaunchKernelGGL(segsum_chunk4_kernel<SCH>, dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows, perm,
-                       seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4);
+    hipLaunchKernelGGL((segsum_chunk4_kernel<SCH, false>), dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows,
+                       perm, seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4, 0.f, 0.f, 0ull, 0ull,
+                       (const unsigned long long*)nullptr);
     hipLaunchKernelGGL(segsum_fix_kernel<SCH>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
     return 0;
   }

@@ -306,6 +306,27 @@ __device__ unsigned g_score_cnt[1];  // zero-initialised; every launch leaves it
 
 int g_score_variant = 1;  // 1: block per impression (default), 0: wave per impression
 
+// The last-arriver tickets above are process-wide __device__ symbols: their address is per
+// DEVICE, so it is looked up for the launch's current device (a process that launches on two
+// devices gets each one's own counter).  Launches that share one device's counter must not
+// overlap (two streams of one device): each launch re-arms it to zero only when its last block
+// arrives, so interleaved tickets would hand the sum to the wrong block.  The engine issues
+// these launches on one stream per device.
+constexpr int MAXDEV = 64;
+unsigned* ticket_addr(const void* sym, unsigned* (&cache)[MAXDEV]) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= MAXDEV) dev = 0;
+  if (cache[dev] == nullptr) {
+    unsigned* p = nullptr;
+    (void)hipGetSymbolAddress((void**)&p, sym);
+    cache[dev] = p;
+  }
+  return cache[dev];
+}
+unsigned* g_score_cnt_addr[MAXDEV] = {};
+unsigned* g_ups_cnt_addr[MAXDEV] = {};
+
 }  // namespace
 
 extern "C" void fr_score_set_variant(int v) { g_score_variant = v; }
@@ -318,11 +339,7 @@ extern "C" int fr_score_ce(const float* cand, const float* user, float* loss, fl
   if (C > MAXC) return 1;
   if (B == 0) return 0;
   if (ci != nullptr || (g_score_variant == 1 && C <= MAXC)) {
-    static unsigned* cnt = [] {
-      unsigned* p = nullptr;
-      (void)hipGetSymbolAddress((void**)&p, HIP_SYMBOL(g_score_cnt));
-      return p;
-    }();
+    unsigned* cnt = ticket_addr(HIP_SYMBOL(g_score_cnt), g_score_cnt_addr);
     hipLaunchKernelGGL(score_ce_block_kernel, dim3(B), dim3(64 * C), 0, s, cand, user, loss, scores, dcand, duser, B,
                        C, D, sigm, ci, loss_total, loss_total != nullptr ? cnt : nullptr);
     return 0;
@@ -345,11 +362,7 @@ extern "C" int fr_user_pool_score(const float* x, const float* e, const float* w
        (uintptr_t)(da8 ? da8 : x)) & 15 || (dpre_b != nullptr && ((uintptr_t)dpre_b & 7)))
     return 1;
   if (B == 0) return 0;
-  static unsigned* cnt = [] {
-    unsigned* p = nullptr;
-    (void)hipGetSymbolAddress((void**)&p, HIP_SYMBOL(g_ups_cnt));
-    return p;
-  }();
+  unsigned* cnt = ticket_addr(HIP_SYMBOL(g_ups_cnt), g_ups_cnt_addr);
   hipLaunchKernelGGL(user_pool_score_kernel<16>, dim3(B), dim3(1024), 0, s, x, e, w2, b2, keep, cand, ci, B, T, D, Q,
                      C, sigm, lossb, scores, dcand, loss_total, cnt, dctx, dpre, (bf16*)dpre_b, da8);
   return 0;

@@ -79,6 +79,14 @@ class IpcAllReduce:
         device (synchronises with it)."""
         return int(self.lib.ipc_status(self.id))
 
+    def status_word(self) -> torch.Tensor:
+        """The status word as a device int32 [1] view (nonzero after a peer timeout): the
+        in-graph Adam skips its update on it (a view of the context's allocation, valid until
+        :meth:`close`)."""
+        if getattr(self, "_status_word", None) is None:
+            self._status_word = self.lib.ipc_status_word(self.id)
+        return self._status_word
+
     def check(self) -> None:
         """Raise if any call since the start timed out (its output was poisoned); one device
         read -- the engine calls it at every epoch end, where it synchronises anyway."""
@@ -89,6 +97,7 @@ class IpcAllReduce:
     def close(self) -> None:
         if self.id is not None:
             torch.cuda.synchronize(self.device)
+            self._status_word = None
             self.lib.ipc_destroy(self.id)
             self.id = None
 

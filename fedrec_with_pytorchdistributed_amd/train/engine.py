@@ -424,7 +424,15 @@ class LocalEngine:
             return te.head(hid, mask)
 
     # -------------------------------------------------------------------------------
-    DEDUP_SYNC_MAX = 8192  # csrc dedup (one kernel chain, then the count read) up to this many ids
+    @property
+    def DEDUP_SYNC_MAX(self) -> int:
+        """Ids up to which the native dedup is one kernel chain ending in its unique-count read
+        (so no event is needed for the main stream); the extension's own constant, read once."""
+        v = getattr(LocalEngine, "_dedup_sync_max", None)
+        if v is None:
+            v = int(native.lib().dedup_sync_max()) if self.device.type == "cuda" else 0
+            LocalEngine._dedup_sync_max = v
+        return v
 
     def prepare(self, batch_fn: Callable[[], Tuple], held: bool = False) -> Prepared:
         """Sample a batch (``batch_fn() -> (cand, his)``) and de-duplicate its news ids.  On the
@@ -589,10 +597,14 @@ class LocalEngine:
         advanced by the caller per replay."""
         c = self.cfg
         srcs, self._grad_srcs = self._grad_srcs, None
+        # a device-epoch IPC all-reduce in the graph: its status word makes Adam skip the update of
+        # a step whose sum timed out (poisoned), and that step's loss reads NaN
+        ipc = getattr(self.grad_allreduce, "ipc", None) if self.grad_allreduce is not None else None
+        skip = ipc.status_word() if ipc is not None else None
         native.require_for(loss).adam_dev(self.flat.flat, self.flat.grad, self.flat.m, self.flat.v, self._adam_step_dev,
                                           loss.reshape(1).float(), self._loss_ring, c.lr, c.adam_beta1, c.adam_beta2,
                                           c.adam_eps, float(scale), srcs,
-                                          list(self.flat.offsets) if srcs is not None else None)
+                                          list(self.flat.offsets) if srcs is not None else None, skip)
 
     # ---- HIP graph of the per-step forward + backward ------------------------------------
     GRAPH_BUCKET = 128  # unique titles are padded up to a multiple of this (padded rows: id 0)
@@ -700,8 +712,13 @@ class LocalEngine:
 
     @torch.no_grad()
     def encode_all(self, grad: bool = False, chunk: int = 2048) -> torch.Tensor:
+        """Every title's news vector ``[N, 400]`` fp32 (eval mode).  Over the hidden-state cache
+        the fused head runs the whole table in one call (three launches: score, pool, fc -- the
+        title index is the cache row); otherwise in chunks of ``chunk`` titles."""
         self.sync_params()
         self.model.eval()
+        if self.fused_head:
+            return self.model.text_encoder.head_rows(self.hcache.flat(), None, self.tokens.shape[2], self.tokens).float()
         out = torch.empty(self.N, self.cfg.news_dim, dtype=torch.float32, device=self.device)
         for s in range(0, self.N, chunk):
             ids = torch.arange(s, min(s + chunk, self.N), device=self.device, dtype=torch.int32)
@@ -923,6 +940,14 @@ class LocalEngine:
                     "val_ndcg@5": float("nan"), "val_ndcg@10": float("nan"), "n_valid": 0}
         return self._valid_metrics(np.concatenate(scores_all, 0), sum(losses))
 
+    def prepare_validation(self, batch_size: int = 256) -> None:
+        """Build the validation split's device sampler now (its arrays go to HBM once); the
+        first :meth:`validate` otherwise pays it inside the round."""
+        if self.device.type == "cuda" and self.fused_user and getattr(self, "_vsampler", None) is None:
+            self._vsampler = DeviceSampler(self.shard.valid, batch_size, self.device, self.cfg.npratio,
+                                           self.cfg.max_his_len, truncate=True, seed=self.cfg.seed, rank=self.rank,
+                                           shuffle=False)
+
     def _validate_device(self, batch_size: int, limit: Optional[int], n_imp: int) -> Tuple[np.ndarray, float]:
         """The validation pass with no host work per batch: the batches are assembled by the
         device sampler's validation mode (``[pos] + negs[-4:]``, client.py:158-165), the news
@@ -930,10 +955,7 @@ class LocalEngine:
         validation, so every title's vector is), scores and the loss sum accumulate in device
         buffers, and ONE copy brings them back.  Same values as the host-batched path
         (``test_device_validation_matches_host_batches``)."""
-        if getattr(self, "_vsampler", None) is None:
-            self._vsampler = DeviceSampler(self.shard.valid, batch_size, self.device, self.cfg.npratio,
-                                           self.cfg.max_his_len, truncate=True, seed=self.cfg.seed, rank=self.rank,
-                                           shuffle=False)
+        self.prepare_validation(batch_size)
         table = self.news_table if self.news_table is not None else self.encode_all(grad=False)
         self.model.eval()
         C = self.cfg.npratio + 1

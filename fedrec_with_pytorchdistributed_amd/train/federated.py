@@ -293,6 +293,9 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     # RNG states and engine counters; the trainable parameters are overwritten by the round's
     # global model below, exactly as the reference's broadcast overwrites them
     csnap = ckpt.client_snapshot_path(cfg.snapshot_path, k) if cfg.snapshot_path else ""
+    if csnap and cfg.save_every and cfg.save_every > 1:
+        obs.log(f"[client {k}] save_every={cfg.save_every} does not apply to client snapshots: they are written "
+                "every round (a resume from an older round would redraw LDP noise / dropout already uploaded)")
     if csnap and os.path.exists(csnap):
         info = ckpt.load_client_state(csnap, model)
         eng.load_state(info["engine"])

@@ -25,7 +25,10 @@ def _metrics(path):
 def test_grad_avg_two_ranks(tmp_path):
     snap = str(tmp_path / "snapshot.pt")
     argv = ["Gradient_Averaging_main.py", "2", "16", "1", *TINY, f"--snapshot_path={snap}"]
-    outs = run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump")})
+    # TORCH_DISTRIBUTED_DEBUG=DETAIL: c10d wraps every process group in its collective checker
+    # (op type, shapes and dtypes compared across ranks before each collective) -- a mismatched
+    # collective sequence fails loudly here instead of hanging
+    outs = run_ranks([argv, argv], {"FEDREC_DUMP_FLAT": str(tmp_path / "dump"), "TORCH_DISTRIBUTED_DEBUG": "DETAIL"})
     _ok(outs)
     a = torch.load(tmp_path / "dump" / "rank0.pt")
     b = torch.load(tmp_path / "dump" / "rank1.pt")
