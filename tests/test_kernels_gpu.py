@@ -712,3 +712,29 @@ def test_device_ops_refuse_non_bf16(dev):
     with pytest.raises(RuntimeError, match="no HIP kernel"):
         O.layer_norm(x, torch.ones(768, device=dev), torch.zeros(768, device=dev), 1e-12)
 
+
+
+def test_adam_dev_skips_on_status_word(dev):
+    """The in-graph Adam with the gradient all-reduce's status word: nonzero (a peer timed out,
+    the sum was poisoned) -> no update of p / m / v and the step's loss slot is NaN; zero -> the
+    ordinary step, equal to the eager fused Adam."""
+    n = 1024
+    lib = native.lib()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    p0 = torch.randn(n, generator=g).to(dev)
+    gr = torch.randn(n, generator=g).to(dev)
+    step = torch.ones(1, dtype=torch.int64, device=dev)
+    loss = torch.full((1,), 1.5, device=dev)
+    for flag in (1, 0):
+        p, m, v = p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+        ring = torch.zeros(8, device=dev)
+        skip = torch.full((1,), flag, dtype=torch.int32, device=dev)
+        lib.adam_dev(p, gr.clone(), m, v, step, loss, ring, 1e-3, 0.9, 0.999, 1e-8, 0.5, None, None, skip)
+        torch.cuda.synchronize()
+        if flag:
+            assert torch.equal(p, p0) and not bool(m.any()) and not bool(v.any())
+            assert torch.isnan(ring[0])
+        else:
+            pe, me, ve = p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+            ops.adam_flat(pe, gr.clone(), me, ve, 1, 1e-3, 0.9, 0.999, 1e-8, 0.5)
+            assert torch.allclose(p, pe, atol=1e-7) and float(ring[0]) == 1.5
