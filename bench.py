@@ -212,6 +212,7 @@ def main() -> int:
     losses = []
     uniq = []  # unique titles per step (the backbone's work; it varies by batch and client)
     host_step = host_next = 0.0  # host time spent launching steps / preparing batches (diagnostic)
+    wait0 = eng.host_wait_s  # ... of which blocked on the run-ahead bound (waiting for the device)
     for _ in range(args.steps):
         if pre.dedup is not None:
             uniq.append(int(pre.dedup[0].numel()))
@@ -376,8 +377,13 @@ def main() -> int:
             "cache_build": cache_info,  # rank 0's breakdown (cooperative at N > 1: 1/W encoded + gather)
             "steps_per_epoch": steps_per_epoch,
             "steady_ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            # launch + next_batch include the host blocking on the run-ahead bound (run_ahead_wait:
+            # the device is the limit then); host_work = what the host itself spends per step
             "host_ms_per_step": {"launch": round(1000.0 * host_step / args.steps, 4),
-                                 "next_batch": round(1000.0 * host_next / args.steps, 4)},
+                                 "next_batch": round(1000.0 * host_next / args.steps, 4),
+                                 "run_ahead_wait": round(1000.0 * (eng.host_wait_s - wait0) / args.steps, 4),
+                                 "host_work": round(1000.0 * (host_step + host_next - (eng.host_wait_s - wait0))
+                                                    / args.steps, 4)},
             "cache_amortized_ms_per_step": round(1000.0 * amort / args.steps, 4),
             "fastest_rank_ms_per_step": round(1000.0 * fastest / args.steps, 3),
             "unique_titles_per_step": None if u_mean is None else round(u_mean, 1),

@@ -245,6 +245,7 @@ class LocalEngine:
         # step counters (tests / bench): graph replays, replays that ran the all-reduce + Adam
         # inside the graph, and optimizer steps issued eagerly from the host
         self.counts = {"replays": 0, "replays_with_optimizer": 0, "eager_optimizer_steps": 0, "eager_steps": 0}
+        self.host_wait_s = 0.0  # host time blocked on the run-ahead bound (_retire): the DEVICE is the limit
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
         # trainable parameters; everything that does calls sync_params() first
@@ -823,7 +824,9 @@ class LocalEngine:
             if old is None:  # covered by the next event queued after it
                 old = next((e for _, e in self._inflight if e is not None), None)
             if old is not None:
+                t0 = time.perf_counter()
                 old.synchronize()
+                self.host_wait_s += time.perf_counter() - t0
 
     # -------------------------------------------------------------------------------
     def train_epoch(self, max_steps: Optional[int] = None, log_every: int = 0,
