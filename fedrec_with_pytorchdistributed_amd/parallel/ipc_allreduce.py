@@ -55,19 +55,41 @@ class IpcAllReduce:
             blocks = int(os.environ.get("FEDREC_IPC_BLOCKS", 32))
         self.cap, self.one_shot_max, self.blocks = int(cap), int(one_shot_max), int(blocks)
         self.timeout_s = float(timeout_s)
-        with torch.cuda.device(device):
-            self.id, h = self.lib.ipc_create(self.cap)
+        self.id = None
+        hb = None
+        try:
+            with torch.cuda.device(device):
+                self.id, h = self.lib.ipc_create(self.cap)
+            hb = bytes(h.numpy().tobytes())
+        except RuntimeError:  # reported below, after every rank has joined the exchange
+            pass
         # every rank must run the same protocol geometry (the barrier waits on blocks x ranks
         # flags; a different one-shot threshold would split one call into different modes)
         geo = (self.cap, self.one_shot_max, self.blocks)
         handles: List[Optional[tuple]] = [None] * self.world
-        dist.all_gather_object(handles, (bytes(h.numpy().tobytes()), geo), group=ctrl_group)
-        if any(g[1] != geo for g in handles):
-            raise RuntimeError(f"IPC all-reduce: ranks disagree on (cap, one_shot_max, blocks): {[g[1] for g in handles]}")
+        dist.all_gather_object(handles, (hb, geo), group=ctrl_group)
+        if any(g[0] is None for g in handles) or any(g[1] != geo for g in handles):
+            if self.id is not None:
+                self.lib.ipc_destroy(self.id)
+                self.id = None
+            raise RuntimeError(f"IPC all-reduce: a rank could not create its region, or the ranks disagree on "
+                               f"(cap, one_shot_max, blocks): {[(g[0] is not None, g[1]) for g in handles]}")
         flat = torch.frombuffer(bytearray(b"".join(g[0] for g in handles)), dtype=torch.uint8)
-        with torch.cuda.device(device):
-            self.lib.ipc_open(self.id, flat, self.rank, self.world, None)
-        dist.barrier(group=ctrl_group)  # every rank opened every region before the first call
+        err = None
+        try:
+            with torch.cuda.device(device):
+                self.lib.ipc_open(self.id, flat, self.rank, self.world, None)
+        except RuntimeError as e:  # (a peer's region could not be mapped here)
+            err = e
+        # every rank learns whether every rank opened every region (one gloo MIN) -- a rank that
+        # failed must not leave the others waiting in a barrier or, worse, in a kernel
+        ok = torch.tensor([0 if err is not None else 1], dtype=torch.int64)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=ctrl_group)
+        if int(ok.item()) == 0:
+            self.lib.ipc_destroy(self.id)
+            self.id = None
+            raise RuntimeError(f"IPC all-reduce: a rank could not open the peers' regions"
+                               + (f" (here: {err})" if err is not None else " (on another rank)"))
         self.epoch = 0
 
     def allreduce_(self, t: torch.Tensor, mode: Optional[str] = None) -> torch.Tensor:
