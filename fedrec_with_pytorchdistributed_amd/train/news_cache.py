@@ -30,8 +30,12 @@ import torch
 
 
 class HiddenCache:
-    def __init__(self, text_encoder, tokens: torch.Tensor, chunk: int = 8192):
-        """``tokens [N, 2, T]`` (int, on the compute device): the client's news table."""
+    def __init__(self, text_encoder, tokens: torch.Tensor, chunk: int = 0):
+        """``tokens [N, 2, T]`` (int, on the compute device): the client's news table.  ``chunk``:
+        titles per backbone call (0: ``FEDREC_CACHE_CHUNK``, default 8192)."""
+        import os
+
+        chunk = int(chunk) or int(os.environ.get("FEDREC_CACHE_CHUNK", "8192"))
         self.te = text_encoder
         self.tokens = tokens
         # the ping-pong GEMM indexes its operands with 32-bit offsets: a chunk's widest
