@@ -199,6 +199,7 @@ namespace {
 constexpr int MCAST_SEG = 96;
 constexpr int MCAST_CHUNK = 8192;  // 256 threads x 4 iterations x 8 elements
 constexpr int MCAST_FILL = 8;
+constexpr int MCAST_TSEG = 8;
 
 struct MultiCast {
   const float* src[MCAST_SEG];
@@ -215,21 +216,60 @@ struct MultiCast {
   signed char fslot[MCAST_SEG];  // -1: none, else index into nsrc / fill
   long nsrc[MCAST_FILL];
   int fill[MCAST_FILL];
+  // transposed bf16 segments (after the others' blocks): fp32 [R, C] -> dst[c * ld + r], 64 x 64
+  // tiles through LDS, any R / C (the register-direct GEMMs' k-contiguous weight copies)
+  int ntseg;
+  const float* tsrc[MCAST_TSEG];
+  bf16* tdst[MCAST_TSEG];
+  int tR[MCAST_TSEG], tC[MCAST_TSEG], tld[MCAST_TSEG];
+  int tblk0[MCAST_TSEG + 1];
 };
 
+__device__ __forceinline__ void mcast_t_tile(const MultiCast& mc, int t) {
+  __shared__ float tile[64][65];
+  int sg = 0;
+  while (sg + 1 < mc.ntseg && mc.tblk0[sg + 1] <= t) ++sg;
+  t -= mc.tblk0[sg];
+  const int R = mc.tR[sg], C = mc.tC[sg], ct = (C + 63) >> 6;
+  const int r0 = (t / ct) * 64, c0 = (t % ct) * 64;
+  const float* src = mc.tsrc[sg];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {  // 64 rows x 64 columns, one float per thread and pass
+    const int r = (tid >> 6) + 4 * i, c = tid & 63;
+    tile[r][c] = (r0 + r < R && c0 + c < C) ? src[(size_t)(r0 + r) * C + c0 + c] : 0.f;
+  }
+  __syncthreads();
+  bf16* dst = mc.tdst[sg];
+  const int ld = mc.tld[sg];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {  // destination row c0 + c, 64 consecutive r
+    const int c = (tid >> 6) + 4 * i, r = tid & 63;
+    if (c0 + c < C && r0 + r < R) dst[(size_t)(c0 + c) * ld + r0 + r] = f2bf(tile[r][c]);
+  }
+}
+
 __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
-  int lo = 0, hi = mc.nseg - 1;  // last segment with blk0 <= blockIdx.x
+  // the transposed tiles first (the lowest block ids start first): their load -> LDS -> store
+  // chain then overlaps the streaming blocks instead of trailing them (+3 us per launch at the end)
+  const int nt = mc.tblk0[mc.ntseg];
+  if ((int)blockIdx.x < nt) {  // block-uniform
+    mcast_t_tile(mc, (int)blockIdx.x);
+    return;
+  }
+  const int bx = (int)blockIdx.x - nt;
+  int lo = 0, hi = mc.nseg - 1;  // last segment with blk0 <= bx
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (mc.blk0[mid] <= (int)blockIdx.x) lo = mid;
+    if (mc.blk0[mid] <= bx) lo = mid;
     else hi = mid - 1;
   }
   const int sg = lo;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bx == 0 && threadIdx.x == 0) {
     if (mc.bump != nullptr) *mc.bump += 1;
     if (mc.bump2 != nullptr) *mc.bump2 += 1;
   }
-  const long base = (long)(blockIdx.x - mc.blk0[sg]) * MCAST_CHUNK;
+  const long base = (long)(bx - mc.blk0[sg]) * MCAST_CHUNK;
   const float4* s4 = (const float4*)mc.src[sg];
   const long n = mc.n[sg];
   const int fs = mc.fslot[sg];
@@ -263,10 +303,27 @@ __global__ __launch_bounds__(256) void multi_cast_kernel(const MultiCast mc) {
 // dropout / noise offset rides in the step's cast launch instead of a launch of its own
 // nsrc (optional): per segment, the source words (< n[i]: fp32 / copy segments only; the
 // rest of the destination gets fill[i]) -- at most MCAST_FILL such segments per launch
+// ntseg transposed segments (tsrc fp32 [tR, tC] -> tdst bf16, element (r, c) at c * tld + r)
+// follow the others in the same launch
 extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                             long long* bump, hipStream_t s, long long* bump2, const long* nsrc, const int* fill) {
-  if (nseg < 1 || nseg > MCAST_SEG) return 1;
+                             long long* bump, hipStream_t s, long long* bump2, const long* nsrc, const int* fill,
+                             int ntseg, const float* const* tsrc, void* const* tdst, const int* tR, const int* tC,
+                             const int* tld) {
+  if (nseg < 1 || nseg > MCAST_SEG || ntseg < 0 || ntseg > MCAST_TSEG) return 1;
   MultiCast mc{};
+  mc.ntseg = ntseg;
+  long tb = 0;
+  for (int i = 0; i < ntseg; ++i) {
+    if (tR[i] <= 0 || tC[i] <= 0 || tld[i] < tR[i]) return 1;
+    mc.tsrc[i] = tsrc[i];
+    mc.tdst[i] = (bf16*)tdst[i];
+    mc.tR[i] = tR[i];
+    mc.tC[i] = tC[i];
+    mc.tld[i] = tld[i];
+    mc.tblk0[i] = (int)tb;
+    tb += (long)((tR[i] + 63) / 64) * ((tC[i] + 63) / 64);
+  }
+  mc.tblk0[ntseg] = (int)tb;
   mc.nseg = nseg;
   mc.bump = bump;
   mc.bump2 = bump2;
@@ -293,8 +350,8 @@ extern "C" int fr_multi_cast(const float* const* src, void* const* dst, const lo
     blk += (n[i] + MCAST_CHUNK - 1) / MCAST_CHUNK;
   }
   mc.blk0[nseg] = (int)blk;
-  if (blk >= (1L << 31)) return 1;
-  hipLaunchKernelGGL(multi_cast_kernel, dim3((unsigned)blk), dim3(256), 0, s, mc);
+  if (blk + tb >= (1L << 31)) return 1;
+  hipLaunchKernelGGL(multi_cast_kernel, dim3((unsigned)(blk + tb)), dim3(256), 0, s, mc);
   return 0;
 }
 

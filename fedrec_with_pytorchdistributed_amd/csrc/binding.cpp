@@ -70,6 +70,8 @@ int fr_ipc_allreduce_local(const int* ids, void* const* xs, int W, long n, int i
                            int blocks, double timeout_s, hipStream_t s);
 int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, int NH, int dk, const int* keep,
                      hipStream_t s, void* ctx_b);
+int fr_user_qkv_attn_fwd(const void* xd, const void* W, const float* bias, int Din, float* qkv, float* ctx,
+                         float* stats, int B, int H, int NH, int dk, const int* keep, hipStream_t s, void* ctx_b);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, void* dqkv, int B, int H, int NH,
                      int dk, const int* keep, hipStream_t s, int out_bf16);
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
@@ -78,6 +80,7 @@ int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, 
                         int R, float* scratch, hipStream_t s, int zero_empty);
 int fr_segsum_chunks(int R);
 void fr_segsum_set_variant(int v);
+void fr_small_gemm_set_rd(int v);
 int fr_user_pool_score(const float* x, const float* e, const float* w2, const float* b2, const int* keep,
                        const float* cand, const int* ci, int B, int T, int D, int Q, int C, int sigm, float* lossb,
                        float* scores, float* dcand, float* loss_total, float* dctx, float* dpre, void* dpre_b,
@@ -129,7 +132,8 @@ int fr_secagg_unmask_exact(const int* x, float* out, long n, const int* H, int W
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, int tile, hipStream_t s);
 int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
-                  long long* bump, hipStream_t s, long long* bump2, const long* nsrc, const int* fill);
+                  long long* bump, hipStream_t s, long long* bump2, const long* nsrc, const int* fill, int ntseg,
+                  const float* const* tsrc, void* const* tdst, const int* tR, const int* tC, const int* tld);
 int fr_multi_cast_t(const float* const* src, void* const* dst, const int* R, const int* C, const int* ld, int nseg,
                     hipStream_t s);
 int fr_multi_copy(const int* const* src, int* const* dst, const long* nsrc, const long* ndst, const int* fill, int n,
@@ -815,6 +819,45 @@ std::tuple<at::Tensor, at::Tensor> user_attention_fwd(const at::Tensor& qkv, int
   return {ctx, stats};
 }
 
+// The Q|K|V projection fused into the attention forward (user_attn.hip user_qkv_attn_fwd_kernel):
+// xd bf16 [B*H, Din] (the gathered, dropped-out history rows), W bf16 [3*heads*head_dim, Din],
+// bias fp32 [3*heads*head_dim] -> (ctx [B, H, D], stats, qkv [B, H, 3D] fp32 -- the backward's
+// input).  H <= 64; ctx_b (optional): ctx rounded to bf16 as well.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> user_qkv_attention_fwd(const at::Tensor& xd, const at::Tensor& W,
+                                                                      const at::Tensor& bias, int64_t B, int64_t heads,
+                                                                      int64_t head_dim,
+                                                                      const c10::optional<at::Tensor>& keep,
+                                                                      const c10::optional<at::Tensor>& ctx_b) {
+  check_dev(xd, "xd");
+  check_dev(W, "W");
+  check_dev(bias, "bias");
+  const c10::DeviceGuard g(xd.device());
+  TORCH_CHECK(xd.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 && bias.scalar_type() == at::kFloat &&
+                  xd.dim() == 2 && W.dim() == 2 && xd.is_contiguous() && W.is_contiguous() && bias.is_contiguous(),
+              "fedrec::user_qkv_attention_fwd: contiguous bf16 xd [B*H, Din], bf16 W [3D, Din], fp32 bias [3D]");
+  const int64_t D = heads * head_dim, Din = xd.size(1);
+  TORCH_CHECK(B > 0 && xd.size(0) % B == 0, "fedrec::user_qkv_attention_fwd: xd rows = B*H");
+  const int64_t H = xd.size(0) / B;
+  TORCH_CHECK(W.size(0) == 3 * D && W.size(1) == Din && bias.numel() == 3 * D && H >= 1 && H <= 64,
+              "fedrec::user_qkv_attention_fwd: W [3D, Din], bias [3D], H <= 64");
+  auto opt = xd.options().dtype(at::kFloat);
+  auto qkv = at::empty({B, H, 3 * D}, opt);
+  auto ctx = at::empty({B, H, D}, opt);
+  auto stats = at::empty({B, heads, H, 2}, opt);
+  void* cb = nullptr;
+  if (ctx_b.has_value()) {
+    check_dev(*ctx_b, "ctx_b");
+    TORCH_CHECK(ctx_b->scalar_type() == at::kBFloat16 && ctx_b->numel() == ctx.numel() && ctx_b->is_contiguous(),
+                "fedrec::user_qkv_attention_fwd: ctx_b bf16 like ctx");
+    cb = ctx_b->data_ptr();
+  }
+  check_rc(fr_user_qkv_attn_fwd(xd.data_ptr(), W.data_ptr(), bias.data_ptr<float>(), (int)Din, qkv.data_ptr<float>(),
+                                ctx.data_ptr<float>(), stats.data_ptr<float>(), (int)B, (int)H, (int)heads,
+                                (int)head_dim, key_mask_ptr(keep, B, H, "user_qkv_attention_fwd"), cur_stream(), cb),
+           "user_qkv_attention_fwd");
+  return {ctx, stats, qkv};
+}
+
 // bf16_out: dqkv in bf16 (the input / weight gradient GEMMs' operand)
 at::Tensor user_attention_bwd(const at::Tensor& qkv, const at::Tensor& stats, const at::Tensor& dctx, int64_t heads,
                               int64_t head_dim, const c10::optional<at::Tensor>& keep, bool bf16_out) {
@@ -1305,6 +1348,28 @@ void colsum_f32(const std::vector<at::Tensor>& X, const std::vector<at::Tensor>&
               "fedrec::colsum_f32: launch failed");
 }
 
+// A cast destination given as a transposed view of a bf16 matrix (dst = T[:, a:b].t(): sizes
+// [R, C], strides (1, ld >= R)) of a contiguous fp32 [R, C] source: the cast writes the
+// transposed copy (multi_cast's T segments; the register-direct GEMMs' k-contiguous weights)
+struct TSegs {
+  std::vector<const float*> src;
+  std::vector<void*> dst;
+  std::vector<int> R, C, ld;
+};
+static bool is_tdst(const at::Tensor& src, const at::Tensor& dst) {
+  return dst.dim() == 2 && src.dim() == 2 && dst.scalar_type() == at::kBFloat16 && src.scalar_type() == at::kFloat &&
+         src.is_contiguous() && src.sizes() == dst.sizes() && dst.stride(0) == 1 && dst.size(0) > 1 &&
+         dst.stride(1) >= dst.size(0) && src.is_cuda() && dst.is_cuda();
+}
+static void add_tseg(TSegs& t, const at::Tensor& src, const at::Tensor& dst) {
+  TORCH_CHECK(t.src.size() < 8, "fedrec: at most 8 transposed cast segments per launch");
+  t.src.push_back(src.data_ptr<float>());
+  t.dst.push_back(dst.data_ptr());
+  t.R.push_back((int)src.size(0));
+  t.C.push_back((int)src.size(1));
+  t.ld.push_back((int)dst.stride(1));
+}
+
 // fp32 tensors -> bf16 / fp32 destinations (contiguous slices allowed) in one launch per 96
 // (adam.hip), any size / alignment; false = not launched (an empty segment).  bump (optional
 // int64 [1] on the same device): advanced by one by the first launch
@@ -1327,27 +1392,37 @@ bool multi_cast(const std::vector<at::Tensor>& src, const std::vector<at::Tensor
                 "fedrec::multi_cast: bump2 must be an int64 [1] tensor on the destinations' device");
     bp2 = (long long*)bump2->data_ptr<int64_t>();
   }
-  std::vector<const float*> sp(n);
-  std::vector<void*> dp(n);
-  std::vector<long> ne(n);
-  std::vector<int> bf(n);
+  std::vector<const float*> sp;
+  std::vector<void*> dp;
+  std::vector<long> ne;
+  std::vector<int> bf;
+  TSegs ts;
   for (size_t i = 0; i < n; ++i) {
+    if (is_tdst(src[i], dst[i])) {
+      add_tseg(ts, src[i], dst[i]);
+      continue;
+    }
     TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && dst[i].is_contiguous() &&
                     src[i].scalar_type() == at::kFloat &&
                     (dst[i].scalar_type() == at::kBFloat16 || dst[i].scalar_type() == at::kFloat) &&
                     src[i].numel() == dst[i].numel(),
-                "fedrec::multi_cast: contiguous fp32 sources, bf16/fp32 destinations of the same size");
-    sp[i] = src[i].data_ptr<float>();
-    dp[i] = dst[i].data_ptr();
-    ne[i] = (long)src[i].numel();
-    bf[i] = dst[i].scalar_type() == at::kBFloat16 ? 1 : 0;
+                "fedrec::multi_cast: contiguous fp32 sources, bf16/fp32 destinations of the same size "
+                "(or transposed bf16 views)");
+    sp.push_back(src[i].data_ptr<float>());
+    dp.push_back(dst[i].data_ptr());
+    ne.push_back((long)src[i].numel());
+    bf.push_back(dst[i].scalar_type() == at::kBFloat16 ? 1 : 0);
   }
-  for (size_t i = 0; i < n; ++i)
+  const size_t nn = sp.size();
+  for (size_t i = 0; i < nn; ++i)
     if (ne[i] <= 0) return false;
-  for (size_t i0 = 0; i0 < n; i0 += 96) {  // 96 segments per launch (kernel-argument size)
-    const int k = (int)std::min<size_t>(96, n - i0);
-    TORCH_CHECK(fr_multi_cast(sp.data() + i0, dp.data() + i0, ne.data() + i0, bf.data() + i0, k, i0 == 0 ? bp : nullptr,
-                              cur_stream(), i0 == 0 ? bp2 : nullptr, nullptr, nullptr) == 0,
+  TORCH_CHECK(nn >= 1, "fedrec::multi_cast: at least one plain segment");
+  for (size_t i0 = 0; i0 < nn; i0 += 96) {  // 96 segments per launch (kernel-argument size)
+    const int k = (int)std::min<size_t>(96, nn - i0);
+    const bool first = i0 == 0;
+    TORCH_CHECK(fr_multi_cast(sp.data() + i0, dp.data() + i0, ne.data() + i0, bf.data() + i0, k, first ? bp : nullptr,
+                              cur_stream(), first ? bp2 : nullptr, nullptr, nullptr, first ? (int)ts.src.size() : 0,
+                              ts.src.data(), ts.dst.data(), ts.R.data(), ts.C.data(), ts.ld.data()) == 0,
                 "fedrec::multi_cast: launch rejected");
   }
   return true;
@@ -1390,12 +1465,18 @@ bool copy_cast(const std::vector<at::Tensor>& csrc, const std::vector<at::Tensor
     bf.push_back(0);
     fv.push_back((int)fill[i]);
   }
+  TSegs ts;
   for (size_t i = 0; i < n; ++i) {
+    if (is_tdst(src[i], dst[i])) {
+      add_tseg(ts, src[i], dst[i]);
+      continue;
+    }
     TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].is_contiguous() && dst[i].is_contiguous() &&
                     src[i].scalar_type() == at::kFloat &&
                     (dst[i].scalar_type() == at::kBFloat16 || dst[i].scalar_type() == at::kFloat) &&
                     src[i].numel() == dst[i].numel(),
-                "fedrec::copy_cast: contiguous fp32 cast sources, bf16/fp32 destinations of the same size");
+                "fedrec::copy_cast: contiguous fp32 cast sources, bf16/fp32 destinations of the same size "
+                "(or transposed bf16 views)");
     if (src[i].numel() == 0) return false;
     sp.push_back(src[i].data_ptr<float>());
     dp.push_back(dst[i].data_ptr());
@@ -1406,7 +1487,8 @@ bool copy_cast(const std::vector<at::Tensor>& csrc, const std::vector<at::Tensor
   }
   if (sp.empty()) return false;
   TORCH_CHECK(fr_multi_cast(sp.data(), dp.data(), ne.data(), bf.data(), (int)sp.size(), bp, cur_stream(), bp2,
-                            ns.data(), fv.data()) == 0,
+                            ns.data(), fv.data(), (int)ts.src.size(), ts.src.data(), ts.dst.data(), ts.R.data(),
+                            ts.C.data(), ts.ld.data()) == 0,
               "fedrec::copy_cast: launch rejected (more than 8 padded copies?)");
   return true;
 }
@@ -1797,6 +1879,7 @@ void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
 void score_set_variant(int64_t v) { fr_score_set_variant((int)v); }
 void segsum_set_variant(int64_t v) { fr_segsum_set_variant((int)v); }
+void small_gemm_set_rd(int64_t v) { fr_small_gemm_set_rd((int)v); }
 void head_score_set_rows(int64_t r) { fr_head_score_set_rows((int)r); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 
@@ -1808,6 +1891,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
   m.def("score_set_variant(int v) -> ()", &score_set_variant);
   m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
+  m.def("small_gemm_set_rd(int v) -> ()", &small_gemm_set_rd);
   m.def("user_pool_score(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep, Tensor table, Tensor ci, int act, Tensor(a!) dcand_out, bool want_bwd) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("head_score_set_rows(int r) -> ()", &head_score_set_rows);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
@@ -1846,6 +1930,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("upool_bwd_da(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool bf16_out=False) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None, Tensor(a!)? ctx_b=None) -> (Tensor, Tensor)");
+  m.def("user_qkv_attention_fwd(Tensor xd, Tensor W, Tensor bias, int B, int heads, int head_dim, Tensor? keep=None, "
+        "Tensor(a!)? ctx_b=None) -> (Tensor, Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None, bool bf16_out=False) -> Tensor");
   m.def("score_ce(Tensor cand, Tensor user, int act, Tensor? ci=None, Tensor(a!)? dcand_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("segment_sum_rows(Tensor rows, Tensor perm, Tensor seg_ptr, int num_out, float clip, float noise_std, int seed, int offset, Tensor? inv=None, bool zero_empty=False, Tensor? dev_off=None) -> Tensor");
@@ -1905,6 +1991,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("additive_pool_bwd", &additive_pool_bwd);
   m.impl("upool_bwd_da", &upool_bwd_da);
   m.impl("user_attention_fwd", &user_attention_fwd);
+  m.impl("user_qkv_attention_fwd", &user_qkv_attention_fwd);
   m.impl("user_attention_bwd", &user_attention_bwd);
   m.impl("score_ce", &score_ce);
   m.impl("user_pool_score", &user_pool_score);

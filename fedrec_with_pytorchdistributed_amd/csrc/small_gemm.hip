@@ -709,6 +709,158 @@ __global__ __launch_bounds__(256) void small_gemm_mixed_kernel(const GemmBatch b
 }
 
 
+// ---- register-direct launches (bf16 x bf16, both operands k-contiguous) -------------------
+// The LDS forms above spend each k-step on one global -> LDS latency behind a barrier: a launch
+// of these shapes (K = 200..1200, ~1-4 tiles per CU) is a chain of such latencies, 13-26 us in
+// the config-2 step for 0.5-3 GFLOP (profiles/r5m_launch_seq.txt).  Here an MFMA fragment is
+// loaded straight into VGPRs: for v_mfma_f32_16x16x32_bf16 a lane needs 8 consecutive k (16 B)
+// of row lane % 16 at k = 8 (lane / 16) of a 32-deep k-step, which is one buffer_load_dwordx4 of
+// a k-contiguous operand.  Each wave owns a (16 FM) x (16 FN) tile and keeps P k-steps of
+// fragments in flight (a ring in registers, statically indexed by unrolling the k loop by P):
+// no LDS, no barrier, the wave waits only for its own oldest k-step.  A block is 4 waves in
+// 2 x 2 over a (32 FM) x (32 FN) block tile (the two waves of a row / column share their A / B
+// lines in L1).  The MFMA takes B as src0, so a lane ends with 4 consecutive columns of one
+// row: float4 epilogue stores (the LDS forms' lanes hold 4 rows of one column: 4-byte stores).
+// Rows past M / N and k past K load as zeros (buffer offsets past the descriptor's range).
+// AF: A fp32 (two 16-B loads per fragment, rounded to bf16 in registers -- the rounding the LDS
+// forms apply on their way into LDS).
+template <int FM, int FN, int P, bool AF = false>
+__global__ __launch_bounds__(256) void small_gemm_rd_kernel(const GemmBatch batch) {
+  int gi;
+  int t = tile_of_block(batch, gi);
+  const GemmDesc& g = batch.d[gi];
+  const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
+  const int split = t % g.splits;
+  t /= g.splits;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = (t / g.tiles_n) * (32 * FM) + (wave >> 1) * (16 * FM);
+  const int n0 = (t % g.tiles_n) * (32 * FN) + (wave & 1) * (16 * FN);
+  const int kbeg = split * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
+  const int fr = lane & 15, fq = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rsa = rsrc_of(g.A), rsb = rsrc_of(g.B);
+  // byte offsets of this lane's fragment rows at k = kbeg + 8 fq (OOB: a row past M / N)
+  uint32_t oa[FM], ob[FN];
+  constexpr uint32_t AES = AF ? 4u : 2u;  // A element bytes
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int r = m0 + i * 16 + fr;
+    oa[i] = r < g.M ? (uint32_t)(r * g.lda + kbeg + 8 * fq) * AES : OOB;
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int r = n0 + j * 16 + fr;
+    ob[j] = r < g.N ? (uint32_t)(r * g.ldb + kbeg + 8 * fq) * 2u : OOB;
+  }
+  const int nk = (kend - kbeg + 31) >> 5;
+  u32x4 ra[P][FM][AF ? 2 : 1], rb[P][FN];
+  auto load = [&](int s, int kt) {  // k-step kt into ring slot s (zeros past kend)
+    const bool kok = kbeg + kt * 32 + 8 * fq < kend;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int h = 0; h < (AF ? 2 : 1); ++h)
+        ra[s][i][h] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, kok ? oa[i] + kt * 32 * AES + 16 * h : OOB, 0, 0));
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      rb[s][j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsb, kok ? ob[j] + kt * 64 : OOB, 0, 0));
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto afrag = [&](int s, int i) -> bf16x8 {
+    if constexpr (!AF) {
+      return __builtin_bit_cast(bf16x8, ra[s][i][0]);
+    } else {
+      bf16x8 o;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[4 * h + q] = f2bf(__uint_as_float(ra[s][i][AF ? h : 0][q]));
+      return o;
+    }
+  };
+  auto mma = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const bf16x8 a = afrag(s, i);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, rb[s][j]), a, acc[i][j], 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < P; ++s) load(s, s);
+  // whole groups of P k-steps with no branch inside (the compiler's wait pass then keeps the
+  // younger slots in flight across the loop edge -- a branch per slot made it wait for every
+  // load at the loop head); loads past the last k-step are zero-filled OOB loads, never used
+  const int nfull = nk / P * P;
+  for (int kt = 0; kt < nfull; kt += P) {
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      mma(s);
+      load(s, kt + s + P);
+      __builtin_amdgcn_sched_barrier(0);  // slot s refills here, not with the whole group at the end
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < P - 1; ++s)
+    if (nfull + s < nk) mma(s);
+  // lane holds C[m0 + 16 i + fr][n0 + 16 j + 4 fq + r], r = 0..3
+  const bool part = g.splits > 1;
+  float* const dst = part ? g.P + (size_t)split * g.M * g.N : g.C;
+  const int ldd = part ? g.N : g.ldc;
+  const bool vec = (ldd & 3) == 0 && (((uintptr_t)dst) & 15) == 0;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + j * 16 + 4 * fq;
+    if (n >= g.N) continue;
+    const bool full = n + 3 < g.N;
+    float bn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!part && g.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bn[r] = n + r < g.N ? g.bias[n + r] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + i * 16 + fr;
+      if (m >= g.M) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      float* c = dst + (size_t)m * ldd + n;
+      if (!part) {
+        float dsc[4] = {1.f, 1.f, 1.f, 1.f};
+        if (g.drop_on == 3) {  // n % 4 == 0 and drop_ld % 16 == 0: one Philox draw for the 4
+          const unsigned long long e = (unsigned long long)m * g.drop_ld + n;
+          const uint4 x = Philox::gen(g.seed, off, e >> 2);
+          const float ik = 1.0f / (1.0f - g.pdrop);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dsc[r] = drop_scale(u4_get(x, r), g.pdrop, ik);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = g.alpha * v[r] + bn[r];
+          if (g.act == 1) v[r] = tanhf(v[r]);
+          v[r] *= dsc[r];
+        }
+      }
+      if (full && vec) {
+        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+        if (!part && g.accumulate) {
+          const float4 p = *(const float4*)c;
+          o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+        }
+        *(float4*)c = o;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < g.N) c[r] = (!part && g.accumulate) ? v[r] + c[r] : v[r];
+      }
+    }
+  }
+}
+
 // split-K epilogue: C = act(alpha * sum_s P[s] + bias) (x the output dropout scale, drop_on 3)
 // (+ C), partials summed in split order (deterministic) -- the single-pass epilogue's order.
 // Each desc owns a block range (red_base); a lane takes 4 consecutive columns of one row: 16-B
@@ -948,6 +1100,83 @@ static bool mixed_dtypes(const GemmBatch& b) {
   return false;
 }
 
+// the register-direct form takes bf16 x bf16 launches whose operands are both k-contiguous
+// (a_mode 0, b_mode 0), no column sums, the output dropout at most
+// (A fp32 or bf16, the same in every desc; B bf16)
+static bool rd_ok(const GemmBatch& b) {
+  for (int i = 0; i < b.n; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (d.a_bf16 != b.d[0].a_bf16 || !d.b_bf16 || d.a_mode != 0 || d.b_mode != 0 || d.asum || d.drop_on == 1 ||
+        d.drop_on == 2 || d.gather_on || d.kseg)
+      return false;
+  }
+  return true;
+}
+
+int g_sg_rd = 0;  // auto picks the register-direct form: 0 off (benchmarks / A-B switch), 1 on
+extern "C" void fr_small_gemm_set_rd(int v) { g_sg_rd = v; }
+
+static int rd_auto(const GemmBatch& b) {
+  if (!g_sg_rd) return 0;
+  long t64 = 0;  // 64 x 64 block tiles of 32 x 32 wave tiles
+  for (int i = 0; i < b.n; ++i) t64 += (long)((b.d[i].M + 63) / 64) * ((b.d[i].N + 63) / 64);
+  return t64 >= 512 ? 1000 + 10 * 1 + 3 : 1000 + 4;  // 128 x 128 / P 3 at >= 2 small tiles per CU
+}
+
+static long launch_rd(GemmBatch& b, int code, float* scratch, hipStream_t s) {
+  const bool allow_split = (code / 100) % 10 != 0;
+  const int f = (code / 10) % 10, P = code % 10;
+  const int FM = (f == 1 || f == 3) ? 4 : 2, FN = (f == 1 || f == 2) ? 4 : 2;
+  if (P < 2 || P > 4 || f > 3) return -7;
+  const int tm = 32 * FM, tn = 32 * FN;
+  int tiles = 0, red_blocks = 0;
+  long need = 0;
+  for (int i = 0; i < b.n; ++i) {
+    GemmDesc& d = b.d[i];
+    d.tiles_n = (d.N + tn - 1) / tn;
+    const int t = ((d.M + tm - 1) / tm) * d.tiles_n;
+    d.splits = allow_split ? choose_splits(t, d.K, true) : 1;
+    d.kchunk = d.splits > 1 ? ((d.K + d.splits - 1) / d.splits + 31) / 32 * 32 : d.K;
+    if (d.splits > 1) d.splits = (d.K + d.kchunk - 1) / d.kchunk;
+    if (d.splits > 1 && d.N % 4 != 0) {
+      d.splits = 1;
+      d.kchunk = d.K;
+    }
+    d.P = nullptr;
+    d.AP = nullptr;
+    d.red_base = red_blocks;
+    d.ared_base = 0;
+    if (d.splits > 1) {
+      d.P = scratch ? scratch + need : nullptr;
+      need += (long)d.splits * d.M * d.N;
+      red_blocks += (int)(((long)d.M * d.N / 4 + 255) / 256);
+    }
+    d.tile_base = tiles;
+    tiles += t * d.splits;
+  }
+  if (scratch == nullptr && need > 0) return need;
+  if (tiles == 0) return 0;
+#define RD_LAUNCH(FM_, FN_, P_)                                                                              \
+  do {                                                                                                     \
+    if (b.d[0].a_bf16) hipLaunchKernelGGL((small_gemm_rd_kernel<FM_, FN_, P_>), dim3(tiles), dim3(256), 0, s, b); \
+    else hipLaunchKernelGGL((small_gemm_rd_kernel<FM_, FN_, P_, true>), dim3(tiles), dim3(256), 0, s, b);   \
+  } while (0)
+#define RD_P(FM_, FN_)          \
+  do {                          \
+    if (P == 2) RD_LAUNCH(FM_, FN_, 2); \
+    else if (P == 3) RD_LAUNCH(FM_, FN_, 3); \
+    else RD_LAUNCH(FM_, FN_, 4); \
+  } while (0)
+  if (FM == 2 && FN == 2) RD_P(2, 2);
+  else if (FM == 4 && FN == 4) RD_P(4, 4);
+  else if (FM == 2) RD_P(2, 4);
+  else RD_P(4, 2);
+#undef RD_P
+#undef RD_LAUNCH
+  if (red_blocks > 0) hipLaunchKernelGGL(splitk_reduce_kernel, dim3(red_blocks), dim3(256), 0, s, b, red_blocks);
+  return 0;
+}
+
 extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats,
                               const unsigned long long* seeds, const unsigned long long* dev_off, int n, float* scratch,
                               int tile, hipStream_t s) {
@@ -984,6 +1213,14 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
   }
   b.n = n;
   const bool fast = fast_ok(b), mixed = mixed_dtypes(b);
+  // register-direct form: tile codes 1000 + 100 s + 10 f + P (s: split-K allowed, f: wave tile
+  // 0 = 32 x 32, 1 = 64 x 64, 2 = 32 x 64, 3 = 64 x 32, P: k-steps in flight 2..4); 0 = auto
+  // (a code the launch's operands do not allow falls back to the automatic choice)
+  if (tile >= 1000 || tile == 0) {
+    const int code = tile == 0 ? rd_auto(b) : tile;
+    if (code >= 1000 && fast && rd_ok(b)) return launch_rd(b, code, scratch, s);
+    tile = 0;
+  }
   // benchmarks / tests: 5 = the 64 x 64 register-queue form (never the DMA ring), 6 / 7 / 8 =
   // the DMA ring with 2 / 3 / 4 stages where it applies, 9 = 2 stages and no split-K
   const bool regq = tile == 5;

@@ -185,46 +185,15 @@ __device__ __forceinline__ bool key_kept(const int* __restrict__ keep, int b, in
   return keep == nullptr || keep[(size_t)b * H + t] != 0;
 }
 
-// SR = 65: 33,008 B of LDS, four blocks per CU (64-row stages, five blocks per CU, measured
-// neutral: profiles/r3_ab_segsum_ua.txt)
-// ctx_b (optional): ctx rounded to bf16 as well (the att_fc1 GEMM's operand)
-template <int SR>
-__global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* __restrict__ qkv,
-                                                                  float* __restrict__ ctx, float* __restrict__ stats,
-                                                                  int H, int NH, const int* __restrict__ keep,
-                                                                  bf16* __restrict__ ctx_b) {
-  __shared__ __attribute__((aligned(16))) float qs[SR][DK];
-  __shared__ __attribute__((aligned(16))) float ks[SR][DK];
-  __shared__ __attribute__((aligned(16))) float vs[SR][DK];
-  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
+// The attention forward of one (impression b, head h) once its Q, K, V slices sit in LDS (rows
+// >= H zero): S = Q K^T, eps-softmax, ctx = P V, (m, 1/l) per row.  Wave w takes query rows
+// [16 w, 16 w + 16).
+__device__ __forceinline__ void attn_fwd_body(float (*qs)[DK], float (*ks)[DK], float (*vs)[DK], float* ps, int b,
+                                              int h, int H, int NH, const int* __restrict__ keep,
+                                              float* __restrict__ ctx, float* __restrict__ stats,
+                                              bf16* __restrict__ ctx_b) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
-  const int ld = 3 * NH * DK, D = NH * DK;
-  const float* base = qkv + (size_t)b * H * ld + h * DK;
-  {  // 3 x 320 float4 chunks over 256 threads, every load in flight before the stores
-    float4 v[3][2];
-#pragma unroll
-    for (int o = 0; o < 3; ++o)
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const int i = tid + 256 * it;
-        const int r = min(min(i, 319) / (DK / 4), H - 1), c = (i % (DK / 4)) * 4;
-        v[o][it] = *(const float4*)(base + (size_t)o * D + (size_t)r * ld + c);
-      }
-    float (*const xs[3])[DK] = {qs, ks, vs};
-#pragma unroll
-    for (int o = 0; o < 3; ++o)
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const int i = tid + 256 * it;
-        const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
-        const bool z = r >= H;
-        const float4 w = make_float4(z ? 0.f : v[o][it].x, z ? 0.f : v[o][it].y, z ? 0.f : v[o][it].z,
-                                     z ? 0.f : v[o][it].w);
-        if (i < 320) *(float4*)&xs[o][r][c] = w;
-      }
-  }
-  __syncthreads();
+  const int D = NH * DK;
   const int i0 = wave * 16;
   if (i0 >= H) return;  // wave-uniform; no barrier follows
   const int NT = (H + 15) / 16;
@@ -299,6 +268,155 @@ __global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* _
       st[1] = inv[r];
     }
   }
+}
+
+// SR = 65: 33,008 B of LDS, four blocks per CU (64-row stages, five blocks per CU, measured
+// neutral: profiles/r3_ab_segsum_ua.txt)
+// ctx_b (optional): ctx rounded to bf16 as well (the att_fc1 GEMM's operand)
+template <int SR>
+__global__ __launch_bounds__(256) void user_attn_fwd_mfma4_kernel(const float* __restrict__ qkv,
+                                                                  float* __restrict__ ctx, float* __restrict__ stats,
+                                                                  int H, int NH, const int* __restrict__ keep,
+                                                                  bf16* __restrict__ ctx_b) {
+  __shared__ __attribute__((aligned(16))) float qs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float ks[SR][DK];
+  __shared__ __attribute__((aligned(16))) float vs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int ld = 3 * NH * DK, D = NH * DK;
+  const float* base = qkv + (size_t)b * H * ld + h * DK;
+  {  // 3 x 320 float4 chunks over 256 threads, every load in flight before the stores
+    float4 v[3][2];
+#pragma unroll
+    for (int o = 0; o < 3; ++o)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int i = tid + 256 * it;
+        const int r = min(min(i, 319) / (DK / 4), H - 1), c = (i % (DK / 4)) * 4;
+        v[o][it] = *(const float4*)(base + (size_t)o * D + (size_t)r * ld + c);
+      }
+    float (*const xs[3])[DK] = {qs, ks, vs};
+#pragma unroll
+    for (int o = 0; o < 3; ++o)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int i = tid + 256 * it;
+        const int r = i / (DK / 4), c = (i - r * (DK / 4)) * 4;
+        const bool z = r >= H;
+        const float4 w = make_float4(z ? 0.f : v[o][it].x, z ? 0.f : v[o][it].y, z ? 0.f : v[o][it].z,
+                                     z ? 0.f : v[o][it].w);
+        if (i < 320) *(float4*)&xs[o][r][c] = w;
+      }
+  }
+  __syncthreads();
+  attn_fwd_body(qs, ks, vs, ps, b, h, H, NH, keep, ctx, stats, ctx_b);
+}
+
+// Q|K|V projection fused into the attention forward (H <= 64, bf16 operands): the block of
+// (b, h) computes its head's [H x 3 DK] slice of X' W^T + bias -- X' = the impression's H
+// gathered, dropped-out history rows (bf16 [B H, Din]), W = the bf16 stack [Wq; Wk; Wv]
+// (rows o D + h DK + c) -- on v_mfma_f32_16x16x32_bf16 with the fragments loaded straight into
+// registers (small_gemm.hip's register-direct form: 4 waves in 2 x 2 over the 64 x 64 padded
+// tile, 3 k-steps in flight, B as src0 so a lane holds 4 consecutive output columns), puts it
+// in LDS (rows >= H zero) and in qkv [B H, 3 D] fp32 (the backward's input), and runs the
+// attention on it.  The separate GEMM launch wrote the same qkv (same MFMA, same k order): one
+// launch and the qkv read-back fewer per step.
+constexpr uint32_t QA_OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t qa_rsrc(const void* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
+}
+
+template <int SR>
+__global__ __launch_bounds__(256) void user_qkv_attn_fwd_kernel(const bf16* __restrict__ xd,
+                                                                const bf16* __restrict__ W,
+                                                                const float* __restrict__ bias, int Din,
+                                                                float* __restrict__ qkv, float* __restrict__ ctx,
+                                                                float* __restrict__ stats, int H, int NH,
+                                                                const int* __restrict__ keep,
+                                                                bf16* __restrict__ ctx_b) {
+  __shared__ __attribute__((aligned(16))) float qs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float ks[SR][DK];
+  __shared__ __attribute__((aligned(16))) float vs[SR][DK];
+  __shared__ __attribute__((aligned(16))) float ps[64 * PLD];
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x / NH, h = blockIdx.x - b * NH;
+  const int D = NH * DK;
+  const int wm = wave >> 1, wn = wave & 1;
+  const __amdgpu_buffer_rsrc_t rsa = qa_rsrc(xd), rsb = qa_rsrc(W);
+  uint32_t oa[2], ob[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = wm * 32 + i * 16 + fr;  // history row of this impression
+    oa[i] = m < H ? (uint32_t)(((size_t)b * H + m) * Din + 8 * fq) * 2u : QA_OOB;
+    const int n = wn * 32 + i * 16 + fr;  // output column: o = n / DK (q, k, v), c = n % DK
+    ob[i] = n < 3 * DK ? (uint32_t)(((n / DK) * D + h * DK + n % DK) * Din + 8 * fq) * 2u : QA_OOB;
+  }
+  constexpr int P = 3;
+  const int nk = (Din + 31) >> 5;
+  u32x4_t ra[P][2], rb[P][2];
+  auto load = [&](int s, int kt) {
+    const bool kok = kt * 32 + 8 * fq < Din;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ra[s][i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsa, kok ? oa[i] + kt * 64 : QA_OOB, 0, 0));
+      rb[s][i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsb, kok ? ob[i] + kt * 64 : QA_OOB, 0, 0));
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, rb[s][j]),
+                                                            __builtin_bit_cast(bf16x8, ra[s][i]), acc[i][j], 0, 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < P; ++s) load(s, s);
+  const int nfull = nk / P * P;
+  for (int kt = 0; kt < nfull; kt += P) {
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      mma(s);
+      load(s, kt + s + P);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < P - 1; ++s)
+    if (nfull + s < nk) mma(s);
+  // lane holds C[m = wm 32 + 16 i + fr][n = wn 32 + 16 j + 4 fq + r]: 4 consecutive columns of one
+  // of q / k / v (DK % 4 == 0)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = wn * 32 + j * 16 + 4 * fq;
+    if (n >= 3 * DK) continue;
+    const int o = n / DK, c = n - o * DK;
+    float (*const xo)[DK] = o == 0 ? qs : (o == 1 ? ks : vs);
+    const float4 bb = *(const float4*)(bias + o * D + h * DK + c);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = wm * 32 + i * 16 + fr;
+      if (m >= SR) continue;
+      const bool real = m < H;
+      const float4 v = real ? make_float4(acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z,
+                                          acc[i][j][3] + bb.w)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      *(float4*)&xo[m][c] = v;
+      if (real) *(float4*)(qkv + ((size_t)b * H + m) * (3 * D) + o * D + h * DK + c) = v;
+    }
+  }
+  __syncthreads();
+  attn_fwd_body(qs, ks, vs, ps, b, h, H, NH, keep, ctx, stats, ctx_b);
 }
 
 // Backward LDS: 38,208 B with PLDB = 68 and 65-row stages -- four blocks per CU.  P and dS share
@@ -665,6 +783,22 @@ extern "C" int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int 
   else
     hipLaunchKernelGGL(user_attn_fwd_mfma4_kernel<65>, dim3(pairs), dim3(256), 0, s, qkv, ctx, stats, H, NH, keep,
                        (bf16*)ctx_b);
+  return 0;
+}
+
+// Q|K|V projection + attention forward in one launch (H <= 64; 1 = not this form's shape, nothing
+// launched): xd bf16 [B H, Din], W bf16 [3 NH dk, Din] (the q / k / v row blocks), bias fp32
+// [3 NH dk]; qkv [B H, 3 NH dk] fp32 is written for the backward
+extern "C" int fr_user_qkv_attn_fwd(const void* xd, const void* W, const float* bias, int Din, float* qkv, float* ctx,
+                                    float* stats, int B, int H, int NH, int dk, const int* keep, hipStream_t s,
+                                    void* ctx_b) {
+  if (dk != DK || H > MAXH || H < 1 || Din % 8 != 0 || Din < 8) return 1;
+  if ((((uintptr_t)xd) & 15) || (((uintptr_t)W) & 15) || (((uintptr_t)bias) & 15) || (((uintptr_t)qkv) & 15)) return 1;
+  if ((double)B * H * Din * 2 >= 2.0e9 || (double)3 * NH * DK * Din * 2 >= 2.0e9) return 1;  // 32-bit buffer offsets
+  const int pairs = B * NH;
+  if (pairs == 0) return 0;
+  hipLaunchKernelGGL(user_qkv_attn_fwd_kernel<65>, dim3(pairs), dim3(256), 0, s, (const bf16*)xd, (const bf16*)W, bias,
+                     Din, qkv, ctx, stats, H, NH, keep, (bf16*)ctx_b);
   return 0;
 }
 

@@ -148,7 +148,8 @@ class TextEncoder(nn.Module):
         ``tokens [N, 2, T]`` int32 masks padding tokens when ``mask_padding`` is on (Q7).
         ``nreal`` (device int32 [1]): titles past it are padding (pooled = 0, no gradient).
         ``w1b`` / ``fcb``: att_fc1's / fc's weight already cast to bf16 this step (one cast launch
-        per step); with ``fcb`` the pool also emits its rows in bf16 for the fc GEMMs."""
+        per step; ``fcb`` may be the pair (fc, fc^T)); with ``fcb`` the pool also emits its rows in
+        bf16 for the fc GEMMs."""
         aa = self.additive_attention
         tok = tokens if self.cfg.mask_padding else None
         pooled, pooled_b = OF.TextHeadFn.apply(aa.att_fc1.weight, aa.att_fc1.bias, aa.att_fc2.weight,
@@ -156,7 +157,8 @@ class TextEncoder(nn.Module):
                                                fcb is not None)
         if fcb is None:
             return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias)
-        return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias, pooled_b, fcb)
+        fcb, fcbt = fcb if isinstance(fcb, tuple) else (fcb, None)
+        return OF.HeadFCFn.apply(pooled, self.fc.weight, self.fc.bias, pooled_b, fcb, fcbt)
 
     def head(self, hidden: torch.Tensor, token_mask: torch.Tensor | None = None) -> torch.Tensor:
         """Trainable head: ``[n,T,D] -> [n,400]`` (fp32).  ``token_mask [n,T]`` excludes padding

@@ -175,6 +175,14 @@ def user_attention_fwd(qkv, heads: int, head_dim: int, keep=None, ctx_b=None):
     return out
 
 
+def user_qkv_attention_fwd(xd, W, bias, B: int, heads: int, head_dim: int, keep=None, ctx_b=None):
+    """Q|K|V projection + attention forward in one launch (device only, H <= 64): ``xd [B*H, Din]``
+    bf16, ``W [3*heads*head_dim, Din]`` bf16, ``bias`` fp32 -> ``(ctx [B,H,D], saved, qkv [B,H,3D])``
+    -- the values of ``small_gemm(xd, W, +bias)`` followed by :func:`user_attention_fwd`."""
+    return tuple(native.require_for(xd).user_qkv_attention_fwd(xd, W, bias, int(B), heads, head_dim, _mask32(keep),
+                                                               ctx_b))
+
+
 def user_attention_bwd(qkv, saved, dctx, heads: int, head_dim: int, keep=None, bf16_out: bool = False):
     """-> ``dqkv`` like qkv (bf16 with ``bf16_out``: the gradient GEMMs' operand)."""
     if _dev(qkv):

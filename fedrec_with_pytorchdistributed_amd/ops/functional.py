@@ -11,6 +11,8 @@ from typing import Optional, Tuple
 
 import math
 
+import os
+
 import torch
 
 from .. import ops
@@ -486,18 +488,28 @@ class EmbedLNFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------------------
 
 
-def _user_weight_bufs(wts, dev):
-    """The user step's compute copies: the bf16 stack [Wq; Wk; Wv; W1] and the fp32 [bq | bk | bv]."""
+def _user_weight_bufs(wts, dev, transposed: bool = False):
+    """The user step's compute copies: the bf16 stack [Wq; Wk; Wv; W1], the fp32 [bq | bk | bv]
+    and (``transposed``) W1^T ``[D, Qd]`` bf16: the dctx GEMM's weight k-contiguous (the
+    register-direct small GEMM).  (The Q|K|V input gradient stays on the LDS-DMA ring over the
+    stored weight: register-direct on a cast W^T measured slower there.)"""
     wq, w1, D = wts[0], wts[6], wts[0].shape[1]
-    return (torch.empty(3 * wq.shape[0] + w1.shape[0], D, device=dev, dtype=torch.bfloat16),
+    bufs = (torch.empty(3 * wq.shape[0] + w1.shape[0], D, device=dev, dtype=torch.bfloat16),
             torch.empty(3 * wq.shape[0], device=dev, dtype=torch.float32))
+    if transposed:
+        bufs += (torch.empty(D, w1.shape[0], device=dev, dtype=torch.bfloat16),)
+    return bufs
 
 
-def _user_cast_lists(wts, wb, bqkv):
+def _user_cast_lists(wts, wb, bqkv, wbt=None):
     wq, bq, wk, bk, wv, bv, w1 = wts[:7]
     D, D3 = wq.shape[1], 3 * wq.shape[0]
-    return ([wq, wk, wv, w1, bq, bk, bv],
-            [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D], bqkv[2 * D:]])
+    src = [wq, wk, wv, w1, bq, bk, bv]
+    dst = [wb[:D], wb[D:2 * D], wb[2 * D:D3], wb[D3:], bqkv[:D], bqkv[D:2 * D], bqkv[2 * D:]]
+    if wbt is not None:  # a transposed view: the cast launch writes W1^T (multi_cast T segment)
+        src.append(w1)
+        dst.append(wbt.t())
+    return src, dst
 
 
 def _step_cast_weights(text_encoder, user_encoder):
@@ -509,26 +521,33 @@ def _step_cast_weights(text_encoder, user_encoder):
 
 
 def step_cast_buffers(text_encoder, user_encoder):
-    """The compute copies :func:`step_weight_casts` fills: ``(w1_bf16, (wb, bqkv), fc_bf16)``."""
+    """The compute copies :func:`step_weight_casts` fills: ``(w1_bf16, (wb, bqkv, wbt), (fc_bf16,
+    fc_bf16^T))`` -- the transposed copies are the input-gradient GEMMs' k-contiguous weights."""
     w, wf, wts = _step_cast_weights(text_encoder, user_encoder)
     w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
     fcb = torch.empty(wf.shape, device=w.device, dtype=torch.bfloat16)
-    return w1b, _user_weight_bufs(wts, w.device), fcb
+    fcbt = (torch.empty(wf.shape[1], wf.shape[0], device=w.device, dtype=torch.bfloat16) if SIDE_WGRAD else None)
+    return w1b, _user_weight_bufs(wts, w.device, transposed=True), (fcb, fcbt)
 
 
 def step_cast_lists(text_encoder, user_encoder, bufs):
     """``(sources, destinations)`` of the step's weight casts into ``bufs`` (step_cast_buffers)."""
     w, wf, wts = _step_cast_weights(text_encoder, user_encoder)
-    w1b, (wb, bqkv), fcb = bufs
-    src, dst = _user_cast_lists(wts, wb, bqkv)
-    return [w.detach(), wf.detach()] + [t.detach() for t in src], [w1b, fcb] + dst
+    w1b, (wb, bqkv, wbt), (fcb, fcbt) = bufs
+    src, dst = _user_cast_lists(wts, wb, bqkv, wbt)
+    src, dst = [w.detach(), wf.detach()] + [t.detach() for t in src], [w1b, fcb] + dst
+    if fcbt is not None:  # (the side-stream form's fc input gradient on W^T)
+        src.append(wf.detach())
+        dst.append(fcbt.t())
+    return src, dst
 
 
 def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     """Every compute copy a fused training step needs, in ONE cast launch: the text head's att_fc1
     weight in bf16 (the head_score operand), its fc weight in bf16 (the fc GEMMs' operand) and the
-    user encoder's bf16 weight stack + fp32 Q|K|V bias (the user step's GEMM operands).  Returns
-    ``(w1_bf16, (wb, bqkv), fc_bf16)``; the att_fc1 and user casts were a cast
+    user encoder's bf16 weight stack + fp32 Q|K|V bias (the user step's GEMM operands), with the
+    transposed copies of the user and fc weights.  Returns ``(w1_bf16, (wb, bqkv, wbt), (fc_bf16,
+    fc_bf16^T))``; the att_fc1 and user casts were a cast
     kernel each (4.7 + 6.2 us per step).  ``bump`` (int64 [1] device counter, optional): advanced
     by one in the same launch -- the step's dropout / noise offset (a torch ``add_`` of its own
     cost 4.8 us at the end of every step).  ``bump2``: a second counter advanced the same way (the
@@ -544,11 +563,43 @@ def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     return bufs
 
 
-# Weight-gradient GEMMs of the user backward held back to ride in a later launch of the same
-# backward (HeadFCFn's: one launch and one split-K reduce fewer per step); an autograd
-# end-of-backward callback runs whatever is still pending, so a backward without that launch
-# still gets its gradients.  The tensors they write are returned to autograd right away (the
-# optimizer / end_backward read them only after the whole backward was queued).
+# Weight-gradient GEMMs on a side stream.  Nothing in the rest of a backward reads a weight
+# gradient: the user encoder's (Q|K|V, att_fc1, the pool's w2) are final once the attention
+# backward ran, the text fc's once the per-news gradient is summed, while the main stream still
+# has the input gradients and the whole text-head backward (~150 us of the config-2 step) to go.
+# They are launched on a per-device side stream forked from the main stream at that point and
+# joined back by an autograd end-of-backward callback, so the optimizer (or the in-graph Adam,
+# or a gradient all-reduce) sees them complete; under HIP-graph capture the fork / join become
+# graph edges and the replay runs them concurrently with the head backward.  Their operands are
+# marked as used on the side stream (record_stream), so the allocator does not hand their memory
+# to the main stream before the side work is done.  Off by default (``FEDREC_SIDE_WGRAD=1``
+# turns it on): measured slower in the config-2 step graph -- steady 0.539-0.549 vs 0.491-0.494
+# ms (gpurun_out/r5q_*.log): the replay of a two-stream graph left ~80 us of device idle before
+# each step (the host's next-batch read waited for the graph), and the head backward kernels
+# slowed beside the weight-gradient GEMMs (head_pool_bwd2 27.5 -> 35.9 us).  Off, the user
+# encoder's weight gradients are held back to ride in the text fc's backward launch (one launch
+# and one split-K reduce fewer), as before.
+# Only inside :func:`side_wgrads` (the engine's training step, whose parameters have no
+# ``.grad`` when the backward starts): autograd then takes the returned tensors as they are.
+# With an existing ``.grad`` it would add the returned tensor into it on the main stream at
+# once -- before the side stream wrote it.
+# register-direct small-GEMM variants (csrc/small_gemm.hip tile codes 1000 + 10 f + P) per
+# call site, measured on the config-2 shapes in the step graph (profiles/r5n_sg_rd.jsonl); a
+# launch whose operands the form does not take falls back to the automatic choice
+RD_ATT_FC1 = 1002 if os.environ.get("FEDREC_SG_RD", "1") != "0" else 0  # 32 x 32 waves, 2 k-steps in flight
+RD_DCTX = 1004 if RD_ATT_FC1 else 0
+RD_FC_DGRAD = 1032 if RD_ATT_FC1 else 0
+
+# the user encoder's Q|K|V projection fused into the attention forward launch (user_attn.hip
+# user_qkv_attn_fwd_kernel); FEDREC_QKV_ATTN=0: the projection as its own small-GEMM launch (A/B)
+FUSED_QKV_ATTN = os.environ.get("FEDREC_QKV_ATTN", "1") != "0"
+
+_SIDE_STREAMS: dict = {}
+_SIDE_JOINS: set = set()
+_SIDE_DEPTH = [0]
+SIDE_WGRAD = os.environ.get("FEDREC_SIDE_WGRAD", "0") == "1"
+
+
 _PENDING_GEMMS: list = []
 
 
@@ -569,6 +620,59 @@ def take_pending_gemms(room: int) -> list:
     return gs
 
 
+def side_active() -> bool:
+    return SIDE_WGRAD and _SIDE_DEPTH[0] > 0
+
+
+class side_wgrads:
+    """Context: weight-gradient GEMMs of backwards run inside it go to the side stream."""
+
+    def __enter__(self):
+        _SIDE_DEPTH[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _SIDE_DEPTH[0] -= 1
+        return False
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def side_gemms(*gs, dev_off=None) -> None:
+    """Launch ``gs`` (one small_gemm launch) on the device's side stream after everything the
+    main stream has queued so far; the main stream waits for it at the end of the backward
+    (must be called from inside an autograd backward).  On the main stream, at once, outside
+    :class:`side_wgrads` or when SIDE_WGRAD is off."""
+    if not SIDE_WGRAD or _SIDE_DEPTH[0] == 0:
+        ops.small_gemm(*gs, dev_off=dev_off)
+        return
+    main = torch.cuda.current_stream(gs[0].A.device)
+    side = _side_stream(main.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        for g in gs:
+            for t in (g.A, g.B, g.C, g.bias, g.asum, g.gidx):
+                if t is not None:
+                    t.record_stream(side)
+        if dev_off is not None:
+            dev_off.record_stream(side)
+        ops.small_gemm(*gs, dev_off=dev_off)
+    key = (main.device, main.stream_id)
+    if key not in _SIDE_JOINS:
+        _SIDE_JOINS.add(key)
+
+        def join():
+            _SIDE_JOINS.discard(key)
+            main.wait_stream(side)
+
+        torch.autograd.Variable._execution_engine.queue_callback(join)
+
+
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None,
                   pool: bool = True):
     """Device user encoder forward over history rows ``src[idx]`` (``src [*, D]`` fp32, ``idx``
@@ -585,34 +689,41 @@ def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_
     D = src.shape[1]
     BH, D3, Qd = B * H, 3 * D, w1.shape[0]
     dev = src.device
+    wbt = None
     if casts is not None:  # the step's one cast launch made them already (step_weight_casts)
-        wb, bqkv = casts
+        wb, bqkv, *rest = casts
+        wbt = rest[0] if rest else None
     else:
         wb, bqkv = _user_weight_bufs(wts, dev)
         ops.native.require_for(src).multi_cast(*_user_cast_lists(wts, wb, bqkv))
     p, seed, off = drop
     xd = ops.gather_dropout(src, idx, p, seed, off, dev_off, bf16_out=True)
-    qkv = torch.empty(BH, D3, device=dev, dtype=torch.float32)
-    ops.small_gemm(ops.Gemm(xd, wb[:D3], qkv, BH, D3, D, D, D, D3, bias=bqkv))  # one N = 3D GEMM
-    q3 = qkv.view(B, H, D3)
     # the attention also writes ctx rounded to bf16 -- what the att_fc1 GEMM and dW1 would round
     # it to on their loads -- so both run as bf16 x bf16 launches (the LDS-DMA small GEMM)
     c3b = torch.empty(B, H, D, device=dev, dtype=torch.bfloat16)
-    c3, stats = ops.user_attention_fwd(q3, heads, hd, keep, c3b)
+    if FUSED_QKV_ATTN and H <= 64 and hd == 20 and D % 8 == 0:
+        # the Q|K|V projection inside the attention launch (the same MFMA products in the same k
+        # order as the GEMM launch it replaces; qkv still written for the backward)
+        c3, stats, q3 = ops.user_qkv_attention_fwd(xd, wb[:D3], bqkv, B, heads, hd, keep, c3b)
+    else:
+        qkv = torch.empty(BH, D3, device=dev, dtype=torch.float32)
+        ops.small_gemm(ops.Gemm(xd, wb[:D3], qkv, BH, D3, D, D, D, D3, bias=bqkv))  # one N = 3D GEMM
+        q3 = qkv.view(B, H, D3)
+        c3, stats = ops.user_attention_fwd(q3, heads, hd, keep, c3b)
     e = torch.empty(BH, Qd, device=dev, dtype=torch.float32)
-    ops.small_gemm(ops.Gemm(c3b, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1))
+    ops.small_gemm(ops.Gemm(c3b, wb[D3:], e, BH, Qd, D, D, D, Qd, bias=b1, act=1), tile=RD_ATT_FC1)
     e3 = e.view(B, H, Qd)
     if not pool:  # the caller runs the pool fused with the scores (UserStepFn)
-        return None, [q3, stats, c3, c3b, e3, None, wb, w2, xd]
+        return None, [q3, stats, c3, c3b, e3, None, wb, w2, xd, wbt]
     u, alpha = ops.additive_pool_fwd(c3, e3, w2, b2, keep)
-    return u, [q3, stats, c3, c3b, e3, alpha, wb, w2, xd]
+    return u, [q3, stats, c3, c3b, e3, alpha, wb, w2, xd, wbt]
 
 
 def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, pre=None,
                   defer: bool = False):
     """Backward of :func:`_user_enc_fwd` for ``du [B, D]``: the input gradient goes into ``dx
     [B*H, D]`` (the dropout backward in the dgrad epilogue) -> the ten weight gradients."""
-    q3, stats, c3, c3b, e3, alpha, wb, w2, xd = saved
+    q3, stats, c3, c3b, e3, alpha, wb, w2, xd, wbt = saved
     D = c3.shape[-1]
     BH, D3 = B * H, 3 * D
     Qd = wb.shape[0] - D3
@@ -636,13 +747,18 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
         dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
         dpre_b = dpre.to(torch.bfloat16)
     dpre2 = dpre.view(BH, Qd)
-    ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1,
-                            accumulate=True))  # += dpre W1
+    if wbt is not None:  # += dpre W1 on the k-contiguous W1^T [D, Qd]: the register-direct GEMM
+        ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wbt, dctx, BH, D, Qd, Qd, Qd, D, accumulate=True),
+                       tile=RD_DCTX)
+    else:
+        ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1,
+                                accumulate=True))  # += dpre W1
     dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep, True).view(BH, D3)
     p, seed, off = drop
     # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,
     # the dropout backward in its epilogue
     ekw = dict(pdrop=p, drop_on=3, drop_ld=D, seed=seed, offset=off) if p > 0 else {}
+    # (on a k-contiguous W^T the register-direct form measured slower here: 28.1 vs 26.5 us)
     dgrad = ops.Gemm(dqkv, wb[:D3], dx, BH, D, D3, D3, D, D, b_mode=1, **ekw)
     # weight gradients: [dWq; dWk; dWv] = [dQ|dK|dV]^T X' (one M = 3D GEMM; X' bf16) and dW1 =
     # dpre^T ctx (fp32 operands: the mixed-dtype kernel); the bias gradients (column sums of
@@ -662,15 +778,19 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
         dw2, db2 = dw2[0], db2[:1]
     if defer and dx.is_cuda:
         # the input gradient now (the news-gradient segment sum reads it next; bf16 x bf16: the
-        # LDS-DMA ring, unsplit), the weight gradients with the text fc's backward launch
+        # LDS-DMA ring, unsplit), the weight gradients on the side stream or held back for the
+        # text fc's backward launch (an end-of-backward callback runs them when no such launch comes)
         ops.small_gemm(dgrad, dev_off=dev_off)
-        _PENDING_GEMMS.clear()  # (left over only by a backward that raised: its tensors are gone)
-        _PENDING_GEMMS.extend(wg)
-        torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_gemms)
+        if side_active():
+            side_gemms(*wg)
+        else:
+            _PENDING_GEMMS.clear()  # (left over only by a backward that raised: its tensors are gone)
+            _PENDING_GEMMS.extend(wg)
+            torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_gemms)
     else:
         ops.small_gemm(dgrad, *wg, dev_off=dev_off)
     # every gradient returned as a fresh view: autograd keeps a returned gradient as .grad only
-    # when nothing else references it and clones it otherwise -- a held-back GEMM still holds
+    # when nothing else references it and clones it otherwise -- a side-stream GEMM still holds
     # gw1 / gb1 (its output), and a clone now would copy them before that GEMM wrote them
     return (gqkv[:D], gbqkv[:D], gqkv[D:2 * D], gbqkv[D:2 * D], gqkv[2 * D:], gbqkv[2 * D:], gw1.view_as(gw1),
             gb1.view_as(gb1), dw2.view(1, -1), db2.view(1))
@@ -817,7 +937,7 @@ class HeadFCFn(torch.autograd.Function):
     GEMM: forward NT, backward dgrad (NN), wgrad (TN) in one launch, bias gradient by colsum."""
 
     @staticmethod
-    def forward(ctx, x, w, b, xb=None, wb=None):
+    def forward(ctx, x, w, b, xb=None, wb=None, wbt=None):
         """``xb`` / ``wb`` (optional): x and w already rounded to bf16 (the pool's second output,
         the step's cast launch) -- the GEMMs round their fp32 operands to bf16 on the way into LDS
         anyway, so the products are the same, at half the bytes and on the bf16 fast path."""
@@ -828,12 +948,12 @@ class HeadFCFn(torch.autograd.Function):
         wg = wb if wb is not None else w
         y = torch.empty(n, N, device=x.device, dtype=torch.float32)
         ops.small_gemm(ops.Gemm(xg, wg, y, n, N, K, K, K, N, bias=b))
-        ctx.save_for_backward(xg, wg)
+        ctx.save_for_backward(xg, wg, wbt)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w, wt = ctx.saved_tensors
         n, K = x.shape
         N = w.shape[0]
         dy = dy.contiguous().float()
@@ -841,9 +961,17 @@ class HeadFCFn(torch.autograd.Function):
 
         dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
         db = torch.empty(N, device=x.device, dtype=torch.float32)
-        # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
-        # launch -- with the user encoder's weight gradients when its backward held them back
-        ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1),
-                       ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db),
-                       *take_pending_gemms(4))
-        return dx, dw, db, None, None
+        # the input gradient on the main stream (the head backward reads it next); the weight and
+        # bias gradient (dy's column sums, from the wgrad's dy tiles) on the side stream
+        wgrad = ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db)
+        if side_active():  # the input gradient here, the weight gradient on the side stream
+            if wt is not None:  # on the k-contiguous W^T [K, N]: the register-direct GEMM (dy fp32 A)
+                ops.small_gemm(ops.Gemm(dy, wt, dx, n, K, N, N, N, K), tile=RD_FC_DGRAD)
+            else:
+                ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1))
+            side_gemms(wgrad)
+        else:
+            # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
+            # launch -- with the user encoder's weight gradients when its backward held them back
+            ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1), wgrad, *take_pending_gemms(4))
+        return dx, dw.view_as(dw), db.view_as(db), None, None, None

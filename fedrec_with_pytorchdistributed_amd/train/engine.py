@@ -29,6 +29,7 @@ Two update schedules (Q3):
 from __future__ import annotations
 
 import collections
+import contextlib
 import math
 import os
 import time
@@ -545,7 +546,10 @@ class LocalEngine:
                 loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
                                           pre is not None and pre.padded, True, his,
                                           casts=casts[1] if casts is not None else None)
-            with obs.range("backward"):
+            # weight gradients beside the rest of the backward (fresh .grad: begin_backward above;
+            # a bucket reducer's per-gradient hooks would read them before the side stream ran)
+            side = OF.side_wgrads() if self.reducer is None else contextlib.nullcontext()
+            with obs.range("backward"), side:
                 loss.backward(self._seed_one())
             if casts is None:
                 self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)

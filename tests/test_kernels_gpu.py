@@ -172,6 +172,30 @@ def test_user_attention(dev, H):
     assert rel_err(dq, dq_ref) < (1e-5 if H <= 64 else 1e-4)
 
 
+@pytest.mark.parametrize("H,masked", [(50, False), (50, True), (17, False), (64, True), (1, False)])
+def test_user_qkv_attention_fused_matches_two_launches(dev, H, masked):
+    """The Q|K|V projection inside the attention launch equals the small-GEMM launch followed by
+    the attention launch bit for bit (same MFMA products, same k order): qkv, ctx, its bf16 copy
+    and the softmax stats; and the fp32 attention oracle on that qkv."""
+    B, NH, DK, Din = 9, 20, 20, 400
+    D3 = 3 * NH * DK
+    torch.manual_seed(H)
+    xd = torch.randn(B * H, Din, device=dev).to(torch.bfloat16)
+    W = (torch.randn(D3, Din, device=dev) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(D3, device=dev)
+    keep = (torch.rand(B, H, device=dev) > 0.3).to(torch.int32) if masked else None
+    cb1 = torch.empty(B, H, NH * DK, device=dev, dtype=torch.bfloat16)
+    ctx1, st1, qkv1 = ops.user_qkv_attention_fwd(xd, W, bias, B, NH, DK, keep, cb1)
+    qkv2 = torch.empty(B * H, D3, device=dev)
+    ops.small_gemm(ops.Gemm(xd, W, qkv2, B * H, D3, Din, Din, Din, D3, bias=bias))
+    cb2 = torch.empty_like(cb1)
+    ctx2, st2 = ops.user_attention_fwd(qkv2.view(B, H, D3), NH, DK, keep, cb2)
+    assert torch.equal(qkv1.view(-1), qkv2.view(-1))
+    assert torch.equal(ctx1, ctx2) and torch.equal(cb1, cb2) and torch.equal(st1, st2)
+    c_ref, _ = ref.user_attention_fwd(qkv2.view(B, H, D3), NH, DK, keep=keep)
+    assert rel_err(ctx1, c_ref) < 1e-5
+
+
 @pytest.mark.parametrize("T", [76, 300])
 def test_additive_pool_long_fp32(dev, T):
     """User-side pooling over long (untruncated, Q6) histories: the generic kernels."""
@@ -525,6 +549,28 @@ def test_multi_cast(dev):
              torch.empty(1000, device=dev)]
     assert native.lib().multi_cast(odd_s, odd_d)
     assert all(torch.equal(b, a.to(b.dtype)) for a, b in zip(odd_s, odd_d))
+
+
+def test_multi_cast_transposed_views(dev):
+    """Transposed bf16 views as cast destinations (the register-direct GEMMs' W^T copies): ragged
+    R / C, side by side in one stacked matrix, beside plain segments of the same launch, and
+    through copy_cast (a step graph's input launch)."""
+    ws = [torch.randn(400, 400, device=dev), torch.randn(200, 400, device=dev), torch.randn(37, 130, device=dev)]
+    stack = torch.full((400, 600), 7.0, device=dev, dtype=torch.bfloat16)
+    odd = torch.empty(130, 40, device=dev, dtype=torch.bfloat16)
+    plain_s, plain_d = torch.randn(1000, device=dev), torch.empty(1000, device=dev, dtype=torch.bfloat16)
+    dsts = [stack[:, :400].t(), stack[:, 400:].t(), odd[:, :37].t()]
+    assert native.lib().multi_cast([plain_s] + ws, [plain_d] + dsts)
+    assert torch.equal(plain_d, plain_s.to(torch.bfloat16))
+    assert torch.equal(stack[:, :400], ws[0].t().to(torch.bfloat16))
+    assert torch.equal(stack[:, 400:], ws[1].t().to(torch.bfloat16))
+    assert torch.equal(odd[:, :37], ws[2].t().to(torch.bfloat16))
+    stack.fill_(0)
+    a, b = torch.arange(10, device=dev, dtype=torch.int32), torch.empty(16, device=dev, dtype=torch.int32)
+    assert native.lib().copy_cast([a], [b], [-1], [plain_s] + ws[:2], [plain_d] + dsts[:2], None, None)
+    assert torch.equal(b[:10], a) and bool((b[10:] == -1).all())
+    assert torch.equal(stack[:, :400], ws[0].t().to(torch.bfloat16))
+    assert torch.equal(stack[:, 400:], ws[1].t().to(torch.bfloat16))
 
 
 @pytest.mark.gpu

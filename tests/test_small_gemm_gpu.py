@@ -238,3 +238,50 @@ def test_dma_ring_transposed_operands_and_asum(dev, a_mode, b_mode, MNK):
     if a_mode == 1:
         ref = A.double().sum(0)
         assert torch.allclose(sums[1].double(), ref, rtol=1e-5, atol=1e-3), float((sums[1].double() - ref).abs().max())
+
+
+# register-direct form (tile codes 1000 + 10 f + P, + 100 with split-K): bf16 B [N, K], bf16 or
+# fp32 A [M, K], the epilogue options of the step's launches, ragged M / N / K
+RD = [1002, 1003, 1004, 1012, 1013, 1023, 1033, 1103]
+
+
+@pytest.mark.parametrize("tile", RD)
+def test_rd_nt_bias_tanh(dev, tile):
+    torch.manual_seed(7)
+    a = torch.randn(3190, 392, device=dev).to(torch.bfloat16)
+    w = (torch.randn(203, 392, device=dev) * 0.05).to(torch.bfloat16)
+    b = torch.randn(203, device=dev)
+    C = torch.zeros(3190, 203, device=dev)
+    _check(Gemm(a, w, C, 3190, 203, 392, 392, 392, 203, bias=b, act=1), tile=tile)
+
+
+@pytest.mark.parametrize("tile", RD)
+def test_rd_dgrad_dropout_accumulate_strided_b(dev, tile):
+    torch.manual_seed(8)
+    dy = torch.randn(3200, 1200, device=dev).to(torch.bfloat16)
+    wt = (torch.randn(400, 1400, device=dev) * 0.05).to(torch.bfloat16)  # [W^T | more]: ldb 1400
+    C = torch.randn(3200, 400, device=dev)
+    _check(Gemm(dy, wt, C, 3200, 400, 1200, 1200, 1400, 400, accumulate=True, pdrop=0.2, drop_on=3, drop_ld=400,
+                seed=4, offset=6), tile=tile)
+    _check(Gemm(dy[:, :200], wt[:, 1200:], C, 3200, 400, 200, 1200, 1400, 400, accumulate=True), tile=tile)
+
+
+@pytest.mark.parametrize("tile", [1002, 1032, 1033])
+def test_rd_fp32_a(dev, tile):
+    torch.manual_seed(9)
+    dy = torch.randn(1565, 400, device=dev)
+    wt = (torch.randn(768, 400, device=dev) * 0.05).to(torch.bfloat16)
+    C = torch.zeros(1565, 768, device=dev)
+    _check(Gemm(dy, wt, C, 1565, 768, 400, 400, 400, 768), tile=tile)
+
+
+def test_rd_matches_lds_form_bitwise(dev):
+    """Same operands, same k order, same fp32 MFMA accumulation: the register-direct C equals the
+    LDS-DMA ring's bit for bit (the two forms are interchangeable per launch)."""
+    torch.manual_seed(10)
+    a = torch.randn(3200, 400, device=dev).to(torch.bfloat16)
+    w = (torch.randn(200, 400, device=dev) * 0.05).to(torch.bfloat16)
+    c1, c2 = torch.zeros(3200, 200, device=dev), torch.zeros(3200, 200, device=dev)
+    ops.small_gemm(Gemm(a, w, c1, 3200, 200, 400, 400, 400, 200), tile=1)
+    ops.small_gemm(Gemm(a, w, c2, 3200, 200, 400, 400, 400, 200), tile=1003)
+    assert torch.equal(c1, c2)
