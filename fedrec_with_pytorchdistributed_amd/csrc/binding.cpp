@@ -72,6 +72,8 @@ int fr_user_attn_fwd(const float* qkv, float* ctx, float* stats, int B, int H, i
                      hipStream_t s, void* ctx_b);
 int fr_user_qkv_attn_fwd(const void* xd, const void* W, const float* bias, int Din, float* qkv, float* ctx,
                          float* stats, int B, int H, int NH, int dk, const int* keep, hipStream_t s, void* ctx_b);
+int fr_user_attn_bwd_dctx(const float* qkv, const float* stats, const float* dctx, void* dqkv, const void* dpre,
+                          const void* w1t, int Qd, int B, int H, int NH, int dk, const int* keep, hipStream_t s);
 int fr_user_attn_bwd(const float* qkv, const float* stats, const float* dctx, void* dqkv, int B, int H, int NH,
                      int dk, const int* keep, hipStream_t s, int out_bf16);
 int fr_score_ce(const float* cand, const float* user, float* loss, float* scores, float* dcand, float* duser, int B,
@@ -856,6 +858,38 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> user_qkv_attention_fwd(const at::
                                 (int)head_dim, key_mask_ptr(keep, B, H, "user_qkv_attention_fwd"), cur_stream(), cb),
            "user_qkv_attention_fwd");
   return {ctx, stats, qkv};
+}
+
+// The attention backward with the additive pool's input-gradient GEMM fused in (user_attn.hip,
+// FD form): dctx = dctx_direct (read, not written) + dpre W1 per head slice; dpre bf16 [B*H, Qd],
+// w1t bf16 [D, Qd] (W1^T, the step's cast).  -> dqkv bf16 [B, H, 3D].  H <= 64.
+at::Tensor user_attention_bwd_dctx(const at::Tensor& qkv, const at::Tensor& stats, const at::Tensor& dctx,
+                                   const at::Tensor& dpre, const at::Tensor& w1t, int64_t heads, int64_t head_dim,
+                                   const c10::optional<at::Tensor>& keep) {
+  check_dev(qkv, "qkv");
+  check_dev(stats, "stats");
+  check_dev(dctx, "dctx");
+  check_dev(dpre, "dpre");
+  check_dev(w1t, "w1t");
+  const c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.dim() == 3 && qkv.is_contiguous(),
+              "fedrec::user_attention_bwd_dctx: fp32 contiguous qkv [B,H,3D]");
+  const int64_t B = qkv.size(0), H = qkv.size(1), D = heads * head_dim;
+  TORCH_CHECK(qkv.size(2) == 3 * D && H <= 64, "fedrec::user_attention_bwd_dctx: qkv width 3D, H <= 64");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() == B * heads * H * 2,
+              "fedrec::user_attention_bwd_dctx: stats");
+  TORCH_CHECK(dctx.scalar_type() == at::kFloat && dctx.is_contiguous() && dctx.numel() == B * H * D,
+              "fedrec::user_attention_bwd_dctx: fp32 contiguous dctx [B,H,D]");
+  TORCH_CHECK(dpre.scalar_type() == at::kBFloat16 && w1t.scalar_type() == at::kBFloat16 && dpre.is_contiguous() &&
+                  w1t.is_contiguous() && dpre.dim() == 2 && w1t.dim() == 2 && dpre.size(0) == B * H &&
+                  w1t.size(0) == D && w1t.size(1) == dpre.size(1),
+              "fedrec::user_attention_bwd_dctx: bf16 dpre [B*H, Qd], bf16 w1t [D, Qd]");
+  auto out = at::empty({B, H, 3 * D}, qkv.options().dtype(at::kBFloat16));
+  check_rc(fr_user_attn_bwd_dctx(qkv.data_ptr<float>(), stats.data_ptr<float>(), dctx.data_ptr<float>(), out.data_ptr(),
+                                 dpre.data_ptr(), w1t.data_ptr(), (int)dpre.size(1), (int)B, (int)H, (int)heads,
+                                 (int)head_dim, key_mask_ptr(keep, B, H, "user_attention_bwd_dctx"), cur_stream()),
+           "user_attention_bwd_dctx");
+  return out;
 }
 
 // bf16_out: dqkv in bf16 (the input / weight gradient GEMMs' operand)
@@ -1930,6 +1964,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("upool_bwd_da(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool bf16_out=False) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("additive_pool_bwd(Tensor x, Tensor e, Tensor alpha, Tensor w2, Tensor g, bool want_dx) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("user_attention_fwd(Tensor qkv, int heads, int head_dim, Tensor? keep=None, Tensor(a!)? ctx_b=None) -> (Tensor, Tensor)");
+  m.def("user_attention_bwd_dctx(Tensor qkv, Tensor stats, Tensor dctx, Tensor dpre, Tensor w1t, int heads, "
+        "int head_dim, Tensor? keep=None) -> Tensor");
   m.def("user_qkv_attention_fwd(Tensor xd, Tensor W, Tensor bias, int B, int heads, int head_dim, Tensor? keep=None, "
         "Tensor(a!)? ctx_b=None) -> (Tensor, Tensor, Tensor)");
   m.def("user_attention_bwd(Tensor qkv, Tensor stats, Tensor dctx, int heads, int head_dim, Tensor? keep=None, bool bf16_out=False) -> Tensor");
@@ -1992,6 +2028,7 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("upool_bwd_da", &upool_bwd_da);
   m.impl("user_attention_fwd", &user_attention_fwd);
   m.impl("user_qkv_attention_fwd", &user_qkv_attention_fwd);
+  m.impl("user_attention_bwd_dctx", &user_attention_bwd_dctx);
   m.impl("user_attention_bwd", &user_attention_bwd);
   m.impl("score_ce", &score_ce);
   m.impl("user_pool_score", &user_pool_score);

@@ -427,12 +427,22 @@ __global__ __launch_bounds__(256) void user_qkv_attn_fwd_kernel(const bf16* __re
 __device__ __forceinline__ float cvt_out(float v, float*) { return v; }
 __device__ __forceinline__ bf16 cvt_out(float v, bf16*) { return f2bf(v); }
 
-template <int SR, int PLDB, typename OT = float>
+// FD: the additive pool's input-gradient GEMM fused in -- dctx = dctx_direct + dpre W1 (dctx_direct
+// = alpha du from the pool's backward, in `dctx`; dpre bf16 [B H, Qd], W1^T bf16 [D, Qd]): the
+// block of (b, h) computes its [H x DK] slice of dpre W1 on v_mfma_f32_16x16x32_bf16 with the
+// fragments loaded straight into registers (wave w: rows 16 w.., both 16-column tiles of the
+// head's DK = 20 columns), adds it to the staged dctx_direct -- (acc + 0) + dctx_direct, the
+// small-GEMM epilogue's arithmetic, so the sum is bitwise the separate launch's -- and runs the
+// attention backward on it.  One launch (and the dctx round trip) fewer per step.
+template <int SR, int PLDB, typename OT = float, bool FD = false>
 __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* __restrict__ qkv,
                                                                   const float* __restrict__ stats,
                                                                   const float* __restrict__ dctx,
                                                                   OT* __restrict__ dqkv, int H, int NH,
-                                                                  const int* __restrict__ keep) {
+                                                                  const int* __restrict__ keep,
+                                                                  const bf16* __restrict__ dpre = nullptr,
+                                                                  const bf16* __restrict__ w1t = nullptr,
+                                                                  int Qd = 0) {
   __shared__ __attribute__((aligned(16))) float qs[SR][DK];
   __shared__ __attribute__((aligned(16))) float ks[SR][DK];
   __shared__ __attribute__((aligned(16))) float vs[SR][DK];
@@ -466,6 +476,65 @@ __global__ __launch_bounds__(256) void user_attn_bwd_mfma4_kernel(const float* _
                                      z ? 0.f : v[o][it].w);
         if (i < 320) *(float4*)&xs[o][r][c] = w;
       }
+  }
+  if constexpr (FD) {
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rsa = qa_rsrc(dpre), rsb = qa_rsrc(w1t);
+    const int m = wave * 16 + fr;
+    const uint32_t oa = m < H ? (uint32_t)(((size_t)b * H + m) * Qd + 8 * fq) * 2u : QA_OOB;
+    uint32_t ob[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = j * 16 + fr;
+      ob[j] = c < DK ? (uint32_t)((h * DK + c) * Qd + 8 * fq) * 2u : QA_OOB;
+    }
+    constexpr int P = 3;
+    const int nk = (Qd + 31) >> 5;
+    u32x4_t ra[P], rb[P][2];
+    auto load = [&](int sl, int kt) {
+      const bool kok = kt * 32 + 8 * fq < Qd;
+      ra[sl] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsa, kok ? oa + kt * 64 : QA_OOB, 0, 0));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        rb[sl][j] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsb, kok ? ob[j] + kt * 64 : QA_OOB, 0, 0));
+    };
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    auto mma = [&](int sl) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, rb[sl][j]),
+                                                         __builtin_bit_cast(bf16x8, ra[sl]), acc[j], 0, 0, 0);
+    };
+#pragma unroll
+    for (int sl = 0; sl < P; ++sl) load(sl, sl);
+    const int nfull = nk / P * P;
+    for (int kt = 0; kt < nfull; kt += P) {
+#pragma unroll
+      for (int sl = 0; sl < P; ++sl) {
+        mma(sl);
+        load(sl, kt + sl + P);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < P - 1; ++sl)
+      if (nfull + sl < nk) mma(sl);
+    __syncthreads();  // the staged dctx_direct rows are in LDS
+    // lane holds (dpre W1)[m][c = 16 j + 4 fq + r]
+    if (m < H) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = j * 16 + 4 * fq;
+        if (c < DK) {
+          float4 g = *(float4*)&gs[m][c];
+          g.x = (acc[j][0] + 0.f) + g.x;
+          g.y = (acc[j][1] + 0.f) + g.y;
+          g.z = (acc[j][2] + 0.f) + g.z;
+          g.w = (acc[j][3] + 0.f) + g.w;
+          *(float4*)&gs[m][c] = g;
+        }
+      }
+    }
   }
   const int i0 = wave * 16;
   const int NT = (H + 15) / 16;
@@ -799,6 +868,22 @@ extern "C" int fr_user_qkv_attn_fwd(const void* xd, const void* W, const float* 
   if (pairs == 0) return 0;
   hipLaunchKernelGGL(user_qkv_attn_fwd_kernel<65>, dim3(pairs), dim3(256), 0, s, (const bf16*)xd, (const bf16*)W, bias,
                      Din, qkv, ctx, stats, H, NH, keep, (bf16*)ctx_b);
+  return 0;
+}
+
+// The attention backward with the pool's dctx GEMM fused in (H <= 64, bf16 dqkv; 1 = not this
+// form's shape, nothing launched): dctx holds dctx_direct (read only), dpre bf16 [B H, Qd], w1t
+// bf16 [NH dk, Qd] (W1^T)
+extern "C" int fr_user_attn_bwd_dctx(const float* qkv, const float* stats, const float* dctx, void* dqkv,
+                                     const void* dpre, const void* w1t, int Qd, int B, int H, int NH, int dk,
+                                     const int* keep, hipStream_t s) {
+  if (dk != DK || H > MAXH || H < 1 || Qd % 8 != 0 || Qd < 8) return 1;
+  if ((((uintptr_t)dpre) & 15) || (((uintptr_t)w1t) & 15)) return 1;
+  if ((double)B * H * Qd * 2 >= 2.0e9) return 1;
+  const int pairs = B * NH;
+  if (pairs == 0) return 0;
+  hipLaunchKernelGGL((user_attn_bwd_mfma4_kernel<65, 68, bf16, true>), dim3(pairs), dim3(256), 0, s, qkv, stats, dctx,
+                     (bf16*)dqkv, H, NH, keep, (const bf16*)dpre, (const bf16*)w1t, Qd);
   return 0;
 }
 

@@ -183,6 +183,14 @@ def user_qkv_attention_fwd(xd, W, bias, B: int, heads: int, head_dim: int, keep=
                                                                ctx_b))
 
 
+def user_attention_bwd_dctx(qkv, saved, dctx, dpre, w1t, heads: int, head_dim: int, keep=None):
+    """Attention backward with the additive pool's input-gradient GEMM fused in (device only,
+    H <= 64): the attention's dctx is ``dctx + dpre @ w1t.T`` (``dctx`` read, not written; ``dpre
+    [B*H, Qd]`` and ``w1t [D, Qd]`` bf16) -> ``dqkv`` bf16 [B, H, 3D]."""
+    return native.require_for(qkv).user_attention_bwd_dctx(qkv.contiguous(), saved, dctx.contiguous(), dpre, w1t,
+                                                           heads, head_dim, _mask32(keep))
+
+
 def user_attention_bwd(qkv, saved, dctx, heads: int, head_dim: int, keep=None, bf16_out: bool = False):
     """-> ``dqkv`` like qkv (bf16 with ``bf16_out``: the gradient GEMMs' operand)."""
     if _dev(qkv):

@@ -590,8 +590,9 @@ RD_ATT_FC1 = 1002 if os.environ.get("FEDREC_SG_RD", "1") != "0" else 0  # 32 x 3
 RD_DCTX = 1004 if RD_ATT_FC1 else 0
 RD_FC_DGRAD = 1032 if RD_ATT_FC1 else 0
 
-# the user encoder's Q|K|V projection fused into the attention forward launch (user_attn.hip
-# user_qkv_attn_fwd_kernel); FEDREC_QKV_ATTN=0: the projection as its own small-GEMM launch (A/B)
+# the user encoder's Q|K|V projection fused into the attention forward launch and the additive
+# pool's input-gradient GEMM into the attention backward launch (user_attn.hip); FEDREC_QKV_ATTN=0:
+# both as their own small-GEMM launches (A/B)
 FUSED_QKV_ATTN = os.environ.get("FEDREC_QKV_ATTN", "1") != "0"
 
 _SIDE_STREAMS: dict = {}
@@ -747,13 +748,17 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
         dctx, dpre, dw2, db2 = ops.additive_pool_bwd(c3, e3, alpha, w2, du, True)
         dpre_b = dpre.to(torch.bfloat16)
     dpre2 = dpre.view(BH, Qd)
-    if wbt is not None:  # += dpre W1 on the k-contiguous W1^T [D, Qd]: the register-direct GEMM
-        ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wbt, dctx, BH, D, Qd, Qd, Qd, D, accumulate=True),
-                       tile=RD_DCTX)
+    if wbt is not None and FUSED_QKV_ATTN and H <= 64 and hd == 20:
+        # dctx += dpre W1 inside the attention backward launch (on the k-contiguous W1^T [D, Qd])
+        dqkv = ops.user_attention_bwd_dctx(q3, stats, dctx, dpre_b.view(BH, Qd), wbt, heads, hd, keep).view(BH, D3)
     else:
-        ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1,
-                                accumulate=True))  # += dpre W1
-    dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep, True).view(BH, D3)
+        if wbt is not None:  # += dpre W1 on W1^T: the register-direct GEMM
+            ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wbt, dctx, BH, D, Qd, Qd, Qd, D, accumulate=True),
+                           tile=RD_DCTX)
+        else:
+            ops.small_gemm(ops.Gemm(dpre_b.view(BH, Qd), wb[D3:], dctx, BH, D, Qd, Qd, D, D, b_mode=1,
+                                    accumulate=True))  # += dpre W1
+        dqkv = ops.user_attention_bwd(q3, stats, dctx, heads, hd, keep, True).view(BH, D3)
     p, seed, off = drop
     # dx = [dQ | dK | dV] [Wq; Wk; Wv] o Z: one GEMM with K = 3D over the bf16 weight stack,
     # the dropout backward in its epilogue

@@ -196,6 +196,29 @@ def test_user_qkv_attention_fused_matches_two_launches(dev, H, masked):
     assert rel_err(ctx1, c_ref) < 1e-5
 
 
+@pytest.mark.parametrize("H,masked", [(50, False), (50, True), (17, False), (64, True)])
+def test_user_attention_bwd_dctx_fused_matches_two_launches(dev, H, masked):
+    """The pool's input-gradient GEMM (dctx += dpre W1) inside the attention backward launch equals
+    the register-direct GEMM launch followed by the attention backward bit for bit, and leaves
+    dctx_direct unchanged."""
+    B, NH, DK, Qd = 9, 20, 20, 200
+    D = NH * DK
+    torch.manual_seed(H + 1)
+    qkv = torch.randn(B, H, 3 * D, device=dev)
+    keep = (torch.rand(B, H, device=dev) > 0.3).to(torch.int32) if masked else None
+    _, stats = ops.user_attention_fwd(qkv, NH, DK, keep)
+    dctx = torch.randn(B, H, D, device=dev)
+    dpre = torch.randn(B * H, Qd, device=dev).to(torch.bfloat16)
+    w1t = (torch.randn(D, Qd, device=dev) * 0.05).to(torch.bfloat16)
+    d0 = dctx.clone()
+    got = ops.user_attention_bwd_dctx(qkv, stats, dctx, dpre, w1t, NH, DK, keep)
+    assert torch.equal(dctx, d0)
+    d2 = dctx.clone()
+    ops.small_gemm(ops.Gemm(dpre, w1t, d2.view(B * H, D), B * H, D, Qd, Qd, Qd, D, accumulate=True), tile=1004)
+    want = ops.user_attention_bwd(qkv, stats, d2, NH, DK, keep, True)
+    assert torch.equal(got, want)
+
+
 @pytest.mark.parametrize("T", [76, 300])
 def test_additive_pool_long_fp32(dev, T):
     """User-side pooling over long (untruncated, Q6) histories: the generic kernels."""
