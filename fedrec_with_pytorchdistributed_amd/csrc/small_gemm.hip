@@ -1126,8 +1126,11 @@ static int rd_auto(const GemmBatch& b) {
 static long launch_rd(GemmBatch& b, int code, float* scratch, hipStream_t s) {
   const bool allow_split = (code / 100) % 10 != 0;
   const int f = (code / 10) % 10, P = code % 10;
-  const int FM = (f == 1 || f == 3) ? 4 : 2, FN = (f == 1 || f == 2) ? 4 : 2;
+  // f: 0 = 32 x 32 waves, 1 = 64 x 64, 2 = 32 x 64, 3 = 64 x 32 (16 x 16 / 16 x 32 / 32 x 16 wave
+  // tiles measured slower on every config-2 shape: profiles/r5_sg_rd_small_tiles.jsonl)
+  static const int FMS[4] = {2, 4, 2, 4}, FNS[4] = {2, 4, 4, 2};
   if (P < 2 || P > 4 || f > 3) return -7;
+  const int FM = FMS[f], FN = FNS[f];
   const int tm = 32 * FM, tn = 32 * FN;
   int tiles = 0, red_blocks = 0;
   long need = 0;
