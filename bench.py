@@ -222,6 +222,7 @@ def main() -> int:
         pre = next_batch()  # the batch of the step after this one (K prepares per K steps)
         host_step += h1 - h0
         host_next += time.perf_counter() - h1
+    waited = eng.host_wait_s - wait0  # read now: the round below adds its own waits
     sync()
     if ctx.initialized:
         dist.barrier(group=ctx.ctrl_group)
@@ -381,8 +382,8 @@ def main() -> int:
             # the device is the limit then); host_work = what the host itself spends per step
             "host_ms_per_step": {"launch": round(1000.0 * host_step / args.steps, 4),
                                  "next_batch": round(1000.0 * host_next / args.steps, 4),
-                                 "run_ahead_wait": round(1000.0 * (eng.host_wait_s - wait0) / args.steps, 4),
-                                 "host_work": round(1000.0 * (host_step + host_next - (eng.host_wait_s - wait0))
+                                 "run_ahead_wait": round(1000.0 * waited / args.steps, 4),
+                                 "host_work": round(1000.0 * (host_step + host_next - waited)
                                                     / args.steps, 4)},
             "cache_amortized_ms_per_step": round(1000.0 * amort / args.steps, 4),
             "fastest_rank_ms_per_step": round(1000.0 * fastest / args.steps, 3),
