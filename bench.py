@@ -213,22 +213,38 @@ def main() -> int:
     uniq = []  # unique titles per step (the backbone's work; it varies by batch and client)
     host_step = host_next = 0.0  # host time spent launching steps / preparing batches (diagnostic)
     wait0 = eng.host_wait_s  # ... of which blocked on the run-ahead bound (waiting for the device)
+    counts0 = dict(eng.counts)
+    # FEDREC_BENCH_EVENTS=1 (diagnostic, off by default): a timing event after every step's launch
+    # on the main stream -- where the device time of the timed window goes (start-up, per step, tail)
+    evs = [] if (os.environ.get("FEDREC_BENCH_EVENTS") == "1" and dev.type == "cuda") else None
+    if evs is not None:
+        evs.append(torch.cuda.Event(enable_timing=True))
+        evs[-1].record()
     for _ in range(args.steps):
         if pre.dedup is not None:
             uniq.append(int(pre.dedup[0].numel()))
         h0 = time.perf_counter()
         losses.append(step(pre))
         h1 = time.perf_counter()
+        if evs is not None:
+            evs.append(torch.cuda.Event(enable_timing=True))
+            evs[-1].record()
         pre = next_batch()  # the batch of the step after this one (K prepares per K steps)
         host_step += h1 - h0
         host_next += time.perf_counter() - h1
     waited = eng.host_wait_s - wait0  # read now: the round below adds its own waits
+    timed_kinds = {k: v - counts0.get(k, 0) for k, v in eng.counts.items()}  # graph replays / captures / eager
     sync()
     if ctx.initialized:
         dist.barrier(group=ctx.ctrl_group)
     sync()
     elapsed = time.perf_counter() - t0
     fastest = elapsed
+    if evs is not None:
+        iv = [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)]
+        print(json.dumps({"bench_events_ms": {"wall": round(1000.0 * elapsed, 4),
+                                               "device_first_to_last": round(evs[0].elapsed_time(evs[-1]), 4),
+                                               "per_step": [round(x, 4) for x in iv]}}), file=sys.stderr, flush=True)
     u_mean = float(np.mean(uniq)) if uniq else None
     if ctx.initialized:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -386,6 +402,7 @@ def main() -> int:
                                  "host_work": round(1000.0 * (host_step + host_next - waited)
                                                     / args.steps, 4)},
             "cache_amortized_ms_per_step": round(1000.0 * amort / args.steps, 4),
+            "timed_step_kinds": timed_kinds,
             "fastest_rank_ms_per_step": round(1000.0 * fastest / args.steps, 3),
             "unique_titles_per_step": None if u_mean is None else round(u_mean, 1),
             "grad_allreduce": None if ar is None else {"kind": ar.kind, "in_step_graph": bool(ar.capturable),

@@ -245,7 +245,8 @@ class LocalEngine:
         self.last_stats: Dict[str, float] = {}
         # step counters (tests / bench): graph replays, replays that ran the all-reduce + Adam
         # inside the graph, and optimizer steps issued eagerly from the host
-        self.counts = {"replays": 0, "replays_with_optimizer": 0, "eager_optimizer_steps": 0, "eager_steps": 0}
+        self.counts = {"replays": 0, "replays_with_optimizer": 0, "eager_optimizer_steps": 0, "eager_steps": 0,
+                       "captures": 0}
         self.host_wait_s = 0.0  # host time blocked on the run-ahead bound (_retire): the DEVICE is the limit
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
@@ -652,6 +653,7 @@ class LocalEngine:
                 self._adam_mirror = -1
             g = _StepGraph(self, pre, ucap, with_adam)
             self._graphs[key] = g
+            self.counts["captures"] += 1
         if not g.precast:
             g.load(pre, U)
         if g.hid_graph is not None:
