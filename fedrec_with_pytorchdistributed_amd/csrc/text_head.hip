@@ -1202,18 +1202,15 @@ __global__ __launch_bounds__(384) void head_pool_bwd3_kernel(const bf16* __restr
     if (tid == 0) db2p[u] = 0.f;
     return;
   }
-  // e rows of this title, in flight first
+  // e rows of this title: loaded once the X rows are consumed (their registers are dead by then;
+  // loading both at once took 141 VGPRs and halved the blocks in flight), in flight through the
+  // wave sums and the softmax backward
   const int EC = Q >> 3, EG = 384 / EC;
   const int ec = tid % EC, egr = tid / EC;
   const bool eact = egr < EG;
   const int eg = eact ? egr : 0;
   bf16* eu = e + (size_t)u * T * Q;
   bf16x8 ev[ETP];
-#pragma unroll
-  for (int i = 0; i < ETP; ++i) {
-    const int t = eg + EG * i;
-    ev[i] = *(const bf16x8*)(eu + (size_t)(t < T ? t : T - 1) * Q + ec * 8);
-  }
   const int id = ids != nullptr ? ids[u] : u;
   const bf16* xe = table + (size_t)id * T * D;
   const float* gu = g + (size_t)u * D;
@@ -1250,6 +1247,13 @@ __global__ __launch_bounds__(384) void head_pool_bwd3_kernel(const bf16* __restr
       }
     }
   }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < ETP; ++i) {
+    const int t = eg + EG * i;
+    ev[i] = *(const bf16x8*)(eu + (size_t)(t < T ? t : T - 1) * Q + ec * 8);
+  }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < TPW; ++i) s[i] = wave_sum(s[i]);
   if (lane == 0) {

@@ -186,7 +186,10 @@ class TextHeadFn(torch.autograd.Function):
 
 
 _HEAD_G: dict = {}
-_HEAD_G_FUSED = __import__("os").environ.get("FEDREC_HEAD_G_FUSED", "0") == "1"
+# pool backward + g rewrite in one launch (head_pool_bwd3, e loaded once the X rows are consumed):
+# 52.4 us vs 27.8 + 22.7 us + a launch boundary; steady 0.4458 / 0.4442 vs 0.4479 / 0.4466 ms
+# (A/B/A/B, 50 steps, gpurun_out/r5ad_*); FEDREC_HEAD_G_FUSED=0: the two launches
+_HEAD_G_FUSED = __import__("os").environ.get("FEDREC_HEAD_G_FUSED", "1") == "1"
 
 
 def _head_g_path(D: int, Q: int, T: int) -> bool:

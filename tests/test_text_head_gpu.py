@@ -279,3 +279,30 @@ def test_head_wgrad_g_matches_fp32(dev, U, padded):
     assert _rel(dw2, cs[0, :R].sum(0)) < 1e-5
     assert _rel(db1, cs[1, :R].sum(0) * w2) < 1e-5
     assert abs(float(db2) - float(db2p.sum())) < 1e-3
+
+
+@pytest.mark.parametrize("U,T,padded", [(1577, 50, True), (257, 50, False), (40, 17, False), (30, 100, True)])
+def test_head_pool_bwd_g_fused_matches_two_launches(dev, U, T, padded):
+    """head_pool_bwd_g (pool backward + the g rewrite of the title's e rows + its column partials
+    in one launch, e loaded after the X rows are consumed) against head_pool_bwd then
+    head_g_rewrite: same arithmetic in the same order -- da, db2p, g and the partials bitwise."""
+    g = torch.Generator(device="cpu").manual_seed(3 * U + T)
+    N, D, Q = 2000, 768, 384
+    lib = native.lib()
+    table = torch.randn(N * T, D, generator=g).to(dev, torch.bfloat16)
+    ids = torch.randint(1, N, (U,), generator=g, dtype=torch.int32)
+    R = U - 11 if padded else U
+    ids[R:] = 0
+    ids = ids.to(dev)
+    nreal = torch.tensor([R], dtype=torch.int32, device=dev) if padded else None
+    alpha = torch.softmax(torch.randn(U, T, generator=g), 1).to(dev)
+    gp = torch.randn(U, D, generator=g).to(dev)
+    e0 = torch.tanh(torch.randn(U * T, Q, generator=g)).to(dev, torch.bfloat16)
+    e1, e2 = e0.clone(), e0.clone()
+    da1, db1, cs1 = lib.head_pool_bwd_g(table, ids, T, alpha, gp, e1, nreal)
+    da2, db2 = lib.head_pool_bwd(table, ids, T, alpha, gp, nreal)
+    cs2 = lib.head_g_rewrite(da2, T, e2, nreal)
+    torch.cuda.synchronize()
+    assert torch.equal(da1, da2) and torch.equal(db1, db2)
+    assert torch.equal(e1, e2)
+    assert torch.equal(cs1, cs2)
