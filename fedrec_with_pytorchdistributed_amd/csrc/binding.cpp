@@ -56,7 +56,8 @@ int fr_head_pool_bwd_g(const void* table, const int* ids, const float* alpha, co
                        int Q, float* da, float* db2p, void* e, float* cs, const int* nreal, hipStream_t s);
 long fr_head_wgrad_g(const void* G, const void* table, const int* ids, const float* cs, const float* db2p,
                      const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2, float* db2,
-                     float* scratch, const int* nreal, hipStream_t s);
+                     float* scratch, const int* nreal, hipStream_t s, const void* pend, int pend_cblocks,
+                     int pend_total);
 int fr_head_g_rewrite(const float* da, int U, int T, int Q, void* e, float* cs, const int* nreal, hipStream_t s);
 void fr_head_wgrad_g_set_kt(int kt);
 int fr_ipc_create(long cap, void* handle_out);
@@ -133,6 +134,11 @@ int fr_secagg_mask_exact(const float* x, int* out, long n, const int* H, int W, 
 int fr_secagg_unmask_exact(const int* x, float* out, long n, const int* H, int W, hipStream_t s);
 long fr_small_gemm(const void* const* ptrs, const int* ints, const float* floats, const unsigned long long* seeds,
                    const unsigned long long* dev_off, int n, float* scratch, int tile, hipStream_t s);
+void fr_small_gemm_set_defer(int on);
+int fr_small_gemm_has_pending();
+int fr_small_gemm_batch_bytes();
+int fr_small_gemm_take_pending(void* dst, int dst_bytes, int* c_blocks, int* total);
+int fr_small_gemm_flush_pending(hipStream_t s);
 int fr_multi_cast(const float* const* src, void* const* dst, const long* n, const int* to_bf16, int nseg,
                   long long* bump, hipStream_t s, long long* bump2, const long* nsrc, const int* fill, int ntseg,
                   const float* const* tsrc, void* const* tdst, const int* tR, const int* tC, const int* tld);
@@ -692,6 +698,9 @@ at::Tensor head_g_rewrite(const at::Tensor& da, int64_t T, at::Tensor e, const c
   return cs;
 }
 
+// the partials of a deferred small-GEMM split-K reduction, held until the launch that reduces them
+static at::Tensor g_sg_pending_scratch;
+
 void head_wgrad_g_set_kt(int64_t kt) { fr_head_wgrad_g_set_kt((int)kt); }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad_g(const at::Tensor& table,
@@ -720,14 +729,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad_g(const at
   float* db2 = dw2 + Q;
   const long need = fr_head_wgrad_g(G.data_ptr(), table.data_ptr(), opt_int_ptr(ids), cs.data_ptr<float>(),
                                     db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
-                                    dW1.data_ptr<float>(), db1, dw2, db2, nullptr, nullptr, cur_stream());
+                                    dW1.data_ptr<float>(), db1, dw2, db2, nullptr, nullptr, cur_stream(), nullptr,
+                                    0, 0);
   TORCH_CHECK(need > 0, "fedrec::head_wgrad_g: unsupported shape");
   auto scratch = at::empty({need}, fopt);
+  // a deferred small-GEMM split-K reduction (the text FC backward's weight gradients) rides in
+  // the reduce launch; its partials stay alive until that launch is enqueued
+  std::vector<unsigned char> pend((size_t)fr_small_gemm_batch_bytes());
+  int pc = 0, pt = 0;
+  const bool has_pend = fr_small_gemm_take_pending(pend.data(), (int)pend.size(), &pc, &pt) != 0;
   check_rc((int)fr_head_wgrad_g(G.data_ptr(), table.data_ptr(), opt_int_ptr(ids), cs.data_ptr<float>(),
                                 db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
                                 dW1.data_ptr<float>(), db1, dw2, db2, scratch.data_ptr<float>(),
-                                opt_nreal(nreal, table), cur_stream()),
+                                opt_nreal(nreal, table), cur_stream(), has_pend ? pend.data() : nullptr, pc, pt),
            "head_wgrad_g");
+  if (has_pend) g_sg_pending_scratch = at::Tensor();
   return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
 }
 
@@ -1353,7 +1369,17 @@ void small_gemm(const std::vector<at::Tensor>& A, const c10::List<c10::optional<
     const long rc = fr_small_gemm(ptrs.data(), iv.data(), fv.data(), sv.data(), dop, (int)n,
                                   scratch.data_ptr<float>(), (int)tile, cur_stream());
     TORCH_CHECK(rc == 0, "fedrec::small_gemm: launch failed (code ", rc, ")");
+    if (fr_small_gemm_has_pending() && !g_sg_pending_scratch.defined()) g_sg_pending_scratch = scratch;
   }
+}
+
+// deferred split-K reductions (ops.functional.deferred_reduces): the next small-GEMM launch whose
+// split descs are all weight gradients leaves its reduction to the text head's reduce launch
+void small_gemm_set_defer(bool on) { fr_small_gemm_set_defer(on ? 1 : 0); }
+bool small_gemm_flush_pending() {
+  const bool had = fr_small_gemm_flush_pending(cur_stream()) != 0;
+  g_sg_pending_scratch = at::Tensor();
+  return had;
 }
 
 // column sums of fp32 matrices [M, N] (row stride ld) into out[N] (accumulate: out += sums)
@@ -1946,6 +1972,8 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("head_g_supported(int D, int Q, int T) -> bool", &head_g_supported);
   m.def("head_wgrad_g_set_kt(int kt) -> ()", &head_wgrad_g_set_kt);
   m.def("head_g_rewrite(Tensor da, int T, Tensor(a!) e, Tensor? nreal=None) -> Tensor");
+  m.def("small_gemm_set_defer(bool on) -> ()", &small_gemm_set_defer);
+  m.def("small_gemm_flush_pending() -> bool", &small_gemm_flush_pending);
   m.def("head_pool_bwd_g(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor(a!) e, Tensor? nreal=None) -> (Tensor, Tensor, Tensor)");
   m.def("head_wgrad_g(Tensor table, Tensor? ids, int T, Tensor G, Tensor cs, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("ipc_create(int cap) -> (int, Tensor)", &ipc_create);

@@ -34,43 +34,22 @@
 // cycles).  A register queue two k-tiles deep (SG_NQ = 2) measured slower on every launch of
 // the config-2 step, even the ones with fewer tiles than CUs (profiles/r3_ab_sg_nq2.txt).
 #include "common.h"
+#include "gemm_batch.h"
 
 #include <stdlib.h>
+#include <string.h>
 
 namespace {
 
 constexpr int TK = 64, LDT = TK + 8;  // LDS row stride 72 bf16 = 144 B
-constexpr int MAXG = 6;
+using fr_sg::GemmBatch;
+using fr_sg::GemmDesc;
+using fr_sg::MAXG;
 #ifndef SG_NQ
 #define SG_NQ 1
 #endif
 
-struct GemmDesc {
-  const void* A;
-  const int* gidx;  // row gather of A (gather_on 1, a_mode 0) or of B (gather_on 2, b_mode 1)
-  const void* B;
-  const void* B2;  // K-segmented B (b_mode 1): rows [kseg, 2 kseg) from B2, [2 kseg, 3 kseg) from B3
-  const void* B3;
-  const float* bias;
-  float* C;
-  float* P;  // split-K partials [splits, M, N] (splits > 1: the reduce kernel does the epilogue)
-  float* asum;  // optional (a_mode 1): asum[m] = sum_k A(m, k) in fp32 -- a weight gradient's bias
-  float* AP;    // gradient dY^T 1 from the dY tiles the GEMM streams; partials [splits, M] if split
-  int M, N, K, lda, ldb, ldc;
-  int a_mode, b_mode, act, accumulate;
-  float alpha, pdrop;
-  int drop_ld, drop_on, gather_on, tiles_n, tile_base, splits, kchunk, kseg;
-  int a_bf16, b_bf16;
-  int red_base;   // first block of this desc's split-K reduction
-  int ared_base;  // first block of its asum partial reduction (split asum descs)
-  unsigned long long seed, offset;  // offset += *dev_off when dev_off is set (graph replays)
-};
 
-struct GemmBatch {
-  GemmDesc d[MAXG];
-  const unsigned long long* dev_off;  // per-launch device counter added to the dropout offsets
-  int n;
-};
 
 // 16 consecutive elements -> raw register bits (fp32: 16 words; bf16: 8 words, 2 per word)
 __device__ __forceinline__ void load16_f32(const float* __restrict__ p, int valid, uint32_t (&v)[16]) {
@@ -868,69 +847,35 @@ __global__ __launch_bounds__(256) void small_gemm_rd_kernel(const GemmBatch batc
 // N % 4 == 0 for every split desc (host-checked); C / bias / accumulate fall back to scalar
 // accesses when a row of C is not 16-byte aligned.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batch, int c_blocks) {
-  if ((int)blockIdx.x >= c_blocks) {  // the asum partials of split descs: asum[m] = sum_s AP[s][m]
-    int ai = -1;
-#pragma unroll
-    for (int i = 0; i < MAXG; ++i)
-      if (i < batch.n && batch.d[i].AP != nullptr && (int)blockIdx.x >= batch.d[i].ared_base) ai = i;
-    if (ai < 0) return;
-    const GemmDesc& a = batch.d[ai];
-    const int m = (blockIdx.x - a.ared_base) * 256 + threadIdx.x;
-    if (m >= a.M) return;
-    float v = a.AP[m];
-    for (int sp = 1; sp < a.splits; ++sp) v += a.AP[(size_t)sp * a.M + m];
-    a.asum[m] = v;
+  fr_sg::splitk_reduce_block(batch, c_blocks, (int)blockIdx.x);
+}
+
+// Deferred split-K reduction (fr_small_gemm_set_defer): a launch whose split descs are all
+// weight gradients (a_mode 1: read only by the optimizer) leaves its reduction pending instead
+// of launching it; the text head's tail reduce (fr_head_wgrad_g) takes it and runs it in extra
+// blocks of its own launch, or fr_small_gemm_flush_pending launches it alone.  One pending
+// reduction at a time (a second deferrable launch reduces at once).
+bool g_defer = false;
+struct PendingReduce {
+  GemmBatch b;
+  int c_blocks, total;
+  bool set;
+};
+PendingReduce g_pend = {};
+
+void finish_reduce(const GemmBatch& b, int c_blocks, int total, hipStream_t s) {
+  if (total <= 0) return;
+  bool deferrable = g_defer && !g_pend.set;
+  for (int i = 0; i < b.n && deferrable; ++i)
+    if (b.d[i].splits > 1 && b.d[i].a_mode != 1) deferrable = false;
+  if (deferrable) {
+    g_pend.b = b;
+    g_pend.c_blocks = c_blocks;
+    g_pend.total = total;
+    g_pend.set = true;
     return;
   }
-  int gi = 0;
-#pragma unroll
-  for (int i = 1; i < MAXG; ++i)
-    if (i < batch.n && batch.d[i].splits > 1 && (int)blockIdx.x >= batch.d[i].red_base) gi = i;
-  const GemmDesc& g = batch.d[gi];
-  if (g.splits <= 1) return;
-  const long q = (long)(blockIdx.x - g.red_base) * 256 + threadIdx.x;
-  const long MN = (long)g.M * g.N;
-  const long e = 4 * q;
-  if (e >= MN) return;
-  const int m = (int)(e / g.N), n = (int)(e - (long)m * g.N);
-  float4 sum = *(const float4*)(g.P + e);
-  for (int sp = 1; sp < g.splits; ++sp) {
-    const float4 t = *(const float4*)(g.P + (size_t)sp * MN + e);
-    sum.x += t.x; sum.y += t.y; sum.z += t.z; sum.w += t.w;
-  }
-  float v[4] = {sum.x, sum.y, sum.z, sum.w};
-  float sc[4] = {1.f, 1.f, 1.f, 1.f};
-  if (g.drop_on == 3) {  // as the single-pass epilogue: elements (m, n..n+3) of the dropped input
-    const unsigned long long off = g.offset + (batch.dev_off ? *batch.dev_off : 0ull);
-    const uint4 x = Philox::gen(g.seed, off, ((unsigned long long)m * g.drop_ld + n) >> 2);
-    const float inv_keep = 1.0f / (1.0f - g.pdrop);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sc[r] = drop_scale(u4_get(x, r), g.pdrop, inv_keep);
-  }
-  float* c = g.C + (size_t)m * g.ldc + n;
-  const bool vec = ((uintptr_t)c & 15) == 0;
-  float cv[4] = {0.f, 0.f, 0.f, 0.f};
-  if (g.accumulate) {
-    if (vec) {
-      const float4 t = *(const float4*)c;
-      cv[0] = t.x; cv[1] = t.y; cv[2] = t.z; cv[3] = t.w;
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cv[r] = c[r];
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float x = g.alpha * v[r] + (g.bias ? g.bias[n + r] : 0.f);
-    if (g.act == 1) x = tanhf(x);
-    x *= sc[r];
-    v[r] = g.accumulate ? cv[r] + x : x;
-  }
-  if (vec)
-    *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
-  else
-#pragma unroll
-    for (int r = 0; r < 4; ++r) c[r] = v[r];
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(total), dim3(256), 0, s, b, c_blocks);
 }
 
 // Deterministic fp32 column sums (bias gradients), two passes: (1) blocks of CS_ROWS rows x
@@ -1176,7 +1121,7 @@ static long launch_rd(GemmBatch& b, int code, float* scratch, hipStream_t s) {
   else RD_P(4, 2);
 #undef RD_P
 #undef RD_LAUNCH
-  if (red_blocks > 0) hipLaunchKernelGGL(splitk_reduce_kernel, dim3(red_blocks), dim3(256), 0, s, b, red_blocks);
+  finish_reduce(b, red_blocks, red_blocks, s);
   return 0;
 }
 
@@ -1317,8 +1262,27 @@ extern "C" long fr_small_gemm(const void* const* ptrs, const int* ints, const fl
     if (d.splits > 1 && d.asum) ared_blocks += (d.M + 255) / 256;
   }
   if (red_blocks + ared_blocks > 0)
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(red_blocks + ared_blocks), dim3(256), 0, s, b, red_blocks);
+    finish_reduce(b, red_blocks, red_blocks + ared_blocks, s);
   return 0;
+}
+
+extern "C" void fr_small_gemm_set_defer(int on) { g_defer = on != 0; }
+extern "C" int fr_small_gemm_has_pending() { return g_pend.set ? 1 : 0; }
+extern "C" int fr_small_gemm_batch_bytes() { return (int)sizeof(GemmBatch); }
+// copies the pending reduction (GemmBatch + its block counts) out and clears it; 0 if none
+extern "C" int fr_small_gemm_take_pending(void* dst, int dst_bytes, int* c_blocks, int* total) {
+  if (!g_pend.set || dst_bytes < (int)sizeof(GemmBatch)) return 0;
+  memcpy(dst, &g_pend.b, sizeof(GemmBatch));
+  *c_blocks = g_pend.c_blocks;
+  *total = g_pend.total;
+  g_pend.set = false;
+  return 1;
+}
+extern "C" int fr_small_gemm_flush_pending(hipStream_t s) {
+  if (!g_pend.set) return 0;
+  g_pend.set = false;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g_pend.total), dim3(256), 0, s, g_pend.b, g_pend.c_blocks);
+  return 1;
 }
 
 // returns the scratch floats needed when part == nullptr (query mode), else launches

@@ -29,8 +29,10 @@
 //
 // Requirements (host-checked in binding.cpp): D % 256 == 0, Q in {128, 256, 384}, T <= 128.
 #include "common.h"
+#include "gemm_batch.h"
 
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -1112,12 +1114,23 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_kernel(const bf16* __restri
 // (fixed summation order: deterministic).  A block owns 64 float4 of dW1: its 4 waves sum the
 // split partials s = w, w+4, ... (independent 16-B loads in flight per lane), then wave 0 adds
 // the 4 wave sums in order.  Then Q/64 blocks do dw2 / db1 the same way, the last block db2.
+// PB: blocks from head_blocks on run a deferred small-GEMM split-K reduction (gemm_batch.h) --
+// the text FC backward's weight gradients, which nothing reads before the optimizer -- so that
+// reduction costs no launch of its own
+template <bool PB = false>
 __global__ __launch_bounds__(256) void head_reduce_kernel(const f32x4* __restrict__ P, const float* __restrict__ dw2p,
                                                           const float* __restrict__ dsump,
                                                           const float* __restrict__ db2p, const float* __restrict__ w2,
                                                           f32x4* __restrict__ dW1, float* __restrict__ db1,
                                                           float* __restrict__ dw2, float* __restrict__ db2, int S, int Q,
-                                                          int D, int U) {
+                                                          int D, int U, const fr_sg::GemmBatch pb = {},
+                                                          int pb_cblocks = 0, int head_blocks = 0) {
+  if constexpr (PB) {
+    if ((int)blockIdx.x >= head_blocks) {
+      fr_sg::splitk_reduce_block(pb, pb_cblocks, (int)blockIdx.x - head_blocks);
+      return;
+    }
+  }
   __shared__ f32x4 part[4][64];
   __shared__ float red[4];
   const long n4 = (long)Q * D / 4;
@@ -1762,8 +1775,8 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
   }
   const long n4 = (long)Q * D / 4;
   const long blocks = (n4 + 63) / 64 + (Q + 63) / 64 + 1;  // dW1 | dw2, db1 | db2
-  hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)P, dw2p, dsump,
-                     db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U);
+  hipLaunchKernelGGL(head_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)P, dw2p,
+                     dsump, db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U, fr_sg::GemmBatch{}, 0, 0);
   return 0;
 }
 
@@ -1812,7 +1825,10 @@ extern "C" void fr_head_wgrad_g_set_kt(int kt) { (void)kt; }  // one form left (
 // (the e buffer after the rewrite), cs its column partials.
 extern "C" long fr_head_wgrad_g(const void* G, const void* table, const int* ids, const float* cs, const float* db2p,
                                 const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2,
-                                float* db2, float* scratch, const int* nreal, hipStream_t s) {
+                                float* db2, float* scratch, const int* nreal, hipStream_t s,
+                                const void* pend, int pend_cblocks, int pend_total) {
+  // pend (optional): a deferred small-GEMM split-K reduction (fr_small_gemm_take_pending), run
+  // in pend_total extra blocks of the reduce launch
   if (!fr_head_g_supported(D, Q, T)) return -1;
   if (g_cus == 0) {
     int dev = 0;
@@ -1842,7 +1858,15 @@ extern "C" long fr_head_wgrad_g(const void* G, const void* table, const int* ids
   }
   const long n4 = (long)Q * D / 4;
   const long blocks = (n4 + 63) / 64 + (Q + 63) / 64 + 1;
-  hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)P, dw2p, dsump,
-                     db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U);
+  if (pend != nullptr && pend_total > 0) {
+    fr_sg::GemmBatch pb;
+    memcpy(&pb, pend, sizeof(pb));
+    hipLaunchKernelGGL(head_reduce_kernel<true>, dim3((unsigned)(blocks + pend_total)), dim3(256), 0, s,
+                       (const f32x4*)P, dw2p, dsump, db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U, pb,
+                       pend_cblocks, (int)blocks);
+  } else {
+    hipLaunchKernelGGL(head_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)P, dw2p,
+                       dsump, db2p, w2, (f32x4*)dW1, db1, dw2, db2, S, Q, D, U, fr_sg::GemmBatch{}, 0, 0);
+  }
   return 0;
 }

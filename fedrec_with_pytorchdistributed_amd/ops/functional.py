@@ -628,8 +628,24 @@ def side_active() -> bool:
     return SIDE_WGRAD and _SIDE_DEPTH[0] > 0
 
 
+# Deferred split-K reduction (inside side_wgrads, i.e. the engine's step without a bucket reducer:
+# no gradient hook reads a weight gradient before the backward ends).  The text fc's backward
+# launch (its input gradient + the fc and user-encoder weight gradients) leaves the split-K
+# reduction of its weight gradients pending, and the text head's reduce launch runs it in extra
+# blocks (csrc/text_head.hip head_reduce_kernel<true>): one launch fewer per step.  Whatever is
+# still pending when the context ends is reduced then.  FEDREC_DEFER_REDUCE=0: reduce at once.
+DEFER_REDUCE = os.environ.get("FEDREC_DEFER_REDUCE", "1") != "0"
+_DEFERRED = [False]
+
+
+def defer_active() -> bool:
+    return DEFER_REDUCE and _SIDE_DEPTH[0] > 0 and not SIDE_WGRAD
+
+
 class side_wgrads:
-    """Context: weight-gradient GEMMs of backwards run inside it go to the side stream."""
+    """Context: weight-gradient GEMMs of backwards run inside it go to the side stream (SIDE_WGRAD)
+    or leave their split-K reduction to a later launch (DEFER_REDUCE); on exit nothing is left
+    pending."""
 
     def __enter__(self):
         _SIDE_DEPTH[0] += 1
@@ -637,6 +653,9 @@ class side_wgrads:
 
     def __exit__(self, *exc):
         _SIDE_DEPTH[0] -= 1
+        if _SIDE_DEPTH[0] == 0 and _DEFERRED[0]:
+            _DEFERRED[0] = False
+            ops.native.lib().small_gemm_flush_pending()
         return False
 
 
@@ -981,5 +1000,15 @@ class HeadFCFn(torch.autograd.Function):
         else:
             # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
             # launch -- with the user encoder's weight gradients when its backward held them back
-            ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1), wgrad, *take_pending_gemms(4))
+            gs = (ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1), wgrad, *take_pending_gemms(4))
+            if defer_active():  # the weight gradients' split-K reduce rides in the head's reduce launch
+                lib = ops.native.require_for(dy)
+                lib.small_gemm_set_defer(True)
+                _DEFERRED[0] = True
+                try:
+                    ops.small_gemm(*gs)
+                finally:
+                    lib.small_gemm_set_defer(False)
+            else:
+                ops.small_gemm(*gs)
         return dx, dw.view_as(dw), db.view_as(db), None, None, None

@@ -64,8 +64,9 @@ def test_step_and_validation_use_only_our_kernels(dev, mask):
 
 def test_default_text_head_kernels(dev):
     """The default step runs the staged-wait form of head_score2 (SW = true) and the G path of the
-    backward (head_g_rewrite + the plain TN GEMM head_wgrad_g, not the round-4 head_wgrad with
-    its in-pipeline rewrite): guards the defaults of csrc/text_head.hip / ops.functional."""
+    backward (head_pool_bwd3: the pool backward with the g rewrite in the same launch, then the
+    plain TN GEMM head_wgrad_g -- not the round-4 head_wgrad with its in-pipeline rewrite, nor the
+    separate head_g_rewrite launch): guards the defaults of csrc/text_head.hip / ops.functional."""
     cfg = FedRecConfig(mode="grad_avg", batch_size=16)  # the headline backbone (Q = 384 head)
     torch.manual_seed(0)
     m = FedRecModel(cfg).to(dev)
@@ -82,8 +83,9 @@ def test_default_text_head_kernels(dev):
     names = _kernel_names(prof)
     hs = [n for n in names if "head_score2_kernel" in n]
     wg = [n for n in names if "head_wgrad_g_kernel" in n]
-    gr = [n for n in names if "head_g_rewrite_kernel" in n]
+    gr = [n for n in names if "head_pool_bwd3_kernel" in n]
     assert hs and wg and gr, sorted(set(n for n in names if "head" in n))
+    assert not [n for n in names if "head_g_rewrite_kernel" in n]  # fused into head_pool_bwd3
     assert not [n for n in names if "head_wgrad_kernel" in n]  # the round-4 form is off by default
     # bool template arguments: mangled "Lb1E" or demangled "true>" (the last template argument)
     assert all("Lb1EE" in n or n.split(">")[0].rstrip().endswith("true") for n in hs), sorted(set(hs))
