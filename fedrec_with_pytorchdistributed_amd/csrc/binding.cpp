@@ -83,6 +83,7 @@ int fr_segment_sum_rows(const float* rows, const int* perm, const int* seg_ptr, 
                         int R, float* scratch, hipStream_t s, int zero_empty);
 int fr_segsum_chunks(int R);
 void fr_segsum_set_variant(int v);
+void fr_segsum_set_ldp_block(int v);
 void fr_small_gemm_set_rd(int v);
 int fr_user_pool_score(const float* x, const float* e, const float* w2, const float* b2, const int* keep,
                        const float* cand, const int* ci, int B, int T, int D, int Q, int C, int sigm, float* lossb,
@@ -1939,6 +1940,7 @@ void title_attn_set_waves(int64_t w) { fr_title_attn_set_waves((int)w); }
 void title_attn_bwd_set_variant(int64_t v) { fr_title_attn_bwd_set_variant((int)v); }
 void score_set_variant(int64_t v) { fr_score_set_variant((int)v); }
 void segsum_set_variant(int64_t v) { fr_segsum_set_variant((int)v); }
+void segsum_set_ldp_block(int64_t v) { fr_segsum_set_ldp_block((int)v); }
 void small_gemm_set_rd(int64_t v) { fr_small_gemm_set_rd((int)v); }
 void head_score_set_rows(int64_t r) { fr_head_score_set_rows((int)r); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
@@ -1951,6 +1953,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("title_attn_bwd_set_variant(int v) -> ()", &title_attn_bwd_set_variant);
   m.def("score_set_variant(int v) -> ()", &score_set_variant);
   m.def("segsum_set_variant(int v) -> ()", &segsum_set_variant);
+  m.def("segsum_set_ldp_block(int v) -> ()", &segsum_set_ldp_block);
   m.def("small_gemm_set_rd(int v) -> ()", &small_gemm_set_rd);
   m.def("user_pool_score(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep, Tensor table, Tensor ci, int act, Tensor(a!) dcand_out, bool want_bwd) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("head_score_set_rows(int r) -> ()", &head_score_set_rows);

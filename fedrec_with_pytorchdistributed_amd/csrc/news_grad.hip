@@ -316,12 +316,102 @@ __global__ __launch_bounds__(256) void segsum_chunk4_kernel(const float4* __rest
   }
 }
 
+// LDP form of the float4 chunk pass with the clip + noise spread over a block: the transform of a
+// chunk's 16 occurrence rows (a row norm, 2 Philox draws + 4 Box-Muller pairs per lane) is the
+// bulk of the work, and one wave per chunk left it on ~220 waves for a config-2-sized batch
+// (29 us vs 9 for the plain pass).  Here one 256-thread block per chunk: wave w transforms rows
+// w, w + 4, ... into LDS, then wave 0 sums the runs exactly as segsum_chunk4_kernel<SC, true>
+// (same transform arithmetic, same summation order: bitwise the same partials and rows).
+template <int SC>
+__global__ __launch_bounds__(256) void segsum_chunk4_ldp_kernel(const float4* __restrict__ rows,
+                                                                const int* __restrict__ perm,
+                                                                const int* __restrict__ seg_ptr,
+                                                                const int* __restrict__ inv, float4* __restrict__ out,
+                                                                float4* __restrict__ scratch, int U, int R, int D4,
+                                                                float clip, float noise_std, unsigned long long seed,
+                                                                unsigned long long offset,
+                                                                const unsigned long long* __restrict__ dev_off) {
+  __shared__ float4 ls[SC][64 * MAXV4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x;
+  const int p0 = c * SC;
+  if (p0 >= R) return;
+  const int p1 = min(p0 + SC, R);
+  const unsigned long long off = offset + (dev_off != nullptr ? *dev_off : 0ull);
+#pragma unroll
+  for (int jj = 0; jj < SC / 4; ++jj) {
+    const int j = w + 4 * jj;
+    const int r = perm[min(p0 + j, p1 - 1)];
+    float4 v[MAXV4];
+#pragma unroll
+    for (int k = 0; k < MAXV4; ++k) {
+      const int d = lane + 64 * k;
+      v[k] = d < D4 ? rows[(size_t)r * D4 + d] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float f = 1.0f;
+    if (clip > 0.f) {
+      float sq = 0.f;
+#pragma unroll
+      for (int k = 0; k < MAXV4; ++k) sq += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+      f = fminf(1.0f, clip / (sqrtf(wave_sum(sq)) + 1e-12f));
+    }
+#pragma unroll
+    for (int k = 0; k < MAXV4; ++k) {
+      const int d = lane + 64 * k;
+      float4 nz = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (noise_std > 0.f && d < D4) {
+        const uint4 rnd = Philox::gen(seed, off, ((unsigned long long)r << 16) | (unsigned)d);
+        const float2 a = box_muller(rnd.x, rnd.y), b = box_muller(rnd.z, rnd.w);
+        nz = make_float4(a.x, a.y, b.x, b.y);
+      }
+      ls[j][d] = make_float4(v[k].x * f + noise_std * nz.x, v[k].y * f + noise_std * nz.y,
+                             v[k].z * f + noise_std * nz.z, v[k].w * f + noise_std * nz.w);
+    }
+  }
+  __syncthreads();
+  if (w != 0) return;
+  int u = inv[perm[p0]];  // segment of position p0
+  int s_beg = seg_ptr[u], s_end = seg_ptr[u + 1];
+  float4 acc[MAXV4];
+#pragma unroll
+  for (int k = 0; k < MAXV4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < SC; ++j) {
+    const int pp = p0 + j;
+    if (pp < p1) {
+#pragma unroll
+      for (int k = 0; k < MAXV4; ++k) {
+        const float4 t = ls[j][lane + 64 * k];
+        acc[k].x += t.x; acc[k].y += t.y; acc[k].z += t.z; acc[k].w += t.w;
+      }
+      if (pp + 1 == s_end || pp + 1 == p1) {  // flush the run of segment u
+        float4* dst;
+        if (s_beg >= p0 && s_end <= p1) dst = out + (size_t)u * D4;
+        else dst = scratch + ((size_t)c * 2 + (s_beg < p0 ? 0 : 1)) * D4;
+#pragma unroll
+        for (int k = 0; k < MAXV4; ++k) {
+          const int d = lane + 64 * k;
+          if (d < D4) dst[d] = acc[k];
+          acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (pp + 1 == s_end && pp + 1 < p1) {
+          ++u;
+          s_beg = s_end;
+          s_end = seg_ptr[u + 1];
+        }
+      }
+    }
+  }
+}
+
+int g_segsum_ldp_block = 1;  // 1: the block-per-chunk LDP pass (default); 0: one wave per chunk (A/B)
 int g_segsum_variant = 2;  // 2: chunked, float4 rows (default); 1: chunked, scalar; 0: one block per output row
 constexpr int SCH = 16;    // chunk length (8-occurrence chunks measured neutral, r3_ab_segsum_ua.txt)
 
 }  // namespace
 
 extern "C" void fr_segsum_set_variant(int v) { g_segsum_variant = v; }
+extern "C" void fr_segsum_set_ldp_block(int v) { g_segsum_ldp_block = v; }
 extern "C" int fr_segsum_chunks(int R) { return (R + SCH - 1) / SCH; }
 
 extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std,
@@ -348,8 +438,13 @@ extern "C" int fr_segment_sum_rows_ldp(const float* rows, const int* perm, const
       (((uintptr_t)rows | (uintptr_t)out | (uintptr_t)scratch) & 15) != 0 || (D / 4) > 65535)
     return 1;
   const int nch = (R + SCH - 1) / SCH;
-  hipLaunchKernelGGL((segsum_chunk4_kernel<SCH, true>), dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows, perm,
-                     seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4, clip, noise_std, seed, offset, dev_off);
+  if (g_segsum_ldp_block)
+    hipLaunchKernelGGL((segsum_chunk4_ldp_kernel<SCH>), dim3(nch), dim3(256), 0, s, (const float4*)rows, perm, seg_ptr,
+                       inv, (float4*)out, (float4*)scratch, U, R, D / 4, clip, noise_std, seed, offset, dev_off);
+  else
+    hipLaunchKernelGGL((segsum_chunk4_kernel<SCH, true>), dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows,
+                       perm, seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4, clip, noise_std, seed, offset,
+                       dev_off);
   hipLaunchKernelGGL(segsum_fix_kernel<SCH>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
   return 0;
 }

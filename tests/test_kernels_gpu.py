@@ -301,6 +301,30 @@ def test_segment_sum_skewed(dev, variant, R, D):
     assert rel_err(out, o_ref) < 1e-6
 
 
+@pytest.mark.parametrize("R,D", [(3521, 400), (37, 400), (16, 64), (2000, 512)])
+def test_segment_sum_ldp_block_form_matches_wave_form(dev, R, D):
+    """The LDP chunk pass with the clip + noise spread over a 256-thread block per chunk (default)
+    against the one-wave-per-chunk form: same transform, same summation order -- bitwise."""
+    g = torch.Generator().manual_seed(7 * R + D)
+    ids = torch.multinomial(1.0 / torch.arange(1, 600, dtype=torch.float64), R, replacement=True, generator=g)
+    ids[torch.rand(R, generator=g) < 0.3] = 0
+    ids = ids.to(torch.int32).to(dev)
+    uniq, inv, perm, ptr = ops.dedup(ids, 600)
+    rows = (torch.randn(R, D, generator=g) * 3).to(dev)
+    lib = native.lib()
+    outs = []
+    try:
+        for form in (0, 1):
+            lib.segsum_set_ldp_block(form)
+            outs.append(ops.segment_sum_rows(rows, inv, uniq.numel(), clip=2.0, noise_std=0.5, seed=11, offset=3,
+                                             seg=(perm, ptr)))
+    finally:
+        lib.segsum_set_ldp_block(1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[1]).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_ldp_noise_statistics(dev):
     R, D = 4096, 400
     rows = torch.zeros(R, D, device=dev)
