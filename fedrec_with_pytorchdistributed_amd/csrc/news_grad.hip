@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void segsum_chunk4_kernel(const float4* __rest
 // (29 us vs 9 for the plain pass).  Here one 256-thread block per chunk: wave w transforms rows
 // w, w + 4, ... into LDS, then wave 0 sums the runs exactly as segsum_chunk4_kernel<SC, true>
 // (same transform arithmetic, same summation order: bitwise the same partials and rows).
-template <int SC>
+template <int SC, bool LDP = true>
 __global__ __launch_bounds__(256) void segsum_chunk4_ldp_kernel(const float4* __restrict__ rows,
                                                                 const int* __restrict__ perm,
                                                                 const int* __restrict__ seg_ptr,
@@ -347,6 +347,11 @@ __global__ __launch_bounds__(256) void segsum_chunk4_ldp_kernel(const float4* __
     for (int k = 0; k < MAXV4; ++k) {
       const int d = lane + 64 * k;
       v[k] = d < D4 ? rows[(size_t)r * D4 + d] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if constexpr (!LDP) {  // plain sum (A/B form of segsum_chunk4_kernel<SC, false>): rows as loaded
+#pragma unroll
+      for (int k = 0; k < MAXV4; ++k) ls[j][lane + 64 * k] = v[k];
+      continue;
     }
     float f = 1.0f;
     if (clip > 0.f) {
@@ -405,13 +410,20 @@ __global__ __launch_bounds__(256) void segsum_chunk4_ldp_kernel(const float4* __
 }
 
 int g_segsum_ldp_block = 1;  // 1: the block-per-chunk LDP pass (default); 0: one wave per chunk (A/B)
+// the block-per-chunk form for the plain sum too (default): steady 0.4406 / 0.4431 vs 0.4430 /
+// 0.4433 ms (A/B/A/B, config 2, profiles/r5_ab_segsum_plain_block.jsonl) -- neutral to slightly
+// better, 29 instead of 161 VGPRs
+int g_segsum_plain_block = 1;
 int g_segsum_variant = 2;  // 2: chunked, float4 rows (default); 1: chunked, scalar; 0: one block per output row
 constexpr int SCH = 16;    // chunk length (8-occurrence chunks measured neutral, r3_ab_segsum_ua.txt)
 
 }  // namespace
 
 extern "C" void fr_segsum_set_variant(int v) { g_segsum_variant = v; }
-extern "C" void fr_segsum_set_ldp_block(int v) { g_segsum_ldp_block = v; }
+extern "C" void fr_segsum_set_ldp_block(int v) {  // bit 0: the LDP pass, bit 1: the plain pass (default 3)
+  g_segsum_ldp_block = v & 1;
+  g_segsum_plain_block = (v >> 1) & 1;
+}
 extern "C" int fr_segsum_chunks(int R) { return (R + SCH - 1) / SCH; }
 
 extern "C" int fr_ldp_rows(const float* rows, float* out, int R, int D, float clip, float noise_std,
@@ -456,9 +468,14 @@ extern "C" int fr_segment_sum_rows(const float* rows, const int* perm, const int
   if (g_segsum_variant == 2 && scratch != nullptr && inv != nullptr && R > 0 && D % 4 == 0 && D <= 256 * MAXV4 &&
       (((uintptr_t)rows | (uintptr_t)out | (uintptr_t)scratch) & 15) == 0) {
     const int nch = (R + SCH - 1) / SCH;
-    hipLaunchKernelGGL((segsum_chunk4_kernel<SCH, false>), dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows,
-                       perm, seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4, 0.f, 0.f, 0ull, 0ull,
-                       (const unsigned long long*)nullptr);
+    if (g_segsum_plain_block)
+      hipLaunchKernelGGL((segsum_chunk4_ldp_kernel<SCH, false>), dim3(nch), dim3(256), 0, s, (const float4*)rows, perm,
+                         seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4, 0.f, 0.f, 0ull, 0ull,
+                         (const unsigned long long*)nullptr);
+    else
+      hipLaunchKernelGGL((segsum_chunk4_kernel<SCH, false>), dim3((nch + 3) / 4), dim3(256), 0, s, (const float4*)rows,
+                         perm, seg_ptr, inv, (float4*)out, (float4*)scratch, U, R, D / 4, 0.f, 0.f, 0ull, 0ull,
+                         (const unsigned long long*)nullptr);
     hipLaunchKernelGGL(segsum_fix_kernel<SCH>, dim3(U), dim3(256), 0, s, seg_ptr, out, scratch, U, D);
     return 0;
   }

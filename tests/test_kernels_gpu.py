@@ -314,15 +314,20 @@ def test_segment_sum_ldp_block_form_matches_wave_form(dev, R, D):
     lib = native.lib()
     outs = []
     try:
-        for form in (0, 1):
+        for form in (2, 3):  # bit 0: the LDP pass on a block per chunk
             lib.segsum_set_ldp_block(form)
             outs.append(ops.segment_sum_rows(rows, inv, uniq.numel(), clip=2.0, noise_std=0.5, seed=11, offset=3,
                                              seg=(perm, ptr)))
-    finally:
+        lib.segsum_set_ldp_block(3)  # the block form for the plain (no LDP) pass as well (default)
+        plain_blk = ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr))
         lib.segsum_set_ldp_block(1)
+        plain = ops.segment_sum_rows(rows, inv, uniq.numel(), seg=(perm, ptr))
+    finally:
+        lib.segsum_set_ldp_block(3)
     torch.cuda.synchronize()
     assert torch.isfinite(outs[1]).all()
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(plain_blk, plain)
 
 
 def test_ldp_noise_statistics(dev):
