@@ -854,11 +854,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmBatch batc
 // weight gradients (a_mode 1: read only by the optimizer) leaves its reduction pending instead
 // of launching it; the text head's tail reduce (fr_head_wgrad_g) takes it and runs it in extra
 // blocks of its own launch, or fr_small_gemm_flush_pending launches it alone.  One pending
-// reduction at a time (a second deferrable launch reduces at once).
+// reduction at a time (a second deferrable launch reduces at once), process-wide: it is taken
+// only on the device it was deferred on, and the caller (ops/functional.py side_wgrads) defers
+// within one backward on one stream and flushes whatever is left when that backward ends.
 bool g_defer = false;
 struct PendingReduce {
   GemmBatch b;
   int c_blocks, total;
+  int device;
   bool set;
 };
 PendingReduce g_pend = {};
@@ -872,6 +875,8 @@ void finish_reduce(const GemmBatch& b, int c_blocks, int total, hipStream_t s) {
     g_pend.b = b;
     g_pend.c_blocks = c_blocks;
     g_pend.total = total;
+    g_pend.device = 0;
+    (void)hipGetDevice(&g_pend.device);
     g_pend.set = true;
     return;
   }
@@ -1272,6 +1277,9 @@ extern "C" int fr_small_gemm_batch_bytes() { return (int)sizeof(GemmBatch); }
 // copies the pending reduction (GemmBatch + its block counts) out and clears it; 0 if none
 extern "C" int fr_small_gemm_take_pending(void* dst, int dst_bytes, int* c_blocks, int* total) {
   if (!g_pend.set || dst_bytes < (int)sizeof(GemmBatch)) return 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != g_pend.device) return 0;  // another device's pending reduction: left for its flush
   memcpy(dst, &g_pend.b, sizeof(GemmBatch));
   *c_blocks = g_pend.c_blocks;
   *total = g_pend.total;
@@ -1281,6 +1289,15 @@ extern "C" int fr_small_gemm_take_pending(void* dst, int dst_bytes, int* c_block
 extern "C" int fr_small_gemm_flush_pending(hipStream_t s) {
   if (!g_pend.set) return 0;
   g_pend.set = false;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != g_pend.device) {  // (not a configuration the engine uses: one device per process)
+    (void)hipSetDevice(g_pend.device);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g_pend.total), dim3(256), 0, 0, g_pend.b, g_pend.c_blocks);
+    (void)hipDeviceSynchronize();
+    (void)hipSetDevice(dev);
+    return 1;
+  }
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g_pend.total), dim3(256), 0, s, g_pend.b, g_pend.c_blocks);
   return 1;
 }
