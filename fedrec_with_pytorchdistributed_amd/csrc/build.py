@@ -6,7 +6,8 @@
 * link with the system linker against torch's *own* ``libamdhip64`` (rpath to torch/lib),
   so the process holds exactly one HIP runtime.
 
-Incremental: objects are rebuilt only when a source or ``common.h`` is newer.
+Incremental: objects are rebuilt only when a source or any ``csrc/*.h`` header is newer (the
+headers carry layouts that several objects share, e.g. ``gemm_batch.h``).
 Usage: ``python -m fedrec_with_pytorchdistributed_amd.csrc.build [--force] [--verbose]``.
 
 ``--sanitize`` builds ``_C_san.so`` instead: the HOST code of every file
@@ -92,7 +93,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8, sanitize: b
     bdir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     tinc, tlib, abi = _torch_paths()
-    common = [HERE / "common.h"]
+    common = sorted(HERE.glob("*.h"))  # every shared header: a layout change rebuilds every object
     kernels = sorted(HERE.glob("*.hip"))
     jobs_list = []
     objs = []
@@ -107,7 +108,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8, sanitize: b
     bsrc = HERE / "binding.cpp"
     bobj = bdir / "binding.o"
     objs.append(bobj)
-    if force or _newer(bobj, [bsrc]):
+    if force or _newer(bobj, [bsrc, *common]):
         cxx, extra = ("g++", ["-O2"]) if not sanitize else (_clangxx(), ["-O1", *SAN, *SAN_CC,
                                                                           "-fno-omit-frame-pointer"])
         jobs_list.append([cxx, *extra, "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",

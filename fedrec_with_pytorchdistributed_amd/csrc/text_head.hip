@@ -1780,6 +1780,8 @@ extern "C" long fr_head_wgrad(const void* e, const void* table, const int* ids, 
   return 0;
 }
 
+extern "C" int fr_small_gemm_batch_bytes();  // small_gemm.hip
+
 // ---- the G path (round 5) -------------------------------------------------------------------
 extern "C" int fr_head_g_supported(int D, int Q, int T) {
   return Q == GQT && D % GKT == 0 && D <= 1024 && T >= 1 && T <= MAXT && fr_head_supported(D, Q, T);
@@ -1859,6 +1861,8 @@ extern "C" long fr_head_wgrad_g(const void* G, const void* table, const int* ids
   const long n4 = (long)Q * D / 4;
   const long blocks = (n4 + 63) / 64 + (Q + 63) / 64 + 1;
   if (pend != nullptr && pend_total > 0) {
+    // the descriptor was laid out by small_gemm.o: both objects must agree on GemmBatch
+    if (fr_small_gemm_batch_bytes() != (int)sizeof(fr_sg::GemmBatch)) return -2;
     fr_sg::GemmBatch pb;
     memcpy(&pb, pend, sizeof(pb));
     hipLaunchKernelGGL(head_reduce_kernel<true>, dim3((unsigned)(blocks + pend_total)), dim3(256), 0, s,

@@ -37,6 +37,10 @@ class CollectiveChecker:
     def record(self, op: str, t: Optional[torch.Tensor] = None, tag: str = "") -> None:
         if not self.enabled:
             return
+        # a call captured into a HIP graph runs once per REPLAY, not here: the replaying code
+        # records it (train/engine.py _graph_step); ranks capture different numbers of graphs
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return
         meta = f"{op}|{str(t.dtype).replace('torch.', '')}|{t.numel()}" if t is not None else op
         rec = f"{meta}|{tag}"
         self.count += 1

@@ -216,6 +216,12 @@ def probe_ipc_grad(ctx: DistContext, nelem: int, timeout_s: float = 600.0, check
     ipc = None
     ok = 1
     ms = [0.0, 0.0]
+
+    def _fail(e):  # pragma: no cover - depends on the node
+        if log is not None:
+            log(f"[client {ctx.client_index}] IPC all-reduce probe failed: {e!r}"[:400])
+        return 0
+
     try:
         ipc = make_ipc_allreduce(ctx, timeout_s=check_timeout_s, device_epoch=True)
         dev = ctx.device
@@ -225,24 +231,36 @@ def probe_ipc_grad(ctx: DistContext, nelem: int, timeout_s: float = 600.0, check
         ipc.allreduce_(b)
         torch.cuda.synchronize(dev)
         ok = int(ipc.status() == 0 and bool(torch.allclose(a, b, rtol=1e-5, atol=1e-5)))
-        for k, fn in enumerate((lambda x: ipc.allreduce_(x), lambda x: dist.all_reduce(x, group=ctx.data_group))):
-            if not ok:
-                break
-            fn(b)
-            torch.cuda.synchronize(dev)
-            dist.barrier(group=ctx.client_ctrl_group)
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                fn(b)
-            torch.cuda.synchronize(dev)
-            ms[k] = 1000.0 * (time.perf_counter() - t0) / reps
-        ok = int(ok and ipc.status() == 0)
     except Exception as e:  # pragma: no cover - depends on the node
-        ok = 0
-        if log is not None:
-            log(f"[client {ctx.client_index}] IPC all-reduce probe failed: {e!r}"[:400])
+        ok = _fail(e)
+    # agree on correctness BEFORE any timing collective: every client then runs the same sequence
+    # of control-group calls (a client that failed alone must not skip the barriers below)
     t = torch.tensor([ok], dtype=torch.int64)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.client_ctrl_group)
+    if int(t.item()):
+        for k, fn in enumerate((lambda x: ipc.allreduce_(x), lambda x: dist.all_reduce(x, group=ctx.data_group))):
+            try:
+                fn(b)
+                torch.cuda.synchronize(dev)
+            except Exception as e:  # pragma: no cover
+                ok = _fail(e)
+            dist.barrier(group=ctx.client_ctrl_group)
+            if not ok:
+                continue
+            try:
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    fn(b)
+                torch.cuda.synchronize(dev)
+                ms[k] = 1000.0 * (time.perf_counter() - t0) / reps
+            except Exception as e:  # pragma: no cover
+                ok = _fail(e)
+        try:
+            ok = int(ok and ipc.status() == 0)
+        except Exception as e:  # pragma: no cover
+            ok = _fail(e)
+        t = torch.tensor([ok], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.client_ctrl_group)
     tm = torch.tensor(ms, dtype=torch.float64)
     dist.all_reduce(tm, op=dist.ReduceOp.MAX, group=ctx.client_ctrl_group)
     info["ok"] = bool(t.item())

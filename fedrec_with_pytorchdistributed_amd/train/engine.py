@@ -46,6 +46,7 @@ from ..eval.metrics import batch_metrics
 from ..models.fedrec_model import FedRecModel
 from ..ops import functional as OF
 from ..ops import native
+from ..parallel.collcheck import CHECK
 from ..utils import obs
 from .news_cache import HiddenCache
 
@@ -233,6 +234,7 @@ class LocalEngine:
         self._one: Optional[torch.Tensor] = None  # seed gradient of the loss (see forward_backward)
         self.hcache = self._make_hidden_cache()
         self.catalog = None  # (CatalogPlan, data group): cooperative cache builds (set_catalog)
+        self.catalog_refused: Optional[str] = None  # why parallel.catalog.attach fell back to local builds
         self._catalog_ctrl = None
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
@@ -667,6 +669,9 @@ class LocalEngine:
         self.counts["replays"] += 1
         if g.adam:
             g.graph.replay()
+            if self.grad_allreduce is not None:  # the captured all-reduce ran in this replay
+                CHECK.record("all_reduce", self.flat.grad,
+                             "grad-ipc" if getattr(self.grad_allreduce, "kind", "") == "ipc" else "grad")
             self.counts["replays_with_optimizer"] += 1
             self.flat.step += 1
             self._adam_mirror += 1

@@ -375,6 +375,41 @@ def test_cooperative_cache_matches_local_build(world):
         assert "CATALOG OK 0.0" in out, out[-2000:]
 
 
+@pytest.mark.parametrize("what", ["backbone", "tokens"])
+def test_cooperative_cache_refuses_divergent_clients(what):
+    """VERDICT r5 item 5 / ADVICE r5: a client whose frozen backbone differs by ONE weight, or
+    whose token row of a shared title differs, must not silently receive the others' hidden
+    states -- every client falls back to its own local build (attach returns None, with the
+    reason), and they all agree on it (no client left waiting in the gather)."""
+    outs = run_ranks([["tests/_catalog_worker.py", "--perturb", what]] * 2, timeout=240)
+    _ok(outs)
+    for _, out in outs:
+        assert "CATALOG REFUSED" in out, out[-2000:]
+        assert ("backbone" in out) if what == "backbone" else ("token rows" in out), out[-2000:]
+
+
+def test_catalog_ids_and_hashes():
+    """Leading zeros do not alias a catalog id; token-row hashes tell rows apart; the
+    transient size counts a ring of pieces, not the union."""
+    import numpy as np
+
+    from fedrec_with_pytorchdistributed_amd.parallel import catalog
+    g = catalog.global_ids(["<unk>", "N123", "N0123", "N0"])
+    assert g[0] == -1 and g[1] == 123 and g[2] < -1 and g[3] == 0
+    tok = torch.zeros(4, 2, 6, dtype=torch.int32)
+    tok[1, 0, :3] = torch.tensor([101, 7, 102])
+    tok[2] = tok[1]
+    tok[3] = tok[1]
+    tok[3, 1, 0] = 1
+    h = catalog.token_row_hashes(tok)
+    assert h[1] == h[2] and len({int(h[0]), int(h[1]), int(h[3])}) == 3
+    with pytest.raises(catalog.CatalogMismatch):
+        catalog._check_token_hashes([np.array([5, 6]), np.array([6, 7])], [np.array([1, 2]), np.array([3, 4])])
+    catalog._check_token_hashes([np.array([5, 6]), np.array([6, 7])], [np.array([1, 2]), np.array([2, 4])])
+    plan = catalog.CatalogPlan(0, 8, 8000, np.zeros(0, np.int64), np.zeros(0, np.int64), 4, 2000, 64000)
+    assert catalog.transient_bytes(plan, 50, 768, 2) == 50 * 768 * 2 * 2000 * (2 * 8 + 2 + 8)
+
+
 @pytest.mark.slow
 def test_grad_avg_cooperative_cache_same_trajectory(tmp_path):
     """GA with the hidden-state cache on: the cooperative build (default at W > 1) and per-client
