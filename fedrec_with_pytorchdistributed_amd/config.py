@@ -140,6 +140,14 @@ class FedRecConfig:
     local_update: str = "auto"  # per_epoch | per_step | auto (per_step for grad_avg)
     param_avg_every: int = 0  # PA: all-reduce every K local steps (0 = once per epoch)
     weighted_fedavg: bool = False  # Q12: reference mean is unweighted (server.py:49)
+    # server-side step on the averaged update (defaults = the reference's plain mean,
+    # server.py:46-50 / Parameter_Averaging_main.py:144-148): the new global model is
+    # theta_g + server_lr * v, v = server_momentum * v + (mean_k theta_k - theta_g) -- FedAvgM
+    # (Hsu et al. 2019) with a server learning rate (Reddi et al. 2021).  Star: at the
+    # coordinator; PA: on every client, identically (the same inputs give bitwise-same models)
+    server_lr: float = 1.0
+    server_momentum: float = 0.0
+    pa_average_moments: bool = False  # PA: average the clients' Adam m / v with the parameters
     sync: str = "trainable"  # Q15: trainable | full (the reference syncs all 116 tensors)
     quorum: float = 1.0  # fraction of clients needed to aggregate a round
     collective_timeout_s: float = 600.0  # reference: 2 days (client.py:227)

@@ -97,14 +97,16 @@ class FlatParams:
                 dst.append(view)
                 src.append(p.grad)
             p.grad = view
+        if dst and not missing and self.grad.is_cuda and all(t.is_contiguous() and t.dtype == torch.float32
+                                                              for t in src):
+            # every fresh gradient into its slot in one copy launch (csrc/adam.hip multi_cast; the
+            # alignment gaps are never written and stay zero; slots already holding their
+            # gradient -- the early-reduced user slice at N > 1 -- are skipped); torch.cat of the
+            # 110M config-5 gradients took ~0.58 ms per step in ~15 launches
+            from ..ops import native
+            if native.lib().multi_cast(src, dst):
+                return
         if dst and not missing and len(dst) == len(self.params):
-            if self.grad.is_cuda and all(t.is_contiguous() and t.dtype == torch.float32 for t in src):
-                # every gradient into its slot in one copy launch (csrc/adam.hip multi_cast; the
-                # alignment gaps are never written and stay zero); torch.cat of the 110M config-5
-                # gradients took ~0.58 ms per step in ~15 launches
-                from ..ops import native
-                if native.lib().multi_cast(src, dst):
-                    return
             # every parameter has a fresh gradient: one cat of [grad, zero gap, grad, ...] into
             # the flat buffer (a single batched copy kernel; the multi-tensor copy took ~18 us
             # for these 4.66 MB).  The alignment gaps get zeros, as the buffer was created.

@@ -637,6 +637,29 @@ def side_active() -> bool:
 DEFER_REDUCE = os.environ.get("FEDREC_DEFER_REDUCE", "1") != "0"
 _DEFERRED = [False]
 
+# Early gradient reduction at N > 1 (DDP's bucket that fires inside the backward): while a step
+# graph with an in-graph all-reduce is captured, the engine sets this callback; the text fc's
+# backward launch -- the one that also computes the held-back user-encoder weight gradients --
+# calls it right after that launch (its split-K reduce then runs at once, not deferred), so the
+# user-encoder slice of the flat gradient is summed over the clients on a side stream while the
+# text-head backward still runs (train/engine.py LocalEngine._early_user_reduce).
+_AFTER_USER_WGRADS = [None]
+
+
+class after_user_wgrads:
+    """Context: ``cb()`` runs once the user encoder's weight gradients are final in a backward."""
+
+    def __init__(self, cb):
+        self.cb = cb
+
+    def __enter__(self):
+        _AFTER_USER_WGRADS[0] = self.cb
+        return self
+
+    def __exit__(self, *exc):
+        _AFTER_USER_WGRADS[0] = None
+        return False
+
 
 def defer_active() -> bool:
     return DEFER_REDUCE and _SIDE_DEPTH[0] > 0 and not SIDE_WGRAD
@@ -1001,7 +1024,8 @@ class HeadFCFn(torch.autograd.Function):
             # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
             # launch -- with the user encoder's weight gradients when its backward held them back
             gs = (ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1), wgrad, *take_pending_gemms(4))
-            if defer_active():  # the weight gradients' split-K reduce rides in the head's reduce launch
+            early = _AFTER_USER_WGRADS[0] if len(gs) > 2 else None
+            if defer_active() and early is None:  # the weight gradients' split-K reduce rides in the head's reduce launch
                 lib = ops.native.require_for(dy)
                 lib.small_gemm_set_defer(True)
                 _DEFERRED[0] = True
@@ -1011,4 +1035,6 @@ class HeadFCFn(torch.autograd.Function):
                     lib.small_gemm_set_defer(False)
             else:
                 ops.small_gemm(*gs)
+            if early is not None:  # the user-encoder weight gradients are final here
+                early()
         return dx, dw.view_as(dw), db.view_as(db), None, None, None

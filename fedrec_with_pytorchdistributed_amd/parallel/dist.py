@@ -176,11 +176,43 @@ def data_ipc(ctx: DistContext, timeout_s: float = 600.0):
 
 
 def _ipc_grad_fn(ctx: DistContext, ipc, W: int):
+    """The IPC all-reduce of the flat gradient.  ``split`` (set by the engine: the element offset
+    where the user encoder's slice of the flat buffer starts, or None): the bucket goes as TWO
+    calls, the user slice first -- the step graph issues that one early, on a side stream, as
+    soon as the user encoder's weight gradients are final (DDP's first bucket), and the text-head
+    slice after the backward (:meth:`finish_early`).  Eager steps issue the same two calls in the
+    same order, so every client's sequence of calls on the context matches whichever path each
+    step took."""
+
     def _ar_ipc(flat_grad: torch.Tensor) -> float:
-        CHECK.record("all_reduce", flat_grad, "grad-ipc")
-        ipc.allreduce_(flat_grad)
+        sp = _ar_ipc.split
+        if sp:
+            CHECK.record("all_reduce", flat_grad[sp:], "grad-ipc-user")
+            ipc.allreduce_(flat_grad[sp:])
+            CHECK.record("all_reduce", flat_grad[:sp], "grad-ipc-head")
+            ipc.allreduce_(flat_grad[:sp])
+        else:
+            CHECK.record("all_reduce", flat_grad, "grad-ipc")
+            ipc.allreduce_(flat_grad)
         return 1.0 / W
 
+    def early(flat_grad: torch.Tensor, side: torch.cuda.Stream) -> None:
+        """The user slice's call on ``side``, forked from the current stream (inside a capture:
+        a graph branch beside the rest of the backward)."""
+        main = torch.cuda.current_stream(flat_grad.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ipc.allreduce_(flat_grad[_ar_ipc.split:])
+
+    def finish_early(flat_grad: torch.Tensor, side: torch.cuda.Stream) -> float:
+        """After :func:`early`: join the side stream, then the text-head slice's call."""
+        torch.cuda.current_stream(flat_grad.device).wait_stream(side)
+        ipc.allreduce_(flat_grad[:_ar_ipc.split])
+        return 1.0 / W
+
+    _ar_ipc.split = None
+    _ar_ipc.early = early
+    _ar_ipc.finish_early = finish_early
     _ar_ipc.check = ipc.check
     _ar_ipc.kind = "ipc"
     # device epochs: the launch is capturable -- the engine puts it inside the step graph, between

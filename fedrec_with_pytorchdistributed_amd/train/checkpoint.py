@@ -58,11 +58,15 @@ def restore_rng(snap: Dict[str, Any]) -> bool:
 
 def save_snapshot(path: str, model: FedRecModel, epoch: int, *, round_idx: Optional[int] = None,
                   optim: bool = True, config: Optional[dict] = None,
-                  engine: Optional[Dict[str, int]] = None) -> None:
+                  engine: Optional[Dict[str, int]] = None, server_opt: Optional[Dict[str, Any]] = None) -> None:
     """``engine``: the engine's own counters (Philox offsets of LDP noise / dropout, sampler
-    epoch) so a resumed run draws fresh randomness instead of replaying the saved one."""
+    epoch) so a resumed run draws fresh randomness instead of replaying the saved one.
+    ``server_opt``: the server-side step's state (train/federated.py ServerStep), if any."""
     snap: Dict[str, Any] = {"MODEL_STATE": cpu_state_dict(model), "EPOCHS_RUN": int(epoch),
                             "NEXT_EPOCH": int(epoch) + 1}
+    if server_opt:
+        snap["SERVER_OPT"] = {k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v)
+                              for k, v in server_opt.items()}
     if optim and model.flat is not None:
         snap["OPTIM_STATE"] = model.flat.state()
     if round_idx is not None:
@@ -87,7 +91,7 @@ def load_snapshot(path: str, model: FedRecModel, map_location="cpu", rng: bool =
     restored = restore_rng(snap) if rng else False
     nxt = int(snap.get("NEXT_EPOCH", int(snap["EPOCHS_RUN"]) + 1))
     return {"epochs_run": int(snap["EPOCHS_RUN"]), "next_epoch": nxt, "round": snap.get("ROUND"),
-            "rng_restored": restored, "engine": snap.get("ENGINE", {})}
+            "rng_restored": restored, "engine": snap.get("ENGINE", {}), "server_opt": snap.get("SERVER_OPT")}
 
 
 def client_snapshot_path(snapshot_path: str, client: int) -> str:

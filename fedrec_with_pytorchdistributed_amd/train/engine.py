@@ -113,6 +113,7 @@ class _StepGraph:
         eng.hcache.ensure()
         side = torch.cuda.Stream(dev)
         self.hid_graph = None
+        self.early = False  # the captured step issues the user slice's all-reduce early (N > 1)
         # (on with a gradient all-reduce only: at one client there is only Adam (7 us) to hide,
         # and the extra replay measured neutral: 66.86k vs 67.15k imp/s, r2_bench_batch6.jsonl)
         # (the fused text head reads the cache by index inside its GEMM: nothing to gather ahead)
@@ -145,12 +146,24 @@ class _StepGraph:
             ar = eng.grad_allreduce if with_adam else None
             eng._adam_gathers = with_adam and ar is None
             eng._precast = eng.step_cast_bufs() if self.precast else None
+            # N > 1 with the IPC all-reduce: the user encoder's slice is reduced early, inside the
+            # backward (a side-stream branch of the graph); only while capturing -- the warm-ups
+            # above run on one rank only when its bucket is new, and must not issue collectives
+            early = (ar is not None and eng._ar_side is not None and getattr(ar, "split", None))
+            hook = OF.after_user_wgrads(eng._early_user_reduce) if early else contextlib.nullcontext()
+            eng._early_issued = False
             with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
-                self.loss = eng.forward_backward(self.cand, self.his, static)
+                with hook:
+                    self.loss = eng.forward_backward(self.cand, self.his, static)
                 if with_adam:  # the step in one graph: backward, [all-reduce,] Adam
-                    scale = ar(eng.flat.grad) if ar is not None else 1.0
+                    if eng._early_issued:
+                        scale = ar.finish_early(eng.flat.grad, eng._ar_side)
+                    else:
+                        scale = ar(eng.flat.grad) if ar is not None else 1.0
                     eng._adam_dev(self.loss, scale)
+            self.early = eng._early_issued
         finally:
+            eng._early_issued = False
             eng._pre_hid = None
             eng._adam_bump = None
             eng._adam_gathers = False
@@ -199,6 +212,15 @@ class LocalEngine:
                                        truncate=not self.q.no_history_truncation, seed=cfg.seed, rank=rank)
         # grad_allreduce(flat_grad) -> scale to apply (1/W); None = local only
         self.grad_allreduce = grad_allreduce
+        # the user encoder's parameters are the flat buffer's tail (registration order): at N > 1
+        # the IPC all-reduce sends that slice in its own call, early (see _early_user_reduce)
+        self._user_first = self._user_slice_start(model)
+        self._ar_side = None
+        self._early_issued = False
+        if (grad_allreduce is not None and getattr(grad_allreduce, "kind", "") == "ipc"
+                and hasattr(grad_allreduce, "split") and self._user_first is not None):
+            grad_allreduce.split = self.flat.offsets[self._user_first]
+            self._ar_side = torch.cuda.Stream(device)
         # or a BucketReducer (large trainable sets: the unfrozen backbone): buckets reduced
         # during the backward as their gradients land (set_reducer)
         self.reducer = None
@@ -248,7 +270,7 @@ class LocalEngine:
         # step counters (tests / bench): graph replays, replays that ran the all-reduce + Adam
         # inside the graph, and optimizer steps issued eagerly from the host
         self.counts = {"replays": 0, "replays_with_optimizer": 0, "eager_optimizer_steps": 0, "eager_steps": 0,
-                       "captures": 0}
+                       "captures": 0, "early_reduces": 0}
         self.host_wait_s = 0.0  # host time blocked on the run-ahead bound (_retire): the DEVICE is the limit
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
@@ -262,6 +284,40 @@ class LocalEngine:
         # while the current step runs, so the dedup's host read of the unique count (the
         # backbone's M) no longer drains the GPU at every step start
         self._prep = torch.cuda.Stream(device) if device.type == "cuda" else None
+
+    def _user_slice_start(self, model) -> Optional[int]:
+        """Index of the first user-encoder parameter in the flat buffer when the user encoder's
+        parameters form its tail (contiguous, after every other one), else None."""
+        ids = {id(p) for p in model.user_encoder.parameters() if p.requires_grad}
+        flags = [id(p) in ids for p in self.flat.params]
+        if not any(flags):
+            return None
+        i0 = flags.index(True)
+        return i0 if i0 > 0 and all(flags[i0:]) else None
+
+    def _early_user_reduce(self) -> None:
+        """Called inside the captured backward once the user encoder's weight gradients are final
+        (ops.functional.after_user_wgrads: after the text fc's backward launch that computes
+        them): their slots of the flat gradient get them (one copy launch) and the IPC all-reduce
+        of that slice starts on a side stream -- beside the text head's pool backward and weight
+        gradient, ~130 us of the step -- as DDP's first bucket fires inside ``loss.backward()``
+        (``Gradient_Averaging_main.py:119``).  The head slice follows after the backward
+        (grad_allreduce.finish_early)."""
+        fl = self.flat
+        src, dst = [], []
+        for p, off in zip(fl.params[self._user_first:], fl.offsets[self._user_first:]):
+            view = fl.grad[off:off + p.numel()].view_as(p)
+            g = p.grad
+            if g is None:
+                view.zero_()
+            elif g.data_ptr() != view.data_ptr():
+                src.append(g if g.is_contiguous() and g.dtype == torch.float32 else g.float().contiguous())
+                dst.append(view)
+            p.grad = view  # end_backward leaves these slots alone
+        if src and not native.require_for(fl.grad).multi_cast(src, dst):
+            torch._foreach_copy_(dst, src)
+        self.grad_allreduce.early(fl.grad, self._ar_side)
+        self._early_issued = True
 
     def set_reducer(self, reducer) -> None:
         """Use a backward-overlapped bucket reducer (``parallel.reducer``) for the gradients."""
@@ -669,9 +725,17 @@ class LocalEngine:
         self.counts["replays"] += 1
         if g.adam:
             g.graph.replay()
-            if self.grad_allreduce is not None:  # the captured all-reduce ran in this replay
-                CHECK.record("all_reduce", self.flat.grad,
-                             "grad-ipc" if getattr(self.grad_allreduce, "kind", "") == "ipc" else "grad")
+            ar = self.grad_allreduce
+            if ar is not None:  # the captured all-reduce ran in this replay (the eager path's records)
+                sp = getattr(ar, "split", None)
+                if sp:
+                    CHECK.record("all_reduce", self.flat.grad[sp:], "grad-ipc-user")
+                    CHECK.record("all_reduce", self.flat.grad[:sp], "grad-ipc-head")
+                else:
+                    CHECK.record("all_reduce", self.flat.grad,
+                                 "grad-ipc" if getattr(ar, "kind", "") == "ipc" else "grad")
+                if g.early:
+                    self.counts["early_reduces"] += 1
             self.counts["replays_with_optimizer"] += 1
             self.flat.step += 1
             self._adam_mirror += 1

@@ -152,14 +152,50 @@ def _dump_flat(model: FedRecModel, ctx: DistContext) -> None:
         torch.save(model.flat.flat.detach().cpu(), os.path.join(d, f"rank{ctx.rank}.pt"))
 
 
-def _resume(cfg: FedRecConfig, model: FedRecModel) -> Tuple[int, Dict]:
+def _resume(cfg: FedRecConfig, model: FedRecModel, server: Optional["ServerStep"] = None) -> Tuple[int, Dict]:
     """(next epoch, engine counters) of ``cfg.snapshot_path`` when it exists (params, Adam
-    moments and RNG states are restored into ``model`` / torch)."""
+    moments and RNG states are restored into ``model`` / torch; the server step's momentum into
+    ``server``)."""
     if cfg.snapshot_path and os.path.exists(cfg.snapshot_path):
         info = ckpt.load_snapshot(cfg.snapshot_path, model)
+        if server is not None:
+            server.load(info.get("server_opt"))
         obs.log(f"resuming from {cfg.snapshot_path}: epochs_run={info['epochs_run']} -> epoch {info['next_epoch']}")
         return info["next_epoch"], info["engine"]
     return 0, {}
+
+
+class ServerStep:
+    """The server-side step on an averaged model (``cfg.server_lr`` / ``cfg.server_momentum``):
+    ``v = momentum * v + (avg - theta_g)``, ``theta = theta_g + lr * v`` -- FedAvgM (Hsu et al.
+    2019, server momentum) with a server learning rate (Reddi et al. 2021).  At lr 1 and
+    momentum 0 it is the plain mean of the reference (``server.py:46-50``,
+    ``Parameter_Averaging_main.py:144-148``) and does nothing.  Computed in fp64 on the host for
+    the coordinator and in fp32 on the device for parameter averaging (every PA client applies it
+    to the same all-reduced mean, so the clients stay bitwise identical)."""
+
+    def __init__(self, lr: float = 1.0, momentum: float = 0.0):
+        self.lr, self.momentum = float(lr), float(momentum)
+        self.v: Optional[torch.Tensor] = None
+
+    @property
+    def active(self) -> bool:
+        return self.lr != 1.0 or self.momentum != 0.0
+
+    def apply(self, theta_g: torch.Tensor, avg: torch.Tensor) -> torch.Tensor:
+        """The new global model from the round's global ``theta_g`` and the clients' mean."""
+        if not self.active:
+            return avg
+        d = avg - theta_g
+        self.v = d if self.v is None else self.v.to(d.device).mul_(self.momentum).add_(d)
+        return theta_g + self.lr * self.v
+
+    def state(self) -> Optional[Dict]:
+        return {"v": self.v} if self.active and self.v is not None else None
+
+    def load(self, st: Optional[Dict]) -> None:
+        if st and st.get("v") is not None:
+            self.v = st["v"].clone()
 
 
 # ---------------------------------------------------------------------------------------
@@ -208,10 +244,13 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     selfcheck(ctx, log=obs.log)
     shard = load_client_shard(cfg, ctx)
     model = build_model(cfg, ctx.device)
-    start, est = _resume(cfg, model)
+    server = ServerStep(cfg.server_lr, cfg.server_momentum)
+    start, est = _resume(cfg, model, server)
     full = cfg.sync == "full"
     _sync_initial(model, ctx, full)
     eng = LocalEngine(cfg, model, shard, ctx.device, rank=ctx.rank, grad_allreduce=None)
+    # the model at the last average (the server step's theta_g): every client holds the same one
+    anchor = model.flat.flat.detach().clone() if server.active else None
     eng.sigma = _maybe_dp(cfg, eng)
     eng.load_state(est)
     eng.epoch = start
@@ -227,8 +266,15 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     def average():
         if ctx.initialized and W > 1:
             before = _backbone_before(model, full)
+            ts = model.sync_tensors(full)
+            if cfg.pa_average_moments:  # the clients' Adam moments averaged with the parameters
+                ts = ts + [model.flat.m, model.flat.v]
             with obs.range("param_allreduce"):
-                comm.allreduce_(model.sync_tensors(full), ctx.data_group, scale=1.0 / W, ipc=ipc)
+                comm.allreduce_(ts, ctx.data_group, scale=1.0 / W, ipc=ipc)
+            if anchor is not None:  # server step on the mean (same inputs on every client)
+                with torch.no_grad():
+                    model.flat.flat.copy_(server.apply(anchor, model.flat.flat))
+                    anchor.copy_(model.flat.flat)
             _backbone_synced(model, full, before)
 
     hook = (lambda n: average() if n % K == 0 else None) if K else None
@@ -248,7 +294,8 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
             writer.write(last)
             obs.log(f"[param_avg] epoch {epoch}: " + ", ".join(f"{k}={last[k]:.4f}" for k in METRIC_KEYS))
             if cfg.save_every and (epoch % cfg.save_every == 0 or epoch == cfg.total_epochs - 1):
-                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict(), engine=eng.state())
+                ckpt.save_snapshot(cfg.snapshot_path, model, epoch, config=cfg.to_dict(), engine=eng.state(),
+                                   server_opt=server.state())
     _dump_flat(model, ctx)
     return last
 
@@ -416,9 +463,11 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     cp = ControlPlane.from_default(run_id, cfg.round_timeout_s)
     W = ctx.num_clients
     model = build_model(cfg, torch.device("cpu"))
+    server = ServerStep(cfg.server_lr, cfg.server_momentum)  # off by default: the plain mean
     start_round = 0
     if cfg.snapshot_path and os.path.exists(cfg.snapshot_path):
         info = ckpt.load_snapshot(cfg.snapshot_path, model)
+        server.load(info.get("server_opt"))
         start_round = int(info.get("round") or 0) + 1 if info.get("round") is not None else 0
         obs.log(f"[server] resuming at round {start_round}")
     writer = _metrics_writer(cfg, True)
@@ -479,6 +528,8 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                     acc += t.double() * w  # server.py:46-50 (unweighted unless weighted_fedavg)
                 new = (acc / sum(weights)).float()
         with torch.no_grad():
+            if server.active:  # FedAvgM / server learning rate on the round's mean (fp64)
+                new = server.apply(model.flat.flat.detach().double(), new.double()).float()
             model.flat.flat.copy_(new)
         dt = time.perf_counter() - t0
         rec = {"round": r, "clients_accepted": len(accepted), "clients": W, "clients_dead": dead, "round_s": dt}
@@ -493,7 +544,8 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
         hist.append(rec)
         obs.log(f"[server] round {r}: {len(accepted)}/{W} clients, {dt:.2f}s, auc={rec.get('valid_auc', float('nan')):.4f}")
         if cfg.snapshot_path:
-            ckpt.save_snapshot(cfg.snapshot_path, model, r, round_idx=r, optim=False, config=cfg.to_dict())
+            ckpt.save_snapshot(cfg.snapshot_path, model, r, round_idx=r, optim=False, config=cfg.to_dict(),
+                               server_opt=server.state())
             gpath = os.path.join(os.path.dirname(os.path.abspath(cfg.snapshot_path)), f"global_model_round{r}.pt")
             ckpt.save_state_dict(gpath, model)
     cp.set(f"r{max(cfg.global_rounds, start_round)}/go", "0")  # server.py:105 stop flag

@@ -55,6 +55,9 @@ def main() -> int:
     c = eg.counts
     assert c["replays"] == a.steps and c["replays_with_optimizer"] == a.steps, c
     assert c["eager_optimizer_steps"] == 0 and c["eager_steps"] == 0, c
+    # the user encoder's slice is reduced early, inside the backward, in every replay (the eager
+    # run below issues the same two calls per step: user slice, then head slice)
+    assert ar.split and c["early_reduces"] == a.steps, (ar.split, c)
     ee, pe, se = run(False)
     assert ee.counts["replays_with_optimizer"] == 0 and ee.counts["eager_optimizer_steps"] == a.steps, ee.counts
     # every client holds the bitwise-same parameters (graph mode), checked over the control group

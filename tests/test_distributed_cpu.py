@@ -162,6 +162,66 @@ def test_star_fedavg_server_plus_two_clients(tmp_path):
         assert cs["ROUND"] == 1 and int(cs["OPTIM_STATE"]["step"]) == 2 and "RNG" in cs and "ENGINE" in cs
 
 
+def test_server_step_math():
+    """ServerStep: identity at the defaults (the reference's plain mean); FedAvgM + server lr:
+    v_r = beta v_{r-1} + (avg_r - theta_r), theta_{r+1} = theta_r + lr v_r."""
+    from fedrec_with_pytorchdistributed_amd.train.federated import ServerStep
+    s0 = ServerStep()
+    th, avg = torch.randn(10), torch.randn(10)
+    assert not s0.active and s0.apply(th, avg) is avg and s0.state() is None
+    s = ServerStep(lr=1.5, momentum=0.9)
+    th0 = torch.zeros(10, dtype=torch.float64)
+    a0, a1 = torch.randn(10, dtype=torch.float64), torch.randn(10, dtype=torch.float64)
+    th1 = s.apply(th0, a0)
+    assert torch.allclose(th1, 1.5 * a0)
+    th2 = s.apply(th1, a1)
+    v = 0.9 * a0 + (a1 - th1)
+    assert torch.allclose(th2, th1 + 1.5 * v)
+    s2 = ServerStep(lr=1.5, momentum=0.9)
+    s2.load(s.state())  # resume carries the momentum
+    assert torch.equal(s2.v, s.v)
+
+
+@pytest.mark.slow
+def test_star_server_learning_rate(tmp_path):
+    """The coordinator's server step (cfg.server_lr): global_{r+1} = global_r + lr (mean_r -
+    global_r), checked from the clients' round-1 uploads (received_model_k.pt) and the saved
+    global models; the snapshot carries the server step's buffer for a resume."""
+    snap = str(tmp_path / "server_snapshot.pt")
+    server = ["server.py", "2", *TINY, f"--snapshot_path={snap}", "--round_artifacts=1", "--server_lr=2.0"]
+    client = ["client.py", "1", "16", "1", "0", "c", *TINY, f"--snapshot_path={tmp_path}/c.pt", "--round_artifacts=1"]
+    _ok(run_ranks([server, client, client], {"FEDREC_STAR_AGG": "upload"}))
+    g0 = torch.load(tmp_path / "global_model_round0.pt", weights_only=True)
+    g1 = torch.load(tmp_path / "global_model_round1.pt", weights_only=True)
+    r0 = torch.load(tmp_path / "received_model_0.pt", weights_only=True)  # round 1's uploads
+    r1 = torch.load(tmp_path / "received_model_1.pt", weights_only=True)
+    for key in ("text_encoder.fc.weight", "user_encoder.additive_attention.att_fc1.weight"):
+        mean1 = (r0[key].double() + r1[key].double()) / 2
+        want = (g0[key].double() + 2.0 * (mean1 - g0[key].double())).float()
+        assert torch.allclose(g1[key], want, atol=1e-6), key
+        if float((mean1 - g0[key].double()).abs().max()) > 1e-5:  # (a key that moved this round)
+            assert not torch.allclose(g1[key], mean1.float(), atol=1e-6), key
+    sd = torch.load(snap, weights_only=True)
+    assert "SERVER_OPT" in sd and sd["SERVER_OPT"]["v"].dtype == torch.float64
+
+
+@pytest.mark.slow
+def test_param_avg_moments_and_server_momentum(tmp_path):
+    """PA with the clients' Adam moments averaged and a server step on the mean: every client
+    applies it to the same all-reduced inputs, so the clients stay bitwise identical; the
+    trajectory differs from the plain mean's."""
+    base = ["Parameter_Averaging_main.py", "2", "8", "1", *TINY, "--local_update=per_step", "--param_avg_every=2"]
+    opt = base + ["--pa_average_moments=1", "--server_momentum=0.9", "--server_lr=1.5",
+                  f"--snapshot_path={tmp_path}/s.pt"]
+    _ok(run_ranks([opt, opt], {"FEDREC_DUMP_FLAT": str(tmp_path / "opt")}))
+    _ok(run_ranks([base + [f"--snapshot_path={tmp_path}/b.pt"]] * 2, {"FEDREC_DUMP_FLAT": str(tmp_path / "base")}))
+    a = torch.load(tmp_path / "opt" / "rank0.pt")
+    assert torch.equal(a, torch.load(tmp_path / "opt" / "rank1.pt"))
+    assert not torch.equal(a, torch.load(tmp_path / "base" / "rank0.pt"))
+    sd = torch.load(tmp_path / "s.pt", weights_only=True)
+    assert "SERVER_OPT" in sd
+
+
 @pytest.mark.slow
 def test_star_fedavg_allreduce_aggregation(tmp_path):
     server = ["server.py", "2", *TINY, f"--snapshot_path={tmp_path}/s.pt"]
