@@ -365,6 +365,21 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     last: Dict = {}
     while True:
         flag = cp.get(f"r{r}/go").decode()
+        if flag == "2":
+            # the run is over and the coordinator asks for the FINAL global model's validation:
+            # the per-round metrics (as the reference's) are each client's LOCAL model after its
+            # local epochs, before the mean; this one scores the aggregate itself
+            local = model.flat.flat.detach().clone()  # the client keeps its own model afterwards
+            before = _backbone_before(model, full)
+            _receive_global(cp, r, model, ctx, full, bcast)
+            _backbone_synced(model, full, before)
+            eng.ensure_cache()
+            va = eng.validate()
+            cp.put_json(f"r{r}/final/{k}", {"client": k, **{m: float(v) for m, v in va.items()
+                                                              if isinstance(v, (int, float))}})
+            with torch.no_grad():
+                model.flat.flat.copy_(local)
+            break
         if flag != "1":
             break
         beat(force=True)
@@ -527,6 +542,7 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                 for t, w in zip(ups, weights):
                     acc += t.double() * w  # server.py:46-50 (unweighted unless weighted_fedavg)
                 new = (acc / sum(weights)).float()
+        last_accepted = list(accepted)
         with torch.no_grad():
             if server.active:  # FedAvgM / server learning rate on the round's mean (fp64)
                 new = server.apply(model.flat.flat.detach().double(), new.double()).float()
@@ -548,5 +564,30 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                                server_opt=server.state())
             gpath = os.path.join(os.path.dirname(os.path.abspath(cfg.snapshot_path)), f"global_model_round{r}.pt")
             ckpt.save_state_dict(gpath, model)
-    cp.set(f"r{max(cfg.global_rounds, start_round)}/go", "0")  # server.py:105 stop flag
+    R = max(cfg.global_rounds, start_round)
+    if hist:
+        # the final global model, validated by the clients on their validation shards (flag "2":
+        # receive, validate, report, stop) -- the per-round records score each client's LOCAL
+        # model after its local epochs, as the reference's Trainer.validate does (client.py:149-171)
+        cp.put_tensor(f"r{R}/global", model.flat.flat)
+        if full:
+            cp.put_tensor(f"r{R}/backbone", _flat_backbone(model))
+        cp.set(f"r{R}/go", "2")
+        finals = []
+        for k in last_accepted:  # (a client declared dead or dropped in the last round is not asked)
+            try:
+                finals.append(cp.get_json(f"r{R}/final/{k}", min(cfg.round_timeout_s, 300.0)))
+            except Exception as e:  # a client gone after the last round: report the others
+                obs.log(f"[server] final evaluation: no report from client {k}: {e}")
+        if finals:
+            rec = {"round": R - 1, "final_global": True, "clients_reporting": len(finals)}
+            for key in ("validation_loss", "valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):
+                vals = [f[key] for f in finals if key in f]
+                if vals:
+                    rec[f"global_{key}"] = float(np.mean(vals))
+            writer.write(rec)
+            hist[-1].update({k2: v for k2, v in rec.items() if k2.startswith("global_")})
+            obs.log(f"[server] final global model: auc={rec.get('global_valid_auc', float('nan')):.4f}")
+    else:
+        cp.set(f"r{R}/go", "0")  # server.py:105 stop flag
     return hist[-1] if hist else {}

@@ -37,6 +37,22 @@ def runs(world, epochs, preset):
         # local_update=per_step is the schedule option that trains like the other modes)
         yield f"star_w{W}", ([["server.py", str(epochs), *common]] +
                              [["client.py", "1", b, "0", "0", "q", "--local_update=per_step", *common]] * W)
+        # server-side step options (off by default): FedAvgM / server lr at the
+        # coordinator, and for PA the clients' Adam moments averaged + the same server step
+        for tag, extra in SERVER_VARIANTS:
+            yield f"star_w{W}_{tag}", ([["server.py", str(epochs), *common, *extra]] +
+                                       [["client.py", "1", b, "0", "0", "q", "--local_update=per_step", *common]] * W)
+        for tag, extra in PA_VARIANTS:
+            yield f"pa8_w{W}_{tag}", [["Parameter_Averaging_main.py", str(epochs), b, "0", "--param_avg_every=8",
+                                       "--local_update=per_step", *common, *extra]] * W
+
+
+SERVER_VARIANTS = [("m9", ["--server_momentum=0.9"]), ("lr3", ["--server_lr=3.0"]),
+                   ("lr3m5", ["--server_lr=3.0", "--server_momentum=0.5"])]
+PA_VARIANTS = [("mv", ["--pa_average_moments=1"]), ("mv_lr2", ["--pa_average_moments=1", "--server_lr=2.0"]),
+               ("mv_m5", ["--pa_average_moments=1", "--server_momentum=0.5"]),
+               ("mv_lr3", ["--pa_average_moments=1", "--server_lr=3.0"]),
+               ("mv_lr2m5", ["--pa_average_moments=1", "--server_lr=2.0", "--server_momentum=0.5"])]
 
 
 def main():
@@ -68,6 +84,11 @@ def main():
         rec = {"run": name, "ok": ok, "wall_s": round(dt, 1), "processes": len(argvs)}
         if ok and os.path.exists(mp):
             rows = [json.loads(l) for l in open(mp) if l.strip()]
+            fin = [r for r in rows if r.get("final_global")]
+            rows = [r for r in rows if not r.get("final_global")]
+            if fin:  # star: the final GLOBAL model's score (the per-round rows score local models)
+                rec["global_valid_auc"] = round(fin[-1].get("global_valid_auc", float("nan")), 4)
+                rec["global_valid_mrr"] = round(fin[-1].get("global_valid_mrr", float("nan")), 4)
             rec["valid_auc"] = [round(r.get("valid_auc", float("nan")), 4) for r in rows]
             rec["valid_mrr"] = [round(r.get("valid_mrr", float("nan")), 4) for r in rows]
             rec["training_loss"] = [round(r.get("training_loss", float("nan")), 4) for r in rows]

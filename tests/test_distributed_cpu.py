@@ -16,9 +16,11 @@ def _ok(outs):
         assert rc == 0, out[-3000:]
 
 
-def _metrics(path):
+def _metrics(path, final=False):
+    """Per-round records (``final=True``: the star coordinator's final global-model record)."""
     with open(path) as f:
-        return [json.loads(l) for l in f if l.strip()]
+        rows = [json.loads(l) for l in f if l.strip()]
+    return [r for r in rows if bool(r.get("final_global")) == final]
 
 
 @pytest.mark.slow
@@ -140,6 +142,10 @@ def test_star_fedavg_server_plus_two_clients(tmp_path):
     _ok(outs)
     hist = _metrics(str(tmp_path / "metrics.jsonl"))
     assert [h["round"] for h in hist] == [0, 1] and all(h["clients_accepted"] == 2 for h in hist)
+    # after the last round the clients score the final GLOBAL model (the per-round rows score
+    # their local models, as the reference's client-side validate does)
+    fin = _metrics(str(tmp_path / "metrics.jsonl"), final=True)
+    assert len(fin) == 1 and fin[0]["clients_reporting"] == 2 and 0.0 <= fin[0]["global_valid_auc"] <= 1.0, fin
     assert os.path.exists(tmp_path / "global_model_round1.pt")
     g = torch.load(tmp_path / "global_model_round1.pt", weights_only=True)
     snapd = torch.load(snap, weights_only=True)
