@@ -75,6 +75,8 @@ def main() -> int:
     ap.add_argument("--cache-warm", type=int, default=512,
                     help="titles run through the backbone (result dropped) before the timed cache build")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--step-events", action="store_true",
+                    help="diagnostic: a timing event after every timed step's launch (device interval per step)")
     ap.add_argument("--news-cache", default="auto", choices=["auto", "hidden", "none"],
                     help="HBM hidden-state cache of the frozen backbone (none = re-encode every step)")
     ap.add_argument("--round", default="auto", choices=["auto", "on", "off"],
@@ -214,9 +216,9 @@ def main() -> int:
     host_step = host_next = 0.0  # host time spent launching steps / preparing batches (diagnostic)
     wait0 = eng.host_wait_s  # ... of which blocked on the run-ahead bound (waiting for the device)
     counts0 = dict(eng.counts)
-    # FEDREC_BENCH_EVENTS=1 (diagnostic, off by default): a timing event after every step's launch
+    # --step-events (diagnostic, off by default): a timing event after every step's launch
     # on the main stream -- where the device time of the timed window goes (start-up, per step, tail)
-    evs = [] if (os.environ.get("FEDREC_BENCH_EVENTS") == "1" and dev.type == "cuda") else None
+    evs = [] if (a.step_events and dev.type == "cuda") else None
     if evs is not None:
         evs.append(torch.cuda.Event(enable_timing=True))
         evs[-1].record()

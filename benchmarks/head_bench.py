@@ -63,17 +63,15 @@ def main():
     out.append({"kernel": "head_pool_bwd", "us": round(t, 1), "TBs": round(M * D * 2 / t / 1e6, 2)})
     t = timeit(lambda: lib.head_wgrad(table, ids, T, e, da, w2, db2p), a.iters)
     out.append({"kernel": "head_wgrad(+reduce)", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1)})
-    # the G path (round 5): g = da (1 - e^2) written once (fused into the pool backward, or a
-    # kernel of its own after it), then a plain TN GEMM over g (k-tile 128 / 256)
+    # the G path (round 5): g = da (1 - e^2) written once by the pool backward, then a plain TN
+    # GEMM over g
     if lib.head_g_supported(D, Q, T):
         eg = e.clone()
         t = timeit(lambda: lib.head_pool_bwd_g(table, ids, T, alpha, gout, eg), a.iters)
         out.append({"kernel": "head_pool_bwd_g (fused)", "us": round(t, 1),
                     "TBs": round(M * (D + 2 * Q) * 2 / t / 1e6, 2)})
-        t = timeit(lambda: lib.head_g_rewrite(da, T, eg), a.iters)
-        out.append({"kernel": "head_g_rewrite", "us": round(t, 1), "TBs": round(M * 2 * Q * 2 / t / 1e6, 2)})
         eg.copy_(e)
-        cs = lib.head_g_rewrite(da, T, eg)
+        _, _, cs = lib.head_pool_bwd_g(table, ids, T, alpha, gout, eg)
         for kt in (4128,):  # (one form left)
             lib.head_wgrad_g_set_kt(kt)
             t = timeit(lambda: lib.head_wgrad_g(table, ids, T, eg, cs, w2, db2p), a.iters)

@@ -148,6 +148,9 @@ class FedRecConfig:
     server_lr: float = 1.0
     server_momentum: float = 0.0
     pa_average_moments: bool = False  # PA: average the clients' Adam m / v with the parameters
+    # unfrozen backbone (GA): reduce the gradient in ~28 MB buckets during the backward (DDP's
+    # reducer, parallel/reducer.py); False = one flat all-reduce after it
+    bucket_reducer: bool = True
     sync: str = "trainable"  # Q15: trainable | full (the reference syncs all 116 tensors)
     quorum: float = 1.0  # fraction of clients needed to aggregate a round
     collective_timeout_s: float = 600.0  # reference: 2 days (client.py:227)

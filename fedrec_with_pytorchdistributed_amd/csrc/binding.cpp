@@ -58,7 +58,6 @@ long fr_head_wgrad_g(const void* G, const void* table, const int* ids, const flo
                      const float* w2, int U, int T, int D, int Q, float* dW1, float* db1, float* dw2, float* db2,
                      float* scratch, const int* nreal, hipStream_t s, const void* pend, int pend_cblocks,
                      int pend_total);
-int fr_head_g_rewrite(const float* da, int U, int T, int Q, void* e, float* cs, const int* nreal, hipStream_t s);
 void fr_head_wgrad_g_set_kt(int kt);
 int fr_ipc_create(long cap, void* handle_out);
 int fr_ipc_open(int id, const void* handles, int me, int W, const long long* local_ptrs);
@@ -675,29 +674,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> head_pool_bwd_g(const at::Tensor&
   return {da, db2p, cs};
 }
 
-// the g rewrite alone (after head_pool_bwd): e [U*T, Q] bf16 -> g in place; returns cs [2, U, Q]
-at::Tensor head_g_rewrite(const at::Tensor& da, int64_t T, at::Tensor e, const c10::optional<at::Tensor>& nreal) {
-  check_dev(da, "da");
-  check_dev(e, "e");
-  TORCH_CHECK(da.scalar_type() == at::kFloat && da.is_contiguous() && da.numel() % T == 0,
-              "fedrec::head_g_rewrite: da fp32 [U*T]");
-  const int64_t U = da.numel() / T;
-  TORCH_CHECK(e.scalar_type() == at::kBFloat16 && e.is_contiguous() && U > 0 && e.numel() % (U * T) == 0,
-              "fedrec::head_g_rewrite: e bf16 [U*T, Q]");
-  const int64_t Q = e.numel() / (U * T);
-  const int* nr = nullptr;
-  if (nreal.has_value()) {
-    TORCH_CHECK(nreal->scalar_type() == at::kInt && nreal->numel() == 1 && nreal->device() == da.device(),
-                "fedrec::head_g_rewrite: nreal int32 [1] on da's device");
-    nr = nreal->data_ptr<int>();
-  }
-  const c10::DeviceGuard dg(da.device());
-  auto cs = at::empty({2, U, Q}, da.options());
-  check_rc(fr_head_g_rewrite(da.data_ptr<float>(), (int)U, (int)T, (int)Q, e.data_ptr(), cs.data_ptr<float>(), nr,
-                             cur_stream()),
-           "head_g_rewrite");
-  return cs;
-}
 
 // the partials of a deferred small-GEMM split-K reduction, held until the launch that reduces them
 static at::Tensor g_sg_pending_scratch;
@@ -1974,7 +1950,6 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("dedup_sync_max() -> int", &dedup_sync_max);
   m.def("head_g_supported(int D, int Q, int T) -> bool", &head_g_supported);
   m.def("head_wgrad_g_set_kt(int kt) -> ()", &head_wgrad_g_set_kt);
-  m.def("head_g_rewrite(Tensor da, int T, Tensor(a!) e, Tensor? nreal=None) -> Tensor");
   m.def("small_gemm_set_defer(bool on) -> ()", &small_gemm_set_defer);
   m.def("small_gemm_flush_pending() -> bool", &small_gemm_flush_pending);
   m.def("head_pool_bwd_g(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor(a!) e, Tensor? nreal=None) -> (Tensor, Tensor, Tensor)");
@@ -2052,7 +2027,6 @@ TORCH_LIBRARY_IMPL(fedrec, CUDA, m) {
   m.impl("head_pool_bwd", &head_pool_bwd);
   m.impl("head_wgrad", &head_wgrad);
   m.impl("head_pool_bwd_g", &head_pool_bwd_g);
-  m.impl("head_g_rewrite", &head_g_rewrite);
   m.impl("head_wgrad_g", &head_wgrad_g);
   m.impl("additive_pool_fwd", &additive_pool_fwd);
   m.impl("additive_pool_bwd", &additive_pool_bwd);

@@ -27,7 +27,8 @@
 //                db1 = w2 sum g column sums; no dpre tensor exists.  w2[q] is applied to the
 //                fp32 result in the split-K reduction.
 //
-// Requirements (host-checked in binding.cpp): D % 256 == 0, Q in {128, 256, 384}, T <= 128.
+// Requirements (host-checked in binding.cpp): D % 256 == 0, Q in {128, 256, 384}, T <= 128 (T <= 96
+// at D = 1024).  Q = 384 (DistilBERT) takes the G path below; Q = 128 / 256 the round-4 head_wgrad.
 #include "common.h"
 #include "gemm_batch.h"
 
@@ -66,138 +67,22 @@ __device__ __forceinline__ u32x4_t lds_read128(uint32_t addr) {
   return v;
 }
 
-// =========================================================================================
-// head_score: e = tanh(X W1^T + b1) (bf16, optional), a = e . w2 + b2 (fp32, from the fp32 e)
-// 128 rows x Q columns per block, BK = 64, 512 threads = 8 waves as 2 (rows) x 4 (columns):
-// 64 rows x Q/4 columns per wave = 4 x QF MFMA tiles of 16x16 (v_mfma_f32_16x16x32_bf16 with
-// W1 as the A operand, so a lane ends with 4 consecutive columns of one row).  LDS: two stages
-// of [128 x 128 B rows | Q x 128 B rows], each 16-B chunk c of row r stored at c ^ (r & 7)
-// (conflict-free ds_read_b128; glds images are lane-linear so the XOR goes on the source).
-// =========================================================================================
-template <int QF>
-__device__ __forceinline__ void score_stage(char* base, const bf16* const (&arow)[2], const bf16* __restrict__ W1,
-                                            int D, int k0, int wave, int lane) {
-  constexpr int Q = QF * 64;
-  const int rsub = lane >> 3, chunk = (lane & 7) ^ rsub;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, arow[i] + k0 + chunk * 8),
-                                     LDS_PTR(void, base + (wave * 16 + i * 8) * 128), 16, 0, 0);
-#pragma unroll
-  for (int i = 0; i < QF; ++i) {
-    const int row = (wave * QF + i) * 8 + rsub;
-    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, W1 + (size_t)row * D + k0 + chunk * 8),
-                                     LDS_PTR(void, base + 128 * 128 + (wave * QF + i) * 8 * 128), 16, 0, 0);
-  }
-  (void)Q;
-}
-
-template <int QF>
-__global__ __launch_bounds__(512, 1) void head_score_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
-                                                            int M, int T, int D, const bf16* __restrict__ W1,
-                                                            const float* __restrict__ b1, const float* __restrict__ w2,
-                                                            const float* __restrict__ b2, bf16* __restrict__ e_out,
-                                                            float* __restrict__ a_out, const int* __restrict__ nreal) {
-  constexpr int Q = QF * 64;
-  constexpr int ST = (128 + Q) * 128;  // stage bytes
-  __shared__ __attribute__((aligned(16))) char smem[2 * ST];
-  const int m0 = blockIdx.x * 128;
-  if (nreal != nullptr && m0 >= min(M, nreal[0] * T)) return;  // only padded titles' rows (never read)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wq = wave & 3;
-  const int rsub = lane >> 3, chunk = (lane & 7) ^ rsub;
-  const bf16* arow[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int gm = m0 + wave * 16 + i * 8 + rsub;
-    gm = gm < M ? gm : M - 1;  // rows past M: any valid row (outputs masked)
-    arow[i] = hrow(table, ids, gm, T, D);
-  }
-  (void)chunk;
-
-  f32x4 acc[QF][4];
-#pragma unroll
-  for (int i = 0; i < QF; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = D / 64;
-  score_stage<QF>(smem, arow, W1, D, 0, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) score_stage<QF>(smem + (cur ^ 1) * ST, arow, W1, D, (kt + 1) * 64, wave, lane);
-    const char* As = smem + cur * ST;
-    const char* Ws = As + 128 * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int phys = ((kk * 4 + fq) ^ (fr & 7)) * 16;
-      bf16x8 x[4], w[QF];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = *(const bf16x8*)(As + (wm * 64 + j * 16 + fr) * 128 + phys);
-#pragma unroll
-      for (int i = 0; i < QF; ++i) w[i] = *(const bf16x8*)(Ws + (wq * QF * 16 + i * 16 + fr) * 128 + phys);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < QF; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[i], x[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // epilogue: lane holds rows m = m0 + wm*64 + j*16 + fr, columns q = qb_i + fq*4 + (0..3)
-  float part[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < QF; i += 2) {
-    float v[2][4][4];  // [frag pair][j][reg]
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int qb = wq * QF * 16 + (i + h) * 16 + fq * 4;
-      const float4 bb = *(const float4*)(b1 + qb);
-      const float4 ww = *(const float4*)(w2 + qb);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[h][j][0] = tanh_fast(acc[i + h][j][0] + bb.x);
-        v[h][j][1] = tanh_fast(acc[i + h][j][1] + bb.y);
-        v[h][j][2] = tanh_fast(acc[i + h][j][2] + bb.z);
-        v[h][j][3] = tanh_fast(acc[i + h][j][3] + bb.w);
-        part[j] += v[h][j][0] * ww.x + v[h][j][1] * ww.y + v[h][j][2] * ww.z + v[h][j][3] * ww.w;
-      }
-    }
-    if (e_out != nullptr) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wm * 64 + j * 16 + fr;
-        store_pair16_if(e_out + (size_t)(m < M ? m : 0) * Q + wq * QF * 16 + i * 16, v[0][j], v[1][j], fq, m < M);
-      }
-    }
-  }
-  float* red = (float*)smem;  // the staging buffers are free (the loop ended on a barrier)
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float s = group4_sum(part[j]);
-    if (fq == 0) red[wq * 128 + wm * 64 + j * 16 + fr] = s;
-  }
-  __syncthreads();
-  if (tid < 128 && m0 + tid < M)
-    a_out[m0 + tid] = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]) + b2[0];
-}
-
 // -----------------------------------------------------------------------------------------
-// head_score2: the same product with the row tile (32 RF rows), the k-tile (BK) and the depth
-// of the LDS pipeline (NST stages, NST - 2 in flight while the MFMAs read one) as parameters.
+// head_score2: e = tanh(X W1^T + b1) (bf16, optional), a = e . w2 + b2 (fp32, from the fp32 e).
+// The A rows come straight from the cache by title index (row m -> cache row ids[m / T] * T +
+// m % T, per-lane glds source addresses); the whole Q sits in one block, so the epilogue forms
+// the score in registers (cross-lane + LDS reduction).  512 threads = 8 waves as WMN (rows) x
+// WQ (columns), v_mfma_f32_16x16x32_bf16 with W1 as the A operand (a lane ends with 4
+// consecutive columns of one row).  The row tile (32 RF rows), the k-tile (BK) and the depth
+// of the LDS pipeline (NST stages, NST - 2 in flight while the MFMAs read one) are parameters.
 // A stage is XP + WP "pieces" of one wave-instruction each (64 lanes x 16 B = RPP rows of BK
 // bf16); wave w issues pieces w, w + 8, ... and pads to PPW pieces with duplicates of the
 // first ones (identical bytes to the same LDS address), so every wave counts the same glds per
 // stage and the waits are counted (vmcnt) rather than drains.  LDS reads are opaque asm (a
 // builtin LDS read after a glds makes the compiler drain vmcnt).  Rows of BK = 32 stages are
 // 64 B: chunk c of row r at c ^ ((r >> 2) & 3) keeps a 16-lane ds_read_b128 group on 64
-// distinct banks; BK = 64 keeps the 128-B rows and c ^ (r & 7) of head_score_kernel.
+// distinct banks; BK = 64 rows are 128 B with chunk c of row r at c ^ (r & 7) (conflict-free
+// ds_read_b128; glds images are lane-linear so the XOR goes on the source).
 // -----------------------------------------------------------------------------------------
 template <int BK>
 __device__ __forceinline__ int hs_swz(int r) {
@@ -412,158 +297,17 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
   }
 }
 
-// =========================================================================================
-// head_pool: per title u, alpha = eps-softmax(a) (stable form exp(a-m) / (sum + 1e-8 e^-m),
-// masked tokens get weight 0), pooled = sum_t alpha_t x_t (fp32).  384 threads: TG t-groups x
-// D/8 column chunks of 16 B.
-// =========================================================================================
-__global__ __launch_bounds__(384) void head_pool_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
-                                                        const float* __restrict__ a, const float* __restrict__ a2,
-                                                        const int* __restrict__ tokens,
-                                                        int T, int D, float* __restrict__ pooled,
-                                                        float* __restrict__ alpha, const int* __restrict__ nreal,
-                                                        bf16* __restrict__ pooled_b) {
-  __shared__ float a_s[MAXT];
-  __shared__ float part[3072];
-  const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (nreal != nullptr && u >= nreal[0]) {  // a padded title of a step graph: exact zeros
-    for (int d = tid; d < D; d += blockDim.x) {
-      pooled[(size_t)u * D + d] = 0.f;
-      if (pooled_b != nullptr) pooled_b[(size_t)u * D + d] = f2bf(0.f);
-    }
-    for (int t = tid; t < T; t += blockDim.x) alpha[(size_t)u * T + t] = 0.f;
-    return;
-  }
-  const int id = ids != nullptr ? ids[u] : u;
-  const bf16* xe = table + (size_t)id * T * D;
-  if (wave == 0) {
-    float av[2], m = -INFINITY;
-    bool keep[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int t = lane + 64 * c;
-      keep[c] = t < T && (tokens == nullptr || tokens[((size_t)id * 2 + 1) * T + t] != 0);
-      av[c] = keep[c] ? (a2 != nullptr ? a[(size_t)u * T + t] + a2[(size_t)u * T + t] : a[(size_t)u * T + t]) : -INFINITY;
-      m = fmaxf(m, av[c]);
-    }
-    m = wave_max(m);
-    if (!(m > -INFINITY)) m = 0.f;  // every token masked: every weight 0
-    float p[2], l = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      p[c] = keep[c] ? __expf(av[c] - m) : 0.f;
-      l += p[c];
-    }
-    const float inv = 1.0f / (wave_sum(l) + 1e-8f * __expf(-m));
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int t = lane + 64 * c;
-      if (t < T) {
-        const float al = p[c] * inv;
-        a_s[t] = al;
-        alpha[(size_t)u * T + t] = al;
-      }
-    }
-  }
-  __syncthreads();
-  const int DC = D >> 3, TG = 384 / DC;
-  const int dc = tid % DC, tg = tid / DC;
-  if (tg < TG) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int t = tg; t < T; t += TG) {
-      const bf16x8 v = *(const bf16x8*)(xe + (size_t)t * D + dc * 8);
-      const float al = a_s[t];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += al * (float)v[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) part[tg * D + dc * 8 + k] = acc[k];
-  }
-  __syncthreads();
-  for (int d = tid; d < D; d += 384) {
-    float s = 0.f;
-    for (int j = 0; j < TG; ++j) s += part[j * D + d];
-    pooled[(size_t)u * D + d] = s;
-    if (pooled_b != nullptr) pooled_b[(size_t)u * D + d] = f2bf(s);  // the fc GEMM's operand rounding
-  }
-}
-
-// =========================================================================================
-// head_pool_bwd: per title, dalpha_t = g . x_t (fp32 g = dL/dpooled), then
-// da_t = alpha_t (dalpha_t - sum_s alpha_s dalpha_s) and db2 partial = sum_t da_t.
-// =========================================================================================
-__global__ __launch_bounds__(256) void head_pool_bwd_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
-                                                            const float* __restrict__ alpha, const float* __restrict__ g,
-                                                            int T, int D, float* __restrict__ da,
-                                                            float* __restrict__ db2p, const int* __restrict__ nreal) {
-  __shared__ float dal[MAXT];
-  const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (nreal != nullptr && u >= nreal[0]) {  // a padded title: no gradient
-    for (int t = tid; t < T; t += blockDim.x) da[(size_t)u * T + t] = 0.f;
-    if (tid == 0) db2p[u] = 0.f;
-    return;
-  }
-  const int id = ids != nullptr ? ids[u] : u;
-  const bf16* xe = table + (size_t)id * T * D;
-  const float* gu = g + (size_t)u * D;
-  const int DC = D >> 3;
-  // lanes over 16-B column chunks (up to 2 per lane: D <= 1024), g chunks in registers
-  float gv[2][8];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int dc = lane + 64 * c;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) gv[c][k] = dc < DC ? gu[dc * 8 + k] : 0.f;
-  }
-  for (int t = wave; t < T; t += 4) {
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int dc = lane + 64 * c;
-      if (dc < DC) {
-        const bf16x8 v = *(const bf16x8*)(xe + (size_t)t * D + dc * 8);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s += (float)v[k] * gv[c][k];
-      }
-    }
-    s = wave_sum(s);
-    if (lane == 0) dal[t] = s;
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float al[2], dv[2], s = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int t = lane + 64 * c;
-      al[c] = t < T ? alpha[(size_t)u * T + t] : 0.f;
-      dv[c] = t < T ? dal[t] : 0.f;
-      s += al[c] * dv[c];
-    }
-    s = wave_sum(s);
-    float sd = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int t = lane + 64 * c;
-      const float v = al[c] * (dv[c] - s);
-      if (t < T) da[(size_t)u * T + t] = v;
-      sd += v;
-    }
-    sd = wave_sum(sd);
-    if (lane == 0) db2p[u] = sd;
-  }
-}
-
 // -----------------------------------------------------------------------------------------
-// Load-first forms of the two pool kernels (the default).  The kernels above start streaming a
-// title's 76.8 KB only after a serial prologue (the softmax behind a barrier; the g . x_t wave
-// sums one token after another), so a block keeps a few 16-B loads in flight at a time: 26 and
-// 31 us per step for what is one 121 MB sweep each.  Here every thread issues ALL of its X
+// The pools, load-first (round 3; the first forms that streamed a title's 76.8 KB after a serial
+// prologue -- 26 and 31 us per step -- were removed in round 6).  Every thread issues ALL of its X
 // chunks first (TPT / TPW registers of 16 B), then works on them:
-//   head_pool2      the softmax runs in every wave (no barrier before the weights), a token's
-//                   weight reaches the lanes by ds_bpermute; then the t-group sums via LDS.
-//   head_pool_bwd2  six waves over tokens t = w, w + 6, ...; the per-token wave sums are
-//                   independent chains the compiler interleaves.
-// Both keep the summation orders of the forms above (bit-identical outputs).
+//   head_pool2      per title u: alpha = eps-softmax(a) (stable form exp(a - m) / (sum + 1e-8
+//                   e^-m), masked tokens weight 0) in every wave (no barrier before the weights;
+//                   a token's weight reaches the lanes by shuffle), pooled = sum_t alpha_t x_t
+//                   (fp32) by TG t-groups x D / 8 column chunks, the t-group sums via LDS.
+//   head_pool_bwd2  per title: dalpha_t = g . x_t, da_t = alpha_t (dalpha_t - sum alpha dalpha),
+//                   db2 partial = sum_t da_t; six waves over tokens t = w, w + 6, ..., the
+//                   per-token wave sums independent chains the compiler interleaves.
 // -----------------------------------------------------------------------------------------
 template <int TPT>
 __global__ __launch_bounds__(384) void head_pool2_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
@@ -858,7 +602,7 @@ __device__ __forceinline__ void wg_transform(uint32_t base, int tid, int wave, f
 }
 
 // IL (the default): the e -> g rewrite of stage st+1 no longer runs as its own LDS round trip
-// in front of stage st's MFMAs (25 us of the 128 in isolation: FEDREC_HEAD_WG=1 measured 104);
+// in front of stage st's MFMAs (25 us of the 128 in isolation: the in-LDS-pass form measured 104);
 // its two LDS reads join the fragment reads, one wait covers both, and its VALU work is spread
 // between the MFMA groups (the MFMAs do not depend on it), its write after them.  The column
 // sums dw2 / db1 accumulate in every block (a few FMAs) and only the k-tile-0 blocks store them.
@@ -1339,76 +1083,6 @@ __global__ __launch_bounds__(384) void head_pool_bwd3_kernel(const bf16* __restr
   }
 }
 
-// head_g_rewrite: the g rewrite alone, after head_pool_bwd2 formed da: title u's e rows -> g
-// (in place) and its column partials cs[0][u] (dw2) / cs[1][u] (dsum).  384 threads: Q/8 chunks
-// x 384/(Q/8) row groups, every e chunk in flight before da is read.
-template <int ETP>
-__global__ __launch_bounds__(384) void head_g_rewrite_kernel(const float* __restrict__ da, int T, int Q,
-                                                             bf16* __restrict__ e, float* __restrict__ cs, int U,
-                                                             const int* __restrict__ nreal) {
-  __shared__ float red[2][3072];
-  const int u = blockIdx.x, tid = threadIdx.x;
-  float* cs0 = cs + (size_t)u * Q;
-  float* cs1 = cs + ((size_t)U + u) * Q;
-  if (nreal != nullptr && u >= nreal[0]) {
-    for (int q = tid; q < Q; q += blockDim.x) {
-      cs0[q] = 0.f;
-      cs1[q] = 0.f;
-    }
-    return;
-  }
-  const int EC = Q >> 3, EG = 384 / EC;
-  const int ec = tid % EC, egr = tid / EC;
-  const bool eact = egr < EG;
-  const int eg = eact ? egr : 0;
-  bf16* eu = e + (size_t)u * T * Q;
-  bf16x8 ev[ETP];
-  float dv[ETP];
-#pragma unroll
-  for (int i = 0; i < ETP; ++i) {
-    const int t = eg + EG * i;
-    const int tc = t < T ? t : T - 1;
-    ev[i] = *(const bf16x8*)(eu + (size_t)tc * Q + ec * 8);
-    dv[i] = da[(size_t)u * T + tc];
-  }
-  float sw2[8], ssum[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) sw2[k] = ssum[k] = 0.f;
-#pragma unroll
-  for (int i = 0; i < ETP; ++i) {
-    const int t = eg + EG * i;
-    if (eact && t < T) {
-      const float dav = dv[i];
-      bf16x8 o;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float f = (float)ev[i][k];
-        o[k] = f2bf(dav * (1.0f - f * f));
-        sw2[k] += dav * f;
-        ssum[k] += (float)o[k];
-      }
-      *(bf16x8*)(eu + (size_t)t * Q + ec * 8) = o;
-    }
-  }
-  if (eact) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      red[0][eg * Q + ec * 8 + k] = sw2[k];
-      red[1][eg * Q + ec * 8 + k] = ssum[k];
-    }
-  }
-  __syncthreads();
-  for (int q = tid; q < Q; q += blockDim.x) {
-    float a0 = 0.f, a1 = 0.f;
-    for (int j = 0; j < EG; ++j) {
-      a0 += red[0][j * Q + q];
-      a1 += red[1][j * Q + q];
-    }
-    cs0[q] = a0;
-    cs1[q] = a1;
-  }
-}
-
 // head_wgrad_g: P[s][q][k] = sum_{m in split s} g_mq x_mk -- a plain TN MFMA GEMM (the g tile
 // arrives ready in bf16).  Tile 384 (q: the whole head width) x 128 (k), 512 threads = 8 waves
 // as 4 (q) x 2 (k) of 96 x 64 (6 x 4 MFMA tiles, 96 accumulators), 4 LDS stages of 32 rows:
@@ -1633,7 +1307,9 @@ int g_score_rows = 0;  // head_score2 row tile: 0 = by the rounds rule, 160 / 19
 extern "C" void fr_head_score_set_rows(int r) { g_score_rows = r; }
 
 extern "C" int fr_head_supported(int D, int Q, int T) {
-  return D % 256 == 0 && D <= 1024 && (Q == 128 || Q == 256 || Q == 384) && T >= 1 && T <= MAXT;
+  // (head_pool2 holds ceil(T / (384 / (D / 8))) <= 32 rows per thread: D = 1024 up to T = 96)
+  return D % 256 == 0 && D <= 1024 && (Q == 128 || Q == 256 || Q == 384) && T >= 1 && T <= MAXT &&
+         (T + 384 / (D / 8) - 1) / (384 / (D / 8)) <= 32;
 }
 
 extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, int D, int Q, const void* W1,
@@ -1669,14 +1345,13 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
                          (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
     return 0;
   }
-  const dim3 grid((M + 127) / 128);
-#define LAUNCH_SCORE(QF)                                                                                          \
-  hipLaunchKernelGGL(head_score_kernel<QF>, grid, dim3(512), 0, s, (const bf16*)table, ids, M, T, D,             \
-                     (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, nreal)
-  if (Q == 384) LAUNCH_SCORE(6);
-  else if (Q == 256) LAUNCH_SCORE(4);
-  else LAUNCH_SCORE(2);
-#undef LAUNCH_SCORE
+  // Q = 128 / 256 (the tiny test backbones): 128-row tiles, the same pipeline
+  if (Q == 256)
+    hipLaunchKernelGGL((head_score2_kernel<4, 4, 64, 2, 4, true>), dim3((M + 127) / 128), dim3(512), 0, s,
+                       (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
+  else
+    hipLaunchKernelGGL((head_score2_kernel<2, 4, 64, 2, 4, true>), dim3((M + 127) / 128), dim3(512), 0, s,
+                       (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
   return 0;
 }
 
@@ -1694,7 +1369,8 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, i
   if (T > MAXT || D % 8 != 0 || D / 8 > 384) return 1;
   if (U == 0) return 0;
   const int TG = 384 / (D / 8), tpt = (T + TG - 1) / TG;
-  if (D <= 3072 && tpt <= 32) {  // load-first form; the first form takes the shapes past it
+  if (tpt > 32) return 1;  // (fr_head_supported excludes these shapes)
+  {
 #define LAUNCH_POOL2(N)                                                                                          \
   hipLaunchKernelGGL(head_pool2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, \
                      pooled, alpha, nreal, (bf16*)pooled_b)
@@ -1704,8 +1380,6 @@ extern "C" int fr_head_pool(const void* table, const int* ids, const float* a, i
 #undef LAUNCH_POOL2
     return 0;
   }
-  hipLaunchKernelGGL(head_pool_kernel, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, a, a2, tokens, T, D, pooled,
-                     alpha, nreal, (bf16*)pooled_b);
   return 0;
 }
 
@@ -1713,8 +1387,8 @@ extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* 
                                 int D, float* da, float* db2p, const int* nreal, hipStream_t s) {
   if (T > MAXT || D % 8 != 0 || D / 8 > 128) return 1;
   if (U == 0) return 0;
-  const int tpw = (T + 5) / 6;
-  if (tpw <= 22) {
+  const int tpw = (T + 5) / 6;  // <= 22 at T <= MAXT
+  {
 #define LAUNCH_PBWD2(N)                                                                                           \
   hipLaunchKernelGGL(head_pool_bwd2_kernel<N>, dim3(U), dim3(384), 0, s, (const bf16*)table, ids, alpha, g, T, D, \
                      da, db2p, nreal)
@@ -1724,8 +1398,6 @@ extern "C" int fr_head_pool_bwd(const void* table, const int* ids, const float* 
 #undef LAUNCH_PBWD2
     return 0;
   }
-  hipLaunchKernelGGL(head_pool_bwd_kernel, dim3(U), dim3(256), 0, s, (const bf16*)table, ids, alpha, g, T, D, da,
-                     db2p, nreal);
   return 0;
 }
 
@@ -1803,21 +1475,6 @@ extern "C" int fr_head_pool_bwd_g(const void* table, const int* ids, const float
   else if (tpw <= 11 && etp <= 8) LAUNCH_PBWD3(11, 8);
   else LAUNCH_PBWD3(22, 16);
 #undef LAUNCH_PBWD3
-  return 0;
-}
-
-// g rewrite alone (after fr_head_pool_bwd): e -> g in place + per-title column partials
-extern "C" int fr_head_g_rewrite(const float* da, int U, int T, int Q, void* e, float* cs, const int* nreal,
-                                 hipStream_t s) {
-  if (Q % 8 != 0 || Q / 8 > 384 || T > MAXT) return 1;
-  if (U == 0) return 0;
-  const int EG = 384 / (Q / 8), etp = (T + EG - 1) / EG;
-#define LAUNCH_GRW(E) \
-  hipLaunchKernelGGL((head_g_rewrite_kernel<E>), dim3(U), dim3(384), 0, s, da, T, Q, (bf16*)e, cs, U, nreal)
-  if (etp <= 7) LAUNCH_GRW(7);
-  else if (etp <= 16) LAUNCH_GRW(16);
-  else return 1;
-#undef LAUNCH_GRW
   return 0;
 }
 

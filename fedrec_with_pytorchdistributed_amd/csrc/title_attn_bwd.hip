@@ -540,7 +540,7 @@ __global__ __launch_bounds__(256, 1) void title_attn_bwd_pkernel(const bf16* __r
 
 int g_tab_variant = 1;  // 1: persistent prefetching (default), 0: one-shot
 int g_tab_cus = 0;
-int g_tab_drop_split = 1;  // dropout backward: split prefetch (FEDREC_TAB_DROP_SPLIT=0: one block)
+int g_tab_drop_split = 1;  // dropout backward: split prefetch (the variant setter's 10: one block)
 
 int tab_cus() {
   if (g_tab_cus == 0) {

@@ -22,7 +22,6 @@ no pretrained weights offline.
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -31,6 +30,11 @@ from torch import nn
 from ..config import BackboneConfig
 from .. import ops
 
+
+# the packed title path (one launch per layer op over the whole batch of titles, packed
+# attention) for the device bf16 backbone; False only in the tests comparing it with the
+# per-op path
+TITLE_PACK = True
 
 class _Embeddings(nn.Module):
     def __init__(self, c: BackboneConfig):
@@ -236,7 +240,7 @@ class Backbone(nn.Module):
         if dropout:
             return _into(self._forward_dropout(tokens, mask, P), out)
         if (tokens.is_cuda and dtype == torch.bfloat16 and c.dim % 256 == 0 and c.n_layers > 0
-                and tokens.shape[1] <= 64 and os.environ.get("FEDREC_TITLE_PACK", "1") != "0"):
+                and tokens.shape[1] <= 64 and TITLE_PACK):
             return self._forward_packed(tokens, mask, P, out)
         x = ops.embed_ln(tokens, P["word"], P["pos"], P["emb_ln_w"], P["emb_ln_b"], c.ln_eps, dtype)
         for L in P["layers"]:

@@ -11,7 +11,6 @@ from typing import Optional, Tuple
 
 import math
 
-import os
 
 import torch
 
@@ -173,11 +172,7 @@ class TextHeadFn(torch.autograd.Function):
         if _head_g_path(table.shape[-1], w2.numel(), ctx.T):
             # the G path: the pool backward also turns e into g = da (1 - e^2) (in place) with the
             # per-title column sums, and the weight gradient is a plain TN GEMM over g
-            if _HEAD_G_FUSED:
-                da, db2p, cs = lib.head_pool_bwd_g(table, ids, ctx.T, alpha, g.contiguous().float(), e, nreal)
-            else:
-                da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
-                cs = lib.head_g_rewrite(da, ctx.T, e, nreal)
+            da, db2p, cs = lib.head_pool_bwd_g(table, ids, ctx.T, alpha, g.contiguous().float(), e, nreal)
             dw1, db1, dw2, db2 = lib.head_wgrad_g(table, ids, ctx.T, e, cs, w2.reshape(-1).contiguous(), db2p, nreal)
         else:
             da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
@@ -186,28 +181,27 @@ class TextHeadFn(torch.autograd.Function):
 
 
 _HEAD_G: dict = {}
-# pool backward + g rewrite in one launch (head_pool_bwd3, e loaded once the X rows are consumed):
-# 52.4 us vs 27.8 + 22.7 us + a launch boundary; steady 0.4458 / 0.4442 vs 0.4479 / 0.4466 ms
-# (A/B/A/B, 50 steps, gpurun_out/r5ad_*); FEDREC_HEAD_G_FUSED=0: the two launches
-_HEAD_G_FUSED = __import__("os").environ.get("FEDREC_HEAD_G_FUSED", "1") == "1"
 
 
 def _head_g_path(D: int, Q: int, T: int) -> bool:
-    """The text head's backward on the G path (``head_pool_bwd_g`` + ``head_wgrad_g``): the
-    default where the shape allows (Q = 384, the DistilBERT head); ``FEDREC_HEAD_G=0`` keeps the
-    round-4 path (the e -> g rewrite inside head_wgrad) for A/B runs."""
-    import os
-
-    key = (int(D), int(Q), int(T), os.environ.get("FEDREC_HEAD_G", "1"))
+    """The text head's backward on the G path (``head_pool_bwd_g``: pool backward + the g
+    rewrite in one launch, 52.4 us vs 27.8 + 22.7 us as two; then ``head_wgrad_g``) where the
+    shape allows (Q = 384, the DistilBERT head); other head widths (Q = 128 / 256: the tiny test
+    backbones) keep the round-4 path (the e -> g rewrite inside ``head_wgrad``)."""
+    key = (int(D), int(Q), int(T))
     if key not in _HEAD_G:
-        _HEAD_G[key] = key[3] != "0" and bool(ops.native.lib().head_g_supported(key[0], key[1], key[2]))
+        _HEAD_G[key] = bool(ops.native.lib().head_g_supported(*key))
     return _HEAD_G[key]
 
 
+# the fused text head over the cache (head_score2 / head_pool2 / G path) wherever the shape allows;
+# False only in tests that compare against the round-2 path (gather + GEMM + AdditivePoolFn)
+FUSED_HEAD = True
+
+
 def fused_head_supported(table_dim: int, query_dim: int, title_len: int) -> bool:
-    """Shapes the fused text-head kernels take (D % 256 == 0, Q in {128, 256, 384}, T <= 128);
-    ``FEDREC_FUSED_HEAD=0`` keeps the round-2 gather + GEMM + pool path for A/B runs."""
-    if __import__("os").environ.get("FEDREC_FUSED_HEAD", "1") == "0":
+    """Shapes the fused text-head kernels take (D % 256 == 0, Q in {128, 256, 384}, T <= 128)."""
+    if not FUSED_HEAD:
         return False
     return bool(ops.native.lib().head_supported(int(table_dim), int(query_dim), int(title_len)))
 
@@ -529,8 +523,7 @@ def step_cast_buffers(text_encoder, user_encoder):
     w, wf, wts = _step_cast_weights(text_encoder, user_encoder)
     w1b = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
     fcb = torch.empty(wf.shape, device=w.device, dtype=torch.bfloat16)
-    fcbt = (torch.empty(wf.shape[1], wf.shape[0], device=w.device, dtype=torch.bfloat16) if SIDE_WGRAD else None)
-    return w1b, _user_weight_bufs(wts, w.device, transposed=True), (fcb, fcbt)
+    return w1b, _user_weight_bufs(wts, w.device, transposed=True), (fcb, None)
 
 
 def step_cast_lists(text_encoder, user_encoder, bufs):
@@ -539,9 +532,6 @@ def step_cast_lists(text_encoder, user_encoder, bufs):
     w1b, (wb, bqkv, wbt), (fcb, fcbt) = bufs
     src, dst = _user_cast_lists(wts, wb, bqkv, wbt)
     src, dst = [w.detach(), wf.detach()] + [t.detach() for t in src], [w1b, fcb] + dst
-    if fcbt is not None:  # (the side-stream form's fc input gradient on W^T)
-        src.append(wf.detach())
-        dst.append(fcbt.t())
     return src, dst
 
 
@@ -566,44 +556,22 @@ def step_weight_casts(text_encoder, user_encoder, bump=None, bump2=None):
     return bufs
 
 
-# Weight-gradient GEMMs on a side stream.  Nothing in the rest of a backward reads a weight
-# gradient: the user encoder's (Q|K|V, att_fc1, the pool's w2) are final once the attention
-# backward ran, the text fc's once the per-news gradient is summed, while the main stream still
-# has the input gradients and the whole text-head backward (~150 us of the config-2 step) to go.
-# They are launched on a per-device side stream forked from the main stream at that point and
-# joined back by an autograd end-of-backward callback, so the optimizer (or the in-graph Adam,
-# or a gradient all-reduce) sees them complete; under HIP-graph capture the fork / join become
-# graph edges and the replay runs them concurrently with the head backward.  Their operands are
-# marked as used on the side stream (record_stream), so the allocator does not hand their memory
-# to the main stream before the side work is done.  Off by default (``FEDREC_SIDE_WGRAD=1``
-# turns it on): measured slower in the config-2 step graph -- steady 0.539-0.549 vs 0.491-0.494
-# ms (gpurun_out/r5q_*.log): the replay of a two-stream graph left ~80 us of device idle before
-# each step (the host's next-batch read waited for the graph), and the head backward kernels
-# slowed beside the weight-gradient GEMMs (head_pool_bwd2 27.5 -> 35.9 us).  Off, the user
-# encoder's weight gradients are held back to ride in the text fc's backward launch (one launch
-# and one split-K reduce fewer), as before.
-# Only inside :func:`side_wgrads` (the engine's training step, whose parameters have no
-# ``.grad`` when the backward starts): autograd then takes the returned tensors as they are.
-# With an existing ``.grad`` it would add the returned tensor into it on the main stream at
-# once -- before the side stream wrote it.
 # register-direct small-GEMM variants (csrc/small_gemm.hip tile codes 1000 + 10 f + P) per
 # call site, measured on the config-2 shapes in the step graph (profiles/r5n_sg_rd.jsonl); a
 # launch whose operands the form does not take falls back to the automatic choice
-RD_ATT_FC1 = 1002 if os.environ.get("FEDREC_SG_RD", "1") != "0" else 0  # 32 x 32 waves, 2 k-steps in flight
-RD_DCTX = 1004 if RD_ATT_FC1 else 0
-RD_FC_DGRAD = 1032 if RD_ATT_FC1 else 0
+RD_ATT_FC1 = 1002  # 32 x 32 waves, 2 k-steps in flight
+RD_DCTX = 1004
 
 # the user encoder's Q|K|V projection fused into the attention forward launch and the additive
-# pool's input-gradient GEMM into the attention backward launch (user_attn.hip); FEDREC_QKV_ATTN=0:
-# both as their own small-GEMM launches (A/B)
-FUSED_QKV_ATTN = os.environ.get("FEDREC_QKV_ATTN", "1") != "0"
+# pool's input-gradient GEMM into the attention backward launch (user_attn.hip) where the shape
+# allows (H <= 64, d_k = 20); False only in tests comparing against the separate launches
+FUSED_QKV_ATTN = True
 
-_SIDE_STREAMS: dict = {}
-_SIDE_JOINS: set = set()
+# (Measured and not kept, round 5: the weight-gradient GEMMs forked onto a side stream beside
+# the rest of the backward -- steady 0.539-0.549 vs 0.491-0.494 ms; every kernel the side work
+# overlapped slowed down, docs/PERFORMANCE.md.  The user encoder's weight gradients are instead
+# held back to ride in the text fc's backward launch.)
 _SIDE_DEPTH = [0]
-SIDE_WGRAD = os.environ.get("FEDREC_SIDE_WGRAD", "0") == "1"
-
-
 _PENDING_GEMMS: list = []
 
 
@@ -624,17 +592,14 @@ def take_pending_gemms(room: int) -> list:
     return gs
 
 
-def side_active() -> bool:
-    return SIDE_WGRAD and _SIDE_DEPTH[0] > 0
-
-
 # Deferred split-K reduction (inside side_wgrads, i.e. the engine's step without a bucket reducer:
 # no gradient hook reads a weight gradient before the backward ends).  The text fc's backward
 # launch (its input gradient + the fc and user-encoder weight gradients) leaves the split-K
 # reduction of its weight gradients pending, and the text head's reduce launch runs it in extra
 # blocks (csrc/text_head.hip head_reduce_kernel<true>): one launch fewer per step.  Whatever is
-# still pending when the context ends is reduced then.  FEDREC_DEFER_REDUCE=0: reduce at once.
-DEFER_REDUCE = os.environ.get("FEDREC_DEFER_REDUCE", "1") != "0"
+# still pending when the context ends is reduced then.  False only in the tests comparing
+# against the standalone reduce.
+DEFER_REDUCE = True
 _DEFERRED = [False]
 
 # Early gradient reduction at N > 1 (DDP's bucket that fires inside the backward): while a step
@@ -662,13 +627,13 @@ class after_user_wgrads:
 
 
 def defer_active() -> bool:
-    return DEFER_REDUCE and _SIDE_DEPTH[0] > 0 and not SIDE_WGRAD
+    return DEFER_REDUCE and _SIDE_DEPTH[0] > 0
 
 
 class side_wgrads:
-    """Context: weight-gradient GEMMs of backwards run inside it go to the side stream (SIDE_WGRAD)
-    or leave their split-K reduction to a later launch (DEFER_REDUCE); on exit nothing is left
-    pending."""
+    """Context: the engine's training step (no bucket reducer): backwards run inside it leave
+    their weight gradients' split-K reduction to a later launch (DEFER_REDUCE); on exit nothing
+    is left pending."""
 
     def __enter__(self):
         _SIDE_DEPTH[0] += 1
@@ -680,43 +645,6 @@ class side_wgrads:
             _DEFERRED[0] = False
             ops.native.lib().small_gemm_flush_pending()
         return False
-
-
-def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    s = _SIDE_STREAMS.get(dev)
-    if s is None:
-        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
-    return s
-
-
-def side_gemms(*gs, dev_off=None) -> None:
-    """Launch ``gs`` (one small_gemm launch) on the device's side stream after everything the
-    main stream has queued so far; the main stream waits for it at the end of the backward
-    (must be called from inside an autograd backward).  On the main stream, at once, outside
-    :class:`side_wgrads` or when SIDE_WGRAD is off."""
-    if not SIDE_WGRAD or _SIDE_DEPTH[0] == 0:
-        ops.small_gemm(*gs, dev_off=dev_off)
-        return
-    main = torch.cuda.current_stream(gs[0].A.device)
-    side = _side_stream(main.device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        for g in gs:
-            for t in (g.A, g.B, g.C, g.bias, g.asum, g.gidx):
-                if t is not None:
-                    t.record_stream(side)
-        if dev_off is not None:
-            dev_off.record_stream(side)
-        ops.small_gemm(*gs, dev_off=dev_off)
-    key = (main.device, main.stream_id)
-    if key not in _SIDE_JOINS:
-        _SIDE_JOINS.add(key)
-
-        def join():
-            _SIDE_JOINS.discard(key)
-            main.wait_stream(side)
-
-        torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 def _user_enc_fwd(src, idx, wts, B: int, H: int, heads: int, hd: int, drop, dev_off, keep, casts=None,
@@ -831,12 +759,9 @@ def _user_enc_bwd(saved, du, dx, B: int, H: int, heads: int, hd: int, drop, dev_
         # LDS-DMA ring, unsplit), the weight gradients on the side stream or held back for the
         # text fc's backward launch (an end-of-backward callback runs them when no such launch comes)
         ops.small_gemm(dgrad, dev_off=dev_off)
-        if side_active():
-            side_gemms(*wg)
-        else:
-            _PENDING_GEMMS.clear()  # (left over only by a backward that raised: its tensors are gone)
-            _PENDING_GEMMS.extend(wg)
-            torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_gemms)
+        _PENDING_GEMMS.clear()  # (left over only by a backward that raised: its tensors are gone)
+        _PENDING_GEMMS.extend(wg)
+        torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_gemms)
     else:
         ops.small_gemm(dgrad, *wg, dev_off=dev_off)
     # every gradient returned as a fresh view: autograd keeps a returned gradient as .grad only
@@ -1003,7 +928,7 @@ class HeadFCFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, wt = ctx.saved_tensors
+        x, w, _ = ctx.saved_tensors
         n, K = x.shape
         N = w.shape[0]
         dy = dy.contiguous().float()
@@ -1011,30 +936,21 @@ class HeadFCFn(torch.autograd.Function):
 
         dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
         db = torch.empty(N, device=x.device, dtype=torch.float32)
-        # the input gradient on the main stream (the head backward reads it next); the weight and
-        # bias gradient (dy's column sums, from the wgrad's dy tiles) on the side stream
         wgrad = ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db)
-        if side_active():  # the input gradient here, the weight gradient on the side stream
-            if wt is not None:  # on the k-contiguous W^T [K, N]: the register-direct GEMM (dy fp32 A)
-                ops.small_gemm(ops.Gemm(dy, wt, dx, n, K, N, N, N, K), tile=RD_FC_DGRAD)
-            else:
-                ops.small_gemm(ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1))
-            side_gemms(wgrad)
-        else:
-            # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
-            # launch -- with the user encoder's weight gradients when its backward held them back
-            gs = (ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1), wgrad, *take_pending_gemms(4))
-            early = _AFTER_USER_WGRADS[0] if len(gs) > 2 else None
-            if defer_active() and early is None:  # the weight gradients' split-K reduce rides in the head's reduce launch
-                lib = ops.native.require_for(dy)
-                lib.small_gemm_set_defer(True)
-                _DEFERRED[0] = True
-                try:
-                    ops.small_gemm(*gs)
-                finally:
-                    lib.small_gemm_set_defer(False)
-            else:
+        # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
+        # launch -- with the user encoder's weight gradients when its backward held them back
+        gs = (ops.Gemm(dy, w, dx, n, K, N, N, K, K, b_mode=1), wgrad, *take_pending_gemms(4))
+        early = _AFTER_USER_WGRADS[0] if len(gs) > 2 else None
+        if defer_active() and early is None:  # the weight gradients' split-K reduce rides in the head's reduce launch
+            lib = ops.native.require_for(dy)
+            lib.small_gemm_set_defer(True)
+            _DEFERRED[0] = True
+            try:
                 ops.small_gemm(*gs)
-            if early is not None:  # the user-encoder weight gradients are final here
-                early()
+            finally:
+                lib.small_gemm_set_defer(False)
+        else:
+            ops.small_gemm(*gs)
+        if early is not None:  # the user-encoder weight gradients are final here
+            early()
         return dx, dw.view_as(dw), db.view_as(db), None, None, None

@@ -217,7 +217,7 @@ def _ipc_grad_fn(ctx: DistContext, ipc, W: int):
     _ar_ipc.kind = "ipc"
     # device epochs: the launch is capturable -- the engine puts it inside the step graph, between
     # the backward and the device-step Adam (one replay per step at N > 1, as at N = 1)
-    _ar_ipc.capturable = os.environ.get("FEDREC_GRAPH_AR", "1") != "0"
+    _ar_ipc.capturable = True
     _ar_ipc.ipc = ipc
     return _ar_ipc
 
@@ -229,9 +229,9 @@ def _rccl_grad_fn(ctx: DistContext, W: int):
         return 1.0 / W
 
     _ar.kind = "rccl" if ctx.device.type == "cuda" else dist.get_backend(ctx.data_group)
-    # RCCL inside a captured graph is opt-in (FEDREC_GRAPH_RCCL=1): the eager call on the optimizer
-    # side stream is the default for the library path
-    _ar.capturable = ctx.device.type == "cuda" and os.environ.get("FEDREC_GRAPH_RCCL", "0") == "1"
+    # the library path stays eager (on the optimizer side stream, after the step graph): the
+    # capturable all-reduce of the step graph is the device-epoch IPC one
+    _ar.capturable = False
     return _ar
 
 

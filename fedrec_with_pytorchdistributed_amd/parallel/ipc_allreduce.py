@@ -24,7 +24,6 @@ Reference call sites this replaces: ``Gradient_Averaging_main.py:119`` (DDP redu
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional
 
 import torch
@@ -50,9 +49,9 @@ class IpcAllReduce:
         if one_shot_max is None:
             # one-shot reads (W - 1) buckets per rank, two-shot 2 (W - 1) / W of one plus a second
             # barrier: one-shot for two ranks, two-shot for larger groups past 512 KB
-            one_shot_max = int(os.environ.get("FEDREC_IPC_ONE_SHOT_MAX", (8 << 20) if world <= 2 else (512 << 10)))
+            one_shot_max = (8 << 20) if world <= 2 else (512 << 10)
         if blocks is None:
-            blocks = int(os.environ.get("FEDREC_IPC_BLOCKS", 32))
+            blocks = 32
         self.cap, self.one_shot_max, self.blocks = int(cap), int(one_shot_max), int(blocks)
         self.timeout_s = float(timeout_s)
         self.id = None

@@ -31,7 +31,6 @@ from __future__ import annotations
 import collections
 import contextlib
 import math
-import os
 import time
 from typing import Callable, Dict, NamedTuple, Optional, Tuple
 
@@ -257,6 +256,9 @@ class LocalEngine:
         self.hcache = self._make_hidden_cache()
         self.catalog = None  # (CatalogPlan, data group): cooperative cache builds (set_catalog)
         self.catalog_refused: Optional[str] = None  # why parallel.catalog.attach fell back to local builds
+        # host-batch validation: encode the whole news table first (auto: when the batches would
+        # touch more titles than it has) | never | always -- the tests pin both forms
+        self.valid_table = "auto"
         self._catalog_ctrl = None
         self.epoch_table = (cfg.epoch_news_table == "on" or cfg.news_cache == "vectors"
                             or (cfg.epoch_news_table == "auto" and self.hcache is not None))
@@ -981,8 +983,8 @@ class LocalEngine:
         table = None
         if self.news_table is not None:
             table = self.news_table
-        elif (os.environ.get("FEDREC_VALID_TABLE", "1") == "2"  # 0: never, 1: auto (default), 2: always
-              or (os.environ.get("FEDREC_VALID_TABLE", "1") == "1" and n_imp * (self.cfg.npratio + 1) > self.N)):
+        elif (self.valid_table == "always"
+              or (self.valid_table == "auto" and n_imp * (self.cfg.npratio + 1) > self.N)):
             table = self.encode_all(grad=False)
             self.model.eval()
         for cand_np, his_np in validation_batches(self.shard.valid, batch_size, self.cfg.npratio,

@@ -207,7 +207,7 @@ def run_grad_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     _sync_initial(model, ctx, cfg.sync == "full")
     # large trainable sets (unfrozen backbone: ~66-110M grads) reduce in ~28 MB buckets during the
     # backward; the frozen backbone's 4.66 MB head + user encoder is one flat bucket per step
-    bucketed = not cfg.backbone.frozen and os.environ.get("FEDREC_BUCKETED", "1") != "0"
+    bucketed = not cfg.backbone.frozen and cfg.bucket_reducer
     if bucketed:
         ar = None
     else:

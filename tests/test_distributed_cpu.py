@@ -70,7 +70,8 @@ def test_bucketed_reducer_matches_flat_allreduce(tmp_path):
     bound, so whole runs differ by grid steps that Adam amplifies on near-zero coordinates.)"""
     base = ["Gradient_Averaging_main.py", "1", "16", "0", *TINY, "--backbone.frozen=0", "--backbone.dropout=0",
             "--backbone.attention_dropout=0"]
-    _ok(run_ranks([base, base], {"FEDREC_DUMP_FLAT": str(tmp_path / "flat"), "FEDREC_BUCKETED": "0"}))
+    flat = base + ["--bucket_reducer=0"]
+    _ok(run_ranks([flat, flat], {"FEDREC_DUMP_FLAT": str(tmp_path / "flat")}))
     _ok(run_ranks([base, base], {"FEDREC_DUMP_FLAT": str(tmp_path / "buck"), "FEDREC_BUCKET_MB": "0.05"}))
     a = torch.load(tmp_path / "flat" / "rank0.pt")
     b = torch.load(tmp_path / "buck" / "rank0.pt")

@@ -241,9 +241,9 @@ def test_validation_news_table_matches_per_batch(dev, monkeypatch):
     m = FedRecModel(cfg).to(dev)
     m.build_flat()
     eng = LocalEngine(cfg, m, make_client_shards("tiny", 1)[0], dev)
-    monkeypatch.setenv("FEDREC_VALID_TABLE", "0")
+    eng.valid_table = "never"
     a = eng.validate(batch_size=64, device_batches=False)
-    monkeypatch.setenv("FEDREC_VALID_TABLE", "2")
+    eng.valid_table = "always"
     b = eng.validate(batch_size=64, device_batches=False)
     assert a["n_valid"] == b["n_valid"] > 0
     for k in ("valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):

@@ -1,7 +1,6 @@
 """Packed title rows (frozen backbone forward): row plan, row-split QKV GEMM, packed attention,
 embedding / LayerNorm row indirection, and the whole backbone against the unpacked path.
 Each kernel is compared with a plain PyTorch fp32 reference of the same op."""
-import os
 
 import pytest
 import torch
@@ -105,17 +104,15 @@ def test_backbone_packed_matches_unpacked(dev):
     te = model.text_encoder
     shard = make_client_shards("tiny", 1)[0]
     text = torch.as_tensor(shard.news_index[:800], dtype=torch.int32).to(dev)
-    old = os.environ.get("FEDREC_TITLE_PACK")
+    from fedrec_with_pytorchdistributed_amd.models import backbone as bb
+
     try:
-        os.environ["FEDREC_TITLE_PACK"] = "0"
+        bb.TITLE_PACK = False
         h0 = te.hidden(text)
-        os.environ["FEDREC_TITLE_PACK"] = "1"
+        bb.TITLE_PACK = True
         h1 = te.hidden(text)
     finally:
-        if old is None:
-            os.environ.pop("FEDREC_TITLE_PACK", None)
-        else:
-            os.environ["FEDREC_TITLE_PACK"] = old
+        bb.TITLE_PACK = True
     assert torch.isfinite(h1.float()).all()
     assert rel_err(h1, h0) < 1e-2
     v0, v1 = te.head(h0), te.head(h1)

@@ -45,7 +45,6 @@ raises(F.multi_cast, [x], [])
 raises(F.multi_cast, [], [x])
 raises(F.multi_copy, [x, x], [x], [0, 0])
 raises(F.head_pool_bwd, bf, None, 50, x, x, None)
-raises(F.head_g_rewrite, x.reshape(-1), 4, bf, None)
 raises(F.head_wgrad_g, bf, None, 50, bf, x, x.reshape(-1), x.reshape(-1), None)
 raises(F.segment_sum_rows, x, i32, i32, 7, 0.0, 0.0, 0, 0, None, False, None)
 raises(F.ipc_allreduce_, 0, x.reshape(-1), 1, 0, 8, 1.0)

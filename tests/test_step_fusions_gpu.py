@@ -4,7 +4,7 @@ arithmetic, so after a few training steps the losses, gradients and parameters a
 those of the unfused launches.
 
 * _HEAD_G_FUSED: the text head's pool backward and g rewrite in one launch (head_pool_bwd3) vs
-  head_pool_bwd2 + head_g_rewrite;
+  head_pool_bwd2 + the g rewrite (a separate launch until round 5, removed in round 6);
 * DEFER_REDUCE: the text fc backward's split-K reduce in the head's reduce launch (see also
   test_deferred_reduce_gpu.py)."""
 import pytest

@@ -37,11 +37,15 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-20))
 
 
-@pytest.mark.parametrize("U,T,masked", [(257, 50, False), (257, 50, True), (40, 17, False), (3, 50, False),
-                                        (1664, 50, False), (40, 64, False), (30, 100, True), (20, 128, False)])
-def test_fused_text_head_matches_fp32_oracle(dev, U, T, masked):
+@pytest.mark.parametrize("U,T,masked,D", [(257, 50, False, 768), (257, 50, True, 768), (40, 17, False, 768),
+                                          (3, 50, False, 768), (1664, 50, False, 768), (40, 64, False, 768),
+                                          (30, 100, True, 768), (20, 128, False, 768),
+                                          (257, 50, True, 256), (1000, 50, False, 512), (30, 96, False, 1024)])
+def test_fused_text_head_matches_fp32_oracle(dev, U, T, masked, D):
+    """(D = 256 / 512: Q = 128 / 256, head_score2's 128-row form and the round-4 weight gradient;
+    D = 1024 at T = 96: the widest head_pool2 form)"""
     g = torch.Generator(device="cpu").manual_seed(U * 100 + T)
-    N, D, Q = 300, 768, 384
+    N, Q = 300, D // 2 if D < 768 else 384
     table = torch.randn(N * T, D, generator=g).to(dev, torch.bfloat16)
     ids = torch.randint(0, N, (U,), generator=g, dtype=torch.int32)
     ids[: min(U, 5)] = 0  # padded slots (the step graphs pad the unique list with news 0)
@@ -120,7 +124,7 @@ def test_engine_head_uses_fused_kernels_over_cache(dev):
     params = [te.additive_attention.att_fc1.weight, te.additive_attention.att_fc1.bias,
               te.additive_attention.att_fc2.weight, te.additive_attention.att_fc2.bias, te.fc.weight, te.fc.bias]
     g1 = torch.autograd.grad(v, params, gv)
-    os.environ["FEDREC_FUSED_HEAD"] = "0"
+    OF.FUSED_HEAD = False
     try:
         te2 = copy.deepcopy(te)
         te2.__dict__.pop("_fused_ok", None)
@@ -131,7 +135,7 @@ def test_engine_head_uses_fused_kernels_over_cache(dev):
                    te2.fc.bias]
         g2 = torch.autograd.grad(v2, params2, gv)
     finally:
-        os.environ.pop("FEDREC_FUSED_HEAD", None)
+        OF.FUSED_HEAD = True
     assert _rel(v, v2) < 5e-3
     for i, (a, b) in enumerate(zip(g1, g2)):
         if i == 3:  # att_fc2.bias: cancellation noise on both paths (see the oracle test)
@@ -224,8 +228,6 @@ def test_head_g_path_matches_round4_path(dev, U, T, padded):
     gradient is a plain TN GEMM over g: head_pool_bwd_g + head_wgrad_g) against the round-4 path
     (the rewrite inside head_wgrad's LDS pipeline).  Both consume the same bf16 g values, so the
     gradients agree to fp32 summation order; padded titles (nreal) are skipped on both."""
-    import os
-
     g = torch.Generator(device="cpu").manual_seed(U + T)
     N, D, Q = 2000, 768, 384
     table = torch.randn(N * T, D, generator=g).to(dev, torch.bfloat16)
@@ -239,19 +241,22 @@ def test_head_g_path_matches_round4_path(dev, U, T, padded):
     w2 = (torch.randn(1, Q, generator=g) / math.sqrt(Q) * 3).to(dev).requires_grad_(True)
     b2 = torch.randn(1, generator=g).to(dev).requires_grad_(True)
     gout = torch.randn(U, D, generator=g).to(dev)
-    assert native.lib().head_g_supported(D, Q, T)
+    lib = native.lib()
+    assert lib.head_g_supported(D, Q, T)
+    w1b = w1.detach().to(torch.bfloat16)
+    w2f = w2.detach().reshape(-1).contiguous()
+    e, a = lib.head_score(table, ids, T, w1b, b1.detach(), w2f, b2.detach().reshape(-1), True, nreal)
+    _, alpha, _ = lib.head_pool(table, ids, T, a, None, nreal, False)
     out = {}
-    for path in ("1", "0"):
-        os.environ["FEDREC_HEAD_G"] = path
-        try:
-            pooled, _ = OF.TextHeadFn.apply(w1, b1, w2, b2, table, ids, T, None, nreal)
-            out[path] = torch.autograd.grad(pooled, (w1, b1, w2, b2), gout)
-        finally:
-            os.environ.pop("FEDREC_HEAD_G", None)
+    eg = e.clone()  # (the G path rewrites e into g in place)
+    da, db2p, cs = lib.head_pool_bwd_g(table, ids, T, alpha, gout, eg, nreal)
+    out["1"] = lib.head_wgrad_g(table, ids, T, eg, cs, w2f, db2p, nreal)
+    da0, db2p0 = lib.head_pool_bwd(table, ids, T, alpha, gout, nreal)
+    out["0"] = lib.head_wgrad(table, ids, T, e, da0, w2f, db2p0, nreal)
     torch.cuda.synchronize()
-    for name, a, b in zip(("dW1", "db1", "dw2"), out["1"][:3], out["0"][:3]):
-        assert torch.isfinite(a).all(), name
-        assert _rel(a, b) < 1e-4, (name, _rel(a, b))
+    for name, a_, b_ in zip(("dW1", "db1", "dw2"), out["1"][:3], out["0"][:3]):
+        assert torch.isfinite(a_).all(), name
+        assert _rel(a_, b_) < 1e-4, (name, _rel(a_, b_))
     assert float((out["1"][3] - out["0"][3]).abs().max()) <= 1e-6 * float(out["0"][2].norm()) + 1e-7
 
 
@@ -282,10 +287,11 @@ def test_head_wgrad_g_matches_fp32(dev, U, padded):
 
 
 @pytest.mark.parametrize("U,T,padded", [(1577, 50, True), (257, 50, False), (40, 17, False), (30, 100, True)])
-def test_head_pool_bwd_g_fused_matches_two_launches(dev, U, T, padded):
+def test_head_pool_bwd_g_matches_pool_bwd_and_oracle(dev, U, T, padded):
     """head_pool_bwd_g (pool backward + the g rewrite of the title's e rows + its column partials
-    in one launch, e loaded after the X rows are consumed) against head_pool_bwd then
-    head_g_rewrite: same arithmetic in the same order -- da, db2p, g and the partials bitwise."""
+    in one launch, e loaded after the X rows are consumed): da / db2p bitwise head_pool_bwd's
+    (same arithmetic, same order); g = da (1 - e^2) rounded to bf16 and the per-title column
+    partials cs[0] = sum_t da_t e_t, cs[1] = sum_t g_t against an fp32 torch oracle."""
     g = torch.Generator(device="cpu").manual_seed(3 * U + T)
     N, D, Q = 2000, 768, 384
     lib = native.lib()
@@ -298,11 +304,18 @@ def test_head_pool_bwd_g_fused_matches_two_launches(dev, U, T, padded):
     alpha = torch.softmax(torch.randn(U, T, generator=g), 1).to(dev)
     gp = torch.randn(U, D, generator=g).to(dev)
     e0 = torch.tanh(torch.randn(U * T, Q, generator=g)).to(dev, torch.bfloat16)
-    e1, e2 = e0.clone(), e0.clone()
+    e1 = e0.clone()
     da1, db1, cs1 = lib.head_pool_bwd_g(table, ids, T, alpha, gp, e1, nreal)
     da2, db2 = lib.head_pool_bwd(table, ids, T, alpha, gp, nreal)
-    cs2 = lib.head_g_rewrite(da2, T, e2, nreal)
     torch.cuda.synchronize()
     assert torch.equal(da1, da2) and torch.equal(db1, db2)
-    assert torch.equal(e1, e2)
-    assert torch.equal(cs1, cs2)
+    n = R * T
+    ef = e0[:n].float()
+    dav = da2.reshape(-1)[:n].view(-1, 1)
+    gref = (dav * (1.0 - ef * ef)).to(torch.bfloat16)
+    # one bf16 ulp: the kernel's fp32 expression may round once differently before the cast
+    assert float(((e1[:n].float() - gref.float()).abs() - gref.float().abs() * 2 ** -7).max()) <= 1e-30
+    cs0 = (dav * ef).view(R, T, Q).sum(1)
+    cs1r = gref.float().view(R, T, Q).sum(1)
+    assert _rel(cs1[0, :R], cs0) < 1e-5, _rel(cs1[0, :R], cs0)
+    assert _rel(cs1[1, :R], cs1r) < 1e-4, _rel(cs1[1, :R], cs1r)
