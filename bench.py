@@ -218,7 +218,7 @@ def main() -> int:
     counts0 = dict(eng.counts)
     # --step-events (diagnostic, off by default): a timing event after every step's launch
     # on the main stream -- where the device time of the timed window goes (start-up, per step, tail)
-    evs = [] if (a.step_events and dev.type == "cuda") else None
+    evs = [] if (args.step_events and dev.type == "cuda") else None
     if evs is not None:
         evs.append(torch.cuda.Event(enable_timing=True))
         evs[-1].record()
