@@ -33,12 +33,22 @@ def main():
     ap.add_argument("--N", type=int, default=65000)
     ap.add_argument("--T", type=int, default=50)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--ids", default="perm", choices=["perm", "sorted", "pool64", "same"],
+                    help="which cache titles a step reads: random (perm, the real case), random sorted, "
+                         "64 distinct titles (L2 / Infinity-Cache resident) or one title: where the X "
+                         "rows are served from, to tell fetch-bound from compute-bound kernels")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     D, Q, T, U = 768, 384, a.T, a.U
     g = torch.Generator(device=dev).manual_seed(0)
     table = torch.randn(a.N * T, D, device=dev, generator=g).to(torch.bfloat16)
     ids = torch.randperm(a.N, device=dev, generator=g)[:U].to(torch.int32)
+    if a.ids == "sorted":
+        ids = ids.sort().values
+    elif a.ids == "pool64":
+        ids = ids[:64].repeat((U + 63) // 64)[:U].contiguous()
+    elif a.ids == "same":
+        ids = ids[:1].repeat(U).contiguous()
     w1 = (torch.randn(Q, D, device=dev, generator=g) / math.sqrt(D)).to(torch.bfloat16)
     b1 = torch.randn(Q, device=dev, generator=g) * 0.1
     w2 = torch.randn(Q, device=dev, generator=g) / math.sqrt(Q)
@@ -51,7 +61,7 @@ def main():
     da, db2p = lib.head_pool_bwd(table, ids, T, alpha, gout)
     out = []
     t = timeit(lambda: lib.head_score(table, ids, T, w1, b1, w2, b2, True), a.iters)
-    out.append({"kernel": "head_score", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1)})
+    out.append({"kernel": "head_score", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1), "ids": a.ids})
     for rows in (192, 160):  # the row tile forced (the default picks by the rounds rule)
         lib.head_score_set_rows(rows)
         t = timeit(lambda: lib.head_score(table, ids, T, w1, b1, w2, b2, True), a.iters)
@@ -90,7 +100,7 @@ def main():
     out.append({"kernel": "r2_wgrad", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1)})
     for r in out:
         r.update({"U": U, "T": T, "M": M})
-        print(json.dumps(r), flush=True)
+        print(json.dumps({**r, "ids": a.ids}), flush=True)
 
 
 if __name__ == "__main__":
