@@ -3,8 +3,10 @@ each switch (a module flag of ops/functional.py) only changes where the arithmet
 arithmetic, so after a few training steps the losses, gradients and parameters are bitwise
 those of the unfused launches.
 
-* _HEAD_G_FUSED: the text head's pool backward and g rewrite in one launch (head_pool_bwd3) vs
-  head_pool_bwd2 + the g rewrite (a separate launch until round 5, removed in round 6);
+* FUSED_QKV_ATTN: the user encoder's Q|K|V projection inside the attention forward launch and
+  the pool's input-gradient GEMM inside the attention backward launch vs their own small-GEMM
+  launches (the text head's pool backward + g rewrite fusion, pinned here until round 5, lost
+  its unfused form in round 6: tests/test_text_head_gpu.py checks it against an fp32 oracle);
 * DEFER_REDUCE: the text fc backward's split-K reduce in the head's reduce launch (see also
   test_deferred_reduce_gpu.py)."""
 import pytest
@@ -34,7 +36,7 @@ def _run(dev, steps, mask_padding=False):
     return torch.stack([torch.as_tensor(x, device=dev).float().reshape(()) for x in losses]), eng.flat.flat.clone()
 
 
-@pytest.mark.parametrize("flag", ["_HEAD_G_FUSED", "DEFER_REDUCE"])
+@pytest.mark.parametrize("flag", ["FUSED_QKV_ATTN", "DEFER_REDUCE"])
 @pytest.mark.parametrize("mask_padding", [False, True])
 def test_step_fusion_is_bitwise(dev, flag, mask_padding):
     saved = getattr(OF, flag)
