@@ -147,6 +147,12 @@ class FedRecConfig:
     # coordinator; PA: on every client, identically (the same inputs give bitwise-same models)
     server_lr: float = 1.0
     server_momentum: float = 0.0
+    # "sgd": the step above; "adam": FedAdam (Reddi et al. 2021) on the pseudo-gradient
+    # d = mean_k theta_k - theta_g: m = momentum m + (1 - momentum) d, v = beta2 v + (1 - beta2)
+    # d^2, theta = theta_g + server_lr m / (sqrt(v) + tau)
+    server_opt: str = "sgd"
+    server_beta2: float = 0.99
+    server_tau: float = 1e-3
     pa_average_moments: bool = False  # PA: average the clients' Adam m / v with the parameters
     # unfrozen backbone (GA): reduce the gradient in ~28 MB buckets during the backward (DDP's
     # reducer, parallel/reducer.py); False = one flat all-reduce after it

@@ -174,28 +174,47 @@ class ServerStep:
     the coordinator and in fp32 on the device for parameter averaging (every PA client applies it
     to the same all-reduced mean, so the clients stay bitwise identical)."""
 
-    def __init__(self, lr: float = 1.0, momentum: float = 0.0):
-        self.lr, self.momentum = float(lr), float(momentum)
-        self.v: Optional[torch.Tensor] = None
+    def __init__(self, lr: float = 1.0, momentum: float = 0.0, opt: str = "sgd", beta2: float = 0.99,
+                 tau: float = 1e-3):
+        if opt not in ("sgd", "adam"):
+            raise ValueError(f"server_opt={opt!r}: expected sgd | adam")
+        self.lr, self.momentum, self.opt = float(lr), float(momentum), opt
+        self.beta2, self.tau = float(beta2), float(tau)
+        self.v: Optional[torch.Tensor] = None  # sgd: the momentum buffer; adam: the first moment
+        self.s: Optional[torch.Tensor] = None  # adam: the second moment
+
+    @classmethod
+    def from_cfg(cls, cfg) -> "ServerStep":
+        return cls(cfg.server_lr, cfg.server_momentum, cfg.server_opt, cfg.server_beta2, cfg.server_tau)
 
     @property
     def active(self) -> bool:
-        return self.lr != 1.0 or self.momentum != 0.0
+        return self.opt == "adam" or self.lr != 1.0 or self.momentum != 0.0
 
     def apply(self, theta_g: torch.Tensor, avg: torch.Tensor) -> torch.Tensor:
         """The new global model from the round's global ``theta_g`` and the clients' mean."""
         if not self.active:
             return avg
         d = avg - theta_g
+        if self.opt == "adam":  # FedAdam: per-coordinate normalised server step
+            self.v = ((1 - self.momentum) * d if self.v is None
+                      else self.v.to(d.device).mul_(self.momentum).add_(d, alpha=1 - self.momentum))
+            self.s = ((1 - self.beta2) * d * d if self.s is None
+                      else self.s.to(d.device).mul_(self.beta2).addcmul_(d, d, value=1 - self.beta2))
+            return theta_g + self.lr * self.v / (self.s.sqrt() + self.tau)
         self.v = d if self.v is None else self.v.to(d.device).mul_(self.momentum).add_(d)
         return theta_g + self.lr * self.v
 
     def state(self) -> Optional[Dict]:
-        return {"v": self.v} if self.active and self.v is not None else None
+        if not self.active or self.v is None:
+            return None
+        return {"v": self.v, **({"s": self.s} if self.s is not None else {})}
 
     def load(self, st: Optional[Dict]) -> None:
         if st and st.get("v") is not None:
             self.v = st["v"].clone()
+        if st and st.get("s") is not None:
+            self.s = st["s"].clone()
 
 
 # ---------------------------------------------------------------------------------------
@@ -244,7 +263,7 @@ def run_param_avg(cfg: FedRecConfig, ctx: DistContext) -> Dict:
     selfcheck(ctx, log=obs.log)
     shard = load_client_shard(cfg, ctx)
     model = build_model(cfg, ctx.device)
-    server = ServerStep(cfg.server_lr, cfg.server_momentum)
+    server = ServerStep.from_cfg(cfg)
     start, est = _resume(cfg, model, server)
     full = cfg.sync == "full"
     _sync_initial(model, ctx, full)
@@ -478,7 +497,7 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
     cp = ControlPlane.from_default(run_id, cfg.round_timeout_s)
     W = ctx.num_clients
     model = build_model(cfg, torch.device("cpu"))
-    server = ServerStep(cfg.server_lr, cfg.server_momentum)  # off by default: the plain mean
+    server = ServerStep.from_cfg(cfg)  # off by default: the plain mean
     start_round = 0
     if cfg.snapshot_path and os.path.exists(cfg.snapshot_path):
         info = ckpt.load_snapshot(cfg.snapshot_path, model)
@@ -544,7 +563,7 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                 new = (acc / sum(weights)).float()
         last_accepted = list(accepted)
         with torch.no_grad():
-            if server.active:  # FedAvgM / server learning rate on the round's mean (fp64)
+            if server.active:  # FedAvgM / server learning rate / FedAdam on the round's mean (fp64)
                 new = server.apply(model.flat.flat.detach().double(), new.double()).float()
             model.flat.flat.copy_(new)
         dt = time.perf_counter() - t0

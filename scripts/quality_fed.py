@@ -48,11 +48,15 @@ def runs(world, epochs, preset):
 
 
 SERVER_VARIANTS = [("m9", ["--server_momentum=0.9"]), ("lr3", ["--server_lr=3.0"]),
-                   ("lr3m5", ["--server_lr=3.0", "--server_momentum=0.5"])]
+                   ("lr3m5", ["--server_lr=3.0", "--server_momentum=0.5"]),
+                   ("adam1e2", ["--server_opt=adam", "--server_lr=0.01", "--server_momentum=0.9"]),
+                   ("adam3e3", ["--server_opt=adam", "--server_lr=0.003", "--server_momentum=0.9"])]
 PA_VARIANTS = [("mv", ["--pa_average_moments=1"]), ("mv_lr2", ["--pa_average_moments=1", "--server_lr=2.0"]),
                ("mv_m5", ["--pa_average_moments=1", "--server_momentum=0.5"]),
                ("mv_lr3", ["--pa_average_moments=1", "--server_lr=3.0"]),
-               ("mv_lr2m5", ["--pa_average_moments=1", "--server_lr=2.0", "--server_momentum=0.5"])]
+               ("mv_lr2m5", ["--pa_average_moments=1", "--server_lr=2.0", "--server_momentum=0.5"]),
+               ("mv_lr4", ["--pa_average_moments=1", "--server_lr=4.0"]),
+               ("k4_mv_lr2", ["--pa_average_moments=1", "--server_lr=2.0", "--param_avg_every=4"])]
 
 
 def main():
@@ -66,7 +70,7 @@ def main():
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     for name, argvs in runs(a.world, a.epochs, a.preset):
-        if a.only and a.only not in name:
+        if a.only and not any(o in name for o in a.only.split(",")):
             continue
         d = os.path.abspath(os.path.join(a.out, name))
         os.makedirs(d, exist_ok=True)

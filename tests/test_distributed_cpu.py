@@ -187,6 +187,18 @@ def test_server_step_math():
     s2 = ServerStep(lr=1.5, momentum=0.9)
     s2.load(s.state())  # resume carries the momentum
     assert torch.equal(s2.v, s.v)
+    # FedAdam: m = b1 m + (1 - b1) d, v = b2 v + (1 - b2) d^2, theta = theta_g + lr m / (sqrt(v) + tau)
+    fa = ServerStep(lr=0.01, momentum=0.9, opt="adam", beta2=0.99, tau=1e-3)
+    t1 = fa.apply(th0, a0)
+    m1, v1 = 0.1 * a0, 0.01 * a0 * a0
+    assert torch.allclose(t1, th0 + 0.01 * m1 / (v1.sqrt() + 1e-3))
+    t2 = fa.apply(t1, a1)
+    d1 = a1 - t1
+    m2, v2 = 0.9 * m1 + 0.1 * d1, 0.99 * v1 + 0.01 * d1 * d1
+    assert torch.allclose(t2, t1 + 0.01 * m2 / (v2.sqrt() + 1e-3))
+    fb = ServerStep(opt="adam")
+    fb.load(fa.state())
+    assert torch.equal(fb.s, fa.s) and torch.equal(fb.v, fa.v)
 
 
 @pytest.mark.slow
