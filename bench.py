@@ -75,6 +75,7 @@ def main() -> int:
     ap.add_argument("--cache-warm", type=int, default=512,
                     help="titles run through the backbone (result dropped) before the timed cache build")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the untimed learning probe after the round")
     ap.add_argument("--step-events", action="store_true",
                     help="diagnostic: a timing event after every timed step's launch (device interval per step)")
     ap.add_argument("--news-cache", default="auto", choices=["auto", "hidden", "none"],
@@ -354,6 +355,27 @@ def main() -> int:
     elif not args.no_valid:
         auc = reduce_valid(eng.validate(batch_size=256, limit=args.valid_limit))
 
+    # learning probe (after everything above, untimed): the reference's sigmoid-CE scorer keeps
+    # this shard at chance (docs/PARITY.md: the reference's own loop does too), so the round's
+    # valid_auc says nothing about whether the engine learns at the headline shape.  One more
+    # local epoch with the plain-CE scorer (score_act=identity, the quality runs' setting) from
+    # where the round left the model, then the validation AUC.  The step graphs were captured
+    # with the reference scorer: they are dropped and re-captured.
+    probe = None
+    if do_round and not args.no_probe:
+        cfg.score_act = "identity"
+        eng._graphs.clear()
+        eng.sync_params()
+        sync()
+        if ctx.initialized:
+            dist.barrier(group=ctx.ctrl_group)
+        tp = time.perf_counter()
+        stp = eng.train_epoch(max_steps=steps_per_epoch)
+        mvp = eng.validate(batch_size=256)
+        probe = {"score_act": "identity", "lr": cfg.lr, "epochs": 1, "steps": stp["steps"],
+                 "train_loss": round(stp["training_loss"], 5), "valid_auc": round(reduce_valid(mvp), 4),
+                 "wall_s": round(max_over_ranks(time.perf_counter() - tp), 3)}
+
     amort = 0.0 if cache_s is None else cache_s * args.steps / steps_per_epoch
     charged = elapsed + amort
     imps = args.batch * args.steps * world
@@ -418,6 +440,7 @@ def main() -> int:
             {"backend": dist.get_backend(ctx.data_group), "size": dist.get_world_size(ctx.data_group)},
             "data_plane_selfcheck": selfcheck or None,
             "ipc_allreduce": ipc_info,
+            "learning_probe": probe,
         }
         if rnd is not None:
             out.update(rnd)
