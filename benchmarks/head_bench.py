@@ -63,10 +63,14 @@ def main():
     t = timeit(lambda: lib.head_score(table, ids, T, w1, b1, w2, b2, True), a.iters)
     out.append({"kernel": "head_score", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1), "ids": a.ids})
     for rows in (192, 160):  # the row tile forced (the default picks by the rounds rule)
-        lib.head_score_set_rows(rows)
-        t = timeit(lambda: lib.head_score(table, ids, T, w1, b1, w2, b2, True), a.iters)
-        out.append({"kernel": f"head_score_{rows}rows", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1)})
+        for ilv in (0, 1):
+            lib.head_score_set_rows(rows)
+            lib.head_score_set_ilv(ilv)
+            t = timeit(lambda: lib.head_score(table, ids, T, w1, b1, w2, b2, True), a.iters)
+            out.append({"kernel": f"head_score_{rows}rows_ilv{ilv}", "us": round(t, 1),
+                        "TFs": round(2 * M * Q * D / t / 1e6, 1)})
     lib.head_score_set_rows(0)
+    lib.head_score_set_ilv(1)
     t = timeit(lambda: lib.head_pool(table, ids, T, sc, None), a.iters)
     out.append({"kernel": "head_pool", "us": round(t, 1), "TBs": round(M * D * 2 / t / 1e6, 2)})
     t = timeit(lambda: lib.head_pool_bwd(table, ids, T, alpha, gout), a.iters)
@@ -82,13 +86,8 @@ def main():
                     "TBs": round(M * (D + 2 * Q) * 2 / t / 1e6, 2)})
         eg.copy_(e)
         _, _, cs = lib.head_pool_bwd_g(table, ids, T, alpha, gout, eg)
-        for kt in (4128,):  # (one form left)
-            lib.head_wgrad_g_set_kt(kt)
-            t = timeit(lambda: lib.head_wgrad_g(table, ids, T, eg, cs, w2, db2p), a.iters)
-            out.append({"kernel": f"head_wgrad_g_kt{kt % 1000}_st{kt // 1000 or 3}(+reduce)", "us": round(t, 1),
-                        "TFs": round(2 * M * Q * D / t / 1e6, 1)})
-        lib.head_wgrad_g_set_kt(4128)
-        lib.head_wgrad_g_set_kt(0)
+        t = timeit(lambda: lib.head_wgrad_g(table, ids, T, eg, cs, w2, db2p), a.iters)
+        out.append({"kernel": "head_wgrad_g(+reduce)", "us": round(t, 1), "TFs": round(2 * M * Q * D / t / 1e6, 1)})
     # the round-2 pieces for reference: gather + plain GEMM + wgrad of a materialised dpre
     hid = table.view(a.N, T, D).index_select(0, ids.long()).reshape(M, D)
     t = timeit(lambda: table.view(a.N, T, D).index_select(0, ids.long()), a.iters)

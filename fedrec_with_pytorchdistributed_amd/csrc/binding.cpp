@@ -89,6 +89,7 @@ int fr_user_pool_score(const float* x, const float* e, const float* w2, const fl
                        float* scores, float* dcand, float* loss_total, float* dctx, float* dpre, void* dpre_b,
                        float* da8, hipStream_t s);
 void fr_head_score_set_rows(int r);
+void fr_head_score_set_ilv(int v);
 int fr_segment_sum_rows_ldp(const float* rows, const int* perm, const int* seg_ptr, const int* inv, float* out, int U,
                             int D, int R, float* scratch, float clip, float noise_std, unsigned long long seed,
                             unsigned long long offset, const unsigned long long* dev_off, hipStream_t s);
@@ -1919,6 +1920,7 @@ void segsum_set_variant(int64_t v) { fr_segsum_set_variant((int)v); }
 void segsum_set_ldp_block(int64_t v) { fr_segsum_set_ldp_block((int)v); }
 void small_gemm_set_rd(int64_t v) { fr_small_gemm_set_rd((int)v); }
 void head_score_set_rows(int64_t r) { fr_head_score_set_rows((int)r); }
+void head_score_set_ilv(int64_t v) { fr_head_score_set_ilv((int)v); }
 void ln_set_wide(int64_t v) { fr_ln_set_wide((int)v); }
 
 }  // namespace
@@ -1933,6 +1935,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("small_gemm_set_rd(int v) -> ()", &small_gemm_set_rd);
   m.def("user_pool_score(Tensor x, Tensor e, Tensor w2, Tensor b2, Tensor? keep, Tensor table, Tensor ci, int act, Tensor(a!) dcand_out, bool want_bwd) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("head_score_set_rows(int r) -> ()", &head_score_set_rows);
+  m.def("head_score_set_ilv(int v) -> ()", &head_score_set_ilv);
   m.def("ln_set_wide(int v) -> ()", &ln_set_wide);
   m.def("linear(Tensor x, Tensor w, Tensor? b, int act, Tensor? residual) -> Tensor");
   m.def("linear_gelu_bwd(Tensor x, Tensor w, Tensor z) -> (Tensor, Tensor)");

@@ -121,7 +121,14 @@ __device__ __forceinline__ void lgkm_tie_rt(int n, u32x4_t& r) {  // n folds to 
   }
 }
 
-template <int QF, int RF, int BK, int NST, int WQ = 4, bool SW = false>
+// ILV (with SW): the next stage's PPW glds pieces are issued between the MFMA rows of this
+// stage (one per row) instead of all at once after the barrier -- an LDS-DMA piece costs ~60-185
+// issue cycles (MI355X_MICROARCH.md, per-instruction table), ~1,000 per wave per stage that
+// otherwise sit between the barrier and the first MFMA.  Standalone (benchmarks/head_bench.py,
+// 1600 titles): 192-row tiles 78.0 -> 67.4 us, 160-row tiles 64.8 -> 61.1 us; inside the step
+// graph neutral (0.4414 vs 0.4414 ms, profiles/r6_ab_head_ilv.jsonl).  The default; the plain
+// form stays for the bitwise test (head_score_set_ilv(0)).
+template <int QF, int RF, int BK, int NST, int WQ = 4, bool SW = false, bool ILV = false>
 __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restrict__ table, const int* __restrict__ ids,
                                                              int M, int T, int D, const bf16* __restrict__ W1,
                                                              const float* __restrict__ b1, const float* __restrict__ w2,
@@ -185,6 +192,13 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
       __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src[i] + k0),
                                        LDS_PTR(void, smem + stage * ST + dst[i]), 16, 0, 0);
   };
+  auto issue_one = [&](int i, int stage, int k0) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_global_load_lds(GLOBAL_PTR(const void, src[i] + k0),
+                                     LDS_PTR(void, smem + stage * ST + dst[i]), 16, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  static_assert(!ILV || (SW && PPW <= KS * QFW), "interleaved issue: one piece per MFMA row");
 
   f32x4 acc[QFW][RFW];
 #pragma unroll
@@ -203,7 +217,9 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
     if (NST >= 4 && younger >= 2) hs_wait_sync<(NST >= 4 ? 2 * PPW : 0)>();
     else if (NST >= 3 && younger >= 1) hs_wait_sync<(NST >= 3 ? PPW : 0)>();
     else hs_wait_sync<0>();
-    if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, (kt + NST - 1) * BK);
+    const bool nxt = kt + NST - 1 < nk;
+    const int nst = (kt + NST - 1) % NST, nk0 = (kt + NST - 1) * BK;
+    if (!ILV && nxt) issue(nst, nk0);
     const uint32_t As = lds0 + (kt % NST) * ST, Ws = As + MR * RB;
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
@@ -233,6 +249,10 @@ __global__ __launch_bounds__(512, 1) void head_score2_kernel(const bf16* __restr
           for (int j = 0; j < RFW; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wr[i]),
                                                                 __builtin_bit_cast(bf16x8, xr[j]), acc[i][j], 0, 0, 0);
+          if constexpr (ILV) {
+            const int pc_ = kk * QFW + i;
+            if (pc_ < PPW && nxt) issue_one(pc_, nst, nk0);
+          }
         }
         __builtin_amdgcn_s_setprio(0);
         continue;
@@ -1112,11 +1132,13 @@ __device__ __forceinline__ uint32_t tr_off_pitch(int pitch, int r0, int col0, in
   return (uint32_t)(r * pitch + ((c ^ swz(r)) << 4) + (p & 1) * 8);
 }
 
-// a fragment = two ds_read_b64_tr_b16 four rows apart: the second at an immediate offset
+// a fragment = two ds_read_b64_tr_b16 four rows apart: the second at an immediate offset.
+// `a` is early-clobber: the first read's destination must not be the address register the
+// second read still needs (the return can land before a queued second read issues).
 template <int OFF>
 __device__ __forceinline__ void tr_read2(uint32_t addr, s16x4& a, s16x4& b) {
   asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:%3"
-               : "=v"(a), "=v"(b)
+               : "=&v"(a), "=v"(b)
                : "v"(addr), "n"(OFF));
 }
 
@@ -1182,7 +1204,7 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_g_kernel(const bf16* __rest
   const uint32_t x_coff = (uint32_t)(k0 + 8 * x_c);  // bf16 elements within the row
   int x_t = (mb + x_row) % T, x_u = (mb + x_row) / T;  // once per block
   const size_t DD = (size_t)D;
-  auto stage = [&](int buf, int m) {
+  auto stage = [&](int buf, int m) __attribute__((always_inline)) {
     char* base = smem + buf * GSTB;
     const char* gm_ptr = (const char*)(G + (size_t)m * GQT);  // uniform
     if (m + WTM <= me) {  // every row of the stage is real (uniform): no per-lane select
@@ -1232,7 +1254,9 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_g_kernel(const bf16* __rest
     else if (inflight == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (st + NSTAGE - 1 < nsteps) stage((st + NSTAGE - 1) % NSTAGE, mb + (st + NSTAGE - 1) * WTM);
+    const bool nxt = st + NSTAGE - 1 < nsteps;
+    const int nbuf = (st + NSTAGE - 1) % NSTAGE;
+    if (nxt) stage(nbuf, mb + (st + NSTAGE - 1) * WTM);
     const uint32_t base = lds0 + (st % NSTAGE) * GSTB;
     s16x4 xr[8];
 #pragma unroll
@@ -1300,11 +1324,13 @@ __global__ __launch_bounds__(512, 1) void head_wgrad_g_kernel(const bf16* __rest
 }
 
 int g_cus = 0;
+int g_score_ilv = 1;  // head_score2: next stage's pieces interleaved with the MFMA rows
 int g_score_rows = 0;  // head_score2 row tile: 0 = by the rounds rule, 160 / 192 forced (benchmarks)
 
 }  // namespace
 
 extern "C" void fr_head_score_set_rows(int r) { g_score_rows = r; }
+extern "C" void fr_head_score_set_ilv(int v) { g_score_ilv = v; }
 
 extern "C" int fr_head_supported(int D, int Q, int T) {
   // (head_pool2 holds ceil(T / (384 / (D / 8))) <= 32 rows per thread: D = 1024 up to T = 96)
@@ -1337,12 +1363,18 @@ extern "C" int fr_head_score(const void* table, const int* ids, int U, int T, in
     const long Me = nreal != nullptr ? std::max<long>((long)M - 64L * T, (long)T) : (long)M;
     const long rounds192 = ((Me + 191) / 192 + g_cus - 1) / g_cus, rounds160 = ((Me + 159) / 160 + g_cus - 1) / g_cus;
     const bool r160 = g_score_rows == 160 || (g_score_rows == 0 && rounds160 * (160 + 384) < rounds192 * (192 + 384));
-    if (r160)
-      hipLaunchKernelGGL((head_score2_kernel<6, 5, 64, 2, 4, true>), dim3((M + 159) / 160), dim3(512), 0, s,
-                         (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
-    else
-      hipLaunchKernelGGL((head_score2_kernel<6, 6, 64, 2, 4, true>), dim3((M + 191) / 192), dim3(512), 0, s,
-                         (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, a_out, Q, nreal);
+#define LAUNCH_S2(RF_, IL_)                                                                                  \
+  hipLaunchKernelGGL((head_score2_kernel<6, RF_, 64, 2, 4, true, IL_>), dim3((M + 32 * RF_ - 1) / (32 * RF_)),     \
+                     dim3(512), 0, s, (const bf16*)table, ids, M, T, D, (const bf16*)W1, b1, w2, b2, (bf16*)e_out, \
+                     a_out, Q, nreal)
+    if (r160) {
+      if (g_score_ilv) LAUNCH_S2(5, true);
+      else LAUNCH_S2(5, false);
+    } else {
+      if (g_score_ilv) LAUNCH_S2(6, true);
+      else LAUNCH_S2(6, false);
+    }
+#undef LAUNCH_S2
     return 0;
   }
   // Q = 128 / 256 (the tiny test backbones): 128-row tiles, the same pipeline

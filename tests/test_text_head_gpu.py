@@ -215,11 +215,15 @@ def test_score_row_tiles_agree_bitwise(dev, U, T):
     outs = []
     try:
         for rows in (192, 160):
-            lib.head_score_set_rows(rows)
-            outs.append(lib.head_score(table, ids, T, w1, b1, w2, b2, True))
+            for ilv in (0, 1):  # (the next stage's loads interleaved with the MFMAs: no arithmetic change)
+                lib.head_score_set_rows(rows)
+                lib.head_score_set_ilv(ilv)
+                outs.append(lib.head_score(table, ids, T, w1, b1, w2, b2, True))
     finally:
         lib.head_score_set_rows(0)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        lib.head_score_set_ilv(1)
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1])
 
 
 @pytest.mark.parametrize("U,T,padded", [(1577, 50, True), (257, 50, False), (40, 17, False), (30, 100, True)])
