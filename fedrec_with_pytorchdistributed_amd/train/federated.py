@@ -398,6 +398,12 @@ def run_star_client(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                                                               if isinstance(v, (int, float))}})
             with torch.no_grad():
                 model.flat.flat.copy_(local)
+            # stay until the coordinator has read every report: the store may live in this
+            # process (rank 0 of the launch), and its exit would cut the others' reports off
+            try:
+                cp.get(f"r{r}/final_ack", min(cfg.round_timeout_s, 300.0) + 30.0)
+            except Exception as e:  # (a coordinator gone: nothing left to wait for)
+                obs.log(f"[client {k}] final evaluation: no acknowledgement: {e}")
             break
         if flag != "1":
             break
@@ -598,6 +604,7 @@ def run_star_server(cfg: FedRecConfig, ctx: DistContext, run_id: str = "star") -
                 finals.append(cp.get_json(f"r{R}/final/{k}", min(cfg.round_timeout_s, 300.0)))
             except Exception as e:  # a client gone after the last round: report the others
                 obs.log(f"[server] final evaluation: no report from client {k}: {e}")
+        cp.set(f"r{R}/final_ack", "1")  # the clients may exit now
         if finals:
             rec = {"round": R - 1, "final_global": True, "clients_reporting": len(finals)}
             for key in ("validation_loss", "valid_auc", "valid_mrr", "val_ndcg@5", "val_ndcg@10"):
