@@ -70,7 +70,8 @@ def main():
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     for name, argvs in runs(a.world, a.epochs, a.preset):
-        if a.only and not any(o in name for o in a.only.split(",")):
+        # --only: comma list of substrings; a trailing "$" asks for the exact run name
+        if a.only and not any((name == o[:-1]) if o.endswith("$") else (o in name) for o in a.only.split(",")):
             continue
         d = os.path.abspath(os.path.join(a.out, name))
         os.makedirs(d, exist_ok=True)
