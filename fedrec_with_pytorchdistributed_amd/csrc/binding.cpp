@@ -685,7 +685,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad_g(const at
                                                                         const c10::optional<at::Tensor>& ids, int64_t T,
                                                                         const at::Tensor& G, const at::Tensor& cs,
                                                                         const at::Tensor& w2, const at::Tensor& db2p,
-                                                                        const c10::optional<at::Tensor>& nreal) {
+                                                                        const c10::optional<at::Tensor>& nreal,
+                                                                        const c10::optional<std::vector<at::Tensor>>& out) {
   const int64_t U = head_titles(table, ids, T), D = table.size(1), Q = w2.numel();
   check_dev(G, "G");
   check_dev(cs, "cs");
@@ -700,11 +701,35 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad_g(const at
   TORCH_CHECK(fr_head_g_supported((int)D, (int)Q, (int)T), "fedrec::head_wgrad_g: unsupported shape");
   const c10::DeviceGuard g(table.device());
   auto fopt = cs.options();
-  auto dW1 = at::empty({Q, D}, fopt);
-  auto small = at::empty({2 * Q + 1}, fopt);
-  float* db1 = small.data_ptr<float>();
-  float* dw2 = db1 + Q;
-  float* db2 = dw2 + Q;
+  at::Tensor dW1, small, o_db1, o_dw2, o_db2;
+  float *db1, *dw2, *db2;
+  if (out.has_value()) {  // the destinations given (the flat gradient buffer's slots): dW1, db1, dw2, db2
+    TORCH_CHECK(out->size() == 4, "fedrec::head_wgrad_g: out = [dW1, db1, dw2, db2]");
+    const int64_t sizes[4] = {Q * D, Q, Q, 1};
+    for (int i = 0; i < 4; ++i) {
+      const auto& t = (*out)[i];
+      check_dev(t, "head_wgrad_g out");
+      TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == sizes[i] &&
+                      t.device() == table.device() && (i > 0 || ((uintptr_t)t.data_ptr() & 15) == 0),
+                  "fedrec::head_wgrad_g: out tensors fp32 contiguous [Q, D] / [Q] / [Q] / [1]");
+    }
+    dW1 = (*out)[0];
+    o_db1 = (*out)[1];
+    o_dw2 = (*out)[2];
+    o_db2 = (*out)[3];
+    db1 = o_db1.data_ptr<float>();
+    dw2 = o_dw2.data_ptr<float>();
+    db2 = o_db2.data_ptr<float>();
+  } else {
+    dW1 = at::empty({Q, D}, fopt);
+    small = at::empty({2 * Q + 1}, fopt);
+    db1 = small.data_ptr<float>();
+    dw2 = db1 + Q;
+    db2 = dw2 + Q;
+    o_db1 = small.narrow(0, 0, Q);
+    o_dw2 = small.narrow(0, Q, Q);
+    o_db2 = small.narrow(0, 2 * Q, 1);
+  }
   const long need = fr_head_wgrad_g(G.data_ptr(), table.data_ptr(), opt_int_ptr(ids), cs.data_ptr<float>(),
                                     db2p.data_ptr<float>(), w2.data_ptr<float>(), (int)U, (int)T, (int)D, (int)Q,
                                     dW1.data_ptr<float>(), db1, dw2, db2, nullptr, nullptr, cur_stream(), nullptr,
@@ -722,7 +747,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_wgrad_g(const at
                                 opt_nreal(nreal, table), cur_stream(), has_pend ? pend.data() : nullptr, pc, pt),
            "head_wgrad_g");
   if (has_pend) g_sg_pending_scratch = at::Tensor();
-  return {dW1, small.narrow(0, 0, Q), small.narrow(0, Q, Q), small.narrow(0, 2 * Q, 1)};
+  return {dW1, o_db1, o_dw2, o_db2};
 }
 
 // user pool backward with da out (column 0 of [n T, 8]) instead of dw2 / db2 (fr_upool_bwd_da)
@@ -1956,7 +1981,7 @@ TORCH_LIBRARY(fedrec, m) {
   m.def("small_gemm_set_defer(bool on) -> ()", &small_gemm_set_defer);
   m.def("small_gemm_flush_pending() -> bool", &small_gemm_flush_pending);
   m.def("head_pool_bwd_g(Tensor table, Tensor? ids, int T, Tensor alpha, Tensor g, Tensor(a!) e, Tensor? nreal=None) -> (Tensor, Tensor, Tensor)");
-  m.def("head_wgrad_g(Tensor table, Tensor? ids, int T, Tensor G, Tensor cs, Tensor w2, Tensor db2p, Tensor? nreal=None) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("head_wgrad_g(Tensor table, Tensor? ids, int T, Tensor G, Tensor cs, Tensor w2, Tensor db2p, Tensor? nreal=None, Tensor(a!)[]? out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("ipc_create(int cap) -> (int, Tensor)", &ipc_create);
   m.def("ipc_open(int id, Tensor handles, int me, int W, Tensor? local_ptrs) -> ()", &ipc_open);
   m.def("ipc_region(int id) -> int", &ipc_region);

@@ -67,7 +67,7 @@ class FlatParams:
         for p in self.params:
             p.grad = None
 
-    def end_backward(self, copy: bool = True):
+    def end_backward(self, copy: bool = True, inplace=()):
         """Gather the fresh gradients into the flat buffer (one multi-tensor copy launch;
         parameters that got no gradient are zeroed) and re-point ``.grad`` at it.
 
@@ -75,12 +75,15 @@ class FlatParams:
         segments): no copy launch; returns each parameter's gradient source in parameter
         order -- the fresh tensor, its flat slot when the gradient already sits there, or None
         (no gradient: Adam writes zeros) -- for the caller to hand to Adam, which writes them
-        into the flat buffer.  The caller keeps the list alive until Adam is queued."""
+        into the flat buffer.  The caller keeps the list alive until Adam is queued.
+
+        ``inplace``: ids of parameters whose gradients the backward wrote straight into their
+        slots (``ops.functional.grads_into``, N > 1): present, not missing."""
         if not copy:
             srcs = []
             for p, off in zip(self.params, self.offsets):
                 view = self.grad[off:off + p.numel()].view_as(p)
-                gr = p.grad
+                gr = view if p.grad is None and id(p) in inplace else p.grad
                 if gr is not None and gr.data_ptr() != view.data_ptr() and (gr.dtype != torch.float32
                                                                            or not gr.is_contiguous()):
                     view.copy_(gr)  # (not expected on the fused step: every gradient is fresh fp32)
@@ -91,7 +94,9 @@ class FlatParams:
         dst, src, missing = [], [], []
         for p, off in zip(self.params, self.offsets):
             view = self.grad[off:off + p.numel()].view_as(p)
-            if p.grad is None:
+            if p.grad is None and id(p) in inplace:
+                pass  # already in its slot
+            elif p.grad is None:
                 missing.append(view)
             elif p.grad.data_ptr() != view.data_ptr():
                 dst.append(view)

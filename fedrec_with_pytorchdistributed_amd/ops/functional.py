@@ -127,6 +127,54 @@ class AdditivePoolFn(torch.autograd.Function):
         return dx, dw1, db1, dw2.reshape(1, -1).to(w2.dtype), db2.reshape(1).to(w2.dtype), None
 
 
+# N > 1 (the engine, around a step's forward + backward): the text head's and its fc's weight
+# gradients go straight into their slots of the flat gradient buffer -- the gradient all-reduce
+# reads them there, and the end-of-backward copy of the six fresh tensors (one launch on the
+# critical path between the backward and the head slice's all-reduce) is gone.  ``_GRAD_INTO``
+# maps id(parameter) -> its flat slot (a view of the parameter's shape); a Function whose weights
+# all have slots writes them in place, returns None for them and records them in
+# ``_GRAD_WRITTEN``, which the engine hands to ``FlatParams.end_backward`` (slots not to zero).
+_GRAD_INTO: dict = {}
+_GRAD_WRITTEN: set = set()
+
+
+class grads_into:
+    """Context: the weight-gradient destinations of :data:`_GRAD_INTO` for the backward run inside it."""
+
+    def __init__(self, mapping: dict):
+        self.mapping = mapping
+
+    def __enter__(self):
+        _GRAD_INTO.clear()
+        _GRAD_INTO.update(self.mapping)
+        _GRAD_WRITTEN.clear()
+        return self
+
+    def __exit__(self, *exc):
+        _GRAD_INTO.clear()
+        return False
+
+
+def take_written() -> set:
+    """ids of the parameters whose gradients a backward wrote in place (and forget them)."""
+    out = set(_GRAD_WRITTEN)
+    _GRAD_WRITTEN.clear()
+    return out
+
+
+def _slots(*params):
+    """The flat-gradient slots of ``params`` (all of them, fp32 contiguous), else None."""
+    if not _GRAD_INTO:
+        return None
+    out = []
+    for p in params:
+        v = _GRAD_INTO.get(id(p))
+        if v is None or v.dtype != torch.float32 or not v.is_contiguous() or v.shape != p.shape:
+            return None
+        out.append(v)
+    return tuple(out), tuple(id(p) for p in params)
+
+
 class TextHeadFn(torch.autograd.Function):
     """The text head's attention pooling (``encoder.py:27-28`` -> ``attention.py:14-26``) over
     GATHERED hidden states: rows of ``table [rows, D]`` (the HBM hidden-state cache, or a
@@ -157,6 +205,7 @@ class TextHeadFn(torch.autograd.Function):
         if need:
             ctx.save_for_backward(table, ids, e, alpha, w2, nreal)
         ctx.T = T
+        ctx.into = _slots(w1, b1, w2, b2) if all(ctx.needs_input_grad[:4]) else None
         ctx.mark_non_differentiable(pooled_b)
         # no zero tensor for pooled_b's (never used) gradient: autograd would otherwise fill one
         # [U, D] bf16 buffer per backward (a 5.5 us fill launch in every config-2 step)
@@ -173,6 +222,12 @@ class TextHeadFn(torch.autograd.Function):
             # the G path: the pool backward also turns e into g = da (1 - e^2) (in place) with the
             # per-title column sums, and the weight gradient is a plain TN GEMM over g
             da, db2p, cs = lib.head_pool_bwd_g(table, ids, ctx.T, alpha, g.contiguous().float(), e, nreal)
+            if ctx.into is not None:  # into the flat gradient's slots (N > 1): no fresh tensors to copy
+                views, pids = ctx.into
+                lib.head_wgrad_g(table, ids, ctx.T, e, cs, w2.reshape(-1).contiguous(), db2p, nreal,
+                                 [v.view(-1) for v in views])
+                _GRAD_WRITTEN.update(pids)
+                return None, None, None, None, None, None, None, None, None, None, None
             dw1, db1, dw2, db2 = lib.head_wgrad_g(table, ids, ctx.T, e, cs, w2.reshape(-1).contiguous(), db2p, nreal)
         else:
             da, db2p = lib.head_pool_bwd(table, ids, ctx.T, alpha, g.contiguous().float(), nreal)
@@ -924,6 +979,7 @@ class HeadFCFn(torch.autograd.Function):
         y = torch.empty(n, N, device=x.device, dtype=torch.float32)
         ops.small_gemm(ops.Gemm(xg, wg, y, n, N, K, K, K, N, bias=b))
         ctx.save_for_backward(xg, wg, wbt)
+        ctx.into = _slots(w, b) if ctx.needs_input_grad[1] and ctx.needs_input_grad[2] else None
         return y
 
     @staticmethod
@@ -934,8 +990,12 @@ class HeadFCFn(torch.autograd.Function):
         dy = dy.contiguous().float()
         dx = torch.empty(n, K, device=x.device, dtype=torch.float32)
 
-        dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
-        db = torch.empty(N, device=x.device, dtype=torch.float32)
+        if ctx.into is not None:  # into the flat gradient's slots (N > 1)
+            (dw, db), pids = ctx.into
+            _GRAD_WRITTEN.update(pids)
+        else:
+            dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+            db = torch.empty(N, device=x.device, dtype=torch.float32)
         wgrad = ops.Gemm(dy, x, dw, N, K, n, N, K, K, a_mode=1, b_mode=1, asum=db)
         # dgrad, wgrad and the bias gradient (dy's column sums, from the wgrad's dy tiles) in one
         # launch -- with the user encoder's weight gradients when its backward held them back
@@ -953,4 +1013,6 @@ class HeadFCFn(torch.autograd.Function):
             ops.small_gemm(*gs)
         if early is not None:  # the user-encoder weight gradients are final here
             early()
+        if ctx.into is not None:
+            return dx, None, None, None, None, None
         return dx, dw.view_as(dw), db.view_as(db), None, None, None

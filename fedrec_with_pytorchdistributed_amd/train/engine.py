@@ -80,6 +80,12 @@ class Prepared(NamedTuple):
 _CAPTURE_MODE = "thread_local"
 
 
+# N > 1: the text head's and its fc's weight gradients are written into the flat gradient buffer
+# by their backward launches (ops.functional.grads_into) instead of fresh tensors that the end of
+# the backward copies there; False only in the test that compares the two
+INPLACE_HEAD_GRADS = True
+
+
 class _StepGraph:
     """Static inputs + the captured graph of one (batch shape, unique-title bucket)."""
 
@@ -273,6 +279,7 @@ class LocalEngine:
         # inside the graph, and optimizer steps issued eagerly from the host
         self.counts = {"replays": 0, "replays_with_optimizer": 0, "eager_optimizer_steps": 0, "eager_steps": 0,
                        "captures": 0, "early_reduces": 0}
+        self.inplace_grads = 0
         self.host_wait_s = 0.0  # host time blocked on the run-ahead bound (_retire): the DEVICE is the limit
         # optimizer overlap (per-step schedule): grads all-reduced + Adam on a side stream while
         # the next step samples, dedups and runs the frozen backbone, none of which reads the
@@ -286,6 +293,13 @@ class LocalEngine:
         # while the current step runs, so the dedup's host read of the unique count (the
         # backbone's M) no longer drains the GPU at every step start
         self._prep = torch.cuda.Stream(device) if device.type == "cuda" else None
+
+    def _grad_slots(self) -> Dict[int, torch.Tensor]:
+        """id(parameter) -> its slot of the flat gradient buffer (a view of the parameter's shape)."""
+        if getattr(self, "_slots", None) is None:
+            fl = self.flat
+            self._slots = {id(p): fl.grad[off:off + p.numel()].view_as(p) for p, off in zip(fl.params, fl.offsets)}
+        return self._slots
 
     def _user_slice_start(self, model) -> Optional[int]:
         """Index of the first user-encoder parameter in the flat buffer when the user encoder's
@@ -599,25 +613,33 @@ class LocalEngine:
                 else:
                     casts = OF.step_weight_casts(self.model.text_encoder, self.model.user_encoder,
                                                  bump=self._rng_step, bump2=self._adam_bump)
-            with obs.range("news_encode"):
-                v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
-                                      w1b=casts[0] if casts is not None else None,
-                                      fcb=casts[2] if casts is not None else None)
-            with obs.range("user_step"):
-                loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
-                                          pre is not None and pre.padded, True, his,
-                                          casts=casts[1] if casts is not None else None)
-            # weight gradients beside the rest of the backward (fresh .grad: begin_backward above;
-            # a bucket reducer's per-gradient hooks would read them before the side stream ran)
-            side = OF.side_wgrads() if self.reducer is None else contextlib.nullcontext()
-            with obs.range("backward"), side:
-                loss.backward(self._seed_one())
+            # N > 1: the text head's and fc's weight gradients straight into the flat buffer (the
+            # all-reduce reads them there; no end-of-backward copy of six fresh tensors)
+            into = (OF.grads_into(self._grad_slots()) if INPLACE_HEAD_GRADS and self.grad_allreduce is not None
+                    and self.reducer is None and not self._adam_gathers else contextlib.nullcontext())
+            with into:
+                with obs.range("news_encode"):
+                    v = self.news_vectors(dd[0], grad=True, nreal=pre.nreal if pre is not None else None,
+                                          w1b=casts[0] if casts is not None else None,
+                                          fcb=casts[2] if casts is not None else None)
+                with obs.range("user_step"):
+                    loss, _ = self._user_loss(v, dd, cand.shape[0], cand.shape[1], his.shape[1],
+                                              pre is not None and pre.padded, True, his,
+                                              casts=casts[1] if casts is not None else None)
+                # weight gradients beside the rest of the backward (fresh .grad: begin_backward
+                # above; a bucket reducer's per-gradient hooks would read them before the side
+                # stream ran)
+                side = OF.side_wgrads() if self.reducer is None else contextlib.nullcontext()
+                with obs.range("backward"), side:
+                    loss.backward(self._seed_one())
+            inplace = OF.take_written()
+            self.inplace_grads = len(inplace)  # (tests: how many slots the last backward wrote in place)
             if casts is None:
                 self._rng_step.add_(1)  # next step's dropout masks (inside a captured graph too)
             if self._adam_gathers:  # the in-graph Adam reads the fresh gradients where they are
-                self._grad_srcs = self.flat.end_backward(copy=False)
+                self._grad_srcs = self.flat.end_backward(copy=False, inplace=inplace)
             else:
-                self.flat.end_backward()
+                self.flat.end_backward(inplace=inplace)
             return loss.detach()
         _, _, cand_v, his_v = self._forward_rows(cand, his, grad_news=True, pre=pre)
         with obs.range("user_fwd"):
